@@ -1,0 +1,44 @@
+"""Loader for the in-tree gfx950 native library (``_C.so``, ops under ``torch.ops.hydra``).
+
+Policy: GPU tensors ALWAYS run the HIP kernels. If the library is missing or
+fails to load while a GPU op is requested we raise instead of silently falling
+back to an eager PyTorch path.  CPU tensors use the plain-torch reference
+implementations in ``hydragnn_amd/ops`` (the numerics oracle for tests).
+"""
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_C.so")
+
+_loaded = False
+_error = None
+
+
+def load():
+    global _loaded, _error
+    if _loaded:
+        return True
+    if not os.path.exists(LIB_PATH):
+        _error = f"{LIB_PATH} not found (run `python -m hydragnn_amd.csrc.build`)"
+        return False
+    try:
+        torch.ops.load_library(LIB_PATH)
+        _loaded = True
+    except Exception as e:  # pragma: no cover - depends on the build
+        _error = f"failed to load {LIB_PATH}: {e}"
+    return _loaded
+
+
+def available():
+    return load()
+
+
+def ops():
+    """Return ``torch.ops.hydra``; raise loudly if the native library is unavailable."""
+    if not load():
+        raise RuntimeError(
+            "hydragnn_amd native HIP library is required for GPU tensors but is unavailable: " + str(_error)
+        )
+    return torch.ops.hydra

@@ -1,0 +1,387 @@
+// Segment-block-diagonal multi-head self-attention (flash style) for GPS (gfx950).
+//
+// Reference: hydragnn/globalAtt/gps.py:126-133 runs torch.nn.MultiheadAttention
+// over `to_dense_batch(x, None)`, i.e. ALL nodes of the mini-batch form ONE
+// sequence [1, N, F] ("batch" scope).  We generalise to a partition of the N
+// tokens into segments (seg_ptr / seg_id): a query attends to the keys of its own
+// segment.  batch scope = one segment (plus one segment holding padding rows),
+// graph scope = one segment per graph (varlen, O(sum n_g^2)).
+//
+// GPS configs use small heads (hidden 64 / 8 heads -> D = 8), where the score
+// work is exp/VALU-bound rather than matrix-bound, so this kernel keeps Q, the
+// running max/sum and the output accumulator in registers (one query row per
+// lane), stages K/V tiles through LDS (broadcast reads, conflict-free), and
+// splits the key range over the 4 waves of a workgroup (merged through LDS at
+// the end) so that N/64 x H workgroups x 4 waves keep all 256 CUs busy.
+// Never materialises the N x N score matrix; backward recomputes P from the
+// saved log-sum-exp (two atomic-free passes: dQ by query rows, dK/dV by key
+// rows).
+#include "common.h"
+
+namespace hy {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+struct AttnCfg {
+  static constexpr int KT = D <= 8 ? 64 : (D <= 16 ? 32 : 16);  // keys per wave tile
+};
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Q/K/V rows: element (n, h, d) at ptr[n * ld + h * D + d].  O: [N, H*D].  LSE: [H, N] (natural log).
+template <int D>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__ Q, const float* __restrict__ K,
+                                                       const float* __restrict__ V, int ld,
+                                                       float* __restrict__ O, float* __restrict__ LSE,
+                                                       const int* __restrict__ seg_id,
+                                                       const int* __restrict__ seg_ptr, int N, int H,
+                                                       float scale) {
+  constexpr int KT = AttnCfg<D>::KT;
+  __shared__ float Ks[4][KT][D];
+  __shared__ float Vs[4][KT][D];
+  __shared__ float Mrg[64][D + 2];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = blockIdx.x * 64 + lane;
+  const bool qv = qi < N;
+  int kb = INT_MAX, ke = 0;
+  if (qv) {
+    const int s = seg_id[qi];
+    kb = seg_ptr[s];
+    ke = seg_ptr[s + 1];
+  }
+  const int ub = wave_min_i(kb), ue = wave_max_i(ke);
+  float q[D], acc[D];
+  const float qs = scale * kLog2e;  // scores in log2 domain
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    q[d] = qv ? Q[(int64_t)qi * ld + h * D + d] * qs : 0.f;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int base = ub; base < ue; base += 4 * KT) {
+    const int t = base + w * KT;
+    for (int idx = lane; idx < KT * D; idx += 64) {
+      const int j = t + idx / D, d = idx % D;
+      const bool ok = j < ue;
+      Ks[w][idx / D][d] = ok ? K[(int64_t)j * ld + h * D + d] : 0.f;
+      Vs[w][idx / D][d] = ok ? V[(int64_t)j * ld + h * D + d] : 0.f;
+    }
+    __syncthreads();
+    if (t < ue) {
+      float s[KT];
+      float mt = -INFINITY;
+#pragma unroll
+      for (int jj = 0; jj < KT; ++jj) {
+        float a = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) a = fmaf(q[d], Ks[w][jj][d], a);
+        const int j = t + jj;
+        s[jj] = (j >= kb && j < ke) ? a : -INFINITY;
+        mt = fmaxf(mt, s[jj]);
+      }
+      if (mt > -INFINITY) {
+        const float mn = fmaxf(m, mt);
+        const float alpha = exp2f(m - mn);  // m=-inf -> 0
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc[d] *= alpha;
+#pragma unroll
+        for (int jj = 0; jj < KT; ++jj) {
+          const float p = exp2f(s[jj] - mn);
+          l += p;
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc[d] = fmaf(p, Vs[w][jj][d], acc[d]);
+        }
+        m = mn;
+      }
+    }
+    __syncthreads();
+  }
+  // merge the 4 key stripes: wave w folds its (m, l, acc) into the running LDS copy
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+      if (step > 0) {
+        const float mo = Mrg[lane][0], lo = Mrg[lane][1];
+        const float M = fmaxf(m, mo);
+        const float fo = (M > -INFINITY) ? exp2f(mo - M) : 0.f;
+        const float fs = (M > -INFINITY) ? exp2f(m - M) : 0.f;
+        l = lo * fo + l * fs;
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc[d] = Mrg[lane][2 + d] * fo + acc[d] * fs;
+        m = M;
+      }
+      if (step < 3) {
+        Mrg[lane][0] = m;
+        Mrg[lane][1] = l;
+#pragma unroll
+        for (int d = 0; d < D; ++d) Mrg[lane][2 + d] = acc[d];
+      } else if (qv) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) O[(int64_t)qi * (H * D) + h * D + d] = acc[d] * inv;
+        LSE[(int64_t)h * N + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : -INFINITY;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// delta[h, i] = sum_d dO[i,h,d] * O[i,h,d]
+__global__ void attn_delta_kernel(const float* __restrict__ dO, const float* __restrict__ O,
+                                  float* __restrict__ delta, int N, int H, int D) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * H) return;
+  const int i = (int)(t / H), h = (int)(t % H);
+  float a = 0.f;
+  for (int d = 0; d < D; ++d) a += dO[(int64_t)i * H * D + h * D + d] * O[(int64_t)i * H * D + h * D + d];
+  delta[(int64_t)h * N + i] = a;
+}
+
+// dQ: one query row per lane, key stripes over 4 waves (same structure as forward).
+template <int D>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
+    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    float* __restrict__ dQ, int lddq, const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int N,
+    int H, float scale) {
+  constexpr int KT = AttnCfg<D>::KT;
+  __shared__ float Ks[4][KT][D];
+  __shared__ float Vs[4][KT][D];
+  __shared__ float Mrg[64][D];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = blockIdx.x * 64 + lane;
+  const bool qv = qi < N;
+  int kb = INT_MAX, ke = 0;
+  if (qv) {
+    const int s = seg_id[qi];
+    kb = seg_ptr[s];
+    ke = seg_ptr[s + 1];
+  }
+  const int ub = wave_min_i(kb), ue = wave_max_i(ke);
+  float q[D], go[D], dq[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    q[d] = qv ? Q[(int64_t)qi * ld + h * D + d] * scale : 0.f;
+    go[d] = qv ? dO[(int64_t)qi * H * D + h * D + d] : 0.f;
+    dq[d] = 0.f;
+  }
+  const float lse = qv ? LSE[(int64_t)h * N + qi] : 0.f;
+  const float dl = qv ? delta[(int64_t)h * N + qi] : 0.f;
+  for (int base = ub; base < ue; base += 4 * KT) {
+    const int t = base + w * KT;
+    for (int idx = lane; idx < KT * D; idx += 64) {
+      const int j = t + idx / D, d = idx % D;
+      const bool ok = j < ue;
+      Ks[w][idx / D][d] = ok ? K[(int64_t)j * ld + h * D + d] : 0.f;
+      Vs[w][idx / D][d] = ok ? V[(int64_t)j * ld + h * D + d] : 0.f;
+    }
+    __syncthreads();
+    if (t < ue) {
+#pragma unroll 4
+      for (int jj = 0; jj < KT; ++jj) {
+        const int j = t + jj;
+        if (j >= kb && j < ke) {
+          float sc = 0.f, dp = 0.f;
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            sc = fmaf(q[d], Ks[w][jj][d], sc);
+            dp = fmaf(go[d], Vs[w][jj][d], dp);
+          }
+          const float p = __expf(sc - lse);
+          const float ds = p * (dp - dl);
+#pragma unroll
+          for (int d = 0; d < D; ++d) dq[d] = fmaf(ds, Ks[w][jj][d], dq[d]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float t = (step > 0 ? Mrg[lane][d] : 0.f) + dq[d];
+        if (step < 3) Mrg[lane][d] = t;
+        else if (qv) dQ[(int64_t)qi * lddq + h * D + d] = t * scale;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dK, dV: one key row per lane, query stripes over 4 waves.
+template <int D>
+__global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
+    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    float* __restrict__ dK, float* __restrict__ dV, int lddkv, const int* __restrict__ seg_id,
+    const int* __restrict__ seg_ptr, int N, int H, float scale) {
+  constexpr int QT = AttnCfg<D>::KT;
+  __shared__ float Qs[4][QT][D];
+  __shared__ float Gs[4][QT][D];
+  __shared__ float Ls[4][QT][2];
+  __shared__ float Mrg[64][2 * D];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kj = blockIdx.x * 64 + lane;
+  const bool kv = kj < N;
+  int qb = INT_MAX, qe = 0;
+  if (kv) {
+    const int s = seg_id[kj];
+    qb = seg_ptr[s];
+    qe = seg_ptr[s + 1];
+  }
+  const int ub = wave_min_i(qb), ue = wave_max_i(qe);
+  float k[D], v[D], dk[D], dv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    k[d] = kv ? K[(int64_t)kj * ld + h * D + d] * scale : 0.f;
+    v[d] = kv ? V[(int64_t)kj * ld + h * D + d] : 0.f;
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+  for (int base = ub; base < ue; base += 4 * QT) {
+    const int t = base + w * QT;
+    for (int idx = lane; idx < QT * D; idx += 64) {
+      const int i = t + idx / D, d = idx % D;
+      const bool ok = i < ue;
+      Qs[w][idx / D][d] = ok ? Q[(int64_t)i * ld + h * D + d] : 0.f;
+      Gs[w][idx / D][d] = ok ? dO[(int64_t)i * H * D + h * D + d] : 0.f;
+    }
+    for (int idx = lane; idx < QT; idx += 64) {
+      const int i = t + idx;
+      const bool ok = i < ue;
+      Ls[w][idx][0] = ok ? LSE[(int64_t)h * N + i] : 0.f;
+      Ls[w][idx][1] = ok ? delta[(int64_t)h * N + i] : 0.f;
+    }
+    __syncthreads();
+    if (t < ue) {
+#pragma unroll 4
+      for (int ii = 0; ii < QT; ++ii) {
+        const int i = t + ii;
+        if (i >= qb && i < qe) {
+          float sc = 0.f, dp = 0.f;
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            sc = fmaf(Qs[w][ii][d], k[d], sc);
+            dp = fmaf(Gs[w][ii][d], v[d], dp);
+          }
+          const float p = __expf(sc - Ls[w][ii][0]);
+          const float ds = p * (dp - Ls[w][ii][1]);
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            dv[d] = fmaf(p, Gs[w][ii][d], dv[d]);
+            dk[d] = fmaf(ds, Qs[w][ii][d], dk[d]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float tk = (step > 0 ? Mrg[lane][d] : 0.f) + dk[d];
+        const float tv = (step > 0 ? Mrg[lane][D + d] : 0.f) + dv[d];
+        if (step < 3) {
+          Mrg[lane][d] = tk;
+          Mrg[lane][D + d] = tv;
+        } else if (kv) {
+          dK[(int64_t)kj * lddkv + h * D + d] = tk * scale;
+          dV[(int64_t)kj * lddkv + h * D + d] = tv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+#define HY_ATTN_DISPATCH(D, ...)                       \
+  switch (D) {                                          \
+    case 4: { constexpr int kD = 4; __VA_ARGS__; break; }   \
+    case 8: { constexpr int kD = 8; __VA_ARGS__; break; }   \
+    case 16: { constexpr int kD = 16; __VA_ARGS__; break; } \
+    case 32: { constexpr int kD = 32; __VA_ARGS__; break; } \
+    case 64: { constexpr int kD = 64; __VA_ARGS__; break; } \
+    default: HY_CHECK(false, "attention head_dim must be one of 4,8,16,32,64, got ", D); \
+  }
+
+// qkv: [N, 3*H*D] packed rows (q | k | v), as produced by the in-projection.
+std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const at::Tensor& seg_id,
+                                            const at::Tensor& seg_ptr, int64_t H, double scale) {
+  HY_CHECK_CUDA(qkv);
+  HY_CHECK_F32(qkv);
+  HY_CHECK(qkv.stride(1) == 1, "qkv rows must be contiguous");
+  HY_CHECK_I32(seg_id);
+  HY_CHECK_I32(seg_ptr);
+  const int64_t N = qkv.size(0);
+  const int64_t F = qkv.size(1) / 3;
+  const int D = (int)(F / H);
+  HY_CHECK(D * H == F, "hidden must be divisible by heads");
+  auto O = at::empty({N, F}, qkv.options());
+  auto LSE = at::empty({H, N}, qkv.options());
+  if (N == 0) return {O, LSE};
+  const int ld = (int)qkv.stride(0);
+  const float* base = qkv.data_ptr<float>();
+  dim3 grid(ceil_div(N, 64), H);
+  HY_ATTN_DISPATCH(D, attn_fwd_kernel<kD><<<grid, 256, 0, stream()>>>(
+                          base, base + F, base + 2 * F, ld, O.data_ptr<float>(), LSE.data_ptr<float>(),
+                          seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, (float)scale));
+  return {O, LSE};
+}
+
+at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& LSE,
+                    const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t H, double scale) {
+  auto dO = dO_.contiguous();
+  HY_CHECK_CUDA(dO);
+  const int64_t N = qkv.size(0);
+  const int64_t F = qkv.size(1) / 3;
+  const int D = (int)(F / H);
+  auto dqkv = at::empty({N, 3 * F}, qkv.options());
+  if (N == 0) return dqkv;
+  auto delta = at::empty({H, N}, qkv.options());
+  attn_delta_kernel<<<ceil_div(N * H, 256), 256, 0, stream()>>>(dO.data_ptr<float>(), O.data_ptr<float>(),
+                                                                 delta.data_ptr<float>(), (int)N, (int)H, D);
+  const int ld = (int)qkv.stride(0);
+  const float* base = qkv.data_ptr<float>();
+  float* dbase = dqkv.data_ptr<float>();
+  dim3 grid(ceil_div(N, 64), H);
+  HY_ATTN_DISPATCH(D, {
+    attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, dO.data_ptr<float>(),
+                                                       LSE.data_ptr<float>(), delta.data_ptr<float>(), dbase,
+                                                       (int)(3 * F), seg_id.data_ptr<int>(),
+                                                       seg_ptr.data_ptr<int>(), (int)N, (int)H, (float)scale);
+    attn_bwd_dkv_kernel<kD><<<grid, 256, 0, stream()>>>(
+        base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
+        dbase + F, dbase + 2 * F, (int)(3 * F), seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H,
+        (float)scale);
+  });
+  return dqkv;
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("attn_fwd(Tensor qkv, Tensor seg_id, Tensor seg_ptr, int H, float scale) -> (Tensor, Tensor)");
+  m.def(
+      "attn_bwd(Tensor dO, Tensor qkv, Tensor O, Tensor LSE, Tensor seg_id, Tensor seg_ptr, int H, float scale) "
+      "-> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("attn_fwd", hy::attn_fwd);
+  m.impl("attn_bwd", hy::attn_bwd);
+}

@@ -1,0 +1,113 @@
+"""In-tree builder for the gfx950 native library ``hydragnn_amd/_C.so``.
+
+Every ``*.hip`` / ``*.cpp`` file in this directory is compiled directly with
+``hipcc --offload-arch=gfx950`` (no hipify, no CUDA shims) against the PyTorch
+headers and linked into one shared object whose ops register themselves under
+``torch.ops.hydra.*`` (TORCH_LIBRARY).  Objects are cached in ``csrc/build/``
+and rebuilt only when a source or header is newer.
+
+Usage:  python -m hydragnn_amd.csrc.build [-j N] [--force]
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+OUT = os.path.join(PKG, "_C.so")
+BUILD = os.path.join(HERE, "build")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch
+
+    root = os.path.dirname(torch.__file__)
+    inc = [os.path.join(root, "include"), os.path.join(root, "include", "torch", "csrc", "api", "include")]
+    lib = os.path.join(root, "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _hipcc():
+    for c in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), "hipcc"):
+        if os.path.sep not in c or os.path.exists(c):
+            return c
+    return "hipcc"
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(HERE, "*.hip")) + glob.glob(os.path.join(HERE, "*.cpp")))
+
+
+def _headers_mtime():
+    hs = glob.glob(os.path.join(HERE, "*.h"))
+    return max([os.path.getmtime(h) for h in hs] + [0.0])
+
+
+def _compile(src, inc, abi, force):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    if (not force) and os.path.exists(obj):
+        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
+            return obj, None
+    py_inc = sysconfig.get_paths()["include"]
+    cmd = [
+        _hipcc(),
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-fPIC",
+        "-std=c++17",
+        "-ffp-contract=fast",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DUSE_ROCM",
+        "-Wno-unused-result",
+        "-Wno-deprecated-declarations",
+        f"-I{HERE}",
+        f"-I{py_inc}",
+    ] + [f"-I{p}" for p in inc] + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"FAILED: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(jobs=None, force=False, verbose=True):
+    os.makedirs(BUILD, exist_ok=True)
+    inc, lib, abi = _torch_paths()
+    srcs = sources()
+    jobs = jobs or min(8, os.cpu_count() or 4, len(srcs) or 1)
+    objs, errs = [], []
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        for obj, err in ex.map(lambda s: _compile(s, inc, abi, force), srcs):
+            objs.append(obj)
+            if err:
+                errs.append(err)
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
+            f"-L{lib}", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{lib}",
+        ]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[hydragnn_amd] built {OUT} from {len(srcs)} sources for {ARCH}")
+    return OUT
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    try:
+        build(a.j, a.force)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,78 @@
+// Multi-tensor fused AdamW / Adam step (gfx950).
+//
+// Replaces torch.optim.AdamW's per-parameter foreach kernels (reference optimizer
+// selection: hydragnn/utils/optimizer/optimizer.py:12-40; DeepSpeed FusedLamb is
+// the reference's only fused optimizer).  One launch updates every parameter:
+// a host-built block table maps each 2048-element chunk to (tensor, offset); the
+// step counter and learning rate live in device memory so the launch can be
+// captured in a hipGraph once and replayed with a changing lr / step.
+#include "common.h"
+
+namespace hy {
+
+struct TensorRef {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+};
+
+constexpr int kChunk = 2048;
+
+// state: [0] = step (float, incremented by the LAST block via atomic ticket), [1] = lr
+__global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict__ refs,
+                                                    const int2* __restrict__ blocks, float* __restrict__ state,
+                                                    float beta1, float beta2, float eps, float wd, int adamw,
+                                                    float grad_scale) {
+  const int2 bt = blocks[blockIdx.x];
+  const TensorRef r = refs[bt.x];
+  const float step = state[0] + 1.f;  // this step's count (state[0] is updated by a follow-up kernel)
+  const float lr = state[1];
+  const float bc1 = 1.f - powf(beta1, step);
+  const float bc2 = 1.f - powf(beta2, step);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const int64_t base = (int64_t)bt.y * kChunk;
+  for (int i = threadIdx.x; i < kChunk; i += 256) {
+    const int64_t k = base + i;
+    if (k >= r.n) break;
+    float g = r.g[k] * grad_scale;
+    float p = r.p[k];
+    if (adamw) p *= (1.f - lr * wd);
+    else g += wd * p;
+    const float m = beta1 * r.m[k] + (1.f - beta1) * g;
+    const float v = beta2 * r.v[k] + (1.f - beta2) * g * g;
+    r.m[k] = m;
+    r.v[k] = v;
+    const float denom = sqrtf(v) / bc2s + eps;
+    r.p[k] = p - step_size * m / denom;
+  }
+}
+
+__global__ void step_incr_kernel(float* state) { state[0] += 1.f; }
+
+void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tensor& state, double beta1,
+                double beta2, double eps, double wd, bool adamw, double grad_scale) {
+  HY_CHECK_CUDA(refs);
+  HY_CHECK(refs.scalar_type() == at::kByte, "refs must be a uint8 blob");
+  HY_CHECK_I32(blocks);
+  HY_CHECK_F32(state);
+  const int nblocks = (int)(blocks.numel() / 2);
+  if (nblocks == 0) return;
+  adamw_kernel<<<nblocks, 256, 0, stream()>>>(reinterpret_cast<const TensorRef*>(refs.data_ptr<uint8_t>()),
+                                              reinterpret_cast<const int2*>(blocks.data_ptr<int>()),
+                                              state.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
+                                              (float)wd, adamw ? 1 : 0, (float)grad_scale);
+  step_incr_kernel<<<1, 1, 0, stream()>>>(state.data_ptr<float>());
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def(
+      "adamw_step(Tensor refs, Tensor blocks, Tensor state, float beta1, float beta2, float eps, float wd, "
+      "bool adamw, float grad_scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) { m.impl("adamw_step", hy::adamw_step); }

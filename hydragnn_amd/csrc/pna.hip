@@ -1,0 +1,306 @@
+// Fused PNA / PNAPlus message + DegreeScalerAggregation (gfx950).
+//
+// Reference semantics (hydragnn/models/PNAPlusStack.py:144-286 and PyG 2.5
+// DegreeScalerAggregation, aggregators [mean,min,max,std] x scalers
+// [identity, amplification, attenuation, linear]):
+//     m_e   = pre_nn(cat[x_i, x_j, enc_e]) * rbf_lin(rbf_e)
+//     agg_n = cat_s scaler_s(deg_n) * cat[mean, min, max, std]_{e->n}(m_e)
+//     Z_n   = cat[x_n, agg_n]                       (input of post_nn)
+// The concat-linear decomposition pre_nn(cat[x_i,x_j,e]) = A[i] + B[j] + C_e,
+// with A|B = x @ [W_i;W_j]^T computed at NODE level (N << E), turns the
+// per-edge GEMM into two gathers. This kernel fuses: gather A[dst], B[src],
+// add C_e, multiply by the radial gate G_e, and the 4-way segment statistics
+// + 4 degree scalers + the concat with x, so m_e never touches HBM in the
+// forward pass.  Edges are CSR-sorted by destination: one contiguous range
+// per node, no atomics, deterministic.
+//
+// The backward recomputes m_e from (A, B, C, G), derives dm_e from the saved
+// statistics (mean/std are read back from Z's identity block), and emits
+//   dpre_e = dm_e * G_e      (== dC_e; dA = segment-sum over dst, fused here;
+//                             dB = segment-sum over src, done by seg_sum with the
+//                             by-source permutation)
+//   dG_e   = dm_e * pre_e
+#include "common.h"
+
+namespace hy {
+
+template <int VEC>
+struct Vec {
+  float v[VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ Vec<VEC> ld(const float* p) {
+  Vec<VEC> r;
+  if constexpr (VEC == 4) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
+  }
+  return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void st(float* p, const Vec<VEC>& r) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) p[i] = r.v[i];
+  }
+}
+
+constexpr float kStdEps = 1e-5f;
+
+// AB: [N, ldab] with A at column offset 0 and B at column offset F.
+template <int VEC>
+__global__ void __launch_bounds__(256) pna_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ AB, int ldab, const float* __restrict__ C,
+    const float* __restrict__ G, const int* __restrict__ src, const int* __restrict__ rowptr,
+    float* __restrict__ Z, int* __restrict__ amin, int* __restrict__ amax, int N, int F, float avg_log,
+    float avg_lin, int tpr, int rpb) {
+  const int n = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int c = threadIdx.x % tpr;
+  if (n >= N) return;
+  const int beg = rowptr[n], end = rowptr[n + 1];
+  const int cnt = end - beg;
+  const float d = (float)max(cnt, 1);
+  const float lg = logf(d + 1.f);
+  const float sc[4] = {1.f, lg / avg_log, avg_log / lg, d / avg_lin};
+  const int ldz = 17 * F;
+  const int nv = F / VEC;
+  for (int v = c; v < nv; v += tpr) {
+    const int f0 = v * VEC;
+    const Vec<VEC> a = ld<VEC>(AB + (int64_t)n * ldab + f0);
+    Vec<VEC> s, s2, mn, mx;
+    int imn[VEC], imx[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      s.v[i] = 0.f; s2.v[i] = 0.f; mn.v[i] = INFINITY; mx.v[i] = -INFINITY; imn[i] = -1; imx[i] = -1;
+    }
+    for (int e = beg; e < end; ++e) {
+      const int j = src[e];
+      const Vec<VEC> b = ld<VEC>(AB + (int64_t)j * ldab + F + f0);
+      Vec<VEC> cc, g;
+      if (C) cc = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc.v[i] = 0.f; }
+      if (G) g = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g.v[i] = 1.f; }
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float m = (a.v[i] + b.v[i] + cc.v[i]) * g.v[i];
+        s.v[i] += m;
+        s2.v[i] = fmaf(m, m, s2.v[i]);
+        if (m < mn.v[i]) { mn.v[i] = m; imn[i] = e; }
+        if (m > mx.v[i]) { mx.v[i] = m; imx[i] = e; }
+      }
+    }
+    Vec<VEC> mean, sd;
+    const float invc = 1.f / d;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mean.v[i] = s.v[i] * invc;
+      const float var = s2.v[i] * invc - mean.v[i] * mean.v[i];
+      float t = sqrtf(fmaxf(var, kStdEps));
+      sd.v[i] = (t <= sqrtf(kStdEps)) ? 0.f : t;
+      if (cnt == 0) { mn.v[i] = 0.f; mx.v[i] = 0.f; }
+    }
+    float* zr = Z + (int64_t)n * ldz;
+    st<VEC>(zr + f0, ld<VEC>(x + (int64_t)n * F + f0));
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      float* zb = zr + F + sidx * 4 * F + f0;
+      Vec<VEC> t0, t1, t2, t3;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        t0.v[i] = mean.v[i] * sc[sidx];
+        t1.v[i] = mn.v[i] * sc[sidx];
+        t2.v[i] = mx.v[i] * sc[sidx];
+        t3.v[i] = sd.v[i] * sc[sidx];
+      }
+      st<VEC>(zb, t0);
+      st<VEC>(zb + F, t1);
+      st<VEC>(zb + 2 * F, t2);
+      st<VEC>(zb + 3 * F, t3);
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      amin[(int64_t)n * F + f0 + i] = imn[i];
+      amax[(int64_t)n * F + f0 + i] = imx[i];
+    }
+  }
+}
+
+template <int VEC>
+__global__ void __launch_bounds__(256) pna_bwd_kernel(
+    const float* __restrict__ dZ, const float* __restrict__ Z, const float* __restrict__ AB, int ldab,
+    const float* __restrict__ C, const float* __restrict__ G, const int* __restrict__ src,
+    const int* __restrict__ rowptr, const int* __restrict__ amin, const int* __restrict__ amax,
+    float* __restrict__ dpre, float* __restrict__ dG, float* __restrict__ dA, int N, int F, float avg_log,
+    float avg_lin, int tpr, int rpb) {
+  const int n = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int c = threadIdx.x % tpr;
+  if (n >= N) return;
+  const int beg = rowptr[n], end = rowptr[n + 1];
+  const int cnt = end - beg;
+  const float d = (float)max(cnt, 1);
+  const float lg = logf(d + 1.f);
+  const float sc[4] = {1.f, lg / avg_log, avg_log / lg, d / avg_lin};
+  const int ldz = 17 * F;
+  const int nv = F / VEC;
+  const float invc = 1.f / d;
+  for (int v = c; v < nv; v += tpr) {
+    const int f0 = v * VEC;
+    const float* dzr = dZ + (int64_t)n * ldz + F + f0;
+    Vec<VEC> dmean, dmin, dmax, dstd;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { dmean.v[i] = 0.f; dmin.v[i] = 0.f; dmax.v[i] = 0.f; dstd.v[i] = 0.f; }
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const float* b = dzr + sidx * 4 * F;
+      const Vec<VEC> g0 = ld<VEC>(b), g1 = ld<VEC>(b + F), g2 = ld<VEC>(b + 2 * F), g3 = ld<VEC>(b + 3 * F);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        dmean.v[i] = fmaf(sc[sidx], g0.v[i], dmean.v[i]);
+        dmin.v[i] = fmaf(sc[sidx], g1.v[i], dmin.v[i]);
+        dmax.v[i] = fmaf(sc[sidx], g2.v[i], dmax.v[i]);
+        dstd.v[i] = fmaf(sc[sidx], g3.v[i], dstd.v[i]);
+      }
+    }
+    const float* zr = Z + (int64_t)n * ldz + F + f0;  // identity block
+    const Vec<VEC> mean = ld<VEC>(zr);
+    const Vec<VEC> sd = ld<VEC>(zr + 3 * F);
+    Vec<VEC> kstd;  // d std / d m_e = (m_e - mean) * kstd
+    int imn[VEC], imx[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      kstd.v[i] = sd.v[i] > 0.f ? dstd.v[i] * invc / sd.v[i] : 0.f;
+      dmean.v[i] *= invc;
+      imn[i] = amin[(int64_t)n * F + f0 + i];
+      imx[i] = amax[(int64_t)n * F + f0 + i];
+    }
+    const Vec<VEC> a = ld<VEC>(AB + (int64_t)n * ldab + f0);
+    Vec<VEC> da;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) da.v[i] = 0.f;
+    for (int e = beg; e < end; ++e) {
+      const int j = src[e];
+      const Vec<VEC> b = ld<VEC>(AB + (int64_t)j * ldab + F + f0);
+      Vec<VEC> cc, g;
+      if (C) cc = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc.v[i] = 0.f; }
+      if (G) g = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g.v[i] = 1.f; }
+      Vec<VEC> dp, dg;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float pre = a.v[i] + b.v[i] + cc.v[i];
+        const float m = pre * g.v[i];
+        float dm = dmean.v[i] + (m - mean.v[i]) * kstd.v[i];
+        if (e == imn[i]) dm += dmin.v[i];
+        if (e == imx[i]) dm += dmax.v[i];
+        dp.v[i] = dm * g.v[i];
+        dg.v[i] = dm * pre;
+        da.v[i] += dp.v[i];
+      }
+      st<VEC>(dpre + (int64_t)e * F + f0, dp);
+      if (dG) st<VEC>(dG + (int64_t)e * F + f0, dg);
+    }
+    st<VEC>(dA + (int64_t)n * F + f0, da);
+  }
+}
+
+static const float* opt_edge_ptr(const c10::optional<at::Tensor>& t, int64_t E, int F, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  HY_CHECK_F32(*t);
+  HY_CHECK(t->is_contiguous(), name, " must be contiguous");
+  HY_CHECK(t->dim() == 2 && t->size(0) == E && t->size(1) == F, name, " must be [E, F]");
+  return t->data_ptr<float>();
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_fwd(const at::Tensor& x, const at::Tensor& AB,
+                                                       const c10::optional<at::Tensor>& C_,
+                                                       const c10::optional<at::Tensor>& G_,
+                                                       const at::Tensor& src, const at::Tensor& rowptr,
+                                                       double avg_log, double avg_lin) {
+  HY_CHECK_CUDA(x);
+  HY_CHECK_F32(x); HY_CHECK_F32(AB);
+  HY_CHECK_I32(src); HY_CHECK_I32(rowptr);
+  HY_CHECK_CONTIG(x);
+  HY_CHECK(AB.stride(1) == 1, "AB rows must be contiguous");
+  const int64_t N = x.size(0);
+  const int F = (int)x.size(1);
+  HY_CHECK(AB.size(0) == N && AB.size(1) == 2 * F, "AB must be [N, 2F]");
+  const float* Cp = opt_edge_ptr(C_, src.numel(), F, "C");
+  const float* Gp = opt_edge_ptr(G_, src.numel(), F, "G");
+  HY_CHECK(rowptr.numel() == N + 1, "rowptr must be [N+1]");
+  auto Z = at::empty({N, 17 * F}, x.options());
+  auto amin = at::empty({N, F}, x.options().dtype(at::kInt));
+  auto amax = at::empty({N, F}, x.options().dtype(at::kInt));
+  if (N == 0) return {Z, amin, amax};
+  const int ldab = (int)AB.stride(0);
+  const bool v4 = (F % 4 == 0) && (ldab % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0);
+  auto g = row_geom(N, v4 ? F : 4 * F);
+  if (v4)
+    pna_fwd_kernel<4><<<g.blocks, 256, 0, stream()>>>(
+        x.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp, Gp,
+        src.data_ptr<int>(), rowptr.data_ptr<int>(), Z.data_ptr<float>(), amin.data_ptr<int>(),
+        amax.data_ptr<int>(), N, F, (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+  else
+    pna_fwd_kernel<1><<<g.blocks, 256, 0, stream()>>>(
+        x.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp, Gp,
+        src.data_ptr<int>(), rowptr.data_ptr<int>(), Z.data_ptr<float>(), amin.data_ptr<int>(),
+        amax.data_ptr<int>(), N, F, (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+  return {Z, amin, amax};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_bwd(const at::Tensor& dZ_, const at::Tensor& Z,
+                                                       const at::Tensor& AB, const c10::optional<at::Tensor>& C_,
+                                                       const c10::optional<at::Tensor>& G_, const at::Tensor& src,
+                                                       const at::Tensor& rowptr, const at::Tensor& amin,
+                                                       const at::Tensor& amax, double avg_log,
+                                                       double avg_lin) {
+  auto dZ = dZ_.contiguous();
+  HY_CHECK_CUDA(dZ);
+  const int64_t N = Z.size(0);
+  const int F = (int)(Z.size(1) / 17);
+  const int64_t E = src.numel();
+  const float* Cp = opt_edge_ptr(C_, E, F, "C");
+  const float* Gp = opt_edge_ptr(G_, E, F, "G");
+  auto dpre = at::empty({E, F}, Z.options());
+  auto dG = Gp ? at::empty({E, F}, Z.options()) : at::empty({0}, Z.options());
+  auto dA = at::empty({N, F}, Z.options());
+  if (N == 0) return {dpre, dG, dA};
+  const int ldab = (int)AB.stride(0);
+  const bool v4 = (F % 4 == 0) && (ldab % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0);
+  auto g = row_geom(N, v4 ? F : 4 * F);
+  if (v4)
+    pna_bwd_kernel<4><<<g.blocks, 256, 0, stream()>>>(
+        dZ.data_ptr<float>(), Z.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp,
+        Gp, src.data_ptr<int>(), rowptr.data_ptr<int>(), amin.data_ptr<int>(),
+        amax.data_ptr<int>(), dpre.data_ptr<float>(), Gp ? dG.data_ptr<float>() : nullptr, dA.data_ptr<float>(), N, F,
+        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+  else
+    pna_bwd_kernel<1><<<g.blocks, 256, 0, stream()>>>(
+        dZ.data_ptr<float>(), Z.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp,
+        Gp, src.data_ptr<int>(), rowptr.data_ptr<int>(), amin.data_ptr<int>(),
+        amax.data_ptr<int>(), dpre.data_ptr<float>(), Gp ? dG.data_ptr<float>() : nullptr, dA.data_ptr<float>(), N, F,
+        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+  return {dpre, dG, dA};
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def(
+      "pna_fwd(Tensor x, Tensor AB, Tensor? C, Tensor? G, Tensor src, Tensor rowptr, float avg_log, "
+      "float avg_lin) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "pna_bwd(Tensor dZ, Tensor Z, Tensor AB, Tensor? C, Tensor? G, Tensor src, Tensor rowptr, Tensor amin, "
+      "Tensor amax, float avg_log, float avg_lin) -> (Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("pna_fwd", hy::pna_fwd);
+  m.impl("pna_bwd", hy::pna_bwd);
+}

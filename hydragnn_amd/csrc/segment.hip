@@ -1,0 +1,251 @@
+// CSR segment reductions, row gathers and arg-scatters (gfx950).
+//
+// These are the atomic-free replacements for torch_scatter / PyG aggregation
+// used by every message-passing stack (reference: torch_scatter calls at
+// hydragnn/models/Base.py:599, EGCLStack.py:292-298, PAINNStack.py:256-257,
+// mace_utils/modules/blocks.py:380-382, and PyG MessagePassing aggr="add"/"mean"/
+// "min"/"max").  Because batches are CSR-sorted by destination once in the
+// collator, every reduction reads a contiguous edge range per node: results are
+// bitwise deterministic and need no float atomics.
+//
+// Backward duality (used by ops/segment.py to get arbitrary-order derivatives):
+//   seg_sum(x, rowptr)             <->  gather_rows(g, seg_id)
+//   gather_rows(x, idx)            <->  seg_sum(g, idx_rowptr, idx_perm)
+//   seg_minmax(x) -> (out, arg)    <->  scatter_arg(g, arg)  /  gather_arg(x, arg)
+#include "common.h"
+
+namespace hy {
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = float4;
+  static __device__ __forceinline__ T zero() { return f4zero(); }
+  static __device__ __forceinline__ T add(T a, T b) { return f4add(a, b); }
+};
+template <>
+struct VecT<1> {
+  using T = float;
+  static __device__ __forceinline__ T zero() { return 0.f; }
+  static __device__ __forceinline__ T add(T a, T b) { return a + b; }
+};
+
+// out[n, :] = sum_{e in [rowptr[n], rowptr[n+1])} x[perm ? perm[e] : e, :] * (scale? 1/deg : 1)
+template <int VEC, bool MEAN>
+__global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ x,
+                                                      const int* __restrict__ rowptr,
+                                                      const int* __restrict__ perm,
+                                                      float* __restrict__ out, int N, int F,
+                                                      int tpr, int rpb) {
+  using V = VecT<VEC>;
+  using T = typename V::T;
+  const int r = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int c = threadIdx.x % tpr;
+  if (r >= N) return;
+  const int beg = rowptr[r], end = rowptr[r + 1];
+  const int nv = F / VEC;
+  const float inv = MEAN ? 1.f / (float)max(end - beg, 1) : 1.f;
+  for (int v = c; v < nv; v += tpr) {
+    T a0 = V::zero(), a1 = V::zero();
+    int e = beg;
+    for (; e + 1 < end; e += 2) {
+      const int r0 = perm ? perm[e] : e;
+      const int r1 = perm ? perm[e + 1] : e + 1;
+      a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
+      a1 = V::add(a1, reinterpret_cast<const T*>(x + (int64_t)r1 * F)[v]);
+    }
+    if (e < end) {
+      const int r0 = perm ? perm[e] : e;
+      a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
+    }
+    T a = V::add(a0, a1);
+    if constexpr (MEAN) {
+      if constexpr (VEC == 4) a = f4scale(a, inv); else a *= inv;
+    }
+    reinterpret_cast<T*>(out + (int64_t)r * F)[v] = a;
+  }
+}
+
+// out[e, :] = x[idx[e], :]
+template <int VEC>
+__global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ x,
+                                                          const int* __restrict__ idx,
+                                                          float* __restrict__ out, int E, int F,
+                                                          int tpr, int rpb) {
+  using T = typename VecT<VEC>::T;
+  const int r = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int c = threadIdx.x % tpr;
+  if (r >= E) return;
+  const int64_t s = idx[r];
+  const int nv = F / VEC;
+  for (int v = c; v < nv; v += tpr)
+    reinterpret_cast<T*>(out + (int64_t)r * F)[v] = reinterpret_cast<const T*>(x + s * F)[v];
+}
+
+// Segment min/max with argument (edge position, -1 for an empty segment -> value 0,
+// matching PyG's scatter(reduce="min"/"max") fill for isolated nodes).
+template <bool IS_MAX>
+__global__ void __launch_bounds__(256) seg_minmax_kernel(const float* __restrict__ x,
+                                                         const int* __restrict__ rowptr,
+                                                         float* __restrict__ out,
+                                                         int* __restrict__ arg, int N, int F) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * F) return;
+  const int n = (int)(t / F), f = (int)(t % F);
+  const int beg = rowptr[n], end = rowptr[n + 1];
+  float best = IS_MAX ? -INFINITY : INFINITY;
+  int besti = -1;
+  for (int e = beg; e < end; ++e) {
+    const float v = x[(int64_t)e * F + f];
+    if (IS_MAX ? (v > best) : (v < best)) { best = v; besti = e; }
+  }
+  out[t] = besti < 0 ? 0.f : best;
+  arg[t] = besti;
+}
+
+// out[E, F] = 0; out[arg[n,f], f] = g[n,f]   (segments are disjoint -> no conflicts)
+__global__ void __launch_bounds__(256) scatter_arg_kernel(const float* __restrict__ g,
+                                                          const int* __restrict__ arg,
+                                                          float* __restrict__ out, int N, int F) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * F) return;
+  const int a = arg[t];
+  if (a >= 0) out[(int64_t)a * F + (t % F)] = g[t];
+}
+
+// out[n,f] = x[arg[n,f], f] (0 when arg < 0)
+__global__ void __launch_bounds__(256) gather_arg_kernel(const float* __restrict__ x,
+                                                         const int* __restrict__ arg,
+                                                         float* __restrict__ out, int N, int F) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * F) return;
+  const int a = arg[t];
+  out[t] = a >= 0 ? x[(int64_t)a * F + (t % F)] : 0.f;
+}
+
+// ---------------------------------------------------------------- host side
+
+static at::Tensor as2d(const at::Tensor& x) { return x.dim() == 1 ? x.unsqueeze(1) : x; }
+
+at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm,
+                   int64_t N, bool mean) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(rowptr.numel() == N + 1, "rowptr must have N+1 entries");
+  const int F = (int)x.size(1);
+  auto out = at::empty({N, F}, x.options());
+  if (N == 0 || F == 0) return out;
+  const int* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    HY_CHECK_I32(*perm);
+    pp = perm->data_ptr<int>();
+  }
+  const bool v4 = (F % 4 == 0);
+  auto g = row_geom(N, v4 ? F : F * 4);
+  if (v4) {
+    if (mean)
+      seg_sum_kernel<4, true><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
+                                                              out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+    else
+      seg_sum_kernel<4, false><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
+                                                               out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+  } else {
+    if (mean)
+      seg_sum_kernel<1, true><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
+                                                              out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+    else
+      seg_sum_kernel<1, false><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
+                                                               out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+  }
+  return x_.dim() == 1 ? out.squeeze(1) : out;
+}
+
+at::Tensor gather_rows(const at::Tensor& x_, const at::Tensor& idx) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_I32(idx);
+  const int64_t E = idx.numel();
+  const int F = (int)x.size(1);
+  auto out = at::empty({E, F}, x.options());
+  if (E == 0 || F == 0) return x_.dim() == 1 ? out.squeeze(1) : out;
+  const bool v4 = (F % 4 == 0);
+  auto g = row_geom(E, v4 ? F : F * 4);
+  if (v4)
+    gather_rows_kernel<4><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), idx.data_ptr<int>(),
+                                                         out.data_ptr<float>(), E, F, g.tpr, g.rows_per_block);
+  else
+    gather_rows_kernel<1><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), idx.data_ptr<int>(),
+                                                         out.data_ptr<float>(), E, F, g.tpr, g.rows_per_block);
+  return x_.dim() == 1 ? out.squeeze(1) : out;
+}
+
+std::tuple<at::Tensor, at::Tensor> seg_minmax(const at::Tensor& x_, const at::Tensor& rowptr, int64_t N,
+                                              bool is_max) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_I32(rowptr);
+  const int F = (int)x.size(1);
+  auto out = at::empty({N, F}, x.options());
+  auto arg = at::empty({N, F}, x.options().dtype(at::kInt));
+  const int64_t tot = N * F;
+  if (tot > 0) {
+    if (is_max)
+      seg_minmax_kernel<true><<<ceil_div(tot, 256), 256, 0, stream()>>>(
+          x.data_ptr<float>(), rowptr.data_ptr<int>(), out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
+    else
+      seg_minmax_kernel<false><<<ceil_div(tot, 256), 256, 0, stream()>>>(
+          x.data_ptr<float>(), rowptr.data_ptr<int>(), out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
+  }
+  return {out, arg};
+}
+
+at::Tensor scatter_arg(const at::Tensor& g_, const at::Tensor& arg, int64_t E) {
+  HY_CHECK_CUDA(g_);
+  auto g = g_.contiguous();
+  HY_CHECK_F32(g);
+  HY_CHECK_I32(arg);
+  const int64_t N = g.size(0);
+  const int F = (int)g.size(1);
+  auto out = at::zeros({E, F}, g.options());
+  if (N * F > 0)
+    scatter_arg_kernel<<<ceil_div(N * F, 256), 256, 0, stream()>>>(g.data_ptr<float>(), arg.data_ptr<int>(),
+                                                                  out.data_ptr<float>(), N, F);
+  return out;
+}
+
+at::Tensor gather_arg(const at::Tensor& x_, const at::Tensor& arg) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_I32(arg);
+  const int64_t N = arg.size(0);
+  const int F = (int)arg.size(1);
+  auto out = at::empty({N, F}, x.options());
+  if (N * F > 0)
+    gather_arg_kernel<<<ceil_div(N * F, 256), 256, 0, stream()>>>(x.data_ptr<float>(), arg.data_ptr<int>(),
+                                                                 out.data_ptr<float>(), N, F);
+  return out;
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("seg_sum(Tensor x, Tensor rowptr, Tensor? perm, int N, bool mean) -> Tensor");
+  m.def("gather_rows(Tensor x, Tensor idx) -> Tensor");
+  m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
+  m.def("scatter_arg(Tensor g, Tensor arg, int E) -> Tensor");
+  m.def("gather_arg(Tensor x, Tensor arg) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("seg_sum", hy::seg_sum);
+  m.impl("gather_rows", hy::gather_rows);
+  m.impl("seg_minmax", hy::seg_minmax);
+  m.impl("scatter_arg", hy::scatter_arg);
+  m.impl("gather_arg", hy::gather_arg);
+}

@@ -1,0 +1,311 @@
+"""HBM-resident graph dataset with host-indexed GPU batch assembly.
+
+MI355X design (SURVEY §7.1 decision 3): with 288 GB of HBM per GPU an entire
+training shard lives on the device.  Every per-sample tensor is concatenated
+once into a field-major pool (node fields [sum n, F], edge fields [sum e, F],
+graph fields [S, F]); per-sample offsets are kept on the HOST.  Building a
+mini-batch then needs no device->host synchronisation:
+
+1. ``plan()`` (host, numpy, ~100 us): from offsets alone it computes the node /
+   edge row lists, destination CSR (edges are pre-sorted by destination inside
+   every sample), source CSR (per-sample stable source permutations are
+   precomputed at load time and concatenated with edge offsets), ``batch`` /
+   ``ptr`` and the attention segments, packed into ONE int32 array;
+2. that array travels in ONE pinned asynchronous H2D copy;
+3. ``assemble()`` (device only) gathers the feature rows out of the HBM pool.
+
+This replaces the reference's CPU DataLoader + PyG ``Batch.from_data_list`` +
+per-step H2D of every feature tensor (``train_validate_test.py:514``) and the
+host-side ``get_head_indices`` loops (``:316-379``): per-head targets come out
+as ready [G, d] / [N, d] tensors.
+
+Static padding (``Np``/``Ep``/``Gp``) produces fixed-shape batches so that
+``assemble`` + forward + backward + optimizer can be captured once in a hipGraph
+and replayed (``train/step.py``): padded nodes form an extra dummy graph (and an
+extra attention segment), padded edges connect the last two padded nodes,
+padded nodes sit at distinct finite positions (no zero-length edges), and the
+device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked reductions.
+"""
+import numpy as np
+import torch
+
+from ..ops.segment import SegIndex
+from .graph import GraphBatch
+
+NODE_KEYS = ("x", "pos", "pe", "forces")
+EDGE_KEYS = ("edge_attr", "rel_pe", "edge_shifts")
+
+_PLAN_FIELDS = ("node_rows", "edge_rows", "src", "dst", "sperm", "rowptr", "srowptr", "batch", "gptr",
+                "aseg_id", "aseg_ptr", "sample_idx", "scalars")
+
+
+class Layout:
+    """Static sizes of one packed batch plan."""
+
+    __slots__ = ("Np", "Ep", "Gp", "padded", "attn_scope", "sizes", "total")
+
+    def __init__(self, Np, Ep, Gp, padded, attn_scope):
+        self.Np, self.Ep, self.Gp, self.padded, self.attn_scope = Np, Ep, Gp, padded, attn_scope
+        na = 3 if attn_scope == "batch" else Gp + 1
+        self.sizes = [Np, Ep, Ep, Ep, Ep, Np + 1, Np + 1, Np, Gp + 1, Np, na, Gp, 4]
+        self.total = int(sum(self.sizes))
+
+    def key(self):
+        return (self.Np, self.Ep, self.Gp, self.padded, self.attn_scope)
+
+
+class DeviceGraphStore:
+    def __init__(self, samples, device, head_types=None, head_dims=None, node_keys=NODE_KEYS, edge_keys=EDGE_KEYS,
+                 graph_keys=("energy",), dtype=torch.float32, attn_scope="batch"):
+        self.device = torch.device(device)
+        self.attn_scope = attn_scope
+        S = len(samples)
+        self.num_samples = S
+        nn_ = np.array([s.num_nodes for s in samples], dtype=np.int64)
+        ne = np.array([s.num_edges for s in samples], dtype=np.int64)
+        self.n_nodes, self.n_edges = nn_, ne
+        self.node_off = np.zeros(S + 1, dtype=np.int64)
+        self.node_off[1:] = np.cumsum(nn_)
+        self.edge_off = np.zeros(S + 1, dtype=np.int64)
+        self.edge_off[1:] = np.cumsum(ne)
+        for s in samples:
+            s.sort_edges_by_dst()
+        self.src_local = np.concatenate([s.edge_index[0].numpy() for s in samples]).astype(np.int64)
+        self.dst_local = np.concatenate([s.edge_index[1].numpy() for s in samples]).astype(np.int64)
+        self.sperm_local = np.concatenate(
+            [np.argsort(s.edge_index[0].numpy(), kind="stable") for s in samples]).astype(np.int64)
+        self.node_keys = [k for k in node_keys if all(k in s for s in samples)]
+        self.edge_keys = [k for k in edge_keys if all(k in s for s in samples)]
+        self.graph_keys = [k for k in graph_keys if all(k in s for s in samples)]
+        self.fields = {}
+        for k in self.node_keys + self.edge_keys:
+            self.fields[k] = torch.cat([s[k].reshape(s[k].shape[0], -1).to(dtype) for s in samples], 0).to(self.device)
+        for k in self.graph_keys:
+            self.fields[k] = torch.stack([s[k].reshape(-1).to(dtype) for s in samples], 0).to(self.device)
+        self.head_types = list(head_types) if head_types is not None else None
+        self.head_dims = list(head_dims) if head_dims is not None else None
+        self.targets_graph, self.targets_node = {}, {}
+        if self.head_types is not None and all("y" in s for s in samples):
+            for ih, (t, d) in enumerate(zip(self.head_types, self.head_dims)):
+                vals = []
+                for s in samples:
+                    yl = s["y_loc"].view(-1)
+                    vals.append(s["y"].view(-1)[int(yl[ih]):int(yl[ih + 1])].view(-1, d).to(dtype))
+                tgt = torch.cat(vals, 0).to(self.device)
+                (self.targets_graph if t == "graph" else self.targets_node)[ih] = tgt
+        self.dataset_name = None
+        if all("dataset_name" in s for s in samples):
+            self.dataset_name = np.array([int(s["dataset_name"].view(-1)[0]) for s in samples], dtype=np.int64)
+            self.dataset_name_dev = torch.from_numpy(self.dataset_name).to(self.device)
+        self._ring = []
+        self._ring_pos = 0
+
+    def __len__(self):
+        return self.num_samples
+
+    def memory_bytes(self):
+        return sum(t.numel() * t.element_size() for t in self.fields.values())
+
+    # ------------------------------------------------------------------ host side
+    def sizes_of(self, indices):
+        idx = np.asarray(indices, dtype=np.int64)
+        return int(self.n_nodes[idx].sum()), int(self.n_edges[idx].sum())
+
+    def layout(self, indices, Np=None, Ep=None, Gp=None):
+        N, E = self.sizes_of(indices)
+        G = len(indices)
+        padded = Np is not None
+        if padded:
+            Np = max(Np, N + 2)
+            Ep = max(Ep if Ep is not None else E, E)
+            Gp = max(Gp if Gp is not None else G + 1, G + 1)
+        else:
+            Np, Ep, Gp = N, E, G
+        return Layout(Np, Ep, Gp, padded, self.attn_scope)
+
+    def plan(self, indices, lay, out=None):
+        """Fill the packed int32 plan for ``indices`` (numpy view ``out`` of size lay.total)."""
+        idx = np.asarray(indices, dtype=np.int64)
+        G = idx.size
+        n = self.n_nodes[idx]
+        e = self.n_edges[idx]
+        N, E = int(n.sum()), int(e.sum())
+        Np, Ep, Gp = lay.Np, lay.Ep, lay.Gp
+        ptr = np.zeros(G + 1, dtype=np.int64)
+        ptr[1:] = np.cumsum(n)
+        eptr = np.zeros(G + 1, dtype=np.int64)
+        eptr[1:] = np.cumsum(e)
+        edge_rows = _ranges(self.edge_off[idx], e)
+        nbase_e = np.repeat(ptr[:-1], e)
+        if out is None:
+            out = np.empty(lay.total, dtype=np.int32)
+        views = []
+        o = 0
+        for sz in lay.sizes:
+            views.append(out[o:o + sz])
+            o += sz
+        (node_rows, erows, src, dst, sperm, rowptr, srowptr, batch, gptr, aseg_id, aseg_ptr, sidx, scal) = views
+        node_rows[:N] = _ranges(self.node_off[idx], n)
+        erows[:E] = edge_rows
+        src[:E] = self.src_local[edge_rows] + nbase_e
+        dst[:E] = self.dst_local[edge_rows] + nbase_e
+        sperm[:E] = self.sperm_local[edge_rows] + np.repeat(eptr[:-1], e)
+        batch[:N] = np.repeat(np.arange(G), n)
+        gptr[:G + 1] = ptr
+        sidx[:G] = idx
+        if lay.padded:
+            node_rows[N:] = -1
+            erows[E:] = -1
+            src[E:] = Np - 2
+            dst[E:] = Np - 1
+            sperm[E:] = np.arange(E, Ep)
+            batch[N:] = G
+            gptr[G + 1:] = Np
+            sidx[G:] = 0
+        cnt = np.bincount(dst, minlength=Np)
+        rowptr[0] = 0
+        np.cumsum(cnt, out=rowptr[1:])
+        scnt = np.bincount(src, minlength=Np)
+        srowptr[0] = 0
+        np.cumsum(scnt, out=srowptr[1:])
+        if lay.attn_scope == "batch":
+            aseg_id[:N] = 0
+            aseg_id[N:] = 1
+            aseg_ptr[:] = (0, N, Np)
+        else:
+            aseg_id[:] = batch
+            aseg_ptr[:] = gptr
+        scal[:] = (N, G, E, 0)
+        return out
+
+    def _slot(self, n, ring=4):
+        cuda = self.device.type == "cuda"
+        if len(self._ring) < ring:
+            self._ring.append([None, None])
+            slot = self._ring[-1]
+        else:
+            slot = self._ring[self._ring_pos % ring]
+            self._ring_pos += 1
+        if slot[1] is not None:
+            slot[1].synchronize()  # the async copy that last read this pinned buffer is done
+        if slot[0] is None or slot[0].numel() < n:
+            slot[0] = torch.empty(max(n, 1 << 16), dtype=torch.int32, pin_memory=cuda)
+        slot[1] = torch.cuda.Event() if cuda else None
+        return slot
+
+    def upload(self, indices, lay, dev_buf=None):
+        """plan() into a pinned buffer and copy it (async) to ``dev_buf`` (or a new device tensor)."""
+        slot = self._slot(lay.total)
+        host = slot[0][:lay.total]
+        self.plan(indices, lay, host.numpy())
+        if self.device.type == "cuda":
+            if dev_buf is None:
+                dev_buf = host.to(self.device, non_blocking=True)
+            else:
+                dev_buf[:lay.total].copy_(host, non_blocking=True)
+            slot[1].record()
+        else:
+            if dev_buf is None:
+                dev_buf = host.clone()
+            else:
+                dev_buf[:lay.total].copy_(host)
+        return dev_buf
+
+    # ------------------------------------------------------------------ device side
+    def assemble(self, dev_buf, lay, host_ids=None):
+        """Build a GraphBatch from a packed device plan (device ops only; graph-capturable)."""
+        views = []
+        o = 0
+        for sz in lay.sizes:
+            views.append(dev_buf[o:o + sz])
+            o += sz
+        (node_rows, erows, src, dst, sperm, rowptr, srowptr, batch, gptr, aseg_id, aseg_ptr, sidx, scal) = views
+        Np, Ep, Gp = lay.Np, lay.Ep, lay.Gp
+        out = {}
+        nrow = node_rows.clamp(min=0).long() if lay.padded else node_rows.long()
+        erow = erows.clamp(min=0).long() if lay.padded else erows.long()
+        sid = sidx.long()
+        nvalid = scal[0]
+        gvalid = scal[1]
+        if lay.padded:
+            nmask = (node_rows >= 0).unsqueeze(1)
+            emask = (erows >= 0).unsqueeze(1)
+        for k in self.node_keys:
+            v = self.fields[k].index_select(0, nrow)
+            if lay.padded:
+                v = v * nmask.to(v.dtype)
+                if k == "pos":
+                    # padded nodes at distinct finite positions: padded edges never have zero length
+                    r = torch.arange(Np, device=v.device, dtype=v.dtype) - nvalid.to(v.dtype)
+                    padpos = torch.stack([2.0 * (r + 1.0), torch.zeros_like(r), torch.zeros_like(r)], 1)
+                    v = v + padpos * (~nmask).to(v.dtype)
+            out[k] = v
+        for k in self.edge_keys:
+            v = self.fields[k].index_select(0, erow)
+            if lay.padded:
+                v = v * emask.to(v.dtype)
+            out[k] = v
+        gmask = None
+        if lay.padded:
+            gmask = torch.arange(Gp, device=dev_buf.device) < gvalid
+        for k in self.graph_keys:
+            v = self.fields[k].index_select(0, sid)
+            if lay.padded:
+                v = v * gmask.view(-1, *([1] * (v.dim() - 1))).to(v.dtype)
+            out[k] = v
+        targets = []
+        if self.head_types is not None:
+            for ih, t in enumerate(self.head_types):
+                if t == "graph" and ih in self.targets_graph:
+                    v = self.targets_graph[ih].index_select(0, sid)
+                    if lay.padded:
+                        v = v * gmask.unsqueeze(1).to(v.dtype)
+                    targets.append(v)
+                elif ih in self.targets_node:
+                    v = self.targets_node[ih].index_select(0, nrow)
+                    if lay.padded:
+                        v = v * nmask.to(v.dtype)
+                    targets.append(v)
+        b = GraphBatch(**out)
+        s = b._store
+        s["edge_index"] = torch.stack([src.long(), dst.long()], 0)
+        s["num_nodes"] = Np
+        s["num_graphs"] = Gp
+        s["batch"] = batch.long()
+        s["ptr"] = gptr.long()
+        s["dst_si"] = SegIndex(dst, rowptr, None, Np)
+        s["src_si"] = SegIndex(src, srowptr, sperm, Np)
+        s["graph_si"] = SegIndex(batch, gptr, None, Gp)
+        s["attn_seg_id"] = aseg_id
+        s["attn_seg_ptr"] = aseg_ptr
+        s["targets"] = targets
+        if lay.padded:
+            s["num_valid"] = nvalid
+            s["graph_mask"] = gmask
+            s["node_mask"] = nmask.view(-1)
+        if self.dataset_name is not None:
+            dn = self.dataset_name_dev.index_select(0, sid)
+            if lay.padded:
+                dn = torch.where(gmask, dn, torch.full_like(dn, -1))
+            s["dataset_name"] = dn.view(-1, 1)
+            if host_ids is not None:
+                s["dataset_ids_host"] = host_ids
+        return b
+
+    def batch(self, indices, Np=None, Ep=None, Gp=None):
+        lay = self.layout(indices, Np, Ep, Gp)
+        dev = self.upload(indices, lay)
+        host_ids = None
+        if self.dataset_name is not None:
+            host_ids = sorted(set(self.dataset_name[np.asarray(indices)].tolist()))
+        return self.assemble(dev, lay, host_ids)
+
+
+def _ranges(starts, counts):
+    """Concatenate arange(s, s+c) for every (s, c) without a Python loop."""
+    counts = np.asarray(counts, dtype=np.int64)
+    tot = int(counts.sum())
+    if tot == 0:
+        return np.zeros(0, dtype=np.int64)
+    shift = np.asarray(starts, dtype=np.int64) - np.concatenate([[0], np.cumsum(counts)[:-1]])
+    return np.repeat(shift, counts) + np.arange(tot, dtype=np.int64)

@@ -1,0 +1,193 @@
+"""Per-sample graph transforms (host reference implementations).
+
+Replaces the PyG transforms used by the reference preprocessing
+(``preprocess/serialized_dataset_loader.py:110-212``,
+``preprocess/graph_samples_checks_and_updates.py:109-413``):
+``RadiusGraph`` / ``RadiusGraphPBC`` (radius graph with ``max_num_neighbors``
+cap), ``Distance`` (edge length, optionally normalised), ``Spherical``,
+``PointPairFeatures``, ``NormalizeRotation``, ``AddLaplacianEigenvectorPE``
+and ``rel_pe``.  Batched GPU versions live in ``ops/graph.py`` (HIP cell-list
+radius graph, batched Jacobi eigensolver); these host versions are the
+oracles and the fallback for CPU preprocessing.
+"""
+import math
+
+import numpy as np
+import torch
+
+
+def radius_graph(pos, r, batch=None, max_num_neighbors=32, loop=False, cap_policy="nearest"):
+    """Edges (j -> i) with ||pos_i - pos_j|| <= r within the same graph.
+
+    ``cap_policy``: "nearest" keeps the closest ``max_num_neighbors`` sources per
+    receiver (``RadiusGraphPBC._limit_neighbors`` semantics); "index" keeps the
+    first found in index order (torch_cluster semantics).  Returns
+    ``edge_index`` [2, E] sorted by destination then distance/index.
+    """
+    pos = torch.as_tensor(pos, dtype=torch.float64)
+    n = pos.shape[0]
+    if batch is None:
+        batch = torch.zeros(n, dtype=torch.long)
+    d = torch.cdist(pos, pos)
+    same = batch.view(-1, 1) == batch.view(1, -1)
+    mask = (d <= r) & same
+    if not loop:
+        mask.fill_diagonal_(False)
+    if n == 0:
+        return torch.zeros(2, 0, dtype=torch.long)
+    if cap_policy == "nearest":
+        key = torch.where(mask, d, torch.full_like(d, float("inf")))
+        k = min(max_num_neighbors, n)
+        vals, nb = torch.topk(key, k, dim=1, largest=False, sorted=True)
+        ok = torch.isfinite(vals)
+        # keep index order inside each receiver's list (stable & deterministic)
+        nb = torch.where(ok, nb, torch.full_like(nb, n))
+        nb, _ = torch.sort(nb, dim=1)
+        ok = nb < n
+    else:
+        # first-found in index order (torch_cluster semantics)
+        csum = torch.cumsum(mask.to(torch.long), dim=1)
+        keep = mask & (csum <= max_num_neighbors)
+        idx = torch.arange(n).view(1, -1).expand(n, n)
+        nb = torch.where(keep, idx, torch.full_like(idx, n))
+        nb, _ = torch.sort(nb, dim=1)
+        nb = nb[:, :max_num_neighbors] if n > max_num_neighbors else nb
+        ok = nb < n
+    dst = torch.arange(n).view(-1, 1).expand_as(nb)[ok]
+    src = nb[ok]
+    return torch.stack([src, dst], 0)
+
+
+def radius_graph_pbc(pos, cell, pbc, r, max_num_neighbors=32, loop=False):
+    """Periodic radius graph over the 27 (or fewer, per non-periodic axis) image
+    cells; returns (edge_index [2,E], edge_shifts [E,3]) with
+    ``pos[dst] - pos[src] + shift`` the minimum-image-consistent vector, nearest
+    ``max_num_neighbors`` kept per receiver (``RadiusGraphPBC``, reference
+    ``graph_samples_checks_and_updates.py:141-343``)."""
+    pos = torch.as_tensor(pos, dtype=torch.float64)
+    cell = torch.as_tensor(cell, dtype=torch.float64).view(3, 3)
+    pbc = [bool(p) for p in torch.as_tensor(pbc).view(-1).tolist()]
+    n = pos.shape[0]
+    # number of images needed per axis: r / (plane spacing)
+    vol = torch.abs(torch.det(cell))
+    reps = []
+    for a in range(3):
+        if not pbc[a]:
+            reps.append(0)
+            continue
+        b, c = cell[(a + 1) % 3], cell[(a + 2) % 3]
+        h = vol / torch.linalg.norm(torch.cross(b, c, dim=0))
+        reps.append(int(math.ceil(r / float(h))))
+    rng = [torch.arange(-k, k + 1, dtype=torch.float64) for k in reps]
+    grid = torch.stack(torch.meshgrid(*rng, indexing="ij"), -1).view(-1, 3)
+    shifts = grid @ cell  # [S,3]
+    # vec[i, j, s] = pos[i] - (pos[j] + shift_s)  -> edge j(+s) -> i with shift = -shift_s
+    srcs, dsts, shs, ds = [], [], [], []
+    for s in range(shifts.shape[0]):
+        diff = pos.view(n, 1, 3) - (pos.view(1, n, 3) + shifts[s])
+        d = torch.linalg.norm(diff, dim=-1)
+        m = d <= r
+        if not loop and bool((grid[s] == 0).all()):
+            m.fill_diagonal_(False)
+        ii, jj = torch.nonzero(m, as_tuple=True)
+        dsts.append(ii)
+        srcs.append(jj)
+        shs.append((-shifts[s]).expand(ii.numel(), 3) * -1.0)
+        ds.append(d[ii, jj])
+    dst = torch.cat(dsts)
+    src = torch.cat(srcs)
+    sh = torch.cat(shs)
+    dist = torch.cat(ds)
+    # cap per receiver: nearest first
+    order = torch.argsort(dst * (dist.max() + 1.0 if dist.numel() else 1.0) + dist)
+    dst, src, sh, dist = dst[order], src[order], sh[order], dist[order]
+    keep = torch.ones_like(dst, dtype=torch.bool)
+    if dst.numel():
+        first = torch.ones_like(dst, dtype=torch.bool)
+        first[1:] = dst[1:] != dst[:-1]
+        idx = torch.arange(dst.numel())
+        start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+        keep = (idx - start) < max_num_neighbors
+    ei = torch.stack([src[keep], dst[keep]], 0)
+    # shift convention: vec = pos[dst] - pos[src] + shift  -> shift = -(image shift of the source)
+    return ei, sh[keep].to(torch.float32) * -1.0
+
+
+def distance(pos, edge_index, shifts=None, norm=True, max_value=None, cat=False, edge_attr=None):
+    """PyG ``Distance``: edge length, optionally divided by max (global max if given)."""
+    vec = pos[edge_index[1]] - pos[edge_index[0]]
+    if shifts is not None:
+        vec = vec + shifts
+    d = torch.linalg.norm(vec, dim=-1, keepdim=True)
+    if norm and d.numel() > 0:
+        d = d / (d.max() if max_value is None else max_value)
+    if cat and edge_attr is not None:
+        return torch.cat([edge_attr.view(edge_attr.shape[0], -1), d.to(edge_attr.dtype)], dim=-1)
+    return d
+
+
+def laplacian_pe(edge_index, num_nodes, k, seed=None, sign_flip=True):
+    """PyG ``AddLaplacianEigenvectorPE(k, is_undirected=True)``: eigenvectors 1..k of the
+    symmetric-normalised Laplacian (ascending eigenvalues, trivial one skipped),
+    zero-padded when the graph is smaller than k+1, random sign per vector."""
+    n = int(num_nodes)
+    A = np.zeros((n, n), dtype=np.float64)
+    ei = np.asarray(edge_index)
+    if ei.size:
+        A[ei[1], ei[0]] = 1.0
+        A[ei[0], ei[1]] = 1.0
+    deg = A.sum(1)
+    dinv = np.where(deg > 0, 1.0 / np.sqrt(np.maximum(deg, 1e-12)), 0.0)
+    L = np.eye(n) - dinv[:, None] * A * dinv[None, :]
+    w, V = np.linalg.eigh(L)
+    V = V[:, np.argsort(w)]
+    pe = np.zeros((n, k), dtype=np.float32)
+    m = min(k, max(n - 1, 0))
+    if m > 0:
+        pe[:, :m] = V[:, 1:m + 1]
+    if sign_flip:
+        rng = np.random.default_rng(seed)
+        pe *= (-1.0 + 2.0 * rng.integers(0, 2, size=(1, k))).astype(np.float32)
+    return torch.from_numpy(pe)
+
+
+def relative_pe(pe, edge_index):
+    return torch.abs(pe[edge_index[0]] - pe[edge_index[1]])
+
+
+def normalize_rotation(pos, max_points=-1, sort=False):
+    """PyG ``NormalizeRotation``: rotate onto the principal axes (PCA via SVD)."""
+    pos = torch.as_tensor(pos)
+    p = pos[:max_points] if max_points > 0 else pos
+    p = p - p.mean(dim=0, keepdim=True)
+    C = p.t() @ p
+    e, v = torch.linalg.eigh(C)
+    if sort:
+        idx = e.argsort(descending=True)
+        v = v[:, idx]
+    return (pos - pos.mean(dim=0, keepdim=True)) @ v
+
+
+def spherical(pos, edge_index, norm=True, max_value=None):
+    """PyG ``Spherical``: (rho, theta, phi) per edge."""
+    vec = pos[edge_index[1]] - pos[edge_index[0]]
+    rho = torch.linalg.norm(vec, dim=-1, keepdim=True)
+    theta = torch.atan2(vec[:, 1], vec[:, 0]).view(-1, 1)
+    theta = theta + (theta < 0).to(theta.dtype) * (2 * math.pi)
+    phi = torch.acos((vec[:, 2] / rho.view(-1).clamp(min=1e-12)).clamp(-1, 1)).view(-1, 1)
+    if norm:
+        rho = rho / (rho.max() if max_value is None else max_value)
+        theta = theta / (2 * math.pi)
+        phi = phi / math.pi
+    return torch.cat([rho, theta, phi], dim=-1)
+
+
+def point_pair_features(pos, normal, edge_index):
+    """PyG ``PointPairFeatures`` (needs per-node normals)."""
+    d = pos[edge_index[0]] - pos[edge_index[1]]
+    n1, n2 = normal[edge_index[1]], normal[edge_index[0]]
+
+    def ang(v1, v2):
+        return torch.atan2(torch.linalg.norm(torch.cross(v1, v2, dim=1), dim=1), (v1 * v2).sum(1))
+
+    return torch.stack([torch.linalg.norm(d, dim=1), ang(n1, d), ang(n2, d), ang(n1, n2)], dim=1)

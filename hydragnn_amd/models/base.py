@@ -1,0 +1,462 @@
+"""Multi-head, multi-branch GNN base model (reference ``hydragnn/models/Base.py:31-752``).
+
+Encoder: ``num_conv_layers`` x [GPSConv(] conv [)] + BatchNorm + activation.
+Decoder: graph heads (mean-pool -> per-branch shared MLP -> per-head MLP) and
+node heads (``mlp`` | ``mlp_per_node`` | ``conv``); multi-branch routing by
+``data.dataset_name``.  Losses: ``loss_hpweighted`` (task-weighted) and
+``energy_force_loss`` (forces = -dE/dpos via double backward).
+
+MI355X-specific differences (semantics preserved):
+* the per-batch message-passing context (CSR SegIndex views, edge features,
+  attention segments) is built once in ``_embedding`` and handed to every
+  layer — no per-layer index rebuilding;
+* branch routing reads the dataset ids the collator already computed on the
+  host (``dataset_ids_host``) instead of ``dataset_name.unique()`` (a device
+  sync per step in the reference, ``Base.py:484``);
+* ``mlp_per_node`` runs one batched GEMM over the node slots instead of a Python
+  loop per node (``Base.py:731-748``).
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn import Linear, ModuleDict, ModuleList, Sequential
+from torch.utils.checkpoint import checkpoint
+
+from ..ops import segment as seg
+from ..ops.attention import make_segments
+from ..utils import tracer as tr
+from ..utils.model import activation_function_selection, loss_function_selection
+from ..utils.print_utils import print_master
+from .gps import GPSConv
+from .layers import BatchNorm, Ctx
+
+
+class Base(nn.Module):
+    is_edge_model = False
+
+    def __init__(self, input_args="", conv_args="", input_dim=1, hidden_dim=8, output_dim=(1,), pe_dim=0,
+                 global_attn_engine=None, global_attn_type=None, global_attn_heads=0, output_type=("graph",),
+                 config_heads=None, activation_function_type="relu", loss_function_type="mse",
+                 equivariance=False, ilossweights_hyperp=1, loss_weights=(1.0,), ilossweights_nll=0,
+                 freeze_conv=False, initial_bias=None, dropout=0.25, num_conv_layers=16, num_nodes=None,
+                 attn_scope="batch"):
+        super().__init__()
+        self.input_args = input_args
+        self.conv_args = conv_args
+        self.global_attn_engine = global_attn_engine
+        self.global_attn_type = global_attn_type
+        self.input_dim = input_dim
+        self.pe_dim = pe_dim
+        self.global_attn_heads = global_attn_heads
+        self.hidden_dim = hidden_dim
+        self.dropout = dropout
+        self.global_attn_dropout = dropout
+        self.num_conv_layers = num_conv_layers
+        self.graph_convs = ModuleList()
+        self.feature_layers = ModuleList()
+        self.num_nodes = num_nodes
+        self.heads_NN = ModuleList()
+        self.config_heads = config_heads or {}
+        self.head_type = list(output_type)
+        self.head_dims = list(output_dim)
+        self.num_heads = len(self.head_dims)
+        self.convs_node_hidden = ModuleDict({})
+        self.batch_norms_node_hidden = ModuleDict({})
+        self.convs_node_output = ModuleDict({})
+        self.batch_norms_node_output = ModuleDict({})
+        self.equivariance = equivariance
+        self.attn_scope = attn_scope
+        self.activation_function_type = activation_function_type
+        self.activation_function = activation_function_selection(activation_function_type)
+        self.var_output = 1 if loss_function_type == "GaussianNLLLoss" else 0
+        self.loss_function_type = loss_function_type
+        self.loss_function = loss_function_selection(loss_function_type)
+        self.ilossweights_nll = ilossweights_nll
+        self.ilossweights_hyperp = ilossweights_hyperp
+        if ilossweights_hyperp * ilossweights_nll == 1:
+            raise ValueError("ilossweights_hyperp and ilossweights_nll cannot be both set to 1.")
+        if ilossweights_hyperp == 1:
+            if len(loss_weights) != self.num_heads:
+                raise ValueError(f"Inconsistent number of loss weights and tasks: {len(loss_weights)} VS "
+                                 f"{self.num_heads}")
+            s = sum(abs(w) for w in loss_weights)
+            self.loss_weights = [w / s for w in loss_weights]
+
+        self.use_edge_attr = bool(getattr(self, "edge_dim", None))
+        self.use_global_attn = bool(global_attn_engine)
+        if self.use_global_attn:
+            self.embed_dim = self.edge_embed_dim = hidden_dim
+        else:
+            self.embed_dim = input_dim
+            self.edge_embed_dim = getattr(self, "edge_dim", None)
+        if self.use_global_attn:
+            self.pos_emb = Linear(pe_dim, hidden_dim, bias=False)
+            if input_dim:
+                self.node_emb = Linear(input_dim, hidden_dim, bias=False)
+                self.node_lin = Linear(2 * hidden_dim, hidden_dim, bias=False)
+            if self.is_edge_model:
+                self.rel_pos_emb = Linear(pe_dim, hidden_dim, bias=False)
+                if self.use_edge_attr:
+                    self.edge_emb = Linear(self.edge_dim, hidden_dim, bias=False)
+                    self.edge_lin = Linear(2 * hidden_dim, hidden_dim, bias=False)
+        self.freeze_conv = freeze_conv
+        self.initial_bias = initial_bias
+        self._init_conv()
+        if freeze_conv:
+            self._freeze_conv()
+        self._multihead()
+        if initial_bias is not None:
+            self._set_bias()
+        self.conv_checkpointing = False
+
+    # ------------------------------------------------------------------ construction
+    def get_conv(self, input_dim, output_dim, edge_dim=None):
+        raise NotImplementedError
+
+    def _apply_global_attn(self, mpnn):
+        if self.use_global_attn and self.global_attn_engine == "GPS":
+            return GPSConv(self.hidden_dim, mpnn, heads=self.global_attn_heads, dropout=self.global_attn_dropout,
+                           attn_type=self.global_attn_type or "multihead")
+        return mpnn
+
+    def _init_conv(self):
+        self.graph_convs.append(
+            self._apply_global_attn(self.get_conv(self.embed_dim, self.hidden_dim, edge_dim=self.edge_embed_dim)))
+        self.feature_layers.append(BatchNorm(self.hidden_dim))
+        for _ in range(self.num_conv_layers - 1):
+            self.graph_convs.append(
+                self._apply_global_attn(self.get_conv(self.hidden_dim, self.hidden_dim, edge_dim=self.edge_embed_dim)))
+            self.feature_layers.append(BatchNorm(self.hidden_dim))
+
+    def _freeze_conv(self):
+        for module in (self.graph_convs, self.feature_layers):
+            for p in module.parameters():
+                p.requires_grad = False
+
+    def _set_bias(self):
+        for head, t in zip(self.heads_NN, self.head_type):
+            if t == "graph":
+                for br in head.values():
+                    br[-1].bias.data.fill_(self.initial_bias)
+
+    def _conv_head_kwargs(self):
+        return {}
+
+    def _init_node_conv(self):
+        nodeconfiglist = self.config_heads["node"]
+        assert self.num_branches == len(nodeconfiglist) or self.num_branches == 1, \
+            "asumming node head has the same branches as graph head, if any"
+        for b in nodeconfiglist:
+            if b["architecture"]["type"] != "conv":
+                return
+        node_feature_ind = [i for i, t in enumerate(self.head_type) if t == "node"]
+        if not node_feature_ind:
+            return
+        for b in nodeconfiglist:
+            bt, arch = b["type"], b["architecture"]
+            nl, hd = arch["num_headlayers"], arch["dim_headlayers"]
+            ch, bh, co, bo = ModuleList(), ModuleList(), ModuleList(), ModuleList()
+            ch.append(self.get_conv(self.hidden_dim, hd[0], **self._conv_head_kwargs()))
+            bh.append(BatchNorm(hd[0]))
+            for il in range(nl - 1):
+                ch.append(self.get_conv(hd[il], hd[il + 1], **self._conv_head_kwargs()))
+                bh.append(BatchNorm(hd[il + 1]))
+            for ih in node_feature_ind:
+                kw = dict(self._conv_head_kwargs())
+                if "last_layer" in kw:
+                    kw["last_layer"] = True
+                co.append(self.get_conv(hd[-1], self.head_dims[ih] * (1 + self.var_output), **kw))
+                bo.append(BatchNorm(self.head_dims[ih] * (1 + self.var_output)))
+            self.convs_node_hidden[bt] = ch
+            self.batch_norms_node_hidden[bt] = bh
+            self.convs_node_output[bt] = co
+            self.batch_norms_node_output[bt] = bo
+
+    def _multihead(self):
+        self.graph_shared = ModuleDict({})
+        self.num_branches = 1
+        if "graph" in self.config_heads:
+            self.num_branches = len(self.config_heads["graph"])
+            for b in self.config_heads["graph"]:
+                ds = b["architecture"]["dim_sharedlayers"]
+                layers = [Linear(self.hidden_dim, ds), self.activation_function]
+                for _ in range(b["architecture"]["num_sharedlayers"] - 1):
+                    layers += [Linear(ds, ds), self.activation_function]
+                self.graph_shared[b["type"]] = Sequential(*layers)
+        if "node" in self.config_heads:
+            self._init_node_conv()
+        inode = 0
+        for ih in range(self.num_heads):
+            head_NN = ModuleDict({})
+            if self.head_type[ih] == "graph":
+                for b in self.config_heads["graph"]:
+                    arch = b["architecture"]
+                    ds, nh, dh = arch["dim_sharedlayers"], arch["num_headlayers"], arch["dim_headlayers"]
+                    layers = [Linear(ds, dh[0]), self.activation_function]
+                    for il in range(nh - 1):
+                        layers += [Linear(dh[il], dh[il + 1]), self.activation_function]
+                    layers.append(Linear(dh[-1], self.head_dims[ih] * (1 + self.var_output)))
+                    head_NN[b["type"]] = Sequential(*layers)
+            elif self.head_type[ih] == "node":
+                for b in self.config_heads["node"]:
+                    bt, arch = b["type"], b["architecture"]
+                    nt = arch["type"]
+                    if nt in ("mlp", "mlp_per_node"):
+                        num_mlp = 1 if nt == "mlp" else self.num_nodes
+                        assert num_mlp is not None, "num_nodes must be positive integer for MLP"
+                        head_NN[bt] = MLPNode(self.hidden_dim, self.head_dims[ih] * (1 + self.var_output), num_mlp,
+                                              arch["dim_headlayers"], nt, self.activation_function)
+                    elif nt == "conv":
+                        ml = ModuleList()
+                        for c, bn in zip(self.convs_node_hidden[bt], self.batch_norms_node_hidden[bt]):
+                            ml.append(c)
+                            ml.append(bn)
+                        ml.append(self.convs_node_output[bt][inode])
+                        ml.append(self.batch_norms_node_output[bt][inode])
+                        head_NN[bt] = ml
+                    else:
+                        raise ValueError("Unknown head NN structure for node features" + nt)
+                if any(b["architecture"]["type"] == "conv" for b in self.config_heads["node"]):
+                    inode += 1
+            else:
+                raise ValueError("Unknown head type" + self.head_type[ih])
+            self.heads_NN.append(head_NN)
+
+    def enable_conv_checkpointing(self):
+        print_master("Enabling checkpointing")
+        self.conv_checkpointing = True
+
+    # ------------------------------------------------------------------ forward
+    def _base_ctx(self, data):
+        N = data.num_nodes
+        dev = data.x.device if data.x is not None else data.pos.device
+        ctx = Ctx(data=data, dst_si=data.get("dst_si"), src_si=data.get("src_si"), graph_si=data.get("graph_si"),
+                  num_valid=data.get("num_valid"), pos=data.pos)
+        if self.use_global_attn:
+            sid, sptr = data.get("attn_seg_id"), data.get("attn_seg_ptr")
+            if sid is None:
+                sid, sptr = make_segments(N, self.attn_scope, ptr=data.get("ptr"), num_valid=data.get("num_valid_host"),
+                                          device=dev)
+            ctx.attn_seg_id, ctx.attn_seg_ptr = sid, sptr
+        return ctx
+
+    def _gps_embed(self, data, ctx, edge_attr=None):
+        x = self.pos_emb(data.pe)
+        if self.input_dim:
+            x = self.node_lin(torch.cat((self.node_emb(data.x.float()), x), 1))
+        if self.is_edge_model:
+            e = self.rel_pos_emb(data.rel_pe)
+            if self.use_edge_attr:
+                e = self.edge_lin(torch.cat((self.edge_emb(edge_attr), e), 1))
+            ctx.edge_attr = e
+        return x
+
+    def _embedding(self, data):
+        ctx = self._base_ctx(data)
+        if self.use_edge_attr:
+            assert data.edge_attr is not None, "Data must have edge attributes if use_edge_attributes is set."
+            ctx.edge_attr = data.edge_attr
+        else:
+            ctx.edge_attr = None
+        if self.use_global_attn:
+            x = self._gps_embed(data, ctx, ctx.edge_attr)
+            return x, data.pos, ctx
+        return data.x, data.pos, ctx
+
+    def _run_conv(self, conv, inv, equiv, ctx):
+        if self.conv_checkpointing and self.training:
+            return checkpoint(lambda a, b: conv(a, b, ctx), inv, equiv, use_reentrant=False)
+        return conv(inv, equiv, ctx)
+
+    def encode(self, data):
+        inv, equiv, ctx = self._embedding(data)
+        for conv, bn in zip(self.graph_convs, self.feature_layers):
+            inv, equiv = self._run_conv(conv, inv, equiv, ctx)
+            inv = self.activation_function(bn(inv, ctx.get("num_valid")))
+        return inv, equiv, ctx
+
+    def _branch_ids(self, data):
+        ids = data.get("dataset_ids_host")
+        if ids is not None:
+            return list(ids)
+        dn = data.get("dataset_name")
+        if dn is None:
+            return [0]
+        return [int(i) for i in torch.unique(dn).tolist()]
+
+    def decode(self, x, equiv, ctx):
+        data = ctx.data
+        gsi = ctx.graph_si
+        if gsi is None:
+            x_graph = x.mean(dim=0, keepdim=True)
+        else:
+            x_graph = seg.segment_mean(x, gsi)
+        outputs, outputs_var = [], []
+        nb = self.num_branches
+        ids = self._branch_ids(data) if nb > 1 else [0]
+        G = x_graph.shape[0]
+        for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
+            if t == "graph":
+                if nb == 1:
+                    out = headloc["branch-0"](self.graph_shared["branch-0"](x_graph))
+                    head, headvar = out[:, :head_dim], out[:, head_dim:] ** 2
+                else:
+                    dn = data.dataset_name.view(-1)
+                    head = x_graph.new_zeros((G, head_dim))
+                    headvar = x_graph.new_zeros((G, head_dim * self.var_output))
+                    for ID in ids:
+                        mask = dn == ID
+                        bt = f"branch-{ID}"
+                        out = headloc[bt](self.graph_shared[bt](x_graph[mask]))
+                        head = head.index_put((mask,), out[:, :head_dim])
+                        headvar = headvar.index_put((mask,), out[:, head_dim:] ** 2)
+            else:
+                nt = self.config_heads["node"][0]["architecture"]["type"]
+                if nb == 1:
+                    x_node = self._node_head(headloc["branch-0"], nt, x, equiv, ctx, data.get("batch"))
+                    head, headvar = x_node[:, :head_dim], x_node[:, head_dim:] ** 2
+                else:
+                    dn = data.dataset_name.view(-1)
+                    batch = data.batch
+                    head = x.new_zeros((x.shape[0], head_dim))
+                    headvar = x.new_zeros((x.shape[0], head_dim * self.var_output))
+                    for ID in ids:
+                        mask_nodes = (dn == ID)[batch]
+                        bt = f"branch-{ID}"
+                        if nt == "conv":
+                            x_node = self._node_head(headloc[bt], nt, x, equiv, ctx, batch)[mask_nodes]
+                        else:
+                            x_node = headloc[bt](x=x[mask_nodes], batch=batch[mask_nodes])
+                        head = head.index_put((mask_nodes,), x_node[:, :head_dim])
+                        headvar = headvar.index_put((mask_nodes,), x_node[:, head_dim:] ** 2)
+            outputs.append(head)
+            outputs_var.append(headvar)
+        if self.var_output:
+            return outputs, outputs_var
+        return outputs
+
+    def _node_head(self, headloc, nt, x, equiv, ctx, batch):
+        if nt == "conv":
+            inv, eq = x, equiv
+            for conv, bn in zip(headloc[0::2], headloc[1::2]):
+                inv, eq = conv(inv, eq, ctx)
+                inv = self.activation_function(bn(inv, ctx.get("num_valid")))
+            return inv
+        return headloc(x=x, batch=batch)
+
+    def forward(self, data):
+        tr.start("enc_forward")
+        x, equiv, ctx = self.encode(data)
+        tr.stop("enc_forward")
+        tr.start("branch_forward")
+        out = self.decode(x, equiv, ctx)
+        tr.stop("branch_forward")
+        return out
+
+    # ------------------------------------------------------------------ losses
+    def loss(self, pred, value, head_index):
+        var = None
+        if self.var_output:
+            var = pred[1]
+            pred = pred[0]
+        if self.ilossweights_nll == 1:
+            return self.loss_nll(pred, value, head_index, var=var)
+        return self.loss_hpweighted(pred, value, head_index, var=var)
+
+    def loss_nll(self, pred, value, head_index, var=None):
+        raise ValueError("loss_nll() not ready yet")
+
+    def _head_value(self, value, head_index, ih, shape):
+        if isinstance(value, (list, tuple)):
+            v = value[ih]
+        else:
+            v = value[head_index[ih]]
+        if v.shape != shape:
+            v = torch.reshape(v, shape)
+        return v
+
+    def loss_hpweighted(self, pred, value, head_index, var=None, weights=None):
+        """Task-weighted sum of per-head losses.  ``value`` is either the packed
+        ``data.y`` (with ``head_index``) or a list of per-head target tensors."""
+        tot_loss = 0
+        tasks_loss = []
+        for ih in range(self.num_heads):
+            hp = pred[ih]
+            hv = self._head_value(value, head_index, ih, hp.shape)
+            if var is None:
+                assert self.loss_function_type != "GaussianNLLLoss", "Expecting var for GaussianNLLLoss, but got None"
+                l = self.loss_function(hp, hv)
+            else:
+                l = self.loss_function(hp, hv, var[ih])
+            tot_loss = tot_loss + l * self.loss_weights[ih]
+            tasks_loss.append(l)
+        return tot_loss, tasks_loss
+
+    def energy_force_loss(self, pred, data):
+        """Energy + force loss; forces = -dE/dpos with create_graph=True (``Base.py:582-636``)."""
+        assert data.pos is not None and data.energy is not None and data.forces is not None, \
+            "data.pos, data.energy, data.forces must be provided for energy-force loss."
+        assert data.pos.requires_grad, "data.pos does not have grad, so force predictions cannot be computed."
+        assert self.num_heads == 1 and self.head_type[0] == "node", \
+            "Force predictions are only supported for models with one head that predict nodal energy."
+        node_energy_pred = pred[0]
+        graph_energy_pred = seg.segment_sum(node_energy_pred, data.graph_si).squeeze().float()
+        graph_energy_true = data.energy.squeeze().float()
+        w = self.loss_weights[0]
+        e_loss = self.loss_function(graph_energy_pred, graph_energy_true)
+        tot = e_loss * w
+        tasks = [e_loss]
+        forces_true = data.forces.float()
+        forces_pred = torch.autograd.grad(graph_energy_pred, data.pos, grad_outputs=torch.ones_like(graph_energy_pred),
+                                          retain_graph=graph_energy_pred.requires_grad, create_graph=True)[0]
+        assert forces_pred is not None, "No gradients were found for data.pos."
+        forces_pred = -forces_pred.float()
+        fw = w * torch.mean(torch.abs(graph_energy_true)) / (torch.mean(torch.abs(forces_true)) + 1e-8)
+        tot = tot + self.loss_function(forces_pred, forces_true) * fw
+        return tot, tasks
+
+    def __str__(self):
+        return "Base"
+
+
+class MLPNode(nn.Module):
+    """Node-level head: a shared MLP (``mlp``) or one MLP per node slot (``mlp_per_node``,
+    fixed-size graphs).  The per-node variant runs as one batched matmul per layer
+    (weights stacked [num_nodes, in, out]) instead of the reference's Python loop."""
+
+    def __init__(self, input_dim, output_dim, num_mlp, hidden_dim_node, node_type, activation_function):
+        super().__init__()
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        self.node_type = node_type
+        self.num_mlp = num_mlp
+        self.activation_function = activation_function
+        self.mlp = ModuleList()
+        for _ in range(num_mlp):
+            layers = [Linear(input_dim, hidden_dim_node[0]), activation_function]
+            for il in range(len(hidden_dim_node) - 1):
+                layers += [Linear(hidden_dim_node[il], hidden_dim_node[il + 1]), activation_function]
+            layers.append(Linear(hidden_dim_node[-1], output_dim))
+            self.mlp.append(Sequential(*layers))
+
+    def forward(self, x, batch):
+        if self.node_type == "mlp":
+            return self.mlp[0](x)
+        nn_ = self.num_mlp
+        G = x.shape[0] // nn_
+        h = x.view(G, nn_, -1).transpose(0, 1)  # [slots, G, F]
+        nlin = len([m for m in self.mlp[0] if isinstance(m, Linear)])
+        li = 0
+        for m in self.mlp[0]:
+            if isinstance(m, Linear):
+                idx = [k for k, mm in enumerate(self.mlp[0]) if isinstance(mm, Linear)][li]
+                W = torch.stack([self.mlp[s][idx].weight for s in range(nn_)])  # [slots, out, in]
+                b = torch.stack([self.mlp[s][idx].bias for s in range(nn_)])  # [slots, out]
+                h = torch.baddbmm(b.unsqueeze(1), h, W.transpose(1, 2))
+                li += 1
+                if li < nlin:
+                    h = self.activation_function(h)
+        return h.transpose(0, 1).reshape(G * nn_, -1)
+
+    def __str__(self):
+        return "MLPNode"

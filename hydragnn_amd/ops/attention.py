@@ -1,0 +1,87 @@
+"""Segment-block-diagonal multi-head self-attention (GPS global attention).
+
+GPU: ``csrc/attention.hip`` flash kernels (fwd + atomic-free bwd).  CPU (and the
+composite/double-backward mode): dense masked softmax reference.
+
+Reference semantics: ``hydragnn/globalAtt/gps.py:126-133`` —
+``torch.nn.MultiheadAttention`` over ``to_dense_batch(x, None)``: all nodes of
+the local mini-batch in one sequence (``scope="batch"``).  ``scope="graph"``
+restricts attention to nodes of the same graph.
+"""
+import math
+
+import torch
+
+from .. import _native
+from . import pna as _pna_mode
+
+
+def make_segments(num_nodes, scope="batch", ptr=None, num_valid=None, device=None):
+    """Return (seg_id int32 [N], seg_ptr int32 [S+1]) for the requested attention scope.
+
+    ``num_valid`` (< N) marks trailing padding rows which form their own segment.
+    """
+    N = int(num_nodes)
+    nv = N if num_valid is None else int(num_valid)
+    if scope == "batch":
+        if nv < N:
+            seg_ptr = torch.tensor([0, nv, N], dtype=torch.int32, device=device)
+            seg_id = torch.zeros(N, dtype=torch.int32, device=device)
+            seg_id[nv:] = 1
+        else:
+            seg_ptr = torch.tensor([0, N], dtype=torch.int32, device=device)
+            seg_id = torch.zeros(N, dtype=torch.int32, device=device)
+        return seg_id, seg_ptr
+    if scope == "graph":
+        assert ptr is not None
+        ptr = ptr.to(device=device, dtype=torch.int32)
+        G = ptr.numel() - 1
+        if int(ptr[-1]) < N:
+            ptr = torch.cat([ptr, torch.tensor([N], dtype=torch.int32, device=device)])
+        counts = (ptr[1:] - ptr[:-1]).long()
+        seg_id = torch.repeat_interleave(torch.arange(ptr.numel() - 1, device=device, dtype=torch.int32), counts)
+        return seg_id, ptr
+    raise ValueError(f"unknown attention scope {scope}")
+
+
+def attention_reference(qkv, heads, seg_id, scale=None):
+    N, F3 = qkv.shape
+    F = F3 // 3
+    D = F // heads
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    q, k, v = qkv[:, :F], qkv[:, F:2 * F], qkv[:, 2 * F:]
+    q = q.reshape(N, heads, D).transpose(0, 1)
+    k = k.reshape(N, heads, D).transpose(0, 1)
+    v = v.reshape(N, heads, D).transpose(0, 1)
+    s = torch.matmul(q, k.transpose(1, 2)) * scale
+    mask = seg_id.view(-1, 1) == seg_id.view(1, -1)
+    s = s.masked_fill(~mask.unsqueeze(0), float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, v)
+    return o.transpose(0, 1).reshape(N, F)
+
+
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, seg_id, seg_ptr, heads, scale):
+        O, LSE = _native.ops().attn_fwd(qkv, seg_id, seg_ptr, heads, scale)
+        ctx.save_for_backward(qkv, O, LSE, seg_id, seg_ptr)
+        ctx.heads, ctx.scale = heads, scale
+        return O
+
+    @staticmethod
+    def backward(ctx, dO):
+        qkv, O, LSE, seg_id, seg_ptr = ctx.saved_tensors
+        dqkv = _native.ops().attn_bwd(dO, qkv, O, LSE, seg_id, seg_ptr, ctx.heads, ctx.scale)
+        return dqkv, None, None, None, None
+
+
+def segment_attention(qkv, heads, seg_id, seg_ptr, scale=None):
+    """Multi-head self-attention on packed ``qkv`` [N, 3F] -> [N, F]."""
+    F = qkv.shape[1] // 3
+    D = F // heads
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    if (qkv.is_cuda and qkv.dtype == torch.float32 and D in (4, 8, 16, 32, 64)
+            and not _pna_mode._state["composite"]):
+        return _FlashAttn.apply(qkv, seg_id, seg_ptr, heads, scale)
+    return attention_reference(qkv, heads, seg_id, scale)

@@ -1,0 +1,139 @@
+"""Fused PNA message + degree-scaler aggregation (see ``csrc/pna.hip``).
+
+Z = cat[x, cat_{s in scalers} s(deg) * cat[mean, min, max, std](m)]  with
+m_e = (A[dst_e] + B[src_e] + C_e) * G_e.
+
+Reference: PyG ``DegreeScalerAggregation`` as used by
+``hydragnn/models/PNAPlusStack.py:164`` / ``PNAStack.py:42-67``; message at
+``PNAPlusStack.py:250-279``.
+
+Two paths:
+* fused (HIP, GPU, first-order autograd): one forward kernel, one backward
+  kernel + one CSR segment-sum over sources.
+* composite (CPU, or whenever a double-backward is needed): built from the
+  differentiable primitives in ``ops.segment``.
+"""
+import math
+
+import torch
+
+from .. import _native
+from . import segment as seg
+
+_state = {"composite": False}
+
+
+class composite_mode:
+    """Force the composite (infinitely differentiable) path, e.g. for force training."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        self.prev = _state["composite"]
+        _state["composite"] = self.enabled
+
+    def __exit__(self, *a):
+        _state["composite"] = self.prev
+
+
+def pna_avg_deg(deg_hist):
+    """avg_deg dict of PyG DegreeScalerAggregation from a degree histogram."""
+    deg = torch.as_tensor(deg_hist, dtype=torch.float64)
+    num_nodes = float(deg.sum())
+    bins = torch.arange(deg.numel(), dtype=torch.float64)
+    return {
+        "lin": float((bins * deg).sum()) / num_nodes,
+        "log": float(((bins + 1).log() * deg).sum()) / num_nodes,
+        "exp": float((bins.exp() * deg).sum()) / num_nodes,
+    }
+
+
+def degree_scalers(deg, avg_deg, scalers):
+    d = deg.clamp(min=1.0).view(-1, 1)
+    out = []
+    for s in scalers:
+        if s == "identity":
+            out.append(torch.ones_like(d))
+        elif s == "amplification":
+            out.append(torch.log(d + 1) / avg_deg["log"])
+        elif s == "attenuation":
+            out.append(avg_deg["log"] / torch.log(d + 1))
+        elif s == "linear":
+            out.append(d / avg_deg["lin"])
+        elif s == "inverse_linear":
+            out.append(avg_deg["lin"] / d)
+        else:
+            raise ValueError(f"unknown PNA scaler {s}")
+    return out
+
+
+def pna_aggregate_composite(m, dst_si, avg_deg, aggregators=("mean", "min", "max", "std"),
+                            scalers=("identity", "amplification", "attenuation", "linear")):
+    """Differentiable reference: [N, len(aggr)*len(scalers)*F]."""
+    aggs = []
+    for a in aggregators:
+        if a == "mean":
+            aggs.append(seg.segment_mean(m, dst_si))
+        elif a == "min":
+            aggs.append(seg.segment_min(m, dst_si))
+        elif a == "max":
+            aggs.append(seg.segment_max(m, dst_si))
+        elif a == "std":
+            aggs.append(seg.segment_std(m, dst_si))
+        elif a == "sum":
+            aggs.append(seg.segment_sum(m, dst_si))
+        elif a == "var":
+            mean = seg.segment_mean(m, dst_si)
+            aggs.append(seg.segment_mean(m * m, dst_si) - mean * mean)
+        else:
+            raise ValueError(f"unknown PNA aggregator {a}")
+    out = torch.cat(aggs, dim=-1)
+    deg = dst_si.degree(out.dtype).to(out.device)
+    return torch.cat([out * s for s in degree_scalers(deg, avg_deg, scalers)], dim=-1)
+
+
+class _PNAFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, AB, C, G, dst_si, src_si, avg_log, avg_lin):
+        Z, amin, amax = _native.ops().pna_fwd(x, AB, C, G, src_si.index, dst_si.rowptr, avg_log, avg_lin)
+        ctx.save_for_backward(Z, AB, C, G, amin, amax)
+        ctx.dst_si, ctx.src_si = dst_si, src_si
+        ctx.avg = (avg_log, avg_lin)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        Z, AB, C, G, amin, amax = ctx.saved_tensors
+        F = Z.shape[1] // 17
+        dpre, dG, dA = _native.ops().pna_bwd(dZ, Z, AB, C, G, ctx.src_si.index, ctx.dst_si.rowptr, amin,
+                                             amax, ctx.avg[0], ctx.avg[1])
+        dB = _native.ops().seg_sum(dpre, ctx.src_si.rowptr, ctx.src_si.perm, ctx.src_si.num_segments, False)
+        dAB = torch.cat([dA, dB], dim=1)
+        dx = dZ[:, :F]
+        return dx, dAB, dpre, dG, None, None, None, None
+
+
+def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
+    """Z = cat[x, PNA-aggregate((A[dst] + B[src] + C) * G)] with default aggregators/scalers.
+
+    ``AB`` is [N, 2F]: columns [0,F) multiply the destination (x_i) and
+    [F,2F) the source (x_j) node features.
+    """
+    F = x.shape[1]
+    fused = (
+        x.is_cuda
+        and not _state["composite"]
+        and x.dtype == torch.float32
+        and AB.dtype == torch.float32
+        and C.dtype == torch.float32
+        and G.dtype == torch.float32
+        and dst_si.perm is None
+    )
+    if fused:
+        return _PNAFused.apply(x.contiguous(), AB, C.contiguous(), G.contiguous(), dst_si, src_si,
+                               float(avg_deg["log"]), float(avg_deg["lin"]))
+    A, B = AB[:, :F], AB[:, F:]
+    m = (seg.gather(A, dst_si) + seg.gather(B, src_si) + C) * G
+    agg = pna_aggregate_composite(m, dst_si, avg_deg)
+    return torch.cat([x, agg], dim=-1)

@@ -1,0 +1,242 @@
+"""Differentiable CSR segment ops (gather / segment-sum / mean / min / max / softmax).
+
+Replaces torch_scatter and PyG aggregation (reference call sites:
+``hydragnn/models/Base.py:599`` scatter_add, ``hydragnn/utils/model/model.py:279-286``
+unsorted_segment_mean, ``EGCLStack.py:292-298`` unsorted_segment_sum,
+``PAINNStack.py:256-257`` index_add_, PyG ``MessagePassing`` aggr).
+
+A :class:`SegIndex` describes how E rows map onto N segments:
+``index[e]`` is the owner segment of row e; ``rowptr``/``perm`` list, for each
+segment, the rows it owns (``perm=None`` means rows are already sorted by
+owner).  Because ``gather`` and ``segment_sum`` over the same SegIndex are each
+other's adjoint, every op here is differentiable to any order (needed for
+force training via double backward, ``Base.py:614-620``).
+
+GPU tensors run the HIP kernels in ``csrc/segment.hip``; CPU tensors run the
+plain-torch reference below (also the numerics oracle for the tests).
+"""
+import torch
+
+from .. import _native
+
+
+class SegIndex:
+    """Row -> segment mapping with a CSR view (all index tensors int32)."""
+
+    __slots__ = ("index", "rowptr", "perm", "num_segments", "_deg", "_index64")
+
+    def __init__(self, index, rowptr, perm, num_segments):
+        self.index = index
+        self.rowptr = rowptr
+        self.perm = perm
+        self.num_segments = int(num_segments)
+        self._deg = None
+        self._index64 = None
+
+    @property
+    def num_rows(self):
+        return self.index.numel()
+
+    @property
+    def index64(self):
+        if self._index64 is None:
+            self._index64 = self.index.long()
+        return self._index64
+
+    def degree(self, dtype=torch.float32):
+        if self._deg is None:
+            self._deg = (self.rowptr[1:] - self.rowptr[:-1]).to(dtype)
+        return self._deg
+
+    def to(self, device):
+        p = None if self.perm is None else self.perm.to(device, non_blocking=True)
+        return SegIndex(self.index.to(device, non_blocking=True), self.rowptr.to(device, non_blocking=True), p,
+                        self.num_segments)
+
+    @staticmethod
+    def from_index(index, num_segments, sorted_=False):
+        """Build from an owner index (any integer dtype)."""
+        index = index.reshape(-1)
+        dev = index.device
+        counts = torch.bincount(index.long(), minlength=num_segments)
+        rowptr = torch.zeros(num_segments + 1, dtype=torch.int32, device=dev)
+        rowptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        perm = None
+        if not sorted_:
+            perm = torch.argsort(index.long(), stable=True).to(torch.int32)
+        return SegIndex(index.to(torch.int32), rowptr, perm, num_segments)
+
+
+def _use_native(t):
+    return t.is_cuda
+
+
+# ------------------------------------------------------------------ CPU reference
+
+def _cpu_segment_sum(x, si):
+    out = x.new_zeros((si.num_segments,) + tuple(x.shape[1:]))
+    return out.index_add_(0, si.index64.to(x.device), x)
+
+
+def _cpu_segment_minmax(x, si, is_max):
+    N = si.num_segments
+    idx = si.index64
+    out = x.new_zeros((N,) + tuple(x.shape[1:]))
+    if x.numel() == 0:
+        return out, torch.full(out.shape, -1, dtype=torch.int32)
+    red = "amax" if is_max else "amin"
+    shp = idx.view(-1, *([1] * (x.dim() - 1))).expand_as(x)
+    out = out.scatter_reduce(0, shp, x, reduce=red, include_self=False)
+    # arg: first row attaining the extremum (ties -> smallest row id)
+    rows = torch.arange(x.shape[0], device=x.device).view(-1, *([1] * (x.dim() - 1))).expand_as(x)
+    hit = x == out[idx]
+    big = torch.full_like(rows, x.shape[0])
+    cand = torch.where(hit, rows, big)
+    arg = torch.full(out.shape, x.shape[0], dtype=torch.long, device=x.device)
+    arg = arg.scatter_reduce(0, shp, cand, reduce="amin", include_self=True)
+    arg = torch.where(arg >= x.shape[0], torch.full_like(arg, -1), arg).to(torch.int32)
+    return out, arg
+
+
+# ------------------------------------------------------------------ autograd fns
+
+class _Gather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, si):
+        ctx.si = si
+        ctx.n = x.shape[0]
+        if _use_native(x) and x.dtype == torch.float32:
+            tail = x.shape[1:]
+            out = _native.ops().gather_rows(x.reshape(x.shape[0], -1), si.index)
+            return out.view((out.shape[0],) + tuple(tail))
+        return x.index_select(0, si.index64.to(x.device))
+
+    @staticmethod
+    def backward(ctx, g):
+        return _SegSum.apply(g, ctx.si), None
+
+
+class _SegSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, si):
+        ctx.si = si
+        if _use_native(x) and x.dtype == torch.float32:
+            tail = x.shape[1:]
+            out = _native.ops().seg_sum(x.reshape(x.shape[0], -1), si.rowptr, si.perm, si.num_segments, False)
+            return out.view((si.num_segments,) + tuple(tail))
+        return _cpu_segment_sum(x, si)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _Gather.apply(g, ctx.si), None
+
+
+class _ScatterArg(torch.autograd.Function):
+    """out[E] = 0; out[arg[n,f], f] = g[n,f]."""
+
+    @staticmethod
+    def forward(ctx, g, arg, E):
+        ctx.save_for_backward(arg)
+        if _use_native(g) and g.dtype == torch.float32:
+            return _native.ops().scatter_arg(g, arg, E)
+        out = g.new_zeros((E,) + tuple(g.shape[1:]))
+        valid = arg >= 0
+        a = torch.where(valid, arg, torch.zeros_like(arg)).long()
+        out.scatter_add_(0, a, torch.where(valid, g, torch.zeros_like(g)))
+        return out
+
+    @staticmethod
+    def backward(ctx, go):
+        (arg,) = ctx.saved_tensors
+        return _GatherArg.apply(go, arg), None, None
+
+
+class _GatherArg(torch.autograd.Function):
+    """out[n,f] = x[arg[n,f], f] (0 when arg<0)."""
+
+    @staticmethod
+    def forward(ctx, x, arg):
+        ctx.save_for_backward(arg)
+        ctx.E = x.shape[0]
+        if _use_native(x) and x.dtype == torch.float32:
+            return _native.ops().gather_arg(x, arg)
+        valid = arg >= 0
+        a = torch.where(valid, arg, torch.zeros_like(arg)).long()
+        return torch.where(valid, torch.gather(x, 0, a), torch.zeros((), dtype=x.dtype, device=x.device))
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        return _ScatterArg.apply(g, arg, ctx.E), None
+
+
+class _SegMinMax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, si, is_max):
+        if _use_native(x) and x.dtype == torch.float32 and si.perm is None and x.dim() == 2:
+            out, arg = _native.ops().seg_minmax(x, si.rowptr, si.num_segments, is_max)
+        else:
+            out, arg = _cpu_segment_minmax(x, si, is_max)
+        ctx.save_for_backward(arg)
+        ctx.E = x.shape[0]
+        ctx.mark_non_differentiable(arg)
+        return out, arg
+
+    @staticmethod
+    def backward(ctx, g, _garg):
+        (arg,) = ctx.saved_tensors
+        return _ScatterArg.apply(g, arg, ctx.E), None, None
+
+
+# ------------------------------------------------------------------ public API
+
+def gather(x, si):
+    """x[si.index] — row gather; backward is a deterministic CSR segment-sum."""
+    return _Gather.apply(x, si)
+
+
+def segment_sum(x, si):
+    return _SegSum.apply(x, si)
+
+
+def segment_mean(x, si):
+    s = _SegSum.apply(x, si)
+    deg = si.degree(s.dtype).clamp(min=1.0).to(s.device)
+    return s / deg.view(-1, *([1] * (s.dim() - 1)))
+
+
+def segment_max(x, si):
+    return _SegMinMax.apply(x, si, True)[0]
+
+
+def segment_min(x, si):
+    return _SegMinMax.apply(x, si, False)[0]
+
+
+def segment_std(x, si, eps=1e-5):
+    """PyG StdAggregation: sqrt(clamp(E[x^2]-E[x]^2, eps)), zeroed where <= sqrt(eps)."""
+    mean = segment_mean(x, si)
+    mean2 = segment_mean(x * x, si)
+    var = mean2 - mean * mean
+    out = var.clamp(min=eps).sqrt()
+    return out.masked_fill(out <= eps ** 0.5, 0.0)
+
+
+def segment_softmax(logits, si):
+    """Softmax of edge logits within each destination segment (GATv2)."""
+    mx = segment_max(logits.detach(), si)
+    z = logits - gather(mx, si)
+    ez = torch.exp(z)
+    den = segment_sum(ez, si)
+    return ez / (gather(den, si) + 1e-16)
+
+
+def scatter_sum_index(x, index, num_segments):
+    """Convenience: unsorted index -> segment sum (builds a SegIndex on the fly)."""
+    si = SegIndex.from_index(index, num_segments)
+    return segment_sum(x, si)
+
+
+def scatter_mean_index(x, index, num_segments):
+    si = SegIndex.from_index(index, num_segments)
+    return segment_mean(x, si)

@@ -1,0 +1,129 @@
+"""Fused multi-tensor AdamW (HIP kernel ``csrc/optim.hip``), hipGraph-capturable.
+
+API-compatible with ``torch.optim.AdamW`` (param_groups, state_dict with
+per-parameter ``step``/``exp_avg``/``exp_avg_sq``), so reference-style
+checkpoints (``optimizer_state_dict``) and ``ReduceLROnPlateau`` work.  The
+learning rate and step counter are device scalars: changing ``lr`` through
+``param_groups`` is picked up at the next ``step()`` without recapturing.
+
+GPU: one kernel launch for all parameters (+1 tiny counter kernel).  CPU: the
+plain-torch update (reference math), used by the CPU tests.
+"""
+import ctypes
+
+import torch
+
+from .. import _native
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, adamw=True):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.adamw = adamw
+        self._tables = None
+        self._dev_state = None
+        self._host_lr = None
+
+    def _init_state(self):
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+
+    def _build_tables(self):
+        """Per param-group (ref blob, block table, device [step, lr])."""
+        tables = []
+        for group in self.param_groups:
+            refs, blocks = [], []
+            ps = [p for p in group["params"] if p.grad is not None]
+            for ti, p in enumerate(ps):
+                st = self.state[p]
+                n = p.numel()
+                assert p.is_contiguous() and p.grad.is_contiguous()
+                refs.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), n))
+                for c in range((n + 2047) // 2048):
+                    blocks.append((ti, c))
+            if not ps:
+                tables.append(None)
+                continue
+            blob = bytearray()
+            for r in refs:
+                blob += ctypes.string_at(ctypes.addressof((ctypes.c_uint64 * 4)(*r[:4])), 32)
+                blob += int(r[4]).to_bytes(8, "little", signed=True)
+            dev = ps[0].device
+            rb = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(dev)
+            bt = torch.tensor(blocks, dtype=torch.int32).view(-1).to(dev)
+            step0 = float(self.state[ps[0]]["step"])
+            state = torch.tensor([step0, group["lr"]], dtype=torch.float32, device=dev)
+            for p in ps:
+                self.state[p]["step"] = state[0]  # shared view: checkpoints see the live count
+            tables.append([rb, bt, state, group["lr"], tuple(p.grad.data_ptr() for p in ps), ps])
+        self._tables = tables
+
+    def _tables_valid(self):
+        if self._tables is None:
+            return False
+        for group, t in zip(self.param_groups, self._tables):
+            ps = [p for p in group["params"] if p.grad is not None]
+            if t is None:
+                if ps:
+                    return False
+                continue
+            if tuple(p.grad.data_ptr() for p in ps) != t[4]:
+                return False
+        return True
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._init_state()
+        gpu = any(p.is_cuda for g in self.param_groups for p in g["params"])
+        if not gpu:
+            self._cpu_step()
+            return loss
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not self._tables_valid():
+            assert not capturing, "FusedAdamW tables must be built before graph capture"
+            self._build_tables()
+        for group, t in zip(self.param_groups, self._tables):
+            if t is None:
+                continue
+            if t[3] != group["lr"] and not capturing:
+                t[2][1].fill_(group["lr"])
+                t[3] = group["lr"]
+            b1, b2 = group["betas"]
+            _native.ops().adamw_step(t[0], t[1], t[2], b1, b2, group["eps"], group["weight_decay"], self.adamw, 1.0)
+        return loss
+
+    def _cpu_step(self):
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                st["step"] += 1
+                t = float(st["step"])
+                g = p.grad
+                if self.adamw:
+                    p.mul_(1 - lr * wd)
+                else:
+                    g = g + wd * p
+                st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+                st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+                bc1 = 1 - b1 ** t
+                bc2 = 1 - b2 ** t
+                denom = (st["exp_avg_sq"].sqrt() / (bc2 ** 0.5)).add_(eps)
+                p.addcdiv_(st["exp_avg"], denom, value=-lr / bc1)
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tables = None

@@ -1,0 +1,236 @@
+"""Data-parallel gradient synchronisation with bucketed, backward-overlapped all-reduce.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
+(``distributed.py:332-351``).  Design for one MI355X node:
+
+* parameters are packed in reverse registration order (≈ the order their
+  gradients become ready in backward) into flat fp32 buckets of
+  ``bucket_cap_mb``; every ``param.grad`` is a *view* into its bucket, so the
+  collective runs on the bucket in place (no pack/unpack copies);
+* a post-accumulate-grad hook per parameter counts readiness; a full bucket is
+  all-reduced immediately with ``async_op=True`` on the process group (RCCL over
+  xGMI for ``nccl``, gloo on CPU), overlapping with the rest of backward;
+* a callback queued on the autograd engine flushes buckets whose parameters
+  received no gradient (``find_unused_parameters`` semantics) and waits for all
+  outstanding collectives before ``backward()`` returns;
+* gradients are pre-scaled by 1/world (SUM == AVG, works for gloo too).
+
+GNN parameter counts are small (≈0.1-50 M), so the default bucket size (25 MB)
+usually yields 1-3 large collectives per step — the regime where ring
+all-reduce over the 7 xGMI links is bandwidth-efficient.
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+
+class _Bucket:
+    __slots__ = ("params", "flat", "offsets", "pending", "work", "launched")
+
+    def __init__(self, params, device, dtype):
+        self.params = params
+        n = sum(p.numel() for p in params)
+        self.flat = torch.zeros(n, device=device, dtype=dtype)
+        self.offsets = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += p.numel()
+        self.pending = len(params)
+        self.work = None
+        self.launched = False
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module, process_group=None, bucket_cap_mb=25.0, find_unused_parameters=False,
+                 broadcast_buffers=True, device_ids=None, output_device=None, gradient_as_bucket_view=True):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.world = dist.get_world_size(process_group)
+        self.find_unused_parameters = find_unused_parameters
+        self.broadcast_buffers = broadcast_buffers
+        self._sync_enabled = True
+        self._callback_queued = False
+        params = [p for p in module.parameters() if p.requires_grad]
+        self._broadcast_module_state()
+        cap = int(bucket_cap_mb * 1024 * 1024)
+        buckets, cur, cur_bytes = [], [], 0
+        for p in reversed(params):
+            nb = p.numel() * p.element_size()
+            if cur and cur_bytes + nb > cap:
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += nb
+        if cur:
+            buckets.append(cur)
+        self.buckets = []
+        self._owner = {}
+        for bi, ps in enumerate(buckets):
+            b = _Bucket(ps, ps[0].device, ps[0].dtype)
+            self.buckets.append(b)
+            for p, off in zip(ps, b.offsets):
+                p.grad = b.flat[off:off + p.numel()].view_as(p)
+                self._owner[p] = bi
+                p.register_post_accumulate_grad_hook(self._make_hook(bi))
+
+    # ------------------------------------------------------------------ state
+    def _broadcast_module_state(self):
+        if self.world <= 1:
+            return
+        with torch.no_grad():
+            for t in list(self.module.parameters()) + list(self.module.buffers()):
+                dist.broadcast(t.data, src=0, group=self.process_group)
+
+    def _sync_buffers(self):
+        if self.broadcast_buffers and self.world > 1:
+            with torch.no_grad():
+                for b in self.module.buffers():
+                    dist.broadcast(b.data, src=0, group=self.process_group)
+
+    # ------------------------------------------------------------------ hooks
+    def _make_hook(self, bi):
+        def hook(p):
+            if not self._sync_enabled:
+                return
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            b = self.buckets[bi]
+            # the engine may have replaced the grad tensor (e.g. first accumulation
+            # with a non-viewable layout): copy into the bucket view then re-alias
+            off = b.offsets[b.params.index(p)]
+            view = b.flat[off:off + p.numel()].view_as(p)
+            if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
+                view.copy_(p.grad)
+                p.grad = view
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch(b)
+
+        return hook
+
+    def _launch(self, b):
+        if b.launched:
+            return
+        b.launched = True
+        if self.world > 1:
+            b.flat.div_(self.world)
+            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+
+    def _finalize(self):
+        self._callback_queued = False
+        for b in self.buckets:
+            if not b.launched:
+                # parameters that received no gradient contribute zeros
+                self._launch(b)
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+            b.launched = False
+            b.pending = len(b.params)
+
+    # ------------------------------------------------------------------ API
+    def forward(self, *args, **kwargs):
+        # Buffers (BN running stats) are broadcast once at construction; per-forward
+        # broadcasts would add a collective to every step (see sync_buffers()).
+        return self.module(*args, **kwargs)
+
+    def sync_buffers(self):
+        self._sync_buffers()
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
+    def zero_grad(self, set_to_none=False):
+        for b in self.buckets:
+            b.flat.zero_()
+        for b in self.buckets:
+            for p, off in zip(b.params, b.offsets):
+                p.grad = b.flat[off:off + p.numel()].view_as(p)
+
+    def flat_grads(self):
+        return [b.flat for b in self.buckets]
+
+    def allreduce_now(self):
+        """Synchronous all-reduce of every bucket (used by the graph-captured step)."""
+        for b in self.buckets:
+            if self.world > 1:
+                b.flat.div_(self.world)
+                dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.process_group)
+
+    def state_dict(self, *a, **k):
+        return super().state_dict(*a, **k)
+
+
+class _SyncBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, group, world):
+        cnt = torch.tensor([x.shape[0]], dtype=x.dtype, device=x.device)
+        stats = torch.cat([x.sum(0), (x * x).sum(0), cnt])
+        dist.all_reduce(stats, group=group)
+        F = x.shape[1]
+        n = stats[-1]
+        mean = stats[:F] / n
+        var = stats[F:2 * F] / n - mean * mean
+        invstd = torch.rsqrt(var + eps)
+        xhat = (x - mean) * invstd
+        ctx.save_for_backward(xhat, invstd, weight, n)
+        ctx.group = group
+        y = xhat * weight + bias if weight is not None else xhat
+        return y, mean, var * n / (n - 1).clamp(min=1)
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _dv):
+        xhat, invstd, weight, n = ctx.saved_tensors
+        F = xhat.shape[1]
+        g = torch.cat([dy.sum(0), (dy * xhat).sum(0)])
+        dbias_local, dweight_local = g[:F].clone(), g[F:].clone()
+        dist.all_reduce(g, group=ctx.group)
+        sdy, sdyx = g[:F], g[F:]
+        w = weight if weight is not None else torch.ones_like(sdy)
+        dx = (dy - sdy / n - xhat * sdyx / n) * invstd * w
+        return dx, (dweight_local if weight is not None else None), (dbias_local if weight is not None else None), \
+            None, None, None
+
+
+class SyncBatchNorm(nn.Module):
+    """Cross-rank batch statistics (all-reduce of [sum, sumsq, count]); SURVEY §2.5 C4."""
+
+    def __init__(self, bn, group=None):
+        super().__init__()
+        self.module = bn
+        self.group = group
+
+    def forward(self, x, num_valid=None):
+        bn = self.module
+        if not bn.training or not dist.is_initialized():
+            return torch.nn.functional.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                                                  bn.training, bn.momentum, bn.eps)
+        y, mean, uvar = _SyncBNFn.apply(x, bn.weight, bn.bias, bn.eps, self.group, dist.get_world_size())
+        with torch.no_grad():
+            bn.running_mean.mul_(1 - bn.momentum).add_(bn.momentum * mean.detach())
+            bn.running_var.mul_(1 - bn.momentum).add_(bn.momentum * uvar.detach())
+            bn.num_batches_tracked.add_(1)
+        return y
+
+
+def convert_sync_batchnorm(model, group=None):
+    from ..models.layers import BatchNorm
+
+    for name, m in list(model.named_modules()):
+        if isinstance(m, BatchNorm):
+            m.module_sync = None
+            bn = m.module
+            m.forward = SyncBatchNorm(bn, group).forward
+    return model

@@ -1,0 +1,213 @@
+"""One training step on the GPU-resident data path, eager or hipGraph-captured.
+
+MI355X design: the GNN workloads of the reference are small-tensor, launch-
+bound problems (OC20 PNAPlus+GPS, hidden 64: a step issues several hundred
+kernels of a few microseconds each).  PyTorch-eager dispatch costs more CPU
+time per kernel than the GPU spends on it, so the production path captures the
+whole step —
+
+    batch assembly (gathers out of the HBM dataset pool) -> forward -> masked
+    loss -> backward -> [gradient all-reduce] -> AdamW
+
+— as hipGraphs (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replays
+them.  Shapes are made static by padding every batch up to a (nodes, edges)
+bucket (``DeviceGraphStore.layout``); one graph is captured per bucket (a
+handful per dataset) with its own memory pool.  For world_size > 1 the step is
+split in two graphs around an eager bucketed all-reduce of the flat gradient
+buffers (RCCL over xGMI): [assemble+fwd+bwd] -> all_reduce -> [optimizer].
+
+The per-step host work is only: draw indices, build the int32 plan (numpy),
+one pinned H2D copy, one or two graph launches.
+"""
+import math
+
+import numpy as np
+import torch
+
+from ..parallel.ddp import DistributedDataParallel
+
+
+def masked_loss(kind, pred, target, mask=None, var=None):
+    """Reference loss functions restricted to rows where ``mask`` is true."""
+    if mask is None:
+        if kind == "mse":
+            return torch.nn.functional.mse_loss(pred, target)
+        if kind == "mae":
+            return torch.nn.functional.l1_loss(pred, target)
+        if kind == "rmse":
+            return torch.sqrt(torch.nn.functional.mse_loss(pred, target))
+        if kind == "smooth_l1":
+            return torch.nn.functional.smooth_l1_loss(pred, target)
+        if kind == "GaussianNLLLoss":
+            return torch.nn.functional.gaussian_nll_loss(pred, target, var)
+        raise ValueError(kind)
+    m = mask.view(-1, *([1] * (pred.dim() - 1))).to(pred.dtype)
+    denom = m.sum() * (pred.numel() // pred.shape[0])
+    diff = pred - target
+    if kind in ("mse", "rmse"):
+        l = (diff * diff * m).sum() / denom
+        return torch.sqrt(l) if kind == "rmse" else l
+    if kind == "mae":
+        return (diff.abs() * m).sum() / denom
+    if kind == "smooth_l1":
+        a = diff.abs()
+        return (torch.where(a < 1.0, 0.5 * a * a, a - 0.5) * m).sum() / denom
+    if kind == "GaussianNLLLoss":
+        v = var.clamp(min=1e-6)
+        return (0.5 * (torch.log(v) + diff * diff / v) * m).sum() / denom
+    raise ValueError(kind)
+
+
+def batch_loss(module, pred, batch):
+    """Task-weighted multi-head loss against the per-head targets of a store batch."""
+    var = None
+    if module.var_output:
+        pred, var = pred
+    tot = 0
+    tasks = []
+    for ih in range(module.num_heads):
+        mask = batch.get("graph_mask") if module.head_type[ih] == "graph" else batch.get("node_mask")
+        v = None if var is None else var[ih]
+        l = masked_loss(module.loss_function_type, pred[ih], batch.targets[ih], mask, v)
+        tot = tot + l * module.loss_weights[ih]
+        tasks.append(l)
+    return tot, tasks
+
+
+class _Captured:
+    def __init__(self):
+        self.g_fwd_bwd = None
+        self.g_opt = None
+        self.dev_plan = None
+        self.loss = None
+        self.lay = None
+
+
+class TrainStep:
+    def __init__(self, model, lr=1e-3, mode="graph", world=1, optimizer=None, weight_decay=0.01,
+                 node_bucket=256, edge_bucket=2048, max_graphs=16):
+        self.model = model
+        self.module = model.module if isinstance(model, DistributedDataParallel) else model
+        self.world = world
+        self.mode = mode
+        dev = next(self.module.parameters()).device
+        self.device = dev
+        if world > 1 and not isinstance(model, DistributedDataParallel):
+            self.model = DistributedDataParallel(model)
+            self.module = self.model.module
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        if optimizer is None:
+            from ..optim.adamw import FusedAdamW
+
+            optimizer = FusedAdamW(params, lr=lr, weight_decay=weight_decay)
+        self.opt = optimizer
+        self.node_bucket, self.edge_bucket = node_bucket, edge_bucket
+        self.max_graphs = max_graphs
+        self.graphs = {}
+        self.pool = None
+        self.B = None
+
+    # ------------------------------------------------------------------ eager
+    def _zero(self):
+        if isinstance(self.model, DistributedDataParallel):
+            self.model.zero_grad()
+        else:
+            self.opt.zero_grad(set_to_none=False)
+
+    def eager(self, store, indices):
+        batch = store.batch(indices)
+        self._zero()
+        pred = self.model(batch)
+        loss, _ = batch_loss(self.module, pred, batch)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    # ------------------------------------------------------------------ graph
+    def bucket_of(self, N, E):
+        nb, eb = self.node_bucket, self.edge_bucket
+        return (int(math.ceil((N + 2) / nb) * nb), int(math.ceil(max(E, 1) / eb) * eb))
+
+    def prepare(self, store, batch_size, samples=256, seed=1234):
+        """Pre-compute the bucket set a random sampler will hit (capture happens lazily)."""
+        self.B = batch_size
+        if self.mode != "graph":
+            return
+        rng = np.random.default_rng(seed)
+        seen = set()
+        for _ in range(samples):
+            idx = rng.choice(len(store), size=min(batch_size, len(store)), replace=False)
+            seen.add(self.bucket_of(*store.sizes_of(idx)))
+        self.expected = sorted(seen)
+
+    def _pick(self, N, E):
+        want = self.bucket_of(N, E)
+        if want in self.graphs:
+            return want
+        cands = [k for k in self.graphs if k[0] >= N + 2 and k[1] >= E]
+        if cands and len(self.graphs) >= self.max_graphs:
+            return min(cands)
+        return want
+
+    def _body_fwd_bwd(self, store, cap):
+        self._zero()
+        batch = store.assemble(cap.dev_plan, cap.lay)
+        pred = self.model(batch)
+        loss, _ = batch_loss(self.module, pred, batch)
+        loss.backward()
+        return loss.detach()
+
+    def _capture(self, store, indices, key):
+        cap = _Captured()
+        Np, Ep = key
+        cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
+        cap.dev_plan = torch.empty(cap.lay.total, dtype=torch.int32, device=self.device)
+        store.upload(indices, cap.lay, cap.dev_plan)
+        ddp = isinstance(self.model, DistributedDataParallel)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up (allocator, kernels, autograd buffers) on real data
+                if ddp:
+                    with self.model.no_sync():
+                        self._body_fwd_bwd(store, cap)
+                    self.model.allreduce_now()
+                else:
+                    self._body_fwd_bwd(store, cap)
+                self.opt.step()
+        torch.cuda.current_stream().wait_stream(s)
+        pool = torch.cuda.graph_pool_handle()
+        cap.g_fwd_bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cap.g_fwd_bwd, pool=pool):
+            if ddp:
+                with self.model.no_sync():
+                    cap.loss = self._body_fwd_bwd(store, cap)
+            else:
+                cap.loss = self._body_fwd_bwd(store, cap)
+                self.opt.step()
+        if ddp:
+            cap.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cap.g_opt, pool=pool):
+                self.opt.step()
+        self.graphs[key] = cap
+        return cap
+
+    def graph_step(self, store, indices):
+        N, E = store.sizes_of(indices)
+        key = self._pick(N, E)
+        cap = self.graphs.get(key)
+        if cap is None:
+            cap = self._capture(store, indices, key)
+            # the capture warm-up already trained on this batch; replay once more as the step
+        lay = store.layout(indices, Np=cap.lay.Np, Ep=cap.lay.Ep, Gp=cap.lay.Gp)
+        store.upload(indices, lay, cap.dev_plan)
+        cap.g_fwd_bwd.replay()
+        if cap.g_opt is not None:
+            self.model.allreduce_now()
+            cap.g_opt.replay()
+        return cap.loss
+
+    def __call__(self, store, indices):
+        if self.mode == "graph" and self.device.type == "cuda":
+            return self.graph_step(store, indices)
+        return self.eager(store, indices)
