@@ -98,6 +98,7 @@ class _PNAFused(torch.autograd.Function):
     def forward(ctx, x, AB, C, G, dst_si, src_si, avg_log, avg_lin):
         Z, amin, amax = _native.ops().pna_fwd(x, AB, C, G, src_si.index, dst_si.rowptr, avg_log, avg_lin)
         ctx.save_for_backward(Z, AB, C, G, amin, amax)
+        ctx.has_C, ctx.has_G = C is not None, G is not None
         ctx.dst_si, ctx.src_si = dst_si, src_si
         ctx.avg = (avg_log, avg_lin)
         return Z
@@ -111,7 +112,9 @@ class _PNAFused(torch.autograd.Function):
         dB = _native.ops().seg_sum(dpre, ctx.src_si.rowptr, ctx.src_si.perm, ctx.src_si.num_segments, False)
         dAB = torch.cat([dA, dB], dim=1)
         dx = dZ[:, :F]
-        return dx, dAB, dpre, dG, None, None, None, None
+        dC = dpre if ctx.has_C else None
+        dG = dG if ctx.has_G else None
+        return dx, dAB, dC, dG, None, None, None, None
 
 
 def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
@@ -126,14 +129,19 @@ def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
         and not _state["composite"]
         and x.dtype == torch.float32
         and AB.dtype == torch.float32
-        and C.dtype == torch.float32
-        and G.dtype == torch.float32
+        and (C is None or C.dtype == torch.float32)
+        and (G is None or G.dtype == torch.float32)
         and dst_si.perm is None
     )
     if fused:
-        return _PNAFused.apply(x.contiguous(), AB, C.contiguous(), G.contiguous(), dst_si, src_si,
+        return _PNAFused.apply(x.contiguous(), AB, None if C is None else C.contiguous(),
+                               None if G is None else G.contiguous(), dst_si, src_si,
                                float(avg_deg["log"]), float(avg_deg["lin"]))
     A, B = AB[:, :F], AB[:, F:]
-    m = (seg.gather(A, dst_si) + seg.gather(B, src_si) + C) * G
+    m = seg.gather(A, dst_si) + seg.gather(B, src_si)
+    if C is not None:
+        m = m + C
+    if G is not None:
+        m = m * G
     agg = pna_aggregate_composite(m, dst_si, avg_deg)
     return torch.cat([x, agg], dim=-1)

@@ -9,7 +9,7 @@ learning rate and step counter are device scalars: changing ``lr`` through
 GPU: one kernel launch for all parameters (+1 tiny counter kernel).  CPU: the
 plain-torch update (reference math), used by the CPU tests.
 """
-import ctypes
+import struct
 
 import torch
 
@@ -50,12 +50,11 @@ class FusedAdamW(torch.optim.Optimizer):
             if not ps:
                 tables.append(None)
                 continue
-            blob = bytearray()
-            for r in refs:
-                blob += ctypes.string_at(ctypes.addressof((ctypes.c_uint64 * 4)(*r[:4])), 32)
-                blob += int(r[4]).to_bytes(8, "little", signed=True)
+            # TensorRef {float* p; const float* g; float* m; float* v; int64 n;} = 40 bytes
+            blob = b"".join(struct.pack("<QQQQq", *r) for r in refs)
+            assert len(blob) == 40 * len(refs) and struct.unpack_from("<QQQQq", blob, 40 * (len(refs) - 1)) == refs[-1]
             dev = ps[0].device
-            rb = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(dev)
+            rb = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
             bt = torch.tensor(blocks, dtype=torch.int32).view(-1).to(dev)
             step0 = float(self.state[ps[0]]["step"])
             state = torch.tensor([step0, group["lr"]], dtype=torch.float32, device=dev)
