@@ -22,9 +22,11 @@ as ready [G, d] / [N, d] tensors.
 Static padding (``Np``/``Ep``/``Gp``) produces fixed-shape batches so that
 ``assemble`` + forward + backward + optimizer can be captured once in a hipGraph
 and replayed (``train/step.py``): padded nodes form an extra dummy graph (and an
-extra attention segment), padded edges connect the last two padded nodes,
-padded nodes sit at distinct finite positions (no zero-length edges), and the
-device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked reductions.
+extra attention segment), padded edges are spread over the padded nodes
+(bounded degree, no self-loops), padded nodes sit at distinct finite positions
+(no zero-length edges), the model zeroes padded node rows after every layer,
+and the device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked
+reductions.
 """
 import numpy as np
 import torch
@@ -156,9 +158,16 @@ class DeviceGraphStore:
         if lay.padded:
             node_rows[N:] = -1
             erows[E:] = -1
-            src[E:] = Np - 2
-            dst[E:] = Np - 1
-            sperm[E:] = np.arange(E, Ep)
+            # padded edges spread evenly over the padded nodes (bounded degrees keep the
+            # dummy rows numerically tame), never self-loops, destination-sorted
+            pn, pe = Np - N, Ep - E
+            if pe:
+                k = np.arange(pe)
+                pd = (k * pn) // pe
+                ps = (pd + 1) % pn
+                dst[E:] = N + pd
+                src[E:] = N + ps
+                sperm[E:] = E + np.argsort(ps, kind="stable")
             batch[N:] = G
             gptr[G + 1:] = Np
             sidx[G:] = 0

@@ -19,7 +19,7 @@ MI355X-specific differences (semantics preserved):
 import torch
 import torch.nn.functional as F
 from torch import nn
-from torch.nn import Linear, ModuleDict, ModuleList, Sequential
+from torch.nn import ModuleDict, ModuleList, Sequential
 from torch.utils.checkpoint import checkpoint
 
 from ..ops import segment as seg
@@ -28,7 +28,7 @@ from ..utils import tracer as tr
 from ..utils.model import activation_function_selection, loss_function_selection
 from ..utils.print_utils import print_master
 from .gps import GPSConv
-from .layers import BatchNorm, Ctx
+from .layers import BatchNorm, Ctx, Linear
 
 
 class Base(nn.Module):
@@ -270,9 +270,15 @@ class Base(nn.Module):
 
     def encode(self, data):
         inv, equiv, ctx = self._embedding(data)
+        nmask = data.get("node_mask")  # statically padded batch: keep dummy rows at zero
+        if nmask is not None:
+            nmask = nmask.view(-1, 1).to(inv.dtype)
+            inv = inv * nmask
         for conv, bn in zip(self.graph_convs, self.feature_layers):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
             inv = self.activation_function(bn(inv, ctx.get("num_valid")))
+            if nmask is not None:
+                inv = inv * nmask
         return inv, equiv, ctx
 
     def _branch_ids(self, data):

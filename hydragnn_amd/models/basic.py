@@ -6,10 +6,10 @@ All aggregations are CSR segment reductions over destination-sorted edges
 """
 import torch
 from torch import nn
-from torch.nn import Linear
 
 from ..ops import segment as seg
 from .base import Base
+from .layers import Linear
 
 
 class GINConv(nn.Module):

@@ -17,7 +17,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.attention import segment_attention
-from .layers import BatchNorm
+from ..ops.linear import linear
+from .layers import BatchNorm, Linear
 
 
 class MultiheadAttention(nn.Module):
@@ -28,7 +29,7 @@ class MultiheadAttention(nn.Module):
         self.num_heads = num_heads
         self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
         self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim)) if bias else None
-        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=bias)
+        self.out_proj = Linear(embed_dim, embed_dim, bias=bias)
         self._reset_parameters()
 
     def _reset_parameters(self):
@@ -38,7 +39,7 @@ class MultiheadAttention(nn.Module):
             nn.init.zeros_(self.out_proj.bias)
 
     def forward(self, x, seg_id, seg_ptr):
-        qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+        qkv = linear(x, self.in_proj_weight, self.in_proj_bias)
         o = segment_attention(qkv, self.num_heads, seg_id, seg_ptr)
         return self.out_proj(o)
 
@@ -56,10 +57,10 @@ class PerformerAttention(nn.Module):
         self.heads = heads
         self.head_channels = head_channels
         inner = heads * head_channels
-        self.q = nn.Linear(channels, inner, bias=qkv_bias)
-        self.k = nn.Linear(channels, inner, bias=qkv_bias)
-        self.v = nn.Linear(channels, inner, bias=qkv_bias)
-        self.attn_out = nn.Linear(inner, channels, bias=attn_out_bias)
+        self.q = Linear(channels, inner, bias=qkv_bias)
+        self.k = Linear(channels, inner, bias=qkv_bias)
+        self.v = Linear(channels, inner, bias=qkv_bias)
+        self.attn_out = Linear(inner, channels, bias=attn_out_bias)
         m = num_features or max(1, int(head_channels * math.log(head_channels)))
         self.register_buffer("proj", torch.randn(m, head_channels))
 
@@ -103,10 +104,10 @@ class GPSConv(nn.Module):
         else:
             raise ValueError(f"{attn_type} is not supported")
         self.mlp = nn.Sequential(
-            nn.Linear(channels, channels * 2),
+            Linear(channels, channels * 2),
             nn.ReLU() if act == "relu" else act,
             nn.Dropout(dropout),
-            nn.Linear(channels * 2, channels),
+            Linear(channels * 2, channels),
             nn.Dropout(dropout),
         )
         self.norm1 = BatchNorm(channels) if norm else None

@@ -3,6 +3,16 @@ import torch
 from torch import nn
 
 
+class Linear(nn.Linear):
+    """``nn.Linear`` (same parameters/state-dict keys) whose backward uses the
+    split-K weight-gradient HIP kernel for tall activations (``ops/linear.py``)."""
+
+    def forward(self, x):
+        from ..ops.linear import linear
+
+        return linear(x, self.weight, self.bias)
+
+
 class BatchNorm(nn.Module):
     """Node-feature batch norm with PyG ``BatchNorm`` parameter naming (``.module``).
 
@@ -48,7 +58,7 @@ class Ctx:
 def mlp(dims, act, last_act=False, bias=True):
     layers = []
     for i in range(len(dims) - 1):
-        layers.append(nn.Linear(dims[i], dims[i + 1], bias=bias))
+        layers.append(Linear(dims[i], dims[i + 1], bias=bias))
         if i < len(dims) - 2 or last_act:
             layers.append(act)
     return nn.Sequential(*layers)

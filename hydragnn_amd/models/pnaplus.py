@@ -19,11 +19,13 @@ Parameter names match the reference (``pre_nns.0.0``, ``post_nns.0.0``, ``lin``,
 import torch
 import torch.nn.functional as F
 from torch import nn
-from torch.nn import Linear, ModuleList, Sequential
+from torch.nn import ModuleList, Sequential
 
 from ..ops.geometry import BesselBasis, edge_vectors_and_lengths
+from ..ops.linear import linear, linear_sum
 from ..ops.pna import pna_avg_deg, pna_message_aggregate
 from .base import Base
+from .layers import Linear
 
 
 class PNAConvFused(nn.Module):
@@ -60,7 +62,7 @@ class PNAConvFused(nn.Module):
         pre = self.pre_nns[0][0]
         W, b = pre.weight, pre.bias
         # AB[:, :F] = W_i x + b (x_i, destination), AB[:, F:] = W_j x (x_j, source): one node GEMM
-        AB = F.linear(x, torch.cat([W[:, :Fi], W[:, Fi:2 * Fi]], 0), torch.cat([b, torch.zeros_like(b)]))
+        AB = linear(x, torch.cat([W[:, :Fi], W[:, Fi:2 * Fi]], 0), torch.cat([b, torch.zeros_like(b)]))
         C = None
         G = None
         if self.plus:
@@ -72,13 +74,13 @@ class PNAConvFused(nn.Module):
                 Wc = We @ enc.weight  # [F, d + F]
                 bc = We @ enc.bias
                 d = self.edge_dim
-                C = torch.addmm(torch.addmm(bc, r, Wc[:, d:].t()), ctx.edge_attr, Wc[:, :d].t())
+                C = linear_sum([(r, Wc[:, d:]), (ctx.edge_attr, Wc[:, :d])], bc)
             else:
-                C = F.linear(r, We, None)
+                C = linear(r, We, None)
             G = self.rbf_lin(rbf)
         elif self.edge_dim is not None and ctx.edge_attr is not None:
             We = W[:, 2 * Fi:]
-            C = F.linear(ctx.edge_attr, We @ self.edge_encoder.weight, We @ self.edge_encoder.bias)
+            C = linear(ctx.edge_attr, We @ self.edge_encoder.weight, We @ self.edge_encoder.bias)
         Z = pna_message_aggregate(x, AB, C, G, ctx.dst_si, ctx.src_si, self.avg_deg)
         out = self.post_nns[0](Z)
         return self.lin(out), equiv

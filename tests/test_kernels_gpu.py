@@ -159,3 +159,67 @@ def test_fused_adamw_matches_cpu():
     for a, b, c in zip(gpu, cpu, ref.param_groups[0]["params"]):
         torch.testing.assert_close(a.detach().cpu(), b.detach(), rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(b.detach(), c.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("F", [64, 7, 300])
+@pytest.mark.parametrize("masked", [False, True])
+def test_batchnorm_fused(F, masked):
+    from hydragnn_amd.ops.norm import _masked_batch_norm, batch_norm
+
+    torch.manual_seed(F)
+    N = 1000
+    x = torch.randn(N, F) * 3 + 1
+    nv = 777 if masked else None
+    bn_c = torch.nn.BatchNorm1d(F)
+    with torch.no_grad():
+        bn_c.weight.uniform_(0.5, 1.5)
+        bn_c.bias.uniform_(-0.5, 0.5)
+    bn_g = torch.nn.BatchNorm1d(F).to(DEV)
+    bn_g.load_state_dict(bn_c.state_dict())
+    xc = x.clone().requires_grad_()
+    yc = _masked_batch_norm(xc, bn_c, nv) if masked else bn_c(xc)
+    xg = x.to(DEV).requires_grad_()
+    nvg = torch.tensor(nv, dtype=torch.int32, device=DEV) if masked else None
+    yg = batch_norm(xg, bn_g, nvg)
+    torch.testing.assert_close(yg.cpu(), yc.detach(), rtol=1e-4, atol=1e-4)
+    g = torch.randn(N, F)
+    yc.backward(g)
+    yg.backward(g.to(DEV))
+    torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn_g.weight.grad.cpu(), bn_c.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn_g.bias.grad.cpu(), bn_c.bias.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn_g.running_mean.cpu(), bn_c.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn_g.running_var.cpu(), bn_c.running_var, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,O,I", [(23000, 64, 64), (5000, 64, 1088), (3000, 7, 130), (1500, 192, 64)])
+def test_linear_wgrad(M, O, I):
+    from hydragnn_amd.ops.linear import linear, linear_sum
+
+    torch.manual_seed(M)
+    x = torch.randn(M, I)
+    W = torch.randn(O, I) / I ** 0.5
+    b = torch.randn(O)
+    xc, Wc, bc = (t.clone().requires_grad_() for t in (x, W, b))
+    xg, Wg, bg = (t.to(DEV).requires_grad_() for t in (x, W, b))
+    yc = torch.nn.functional.linear(xc, Wc, bc)
+    yg = linear(xg, Wg, bg)
+    g = torch.randn(M, O)
+    yc.backward(g)
+    yg.backward(g.to(DEV))
+    torch.testing.assert_close(yg.detach().cpu(), yc.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(Wg.grad.cpu(), Wc.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bg.grad.cpu(), bc.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-4, atol=1e-4)
+    # two-input sum form
+    x2 = torch.randn(M, 5)
+    W2 = torch.randn(O, 5)
+    W2c, W2g = W2.clone().requires_grad_(), W2.to(DEV).requires_grad_()
+    Wc.grad = None
+    Wg.grad = None
+    yc = torch.nn.functional.linear(xc, Wc, bc) + x2 @ W2c.t()
+    yg = linear_sum([(xg, Wg), (x2.to(DEV), W2g)], bg)
+    yc.backward(g)
+    yg.backward(g.to(DEV))
+    torch.testing.assert_close(W2g.grad.cpu(), W2c.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(Wg.grad.cpu(), Wc.grad, rtol=1e-4, atol=1e-3)
