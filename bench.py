@@ -94,6 +94,7 @@ def main():
         return idx
 
     step.prepare(store, B)
+    step.precapture(store, B)
     for _ in range(args.warmup):
         step(store, next_indices())
     torch.cuda.synchronize()
@@ -102,7 +103,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step(store, next_indices())
+        loss, _ = step(store, next_indices())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -270,3 +270,45 @@ def collate(samples, build_csr=True):
 # PyG-compatible alias
 Data = Graph
 Batch = GraphBatch
+
+
+def head_targets(batch, head_types, head_dims):
+    """Unpack the packed ``y``/``y_loc`` of a collated batch into per-head targets
+    ([G, d] for graph heads, [N, d] for node heads), vectorised — replaces the
+    reference's per-batch host index loops (``train_validate_test.py:316-379``)."""
+    y = batch.y.reshape(-1)
+    yl = batch.y_loc.to(y.device).long()
+    G = yl.shape[0]
+    total = yl[:, -1]
+    start = torch.cumsum(total, 0) - total
+    out = []
+    ptr = batch.ptr.to(y.device).long()
+    nnodes = ptr[1:] - ptr[:-1]
+    for ih, (t, d) in enumerate(zip(head_types, head_dims)):
+        base = start + yl[:, ih]
+        if t == "graph":
+            idx = base.view(-1, 1) + torch.arange(d, device=y.device).view(1, -1)
+            out.append(y[idx.reshape(-1)].view(G, d))
+        else:
+            bnode = torch.repeat_interleave(torch.arange(G, device=y.device), nnodes)
+            local = torch.arange(bnode.numel(), device=y.device) - ptr[bnode]
+            idx = (base[bnode] + local * d).view(-1, 1) + torch.arange(d, device=y.device).view(1, -1)
+            out.append(y[idx.reshape(-1)].view(-1, d))
+    return out
+
+
+def get_head_indices(head_types, head_dims, batch):
+    """Reference-compatible flat indices into ``batch.y`` per head."""
+    y = batch.y.reshape(-1)
+    yl = batch.y_loc.long()
+    G = yl.shape[0]
+    if len(head_types) == 1:
+        return [torch.arange(y.numel())]
+    total = yl[:, -1]
+    start = torch.cumsum(total, 0) - total
+    out = []
+    for ih in range(len(head_types)):
+        s = start + yl[:, ih]
+        e = start + yl[:, ih + 1]
+        out.append(torch.cat([torch.arange(int(a), int(b)) for a, b in zip(s, e)]))
+    return out

@@ -1,0 +1,93 @@
+"""``run_training(config | path)`` (reference ``hydragnn/run_training.py:49-182``).
+
+Pipeline: logging -> process group -> data (raw -> serialized -> splits ->
+loaders) -> ``update_config`` -> model -> DDP wrap (bucketed RCCL all-reduce) ->
+optimizer + ``ReduceLROnPlateau(factor=0.5, patience=5, min_lr=1e-5)`` ->
+optional resume -> ``train_validate_test`` -> ``save_model`` -> timers.
+
+On a GPU the splits are moved into HBM (``DeviceGraphStore``) and training
+batches run through the hipGraph-captured ``TrainStep`` (set
+``HYDRAGNN_CAPTURE=0`` for eager, ``HYDRAGNN_DEVICE_DATA=0`` for the host
+loader path).  Force training (``compute_grad_energy``) uses the eager
+double-backward path.
+"""
+import json
+import os
+from functools import singledispatch
+
+import torch
+import torch.distributed as dist
+
+from .data.load_data import dataset_loading_and_splitting, to_device_loaders
+from .models.create import create_model_config
+from .parallel.distributed import get_device, get_distributed_model, setup_ddp
+from .train.step import TrainStep
+from .train.train_validate_test import train_validate_test
+from .utils.config_utils import get_log_name_config, save_config, update_config
+from .utils.model import get_summary_writer, load_existing_model_config, save_model
+from .utils.optimizer import select_optimizer
+from .utils.print_utils import print_distributed, setup_log
+from .utils.time_utils import print_timers
+
+
+@singledispatch
+def run_training(config, use_deepspeed=False):
+    raise TypeError("Input must be filename string or configuration dictionary.")
+
+
+@run_training.register
+def _(config_file: str, use_deepspeed=False):
+    with open(config_file, "r") as f:
+        config = json.load(f)
+    return run_training(config, use_deepspeed)
+
+
+def _device_path_enabled(config):
+    return torch.cuda.is_available() and int(os.getenv("HYDRAGNN_DEVICE_DATA", "1")) == 1
+
+
+@run_training.register
+def _(config: dict, use_deepspeed=False):
+    assert not use_deepspeed, "DeepSpeed is not part of hydragnn_amd (ZeRO-1 via Optimizer.use_zero_redundancy)"
+    verbosity = config["Verbosity"]["level"]
+    os.environ.setdefault("SERIALIZED_DATA_PATH", os.getcwd())
+    setup_log(get_log_name_config(config))
+    setup_ddp()
+    train_loader, val_loader, test_loader = dataset_loading_and_splitting(config=config)
+    config = update_config(config, train_loader, val_loader, test_loader)
+    vis = config.get("Visualization", {})
+    plot_init_solution = vis.get("plot_init_solution", False)
+    plot_hist_solution = vis.get("plot_hist_solution", False)
+    create_plots = vis.get("create_plots", False)
+    nn_cfg = config["NeuralNetwork"]
+    model = create_model_config(config=nn_cfg, verbosity=verbosity)
+    log_name = get_log_name_config(config)
+    model = get_distributed_model(model, verbosity, sync_batch_norm=nn_cfg["Architecture"].get("SyncBatchNorm", False),
+                                  find_unused_parameters=True)
+    optimizer = select_optimizer(model, nn_cfg["Training"]["Optimizer"])
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=0.5, patience=5,
+                                                           min_lr=0.00001)
+    writer = get_summary_writer(log_name)
+    if dist.is_initialized():
+        dist.barrier()
+    save_config(config, log_name)
+    load_existing_model_config(model, nn_cfg["Training"], optimizer=optimizer)
+    compute_grad_energy = nn_cfg["Training"].get("compute_grad_energy", False)
+    engine = None
+    if _device_path_enabled(config):
+        module = model.module if hasattr(model, "module") else model
+        train_loader, val_loader, test_loader = to_device_loaders(
+            (train_loader, val_loader, test_loader), get_device(), module.head_type, module.head_dims,
+            attn_scope=getattr(module, "attn_scope", "batch"))
+        mode = "graph" if (int(os.getenv("HYDRAGNN_CAPTURE", "1")) == 1 and not compute_grad_energy) else "eager"
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer)
+        engine.prepare(train_loader.store, train_loader.batch_size)
+    print_distributed(verbosity, f"model: {nn_cfg['Architecture']['mpnn_type']}, "
+                                 f"params: {sum(p.numel() for p in model.parameters())}")
+    train_validate_test(model, optimizer, train_loader, val_loader, test_loader, writer, scheduler, nn_cfg, log_name,
+                        verbosity, plot_init_solution, plot_hist_solution, create_plots,
+                        compute_grad_energy=compute_grad_energy, step_engine=engine)
+    save_model(model, optimizer, log_name)
+    print_timers(verbosity)
+    return model

@@ -74,12 +74,35 @@ def batch_loss(module, pred, batch):
     return tot, tasks
 
 
+class FlatGrads:
+    """All parameter gradients as views of ONE flat buffer: zero_grad is a single
+    memset (instead of one fill kernel per parameter) and the buffer is the unit
+    of the gradient all-reduce."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device if self.params else "cpu"
+        self.flat = torch.zeros(n, device=dev, dtype=self.params[0].dtype if self.params else torch.float32)
+        self.attach()
+
+    def attach(self):
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero(self):
+        self.flat.zero_()
+
+
 class _Captured:
     def __init__(self):
         self.g_fwd_bwd = None
         self.g_opt = None
         self.dev_plan = None
         self.loss = None
+        self.tasks = None
         self.lay = None
 
 
@@ -101,6 +124,7 @@ class TrainStep:
 
             optimizer = FusedAdamW(params, lr=lr, weight_decay=weight_decay)
         self.opt = optimizer
+        self.flat_grads = None if isinstance(self.model, DistributedDataParallel) else FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket
         self.max_graphs = max_graphs
         self.graphs = {}
@@ -112,16 +136,16 @@ class TrainStep:
         if isinstance(self.model, DistributedDataParallel):
             self.model.zero_grad()
         else:
-            self.opt.zero_grad(set_to_none=False)
+            self.flat_grads.zero()
 
     def eager(self, store, indices):
         batch = store.batch(indices)
         self._zero()
         pred = self.model(batch)
-        loss, _ = batch_loss(self.module, pred, batch)
+        loss, tasks = batch_loss(self.module, pred, batch)
         loss.backward()
         self.opt.step()
-        return loss.detach()
+        return loss.detach(), [t.detach() for t in tasks]
 
     # ------------------------------------------------------------------ graph
     def bucket_of(self, N, E):
@@ -140,6 +164,22 @@ class TrainStep:
             seen.add(self.bucket_of(*store.sizes_of(idx)))
         self.expected = sorted(seen)
 
+    def precapture(self, store, batch_size, max_draws=2000, seed=4321):
+        """Capture every bucket ``prepare`` predicted, on real batches drawn at random,
+        so no capture (hundreds of ms) lands inside a timed/training region."""
+        if self.mode != "graph" or self.device.type != "cuda":
+            return
+        rng = np.random.default_rng(seed)
+        todo = set(getattr(self, "expected", []))
+        for _ in range(max_draws):
+            if not todo:
+                break
+            idx = rng.choice(len(store), size=min(batch_size, len(store)), replace=False)
+            key = self.bucket_of(*store.sizes_of(idx))
+            if key in todo and key not in self.graphs:
+                self._capture(store, idx, key)
+                todo.discard(key)
+
     def _pick(self, N, E):
         want = self.bucket_of(N, E)
         if want in self.graphs:
@@ -153,11 +193,40 @@ class TrainStep:
         self._zero()
         batch = store.assemble(cap.dev_plan, cap.lay)
         pred = self.model(batch)
-        loss, _ = batch_loss(self.module, pred, batch)
+        loss, tasks = batch_loss(self.module, pred, batch)
         loss.backward()
-        return loss.detach()
+        return loss.detach(), [t.detach() for t in tasks]
+
+    def _opt_state_tensors(self):
+        out = []
+        for v in getattr(self.opt, "state", {}).values():
+            for t in v.values():
+                if torch.is_tensor(t):
+                    out.append(t)
+        return out
+
+    def _snapshot(self):
+        ts = list(self.module.parameters()) + list(self.module.buffers()) + self._opt_state_tensors()
+        tables = [t for t in (getattr(self.opt, "_tables", None) or []) if t is not None]
+        return {"pairs": [(t, t.detach().clone()) for t in ts], "ids": {id(t) for t in ts},
+                "steps": [float(t[2][0]) for t in tables]}
+
+    @torch.no_grad()
+    def _restore(self, snap):
+        for t, v in snap["pairs"]:
+            t.copy_(v)
+        for t in self._opt_state_tensors():  # created during warm-up -> fresh (zero) state
+            if id(t) not in snap["ids"]:
+                t.zero_()
+        tables = [t for t in (getattr(self.opt, "_tables", None) or []) if t is not None]
+        for i, t in enumerate(tables):
+            t[2][0].fill_(snap["steps"][i] if i < len(snap["steps"]) else 0.0)
 
     def _capture(self, store, indices, key):
+        """Warm up + capture one bucket.  Parameters, buffers and optimizer state are
+        restored afterwards, so the warm-up iterations do not count as training steps."""
+        torch.cuda.synchronize()
+        snap = self._snapshot()
         cap = _Captured()
         Np, Ep = key
         cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
@@ -181,15 +250,17 @@ class TrainStep:
         with torch.cuda.graph(cap.g_fwd_bwd, pool=pool):
             if ddp:
                 with self.model.no_sync():
-                    cap.loss = self._body_fwd_bwd(store, cap)
+                    cap.loss, cap.tasks = self._body_fwd_bwd(store, cap)
             else:
-                cap.loss = self._body_fwd_bwd(store, cap)
+                cap.loss, cap.tasks = self._body_fwd_bwd(store, cap)
                 self.opt.step()
         if ddp:
             cap.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(cap.g_opt, pool=pool):
                 self.opt.step()
         self.graphs[key] = cap
+        torch.cuda.synchronize()
+        self._restore(snap)
         return cap
 
     def graph_step(self, store, indices):
@@ -205,7 +276,7 @@ class TrainStep:
         if cap.g_opt is not None:
             self.model.allreduce_now()
             cap.g_opt.replay()
-        return cap.loss
+        return cap.loss, cap.tasks
 
     def __call__(self, store, indices):
         if self.mode == "graph" and self.device.type == "cuda":

@@ -1,0 +1,370 @@
+"""Epoch loop, train / validate / test (reference ``hydragnn/train/train_validate_test.py:39-748``).
+
+Same control flow and outputs as the reference (per-epoch train/val/test losses
+and per-task losses, ReduceLROnPlateau on the validation loss, EarlyStopping,
+Checkpoint, Slurm walltime guard, ``HYDRAGNN_MAX_NUM_BATCH``,
+``HYDRAGNN_VALTEST``, ``HYDRAGNN_TRACE_LEVEL`` region tracing, the profiler
+schedule, ``test()`` returning gathered true/predicted values per head).
+
+MI355X data path: when the loaders are ``DeviceGraphLoader`` (HBM-resident
+splits) the training batches run through ``TrainStep`` — batch assembly,
+forward, backward, gradient all-reduce and the fused optimizer captured as
+hipGraphs — and evaluation runs on device-assembled batches.  Host loaders
+(``GraphDataLoader``, e.g. CPU/gloo runs) take the eager path.
+"""
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..data.graph import head_targets
+from ..data.loader import DeviceGraphLoader
+from ..ops.pna import composite_mode
+from ..parallel.distributed import check_remaining, get_comm_size_and_rank, get_device
+from ..utils import tracer as tr
+from ..utils.model import Checkpoint, EarlyStopping
+from ..utils.print_utils import iterate_tqdm, print_distributed
+from ..utils.profile import Profiler
+from ..utils.time_utils import Timer
+from .step import TrainStep, batch_loss
+
+
+def _module(model):
+    return model.module if hasattr(model, "module") else model
+
+
+def get_nbatch(loader):
+    nbatch = len(loader)
+    env = os.getenv("HYDRAGNN_MAX_NUM_BATCH")
+    if env is not None:
+        nbatch = min(nbatch, int(env))
+    return nbatch
+
+
+def prepare_batch(data, module, device):
+    """Host batch -> device + per-head targets; device batches pass through."""
+    if data.get("targets") is not None:
+        return data
+    if data.x is not None and data.x.device != device:
+        data = data.to(device, non_blocking=True)
+    data["targets"] = head_targets(data, module.head_type, module.head_dims) if data.get("y") is not None else []
+    return data
+
+
+def _loss(module, pred, data, compute_grad_energy):
+    if compute_grad_energy:
+        return module.energy_force_loss(pred, data)
+    return batch_loss(module, pred, data)
+
+
+@torch.no_grad()
+def reduce_values_ranks(local_tensor):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = local_tensor.clone()
+        if not t.is_cuda and dist.get_backend() != "gloo":
+            from ..parallel.distributed import host_group
+
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=host_group())
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t / dist.get_world_size()
+    return local_tensor
+
+
+reduce_values_ranks_dist = reduce_values_ranks
+
+
+@torch.no_grad()
+def gather_tensor_ranks(head_values):
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return head_values
+    W = dist.get_world_size()
+    dev = head_values.device
+    size_local = torch.tensor([head_values.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.ones_like(size_local) for _ in range(W)]
+    dist.all_gather(sizes, size_local)
+    sizes = torch.cat(sizes)
+    mx = int(sizes.max())
+    padded = torch.zeros((mx,) + tuple(head_values.shape[1:]), dtype=head_values.dtype, device=dev)
+    padded[: head_values.shape[0]] = head_values
+    lst = [torch.empty_like(padded) for _ in range(W)]
+    dist.all_gather(lst, padded)
+    return torch.cat([t[: int(s)] for t, s in zip(lst, sizes)], 0)
+
+
+def train(loader, model, opt, verbosity, profiler=None, use_deepspeed=False, compute_grad_energy=False,
+          step_engine=None):
+    module = _module(model)
+    device = next(module.parameters()).device
+    total_error = torch.tensor(0.0, device=device)
+    tasks_error = torch.zeros(module.num_heads, device=device)
+    num_samples = 0
+    model.train()
+    nbatch = get_nbatch(loader)
+    trace_level = int(os.getenv("HYDRAGNN_TRACE_LEVEL", "0"))
+    sync = {"cudasync": trace_level > 0}
+    use_engine = step_engine is not None and isinstance(loader, DeviceGraphLoader) and not compute_grad_energy
+    tr.start("dataload", **sync)
+    it = loader.index_batches() if use_engine else iter(loader)
+    for ibatch, data in iterate_tqdm(enumerate(it), verbosity, desc="Train", total=nbatch):
+        if ibatch >= nbatch:
+            break
+        tr.stop("dataload", **sync)
+        if use_engine:
+            tr.start("step", **sync)
+            loss, tasks = step_engine(loader.store, data)
+            tr.stop("step", **sync)
+            ng = len(data)
+        else:
+            tr.start("zero_grad")
+            if step_engine is not None:
+                step_engine._zero()
+            else:
+                opt.zero_grad()
+            tr.stop("zero_grad")
+            tr.start("forward", **sync)
+            data = prepare_batch(data, module, device)
+            if compute_grad_energy:
+                data.pos.requires_grad_(True)
+                with composite_mode(True):
+                    pred = model(data)
+                    loss, tasks = _loss(module, pred, data, True)
+            else:
+                pred = model(data)
+                loss, tasks = _loss(module, pred, data, False)
+            tr.stop("forward", **sync)
+            tr.start("backward", **sync)
+            if compute_grad_energy:
+                with composite_mode(True):
+                    loss.backward()
+            else:
+                loss.backward()
+            tr.stop("backward", **sync)
+            tr.start("opt_step", **sync)
+            opt.step()
+            tr.stop("opt_step", **sync)
+            ng = data.get("num_graphs_real", data.num_graphs)
+        if profiler is not None:
+            profiler.step()
+        with torch.no_grad():
+            total_error += loss.detach() * ng
+            num_samples += ng
+            for k in range(len(tasks)):
+                tasks_error[k] += tasks[k].detach() * ng
+        if ibatch < nbatch - 1:
+            tr.start("dataload", **sync)
+    n = max(num_samples, 1)
+    return total_error / n, tasks_error / n
+
+
+def _eval_batches(loader, nbatch):
+    for ibatch, data in enumerate(loader):
+        if ibatch >= nbatch:
+            break
+        yield data
+
+
+@torch.no_grad()
+def validate(loader, model, verbosity, reduce_ranks=True, compute_grad_energy=False):
+    module = _module(model)
+    device = next(module.parameters()).device
+    total_error = torch.tensor(0.0, device=device)
+    tasks_error = torch.zeros(module.num_heads, device=device)
+    num_samples = 0
+    model.eval()
+    nbatch = get_nbatch(loader)
+    for data in iterate_tqdm(_eval_batches(loader, nbatch), verbosity, desc="Validate", total=nbatch):
+        data = prepare_batch(data, module, device)
+        if compute_grad_energy:
+            with torch.enable_grad(), composite_mode(True):
+                data.pos.requires_grad_(True)
+                pred = model(data)
+                err, tasks = _loss(module, pred, data, True)
+        else:
+            pred = model(data)
+            err, tasks = _loss(module, pred, data, False)
+        ng = data.get("num_graphs_real", data.num_graphs)
+        total_error += err.detach() * ng
+        num_samples += ng
+        for k in range(len(tasks)):
+            tasks_error[k] += tasks[k].detach() * ng
+    n = max(num_samples, 1)
+    val_error, tasks_error = total_error / n, tasks_error / n
+    if reduce_ranks:
+        val_error = reduce_values_ranks(val_error)
+        tasks_error = reduce_values_ranks(tasks_error)
+    return val_error, tasks_error
+
+
+@torch.no_grad()
+def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compute_grad_energy=False):
+    module = _module(model)
+    device = next(module.parameters()).device
+    total_error = torch.tensor(0.0, device=device)
+    tasks_error = torch.zeros(module.num_heads, device=device)
+    num_samples = 0
+    model.eval()
+    nbatch = get_nbatch(loader)
+    true_values = [[] for _ in range(module.num_heads)]
+    predicted_values = [[] for _ in range(module.num_heads)]
+    for data in iterate_tqdm(_eval_batches(loader, nbatch), verbosity, desc="Test", total=nbatch):
+        data = prepare_batch(data, module, device)
+        if compute_grad_energy:
+            with torch.enable_grad(), composite_mode(True):
+                data.pos.requires_grad_(True)
+                pred = model(data)
+                err, tasks = _loss(module, pred, data, True)
+        else:
+            pred = model(data)
+            err, tasks = _loss(module, pred, data, False)
+        ng = data.get("num_graphs_real", data.num_graphs)
+        total_error += err.detach() * ng
+        num_samples += ng
+        for k in range(len(tasks)):
+            tasks_error[k] += tasks[k].detach() * ng
+        if return_samples and not compute_grad_energy:
+            p = pred[0] if module.var_output else pred
+            for ih in range(module.num_heads):
+                true_values[ih].append(data.targets[ih].reshape(-1, 1))
+                predicted_values[ih].append(p[ih].reshape(-1, 1))
+    n = max(num_samples, 1)
+    test_error, tasks_error = total_error / n, tasks_error / n
+    if return_samples and true_values[0]:
+        for ih in range(module.num_heads):
+            true_values[ih] = torch.cat(true_values[ih], 0)
+            predicted_values[ih] = torch.cat(predicted_values[ih], 0)
+    if reduce_ranks:
+        test_error = reduce_values_ranks(test_error)
+        tasks_error = reduce_values_ranks(tasks_error)
+        if return_samples and len(true_values[0]) > 0:
+            for ih in range(module.num_heads):
+                true_values[ih] = gather_tensor_ranks(true_values[ih])
+                predicted_values[ih] = gather_tensor_ranks(predicted_values[ih])
+    return test_error, tasks_error, true_values, predicted_values
+
+
+def train_validate_test(model, optimizer, train_loader, val_loader, test_loader, writer, scheduler, config,
+                        model_with_config_name, verbosity=0, plot_init_solution=True, plot_hist_solution=False,
+                        create_plots=False, use_deepspeed=False, compute_grad_energy=False, step_engine=None,
+                        trainer_state=None):
+    module = _module(model)
+    tcfg = config["Training"]
+    num_epoch = tcfg["num_epoch"]
+    early = tcfg.get("EarlyStopping", False)
+    check_time = tcfg.get("CheckRemainingTime", False)
+    save_ckpt = tcfg.get("Checkpoint", False)
+    device = next(module.parameters()).device
+    H = module.num_heads
+    total_loss = {k: torch.zeros(num_epoch, device=device) for k in ("train", "val", "test")}
+    task_loss = {k: torch.zeros((num_epoch, H), device=device) for k in ("train", "val", "test")}
+    visualizer = None
+    if create_plots:
+        from ..postprocess.visualizer import Visualizer
+
+        node_feature, nodes_num = [], []
+        for d in test_loader.dataset:
+            node_feature.extend(d.x.tolist())
+            nodes_num.append(d.num_nodes)
+        visualizer = Visualizer(model_with_config_name, node_feature=node_feature, num_heads=H,
+                                head_dims=module.head_dims, num_nodes_list=nodes_num)
+        visualizer.num_nodes_plot()
+        if plot_init_solution:
+            _, _, tv, pv = test(test_loader, model, verbosity)
+            visualizer.create_scatter_plots(tv, pv, output_names=config["Variables_of_interest"]["output_names"],
+                                            iepoch=-1)
+    profiler = Profiler("./logs/" + model_with_config_name)
+    if "Profile" in config:
+        profiler.setup(config["Profile"])
+    earlystopper = EarlyStopping(patience=tcfg.get("patience", 10)) if early else None
+    checkpoint = Checkpoint(name=model_with_config_name, warmup=tcfg.get("checkpoint_warmup", 0)) if save_ckpt else None
+    if trainer_state is not None:
+        if earlystopper is not None and "early_stopping" in trainer_state:
+            earlystopper.load_state_dict(trainer_state["early_stopping"])
+    timer = Timer("train_validate_test")
+    timer.start()
+    epoch_start = tcfg.get("epoch_start", 0)
+    metrics_path = os.path.join("./logs", model_with_config_name, "metrics.jsonl")
+    _, rank = get_comm_size_and_rank()
+    epoch = epoch_start - 1
+    for epoch in range(epoch_start, num_epoch):
+        os.environ["HYDRAGNN_EPOCH"] = str(epoch)
+        t0 = time.time()
+        profiler.set_current_epoch(epoch)
+        for ld in (train_loader, val_loader, test_loader):
+            if getattr(ld.sampler, "set_epoch", None) is not None:
+                ld.sampler.set_epoch(epoch)
+        with profiler as prof:
+            tr.enable()
+            tr.start("train")
+            train_loss, train_tasks = train(train_loader, model, optimizer, verbosity, profiler=prof,
+                                            compute_grad_energy=compute_grad_energy, step_engine=step_engine)
+            tr.stop("train")
+            tr.disable()
+            if epoch == 0:
+                tr.reset()
+        t_train = time.time() - t0
+        if rank == 0:
+            from ..utils.metrics import log_json
+
+            ntrain = min(len(train_loader), get_nbatch(train_loader)) * train_loader.batch_size
+            log_json(metrics_path, epoch=epoch, train_loss=float(train_loss), train_seconds=t_train,
+                     graphs_per_sec_rank0=ntrain / max(t_train, 1e-9))
+        if int(os.getenv("HYDRAGNN_VALTEST", "1")) == 0:
+            continue
+        val_loss, val_tasks = validate(val_loader, model, verbosity, reduce_ranks=True,
+                                       compute_grad_energy=compute_grad_energy)
+        test_loss, test_tasks, tv, pv = test(test_loader, model, verbosity, reduce_ranks=True,
+                                             return_samples=plot_hist_solution,
+                                             compute_grad_energy=compute_grad_energy)
+        if scheduler is not None:
+            scheduler.step(float(val_loss))
+        if writer is not None:
+            writer.add_scalar("train error", train_loss, epoch)
+            writer.add_scalar("validate error", val_loss, epoch)
+            writer.add_scalar("test error", test_loss, epoch)
+            for k in range(H):
+                writer.add_scalar("train error of task" + str(k), train_tasks[k], epoch)
+        print_distributed(verbosity, f"Epoch: {epoch:02d}, Train Loss: {float(train_loss):.8f}, "
+                                     f"Val Loss: {float(val_loss):.8f}, Test Loss: {float(test_loss):.8f}")
+        print_distributed(verbosity, "Tasks Train Loss:", [float(t) for t in train_tasks])
+        print_distributed(verbosity, "Tasks Val Loss:", [float(t) for t in val_tasks])
+        print_distributed(verbosity, "Tasks Test Loss:", [float(t) for t in test_tasks])
+        total_loss["train"][epoch], total_loss["val"][epoch], total_loss["test"][epoch] = \
+            train_loss, val_loss, test_loss
+        task_loss["train"][epoch], task_loss["val"][epoch], task_loss["test"][epoch] = \
+            train_tasks, val_tasks, test_tasks
+        if plot_hist_solution and visualizer is not None:
+            visualizer.create_scatter_plots(tv, pv, output_names=config["Variables_of_interest"]["output_names"],
+                                            iepoch=epoch)
+        if checkpoint is not None:
+            if checkpoint(model, optimizer, float(reduce_values_ranks(val_loss))):
+                print_distributed(verbosity, "Creating Checkpoint: %f" % checkpoint.min_perf_metric)
+            print_distributed(verbosity, "Best Performance Metric: %f" % checkpoint.min_perf_metric)
+        if earlystopper is not None and earlystopper(float(reduce_values_ranks(val_loss))):
+            print_distributed(verbosity,
+                              "Early stopping executed at epoch = %d due to val_loss not decreasing" % epoch)
+            break
+        if check_time and check_remaining(t0):
+            print_distributed(verbosity, "No time left. Early stop.")
+            break
+    timer.stop()
+    if trainer_state is not None:
+        trainer_state["epoch"] = epoch + 1
+        if earlystopper is not None:
+            trainer_state["early_stopping"] = earlystopper.state_dict()
+    if create_plots:
+        for k in total_loss:
+            total_loss[k] = reduce_values_ranks(total_loss[k])
+            task_loss[k] = reduce_values_ranks(task_loss[k])
+        _, _, tv, pv = test(test_loader, model, verbosity)
+        if config["Variables_of_interest"].get("denormalize_output"):
+            from ..postprocess.postprocess import output_denormalize
+
+            tv, pv = output_denormalize(config["Variables_of_interest"]["y_minmax"], tv, pv)
+        if rank == 0 and visualizer is not None:
+            names = config["Variables_of_interest"]["output_names"]
+            visualizer.create_plot_global(tv, pv, output_names=names)
+            visualizer.create_scatter_plots(tv, pv, output_names=names)
+            visualizer.plot_history(total_loss["train"], total_loss["val"], total_loss["test"], task_loss["train"],
+                                    task_loss["val"], task_loss["test"], module.loss_weights, names)

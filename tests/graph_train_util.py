@@ -1,0 +1,68 @@
+"""Shared driver of the end-to-end accuracy tests (reference ``tests/test_graphs.py:26-198``):
+generate the deterministic dataset (rank 0), run_training, run_prediction, check the
+per-head RMSE and sample-MAE thresholds."""
+import os
+import zlib
+
+import torch
+
+import hydragnn_amd
+from hydragnn_amd.data.lsms import deterministic_graph_data
+from hydragnn_amd.parallel.distributed import get_comm_size_and_rank
+from hydragnn_amd.utils.config_utils import merge_config
+
+from ci_configs import ci, thresholds
+
+
+def unittest_train_model(mpnn_type, global_attn_engine, global_attn_type, ci_input, use_lengths, workdir,
+                         overwrite_config=None, num_samples_tot=500):
+    torch.manual_seed(97)
+    _, rank = get_comm_size_and_rank()
+    os.environ["SERIALIZED_DATA_PATH"] = workdir
+    config = ci(ci_input)
+    arch = config["NeuralNetwork"]["Architecture"]
+    arch["global_attn_engine"] = global_attn_engine
+    arch["global_attn_type"] = global_attn_type
+    arch["mpnn_type"] = mpnn_type
+    if overwrite_config:
+        config = merge_config(config, overwrite_config)
+    # reuse serialized files when present
+    for split in list(config["Dataset"]["path"].keys()):
+        name = config["Dataset"]["name"] + ("" if split == "total" else "_" + split) + ".pkl"
+        pkl = os.path.join(workdir, "serialized_dataset", name)
+        if os.path.exists(pkl):
+            config["Dataset"]["path"][split] = pkl
+    if mpnn_type == "MFC" and ci_input == "ci_multihead":
+        arch["task_weights"][0] = 2
+    if use_lengths:
+        arch["edge_features"] = ["lengths"]
+    if rank == 0:
+        pkl_input = list(config["Dataset"]["path"].values())[0].endswith(".pkl")
+        if not pkl_input:
+            for split, path in config["Dataset"]["path"].items():
+                full = os.path.join(workdir, path)
+                config["Dataset"]["path"][split] = full
+                os.makedirs(full, exist_ok=True)
+                perc = config["NeuralNetwork"]["Training"]["perc_train"]
+                n = {"total": num_samples_tot, "train": int(num_samples_tot * perc)}.get(
+                    split, int(num_samples_tot * (1 - perc) * 0.5))
+                if not os.listdir(full):
+                    deterministic_graph_data(full, number_configurations=n, seed=zlib.crc32(f"{split}-{n}".encode()) % 10000)
+    else:
+        for split, path in config["Dataset"]["path"].items():
+            if not path.endswith(".pkl"):
+                config["Dataset"]["path"][split] = os.path.join(workdir, path)
+    cwd = os.getcwd()
+    os.chdir(workdir)
+    try:
+        hydragnn_amd.run_training(config)
+        error, error_task, true_values, pred_values = hydragnn_amd.run_prediction(config)
+    finally:
+        os.chdir(cwd)
+    t = thresholds(mpnn_type, ci_input, use_lengths)
+    for ih in range(len(true_values)):
+        assert float(error_task[ih]) < t[0], f"head {ih} RMSE {float(error_task[ih])} >= {t[0]}"
+        mae = torch.nn.functional.l1_loss(pred_values[ih], true_values[ih])
+        assert float(mae) < t[1], f"head {ih} MAE {float(mae)} >= {t[1]}"
+    assert float(error) < t[0], f"total error {float(error)} >= {t[0]}"
+    return float(error)

@@ -67,10 +67,8 @@ def test_graph_step_matches_eager():
     graph = TrainStep(m2, mode="graph", node_bucket=4096, edge_bucket=1 << 16)
     graph.prepare(s, 16)
     batches = [list(range(i, i + 16)) for i in range(0, 48, 8)]
-    # the capture warm-up trains twice on the first batch: mirror it eagerly
-    eager(s, batches[0])
-    eager(s, batches[0])
-    le = [float(eager(s, b)) for b in batches]
-    lg = [float(graph(s, b)) for b in batches]
+    # capture warm-up iterations are rolled back: both paths see exactly the same steps
+    le = [float(eager(s, b)[0]) for b in batches]
+    lg = [float(graph(s, b)[0]) for b in batches]
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (le, lg)

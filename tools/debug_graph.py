@@ -21,7 +21,7 @@ for it in range(40):
     idx = rng.choice(len(store), 32, replace=False)
     N, E = store.sizes_of(idx)
     torch.cuda.synchronize(); t = time.perf_counter()
-    l = step(store, idx)
+    l, _ = step(store, idx)
     torch.cuda.synchronize(); dt = time.perf_counter() - t
     bad = [n for n, p in model.named_parameters() if not torch.isfinite(p).all()]
     print(it, N, E, step._pick(N, E), "loss", float(l), "ms", round(dt * 1e3, 2), "nonfinite params", bad[:3], flush=True)
