@@ -6,13 +6,17 @@
 // 64x64 gradient becomes 1-4 workgroups walking 20k+ rows (rocprof on MI355X:
 // 30-105 us per call with 1-4 WGs busy on a 256-CU chip).  Here the reduction
 // dimension is split instead:
-//   pass 1: workgroup (tile, slab) owns a 64x64 output tile and a slab of rows;
-//           each of its 4 waves walks an interleaved subset of the slab's rows
-//           with no LDS staging and no barriers (lane = 8x8 register block,
-//           2 float4 loads of dY and of X per row feed 64 FMAs; 2-row unroll for
-//           load/FMA overlap), the 4 wave accumulators are folded through a
-//           padded (conflict-free) LDS image, and one fp32 partial per slab is
-//           written (bias sums ride along as an extra row block);
+//   pass 1: workgroup (tile, slab) owns a 64x64 output tile and a slab of >=128
+//           rows.  The slab streams through LDS in 32-row chunks, double
+//           buffered: all 256 threads issue the float4 loads of chunk c+1 before
+//           computing chunk c, so one HBM/L2 latency covers 32 rows (the first
+//           version, one row pair in flight per wave, was latency-bound at
+//           ~17 us per call).  Each lane owns an 8x8 register block of the
+//           output (2 ds_read_b128 of dY + 2 of X feed 64 FMAs, 8 distinct
+//           addresses per wave instruction -> broadcast, no bank conflicts);
+//           waves take interleaved rows of the chunk, their accumulators are
+//           folded in a fixed order through a padded LDS image, and the
+//           partial tile (+ bias column sums) is written coalesced;
 //   pass 2: the S slab partials are summed in a fixed order, 4 waves per
 //           64-output group (deterministic: no float atomics).
 // fp32 in / fp32 accumulate: FMA-bound at the VALU rate, which on gfx950 equals
@@ -23,14 +27,29 @@ namespace hy {
 
 constexpr int kWT = 64;  // output tile edge
 
-__device__ __forceinline__ void load8(const float* p, int valid, bool vec, float (&v)[8]) {
-  if (vec && valid >= 8) {
-    const float4 a = *reinterpret_cast<const float4*>(p);
-    const float4 b = *reinterpret_cast<const float4*>(p + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  } else {
+constexpr int kWC = 32;  // rows per LDS chunk
+
+// Stage a 32-row x 64-col chunk of one operand: thread t -> rows t/16 and t/16+16, float4 column t%16.
+__device__ __forceinline__ void wg_load(const float* __restrict__ base, int ld, int col0, int ncol, int row0,
+                                        int rend, bool vec, int t, float4 (&r)[2]) {
+  const int c = (t & 15) * 4;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = k < valid ? p[k] : 0.f;
+  for (int h = 0; h < 2; ++h) {
+    const int row = row0 + (t >> 4) + 16 * h;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < rend) {
+      const float* p = base + (int64_t)row * ld + col0 + c;
+      const int valid = ncol - (col0 + c);
+      if (vec && valid >= 4) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        v.x = valid > 0 ? p[0] : 0.f;
+        v.y = valid > 1 ? p[1] : 0.f;
+        v.z = valid > 2 ? p[2] : 0.f;
+        v.w = valid > 3 ? p[3] : 0.f;
+      }
+    }
+    r[h] = v;
   }
 }
 
@@ -39,85 +58,93 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
                                                             const float* __restrict__ X, int ldx,
                                                             float* __restrict__ part, int with_bias, int M, int O,
                                                             int I, int rows_per_block, int tiles_i) {
-  __shared__ float red[64 * 65];
+  // 2 buffers x (dY, X) x 32 rows x 64 floats = 32 KB; reused for the wave fold afterwards
+  __shared__ float4 smem[2 * 2 * kWC * 16];
+  float4* Ys = smem;                  // [2][kWC][16]
+  float4* Xs = smem + 2 * kWC * 16;   // [2][kWC][16]
   const int tile = blockIdx.x;
   const int to0 = (tile / tiles_i) * kWT, ti0 = (tile % tiles_i) * kWT;
   const int s = blockIdx.y;
   const int r0 = s * rows_per_block, r1 = min(M, r0 + rows_per_block);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ob = (lane >> 3) * 8, ib = (lane & 7) * 8;
-  const int ov = max(0, min(8, O - (to0 + ob))), iv = max(0, min(8, I - (ti0 + ib)));
-  const bool vy = ((ldy & 3) == 0) && (((to0 + ob) & 3) == 0);
-  const bool vx = ((ldx & 3) == 0) && (((ti0 + ib) & 3) == 0);
-  const bool bias_lane = with_bias && ti0 == 0 && ib == 0;
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int obq = (lane >> 3) * 2, ibq = (lane & 7) * 2;  // float4 column index of this lane's 8-block
+  const bool vy = (ldy & 3) == 0 && (to0 & 3) == 0;
+  const bool vx = (ldx & 3) == 0 && (ti0 & 3) == 0;
+  const bool bias_lane = with_bias && ti0 == 0 && (lane & 7) == 0;
   float acc[8][8];
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
     for (int b = 0; b < 8; ++b) acc[a][b] = 0.f;
   float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* yb = dY + to0 + ob;
-  const float* xb = X + ti0 + ib;
-  int r = r0 + w;
-  for (; r + 4 < r1; r += 8) {
-    float ya[8], xa[8], yc[8], xc[8];
-    load8(yb + (int64_t)r * ldy, ov, vy, ya);
-    load8(xb + (int64_t)r * ldx, iv, vx, xa);
-    load8(yb + (int64_t)(r + 4) * ldy, ov, vy, yc);
-    load8(xb + (int64_t)(r + 4) * ldx, iv, vx, xc);
+  const int nch = (r1 - r0 + kWC - 1) / kWC;
+  float4 ry[2], rx[2];
+  if (nch > 0) {
+    wg_load(dY, ldy, to0, O, r0, r1, vy, t, ry);
+    wg_load(X, ldx, ti0, I, r0, r1, vx, t, rx);
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = fmaf(ya[a], xa[b], acc[a][b]);
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = fmaf(yc[a], xc[b], acc[a][b]);
-    if (bias_lane) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a) bacc[a] += ya[a] + yc[a];
+    for (int h = 0; h < 2; ++h) {
+      Ys[((t >> 4) + 16 * h) * 16 + (t & 15)] = ry[h];
+      Xs[((t >> 4) + 16 * h) * 16 + (t & 15)] = rx[h];
     }
   }
-  for (; r < r1; r += 4) {
-    float ya[8], xa[8];
-    load8(yb + (int64_t)r * ldy, ov, vy, ya);
-    load8(xb + (int64_t)r * ldx, iv, vx, xa);
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = fmaf(ya[a], xa[b], acc[a][b]);
-    if (bias_lane) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a) bacc[a] += ya[a];
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int b = c & 1;
+    const bool more = c + 1 < nch;
+    if (more) {  // issue the next chunk's global loads before computing this one
+      wg_load(dY, ldy, to0, O, r0 + (c + 1) * kWC, r1, vy, t, ry);
+      wg_load(X, ldx, ti0, I, r0 + (c + 1) * kWC, r1, vx, t, rx);
     }
+    const float4* yb = Ys + b * kWC * 16;
+    const float4* xb = Xs + b * kWC * 16;
+#pragma unroll 2
+    for (int rr = w; rr < kWC; rr += 4) {
+      const float4 y0 = yb[rr * 16 + obq], y1 = yb[rr * 16 + obq + 1];
+      const float4 x0 = xb[rr * 16 + ibq], x1 = xb[rr * 16 + ibq + 1];
+      const float ya[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+      const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[a][q] = fmaf(ya[a], xa[q], acc[a][q]);
+      if (bias_lane) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) bacc[a] += ya[a];
+      }
+    }
+    if (more) {
+      float4* yn = Ys + (b ^ 1) * kWC * 16;
+      float4* xn = Xs + (b ^ 1) * kWC * 16;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        yn[((t >> 4) + 16 * h) * 16 + (t & 15)] = ry[h];
+        xn[((t >> 4) + 16 * h) * 16 + (t & 15)] = rx[h];
+      }
+    }
+    __syncthreads();
   }
-  // fold the 4 wave accumulators (fixed order) through LDS, [lane][65] padding
+  // fold the 4 wave accumulators in a fixed order through LDS ([lane][65] padding)
+  float* red = reinterpret_cast<float*>(smem);
   for (int step = 0; step < 4; ++step) {
     if (w == step) {
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const float v = acc[a][b] + (step > 0 ? red[lane * 65 + a * 8 + b] : 0.f);
-          red[lane * 65 + a * 8 + b] = v;
-          acc[a][b] = v;
+        for (int q = 0; q < 8; ++q) {
+          const float v = acc[a][q] + (step > 0 ? red[lane * 65 + a * 8 + q] : 0.f);
+          red[lane * 65 + a * 8 + q] = v;
         }
     }
     __syncthreads();
   }
-  // bias: the 8 lanes with ib == 0 in every wave hold partial column sums
+  // coalesced write of the 64x64 partial tile
   float* P = part + (int64_t)s * ((int64_t)O * I + O);
-  if (w == 3) {
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      const int o = to0 + ob + a;
-      if (o >= O) break;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int i = ti0 + ib + b;
-        if (i < I) P[(int64_t)o * I + i] = acc[a][b];
-      }
-    }
+  for (int idx = t; idx < kWT * kWT; idx += 256) {
+    const int oo = idx >> 6, ii = idx & 63;
+    const int o = to0 + oo, i = ti0 + ii;
+    if (o < O && i < I) P[(int64_t)o * I + i] = red[((oo >> 3) * 8 + (ii >> 3)) * 65 + (oo & 7) * 8 + (ii & 7)];
   }
   if (with_bias && ti0 == 0) {
     __syncthreads();
@@ -126,19 +153,12 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
       for (int a = 0; a < 8; ++a) red[(w * 8 + (lane >> 3)) * 8 + a] = bacc[a];
     }
     __syncthreads();
-    if (w == 0 && lane < 8) {
-      // lane k sums the 4 waves' values for o block k (fixed order)
-      float t[8];
-#pragma unroll
-      for (int a = 0; a < 8; ++a) t[a] = 0.f;
-      for (int ww = 0; ww < 4; ++ww)
-#pragma unroll
-        for (int a = 0; a < 8; ++a) t[a] += red[(ww * 8 + lane) * 8 + a];
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const int o = to0 + lane * 8 + a;
-        if (o < O) P[(int64_t)O * I + o] = t[a];
-      }
+    if (t < 64) {
+      const int kb = t >> 3, a = t & 7;  // o = kb*8 + a
+      const float v = red[(0 * 8 + kb) * 8 + a] + red[(1 * 8 + kb) * 8 + a] + red[(2 * 8 + kb) * 8 + a] +
+                      red[(3 * 8 + kb) * 8 + a];
+      const int o = to0 + t;
+      if (o < O) P[(int64_t)O * I + o] = v;
     }
   }
 }
@@ -149,16 +169,16 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j = (int64_t)blockIdx.x * 64 + lane;
-  float a0 = 0.f, a1 = 0.f;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (j < n) {
     int s = w;
-    for (; s + 4 < S; s += 8) {
-      a0 += part[(int64_t)s * ld + j];
-      a1 += part[(int64_t)(s + 4) * ld + j];
+    for (; s + 28 < S; s += 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += part[(int64_t)(s + 4 * k) * ld + j];
     }
-    for (; s < S; s += 4) a0 += part[(int64_t)s * ld + j];
+    for (int k = 0; s < S; s += 4, ++k) a[k & 7] += part[(int64_t)s * ld + j];
   }
-  red[w][lane] = a0 + a1;
+  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (w == 0 && j < n) out[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
@@ -182,8 +202,8 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
   }
   const int tiles_o = ceil_div(O, kWT), tiles_i = ceil_div(I, kWT);
   const int tiles = tiles_o * tiles_i;
-  // ~2 x 256 workgroups; >= 64 rows per slab (16 rows per wave)
-  int S = (int)std::min<int64_t>(ceil_div(M, 64), std::max(1, 512 / tiles));
+  // >= 128 rows (4 LDS chunks) per slab, ~256 workgroups in total
+  int S = (int)std::min<int64_t>(ceil_div(M, 128), std::max(1, 256 / tiles));
   S = std::max(S, 1);
   const int rpb = (int)((M + S - 1) / S);
   S = ceil_div(M, rpb);

@@ -20,6 +20,7 @@ def create_model_config(config, verbosity=0, use_gpu=True):
         a.get("equivariance", False), a.get("correlation"), a.get("max_ell"), a.get("node_max_ell"),
         a.get("avg_num_neighbors"), t.get("conv_checkpointing", False), verbosity, use_gpu,
         attn_scope=a.get("global_attn_scope", "batch"), dropout=a.get("dropout", 0.25),
+        init_seed=a.get("init_seed", 0),
     )
 
 
@@ -31,10 +32,10 @@ def create_model(mpnn_type, input_dim, hidden_dim, output_dim, pe_dim, global_at
                  out_emb_size=None, envelope_exponent=None, num_spherical=None, num_gaussians=None, num_filters=None,
                  radius=None, equivariance=False, correlation=None, max_ell=None, node_max_ell=None,
                  avg_num_neighbors=None, conv_checkpointing=False, verbosity=0, use_gpu=True, attn_scope="batch",
-                 dropout=0.25):
+                 dropout=0.25, init_seed=0):
     timer = Timer("create_model")
     timer.start()
-    torch.manual_seed(0)
+    torch.manual_seed(init_seed)  # reference seeds 0; "init_seed" is an extension key
     device = get_device(use_gpu, verbosity_level=verbosity)
     common = dict(input_dim=input_dim, hidden_dim=hidden_dim, output_dim=output_dim, pe_dim=pe_dim,
                   global_attn_engine=global_attn_engine, global_attn_type=global_attn_type,

@@ -18,6 +18,7 @@ CPU_CASES = [
     ("PNAPlus", "", "", "ci", False),
     ("PNAPlus", "GPS", "multihead", "ci", False),
     ("PNA", "", "", "ci_multihead", False),
+    ("PNA", "", "", "ci", True),
 ]
 
 
