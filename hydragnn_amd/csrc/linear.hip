@@ -163,24 +163,31 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
   }
 }
 
-// out[j] = sum_s part[s * ld + j]; block = 64 outputs x 4 waves splitting s; fixed order
-__global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                           int S, int64_t n, int64_t ld) {
-  __shared__ float red[4][64];
+// out[j] = sum_s part[s * ld + j]; block = 64 outputs x 16 waves splitting s; fixed order
+constexpr int kSpWaves = 16;
+__global__ void __launch_bounds__(64 * kSpWaves) sum_partials_kernel(const float* __restrict__ part,
+                                                                     float* __restrict__ out, int S, int64_t n,
+                                                                     int64_t ld) {
+  __shared__ float red[kSpWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j = (int64_t)blockIdx.x * 64 + lane;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (j < n) {
-    int s = w;
-    for (; s + 28 < S; s += 32) {
+    int s = w, k = 0;
+    for (; s + 3 * kSpWaves < S; s += 4 * kSpWaves) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] += part[(int64_t)(s + 4 * k) * ld + j];
+      for (int q = 0; q < 4; ++q) a[q] += part[(int64_t)(s + q * kSpWaves) * ld + j];
     }
-    for (int k = 0; s < S; s += 4, ++k) a[k & 7] += part[(int64_t)s * ld + j];
+    for (; s < S; s += kSpWaves, ++k) a[k & 3] += part[(int64_t)s * ld + j];
   }
-  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
-  if (w == 0 && j < n) out[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && j < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < kSpWaves; ++q) t += red[q][lane];
+    out[j] = t;
+  }
 }
 
 std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at::Tensor& X_, bool with_bias) {
@@ -202,10 +209,14 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
   }
   const int tiles_o = ceil_div(O, kWT), tiles_i = ceil_div(I, kWT);
   const int tiles = tiles_o * tiles_i;
-  // >= 128 rows (4 LDS chunks) per slab, ~256 workgroups in total
-  int S = (int)std::min<int64_t>(ceil_div(M, 128), std::max(1, 256 / tiles));
+  // One workgroup's 64x64 tile costs 64 FMAs per lane per row, so a slab must stay
+  // short for the grid to fill 256 CUs: >= 32 rows (one LDS chunk) per slab and up to
+  // ~512 workgroups (measured: 128-row slabs -> 22 WGs for a 2816-row node GEMM,
+  // 16 us; the partial-sum pass is cheap next to that).
+  int S = (int)std::min<int64_t>(ceil_div(M, kWC), std::max(1, 512 / tiles));
   S = std::max(S, 1);
-  const int rpb = (int)((M + S - 1) / S);
+  int rpb = (int)((M + S - 1) / S);
+  rpb = ceil_div(rpb, kWC) * kWC;
   S = ceil_div(M, rpb);
   const int64_t ld = (int64_t)O * I + O;
   auto part = at::empty({S, ld}, dY.options());
@@ -214,7 +225,7 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
                                                    (int)X.stride(0), part.data_ptr<float>(), with_bias ? 1 : 0,
                                                    (int)M, O, I, rpb, tiles_i);
   // dW block [0, O*I) and bias block [O*I, O*I+O) are contiguous in both part and out
-  sum_partials_kernel<<<ceil_div(n, 64), 256, 0, stream()>>>(part.data_ptr<float>(), out.data_ptr<float>(), S, n, ld);
+  sum_partials_kernel<<<ceil_div(n, 64), 64 * kSpWaves, 0, stream()>>>(part.data_ptr<float>(), out.data_ptr<float>(), S, n, ld);
   return {dW, db};
 }
 

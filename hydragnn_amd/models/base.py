@@ -23,7 +23,9 @@ from torch.nn import ModuleDict, ModuleList, Sequential
 from torch.utils.checkpoint import checkpoint
 
 from ..ops import segment as seg
+from ..ops import rng as _rng
 from ..ops.attention import make_segments
+from ..ops.norm import norm_add
 from ..utils import tracer as tr
 from ..utils.model import activation_function_selection, loss_function_selection
 from ..utils.print_utils import print_master
@@ -276,7 +278,12 @@ class Base(nn.Module):
             inv = inv * nmask
         for conv, bn in zip(self.graph_convs, self.feature_layers):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
-            inv = self.activation_function(bn(inv, ctx.get("num_valid")))
+            if isinstance(self.activation_function, torch.nn.ReLU) and isinstance(bn, BatchNorm):
+                # BN -> ReLU -> padding mask in one fused launch (ops.norm.norm_add)
+                inv = norm_add(inv, bn, ctx.get("num_valid"), relu=True, zero_pad=nmask is not None)
+                continue
+            h = bn(inv, ctx.get("num_valid")) if isinstance(bn, BatchNorm) else bn(inv)
+            inv = self.activation_function(h)
             if nmask is not None:
                 inv = inv * nmask
         return inv, equiv, ctx
@@ -350,7 +357,14 @@ class Base(nn.Module):
             return inv
         return headloc(x=x, batch=batch)
 
+    def _dev_type(self):
+        for p in self.parameters():
+            return p.device.type
+        return "cpu"
+
     def forward(self, data):
+        if self.training and self._dev_type() == "cuda":
+            _rng.advance(next(self.parameters()).device)  # fresh dropout masks per step (graph-safe)
         tr.start("enc_forward")
         x, equiv, ctx = self.encode(data)
         tr.stop("enc_forward")

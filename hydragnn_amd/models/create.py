@@ -69,7 +69,7 @@ def create_model(mpnn_type, input_dim, hidden_dim, output_dim, pe_dim, global_at
     elif mpnn_type == "SchNet":
         assert num_gaussians is not None and num_filters is not None and radius is not None, \
             "SchNet requires num_gaussians, num_filters and radius."
-        model = stacks.SCFStack("", "", num_gaussians, num_filters, radius, edge_dim=edge_dim,
+        model = stacks.SCFStack("", "", num_filters, edge_dim, num_gaussians, radius,
                                 max_neighbours=max_neighbours, **common)
     elif mpnn_type == "DimeNet":
         for k, v in dict(basis_emb_size=basis_emb_size, envelope_exponent=envelope_exponent,
@@ -79,7 +79,7 @@ def create_model(mpnn_type, input_dim, hidden_dim, output_dim, pe_dim, global_at
             assert v is not None, f"DimeNet requires {k} input."
         model = stacks.DIMEStack("", "", basis_emb_size, envelope_exponent, int_emb_size, out_emb_size,
                                  num_after_skip, num_before_skip, num_radial, num_spherical, edge_dim, radius,
-                                 max_neighbours, **common)
+                                 max_neighbours=max_neighbours, **common)
     elif mpnn_type == "EGNN":
         model = stacks.EGCLStack("", "", edge_dim, **common)
     elif mpnn_type == "PAINN":

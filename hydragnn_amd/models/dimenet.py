@@ -1,0 +1,292 @@
+"""DimeNet++ stack (reference ``hydragnn/models/DIMEStack.py:34-305``; PyG
+``InteractionPPBlock`` / ``OutputPPBlock`` / ``SphericalBasisLayer`` semantics).
+
+Per layer:  x <- lin(x);  m_ji = act(lin(cat[x_i, x_j, act(lin_rbf rbf_ji)(, act(edge_lin e))]))
+            (HydraEmbeddingBlock, i = destination, j = source)
+            m_ji <- InteractionPP(m, rbf, sbf, triplets)
+            x_i  <- OutputPP: lin(act(lins(lin_up(sum_{j} lin_rbf(rbf_ji) * m_ji))))
+
+Triplets (k -> j -> i, k != i) come straight from the destination CSR: the
+in-edges of j are one contiguous segment, so for edge e_ji the candidates k->j
+are ``rowptr[j]..rowptr[j+1]`` — no sparse-tensor indexing.  Triplets are emitted
+grouped by e_ji, so the k->j => j->i message reduction is a sorted (atomic-free)
+segment sum.  The spherical basis uses spherical Bessel functions j_l(z_ln r)
+(zeros from scipy, evaluated in float64 by upward recurrence) times zonal
+harmonics Y_l^0(angle) = sqrt((2l+1)/4pi) P_l(cos angle), enveloped as in PyG.
+"""
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from ..ops import segment as seg
+from ..ops.geometry import BesselBasis, Envelope, edge_vectors_and_lengths
+from .base import Base
+
+
+# ----------------------------------------------------------------------------- bases
+def _sph_jn_np(l, x):
+    from scipy.special import spherical_jn
+
+    return spherical_jn(l, x)
+
+
+def bessel_zeros(n, k):
+    """First k positive zeros of j_l for l < n (n x k array)."""
+    from scipy.optimize import brentq
+
+    zeros = np.zeros((n, k))
+    zeros[0] = np.arange(1, k + 1) * np.pi
+    pts = np.arange(1, k + n) * np.pi
+    racines = np.zeros(k + n - 1)
+    for l in range(1, n):
+        for j in range(k + n - 1 - l):
+            racines[j] = brentq(lambda x: _sph_jn_np(l, x), pts[j], pts[j + 1])
+        pts = racines.copy()
+        zeros[l][:k] = racines[:k]
+    return zeros
+
+
+def _sph_jn_torch(lmax, x):
+    """[j_0(x) .. j_lmax(x)] by upward recurrence (float64 for stability)."""
+    x = x.to(torch.float64)
+    s, c = torch.sin(x), torch.cos(x)
+    out = [s / x]
+    if lmax >= 1:
+        out.append(s / (x * x) - c / x)
+    for l in range(1, lmax):
+        out.append((2 * l + 1) / x * out[l] - out[l - 1])
+    return out
+
+
+def _legendre(lmax, t):
+    p = [torch.ones_like(t)]
+    if lmax >= 1:
+        p.append(t)
+    for l in range(1, lmax):
+        p.append(((2 * l + 1) * t * p[l] - l * p[l - 1]) / (l + 1))
+    return p
+
+
+class SphericalBasisLayer(nn.Module):
+    def __init__(self, num_spherical, num_radial, cutoff=5.0, envelope_exponent=5):
+        super().__init__()
+        assert num_radial <= 64
+        self.num_spherical, self.num_radial = num_spherical, num_radial
+        self.cutoff = float(cutoff)
+        self.envelope = Envelope(envelope_exponent)
+        z = bessel_zeros(num_spherical, num_radial)
+        norm = np.zeros_like(z)
+        for l in range(num_spherical):
+            norm[l] = 1.0 / np.sqrt(0.5 * _sph_jn_np(l + 1, z[l]) ** 2)
+        self.register_buffer("zeros", torch.tensor(z, dtype=torch.float64), persistent=False)
+        self.register_buffer("norm", torch.tensor(norm, dtype=torch.float64), persistent=False)
+
+    def forward(self, dist, angle, idx_kj):
+        n, k = self.num_spherical, self.num_radial
+        d = (dist / self.cutoff).to(torch.float64)
+        rbf = []
+        for l in range(n):
+            x = d.view(-1, 1) * self.zeros[l].view(1, -1)  # [E, k]
+            rbf.append(self.norm[l].view(1, -1) * _sph_jn_torch(l, x)[l])
+        rbf = torch.stack(rbf, 1).to(dist.dtype)  # [E, n, k]
+        rbf = self.envelope(dist / self.cutoff).view(-1, 1, 1) * rbf
+        t = torch.cos(angle.to(torch.float64))
+        P = _legendre(n - 1, t)
+        cbf = torch.stack([math.sqrt((2 * l + 1) / (4 * math.pi)) * P[l] for l in range(n)], 1).to(dist.dtype)
+        return (seg.gather(rbf.reshape(-1, n * k), idx_kj).view(-1, n, k) * cbf.view(-1, n, 1)).reshape(-1, n * k)
+
+
+# ----------------------------------------------------------------------------- triplets
+def triplets_csr(dst_si, src_si, num_nodes):
+    """(idx_kj, idx_ji) for all k->j->i with k != i, grouped by e_ji (ascending)."""
+    dev = dst_si.rowptr.device
+    src = src_si.index.long()
+    dst = dst_si.index.long()
+    rowptr = dst_si.rowptr.long()
+    E = src.numel()
+    deg_j = rowptr[src + 1] - rowptr[src]  # in-degree of j for every edge j->i
+    e_ji = torch.repeat_interleave(torch.arange(E, device=dev), deg_j)
+    start = torch.repeat_interleave(rowptr[src], deg_j)
+    off = torch.arange(e_ji.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(deg_j, 0) - deg_j, deg_j)
+    e_kj = start + off
+    keep = src[e_kj] != dst[e_ji]  # k != i
+    return e_kj[keep], e_ji[keep]
+
+
+# ----------------------------------------------------------------------------- blocks
+def _glorot_orthogonal(w, scale=2.0):
+    nn.init.orthogonal_(w)
+    s = scale / ((w.size(0) + w.size(1)) * w.var())
+    w.data *= s.sqrt()
+
+
+class ResidualLayer(nn.Module):
+    def __init__(self, hidden, act):
+        super().__init__()
+        self.act = act
+        self.lin1 = nn.Linear(hidden, hidden)
+        self.lin2 = nn.Linear(hidden, hidden)
+        for l in (self.lin1, self.lin2):
+            _glorot_orthogonal(l.weight)
+            l.bias.data.fill_(0)
+
+    def forward(self, x):
+        return x + self.act(self.lin2(self.act(self.lin1(x))))
+
+
+class HydraEmbeddingBlock(nn.Module):
+    def __init__(self, num_radial, hidden_channels, act, edge_dim=None):
+        super().__init__()
+        self.act = act
+        self.lin_rbf = nn.Linear(num_radial, hidden_channels)
+        if edge_dim is not None:
+            self.edge_lin = nn.Linear(edge_dim, hidden_channels)
+            self.lin = nn.Linear(4 * hidden_channels, hidden_channels)
+        else:
+            self.lin = nn.Linear(3 * hidden_channels, hidden_channels)
+
+    def forward(self, x, rbf, dst_si, src_si, edge_attr=None):
+        H = x.shape[1]
+        W = self.lin.weight
+        nb = torch.nn.functional.linear(x, torch.cat([W[:, :H], W[:, H:2 * H]], 0))  # [x_i | x_j] blocks
+        h = seg.gather(nb[:, :W.shape[0]], dst_si) + seg.gather(nb[:, W.shape[0]:], src_si) + self.lin.bias
+        h = h + torch.nn.functional.linear(self.act(self.lin_rbf(rbf)), W[:, 2 * H:3 * H])
+        if edge_attr is not None and hasattr(self, "edge_lin"):
+            h = h + torch.nn.functional.linear(self.act(self.edge_lin(edge_attr)), W[:, 3 * H:])
+        return self.act(h)
+
+
+class InteractionPPBlock(nn.Module):
+    def __init__(self, hidden_channels, int_emb_size, basis_emb_size, num_spherical, num_radial, num_before_skip,
+                 num_after_skip, act):
+        super().__init__()
+        self.act = act
+        self.lin_rbf1 = nn.Linear(num_radial, basis_emb_size, bias=False)
+        self.lin_rbf2 = nn.Linear(basis_emb_size, hidden_channels, bias=False)
+        self.lin_sbf1 = nn.Linear(num_spherical * num_radial, basis_emb_size, bias=False)
+        self.lin_sbf2 = nn.Linear(basis_emb_size, int_emb_size, bias=False)
+        self.lin_kj = nn.Linear(hidden_channels, hidden_channels)
+        self.lin_ji = nn.Linear(hidden_channels, hidden_channels)
+        self.lin_down = nn.Linear(hidden_channels, int_emb_size, bias=False)
+        self.lin_up = nn.Linear(int_emb_size, hidden_channels, bias=False)
+        self.layers_before_skip = nn.ModuleList([ResidualLayer(hidden_channels, act) for _ in range(num_before_skip)])
+        self.lin = nn.Linear(hidden_channels, hidden_channels)
+        self.layers_after_skip = nn.ModuleList([ResidualLayer(hidden_channels, act) for _ in range(num_after_skip)])
+        for l in (self.lin_rbf1, self.lin_rbf2, self.lin_sbf1, self.lin_sbf2, self.lin_kj, self.lin_ji,
+                  self.lin_down, self.lin_up, self.lin):
+            _glorot_orthogonal(l.weight)
+            if l.bias is not None:
+                l.bias.data.fill_(0)
+
+    def forward(self, x, rbf, sbf, kj_si, ji_si):
+        x_ji = self.act(self.lin_ji(x))
+        x_kj = self.act(self.lin_kj(x)) * self.lin_rbf2(self.lin_rbf1(rbf))
+        x_kj = self.act(self.lin_down(x_kj))
+        sbf = self.lin_sbf2(self.lin_sbf1(sbf))
+        x_kj = seg.segment_sum(seg.gather(x_kj, kj_si) * sbf, ji_si)
+        h = x_ji + self.act(self.lin_up(x_kj))
+        for layer in self.layers_before_skip:
+            h = layer(h)
+        h = self.act(self.lin(h)) + x
+        for layer in self.layers_after_skip:
+            h = layer(h)
+        return h
+
+
+class OutputPPBlock(nn.Module):
+    def __init__(self, num_radial, hidden_channels, out_emb_channels, out_channels, num_layers, act):
+        super().__init__()
+        self.act = act
+        self.lin_rbf = nn.Linear(num_radial, hidden_channels, bias=False)
+        self.lin_up = nn.Linear(hidden_channels, out_emb_channels, bias=False)
+        self.lins = nn.ModuleList([nn.Linear(out_emb_channels, out_emb_channels) for _ in range(num_layers)])
+        self.lin = nn.Linear(out_emb_channels, out_channels, bias=False)
+        _glorot_orthogonal(self.lin_rbf.weight)
+        _glorot_orthogonal(self.lin_up.weight)
+        for l in self.lins:
+            _glorot_orthogonal(l.weight)
+            l.bias.data.fill_(0)
+        _glorot_orthogonal(self.lin.weight)
+
+    def forward(self, m, rbf, dst_si):
+        x = seg.segment_sum(self.lin_rbf(rbf) * m, dst_si)
+        x = self.lin_up(x)
+        for l in self.lins:
+            x = self.act(l(x))
+        return self.lin(x)
+
+
+class DimeNetLayer(nn.Module):
+    def __init__(self, lin, emb, inter, dec):
+        super().__init__()
+        self.lin, self.emb, self.inter, self.dec = lin, emb, inter, dec
+
+    def forward(self, inv, equiv, ctx):
+        x = self.lin(inv)
+        m = self.emb(x, ctx.rbf, ctx.dst_si, ctx.src_si, ctx.edge_attr)
+        m = self.inter(m, ctx.rbf, ctx.sbf, ctx.kj_si, ctx.ji_si)
+        return self.dec(m, ctx.rbf, ctx.dst_si), equiv
+
+
+class DIMEStack(Base):
+    is_edge_model = True
+
+    def __init__(self, input_args, conv_args, basis_emb_size, envelope_exponent, int_emb_size, out_emb_size,
+                 num_after_skip, num_before_skip, num_radial, num_spherical, edge_dim, radius, *args,
+                 max_neighbours=None, **kwargs):
+        self.basis_emb_size = basis_emb_size
+        self.int_emb_size = int_emb_size
+        self.out_emb_size = out_emb_size
+        self.num_radial = num_radial
+        self.num_spherical = num_spherical
+        self.num_before_skip = num_before_skip
+        self.num_after_skip = num_after_skip
+        self.edge_dim = edge_dim
+        self.radius = radius
+        super().__init__(input_args, conv_args, *args, **kwargs)
+        self.rbf = BesselBasis(num_radial, radius, envelope_exponent)
+        self.sbf = SphericalBasisLayer(num_spherical, num_radial, radius, envelope_exponent)
+
+    def _init_conv(self):
+        self.graph_convs.append(self._apply_global_attn(
+            self.get_conv(self.embed_dim, self.hidden_dim, edge_dim=self.edge_embed_dim)))
+        self.feature_layers.append(nn.Identity())
+        for _ in range(self.num_conv_layers - 1):
+            self.graph_convs.append(self._apply_global_attn(
+                self.get_conv(self.hidden_dim, self.hidden_dim, edge_dim=self.edge_embed_dim)))
+            self.feature_layers.append(nn.Identity())
+
+    def get_conv(self, input_dim, output_dim, edge_dim=None):
+        hidden = output_dim if input_dim == 1 else input_dim
+        assert hidden > 1, "DimeNet requires more than one hidden dimension between input_dim and output_dim."
+        act = nn.SiLU()
+        lin = nn.Linear(input_dim, hidden)
+        emb = HydraEmbeddingBlock(self.num_radial, hidden, act, edge_dim=edge_dim)
+        inter = InteractionPPBlock(hidden, self.int_emb_size, self.basis_emb_size, self.num_spherical,
+                                   self.num_radial, self.num_before_skip, self.num_after_skip, act)
+        dec = OutputPPBlock(self.num_radial, hidden, self.out_emb_size, output_dim, 1, act)
+        return DimeNetLayer(lin, emb, inter, dec)
+
+    def _embedding(self, data):
+        x, pos, ctx = super()._embedding(data)
+        assert data.pos is not None, "DimeNet requires node positions (data.pos) to be set."
+        N = data.num_nodes
+        idx_kj, idx_ji = triplets_csr(ctx.dst_si, ctx.src_si, N)
+        E = ctx.dst_si.index.numel()
+        ctx.kj_si = seg.SegIndex.from_index(idx_kj, E, sorted_=False)
+        ctx.ji_si = seg.SegIndex.from_index(idx_ji, E, sorted_=True)
+        vec, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
+        pos_ji = seg.gather(vec, ctx.ji_si)
+        pos_ki = seg.gather(vec, ctx.kj_si) + pos_ji
+        a = (pos_ji * pos_ki).sum(-1)
+        b = torch.linalg.cross(pos_ji, pos_ki).norm(dim=-1)
+        angle = torch.atan2(b, a)
+        d = dist.view(-1)
+        ctx.rbf = self.rbf(d)
+        ctx.sbf = self.sbf(d, angle, ctx.kj_si)
+        return x, pos, ctx
+
+    def __str__(self):
+        return "DIMEStack"

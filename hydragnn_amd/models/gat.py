@@ -1,0 +1,180 @@
+"""GAT stack (reference ``hydragnn/models/GATStack.py:21-208`` over PyG ``GATv2Conv``,
+heads=6, negative_slope=0.05, add_self_loops=True).
+
+GATv2 per head h (C channels each), i = destination, j = source:
+
+    g_ij   = x_l[j] + x_r[i] (+ W_e e_ij)        x_l = lin_l(x), x_r = lin_r(x)
+    s_ij   = att_h . leaky_relu(g_ij)
+    a_ij   = softmax_{j in N(i) ∪ {i}}(s_ij), dropout(p)
+    out_i  = sum_j a_ij x_l[j]     -> concat heads (or mean) + bias
+
+Self loops are NOT materialised as extra edges (that would rebuild the CSR every
+batch): the self term is evaluated per node and folded into the segment softmax
+(max / exp-sum / weighted sum over the incoming CSR segment plus one node-local
+element).  With edge features the self-loop attribute is the mean of the node's
+incoming edge attributes (PyG ``fill_value="mean"``).  Input graphs are assumed
+loop-free (radius graphs are built with loop=False), so PyG's
+remove-then-add-self-loops is the identity on the existing edges.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops import rng as _rng
+from ..ops import segment as seg
+from ..ops.linear import linear
+from .base import Base
+from .layers import BatchNorm
+
+
+class GATv2Conv(nn.Module):
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2, dropout=0.0,
+                 add_self_loops=True, edge_dim=None, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.concat = concat
+        self.negative_slope = negative_slope
+        self.dropout = dropout
+        self.add_self_loops = add_self_loops
+        self.edge_dim = edge_dim
+        H, C = heads, out_channels
+        self.lin_l = nn.Linear(in_channels, H * C, bias=bias)
+        self.lin_r = nn.Linear(in_channels, H * C, bias=bias)
+        self.att = nn.Parameter(torch.empty(1, H, C))
+        self.lin_edge = nn.Linear(edge_dim, H * C, bias=False) if edge_dim is not None else None
+        self.bias = nn.Parameter(torch.empty(H * C if concat else C)) if bias else None
+        self._salt = _rng.new_salt()
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.lin_l.weight)
+        nn.init.xavier_uniform_(self.lin_r.weight)
+        if self.lin_l.bias is not None:
+            nn.init.zeros_(self.lin_l.bias)
+            nn.init.zeros_(self.lin_r.bias)
+        if self.lin_edge is not None:
+            nn.init.xavier_uniform_(self.lin_edge.weight)
+        nn.init.xavier_uniform_(self.att)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def forward(self, inv, equiv, ctx):
+        x = inv
+        N = x.shape[0]
+        H, C = self.heads, self.out_channels
+        W = torch.cat([self.lin_l.weight, self.lin_r.weight], 0)
+        b = torch.cat([self.lin_l.bias, self.lin_r.bias]) if self.lin_l.bias is not None else None
+        lr = linear(x, W, b)  # one node GEMM for both projections
+        xl, xr = lr[:, :H * C], lr[:, H * C:]
+        dst_si, src_si = ctx.dst_si, ctx.src_si
+        xl_j = seg.gather(xl, src_si)
+        g = xl_j + seg.gather(xr, dst_si)
+        e = ctx.edge_attr if self.lin_edge is not None else None
+        if e is not None:
+            g = g + linear(e, self.lin_edge.weight)
+        s = (F.leaky_relu(g, self.negative_slope).view(-1, H, C) * self.att).sum(-1)  # [E, H]
+        if self.add_self_loops:
+            gs = xl + xr
+            if e is not None:
+                gs = gs + linear(seg.segment_mean(e, dst_si), self.lin_edge.weight)
+            ss = (F.leaky_relu(gs, self.negative_slope).view(-1, H, C) * self.att).sum(-1)  # [N, H]
+            mx = torch.maximum(seg.segment_max(s.detach(), dst_si), ss.detach())
+        else:
+            ss = None
+            mx = seg.segment_max(s.detach(), dst_si)
+        es = torch.exp(s - seg.gather(mx, dst_si))
+        den = seg.segment_sum(es, dst_si)
+        if ss is not None:
+            ess = torch.exp(ss - mx)
+            den = den + ess
+        inv_den = 1.0 / (den + 1e-16)
+        a = es * seg.gather(inv_den, dst_si)
+        a = _rng.dropout(a, self.dropout, self.training, self._salt)
+        out = seg.segment_sum((xl_j.view(-1, H, C) * a.unsqueeze(-1)).view(-1, H * C), dst_si)
+        if ss is not None:
+            asf = ess * inv_den
+            if self.training and self.dropout > 0:
+                asf = _rng.dropout(asf, self.dropout, True, self._salt + 1000003)
+            out = out + (xl.view(-1, H, C) * asf.unsqueeze(-1)).view(-1, H * C)
+        out = out.view(N, H, C)
+        out = out.reshape(N, H * C) if self.concat else out.mean(1)
+        if self.bias is not None:
+            out = out + self.bias
+        return out, equiv
+
+    def __repr__(self):
+        return f"GATv2Conv({self.in_channels}, {self.out_channels}, heads={self.heads})"
+
+
+class _GATBlock(nn.Module):
+    """GATv2 followed by the optional GPS output projection (reference ``out_lin``)."""
+
+    def __init__(self, gat, out_lin):
+        super().__init__()
+        self.gat = gat
+        self.out_lin = out_lin
+
+    def forward(self, inv, equiv, ctx):
+        h, equiv = self.gat(inv, equiv, ctx)
+        return self.out_lin(h), equiv
+
+
+class GATStack(Base):
+    is_edge_model = True
+
+    def __init__(self, input_args, conv_args, heads, negative_slope, edge_dim, *args, **kwargs):
+        self.heads = heads
+        self.negative_slope = negative_slope
+        self.edge_dim = edge_dim
+        super().__init__(input_args, conv_args, *args, **kwargs)
+
+    def _init_conv(self):
+        H = self.heads
+        n = self.num_conv_layers
+        if self.use_global_attn:
+            dims = [(self.embed_dim, True)] + [(self.hidden_dim, True)] * (n - 2) + [(self.hidden_dim, False)]
+            widths = [self.hidden_dim] * n
+        else:
+            dims = [(self.embed_dim, True)] + [(self.hidden_dim * H, True)] * (n - 2) + [(self.hidden_dim * H, False)]
+            widths = [self.hidden_dim * H] * (n - 1) + [self.hidden_dim]
+        for (din, concat), w in zip(dims, widths):
+            self.graph_convs.append(self._apply_global_attn(
+                self.get_conv(din, self.hidden_dim, concat=concat, edge_dim=self.edge_embed_dim)))
+            self.feature_layers.append(BatchNorm(w))
+
+    def _init_node_conv(self):
+        nodeconfiglist = self.config_heads["node"]
+        assert self.num_branches == len(nodeconfiglist), "asumming node head has the same branches as graph head, if any"
+        for b in nodeconfiglist:
+            if b["architecture"]["type"] != "conv":
+                return
+        node_feature_ind = [i for i, t in enumerate(self.head_type) if t == "node"]
+        if not node_feature_ind:
+            return
+        H = self.heads
+        for b in nodeconfiglist:
+            bt, arch = b["type"], b["architecture"]
+            nl, hd = arch["num_headlayers"], arch["dim_headlayers"]
+            ch, bh, co, bo = nn.ModuleList(), nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+            ch.append(self.get_conv(self.hidden_dim, hd[0], True))
+            bh.append(BatchNorm(hd[0] * H))
+            for il in range(nl - 1):
+                ch.append(self.get_conv(hd[il] * H, hd[il + 1], True))
+                bh.append(BatchNorm(hd[il + 1] * H))
+            for ih in node_feature_ind:
+                co.append(self.get_conv(hd[-1] * H, self.head_dims[ih], False))
+                bo.append(BatchNorm(self.head_dims[ih]))
+            self.convs_node_hidden[bt] = ch
+            self.batch_norms_node_hidden[bt] = bh
+            self.convs_node_output[bt] = co
+            self.batch_norms_node_output[bt] = bo
+
+    def get_conv(self, input_dim, output_dim, concat=True, edge_dim=None):
+        gat = GATv2Conv(input_dim, output_dim, heads=self.heads, negative_slope=self.negative_slope,
+                        dropout=self.dropout, add_self_loops=True, edge_dim=edge_dim, concat=concat)
+        out_lin = nn.Linear(self.hidden_dim * self.heads, self.hidden_dim) if (self.use_global_attn and concat) \
+            else nn.Identity()
+        return _GATBlock(gat, out_lin)
+
+    def __str__(self):
+        return "GATStack"

@@ -18,6 +18,8 @@ from torch import nn
 
 from ..ops.attention import segment_attention
 from ..ops.linear import linear
+from ..ops.norm import norm_add
+from ..ops.rng import dropout as rng_dropout, new_salt
 from .layers import BatchNorm, Linear
 
 
@@ -114,21 +116,23 @@ class GPSConv(nn.Module):
         self.norm2 = BatchNorm(channels) if norm else None
         self.norm3 = BatchNorm(channels) if norm else None
 
-    def _norm(self, n, h, ctx):
-        return h if n is None else n(h, ctx.get("num_valid"))
+        # dropout call-site ids for the counter-hash dropout (ops/rng.py)
+        self._salts = [new_salt() for _ in range(4)]
 
     def forward(self, inv, equiv, ctx):
+        nv = ctx.get("num_valid")
+        tr = self.training
         hs = []
         if self.conv is not None:
             h, equiv = self.conv(inv, equiv, ctx)
-            h = F.dropout(h, p=self.dropout, training=self.training)
-            hs.append(self._norm(self.norm1, h + inv, ctx))
+            # BN1(dropout(h) + x): one fused launch each way on the GPU
+            hs.append(norm_add(h, self.norm1, nv, residual=inv, p=self.dropout, salt=self._salts[0], training=tr))
         h = self.attn(inv, ctx.attn_seg_id, ctx.attn_seg_ptr)
-        h = F.dropout(h, p=self.dropout, training=self.training)
-        hs.append(self._norm(self.norm2, h + inv, ctx))
+        hs.append(norm_add(h, self.norm2, nv, residual=inv, p=self.dropout, salt=self._salts[1], training=tr))
         out = hs[0] if len(hs) == 1 else hs[0] + hs[1]
-        out = out + self.mlp(out)
-        out = self._norm(self.norm3, out, ctx)
+        lin1, act, _, lin2, _ = self.mlp
+        m = rng_dropout(act(lin1(out)), self.dropout, tr, self._salts[2])
+        out = norm_add(lin2(m), self.norm3, nv, residual=out, p=self.dropout, salt=self._salts[3], training=tr)
         return out, equiv
 
     def __repr__(self):

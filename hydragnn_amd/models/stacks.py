@@ -9,7 +9,7 @@ _lazy = {
     "DIMEStack": ".dimenet",
     "EGCLStack": ".egnn",
     "PAINNStack": ".painn",
-    "PNAEqStack": ".pnaeq",
+    "PNAEqStack": ".painn",
     "MACEStack": ".mace",
 }
 

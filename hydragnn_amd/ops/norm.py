@@ -75,3 +75,69 @@ def _masked_batch_norm(x, bn, num_valid):
     if bn.weight is not None:
         y = y * bn.weight + bn.bias
     return y
+
+
+class _BNAddFused(torch.autograd.Function):
+    """y = [relu](BN(dropout_p(a) + b)), rows >= num_valid zeroed if zero_pad (one kernel each way)."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight, bias, nv, rmean, rvar, nbt, rng, salt, p, momentum, eps, relu, zero_pad):
+        y, z, mean, invstd = _native.ops().bn_fused_fwd(a, b, nv, weight, bias, rmean, rvar, nbt, rng, salt, p,
+                                                         momentum, eps, relu, zero_pad)
+        if z.numel() == 0 and a.numel() != 0:
+            z = a
+        ctx.save_for_backward(z, mean, invstd, weight, bias, nv, rng)
+        ctx.cfg = (salt, p, relu, zero_pad, b is not None, weight is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, mean, invstd, weight, bias, nv, rng = ctx.saved_tensors
+        salt, p, relu, zero_pad, has_b, has_w = ctx.cfg
+        dz, da, dw, db = _native.ops().bn_fused_bwd(dy, z, nv, mean, invstd, weight, bias, rng, salt, p, relu,
+                                                    zero_pad)
+        if not (rng is not None and p > 0):
+            da = dz
+        return (da, dz if has_b else None, dw if has_w else None, db if has_w else None,
+                None, None, None, None, None, None, None, None, None, None, None)
+
+
+FUSED_MAX_ROWS = 1 << 30  # two-launch slab kernels scale with N
+
+
+def norm_add(a, bn, num_valid=None, residual=None, p=0.0, relu=False, zero_pad=False, salt=0, training=None):
+    """``[relu](BN(dropout_p(a) + residual))``, optionally zeroing rows >= num_valid.
+
+    The GPS / encoder epilogue (reference gps.py:120-150, Base.py:466) as a single
+    HIP launch forward and backward in GPU training mode; torch ops otherwise.
+    ``bn`` may be None (no normalisation).
+    """
+    from . import rng as _rng
+
+    if training is None:
+        training = bn.training if bn is not None else False
+    drop_p = float(p) if (training and p > 0) else 0.0
+    mod = bn.module if (bn is not None and hasattr(bn, "module")) else bn
+    bn_train = mod is not None and (mod.training or not mod.track_running_stats)
+    if (mod is not None and bn_train and a.is_cuda and a.dtype == torch.float32 and a.dim() == 2
+            and a.shape[0] <= FUSED_MAX_ROWS and not _mode._state["composite"] and mod.momentum is not None):
+        nv = _as_nv(num_valid, a.device)
+        track = mod.training and mod.track_running_stats
+        rm = mod.running_mean if track else None
+        rv = mod.running_var if track else None
+        nbt = mod.num_batches_tracked if (track and mod.num_batches_tracked is not None) else None
+        rng = _rng.counter(a.device) if drop_p > 0 else None
+        b = residual.contiguous() if residual is not None else None
+        return _BNAddFused.apply(a.contiguous(), b, mod.weight, mod.bias, nv, rm, rv, nbt, rng, int(salt), drop_p,
+                                 float(mod.momentum), float(mod.eps), bool(relu), bool(zero_pad))
+    h = _rng.dropout(a, drop_p, drop_p > 0, salt)
+    if residual is not None:
+        h = h + residual
+    if mod is not None:
+        h = batch_norm(h, mod, num_valid)
+    if relu:
+        h = torch.relu(h)
+    if zero_pad and num_valid is not None:
+        rows = torch.arange(h.shape[0], device=h.device).view(-1, 1)
+        h = h * (rows < num_valid).to(h.dtype)
+    return h

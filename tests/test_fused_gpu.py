@@ -1,0 +1,104 @@
+"""Numerics of the fused dropout+residual+BatchNorm(+ReLU, +padding mask) kernel
+(``csrc/norm_fused.hip``) against a plain fp32 PyTorch composite of the same op."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(a, b, mask_scale, bn, nv, relu, zero_pad):
+    z = a * mask_scale if mask_scale is not None else a
+    if b is not None:
+        z = z + b
+    zz = z[:nv]
+    mean = zz.mean(0)
+    var = zz.var(0, unbiased=False)
+    y = (z - mean) * torch.rsqrt(var + bn.eps) * bn.weight + bn.bias
+    if relu:
+        y = torch.relu(y)
+    if zero_pad:
+        m = (torch.arange(z.shape[0], device=z.device) < nv).float().view(-1, 1)
+        y = y * m
+    return y, mean, var
+
+
+@pytest.mark.parametrize("N,C", [(2816, 64), (1000, 50), (17, 8), (9000, 128)])
+@pytest.mark.parametrize("resid", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+@pytest.mark.parametrize("relu,zero_pad", [(False, False), (True, True)])
+def test_norm_add(N, C, resid, p, relu, zero_pad):
+    from hydragnn_amd import _native
+    from hydragnn_amd.models.layers import BatchNorm
+    from hydragnn_amd.ops import rng
+    from hydragnn_amd.ops.norm import norm_add
+
+    torch.manual_seed(N + C)
+    dev = "cuda"
+    nv = N - N // 7
+    a = torch.randn(N, C, device=dev, requires_grad=True)
+    b = torch.randn(N, C, device=dev, requires_grad=True) if resid else None
+    bn = BatchNorm(C).to(dev)
+    with torch.no_grad():
+        bn.module.weight.uniform_(0.5, 1.5)
+        bn.module.bias.uniform_(-0.5, 0.5)
+    bn.train()
+    rng.advance(dev)
+    salt = 12345
+    y = norm_add(a, bn, torch.tensor([nv], dtype=torch.int32, device=dev), residual=b, p=p, relu=relu,
+                 zero_pad=zero_pad, salt=salt, training=True)
+    ms = None
+    if p > 0:
+        ms = _native.ops().dropout_hash(torch.ones(N, C, device=dev), rng.counter(dev), salt, p)
+        frac = float((ms == 0).float().mean())
+        assert abs(frac - p) < 4 * (p * (1 - p) / (N * C)) ** 0.5 + 0.01, frac
+    a2 = a.detach().clone().requires_grad_()
+    b2 = b.detach().clone().requires_grad_() if resid else None
+    w2 = bn.module.weight.detach().clone().requires_grad_()
+    bb2 = bn.module.bias.detach().clone().requires_grad_()
+
+    class _BN:
+        eps = bn.module.eps
+        weight = w2
+        bias = bb2
+
+    yr, mean, var = _ref(a2, b2, ms, _BN, nv, relu, zero_pad)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    # running stats (momentum 0.1, unbiased var)
+    torch.testing.assert_close(bn.module.running_mean, 0.1 * mean.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.module.running_var, 0.9 + 0.1 * var.detach() * nv / (nv - 1), rtol=1e-4,
+                               atol=1e-5)
+    assert int(bn.module.num_batches_tracked) == 1
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    torch.testing.assert_close(a.grad, a2.grad, rtol=1e-3, atol=1e-4)
+    if resid:
+        torch.testing.assert_close(b.grad, b2.grad, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.module.weight.grad, w2.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.module.bias.grad, bb2.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_hash_dropout_graph_replay_changes_mask():
+    """The counter advance is captured: every replay draws a new mask."""
+    from hydragnn_amd.ops import rng
+
+    dev = "cuda"
+    x = torch.ones(4096, device=dev)
+    rng.advance(dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            rng.advance(dev)
+            y = rng.dropout(x, 0.5, True, 7)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        rng.advance(dev)
+        y = rng.dropout(x, 0.5, True, 7)
+    g.replay()
+    m1 = y.clone()
+    g.replay()
+    m2 = y.clone()
+    assert not torch.equal(m1, m2)
+    assert abs(float((m1 == 0).float().mean()) - 0.5) < 0.05
