@@ -18,7 +18,7 @@
 // 11-13 us for [2816, 64]: column-strided float4 loads touch a cache line per
 // row and only C/4 CUs work.)
 //
-// Dropout uses a counter-based hash (splitmix64 of seed, call-site salt, element
+// Dropout uses a counter-based hash (lowbias32 of seed, call-site salt, element
 // index) with the seed read from a device int64 counter: capture-safe in hipGraphs
 // (the counter is advanced by a captured kernel each step) and recomputed in the
 // backward instead of storing a mask.
@@ -98,12 +98,25 @@ __device__ __forceinline__ void set_el<1>(float& v, int, float x) {
 // Slab geometry: a 256-thread workgroup owns kSlab consecutive rows; `tpr` threads
 // cover one row (V channels each, coalesced along the row) and the block covers
 // 256/tpr rows per step.  Channel groups beyond tpr*V loop.
-constexpr int kSlab = 128;
 constexpr int kBlk = 256;
+constexpr int kRows = 4;  // rows per thread per slab, all loads issued before use
 
 struct Geo {
-  int tpr, rpb, ngrp;  // threads per row, rows per block-step, channel groups (C / V)
+  int tpr, rpb, ngrp, slab;  // threads per row, rows per block-step, channel groups (C / V), rows per block
 };
+
+
+// Sum over the S slab partials of channel c, T threads per channel (thread j takes
+// s = j, j+T, ...), folded across the T threads in a fixed order.  red: [kBlk].
+__device__ __forceinline__ float chan_sum(float v, float* red, int T) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  float t = 0.f;
+  const int base = (threadIdx.x / T) * T;
+  for (int q = 0; q < T; ++q) t += red[base + q];
+  __syncthreads();
+  return t;
+}
 
 template <int V>
 __device__ __forceinline__ typename VecT<V>::T ldv(const float* p) {
@@ -155,39 +168,56 @@ __global__ void __launch_bounds__(kBlk)
     bnf_stats_kernel(const float* __restrict__ a, const float* __restrict__ b, const int* __restrict__ nvp,
                      const int64_t* __restrict__ rng, int64_t salt, float p, float* __restrict__ z,
                      float* __restrict__ part, int N, int C, Geo g) {
+  using T = typename VecT<V>::T;
   __shared__ float red[kBlk * V];
+  __shared__ float smean[kBlk];
   const int Nv = nvp ? min(*nvp, N) : N;
   const DropCfg d = drop_cfg(rng, salt, p);
-  const int r0 = blockIdx.x * kSlab, r1 = min(N, r0 + kSlab), rv1 = min(Nv, r1);
+  const int r0 = blockIdx.x * g.slab, r1 = min(N, r0 + g.slab), rv1 = min(Nv, r1);
   const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
   const bool fused = z != nullptr;
-  const float* zr = fused ? z : a;
   for (int cg0 = 0; cg0 < g.ngrp; cg0 += g.tpr) {
     const int cg = cg0 + cg_l;
     const bool act = cg < g.ngrp;
     const int c0 = cg * V;
+    T v[kRows];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (act && r < r1) v[i] = ldv<V>(a + (int64_t)r * C + c0);
+    }
+    if (fused) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) {
+        const int r = r0 + rl + i * g.rpb;
+        if (act && r < r1) {
+          const int64_t off = (int64_t)r * C + c0;
+          T bb;
+          if (b) bb = ldv<V>(b + off);
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            float x = el<V>(v[i], k);
+            if (d.on) x = keep_elem(d.seed, (uint32_t)(off + k), d.thresh) ? x * d.scale : 0.f;
+            if (b) x += el<V>(bb, k);
+            set_el<V>(v[i], k, x);
+          }
+          stv<V>(z + off, v[i]);
+        }
+      }
+    }
     float sm[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) sm[k] = 0.f;
-    if (act) {
-      for (int r = r0 + rl; r < r1; r += g.rpb) {
-        const int64_t off = (int64_t)r * C + c0;
-        typename VecT<V>::T v;
-        if (fused) {
-          v = make_z<V>(a, b, d, off);
-          stv<V>(z + off, v);
-        } else {
-          v = ldv<V>(a + off);
-        }
-        if (r < rv1) {
 #pragma unroll
-          for (int k = 0; k < V; ++k) sm[k] += el<V>(v, k);
-        }
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (act && r < rv1) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) sm[k] += el<V>(v[i], k);
       }
     }
     fold_rows<V>(sm, red, rl, cg_l, g);
     const float cnt = (float)max(rv1 - r0, 0);
-    __shared__ float smean[kBlk];
     if (rl == 0 && act) {
 #pragma unroll
       for (int k = 0; k < V; ++k) smean[cg_l * V + k] = cnt > 0.f ? sm[k] / cnt : 0.f;
@@ -199,12 +229,13 @@ __global__ void __launch_bounds__(kBlk)
       mu[k] = act ? smean[cg_l * V + k] : 0.f;
       m2[k] = 0.f;
     }
-    if (act) {
-      for (int r = r0 + rl; r < rv1; r += g.rpb) {  // own writes: same thread, visible
-        const typename VecT<V>::T v = ldv<V>(zr + (int64_t)r * C + c0);
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (act && r < rv1) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-          const float t = el<V>(v, k) - mu[k];
+          const float t = el<V>(v[i], k) - mu[k];
           m2[k] = fmaf(t, t, m2[k]);
         }
       }
@@ -223,8 +254,9 @@ __global__ void __launch_bounds__(kBlk)
   }
 }
 
-// forward pass 2: combine the S slab statistics (Chan, fixed order) per channel, then
-// normalise this block's slab.
+// forward pass 2: every workgroup folds the S slab stats (exact two-pass combine,
+// T threads per channel, fixed order), then y = z * scale + shift (+relu, padding
+// rows -> 0) for its slab; workgroup 0 writes the saved stats and running stats.
 template <int V>
 __global__ void __launch_bounds__(kBlk)
     bnf_apply_kernel(const float* __restrict__ zr, const int* __restrict__ nvp, const float* __restrict__ part, int S,
@@ -233,55 +265,105 @@ __global__ void __launch_bounds__(kBlk)
                      int zero_pad, float* __restrict__ y, float* __restrict__ smean, float* __restrict__ sinvstd,
                      int N, int C, Geo g) {
   extern __shared__ float sh[];  // scale[C], shift[C]
+  __shared__ float red[kBlk];
   float* scl = sh;
   float* shf = sh + C;
   const int Nv = nvp ? min(*nvp, N) : N;
-  for (int c = threadIdx.x; c < C; c += kBlk) {
-    float n = 0.f, m = 0.f, M2 = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float* P = part + (int64_t)s * 3 * C;
-      const float nb = P[c];
-      if (nb <= 0.f) continue;
-      const float mb = P[C + c], M2b = P[2 * C + c];
-      const float nn = n + nb;
-      const float dl = mb - m;
-      m += dl * (nb / nn);
-      M2 += M2b + dl * dl * (n * nb / nn);
-      n = nn;
+  const int r0 = blockIdx.x * g.slab, r1 = min(N, r0 + g.slab);
+  const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
+  // prefetch this slab's rows (first channel-group pass) before touching the partials
+  typename VecT<V>::T v[kRows];
+  {
+    const int c0 = cg_l * V;
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (cg_l < g.ngrp && r < r1) v[i] = ldv<V>(zr + (int64_t)r * C + c0);
     }
-    const float var = n > 0.f ? M2 / n : 0.f;
-    const float is = rsqrtf(var + eps);
-    const float ww = w ? w[c] : 1.f, bb = beta ? beta[c] : 0.f;
-    scl[c] = is * ww;
-    shf[c] = bb - m * is * ww;
-    if (blockIdx.x == 0) {
-      smean[c] = m;
-      sinvstd[c] = is;
-      if (rmean) {
-        const float unb = n > 1.f ? var * n / (n - 1.f) : var;
-        rmean[c] = (1.f - momentum) * rmean[c] + momentum * m;
-        rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  }
+  const int TT = max(1, kBlk / C);
+  for (int cb = 0; cb < C; cb += kBlk / TT) {
+    const int c = cb + threadIdx.x / TT, j = threadIdx.x % TT;
+    const bool ok = c < C && threadIdx.x < (kBlk / TT) * TT;
+    // all of this thread's partials in registers (one memory round trip)
+    constexpr int kQ = 16;
+    float qn[kQ], qm[kQ], q2[kQ];
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      const int q = j + t * TT;
+      const bool in = ok && q < S;
+      qn[t] = in ? part[(int64_t)q * 3 * C + c] : 0.f;
+      qm[t] = in ? part[(int64_t)q * 3 * C + C + c] : 0.f;
+      q2[t] = in ? part[(int64_t)q * 3 * C + 2 * C + c] : 0.f;
+    }
+    float n = 0.f, sm = 0.f;
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      n += qn[t];
+      sm = fmaf(qn[t], qm[t], sm);
+    }
+    for (int q = j + kQ * TT; ok && q < S; q += TT) {  // rare: more than 16 partials per thread
+      const float nb = part[(int64_t)q * 3 * C + c];
+      n += nb;
+      sm = fmaf(nb, part[(int64_t)q * 3 * C + C + c], sm);
+    }
+    n = chan_sum(n, red, TT);
+    sm = chan_sum(sm, red, TT);
+    const float mean = n > 0.f ? sm / n : 0.f;
+    float M2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      const float dl = qm[t] - mean;
+      M2 += q2[t] + qn[t] * dl * dl;
+    }
+    for (int q = j + kQ * TT; ok && q < S; q += TT) {
+      const float* P = part + (int64_t)q * 3 * C;
+      const float dl = P[C + c] - mean;
+      M2 += P[2 * C + c] + P[c] * dl * dl;
+    }
+    M2 = chan_sum(M2, red, TT);
+    if (ok && j == 0) {
+      const float var = n > 0.f ? M2 / n : 0.f;
+      const float is = rsqrtf(var + eps);
+      const float ww = w ? w[c] : 1.f, bb = beta ? beta[c] : 0.f;
+      scl[c] = is * ww;
+      shf[c] = bb - mean * is * ww;
+      if (blockIdx.x == 0) {
+        smean[c] = mean;
+        sinvstd[c] = is;
+        if (rmean) {
+          const float unb = n > 1.f ? var * n / (n - 1.f) : var;
+          rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+          rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+        }
       }
     }
   }
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   __syncthreads();
-  const int r0 = blockIdx.x * kSlab, r1 = min(N, r0 + kSlab);
-  const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
   for (int cg = cg_l; cg < g.ngrp; cg += g.tpr) {
     const int c0 = cg * V;
-    for (int r = r0 + rl; r < r1; r += g.rpb) {
-      const int64_t off = (int64_t)r * C + c0;
-      const typename VecT<V>::T v = ldv<V>(zr + off);
-      typename VecT<V>::T o;
-      const bool pad = zero_pad && r >= Nv;
+    if (cg != cg_l) {  // further channel-group passes (C > 4 * tpr): load now
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        float t = fmaf(el<V>(v, k), scl[c0 + k], shf[c0 + k]);
-        if (relu) t = fmaxf(t, 0.f);
-        set_el<V>(o, k, pad ? 0.f : t);
+      for (int i = 0; i < kRows; ++i) {
+        const int r = r0 + rl + i * g.rpb;
+        if (r < r1) v[i] = ldv<V>(zr + (int64_t)r * C + c0);
       }
-      stv<V>(y + off, o);
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (r < r1) {
+        typename VecT<V>::T o;
+        const bool pad = zero_pad && r >= Nv;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          float t = fmaf(el<V>(v[i], k), scl[c0 + k], shf[c0 + k]);
+          if (relu) t = fmaxf(t, 0.f);
+          set_el<V>(o, k, pad ? 0.f : t);
+        }
+        stv<V>(y + (int64_t)r * C + c0, o);
+      }
     }
   }
 }
@@ -296,7 +378,7 @@ __global__ void __launch_bounds__(kBlk)
   __shared__ float red[kBlk * V];
   const int Nv = nvp ? min(*nvp, N) : N;
   const int Ns = zero_pad ? Nv : N;
-  const int r0 = blockIdx.x * kSlab, r1 = min(Ns, r0 + kSlab);
+  const int r0 = blockIdx.x * g.slab, r1 = min(Ns, r0 + g.slab);
   const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
   for (int cg0 = 0; cg0 < g.ngrp; cg0 += g.tpr) {
     const int cg = cg0 + cg_l;
@@ -311,15 +393,23 @@ __global__ void __launch_bounds__(kBlk)
       ww[k] = (act && w) ? w[c0 + k] : 1.f;
       bb[k] = (act && beta) ? beta[c0 + k] : 0.f;
     }
-    if (act) {
-      for (int r = r0 + rl; r < r1; r += g.rpb) {
-        const int64_t off = (int64_t)r * C + c0;
-        const typename VecT<V>::T gv = ldv<V>(dy + off);
-        const typename VecT<V>::T zv = ldv<V>(z + off);
+    typename VecT<V>::T gv[kRows], zv[kRows];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (act && r < r1) {
+        gv[i] = ldv<V>(dy + (int64_t)r * C + c0);
+        zv[i] = ldv<V>(z + (int64_t)r * C + c0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (act && r < r1) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-          const float xh = (el<V>(zv, k) - mu[k]) * is[k];
-          float gg = el<V>(gv, k);
+          const float xh = (el<V>(zv[i], k) - mu[k]) * is[k];
+          float gg = el<V>(gv[i], k);
           if (relu && fmaf(xh, ww[k], bb[k]) <= 0.f) gg = 0.f;
           sg[k] += gg;
           sx[k] = fmaf(gg, xh, sx[k]);
@@ -349,27 +439,61 @@ __global__ void __launch_bounds__(kBlk)
                      float* __restrict__ dz, float* __restrict__ da, float* __restrict__ dw, float* __restrict__ db,
                      int N, int C, Geo g) {
   extern __shared__ float sh[];  // sum g [C], sum g*xhat [C]
+  __shared__ float red[kBlk];
   float* Sg = sh;
   float* Sx = sh + C;
   const int Nv = nvp ? min(*nvp, N) : N;
-  for (int c = threadIdx.x; c < C; c += kBlk) {
-    float a0 = 0.f, a1 = 0.f;
-    for (int s = 0; s < S; ++s) {
-      a0 += part[(int64_t)s * 2 * C + c];
-      a1 += part[(int64_t)s * 2 * C + C + c];
+  const int r0 = blockIdx.x * g.slab, r1 = min(N, r0 + g.slab);
+  const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
+  typename VecT<V>::T gvs[kRows], zvs[kRows];
+  {
+    const int c0 = cg_l * V;
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (cg_l < g.ngrp && r < r1) {
+        gvs[i] = ldv<V>(dy + (int64_t)r * C + c0);
+        zvs[i] = ldv<V>(z + (int64_t)r * C + c0);
+      }
     }
-    Sg[c] = a0;
-    Sx[c] = a1;
-    if (blockIdx.x == 0) {
-      if (dw) dw[c] = a1;
-      if (db) db[c] = a0;
+  }
+  const int TT = max(1, kBlk / C);
+  for (int cb = 0; cb < C; cb += kBlk / TT) {
+    const int c = cb + threadIdx.x / TT, j = threadIdx.x % TT;
+    const bool ok = c < C && threadIdx.x < (kBlk / TT) * TT;
+    constexpr int kQ = 16;
+    float qa[kQ], qb[kQ];
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      const int q = j + t * TT;
+      const bool in = ok && q < S;
+      qa[t] = in ? part[(int64_t)q * 2 * C + c] : 0.f;
+      qb[t] = in ? part[(int64_t)q * 2 * C + C + c] : 0.f;
+    }
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      a0 += qa[t];
+      a1 += qb[t];
+    }
+    for (int q = j + kQ * TT; ok && q < S; q += TT) {
+      a0 += part[(int64_t)q * 2 * C + c];
+      a1 += part[(int64_t)q * 2 * C + C + c];
+    }
+    a0 = chan_sum(a0, red, TT);
+    a1 = chan_sum(a1, red, TT);
+    if (ok && j == 0) {
+      Sg[c] = a0;
+      Sx[c] = a1;
+      if (blockIdx.x == 0) {
+        if (dw) dw[c] = a1;
+        if (db) db[c] = a0;
+      }
     }
   }
   __syncthreads();
   const DropCfg d = drop_cfg(rng, salt, p);
   const float inv_n = Nv > 0 ? 1.f / (float)Nv : 0.f;
-  const int r0 = blockIdx.x * kSlab, r1 = min(N, r0 + kSlab);
-  const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
   for (int cg = cg_l; cg < g.ngrp; cg += g.tpr) {
     const int c0 = cg * V;
     float mu[V], is[V], ww[V], bb[V];
@@ -380,10 +504,23 @@ __global__ void __launch_bounds__(kBlk)
       ww[k] = w ? w[c0 + k] : 1.f;
       bb[k] = beta ? beta[c0 + k] : 0.f;
     }
-    for (int r = r0 + rl; r < r1; r += g.rpb) {
+    if (cg != cg_l) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) {
+        const int r = r0 + rl + i * g.rpb;
+        if (r < r1) {
+          gvs[i] = ldv<V>(dy + (int64_t)r * C + c0);
+          zvs[i] = ldv<V>(z + (int64_t)r * C + c0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int r = r0 + rl + i * g.rpb;
+      if (r >= r1) continue;
       const int64_t off = (int64_t)r * C + c0;
-      const typename VecT<V>::T gv = ldv<V>(dy + off);
-      const typename VecT<V>::T zv = ldv<V>(z + off);
+      const typename VecT<V>::T gv = gvs[i];
+      const typename VecT<V>::T zv = zvs[i];
       typename VecT<V>::T o, od;
       const bool valid = r < Nv;
 #pragma unroll
@@ -414,7 +551,7 @@ static Geo make_geo(int C, int V) {
   const int ngrp = C / V;
   int tpr = 1;
   while (tpr < ngrp && tpr < 64) tpr <<= 1;
-  return Geo{tpr, kBlk / tpr, ngrp};
+  return Geo{tpr, kBlk / tpr, ngrp, (kBlk / tpr) * kRows};
 }
 
 // returns (y, z, mean, invstd); z is empty (use `a`) when neither dropout nor residual is fused
@@ -451,26 +588,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fused_fwd(
   const float* bp = has_b ? b->data_ptr<float>() : nullptr;
   float* zp = fused_z ? z.data_ptr<float>() : nullptr;
   const float* zr = fused_z ? z.data_ptr<float>() : a.data_ptr<float>();
-  const int S = ceil_div(N, kSlab);
+  const Geo g0 = make_geo(C, C % 4 == 0 ? 4 : 1);
+  const int S = ceil_div(N, g0.slab);
   at::Tensor part = at::empty({S, 3, C}, opt);
   const size_t lds = 2 * (size_t)C * sizeof(float);
-  if (C % 4 == 0) {
-    const Geo g = make_geo(C, 4);
-    bnf_stats_kernel<4><<<S, kBlk, 0, stream()>>>(a.data_ptr<float>(), bp, nvp, rp, salt, (float)p, zp,
-                                                  part.data_ptr<float>(), N, C, g);
-    bnf_apply_kernel<4><<<S, kBlk, lds, stream()>>>(zr, nvp, part.data_ptr<float>(), S, optf(w), optf(beta), rm, rv,
-                                                    nb, (float)momentum, (float)eps, relu, zero_pad,
-                                                    y.data_ptr<float>(), mean.data_ptr<float>(),
-                                                    invstd.data_ptr<float>(), N, C, g);
-  } else {
-    const Geo g = make_geo(C, 1);
-    bnf_stats_kernel<1><<<S, kBlk, 0, stream()>>>(a.data_ptr<float>(), bp, nvp, rp, salt, (float)p, zp,
-                                                  part.data_ptr<float>(), N, C, g);
-    bnf_apply_kernel<1><<<S, kBlk, lds, stream()>>>(zr, nvp, part.data_ptr<float>(), S, optf(w), optf(beta), rm, rv,
-                                                    nb, (float)momentum, (float)eps, relu, zero_pad,
-                                                    y.data_ptr<float>(), mean.data_ptr<float>(),
-                                                    invstd.data_ptr<float>(), N, C, g);
+#define HY_BNF(VV)                                                                                                 \
+  {                                                                                                                \
+    const Geo g = make_geo(C, VV);                                                                                 \
+    bnf_stats_kernel<VV><<<S, kBlk, 0, stream()>>>(a.data_ptr<float>(), bp, nvp, rp, salt, (float)p, zp,          \
+                                                   part.data_ptr<float>(), N, C, g);                              \
+    bnf_apply_kernel<VV><<<S, kBlk, lds, stream()>>>(zr, nvp, part.data_ptr<float>(), S, optf(w), optf(beta), rm,  \
+                                                     rv, nb, (float)momentum, (float)eps, relu, zero_pad,         \
+                                                     y.data_ptr<float>(), mean.data_ptr<float>(),                 \
+                                                     invstd.data_ptr<float>(), N, C, g);                          \
   }
+  if (C % 4 == 0) HY_BNF(4) else HY_BNF(1)
+#undef HY_BNF
   return {y, z, mean, invstd};
 }
 
@@ -491,30 +624,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fused_bwd(
   const int* nvp = nv.has_value() && nv->defined() ? nv->data_ptr<int>() : nullptr;
   const int64_t* rp = drop ? rng->data_ptr<int64_t>() : nullptr;
   float* dap = drop ? da.data_ptr<float>() : nullptr;
-  const int S = ceil_div(N, kSlab);
+  const Geo g0 = make_geo(C, C % 4 == 0 ? 4 : 1);
+  const int S = ceil_div(N, g0.slab);
   at::Tensor part = at::empty({S, 2, C}, z.options());  // every slab writes its (possibly zero) sums
   const size_t lds = 2 * (size_t)C * sizeof(float);
-  if (C % 4 == 0) {
-    const Geo g = make_geo(C, 4);
-    bnb_partial_kernel<4><<<S, kBlk, 0, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,
-                                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),
-                                                    optf(beta), relu, zero_pad, part.data_ptr<float>(), N, C, g);
-    bnb_apply_kernel<4><<<S, kBlk, lds, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,
-                                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),
-                                                    optf(beta), part.data_ptr<float>(), S, rp, salt, (float)p, relu,
-                                                    zero_pad, dz.data_ptr<float>(), dap, dw.data_ptr<float>(),
-                                                    db.data_ptr<float>(), N, C, g);
-  } else {
-    const Geo g = make_geo(C, 1);
-    bnb_partial_kernel<1><<<S, kBlk, 0, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,
-                                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),
-                                                    optf(beta), relu, zero_pad, part.data_ptr<float>(), N, C, g);
-    bnb_apply_kernel<1><<<S, kBlk, lds, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,
-                                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),
-                                                    optf(beta), part.data_ptr<float>(), S, rp, salt, (float)p, relu,
-                                                    zero_pad, dz.data_ptr<float>(), dap, dw.data_ptr<float>(),
-                                                    db.data_ptr<float>(), N, C, g);
+#define HY_BNB(VV)                                                                                                 \
+  {                                                                                                                \
+    const Geo g = make_geo(C, VV);                                                                                 \
+    bnb_partial_kernel<VV><<<S, kBlk, 0, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,               \
+                                                     mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),   \
+                                                     optf(beta), relu, zero_pad, part.data_ptr<float>(), N, C, g);\
+    bnb_apply_kernel<VV><<<S, kBlk, lds, stream()>>>(dy.data_ptr<float>(), z.data_ptr<float>(), nvp,               \
+                                                     mean.data_ptr<float>(), invstd.data_ptr<float>(), optf(w),   \
+                                                     optf(beta), part.data_ptr<float>(), S, rp, salt, (float)p,   \
+                                                     relu, zero_pad, dz.data_ptr<float>(), dap,                   \
+                                                     dw.data_ptr<float>(), db.data_ptr<float>(), N, C, g);        \
   }
+  if (C % 4 == 0) HY_BNB(4) else HY_BNB(1)
+#undef HY_BNB
   return {dz, da, dw, db};
 }
 

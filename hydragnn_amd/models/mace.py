@@ -1,0 +1,399 @@
+"""MACE stack (reference ``hydragnn/models/MACEStack.py:75-546`` and
+``hydragnn/utils/model/mace_utils/modules/blocks.py``) on the in-house O(3) toolkit
+(``ops/o3.py``; e3nn is not available, basis/sign parity with e3nn is unpinned,
+equivariance is tested directly).
+
+Per layer (``RealAgnosticAttResidualInteractionBlock`` + ``EquivariantProductBasisBlock``):
+
+    sc   = skip_linear(h)
+    m_i  = linear( sum_{j->i} TP_uvu(linear_up(h)_j, [e_ij ⊕] Y(r̂_ij); FCN([R(r_ij), down(h)_j, down(h)_i])) ) / avg_neighbours
+    h'   = linear(SymmetricContraction_{correlation}(m_i; element_i)) + sc
+    h'   = sizing(h')   -> split into scalars (inv) and l > 0 blocks (equiv)
+
+and a read-out after the embedding and after every layer whose predictions are
+*summed* (linear read-outs, a non-linear one after the last layer).  Messages are
+reduced with the CSR segment sum over destinations (deterministic, HIP on GPU).
+"""
+import math
+import warnings
+
+import torch
+from torch import nn
+from torch.nn import ModuleDict, ModuleList, Sequential
+
+from ..ops import o3
+from ..ops import segment as seg
+from ..ops.geometry import edge_vectors_and_lengths
+from .base import Base
+from .layers import Linear
+
+NUM_ELEMENTS = 118
+
+
+# ----------------------------------------------------------------------------- radial
+class MACEBesselBasis(nn.Module):
+    """sqrt(2/r_max) sin(n pi r / r_max) / r (reference ``radial.py:23-63``)."""
+
+    def __init__(self, r_max, num_basis=8, trainable=False):
+        super().__init__()
+        w = math.pi / r_max * torch.linspace(1.0, num_basis, num_basis)
+        if trainable:
+            self.bessel_weights = nn.Parameter(w)
+        else:
+            self.register_buffer("bessel_weights", w)
+        self.prefactor = math.sqrt(2.0 / r_max)
+
+    def forward(self, x):
+        return self.prefactor * torch.sin(self.bessel_weights * x) / x
+
+
+class GaussianBasis(nn.Module):
+    def __init__(self, r_max, num_basis=128, trainable=False):
+        super().__init__()
+        gw = torch.linspace(0.0, r_max, num_basis)
+        if trainable:
+            self.gaussian_weights = nn.Parameter(gw)
+        else:
+            self.register_buffer("gaussian_weights", gw)
+        self.coeff = -0.5 / (r_max / (num_basis - 1)) ** 2
+
+    def forward(self, x):
+        return torch.exp(self.coeff * (x - self.gaussian_weights) ** 2)
+
+
+class ChebychevBasis(nn.Module):
+    def __init__(self, r_max, num_basis=8):
+        super().__init__()
+        self.r_max, self.num_basis = r_max, num_basis
+        self.register_buffer("n", torch.arange(1, num_basis + 1).float())
+
+    def forward(self, x):
+        t = x.expand(-1, self.num_basis)
+        return torch.special.chebyshev_polynomial_t(t, self.n)
+
+
+class PolynomialCutoff(nn.Module):
+    def __init__(self, r_max, p=6):
+        super().__init__()
+        self.r_max, self.p = float(r_max), float(p)
+
+    def forward(self, x):
+        p, u = self.p, x / self.r_max
+        env = (1.0 - (p + 1.0) * (p + 2.0) / 2.0 * u ** p + p * (p + 2.0) * u ** (p + 1)
+               - p * (p + 1.0) / 2.0 * u ** (p + 2))
+        return env * (x < self.r_max)
+
+
+class RadialEmbeddingBlock(nn.Module):
+    def __init__(self, r_max, num_bessel, num_polynomial_cutoff, radial_type="bessel", distance_transform=None):
+        super().__init__()
+        if radial_type in (None, "bessel"):
+            self.bessel_fn = MACEBesselBasis(r_max, num_bessel)
+        elif radial_type == "gaussian":
+            self.bessel_fn = GaussianBasis(r_max, num_bessel)
+        elif radial_type == "chebyshev":
+            self.bessel_fn = ChebychevBasis(r_max, num_bessel)
+        else:
+            raise ValueError(f"unknown radial_type {radial_type}")
+        if distance_transform not in (None, "None"):
+            raise NotImplementedError("MACE distance transforms (Agnesi/Soft) need covalent-radius tables "
+                                      "(ase) that are not available in this build")
+        self.cutoff_fn = PolynomialCutoff(r_max, num_polynomial_cutoff)
+        self.out_dim = num_bessel
+
+    def forward(self, edge_lengths):
+        return self.bessel_fn(edge_lengths) * self.cutoff_fn(edge_lengths)
+
+
+# ----------------------------------------------------------------------------- blocks
+def _to_channels(x, irreps):
+    """flat e3nn layout (blocks of [H, 2l+1], equal H) -> [N, H, sum(2l+1)]."""
+    N = x.shape[0]
+    out = []
+    for (a, b), (m, l, _) in zip(irreps.slices(), irreps.blocks):
+        out.append(x[:, a:b].reshape(N, m, 2 * l + 1))
+    return torch.cat(out, -1)
+
+
+class InteractionBlock(nn.Module):
+    """RealAgnosticAttResidualInteractionBlock (reference ``blocks.py:286-388``)."""
+
+    def __init__(self, node_feats_irreps, edge_attrs_irreps, num_edge_feats, target_irreps, hidden_irreps,
+                 avg_num_neighbors):
+        super().__init__()
+        self.node_feats_irreps, self.edge_attrs_irreps = node_feats_irreps, edge_attrs_irreps
+        self.target_irreps, self.hidden_irreps = target_irreps, hidden_irreps
+        self.avg_num_neighbors = avg_num_neighbors
+        n_down = hidden_irreps.count(0, 1)
+        self.linear_up = o3.O3Linear(node_feats_irreps, node_feats_irreps)
+        irreps_mid, ins = o3.tp_uvu_instructions(node_feats_irreps, edge_attrs_irreps, target_irreps)
+        self.conv_tp = o3.TensorProductUVU(node_feats_irreps, edge_attrs_irreps, irreps_mid, ins)
+        self.linear_down = o3.O3Linear(node_feats_irreps, o3.Irreps([(n_down, 0, 1)]))
+        self.conv_tp_weights = o3.FullyConnectedNet([num_edge_feats + 2 * n_down] + 3 * [n_down]
+                                                    + [self.conv_tp.weight_numel])
+        self.linear = o3.O3Linear(irreps_mid.simplify(), target_irreps)
+        self.skip_linear = o3.O3Linear(node_feats_irreps, hidden_irreps)
+
+    def forward(self, h, edge_attrs, edge_feats, dst_si, src_si):
+        sc = self.skip_linear(h)
+        up = self.linear_up(h)
+        down = self.linear_down(h)
+        w = self.conv_tp_weights(torch.cat([edge_feats, seg.gather(down, src_si), seg.gather(down, dst_si)], -1))
+        mji = self.conv_tp(seg.gather(up, src_si), edge_attrs, w)
+        msg = self.linear(seg.segment_sum(mji, dst_si)) / self.avg_num_neighbors
+        return _to_channels(msg, self.target_irreps), sc
+
+
+class EquivariantProductBasisBlock(nn.Module):
+    def __init__(self, lmax_in, target_irreps, correlation, num_features, num_elements, use_sc=True):
+        super().__init__()
+        self.use_sc = use_sc
+        self.symmetric_contractions = o3.SymmetricContraction(lmax_in, target_irreps, correlation, num_features,
+                                                              num_elements)
+        self.linear = o3.O3Linear(target_irreps, target_irreps)
+
+    def forward(self, x, sc, elem):
+        out = self.linear(self.symmetric_contractions(x, elem))
+        return out + sc if (self.use_sc and sc is not None) else out
+
+
+class MACELayer(nn.Module):
+    def __init__(self, inter, prod, sizing, n_scalars_out):
+        super().__init__()
+        self.inter, self.prod, self.sizing = inter, prod, sizing
+        self.n_scalars_out = n_scalars_out
+
+    def forward(self, inv, equiv, ctx):
+        h = torch.cat([inv, equiv], 1)
+        m, sc = self.inter(h, ctx.edge_attributes, ctx.edge_features, ctx.dst_si, ctx.src_si)
+        h = self.sizing(self.prod(m, sc, ctx.elem))
+        return h[:, :self.n_scalars_out], h[:, self.n_scalars_out:]
+
+
+class _ScalarLinear(nn.Module):
+    """o3.Linear(irreps -> n x 0e): only the scalar block contributes (no bias)."""
+
+    def __init__(self, irreps_in, n_out):
+        super().__init__()
+        self.lin = o3.O3Linear(irreps_in, o3.Irreps([(n_out, 0, 1)]))
+
+    def forward(self, x):
+        return self.lin(x)
+
+
+class MultiheadDecoderBlock(nn.Module):
+    """Linear (intermediate) or non-linear (last) MACE read-out over all heads
+    (reference ``blocks.py:417-767``)."""
+
+    def __init__(self, nonlinear, input_irreps, config_heads, head_dims, head_type, num_heads, act, num_nodes):
+        super().__init__()
+        self.nonlinear = nonlinear
+        self.head_dims, self.head_type, self.num_heads = head_dims, head_type, num_heads
+        self.config_heads = config_heads
+        self.input_scalar_dim = input_irreps.count(0, 1)
+        self.graph_shared = ModuleDict({})
+        self.heads_NN = ModuleList()
+        self.num_branches = len(config_heads["graph"]) if "graph" in config_heads else (
+            len(config_heads["node"]) if "node" in config_heads else 1)
+        if nonlinear and "graph" in config_heads:
+            for b in config_heads["graph"]:
+                a = b["architecture"]
+                ds = a["dim_sharedlayers"]
+                layers = [Linear(self.input_scalar_dim, ds), act]
+                for _ in range(a["num_sharedlayers"] - 1):
+                    layers += [Linear(ds, ds), act]
+                self.graph_shared[b["type"]] = Sequential(*layers)
+        for ih in range(num_heads):
+            hn = ModuleDict({})
+            if head_type[ih] == "graph":
+                for b in config_heads["graph"]:
+                    a = b["architecture"]
+                    if nonlinear:
+                        dh = a["dim_headlayers"]
+                        layers = [Linear(a["dim_sharedlayers"], dh[0]), act]
+                        for il in range(a["num_headlayers"] - 1):
+                            layers += [Linear(dh[il], dh[il + 1]), act]
+                        layers.append(Linear(dh[-1], head_dims[ih]))
+                    else:
+                        layers = [Linear(self.input_scalar_dim, head_dims[ih])]
+                    hn[b["type"]] = Sequential(*layers)
+            elif head_type[ih] == "node":
+                for b in config_heads["node"]:
+                    a = b["architecture"]
+                    if a["type"] == "conv":
+                        raise ValueError("Node-level convolutional layers are not supported in MACE")
+                    if a["type"] == "mlp_per_node":
+                        raise ValueError("mlp_per_node heads are not supported for MACE in this build")
+                    if nonlinear:
+                        dh = a["dim_headlayers"]
+                        layers = [_ScalarLinear(input_irreps, dh[0]), act]
+                        for il in range(len(dh) - 1):
+                            layers += [Linear(dh[il], dh[il + 1]), act]
+                        layers.append(Linear(dh[-1], head_dims[ih]))
+                    else:
+                        layers = [_ScalarLinear(input_irreps, head_dims[ih])]
+                    hn[b["type"]] = Sequential(*layers)
+            else:
+                raise ValueError("Unknown head type" + head_type[ih])
+            self.heads_NN.append(hn)
+
+    def forward(self, node_features, ctx, ids):
+        gsi = ctx.graph_si
+        sc = node_features[:, :self.input_scalar_dim]
+        gfeat = sc.mean(0, keepdim=True) if gsi is None else seg.segment_mean(sc, gsi)
+        data = ctx.data
+        outs = []
+        for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
+            if t == "graph":
+                if self.num_branches == 1 or len(ids) <= 1:
+                    bt = f"branch-{ids[0] if ids else 0}" if self.num_branches > 1 else "branch-0"
+                    x = self.graph_shared[bt](gfeat) if self.nonlinear else gfeat
+                    outs.append(hn[bt](x)[:, :hd])
+                else:
+                    dn = data.dataset_name.view(-1)
+                    head = gfeat.new_zeros(gfeat.shape[0], hd)
+                    for ID in ids:
+                        mask = dn == ID
+                        bt = f"branch-{ID}"
+                        x = gfeat[mask]
+                        x = self.graph_shared[bt](x) if self.nonlinear else x
+                        head = head.index_put((mask,), hn[bt](x)[:, :hd])
+                    outs.append(head)
+            else:
+                if self.num_branches == 1 or len(ids) <= 1:
+                    bt = f"branch-{ids[0] if ids else 0}" if self.num_branches > 1 else "branch-0"
+                    outs.append(hn[bt](node_features)[:, :hd])
+                else:
+                    dn = data.dataset_name.view(-1)
+                    head = node_features.new_zeros(node_features.shape[0], hd)
+                    for ID in ids:
+                        mask = (dn == ID)[data.batch]
+                        head = head.index_put((mask,), hn[f"branch-{ID}"](node_features[mask])[:, :hd])
+                    outs.append(head)
+        return outs
+
+
+# ----------------------------------------------------------------------------- stack
+def process_node_attributes(x, num_elements=NUM_ELEMENTS):
+    """Atomic numbers (data.x) -> one-hot [N, 118] (reference ``MACEStack.py:485-520``)."""
+    z = x.squeeze()
+    if z.dim() == 0:
+        z = z.view(1)
+    assert z.dim() == 1, "MACE only supports raw atomic numbers as node_attributes (1D data.x)."
+    if not bool(torch.all(z == z.round())):
+        warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x contains floats.")
+    if not bool(torch.all((z >= 1) & (z <= num_elements))):
+        warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x is not in 1-118.")
+        z = z.clamp(1, 118)
+    idx = (z - 1).long()
+    return torch.nn.functional.one_hot(idx, num_classes=num_elements).float(), idx
+
+
+class MACEStack(Base):
+    is_edge_model = True
+
+    def __init__(self, input_args, conv_args, r_max, radial_type, distance_transform, num_bessel, edge_dim, max_ell,
+                 node_max_ell, avg_num_neighbors, num_polynomial_cutoff, correlation, *args, **kwargs):
+        self.max_ell = max_ell
+        self.node_max_ell = node_max_ell
+        self.edge_dim = edge_dim
+        self.avg_num_neighbors = avg_num_neighbors
+        self.num_elements = NUM_ELEMENTS
+        self.num_polynomial_cutoff = 5 if num_polynomial_cutoff is None else num_polynomial_cutoff
+        corr = 2 if correlation is None else correlation
+        self.correlation = corr if isinstance(corr, (list, tuple)) else [corr]
+        self.radial_type = "bessel" if radial_type is None else radial_type
+        self.num_bessel = num_bessel
+        self.r_max = r_max
+        super().__init__(input_args, conv_args, *args, **kwargs)
+        self.radial_embedding = RadialEmbeddingBlock(r_max, num_bessel, self.num_polynomial_cutoff, self.radial_type,
+                                                     distance_transform)
+        self.node_embedding = o3.O3Linear(o3.Irreps([(self.num_elements, 0, 1)]),
+                                          o3.Irreps([(self.hidden_dim, 0, 1)]))
+
+    # decoders are built per layer; Base's multi-head decoder is not used
+    def _multihead(self):
+        self.num_branches = len(self.config_heads["graph"]) if "graph" in self.config_heads else 1
+
+    def _init_conv(self):
+        H = self.hidden_dim
+        self.sh_irreps = o3.Irreps.sh(self.max_ell)
+        if self.use_edge_attr:
+            self.edge_attrs_irreps = (o3.Irreps([(self.edge_dim, 0, 1)]) + self.sh_irreps).simplify()
+        else:
+            self.edge_attrs_irreps = self.sh_irreps
+        hidden = o3.Irreps.natural(H, self.node_max_ell)
+        final = o3.Irreps.natural(H, 0)
+        self.multihead_decoders = ModuleList()
+        n = self.num_conv_layers
+        dec = lambda nonlin, irr: MultiheadDecoderBlock(nonlin, irr, self.config_heads, self.head_dims,  # noqa: E731
+                                                         self.head_type, self.num_heads, self.activation_function,
+                                                         self.num_nodes)
+        self.multihead_decoders.append(dec(n == 1, o3.Irreps([(self.num_elements, 0, 1)])))
+        for i in range(n):
+            last = i == n - 1
+            self.graph_convs.append(self._apply_global_attn(self.get_conv(H, H, first_layer=i == 0, last_layer=last)))
+            self.feature_layers.append(nn.Identity())
+            self.multihead_decoders.append(dec(last, final if last else hidden))
+
+    def get_conv(self, input_dim, output_dim, first_layer=False, last_layer=False):
+        hidden_dim = output_dim if input_dim == 1 else input_dim
+        node_feats = o3.Irreps.natural(input_dim, 0 if first_layer else self.node_max_ell)
+        hidden = o3.Irreps.natural(hidden_dim, self.node_max_ell)
+        interaction = o3.Irreps.natural(hidden_dim, self.max_ell)
+        output = o3.Irreps.natural(output_dim, self.node_max_ell)
+        if last_layer:
+            hidden = o3.Irreps.natural(hidden_dim, 0)
+            output = o3.Irreps.natural(output_dim, 0)
+        # under GPS the edge features are the hidden-width relative-PE encoding (reference
+        # MACEStack.py:455-462); size the radial MLP input for it (the reference would not run)
+        n_edge = self.hidden_dim if (self.use_global_attn and self.is_edge_model) else self.num_bessel
+        inter = InteractionBlock(node_feats, self.edge_attrs_irreps, n_edge, interaction, hidden,
+                                 self.avg_num_neighbors)
+        prod = EquivariantProductBasisBlock(self.max_ell, hidden, self.correlation[0], hidden_dim, self.num_elements,
+                                            use_sc=True)
+        sizing = o3.O3Linear(hidden, output)
+        return MACELayer(inter, prod, sizing, output.count(0, 1))
+
+    def _embedding(self, data):
+        ctx = self._base_ctx(data)
+        assert data.pos is not None, "MACE requires node positions (data.pos) to be set."
+        pos = data.pos
+        # centre positions per graph (reference MACEStack.py:411-419)
+        if ctx.graph_si is None:
+            pos = pos - pos.mean(0, keepdim=True)
+        else:
+            pos = pos - seg.gather(seg.segment_mean(pos, ctx.graph_si), ctx.graph_si)
+        vec, dist = edge_vectors_and_lengths(pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
+        node_attrs, elem = process_node_attributes(data.x)
+        ctx.node_attributes, ctx.elem = node_attrs, elem
+        node_feats = self.node_embedding(node_attrs)
+        ea = o3.spherical_harmonics(self.max_ell, vec)
+        if self.use_edge_attr:
+            ea = torch.cat([data.edge_attr, ea], 1)
+        ctx.edge_attributes = ea
+        ctx.edge_features = self.radial_embedding(dist)
+        if self.use_global_attn:
+            x = self.pos_emb(data.pe)
+            if self.input_dim:
+                x = self.node_lin(torch.cat((node_feats, x), 1))
+            if self.is_edge_model:
+                e = self.rel_pos_emb(data.rel_pe)
+                if self.use_edge_attr:
+                    e = self.edge_lin(torch.cat((ctx.edge_features, e), 1))
+                ctx.edge_features = e
+            return x[:, :self.hidden_dim], x[:, self.hidden_dim:], ctx
+        return node_feats[:, :self.hidden_dim], node_feats[:, self.hidden_dim:], ctx
+
+    def forward(self, data):
+        inv, equiv, ctx = self._embedding(data)
+        ids = self._branch_ids(data) if self.num_branches > 1 else [0]
+        outputs = self.multihead_decoders[0](ctx.node_attributes, ctx, ids)
+        for conv, readout in zip(self.graph_convs, self.multihead_decoders[1:]):
+            inv, equiv = self._run_conv(conv, inv, equiv, ctx)
+            out = readout(torch.cat([inv, equiv], 1), ctx, ids)
+            outputs = [a + b for a, b in zip(outputs, out)]
+        return outputs
+
+    def __str__(self):
+        return "MACEStack"

@@ -1,0 +1,386 @@
+"""Minimal O(3)-equivariant toolkit for MACE (replaces the e3nn pieces the reference
+uses: ``o3.SphericalHarmonics``, ``o3.Linear``, ``o3.TensorProduct`` (uvu),
+``nn.FullyConnectedNet``, and MACE's ``SymmetricContraction`` / ``U_matrix_real``;
+reference ``hydragnn/utils/model/mace_utils/*``, ``irreps_tools.py``).
+
+Conventions (self-consistent; e3nn is not installed here, so bit-parity with e3nn's
+basis/sign choices is *unpinned* and equivariance is verified by rotation tests):
+
+* real spherical harmonics, component normalisation (sum_m Y_lm^2 = 2l+1 on the
+  unit sphere), m ordered -l..l, built from polynomials in (x, y, z) (smooth,
+  differentiable to any order for force training);
+* Wigner-D matrices of this basis are fitted numerically (least squares on random
+  points), Wigner-3j tensors are the unit-norm invariant of D1 x D2 x D3 (null space
+  over two generic rotations, sign fixed by the first significant entry);
+* irreps are lists of (mul, l, parity) with parity (-1)^l for everything MACE
+  builds here ("natural" parity), flat layout per irrep block = [mul, 2l+1]
+  (e3nn layout).
+"""
+import itertools
+import math
+from functools import lru_cache
+
+import numpy as np
+import torch
+from torch import nn
+
+
+# ----------------------------------------------------------------------------- irreps
+class Irreps:
+    """Ordered list of (mul, l, p) blocks; flat layout mul-major within a block."""
+
+    def __init__(self, blocks):
+        self.blocks = [(int(m), int(l), int(p)) for m, l, p in blocks if m > 0]
+
+    @staticmethod
+    def natural(mul, lmax, lmin=0):
+        return Irreps([(mul, l, (-1) ** l) for l in range(lmin, lmax + 1)])
+
+    @staticmethod
+    def sh(lmax):
+        return Irreps([(1, l, (-1) ** l) for l in range(lmax + 1)])
+
+    @property
+    def dim(self):
+        return sum(m * (2 * l + 1) for m, l, _ in self.blocks)
+
+    def count(self, l, p):
+        return sum(m for m, ll, pp in self.blocks if ll == l and pp == p)
+
+    @property
+    def num_irreps(self):
+        return sum(m for m, _, _ in self.blocks)
+
+    @property
+    def lmax(self):
+        return max(l for _, l, _ in self.blocks)
+
+    def slices(self):
+        out, o = [], 0
+        for m, l, p in self.blocks:
+            d = m * (2 * l + 1)
+            out.append((o, o + d))
+            o += d
+        return out
+
+    def simplify(self):
+        """Merge consecutive blocks with the same (l, p)."""
+        out = []
+        for m, l, p in self.blocks:
+            if out and out[-1][1] == l and out[-1][2] == p:
+                out[-1] = (out[-1][0] + m, l, p)
+            else:
+                out.append((m, l, p))
+        return Irreps(out)
+
+    def sort(self):
+        """Stable sort by (l, -p-ish) like e3nn (l ascending, even before odd); returns (irreps, perm)."""
+        key = [(l, -p, i) for i, (_, l, p) in enumerate(self.blocks)]
+        order = sorted(range(len(self.blocks)), key=lambda i: key[i])
+        inv = [0] * len(order)
+        for new, old in enumerate(order):
+            inv[old] = new
+        return Irreps([self.blocks[i] for i in order]), inv
+
+    def __iter__(self):
+        return iter(self.blocks)
+
+    def __len__(self):
+        return len(self.blocks)
+
+    def __add__(self, other):
+        return Irreps(self.blocks + other.blocks)
+
+    def __repr__(self):
+        return " + ".join(f"{m}x{l}{'e' if p == 1 else 'o'}" for m, l, p in self.blocks)
+
+
+def create_irreps_string(n, ell):
+    """Reference ``irreps_tools.create_irreps_string``: n x l, parity (-1)^l, l = 0..ell."""
+    return Irreps.natural(n, ell)
+
+
+# ----------------------------------------------------------------------------- spherical harmonics
+def spherical_harmonics(lmax, vec, normalize=True, eps=0.0):
+    """Real SH, component normalisation, [..., (lmax+1)^2] with m = -l..l per l."""
+    if normalize:
+        vec = vec / (torch.linalg.vector_norm(vec, dim=-1, keepdim=True) + eps)
+    x, y, z = vec[..., 0], vec[..., 1], vec[..., 2]
+    A = [torch.ones_like(x)]
+    B = [torch.zeros_like(x)]
+    for m in range(lmax):
+        A.append(x * A[m] - y * B[m])
+        B.append(x * B[m] + y * A[m])
+    # reduced associated Legendre Q[l][m] (P_l^m / (1-z^2)^{m/2}, no Condon-Shortley phase)
+    Q = [[None] * (lmax + 1) for _ in range(lmax + 1)]
+    for m in range(lmax + 1):
+        Q[m][m] = torch.full_like(z, float(np.prod(np.arange(2 * m - 1, 0, -2)) if m > 0 else 1.0))
+        if m + 1 <= lmax:
+            Q[m + 1][m] = (2 * m + 1) * z * Q[m][m]
+        for l in range(m + 2, lmax + 1):
+            Q[l][m] = ((2 * l - 1) * z * Q[l - 1][m] - (l + m - 1) * Q[l - 2][m]) / (l - m)
+    out = []
+    for l in range(lmax + 1):
+        for m in range(-l, l + 1):
+            am = abs(m)
+            c = math.sqrt((2 * l + 1) * math.factorial(l - am) / math.factorial(l + am))
+            if m == 0:
+                out.append(c * Q[l][0])
+            elif m > 0:
+                out.append(c * math.sqrt(2.0) * Q[l][am] * A[am])
+            else:
+                out.append(c * math.sqrt(2.0) * Q[l][am] * B[am])
+    return torch.stack(out, -1)
+
+
+def _rand_rot(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    a, b, c, d = q
+    return np.array([[a * a + b * b - c * c - d * d, 2 * (b * c - a * d), 2 * (b * d + a * c)],
+                     [2 * (b * c + a * d), a * a - b * b + c * c - d * d, 2 * (c * d - a * b)],
+                     [2 * (b * d - a * c), 2 * (c * d + a * b), a * a - b * b - c * c + d * d]])
+
+
+def wigner_D(l, R):
+    """D^l(R) in the real SH basis above: Y_l(R x) = D Y_l(x)."""
+    rng = np.random.default_rng(1234 + l)
+    X = rng.normal(size=(max(64, 8 * (2 * l + 1)), 3))
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Xt = torch.tensor(X, dtype=torch.float64)
+    Rt = torch.tensor(R, dtype=torch.float64)
+    sl = slice(l * l, (l + 1) * (l + 1))
+    Y = spherical_harmonics(l, Xt)[:, sl]
+    YR = spherical_harmonics(l, Xt @ Rt.T)[:, sl]
+    D = torch.linalg.lstsq(Y, YR).solution.T
+    return D.numpy()
+
+
+@lru_cache(maxsize=None)
+def _rotations():
+    rng = np.random.default_rng(7)
+    return [_rand_rot(rng) for _ in range(2)]
+
+
+@lru_cache(maxsize=None)
+def wigner_3j(l1, l2, l3):
+    """Unit-norm invariant tensor [2l1+1, 2l2+1, 2l3+1] (zeros if it does not exist)."""
+    if not (abs(l1 - l2) <= l3 <= l1 + l2):
+        return torch.zeros(2 * l1 + 1, 2 * l2 + 1, 2 * l3 + 1, dtype=torch.float64)
+    rows = []
+    n = (2 * l1 + 1) * (2 * l2 + 1) * (2 * l3 + 1)
+    for R in _rotations():
+        K = np.kron(np.kron(wigner_D(l1, R), wigner_D(l2, R)), wigner_D(l3, R))
+        rows.append(K - np.eye(n))
+    M = np.concatenate(rows, 0)
+    _, s, vt = np.linalg.svd(M)
+    v = vt[-1]
+    assert s[-1] < 1e-6 * max(1.0, s[0]), f"no 3j invariant for ({l1},{l2},{l3})"
+    v = v / np.linalg.norm(v)
+    i = int(np.argmax(np.abs(v) > 1e-6))
+    if v[i] < 0:
+        v = -v
+    return torch.tensor(v.reshape(2 * l1 + 1, 2 * l2 + 1, 2 * l3 + 1), dtype=torch.float64)
+
+
+# ----------------------------------------------------------------------------- layers
+class O3Linear(nn.Module):
+    """e3nn ``o3.Linear`` semantics: per (l, p) channel mixing, N(0,1) weights scaled by
+    1/sqrt(fan_in) in the forward ("element" path normalisation), no bias."""
+
+    def __init__(self, irreps_in, irreps_out):
+        super().__init__()
+        self.irreps_in, self.irreps_out = irreps_in, irreps_out
+        self.paths = []
+        numel = 0
+        for io, (mo, lo, po) in enumerate(irreps_out.blocks):
+            ins = [ii for ii, (mi, li, pi) in enumerate(irreps_in.blocks) if li == lo and pi == po]
+            fan = sum(irreps_in.blocks[ii][0] for ii in ins)
+            for ii in ins:
+                mi = irreps_in.blocks[ii][0]
+                self.paths.append((ii, io, numel, mi, mo, 1.0 / math.sqrt(fan)))
+                numel += mi * mo
+        self.weight = nn.Parameter(torch.randn(numel))
+        self.sl_in, self.sl_out = irreps_in.slices(), irreps_out.slices()
+
+    def forward(self, x):
+        N = x.shape[0]
+        outs = [None] * len(self.irreps_out.blocks)
+        for ii, io, off, mi, mo, a in self.paths:
+            l = self.irreps_in.blocks[ii][1]
+            d = 2 * l + 1
+            xi = x[:, self.sl_in[ii][0]:self.sl_in[ii][1]].reshape(N, mi, d)
+            W = self.weight[off:off + mi * mo].view(mi, mo) * a
+            y = torch.einsum("nud,uv->nvd", xi, W)
+            outs[io] = y if outs[io] is None else outs[io] + y
+        res = []
+        for io, (mo, lo, _) in enumerate(self.irreps_out.blocks):
+            o = outs[io]
+            if o is None:
+                o = x.new_zeros(N, mo, 2 * lo + 1)
+            res.append(o.reshape(N, -1))
+        return torch.cat(res, -1)
+
+
+def _silu_2mom():
+    z = np.linspace(-12, 12, 200001)
+    pdf = np.exp(-z * z / 2) / math.sqrt(2 * math.pi)
+    s = z / (1 + np.exp(-z))
+    return 1.0 / math.sqrt(np.trapz(s * s * pdf, z))
+
+
+_SILU_C = _silu_2mom()
+
+
+class FullyConnectedNet(nn.Module):
+    """e3nn ``nn.FullyConnectedNet`` with silu: no biases, N(0,1) weights, 1/sqrt(fan_in),
+    second-moment-normalised activation between layers."""
+
+    def __init__(self, dims):
+        super().__init__()
+        self.dims = list(dims)
+        self.weights = nn.ParameterList([nn.Parameter(torch.randn(a, b)) for a, b in zip(dims[:-1], dims[1:])])
+
+    def forward(self, x):
+        n = len(self.weights)
+        for i, W in enumerate(self.weights):
+            x = x @ W / math.sqrt(W.shape[0])
+            if i < n - 1:
+                x = torch.nn.functional.silu(x) * _SILU_C
+        return x
+
+
+def tp_uvu_instructions(irreps1, irreps2, target):
+    """Reference ``tp_out_irreps_with_instructions``: all (l1 x l2 -> l3) with l3 (and
+    parity) in target; output blocks sorted; instructions (i1, i2, i_out)."""
+    out, ins = [], []
+    tgt = {(l, p) for _, l, p in target.blocks}
+    for i, (m1, l1, p1) in enumerate(irreps1.blocks):
+        for j, (_, l2, p2) in enumerate(irreps2.blocks):
+            for l3 in range(abs(l1 - l2), l1 + l2 + 1):
+                p3 = p1 * p2
+                if (l3, p3) in tgt:
+                    ins.append((i, j, len(out)))
+                    out.append((m1, l3, p3))
+    irr = Irreps(out)
+    srt, perm = irr.sort()
+    ins = sorted([(a, b, perm[k]) for a, b, k in ins], key=lambda t: t[2])
+    return srt, ins
+
+
+class TensorProductUVU(nn.Module):
+    """Channel-wise ("uvu") tensor product with per-edge external weights:
+    out[e, u, m3] (block k) = sqrt(2 l3 + 1) sum_v w[e, k, u, v] sum_{m1 m2} C[m1 m2 m3] x1[e, u, m1] x2[e, v, m2]."""
+
+    def __init__(self, irreps1, irreps2, irreps_out, instructions):
+        super().__init__()
+        self.irreps1, self.irreps2, self.irreps_out = irreps1, irreps2, irreps_out
+        self.ins = instructions
+        self.sl1, self.sl2 = irreps1.slices(), irreps2.slices()
+        self.weight_numel = 0
+        self.woff = []
+        for i, j, k in instructions:
+            m1, l1, _ = irreps1.blocks[i]
+            m2, l2, _ = irreps2.blocks[j]
+            l3 = irreps_out.blocks[k][1]
+            self.woff.append((self.weight_numel, m1, m2))
+            self.weight_numel += m1 * m2
+            self.register_buffer(f"cg_{l1}_{l2}_{l3}", wigner_3j(l1, l2, l3).float() * math.sqrt(2 * l3 + 1),
+                                 persistent=False)
+
+    def forward(self, x1, x2, w):
+        E = x1.shape[0]
+        outs = [None] * len(self.irreps_out.blocks)
+        for (i, j, k), (off, m1, m2) in zip(self.ins, self.woff):
+            l1, l2, l3 = self.irreps1.blocks[i][1], self.irreps2.blocks[j][1], self.irreps_out.blocks[k][1]
+            a = x1[:, self.sl1[i][0]:self.sl1[i][1]].reshape(E, m1, 2 * l1 + 1)
+            b = x2[:, self.sl2[j][0]:self.sl2[j][1]].reshape(E, m2, 2 * l2 + 1)
+            C = getattr(self, f"cg_{l1}_{l2}_{l3}")
+            ww = w[:, off:off + m1 * m2].view(E, m1, m2)
+            bv = torch.einsum("evj,euv->euj", b, ww) if m2 > 1 else b * ww  # [E, u, 2l2+1]
+            y = torch.einsum("eui,euj,ijk->euk", a, bv, C)
+            outs[k] = y.reshape(E, -1)
+        return torch.cat(outs, -1)
+
+
+# ----------------------------------------------------------------------------- symmetric contraction
+@lru_cache(maxsize=None)
+def u_matrix(lmax_in, L, nu):
+    """Basis of symmetric equivariant maps Sym^nu(V) -> V_L, V = (+)_{l<=lmax_in} V_l with
+    parity (-1)^l, output parity (-1)^L.  Returns [2L+1, d, ..., d (nu), K] (float64)."""
+    d = (lmax_in + 1) ** 2
+    # coupling paths: (l, parity, tensor [2l+1, d^k])
+    paths = []
+    for l in range(lmax_in + 1):
+        T = torch.zeros(2 * l + 1, d, dtype=torch.float64)
+        T[:, l * l:(l + 1) * (l + 1)] = torch.eye(2 * l + 1, dtype=torch.float64)
+        paths.append((l, (-1) ** l, T))
+    for step in range(nu - 1):
+        remaining = nu - 2 - step  # factors still to couple after this one
+        new = []
+        for lp, pp, T in paths:
+            for l in range(lmax_in + 1):
+                for lo in range(abs(lp - l), lp + l + 1):
+                    if abs(lo - L) > remaining * lmax_in:  # can no longer reach L
+                        continue
+                    C = wigner_3j(lp, l, lo) * math.sqrt(2 * lo + 1)
+                    E = torch.zeros(2 * l + 1, d, dtype=torch.float64)
+                    E[:, l * l:(l + 1) * (l + 1)] = torch.eye(2 * l + 1, dtype=torch.float64)
+                    # T'[mo, prev..., i] = sum_{mp, m} C[mp, m, mo] T[mp, prev] E[m, i]
+                    Tn = torch.einsum("abo,ap,bi->opi", C, T, E).reshape(2 * lo + 1, -1)
+                    new.append((lo, pp * (-1) ** l, Tn))
+        paths = new
+    sel = [T for l, p, T in paths if l == L and p == (-1) ** L]
+    if not sel:
+        return torch.zeros((2 * L + 1,) + (d,) * nu + (0,), dtype=torch.float64)
+    X = torch.stack([T.reshape((2 * L + 1,) + (d,) * nu) for T in sel], 0)  # [P, M, d..]
+    perms = list(itertools.permutations(range(nu)))
+    Xs = sum(X.permute(0, 1, *[2 + q for q in pm]) for pm in perms) / len(perms)
+    Mx = Xs.reshape(Xs.shape[0], -1)
+    U, s, Vt = torch.linalg.svd(Mx, full_matrices=False)
+    keep = s > 1e-8 * max(1.0, float(s[0]) if s.numel() else 1.0)
+    B = Vt[keep]  # [K, M*d^nu] orthonormal rows
+    K = B.shape[0]
+    return B.T.reshape((2 * L + 1,) + (d,) * nu + (K,))
+
+
+class Contraction(nn.Module):
+    def __init__(self, lmax_in, L, correlation, num_features, num_elements):
+        super().__init__()
+        self.L, self.correlation = L, correlation
+        self.d = (lmax_in + 1) ** 2
+        self.weights = nn.ParameterList()
+        for nu in range(1, correlation + 1):
+            U = u_matrix(lmax_in, L, nu).float()
+            self.register_buffer(f"U_{nu}", U, persistent=False)
+            K = U.shape[-1]
+            self.weights.append(nn.Parameter(torch.randn(num_elements, K, num_features) / max(K, 1)))
+
+    def forward(self, x, elem):
+        """x [N, H, d]; elem [N] element index -> [N, H, 2L+1]."""
+        N, H, d = x.shape
+        out = None
+        for nu in range(self.correlation, 0, -1):
+            U = getattr(self, f"U_{nu}")
+            K = U.shape[-1]
+            W = self.weights[nu - 1][elem]  # [N, K, H]
+            P = U.reshape(-1, K)  # [M d^nu, K]
+            c = torch.einsum("pk,nkc->ncp", P, W) if K > 0 else x.new_zeros(N, H, P.shape[0])
+            out = c if out is None else out + c
+            out = torch.einsum("ncpi,nci->ncp", out.view(N, H, -1, d), x)
+        return out  # [N, H, 2L+1]
+
+
+class SymmetricContraction(nn.Module):
+    """MACE product basis: per output irrep L of ``irreps_out``, sum_{nu<=correlation}
+    sum_k W_{nu,k}(element) U_{nu,k} . x^{(x) nu}, channel-wise."""
+
+    def __init__(self, lmax_in, irreps_out, correlation, num_features, num_elements):
+        super().__init__()
+        self.irreps_out = irreps_out
+        self.contractions = nn.ModuleList([Contraction(lmax_in, l, correlation, num_features, num_elements)
+                                           for _, l, _ in irreps_out.blocks])
+
+    def forward(self, x, elem):
+        N = x.shape[0]
+        return torch.cat([c(x, elem).reshape(N, -1) for c in self.contractions], -1)
