@@ -35,6 +35,9 @@ from .layers import BatchNorm, Ctx, Linear
 
 class Base(nn.Module):
     is_edge_model = False
+    # False for stacks whose forward has data-dependent shapes (in-forward radius graphs,
+    # triplet lists): the training engine then runs them eagerly instead of in a hipGraph
+    capturable = True
 
     def __init__(self, input_args="", conv_args="", input_dim=1, hidden_dim=8, output_dim=(1,), pe_dim=0,
                  global_attn_engine=None, global_attn_type=None, global_attn_heads=0, output_type=("graph",),

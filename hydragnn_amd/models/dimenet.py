@@ -232,6 +232,7 @@ class DimeNetLayer(nn.Module):
 
 class DIMEStack(Base):
     is_edge_model = True
+    capturable = False  # triplet count is data dependent
 
     def __init__(self, input_args, conv_args, basis_emb_size, envelope_exponent, int_emb_size, out_emb_size,
                  num_after_skip, num_before_skip, num_radial, num_spherical, edge_dim, radius, *args,

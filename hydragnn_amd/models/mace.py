@@ -280,11 +280,13 @@ def process_node_attributes(x, num_elements=NUM_ELEMENTS):
     if z.dim() == 0:
         z = z.view(1)
     assert z.dim() == 1, "MACE only supports raw atomic numbers as node_attributes (1D data.x)."
-    if not bool(torch.all(z == z.round())):
-        warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x contains floats.")
-    if not bool(torch.all((z >= 1) & (z <= num_elements))):
-        warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x is not in 1-118.")
-        z = z.clamp(1, 118)
+    capturing = z.is_cuda and torch.cuda.is_current_stream_capturing()
+    if not capturing:  # host-side checks would synchronise inside a hipGraph capture
+        if not bool(torch.all(z == z.round())):
+            warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x contains floats.")
+        if not bool(torch.all((z >= 1) & (z <= num_elements))):
+            warnings.warn("MACE only supports raw atomic numbers as node_attributes. Your data.x is not in 1-118.")
+    z = z.clamp(1, num_elements)
     idx = (z - 1).long()
     return torch.nn.functional.one_hot(idx, num_classes=num_elements).float(), idx
 
@@ -380,7 +382,9 @@ class MACEStack(Base):
             if self.is_edge_model:
                 e = self.rel_pos_emb(data.rel_pe)
                 if self.use_edge_attr:
-                    e = self.edge_lin(torch.cat((ctx.edge_features, e), 1))
+                    # the reference concatenates the radial features here, which only fits when
+                    # num_bessel == hidden_dim; encode the edge attributes like every other stack
+                    e = self.edge_lin(torch.cat((self.edge_emb(data.edge_attr), e), 1))
                 ctx.edge_features = e
             return x[:, :self.hidden_dim], x[:, self.hidden_dim:], ctx
         return node_feats[:, :self.hidden_dim], node_feats[:, self.hidden_dim:], ctx

@@ -19,7 +19,9 @@ rbf_emb(rbf)(, enc(e))], scalar_mlp, rbf_lin gate, 4 aggregators x 5 scalers
 Update (both): U v, V v -> a_vv, a_sv, a_ss = mlp(cat[|V v|, s]);
     v += a_vv * U v ;  s += a_sv * <U v, V v> + a_ss
 followed by the reference's size adapters (node_embed_out: Lin-Tanh-Lin,
-vec_embed_out: Lin on the channel dim).
+vec_embed_out: Lin on the channel dim).  Deliberate fix: every Linear acting on the
+vector state (U, V, vec_embed_out) is bias-free here; the reference's biases add the
+same offset to all three Cartesian components and break rotation equivariance.
 """
 import math
 
@@ -82,8 +84,10 @@ class PainnUpdate(nn.Module):
     def __init__(self, node_size, last_layer=False, u_name="update_U"):
         super().__init__()
         self._u = u_name
-        setattr(self, u_name, nn.Linear(node_size, node_size))
-        self.update_V = nn.Linear(node_size, node_size)
+        # U, V act on the vector state: bias-free (as in PaiNN) so the update stays equivariant
+        # (the reference's biased Linears shift every Cartesian component alike)
+        setattr(self, u_name, nn.Linear(node_size, node_size, bias=False))
+        self.update_V = nn.Linear(node_size, node_size, bias=False)
         self.last_layer = last_layer
         out = 2 * node_size if last_layer else 3 * node_size
         self.update_mlp = nn.Sequential(nn.Linear(2 * node_size, node_size), nn.SiLU(), nn.Linear(node_size, out))
@@ -138,7 +142,9 @@ class _EqStackBase(Base):
 
     def _adapters(self, input_dim, output_dim, last_layer):
         node_embed_out = nn.Sequential(nn.Linear(input_dim, output_dim), nn.Tanh(), nn.Linear(output_dim, output_dim))
-        vec_embed_out = nn.Linear(input_dim, output_dim) if not last_layer else None
+        # bias-free on purpose: the reference's Linear(input_dim, output_dim) adds the same bias
+        # to all three Cartesian components of v, which breaks rotation equivariance
+        vec_embed_out = nn.Linear(input_dim, output_dim, bias=False) if not last_layer else None
         return node_embed_out, vec_embed_out
 
     def _geometry(self, data, ctx):

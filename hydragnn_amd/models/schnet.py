@@ -72,6 +72,10 @@ class CFConv(nn.Module):
 class SCFStack(Base):
     is_edge_model = True
 
+    @property
+    def capturable(self):  # the in-forward radius graph has a data-dependent edge count
+        return bool(self.use_edge_attr or (self.use_global_attn and self.is_edge_model))
+
     def __init__(self, input_args, conv_args, num_filters, edge_dim, num_gaussians, radius, *args,
                  max_neighbours=None, **kwargs):
         self.radius = radius

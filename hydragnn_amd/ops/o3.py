@@ -226,7 +226,7 @@ def _silu_2mom():
     z = np.linspace(-12, 12, 200001)
     pdf = np.exp(-z * z / 2) / math.sqrt(2 * math.pi)
     s = z / (1 + np.exp(-z))
-    return 1.0 / math.sqrt(np.trapz(s * s * pdf, z))
+    return 1.0 / math.sqrt(np.trapezoid(s * s * pdf, z))
 
 
 _SILU_C = _silu_2mom()

@@ -1,12 +1,11 @@
 """End-to-end accuracy tests: run_training + run_prediction on the deterministic CI
-dataset with the reference thresholds (reference ``tests/test_graphs.py``).
+dataset with the reference thresholds (reference ``tests/test_graphs.py:200-320``,
+same model matrix).
 
 CPU (driver's ``-m "not gpu"`` run): a fast representative subset.
-GPU (``-m gpu``): the full model matrix through the MI355X path (HBM-resident data,
-hipGraph-captured steps, HIP kernels).
+GPU (``-m gpu``): the full reference matrix through the MI355X path (HBM-resident
+data, hipGraph-captured steps where shapes allow, HIP kernels).
 """
-import os
-
 import pytest
 
 from graph_train_util import unittest_train_model
@@ -19,7 +18,16 @@ CPU_CASES = [
     ("PNAPlus", "GPS", "multihead", "ci", False),
     ("PNA", "", "", "ci_multihead", False),
     ("PNA", "", "", "ci", True),
+    ("EGNN", "", "", "ci", False),
+    ("CGCNN", "", "", "ci", False),
 ]
+
+ALL_MODELS = ["SAGE", "GIN", "GAT", "MFC", "PNA", "PNAPlus", "CGCNN", "SchNet", "DimeNet", "EGNN", "PNAEq", "PAINN",
+              "MACE"]
+EDGE_MODELS = ["GAT", "PNA", "PNAPlus", "CGCNN", "SchNet", "DimeNet", "EGNN", "PNAEq", "PAINN"]
+EQUIVARIANT = ["EGNN", "SchNet", "PNAEq", "PAINN", "MACE"]
+VECTOR_OUT = ["GAT", "PNA", "PNAPlus", "SchNet", "DimeNet", "EGNN", "PNAEq"]
+CONV_HEAD = ["SAGE", "GIN", "GAT", "MFC", "PNA", "PNAPlus", "SchNet", "DimeNet", "EGNN", "PNAEq", "PAINN"]
 
 
 @pytest.fixture(scope="module")
@@ -33,23 +41,38 @@ def test_train_cpu(mpnn_type, engine, attn, ci_input, lengths, workdir, monkeypa
     unittest_train_model(mpnn_type, engine, attn, ci_input, lengths, workdir)
 
 
-GPU_MODELS = ["SAGE", "GIN", "MFC", "PNA", "PNAPlus"]
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("mpnn_type", GPU_MODELS)
+@pytest.mark.parametrize("mpnn_type", ALL_MODELS)
 @pytest.mark.parametrize("ci_input", ["ci", "ci_multihead"])
 def test_train_gpu(mpnn_type, ci_input, workdir):
     unittest_train_model(mpnn_type, "", "", ci_input, False, workdir)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mpnn_type", ["PNA", "PNAPlus"])
-def test_train_gpu_gps(mpnn_type, workdir):
-    unittest_train_model(mpnn_type, "GPS", "multihead", "ci", False, workdir)
+@pytest.mark.parametrize("mpnn_type", EDGE_MODELS + ["MACE"])
+def test_train_gpu_lengths(mpnn_type, workdir):
+    unittest_train_model(mpnn_type, "", "", "ci", True, workdir)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mpnn_type", ["PNA", "PNAPlus"])
-def test_train_gpu_lengths(mpnn_type, workdir):
-    unittest_train_model(mpnn_type, "", "", "ci", True, workdir)
+@pytest.mark.parametrize("mpnn_type", EDGE_MODELS)
+def test_train_gpu_lengths_gps(mpnn_type, workdir):
+    unittest_train_model(mpnn_type, "GPS", "multihead", "ci", True, workdir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mpnn_type", EQUIVARIANT)
+def test_train_gpu_equivariant(mpnn_type, workdir):
+    unittest_train_model(mpnn_type, "", "", "ci_equivariant", False, workdir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mpnn_type", VECTOR_OUT)
+def test_train_gpu_vectoroutput(mpnn_type, workdir):
+    unittest_train_model(mpnn_type, "", "", "ci_vectoroutput", True, workdir)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mpnn_type", CONV_HEAD)
+def test_train_gpu_conv_head(mpnn_type, workdir):
+    unittest_train_model(mpnn_type, "", "", "ci_conv_head", False, workdir)

@@ -1,0 +1,121 @@
+"""CPU tests of the model families: every stack builds and runs forward/backward
+(with and without GPS), and the geometric ones are invariant to rotations and
+translations of the input positions (reference semantics: invariant scalar heads).
+Reference models: ``hydragnn/models/*Stack.py``; the e3nn-free O(3) toolkit of MACE
+is checked for basis orthogonality / equivariance directly."""
+import numpy as np
+import pytest
+import torch
+
+from hydragnn_amd.data.graph import collate
+from hydragnn_amd.data.synthetic import degree_histogram, oc20_like
+from hydragnn_amd.models.create import create_model
+from hydragnn_amd.ops import o3
+
+HEADS = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 2, "dim_sharedlayers": 8,
+                                                          "num_headlayers": 2, "dim_headlayers": [8, 8]}}],
+         "node": [{"type": "branch-0", "architecture": {"num_headlayers": 2, "dim_headlayers": [8, 8],
+                                                         "type": "mlp"}}]}
+
+ALL = ["GIN", "SAGE", "MFC", "PNA", "PNAPlus", "GAT", "CGCNN", "SchNet", "DimeNet", "EGNN", "PAINN", "PNAEq", "MACE"]
+GEOMETRIC = ["PNAPlus", "SchNet", "DimeNet", "EGNN", "PAINN", "PNAEq", "MACE"]
+
+
+def _samples(n=4, atomic=False):
+    s = oc20_like(n, seed=3, radius=5.0, max_neighbours=8, pe_dim=4, min_atoms=6, max_atoms=14)
+    for g in s:
+        g.edge_attr = torch.ones(g.edge_index.shape[1], 1)
+        if atomic:
+            g.x = torch.randint(1, 9, (g.x.shape[0], 1)).float()
+    return s
+
+
+def _model(mt, samples, gps=False, eq=False):
+    deg = degree_histogram(samples, max_degree=10)
+    in_dim = samples[0].x.shape[1]
+    hidden = in_dim if (mt == "CGCNN" and not gps) else 12
+    torch.manual_seed(0)
+    return create_model(mt, in_dim, hidden, [1, 1], 4, "GPS" if gps else "", "multihead", 2, ["graph", "node"], HEADS,
+                        "relu", "mse", [1.0, 1.0], 2, pna_deg=deg, edge_dim=1 if gps else None, envelope_exponent=5,
+                        num_radial=5, radius=5.0, max_neighbours=8, num_gaussians=8, num_filters=12,
+                        basis_emb_size=4, int_emb_size=8, out_emb_size=8, num_after_skip=1, num_before_skip=1,
+                        num_spherical=3, equivariance=eq, use_gpu=False, max_ell=2, node_max_ell=1,
+                        avg_num_neighbors=5.0, correlation=2, dropout=0.0)
+
+
+@pytest.mark.parametrize("mt", ALL)
+@pytest.mark.parametrize("gps", [False, True])
+def test_forward_backward(mt, gps):
+    samples = _samples(atomic=(mt == "MACE"))
+    m = _model(mt, samples, gps=gps)
+    m.train()
+    b = collate(samples)
+    pred = m(b)
+    assert pred[0].shape == (len(samples), 1) and pred[1].shape == (b.num_nodes, 1)
+    sum(p.pow(2).mean() for p in pred).backward()
+    n_grad = sum(1 for p in m.parameters() if p.grad is not None)
+    assert n_grad > 0
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def _rot(seed):
+    return torch.tensor(o3._rand_rot(np.random.default_rng(seed)), dtype=torch.float32)
+
+
+@pytest.mark.parametrize("mt", GEOMETRIC)
+@pytest.mark.parametrize("eq", [False, True])
+def test_rotation_translation_invariance(mt, eq):
+    samples = _samples(atomic=(mt == "MACE"))
+    m = _model(mt, samples, eq=eq)
+    m.eval()
+    b1 = collate([s.clone() for s in samples])
+    b2 = collate([s.clone() for s in samples])
+    b2.pos = b2.pos @ _rot(11).T + torch.tensor([1.5, -2.0, 0.25])
+    with torch.no_grad():
+        p1, p2 = m(b1), m(b2)
+    for a, c in zip(p1, p2):
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("mt", ["GIN", "PNA", "EGNN", "MACE"])
+def test_graph_permutation_invariance(mt):
+    samples = _samples(atomic=(mt == "MACE"))
+    m = _model(mt, samples)
+    m.eval()
+    with torch.no_grad():
+        p1 = m(collate(samples))
+        p2 = m(collate(samples[::-1]))
+    torch.testing.assert_close(p1[0], p2[0].flip(0), rtol=1e-4, atol=1e-5)
+
+
+def test_o3_basis():
+    R = torch.tensor(o3._rand_rot(np.random.default_rng(3)), dtype=torch.float64)
+    v = torch.randn(20, 3, dtype=torch.float64)
+    Y, YR = o3.spherical_harmonics(3, v), o3.spherical_harmonics(3, v @ R.T)
+    for l in range(4):
+        sl = slice(l * l, (l + 1) ** 2)
+        assert torch.allclose((Y[:, sl] ** 2).sum(-1), torch.full((20,), 2.0 * l + 1, dtype=torch.float64))
+        D = torch.tensor(o3.wigner_D(l, R.numpy()))
+        assert torch.allclose(YR[:, sl], Y[:, sl] @ D.T, atol=1e-10)
+        assert torch.allclose(D @ D.T, torch.eye(2 * l + 1, dtype=torch.float64), atol=1e-10)
+    # 3j invariance
+    C = o3.wigner_3j(1, 2, 2)
+    D1, D2 = [torch.tensor(o3.wigner_D(l, R.numpy())) for l in (1, 2)]
+    CR = torch.einsum("ai,bj,ck,ijk->abc", D1, D2, D2, C)
+    assert torch.allclose(CR, C, atol=1e-9) and abs(float(C.norm()) - 1.0) < 1e-12
+
+
+def test_symmetric_contraction_equivariance():
+    torch.manual_seed(0)
+    H, lmax = 3, 2
+    sc = o3.SymmetricContraction(lmax, o3.Irreps.natural(H, 1), 3, H, 5).double()
+    R = torch.tensor(o3._rand_rot(np.random.default_rng(5)), dtype=torch.float64)
+    Ds = [torch.tensor(o3.wigner_D(l, R.numpy())) for l in range(lmax + 1)]
+    Dfull = torch.block_diag(*Ds)
+    x = torch.randn(7, H, (lmax + 1) ** 2, dtype=torch.float64)
+    elem = torch.randint(0, 5, (7,))
+    y1 = sc(x @ Dfull.T, elem)
+    y0 = sc(x, elem)
+    # output blocks: H x 0e then H x 1o (flat layout [H, 2l+1] per block)
+    torch.testing.assert_close(y1[:, :H], y0[:, :H])
+    torch.testing.assert_close(y1[:, H:].view(7, H, 3), y0[:, H:].view(7, H, 3) @ Ds[1].T)
