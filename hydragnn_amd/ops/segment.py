@@ -71,6 +71,13 @@ def _use_native(t):
     return t.is_cuda
 
 
+def _width(tail):
+    w = 1
+    for d in tail:
+        w *= int(d)
+    return w
+
+
 # ------------------------------------------------------------------ CPU reference
 
 def _cpu_segment_sum(x, si):
@@ -107,7 +114,7 @@ class _Gather(torch.autograd.Function):
         ctx.n = x.shape[0]
         if _use_native(x) and x.dtype == torch.float32:
             tail = x.shape[1:]
-            out = _native.ops().gather_rows(x.reshape(x.shape[0], -1), si.index)
+            out = _native.ops().gather_rows(x.reshape(x.shape[0], _width(tail)), si.index)
             return out.view((out.shape[0],) + tuple(tail))
         return x.index_select(0, si.index64.to(x.device))
 
@@ -122,7 +129,8 @@ class _SegSum(torch.autograd.Function):
         ctx.si = si
         if _use_native(x) and x.dtype == torch.float32:
             tail = x.shape[1:]
-            out = _native.ops().seg_sum(x.reshape(x.shape[0], -1), si.rowptr, si.perm, si.num_segments, False)
+            out = _native.ops().seg_sum(x.reshape(x.shape[0], _width(tail)), si.rowptr, si.perm, si.num_segments,
+                                        False)
             return out.view((si.num_segments,) + tuple(tail))
         return _cpu_segment_sum(x, si)
 
