@@ -101,6 +101,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    mark = os.environ.get("HYDRA_PROFILE_MARK") == "1"
+    if mark:  # a distinctive spin kernel brackets the timed steps in rocprof traces
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss, _ = step(store, next_indices())
@@ -109,6 +113,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if mark:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

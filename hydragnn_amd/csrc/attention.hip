@@ -12,7 +12,8 @@
 // running max/sum and the output accumulator in registers (one query row per
 // lane), stages K/V tiles through LDS (broadcast reads, conflict-free), and
 // splits the key range over the 4 waves of a workgroup (merged through LDS at
-// the end) so that N/64 x H workgroups x 4 waves keep all 256 CUs busy.
+// the end) and over S workgroups (merged by a combine pass), so that
+// N/64 x H x S workgroups x 4 waves keep all 256 CUs busy.
 // Never materialises the N x N score matrix; backward recomputes P from the
 // saved log-sum-exp (two atomic-free passes: dQ by query rows, dK/dV by key
 // rows).
@@ -38,19 +39,37 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 
+// Work decomposition (gfx950, 256 CUs): grid = (query blocks of 64, heads, key
+// splits S).  Each workgroup's 4 waves share one 64-query block and stripe the
+// keys of split s (KT-key tiles staged in LDS, broadcast reads); their online-
+// softmax states are merged through LDS and written as a partial (m, l, acc)
+// per (split, head, query).  A combine pass merges the S partials in a fixed
+// order (deterministic).  S is chosen on the host so that the launch has
+// >= ~6 workgroups per CU: the GPS batch-scope sequence (N ~ 2.3k tokens, 8
+// heads) has only 40 x 8 = 320 query blocks, which left the chip at ~1.25
+// waves per SIMD and latency-bound (rocprof: 84 us fwd) before the split.
+//
 // Q/K/V rows: element (n, h, d) at ptr[n * ld + h * D + d].  O: [N, H*D].  LSE: [H, N] (natural log).
+// part: [S][H][N][D + 2]  (m in log2 units, l, acc[D])
+__device__ __forceinline__ void split_range(int ub, int ue, int S, int s, int KT, int& cb, int& ce) {
+  const int L = max(ue - ub, 0);
+  const int C = ((L + S - 1) / S + KT - 1) / KT * KT;
+  cb = ub + s * C;
+  ce = min(ue, cb + C);
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__ Q, const float* __restrict__ K,
                                                        const float* __restrict__ V, int ld,
-                                                       float* __restrict__ O, float* __restrict__ LSE,
+                                                       float* __restrict__ part,
                                                        const int* __restrict__ seg_id,
-                                                       const int* __restrict__ seg_ptr, int N, int H,
+                                                       const int* __restrict__ seg_ptr, int N, int H, int S,
                                                        float scale) {
   constexpr int KT = AttnCfg<D>::KT;
   __shared__ float Ks[4][KT][D];
   __shared__ float Vs[4][KT][D];
   __shared__ float Mrg[64][D + 2];
-  const int h = blockIdx.y;
+  const int h = blockIdx.y, sp = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = blockIdx.x * 64 + lane;
   const bool qv = qi < N;
@@ -60,7 +79,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
     kb = seg_ptr[s];
     ke = seg_ptr[s + 1];
   }
-  const int ub = wave_min_i(kb), ue = wave_max_i(ke);
+  int cb, ce;
+  split_range(wave_min_i(kb), wave_max_i(ke), S, sp, KT, cb, ce);
   float q[D], acc[D];
   const float qs = scale * kLog2e;  // scores in log2 domain
 #pragma unroll
@@ -69,16 +89,16 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
     acc[d] = 0.f;
   }
   float m = -INFINITY, l = 0.f;
-  for (int base = ub; base < ue; base += 4 * KT) {
+  for (int base = cb; base < ce; base += 4 * KT) {
     const int t = base + w * KT;
     for (int idx = lane; idx < KT * D; idx += 64) {
       const int j = t + idx / D, d = idx % D;
-      const bool ok = j < ue;
+      const bool ok = j < ce;
       Ks[w][idx / D][d] = ok ? K[(int64_t)j * ld + h * D + d] : 0.f;
       Vs[w][idx / D][d] = ok ? V[(int64_t)j * ld + h * D + d] : 0.f;
     }
     __syncthreads();
-    if (t < ue) {
+    if (t < ce) {
       float s[KT];
       float mt = -INFINITY;
 #pragma unroll
@@ -87,7 +107,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
 #pragma unroll
         for (int d = 0; d < D; ++d) a = fmaf(q[d], Ks[w][jj][d], a);
         const int j = t + jj;
-        s[jj] = (j >= kb && j < ke) ? a : -INFINITY;
+        s[jj] = (j >= kb && j < ke && j < ce) ? a : -INFINITY;
         mt = fmaxf(mt, s[jj]);
       }
       if (mt > -INFINITY) {
@@ -127,14 +147,45 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
 #pragma unroll
         for (int d = 0; d < D; ++d) Mrg[lane][2 + d] = acc[d];
       } else if (qv) {
-        const float inv = l > 0.f ? 1.f / l : 0.f;
+        float* P = part + (((int64_t)sp * H + h) * N + qi) * (D + 2);
+        P[0] = m;
+        P[1] = l;
 #pragma unroll
-        for (int d = 0; d < D; ++d) O[(int64_t)qi * (H * D) + h * D + d] = acc[d] * inv;
-        LSE[(int64_t)h * N + qi] = l > 0.f ? (m + log2f(l)) / kLog2e : -INFINITY;
+        for (int d = 0; d < D; ++d) P[2 + d] = acc[d];
       }
     }
     __syncthreads();
   }
+}
+
+// Merge the S split partials of every (head, query) in a fixed order -> O, LSE.
+template <int D>
+__global__ void __launch_bounds__(256) attn_fwd_combine_kernel(const float* __restrict__ part,
+                                                               float* __restrict__ O, float* __restrict__ LSE,
+                                                               int N, int H, int S) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * H) return;
+  const int h = (int)(t / N), qi = (int)(t % N);
+  const int64_t sstride = (int64_t)H * N * (D + 2);
+  const float* P = part + ((int64_t)h * N + qi) * (D + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < S; ++s) M = fmaxf(M, P[s * sstride]);
+  float l = 0.f, acc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) acc[d] = 0.f;
+  if (M > -INFINITY) {
+    for (int s = 0; s < S; ++s) {
+      const float* p = P + s * sstride;
+      const float f = exp2f(p[0] - M);  // p[0] = -inf -> 0
+      l = fmaf(p[1], f, l);
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[d] = fmaf(p[2 + d], f, acc[d]);
+    }
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) O[(int64_t)qi * (H * D) + h * D + d] = acc[d] * inv;
+  LSE[(int64_t)h * N + qi] = l > 0.f ? (M + log2f(l)) / kLog2e : -INFINITY;
 }
 
 // delta[h, i] = sum_d dO[i,h,d] * O[i,h,d]
@@ -148,18 +199,19 @@ __global__ void attn_delta_kernel(const float* __restrict__ dO, const float* __r
   delta[(int64_t)h * N + i] = a;
 }
 
-// dQ: one query row per lane, key stripes over 4 waves (same structure as forward).
+// dQ: one query row per lane, key stripes over 4 waves, key splits over blockIdx.z.
+// Output rows (already scaled) at dQ + z * split_stride + i * lddq + h * D.
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
     const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
-    float* __restrict__ dQ, int lddq, const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int N,
-    int H, float scale) {
+    float* __restrict__ dQ, int lddq, int64_t split_stride, const int* __restrict__ seg_id,
+    const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
   constexpr int KT = AttnCfg<D>::KT;
   __shared__ float Ks[4][KT][D];
   __shared__ float Vs[4][KT][D];
   __shared__ float Mrg[64][D];
-  const int h = blockIdx.y;
+  const int h = blockIdx.y, sp = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = blockIdx.x * 64 + lane;
   const bool qv = qi < N;
@@ -169,7 +221,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
     kb = seg_ptr[s];
     ke = seg_ptr[s + 1];
   }
-  const int ub = wave_min_i(kb), ue = wave_max_i(ke);
+  int cb, ce;
+  split_range(wave_min_i(kb), wave_max_i(ke), S, sp, KT, cb, ce);
   float q[D], go[D], dq[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -179,20 +232,20 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
   }
   const float lse = qv ? LSE[(int64_t)h * N + qi] : 0.f;
   const float dl = qv ? delta[(int64_t)h * N + qi] : 0.f;
-  for (int base = ub; base < ue; base += 4 * KT) {
+  for (int base = cb; base < ce; base += 4 * KT) {
     const int t = base + w * KT;
     for (int idx = lane; idx < KT * D; idx += 64) {
       const int j = t + idx / D, d = idx % D;
-      const bool ok = j < ue;
+      const bool ok = j < ce;
       Ks[w][idx / D][d] = ok ? K[(int64_t)j * ld + h * D + d] : 0.f;
       Vs[w][idx / D][d] = ok ? V[(int64_t)j * ld + h * D + d] : 0.f;
     }
     __syncthreads();
-    if (t < ue) {
+    if (t < ce) {
 #pragma unroll 4
       for (int jj = 0; jj < KT; ++jj) {
         const int j = t + jj;
-        if (j >= kb && j < ke) {
+        if (j >= kb && j < ke && j < ce) {
           float sc = 0.f, dp = 0.f;
 #pragma unroll
           for (int d = 0; d < D; ++d) {
@@ -214,26 +267,26 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
       for (int d = 0; d < D; ++d) {
         const float t = (step > 0 ? Mrg[lane][d] : 0.f) + dq[d];
         if (step < 3) Mrg[lane][d] = t;
-        else if (qv) dQ[(int64_t)qi * lddq + h * D + d] = t * scale;
+        else if (qv) dQ[sp * split_stride + (int64_t)qi * lddq + h * D + d] = t * scale;
       }
     }
     __syncthreads();
   }
 }
 
-// dK, dV: one key row per lane, query stripes over 4 waves.
+// dK, dV: one key row per lane, query stripes over 4 waves, query splits over blockIdx.z.
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
     const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
     const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
-    float* __restrict__ dK, float* __restrict__ dV, int lddkv, const int* __restrict__ seg_id,
-    const int* __restrict__ seg_ptr, int N, int H, float scale) {
+    float* __restrict__ dK, float* __restrict__ dV, int lddkv, int64_t split_stride,
+    const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
   constexpr int QT = AttnCfg<D>::KT;
   __shared__ float Qs[4][QT][D];
   __shared__ float Gs[4][QT][D];
   __shared__ float Ls[4][QT][2];
   __shared__ float Mrg[64][2 * D];
-  const int h = blockIdx.y;
+  const int h = blockIdx.y, sp = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kj = blockIdx.x * 64 + lane;
   const bool kv = kj < N;
@@ -243,7 +296,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
     qb = seg_ptr[s];
     qe = seg_ptr[s + 1];
   }
-  const int ub = wave_min_i(qb), ue = wave_max_i(qe);
+  int cb, ce;
+  split_range(wave_min_i(qb), wave_max_i(qe), S, sp, QT, cb, ce);
   float k[D], v[D], dk[D], dv[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -252,26 +306,26 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
     dk[d] = 0.f;
     dv[d] = 0.f;
   }
-  for (int base = ub; base < ue; base += 4 * QT) {
+  for (int base = cb; base < ce; base += 4 * QT) {
     const int t = base + w * QT;
     for (int idx = lane; idx < QT * D; idx += 64) {
       const int i = t + idx / D, d = idx % D;
-      const bool ok = i < ue;
+      const bool ok = i < ce;
       Qs[w][idx / D][d] = ok ? Q[(int64_t)i * ld + h * D + d] : 0.f;
       Gs[w][idx / D][d] = ok ? dO[(int64_t)i * H * D + h * D + d] : 0.f;
     }
     for (int idx = lane; idx < QT; idx += 64) {
       const int i = t + idx;
-      const bool ok = i < ue;
+      const bool ok = i < ce;
       Ls[w][idx][0] = ok ? LSE[(int64_t)h * N + i] : 0.f;
       Ls[w][idx][1] = ok ? delta[(int64_t)h * N + i] : 0.f;
     }
     __syncthreads();
-    if (t < ue) {
+    if (t < ce) {
 #pragma unroll 4
       for (int ii = 0; ii < QT; ++ii) {
         const int i = t + ii;
-        if (i >= qb && i < qe) {
+        if (i >= qb && i < qe && i < ce) {
           float sc = 0.f, dp = 0.f;
 #pragma unroll
           for (int d = 0; d < D; ++d) {
@@ -300,13 +354,34 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
           Mrg[lane][d] = tk;
           Mrg[lane][D + d] = tv;
         } else if (kv) {
-          dK[(int64_t)kj * lddkv + h * D + d] = tk * scale;
-          dV[(int64_t)kj * lddkv + h * D + d] = tv;
+          dK[sp * split_stride + (int64_t)kj * lddkv + h * D + d] = tk * scale;
+          dV[sp * split_stride + (int64_t)kj * lddkv + h * D + d] = tv;
         }
       }
     }
     __syncthreads();
   }
+}
+
+// dqkv[i, c] = sum_s part[s, i, c]  over the query-split partials (c < F, Sq of them)
+// and the key-split partials (c >= F, Sk of them); fixed order, float4 columns.
+__global__ void __launch_bounds__(256) attn_bwd_sum_kernel(const float4* __restrict__ pq, int Sq,
+                                                           const float4* __restrict__ pkv, int Sk,
+                                                           float4* __restrict__ dqkv, int64_t N, int F4) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = N * 3 * F4;
+  if (t >= tot) return;
+  const int64_t i = t / (3 * F4);
+  const int c = (int)(t % (3 * F4));
+  float4 a = f4zero();
+  if (c < F4) {
+    const int64_t st = N * F4;
+    for (int s = 0; s < Sq; ++s) a = f4add(a, pq[s * st + i * F4 + c]);
+  } else {
+    const int64_t st = N * 2 * F4;
+    for (int s = 0; s < Sk; ++s) a = f4add(a, pkv[s * st + i * 2 * F4 + (c - F4)]);
+  }
+  dqkv[t] = a;
 }
 
 #define HY_ATTN_DISPATCH(D, ...)                       \
@@ -319,9 +394,24 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
     default: HY_CHECK(false, "attention head_dim must be one of 4,8,16,32,64, got ", D); \
   }
 
+static int attn_keytile(int D) { return D <= 8 ? 64 : (D <= 16 ? 32 : 16); }
+
+// Number of key (or query) splits: enough workgroups to fill the chip (~6 per CU at
+// the fwd kernel's register budget), but never less than two 4-wave tiles per split.
+// max_span: host bound on the longest attention segment (N for batch scope).
+static int attn_splits(int64_t N, int64_t H, int D, int64_t max_span, int64_t split_override) {
+  if (split_override > 0) return (int)split_override;
+  const int64_t blocks = (int64_t)ceil_div(N, 64) * H;
+  const int64_t want = std::max<int64_t>(1, (1536 + blocks - 1) / blocks);
+  const int64_t per = 2 * 4 * attn_keytile(D);
+  const int64_t cap = std::max<int64_t>(1, (max_span + 64 + per - 1) / per);
+  return (int)std::min<int64_t>(std::min(want, cap), 32);
+}
+
 // qkv: [N, 3*H*D] packed rows (q | k | v), as produced by the in-projection.
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const at::Tensor& seg_id,
-                                            const at::Tensor& seg_ptr, int64_t H, double scale) {
+                                            const at::Tensor& seg_ptr, int64_t H, double scale, int64_t max_span,
+                                            int64_t splits) {
   HY_CHECK_CUDA(qkv);
   HY_CHECK_F32(qkv);
   HY_CHECK(qkv.stride(1) == 1, "qkv rows must be contiguous");
@@ -331,20 +421,28 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const at::Ten
   const int64_t F = qkv.size(1) / 3;
   const int D = (int)(F / H);
   HY_CHECK(D * H == F, "hidden must be divisible by heads");
+  HY_CHECK(seg_id.numel() == N, "seg_id must have one entry per row");
   auto O = at::empty({N, F}, qkv.options());
   auto LSE = at::empty({H, N}, qkv.options());
   if (N == 0) return {O, LSE};
   const int ld = (int)qkv.stride(0);
   const float* base = qkv.data_ptr<float>();
-  dim3 grid(ceil_div(N, 64), H);
-  HY_ATTN_DISPATCH(D, attn_fwd_kernel<kD><<<grid, 256, 0, stream()>>>(
-                          base, base + F, base + 2 * F, ld, O.data_ptr<float>(), LSE.data_ptr<float>(),
-                          seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, (float)scale));
+  const int S = attn_splits(N, H, D, max_span > 0 ? max_span : N, splits);
+  auto part = at::empty({(int64_t)S * H * N * (D + 2)}, qkv.options());
+  dim3 grid(ceil_div(N, 64), H, S);
+  HY_ATTN_DISPATCH(D, {
+    attn_fwd_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, part.data_ptr<float>(),
+                                                    seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H,
+                                                    S, (float)scale);
+    attn_fwd_combine_kernel<kD><<<ceil_div(N * H, 256), 256, 0, stream()>>>(
+        part.data_ptr<float>(), O.data_ptr<float>(), LSE.data_ptr<float>(), (int)N, (int)H, S);
+  });
   return {O, LSE};
 }
 
 at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& LSE,
-                    const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t H, double scale) {
+                    const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t H, double scale, int64_t max_span,
+                    int64_t splits) {
   auto dO = dO_.contiguous();
   HY_CHECK_CUDA(dO);
   const int64_t N = qkv.size(0);
@@ -358,27 +456,49 @@ at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tens
   const int ld = (int)qkv.stride(0);
   const float* base = qkv.data_ptr<float>();
   float* dbase = dqkv.data_ptr<float>();
-  dim3 grid(ceil_div(N, 64), H);
+  const int S = attn_splits(N, H, D, max_span > 0 ? max_span : N, splits);
+  dim3 grid(ceil_div(N, 64), H, S);
+  if (S == 1) {
+    HY_ATTN_DISPATCH(D, {
+      attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(
+          base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
+          dbase, (int)(3 * F), 0, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, 1, (float)scale);
+      attn_bwd_dkv_kernel<kD><<<grid, 256, 0, stream()>>>(
+          base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
+          dbase + F, dbase + 2 * F, (int)(3 * F), 0, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N,
+          (int)H, 1, (float)scale);
+    });
+    return dqkv;
+  }
+  auto pq = at::empty({(int64_t)S * N * F}, qkv.options());
+  auto pkv = at::empty({(int64_t)S * N * 2 * F}, qkv.options());
   HY_ATTN_DISPATCH(D, {
-    attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, dO.data_ptr<float>(),
-                                                       LSE.data_ptr<float>(), delta.data_ptr<float>(), dbase,
-                                                       (int)(3 * F), seg_id.data_ptr<int>(),
-                                                       seg_ptr.data_ptr<int>(), (int)N, (int)H, (float)scale);
+    attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(
+        base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
+        pq.data_ptr<float>(), (int)F, N * F, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, S,
+        (float)scale);
     attn_bwd_dkv_kernel<kD><<<grid, 256, 0, stream()>>>(
         base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
-        dbase + F, dbase + 2 * F, (int)(3 * F), seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H,
-        (float)scale);
+        pkv.data_ptr<float>(), pkv.data_ptr<float>() + F, (int)(2 * F), N * 2 * F, seg_id.data_ptr<int>(),
+        seg_ptr.data_ptr<int>(), (int)N, (int)H, S, (float)scale);
   });
+  const int F4 = (int)(F / 4);
+  HY_CHECK(F % 4 == 0, "attention hidden must be a multiple of 4");
+  attn_bwd_sum_kernel<<<ceil_div(N * 3 * F4, 256), 256, 0, stream()>>>(
+      reinterpret_cast<const float4*>(pq.data_ptr<float>()), S, reinterpret_cast<const float4*>(pkv.data_ptr<float>()),
+      S, reinterpret_cast<float4*>(dbase), N, F4);
   return dqkv;
 }
 
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("attn_fwd(Tensor qkv, Tensor seg_id, Tensor seg_ptr, int H, float scale) -> (Tensor, Tensor)");
   m.def(
-      "attn_bwd(Tensor dO, Tensor qkv, Tensor O, Tensor LSE, Tensor seg_id, Tensor seg_ptr, int H, float scale) "
-      "-> Tensor");
+      "attn_fwd(Tensor qkv, Tensor seg_id, Tensor seg_ptr, int H, float scale, int max_span, int splits) "
+      "-> (Tensor, Tensor)");
+  m.def(
+      "attn_bwd(Tensor dO, Tensor qkv, Tensor O, Tensor LSE, Tensor seg_id, Tensor seg_ptr, int H, float scale, "
+      "int max_span, int splits) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

@@ -145,6 +145,12 @@ class Base(nn.Module):
                     br[-1].bias.data.fill_(self.initial_bias)
 
     def _conv_head_kwargs(self):
+        """Extra get_conv kwargs for node conv heads: the encoder's edge width, so that
+        heads see the same (possibly GPS-embedded) edge_attr as the conv layers."""
+        import inspect
+
+        if "edge_dim" in inspect.signature(self.get_conv).parameters:
+            return {"edge_dim": self.edge_embed_dim}
         return {}
 
     def _init_node_conv(self):

@@ -132,7 +132,7 @@ class EGCLStack(Base):
                      equivariant=self.equivariance and not last_layer)
 
     def _conv_head_kwargs(self):
-        return {"last_layer": False}
+        return {"last_layer": False, "edge_dim": self.edge_embed_dim}
 
     def _embedding(self, data):
         x, pos, ctx = super()._embedding(data)

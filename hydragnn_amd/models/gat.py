@@ -156,24 +156,27 @@ class GATStack(Base):
             bt, arch = b["type"], b["architecture"]
             nl, hd = arch["num_headlayers"], arch["dim_headlayers"]
             ch, bh, co, bo = nn.ModuleList(), nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
-            ch.append(self.get_conv(self.hidden_dim, hd[0], True))
+            ed = self.edge_embed_dim
+            ch.append(self.get_conv(self.hidden_dim, hd[0], True, edge_dim=ed, head=True))
             bh.append(BatchNorm(hd[0] * H))
             for il in range(nl - 1):
-                ch.append(self.get_conv(hd[il] * H, hd[il + 1], True))
+                ch.append(self.get_conv(hd[il] * H, hd[il + 1], True, edge_dim=ed, head=True))
                 bh.append(BatchNorm(hd[il + 1] * H))
             for ih in node_feature_ind:
-                co.append(self.get_conv(hd[-1] * H, self.head_dims[ih], False))
+                co.append(self.get_conv(hd[-1] * H, self.head_dims[ih], False, edge_dim=ed, head=True))
                 bo.append(BatchNorm(self.head_dims[ih]))
             self.convs_node_hidden[bt] = ch
             self.batch_norms_node_hidden[bt] = bh
             self.convs_node_output[bt] = co
             self.batch_norms_node_output[bt] = bo
 
-    def get_conv(self, input_dim, output_dim, concat=True, edge_dim=None):
+    def get_conv(self, input_dim, output_dim, concat=True, edge_dim=None, head=False):
         gat = GATv2Conv(input_dim, output_dim, heads=self.heads, negative_slope=self.negative_slope,
                         dropout=self.dropout, add_self_loops=True, edge_dim=edge_dim, concat=concat)
-        out_lin = nn.Linear(self.hidden_dim * self.heads, self.hidden_dim) if (self.use_global_attn and concat) \
-            else nn.Identity()
+        # GPS layers project the concatenated heads back to hidden_dim (GATStack.py:187-190);
+        # node conv heads keep their head-concatenated width for the following BatchNorm
+        out_lin = nn.Linear(self.hidden_dim * self.heads, self.hidden_dim) \
+            if (self.use_global_attn and concat and not head) else nn.Identity()
         return _GATBlock(gat, out_lin)
 
     def __str__(self):

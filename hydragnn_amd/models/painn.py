@@ -138,7 +138,7 @@ class _EqStackBase(Base):
             self.feature_layers.append(nn.Identity())
 
     def _conv_head_kwargs(self):
-        return {"last_layer": False}
+        return {"last_layer": False, **super()._conv_head_kwargs()}
 
     def _adapters(self, input_dim, output_dim, last_layer):
         node_embed_out = nn.Sequential(nn.Linear(input_dim, output_dim), nn.Tanh(), nn.Linear(output_dim, output_dim))

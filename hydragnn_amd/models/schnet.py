@@ -104,7 +104,7 @@ class SCFStack(Base):
                       equivariant=self.equivariance and not last_layer)
 
     def _conv_head_kwargs(self):
-        return {"last_layer": False}
+        return {"last_layer": False, **super()._conv_head_kwargs()}
 
     def _embedding(self, data):
         x, pos, ctx = super()._embedding(data)

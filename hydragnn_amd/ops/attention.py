@@ -9,6 +9,7 @@ the local mini-batch in one sequence (``scope="batch"``).  ``scope="graph"``
 restricts attention to nodes of the same graph.
 """
 import math
+import os
 
 import torch
 
@@ -61,18 +62,31 @@ def attention_reference(qkv, heads, seg_id, scale=None):
     return o.transpose(0, 1).reshape(N, F)
 
 
+_SPLITS = int(os.environ.get("HYDRA_ATTN_SPLITS", "0"))  # 0 = kernel heuristic
+
+
+def _max_span(n, seg_ptr):
+    """Host-side bound on the longest segment (shape arithmetic only: capture-safe).
+    Only the split heuristic uses it; correctness never depends on it."""
+    nseg = seg_ptr.numel() - 1
+    if nseg <= 2:
+        return n
+    return min(n, 4 * ((n + nseg - 1) // nseg))
+
+
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, seg_id, seg_ptr, heads, scale):
-        O, LSE = _native.ops().attn_fwd(qkv, seg_id, seg_ptr, heads, scale)
+        span = _max_span(qkv.shape[0], seg_ptr)
+        O, LSE = _native.ops().attn_fwd(qkv, seg_id, seg_ptr, heads, scale, span, _SPLITS)
         ctx.save_for_backward(qkv, O, LSE, seg_id, seg_ptr)
-        ctx.heads, ctx.scale = heads, scale
+        ctx.heads, ctx.scale, ctx.span = heads, scale, span
         return O
 
     @staticmethod
     def backward(ctx, dO):
         qkv, O, LSE, seg_id, seg_ptr = ctx.saved_tensors
-        dqkv = _native.ops().attn_bwd(dO, qkv, O, LSE, seg_id, seg_ptr, ctx.heads, ctx.scale)
+        dqkv = _native.ops().attn_bwd(dO, qkv, O, LSE, seg_id, seg_ptr, ctx.heads, ctx.scale, ctx.span, _SPLITS)
         return dqkv, None, None, None, None
 
 

@@ -43,7 +43,9 @@ def _(config_file: str, use_deepspeed=False):
 
 
 def _device_path_enabled(config):
-    return torch.cuda.is_available() and int(os.getenv("HYDRAGNN_DEVICE_DATA", "1")) == 1
+    # HYDRAGNN_DEVICE_DATA=2 forces the store/padded-step path on CPU (tests of the padding logic)
+    flag = int(os.getenv("HYDRAGNN_DEVICE_DATA", "1"))
+    return flag == 2 or (torch.cuda.is_available() and flag == 1)
 
 
 @run_training.register

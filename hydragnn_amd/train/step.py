@@ -301,7 +301,22 @@ class TrainStep:
             cap.g_opt.replay()
         return cap.loss, cap.tasks
 
+    def padded_step(self, store, indices):
+        """The captured step's exact computation (static padded bucket shapes) run
+        eagerly — the CPU twin of ``graph_step`` used to test the padding logic."""
+        N, E = store.sizes_of(indices)
+        Np, Ep = self.bucket_of(N, E)
+        lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
+        cap = _Captured()
+        cap.lay = lay
+        cap.dev_plan = store.upload(indices, lay)
+        loss, tasks = self._body_fwd_bwd(store, cap)
+        self.opt.step()
+        return loss, tasks
+
     def __call__(self, store, indices):
-        if self.mode == "graph" and self.device.type == "cuda":
-            return self.graph_step(store, indices)
+        if self.mode == "graph":
+            if self.device.type == "cuda":
+                return self.graph_step(store, indices)
+            return self.padded_step(store, indices)
         return self.eager(store, indices)

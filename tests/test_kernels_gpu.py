@@ -135,6 +135,32 @@ def test_attention_long_sequence():
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("splits", [1, 2, 3, 7, 16])
+@pytest.mark.parametrize("scope", ["batch", "graph"])
+def test_attention_key_splits(splits, scope):
+    """Every split count (explicit, bypassing the heuristic) gives the same fwd/bwd."""
+    from hydragnn_amd import _native
+
+    H, D = 8, 8
+    F = H * D
+    torch.manual_seed(splits)
+    ptr = torch.tensor([0, 300, 301, 700, 1333])
+    N = 1400
+    seg_id, seg_ptr = make_segments(N, scope, ptr=ptr, num_valid=1333)
+    qkv = torch.randn(N, 3 * F)
+    qc = qkv.clone().requires_grad_()
+    ref = attention_reference(qc, H, seg_id)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    scale = 1.0 / D ** 0.5
+    ops = _native.ops()
+    qd, sid, sptr = qkv.to(DEV), seg_id.to(DEV), seg_ptr.to(DEV)
+    O, LSE = ops.attn_fwd(qd, sid, sptr, H, scale, N, splits)
+    torch.testing.assert_close(O.cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
+    dqkv = ops.attn_bwd(g.to(DEV), qd, O, LSE, sid, sptr, H, scale, N, splits)
+    torch.testing.assert_close(dqkv.cpu(), qc.grad, rtol=2e-4, atol=2e-4)
+
+
 def test_fused_adamw_matches_cpu():
     from hydragnn_amd.optim.adamw import FusedAdamW
 

@@ -14,6 +14,8 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--last-fraction", type=float, default=1.0)
     ap.add_argument("--last-ms", type=float, default=None, help="keep only the final MS of the timeline")
+    ap.add_argument("--between", default=None,
+                    help="keep only kernels between the last two dispatches whose name contains this (e.g. sleep)")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--steps", type=int, default=1)
     a = ap.parse_args()
@@ -28,6 +30,10 @@ def main():
     if a.last_ms is not None:
         cut = t1 - a.last_ms * 1e6
     rows = [r for r in rows if r[1] >= cut]
+    if a.between:
+        marks = [i for i, r in enumerate(rows) if a.between in r[0]]
+        assert len(marks) >= 2, f"need two '{a.between}' marker kernels, found {len(marks)}"
+        rows = rows[marks[-2] + 1:marks[-1]]
     agg = {}
     for name, s, e, gx, wx, vg, ag, lds in rows:
         d = agg.setdefault(name, [0, 0.0, gx // max(wx, 1), vg, ag, lds])
