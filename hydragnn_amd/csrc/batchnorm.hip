@@ -17,7 +17,11 @@ constexpr int kBnRows = 128;  // rows per slab
 
 __device__ __forceinline__ int nvalid_of(const int* nv, int N) { return nv ? min(*nv, N) : N; }
 
-// part: [S][3][F] = (count, mean, M2) per slab, per column
+// part: [S][3][F] = (count, mean, std) per slab, per column.  Two passes over the
+// (L2-hot) slab: mean first, then M2 = sum (x - mean)^2 — no E[x^2] - E[x]^2
+// cancellation, and no overflow of sum x^2 for large activations (|x| ~ 1e19
+// appears when a deep multiplicative stack such as DimeNet drifts in training;
+// the one-pass form turned that into inf - inf = NaN statistics).
 __global__ void __launch_bounds__(256) bn_fwd_partial_kernel(const float* __restrict__ x, const int* __restrict__ nv,
                                                              float* __restrict__ part, int N, int F, int tpr) {
   const int s = blockIdx.x;
@@ -25,50 +29,64 @@ __global__ void __launch_bounds__(256) bn_fwd_partial_kernel(const float* __rest
   const int r0 = s * kBnRows, r1 = min(Nv, r0 + kBnRows);
   const int rl = threadIdx.x / tpr, c = threadIdx.x % tpr;
   const int rpb = 256 / tpr;
-  __shared__ float red[256 * 2];
-  for (int f = c; f < F; f += tpr) {
-    float sm = 0.f, sq = 0.f;
-    for (int r = r0 + rl; r < r1; r += rpb) {
-      const float v = x[(int64_t)r * F + f];
-      sm += v;
-      sq = fmaf(v, v, sq);
-    }
+  const float n = (float)max(r1 - r0, 0);
+  __shared__ float red[256];
+  __shared__ double redd[256];
+  __shared__ float smu[64];
+  // every thread runs the same number of column passes (barriers stay uniform)
+  for (int f0 = 0; f0 < F; f0 += tpr) {
+    const int f = f0 + c;
+    const bool act = f < F;
+    float sm = 0.f;
+    if (act)
+      for (int r = r0 + rl; r < r1; r += rpb) sm += x[(int64_t)r * F + f];
     red[threadIdx.x] = sm;
-    red[256 + threadIdx.x] = sq;
     __syncthreads();
     if (rl == 0) {
-      float a = 0.f, b = 0.f;
-      for (int k = 0; k < rpb; ++k) {
-        a += red[k * tpr + c];
-        b += red[256 + k * tpr + c];
+      float a = 0.f;
+      for (int k = 0; k < rpb; ++k) a += red[k * tpr + c];
+      smu[c] = n > 0.f ? a / n : 0.f;
+    }
+    __syncthreads();
+    const float mu = smu[c];
+    double sq = 0.0;  // fp64: (x - mu)^2 overflows fp32 for |x| > 1.8e19
+    if (act)
+      for (int r = r0 + rl; r < r1; r += rpb) {
+        const double t = (double)x[(int64_t)r * F + f] - (double)mu;
+        sq = fma(t, t, sq);
       }
-      const float n = (float)max(r1 - r0, 0);
-      const float mean = n > 0.f ? a / n : 0.f;
-      const float m2 = n > 0.f ? fmaxf(b - n * mean * mean, 0.f) : 0.f;
+    redd[threadIdx.x] = sq;
+    __syncthreads();
+    if (rl == 0 && act) {
+      double b = 0.0;
+      for (int k = 0; k < rpb; ++k) b += redd[k * tpr + c];
       part[((int64_t)s * 3 + 0) * F + f] = n;
-      part[((int64_t)s * 3 + 1) * F + f] = mean;
-      part[((int64_t)s * 3 + 2) * F + f] = m2;
+      part[((int64_t)s * 3 + 1) * F + f] = mu;
+      part[((int64_t)s * 3 + 2) * F + f] = n > 0.f ? (float)sqrt(b / (double)n) : 0.f;  // slab std
     }
     __syncthreads();
   }
 }
 
-// combine slabs (Chan); returns mean, biased var
-__device__ __forceinline__ void bn_combine(const float* part, int S, int F, int f, float& mean, float& var) {
-  float n = 0.f, m = 0.f, M2 = 0.f;
+// combine slabs in a fixed order (fp64): mean, biased var
+__device__ __forceinline__ void bn_combine(const float* part, int S, int F, int f, float& mean, double& var) {
+  double n = 0.0, sm = 0.0;
   for (int s = 0; s < S; ++s) {
-    const float nb = part[((int64_t)s * 3 + 0) * F + f];
-    if (nb <= 0.f) continue;
-    const float mb = part[((int64_t)s * 3 + 1) * F + f];
-    const float M2b = part[((int64_t)s * 3 + 2) * F + f];
-    const float nn = n + nb;
-    const float d = mb - m;
-    m += d * nb / nn;
-    M2 += M2b + d * d * n * nb / nn;
-    n = nn;
+    const double nb = part[((int64_t)s * 3 + 0) * F + f];
+    n += nb;
+    sm += nb * (double)part[((int64_t)s * 3 + 1) * F + f];
   }
-  mean = m;
-  var = n > 0.f ? M2 / n : 0.f;
+  const double m = n > 0.0 ? sm / n : 0.0;
+  double M2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double nb = part[((int64_t)s * 3 + 0) * F + f];
+    if (nb <= 0.0) continue;
+    const double d = (double)part[((int64_t)s * 3 + 1) * F + f] - m;
+    const double sd = part[((int64_t)s * 3 + 2) * F + f];
+    M2 += nb * (sd * sd + d * d);
+  }
+  mean = (float)m;
+  var = n > 0.0 ? M2 / n : 0.0;
 }
 
 __global__ void __launch_bounds__(256) bn_fwd_apply_kernel(
@@ -80,9 +98,10 @@ __global__ void __launch_bounds__(256) bn_fwd_apply_kernel(
   float* smean = sh;
   float* sinv = sh + F;
   for (int f = threadIdx.x; f < F; f += 256) {
-    float mean, var;
+    float mean;
+    double var;
     bn_combine(part, S, F, f, mean, var);
-    const float inv = rsqrtf(var + eps);
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
     smean[f] = mean;
     sinv[f] = inv;
     if (blockIdx.x == 0) {
@@ -90,7 +109,7 @@ __global__ void __launch_bounds__(256) bn_fwd_apply_kernel(
       save_invstd[f] = inv;
       if (rmean) {
         const int Nv = nvalid_of(nv, N);
-        const float unb = Nv > 1 ? var * (float)Nv / (float)(Nv - 1) : var;
+        const float unb = (float)(Nv > 1 ? var * (double)Nv / (double)(Nv - 1) : var);
         rmean[f] = (1.f - momentum) * rmean[f] + momentum * mean;
         rvar[f] = (1.f - momentum) * rvar[f] + momentum * unb;
       }
@@ -118,18 +137,22 @@ __global__ void __launch_bounds__(256) bn_bwd_partial_kernel(const float* __rest
   const int rl = threadIdx.x / tpr, c = threadIdx.x % tpr;
   const int rpb = 256 / tpr;
   __shared__ float red[256 * 2];
-  for (int f = c; f < F; f += tpr) {
-    const float mu = mean[f], is = invstd[f];
+  for (int f0 = 0; f0 < F; f0 += tpr) {
+    const int f = f0 + c;
+    const bool act = f < F;
     float a = 0.f, b = 0.f;
-    for (int r = r0 + rl; r < r1; r += rpb) {
-      const float g = dy[(int64_t)r * F + f];
-      a += g;
-      b = fmaf(g, (x[(int64_t)r * F + f] - mu) * is, b);
+    if (act) {
+      const float mu = mean[f], is = invstd[f];
+      for (int r = r0 + rl; r < r1; r += rpb) {
+        const float g = dy[(int64_t)r * F + f];
+        a += g;
+        b = fmaf(g, (x[(int64_t)r * F + f] - mu) * is, b);
+      }
     }
     red[threadIdx.x] = a;
     red[256 + threadIdx.x] = b;
     __syncthreads();
-    if (rl == 0) {
+    if (rl == 0 && act) {
       float sa = 0.f, sb = 0.f;
       for (int k = 0; k < rpb; ++k) {
         sa += red[k * tpr + c];

@@ -118,6 +118,16 @@ __device__ __forceinline__ float chan_sum(float v, float* red, int T) {
   return t;
 }
 
+__device__ __forceinline__ double chan_sum_d(double v, double* red, int T) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  double t = 0.0;
+  const int base = (threadIdx.x / T) * T;
+  for (int q = 0; q < T; ++q) t += red[base + q];
+  __syncthreads();
+  return t;
+}
+
 template <int V>
 __device__ __forceinline__ typename VecT<V>::T ldv(const float* p) {
   return *reinterpret_cast<const typename VecT<V>::T*>(p);
@@ -162,7 +172,28 @@ __device__ __forceinline__ void fold_rows(float (&v)[V], float* red, int rl, int
   __syncthreads();
 }
 
-// forward pass 1: z (if fused) + per-slab (count, mean, M2) -> part[S][3][C]
+// fp64 variant of fold_rows for the squared deviations (red: [kBlk * V] doubles).
+template <int V>
+__device__ __forceinline__ void fold_rows_d(double (&v)[V], double* red, int rl, int cg_l, const Geo& g) {
+#pragma unroll
+  for (int k = 0; k < V; ++k) red[threadIdx.x * V + k] = v[k];
+  __syncthreads();
+  if (rl == 0) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      double s = 0.0;
+      for (int q = 0; q < g.rpb; ++q) s += red[(q * g.tpr + cg_l) * V + k];
+      v[k] = s;
+    }
+  }
+  __syncthreads();
+}
+
+// forward pass 1: z (if fused) + per-slab (count, mean, std) -> part[S][3][C].
+// Squared deviations accumulate in fp64 and the slab spread is stored as a standard
+// deviation: activations of |x| > 1.8e19 (seen when deep multiplicative stacks drift)
+// would overflow an fp32 sum of squares / variance, and the CPU reference (torch's
+// fp64-accumulating CPU BatchNorm) trains through them.
 template <int V>
 __global__ void __launch_bounds__(kBlk)
     bnf_stats_kernel(const float* __restrict__ a, const float* __restrict__ b, const int* __restrict__ nvp,
@@ -170,6 +201,7 @@ __global__ void __launch_bounds__(kBlk)
                      float* __restrict__ part, int N, int C, Geo g) {
   using T = typename VecT<V>::T;
   __shared__ float red[kBlk * V];
+  __shared__ double redd[kBlk * V];
   __shared__ float smean[kBlk];
   const int Nv = nvp ? min(*nvp, N) : N;
   const DropCfg d = drop_cfg(rng, salt, p);
@@ -223,11 +255,12 @@ __global__ void __launch_bounds__(kBlk)
       for (int k = 0; k < V; ++k) smean[cg_l * V + k] = cnt > 0.f ? sm[k] / cnt : 0.f;
     }
     __syncthreads();
-    float mu[V], m2[V];
+    float mu[V];
+    double m2[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       mu[k] = act ? smean[cg_l * V + k] : 0.f;
-      m2[k] = 0.f;
+      m2[k] = 0.0;
     }
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
@@ -235,19 +268,19 @@ __global__ void __launch_bounds__(kBlk)
       if (act && r < rv1) {
 #pragma unroll
         for (int k = 0; k < V; ++k) {
-          const float t = el<V>(v[i], k) - mu[k];
-          m2[k] = fmaf(t, t, m2[k]);
+          const double t = (double)el<V>(v[i], k) - (double)mu[k];
+          m2[k] = fma(t, t, m2[k]);
         }
       }
     }
-    fold_rows<V>(m2, red, rl, cg_l, g);
+    fold_rows_d<V>(m2, redd, rl, cg_l, g);
     if (rl == 0 && act) {
       float* P = part + (int64_t)blockIdx.x * 3 * C;
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         P[c0 + k] = cnt;
         P[C + c0 + k] = mu[k];
-        P[2 * C + c0 + k] = m2[k];
+        P[2 * C + c0 + k] = cnt > 0.f ? (float)sqrt(m2[k] / (double)cnt) : 0.f;
       }
     }
     __syncthreads();
@@ -266,6 +299,7 @@ __global__ void __launch_bounds__(kBlk)
                      int N, int C, Geo g) {
   extern __shared__ float sh[];  // scale[C], shift[C]
   __shared__ float red[kBlk];
+  __shared__ double redd[kBlk];
   float* scl = sh;
   float* shf = sh + C;
   const int Nv = nvp ? min(*nvp, N) : N;
@@ -310,21 +344,22 @@ __global__ void __launch_bounds__(kBlk)
     n = chan_sum(n, red, TT);
     sm = chan_sum(sm, red, TT);
     const float mean = n > 0.f ? sm / n : 0.f;
-    float M2 = 0.f;
+    double M2 = 0.0;  // sum_s n_s (std_s^2 + (mean_s - mean)^2), fp64 (see pass 1)
 #pragma unroll
     for (int t = 0; t < kQ; ++t) {
-      const float dl = qm[t] - mean;
-      M2 += q2[t] + qn[t] * dl * dl;
+      const double dl = (double)qm[t] - (double)mean, sd = q2[t];
+      M2 += (double)qn[t] * (sd * sd + dl * dl);
     }
     for (int q = j + kQ * TT; ok && q < S; q += TT) {
       const float* P = part + (int64_t)q * 3 * C;
-      const float dl = P[C + c] - mean;
-      M2 += P[2 * C + c] + P[c] * dl * dl;
+      const double dl = (double)P[C + c] - (double)mean, sd = P[2 * C + c];
+      M2 += (double)P[c] * (sd * sd + dl * dl);
     }
-    M2 = chan_sum(M2, red, TT);
+    M2 = chan_sum_d(M2, redd, TT);
     if (ok && j == 0) {
-      const float var = n > 0.f ? M2 / n : 0.f;
-      const float is = rsqrtf(var + eps);
+      const double vard = n > 0.f ? M2 / (double)n : 0.0;
+      const float var = (float)vard;
+      const float is = (float)(1.0 / sqrt(vard + (double)eps));
       const float ww = w ? w[c] : 1.f, bb = beta ? beta[c] : 0.f;
       scl[c] = is * ww;
       shf[c] = bb - mean * is * ww;

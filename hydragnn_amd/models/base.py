@@ -281,20 +281,19 @@ class Base(nn.Module):
 
     def encode(self, data):
         inv, equiv, ctx = self._embedding(data)
-        nmask = data.get("node_mask")  # statically padded batch: keep dummy rows at zero
-        if nmask is not None:
-            nmask = nmask.view(-1, 1).to(inv.dtype)
-            inv = inv * nmask
+        keep = data.get("node_mask")  # statically padded batch: keep dummy rows at zero
+        if keep is not None:
+            inv = _zero_rows(inv, keep)
         for conv, bn in zip(self.graph_convs, self.feature_layers):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
             if isinstance(self.activation_function, torch.nn.ReLU) and isinstance(bn, BatchNorm):
                 # BN -> ReLU -> padding mask in one fused launch (ops.norm.norm_add)
-                inv = norm_add(inv, bn, ctx.get("num_valid"), relu=True, zero_pad=nmask is not None)
+                inv = norm_add(inv, bn, ctx.get("num_valid"), relu=True, zero_pad=keep is not None)
                 continue
             h = bn(inv, ctx.get("num_valid")) if isinstance(bn, BatchNorm) else bn(inv)
             inv = self.activation_function(h)
-            if nmask is not None:
-                inv = inv * nmask
+            if keep is not None:
+                inv = _zero_rows(inv, keep)
         return inv, equiv, ctx
 
     def _branch_ids(self, data):
@@ -360,9 +359,12 @@ class Base(nn.Module):
     def _node_head(self, headloc, nt, x, equiv, ctx, batch):
         if nt == "conv":
             inv, eq = x, equiv
+            keep = ctx.data.get("node_mask")  # statically padded batch: dummy rows -> exact zeros
             for conv, bn in zip(headloc[0::2], headloc[1::2]):
                 inv, eq = conv(inv, eq, ctx)
                 inv = self.activation_function(bn(inv, ctx.get("num_valid")))
+                if keep is not None:  # (equivariant state may be positions: left untouched)
+                    inv = _zero_rows(inv, keep)
             return inv
         return headloc(x=x, batch=batch)
 
@@ -446,6 +448,11 @@ class Base(nn.Module):
 
     def __str__(self):
         return "Base"
+
+
+def _zero_rows(t, keep):
+    """Rows where ``keep`` is False -> 0 (NaN/inf-safe, unlike multiplying by a mask)."""
+    return torch.where(keep.view(-1, *([1] * (t.dim() - 1))), t, torch.zeros((), dtype=t.dtype, device=t.device))
 
 
 class MLPNode(nn.Module):

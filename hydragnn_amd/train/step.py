@@ -41,9 +41,11 @@ def masked_loss(kind, pred, target, mask=None, var=None):
         if kind == "GaussianNLLLoss":
             return torch.nn.functional.gaussian_nll_loss(pred, target, var)
         raise ValueError(kind)
-    m = mask.view(-1, *([1] * (pred.dim() - 1))).to(pred.dtype)
+    keep = mask.view(-1, *([1] * (pred.dim() - 1)))
+    m = keep.to(pred.dtype)
     denom = m.sum() * (pred.numel() // pred.shape[0])
-    diff = pred - target
+    # padded rows never reach the loss, whatever they hold (NaN-safe select, not a product)
+    diff = torch.where(keep, pred - target, torch.zeros((), dtype=pred.dtype, device=pred.device))
     if kind in ("mse", "rmse"):
         l = (diff * diff * m).sum() / denom
         return torch.sqrt(l) if kind == "rmse" else l
@@ -53,7 +55,7 @@ def masked_loss(kind, pred, target, mask=None, var=None):
         a = diff.abs()
         return (torch.where(a < 1.0, 0.5 * a * a, a - 0.5) * m).sum() / denom
     if kind == "GaussianNLLLoss":
-        v = var.clamp(min=1e-6)
+        v = torch.where(keep, var, torch.ones((), dtype=var.dtype, device=var.device)).clamp(min=1e-6)
         return (0.5 * (torch.log(v) + diff * diff / v) * m).sum() / denom
     raise ValueError(kind)
 

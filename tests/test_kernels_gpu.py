@@ -218,6 +218,32 @@ def test_batchnorm_fused(F, masked):
     torch.testing.assert_close(bn_g.running_var.cpu(), bn_c.running_var, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_batchnorm_huge_activations(fused):
+    """|x| ~ 1e21 (an fp32 sum of squares overflows; torch's own fp32 BatchNorm returns all
+    zeros here): the fp64-accumulated statistics give the exact normalisation, no inf/NaN
+    (both the standalone and the fused BN kernels)."""
+    from hydragnn_amd.ops.norm import batch_norm, norm_add
+
+    torch.manual_seed(0)
+    N, F = 700, 20
+    x = (torch.randn(N, F) + 0.5) * 1e21
+    bn_c = torch.nn.BatchNorm1d(F)
+    bn_g = torch.nn.BatchNorm1d(F).to(DEV)
+    xd = x.double()
+    yc = ((xd - xd.mean(0)) / torch.sqrt(xd.var(0, unbiased=False) + bn_c.eps)).float()
+    xg = x.to(DEV)
+    if fused:
+        from hydragnn_amd.models.layers import BatchNorm
+
+        m = BatchNorm(F).to(DEV)
+        yg = norm_add(xg, m, None, relu=False)
+    else:
+        yg = batch_norm(xg, bn_g, None)
+    assert torch.isfinite(yg).all()
+    torch.testing.assert_close(yg.cpu(), yc.detach(), rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.parametrize("M,O,I", [(23000, 64, 64), (5000, 64, 1088), (3000, 7, 130), (1500, 192, 64)])
 def test_linear_wgrad(M, O, I):
     from hydragnn_amd.ops.linear import linear, linear_sum
