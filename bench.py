@@ -55,10 +55,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
+    # (RCCL refuses duplicate devices); the driver's N-GPU runs use RCCL ("nccl").
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(local % ndev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{local % ndev}")
 
     from hydragnn_amd.data.synthetic import oc20_like, degree_histogram
     from hydragnn_amd.data.device_store import DeviceGraphStore

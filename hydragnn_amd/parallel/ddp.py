@@ -75,7 +75,7 @@ class DistributedDataParallel(nn.Module):
             for p, off in zip(ps, b.offsets):
                 p.grad = b.flat[off:off + p.numel()].view_as(p)
                 self._owner[p] = bi
-                p.register_post_accumulate_grad_hook(self._make_hook(bi))
+                p.register_post_accumulate_grad_hook(self._make_hook(bi, off))
 
     # ------------------------------------------------------------------ state
     def _broadcast_module_state(self):
@@ -92,7 +92,7 @@ class DistributedDataParallel(nn.Module):
                     dist.broadcast(b.data, src=0, group=self.process_group)
 
     # ------------------------------------------------------------------ hooks
-    def _make_hook(self, bi):
+    def _make_hook(self, bi, off):
         def hook(p):
             if not self._sync_enabled:
                 return
@@ -102,7 +102,6 @@ class DistributedDataParallel(nn.Module):
             b = self.buckets[bi]
             # the engine may have replaced the grad tensor (e.g. first accumulation
             # with a non-viewable layout): copy into the bucket view then re-alias
-            off = b.offsets[b.params.index(p)]
             view = b.flat[off:off + p.numel()].view_as(p)
             if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
                 view.copy_(p.grad)

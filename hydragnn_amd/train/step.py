@@ -312,7 +312,12 @@ class TrainStep:
         cap = _Captured()
         cap.lay = lay
         cap.dev_plan = store.upload(indices, lay)
-        loss, tasks = self._body_fwd_bwd(store, cap)
+        if isinstance(self.model, DistributedDataParallel):  # same sync structure as graph_step
+            with self.model.no_sync():
+                loss, tasks = self._body_fwd_bwd(store, cap)
+            self.model.allreduce_now()
+        else:
+            loss, tasks = self._body_fwd_bwd(store, cap)
         self.opt.step()
         return loss, tasks
 
