@@ -261,11 +261,14 @@ class TrainStep:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(2):  # warm-up (allocator, kernels, autograd buffers) on real data
+            # warm-up (allocator, kernels, autograd buffers) on real data.  No collective
+            # here: ranks capture different buckets at different times (their batches
+            # differ), so a capture must be purely local or the ranks' collective
+            # sequences diverge and deadlock.  The warm-up updates are rolled back below.
+            for _ in range(2):
                 if ddp:
                     with self.model.no_sync():
                         self._body_fwd_bwd(store, cap)
-                    self.model.allreduce_now()
                 else:
                     self._body_fwd_bwd(store, cap)
                 self.opt.step()
