@@ -23,6 +23,21 @@ namespace hy {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
+// Packed fp32 (v_pk_fma_f32 on gfx950): two lanes of math per VALU op.  The
+// D-wide dot products and rank-1 updates of the inner loops run on float2 pairs,
+// halving the FMA instruction count (the kernels are VALU-issue bound at D = 8).
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat2(float v) { return f2{v, v}; }
+
+template <int D>
+__device__ __forceinline__ float pdot(const f2 (&a)[D / 2], const f2* __restrict__ b) {
+  f2 t = a[0] * b[0];
+#pragma unroll
+  for (int d = 1; d < D / 2; ++d) t = pfma(a[d], b[d], t);
+  return t.x + t.y;
+}
+
 template <int D>
 struct AttnCfg {
   static constexpr int KT = D <= 8 ? 64 : (D <= 16 ? 32 : 16);  // keys per wave tile
@@ -66,8 +81,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
                                                        const int* __restrict__ seg_ptr, int N, int H, int S,
                                                        float scale) {
   constexpr int KT = AttnCfg<D>::KT;
-  __shared__ float Ks[4][KT][D];
-  __shared__ float Vs[4][KT][D];
+  __shared__ __attribute__((aligned(16))) float Ks[4][KT][D];
+  __shared__ __attribute__((aligned(16))) float Vs[4][KT][D];
   __shared__ float Mrg[64][D + 2];
   const int h = blockIdx.y, sp = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -81,12 +96,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
   }
   int cb, ce;
   split_range(wave_min_i(kb), wave_max_i(ke), S, sp, KT, cb, ce);
-  float q[D], acc[D];
+  f2 q[D / 2], acc[D / 2];
   const float qs = scale * kLog2e;  // scores in log2 domain
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    q[d] = qv ? Q[(int64_t)qi * ld + h * D + d] * qs : 0.f;
-    acc[d] = 0.f;
+  for (int d = 0; d < D / 2; ++d) {
+    q[d] = qv ? f2{Q[(int64_t)qi * ld + h * D + 2 * d], Q[(int64_t)qi * ld + h * D + 2 * d + 1]} * qs : splat2(0.f);
+    acc[d] = splat2(0.f);
   }
   float m = -INFINITY, l = 0.f;
   for (int base = cb; base < ce; base += 4 * KT) {
@@ -103,9 +118,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
       float mt = -INFINITY;
 #pragma unroll
       for (int jj = 0; jj < KT; ++jj) {
-        float a = 0.f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) a = fmaf(q[d], Ks[w][jj][d], a);
+        const float a = pdot<D>(q, reinterpret_cast<const f2*>(&Ks[w][jj][0]));
         const int j = t + jj;
         s[jj] = (j >= kb && j < ke && j < ce) ? a : -INFINITY;
         mt = fmaxf(mt, s[jj]);
@@ -115,13 +128,15 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
         const float alpha = exp2f(m - mn);  // m=-inf -> 0
         l *= alpha;
 #pragma unroll
-        for (int d = 0; d < D; ++d) acc[d] *= alpha;
+        for (int d = 0; d < D / 2; ++d) acc[d] *= alpha;
 #pragma unroll
         for (int jj = 0; jj < KT; ++jj) {
           const float p = exp2f(s[jj] - mn);
           l += p;
+          const f2* vr = reinterpret_cast<const f2*>(&Vs[w][jj][0]);
+          const f2 pp = splat2(p);
 #pragma unroll
-          for (int d = 0; d < D; ++d) acc[d] = fmaf(p, Vs[w][jj][d], acc[d]);
+          for (int d = 0; d < D / 2; ++d) acc[d] = pfma(pp, vr[d], acc[d]);
         }
         m = mn;
       }
@@ -138,20 +153,134 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const float* __restrict__
         const float fs = (M > -INFINITY) ? exp2f(m - M) : 0.f;
         l = lo * fo + l * fs;
 #pragma unroll
-        for (int d = 0; d < D; ++d) acc[d] = Mrg[lane][2 + d] * fo + acc[d] * fs;
+        for (int d = 0; d < D / 2; ++d)
+          acc[d] = f2{Mrg[lane][2 + 2 * d], Mrg[lane][3 + 2 * d]} * fo + acc[d] * fs;
         m = M;
       }
       if (step < 3) {
         Mrg[lane][0] = m;
         Mrg[lane][1] = l;
 #pragma unroll
-        for (int d = 0; d < D; ++d) Mrg[lane][2 + d] = acc[d];
+        for (int d = 0; d < D / 2; ++d) {
+          Mrg[lane][2 + 2 * d] = acc[d].x;
+          Mrg[lane][3 + 2 * d] = acc[d].y;
+        }
       } else if (qv) {
         float* P = part + (((int64_t)sp * H + h) * N + qi) * (D + 2);
         P[0] = m;
         P[1] = l;
 #pragma unroll
-        for (int d = 0; d < D; ++d) P[2 + d] = acc[d];
+        for (int d = 0; d < D / 2; ++d) {
+          P[2 + 2 * d] = acc[d].x;
+          P[3 + 2 * d] = acc[d].y;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Scalar-operand variant of the forward kernel (D <= 16).  All 64 lanes of a wave
+// need every key/value row of the stripe, so instead of staging K/V through LDS
+// (64-lane broadcast ds_read_b128: 1 KB of LDS data path per 16 B used, which
+// bounded the LDS version at ~54 us for the OC20 shape) the rows are fetched with
+// wave-uniform addresses -> s_load into SGPRs, and the VALU math takes them as
+// scalar operands.  Each wave owns a contiguous quarter of the split's keys;
+// the 4 stripes are merged through LDS exactly as in attn_fwd_kernel.
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int D>
+__global__ void __launch_bounds__(256) attn_fwd_sk_kernel(const float* __restrict__ Q, const float* __restrict__ K,
+                                                          const float* __restrict__ V, int ld,
+                                                          float* __restrict__ part,
+                                                          const int* __restrict__ seg_id,
+                                                          const int* __restrict__ seg_ptr, int N, int H, int S,
+                                                          float scale) {
+  constexpr int U = 8;  // keys per online-softmax chunk
+  __shared__ float Mrg[64][D + 2];
+  const int h = blockIdx.y, sp = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
+  const int qi = blockIdx.x * 64 + lane;
+  const bool qv = qi < N;
+  int kb = INT_MAX, ke = 0;
+  if (qv) {
+    const int s = seg_id[qi];
+    kb = seg_ptr[s];
+    ke = seg_ptr[s + 1];
+  }
+  int cb, ce;
+  split_range(uniform(wave_min_i(kb)), uniform(wave_max_i(ke)), S, sp, 4 * U, cb, ce);
+  const int L4 = ((max(ce - cb, 0) + 4 * U - 1) / (4 * U)) * U;  // stripe length, multiple of U
+  const int wb = uniform(cb + w * L4), we = uniform(min(ce, wb + L4));
+  f2 q[D / 2], acc[D / 2];
+  const float qs = scale * kLog2e;  // scores in log2 domain
+#pragma unroll
+  for (int d = 0; d < D / 2; ++d) {
+    q[d] = qv ? f2{Q[(int64_t)qi * ld + h * D + 2 * d], Q[(int64_t)qi * ld + h * D + 2 * d + 1]} * qs : splat2(0.f);
+    acc[d] = splat2(0.f);
+  }
+  float m = -INFINITY, l = 0.f;
+  const int klo = max(kb, wb), khi = min(ke, we);  // this lane's valid keys in the stripe
+  for (int j0 = wb; j0 < we; j0 += U) {
+    float s[U];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(j0 + u, we - 1);  // uniform, in range
+      const f2* kr = reinterpret_cast<const f2*>(K + (int64_t)j * ld + h * D);
+      const float a = pdot<D>(q, kr);
+      s[u] = (j0 + u >= klo && j0 + u < khi) ? a : -INFINITY;
+      mt = fmaxf(mt, s[u]);
+    }
+    const float mn = fmaxf(m, mt);
+    if (mn > -INFINITY) {
+      const float alpha = exp2f(m - mn);
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) acc[d] *= alpha;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = min(j0 + u, we - 1);
+        const f2* vr = reinterpret_cast<const f2*>(V + (int64_t)j * ld + h * D);
+        const float p = exp2f(s[u] - mn);  // -inf -> 0
+        l += p;
+        const f2 pp = splat2(p);
+#pragma unroll
+        for (int d = 0; d < D / 2; ++d) acc[d] = pfma(pp, vr[d], acc[d]);
+      }
+      m = mn;
+    }
+  }
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+      if (step > 0) {
+        const float mo = Mrg[lane][0], lo = Mrg[lane][1];
+        const float M = fmaxf(m, mo);
+        const float fo = (M > -INFINITY) ? exp2f(mo - M) : 0.f;
+        const float fs = (M > -INFINITY) ? exp2f(m - M) : 0.f;
+        l = lo * fo + l * fs;
+#pragma unroll
+        for (int d = 0; d < D / 2; ++d)
+          acc[d] = f2{Mrg[lane][2 + 2 * d], Mrg[lane][3 + 2 * d]} * fo + acc[d] * fs;
+        m = M;
+      }
+      if (step < 3) {
+        Mrg[lane][0] = m;
+        Mrg[lane][1] = l;
+#pragma unroll
+        for (int d = 0; d < D / 2; ++d) {
+          Mrg[lane][2 + 2 * d] = acc[d].x;
+          Mrg[lane][3 + 2 * d] = acc[d].y;
+        }
+      } else if (qv) {
+        float* P = part + (((int64_t)sp * H + h) * N + qi) * (D + 2);
+        P[0] = m;
+        P[1] = l;
+#pragma unroll
+        for (int d = 0; d < D / 2; ++d) {
+          P[2 + 2 * d] = acc[d].x;
+          P[3 + 2 * d] = acc[d].y;
+        }
       }
     }
     __syncthreads();
@@ -208,8 +337,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
     float* __restrict__ dQ, int lddq, int64_t split_stride, const int* __restrict__ seg_id,
     const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
   constexpr int KT = AttnCfg<D>::KT;
-  __shared__ float Ks[4][KT][D];
-  __shared__ float Vs[4][KT][D];
+  __shared__ __attribute__((aligned(16))) float Ks[4][KT][D];
+  __shared__ __attribute__((aligned(16))) float Vs[4][KT][D];
   __shared__ float Mrg[64][D];
   const int h = blockIdx.y, sp = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -223,12 +352,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
   }
   int cb, ce;
   split_range(wave_min_i(kb), wave_max_i(ke), S, sp, KT, cb, ce);
-  float q[D], go[D], dq[D];
+  f2 q[D / 2], go[D / 2], dq[D / 2];
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    q[d] = qv ? Q[(int64_t)qi * ld + h * D + d] * scale : 0.f;
-    go[d] = qv ? dO[(int64_t)qi * H * D + h * D + d] : 0.f;
-    dq[d] = 0.f;
+  for (int d = 0; d < D / 2; ++d) {
+    const int64_t o = (int64_t)qi * ld + h * D + 2 * d;
+    const int64_t og = (int64_t)qi * H * D + h * D + 2 * d;
+    q[d] = qv ? f2{Q[o], Q[o + 1]} * scale : splat2(0.f);
+    go[d] = qv ? f2{dO[og], dO[og + 1]} : splat2(0.f);
+    dq[d] = splat2(0.f);
   }
   const float lse = qv ? LSE[(int64_t)h * N + qi] : 0.f;
   const float dl = qv ? delta[(int64_t)h * N + qi] : 0.f;
@@ -246,16 +377,13 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
       for (int jj = 0; jj < KT; ++jj) {
         const int j = t + jj;
         if (j >= kb && j < ke && j < ce) {
-          float sc = 0.f, dp = 0.f;
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            sc = fmaf(q[d], Ks[w][jj][d], sc);
-            dp = fmaf(go[d], Vs[w][jj][d], dp);
-          }
+          const f2* kr = reinterpret_cast<const f2*>(&Ks[w][jj][0]);
+          const float sc = pdot<D>(q, kr);
+          const float dp = pdot<D>(go, reinterpret_cast<const f2*>(&Vs[w][jj][0]));
           const float p = __expf(sc - lse);
-          const float ds = p * (dp - dl);
+          const f2 ds = splat2(p * (dp - dl));
 #pragma unroll
-          for (int d = 0; d < D; ++d) dq[d] = fmaf(ds, Ks[w][jj][d], dq[d]);
+          for (int d = 0; d < D / 2; ++d) dq[d] = pfma(ds, kr[d], dq[d]);
         }
       }
     }
@@ -264,10 +392,17 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(
   for (int step = 0; step < 4; ++step) {
     if (w == step) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const float t = (step > 0 ? Mrg[lane][d] : 0.f) + dq[d];
-        if (step < 3) Mrg[lane][d] = t;
-        else if (qv) dQ[sp * split_stride + (int64_t)qi * lddq + h * D + d] = t * scale;
+      for (int d = 0; d < D / 2; ++d) {
+        const float t0 = (step > 0 ? Mrg[lane][2 * d] : 0.f) + dq[d].x;
+        const float t1 = (step > 0 ? Mrg[lane][2 * d + 1] : 0.f) + dq[d].y;
+        if (step < 3) {
+          Mrg[lane][2 * d] = t0;
+          Mrg[lane][2 * d + 1] = t1;
+        } else if (qv) {
+          float* o = dQ + sp * split_stride + (int64_t)qi * lddq + h * D + 2 * d;
+          o[0] = t0 * scale;
+          o[1] = t1 * scale;
+        }
       }
     }
     __syncthreads();
@@ -282,8 +417,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
     float* __restrict__ dK, float* __restrict__ dV, int lddkv, int64_t split_stride,
     const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
   constexpr int QT = AttnCfg<D>::KT;
-  __shared__ float Qs[4][QT][D];
-  __shared__ float Gs[4][QT][D];
+  __shared__ __attribute__((aligned(16))) float Qs[4][QT][D];
+  __shared__ __attribute__((aligned(16))) float Gs[4][QT][D];
   __shared__ float Ls[4][QT][2];
   __shared__ float Mrg[64][2 * D];
   const int h = blockIdx.y, sp = blockIdx.z;
@@ -298,13 +433,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
   }
   int cb, ce;
   split_range(wave_min_i(qb), wave_max_i(qe), S, sp, QT, cb, ce);
-  float k[D], v[D], dk[D], dv[D];
+  f2 k[D / 2], v[D / 2], dk[D / 2], dv[D / 2];
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    k[d] = kv ? K[(int64_t)kj * ld + h * D + d] * scale : 0.f;
-    v[d] = kv ? V[(int64_t)kj * ld + h * D + d] : 0.f;
-    dk[d] = 0.f;
-    dv[d] = 0.f;
+  for (int d = 0; d < D / 2; ++d) {
+    const int64_t o = (int64_t)kj * ld + h * D + 2 * d;
+    k[d] = kv ? f2{K[o], K[o + 1]} * scale : splat2(0.f);
+    v[d] = kv ? f2{V[o], V[o + 1]} : splat2(0.f);
+    dk[d] = splat2(0.f);
+    dv[d] = splat2(0.f);
   }
   for (int base = cb; base < ce; base += 4 * QT) {
     const int t = base + w * QT;
@@ -326,18 +462,17 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
       for (int ii = 0; ii < QT; ++ii) {
         const int i = t + ii;
         if (i >= qb && i < qe && i < ce) {
-          float sc = 0.f, dp = 0.f;
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-            sc = fmaf(Qs[w][ii][d], k[d], sc);
-            dp = fmaf(Gs[w][ii][d], v[d], dp);
-          }
+          const f2* qr = reinterpret_cast<const f2*>(&Qs[w][ii][0]);
+          const f2* gr = reinterpret_cast<const f2*>(&Gs[w][ii][0]);
+          const float sc = pdot<D>(k, qr);
+          const float dp = pdot<D>(v, gr);
           const float p = __expf(sc - Ls[w][ii][0]);
-          const float ds = p * (dp - Ls[w][ii][1]);
+          const f2 pp = splat2(p);
+          const f2 ds = splat2(p * (dp - Ls[w][ii][1]));
 #pragma unroll
-          for (int d = 0; d < D; ++d) {
-            dv[d] = fmaf(p, Gs[w][ii][d], dv[d]);
-            dk[d] = fmaf(ds, Qs[w][ii][d], dk[d]);
+          for (int d = 0; d < D / 2; ++d) {
+            dv[d] = pfma(pp, gr[d], dv[d]);
+            dk[d] = pfma(ds, qr[d], dk[d]);
           }
         }
       }
@@ -347,15 +482,165 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(
   for (int step = 0; step < 4; ++step) {
     if (w == step) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const float tk = (step > 0 ? Mrg[lane][d] : 0.f) + dk[d];
-        const float tv = (step > 0 ? Mrg[lane][D + d] : 0.f) + dv[d];
+      for (int d = 0; d < D / 2; ++d) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = 2 * d + e;
+          const float tk = (step > 0 ? Mrg[lane][c] : 0.f) + (e ? dk[d].y : dk[d].x);
+          const float tv = (step > 0 ? Mrg[lane][D + c] : 0.f) + (e ? dv[d].y : dv[d].x);
+          if (step < 3) {
+            Mrg[lane][c] = tk;
+            Mrg[lane][D + c] = tv;
+          } else if (kv) {
+            dK[sp * split_stride + (int64_t)kj * lddkv + h * D + c] = tk * scale;
+            dV[sp * split_stride + (int64_t)kj * lddkv + h * D + c] = tv;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Scalar-operand backward kernels (D <= 16), same stripe structure as attn_fwd_sk_kernel.
+template <int D>
+__global__ void __launch_bounds__(256) attn_bwd_dq_sk_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
+    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    float* __restrict__ dQ, int lddq, int64_t split_stride, const int* __restrict__ seg_id,
+    const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
+  constexpr int U = 8;
+  __shared__ float Mrg[64][D];
+  const int h = blockIdx.y, sp = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
+  const int qi = blockIdx.x * 64 + lane;
+  const bool qv = qi < N;
+  int kb = INT_MAX, ke = 0;
+  if (qv) {
+    const int s = seg_id[qi];
+    kb = seg_ptr[s];
+    ke = seg_ptr[s + 1];
+  }
+  int cb, ce;
+  split_range(uniform(wave_min_i(kb)), uniform(wave_max_i(ke)), S, sp, 4 * U, cb, ce);
+  const int L4 = ((max(ce - cb, 0) + 4 * U - 1) / (4 * U)) * U;
+  const int wb = uniform(cb + w * L4), we = uniform(min(ce, wb + L4));
+  f2 q[D / 2], go[D / 2], dq[D / 2];
+#pragma unroll
+  for (int d = 0; d < D / 2; ++d) {
+    const int64_t o = (int64_t)qi * ld + h * D + 2 * d;
+    const int64_t og = (int64_t)qi * H * D + h * D + 2 * d;
+    q[d] = qv ? f2{Q[o], Q[o + 1]} * scale : splat2(0.f);
+    go[d] = qv ? f2{dO[og], dO[og + 1]} : splat2(0.f);
+    dq[d] = splat2(0.f);
+  }
+  const float lse = qv ? LSE[(int64_t)h * N + qi] : 0.f;
+  const float dl = qv ? delta[(int64_t)h * N + qi] : 0.f;
+  const int klo = max(kb, wb), khi = min(ke, we);
+  for (int j0 = wb; j0 < we; j0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(j0 + u, we - 1);
+      const f2* kr = reinterpret_cast<const f2*>(K + (int64_t)j * ld + h * D);
+      const f2* vr = reinterpret_cast<const f2*>(V + (int64_t)j * ld + h * D);
+      const float sc = pdot<D>(q, kr);
+      const float dp = pdot<D>(go, vr);
+      const bool ok = j0 + u >= klo && j0 + u < khi;
+      const float p = ok ? __expf(sc - lse) : 0.f;
+      const f2 ds = splat2(p * (dp - dl));
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) dq[d] = pfma(ds, kr[d], dq[d]);
+    }
+  }
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) {
+        const float t0 = (step > 0 ? Mrg[lane][2 * d] : 0.f) + dq[d].x;
+        const float t1 = (step > 0 ? Mrg[lane][2 * d + 1] : 0.f) + dq[d].y;
         if (step < 3) {
-          Mrg[lane][d] = tk;
-          Mrg[lane][D + d] = tv;
-        } else if (kv) {
-          dK[sp * split_stride + (int64_t)kj * lddkv + h * D + d] = tk * scale;
-          dV[sp * split_stride + (int64_t)kj * lddkv + h * D + d] = tv;
+          Mrg[lane][2 * d] = t0;
+          Mrg[lane][2 * d + 1] = t1;
+        } else if (qv) {
+          float* o = dQ + sp * split_stride + (int64_t)qi * lddq + h * D + 2 * d;
+          o[0] = t0 * scale;
+          o[1] = t1 * scale;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) attn_bwd_dkv_sk_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int ld,
+    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    float* __restrict__ dK, float* __restrict__ dV, int lddkv, int64_t split_stride,
+    const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int N, int H, int S, float scale) {
+  constexpr int U = 8;
+  __shared__ float Mrg[64][2 * D];
+  const int h = blockIdx.y, sp = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
+  const int kj = blockIdx.x * 64 + lane;
+  const bool kv = kj < N;
+  int qb = INT_MAX, qe = 0;
+  if (kv) {
+    const int s = seg_id[kj];
+    qb = seg_ptr[s];
+    qe = seg_ptr[s + 1];
+  }
+  int cb, ce;
+  split_range(uniform(wave_min_i(qb)), uniform(wave_max_i(qe)), S, sp, 4 * U, cb, ce);
+  const int L4 = ((max(ce - cb, 0) + 4 * U - 1) / (4 * U)) * U;
+  const int wb = uniform(cb + w * L4), we = uniform(min(ce, wb + L4));
+  f2 k[D / 2], v[D / 2], dk[D / 2], dv[D / 2];
+#pragma unroll
+  for (int d = 0; d < D / 2; ++d) {
+    const int64_t o = (int64_t)kj * ld + h * D + 2 * d;
+    k[d] = kv ? f2{K[o], K[o + 1]} * scale : splat2(0.f);
+    v[d] = kv ? f2{V[o], V[o + 1]} : splat2(0.f);
+    dk[d] = splat2(0.f);
+    dv[d] = splat2(0.f);
+  }
+  const int ilo = max(qb, wb), ihi = min(qe, we);
+  const float* Lh = LSE + (int64_t)h * N;
+  const float* Dh = delta + (int64_t)h * N;
+  for (int i0 = wb; i0 < we; i0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u, we - 1);
+      const f2* qr = reinterpret_cast<const f2*>(Q + (int64_t)i * ld + h * D);
+      const f2* gr = reinterpret_cast<const f2*>(dO + (int64_t)i * H * D + h * D);
+      const float sc = pdot<D>(k, qr);
+      const float dp = pdot<D>(v, gr);
+      const bool ok = i0 + u >= ilo && i0 + u < ihi;
+      const float p = ok ? __expf(sc - Lh[i]) : 0.f;
+      const f2 pp = splat2(p);
+      const f2 ds = splat2(p * (dp - Dh[i]));
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) {
+        dv[d] = pfma(pp, gr[d], dv[d]);
+        dk[d] = pfma(ds, qr[d], dk[d]);
+      }
+    }
+  }
+  for (int step = 0; step < 4; ++step) {
+    if (w == step) {
+#pragma unroll
+      for (int d = 0; d < D / 2; ++d) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = 2 * d + e;
+          const float tk = (step > 0 ? Mrg[lane][c] : 0.f) + (e ? dk[d].y : dk[d].x);
+          const float tv = (step > 0 ? Mrg[lane][D + c] : 0.f) + (e ? dv[d].y : dv[d].x);
+          if (step < 3) {
+            Mrg[lane][c] = tk;
+            Mrg[lane][D + c] = tv;
+          } else if (kv) {
+            dK[sp * split_stride + (int64_t)kj * lddkv + h * D + c] = tk * scale;
+            dV[sp * split_stride + (int64_t)kj * lddkv + h * D + c] = tv;
+          }
         }
       }
     }
@@ -394,6 +679,23 @@ __global__ void __launch_bounds__(256) attn_bwd_sum_kernel(const float4* __restr
     default: HY_CHECK(false, "attention head_dim must be one of 4,8,16,32,64, got ", D); \
   }
 
+// HYDRA_ATTN_LDS=1 selects the LDS-staged kernels for every head size (A/B testing).
+static bool attn_scalar_path() {
+  static const bool v = [] {
+    const char* e = std::getenv("HYDRA_ATTN_LDS");
+    return !(e && e[0] == '1');
+  }();
+  return v;
+}
+
+static bool attn_scalar_bwd() {
+  static const bool v = [] {
+    const char* e = std::getenv("HYDRA_ATTN_SCALAR_BWD");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 static int attn_keytile(int D) { return D <= 8 ? 64 : (D <= 16 ? 32 : 16); }
 
 // Number of key (or query) splits: enough workgroups to fill the chip (~6 per CU at
@@ -431,14 +733,29 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const at::Ten
   auto part = at::empty({(int64_t)S * H * N * (D + 2)}, qkv.options());
   dim3 grid(ceil_div(N, 64), H, S);
   HY_ATTN_DISPATCH(D, {
-    attn_fwd_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, part.data_ptr<float>(),
-                                                    seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H,
-                                                    S, (float)scale);
+    if (kD <= 16 && attn_scalar_path())
+      attn_fwd_sk_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, part.data_ptr<float>(),
+                                                         seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N,
+                                                         (int)H, S, (float)scale);
+    else
+      attn_fwd_kernel<kD><<<grid, 256, 0, stream()>>>(base, base + F, base + 2 * F, ld, part.data_ptr<float>(),
+                                                      seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H,
+                                                      S, (float)scale);
     attn_fwd_combine_kernel<kD><<<ceil_div(N * H, 256), 256, 0, stream()>>>(
         part.data_ptr<float>(), O.data_ptr<float>(), LSE.data_ptr<float>(), (int)N, (int)H, S);
   });
   return {O, LSE};
 }
+
+// kernel selection for the backward: scalar-operand kernels for D <= 16
+// (measured on MI355X, N=2560, H=8, D=8: the scalar-operand backward is slower —
+// 184 vs 130 us — so it is opt-in via HYDRA_ATTN_SCALAR_BWD=1; the forward gains ~10%)
+#define HY_DQ(kD)                                                                            \
+  ((kD) <= 16 && attn_scalar_bwd() ? attn_bwd_dq_sk_kernel<kD> : attn_bwd_dq_kernel<kD>) \
+      <<<grid, 256, 0, stream()>>>
+#define HY_DKV(kD)                                                                               \
+  ((kD) <= 16 && attn_scalar_bwd() ? attn_bwd_dkv_sk_kernel<kD> : attn_bwd_dkv_kernel<kD>) \
+      <<<grid, 256, 0, stream()>>>
 
 at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tensor& O, const at::Tensor& LSE,
                     const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t H, double scale, int64_t max_span,
@@ -460,10 +777,10 @@ at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tens
   dim3 grid(ceil_div(N, 64), H, S);
   if (S == 1) {
     HY_ATTN_DISPATCH(D, {
-      attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(
+      HY_DQ(kD)(
           base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
           dbase, (int)(3 * F), 0, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, 1, (float)scale);
-      attn_bwd_dkv_kernel<kD><<<grid, 256, 0, stream()>>>(
+      HY_DKV(kD)(
           base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
           dbase + F, dbase + 2 * F, (int)(3 * F), 0, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N,
           (int)H, 1, (float)scale);
@@ -473,11 +790,11 @@ at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tens
   auto pq = at::empty({(int64_t)S * N * F}, qkv.options());
   auto pkv = at::empty({(int64_t)S * N * 2 * F}, qkv.options());
   HY_ATTN_DISPATCH(D, {
-    attn_bwd_dq_kernel<kD><<<grid, 256, 0, stream()>>>(
+    HY_DQ(kD)(
         base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
         pq.data_ptr<float>(), (int)F, N * F, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, S,
         (float)scale);
-    attn_bwd_dkv_kernel<kD><<<grid, 256, 0, stream()>>>(
+    HY_DKV(kD)(
         base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(), delta.data_ptr<float>(),
         pkv.data_ptr<float>(), pkv.data_ptr<float>() + F, (int)(2 * F), N * 2 * F, seg_id.data_ptr<int>(),
         seg_ptr.data_ptr<int>(), (int)N, (int)H, S, (float)scale);

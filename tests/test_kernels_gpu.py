@@ -161,6 +161,19 @@ def test_attention_key_splits(splits, scope):
     torch.testing.assert_close(dqkv.cpu(), qc.grad, rtol=2e-4, atol=2e-4)
 
 
+def test_attention_scalar_backward_kernels():
+    """The opt-in scalar-operand backward kernels (HYDRA_ATTN_SCALAR_BWD=1) in a subprocess."""
+    import subprocess
+    import sys
+
+    code = ("import torch, sys; sys.path.insert(0, '.'); from tests.test_kernels_gpu import test_attention_key_splits;"
+            "[test_attention_key_splits(s, sc) for s in (1, 5) for sc in ('batch', 'graph')]; print('ok')")
+    env = dict(__import__("os").environ, HYDRA_ATTN_SCALAR_BWD="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
 def test_fused_adamw_matches_cpu():
     from hydragnn_amd.optim.adamw import FusedAdamW
 

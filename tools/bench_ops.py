@@ -43,8 +43,8 @@ def bench_wgrad():
     ops = _native.ops()
     x0 = torch.zeros(256, device="cuda")
     print(f"floor: fill(256) in graph {graph_time(lambda: x0.fill_(1.0)):.2f} us", flush=True)
-    for M, O, I in [(2816, 64, 64), (22528, 64, 64), (2816, 64, 1088), (2816, 192, 64), (22528, 64, 65),
-                    (2816, 128, 64)]:
+    for M, O, I in [(2560, 64, 64), (2560, 128, 64), (2560, 64, 1088), (2560, 192, 64), (2560, 64, 128),
+                    (22528, 64, 64), (22528, 64, 6), (22528, 64, 1), (22528, 64, 65)]:
         dy = torch.randn(M, O, device="cuda")
         x = torch.randn(M, I, device="cuda")
         t_k = graph_time(lambda: ops.linear_wgrad(dy, x, True))
