@@ -78,18 +78,24 @@ class DistributedDataParallel(nn.Module):
                 p.register_post_accumulate_grad_hook(self._make_hook(bi, off))
 
     # ------------------------------------------------------------------ state
+    def _src(self):
+        """Global rank of the group's first member (torch.distributed takes global src ranks)."""
+        if self.process_group is None or self.process_group == dist.group.WORLD:
+            return 0
+        return dist.get_global_rank(self.process_group, 0)
+
     def _broadcast_module_state(self):
         if self.world <= 1:
             return
         with torch.no_grad():
             for t in list(self.module.parameters()) + list(self.module.buffers()):
-                dist.broadcast(t.data, src=0, group=self.process_group)
+                dist.broadcast(t.data, src=self._src(), group=self.process_group)
 
     def _sync_buffers(self):
         if self.broadcast_buffers and self.world > 1:
             with torch.no_grad():
                 for b in self.module.buffers():
-                    dist.broadcast(b.data, src=0, group=self.process_group)
+                    dist.broadcast(b.data, src=self._src(), group=self.process_group)
 
     # ------------------------------------------------------------------ hooks
     def _make_hook(self, bi, off):

@@ -34,11 +34,21 @@ def _module(model):
     return model.module if hasattr(model, "module") else model
 
 
-def get_nbatch(loader):
+def get_nbatch(loader, synchronize=False):
+    """Batches per epoch (``train_validate_test.py:39-49``).  With ``synchronize`` the count is
+    the minimum over ranks: every training batch runs gradient collectives, so ranks whose
+    loaders differ in length (task-parallel branches over datasets of different sizes)
+    must stop together or their collective sequences diverge."""
     nbatch = len(loader)
     env = os.getenv("HYDRAGNN_MAX_NUM_BATCH")
     if env is not None:
         nbatch = min(nbatch, int(env))
+    if synchronize and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        from ..parallel.distributed import host_group
+
+        t = torch.tensor([nbatch], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
+        nbatch = int(t.item())
     return nbatch
 
 
@@ -101,7 +111,7 @@ def train(loader, model, opt, verbosity, profiler=None, use_deepspeed=False, com
     tasks_error = torch.zeros(module.num_heads, device=device)
     num_samples = 0
     model.train()
-    nbatch = get_nbatch(loader)
+    nbatch = get_nbatch(loader, synchronize=True)
     trace_level = int(os.getenv("HYDRAGNN_TRACE_LEVEL", "0"))
     sync = {"cudasync": trace_level > 0}
     use_engine = step_engine is not None and isinstance(loader, DeviceGraphLoader) and not compute_grad_energy

@@ -69,8 +69,16 @@ def _state_dict_with_prefix(model):
 
 
 def save_model(model, optimizer, name, path="./logs/", use_deepspeed=False):
-    """Rank-0 save in the reference ``.pk`` layout (``model.py:63-106``)."""
+    """Rank-0 save in the reference ``.pk`` layout (``model.py:63-106``).  A task-parallel
+    model (``MultiTaskModelMP``) saves from rank 0 of every branch group instead, so each
+    branch checkpoint is written once (reference ``model.py:70-77``)."""
     rank = dist.get_rank() if dist.is_initialized() else 0
+    head_pg = getattr(model, "head_pg", None)
+    if head_pg is not None and dist.is_initialized():
+        rank = dist.get_rank(head_pg)
+        suffix = f"_branch{model.branch_id}"
+        if not name.endswith(suffix):
+            name = name + suffix
     if optimizer is not None and hasattr(optimizer, "consolidate_state_dict"):
         optimizer.consolidate_state_dict()
     if rank != 0:

@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2, CPU) tests of the data-parallel runtime.
+"""Multi-process (gloo, CPU) tests of the data- and task-parallel runtime.
 
 The reference runs its whole suite a second time under ``mpirun -n 2`` with gloo
 (``.github/workflows/CI.yml:55-56``); here each test spawns 2 ranks with
@@ -6,7 +6,8 @@ The reference runs its whole suite a second time under ``mpirun -n 2`` with gloo
 backward-overlapped all-reduce (``parallel/ddp.py``) == full-batch gradients;
 the padded/captured train-step sync structure keeps ranks bit-identical; ZeRO-1
 == AdamW; SyncBatchNorm == BatchNorm over the concatenated batch; metric
-reductions; and an end-to-end 2-rank ``run_training`` on the CI data.
+reductions; task-parallel MultiTaskModelMP over 4 ranks / 2 branches; and an
+end-to-end 2-rank ``run_training`` on the CI data.
 """
 import os
 import socket
@@ -190,6 +191,43 @@ def _train_body(rank, world, workdir):
                          overwrite_config={"NeuralNetwork": {"Training": {"num_epoch": 30}}})
 
 
+def _task_parallel_body(rank, world):
+    from hydragnn_amd.data.graph import collate
+    from hydragnn_amd.data.synthetic import degree_histogram, oc20_like
+    from hydragnn_amd.models.create import create_model
+    from hydragnn_amd.models.multitask import MultiTaskModelMP, branch_groups
+
+    bid, group, lists = branch_groups([3, 1])
+    assert lists == [[0, 1, 2], [3]]
+    samples = oc20_like(8, seed=20 + rank, radius=5.0, max_neighbours=8, pe_dim=2, min_atoms=5, max_atoms=10)
+    for g in samples:
+        g.dataset_name = torch.tensor([[bid]])
+    heads = {"graph": [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                                  "num_headlayers": 1, "dim_headlayers": [8]}}
+                       for b in range(2)]}
+    torch.manual_seed(0)
+    base = create_model("EGNN", 4, 12, [1], 2, "", "multihead", 1, ["graph"], heads, "relu", "mse", [1.0], 2,
+                        use_gpu=False, edge_dim=None, dropout=0.0)
+    model = MultiTaskModelMP(base, bid, group)
+    names = [n for n, _ in model.named_parameters()]
+    assert not any(f"branch-{1 - bid}" in n for n in names), "other branch not pruned"
+    b = collate(samples)
+    pred = model(b)
+    pred[0].pow(2).mean().backward()
+    enc = torch.cat([p.grad.reshape(-1) for n, p in model.named_parameters()
+                     if not n.startswith(("graph_shared", "heads_NN"))])
+    dec = torch.cat([p.grad.reshape(-1) for n, p in model.named_parameters()
+                     if n.startswith(("graph_shared", "heads_NN"))])
+    allenc = [torch.empty_like(enc) for _ in range(world)]
+    dist.all_gather(allenc, enc)
+    for t in allenc[1:]:
+        torch.testing.assert_close(t, allenc[0])
+    alldec = [torch.empty_like(dec) for _ in range(world)]
+    dist.all_gather(alldec, dec)  # branch 0's ranks agree with each other
+    for r in lists[bid]:
+        torch.testing.assert_close(alldec[r], dec)
+
+
 # ---------------------------------------------------------------------------- tests
 
 def test_ddp_bucketed_allreduce_matches_full_batch():
@@ -210,6 +248,10 @@ def test_syncbatchnorm_matches_full_batch():
 
 def test_metric_reductions():
     run_ranks("_reduce_body")
+
+
+def test_task_parallel_multibranch_four_ranks():
+    run_ranks("_task_parallel_body", world=4)
 
 
 @pytest.mark.slow

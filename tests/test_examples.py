@@ -1,0 +1,80 @@
+"""Example smoke tests (reference ``tests/test_examples.py``: qm9 / md17 / LennardJones
+drivers run as subprocesses).  Tiny sample counts and 1-2 epochs: they check that
+each driver's data generation, config and training path run end to end on CPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(ROOT, "examples")
+
+
+def _run(script, args, tmp_path, nproc=1, timeout=600):
+    env = dict(os.environ, HYDRAGNN_DEVICE_DATA="0", OMP_NUM_THREADS="2")
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(EX, script), "--workdir", str(tmp_path)] + args
+        env["HYDRAGNN_MASTER_PORT"] = str(29000 + (abs(hash(script + str(args))) % 2000))
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", f"--master-port={31000 + abs(hash(script)) % 2000}",
+               os.path.join(EX, script)] + args
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def _result(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("mpnn_type", ["SchNet", "PNA", "EGNN"])
+def test_qm9(mpnn_type, tmp_path):
+    r = _result(_run("qm9/qm9.py", ["--num_samples", "40", "--num_epoch", "1", "--mpnn_type", mpnn_type], tmp_path))
+    assert r["test_error"] == r["test_error"]  # finite, not NaN
+
+
+def test_md17_graph_energy(tmp_path):
+    r = _result(_run("md17/md17.py", ["--num_samples", "30", "--num_epoch", "1"], tmp_path))
+    assert r["test_error"] == r["test_error"]
+
+
+@pytest.mark.parametrize("mpnn_type", ["PAINN", "SchNet"])
+def test_md17_forces(mpnn_type, tmp_path):
+    r = _result(_run("md17/md17.py", ["--inputfile", "md17_forces.json", "--num_samples", "24", "--num_epoch", "2",
+                                      "--mpnn_type", mpnn_type], tmp_path))
+    assert r["test_error"] == r["test_error"]
+
+
+@pytest.mark.parametrize("mpnn_type", ["DimeNet", "EGNN"])
+def test_lennard_jones_forces(mpnn_type, tmp_path):
+    r = _result(_run("LennardJones/lj.py", ["--num_samples", "20", "--num_epoch", "2", "--mpnn_type", mpnn_type],
+                     tmp_path))
+    assert r["test_error"] == r["test_error"]
+
+
+@pytest.mark.parametrize("cfg", ["open_catalyst_energy.json", "open_catalyst_gps.json"])
+def test_open_catalyst(cfg, tmp_path):
+    r = _result(_run("open_catalyst_2020/train.py", ["--inputfile", cfg, "--num_samples", "24", "--num_epoch", "1"],
+                     tmp_path))
+    assert r["test_error"] == r["test_error"]
+
+
+def test_multibranch_data_parallel(tmp_path):
+    r = _result(_run("multibranch/train.py", ["--num_samples", "40", "--num_epoch", "1"], tmp_path))
+    assert len(r["task_errors"]) == 2
+
+
+def test_multibranch_task_parallel_three_ranks(tmp_path):
+    _run("multibranch/train.py", ["--task_parallel", "--num_samples", "40", "--num_epoch", "1"], tmp_path, nproc=3)
+    logs = os.listdir(os.path.join(tmp_path, "logs"))
+    assert sum(1 for d in logs if "_branch" in d) == 3
+
+
+@pytest.mark.slow
+def test_lsms(tmp_path):
+    r = _result(_run("lsms/lsms.py", ["--num_samples", "300", "--num_epoch", "2"], tmp_path))
+    assert len(r["task_errors"]) == 3
