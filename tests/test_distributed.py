@@ -38,7 +38,13 @@ def _entry(rank, world, port, fn_name, args, errq):
                           LOCAL_RANK=str(rank), HYDRAGNN_BACKEND="gloo", HYDRAGNN_MASTER_PORT=str(port))
         torch.set_num_threads(2)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        globals()[fn_name](rank, world, *args)
+        fn = globals().get(fn_name)
+        if fn is None:  # bodies defined in other test modules: "module:function"
+            import importlib
+
+            mod, _, name = fn_name.partition(":")
+            fn = getattr(importlib.import_module(mod), name)
+        fn(rank, world, *args)
         dist.barrier()
         dist.destroy_process_group()
     except Exception:  # noqa: BLE001
