@@ -102,6 +102,11 @@ class SphericalBasisLayer(nn.Module):
 def triplets_csr(dst_si, src_si, num_nodes):
     """(idx_kj, idx_ji) for all k->j->i with k != i, grouped by e_ji (ascending)."""
     dev = dst_si.rowptr.device
+    if dst_si.rowptr.is_cuda:  # HIP count/scan/fill builder (csrc/graph.hip), same order as below
+        from .. import _native
+
+        ei = torch.stack([src_si.index.long(), dst_si.index.long()], 0)
+        return _native.ops().triplets(ei, dst_si.rowptr.to(torch.int32))
     src = src_si.index.long()
     dst = dst_si.index.long()
     rowptr = dst_si.rowptr.long()

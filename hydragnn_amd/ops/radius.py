@@ -11,12 +11,56 @@ import torch
 from .segment import SegIndex
 
 
+def _graph_ptr(batch, n):
+    """node->graph ids (contiguous graphs) -> (node_graph int32, gptr int32 [G+1])."""
+    b = batch.to(torch.int32)
+    G = int(batch.max()) + 1 if n else 0
+    counts = torch.bincount(batch.long(), minlength=G)
+    gptr = torch.zeros(G + 1, dtype=torch.int32, device=batch.device)
+    gptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return b, gptr
+
+
+def pbc_reps(cell, pbc, r):
+    """Periodic image extents per graph: ceil(r / lattice-plane spacing) on periodic axes.
+    cell [G, 3, 3] (rows = lattice vectors), pbc [G, 3] bool -> int32 [G, 3]."""
+    cell = cell.double().view(-1, 3, 3)
+    vol = torch.det(cell).abs()
+    reps = []
+    for a in range(3):
+        b, c = cell[:, (a + 1) % 3], cell[:, (a + 2) % 3]
+        h = vol / torch.linalg.norm(torch.cross(b, c, dim=1), dim=1)
+        reps.append(torch.ceil(r / h))
+    out = torch.stack(reps, 1).to(torch.int32)
+    return out * torch.as_tensor(pbc, device=out.device).view(-1, 3).to(torch.int32)
+
+
+def radius_graph_device(pos, batch, r, max_num_neighbors=32, loop=False, cap_policy="index", cell=None,
+                        reps=None):
+    """HIP radius graph (``csrc/graph.hip``): (edge_index [2, E], shifts [E, 3] or None).
+
+    ``cell`` [G, 3, 3] / ``reps`` [G, 3] enable periodic images per graph; ``cap_policy``
+    "index" (torch_cluster: first sources in index order) or "nearest" (RadiusGraphPBC)."""
+    from .. import _native
+
+    n = pos.shape[0]
+    if batch is None:
+        batch = torch.zeros(n, dtype=torch.long, device=pos.device)
+    node_graph, gptr = _graph_ptr(batch.to(pos.device), n)
+    k = -1 if max_num_neighbors is None else int(max_num_neighbors)
+    ei, sh = _native.ops().radius_graph(pos.detach(), node_graph, gptr, float(r), k, bool(loop),
+                                        cap_policy == "nearest", cell, reps)
+    return ei, (sh if cell is not None else None)
+
+
 def radius_edges(pos, batch, r, max_num_neighbors=32, loop=False, chunk=4096):
     """edge_index [2, E] (row 0 = source j, row 1 = receiver i), sorted by receiver."""
     n = pos.shape[0]
     dev = pos.device
     if n == 0:
         return torch.zeros(2, 0, dtype=torch.long, device=dev)
+    if pos.is_cuda:  # HIP two-pass builder; same cap semantics as the torch path below
+        return radius_graph_device(pos, batch, r, max_num_neighbors, loop)[0]
     if batch is None:
         batch = torch.zeros(n, dtype=torch.long, device=dev)
     batch = batch.to(dev).long()
