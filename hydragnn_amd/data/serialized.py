@@ -112,14 +112,17 @@ class SerializedDataLoader:
             from ..parallel.distributed import comm_reduce
 
             mx = float(comm_reduce(torch.tensor([mx], dtype=torch.float64), dist.ReduceOp.MAX)[0])
-        for d in dataset:
+        pes = None
+        if self.pe_dim:  # all Laplacians in one batched launch on the GPU (HIP Jacobi), host otherwise
+            pes = T.laplacian_pe_batch(dataset, self.pe_dim, device="cuda" if torch.cuda.is_available() else None)
+        for i, d in enumerate(dataset):
             d.edge_attr = (d.edge_attr / mx).to(torch.float32)
             if self.spherical:
                 d.edge_attr = torch.cat([d.edge_attr, T.spherical(d.pos, d.edge_index)], -1)
             if self.ppf and d.get("normal") is not None:
                 d.edge_attr = torch.cat([d.edge_attr, T.point_pair_features(d.pos, d.normal, d.edge_index)], -1)
             if self.pe_dim:
-                d.pe = T.laplacian_pe(d.edge_index, d.num_nodes, self.pe_dim)
+                d.pe = pes[i]
                 d.rel_pe = T.relative_pe(d.pe, d.edge_index)
             update_predicted_values(self.types, self.output_index, self.graph_feature_dim, self.node_feature_dim, d)
             update_atom_features(self.input_node_features, d)

@@ -125,3 +125,51 @@ def test_triplets_hip():
     g = b.to("cuda")
     kj2, ji2 = triplets_csr(g.dst_si, g.src_si, g.num_nodes)
     assert torch.equal(kj2.cpu(), kj) and torch.equal(ji2.cpu(), ji)
+
+
+def _lap(ei, n):
+    A = torch.zeros(n, n, dtype=torch.float64)
+    A[ei[1], ei[0]] = 1.0
+    A[ei[0], ei[1]] = 1.0
+    d = A.sum(1)
+    di = torch.where(d > 0, d.clamp(min=1e-12).rsqrt(), torch.zeros_like(d))
+    return torch.eye(n, dtype=torch.float64) - di[:, None] * A * di[None, :]
+
+
+def test_laplacian_pe_host():
+    from hydragnn_amd.data.synthetic import oc20_like
+    from hydragnn_amd.data.transforms import laplacian_pe
+
+    s = oc20_like(1, seed=1, min_atoms=12, max_atoms=12, radius=5.0, max_neighbours=6, pe_dim=1)[0]
+    pe = laplacian_pe(s.edge_index, s.num_nodes, 4, seed=0).double()
+    L = _lap(s.edge_index, s.num_nodes)
+    lam = torch.linalg.eigvalsh(L)[1:5]
+    for c in range(4):
+        v = pe[:, c]
+        torch.testing.assert_close(L @ v, lam[c] * v, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_laplacian_pe_hip_jacobi():
+    """Batched Jacobi eigenvectors: unit norm, L v = lambda v with the eigenvalues of the
+    host solver (subspace-exact for degenerate eigenvalues), zero padding for tiny graphs."""
+    from hydragnn_amd.data.synthetic import oc20_like
+    from hydragnn_amd.data.transforms import laplacian_pe_batch
+
+    samples = oc20_like(12, seed=4, min_atoms=2, max_atoms=126, radius=6.0, max_neighbours=8, pe_dim=1)
+    k = 6
+    pes = laplacian_pe_batch(samples, k, seed=0, device="cuda")
+    for s, pe in zip(samples, pes):
+        n = s.num_nodes
+        L = _lap(s.edge_index, n)
+        lam = torch.linalg.eigvalsh(L)
+        pe = pe.double()
+        for c in range(k):
+            v = pe[:, c]
+            if c + 1 >= n:
+                assert float(v.abs().max()) == 0.0
+                continue
+            assert abs(float(v.norm()) - 1.0) < 1e-3
+            lv = float(v @ L @ v)
+            assert abs(lv - float(lam[c + 1])) < 1e-3, (n, c, lv, float(lam[c + 1]))
+            assert float((L @ v - lv * v).norm()) < 5e-3
