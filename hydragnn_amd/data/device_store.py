@@ -301,13 +301,38 @@ class DeviceGraphStore:
                 s["dataset_ids_host"] = host_ids
         return b
 
+    def branch_order(self, indices):
+        """Stable-sort a batch's sample indices by ``dataset_name`` and return
+        (indices, [(ID, g0, g1)], [(ID, n0, n1)]): every branch's graphs (and their
+        nodes) become one contiguous range, known on the host (multi-branch decode
+        without masks / host syncs)."""
+        idx = np.asarray(indices, dtype=np.int64)
+        dn = self.dataset_name[idx]
+        order = np.argsort(dn, kind="stable")
+        idx, dn = idx[order], dn[order]
+        nn_ = self.n_nodes[idx]
+        gr, nr = [], []
+        g0, n0 = 0, 0
+        for ID in np.unique(dn):
+            c = int((dn == ID).sum())
+            m = int(nn_[g0:g0 + c].sum())
+            gr.append((int(ID), g0, g0 + c))
+            nr.append((int(ID), n0, n0 + m))
+            g0, n0 = g0 + c, n0 + m
+        return idx.tolist(), gr, nr
+
     def batch(self, indices, Np=None, Ep=None, Gp=None):
+        host_ids, ranges = None, None
+        if self.dataset_name is not None:
+            indices, gr, nr = self.branch_order(indices)
+            host_ids = [g[0] for g in gr]
+            ranges = (gr, nr)
         lay = self.layout(indices, Np, Ep, Gp)
         dev = self.upload(indices, lay)
-        host_ids = None
-        if self.dataset_name is not None:
-            host_ids = sorted(set(self.dataset_name[np.asarray(indices)].tolist()))
-        return self.assemble(dev, lay, host_ids)
+        b = self.assemble(dev, lay, host_ids)
+        if ranges is not None:
+            b._store["branch_graph_ranges"], b._store["branch_node_ranges"] = ranges
+        return b
 
 
 def _ranges(starts, counts):

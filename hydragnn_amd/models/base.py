@@ -314,6 +314,8 @@ class Base(nn.Module):
             x_graph = seg.segment_mean(x, gsi)
         outputs, outputs_var = [], []
         nb = self.num_branches
+        if nb > 1 and data.get("branch_graph_ranges") is not None:
+            return self._decode_ranges(x, x_graph, equiv, ctx)
         ids = self._branch_ids(data) if nb > 1 else [0]
         G = x_graph.shape[0]
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
@@ -352,6 +354,42 @@ class Base(nn.Module):
                         headvar = headvar.index_put((mask_nodes,), x_node[:, head_dim:] ** 2)
             outputs.append(head)
             outputs_var.append(headvar)
+        if self.var_output:
+            return outputs, outputs_var
+        return outputs
+
+    def _decode_ranges(self, x, x_graph, equiv, ctx):
+        """Multi-branch decode for batches whose graphs are grouped by branch (the store
+        orders every batch by ``dataset_name`` and hands the host-side ranges over):
+        each branch head runs on a contiguous slice and the outputs are concatenated —
+        no boolean masks, no nonzero()/index_put host syncs (``Base.py:482-560``
+        semantics otherwise unchanged)."""
+        data = ctx.data
+        granges, nranges = data.branch_graph_ranges, data.branch_node_ranges
+        G, N = x_graph.shape[0], x.shape[0]
+        nt = self.config_heads["node"][0]["architecture"]["type"] if "node" in self.config_heads else None
+        outputs, outputs_var = [], []
+        for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
+            parts = []
+            if t == "graph":
+                for ID, g0, g1 in granges:
+                    bt = f"branch-{ID}"
+                    parts.append(headloc[bt](self.graph_shared[bt](x_graph[g0:g1])))
+                total, end = G, granges[-1][2] if granges else 0
+            else:
+                for ID, n0, n1 in nranges:
+                    bt = f"branch-{ID}"
+                    if nt == "conv":
+                        parts.append(self._node_head(headloc[bt], nt, x, equiv, ctx, data.batch)[n0:n1])
+                    else:
+                        parts.append(headloc[bt](x=x[n0:n1], batch=data.batch[n0:n1]))
+                total, end = N, nranges[-1][2] if nranges else 0
+            width = head_dim * (1 + self.var_output)
+            if end < total:  # trailing padding rows of a statically padded batch
+                parts.append(x.new_zeros((total - end, width)))
+            out = torch.cat(parts, 0) if len(parts) > 1 else parts[0]
+            outputs.append(out[:, :head_dim])
+            outputs_var.append(out[:, head_dim:] ** 2)
         if self.var_output:
             return outputs, outputs_var
         return outputs

@@ -243,6 +243,23 @@ class MultiheadDecoderBlock(nn.Module):
         gfeat = sc.mean(0, keepdim=True) if gsi is None else seg.segment_mean(sc, gsi)
         data = ctx.data
         outs = []
+        granges, nranges = data.get("branch_graph_ranges"), data.get("branch_node_ranges")
+        if self.num_branches > 1 and granges is not None and len(granges) > 1:
+            # store batches are grouped by branch: contiguous slices, no masks / host syncs
+            for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
+                feats, rng, total = (gfeat, granges, gfeat.shape[0]) if t == "graph" else \
+                    (node_features, nranges, node_features.shape[0])
+                parts = []
+                for ID, a, b in rng:
+                    bt = f"branch-{ID}"
+                    x = feats[a:b]
+                    if t == "graph" and self.nonlinear:
+                        x = self.graph_shared[bt](x)
+                    parts.append(hn[bt](x)[:, :hd])
+                if rng[-1][2] < total:
+                    parts.append(feats.new_zeros(total - rng[-1][2], hd))
+                outs.append(torch.cat(parts, 0))
+            return outs
         for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
             if t == "graph":
                 if self.num_branches == 1 or len(ids) <= 1:

@@ -211,7 +211,10 @@ class O3Linear(nn.Module):
             d = 2 * l + 1
             xi = x[:, self.sl_in[ii][0]:self.sl_in[ii][1]].reshape(N, mi, d)
             W = self.weight[off:off + mi * mo].view(mi, mo) * a
-            y = torch.einsum("nud,uv->nvd", xi, W)
+            if d == 1:  # scalars: a plain [N, mi] x [mi, mo] GEMM
+                y = (xi.reshape(N, mi) @ W).view(N, mo, 1)
+            else:  # one (N*d, mi) x (mi, mo) GEMM instead of an N-batched tiny bmm
+                y = (xi.transpose(1, 2).reshape(N * d, mi) @ W).view(N, d, mo).transpose(1, 2)
             outs[io] = y if outs[io] is None else outs[io] + y
         res = []
         for io, (mo, lo, _) in enumerate(self.irreps_out.blocks):
@@ -268,6 +271,25 @@ def tp_uvu_instructions(irreps1, irreps2, target):
     return srt, ins
 
 
+class _TPUVU(torch.autograd.Function):
+    """HIP uvu tensor product (first-order autograd; composite mode uses the einsum path)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, w, ins, cg, out_dim):
+        from .. import _native
+
+        ctx.save_for_backward(x1, x2, w, ins, cg)
+        return _native.ops().tp_uvu_fwd(x1, x2, w, ins, cg, out_dim)
+
+    @staticmethod
+    def backward(ctx, go):
+        from .. import _native
+
+        x1, x2, w, ins, cg = ctx.saved_tensors
+        g1, g2, gw = _native.ops().tp_uvu_bwd(go, x1, x2, w, ins, cg)
+        return g1, g2, gw, None, None, None
+
+
 class TensorProductUVU(nn.Module):
     """Channel-wise ("uvu") tensor product with per-edge external weights:
     out[e, u, m3] (block k) = sqrt(2 l3 + 1) sum_v w[e, k, u, v] sum_{m1 m2} C[m1 m2 m3] x1[e, u, m1] x2[e, v, m2]."""
@@ -288,7 +310,28 @@ class TensorProductUVU(nn.Module):
             self.register_buffer(f"cg_{l1}_{l2}_{l3}", wigner_3j(l1, l2, l3).float() * math.sqrt(2 * l3 + 1),
                                  persistent=False)
 
+        # native (HIP) path tables: the second operand carries one channel per l (spherical
+        # harmonics), which is the case the fused kernel implements (csrc/equivariant.hip)
+        self.native_ok = all(m2 == 1 for _, _, m2 in self.woff) and irreps2.lmax <= 3
+        rows, cgs, cgoff = [], [], 0
+        so = irreps_out.slices()
+        for (i, j, k), (off, m1, m2) in zip(instructions, self.woff):
+            l1, l2, l3 = irreps1.blocks[i][1], irreps2.blocks[j][1], irreps_out.blocks[k][1]
+            rows.append([l1, l2, l3, m1, self.sl1[i][0], self.sl2[j][0], off, so[k][0], cgoff])
+            c = getattr(self, f"cg_{l1}_{l2}_{l3}").reshape(-1)
+            cgs.append(c)
+            cgoff += c.numel()
+        self.register_buffer("_ins", torch.tensor(rows, dtype=torch.int32), persistent=False)
+        self.register_buffer("_cg", torch.cat(cgs) if cgs else torch.zeros(0), persistent=False)
+
     def forward(self, x1, x2, w):
+        from . import pna as _mode
+
+        if x1.is_cuda and self.native_ok and x1.dtype == torch.float32 and not _mode._state["composite"]:
+            return _TPUVU.apply(x1, x2, w, self._ins, self._cg, self.irreps_out.dim)
+        return self.forward_reference(x1, x2, w)
+
+    def forward_reference(self, x1, x2, w):
         E = x1.shape[0]
         outs = [None] * len(self.irreps_out.blocks)
         for (i, j, k), (off, m1, m2) in zip(self.ins, self.woff):
@@ -363,11 +406,22 @@ class Contraction(nn.Module):
         for nu in range(self.correlation, 0, -1):
             U = getattr(self, f"U_{nu}")
             K = U.shape[-1]
-            W = self.weights[nu - 1][elem]  # [N, K, H]
             P = U.reshape(-1, K)  # [M d^nu, K]
-            c = torch.einsum("pk,nkc->ncp", P, W) if K > 0 else x.new_zeros(N, H, P.shape[0])
+            if K > 0:
+                # per-element weights: one-hot(elem) @ W as a GEMM (its backward is a GEMM too,
+                # not a sort-based index_put), then one (N*H, K) x (K, M d^nu) GEMM
+                Wt = self.weights[nu - 1]
+                if elem.dim() == 2:  # one-hot [N, num_elements]
+                    W = (elem @ Wt.reshape(Wt.shape[0], -1)).view(N, K, H)
+                else:
+                    W = Wt[elem]
+                W = W.transpose(1, 2).reshape(N * H, K)
+                c = (W @ P.t()).view(N, H, -1)
+            else:
+                c = x.new_zeros(N, H, P.shape[0])
             out = c if out is None else out + c
-            out = torch.einsum("ncpi,nci->ncp", out.view(N, H, -1, d), x)
+            # contract the last input index with x: broadcast multiply + reduce (no tiny bmm)
+            out = (out.view(N, H, -1, d) * x.unsqueeze(2)).sum(-1)
         return out  # [N, H, 2L+1]
 
 
@@ -382,5 +436,8 @@ class SymmetricContraction(nn.Module):
                                            for _, l, _ in irreps_out.blocks])
 
     def forward(self, x, elem):
+        """``elem``: element indices [N] or a one-hot / soft assignment [N, num_elements]."""
         N = x.shape[0]
+        if elem.dim() == 1:
+            elem = torch.nn.functional.one_hot(elem.long(), self.contractions[0].weights[0].shape[0]).to(x.dtype)
         return torch.cat([c(x, elem).reshape(N, -1) for c in self.contractions], -1)

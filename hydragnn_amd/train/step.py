@@ -143,6 +143,10 @@ class TrainStep:
             from ..optim.adamw import FusedAdamW
 
             optimizer = FusedAdamW(params, lr=lr, weight_decay=weight_decay)
+        if mode == "graph" and getattr(self.module, "num_branches", 1) > 1:
+            # multi-branch decode routes graphs by their (host-known) branch ranges, which
+            # change from batch to batch: such models step eagerly
+            self.mode = mode = "eager"
         self.opt = optimizer
         self.flat_grads = None if isinstance(self.model, DistributedDataParallel) else FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket

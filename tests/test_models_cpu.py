@@ -119,3 +119,32 @@ def test_symmetric_contraction_equivariance():
     # output blocks: H x 0e then H x 1o (flat layout [H, 2l+1] per block)
     torch.testing.assert_close(y1[:, :H], y0[:, :H])
     torch.testing.assert_close(y1[:, H:].view(7, H, 3), y0[:, H:].view(7, H, 3) @ Ds[1].T)
+
+
+@pytest.mark.parametrize("node_type", ["mlp", "conv"])
+def test_multibranch_range_decode_matches_mask_decode(node_type):
+    """Store batches are grouped by branch and decoded by contiguous host ranges; the result
+    equals the boolean-mask decode of the reference (``Base.py:482-560``)."""
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+
+    samples = _samples(9)
+    for i, s in enumerate(samples):
+        s.dataset_name = torch.tensor([[i % 3]])
+    heads = {"graph": [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                                  "num_headlayers": 1, "dim_headlayers": [8]}}
+                       for b in range(3)],
+             "node": [{"type": f"branch-{b}", "architecture": {"num_headlayers": 1, "dim_headlayers": [8],
+                                                                 "type": node_type}} for b in range(3)]}
+    torch.manual_seed(0)
+    m = create_model("GIN", samples[0].x.shape[1], 12, [1, 1], 0, "", "", 0, ["graph", "node"], heads, "relu", "mse",
+                     [1.0, 1.0], 2, use_gpu=False, dropout=0.0)
+    m.eval()
+    store = DeviceGraphStore(samples, "cpu")
+    b = store.batch([4, 0, 7, 2, 5, 1])
+    assert [r[0] for r in b.branch_graph_ranges] == [0, 1, 2]
+    with torch.no_grad():
+        fast = m(b)
+        del b._store["branch_graph_ranges"], b._store["branch_node_ranges"]
+        slow = m(b)
+    for a, c in zip(fast, slow):
+        torch.testing.assert_close(a, c)

@@ -1,0 +1,171 @@
+"""Training throughput of the other BASELINE.json configurations on one MI355X
+(``bench.py`` is the driver's headline: config 4, OC20 PNAPlus + GPS).
+
+  2  qm9_schnet        QM9-shaped molecules, SchNet 4 layers, graph energy head, batch 64
+                       (in-forward radius graph -> eager step)
+  3  md17_painn_forces MD17-shaped frames, PAINN (equivariant), node energy head, energy +
+                       forces = -dE/dpos (compute_grad_energy, double backward), batch 32
+  5a multibranch_egnn  SC25 multibranch shape: EGNN hidden 866 x 4, 5 branches, graph energy +
+                       node force heads (3 x 889), batch 128, branch routing by dataset_name
+  5b multibranch_mace  the BASELINE.json variant of config 5 with MACE (hidden 64, l_max 2,
+                       correlation 2, 3 layers), 5 branches, batch 32
+
+All synthetic data / random-init weights, fp32.  Prints one JSON line per config.
+Usage: python tools/bench_configs.py [names...] [--steps 20] [--warmup 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hydragnn_amd.data.device_store import DeviceGraphStore  # noqa: E402
+from hydragnn_amd.data.graph import Graph  # noqa: E402
+from hydragnn_amd.data.synthetic import degree_histogram, md_trajectory, molecules_like  # noqa: E402
+from hydragnn_amd.data.transforms import radius_graph  # noqa: E402
+from hydragnn_amd.models.create import create_model  # noqa: E402
+from hydragnn_amd.ops.pna import composite_mode  # noqa: E402
+from hydragnn_amd.train.step import TrainStep  # noqa: E402
+
+
+def _with_edges(samples, r, k):
+    for s in samples:
+        s.edge_index = radius_graph(s.pos, r, max_num_neighbors=k)
+        s.edge_attr = (s.pos[s.edge_index[1]] - s.pos[s.edge_index[0]]).norm(dim=-1, keepdim=True) / r
+        s.sort_edges_by_dst()
+    return samples
+
+
+def _gheads(nb, dims, shared=50):
+    return [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 2, "dim_sharedlayers": shared,
+                                                     "num_headlayers": len(dims), "dim_headlayers": dims}}
+            for b in range(nb)]
+
+
+def _nheads(nb, dims):
+    return [{"type": f"branch-{b}", "architecture": {"num_headlayers": len(dims), "dim_headlayers": dims,
+                                                     "type": "mlp"}} for b in range(nb)]
+
+
+def qm9_schnet(dev):
+    s = _with_edges(molecules_like(1024, seed=1), 7.0, 5)
+    heads = {"graph": _gheads(1, [50, 25], 5)}
+    m = create_model("SchNet", 1, 64, [1], 0, "", "", 0, ["graph"], heads, "relu", "mse", [1.0], 4,
+                     num_gaussians=50, num_filters=64, radius=7.0, max_neighbours=5, dropout=0.0)
+    return m, s, 64, ["graph"], [1], False
+
+
+def md17_painn_forces(dev):
+    s = _with_edges(md_trajectory(1024, seed=2, num_atoms=21), 5.0, 20)
+    heads = {"node": _nheads(1, [64, 32])}
+    m = create_model("PAINN", 1, 64, [1], 0, "", "", 0, ["node"], heads, "relu", "mse", [1.0], 3,
+                     num_radial=6, radius=5.0, max_neighbours=20, edge_dim=None, equivariance=True, dropout=0.0)
+    return m, s, 32, ["node"], [1], True
+
+
+def _multibranch(mpnn, dev, hidden, layers, hd, batch, in_dim=4, **kw):
+    out = []
+    for k in range(5):
+        for t in molecules_like(384, seed=10 + k, min_atoms=4 + 3 * k, max_atoms=12 + 6 * k, with_forces=True):
+            x = torch.cat([t.x, t.pos, t.forces], 1)
+            out.append(Graph(x=x, pos=t.pos, y=t.y, forces=t.forces, dataset_name=torch.tensor([[k]])))
+    out = _with_edges(out, 5.0, 20)
+    for g in out:  # node target = forces (3); graph target = energy per atom
+        g.x = g.x[:, :in_dim]
+    heads = {"graph": _gheads(5, hd), "node": _nheads(5, hd)}
+    m = create_model(mpnn, in_dim, hidden, [1, 3], 0, "", "", 0, ["graph", "node"], heads, "relu", "mae", [1.0, 100.0],
+                     layers, radius=5.0, max_neighbours=20, edge_dim=1, dropout=0.0, **kw)
+    return m, out, batch, ["graph", "node"], [1, 3], False
+
+
+def multibranch_egnn(dev):
+    return _multibranch("EGNN", dev, 866, 4, [889, 889, 889], 128, equivariance=True)
+
+
+def multibranch_mace(dev):
+    return _multibranch("MACE", dev, 64, 3, [64, 64], 32, max_ell=2, node_max_ell=1, correlation=2, num_radial=8,
+                        envelope_exponent=5, radial_type="bessel", avg_num_neighbors=12.0,
+                        in_dim=1)  # MACE embeds raw atomic numbers
+
+
+CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
+           "multibranch_mace": multibranch_mace}
+
+
+def _targets_for_store(samples, head_types):
+    """Attach per-head targets the store packs: graph -> y, node -> forces."""
+    for s in samples:
+        ys = []
+        for t in head_types:
+            ys.append(s.y.view(-1, 1) if t == "graph" else s.forces.reshape(-1, 1))
+        s.y = torch.cat(ys, 0)
+        s.y_loc = torch.tensor([[0] + list(np.cumsum([y.numel() for y in ys]))])
+    return samples
+
+
+def run(name, steps, warmup, dev):
+    model, samples, B, ht, hd, forces = CONFIGS[name](dev)
+    model = model.to(dev)
+    if not forces:
+        samples = _targets_for_store(samples, ht)
+    store = DeviceGraphStore(samples, dev, head_types=None if forces else ht, head_dims=None if forces else hd)
+    rng = np.random.default_rng(0)
+    if forces:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+
+        def step(idx):
+            b = store.batch(idx)
+            b.pos.requires_grad_(True)
+            opt.zero_grad(set_to_none=True)
+            with composite_mode(True):
+                pred = model(b)
+                loss, _ = model.energy_force_loss(pred, b)
+                loss.backward()
+            opt.step()
+            return loss
+    else:
+        ts = TrainStep(model, lr=1e-3, mode="eager")
+
+        def step(idx):
+            return ts(store, idx)[0]
+    draw = lambda: list(rng.choice(len(store), size=B, replace=False))  # noqa: E731
+    for _ in range(warmup):
+        step(draw())
+    torch.cuda.synchronize()
+    if os.environ.get("BENCH_OP_PROFILE") == "1":  # op-level attribution of 3 steps
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(3):
+                step(draw())
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=45), flush=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step(draw())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    nodes = float(np.mean([s.num_nodes for s in samples]))
+    return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
+            "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
+            "params": sum(p.numel() for p in model.parameters()), "dtype": "fp32", "final_loss": float(loss),
+            "data": "synthetic", "mode": "eager"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="*", default=list(CONFIGS))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for n in a.names:
+        print(json.dumps(run(n, a.steps, a.warmup, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
