@@ -112,9 +112,21 @@ def main():
     if mark:  # a distinctive spin kernel brackets the timed steps in rocprof traces
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
+    # pure host cost of one step's index plan (numpy layout + packing), no GPU involved
+    hp = time.perf_counter()
+    for _ in range(20):
+        idx = next_indices()
+        N_, E_ = store.sizes_of(idx)
+        Np_, Ep_ = step.bucket_of(N_, E_)
+        lay_ = store.layout(idx, Np=Np_, Ep=Ep_, Gp=len(idx) + 1)
+        store.plan(idx, lay_, np.empty(lay_.total, dtype=np.int32))
+    plan_ms = 1000.0 * (time.perf_counter() - hp) / 20
+    host = 0.0  # host time spent issuing steps (index plan + upload + replay launch)
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         loss, _ = step(store, next_indices())
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -156,6 +168,10 @@ def main():
                 "attn_scope": args.attn_scope,
                 "mode": args.mode,
                 "final_loss": float(loss) if loss is not None else None,
+                "host_ms_per_step": round(1000.0 * host / args.steps, 4),
+                "host_plan_ms": round(plan_ms, 4),
+                "host_phases_ms": {k: round(1000.0 * v / max(step.host_times.get("n", 1), 1), 4)
+                                   for k, v in step.host_times.items() if k != "n"} if step.host_times else None,
             },
         }
         print(json.dumps(out), flush=True)

@@ -289,6 +289,150 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_bwd(const at::Tensor& dZ_, co
   return {dpre, dG, dA};
 }
 
+// ---------------------------------------------------------------------------------
+// Derived weights of one PNAPlus conv with an edge encoder (concat-linear
+// decomposition, PNAPlusStack.py:250-279).  pre_nn weight W [F, 3F] has column
+// blocks (x_i | x_j | enc_e); the edge encoder maps cat[e (d), r (F)] -> F.  The
+// per-step weight algebra
+//     Wab = [W_i; W_j]            [2F, F]   (node GEMM  x @ Wab^T)
+//     Wr  = W_e @ encW[:, d:]     [F, F]    (edge GEMM  r @ Wr^T)
+//     Wd  = W_e @ encW[:, :d]     [F, d]
+//     bc  = W_e @ encb + b        [F]       (pre_nn bias moved onto the edge term)
+// was ~25 tiny torch kernels per layer per step (cat, slices, their zero-fill/copy
+// backward, accumulation adds, mm/mv); here it is one launch forward and one
+// backward.  Copies are one element per thread; every dot product is owned by ONE
+// wave (lanes split the reduction, then a shuffle reduction), so each output
+// costs one round of coalesced L2 loads instead of a serial K-long load chain.
+
+// sum_k a[k * sa] * b[k * sb], k < K, reduced over the wave (all lanes get it)
+__device__ __forceinline__ float wave_dot(const float* __restrict__ a, int sa, const float* __restrict__ b, int sb,
+                                          int K) {
+  float acc = 0.f;
+  for (int k = lane_id(); k < K; k += 64) acc = fmaf(a[(int64_t)k * sa], b[(int64_t)k * sb], acc);
+  return wave_sum(acc);
+}
+
+__global__ void __launch_bounds__(256) pna_wprep_fwd_kernel(const float* __restrict__ W, const float* __restrict__ b,
+                                                            const float* __restrict__ encW,
+                                                            const float* __restrict__ encb, float* __restrict__ Wab,
+                                                            float* __restrict__ Wr, float* __restrict__ Wd,
+                                                            float* __restrict__ bc, int F, int d) {
+  const int ld = 3 * F, le = d + F;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t idx = tid; idx < 2 * F * F; idx += nthreads) {
+    const int r = (int)(idx / F), c = (int)(idx % F);
+    Wab[idx] = W[(r % F) * ld + (r / F) * F + c];
+  }
+  // dot products: Wr (F*F), Wd (F*d), bc (F) -- one wave each
+  const int64_t nd = (int64_t)F * F + (int64_t)F * d + F;
+  const int64_t nwaves = nthreads / 64;
+  for (int64_t q = tid / 64; q < nd; q += nwaves) {
+    float v;
+    float* dst;
+    if (q < F * F) {
+      const int o = (int)(q / F), c = (int)(q % F);
+      v = wave_dot(W + o * ld + 2 * F, 1, encW + d + c, le, F);
+      dst = Wr + q;
+    } else if (q < (int64_t)F * F + F * d) {
+      const int64_t k = q - F * F;
+      const int o = (int)(k / d), c = (int)(k % d);
+      v = wave_dot(W + o * ld + 2 * F, 1, encW + c, le, F);
+      dst = Wd + k;
+    } else {
+      const int o = (int)(q - F * F - (int64_t)F * d);
+      v = wave_dot(W + o * ld + 2 * F, 1, encb, 1, F) + b[o];
+      dst = bc + o;
+    }
+    if (lane_id() == 0) *dst = v;
+  }
+}
+
+// Backward of pna_wprep_fwd: dW [F,3F], db [F], dencW [F, d+F], dencb [F].
+__global__ void __launch_bounds__(256) pna_wprep_bwd_kernel(
+    const float* __restrict__ dWab, const float* __restrict__ dWr, const float* __restrict__ dWd,
+    const float* __restrict__ dbc, const float* __restrict__ W, const float* __restrict__ encW,
+    const float* __restrict__ encb, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dencW,
+    float* __restrict__ dencb, int F, int d) {
+  const int ld = 3 * F, le = d + F;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t idx = tid; idx < 2 * F * F + F; idx += nthreads) {  // copies: dW[:, :2F], db
+    if (idx < 2 * F * F) {
+      const int o = (int)(idx / (2 * F)), c = (int)(idx % (2 * F));
+      dW[o * ld + c] = dWab[((c / F) * F + o) * F + (c % F)];
+    } else {
+      db[idx - 2 * F * F] = dbc[idx - 2 * F * F];
+    }
+  }
+  // dots: dW_e (F*F, K = d + F + 1), dencW (F*(d+F), K = F), dencb (F, K = F)
+  const int64_t nd = (int64_t)F * F + (int64_t)F * le + F;
+  const int64_t nwaves = nthreads / 64;
+  for (int64_t q = tid / 64; q < nd; q += nwaves) {
+    float v;
+    float* dst;
+    if (q < F * F) {  // dW_e[o, j] = sum_c dWd[o,c] encW[j,c] + sum_c dWr[o,c] encW[j,d+c] + dbc[o] encb[j]
+      const int o = (int)(q / F), j = (int)(q % F);
+      v = wave_dot(dWr + o * F, 1, encW + j * le + d, 1, F) + dbc[o] * encb[j];
+      if (d > 0) v += wave_dot(dWd + o * d, 1, encW + j * le, 1, d);
+      dst = dW + o * ld + 2 * F + j;
+    } else if (q < (int64_t)F * F + (int64_t)F * le) {  // dencW[j, c] = sum_o W_e[o, j] [dWd | dWr][o, c]
+      const int64_t k = q - F * F;
+      const int j = (int)(k / le), c = (int)(k % le);
+      v = c < d ? wave_dot(W + 2 * F + j, ld, dWd + c, d, F) : wave_dot(W + 2 * F + j, ld, dWr + (c - d), F, F);
+      dst = dencW + k;
+    } else {
+      const int j = (int)(q - F * F - (int64_t)F * le);
+      v = wave_dot(W + 2 * F + j, ld, dbc, 1, F);
+      dst = dencb + j;
+    }
+    if (lane_id() == 0) *dst = v;
+  }
+}
+
+// one wave per dot product (64 lanes), capped at 2048 workgroups
+static int wprep_grid(int64_t dots) { return (int)std::min<int64_t>(ceil_div(dots * 64, 256), 2048); }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pna_wprep_fwd(const at::Tensor& W_, const at::Tensor& b_,
+                                                                         const at::Tensor& encW_,
+                                                                         const at::Tensor& encb_) {
+  HY_CHECK_CUDA(W_);
+  auto W = W_.contiguous(), b = b_.contiguous(), encW = encW_.contiguous(), encb = encb_.contiguous();
+  HY_CHECK_F32(W); HY_CHECK_F32(b); HY_CHECK_F32(encW); HY_CHECK_F32(encb);
+  const int F = (int)W.size(0);
+  HY_CHECK(W.dim() == 2 && W.size(1) == 3 * F, "pna_wprep: W must be [F, 3F]");
+  HY_CHECK(encW.dim() == 2 && encW.size(0) == F && encW.size(1) > F, "pna_wprep: encW must be [F, d+F]");
+  HY_CHECK(b.numel() == F && encb.numel() == F, "pna_wprep: biases must have F entries");
+  const int d = (int)encW.size(1) - F;
+  auto Wab = at::empty({2 * F, F}, W.options()), Wr = at::empty({F, F}, W.options());
+  auto Wd = at::empty({F, d}, W.options()), bc = at::empty({F}, W.options());
+  const int64_t total = (int64_t)F * F + (int64_t)F * d + F;
+  pna_wprep_fwd_kernel<<<wprep_grid(total), 256, 0, stream()>>>(W.data_ptr<float>(), b.data_ptr<float>(),
+                                                               encW.data_ptr<float>(), encb.data_ptr<float>(),
+                                                               Wab.data_ptr<float>(), Wr.data_ptr<float>(),
+                                                               Wd.data_ptr<float>(), bc.data_ptr<float>(), F, d);
+  return {Wab, Wr, Wd, bc};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pna_wprep_bwd(const at::Tensor& dWab_, const at::Tensor& dWr_,
+                                                                         const at::Tensor& dWd_, const at::Tensor& dbc_,
+                                                                         const at::Tensor& W_, const at::Tensor& encW_,
+                                                                         const at::Tensor& encb_) {
+  auto dWab = dWab_.contiguous(), dWr = dWr_.contiguous(), dWd = dWd_.contiguous(), dbc = dbc_.contiguous();
+  auto W = W_.contiguous(), encW = encW_.contiguous(), encb = encb_.contiguous();
+  const int F = (int)W.size(0), d = (int)encW.size(1) - F;
+  HY_CHECK(dWab.numel() == 2 * F * F && dWr.numel() == F * F && dWd.numel() == F * d && dbc.numel() == F,
+           "pna_wprep_bwd: gradient shapes do not match the forward");
+  auto dW = at::empty_like(W), db = at::empty({F}, W.options());
+  auto dencW = at::empty_like(encW), dencb = at::empty({F}, W.options());
+  const int64_t total = (int64_t)F * F + (int64_t)F * (d + F) + F;
+  pna_wprep_bwd_kernel<<<wprep_grid(total), 256, 0, stream()>>>(
+      dWab.data_ptr<float>(), dWr.data_ptr<float>(), dWd.data_ptr<float>(), dbc.data_ptr<float>(),
+      W.data_ptr<float>(), encW.data_ptr<float>(), encb.data_ptr<float>(), dW.data_ptr<float>(),
+      db.data_ptr<float>(), dencW.data_ptr<float>(), dencb.data_ptr<float>(), F, d);
+  return {dW, db, dencW, dencb};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
@@ -298,9 +442,15 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "pna_bwd(Tensor dZ, Tensor Z, Tensor AB, Tensor? C, Tensor? G, Tensor src, Tensor rowptr, Tensor amin, "
       "Tensor amax, float avg_log, float avg_lin) -> (Tensor, Tensor, Tensor)");
+  m.def("pna_wprep_fwd(Tensor W, Tensor b, Tensor encW, Tensor encb) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "pna_wprep_bwd(Tensor dWab, Tensor dWr, Tensor dWd, Tensor dbc, Tensor W, Tensor encW, Tensor encb) -> "
+      "(Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("pna_fwd", hy::pna_fwd);
   m.impl("pna_bwd", hy::pna_bwd);
+  m.impl("pna_wprep_fwd", hy::pna_wprep_fwd);
+  m.impl("pna_wprep_bwd", hy::pna_wprep_bwd);
 }

@@ -1,0 +1,344 @@
+// Fused radial features of a PNAPlus stack (gfx950).
+//
+// Reference: PNAPlusStack (hydragnn/models/PNAPlusStack.py:40-304) computes once per
+// batch  rbf = BesselBasisLayer(dist)  (DimeNet envelope u(d/c) * sin(freq_k d/c),
+// learnable freq) and then, in EVERY conv layer l,
+//     r_l = ReLU(rbf_emb_l(rbf))      [E, F]   (Linear(K, F) + ReLU)
+//     G_l = rbf_lin_l(rbf)            [E, F]   (Linear(K, F), no bias)
+// With K = num_radial ~ 6 these are K-deep dot products per output: pure memory/launch
+// cost.  As torch ops the Bessel basis, 2L GEMMs, L ReLUs and their backward (2L
+// weight-gradient reductions, 2L input-gradient GEMMs + accumulation, the basis'
+// elementwise chain) are ~50 launches per step for a 3-layer stack.  Here:
+//   forward : one kernel: the basis values are computed once per (edge, k) into LDS,
+//             lanes stream the features and write r_l, G_l for all layers;
+//   backward: one kernel: per-workgroup partial sums of dW_emb, db_emb, dW_lin
+//             (lanes over features), then the per-edge drbf_k = sum_l sum_f dr_l
+//             W_emb_l + dG_l W_lin_l (threads over edges, rows L2-hot), ddist and
+//             dfreq -> one fixed-order partial-sum pass.
+// Deterministic, no atomics.  Double backward (forces) uses the torch composite.
+#include "common.h"
+
+namespace hy {
+
+constexpr int kRadMaxK = 16;
+constexpr int kRadMaxL = 8;
+constexpr int kRadBwdEdges = 64;      // edges per backward workgroup (partials per WG)
+
+struct RadEnv {
+  float inv_c;       // 1 / cutoff
+  float p, a, b, c;  // envelope u(x) = 1/x + a x^(p-1) + b x^p + c x^(p+1) for x < 1
+  int pe;            // p - 1 (the integer envelope exponent)
+};
+
+__device__ __forceinline__ void envelope(const RadEnv& ev, float x, float& u, float& du) {
+  if (x >= 1.f || x <= 0.f) {
+    u = 0.f;
+    du = 0.f;
+    return;
+  }
+  float xp0 = 1.f;
+  for (int i = 0; i < ev.pe; ++i) xp0 *= x;
+  const float xp1 = xp0 * x, xp2 = xp1 * x;
+  u = 1.f / x + ev.a * xp0 + ev.b * xp1 + ev.c * xp2;
+  du = -1.f / (x * x) + (ev.a * (ev.p - 1.f) * xp0 + ev.b * ev.p * xp1 + ev.c * (ev.p + 1.f) * xp2) / x;
+}
+
+// W layout: Wemb [L][F][K], bemb [L][F], Wlin [L][F][K];  out R, Gt: [L][E][F]
+// Block: 16 edges; the 16 x K basis values are computed ONCE (one thread each) into
+// LDS, then each wave streams 4 edges x F features with the (l, f) weights held in
+// registers.
+constexpr int kRadFwdEdges = 16;
+
+__global__ void __launch_bounds__(256) radial_fwd_kernel(const float* __restrict__ dist, int64_t E,
+                                                         const float* __restrict__ freq, int K,
+                                                         const float* __restrict__ Wemb,
+                                                         const float* __restrict__ bemb,
+                                                         const float* __restrict__ Wlin, int L, int F, RadEnv ev,
+                                                         float* __restrict__ R, float* __restrict__ Gt) {
+  __shared__ float rb[kRadFwdEdges][kRadMaxK];
+  const int64_t e0 = (int64_t)blockIdx.x * kRadFwdEdges;
+  const int ne = (int)min<int64_t>(kRadFwdEdges, E - e0);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int idx = threadIdx.x; idx < ne * K; idx += blockDim.x) {
+    const int el = idx / K, k = idx % K;
+    const float x = dist[e0 + el] * ev.inv_c;
+    float u, du;
+    envelope(ev, x, u, du);
+    rb[el][k] = u * sinf(freq[k] * x);
+  }
+  __syncthreads();
+  for (int f = lane; f < F; f += 64) {
+    for (int l = 0; l < L; ++l) {
+      float we[kRadMaxK], wl[kRadMaxK];
+#pragma unroll
+      for (int k = 0; k < kRadMaxK; ++k) {
+        we[k] = k < K ? Wemb[((int64_t)l * F + f) * K + k] : 0.f;
+        wl[k] = k < K ? Wlin[((int64_t)l * F + f) * K + k] : 0.f;
+      }
+      const float b0 = bemb[l * F + f];
+      for (int el = w; el < ne; el += 4) {
+        float r = b0, g = 0.f;
+#pragma unroll
+        for (int k = 0; k < kRadMaxK; ++k) {
+          if (k < K) {
+            r = fmaf(we[k], rb[el][k], r);
+            g = fmaf(wl[k], rb[el][k], g);
+          }
+        }
+        const int64_t o = ((int64_t)l * E + e0 + el) * F + f;
+        R[o] = fmaxf(r, 0.f);
+        Gt[o] = g;
+      }
+    }
+  }
+}
+
+// part layout per workgroup: [L][F][2K+1] (dWemb k, dWlin k, dbemb) then [K] dfreq.
+// Block: 64 edges, wave w owns edges w, w+4, ... in the weight-gradient pass:
+// per (f-chunk, layer) the lanes accumulate their features' weight gradients over
+// the wave's edges.  Then 4 threads per edge reduce drbf over (layer, feature) with the weights
+// broadcast from LDS (rows still L2-hot), and per-edge ddist / dfreq terms follow.
+__global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict__ dR, const float* __restrict__ dG,
+                                                         const float* __restrict__ R,
+                                                         const float* __restrict__ dist, int64_t E,
+                                                         const float* __restrict__ freq, int K,
+                                                         const float* __restrict__ Wemb,
+                                                         const float* __restrict__ Wlin, int L, int F, RadEnv ev,
+                                                         float* __restrict__ ddist, float* __restrict__ part,
+                                                         int64_t part_ld) {
+  __shared__ float rb[kRadBwdEdges][kRadMaxK];
+  __shared__ float drb[kRadBwdEdges][4][kRadMaxK];  // 4 feature-quarter partials per edge
+  __shared__ float fold[4][64][2 * kRadMaxK + 1];
+  extern __shared__ float wsm[];  // [2][L][F][K]: W_emb then W_lin
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t e0 = (int64_t)blockIdx.x * kRadBwdEdges;
+  const int ne = (int)min<int64_t>(kRadBwdEdges, E - e0);
+  const int per = 2 * K + 1;
+  float* P = part + blockIdx.x * part_ld;
+  for (int idx = threadIdx.x; idx < kRadBwdEdges * kRadMaxK; idx += blockDim.x) {
+    const int el = idx / kRadMaxK, k = idx % kRadMaxK;
+    float v = 0.f;
+    if (el < ne && k < K) {
+      const float x = dist[e0 + el] * ev.inv_c;
+      float u, du;
+      envelope(ev, x, u, du);
+      v = u * sinf(freq[k] * x);
+    }
+    rb[el][k] = v;
+  }
+  for (int idx = threadIdx.x; idx < L * F * K; idx += blockDim.x) {
+    wsm[idx] = Wemb[idx];
+    wsm[L * F * K + idx] = Wlin[idx];
+  }
+  __syncthreads();
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int f = f0 + lane;
+    const bool fv = f < F;
+    for (int l = 0; l < L; ++l) {
+      float aWe[kRadMaxK], aWl[kRadMaxK], ab = 0.f;
+#pragma unroll
+      for (int k = 0; k < kRadMaxK; ++k) aWe[k] = aWl[k] = 0.f;
+      for (int el = w; el < ne; el += 4) {
+        float dr = 0.f, dg = 0.f;
+        if (fv) {
+          const int64_t o = ((int64_t)l * E + e0 + el) * F + f;
+          dr = R[o] > 0.f ? dR[o] : 0.f;
+          dg = dG[o];
+        }
+        ab += dr;
+#pragma unroll
+        for (int k = 0; k < kRadMaxK; ++k) {
+          if (k < K) {
+            aWe[k] = fmaf(dr, rb[el][k], aWe[k]);
+            aWl[k] = fmaf(dg, rb[el][k], aWl[k]);
+          }
+        }
+      }
+      // fold the 4 waves (fixed order) and write this block's partial
+#pragma unroll
+      for (int k = 0; k < kRadMaxK; ++k) {
+        if (k < K) {
+          fold[w][lane][k] = aWe[k];
+          fold[w][lane][K + k] = aWl[k];
+        }
+      }
+      fold[w][lane][2 * K] = ab;
+      __syncthreads();
+      if (fv) {
+        for (int q = w; q < per; q += 4) {
+          const float v = ((fold[0][lane][q] + fold[1][lane][q]) + fold[2][lane][q]) + fold[3][lane][q];
+          P[((int64_t)l * F + f) * per + q] = v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // drbf_k[e] = sum_l sum_f dr W_emb[l,f,k] + dg W_lin[l,f,k]: 4 threads per edge
+  // (feature quarters, rows L2-hot from the pass above), weights broadcast from LDS
+  {
+    const int el = threadIdx.x >> 2, q = threadIdx.x & 3;
+    float acc[kRadMaxK];
+#pragma unroll
+    for (int k = 0; k < kRadMaxK; ++k) acc[k] = 0.f;
+    if (el < ne) {
+      for (int l = 0; l < L; ++l) {
+        const int64_t row = ((int64_t)l * E + e0 + el) * F;
+        for (int f = q; f < F; f += 4) {
+          const float dr = R[row + f] > 0.f ? dR[row + f] : 0.f, dg = dG[row + f];
+          const float* we = wsm + ((int64_t)l * F + f) * K;
+          const float* wl = wsm + (int64_t)L * F * K + ((int64_t)l * F + f) * K;
+#pragma unroll
+          for (int k = 0; k < kRadMaxK; ++k)
+            if (k < K) acc[k] = fmaf(dr, we[k], fmaf(dg, wl[k], acc[k]));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kRadMaxK; ++k) drb[el][q][k] = acc[k];
+  }
+  __syncthreads();
+  // per edge: ddist = sum_k drbf_k d rbf_k / d dist; per-edge dfreq terms into rb (reused)
+  if (threadIdx.x < kRadBwdEdges) {
+    const int el = threadIdx.x;
+    float dd = 0.f;
+    float x = 0.f, u = 0.f, du = 0.f;
+    if (el < ne) {
+      x = dist[e0 + el] * ev.inv_c;
+      envelope(ev, x, u, du);
+    }
+    for (int k = 0; k < K; ++k) {
+      float sn, cs;
+      sincosf(freq[k] * x, &sn, &cs);
+      const float g = el < ne ? ((drb[el][0][k] + drb[el][1][k]) + drb[el][2][k]) + drb[el][3][k] : 0.f;
+      dd += g * (du * sn + u * cs * freq[k]);
+      rb[el][k] = g * u * cs * x;  // d rbf_k / d freq_k contribution
+    }
+    if (el < ne) ddist[e0 + el] = dd * ev.inv_c;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    float a = 0.f;
+    for (int el = 0; el < kRadBwdEdges; ++el) a += rb[el][k];
+    P[(int64_t)L * F * per + k] = a;
+  }
+}
+
+// out[j] = sum_b part[b * ld + j]: 64 columns per block, 16 waves split the partials,
+// folded in a fixed order (deterministic)
+constexpr int kRadSumWaves = 16;
+__global__ void __launch_bounds__(64 * kRadSumWaves) radial_sum_kernel(const float* __restrict__ part, int nb,
+                                                                       int64_t n, int64_t ld,
+                                                                       float* __restrict__ out) {
+  __shared__ float red[kRadSumWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (j < n) {
+    int b = w;
+    for (; b + kRadSumWaves < nb; b += 2 * kRadSumWaves) {
+      a0 += part[(int64_t)b * ld + j];
+      a1 += part[(int64_t)(b + kRadSumWaves) * ld + j];
+    }
+    if (b < nb) a0 += part[(int64_t)b * ld + j];
+  }
+  red[w][lane] = a0 + a1;
+  __syncthreads();
+  if (w == 0 && j < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < kRadSumWaves; ++q) t += red[q][lane];
+    out[j] = t;
+  }
+}
+
+static RadEnv make_env(double cutoff, int64_t exponent) {
+  RadEnv ev;
+  const double p = (double)exponent + 1.0;
+  ev.inv_c = (float)(1.0 / cutoff);
+  ev.p = (float)p;
+  ev.a = (float)(-(p + 1.0) * (p + 2.0) / 2.0);
+  ev.b = (float)(p * (p + 2.0));
+  ev.c = (float)(-p * (p + 1.0) / 2.0);
+  ev.pe = (int)exponent;
+  return ev;
+}
+
+static void check_w(const at::Tensor& t, int64_t L, int64_t F, int64_t K, const char* name) {
+  HY_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), name, " must be contiguous fp32 on GPU");
+  HY_CHECK(t.dim() == 3 && t.size(0) == L && t.size(1) == F && t.size(2) == K, name, " must be [L, F, K]");
+}
+
+std::tuple<at::Tensor, at::Tensor> radial_fwd(const at::Tensor& dist_, const at::Tensor& freq_, const at::Tensor& Wemb,
+                                              const at::Tensor& bemb, const at::Tensor& Wlin, double cutoff,
+                                              int64_t exponent) {
+  HY_CHECK_CUDA(dist_);
+  auto dist = dist_.contiguous(), freq = freq_.contiguous();
+  HY_CHECK_F32(dist);
+  HY_CHECK_F32(freq);
+  const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
+  HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL, "radial: 1 <= K <= 16, 1 <= L <= 8");
+  check_w(Wemb, L, F, K, "Wemb");
+  check_w(Wlin, L, F, K, "Wlin");
+  HY_CHECK(bemb.is_contiguous() && bemb.numel() == L * F, "bemb must be [L, F]");
+  auto R = at::empty({L, E, F}, dist.options()), Gt = at::empty({L, E, F}, dist.options());
+  if (E == 0) return {R, Gt};
+  radial_fwd_kernel<<<ceil_div(E, kRadFwdEdges), 256, 0, stream()>>>(
+      dist.data_ptr<float>(), E, freq.data_ptr<float>(), (int)K, Wemb.data_ptr<float>(), bemb.data_ptr<float>(),
+      Wlin.data_ptr<float>(), (int)L, (int)F, make_env(cutoff, exponent), R.data_ptr<float>(), Gt.data_ptr<float>());
+  return {R, Gt};
+}
+
+// returns ddist [E], dfreq [K], dWemb [L,F,K], dbemb [L,F], dWlin [L,F,K]
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bwd(
+    const at::Tensor& dR_, const at::Tensor& dG_, const at::Tensor& R, const at::Tensor& dist_,
+    const at::Tensor& freq_, const at::Tensor& Wemb, const at::Tensor& Wlin, double cutoff, int64_t exponent) {
+  auto dR = dR_.contiguous(), dG = dG_.contiguous(), dist = dist_.contiguous(), freq = freq_.contiguous();
+  const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
+  HY_CHECK(dR.sizes() == R.sizes() && dG.sizes() == R.sizes() && R.is_contiguous(), "radial_bwd: grad shapes");
+  HY_CHECK(2 * L * F * K * (int64_t)sizeof(float) <= 64 * 1024, "radial_bwd: L*F*K must be <= 8192");
+  const int64_t per = 2 * K + 1;
+  const int64_t ld = L * F * per + K;
+  const int nb = std::max(1, ceil_div(E, kRadBwdEdges));
+  auto part = at::empty({nb, ld}, dist.options());
+  auto sums = at::empty({ld}, dist.options());
+  auto ddist = at::empty({E}, dist.options());
+  if (E > 0) {
+    static bool attr = [] {
+      hipFuncSetAttribute((const void*)radial_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+      return true;
+    }();
+    (void)attr;
+    radial_bwd_kernel<<<nb, 256, 2 * L * F * K * sizeof(float), stream()>>>(dR.data_ptr<float>(), dG.data_ptr<float>(), R.data_ptr<float>(),
+                                                dist.data_ptr<float>(), E, freq.data_ptr<float>(), (int)K,
+                                                Wemb.data_ptr<float>(), Wlin.data_ptr<float>(), (int)L, (int)F,
+                                                make_env(cutoff, exponent), ddist.data_ptr<float>(),
+                                                part.data_ptr<float>(), ld);
+    radial_sum_kernel<<<ceil_div(ld, 64), 64 * kRadSumWaves, 0, stream()>>>(part.data_ptr<float>(), nb, ld, ld,
+                                                                            sums.data_ptr<float>());
+  } else {
+    sums.zero_();
+  }
+  auto g = sums.narrow(0, 0, L * F * per).view({L, F, per});
+  auto dWemb = g.narrow(2, 0, K).contiguous();
+  auto dWlin = g.narrow(2, K, K).contiguous();
+  auto dbemb = g.select(2, 2 * K).contiguous();
+  auto dfreq = sums.narrow(0, L * F * per, K);
+  return {ddist, dfreq, dWemb, dbemb, dWlin};
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def(
+      "radial_fwd(Tensor dist, Tensor freq, Tensor Wemb, Tensor bemb, Tensor Wlin, float cutoff, int exponent) -> "
+      "(Tensor, Tensor)");
+  m.def(
+      "radial_bwd(Tensor dR, Tensor dG, Tensor R, Tensor dist, Tensor freq, Tensor Wemb, Tensor Wlin, float cutoff, "
+      "int exponent) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("radial_fwd", hy::radial_fwd);
+  m.impl("radial_bwd", hy::radial_bwd);
+}

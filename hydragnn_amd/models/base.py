@@ -25,6 +25,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops import segment as seg
 from ..ops import rng as _rng
 from ..ops.attention import make_segments
+from ..ops.mlp import sequential_chain
 from ..ops.norm import norm_add
 from ..utils import tracer as tr
 from ..utils.model import activation_function_selection, loss_function_selection
@@ -321,7 +322,7 @@ class Base(nn.Module):
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
             if t == "graph":
                 if nb == 1:
-                    out = headloc["branch-0"](self.graph_shared["branch-0"](x_graph))
+                    out = sequential_chain(x_graph, self.graph_shared["branch-0"], headloc["branch-0"])
                     head, headvar = out[:, :head_dim], out[:, head_dim:] ** 2
                 else:
                     dn = data.dataset_name.view(-1)
@@ -330,7 +331,7 @@ class Base(nn.Module):
                     for ID in ids:
                         mask = dn == ID
                         bt = f"branch-{ID}"
-                        out = headloc[bt](self.graph_shared[bt](x_graph[mask]))
+                        out = sequential_chain(x_graph[mask], self.graph_shared[bt], headloc[bt])
                         head = head.index_put((mask,), out[:, :head_dim])
                         headvar = headvar.index_put((mask,), out[:, head_dim:] ** 2)
             else:
@@ -374,7 +375,7 @@ class Base(nn.Module):
             if t == "graph":
                 for ID, g0, g1 in granges:
                     bt = f"branch-{ID}"
-                    parts.append(headloc[bt](self.graph_shared[bt](x_graph[g0:g1])))
+                    parts.append(sequential_chain(x_graph[g0:g1], self.graph_shared[bt], headloc[bt]))
                 total, end = G, granges[-1][2] if granges else 0
             else:
                 for ID, n0, n1 in nranges:

@@ -23,7 +23,8 @@ from torch.nn import ModuleList, Sequential
 
 from ..ops.geometry import BesselBasis, edge_vectors_and_lengths
 from ..ops.linear import linear, linear_sum
-from ..ops.pna import pna_avg_deg, pna_message_aggregate
+from ..ops.pna import pna_avg_deg, pna_message_aggregate, pna_weight_prep
+from ..ops.radial import fused_ok, radial_features
 from .base import Base
 from .layers import Linear
 
@@ -61,29 +62,36 @@ class PNAConvFused(nn.Module):
         Fi = self.F_in
         pre = self.pre_nns[0][0]
         W, b = pre.weight, pre.bias
-        # AB[:, :F] = W_i x + b (x_i, destination), AB[:, F:] = W_j x (x_j, source): one node GEMM
-        AB = linear(x, torch.cat([W[:, :Fi], W[:, Fi:2 * Fi]], 0), torch.cat([b, torch.zeros_like(b)]))
         C = None
         G = None
-        if self.plus:
-            rbf = ctx.rbf
-            r = self.rbf_emb(rbf)
+        if self.plus and self.edge_dim is not None and ctx.edge_attr is not None:
+            # all weight algebra in one launch; the pre_nn bias rides on the edge term C
+            enc = self.edge_encoder
+            Wab, Wr, Wd, bc = pna_weight_prep(W, b, enc.weight, enc.bias)
+            AB = linear(x, Wab, None)
+            r, G = self._radial(ctx)
+            C = linear_sum([(r, Wr), (ctx.edge_attr, Wd)], bc)
+        else:
+            # AB[:, :F] = W_i x + b (x_i, destination), AB[:, F:] = W_j x (x_j, source): one node GEMM
+            AB = linear(x, torch.cat([W[:, :Fi], W[:, Fi:2 * Fi]], 0), torch.cat([b, torch.zeros_like(b)]))
             We = W[:, 2 * Fi:]
-            if self.edge_dim is not None and ctx.edge_attr is not None:
-                enc = self.edge_encoder
-                Wc = We @ enc.weight  # [F, d + F]
-                bc = We @ enc.bias
-                d = self.edge_dim
-                C = linear_sum([(r, Wc[:, d:]), (ctx.edge_attr, Wc[:, :d])], bc)
-            else:
+            if self.plus:
+                r, G = self._radial(ctx)
                 C = linear(r, We, None)
-            G = self.rbf_lin(rbf)
-        elif self.edge_dim is not None and ctx.edge_attr is not None:
-            We = W[:, 2 * Fi:]
-            C = linear(ctx.edge_attr, We @ self.edge_encoder.weight, We @ self.edge_encoder.bias)
+            elif self.edge_dim is not None and ctx.edge_attr is not None:
+                C = linear(ctx.edge_attr, We @ self.edge_encoder.weight, We @ self.edge_encoder.bias)
         Z = pna_message_aggregate(x, AB, C, G, ctx.dst_si, ctx.src_si, self.avg_deg)
         out = self.post_nns[0](Z)
         return self.lin(out), equiv
+
+    def _radial(self, ctx):
+        """(ReLU(rbf_emb(rbf)), rbf_lin(rbf)): precomputed for the whole stack by the
+        fused radial kernel when available (``ctx.radial``), else from ``ctx.rbf``."""
+        rad = ctx.get("radial")
+        if rad is not None and id(self) in rad:
+            return rad[id(self)]
+        rbf = ctx.rbf if ctx.get("rbf") is not None else ctx.rbf_basis(ctx.dist)
+        return self.rbf_emb(rbf), self.rbf_lin(rbf)
 
     def __repr__(self):
         return f"PNAConv{'Plus' if self.plus else ''}({self.in_channels}, {self.out_channels}, edge_dim={self.edge_dim})"
@@ -112,8 +120,23 @@ class PNAPlusStack(Base):
         x, pos, ctx = super()._embedding(data)
         assert data.pos is not None, "PNA+ requires node positions (data.pos) to be set."
         _, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
-        ctx.rbf = self.rbf(dist.squeeze(-1))
+        dist = dist.squeeze(-1)
+        convs = self._stack_convs()
+        if fused_ok(dist, self.rbf, convs):
+            # Bessel basis + every layer's rbf_emb/rbf_lin in one launch (ops/radial.py)
+            ctx.radial = {id(c): rg for c, rg in zip(convs, radial_features(dist, self.rbf, convs))}
+            ctx.rbf, ctx.rbf_basis, ctx.dist = None, self.rbf, dist
+        else:
+            ctx.rbf = self.rbf(dist)
         return x, pos, ctx
+
+    def _stack_convs(self):
+        out = []
+        for c in self.graph_convs:
+            c = getattr(c, "conv", c)  # GPS wraps the local conv
+            if isinstance(c, PNAConvFused) and c.plus:
+                out.append(c)
+        return out
 
     def __str__(self):
         return "PNAPlusStack"

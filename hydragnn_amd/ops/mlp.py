@@ -1,0 +1,78 @@
+"""Fused Linear/ReLU chains for the graph-level heads (``csrc/mlp.hip``).
+
+Reference: the per-branch shared MLP + per-head MLP of ``Base._multihead``
+(``hydragnn/models/Base.py:246-287``) applied to pooled graph features.  On the
+GPU a chain of up to 8 Linear(+ReLU) layers of width <= 128 over <= 64 rows is
+one forward and one backward launch; anything else (CPU, other activations,
+composite/double-backward mode) runs the modules as written.
+"""
+import torch
+from torch import nn
+
+from .. import _native
+from . import pna as _mode
+
+MAX_ROWS = 64
+MAX_DIM = 128
+MAX_LAYERS = 8
+MAX_LDS = 159 * 1024
+
+
+def _lds_ok(G, dims):
+    """LDS footprint of the fused kernels (``csrc/mlp.hip`` fwd_lds / bwd_lds)."""
+    w = sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+    md = max(dims) + 1
+    fwd = 4 * (w + 2 * G * md)
+    bwd = 4 * (w + G * (sum(dims[1:]) + dims[0] + md))
+    return max(fwd, bwd) <= MAX_LDS
+
+
+class _FusedMLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, relu, *params):
+        out, acts = _native.ops().mlp_fwd(x, params[0::2], params[1::2], relu)
+        ctx.save_for_backward(x, acts, *params)
+        ctx.relu = relu
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, acts, *params = ctx.saved_tensors
+        dx, dWs, dbs = _native.ops().mlp_bwd(dout, x, acts, params[0::2], params[1::2], ctx.relu)
+        grads = []
+        for dW, db in zip(dWs, dbs):
+            grads += [dW, db]
+        return (dx, None, *grads)
+
+
+def _chain(seqs):
+    """[(Linear, relu_after)] for Sequentials made only of Linear and ReLU, else None."""
+    layers = []
+    for s in seqs:
+        for m in s:
+            if isinstance(m, nn.Linear):
+                if m.bias is None:
+                    return None
+                layers.append([m, False])
+            elif isinstance(m, nn.ReLU) and layers and not layers[-1][1]:
+                layers[-1][1] = True
+            else:
+                return None
+    return layers
+
+
+def sequential_chain(x, *seqs):
+    """``seqs[-1](...seqs[0](x))`` — fused on the GPU when the chain qualifies."""
+    if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and not _mode._state["composite"] \
+            and 0 < x.shape[0] <= MAX_ROWS:
+        layers = _chain(seqs)
+        dims = [x.shape[1]] + [m.weight.shape[0] for m, _ in layers] if layers else []
+        if layers and len(layers) <= MAX_LAYERS and max(dims) <= MAX_DIM and _lds_ok(x.shape[0], dims) and \
+                all(m.weight.dtype == torch.float32 for m, _ in layers):
+            params = []
+            for m, _ in layers:
+                params += [m.weight, m.bias]
+            return _FusedMLP.apply(x.contiguous(), [int(r) for _, r in layers], *params)
+    for s in seqs:
+        x = s(x)
+    return x

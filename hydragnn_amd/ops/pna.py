@@ -117,6 +117,32 @@ class _PNAFused(torch.autograd.Function):
         return dx, dAB, dC, dG, None, None, None, None
 
 
+class _PNAWeightPrep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, W, b, encW, encb):
+        out = _native.ops().pna_wprep_fwd(W, b, encW, encb)
+        ctx.save_for_backward(W, encW, encb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dWab, dWr, dWd, dbc):
+        W, encW, encb = ctx.saved_tensors
+        return _native.ops().pna_wprep_bwd(dWab, dWr, dWd, dbc, W, encW, encb)
+
+
+def pna_weight_prep(W, b, encW, encb):
+    """Derived weights of a PNAPlus conv with edge encoder (``csrc/pna.hip``):
+    ``Wab = [W_i; W_j]``, ``Wr = W_e encW[:, d:]``, ``Wd = W_e encW[:, :d]``,
+    ``bc = W_e encb + b`` for ``pre_nn`` weight ``W = [W_i | W_j | W_e]``.  One HIP
+    launch each way on the GPU; torch algebra on CPU / in composite mode."""
+    F = W.shape[0]
+    d = encW.shape[1] - F
+    if W.is_cuda and not _state["composite"] and W.dtype == torch.float32 and encW.dtype == torch.float32:
+        return _PNAWeightPrep.apply(W, b, encW, encb)
+    We = W[:, 2 * F:]
+    return torch.cat([W[:, :F], W[:, F:2 * F]], 0), We @ encW[:, d:], We @ encW[:, :d], We @ encb + b
+
+
 def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
     """Z = cat[x, PNA-aggregate((A[dst] + B[src] + C) * G)] with default aggregators/scalers.
 

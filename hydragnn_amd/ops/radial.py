@@ -1,0 +1,52 @@
+"""Fused Bessel radial basis + per-layer radial projections of a PNAPlus stack
+(``csrc/radial.hip``).
+
+Reference: ``PNAPlusStack`` (``hydragnn/models/PNAPlusStack.py:40-304``) computes
+``rbf = BesselBasisLayer(dist)`` once and, in every conv layer l,
+``r_l = ReLU(rbf_emb_l(rbf))`` and ``G_l = rbf_lin_l(rbf)``.  On the GPU all of it
+is one forward and two backward launches for the whole stack (instead of ~50 small
+torch kernels); CPU tensors and composite (double-backward) mode use the modules.
+"""
+import torch
+
+from .. import _native
+from . import pna as _mode
+
+MAX_K = 16
+MAX_L = 8
+
+
+class _Radial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dist, freq, Wemb, bemb, Wlin, cutoff, exponent):
+        R, Gt = _native.ops().radial_fwd(dist, freq, Wemb, bemb, Wlin, cutoff, exponent)
+        ctx.save_for_backward(R, dist, freq, Wemb, Wlin)
+        ctx.cfg = (cutoff, exponent)
+        return R, Gt
+
+    @staticmethod
+    def backward(ctx, dR, dG):
+        R, dist, freq, Wemb, Wlin = ctx.saved_tensors
+        ddist, dfreq, dWemb, dbemb, dWlin = _native.ops().radial_bwd(dR, dG, R, dist, freq, Wemb, Wlin, *ctx.cfg)
+        return ddist, dfreq, dWemb, dbemb, dWlin, None, None
+
+
+def fused_ok(dist, basis, convs):
+    if not (dist.is_cuda and dist.dtype == torch.float32 and not _mode._state["composite"]
+            and 0 < len(convs) <= MAX_L and basis.freq.numel() <= MAX_K):
+        return False
+    shape = convs[0].rbf_emb[0].weight.shape  # [F, K]; all layers equal, weights fit 64 KB LDS
+    return all(c.rbf_emb[0].weight.shape == shape for c in convs) and len(convs) * shape[0] * shape[1] <= 8192
+
+
+def radial_features(dist, basis, convs):
+    """[(r_l, G_l)] for PNAPlus convs ``convs`` sharing the Bessel basis ``basis``."""
+    if not fused_ok(dist, basis, convs):
+        rbf = basis(dist)
+        return [(c.rbf_emb(rbf), c.rbf_lin(rbf)) for c in convs]
+    Wemb = torch.stack([c.rbf_emb[0].weight for c in convs])
+    bemb = torch.stack([c.rbf_emb[0].bias for c in convs])
+    Wlin = torch.stack([c.rbf_lin.weight for c in convs])
+    R, Gt = _Radial.apply(dist.contiguous(), basis.freq, Wemb, bemb, Wlin, float(basis.cutoff),
+                          int(basis.envelope.p - 1))
+    return [(R[i], Gt[i]) for i in range(len(convs))]

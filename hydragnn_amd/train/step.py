@@ -20,6 +20,8 @@ The per-step host work is only: draw indices, build the int32 plan (numpy),
 one pinned H2D copy, one or two graph launches.
 """
 import math
+import os
+import time
 
 import numpy as np
 import torch
@@ -151,6 +153,8 @@ class TrainStep:
         self.flat_grads = None if isinstance(self.model, DistributedDataParallel) else FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket
         self.max_graphs = max_graphs
+        # HYDRA_STEP_TIMING=1: accumulate host seconds per graph_step phase
+        self.host_times = {} if os.environ.get("HYDRA_STEP_TIMING") == "1" else None
         self.graphs = {}
         self.pool = None
         self.B = None
@@ -181,7 +185,7 @@ class TrainStep:
         nb, eb = self.node_bucket, self.edge_bucket
         return (int(math.ceil((N + 2) / nb) * nb), int(math.ceil(max(E, 1) / eb) * eb))
 
-    def prepare(self, store, batch_size, samples=256, seed=1234):
+    def prepare(self, store, batch_size, samples=1024, seed=1234):
         """Pre-compute the bucket set a random sampler will hit (capture happens lazily)."""
         self.B = batch_size
         if self.mode != "graph":
@@ -208,13 +212,16 @@ class TrainStep:
             if key in todo and key not in self.graphs:
                 self._capture(store, idx, key)
                 todo.discard(key)
+        self._frozen = bool(self.graphs)
 
     def _pick(self, N, E):
         want = self.bucket_of(N, E)
         if want in self.graphs:
             return want
         cands = [k for k in self.graphs if k[0] >= N + 2 and k[1] >= E]
-        if cands and len(self.graphs) >= self.max_graphs:
+        # after precapture (or at the cap) a rare unseen bucket replays the smallest
+        # captured bucket that fits: extra padding costs microseconds, a capture ~50 ms
+        if cands and (getattr(self, "_frozen", False) or len(self.graphs) >= self.max_graphs):
             return min(cands)
         return want
 
@@ -302,9 +309,18 @@ class TrainStep:
         if cap is None:
             cap = self._capture(store, indices, key)
             # the capture warm-up already trained on this batch; replay once more as the step
+        tm = self.host_times
+        t0 = time.perf_counter() if tm is not None else 0.0
         lay = store.layout(indices, Np=cap.lay.Np, Ep=cap.lay.Ep, Gp=cap.lay.Gp)
         store.upload(indices, lay, cap.dev_plan)
+        if tm is not None:
+            t1 = time.perf_counter()
         cap.g_fwd_bwd.replay()
+        if tm is not None:
+            t2 = time.perf_counter()
+            tm["plan+upload"] = tm.get("plan+upload", 0.0) + (t1 - t0)
+            tm["replay"] = tm.get("replay", 0.0) + (t2 - t1)
+            tm["n"] = tm.get("n", 0) + 1
         if cap.g_opt is not None:
             self.model.allreduce_now()
             cap.g_opt.replay()

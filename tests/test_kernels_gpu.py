@@ -11,7 +11,7 @@ import torch
 from hydragnn_amd import _native
 from hydragnn_amd.ops import segment as seg
 from hydragnn_amd.ops.attention import attention_reference, make_segments, segment_attention
-from hydragnn_amd.ops.pna import pna_avg_deg, pna_message_aggregate
+from hydragnn_amd.ops.pna import composite_mode, pna_avg_deg, pna_message_aggregate, pna_weight_prep
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -102,6 +102,24 @@ def test_pna_fused_vs_composite(F, with_edges):
     zg.backward(g.to(DEV))
     for a, b in zip(gpu, cpu):
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=2e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("F,d", [(64, 1), (32, 3), (5, 2)])
+def test_pna_weight_prep(F, d):
+    g = torch.Generator().manual_seed(F + d)
+    ps = [torch.randn(*sh, generator=g) for sh in ((F, 3 * F), (F,), (F, d + F), (F,))]
+    outs_g = [torch.randn(*sh, generator=g) for sh in ((2 * F, F), (F, F), (F, d), (F,))]
+
+    def run(dev, composite):
+        xs = [p.detach().clone().to(dev).requires_grad_(True) for p in ps]
+        with composite_mode(composite):
+            outs = pna_weight_prep(*xs)
+        sum((o * go.to(dev)).sum() for o, go in zip(outs, outs_g)).backward()
+        return [o.detach().cpu() for o in outs], [x.grad.cpu() for x in xs]
+
+    (o_ref, g_ref), (o_hip, g_hip) = run("cpu", True), run(DEV, False)
+    for a, b in zip(o_hip + g_hip, o_ref + g_ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("D", [4, 8, 16, 32, 64])
@@ -316,3 +334,75 @@ def test_tp_uvu_native_matches_reference(lmax_node, lmax_sh):
     out.backward(g.to(DEV))
     for a, b in zip(gin, ref_in):
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("G,dims,relus", [(33, [64, 50, 50, 50, 25, 1], [1, 1, 1, 1, 0]),
+                                          (64, [7, 128, 3], [1, 0]), (1, [16, 8], [1])])
+def test_fused_mlp_chain(G, dims, relus):
+    from torch import nn
+
+    from hydragnn_amd.ops.mlp import sequential_chain
+
+    torch.manual_seed(G)
+    mods = []
+    for i, r in enumerate(relus):
+        mods.append(nn.Linear(dims[i], dims[i + 1]))
+        if r:
+            mods.append(nn.ReLU())
+    seq = nn.Sequential(*mods[:2]), nn.Sequential(*mods[2:])
+    x = torch.randn(G, dims[0])
+    go = torch.randn(G, dims[-1])
+
+    def run(dev):
+        for s in seq:
+            s.to(dev).zero_grad()
+        xx = x.clone().to(dev).requires_grad_(True)
+        out = sequential_chain(xx, *seq) if dev == DEV else seq[1](seq[0](xx))
+        (out * go.to(dev)).sum().backward()
+        grads = [p.grad.cpu().clone() for s in seq for p in s.parameters()]
+        return out.detach().cpu(), xx.grad.cpu(), grads
+
+    o_r, dx_r, g_r = run("cpu")
+    o_h, dx_h, g_h = run(DEV)
+    torch.testing.assert_close(o_h, o_r, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dx_h, dx_r, rtol=1e-5, atol=1e-5)
+    for a, b in zip(g_h, g_r):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("E,F,K,L", [(3000, 64, 6, 3), (257, 70, 8, 1)])
+def test_radial_features(E, F, K, L):
+    from torch import nn
+
+    from hydragnn_amd.ops.geometry import BesselBasis
+    from hydragnn_amd.ops.radial import radial_features
+
+    torch.manual_seed(E)
+
+    class _C(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.rbf_emb = nn.Sequential(nn.Linear(K, F), nn.ReLU())
+            self.rbf_lin = nn.Linear(K, F, bias=False)
+
+    basis = BesselBasis(K, cutoff=5.0, envelope_exponent=5)
+    convs = nn.ModuleList([_C() for _ in range(L)])
+    dist = 0.3 + torch.rand(E) * 5.7  # some edges beyond the cutoff
+    gos = [(torch.randn(E, F), torch.randn(E, F)) for _ in range(L)]
+
+    def run(dev):
+        basis.to(dev).zero_grad()
+        convs.to(dev).zero_grad()
+        d = dist.clone().to(dev).requires_grad_(True)
+        outs = radial_features(d, basis, list(convs))
+        loss = sum((r * a.to(dev)).sum() + (g * b.to(dev)).sum() for (r, g), (a, b) in zip(outs, gos))
+        loss.backward()
+        grads = [d.grad, basis.freq.grad] + [p.grad for p in convs.parameters()]
+        return [t.detach().cpu() for rg in outs for t in rg], [g.detach().cpu().clone() for g in grads]
+
+    o_r, g_r = run("cpu")
+    o_h, g_h = run(DEV)
+    for a, b in zip(o_h, o_r):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+    for a, b in zip(g_h, g_r):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * max(1.0, float(b.abs().max())))

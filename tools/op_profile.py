@@ -15,6 +15,8 @@ from hydragnn_amd.models.create import create_model  # noqa: E402
 from hydragnn_amd.train.step import TrainStep  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+padded = "--padded" in sys.argv  # the captured step's computation (static padded buckets), run eagerly
+stacks = "--stacks" in sys.argv  # python call sites of the small elementwise kernels
 dev = torch.device("cuda:0")
 samples = oc20_like(256, seed=1000, radius=10.0, max_neighbours=10, pe_dim=16)
 deg = degree_histogram(samples, max_degree=10).to(torch.float64)
@@ -26,14 +28,15 @@ model = create_model("PNAPlus", 4, 64, [1], 16, "GPS", "multihead", 8, ["graph"]
 store = DeviceGraphStore(samples, dev, head_types=["graph"], head_dims=[1])
 step = TrainStep(model, lr=1e-3, mode="eager")
 rng = np.random.default_rng(0)
+run = step.padded_step if padded else step
 for _ in range(3):
-    step(store, list(rng.choice(len(store), 32, replace=False)))
+    run(store, list(rng.choice(len(store), 32, replace=False)))
 torch.cuda.synchronize()
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=stacks) as prof:
     for _ in range(steps):
-        step(store, list(rng.choice(len(store), 32, replace=False)))
+        run(store, list(rng.choice(len(store), 32, replace=False)))
     torch.cuda.synchronize()
 ka = prof.key_averages()
 rows = []
@@ -48,3 +51,10 @@ tot = sum(r[0] for r in rows)
 print(f"self device time per step: {tot / 1e3:.3f} ms")
 for dt, n, k in rows[:70]:
     print(f"{dt:9.1f} us {n:7.1f}/step  {k[:120]}")
+if stacks:  # shapes of the small elementwise ops (autograd accumulation has no python stack)
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key in ("aten::add_", "aten::fill_", "aten::add", "aten::copy_", "aten::mul", "aten::where",
+                     "aten::cat", "aten::mm", "aten::clamp_min", "aten::sum", "aten::addmv_") and \
+                getattr(e, "self_device_time_total", 0) > 0:
+            print(f"--- {e.key:16s} {e.count / steps:5.1f}/step {e.self_device_time_total / steps:7.1f} us  "
+                  f"{str(e.input_shapes)[:120]}")
