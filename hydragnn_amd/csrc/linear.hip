@@ -30,30 +30,38 @@ constexpr int kWT = 64;  // output tile edge
 constexpr int kWC = 32;  // rows per LDS chunk
 
 // Stage a 32-row x 64-col chunk of one operand: thread t -> rows t/16 and t/16+16, float4 column t%16.
+// Branch-free: row and column indices are clamped into range and out-of-range values
+// zeroed by selects.  (The first version guarded each load with if/else; the
+// compiler then drained the memory counter after every load, serialising the
+// "next chunk in flight" prefetch.)  VEC: ld, col0 and ncol are multiples of 4.
+template <bool VEC>
 __device__ __forceinline__ void wg_load(const float* __restrict__ base, int ld, int col0, int ncol, int row0,
-                                        int rend, bool vec, int t, float4 (&r)[2]) {
-  const int c = (t & 15) * 4;
+                                        int rend, int t, float4 (&r)[2]) {
+  const int c = col0 + (t & 15) * 4;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int row = row0 + (t >> 4) + 16 * h;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < rend) {
-      const float* p = base + (int64_t)row * ld + col0 + c;
-      const int valid = ncol - (col0 + c);
-      if (vec && valid >= 4) {
-        v = *reinterpret_cast<const float4*>(p);
-      } else {
-        v.x = valid > 0 ? p[0] : 0.f;
-        v.y = valid > 1 ? p[1] : 0.f;
-        v.z = valid > 2 ? p[2] : 0.f;
-        v.w = valid > 3 ? p[3] : 0.f;
-      }
+    const int row_u = row0 + (t >> 4) + 16 * h;
+    const bool rv = row_u < rend;
+    const float* p = base + (int64_t)min(row_u, rend - 1) * ld;
+    float4 v;
+    if constexpr (VEC) {
+      const bool cv = c < ncol;
+      v = *reinterpret_cast<const float4*>(p + min(c, ncol - 4));
+      if (!(rv && cv)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const float a0 = p[min(c, ncol - 1)], a1 = p[min(c + 1, ncol - 1)];
+      const float a2 = p[min(c + 2, ncol - 1)], a3 = p[min(c + 3, ncol - 1)];
+      v.x = rv && c < ncol ? a0 : 0.f;
+      v.y = rv && c + 1 < ncol ? a1 : 0.f;
+      v.z = rv && c + 2 < ncol ? a2 : 0.f;
+      v.w = rv && c + 3 < ncol ? a3 : 0.f;
     }
     r[h] = v;
   }
 }
 
 // part layout: [S][O*I + O]   (dW partial, then db partial)
+template <bool VY, bool VX>
 __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restrict__ dY, int ldy,
                                                             const float* __restrict__ X, int ldx,
                                                             float* __restrict__ part, int with_bias, int M, int O,
@@ -69,8 +77,6 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int obq = (lane >> 3) * 2, ibq = (lane & 7) * 2;  // float4 column index of this lane's 8-block
-  const bool vy = (ldy & 3) == 0 && (to0 & 3) == 0;
-  const bool vx = (ldx & 3) == 0 && (ti0 & 3) == 0;
   const bool bias_lane = with_bias && ti0 == 0 && (lane & 7) == 0;
   float acc[8][8];
 #pragma unroll
@@ -81,8 +87,8 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
   const int nch = (r1 - r0 + kWC - 1) / kWC;
   float4 ry[2], rx[2];
   if (nch > 0) {
-    wg_load(dY, ldy, to0, O, r0, r1, vy, t, ry);
-    wg_load(X, ldx, ti0, I, r0, r1, vx, t, rx);
+    wg_load<VY>(dY, ldy, to0, O, r0, r1, t, ry);
+    wg_load<VX>(X, ldx, ti0, I, r0, r1, t, rx);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       Ys[((t >> 4) + 16 * h) * 16 + (t & 15)] = ry[h];
@@ -94,8 +100,8 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
     const int b = c & 1;
     const bool more = c + 1 < nch;
     if (more) {  // issue the next chunk's global loads before computing this one
-      wg_load(dY, ldy, to0, O, r0 + (c + 1) * kWC, r1, vy, t, ry);
-      wg_load(X, ldx, ti0, I, r0 + (c + 1) * kWC, r1, vx, t, rx);
+      wg_load<VY>(dY, ldy, to0, O, r0 + (c + 1) * kWC, r1, t, ry);
+      wg_load<VX>(X, ldx, ti0, I, r0 + (c + 1) * kWC, r1, t, rx);
     }
     const float4* yb = Ys + b * kWC * 16;
     const float4* xb = Xs + b * kWC * 16;
@@ -221,9 +227,21 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
   const int64_t ld = (int64_t)O * I + O;
   auto part = at::empty({S, ld}, dY.options());
   dim3 grid(tiles, S);
-  wgrad_partial_kernel<<<grid, 256, 0, stream()>>>(dY.data_ptr<float>(), (int)dY.stride(0), X.data_ptr<float>(),
-                                                   (int)X.stride(0), part.data_ptr<float>(), with_bias ? 1 : 0,
-                                                   (int)M, O, I, rpb, tiles_i);
+  const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0;
+  const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0;
+#define HY_WGRAD(A, B)                                                                                            \
+  wgrad_partial_kernel<A, B><<<grid, 256, 0, stream()>>>(dY.data_ptr<float>(), (int)dY.stride(0),               \
+                                                         X.data_ptr<float>(), (int)X.stride(0), part.data_ptr<float>(), \
+                                                         with_bias ? 1 : 0, (int)M, O, I, rpb, tiles_i)
+  if (vy && vx)
+    HY_WGRAD(true, true);
+  else if (vy)
+    HY_WGRAD(true, false);
+  else if (vx)
+    HY_WGRAD(false, true);
+  else
+    HY_WGRAD(false, false);
+#undef HY_WGRAD
   // dW block [0, O*I) and bias block [O*I, O*I+O) are contiguous in both part and out
   sum_partials_kernel<<<ceil_div(n, 64), 64 * kSpWaves, 0, stream()>>>(part.data_ptr<float>(), out.data_ptr<float>(), S, n, ld);
   return {dW, db};

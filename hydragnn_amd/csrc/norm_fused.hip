@@ -105,6 +105,12 @@ struct Geo {
   int tpr, rpb, ngrp, slab;  // threads per row, rows per block-step, channel groups (C / V), rows per block
 };
 
+// Row index clamped into [0, r1): loads are issued unconditionally at clamped
+// addresses and masked where used.  A guarded (if/else) load makes the compiler
+// drain the memory counter at the branch join, serialising the kRows loads a
+// thread is meant to have in flight.
+__device__ __forceinline__ int rowc(int r, int r1) { return max(min(r, r1 - 1), 0); }
+
 
 // Sum over the S slab partials of channel c, T threads per channel (thread j takes
 // s = j, j+T, ...), folded across the T threads in a fixed order.  red: [kBlk].
@@ -212,11 +218,15 @@ __global__ void __launch_bounds__(kBlk)
     const int cg = cg0 + cg_l;
     const bool act = cg < g.ngrp;
     const int c0 = cg * V;
-    T v[kRows];
+    // unconditional loads at clamped addresses (see rowc); validity is applied where
+    // the values are used
+    const int c0c = min(cg, g.ngrp - 1) * V;
+    T v[kRows], bbv[kRows];
 #pragma unroll
-    for (int i = 0; i < kRows; ++i) {
-      const int r = r0 + rl + i * g.rpb;
-      if (act && r < r1) v[i] = ldv<V>(a + (int64_t)r * C + c0);
+    for (int i = 0; i < kRows; ++i) v[i] = ldv<V>(a + (int64_t)rowc(r0 + rl + i * g.rpb, r1) * C + c0c);
+    if (fused && b) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) bbv[i] = ldv<V>(b + (int64_t)rowc(r0 + rl + i * g.rpb, r1) * C + c0c);
     }
     if (fused) {
 #pragma unroll
@@ -224,8 +234,7 @@ __global__ void __launch_bounds__(kBlk)
         const int r = r0 + rl + i * g.rpb;
         if (act && r < r1) {
           const int64_t off = (int64_t)r * C + c0;
-          T bb;
-          if (b) bb = ldv<V>(b + off);
+          const T bb = bbv[i];
 #pragma unroll
           for (int k = 0; k < V; ++k) {
             float x = el<V>(v[i], k);
@@ -308,12 +317,9 @@ __global__ void __launch_bounds__(kBlk)
   // prefetch this slab's rows (first channel-group pass) before touching the partials
   typename VecT<V>::T v[kRows];
   {
-    const int c0 = cg_l * V;
+    const int c0 = min(cg_l, g.ngrp - 1) * V;
 #pragma unroll
-    for (int i = 0; i < kRows; ++i) {
-      const int r = r0 + rl + i * g.rpb;
-      if (cg_l < g.ngrp && r < r1) v[i] = ldv<V>(zr + (int64_t)r * C + c0);
-    }
+    for (int i = 0; i < kRows; ++i) v[i] = ldv<V>(zr + (int64_t)rowc(r0 + rl + i * g.rpb, r1) * C + c0);
   }
   const int TT = max(1, kBlk / C);
   for (int cb = 0; cb < C; cb += kBlk / TT) {
@@ -322,13 +328,17 @@ __global__ void __launch_bounds__(kBlk)
     // all of this thread's partials in registers (one memory round trip)
     constexpr int kQ = 16;
     float qn[kQ], qm[kQ], q2[kQ];
+    const int cc = min(c, C - 1);
 #pragma unroll
     for (int t = 0; t < kQ; ++t) {
-      const int q = j + t * TT;
-      const bool in = ok && q < S;
-      qn[t] = in ? part[(int64_t)q * 3 * C + c] : 0.f;
-      qm[t] = in ? part[(int64_t)q * 3 * C + C + c] : 0.f;
-      q2[t] = in ? part[(int64_t)q * 3 * C + 2 * C + c] : 0.f;
+      const int64_t o = (int64_t)min(j + t * TT, S - 1) * 3 * C + cc;
+      qn[t] = part[o];
+      qm[t] = part[o + C];
+      q2[t] = part[o + 2 * C];
+    }
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      if (!(ok && j + t * TT < S)) qn[t] = qm[t] = q2[t] = 0.f;
     }
     float n = 0.f, sm = 0.f;
 #pragma unroll
@@ -420,22 +430,21 @@ __global__ void __launch_bounds__(kBlk)
     const bool act = cg < g.ngrp;
     const int c0 = cg * V;
     float sg[V], sx[V], mu[V], is[V], ww[V], bb[V];
+    const int c0c = min(cg, g.ngrp - 1) * V;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       sg[k] = sx[k] = 0.f;
-      mu[k] = act ? mean[c0 + k] : 0.f;
-      is[k] = act ? invstd[c0 + k] : 0.f;
-      ww[k] = (act && w) ? w[c0 + k] : 1.f;
-      bb[k] = (act && beta) ? beta[c0 + k] : 0.f;
+      mu[k] = mean[c0c + k];
+      is[k] = invstd[c0c + k];
+      ww[k] = w ? w[c0c + k] : 1.f;
+      bb[k] = beta ? beta[c0c + k] : 0.f;
     }
     typename VecT<V>::T gv[kRows], zv[kRows];
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
-      const int r = r0 + rl + i * g.rpb;
-      if (act && r < r1) {
-        gv[i] = ldv<V>(dy + (int64_t)r * C + c0);
-        zv[i] = ldv<V>(z + (int64_t)r * C + c0);
-      }
+      const int64_t off = (int64_t)rowc(r0 + rl + i * g.rpb, r1) * C + c0c;
+      gv[i] = ldv<V>(dy + off);
+      zv[i] = ldv<V>(z + off);
     }
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
@@ -482,14 +491,12 @@ __global__ void __launch_bounds__(kBlk)
   const int rl = threadIdx.x / g.tpr, cg_l = threadIdx.x % g.tpr;
   typename VecT<V>::T gvs[kRows], zvs[kRows];
   {
-    const int c0 = cg_l * V;
+    const int c0 = min(cg_l, g.ngrp - 1) * V;
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
-      const int r = r0 + rl + i * g.rpb;
-      if (cg_l < g.ngrp && r < r1) {
-        gvs[i] = ldv<V>(dy + (int64_t)r * C + c0);
-        zvs[i] = ldv<V>(z + (int64_t)r * C + c0);
-      }
+      const int64_t off = (int64_t)rowc(r0 + rl + i * g.rpb, r1) * C + c0;
+      gvs[i] = ldv<V>(dy + off);
+      zvs[i] = ldv<V>(z + off);
     }
   }
   const int TT = max(1, kBlk / C);
@@ -498,12 +505,16 @@ __global__ void __launch_bounds__(kBlk)
     const bool ok = c < C && threadIdx.x < (kBlk / TT) * TT;
     constexpr int kQ = 16;
     float qa[kQ], qb[kQ];
+    const int cc = min(c, C - 1);
 #pragma unroll
     for (int t = 0; t < kQ; ++t) {
-      const int q = j + t * TT;
-      const bool in = ok && q < S;
-      qa[t] = in ? part[(int64_t)q * 2 * C + c] : 0.f;
-      qb[t] = in ? part[(int64_t)q * 2 * C + C + c] : 0.f;
+      const int64_t o = (int64_t)min(j + t * TT, S - 1) * 2 * C + cc;
+      qa[t] = part[o];
+      qb[t] = part[o + C];
+    }
+#pragma unroll
+    for (int t = 0; t < kQ; ++t) {
+      if (!(ok && j + t * TT < S)) qa[t] = qb[t] = 0.f;
     }
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll

@@ -11,16 +11,17 @@
 // elementwise chain) are ~50 launches per step for a 3-layer stack.  Here:
 //   forward : one kernel: the basis values are computed once per (edge, k) into LDS,
 //             lanes stream the features and write r_l, G_l for all layers;
-//   backward: one kernel: per-workgroup partial sums of dW_emb, db_emb, dW_lin
-//             (lanes over features), then the per-edge drbf_k = sum_l sum_f dr_l
-//             W_emb_l + dG_l W_lin_l (threads over edges, rows L2-hot), ddist and
-//             dfreq -> one fixed-order partial-sum pass.
+//   backward: one kernel, one pass over (R, dR, dG): per-workgroup partial sums
+//             of dW_emb, db_emb, dW_lin (lanes over features) and the per-edge
+//             drbf_k = sum_l sum_f dr_l W_emb_l + dG_l W_lin_l (register
+//             accumulators, one wave reduction per (edge, k)), ddist and dfreq ->
+//             one fixed-order partial-sum pass.
 // Deterministic, no atomics.  Double backward (forces) uses the torch composite.
 #include "common.h"
 
 namespace hy {
 
-constexpr int kRadMaxK = 16;
+constexpr int kRadMaxK = 8;
 constexpr int kRadMaxL = 8;
 constexpr int kRadBwdEdges = 64;      // edges per backward workgroup (partials per WG)
 
@@ -46,21 +47,22 @@ __device__ __forceinline__ void envelope(const RadEnv& ev, float x, float& u, fl
 // W layout: Wemb [L][F][K], bemb [L][F], Wlin [L][F][K];  out R, Gt: [L][E][F]
 // Block: 16 edges; the 16 x K basis values are computed ONCE (one thread each) into
 // LDS, then each wave streams 4 edges x F features with the (l, f) weights held in
-// registers.
+// registers.  K is a template parameter (loops fully unrolled, no guards).
 constexpr int kRadFwdEdges = 16;
 
+template <int K>
 __global__ void __launch_bounds__(256) radial_fwd_kernel(const float* __restrict__ dist, int64_t E,
-                                                         const float* __restrict__ freq, int K,
+                                                         const float* __restrict__ freq,
                                                          const float* __restrict__ Wemb,
                                                          const float* __restrict__ bemb,
                                                          const float* __restrict__ Wlin, int L, int F, RadEnv ev,
                                                          float* __restrict__ R, float* __restrict__ Gt) {
-  __shared__ float rb[kRadFwdEdges][kRadMaxK];
+  __shared__ float rb[kRadFwdEdges][K];
   const int64_t e0 = (int64_t)blockIdx.x * kRadFwdEdges;
   const int ne = (int)min<int64_t>(kRadFwdEdges, E - e0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int idx = threadIdx.x; idx < ne * K; idx += blockDim.x) {
-    const int el = idx / K, k = idx % K;
+  if (threadIdx.x < ne * K) {
+    const int el = threadIdx.x / K, k = threadIdx.x % K;
     const float x = dist[e0 + el] * ev.inv_c;
     float u, du;
     envelope(ev, x, u, du);
@@ -69,21 +71,19 @@ __global__ void __launch_bounds__(256) radial_fwd_kernel(const float* __restrict
   __syncthreads();
   for (int f = lane; f < F; f += 64) {
     for (int l = 0; l < L; ++l) {
-      float we[kRadMaxK], wl[kRadMaxK];
+      float we[K], wl[K];
 #pragma unroll
-      for (int k = 0; k < kRadMaxK; ++k) {
-        we[k] = k < K ? Wemb[((int64_t)l * F + f) * K + k] : 0.f;
-        wl[k] = k < K ? Wlin[((int64_t)l * F + f) * K + k] : 0.f;
+      for (int k = 0; k < K; ++k) {
+        we[k] = Wemb[((int64_t)l * F + f) * K + k];
+        wl[k] = Wlin[((int64_t)l * F + f) * K + k];
       }
       const float b0 = bemb[l * F + f];
       for (int el = w; el < ne; el += 4) {
         float r = b0, g = 0.f;
 #pragma unroll
-        for (int k = 0; k < kRadMaxK; ++k) {
-          if (k < K) {
-            r = fmaf(we[k], rb[el][k], r);
-            g = fmaf(wl[k], rb[el][k], g);
-          }
+        for (int k = 0; k < K; ++k) {
+          r = fmaf(we[k], rb[el][k], r);
+          g = fmaf(wl[k], rb[el][k], g);
         }
         const int64_t o = ((int64_t)l * E + e0 + el) * F + f;
         R[o] = fmaxf(r, 0.f);
@@ -94,31 +94,34 @@ __global__ void __launch_bounds__(256) radial_fwd_kernel(const float* __restrict
 }
 
 // part layout per workgroup: [L][F][2K+1] (dWemb k, dWlin k, dbemb) then [K] dfreq.
-// Block: 64 edges, wave w owns edges w, w+4, ... in the weight-gradient pass:
-// per (f-chunk, layer) the lanes accumulate their features' weight gradients over
-// the wave's edges.  Then 4 threads per edge reduce drbf over (layer, feature) with the weights
-// broadcast from LDS (rows still L2-hot), and per-edge ddist / dfreq terms follow.
+// Block: 64 edges, wave w owns the 16 edges w*16 .. w*16+15; lanes own features.
+// ONE pass over (R, dR, dG): per (f-chunk, layer) the wave's 16 rows are loaded
+// at once (one latency round); each lane accumulates its features' weight
+// gradients (folded over the 4 waves in LDS, fixed order) AND its share of every
+// edge's input-side term  sum_f dr W_emb[f,k] + dg W_lin[f,k]  in registers
+// (16 x K accumulators), which are wave-reduced once at the end.
+template <int K>
 __global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict__ dR, const float* __restrict__ dG,
                                                          const float* __restrict__ R,
                                                          const float* __restrict__ dist, int64_t E,
-                                                         const float* __restrict__ freq, int K,
+                                                         const float* __restrict__ freq,
                                                          const float* __restrict__ Wemb,
                                                          const float* __restrict__ Wlin, int L, int F, RadEnv ev,
                                                          float* __restrict__ ddist, float* __restrict__ part,
                                                          int64_t part_ld) {
-  __shared__ float rb[kRadBwdEdges][kRadMaxK];
-  __shared__ float drb[kRadBwdEdges][4][kRadMaxK];  // 4 feature-quarter partials per edge
-  __shared__ float fold[4][64][2 * kRadMaxK + 1];
-  extern __shared__ float wsm[];  // [2][L][F][K]: W_emb then W_lin
+  constexpr int kPer = kRadBwdEdges / 4;
+  constexpr int per = 2 * K + 1;
+  __shared__ float rb[kRadBwdEdges][K];
+  __shared__ float drb[kRadBwdEdges][K];
+  __shared__ float fold[4][64][per];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t e0 = (int64_t)blockIdx.x * kRadBwdEdges;
   const int ne = (int)min<int64_t>(kRadBwdEdges, E - e0);
-  const int per = 2 * K + 1;
   float* P = part + blockIdx.x * part_ld;
-  for (int idx = threadIdx.x; idx < kRadBwdEdges * kRadMaxK; idx += blockDim.x) {
-    const int el = idx / kRadMaxK, k = idx % kRadMaxK;
+  for (int idx = threadIdx.x; idx < kRadBwdEdges * K; idx += blockDim.x) {
+    const int el = idx / K, k = idx % K;
     float v = 0.f;
-    if (el < ne && k < K) {
+    if (el < ne) {
       const float x = dist[e0 + el] * ev.inv_c;
       float u, du;
       envelope(ev, x, u, du);
@@ -126,41 +129,54 @@ __global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict
     }
     rb[el][k] = v;
   }
-  for (int idx = threadIdx.x; idx < L * F * K; idx += blockDim.x) {
-    wsm[idx] = Wemb[idx];
-    wsm[L * F * K + idx] = Wlin[idx];
-  }
   __syncthreads();
+  float acc[kPer][K];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i)
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[i][k] = 0.f;
   for (int f0 = 0; f0 < F; f0 += 64) {
     const int f = f0 + lane;
     const bool fv = f < F;
     for (int l = 0; l < L; ++l) {
-      float aWe[kRadMaxK], aWl[kRadMaxK], ab = 0.f;
+      float we[K], wl[K], aWe[K], aWl[K], ab = 0.f;
 #pragma unroll
-      for (int k = 0; k < kRadMaxK; ++k) aWe[k] = aWl[k] = 0.f;
-      for (int el = w; el < ne; el += 4) {
-        float dr = 0.f, dg = 0.f;
-        if (fv) {
-          const int64_t o = ((int64_t)l * E + e0 + el) * F + f;
-          dr = R[o] > 0.f ? dR[o] : 0.f;
-          dg = dG[o];
-        }
+      for (int k = 0; k < K; ++k) {
+        const int64_t wo = ((int64_t)l * F + min(f, F - 1)) * K + k;
+        we[k] = fv ? Wemb[wo] : 0.f;
+        wl[k] = fv ? Wlin[wo] : 0.f;
+        aWe[k] = aWl[k] = 0.f;
+      }
+      float vr[kPer], vd[kPer], vg[kPer];
+      // unconditional loads (clamped indices, masked after): a guarded load makes
+      // the compiler drain the memory counter per row, serialising the 16 loads
+      const int fc = min(f, F - 1);
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int el = min(w * kPer + i, ne - 1);
+        const int64_t o = ((int64_t)l * E + e0 + el) * F + fc;
+        vr[i] = R[o];
+        vd[i] = dR[o];
+        vg[i] = dG[o];
+      }
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int el = w * kPer + i;
+        const bool ok = fv && el < ne;
+        const float dr = ok && vr[i] > 0.f ? vd[i] : 0.f, dg = ok ? vg[i] : 0.f;
         ab += dr;
 #pragma unroll
-        for (int k = 0; k < kRadMaxK; ++k) {
-          if (k < K) {
-            aWe[k] = fmaf(dr, rb[el][k], aWe[k]);
-            aWl[k] = fmaf(dg, rb[el][k], aWl[k]);
-          }
+        for (int k = 0; k < K; ++k) {
+          aWe[k] = fmaf(dr, rb[el][k], aWe[k]);
+          aWl[k] = fmaf(dg, rb[el][k], aWl[k]);
+          acc[i][k] = fmaf(dr, we[k], fmaf(dg, wl[k], acc[i][k]));
         }
       }
       // fold the 4 waves (fixed order) and write this block's partial
 #pragma unroll
-      for (int k = 0; k < kRadMaxK; ++k) {
-        if (k < K) {
-          fold[w][lane][k] = aWe[k];
-          fold[w][lane][K + k] = aWl[k];
-        }
+      for (int k = 0; k < K; ++k) {
+        fold[w][lane][k] = aWe[k];
+        fold[w][lane][K + k] = aWl[k];
       }
       fold[w][lane][2 * K] = ab;
       __syncthreads();
@@ -173,28 +189,13 @@ __global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict
       __syncthreads();
     }
   }
-  // drbf_k[e] = sum_l sum_f dr W_emb[l,f,k] + dg W_lin[l,f,k]: 4 threads per edge
-  // (feature quarters, rows L2-hot from the pass above), weights broadcast from LDS
-  {
-    const int el = threadIdx.x >> 2, q = threadIdx.x & 3;
-    float acc[kRadMaxK];
 #pragma unroll
-    for (int k = 0; k < kRadMaxK; ++k) acc[k] = 0.f;
-    if (el < ne) {
-      for (int l = 0; l < L; ++l) {
-        const int64_t row = ((int64_t)l * E + e0 + el) * F;
-        for (int f = q; f < F; f += 4) {
-          const float dr = R[row + f] > 0.f ? dR[row + f] : 0.f, dg = dG[row + f];
-          const float* we = wsm + ((int64_t)l * F + f) * K;
-          const float* wl = wsm + (int64_t)L * F * K + ((int64_t)l * F + f) * K;
+  for (int i = 0; i < kPer; ++i) {
 #pragma unroll
-          for (int k = 0; k < kRadMaxK; ++k)
-            if (k < K) acc[k] = fmaf(dr, we[k], fmaf(dg, wl[k], acc[k]));
-        }
-      }
+    for (int k = 0; k < K; ++k) {
+      const float c = wave_sum(acc[i][k]);
+      if (lane == 0) drb[w * kPer + i][k] = c;
     }
-#pragma unroll
-    for (int k = 0; k < kRadMaxK; ++k) drb[el][q][k] = acc[k];
   }
   __syncthreads();
   // per edge: ddist = sum_k drbf_k d rbf_k / d dist; per-edge dfreq terms into rb (reused)
@@ -206,10 +207,11 @@ __global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict
       x = dist[e0 + el] * ev.inv_c;
       envelope(ev, x, u, du);
     }
+#pragma unroll
     for (int k = 0; k < K; ++k) {
       float sn, cs;
       sincosf(freq[k] * x, &sn, &cs);
-      const float g = el < ne ? ((drb[el][0][k] + drb[el][1][k]) + drb[el][2][k]) + drb[el][3][k] : 0.f;
+      const float g = el < ne ? drb[el][k] : 0.f;
       dd += g * (du * sn + u * cs * freq[k]);
       rb[el][k] = g * u * cs * x;  // d rbf_k / d freq_k contribution
     }
@@ -277,15 +279,30 @@ std::tuple<at::Tensor, at::Tensor> radial_fwd(const at::Tensor& dist_, const at:
   HY_CHECK_F32(dist);
   HY_CHECK_F32(freq);
   const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
-  HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL, "radial: 1 <= K <= 16, 1 <= L <= 8");
+  HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL, "radial: 1 <= K <= 8, 1 <= L <= 8");
   check_w(Wemb, L, F, K, "Wemb");
   check_w(Wlin, L, F, K, "Wlin");
   HY_CHECK(bemb.is_contiguous() && bemb.numel() == L * F, "bemb must be [L, F]");
   auto R = at::empty({L, E, F}, dist.options()), Gt = at::empty({L, E, F}, dist.options());
   if (E == 0) return {R, Gt};
-  radial_fwd_kernel<<<ceil_div(E, kRadFwdEdges), 256, 0, stream()>>>(
-      dist.data_ptr<float>(), E, freq.data_ptr<float>(), (int)K, Wemb.data_ptr<float>(), bemb.data_ptr<float>(),
-      Wlin.data_ptr<float>(), (int)L, (int)F, make_env(cutoff, exponent), R.data_ptr<float>(), Gt.data_ptr<float>());
+  const auto ev = make_env(cutoff, exponent);
+  const dim3 grid(ceil_div(E, kRadFwdEdges));
+#define HY_RAD_FWD(KK)                                                                                            \
+  radial_fwd_kernel<KK><<<grid, 256, 0, stream()>>>(dist.data_ptr<float>(), E, freq.data_ptr<float>(),            \
+                                                    Wemb.data_ptr<float>(), bemb.data_ptr<float>(),               \
+                                                    Wlin.data_ptr<float>(), (int)L, (int)F, ev, R.data_ptr<float>(), \
+                                                    Gt.data_ptr<float>())
+  switch (K) {
+    case 1: HY_RAD_FWD(1); break;
+    case 2: HY_RAD_FWD(2); break;
+    case 3: HY_RAD_FWD(3); break;
+    case 4: HY_RAD_FWD(4); break;
+    case 5: HY_RAD_FWD(5); break;
+    case 6: HY_RAD_FWD(6); break;
+    case 7: HY_RAD_FWD(7); break;
+    default: HY_RAD_FWD(8); break;
+  }
+#undef HY_RAD_FWD
   return {R, Gt};
 }
 
@@ -296,7 +313,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
   auto dR = dR_.contiguous(), dG = dG_.contiguous(), dist = dist_.contiguous(), freq = freq_.contiguous();
   const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
   HY_CHECK(dR.sizes() == R.sizes() && dG.sizes() == R.sizes() && R.is_contiguous(), "radial_bwd: grad shapes");
-  HY_CHECK(2 * L * F * K * (int64_t)sizeof(float) <= 64 * 1024, "radial_bwd: L*F*K must be <= 8192");
   const int64_t per = 2 * K + 1;
   const int64_t ld = L * F * per + K;
   const int nb = std::max(1, ceil_div(E, kRadBwdEdges));
@@ -304,16 +320,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
   auto sums = at::empty({ld}, dist.options());
   auto ddist = at::empty({E}, dist.options());
   if (E > 0) {
-    static bool attr = [] {
-      hipFuncSetAttribute((const void*)radial_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-      return true;
-    }();
-    (void)attr;
-    radial_bwd_kernel<<<nb, 256, 2 * L * F * K * sizeof(float), stream()>>>(dR.data_ptr<float>(), dG.data_ptr<float>(), R.data_ptr<float>(),
-                                                dist.data_ptr<float>(), E, freq.data_ptr<float>(), (int)K,
-                                                Wemb.data_ptr<float>(), Wlin.data_ptr<float>(), (int)L, (int)F,
-                                                make_env(cutoff, exponent), ddist.data_ptr<float>(),
-                                                part.data_ptr<float>(), ld);
+    const auto ev = make_env(cutoff, exponent);
+#define HY_RAD_BWD(KK)                                                                                              \
+  radial_bwd_kernel<KK><<<nb, 256, 0, stream()>>>(dR.data_ptr<float>(), dG.data_ptr<float>(), R.data_ptr<float>(), \
+                                                  dist.data_ptr<float>(), E, freq.data_ptr<float>(),               \
+                                                  Wemb.data_ptr<float>(), Wlin.data_ptr<float>(), (int)L, (int)F,   \
+                                                  ev, ddist.data_ptr<float>(), part.data_ptr<float>(), ld)
+    switch (K) {
+      case 1: HY_RAD_BWD(1); break;
+      case 2: HY_RAD_BWD(2); break;
+      case 3: HY_RAD_BWD(3); break;
+      case 4: HY_RAD_BWD(4); break;
+      case 5: HY_RAD_BWD(5); break;
+      case 6: HY_RAD_BWD(6); break;
+      case 7: HY_RAD_BWD(7); break;
+      default: HY_RAD_BWD(8); break;
+    }
+#undef HY_RAD_BWD
     radial_sum_kernel<<<ceil_div(ld, 64), 64 * kRadSumWaves, 0, stream()>>>(part.data_ptr<float>(), nb, ld, ld,
                                                                             sums.data_ptr<float>());
   } else {

@@ -2,8 +2,8 @@
 
 Reference: the per-branch shared MLP + per-head MLP of ``Base._multihead``
 (``hydragnn/models/Base.py:246-287``) applied to pooled graph features.  On the
-GPU a chain of up to 8 Linear(+ReLU) layers of width <= 128 over <= 64 rows is
-one forward and one backward launch; anything else (CPU, other activations,
+GPU a chain of up to 8 Linear(+ReLU) layers of width <= 128 over <= 1024 rows is
+one forward and two backward launches; anything else (CPU, other activations,
 composite/double-backward mode) runs the modules as written.
 """
 import torch
@@ -12,7 +12,8 @@ from torch import nn
 from .. import _native
 from . import pna as _mode
 
-MAX_ROWS = 64
+MAX_ROWS = 1024
+ROWS = 4  # rows per workgroup (csrc/mlp.hip kMlpRows)
 MAX_DIM = 128
 MAX_LAYERS = 8
 MAX_LDS = 159 * 1024
@@ -22,8 +23,8 @@ def _lds_ok(G, dims):
     """LDS footprint of the fused kernels (``csrc/mlp.hip`` fwd_lds / bwd_lds)."""
     w = sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
     md = max(dims) + 1
-    fwd = 4 * (w + 2 * G * md)
-    bwd = 4 * (w + G * (sum(dims[1:]) + dims[0] + md))
+    fwd = 4 * (w + 2 * ROWS * md)
+    bwd = 4 * (w + ROWS * (sum(dims[1:]) + dims[0] + md))
     return max(fwd, bwd) <= MAX_LDS
 
 

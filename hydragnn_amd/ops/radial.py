@@ -12,7 +12,7 @@ import torch
 from .. import _native
 from . import pna as _mode
 
-MAX_K = 16
+MAX_K = 8
 MAX_L = 8
 
 
@@ -35,8 +35,8 @@ def fused_ok(dist, basis, convs):
     if not (dist.is_cuda and dist.dtype == torch.float32 and not _mode._state["composite"]
             and 0 < len(convs) <= MAX_L and basis.freq.numel() <= MAX_K):
         return False
-    shape = convs[0].rbf_emb[0].weight.shape  # [F, K]; all layers equal, weights fit 64 KB LDS
-    return all(c.rbf_emb[0].weight.shape == shape for c in convs) and len(convs) * shape[0] * shape[1] <= 8192
+    shape = convs[0].rbf_emb[0].weight.shape  # [F, K]: all layers equal
+    return all(c.rbf_emb[0].weight.shape == shape for c in convs)
 
 
 def radial_features(dist, basis, convs):

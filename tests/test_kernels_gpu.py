@@ -337,7 +337,7 @@ def test_tp_uvu_native_matches_reference(lmax_node, lmax_sh):
 
 
 @pytest.mark.parametrize("G,dims,relus", [(33, [64, 50, 50, 50, 25, 1], [1, 1, 1, 1, 0]),
-                                          (64, [7, 128, 3], [1, 0]), (1, [16, 8], [1])])
+                                          (203, [7, 128, 3], [1, 0]), (1, [16, 8], [1])])
 def test_fused_mlp_chain(G, dims, relus):
     from torch import nn
 
