@@ -47,21 +47,46 @@ def parse():
     return ap.parse_args()
 
 
+def _spawn(args):
+    """``--gpus N`` without a launcher: start N ranks (one per GPU) through
+    torch.distributed.run as a CHILD process and exit with its code.  Runs before
+    anything touches the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
     # (RCCL refuses duplicate devices); the driver's N-GPU runs use RCCL ("nccl").
     backend = os.environ.get("BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
-    if world > 1:
+    use_pg = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ  # 1-rank torchrun runs keep the PG
+    if use_pg:
         torch.cuda.set_device(local % ndev)
         if backend == "nccl":
+            from hydragnn_amd.parallel.distributed import rccl_env
+
+            rccl_env()
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)

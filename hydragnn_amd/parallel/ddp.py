@@ -20,6 +20,7 @@ usually yields 1-3 large collectives per step — the regime where ring
 all-reduce over the 7 xGMI links is bandwidth-efficient.
 """
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -176,6 +177,145 @@ class DistributedDataParallel(nn.Module):
 
     def state_dict(self, *a, **k):
         return super().state_dict(*a, **k)
+
+
+class BucketedGradSync:
+    """Gradient all-reduce for the hipGraph-captured training step, overlapped with
+    backward (reference DDP ``distributed.py:332-351``).
+
+    All gradients live in ONE flat fp32 buffer laid out in reverse parameter order
+    (≈ the order backward produces them) and cut into contiguous buckets.  Backward
+    runs with ``p.grad = None`` so autograd hands over each fresh gradient without an
+    accumulate kernel; a post-accumulate hook counts the bucket down and, when the
+    bucket is complete, packs it (one batched copy + the 1/world pre-scale) on the
+    compute stream and launches its all-reduce on a dedicated high-priority comm
+    stream that waits only on that pack.  The rest of backward keeps running on the
+    compute stream while RCCL moves the bucket over xGMI; ``finish`` joins the comm
+    stream back before the optimizer reads the buffer.
+
+    Captured inside ``torch.cuda.graph`` the event fork/join becomes graph edges, so
+    the replayed step is ONE graph launch whose collective nodes run concurrently
+    with the remaining backward kernels.  On CPU tensors (gloo) the same code issues
+    async collectives and waits for them in ``finish``.
+    """
+
+    def __init__(self, params, process_group=None, bucket_cap_mb=None, min_buckets=2):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        order = list(reversed(self.params))
+        total = sum(p.numel() for p in order)
+        dev = order[0].device
+        self.flat = torch.zeros(total, device=dev, dtype=order[0].dtype)
+        nbytes = total * self.flat.element_size()
+        if bucket_cap_mb is None:
+            # small GNN models: a few buckets so the first all-reduce starts mid-backward; large
+            # models: 32 MB buckets (bandwidth-efficient ring size over the xGMI links)
+            cap = min(max(nbytes // min_buckets + 1, 256 * 1024), 32 * 1024 * 1024)
+        else:
+            cap = int(bucket_cap_mb * 1024 * 1024)
+        self.offset = {}
+        self.buckets = []  # (start, end, [params])
+        off, start, cur, cur_b = 0, 0, [], 0
+        for p in order:
+            nb = p.numel() * self.flat.element_size()
+            if cur and cur_b + nb > cap:
+                self.buckets.append((start, off, cur))
+                start, cur, cur_b = off, [], 0
+            self.offset[p] = off
+            cur.append(p)
+            cur_b += nb
+            off += p.numel()
+        if cur:
+            self.buckets.append((start, off, cur))
+        self.bucket_of = {}
+        for bi, (_, _, ps) in enumerate(self.buckets):
+            for p in ps:
+                self.bucket_of[p] = bi
+        self.pending = [0] * len(self.buckets)
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self.active = False
+        self.next = 0
+        self.comm = torch.cuda.Stream(device=dev, priority=-1) if dev.type == "cuda" else None
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(self._hook)
+        self.attach()
+
+    # -- grad storage
+    def attach(self):
+        for p in self.params:
+            o = self.offset[p]
+            p.grad = self.flat[o:o + p.numel()].view_as(p)
+
+    def release(self):
+        for p in self.params:
+            p.grad = None
+
+    def zero(self):
+        self.flat.zero_()
+
+    # -- sync protocol: begin() before backward, finish() after it
+    def begin(self):
+        # HYDRA_GRADSYNC_FORCE=1 exercises the collective path on a 1-rank group (tests)
+        self.active = self.world > 1 or (dist.is_initialized() and os.environ.get("HYDRA_GRADSYNC_FORCE") == "1")
+        self.pending = [len(ps) for (_, _, ps) in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self.next = 0
+
+    def _hook(self, p):
+        if not self.active:
+            return
+        bi = self.bucket_of[p]
+        self.pending[bi] -= 1
+        # launch in bucket-index order only: every rank then issues the identical
+        # collective sequence whatever order its autograd engine finished buckets in
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def _pack(self, bi):
+        s, e, ps = self.buckets[bi]
+        gs = [p.grad.reshape(-1) if p.grad is not None else
+              torch.zeros(p.numel(), device=self.flat.device, dtype=self.flat.dtype) for p in ps]
+        out = self.flat[s:e]
+        if len(gs) == 1:
+            out.copy_(gs[0])
+        else:
+            torch.cat(gs, out=out)
+        return out
+
+    def _launch(self, bi):
+        if self.launched[bi]:
+            return
+        self.launched[bi] = True
+        buf = self._pack(bi)
+        buf.mul_(1.0 / self.world)
+        if self.comm is None:
+            self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            return
+        self.comm.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.comm):
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+
+    def finish(self):
+        """Flush buckets never completed (parameters without a gradient), join the comm
+        stream, re-attach the flat views as ``p.grad``."""
+        if self.active:
+            for bi in range(len(self.buckets)):
+                if not self.launched[bi]:
+                    self._launch(bi)
+            if self.comm is not None:
+                torch.cuda.current_stream().wait_stream(self.comm)
+            for w in self.works:
+                w.wait()
+        else:
+            for bi in range(len(self.buckets)):
+                self._pack(bi)
+        self.works = []
+        self.active = False
+        self.attach()
 
 
 class _SyncBNFn(torch.autograd.Function):

@@ -65,6 +65,20 @@ def _default_backend():
     return "gloo"
 
 
+def rccl_env():
+    """RCCL settings for one MI355X node (xGMI, fully connected peers).
+
+    * ``NCCL_GRAPH_REGISTER=0``: the training step captures its gradient all-reduces
+      into a hipGraph; with user-buffer registration off, capture is purely local
+      (no peer handshake at capture time), so ranks may capture at different times.
+    * P2P stays enabled (the reference Frontier scripts' ``NCCL_P2P_DISABLE=1`` is a
+      multi-node workaround, SURVEY §5.8, and would route intra-node traffic
+      through host memory).
+    Existing user settings win."""
+    os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
 def setup_ddp(use_deepspeed=False, backend=None):
     """Initialise ``torch.distributed`` (``env://``, 1800 s timeout); returns (world_size, rank)."""
     if dist.is_initialized():
@@ -86,6 +100,7 @@ def setup_ddp(use_deepspeed=False, backend=None):
     os.environ["RANK"] = str(rank)
     os.environ.setdefault("LOCAL_RANK", str(get_local_rank()))
     if backend == "nccl" and torch.cuda.is_available():
+        rccl_env()
         torch.cuda.set_device(get_local_rank() % max(torch.cuda.device_count(), 1))
     dist.init_process_group(backend=backend, init_method="env://", timeout=timedelta(seconds=1800),
                             world_size=world_size, rank=rank)

@@ -1,32 +1,73 @@
 """ZeRO-1 optimizer-state sharding (reference: ``torch.distributed.optim.ZeroRedundancyOptimizer``
 selected by ``Optimizer.use_zero_redundancy``, ``utils/optimizer/optimizer.py:43-113``).
 
-Parameters are partitioned greedily by size over the ranks; every rank keeps
-optimizer state only for its shard and steps it, then each owner broadcasts its
-updated shard as ONE packed buffer (world_size collectives per step, not one
-per tensor).  ``consolidate_state_dict()`` gathers the full state to rank 0 for
+MI355X design — flat, element-sharded, two collectives per step:
+
+* every parameter is re-homed into ONE flat fp32 buffer ``P`` (``p.data`` becomes a
+  view), padded to a multiple of the world size; rank ``r`` owns the contiguous
+  slice ``P[r*S:(r+1)*S]`` and keeps optimizer state only for it;
+* ``step()``: the flat gradient ``G`` is **reduce-scattered** (each rank receives
+  the averaged gradient of its slice — RCCL over xGMI; ``reduce_grads=False`` when a
+  DDP wrapper already averaged the gradients, then the slice is just read), the
+  inner optimizer updates the slice, and the updated slices are **all-gathered**
+  back into ``P``.  Bytes on the wire: 1x reduce-scatter + 1x all-gather of the
+  parameter vector, i.e. the same as one all-reduce (vs. the reference's
+  all-reduce + world_size broadcasts);
+* element-wise optimizers (SGD/Adam/AdamW/Adadelta/Adagrad/Adamax/RMSprop) are
+  exactly the unsharded update.  Optimizers with per-tensor statistics
+  (FusedLAMB's trust ratio) use per-parameter ownership instead (greedy by size)
+  with the same all-gather of owner slices.
+
+``consolidate_state_dict()`` gathers every shard's state to rank ``to`` for
 checkpointing (reference ``model.py:67-68``).
 """
 import torch
 import torch.distributed as dist
 
 
+def _gloo(group):
+    return dist.get_backend(group) == "gloo"
+
+
 class ZeroRedundancyOptimizer(torch.optim.Optimizer):
-    def __init__(self, params, optimizer_factory, process_group=None):
-        params = list(params)
+    def __init__(self, params, optimizer_factory, process_group=None, reduce_grads=False, elementwise=True):
+        params = [p for p in params]
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
-        sizes = [0] * self.world
-        self.owner = {}
-        self.shards = [[] for _ in range(self.world)]
-        for p in sorted(params, key=lambda t: -t.numel()):
-            r = min(range(self.world), key=lambda k: sizes[k])
-            sizes[r] += p.numel()
-            self.shards[r].append(p)
-            self.owner[p] = r
+        self.reduce_grads = reduce_grads
+        self.elementwise = elementwise
         self.all_params = params
-        local = self.shards[self.rank]
+        total = sum(p.numel() for p in params)
+        S = (total + self.world - 1) // self.world
+        dev = params[0].device
+        dt = params[0].dtype
+        self.S = S
+        self.flat = torch.zeros(S * self.world, device=dev, dtype=dt)
+        self.flat_grad = torch.zeros_like(self.flat)
+        self.offset = {}
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.data.reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+                self.offset[p] = off
+                off += n
+        if elementwise:
+            lo = self.rank * S
+            self.shard = torch.nn.Parameter(self.flat[lo:lo + S], requires_grad=True)
+            self.shard.grad = torch.zeros(S, device=dev, dtype=dt)
+            local = [self.shard]
+            self.owner_ranges = [(r * S, (r + 1) * S) for r in range(self.world)]
+        else:
+            sizes = [0] * self.world
+            self.shards = [[] for _ in range(self.world)]
+            for p in sorted(params, key=lambda t: -t.numel()):
+                r = min(range(self.world), key=lambda k: sizes[k])
+                sizes[r] += p.numel()
+                self.shards[r].append(p)
+            local = self.shards[self.rank]
         self.optim = optimizer_factory(local) if local else None
         super().__init__(params, {"lr": self.optim.defaults["lr"] if self.optim else 0.0})
         if self.optim is not None:
@@ -34,12 +75,46 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
             self.param_groups[0]["lr"] = self.optim.param_groups[0]["lr"]
         self._consolidated = None
 
+    # ------------------------------------------------------------------ step
+    def _pack_grads(self):
+        for p in self.all_params:
+            if p.grad is None:
+                continue
+            o = self.offset[p]
+            view = self.flat_grad[o:o + p.numel()]
+            if p.grad.data_ptr() != view.data_ptr():
+                view.copy_(p.grad.reshape(-1))
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         if self.optim is not None:
             for g in self.optim.param_groups:
                 g["lr"] = self.param_groups[0]["lr"]
+        if self.elementwise:
+            self._pack_grads()
+            lo = self.rank * self.S
+            if self.world > 1 and self.reduce_grads:
+                if _gloo(self.group):
+                    dist.all_reduce(self.flat_grad, group=self.group)
+                    self.shard.grad.copy_(self.flat_grad[lo:lo + self.S])
+                else:
+                    dist.reduce_scatter_tensor(self.shard.grad, self.flat_grad, group=self.group)
+                self.shard.grad.mul_(1.0 / self.world)
+            else:
+                self.shard.grad.copy_(self.flat_grad[lo:lo + self.S])
+            self.optim.step()
+            if self.world > 1:
+                self._all_gather_flat()
+            return loss
+        if self.world > 1 and self.reduce_grads:
+            self._pack_grads()
+            dist.all_reduce(self.flat_grad, group=self.group)
+            self.flat_grad.mul_(1.0 / self.world)
+            for p in self.all_params:
+                o = self.offset[p]
+                p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+        if self.optim is not None:
             self.optim.step()
         if self.world > 1:
             for r in range(self.world):
@@ -55,6 +130,18 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
                     off += p.numel()
         return loss
 
+    def _all_gather_flat(self):
+        lo = self.rank * self.S
+        mine = self.flat[lo:lo + self.S]
+        if _gloo(self.group):
+            outs = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(outs, mine.clone(), group=self.group)
+            for r, t in enumerate(outs):
+                if r != self.rank:
+                    self.flat[r * self.S:(r + 1) * self.S].copy_(t)
+        else:
+            dist.all_gather_into_tensor(self.flat, mine.clone(), group=self.group)
+
     def zero_grad(self, set_to_none=True):
         for p in self.all_params:
             if p.grad is not None:
@@ -63,6 +150,7 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
                 else:
                     p.grad.zero_()
 
+    # ------------------------------------------------------------------ state
     def consolidate_state_dict(self, to=0):
         """Gather every shard's optimizer state on rank ``to``."""
         local = self.optim.state_dict() if self.optim is not None else None
@@ -75,9 +163,10 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
 
     def state_dict(self):
         if self._consolidated is not None:
-            return {"shards": self._consolidated, "param_groups": self.param_groups_meta()}
+            return {"shards": self._consolidated, "param_groups": self.param_groups_meta(),
+                    "layout": "flat" if self.elementwise else "param"}
         return {"shards": [self.optim.state_dict() if self.optim is not None else None],
-                "param_groups": self.param_groups_meta()}
+                "param_groups": self.param_groups_meta(), "layout": "flat" if self.elementwise else "param"}
 
     def param_groups_meta(self):
         return [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]

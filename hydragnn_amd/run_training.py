@@ -86,6 +86,13 @@ def _(config: dict, use_deepspeed=False):
         world = dist.get_world_size() if dist.is_initialized() else 1
         engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer)
         engine.prepare(train_loader.store, train_loader.batch_size)
+    from .parallel.zero import ZeroRedundancyOptimizer
+
+    if isinstance(optimizer, ZeroRedundancyOptimizer) and hasattr(model, "_sync_enabled") and \
+            (engine is None or engine.sync is None):
+        # eager DDP + ZeRO-1: the optimizer reduce-scatters the gradients itself (no all-reduce)
+        model._sync_enabled = False
+        optimizer.reduce_grads = True
     print_distributed(verbosity, f"model: {nn_cfg['Architecture']['mpnn_type']}, "
                                  f"params: {sum(p.numel() for p in model.parameters())}")
     train_validate_test(model, optimizer, train_loader, val_loader, test_loader, writer, scheduler, nn_cfg, log_name,

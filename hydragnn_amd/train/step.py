@@ -12,9 +12,11 @@ whole step —
 — as hipGraphs (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replays
 them.  Shapes are made static by padding every batch up to a (nodes, edges)
 bucket (``DeviceGraphStore.layout``); one graph is captured per bucket (a
-handful per dataset) with its own memory pool.  For world_size > 1 the step is
-split in two graphs around an eager bucketed all-reduce of the flat gradient
-buffers (RCCL over xGMI): [assemble+fwd+bwd] -> all_reduce -> [optimizer].
+handful per dataset) with its own memory pool.  For world_size > 1 the bucketed
+gradient all-reduces (RCCL over xGMI) are captured INTO the same graph on a
+comm stream that forks off backward as each bucket completes
+(``parallel.ddp.BucketedGradSync``): one graph launch per step, collectives
+overlapped with the remaining backward kernels.
 
 The per-step host work is only: draw indices, build the int32 plan (numpy),
 one pinned H2D copy, one or two graph launches.
@@ -26,7 +28,7 @@ import time
 import numpy as np
 import torch
 
-from ..parallel.ddp import DistributedDataParallel
+from ..parallel.ddp import BucketedGradSync, DistributedDataParallel
 
 
 def masked_loss(kind, pred, target, mask=None, var=None):
@@ -118,6 +120,14 @@ class FlatGrads:
         self.attach()
 
 
+def _broadcast_state(module):
+    import torch.distributed as dist
+
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src=0)
+
+
 class _Captured:
     def __init__(self):
         self.g_fwd_bwd = None
@@ -130,27 +140,40 @@ class _Captured:
 
 class TrainStep:
     def __init__(self, model, lr=1e-3, mode="graph", world=1, optimizer=None, weight_decay=0.01,
-                 node_bucket=256, edge_bucket=2048, max_graphs=16):
+                 node_bucket=256, edge_bucket=2048, max_graphs=16, bucket_cap_mb=None):
         self.model = model
         self.module = model.module if isinstance(model, DistributedDataParallel) else model
         self.world = world
         self.mode = mode
         dev = next(self.module.parameters()).device
         self.device = dev
-        if world > 1 and not isinstance(model, DistributedDataParallel):
-            self.model = DistributedDataParallel(model)
-            self.module = self.model.module
-        params = [p for p in self.model.parameters() if p.requires_grad]
-        if optimizer is None:
-            from ..optim.adamw import FusedAdamW
-
-            optimizer = FusedAdamW(params, lr=lr, weight_decay=weight_decay)
         if mode == "graph" and getattr(self.module, "num_branches", 1) > 1:
             # multi-branch decode routes graphs by their (host-known) branch ranges, which
             # change from batch to batch: such models step eagerly
             self.mode = mode = "eager"
+        if world > 1 and mode == "eager" and not isinstance(model, DistributedDataParallel):
+            self.model = DistributedDataParallel(model)
+            self.module = self.model.module
+        params = [p for p in self.module.parameters() if p.requires_grad]
+        if optimizer is None:
+            from ..optim.adamw import FusedAdamW
+
+            optimizer = FusedAdamW(params, lr=lr, weight_decay=weight_decay)
         self.opt = optimizer
-        self.flat_grads = None if isinstance(self.model, DistributedDataParallel) else FlatGrads(params)
+        self.sync = None
+        self.flat_grads = None
+        if mode == "graph":
+            # captured / padded steps: gradients in one flat buffer; for world > 1 its buckets
+            # are all-reduced on a comm stream while backward is still running
+            if isinstance(self.model, DistributedDataParallel):
+                self.model._sync_enabled = False  # the wrapper's own hooks stand down
+                self.model = self.module
+            elif world > 1:
+                _broadcast_state(self.module)
+            cap = bucket_cap_mb if world > 1 else 1e9
+            self.sync = BucketedGradSync(params, bucket_cap_mb=cap)
+        elif not isinstance(self.model, DistributedDataParallel):
+            self.flat_grads = FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket
         self.max_graphs = max_graphs
         # HYDRA_STEP_TIMING=1: accumulate host seconds per graph_step phase
@@ -161,12 +184,20 @@ class TrainStep:
 
     # ------------------------------------------------------------------ eager
     def _zero(self):
-        if isinstance(self.model, DistributedDataParallel):
+        if self.sync is not None:
+            self.sync.release()
+        elif isinstance(self.model, DistributedDataParallel):
             self.model.zero_grad()
         else:
             self.flat_grads.release()
 
-    def _backward(self, loss):
+    def _backward(self, loss, sync=True):
+        if self.sync is not None:
+            if sync:
+                self.sync.begin()
+            loss.backward()
+            self.sync.finish()
+            return
         loss.backward()
         if self.flat_grads is not None:
             self.flat_grads.gather()
@@ -225,12 +256,12 @@ class TrainStep:
             return min(cands)
         return want
 
-    def _body_fwd_bwd(self, store, cap):
+    def _body_fwd_bwd(self, store, cap, sync=True):
         self._zero()
         batch = store.assemble(cap.dev_plan, cap.lay)
         pred = self.model(batch)
         loss, tasks = batch_loss(self.module, pred, batch)
-        self._backward(loss)
+        self._backward(loss, sync=sync)
         return loss.detach(), [t.detach() for t in tasks]
 
     def _opt_state_tensors(self):
@@ -268,32 +299,28 @@ class TrainStep:
         cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap.dev_plan = torch.empty(cap.lay.total, dtype=torch.int32, device=self.device)
         store.upload(indices, cap.lay, cap.dev_plan)
-        ddp = isinstance(self.model, DistributedDataParallel)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             # warm-up (allocator, kernels, autograd buffers) on real data.  No collective
             # here: ranks capture different buckets at different times (their batches
-            # differ), so a capture must be purely local or the ranks' collective
-            # sequences diverge and deadlock.  The warm-up updates are rolled back below.
+            # differ), so warm-up must be purely local.  Capture only RECORDS the bucket
+            # all-reduces into the graph (RCCL graph capture; user-buffer registration is
+            # off, see parallel/distributed.py), nothing is exchanged until replay, where
+            # every rank replays exactly one step graph per step.  The warm-up updates are
+            # rolled back below.
             for _ in range(2):
-                if ddp:
-                    with self.model.no_sync():
-                        self._body_fwd_bwd(store, cap)
-                else:
-                    self._body_fwd_bwd(store, cap)
+                self._body_fwd_bwd(store, cap, sync=False)
                 self.opt.step()
         torch.cuda.current_stream().wait_stream(s)
         pool = torch.cuda.graph_pool_handle()
         cap.g_fwd_bwd = torch.cuda.CUDAGraph()
+        split = self.world > 1 and not self._graph_collectives()
         with torch.cuda.graph(cap.g_fwd_bwd, pool=pool):
-            if ddp:
-                with self.model.no_sync():
-                    cap.loss, cap.tasks = self._body_fwd_bwd(store, cap)
-            else:
-                cap.loss, cap.tasks = self._body_fwd_bwd(store, cap)
+            cap.loss, cap.tasks = self._body_fwd_bwd(store, cap, sync=not split)
+            if not split:
                 self.opt.step()
-        if ddp:
+        if split:  # gloo rehearsal on one GPU: [fwd+bwd] -> eager all-reduce -> [optimizer]
             cap.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(cap.g_opt, pool=pool):
                 self.opt.step()
@@ -322,9 +349,18 @@ class TrainStep:
             tm["replay"] = tm.get("replay", 0.0) + (t2 - t1)
             tm["n"] = tm.get("n", 0) + 1
         if cap.g_opt is not None:
-            self.model.allreduce_now()
+            import torch.distributed as dist
+
+            self.sync.flat.mul_(1.0 / self.world)
+            dist.all_reduce(self.sync.flat)
             cap.g_opt.replay()
         return cap.loss, cap.tasks
+
+    def _graph_collectives(self):
+        """Collectives can live inside the captured graph only on RCCL ("nccl")."""
+        import torch.distributed as dist
+
+        return dist.is_initialized() and dist.get_backend() == "nccl"
 
     def padded_step(self, store, indices):
         """The captured step's exact computation (static padded bucket shapes) run
@@ -335,12 +371,7 @@ class TrainStep:
         cap = _Captured()
         cap.lay = lay
         cap.dev_plan = store.upload(indices, lay)
-        if isinstance(self.model, DistributedDataParallel):  # same sync structure as graph_step
-            with self.model.no_sync():
-                loss, tasks = self._body_fwd_bwd(store, cap)
-            self.model.allreduce_now()
-        else:
-            loss, tasks = self._body_fwd_bwd(store, cap)
+        loss, tasks = self._body_fwd_bwd(store, cap)  # same bucketed sync as graph_step
         self.opt.step()
         return loss, tasks
 

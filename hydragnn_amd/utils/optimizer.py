@@ -43,7 +43,7 @@ def select_zero_redundancy_optimizer(model, optimizer_config):
     params = [p for p in model.parameters() if p.requires_grad]
     name = optimizer_config.get("type", "AdamW")
     lr = optimizer_config["learning_rate"]
-    return ZeroRedundancyOptimizer(params, lambda ps: _make(name, ps, lr))
+    return ZeroRedundancyOptimizer(params, lambda ps: _make(name, ps, lr), elementwise=name != "FusedLAMB")
 
 
 def select_optimizer(model, config):

@@ -96,6 +96,37 @@ def _ddp_body(rank, world):
         torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-6, msg=n)
 
 
+def _bucketed_sync_body(rank, world):
+    """BucketedGradSync (captured-step gradient sync, several buckets launched in index
+    order from backward hooks) == the average of the ranks' local gradients."""
+    import copy
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.train.step import TrainStep, batch_loss
+
+    samples, model = _store_model()
+    ref = copy.deepcopy(model)
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])
+    step = TrainStep(model, lr=0.0, mode="graph", world=world, node_bucket=64, edge_bucket=512,
+                     bucket_cap_mb=0.004)
+    assert len(step.sync.buckets) > 2
+    idx = [4 * rank + k for k in range(4)]
+    step(store, idx)
+    # local gradient of the same padded batch, no sync
+    N, E = store.sizes_of(idx)
+    Np, Ep = step.bucket_of(N, E)
+    batch = store.assemble(store.upload(idx, store.layout(idx, Np=Np, Ep=Ep, Gp=5)),
+                           store.layout(idx, Np=Np, Ep=Ep, Gp=5))
+    loss, _ = batch_loss(ref, ref(batch), batch)
+    loss.backward()
+    local = torch.cat([p.grad.reshape(-1) for p in ref.parameters() if p.requires_grad])
+    allg = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(allg, local)
+    want = sum(allg) / world
+    got = torch.cat([p.grad.reshape(-1) for p in step.module.parameters() if p.requires_grad])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+
+
 def _store_model():
     from hydragnn_amd.data.synthetic import degree_histogram, oc20_like
     from hydragnn_amd.models.create import create_model
@@ -153,6 +184,22 @@ def _zero_body(rank, world):
     st = opt.consolidate_state_dict(to=0)
     if rank == 0:
         assert opt.state_dict() is not None
+    # reduce_grads: per-rank gradients are reduce-scattered by the optimizer itself
+    torch.manual_seed(6)
+    ref, sh = _mlp(), _mlp()
+    opt_ref = torch.optim.AdamW(ref.parameters(), lr=1e-2)
+    opt = ZeroRedundancyOptimizer(list(sh.parameters()), lambda ps: torch.optim.AdamW(ps, lr=1e-2),
+                                  reduce_grads=True)
+    for it in range(3):
+        g = [[torch.randn_like(p) for p in ref.parameters()] for _ in range(world)]
+        for i, p in enumerate(ref.parameters()):
+            p.grad = sum(g[r][i] for r in range(world)) / world
+        for i, p in enumerate(sh.parameters()):
+            p.grad = g[rank][i].clone()
+        opt_ref.step()
+        opt.step()
+    for a, b in zip(sh.parameters(), ref.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
 
 
 def _syncbn_body(rank, world):
@@ -242,6 +289,10 @@ def test_ddp_bucketed_allreduce_matches_full_batch():
 
 def test_trainstep_ranks_stay_in_sync():
     run_ranks("_trainstep_body")
+
+
+def test_bucketed_grad_sync_matches_rank_average():
+    run_ranks("_bucketed_sync_body")
 
 
 def test_zero1_matches_adamw():
