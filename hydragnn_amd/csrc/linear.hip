@@ -227,8 +227,11 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
   const int64_t ld = (int64_t)O * I + O;
   auto part = at::empty({S, ld}, dY.options());
   dim3 grid(tiles, S);
-  const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0;
-  const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0;
+  // float4 path: row stride, width AND base address 16-byte aligned (a column-narrowed
+  // view can have an odd storage offset)
+  auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+  const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
+  const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);
 #define HY_WGRAD(A, B)                                                                                            \
   wgrad_partial_kernel<A, B><<<grid, 256, 0, stream()>>>(dY.data_ptr<float>(), (int)dY.stride(0),               \
                                                          X.data_ptr<float>(), (int)X.stride(0), part.data_ptr<float>(), \

@@ -300,7 +300,8 @@ std::tuple<at::Tensor, at::Tensor> radial_fwd(const at::Tensor& dist_, const at:
     case 5: HY_RAD_FWD(5); break;
     case 6: HY_RAD_FWD(6); break;
     case 7: HY_RAD_FWD(7); break;
-    default: HY_RAD_FWD(8); break;
+    case 8: HY_RAD_FWD(8); break;
+    default: HY_CHECK(false, "radial_fwd: unsupported basis size ", K);
   }
 #undef HY_RAD_FWD
   return {R, Gt};
@@ -312,6 +313,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
     const at::Tensor& freq_, const at::Tensor& Wemb, const at::Tensor& Wlin, double cutoff, int64_t exponent) {
   auto dR = dR_.contiguous(), dG = dG_.contiguous(), dist = dist_.contiguous(), freq = freq_.contiguous();
   const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
+  HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL, "radial_bwd: 1 <= K <= 8, 1 <= L <= 8");
+  check_w(Wemb, L, F, K, "Wemb");
+  check_w(Wlin, L, F, K, "Wlin");
   HY_CHECK(dR.sizes() == R.sizes() && dG.sizes() == R.sizes() && R.is_contiguous(), "radial_bwd: grad shapes");
   const int64_t per = 2 * K + 1;
   const int64_t ld = L * F * per + K;
@@ -334,7 +338,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
       case 5: HY_RAD_BWD(5); break;
       case 6: HY_RAD_BWD(6); break;
       case 7: HY_RAD_BWD(7); break;
-      default: HY_RAD_BWD(8); break;
+      case 8: HY_RAD_BWD(8); break;
+      default: HY_CHECK(false, "radial_bwd: unsupported basis size ", K);
     }
 #undef HY_RAD_BWD
     radial_sum_kernel<<<ceil_div(ld, 64), 64 * kRadSumWaves, 0, stream()>>>(part.data_ptr<float>(), nb, ld, ld,

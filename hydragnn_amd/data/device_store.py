@@ -221,8 +221,71 @@ class DeviceGraphStore:
         return dev_buf
 
     # ------------------------------------------------------------------ device side
+    def _assemble_native(self, dev_buf, lay):
+        """One HIP launch (``csrc/assemble.hip``) for every per-batch tensor."""
+        from .. import _native
+
+        offs, o = [], 0
+        for sz in lay.sizes:
+            offs.append(o)
+            o += sz
+        th = [(ih, t) for ih, t in enumerate(self.head_types or [])]
+        node_t = [ih for ih, t in th if t != "graph" and ih in self.targets_node]
+        graph_t = [ih for ih, t in th if t == "graph" and ih in self.targets_graph]
+        node_src = [self.fields[k] for k in self.node_keys] + [self.targets_node[ih] for ih in node_t]
+        edge_src = [self.fields[k] for k in self.edge_keys]
+        graph_src = [self.fields[k] for k in self.graph_keys] + [self.targets_graph[ih] for ih in graph_t]
+        pos_field = self.node_keys.index("pos") if (lay.padded and "pos" in self.node_keys) else -1
+        outs = _native.ops().store_assemble(dev_buf, lay.Np, lay.Ep, lay.Gp, lay.padded, offs, node_src, edge_src,
+                                            graph_src, pos_field)
+        nn_, ne, ng = len(node_src), len(edge_src), len(graph_src)
+        fields = {}
+        for k, t in zip(self.node_keys, outs[:len(self.node_keys)]):
+            fields[k] = t
+        tn = dict(zip(node_t, outs[len(self.node_keys):nn_]))
+        for k, t in zip(self.edge_keys, outs[nn_:nn_ + ne]):
+            fields[k] = t
+        gout = outs[nn_ + ne:nn_ + ne + ng]
+        for k, t in zip(self.graph_keys, gout[:len(self.graph_keys)]):
+            fields[k] = t
+        tg = dict(zip(graph_t, gout[len(self.graph_keys):]))
+        targets = [tg[ih] if ih in tg else tn[ih] for ih, _ in th if ih in tg or ih in tn]
+        edge_index, batch_l, ptr_l, nmask, gmask = outs[nn_ + ne + ng:]
+        return fields, targets, edge_index, batch_l, ptr_l, nmask, gmask
+
     def assemble(self, dev_buf, lay, host_ids=None):
         """Build a GraphBatch from a packed device plan (device ops only; graph-capturable)."""
+        if dev_buf.is_cuda and self.dataset_name is None:
+            views = []
+            o = 0
+            for sz in lay.sizes:
+                views.append(dev_buf[o:o + sz])
+                o += sz
+            (_, _, src, dst, sperm, rowptr, srowptr, batch, gptr, aseg_id, aseg_ptr, _, scal) = views
+            fields, targets, edge_index, batch_l, ptr_l, nmask, gmask = self._assemble_native(dev_buf, lay)
+            b = GraphBatch(**fields)
+            s = b._store
+            s["edge_index"] = edge_index
+            s["num_nodes"] = lay.Np
+            s["num_graphs"] = lay.Gp
+            s["batch"] = batch_l
+            s["ptr"] = ptr_l
+            s["dst_si"] = SegIndex(dst, rowptr, None, lay.Np)
+            s["src_si"] = SegIndex(src, srowptr, sperm, lay.Np)
+            s["graph_si"] = SegIndex(batch, gptr, None, lay.Gp)
+            s["attn_seg_id"] = aseg_id
+            s["attn_seg_ptr"] = aseg_ptr
+            s["targets"] = targets
+            if lay.padded:
+                s["num_valid"] = scal[0]
+                s["graph_mask"] = gmask
+                s["node_mask"] = nmask
+            return b
+        return self._assemble_torch(dev_buf, lay, host_ids)
+
+    def _assemble_torch(self, dev_buf, lay, host_ids=None):
+        """Plain-torch assembly: the CPU path, multi-branch batches, and the oracle of the
+        native kernel's tests."""
         views = []
         o = 0
         for sz in lay.sizes:

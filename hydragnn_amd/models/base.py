@@ -114,6 +114,7 @@ class Base(nn.Module):
         if initial_bias is not None:
             self._set_bias()
         self.conv_checkpointing = False
+        _rng.assign_salts(self)
 
     # ------------------------------------------------------------------ construction
     def get_conv(self, input_dim, output_dim, edge_dim=None):

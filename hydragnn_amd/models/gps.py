@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.attention import segment_attention
-from ..ops.linear import linear
+from ..ops.linear import ACT_RELU, linear
 from ..ops.norm import norm_add
 from ..ops.rng import dropout as rng_dropout, new_salt
 from .layers import BatchNorm, Linear
@@ -131,7 +131,11 @@ class GPSConv(nn.Module):
         hs.append(norm_add(h, self.norm2, nv, residual=inv, p=self.dropout, salt=self._salts[1], training=tr))
         out = hs[0] if len(hs) == 1 else hs[0] + hs[1]
         lin1, act, _, lin2, _ = self.mlp
-        m = rng_dropout(act(lin1(out)), self.dropout, tr, self._salts[2])
+        if isinstance(act, nn.ReLU):  # bias + ReLU in the GEMM epilogue
+            h = linear(out, lin1.weight, lin1.bias, act=ACT_RELU)
+        else:
+            h = act(lin1(out))
+        m = rng_dropout(h, self.dropout, tr, self._salts[2])
         out = norm_add(lin2(m), self.norm3, nv, residual=out, p=self.dropout, salt=self._salts[3], training=tr)
         return out, equiv
 

@@ -96,6 +96,6 @@ def segment_attention(qkv, heads, seg_id, seg_ptr, scale=None):
     D = F // heads
     scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
     if (qkv.is_cuda and qkv.dtype == torch.float32 and D in (4, 8, 16, 32, 64)
-            and not _pna_mode._state["composite"]):
+            and _pna_mode.fused("attn")):
         return _FlashAttn.apply(qkv, seg_id, seg_ptr, heads, scale)
     return attention_reference(qkv, heads, seg_id, scale)

@@ -1,18 +1,90 @@
-"""Linear layer for tall-skinny (edge / node row) activations.
+"""Linear layers on the MFMA GEMM engine (``csrc/gemm.hip``).
 
-Forward and input-gradient use the BLAS GEMM (rocBLAS/hipBLASLt: a plain
-library GEMM tiled over many rows).  The weight/bias gradient — a reduction
-over all rows into a tiny [out, in] matrix, which library heuristics map onto
-1-4 workgroups — runs on the split-K HIP kernel in ``csrc/linear.hip``.
-Composite mode (double backward) and CPU tensors use ``F.linear``.
+Forward: ``Y = act(sum_p X_p W_p^T + b) (+ residual)`` — one launch, the
+concat-linear blocks ``X_p`` never concatenated, bias / ReLU / residual in the
+epilogue.  Backward: ONE launch producing every ``dX_p``, every ``dW_p`` and
+``db`` (split-K weight gradients reduced inside the launch), with the ReLU
+derivative applied while staging ``dY``.  Compare the library path it
+replaces: GEMM + bias/act elementwise kernels forward, and dgrad GEMM +
+wgrad-partial + partial-sum (+ act-backward) backward — 4-6 launches per layer.
+
+Precision (``set_precision`` / ``Training.precision``):
+* ``"fp32"`` (default; the reference's numerics): v_mfma_f32_16x16x4_f32, exact fp32;
+* ``"bf16"``: v_mfma_f32_16x16x32_bf16 — operands rounded to bf16 as they are
+  staged into LDS, fp32 accumulation, fp32 storage and master weights.
+
+CPU tensors, non-fp32 dtypes and composite mode (double backward for force
+training) use ``F.linear``.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .. import _native
 from . import pna as _mode
 
-MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+_PREC = {"fp32": 0, "bf16": 1}
+_state = {"prec": _PREC.get(os.environ.get("HYDRA_PRECISION", "fp32"), 0)}
+
+ACT_NONE, ACT_RELU = 0, 1
+
+
+def set_precision(name):
+    """Global GEMM compute precision: "fp32" or "bf16"."""
+    _state["prec"] = _PREC[name]
+
+
+def get_precision():
+    return "bf16" if _state["prec"] == 1 else "fp32"
+
+
+class precision:
+    """Context manager: ``with precision("bf16"): ...``."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = _state["prec"]
+        _state["prec"] = _PREC[self.name]
+
+    def __exit__(self, *a):
+        _state["prec"] = self.prev
+
+
+def _row_contig(t):
+    return t if (t.stride(-1) == 1 or t.shape[-1] == 1) else t.contiguous()
+
+
+class _MM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, act, prec, b, residual, *xw):
+        xs, ws = list(xw[0::2]), list(xw[1::2])
+        y = _native.ops().mm_fwd(xs, ws, b, residual, act, prec)
+        ctx.act, ctx.prec = act, prec
+        ctx.has_b, ctx.has_res = b is not None, residual is not None
+        ctx.n = len(xs)
+        ctx.save_for_backward(*xs, *ws, *( [y] if act == ACT_RELU else []))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        n = ctx.n
+        xs, ws = list(t[:n]), list(t[n:2 * n])
+        y = t[2 * n] if ctx.act == ACT_RELU else None
+        need_dx = [int(ctx.needs_input_grad[4 + 2 * j]) for j in range(n)]
+        need_dw = any(ctx.needs_input_grad[5 + 2 * j] for j in range(n))
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        outs = _native.ops().mm_bwd(dy.contiguous() if y is not None else _row_contig(dy), y, xs, ws, need_dx, need_dw, want_b, ctx.prec)
+        dxs, dws, db = outs[:n], outs[n:2 * n], outs[2 * n]
+        grads = []
+        for j in range(n):
+            grads.append(dxs[j] if need_dx[j] else None)
+            grads.append(dws[j] if ctx.needs_input_grad[5 + 2 * j] else None)
+        dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
+        return (None, None, db if want_b else None, dres, *grads)
 
 
 class _TallLinear(torch.autograd.Function):
@@ -32,14 +104,6 @@ class _TallLinear(torch.autograd.Function):
             if not ctx.has_b:
                 db = None
         return dx, dW, db
-
-
-def linear(x, W, b=None):
-    if (x.is_cuda and x.dim() == 2 and x.shape[0] >= MIN_ROWS and x.dtype == torch.float32
-            and W.dtype == torch.float32 and not _mode._state["composite"] and torch.is_grad_enabled()
-            and (W.requires_grad or x.requires_grad)):
-        return _TallLinear.apply(x, W, b)
-    return F.linear(x, W, b)
 
 
 class _TallLinearSum(torch.autograd.Function):
@@ -75,16 +139,74 @@ class _TallLinearSum(torch.autograd.Function):
         return (db, *grads)
 
 
-def linear_sum(pairs, b=None):
-    """sum_k F.linear(x_k, W_k) + b with the split-K weight-gradient kernel."""
-    x0 = pairs[0][0]
-    if (x0.is_cuda and x0.shape[0] >= MIN_ROWS and x0.dtype == torch.float32 and not _mode._state["composite"]
-            and torch.is_grad_enabled()):
+class _EngineSumF32(_TallLinearSum):
+    """fp32 concat-linear: one engine launch forward (instead of one GEMM per input block),
+    library dgrad + split-K wgrad backward."""
+
+    @staticmethod
+    def forward(ctx, b, *xw):
+        xs, ws = xw[0::2], xw[1::2]
+        ctx.save_for_backward(*xs, *ws)
+        ctx.k = len(xs)
+        ctx.has_b = b is not None
+        return _native.ops().mm_fwd([_row_contig(x) for x in xs], [_row_contig(w) for w in ws], b, None, 0, 0)
+
+
+MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+
+
+def _engine_ok(tensors):
+    return _mode.fused("linear") and all(
+        t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 for t in tensors)
+
+
+def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
+    """``act(sum_k x_k @ W_k^T + b) (+ residual)`` for 1-3 (x_k, W_k) pairs.
+
+    bf16 precision: the MFMA engine for forward and backward.  fp32: measured on MI355X
+    (tools/bench_mm.py, profiles/r2_bench_mm.log) the library GEMM is faster for the
+    plain single-input forward and the dgrad of these shapes, and the engine's in-launch
+    split-K reduction loses to a separate reduce launch whenever the grid has more than a
+    few dozen workgroups (agent-scope release fences under load), so fp32 uses: library
+    GEMM forward + dgrad, split-K weight-gradient kernel + reduce, and the engine only for
+    multi-input concat-linear forwards (one launch instead of one per input block)."""
+    assert not (act == ACT_RELU and residual is not None), "residual is added after the activation: relu+residual unsupported"
+    xs = [p[0] for p in pairs]
+    ws = [p[1] for p in pairs]
+    engine = len(pairs) <= 3 and _engine_ok(xs + ws) and xs[0].shape[0] > 0 and \
+        (residual is None or (residual.is_cuda and residual.dtype == torch.float32))
+    if engine and _state["prec"] == 1:
         flat = []
-        for x, w in pairs:
+        for x, w in zip(xs, ws):
+            flat += [_row_contig(x), _row_contig(w)]
+        return _MM.apply(act, _state["prec"], b, None if residual is None else _row_contig(residual), *flat)
+    tall = engine and xs[0].shape[0] >= MIN_ROWS and torch.is_grad_enabled() and \
+        any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
+    if len(pairs) == 1:
+        y = _TallLinear.apply(xs[0], ws[0], b) if tall else F.linear(xs[0], ws[0], b)
+    elif tall:
+        flat = []
+        for x, w in zip(xs, ws):
             flat += [x, w]
-        return _TallLinearSum.apply(b, *flat)
-    y = F.linear(pairs[0][0], pairs[0][1], b)
-    for x, w in pairs[1:]:
-        y = y + F.linear(x, w)
+        y = _EngineSumF32.apply(b, *flat)
+    else:
+        y = F.linear(xs[0], ws[0], b)
+        for x, w in zip(xs[1:], ws[1:]):
+            y = y + F.linear(x, w)
+    if act == ACT_RELU:
+        y = torch.relu(y)
+    if residual is not None:
+        y = y + residual
     return y
+
+
+def linear(x, W, b=None, act=ACT_NONE):
+    if x.dim() != 2:
+        sh = x.shape
+        return linear(x.reshape(-1, sh[-1]), W, b, act).view(*sh[:-1], W.shape[0])
+    return linear_act([(x, W)], b, act)
+
+
+def linear_sum(pairs, b=None):
+    """sum_k F.linear(x_k, W_k) + b in one launch (no concatenation)."""
+    return linear_act(pairs, b)

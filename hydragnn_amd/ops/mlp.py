@@ -64,7 +64,7 @@ def _chain(seqs):
 
 def sequential_chain(x, *seqs):
     """``seqs[-1](...seqs[0](x))`` — fused on the GPU when the chain qualifies."""
-    if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and not _mode._state["composite"] \
+    if x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and _mode.fused("mlp") \
             and 0 < x.shape[0] <= MAX_ROWS:
         layers = _chain(seqs)
         dims = [x.shape[1]] + [m.weight.shape[0] for m, _ in layers] if layers else []

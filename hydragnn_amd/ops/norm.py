@@ -43,7 +43,7 @@ def _as_nv(num_valid, device):
 
 def batch_norm(x, bn, num_valid=None):
     training = bn.training or not bn.track_running_stats
-    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and training and not _mode._state["composite"]
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and training and _mode.fused("norm")
             and bn.momentum is not None):
         if bn.track_running_stats and bn.num_batches_tracked is not None and bn.training:
             bn.num_batches_tracked.add_(1)
@@ -120,7 +120,7 @@ def norm_add(a, bn, num_valid=None, residual=None, p=0.0, relu=False, zero_pad=F
     mod = bn.module if (bn is not None and hasattr(bn, "module")) else bn
     bn_train = mod is not None and (mod.training or not mod.track_running_stats)
     if (mod is not None and bn_train and a.is_cuda and a.dtype == torch.float32 and a.dim() == 2
-            and a.shape[0] <= FUSED_MAX_ROWS and not _mode._state["composite"] and mod.momentum is not None):
+            and a.shape[0] <= FUSED_MAX_ROWS and _mode.fused("norm") and mod.momentum is not None):
         nv = _as_nv(num_valid, a.device)
         track = mod.training and mod.track_running_stats
         rm = mod.running_mean if track else None

@@ -327,7 +327,7 @@ class TensorProductUVU(nn.Module):
     def forward(self, x1, x2, w):
         from . import pna as _mode
 
-        if x1.is_cuda and self.native_ok and x1.dtype == torch.float32 and not _mode._state["composite"]:
+        if x1.is_cuda and self.native_ok and x1.dtype == torch.float32 and _mode.fused("tp"):
             return _TPUVU.apply(x1, x2, w, self._ins, self._cg, self.irreps_out.dim)
         return self.forward_reference(x1, x2, w)
 

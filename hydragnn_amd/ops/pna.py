@@ -20,7 +20,16 @@ import torch
 from .. import _native
 from . import segment as seg
 
-_state = {"composite": False}
+import os
+
+_state = {"composite": False, "off": set(filter(None, os.environ.get("HYDRA_UNFUSED", "").split(",")))}
+
+
+def fused(name):
+    """True when the fused HIP path of op family ``name`` may run: not in composite mode
+    (double backward) and not switched off with ``HYDRA_UNFUSED=name[,name...]`` (bisecting
+    numerics: pna, wprep, linear, mlp, norm, radial, attn, tp, segment)."""
+    return not _state["composite"] and name not in _state["off"]
 
 
 class composite_mode:
@@ -137,7 +146,7 @@ def pna_weight_prep(W, b, encW, encb):
     launch each way on the GPU; torch algebra on CPU / in composite mode."""
     F = W.shape[0]
     d = encW.shape[1] - F
-    if W.is_cuda and not _state["composite"] and W.dtype == torch.float32 and encW.dtype == torch.float32:
+    if W.is_cuda and fused("wprep") and W.dtype == torch.float32 and encW.dtype == torch.float32:
         return _PNAWeightPrep.apply(W, b, encW, encb)
     We = W[:, 2 * F:]
     return torch.cat([W[:, :F], W[:, F:2 * F]], 0), We @ encW[:, d:], We @ encW[:, :d], We @ encb + b
@@ -152,7 +161,7 @@ def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
     F = x.shape[1]
     fused = (
         x.is_cuda
-        and not _state["composite"]
+        and fused("pna")
         and x.dtype == torch.float32
         and AB.dtype == torch.float32
         and (C is None or C.dtype == torch.float32)

@@ -32,7 +32,7 @@ class _Radial(torch.autograd.Function):
 
 
 def fused_ok(dist, basis, convs):
-    if not (dist.is_cuda and dist.dtype == torch.float32 and not _mode._state["composite"]
+    if not (dist.is_cuda and dist.dtype == torch.float32 and _mode.fused("radial")
             and 0 < len(convs) <= MAX_L and basis.freq.numel() <= MAX_K):
         return False
     shape = convs[0].rbf_emb[0].weight.shape  # [F, K]: all layers equal

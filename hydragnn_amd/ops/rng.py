@@ -18,8 +18,18 @@ _salts = itertools.count(1)
 
 
 def new_salt():
-    """Distinct, creation-order-deterministic id for a dropout call site."""
+    """Distinct id for a dropout call site (renumbered per model by ``assign_salts``)."""
     return next(_salts)
+
+
+def assign_salts(model):
+    """Number every dropout call site of ``model`` 1, 2, ... in module order, so the masks
+    of a model depend only on the model (not on how many models were built before)."""
+    k = 0
+    for m in model.modules():
+        if hasattr(m, "_salts"):
+            m._salts = list(range(k + 1, k + 1 + len(m._salts)))
+            k += len(m._salts)
 
 
 def _key(device):
@@ -30,12 +40,19 @@ def _key(device):
 
 
 def counter(device):
+    """Per-device counter seeded from ``torch.initial_seed()``; re-seeded in place when
+    ``torch.manual_seed`` changed the seed since (so a run's dropout masks depend only on
+    its own seed, not on what ran earlier in the process — torch.Generator semantics)."""
     key = _key(device)
-    c = _counters.get(key)
-    if c is None:
-        c = torch.tensor([torch.initial_seed() & 0x7FFFFFFF], dtype=torch.int64, device=device)
-        _counters[key] = c
-    return c
+    seed = torch.initial_seed() & 0x7FFFFFFF
+    ent = _counters.get(key)
+    if ent is None:
+        ent = [torch.tensor([seed], dtype=torch.int64, device=device), seed]
+        _counters[key] = ent
+    elif ent[1] != seed and not (ent[0].is_cuda and torch.cuda.is_current_stream_capturing()):
+        ent[0].fill_(seed)
+        ent[1] = seed
+    return ent[0]
 
 
 def advance(device):

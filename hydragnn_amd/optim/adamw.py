@@ -84,7 +84,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 loss = closure()
         self._init_state()
         gpu = any(p.is_cuda for g in self.param_groups for p in g["params"])
-        if not gpu:
+        from ..ops.pna import fused
+
+        if not gpu or not fused("adamw"):
             self._cpu_step()
             return loss
         capturing = torch.cuda.is_current_stream_capturing()

@@ -250,10 +250,11 @@ class TrainStep:
         if want in self.graphs:
             return want
         cands = [k for k in self.graphs if k[0] >= N + 2 and k[1] >= E]
-        # after precapture (or at the cap) a rare unseen bucket replays the smallest
-        # captured bucket that fits: extra padding costs microseconds, a capture ~50 ms
+        # after precapture (or at the cap) a rare unseen bucket replays the captured bucket
+        # with the least padded work that fits: extra padding costs microseconds, a capture
+        # ~50 ms.  Edge rows cost ~1/avg_degree of a node row (attention, dense maps).
         if cands and (getattr(self, "_frozen", False) or len(self.graphs) >= self.max_graphs):
-            return min(cands)
+            return min(cands, key=lambda k: (k[0] - N) + (k[1] - E) / 8.0)
         return want
 
     def _body_fwd_bwd(self, store, cap, sync=True):

@@ -102,3 +102,32 @@ def test_hash_dropout_graph_replay_changes_mask():
     m2 = y.clone()
     assert not torch.equal(m1, m2)
     assert abs(float((m1 == 0).float().mean()) - 0.5) < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("padded", [False, True])
+def test_native_store_assemble_matches_torch(padded):
+    """csrc/assemble.hip (one launch) == the plain-torch batch assembly, field by field."""
+    import numpy as np
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.data.synthetic import oc20_like
+
+    samples = oc20_like(12, seed=3, radius=6.0, max_neighbours=8, pe_dim=4, min_atoms=5, max_atoms=20)
+    for s in samples:
+        s["y"] = torch.cat([s["energy"].reshape(-1), s["x"][:, 0]])
+        s["y_loc"] = torch.tensor([[0, 1, 1 + s.num_nodes]])
+    store = DeviceGraphStore(samples, "cuda", head_types=["graph", "node"], head_dims=[1, 1])
+    idx = [3, 0, 7, 5, 11]
+    N, E = store.sizes_of(idx)
+    lay = store.layout(idx, Np=N + 37, Ep=E + 100, Gp=len(idx) + 1) if padded else store.layout(idx)
+    dev = store.upload(idx, lay)
+    a = store.assemble(dev, lay)
+    b = store._assemble_torch(dev, lay)
+    for k in list(store.node_keys) + list(store.edge_keys) + list(store.graph_keys) + ["edge_index", "batch", "ptr"]:
+        torch.testing.assert_close(a[k], b[k], msg=k)
+    for ta, tb in zip(a.targets, b.targets):
+        torch.testing.assert_close(ta, tb)
+    if padded:
+        assert torch.equal(a.node_mask, b.node_mask) and torch.equal(a.graph_mask, b.graph_mask)
+    assert np.isfinite(a.pos.cpu().numpy()).all()

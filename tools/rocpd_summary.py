@@ -18,6 +18,7 @@ def main():
                     help="keep only kernels between the last two dispatches whose name contains this (e.g. sleep)")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--sequence", type=int, default=0, help="print the last N dispatches in launch order")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute("select name, start, end, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, lds_size "
@@ -34,6 +35,10 @@ def main():
         marks = [i for i, r in enumerate(rows) if a.between in r[0]]
         assert len(marks) >= 2, f"need two '{a.between}' marker kernels, found {len(marks)}"
         rows = rows[marks[-2] + 1:marks[-1]]
+    if a.sequence:
+        for name, s, e, gx, wx, vg, ag, lds in rows[-a.sequence:]:
+            print(f"{(e - s) / 1e3:8.2f} us  wgs {gx // max(wx, 1):6d}  {name[:120]}")
+        return
     agg = {}
     for name, s, e, gx, wx, vg, ag, lds in rows:
         d = agg.setdefault(name, [0, 0.0, gx // max(wx, 1), vg, ag, lds])
