@@ -61,7 +61,7 @@ def _compile(src, inc, abi, force):
         "-O3",
         "-fPIC",
         "-std=c++17",
-        "-ffp-contract=fast",
+        "-ffp-contract=fast-honor-pragmas",
         f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
         "-DUSE_ROCM",
         "-Wno-unused-result",

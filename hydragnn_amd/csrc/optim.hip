@@ -20,11 +20,17 @@ struct TensorRef {
 
 constexpr int kChunk = 2048;
 
-// state: [0] = step (float, incremented by the LAST block via atomic ticket), [1] = lr
+// state: [0] = step (advanced by step_incr_kernel after the update), [1] = lr,
+// [2] = number of steps skipped by the non-finite guard.
+// guard (optional): the step's loss; a NaN/Inf loss skips the whole update on the device
+// (no host sync, capture-safe) and is counted in state[2] (SURVEY §5.3 step guard).
+__device__ __forceinline__ bool guard_bad(const float* guard) { return guard && !isfinite(*guard); }
+
 __global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict__ refs,
                                                     const int2* __restrict__ blocks, float* __restrict__ state,
                                                     float beta1, float beta2, float eps, float wd, int adamw,
-                                                    float grad_scale) {
+                                                    float grad_scale, const float* __restrict__ guard) {
+  if (guard_bad(guard)) return;
   const int2 bt = blocks[blockIdx.x];
   const TensorRef r = refs[bt.x];
   const float step = state[0] + 1.f;  // this step's count (state[0] is updated by a follow-up kernel)
@@ -50,10 +56,22 @@ __global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict_
   }
 }
 
-__global__ void step_incr_kernel(float* state) { state[0] += 1.f; }
+__global__ void step_incr_kernel(float* state, const float* guard, int has_skip) {
+  if (guard_bad(guard)) {
+    if (has_skip) state[2] += 1.f;
+    return;
+  }
+  state[0] += 1.f;
+}
 
 void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tensor& state, double beta1,
-                double beta2, double eps, double wd, bool adamw, double grad_scale) {
+                double beta2, double eps, double wd, bool adamw, double grad_scale,
+                const c10::optional<at::Tensor>& guard) {
+  const float* gp = nullptr;
+  if (guard.has_value() && guard->defined()) {
+    HY_CHECK(guard->is_cuda() && guard->scalar_type() == at::kFloat && guard->numel() == 1, "guard: fp32 scalar");
+    gp = guard->data_ptr<float>();
+  }
   HY_CHECK_CUDA(refs);
   HY_CHECK(refs.scalar_type() == at::kByte, "refs must be a uint8 blob");
   HY_CHECK_I32(blocks);
@@ -63,8 +81,8 @@ void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tens
   adamw_kernel<<<nblocks, 256, 0, stream()>>>(reinterpret_cast<const TensorRef*>(refs.data_ptr<uint8_t>()),
                                               reinterpret_cast<const int2*>(blocks.data_ptr<int>()),
                                               state.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
-                                              (float)wd, adamw ? 1 : 0, (float)grad_scale);
-  step_incr_kernel<<<1, 1, 0, stream()>>>(state.data_ptr<float>());
+                                              (float)wd, adamw ? 1 : 0, (float)grad_scale, gp);
+  step_incr_kernel<<<1, 1, 0, stream()>>>(state.data_ptr<float>(), gp, state.numel() > 2 ? 1 : 0);
 }
 
 }  // namespace hy
@@ -72,7 +90,7 @@ void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tens
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "adamw_step(Tensor refs, Tensor blocks, Tensor state, float beta1, float beta2, float eps, float wd, "
-      "bool adamw, float grad_scale) -> ()");
+      "bool adamw, float grad_scale, Tensor? guard=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) { m.impl("adamw_step", hy::adamw_step); }

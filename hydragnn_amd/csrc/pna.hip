@@ -54,6 +54,22 @@ __device__ __forceinline__ void st(float* p, const Vec<VEC>& r) {
 
 constexpr float kStdEps = 1e-5f;
 
+// PyG's StdAggregation evaluates var = E[m^2] - E[m]^2 with rounded products (separate
+// torch kernels); these helpers keep the compiler from contracting them into FMAs
+// (the build uses -ffp-contract=fast), see the note in pna_fwd_kernel.
+__device__ __forceinline__ float add_sq_nofma(float acc, float m) {
+#pragma clang fp contract(off)
+  const float sq = m * m;
+  return acc + sq;
+}
+__device__ __forceinline__ float var_nofma(float s, float s2, float d, float& mean) {
+#pragma clang fp contract(off)
+  mean = s / d;
+  const float m2 = s2 / d;
+  const float mm = mean * mean;
+  return m2 - mm;
+}
+
 // AB: [N, ldab] with A at column offset 0 and B at column offset F.
 template <int VEC>
 __global__ void __launch_bounds__(256) pna_fwd_kernel(
@@ -90,17 +106,22 @@ __global__ void __launch_bounds__(256) pna_fwd_kernel(
       for (int i = 0; i < VEC; ++i) {
         const float m = (a.v[i] + b.v[i] + cc.v[i]) * g.v[i];
         s.v[i] += m;
-        s2.v[i] = fmaf(m, m, s2.v[i]);
+        s2.v[i] = add_sq_nofma(s2.v[i], m);  // no FMA: see the variance note below
         if (m < mn.v[i]) { mn.v[i] = m; imn[i] = e; }
         if (m > mx.v[i]) { mx.v[i] = m; imx[i] = e; }
       }
     }
+    // var = E[m^2] - E[m]^2 exactly as PyG's StdAggregation evaluates it (rounded products,
+    // true divisions, NO fused multiply-add).  The formula cancels catastrophically when the
+    // messages of a node are (nearly) equal; with FMA contraction the rounding error of m^2
+    // survives the cancellation (var = fl(m^2) - m^2 != 0 for a single neighbour), crosses
+    // the 1e-5 clamp for |m| >~ 20 and switches std from 0 to >= 3e-3 — a systematic
+    // forward difference that the trajectory bisection (tools/trajectory_bisect.py) traced
+    // as the only source of GPU-vs-CPU training drift.
     Vec<VEC> mean, sd;
-    const float invc = 1.f / d;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      mean.v[i] = s.v[i] * invc;
-      const float var = s2.v[i] * invc - mean.v[i] * mean.v[i];
+      const float var = var_nofma(s.v[i], s2.v[i], d, mean.v[i]);
       float t = sqrtf(fmaxf(var, kStdEps));
       sd.v[i] = (t <= sqrtf(kStdEps)) ? 0.f : t;
       if (cnt == 0) { mn.v[i] = 0.f; mx.v[i] = 0.f; }

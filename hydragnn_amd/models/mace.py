@@ -95,14 +95,26 @@ class RadialEmbeddingBlock(nn.Module):
             self.bessel_fn = ChebychevBasis(r_max, num_bessel)
         else:
             raise ValueError(f"unknown radial_type {radial_type}")
-        if distance_transform not in (None, "None"):
-            raise NotImplementedError("MACE distance transforms (Agnesi/Soft) need covalent-radius tables "
-                                      "(ase) that are not available in this build")
+        from ..ops.covalent import AgnesiTransform, SoftTransform
+
+        if distance_transform in (None, "None"):
+            self.distance_transform = None
+        elif distance_transform == "Agnesi":
+            self.distance_transform = AgnesiTransform()
+        elif distance_transform == "Soft":
+            self.distance_transform = SoftTransform()
+        else:
+            raise ValueError(f"unknown distance_transform {distance_transform}")
         self.cutoff_fn = PolynomialCutoff(r_max, num_polynomial_cutoff)
         self.out_dim = num_bessel
 
-    def forward(self, edge_lengths):
-        return self.bessel_fn(edge_lengths) * self.cutoff_fn(edge_lengths)
+    def forward(self, edge_lengths, z_src=None, z_dst=None):
+        """(reference ``blocks.py:148-162``): the cutoff acts on the raw length, the basis on
+        the (optionally) transformed one."""
+        cutoff = self.cutoff_fn(edge_lengths)
+        if self.distance_transform is not None:
+            edge_lengths = self.distance_transform(edge_lengths, z_src, z_dst)
+        return self.bessel_fn(edge_lengths) * cutoff
 
 
 # ----------------------------------------------------------------------------- blocks
@@ -391,7 +403,11 @@ class MACEStack(Base):
         if self.use_edge_attr:
             ea = torch.cat([data.edge_attr, ea], 1)
         ctx.edge_attributes = ea
-        ctx.edge_features = self.radial_embedding(dist)
+        z = elem + 1  # one-hot index -> atomic number (covalent-radius table index)
+        if self.radial_embedding.distance_transform is not None:
+            ctx.edge_features = self.radial_embedding(dist, z[ctx.src_si.index64], z[ctx.dst_si.index64])
+        else:
+            ctx.edge_features = self.radial_embedding(dist)
         if self.use_global_attn:
             x = self.pos_emb(data.pe)
             if self.input_dim:

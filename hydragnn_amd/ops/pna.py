@@ -159,7 +159,7 @@ def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
     [F,2F) the source (x_j) node features.
     """
     F = x.shape[1]
-    fused = (
+    use_fused = (
         x.is_cuda
         and fused("pna")
         and x.dtype == torch.float32
@@ -168,7 +168,7 @@ def pna_message_aggregate(x, AB, C, G, dst_si, src_si, avg_deg):
         and (G is None or G.dtype == torch.float32)
         and dst_si.perm is None
     )
-    if fused:
+    if use_fused:
         return _PNAFused.apply(x.contiguous(), AB, None if C is None else C.contiguous(),
                                None if G is None else G.contiguous(), dst_si, src_si,
                                float(avg_deg["log"]), float(avg_deg["lin"]))

@@ -24,6 +24,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self._tables = None
         self._dev_state = None
         self._host_lr = None
+        # optional NaN/Inf guard: the step's loss tensor; a non-finite loss skips the update on
+        # the device (captured into the step graph, no host sync) and is counted
+        self.guard = None
+        self._skipped_cpu = 0
 
     def _init_state(self):
         for group in self.param_groups:
@@ -57,7 +61,7 @@ class FusedAdamW(torch.optim.Optimizer):
             rb = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
             bt = torch.tensor(blocks, dtype=torch.int32).view(-1).to(dev)
             step0 = float(self.state[ps[0]]["step"])
-            state = torch.tensor([step0, group["lr"]], dtype=torch.float32, device=dev)
+            state = torch.tensor([step0, group["lr"], 0.0], dtype=torch.float32, device=dev)
             for p in ps:
                 self.state[p]["step"] = state[0]  # shared view: checkpoints see the live count
             tables.append([rb, bt, state, group["lr"], tuple(p.grad.data_ptr() for p in ps), ps])
@@ -100,10 +104,24 @@ class FusedAdamW(torch.optim.Optimizer):
                 t[2][1].fill_(group["lr"])
                 t[3] = group["lr"]
             b1, b2 = group["betas"]
-            _native.ops().adamw_step(t[0], t[1], t[2], b1, b2, group["eps"], group["weight_decay"], self.adamw, 1.0)
+            g = self.guard if (self.guard is not None and self.guard.is_cuda) else None
+            _native.ops().adamw_step(t[0], t[1], t[2], b1, b2, group["eps"], group["weight_decay"], self.adamw, 1.0,
+                                     None if g is None else g.reshape(1).float())
         return loss
 
+    def skipped_steps(self):
+        """Updates skipped by the non-finite guard so far (one device read)."""
+        n = self._skipped_cpu
+        for t in self._tables or []:
+            if t is not None:
+                n += int(t[2][2].item())
+                break
+        return n
+
     def _cpu_step(self):
+        if self.guard is not None and not self.guard.is_cuda and not bool(torch.isfinite(self.guard).all()):
+            self._skipped_cpu += 1
+            return
         for group in self.param_groups:
             b1, b2 = group["betas"]
             lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]

@@ -74,6 +74,13 @@ def _(config: dict, use_deepspeed=False):
         dist.barrier()
     save_config(config, log_name)
     load_existing_model_config(model, nn_cfg["Training"], optimizer=optimizer)
+    trainer_state = {}
+    if nn_cfg["Training"].get("continue"):
+        from .train.train_validate_test import restore_trainer_state
+        from .utils.model import load_trainer_state
+
+        trainer_state = load_trainer_state(nn_cfg["Training"]["startfrom"]) or {}
+        restore_trainer_state(trainer_state, scheduler)
     compute_grad_energy = nn_cfg["Training"].get("compute_grad_energy", False)
     engine = None
     if _device_path_enabled(config):
@@ -97,7 +104,7 @@ def _(config: dict, use_deepspeed=False):
                                  f"params: {sum(p.numel() for p in model.parameters())}")
     train_validate_test(model, optimizer, train_loader, val_loader, test_loader, writer, scheduler, nn_cfg, log_name,
                         verbosity, plot_init_solution, plot_hist_solution, create_plots,
-                        compute_grad_energy=compute_grad_energy, step_engine=engine)
+                        compute_grad_energy=compute_grad_energy, step_engine=engine, trainer_state=trainer_state)
     save_model(model, optimizer, log_name)
     print_timers(verbosity)
     return model

@@ -208,6 +208,7 @@ class TrainStep:
         pred = self.model(batch)
         loss, tasks = batch_loss(self.module, pred, batch)
         self._backward(loss)
+        self._set_guard(loss)
         self.opt.step()
         return loss.detach(), [t.detach() for t in tasks]
 
@@ -263,7 +264,15 @@ class TrainStep:
         pred = self.model(batch)
         loss, tasks = batch_loss(self.module, pred, batch)
         self._backward(loss, sync=sync)
+        self._set_guard(loss)
         return loss.detach(), [t.detach() for t in tasks]
+
+    def _set_guard(self, loss):
+        """NaN/Inf step guard: optimizers that support it skip the update on the device."""
+        if hasattr(self.opt, "guard"):
+            self.opt.guard = loss.detach()
+        elif hasattr(getattr(self.opt, "optim", None), "guard"):  # ZeRO wrapper
+            self.opt.optim.guard = loss.detach()
 
     def _opt_state_tensors(self):
         out = []

@@ -152,6 +152,8 @@ def train(loader, model, opt, verbosity, profiler=None, use_deepspeed=False, com
                 loss.backward()
             tr.stop("backward", **sync)
             tr.start("opt_step", **sync)
+            if hasattr(opt, "guard"):
+                opt.guard = loss.detach()
             opt.step()
             tr.stop("opt_step", **sync)
             ng = data.get("num_graphs_real", data.num_graphs)
@@ -254,6 +256,34 @@ def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compu
     return test_error, tasks_error, true_values, predicted_values
 
 
+def _record_trainer_state(st, epoch, scheduler, earlystopper, checkpoint):
+    st["epoch"] = epoch + 1
+    if scheduler is not None and hasattr(scheduler, "state_dict"):
+        st["scheduler"] = {k: v for k, v in scheduler.state_dict().items() if isinstance(v, (int, float, str, list))}
+    if earlystopper is not None:
+        st["early_stopping"] = earlystopper.state_dict()
+    if checkpoint is not None:
+        st["checkpoint_min"] = float(checkpoint.min_perf_metric)
+    st["torch_rng"] = torch.get_rng_state()
+    if torch.cuda.is_available():
+        st["cuda_rng"] = torch.cuda.get_rng_state_all()
+
+
+def restore_trainer_state(st, scheduler=None):
+    """Scheduler + RNG part of a loaded trainer state (epoch / early stop / checkpoint
+    counters are applied by ``train_validate_test``)."""
+    if st is None:
+        return
+    if scheduler is not None and "scheduler" in st:
+        sd = scheduler.state_dict()
+        sd.update(st["scheduler"])
+        scheduler.load_state_dict(sd)
+    if "torch_rng" in st:
+        torch.set_rng_state(st["torch_rng"])
+    if "cuda_rng" in st and torch.cuda.is_available() and len(st["cuda_rng"]) == torch.cuda.device_count():
+        torch.cuda.set_rng_state_all(st["cuda_rng"])
+
+
 def train_validate_test(model, optimizer, train_loader, val_loader, test_loader, writer, scheduler, config,
                         model_with_config_name, verbosity=0, plot_init_solution=True, plot_hist_solution=False,
                         create_plots=False, use_deepspeed=False, compute_grad_energy=False, step_engine=None,
@@ -291,9 +321,14 @@ def train_validate_test(model, optimizer, train_loader, val_loader, test_loader,
     if trainer_state is not None:
         if earlystopper is not None and "early_stopping" in trainer_state:
             earlystopper.load_state_dict(trainer_state["early_stopping"])
+        if checkpoint is not None and "checkpoint_min" in trainer_state:
+            checkpoint.min_perf_metric = float(trainer_state["checkpoint_min"])
     timer = Timer("train_validate_test")
     timer.start()
     epoch_start = tcfg.get("epoch_start", 0)
+    if trainer_state is not None and "epoch_start" not in tcfg and 0 < int(trainer_state.get("epoch", 0)) < num_epoch:
+        epoch_start = int(trainer_state["epoch"])  # resume where the saved (unfinished) run stopped
+    skipped_seen = 0
     metrics_path = os.path.join("./logs", model_with_config_name, "metrics.jsonl")
     _, rank = get_comm_size_and_rank()
     epoch = epoch_start - 1
@@ -314,6 +349,13 @@ def train_validate_test(model, optimizer, train_loader, val_loader, test_loader,
             if epoch == 0:
                 tr.reset()
         t_train = time.time() - t0
+        sk = getattr(getattr(optimizer, "optim", optimizer), "skipped_steps", None)
+        if sk is not None:
+            n_skipped = sk()
+            if n_skipped > skipped_seen:
+                print_distributed(verbosity, f"WARNING: {n_skipped - skipped_seen} training step(s) with a non-finite "
+                                             f"loss skipped in epoch {epoch} (NaN/Inf guard)")
+                skipped_seen = n_skipped
         if rank == 0:
             from ..utils.metrics import log_json
 
@@ -355,6 +397,11 @@ def train_validate_test(model, optimizer, train_loader, val_loader, test_loader,
             print_distributed(verbosity,
                               "Early stopping executed at epoch = %d due to val_loss not decreasing" % epoch)
             break
+        if trainer_state is not None:
+            _record_trainer_state(trainer_state, epoch, scheduler, earlystopper, checkpoint)
+            from ..utils.model import save_trainer_state
+
+            save_trainer_state(model_with_config_name, trainer_state)
         if check_time and check_remaining(t0):
             print_distributed(verbosity, "No time left. Early stop.")
             break

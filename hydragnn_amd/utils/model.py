@@ -125,6 +125,30 @@ def load_existing_model_config(model, config, path="./logs/", optimizer=None, us
         load_existing_model(model, model_name, path, optimizer, use_deepspeed)
 
 
+def trainer_state_path(name, path="./logs/"):
+    return os.path.join(path, name, name + "_trainer_state.pk")
+
+
+def save_trainer_state(name, state, path="./logs/"):
+    """Sidecar next to the ``.pk`` checkpoint with what the reference does not persist
+    (SURVEY §5.4): next epoch, LR-scheduler state, early-stopping counters, RNG states.
+    Plain tensors/numbers only, so it loads with ``weights_only=True``."""
+    if dist.is_initialized() and dist.get_rank() != 0:
+        return
+    d = os.path.join(path, name)
+    os.makedirs(d, exist_ok=True)
+    tmp = trainer_state_path(name, path) + ".tmp"
+    torch.save(state, tmp)
+    os.replace(tmp, trainer_state_path(name, path))
+
+
+def load_trainer_state(name, path="./logs/"):
+    f = trainer_state_path(name, path)
+    if not os.path.exists(f):
+        return None
+    return torch.load(f, map_location="cpu", weights_only=True)
+
+
 def get_summary_writer(name, path="./logs/"):
     """TensorBoard is not installed: return a JSONL scalar writer with the same add_scalar API."""
     from .metrics import ScalarWriter

@@ -76,11 +76,15 @@ def test_graph_step_matches_eager():
 
 def test_ci_pna_trajectory_cpu_vs_gpu_captured():
     """The CI-sized PNA+lengths model (hidden 8, 2 layers, lr 0.02 — the configuration of the
-    end-to-end accuracy tests): 25 training steps on the CPU twin of the captured step
-    (padded batches, plain-torch ops) and on the MI355X hipGraph path (HIP kernels) from the
-    same init and batches.  The per-step losses agree to fp32 rounding: the GPU path has no
-    systematic difference from the CPU path (e2e threshold misses are initialisation
-    collapses, identical on both; see tests/graph_train_util.py)."""
+    end-to-end accuracy tests): 25 training steps on the CPU reference path and on the
+    MI355X hipGraph path (HIP kernels) from the same init and batches.  The GPU trajectory
+    must stay as close to the CPU fp32 one as the CPU fp64 trajectory does.
+
+    Regression test for the round-1 "GPU converges 2x worse" report: the fused PNA kernel's
+    E[m^2]-E[m]^2 was contracted into an FMA (var = fl(m^2) - m^2 != 0 for one-neighbour
+    nodes), which switched std from 0 to >= 3e-3 with a 1/std gradient amplification; the
+    trajectories then drifted apart by ~4e-4 within 25 steps (tools/trajectory_bisect.py
+    isolated the pna op family; profiles/r2_trajectory_bisect_{before,after}_fix.log)."""
     from hydragnn_amd.optim.adamw import FusedAdamW
 
     samples = oc20_like(96, seed=8, min_atoms=4, max_atoms=12, radius=4.0, max_neighbours=6, pe_dim=1)
@@ -92,29 +96,19 @@ def test_ci_pna_trajectory_cpu_vs_gpu_captured():
     deg = degree_histogram(samples, 6)
     heads = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 2, "dim_sharedlayers": 4,
                                                              "num_headlayers": 2, "dim_headlayers": [10, 10]}}]}
-    m_cpu = create_model("PNA", 1, 8, [1], 1, None, None, 0, ["graph"], heads, "relu", "mse", [1.0], 2, pna_deg=deg,
-                         edge_dim=1, use_gpu=False, init_seed=3)
-    m_gpu = copy.deepcopy(m_cpu).cuda()
-    m_pert = copy.deepcopy(m_cpu)  # control: the CPU run from weights perturbed by ~1e-7 relative
-    with torch.no_grad():
-        gp = torch.Generator().manual_seed(1)
-        for p in m_pert.parameters():
-            p.mul_(1 + 1e-7 * torch.randn(p.shape, generator=gp))
-    s_cpu = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])
-    s_gpu = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
+    base = create_model("PNA", 1, 8, [1], 1, None, None, 0, ["graph"], heads, "relu", "mse", [1.0], 2, pna_deg=deg,
+                        edge_dim=1, use_gpu=False, init_seed=3)
 
-    def run(m, store):
+    def run(dev, dtype=torch.float32):
+        m = copy.deepcopy(base).to(dev, dtype)
+        st = DeviceGraphStore(samples, dev, head_types=["graph"], head_dims=[1], dtype=dtype)
         t = TrainStep(m, mode="graph", optimizer=FusedAdamW(m.parameters(), lr=0.02), node_bucket=128,
                       edge_bucket=1024)
         g = torch.Generator().manual_seed(0)
-        return [float(t(store, torch.randperm(96, generator=g)[:32].tolist())[0]) for _ in range(25)]
+        return [float(t(st, torch.randperm(96, generator=g)[:32].tolist())[0]) for _ in range(25)]
 
-    lc, lp, lg = run(m_cpu, s_cpu), run(m_pert, s_cpu), run(m_gpu, s_gpu)
+    lc, l64, lg = run("cpu"), run("cpu", torch.float64), run("cuda")
     scale = sum(abs(v) for v in lc) / len(lc)
-    for i in range(8):  # early steps: fp32 rounding only
-        assert abs(lg[i] - lc[i]) <= 1e-3 * abs(lc[i]) + 1e-3 * scale, (i, lc[i], lg[i])
-    # later steps drift apart chaotically (lr 0.02 on a hidden-8 model); the GPU/CPU gap is
-    # of the same order as the gap a 1e-7 weight perturbation opens on the CPU alone
     d_gpu = max(abs(a - b) for a, b in zip(lc, lg))
-    d_ctl = max(abs(a - b) for a, b in zip(lc, lp))
-    assert d_gpu <= 10 * d_ctl + 1e-3 * scale, (d_gpu, d_ctl, lc, lp, lg)
+    d_64 = max(abs(a - b) for a, b in zip(lc, l64))
+    assert d_gpu <= 10 * d_64 + 1e-5 * scale, (d_gpu, d_64, lc, lg)

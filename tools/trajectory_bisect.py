@@ -34,6 +34,8 @@ base = create_model(MODEL, 1, 8, [1], 1, None, None, 0, ["graph"], heads, "relu"
 
 
 def run(dev, dtype=torch.float32, mode_="graph", off=()):
+    if "adamw" in off:
+        mode_ = "eager"  # the torch AdamW reads its step counter on the host: not capturable
     mode._state["off"] = set(off)
     m = copy.deepcopy(base).to(dev, dtype)
     st = DeviceGraphStore(samples, dev, head_types=["graph"], head_dims=[1], dtype=dtype)
