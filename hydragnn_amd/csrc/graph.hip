@@ -170,6 +170,253 @@ std::tuple<at::Tensor, at::Tensor> radius_graph(const at::Tensor& pos_, const at
   return {ei, sh};
 }
 
+// ------------------------------------------------------------------ cell-list radius graph
+// O(N) builder for large graphs (10^4-10^6-atom structures in preprocessing,
+// where the per-graph O(n^2) scan above stops scaling).  Per graph a grid of cells of edge
+// >= r (fractional coordinates for periodic cells, so triclinic lattices work; the grid of
+// a periodic axis tiles the cell exactly and wraps); atoms are sorted by cell (stable
+// radix sort on the host side of the op), then one thread per receiver visits only the
+// stencil of cells within r.  Periodic stencil: offsets o in [-s, s] per axis map to the
+// neighbour bin (b+o) mod nb and the image floor((b+o)/nb), so every (atom, image) pair
+// is visited once even for cells thinner than r.  Cap policies as above: "index" keeps
+// the first max_nb sources in (image, index) order of the brute-force enumeration,
+// "nearest" the max_nb closest; uncapped lists are ordered the same way by a final sort.
+struct CellGrid {
+  const float* inv;   // [G, 9] inverse cell (fractional = pos @ inv), periodic graphs
+  const float* cell;  // [G, 9] rows = lattice vectors, periodic graphs
+  const float* lo;    // [G, 3] bbox minimum, non-periodic graphs
+  const int* nb;      // [G, 3] bins per axis
+  const int* st;      // [G, 3] stencil half-width per axis
+  const int* rep;     // [G, 3] brute-force image extents (ordering key), periodic graphs
+  const int64_t* off; // [G+1] first global cell of each graph
+  int periodic;
+  float r;
+};
+
+__device__ __forceinline__ void cell_of(const CellGrid& cg, int g, float x, float y, float z, int (&b)[3],
+                                        int (&w)[3]) {
+  if (cg.periodic) {
+    const float* iv = cg.inv + 9 * g;
+    const float f[3] = {x * iv[0] + y * iv[3] + z * iv[6], x * iv[1] + y * iv[4] + z * iv[7],
+                        x * iv[2] + y * iv[5] + z * iv[8]};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float fl = floorf(f[a]);
+      w[a] = (int)fl;  // lattice translations that wrap the atom into the cell
+      b[a] = min(max((int)((f[a] - fl) * cg.nb[3 * g + a]), 0), cg.nb[3 * g + a] - 1);
+    }
+  } else {
+    const float p[3] = {x, y, z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      w[a] = 0;
+      b[a] = min(max((int)((p[a] - cg.lo[3 * g + a]) / cg.r), 0), cg.nb[3 * g + a] - 1);
+    }
+  }
+}
+
+__global__ void cell_assign_kernel(const float* __restrict__ pos, const int* __restrict__ node_graph, int N,
+                                   CellGrid cg, int64_t* __restrict__ cell_id, int* __restrict__ wrap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int g = node_graph[i];
+  int b[3], w[3];
+  cell_of(cg, g, pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], b, w);
+  const int* nb = cg.nb + 3 * g;
+  cell_id[i] = cg.off[g] + ((int64_t)b[0] * nb[1] + b[1]) * nb[2] + b[2];
+  wrap[3 * i] = w[0];
+  wrap[3 * i + 1] = w[1];
+  wrap[3 * i + 2] = w[2];
+}
+
+template <bool FILL, int POLICY>  // POLICY 0: uncapped, 1: index cap, 2: nearest cap
+__global__ void __launch_bounds__(256) cell_radius_kernel(
+    const float* __restrict__ pos, const int* __restrict__ node_graph, const int* __restrict__ wrap,
+    const int64_t* __restrict__ cell_start, const int64_t* __restrict__ order, int N, float r2, int max_nb, int loop,
+    CellGrid cg, int* __restrict__ counts, const int64_t* __restrict__ rowptr, int64_t* __restrict__ src,
+    int64_t* __restrict__ dst, float* __restrict__ shifts, int64_t* __restrict__ keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int g = node_graph[i];
+  const float xi = pos[3 * i], yi = pos[3 * i + 1], zi = pos[3 * i + 2];
+  int bi[3], wi[3];
+  cell_of(cg, g, xi, yi, zi, bi, wi);
+  const int* nb = cg.nb + 3 * g;
+  const int* stn = cg.st + 3 * g;
+  float c[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int rx = 0, ry = 0, rz = 0;
+  if (cg.periodic) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) c[t] = cg.cell[9 * g + t];
+    rx = cg.rep[3 * g];
+    ry = cg.rep[3 * g + 1];
+    rz = cg.rep[3 * g + 2];
+  }
+  const int64_t base = FILL ? rowptr[i] : 0;
+  constexpr int L = POLICY ? kMaxNearest : 1;
+  uint64_t lk[L];  // ordering key: (d2 bits, j) for nearest, (image, j) for index order
+  int lj[L], la[L], lb[L], lc[L];
+  int nn = 0, cnt = 0;
+  for (int ox = -stn[0]; ox <= stn[0]; ++ox)
+    for (int oy = -stn[1]; oy <= stn[1]; ++oy)
+      for (int oz = -stn[2]; oz <= stn[2]; ++oz) {
+        const int o[3] = {ox, oy, oz};
+        int bn[3], im[3];
+        bool ok = true;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const int t = bi[a] + o[a];
+          if (cg.periodic) {
+            bn[a] = ((t % nb[a]) + nb[a]) % nb[a];
+            im[a] = (t - bn[a]) / nb[a];  // floor division
+          } else {
+            bn[a] = t;
+            im[a] = 0;
+            ok = ok && t >= 0 && t < nb[a];
+          }
+        }
+        if (!ok) continue;
+        const int64_t cidx = cg.off[g] + ((int64_t)bn[0] * nb[1] + bn[1]) * nb[2] + bn[2];
+        for (int64_t k = cell_start[cidx]; k < cell_start[cidx + 1]; ++k) {
+          const int j = (int)order[k];
+          // brute-force image of the source relative to the receiver's raw position
+          const int a = im[0] - wrap[3 * j] + wi[0], b = im[1] - wrap[3 * j + 1] + wi[1],
+                    e = im[2] - wrap[3 * j + 2] + wi[2];
+          if (!loop && j == i && a == 0 && b == 0 && e == 0) continue;
+          const float sx = a * c[0] + b * c[3] + e * c[6];
+          const float sy = a * c[1] + b * c[4] + e * c[7];
+          const float sz = a * c[2] + b * c[5] + e * c[8];
+          const float dx = xi - (pos[3 * j] + sx), dy = yi - (pos[3 * j + 1] + sy), dz = zi - (pos[3 * j + 2] + sz);
+          const float d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 > r2) continue;
+          const int img = ((a + rx) * (2 * ry + 1) + (b + ry)) * (2 * rz + 1) + (e + rz);
+          if constexpr (POLICY == 0) {
+            if constexpr (FILL) {
+              const int64_t q = base + cnt;
+              src[q] = j;
+              dst[q] = i;
+              keys[q] = ((int64_t)i << 40) + ((int64_t)img << 24) + j;  // row-major (dst, image, src)
+              if (shifts) {
+                shifts[3 * q] = -sx;
+                shifts[3 * q + 1] = -sy;
+                shifts[3 * q + 2] = -sz;
+              }
+            }
+            ++cnt;
+          } else {
+            const uint64_t key = ((uint64_t)(POLICY == 2 ? __float_as_uint(d2) : (unsigned)img) << 32) | (unsigned)j;
+            if (nn == max_nb && key >= lk[nn - 1]) continue;
+            int p = nn < max_nb ? nn++ : nn - 1;
+            while (p > 0 && lk[p - 1] > key) {
+              lk[p] = lk[p - 1];
+              lj[p] = lj[p - 1];
+              la[p] = la[p - 1];
+              lb[p] = lb[p - 1];
+              lc[p] = lc[p - 1];
+              --p;
+            }
+            lk[p] = key;
+            lj[p] = j;
+            la[p] = a;
+            lb[p] = b;
+            lc[p] = e;
+          }
+        }
+      }
+  if constexpr (POLICY != 0) {
+    cnt = nn;
+    if constexpr (FILL) {
+      for (int t = 0; t < nn; ++t) {
+        const int64_t q = base + t;
+        src[q] = lj[t];
+        dst[q] = i;
+        if (shifts) {
+          shifts[3 * q] = -(la[t] * c[0] + lb[t] * c[3] + lc[t] * c[6]);
+          shifts[3 * q + 1] = -(la[t] * c[1] + lb[t] * c[4] + lc[t] * c[7]);
+          shifts[3 * q + 2] = -(la[t] * c[2] + lb[t] * c[5] + lc[t] * c[8]);
+        }
+      }
+    }
+  }
+  if constexpr (!FILL) counts[i] = cnt;
+}
+
+// grid: int32 [G, 9] = (nb[3], st[3], rep[3]); geo: f32 [G, 21] = (inv[9], cell[9], lo[3]); off int64 [G+1]
+std::tuple<at::Tensor, at::Tensor> radius_graph_cells(const at::Tensor& pos_, const at::Tensor& node_graph,
+                                                      const at::Tensor& grid, const at::Tensor& geo,
+                                                      const at::Tensor& off, double r, int64_t max_nb, bool loop,
+                                                      bool nearest, bool periodic) {
+  HY_CHECK_CUDA(pos_);
+  auto pos = pos_.to(at::kFloat).contiguous();
+  HY_CHECK(pos.dim() == 2 && pos.size(1) == 3, "pos must be [N, 3]");
+  HY_CHECK_I32(node_graph);
+  const int N = (int)pos.size(0);
+  const int G = (int)off.numel() - 1;
+  HY_CHECK(grid.scalar_type() == at::kInt && grid.is_contiguous() && grid.numel() == 9 * G, "grid must be int32 [G, 9]");
+  HY_CHECK(geo.scalar_type() == at::kFloat && geo.is_contiguous() && geo.numel() == 21 * G, "geo must be f32 [G, 21]");
+  HY_CHECK(off.scalar_type() == at::kLong && off.is_contiguous(), "off must be int64 [G+1]");
+  HY_CHECK(max_nb < 0 || max_nb <= kMaxNearest, "capped cell-list builder supports max_num_neighbors <= ", kMaxNearest);
+  auto i64 = pos.options().dtype(at::kLong);
+  if (N == 0) return {at::empty({2, 0}, i64), at::empty({0, 3}, pos.options())};
+  // per-graph columns (strided views into the two small tables)
+  auto nbT = grid.narrow(1, 0, 3).contiguous(), stT = grid.narrow(1, 3, 3).contiguous(),
+       repT = grid.narrow(1, 6, 3).contiguous();
+  auto invT = geo.narrow(1, 0, 9).contiguous(), cellT = geo.narrow(1, 9, 9).contiguous(),
+       loT = geo.narrow(1, 18, 3).contiguous();
+  CellGrid cg{invT.data_ptr<float>(), cellT.data_ptr<float>(), loT.data_ptr<float>(), nbT.data_ptr<int>(),
+              stT.data_ptr<int>(), repT.data_ptr<int>(), off.data_ptr<int64_t>(), periodic ? 1 : 0, (float)r};
+  auto cell_id = at::empty({N}, i64);
+  auto wrap = at::empty({N, 3}, pos.options().dtype(at::kInt));
+  const int blocks = ceil_div(N, 256);
+  cell_assign_kernel<<<blocks, 256, 0, stream()>>>(pos.data_ptr<float>(), node_graph.data_ptr<int>(), N, cg,
+                                                   cell_id.data_ptr<int64_t>(), wrap.data_ptr<int>());
+  auto sorted = at::sort(cell_id, /*stable=*/true, 0, false);
+  auto order = std::get<1>(sorted).contiguous();
+  const int64_t ncells = off[G].item<int64_t>();  // host sync (grid size known on the host anyway)
+  auto ccount = at::bincount(cell_id, {}, ncells);
+  auto cell_start = at::zeros({ncells + 1}, i64);
+  cell_start.narrow(0, 1, ncells).copy_(at::cumsum(ccount, 0));
+  auto counts = at::empty({N}, pos.options().dtype(at::kInt));
+  const float r2 = (float)(r * r);
+  const int cap = max_nb > 0 ? (int)max_nb : 0;
+  const int policy = cap == 0 ? 0 : (nearest ? 2 : 1);
+  const float* P = pos.data_ptr<float>();
+  const int* NG = node_graph.data_ptr<int>();
+  const int* W = wrap.data_ptr<int>();
+  const int64_t* CS = cell_start.data_ptr<int64_t>();
+  const int64_t* OR = order.data_ptr<int64_t>();
+  const int lp = loop ? 1 : 0;
+#define HY_CELL(FILL, POL, ...)                                                                                 \
+  cell_radius_kernel<FILL, POL><<<blocks, 256, 0, stream()>>>(P, NG, W, CS, OR, N, r2, cap, lp, cg, __VA_ARGS__)
+  if (policy == 0) HY_CELL(false, 0, counts.data_ptr<int>(), nullptr, nullptr, nullptr, nullptr, nullptr);
+  else if (policy == 1) HY_CELL(false, 1, counts.data_ptr<int>(), nullptr, nullptr, nullptr, nullptr, nullptr);
+  else HY_CELL(false, 2, counts.data_ptr<int>(), nullptr, nullptr, nullptr, nullptr, nullptr);
+  auto rowptr = at::zeros({N + 1}, i64);
+  rowptr.narrow(0, 1, N).copy_(at::cumsum(counts, 0));
+  const int64_t E = rowptr[N].item<int64_t>();
+  auto ei = at::empty({2, E}, i64);
+  at::Tensor sh = periodic ? at::empty({E, 3}, pos.options()) : at::empty({0, 3}, pos.options());
+  if (E > 0) {
+    int64_t* s = ei.data_ptr<int64_t>();
+    float* shp = periodic ? sh.data_ptr<float>() : nullptr;
+    const int64_t* RP = rowptr.data_ptr<int64_t>();
+    if (policy == 0) {
+      auto keys = at::empty({E}, i64);
+      HY_CELL(true, 0, nullptr, RP, s, s + E, shp, keys.data_ptr<int64_t>());
+      // stencil order -> (dst, image, src) order, deterministic whatever the cell layout
+      auto perm = std::get<1>(at::sort(keys, /*stable=*/true, 0, false));
+      ei = ei.index_select(1, perm);
+      if (periodic) sh = sh.index_select(0, perm);
+    } else if (policy == 1) {
+      HY_CELL(true, 1, nullptr, RP, s, s + E, shp, nullptr);
+    } else {
+      HY_CELL(true, 2, nullptr, RP, s, s + E, shp, nullptr);
+    }
+  }
+#undef HY_CELL
+  return {ei, sh};
+}
+
 // ------------------------------------------------------------------ triplets
 template <bool FILL>
 __global__ void __launch_bounds__(256) triplet_kernel(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
@@ -225,9 +472,13 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "radius_graph(Tensor pos, Tensor node_graph, Tensor gptr, float r, int max_nb, bool loop, bool nearest, "
       "Tensor? cell, Tensor? reps) -> (Tensor, Tensor)");
   m.def("triplets(Tensor edge_index, Tensor rowptr) -> (Tensor, Tensor)");
+  m.def(
+      "radius_graph_cells(Tensor pos, Tensor node_graph, Tensor grid, Tensor geo, Tensor off, float r, int max_nb, "
+      "bool loop, bool nearest, bool periodic) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radius_graph", hy::radius_graph);
   m.impl("triplets", hy::triplets);
+  m.impl("radius_graph_cells", hy::radius_graph_cells);
 }

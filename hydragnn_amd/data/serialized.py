@@ -94,14 +94,27 @@ class SerializedDataLoader:
     def process(self, dataset):
         import torch.distributed as dist
 
-        for d in dataset:
+        gpu_graphs = None
+        if torch.cuda.is_available() and dataset and os.environ.get("HYDRAGNN_GPU_PREPROCESS", "1") == "1" and \
+                (not self.pbc or all(d.get("pbc") is None or bool(torch.as_tensor(d.pbc).all()) for d in dataset)):
+            if self.rotational_invariance:
+                for d in dataset:
+                    d.pos = T.normalize_rotation(d.pos).to(torch.float32)
+            gpu_graphs = T.build_radius_graphs_gpu(dataset, self.radius, self.max_neighbours, pbc=self.pbc)
+        for gi, d in enumerate(dataset):
+            if gpu_graphs is not None:
+                d.edge_index, sh = gpu_graphs[gi]
+                if sh is not None:
+                    d.edge_shifts = sh
+                d.edge_attr = T.distance(d.pos, d.edge_index, shifts=sh, norm=False)
+                continue
             if self.rotational_invariance:
                 d.pos = T.normalize_rotation(d.pos).to(torch.float32)
             if self.pbc:
                 cell = d.get("cell")
                 assert cell is not None, "periodic_boundary_conditions requires data.cell"
-                ei, sh = T.radius_graph_pbc(d.pos, cell, d.get("pbc", [True, True, True]), self.radius,
-                                            self.max_neighbours)
+                ei, sh, _ = T.radius_graph_pbc_robust(d.pos, cell, d.get("pbc", [True, True, True]),
+                                                      self.radius, self.max_neighbours)
                 d.edge_index, d.edge_shifts = ei, sh
                 d.edge_attr = T.distance(d.pos, ei, shifts=sh, norm=False)
             else:

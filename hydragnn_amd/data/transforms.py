@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 
-def radius_graph(pos, r, batch=None, max_num_neighbors=32, loop=False, cap_policy="nearest"):
+def radius_graph(pos, r, batch=None, max_num_neighbors=32, loop=False, cap_policy="index"):
     """Edges (j -> i) with ||pos_i - pos_j|| <= r within the same graph.
 
     ``cap_policy``: "nearest" keeps the closest ``max_num_neighbors`` sources per
@@ -111,6 +111,84 @@ def radius_graph_pbc(pos, cell, pbc, r, max_num_neighbors=32, loop=False):
     ei = torch.stack([src[keep], dst[keep]], 0)
     # shift convention: vec = pos[dst] - pos[src] + shift  -> shift = -(image shift of the source)
     return ei, sh[keep].to(torch.float32) * -1.0
+
+
+def missing_receivers(edge_index, num_nodes):
+    """Nodes that receive no edge."""
+    dst = torch.as_tensor(edge_index)[1]
+    has = torch.zeros(int(num_nodes), dtype=torch.bool)
+    if dst.numel():
+        has[dst] = True
+    return (~has).nonzero().view(-1)
+
+
+def ensure_connected(edge_index, edge_shifts, num_nodes, seed=None):
+    """Give every receiver-less node one artificial incoming edge from a random other node
+    with zero cell shift (reference ``RadiusGraphPBC._ensure_connected``,
+    ``graph_samples_checks_and_updates.py:284-307``).  Returns (edge_index, edge_shifts,
+    number of edges added)."""
+    miss = missing_receivers(edge_index, num_nodes)
+    if miss.numel() == 0:
+        return edge_index, edge_shifts, 0
+    print(f"WARNING: {miss.numel()} node(s) receive no edge; adding artificial edges", flush=True)
+    rng = np.random.default_rng(seed)
+    src = []
+    for m in miss.tolist():
+        if num_nodes > 1:
+            s = int(rng.integers(num_nodes - 1))
+            src.append(s + (s >= m))  # uniform over the other nodes
+        else:
+            src.append(0)
+    add = torch.stack([torch.tensor(src, dtype=edge_index.dtype), miss.to(edge_index.dtype)], 0)
+    ei = torch.cat([edge_index, add], 1)
+    sh = None if edge_shifts is None else torch.cat([edge_shifts, edge_shifts.new_zeros(miss.numel(), 3)], 0)
+    return ei, sh, int(miss.numel())
+
+
+def radius_graph_pbc_robust(pos, cell, pbc, r, max_num_neighbors=32, loop=False, multiplier=1.25, max_attempts=3,
+                            seed=None):
+    """``radius_graph_pbc`` with the reference's failure handling (``RadiusGraphPBC.__call__``,
+    ``graph_samples_checks_and_updates.py:161-222``): while some node receives no edge the
+    cutoff grows by ``multiplier`` (at most ``max_attempts`` builds), then any node still
+    without a receiver edge gets an artificial one (``ensure_connected``).  Returns
+    (edge_index, edge_shifts, cutoff used)."""
+    n = int(torch.as_tensor(pos).shape[0])
+    cutoff = float(r)
+    for attempt in range(max_attempts):
+        ei, sh = radius_graph_pbc(pos, cell, pbc, cutoff, max_num_neighbors, loop)
+        if missing_receivers(ei, n).numel() == 0:
+            return ei, sh, cutoff
+        if attempt < max_attempts - 1:
+            print(f"Not all nodes receive an edge, expanding radius from {cutoff} -> {cutoff * multiplier}",
+                  flush=True)
+            cutoff *= multiplier
+    ei, sh, _ = ensure_connected(ei, sh, n, seed)
+    return ei, sh, cutoff
+
+
+def local_cartesian(pos, edge_index, shifts=None, norm=True, interval=(0.0, 1.0), cat=False, edge_attr=None):
+    """PyG ``LocalCartesian`` / reference ``PBCLocalCartesian`` (``:379-413``): relative
+    Cartesian offset pos[src] - pos[dst] (- shift), optionally scaled per receiver by its
+    largest |component| into ``interval``."""
+    row, col = edge_index[0], edge_index[1]
+    cart = pos[row] - pos[col]
+    if shifts is not None:
+        cart = cart - shifts
+    if norm and cart.numel():
+        n = pos.shape[0]
+        mx = torch.zeros(n, dtype=cart.dtype).scatter_reduce(0, col, cart.abs().max(dim=-1).values, "amax",
+                                                              include_self=True)
+        length = interval[1] - interval[0]
+        center = (interval[0] + interval[1]) / 2
+        cart = length * cart / (2 * mx[col].clamp_min(1e-9).view(-1, 1)) + center
+    if cat and edge_attr is not None:
+        return torch.cat([edge_attr.view(edge_attr.shape[0], -1), cart.to(edge_attr.dtype)], dim=-1)
+    return cart
+
+
+def pbc_distance(pos, edge_index, shifts, norm=True, max_value=None, cat=False, edge_attr=None):
+    """Reference ``PBCDistance`` (``:346-376``): ``distance`` with the periodic shift added."""
+    return distance(pos, edge_index, shifts=shifts, norm=norm, max_value=max_value, cat=cat, edge_attr=edge_attr)
 
 
 def distance(pos, edge_index, shifts=None, norm=True, max_value=None, cat=False, edge_attr=None):
@@ -214,3 +292,53 @@ def laplacian_pe_batch(samples, k, seed=None, device=None, max_sweeps=30, tol=1e
                                        signs.to(dev), int(max_sweeps), float(tol))
     pe = pe.cpu()
     return [pe[int(b.ptr[g]):int(b.ptr[g + 1])] for g in range(len(samples))]
+
+
+def build_radius_graphs_gpu(samples, r, max_num_neighbors, pbc=False, device="cuda"):
+    """Radius graphs of a whole dataset in ONE batched launch of the cell-list HIP builder
+    (``ops.radius.radius_graph_cells``) instead of one host ``cdist`` per sample.  Periodic
+    samples use the "nearest" cap (RadiusGraphPBC) and then the reference's retry /
+    connectivity repair per sample (``radius_graph_pbc_robust``); non-periodic samples the
+    torch_cluster "index" cap.  Returns a list of (edge_index, edge_shifts or None) on the CPU."""
+    from ..ops.radius import radius_graph_cells
+
+    dev = torch.device(device)
+    n = [int(s.num_nodes) for s in samples]
+    pos = torch.cat([s.pos.to(torch.float32) for s in samples]).to(dev)
+    batch = torch.repeat_interleave(torch.arange(len(samples)), torch.tensor(n)).to(dev)
+    cell = None
+    if pbc:
+        cell = torch.stack([torch.as_tensor(s.cell, dtype=torch.float32).view(3, 3) for s in samples]).to(dev)
+    cap = None if max_num_neighbors is None else int(max_num_neighbors)
+    policy = "nearest" if pbc else "index"
+    native_cap = cap if (cap is not None and cap <= 64) else None
+    ei, sh = radius_graph_cells(pos, batch, r, native_cap, cap_policy=policy, cell=cell)
+    if cap is not None and native_cap is None:  # wide caps: uncapped build, cap per receiver here
+        if policy == "nearest":
+            vec = pos[ei[1]] - pos[ei[0]] + (sh if sh is not None else 0.0)
+            d = vec.norm(dim=1)
+            order = torch.argsort(ei[1].double() * (float(d.max()) + 1.0 if d.numel() else 1.0) + d.double(),
+                                  stable=True)
+            ei = ei[:, order]
+            sh = sh[order] if sh is not None else None
+        dst = ei[1]
+        first = torch.ones_like(dst, dtype=torch.bool)
+        first[1:] = dst[1:] != dst[:-1]
+        idx = torch.arange(dst.numel(), device=dev)
+        start = torch.cummax(torch.where(first, idx, torch.zeros_like(idx)), 0).values
+        keep = (idx - start) < cap
+        ei = ei[:, keep]
+        sh = sh[keep] if sh is not None else None
+    ei, sh = ei.cpu(), (sh.cpu() if sh is not None else None)
+    off = np.concatenate([[0], np.cumsum(n)])
+    bounds = torch.searchsorted(ei[1].contiguous(), torch.as_tensor(off, dtype=torch.long))
+    out = []
+    for g, s in enumerate(samples):
+        a, b = int(bounds[g]), int(bounds[g + 1])
+        e = ei[:, a:b] - int(off[g])
+        shg = sh[a:b] if sh is not None else None
+        if pbc and missing_receivers(e, n[g]).numel():
+            e, shg, _ = radius_graph_pbc_robust(s.pos, s.cell, s.get("pbc", [True, True, True]), r,
+                                                cap if cap is not None else 1 << 30)
+        out.append((e, shg))
+    return out

@@ -14,6 +14,7 @@ from torch import nn
 
 from ..ops import segment as seg
 from ..ops.linear import linear
+from .layers import Linear
 from .base import Base
 
 
@@ -23,8 +24,8 @@ class CGConv(nn.Module):
         assert aggr == "add" and not batch_norm, "HydraGNN uses CGConv(aggr='add', batch_norm=False)"
         self.channels = channels
         self.dim = dim or 0
-        self.lin_f = nn.Linear(2 * channels + self.dim, channels, bias=bias)
-        self.lin_s = nn.Linear(2 * channels + self.dim, channels, bias=bias)
+        self.lin_f = Linear(2 * channels + self.dim, channels, bias=bias)
+        self.lin_s = Linear(2 * channels + self.dim, channels, bias=bias)
 
     def forward(self, inv, equiv, ctx):
         x = inv

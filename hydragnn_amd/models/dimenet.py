@@ -22,6 +22,7 @@ from torch import nn
 
 from ..ops import segment as seg
 from ..ops.geometry import BesselBasis, Envelope, edge_vectors_and_lengths
+from .layers import Linear
 from .base import Base
 
 
@@ -131,8 +132,8 @@ class ResidualLayer(nn.Module):
     def __init__(self, hidden, act):
         super().__init__()
         self.act = act
-        self.lin1 = nn.Linear(hidden, hidden)
-        self.lin2 = nn.Linear(hidden, hidden)
+        self.lin1 = Linear(hidden, hidden)
+        self.lin2 = Linear(hidden, hidden)
         for l in (self.lin1, self.lin2):
             _glorot_orthogonal(l.weight)
             l.bias.data.fill_(0)
@@ -145,12 +146,12 @@ class HydraEmbeddingBlock(nn.Module):
     def __init__(self, num_radial, hidden_channels, act, edge_dim=None):
         super().__init__()
         self.act = act
-        self.lin_rbf = nn.Linear(num_radial, hidden_channels)
+        self.lin_rbf = Linear(num_radial, hidden_channels)
         if edge_dim is not None:
-            self.edge_lin = nn.Linear(edge_dim, hidden_channels)
-            self.lin = nn.Linear(4 * hidden_channels, hidden_channels)
+            self.edge_lin = Linear(edge_dim, hidden_channels)
+            self.lin = Linear(4 * hidden_channels, hidden_channels)
         else:
-            self.lin = nn.Linear(3 * hidden_channels, hidden_channels)
+            self.lin = Linear(3 * hidden_channels, hidden_channels)
 
     def forward(self, x, rbf, dst_si, src_si, edge_attr=None):
         H = x.shape[1]
@@ -168,16 +169,16 @@ class InteractionPPBlock(nn.Module):
                  num_after_skip, act):
         super().__init__()
         self.act = act
-        self.lin_rbf1 = nn.Linear(num_radial, basis_emb_size, bias=False)
-        self.lin_rbf2 = nn.Linear(basis_emb_size, hidden_channels, bias=False)
-        self.lin_sbf1 = nn.Linear(num_spherical * num_radial, basis_emb_size, bias=False)
-        self.lin_sbf2 = nn.Linear(basis_emb_size, int_emb_size, bias=False)
-        self.lin_kj = nn.Linear(hidden_channels, hidden_channels)
-        self.lin_ji = nn.Linear(hidden_channels, hidden_channels)
-        self.lin_down = nn.Linear(hidden_channels, int_emb_size, bias=False)
-        self.lin_up = nn.Linear(int_emb_size, hidden_channels, bias=False)
+        self.lin_rbf1 = Linear(num_radial, basis_emb_size, bias=False)
+        self.lin_rbf2 = Linear(basis_emb_size, hidden_channels, bias=False)
+        self.lin_sbf1 = Linear(num_spherical * num_radial, basis_emb_size, bias=False)
+        self.lin_sbf2 = Linear(basis_emb_size, int_emb_size, bias=False)
+        self.lin_kj = Linear(hidden_channels, hidden_channels)
+        self.lin_ji = Linear(hidden_channels, hidden_channels)
+        self.lin_down = Linear(hidden_channels, int_emb_size, bias=False)
+        self.lin_up = Linear(int_emb_size, hidden_channels, bias=False)
         self.layers_before_skip = nn.ModuleList([ResidualLayer(hidden_channels, act) for _ in range(num_before_skip)])
-        self.lin = nn.Linear(hidden_channels, hidden_channels)
+        self.lin = Linear(hidden_channels, hidden_channels)
         self.layers_after_skip = nn.ModuleList([ResidualLayer(hidden_channels, act) for _ in range(num_after_skip)])
         for l in (self.lin_rbf1, self.lin_rbf2, self.lin_sbf1, self.lin_sbf2, self.lin_kj, self.lin_ji,
                   self.lin_down, self.lin_up, self.lin):
@@ -204,10 +205,10 @@ class OutputPPBlock(nn.Module):
     def __init__(self, num_radial, hidden_channels, out_emb_channels, out_channels, num_layers, act):
         super().__init__()
         self.act = act
-        self.lin_rbf = nn.Linear(num_radial, hidden_channels, bias=False)
-        self.lin_up = nn.Linear(hidden_channels, out_emb_channels, bias=False)
-        self.lins = nn.ModuleList([nn.Linear(out_emb_channels, out_emb_channels) for _ in range(num_layers)])
-        self.lin = nn.Linear(out_emb_channels, out_channels, bias=False)
+        self.lin_rbf = Linear(num_radial, hidden_channels, bias=False)
+        self.lin_up = Linear(hidden_channels, out_emb_channels, bias=False)
+        self.lins = nn.ModuleList([Linear(out_emb_channels, out_emb_channels) for _ in range(num_layers)])
+        self.lin = Linear(out_emb_channels, out_channels, bias=False)
         _glorot_orthogonal(self.lin_rbf.weight)
         _glorot_orthogonal(self.lin_up.weight)
         for l in self.lins:
@@ -268,7 +269,7 @@ class DIMEStack(Base):
         hidden = output_dim if input_dim == 1 else input_dim
         assert hidden > 1, "DimeNet requires more than one hidden dimension between input_dim and output_dim."
         act = nn.SiLU()
-        lin = nn.Linear(input_dim, hidden)
+        lin = Linear(input_dim, hidden)
         emb = HydraEmbeddingBlock(self.num_radial, hidden, act, edge_dim=edge_dim)
         inter = InteractionPPBlock(hidden, self.int_emb_size, self.basis_emb_size, self.num_spherical,
                                    self.num_radial, self.num_before_skip, self.num_after_skip, act)

@@ -22,6 +22,7 @@ from torch import nn
 from ..ops import segment as seg
 from ..ops.geometry import edge_vectors_and_lengths
 from ..ops.linear import linear
+from .layers import Linear
 from .base import Base
 
 
@@ -49,21 +50,21 @@ class E_GCL(nn.Module):
         self.equivariant = equivariant
         self.edge_attr_dim = edge_attr_dim or 0
         self.edge_mlp = nn.Sequential(
-            nn.Linear(2 * input_channels + 1 + self.edge_attr_dim, hidden_channels), act_fn,
-            nn.Linear(hidden_channels, hidden_channels), act_fn)
+            Linear(2 * input_channels + 1 + self.edge_attr_dim, hidden_channels), act_fn,
+            Linear(hidden_channels, hidden_channels), act_fn)
         self.node_mlp = nn.Sequential(
-            nn.Linear(hidden_channels + input_channels + nodes_attr_dim, hidden_channels), act_fn,
-            nn.Linear(hidden_channels, output_channels))
+            Linear(hidden_channels + input_channels + nodes_attr_dim, hidden_channels), act_fn,
+            Linear(hidden_channels, output_channels))
         self.clamp = clamp
         if equivariant:
-            layer = nn.Linear(hidden_channels, 1, bias=False)
+            layer = Linear(hidden_channels, 1, bias=False)
             nn.init.xavier_uniform_(layer.weight, gain=0.001)
-            mods = [nn.Linear(hidden_channels, hidden_channels), act_fn, layer]
+            mods = [Linear(hidden_channels, hidden_channels), act_fn, layer]
             if tanh:
                 mods.append(nn.Tanh())
             self.coord_mlp = nn.Sequential(*mods)
         if attention:
-            self.att_mlp = nn.Sequential(nn.Linear(hidden_channels, 1), nn.Sigmoid())
+            self.att_mlp = nn.Sequential(Linear(hidden_channels, 1), nn.Sigmoid())
         self.act_fn = act_fn
 
     def edge_model(self, x, radial, edge_attr, dst_si, src_si):

@@ -24,7 +24,7 @@ from ..ops import rng as _rng
 from ..ops import segment as seg
 from ..ops.linear import linear
 from .base import Base
-from .layers import BatchNorm
+from .layers import BatchNorm, Linear
 
 
 class GATv2Conv(nn.Module):
@@ -38,10 +38,10 @@ class GATv2Conv(nn.Module):
         self.add_self_loops = add_self_loops
         self.edge_dim = edge_dim
         H, C = heads, out_channels
-        self.lin_l = nn.Linear(in_channels, H * C, bias=bias)
-        self.lin_r = nn.Linear(in_channels, H * C, bias=bias)
+        self.lin_l = Linear(in_channels, H * C, bias=bias)
+        self.lin_r = Linear(in_channels, H * C, bias=bias)
         self.att = nn.Parameter(torch.empty(1, H, C))
-        self.lin_edge = nn.Linear(edge_dim, H * C, bias=False) if edge_dim is not None else None
+        self.lin_edge = Linear(edge_dim, H * C, bias=False) if edge_dim is not None else None
         self.bias = nn.Parameter(torch.empty(H * C if concat else C)) if bias else None
         self._salt = _rng.new_salt()
         self.reset_parameters()
@@ -175,7 +175,7 @@ class GATStack(Base):
                         dropout=self.dropout, add_self_loops=True, edge_dim=edge_dim, concat=concat)
         # GPS layers project the concatenated heads back to hidden_dim (GATStack.py:187-190);
         # node conv heads keep their head-concatenated width for the following BatchNorm
-        out_lin = nn.Linear(self.hidden_dim * self.heads, self.hidden_dim) \
+        out_lin = Linear(self.hidden_dim * self.heads, self.hidden_dim) \
             if (self.use_global_attn and concat and not head) else nn.Identity()
         return _GATBlock(gat, out_lin)
 

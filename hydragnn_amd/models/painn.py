@@ -31,6 +31,7 @@ from torch import nn
 from ..ops import segment as seg
 from ..ops.geometry import edge_vectors_and_lengths
 from ..ops.pna import degree_scalers, pna_avg_deg
+from .layers import Linear
 from .base import Base
 
 
@@ -61,10 +62,10 @@ class PainnMessage(nn.Module):
         super().__init__()
         self.node_size, self.num_radial, self.cutoff, self.edge_dim = node_size, num_radial, cutoff, edge_dim
         F = node_size
-        self.scalar_message_mlp = nn.Sequential(nn.Linear(F, F), nn.SiLU(), nn.Linear(F, 3 * F))
-        self.filter_layer = nn.Linear(num_radial, 3 * F)
+        self.scalar_message_mlp = nn.Sequential(Linear(F, F), nn.SiLU(), Linear(F, 3 * F))
+        self.filter_layer = Linear(num_radial, 3 * F)
         if edge_dim is not None:
-            self.edge_filter = nn.Sequential(nn.Linear(edge_dim, F), nn.SiLU(), nn.Linear(F, 3 * F))
+            self.edge_filter = nn.Sequential(Linear(edge_dim, F), nn.SiLU(), Linear(F, 3 * F))
 
     def forward(self, s, v, ctx):
         F = self.node_size
@@ -86,11 +87,11 @@ class PainnUpdate(nn.Module):
         self._u = u_name
         # U, V act on the vector state: bias-free (as in PaiNN) so the update stays equivariant
         # (the reference's biased Linears shift every Cartesian component alike)
-        setattr(self, u_name, nn.Linear(node_size, node_size, bias=False))
-        self.update_V = nn.Linear(node_size, node_size, bias=False)
+        setattr(self, u_name, Linear(node_size, node_size, bias=False))
+        self.update_V = Linear(node_size, node_size, bias=False)
         self.last_layer = last_layer
         out = 2 * node_size if last_layer else 3 * node_size
-        self.update_mlp = nn.Sequential(nn.Linear(2 * node_size, node_size), nn.SiLU(), nn.Linear(node_size, out))
+        self.update_mlp = nn.Sequential(Linear(2 * node_size, node_size), nn.SiLU(), Linear(node_size, out))
 
     def forward(self, s, v):
         F = s.shape[-1]
@@ -141,10 +142,10 @@ class _EqStackBase(Base):
         return {"last_layer": False, **super()._conv_head_kwargs()}
 
     def _adapters(self, input_dim, output_dim, last_layer):
-        node_embed_out = nn.Sequential(nn.Linear(input_dim, output_dim), nn.Tanh(), nn.Linear(output_dim, output_dim))
+        node_embed_out = nn.Sequential(Linear(input_dim, output_dim), nn.Tanh(), Linear(output_dim, output_dim))
         # bias-free on purpose: the reference's Linear(input_dim, output_dim) adds the same bias
         # to all three Cartesian components of v, which breaks rotation equivariance
-        vec_embed_out = nn.Linear(input_dim, output_dim, bias=False) if not last_layer else None
+        vec_embed_out = Linear(input_dim, output_dim, bias=False) if not last_layer else None
         return node_embed_out, vec_embed_out
 
     def _geometry(self, data, ctx):
@@ -193,15 +194,15 @@ class PNAEqMessage(nn.Module):
         self.aggregators, self.scalers = tuple(aggregators), tuple(scalers)
         self.register_buffer("deg", torch.as_tensor(deg, dtype=torch.float32))
         self.avg_deg = pna_avg_deg(self.deg)
-        self.pre_nns = nn.ModuleList([nn.Sequential(nn.Linear((4 if edge_dim else 3) * F, F))])
+        self.pre_nns = nn.ModuleList([nn.Sequential(Linear((4 if edge_dim else 3) * F, F))])
         self.post_nns = nn.ModuleList([nn.Sequential(
-            nn.Linear((len(aggregators) * len(scalers) + 1) * F, F))])
-        self.rbf_emb = nn.Sequential(nn.Linear(num_radial, F), nn.Tanh())
+            Linear((len(aggregators) * len(scalers) + 1) * F, F))])
+        self.rbf_emb = nn.Sequential(Linear(num_radial, F), nn.Tanh())
         if edge_dim is not None:
-            self.edge_encoder = nn.Linear(edge_dim, F)
-        self.rbf_lin = nn.Linear(num_radial, 3 * F, bias=False)
-        self.scalar_message_mlp = nn.Sequential(nn.Linear(F, F), nn.Tanh(), nn.Linear(F, F), nn.SiLU(),
-                                                nn.Linear(F, 3 * F))
+            self.edge_encoder = Linear(edge_dim, F)
+        self.rbf_lin = Linear(num_radial, 3 * F, bias=False)
+        self.scalar_message_mlp = nn.Sequential(Linear(F, F), nn.Tanh(), Linear(F, F), nn.SiLU(),
+                                                Linear(F, 3 * F))
 
     def _aggregate(self, m, si):
         aggs = []

@@ -21,6 +21,7 @@ from torch import nn
 from ..ops import segment as seg
 from ..ops.geometry import GaussianSmearing, edge_vectors_and_lengths
 from ..ops.radius import interaction_graph
+from .layers import Linear
 from .base import Base
 
 
@@ -37,15 +38,15 @@ class CFConv(nn.Module):
     def __init__(self, in_channels, out_channels, num_filters, nn_, cutoff, equivariant):
         super().__init__()
         self.in_channels, self.out_channels = in_channels, out_channels
-        self.lin1 = nn.Linear(in_channels, num_filters, bias=False)
-        self.lin2 = nn.Linear(num_filters, out_channels)
+        self.lin1 = Linear(in_channels, num_filters, bias=False)
+        self.lin2 = Linear(num_filters, out_channels)
         self.nn = nn_
         self.cutoff = cutoff
         self.equivariant = equivariant
         if equivariant:
-            layer = nn.Linear(num_filters, 1, bias=False)
+            layer = Linear(num_filters, 1, bias=False)
             nn.init.xavier_uniform_(layer.weight, gain=0.001)
-            self.coord_mlp = nn.Sequential(nn.Linear(num_filters, num_filters), nn.ReLU(), layer)
+            self.coord_mlp = nn.Sequential(Linear(num_filters, num_filters), nn.ReLU(), layer)
         nn.init.xavier_uniform_(self.lin1.weight)
         nn.init.xavier_uniform_(self.lin2.weight)
         self.lin2.bias.data.fill_(0)
@@ -98,8 +99,8 @@ class SCFStack(Base):
 
     def get_conv(self, input_dim, output_dim, last_layer=False, edge_dim=None):
         mlp_in = self.num_gaussians + edge_dim if edge_dim else self.num_gaussians
-        mlp = nn.Sequential(nn.Linear(mlp_in, self.num_filters), ShiftedSoftplus(),
-                            nn.Linear(self.num_filters, self.num_filters))
+        mlp = nn.Sequential(Linear(mlp_in, self.num_filters), ShiftedSoftplus(),
+                            Linear(self.num_filters, self.num_filters))
         return CFConv(input_dim, output_dim, self.num_filters, mlp, self.radius,
                       equivariant=self.equivariance and not last_layer)
 

@@ -92,3 +92,50 @@ def csr_views(edge_index, n):
 def interaction_graph(pos, batch, r, max_num_neighbors=32):
     ei = radius_edges(pos, batch, r, max_num_neighbors)
     return csr_views(ei, pos.shape[0])
+
+
+def radius_graph_cells(pos, batch, r, max_num_neighbors=None, loop=False, cap_policy="index", cell=None):
+    """Cell-list (binned) HIP radius graph (``csrc/graph.hip`` ``radius_graph_cells``): O(N) for
+    large structures, same output as ``radius_graph_device`` (edge set, cap policies, CSR order
+    by receiver, shifts convention).  ``cell`` [G, 3, 3] (fully periodic graphs) or None.
+    Returns (edge_index [2, E], shifts [E, 3] or None)."""
+    from .. import _native
+
+    dev = pos.device
+    n = pos.shape[0]
+    if batch is None:
+        batch = torch.zeros(n, dtype=torch.long, device=dev)
+    batch = batch.to(dev).long()
+    node_graph, gptr = _graph_ptr(batch, n)
+    G = gptr.numel() - 1
+    p = pos.detach().to(torch.float32)
+    k = -1 if max_num_neighbors is None else int(max_num_neighbors)
+    if cell is not None:
+        cellf = torch.as_tensor(cell, dtype=torch.float64, device=dev).view(-1, 3, 3)
+        inv = torch.linalg.inv(cellf)
+        vol = torch.abs(torch.linalg.det(cellf))
+        h = torch.stack([vol / torch.linalg.norm(torch.cross(cellf[:, (a + 1) % 3], cellf[:, (a + 2) % 3], dim=1),
+                                                 dim=1) for a in range(3)], 1)  # plane spacings [G, 3]
+        nb = torch.clamp(torch.floor(h / r), min=1, max=512)
+        st = torch.ceil(r / (h / nb) - 1e-9).clamp(min=1)
+        rep = torch.ceil(r / h)
+        lo = torch.zeros(G, 3, dtype=torch.float64, device=dev)
+        geo = torch.cat([inv.reshape(G, 9), cellf.reshape(G, 9), lo], 1)
+    else:
+        lo = torch.full((G, 3), float("inf"), dtype=torch.float32, device=dev).scatter_reduce(
+            0, batch.view(-1, 1).expand(-1, 3), p, "amin", include_self=True)
+        hi = torch.full((G, 3), float("-inf"), dtype=torch.float32, device=dev).scatter_reduce(
+            0, batch.view(-1, 1).expand(-1, 3), p, "amax", include_self=True)
+        ext = (hi - lo).clamp(min=0)
+        nb = torch.clamp(torch.floor(ext / r) + 1, min=1, max=1024).double()
+        st = torch.ones_like(nb)
+        rep = torch.zeros_like(nb)
+        z9 = torch.zeros(G, 9, dtype=torch.float64, device=dev)
+        geo = torch.cat([z9, z9, lo.double()], 1)
+    grid = torch.cat([nb, st, rep], 1).to(torch.int32).contiguous()
+    cells = nb.prod(1).long()
+    off = torch.zeros(G + 1, dtype=torch.long, device=dev)
+    off[1:] = torch.cumsum(cells, 0)
+    ei, sh = _native.ops().radius_graph_cells(p, node_graph, grid, geo.to(torch.float32).contiguous(), off, float(r),
+                                              k, bool(loop), cap_policy == "nearest", cell is not None)
+    return ei, (sh if cell is not None else None)

@@ -62,6 +62,12 @@ def _(config: dict, use_deepspeed=False):
     plot_hist_solution = vis.get("plot_hist_solution", False)
     create_plots = vis.get("create_plots", False)
     nn_cfg = config["NeuralNetwork"]
+    # Training.precision (extension key): "fp32" (reference numerics) or "bf16" (MFMA bf16
+    # GEMMs with fp32 accumulation / storage / master weights; geometry, segment
+    # reductions and normalisation stay fp32)
+    from .ops.linear import set_precision
+
+    set_precision(nn_cfg["Training"].get("precision", "fp32"))
     model = create_model_config(config=nn_cfg, verbosity=verbosity)
     log_name = get_log_name_config(config)
     model = get_distributed_model(model, verbosity, sync_batch_norm=nn_cfg["Architecture"].get("SyncBatchNorm", False),

@@ -173,3 +173,114 @@ def test_laplacian_pe_hip_jacobi():
             lv = float(v @ L @ v)
             assert abs(lv - float(lam[c + 1])) < 1e-3, (n, c, lv, float(lam[c + 1]))
             assert float((L @ v - lv * v).norm()) < 5e-3
+
+
+def test_pbc_radius_retry_expands_cutoff():
+    """Reference RadiusGraphPBC: when a node receives no edge the cutoff grows x1.25 (<= 3 builds)."""
+    from hydragnn_amd.data.transforms import missing_receivers, radius_graph_pbc_robust
+
+    cell = torch.eye(3) * 10.0
+    pos = torch.tensor([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [5.0, 5.0, 5.0]])
+    ei, sh, cutoff = radius_graph_pbc_robust(pos, cell, [True] * 3, 4.0, max_num_neighbors=10)
+    # atom 2 is 5*sqrt(3)-ish = 7.8 A away from the pair in the minimum image: 4 -> 5 -> 6.25 fails twice,
+    # then the artificial edge is added
+    assert missing_receivers(ei, 3).numel() == 0
+    assert abs(cutoff - 6.25) < 1e-9
+    ei2, _, c2 = radius_graph_pbc_robust(pos, cell, [True] * 3, 7.0, max_num_neighbors=10)
+    assert abs(c2 - 8.75) < 1e-9 and missing_receivers(ei2, 3).numel() == 0
+
+
+def test_ensure_connected_adds_one_edge_per_isolated_node():
+    from hydragnn_amd.data.transforms import ensure_connected
+
+    ei = torch.tensor([[0, 1], [1, 0]])
+    sh = torch.zeros(2, 3)
+    ei2, sh2, added = ensure_connected(ei, sh, 4, seed=0)
+    assert added == 2 and ei2.shape[1] == 4 and sh2.shape == (4, 3)
+    assert sorted(ei2[1, 2:].tolist()) == [2, 3]
+    assert all(int(s) != int(d) for s, d in zip(ei2[0, 2:], ei2[1, 2:]))
+
+
+def test_pbc_descriptors():
+    from hydragnn_amd.data.transforms import local_cartesian, pbc_distance
+
+    pos = torch.tensor([[0.0, 0.0, 0.0], [9.5, 0.0, 0.0]])
+    ei = torch.tensor([[1], [0]])
+    sh = torch.tensor([[10.0, 0.0, 0.0]])  # vec = pos[dst] - pos[src] + shift = 0.5
+    d = pbc_distance(pos, ei, sh, norm=False)
+    assert torch.allclose(d, torch.tensor([[0.5]]))
+    c = local_cartesian(pos, ei, sh, norm=False)
+    assert torch.allclose(c, torch.tensor([[-0.5, 0.0, 0.0]]))
+    cn = local_cartesian(pos, ei, sh, norm=True)
+    assert torch.allclose(cn, torch.tensor([[0.0, 0.5, 0.5]]))
+
+
+def test_radius_graph_default_cap_is_index_order():
+    """Non-PBC default follows torch_cluster (first sources in index order), not nearest."""
+    pos = torch.tensor([[0.0, 0, 0], [0.9, 0, 0], [0.1, 0, 0], [0.2, 0, 0]])
+    ei = radius_graph(pos, 1.0, max_num_neighbors=1)
+    first = {int(d): int(s) for s, d in zip(ei[0], ei[1])}
+    assert first[0] == 1  # index order keeps node 1 although node 2 is nearer
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy,cap", [("index", 12), ("nearest", 12), ("index", None)])
+def test_cell_list_radius_graph_matches_brute_force(policy, cap):
+    """Cell-list HIP builder == the brute-force HIP builder (edge set AND order), batched
+    non-periodic graphs of different extents."""
+    from hydragnn_amd.ops.radius import radius_graph_cells, radius_graph_device
+
+    torch.manual_seed(0)
+    sizes = [50, 300, 7, 1200]
+    pos = torch.cat([torch.rand(n, 3) * (n ** (1 / 3)) * 1.6 for n in sizes]).cuda()
+    batch = torch.cat([torch.full((n,), g, dtype=torch.long) for g, n in enumerate(sizes)]).cuda()
+    a, _ = radius_graph_cells(pos, batch, 2.1, cap, cap_policy=policy)
+    b, _ = radius_graph_device(pos, batch, 2.1, cap if cap is not None else None, cap_policy=policy)
+    assert torch.equal(a.cpu(), b.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["index", "nearest"])
+def test_cell_list_radius_graph_periodic_triclinic(policy):
+    from hydragnn_amd.ops.radius import pbc_reps, radius_graph_cells, radius_graph_device
+
+    torch.manual_seed(1)
+    cells = [torch.tensor([[6.0, 0, 0], [1.5, 5.5, 0], [0.7, 0.4, 7.0]]), torch.eye(3) * 2.5,
+             torch.tensor([[12.0, 0, 0], [0, 9.0, 0], [2.0, 0, 10.0]])]
+    counts = [40, 5, 300]
+    pos = torch.cat([torch.rand(n, 3) @ c for n, c in zip(counts, cells)]).cuda()
+    batch = torch.cat([torch.full((n,), g, dtype=torch.long) for g, n in enumerate(counts)]).cuda()
+    cell = torch.stack(cells).cuda()
+    reps = pbc_reps(cell, torch.ones(3, 3, dtype=torch.bool), 3.1)
+    a, sa = radius_graph_cells(pos, batch, 3.1, 16, cap_policy=policy, cell=cell)
+    b, sb = radius_graph_device(pos, batch, 3.1, 16, cap_policy=policy, cell=cell, reps=reps)
+    assert torch.equal(a.cpu(), b.cpu())
+    torch.testing.assert_close(sa.cpu(), sb.cpu(), rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_cell_list_radius_graph_large_structure_linear_time():
+    """A 100k-atom structure (the O(N) case): edges agree with a host reference on a sample
+    of receivers, and the build is fast."""
+    import time
+
+    from hydragnn_amd.ops.radius import radius_graph_cells
+
+    torch.manual_seed(2)
+    n = 100_000
+    L = (n / 0.08) ** (1 / 3)
+    pos = (torch.rand(n, 3) * L).cuda()
+    radius_graph_cells(pos[:1000], None, 3.0)  # warm-up
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ei, _ = radius_graph_cells(pos, None, 3.0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    assert dt < 2.0, dt
+    p = pos.cpu().double()
+    ei = ei.cpu()
+    for i in (0, 12345, 99999):
+        want = ((p - p[i]).norm(dim=1) <= 3.0).nonzero().view(-1)
+        want = want[want != i]
+        got = ei[0][ei[1] == i].sort().values
+        assert torch.equal(got, want.sort().values)

@@ -28,6 +28,7 @@ from hydragnn_amd.data.graph import Graph  # noqa: E402
 from hydragnn_amd.data.synthetic import degree_histogram, md_trajectory, molecules_like  # noqa: E402
 from hydragnn_amd.data.transforms import radius_graph  # noqa: E402
 from hydragnn_amd.models.create import create_model  # noqa: E402
+from hydragnn_amd.ops.linear import get_precision  # noqa: E402
 from hydragnn_amd.ops.pna import composite_mode  # noqa: E402
 from hydragnn_amd.train.step import TrainStep  # noqa: E402
 
@@ -152,7 +153,7 @@ def run(name, steps, warmup, dev):
     nodes = float(np.mean([s.num_nodes for s in samples]))
     return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
             "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
-            "params": sum(p.numel() for p in model.parameters()), "dtype": "fp32", "final_loss": float(loss),
+            "params": sum(p.numel() for p in model.parameters()), "dtype": get_precision(), "final_loss": float(loss),
             "data": "synthetic", "mode": "eager"}
 
 
@@ -161,7 +162,11 @@ def main():
     ap.add_argument("names", nargs="*", default=list(CONFIGS))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
+    from hydragnn_amd.ops.linear import set_precision
+
+    set_precision(a.precision)
     dev = torch.device("cuda:0")
     for n in a.names:
         print(json.dumps(run(n, a.steps, a.warmup, dev)), flush=True)
