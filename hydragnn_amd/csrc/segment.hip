@@ -31,8 +31,21 @@ struct VecT<1> {
   static __device__ __forceinline__ T add(T a, T b) { return a + b; }
 };
 
+template <typename T>
+__device__ __forceinline__ T shfl_xor_t(T v, int o);
+template <>
+__device__ __forceinline__ float shfl_xor_t<float>(float v, int o) { return __shfl_xor(v, o, 64); }
+template <>
+__device__ __forceinline__ float4 shfl_xor_t<float4>(float4 v, int o) {
+  return make_float4(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64), __shfl_xor(v.z, o, 64), __shfl_xor(v.w, o, 64));
+}
+
 // out[n, :] = sum_{e in [rowptr[n], rowptr[n+1])} x[perm ? perm[e] : e, :] * (scale? 1/deg : 1)
-template <int VEC, bool MEAN>
+// Load balance: a segment is served by KS x tpr threads of one wave — KS
+// interleaved row streams per column group, folded by a fixed xor butterfly (deterministic)
+// — so a hub node with 70 in-edges (torch_cluster "index" caps make low-index atoms the
+// source of every neighbourhood) costs ~70/KS dependent loads instead of 70.
+template <int VEC, bool MEAN, int KS>
 __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ x,
                                                       const int* __restrict__ rowptr,
                                                       const int* __restrict__ perm,
@@ -40,18 +53,20 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
                                                       int tpr, int rpb) {
   using V = VecT<VEC>;
   using T = typename V::T;
-  const int r = blockIdx.x * rpb + threadIdx.x / tpr;
-  const int c = threadIdx.x % tpr;
+  const int tg = tpr * KS;
+  const int r = blockIdx.x * rpb + threadIdx.x / tg;
+  const int lt = threadIdx.x % tg;
+  const int c = lt % tpr, k = lt / tpr;
   if (r >= N) return;
   const int beg = rowptr[r], end = rowptr[r + 1];
   const int nv = F / VEC;
   const float inv = MEAN ? 1.f / (float)max(end - beg, 1) : 1.f;
   for (int v = c; v < nv; v += tpr) {
     T a0 = V::zero(), a1 = V::zero();
-    int e = beg;
-    for (; e + 1 < end; e += 2) {
+    int e = beg + k;
+    for (; e + KS < end; e += 2 * KS) {
       const int r0 = perm ? perm[e] : e;
-      const int r1 = perm ? perm[e + 1] : e + 1;
+      const int r1 = perm ? perm[e + KS] : e + KS;
       a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
       a1 = V::add(a1, reinterpret_cast<const T*>(x + (int64_t)r1 * F)[v]);
     }
@@ -60,6 +75,9 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
       a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
     }
     T a = V::add(a0, a1);
+#pragma unroll
+    for (int o = 1; o < KS; o <<= 1) a = V::add(a, shfl_xor_t<T>(a, o * tpr));
+    if (k != 0) continue;
     if constexpr (MEAN) {
       if constexpr (VEC == 4) a = f4scale(a, inv); else a *= inv;
     }
@@ -145,21 +163,22 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   }
   const bool v4 = (F % 4 == 0);
   auto g = row_geom(N, v4 ? F : F * 4);
+  // KS row streams per segment, as long as one segment's threads stay inside a wave
+  const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);
+  const int rpb = 256 / (g.tpr * ks);
+  const int blocks = (int)std::max<int64_t>(1, (N + rpb - 1) / rpb);
+#define HY_SEG_SUM(VEC, MEAN, KS)                                                                              \
+  seg_sum_kernel<VEC, MEAN, KS><<<blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, \
+                                                              out.data_ptr<float>(), N, F, g.tpr, rpb)
+#define HY_SEG_SUM_KS(VEC, MEAN) \
+  if (ks == 4) HY_SEG_SUM(VEC, MEAN, 4); else if (ks == 2) HY_SEG_SUM(VEC, MEAN, 2); else HY_SEG_SUM(VEC, MEAN, 1)
   if (v4) {
-    if (mean)
-      seg_sum_kernel<4, true><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
-                                                              out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
-    else
-      seg_sum_kernel<4, false><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
-                                                               out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+    if (mean) { HY_SEG_SUM_KS(4, true); } else { HY_SEG_SUM_KS(4, false); }
   } else {
-    if (mean)
-      seg_sum_kernel<1, true><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
-                                                              out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
-    else
-      seg_sum_kernel<1, false><<<g.blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,
-                                                               out.data_ptr<float>(), N, F, g.tpr, g.rows_per_block);
+    if (mean) { HY_SEG_SUM_KS(1, true); } else { HY_SEG_SUM_KS(1, false); }
   }
+#undef HY_SEG_SUM_KS
+#undef HY_SEG_SUM
   return x_.dim() == 1 ? out.squeeze(1) : out;
 }
 

@@ -33,7 +33,8 @@ def oc20_like(num_graphs, seed=0, min_atoms=20, max_atoms=126, radius=10.0, max_
         L = (n / density) ** (1.0 / 3.0)
         pos = torch.from_numpy(rng.uniform(0.0, L, size=(n, 3))).to(torch.float32)
         z = torch.from_numpy(rng.integers(1, 84, size=(n,))).to(torch.float32)
-        ei = radius_graph(pos, radius, max_num_neighbors=max_neighbours)
+        # OC20's AtomsToGraphs keeps the nearest neighbours (radius_graph_pbc in fairchem)
+        ei = radius_graph(pos, radius, max_num_neighbors=max_neighbours, cap_policy="nearest")
         vec = pos[ei[1]] - pos[ei[0]]
         length = torch.linalg.norm(vec, dim=-1, keepdim=True)
         edge_attr = length / radius

@@ -153,6 +153,7 @@ class _EngineSumF32(_TallLinearSum):
 
 
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+BIG_GEMM = 1 << 30  # M*N*K above which bf16 maps go to the library's large-tile kernels
 
 
 def _engine_ok(tensors):
@@ -175,6 +176,13 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     ws = [p[1] for p in pairs]
     engine = len(pairs) <= 3 and _engine_ok(xs + ws) and xs[0].shape[0] > 0 and \
         (residual is None or (residual.is_cuda and residual.dtype == torch.float32))
+    if engine and _state["prec"] == 1 and len(pairs) == 1 and residual is None and \
+            xs[0].shape[0] * ws[0].shape[0] * ws[0].shape[1] >= BIG_GEMM:
+        # big dense maps (e.g. the SC25 EGNN's 866-wide edge/node MLPs): the library's tuned
+        # 256x256-tile bf16 MFMA GEMMs (hipBLASLt), bf16 in / fp32 accumulate, fp32 out
+        y = F.linear(xs[0].to(torch.bfloat16), ws[0].to(torch.bfloat16),
+                     None if b is None else b.to(torch.bfloat16)).float()
+        return torch.relu(y) if act == ACT_RELU else y
     if engine and _state["prec"] == 1:
         flat = []
         for x, w in zip(xs, ws):
