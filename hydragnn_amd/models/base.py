@@ -471,20 +471,33 @@ class Base(nn.Module):
         assert self.num_heads == 1 and self.head_type[0] == "node", \
             "Force predictions are only supported for models with one head that predict nodal energy."
         node_energy_pred = pred[0]
-        graph_energy_pred = seg.segment_sum(node_energy_pred, data.graph_si).squeeze().float()
-        graph_energy_true = data.energy.squeeze().float()
+        graph_energy_pred = seg.segment_sum(node_energy_pred, data.graph_si).squeeze(-1).float()
+        graph_energy_true = data.energy.reshape(graph_energy_pred.shape).float()
         w = self.loss_weights[0]
-        e_loss = self.loss_function(graph_energy_pred, graph_energy_true)
-        tot = e_loss * w
-        tasks = [e_loss]
+        gmask, nmask = data.get("graph_mask"), data.get("node_mask")
         forces_true = data.forces.float()
         forces_pred = torch.autograd.grad(graph_energy_pred, data.pos, grad_outputs=torch.ones_like(graph_energy_pred),
                                           retain_graph=graph_energy_pred.requires_grad, create_graph=True)[0]
         assert forces_pred is not None, "No gradients were found for data.pos."
         forces_pred = -forces_pred.float()
-        fw = w * torch.mean(torch.abs(graph_energy_true)) / (torch.mean(torch.abs(forces_true)) + 1e-8)
-        tot = tot + self.loss_function(forces_pred, forces_true) * fw
-        return tot, tasks
+        if gmask is None:
+            e_loss = self.loss_function(graph_energy_pred, graph_energy_true)
+            f_loss = self.loss_function(forces_pred, forces_true)
+            fw = w * torch.mean(torch.abs(graph_energy_true)) / (torch.mean(torch.abs(forces_true)) + 1e-8)
+        else:
+            # statically padded batch (captured step): the dummy graph / padding atoms are masked out
+            from ..train.step import masked_loss
+
+            kind = self.loss_function_type
+            e_loss = masked_loss(kind, graph_energy_pred.view(-1, 1), graph_energy_true.view(-1, 1), gmask)
+            f_loss = masked_loss(kind, forces_pred, forces_true, nmask)
+            ge = torch.where(gmask, graph_energy_true.abs(), torch.zeros_like(graph_energy_true)).sum() / \
+                gmask.sum().clamp(min=1)
+            fa = torch.where(nmask.view(-1, 1), forces_true.abs(), torch.zeros_like(forces_true)).sum() / \
+                (nmask.sum().clamp(min=1) * 3)
+            fw = w * ge / (fa + 1e-8)
+        tot = e_loss * w + f_loss * fw
+        return tot, [e_loss]
 
     def __str__(self):
         return "Base"

@@ -81,6 +81,18 @@ class PainnMessage(nn.Module):
         return s, v
 
 
+def safe_vector_norm(v, dim):
+    """||v|| with a zero (not NaN) first AND second derivative at v = 0.
+
+    Nodes with no incoming message keep v = 0 (padding atoms of a captured bucket, or
+    isolated atoms); ``torch.linalg.vector_norm``'s double backward is 0/0 there, which
+    poisons force training (``energy_force_loss`` differentiates twice).  Equal to the
+    plain norm wherever v != 0."""
+    n2 = (v * v).sum(dim)
+    nz = n2 > 0
+    return torch.where(nz, torch.sqrt(torch.where(nz, n2, torch.ones_like(n2))), torch.zeros_like(n2))
+
+
 class PainnUpdate(nn.Module):
     def __init__(self, node_size, last_layer=False, u_name="update_U"):
         super().__init__()
@@ -97,7 +109,7 @@ class PainnUpdate(nn.Module):
         F = s.shape[-1]
         Uv = getattr(self, self._u)(v)
         Vv = self.update_V(v)
-        a = self.update_mlp(torch.cat((torch.linalg.vector_norm(Vv, dim=1), s), dim=-1))
+        a = self.update_mlp(torch.cat((safe_vector_norm(Vv, 1), s), dim=-1))
         inner = (Uv * Vv).sum(1)
         if self.last_layer:
             a_sv, a_ss = a[:, :F], a[:, F:]

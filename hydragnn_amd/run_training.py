@@ -94,10 +94,11 @@ def _(config: dict, use_deepspeed=False):
         train_loader, val_loader, test_loader = to_device_loaders(
             (train_loader, val_loader, test_loader), get_device(), module.head_type, module.head_dims,
             attn_scope=getattr(module, "attn_scope", "batch"))
-        mode = "graph" if (int(os.getenv("HYDRAGNN_CAPTURE", "1")) == 1 and not compute_grad_energy
+        mode = "graph" if (int(os.getenv("HYDRAGNN_CAPTURE", "1")) == 1
                            and getattr(module, "capturable", True)) else "eager"
         world = dist.get_world_size() if dist.is_initialized() else 1
-        engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer)
+        engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer,
+                           compute_grad_energy=compute_grad_energy)
         engine.prepare(train_loader.store, train_loader.batch_size)
     from .parallel.zero import ZeroRedundancyOptimizer
 

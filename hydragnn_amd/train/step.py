@@ -140,7 +140,11 @@ class _Captured:
 
 class TrainStep:
     def __init__(self, model, lr=1e-3, mode="graph", world=1, optimizer=None, weight_decay=0.01,
-                 node_bucket=256, edge_bucket=2048, max_graphs=16, bucket_cap_mb=None):
+                 node_bucket=256, edge_bucket=2048, max_graphs=16, bucket_cap_mb=None, compute_grad_energy=False):
+        # compute_grad_energy: energy + force loss with forces = -dE/dpos (double backward,
+        # reference Base.energy_force_loss); the whole step — including the create_graph
+        # backward through the segment ops — is captured like any other step
+        self.forces = compute_grad_energy
         self.model = model
         self.module = model.module if isinstance(model, DistributedDataParallel) else model
         self.world = world
@@ -192,6 +196,14 @@ class TrainStep:
             self.flat_grads.release()
 
     def _backward(self, loss, sync=True):
+        if self.forces:
+            from ..ops.pna import composite_mode
+
+            with composite_mode(True):
+                return self._backward_impl(loss, sync)
+        return self._backward_impl(loss, sync)
+
+    def _backward_impl(self, loss, sync=True):
         if self.sync is not None:
             if sync:
                 self.sync.begin()
@@ -205,8 +217,7 @@ class TrainStep:
     def eager(self, store, indices):
         batch = store.batch(indices)
         self._zero()
-        pred = self.model(batch)
-        loss, tasks = batch_loss(self.module, pred, batch)
+        loss, tasks = self._loss(batch)
         self._backward(loss)
         self._set_guard(loss)
         self.opt.step()
@@ -258,11 +269,21 @@ class TrainStep:
             return min(cands, key=lambda k: (k[0] - N) + (k[1] - E) / 8.0)
         return want
 
+    def _loss(self, batch):
+        if self.forces:
+            from ..ops.pna import composite_mode
+
+            batch.pos.requires_grad_(True)
+            with composite_mode(True):  # every op on the pos -> E path must be twice differentiable
+                pred = self.model(batch)
+                return self.module.energy_force_loss(pred, batch)
+        pred = self.model(batch)
+        return batch_loss(self.module, pred, batch)
+
     def _body_fwd_bwd(self, store, cap, sync=True):
         self._zero()
         batch = store.assemble(cap.dev_plan, cap.lay)
-        pred = self.model(batch)
-        loss, tasks = batch_loss(self.module, pred, batch)
+        loss, tasks = self._loss(batch)
         self._backward(loss, sync=sync)
         self._set_guard(loss)
         return loss.detach(), [t.detach() for t in tasks]

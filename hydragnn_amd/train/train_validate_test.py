@@ -114,7 +114,8 @@ def train(loader, model, opt, verbosity, profiler=None, use_deepspeed=False, com
     nbatch = get_nbatch(loader, synchronize=True)
     trace_level = int(os.getenv("HYDRAGNN_TRACE_LEVEL", "0"))
     sync = {"cudasync": trace_level > 0}
-    use_engine = step_engine is not None and isinstance(loader, DeviceGraphLoader) and not compute_grad_energy
+    use_engine = step_engine is not None and isinstance(loader, DeviceGraphLoader) and \
+        (not compute_grad_energy or getattr(step_engine, "forces", False))
     tr.start("dataload", **sync)
     it = loader.index_batches() if use_engine else iter(loader)
     for ibatch, data in iterate_tqdm(enumerate(it), verbosity, desc="Train", total=nbatch):

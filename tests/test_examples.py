@@ -49,8 +49,10 @@ def test_md17_forces(mpnn_type, tmp_path):
     assert r["test_error"] == r["test_error"]
 
 
-@pytest.mark.parametrize("mpnn_type", ["DimeNet", "EGNN"])
+@pytest.mark.parametrize("mpnn_type", ["PNAPlus", "SchNet", "DimeNet", "EGNN", "PNAEq", "PAINN", "MACE"])
 def test_lennard_jones_forces(mpnn_type, tmp_path):
+    """Reference ``tests/test_examples.py:65-87``: the LJ grad-forces example over all 7 stacks
+    whose energies depend on positions (forces = -dE/dpos, double backward)."""
     r = _result(_run("LennardJones/lj.py", ["--num_samples", "20", "--num_epoch", "2", "--mpnn_type", mpnn_type],
                      tmp_path))
     assert r["test_error"] == r["test_error"]

@@ -1,0 +1,65 @@
+"""Force training (energy + forces = -dE/dpos, reference ``Base.energy_force_loss``,
+``Base.py:582-636``) through the training engine: the statically padded step (the CPU
+twin of the captured hipGraph step) equals the eager step, i.e. the dummy graph and
+padding atoms are masked out of both the energy and the force loss."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from hydragnn_amd.data.device_store import DeviceGraphStore
+from hydragnn_amd.data.synthetic import md_trajectory
+from hydragnn_amd.data.transforms import radius_graph
+from hydragnn_amd.models.create import create_model
+from hydragnn_amd.train.step import TrainStep
+
+HEADS = {"node": [{"type": "branch-0", "architecture": {"num_headlayers": 2, "dim_headlayers": [16, 16],
+                                                        "type": "mlp"}}]}
+
+
+def _samples(n=16):
+    s = md_trajectory(n, seed=2, num_atoms=9)
+    for d in s:
+        d.edge_index = radius_graph(d.pos, 5.0, max_num_neighbors=8)
+        d.edge_attr = (d.pos[d.edge_index[1]] - d.pos[d.edge_index[0]]).norm(dim=-1, keepdim=True) / 5.0
+        d.sort_edges_by_dst()
+    return s
+
+
+def _model(mpnn):
+    return create_model(mpnn, 1, 16, [1], 0, "", "", 0, ["node"], HEADS, "relu", "mae", [1.0], 2, num_nodes=9,
+                        edge_dim=1, radius=5.0, num_radial=6, envelope_exponent=5, equivariance=True, use_gpu=False,
+                        dropout=0.0, max_neighbours=8, pna_deg=[0, 2, 4, 6, 8, 10, 6, 4, 2])
+
+
+@pytest.mark.parametrize("mpnn", ["PAINN", "EGNN", "PNAEq"])
+def test_padded_force_step_equals_eager(mpnn):
+    samples = _samples()
+    m1 = _model(mpnn)
+    m2 = copy.deepcopy(m1)
+    store = DeviceGraphStore(samples, "cpu")
+    eager = TrainStep(m1, lr=1e-3, mode="eager", compute_grad_energy=True)
+    padded = TrainStep(m2, lr=1e-3, mode="graph", compute_grad_energy=True, node_bucket=64, edge_bucket=512)
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        idx = list(rng.choice(len(store), 4, replace=False))
+        le = float(eager(store, idx)[0])
+        lp = float(padded(store, idx)[0])
+        assert abs(le - lp) <= 1e-4 * max(1.0, abs(le)), (le, lp)
+
+
+@pytest.mark.gpu
+def test_captured_force_step_matches_eager_gpu():
+    samples = _samples()
+    m1 = _model("PAINN").cuda()
+    m2 = copy.deepcopy(m1)
+    store = DeviceGraphStore(samples, "cuda")
+    eager = TrainStep(m1, lr=1e-3, mode="eager", compute_grad_energy=True)
+    graph = TrainStep(m2, lr=1e-3, mode="graph", compute_grad_energy=True, node_bucket=64, edge_bucket=512)
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        idx = list(rng.choice(len(store), 4, replace=False))
+        le = float(eager(store, idx)[0])
+        lg = float(graph(store, idx)[0])
+        assert abs(le - lg) <= 1e-3 * max(1.0, abs(le)), (le, lg)

@@ -116,18 +116,13 @@ def run(name, steps, warmup, dev):
     store = DeviceGraphStore(samples, dev, head_types=None if forces else ht, head_dims=None if forces else hd)
     rng = np.random.default_rng(0)
     if forces:
-        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        ts = TrainStep(model, lr=1e-3, mode=os.environ.get("BENCH_FORCES_MODE", "graph"), compute_grad_energy=True,
+                       node_bucket=512, edge_bucket=4096)
+        ts.prepare(store, B)
+        ts.precapture(store, B)
 
         def step(idx):
-            b = store.batch(idx)
-            b.pos.requires_grad_(True)
-            opt.zero_grad(set_to_none=True)
-            with composite_mode(True):
-                pred = model(b)
-                loss, _ = model.energy_force_loss(pred, b)
-                loss.backward()
-            opt.step()
-            return loss
+            return ts(store, idx)[0]
     else:
         ts = TrainStep(model, lr=1e-3, mode="eager")
 
