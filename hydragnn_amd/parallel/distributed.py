@@ -61,7 +61,11 @@ def _default_backend():
     if os.getenv("HYDRAGNN_BACKEND"):
         return os.environ["HYDRAGNN_BACKEND"]
     if dist.is_nccl_available() and torch.cuda.is_available():
-        return "nccl"
+        # RCCL needs one GPU per rank; oversubscribed local ranks (e.g. a 3-rank test on a
+        # 1-GPU box) fall back to gloo, which also carries CUDA tensors
+        local_world = int(os.getenv("LOCAL_WORLD_SIZE", "1"))
+        if local_world <= torch.cuda.device_count():
+            return "nccl"
     return "gloo"
 
 

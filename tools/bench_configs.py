@@ -149,7 +149,7 @@ def run(name, steps, warmup, dev):
     return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
             "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
             "params": sum(p.numel() for p in model.parameters()), "dtype": get_precision(), "final_loss": float(loss),
-            "data": "synthetic", "mode": "eager"}
+            "data": "synthetic", "mode": ts.mode}
 
 
 def main():
