@@ -35,10 +35,38 @@ def available():
     return load()
 
 
+class _SyncOps:
+    """``HYDRA_DEBUG_SYNC=1`` (SURVEY §5.2 debug mode): every native op is followed by a
+    device synchronisation, so an asynchronous kernel fault (bad index, NaN trap, launch
+    failure) is reported at the op that caused it, with the op's name, instead of at a later
+    unrelated sync.  Not capture-safe; debugging only."""
+
+    def __init__(self, ns):
+        self._ns = ns
+
+    def __getattr__(self, name):
+        op = getattr(self._ns, name)
+
+        def run(*args, **kwargs):
+            out = op(*args, **kwargs)
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize()
+                except RuntimeError as e:
+                    raise RuntimeError(f"HYDRA_DEBUG_SYNC: device error after hydra::{name}: {e}") from e
+            return out
+
+        return run
+
+
+def debug_sync():
+    return os.environ.get("HYDRA_DEBUG_SYNC", "0") == "1"
+
+
 def ops():
     """Return ``torch.ops.hydra``; raise loudly if the native library is unavailable."""
     if not load():
         raise RuntimeError(
             "hydragnn_amd native HIP library is required for GPU tensors but is unavailable: " + str(_error)
         )
-    return torch.ops.hydra
+    return _SyncOps(torch.ops.hydra) if debug_sync() else torch.ops.hydra

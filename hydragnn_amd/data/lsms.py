@@ -174,6 +174,23 @@ def read_xyz(filepath, node_feature_dim=(), node_feature_col=(), graph_feature_d
 READERS = {"LSMS": read_lsms, "unit_test": read_lsms, "CFG": read_cfg, "XYZ": read_xyz}
 
 
+def check_same_count_across_ranks(n, what=""):
+    """All-reduce MIN and MAX of a host count over the host (gloo) group; raise if ranks disagree."""
+    import torch
+    import torch.distributed as dist
+
+    from ..parallel.distributed import host_group
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return n
+    t = torch.tensor([n, -n], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_group())
+    if int(t[0]) != n or int(-t[1]) != n:
+        raise RuntimeError(f"rank {dist.get_rank()} sees {n} files in {what}; ranks disagree "
+                           f"(min {int(-t[1])}, max {int(t[0])})")
+    return n
+
+
 class RawDataLoader:
     """Raw directories -> normalised serialized split files (``raw_dataset_loader.py:26-277``)."""
 
@@ -217,6 +234,9 @@ class RawDataLoader:
 
                 random.seed(43)
                 random.shuffle(files)
+                # C16 (``raw_dataset_loader.py:115-118``): every rank must see the same directory
+                # listing before splitting it, or the per-rank shards overlap / drop files
+                check_same_count_across_ranks(len(files), raw_path)
                 files = list(nsplit(files, dist.get_world_size()))[dist.get_rank()]
             dataset = []
             for name in files:

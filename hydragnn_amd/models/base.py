@@ -463,8 +463,10 @@ class Base(nn.Module):
             tasks_loss.append(l)
         return tot_loss, tasks_loss
 
-    def energy_force_loss(self, pred, data):
-        """Energy + force loss; forces = -dE/dpos with create_graph=True (``Base.py:582-636``)."""
+    def energy_force_predict(self, pred, data, create_graph=True):
+        """(graph energy pred, graph energy true, forces pred, forces true) with
+        forces = -dE/dpos (``Base.py:582-636``); ``create_graph`` keeps the force graph for the
+        double backward of training."""
         assert data.pos is not None and data.energy is not None and data.forces is not None, \
             "data.pos, data.energy, data.forces must be provided for energy-force loss."
         assert data.pos.requires_grad, "data.pos does not have grad, so force predictions cannot be computed."
@@ -473,13 +475,17 @@ class Base(nn.Module):
         node_energy_pred = pred[0]
         graph_energy_pred = seg.segment_sum(node_energy_pred, data.graph_si).squeeze(-1).float()
         graph_energy_true = data.energy.reshape(graph_energy_pred.shape).float()
+        forces_pred = torch.autograd.grad(graph_energy_pred, data.pos, grad_outputs=torch.ones_like(graph_energy_pred),
+                                          retain_graph=graph_energy_pred.requires_grad and create_graph,
+                                          create_graph=create_graph)[0]
+        assert forces_pred is not None, "No gradients were found for data.pos."
+        return graph_energy_pred, graph_energy_true, -forces_pred.float(), data.forces.float()
+
+    def energy_force_loss(self, pred, data):
+        """Energy + force loss; forces = -dE/dpos with create_graph=True (``Base.py:582-636``)."""
+        graph_energy_pred, graph_energy_true, forces_pred, forces_true = self.energy_force_predict(pred, data)
         w = self.loss_weights[0]
         gmask, nmask = data.get("graph_mask"), data.get("node_mask")
-        forces_true = data.forces.float()
-        forces_pred = torch.autograd.grad(graph_energy_pred, data.pos, grad_outputs=torch.ones_like(graph_energy_pred),
-                                          retain_graph=graph_energy_pred.requires_grad, create_graph=True)[0]
-        assert forces_pred is not None, "No gradients were found for data.pos."
-        forces_pred = -forces_pred.float()
         if gmask is None:
             e_loss = self.loss_function(graph_energy_pred, graph_energy_true)
             f_loss = self.loss_function(forces_pred, forces_true)

@@ -58,7 +58,8 @@ def prepare_batch(data, module, device):
         return data
     if data.x is not None and data.x.device != device:
         data = data.to(device, non_blocking=True)
-    data["targets"] = head_targets(data, module.head_type, module.head_dims) if data.get("y") is not None else []
+    data["targets"] = head_targets(data, module.head_type, module.head_dims) \
+        if data.get("y") is not None and data.get("y_loc") is not None else []
     return data
 
 
@@ -210,8 +211,43 @@ def validate(loader, model, verbosity, reduce_ranks=True, compute_grad_energy=Fa
     return val_error, tasks_error
 
 
+def _dump_force_samples(records, data, e_pred, e_true, f_pred, f_true):
+    """Per-sample energy/force records of ``HYDRAGNN_DUMP_TESTDATA=1`` (reference
+    ``train_validate_test.py:642-705``: energy true/pred, flattened forces true/pred, mean
+    per-atom force error)."""
+    ptr = data.ptr.tolist()
+    for i in range(len(ptr) - 1):
+        lo, hi = ptr[i], ptr[i + 1]
+        ft, fp = f_true[lo:hi].detach().cpu(), f_pred[lo:hi].detach().cpu()
+        records.append({"energy_true": float(e_true[i]), "forces_true": ft.flatten(),
+                        "energy_pred": float(e_pred[i]), "forces_pred": fp.flatten(),
+                        "forces_average_error_per_atom": (ft - fp).norm(dim=1).mean()})
+
+
+def _dump_samples(records, data, pred, module):
+    p = pred[0] if module.var_output else pred
+    ptr = data.ptr.tolist()
+    for i in range(len(ptr) - 1):
+        rec = {}
+        for ih in range(module.num_heads):
+            t = data.targets[ih]
+            if module.head_type[ih] == "graph":
+                rec[f"head{ih}_true"], rec[f"head{ih}_pred"] = t[i].detach().cpu(), p[ih][i].detach().cpu()
+            else:
+                lo, hi = ptr[i], ptr[i + 1]
+                rec[f"head{ih}_true"], rec[f"head{ih}_pred"] = t[lo:hi].detach().cpu(), p[ih][lo:hi].detach().cpu()
+        records.append(rec)
+
+
 @torch.no_grad()
 def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compute_grad_energy=False):
+    """Test-set error (+ per-head true/pred samples).
+
+    Force runs (``compute_grad_energy``) return per-graph energies as head 0's samples
+    (prediction = sum of the node-energy head; the round-1 code returned nothing).  With
+    ``HYDRAGNN_DUMP_TESTDATA=1`` every rank writes its per-sample records to
+    ``testdata_rank{r}.pt`` (a list of dicts of tensors/floats; ``torch.load(...,
+    weights_only=True)`` reads it back; the reference pickles the same fields)."""
     module = _module(model)
     device = next(module.parameters()).device
     total_error = torch.tensor(0.0, device=device)
@@ -219,6 +255,8 @@ def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compu
     num_samples = 0
     model.eval()
     nbatch = get_nbatch(loader)
+    dump = int(os.getenv("HYDRAGNN_DUMP_TESTDATA", "0")) == 1
+    records = [] if dump else None
     true_values = [[] for _ in range(module.num_heads)]
     predicted_values = [[] for _ in range(module.num_heads)]
     for data in iterate_tqdm(_eval_batches(loader, nbatch), verbosity, desc="Test", total=nbatch):
@@ -228,25 +266,39 @@ def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compu
                 data.pos.requires_grad_(True)
                 pred = model(data)
                 err, tasks = _loss(module, pred, data, True)
+                if return_samples or dump:
+                    e_pred, e_true, f_pred, f_true = module.energy_force_predict(pred, data, create_graph=False)
+            if return_samples:
+                true_values[0].append(e_true.detach().reshape(-1, 1))
+                predicted_values[0].append(e_pred.detach().reshape(-1, 1))
+            if dump:
+                _dump_force_samples(records, data, e_pred, e_true, f_pred, f_true)
         else:
             pred = model(data)
             err, tasks = _loss(module, pred, data, False)
+            if return_samples:
+                p = pred[0] if module.var_output else pred
+                for ih in range(module.num_heads):
+                    true_values[ih].append(data.targets[ih].reshape(-1, 1))
+                    predicted_values[ih].append(p[ih].reshape(-1, 1))
+            if dump:
+                _dump_samples(records, data, pred, module)
         ng = data.get("num_graphs_real", data.num_graphs)
         total_error += err.detach() * ng
         num_samples += ng
         for k in range(len(tasks)):
             tasks_error[k] += tasks[k].detach() * ng
-        if return_samples and not compute_grad_energy:
-            p = pred[0] if module.var_output else pred
-            for ih in range(module.num_heads):
-                true_values[ih].append(data.targets[ih].reshape(-1, 1))
-                predicted_values[ih].append(p[ih].reshape(-1, 1))
+    if dump:
+        from ..parallel.distributed import get_comm_size_and_rank
+
+        torch.save(records, f"testdata_rank{get_comm_size_and_rank()[1]}.pt")
     n = max(num_samples, 1)
     test_error, tasks_error = total_error / n, tasks_error / n
-    if return_samples and true_values[0]:
+    if return_samples and len(true_values[0]) > 0:
         for ih in range(module.num_heads):
-            true_values[ih] = torch.cat(true_values[ih], 0)
-            predicted_values[ih] = torch.cat(predicted_values[ih], 0)
+            if true_values[ih]:
+                true_values[ih] = torch.cat(true_values[ih], 0)
+                predicted_values[ih] = torch.cat(predicted_values[ih], 0)
     if reduce_ranks:
         test_error = reduce_values_ranks(test_error)
         tasks_error = reduce_values_ranks(tasks_error)

@@ -46,23 +46,41 @@ class Timer:
 
 
 def gather_timers():
-    """Return {name: (min, max, avg, calls)} over ranks (one host collective)."""
+    """Return {name: (min, max, avg, calls)} over ranks.
+
+    Ranks may have timed different regions (a branch-only timer, an early-stop path),
+    so the name sets are first unioned (one ``all_gather_object``) and every rank then
+    reduces the SAME aligned vector; a rank that never ran a timer contributes 0 s to
+    the sum and is excluded from min/max.  Sorting only the local names (the round-1
+    code, and the reference's per-name collectives, Appendix D #13) mismatches or hangs."""
     import torch.distributed as dist
 
     names = sorted(Timer.timers_local)
-    vals = torch.tensor([Timer.timers_local[n] for n in names], dtype=torch.float64)
-    if dist.is_initialized() and dist.get_world_size() > 1 and names:
+    distributed = dist.is_initialized() and dist.get_world_size() > 1
+    if distributed:
         from ..parallel.distributed import host_group
 
         g = host_group()
-        mn, mx, sm = vals.clone(), vals.clone(), vals.clone()
+        lists = [None] * dist.get_world_size()
+        dist.all_gather_object(lists, names, group=g)
+        names = sorted(set().union(*lists))
+    have = torch.tensor([n in Timer.timers_local for n in names], dtype=torch.bool)
+    vals = torch.tensor([Timer.timers_local.get(n, 0.0) for n in names], dtype=torch.float64)
+    calls = torch.tensor([Timer.number_calls.get(n, 0) for n in names], dtype=torch.float64)
+    if distributed and names:
+        inf = torch.full_like(vals, float("inf"))
+        mn = torch.where(have, vals, inf)
+        mx = torch.where(have, vals, -inf)
+        sm, cnt, nr = vals.clone(), calls.clone(), have.double()
         dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=g)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=g)
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM, group=g)
-        avg = sm / dist.get_world_size()
+        for t in (sm, cnt, nr):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
+        avg = sm / nr.clamp(min=1)
+        calls = cnt
     else:
         mn = mx = avg = vals
-    return {n: (float(mn[i]), float(mx[i]), float(avg[i]), Timer.number_calls[n]) for i, n in enumerate(names)}
+    return {n: (float(mn[i]), float(mx[i]), float(avg[i]), int(calls[i])) for i, n in enumerate(names)}
 
 
 def print_timers(verbosity):

@@ -47,9 +47,10 @@ def unittest_train_model(mpnn_type, global_attn_engine, global_attn_type, ci_inp
     raise err
 
 
-def _train_once(mpnn_type, global_attn_engine, global_attn_type, ci_input, use_lengths, workdir, overwrite_config,
-                num_samples_tot, init_seed):
-    torch.manual_seed(int(os.environ.get("HYDRAGNN_TEST_SEED", "97")))
+def ci_config(mpnn_type, ci_input, workdir, overwrite_config=None, num_samples_tot=500, init_seed=0,
+              use_lengths=False, global_attn_engine="", global_attn_type=""):
+    """The CI config with dataset paths resolved under ``workdir``; rank 0 generates the
+    deterministic BCC dataset the first time (reference ``tests/test_graphs.py:40-95``)."""
     _, rank = get_comm_size_and_rank()
     os.environ["SERIALIZED_DATA_PATH"] = workdir
     config = ci(ci_input)
@@ -87,13 +88,28 @@ def _train_once(mpnn_type, global_attn_engine, global_attn_type, ci_input, use_l
         for split, path in config["Dataset"]["path"].items():
             if not path.endswith(".pkl"):
                 config["Dataset"]["path"][split] = os.path.join(workdir, path)
+    return config
+
+
+def run_ci(mpnn_type, ci_input, workdir, overwrite_config=None, num_samples_tot=500, init_seed=0, predict=True,
+           **kw):
+    """run_training (+ run_prediction) of a CI config inside ``workdir`` (logs/ land there)."""
+    config = ci_config(mpnn_type, ci_input, workdir, overwrite_config, num_samples_tot, init_seed, **kw)
     cwd = os.getcwd()
     os.chdir(workdir)
     try:
         hydragnn_amd.run_training(config)
-        error, error_task, true_values, pred_values = hydragnn_amd.run_prediction(config)
+        return hydragnn_amd.run_prediction(config) if predict else None
     finally:
         os.chdir(cwd)
+
+
+def _train_once(mpnn_type, global_attn_engine, global_attn_type, ci_input, use_lengths, workdir, overwrite_config,
+                num_samples_tot, init_seed):
+    torch.manual_seed(int(os.environ.get("HYDRAGNN_TEST_SEED", "97")))
+    error, error_task, true_values, pred_values = run_ci(
+        mpnn_type, ci_input, workdir, overwrite_config, num_samples_tot, init_seed, use_lengths=use_lengths,
+        global_attn_engine=global_attn_engine, global_attn_type=global_attn_type)
     t = thresholds(mpnn_type, ci_input, use_lengths)
     for ih in range(len(true_values)):
         assert float(error_task[ih]) < t[0], f"head {ih} RMSE {float(error_task[ih])} >= {t[0]}"

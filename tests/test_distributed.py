@@ -236,6 +236,37 @@ def _reduce_body(rank, world):
     assert allrows.shape[0] == sum(r + 2 for r in range(world))
 
 
+def _timers_body(rank, world):
+    """Ranks time different regions (rank 1 has an extra timer, rank 0 one of its own):
+    the reduction unions the names and never mismatches or hangs (ref Appendix D #13)."""
+    from hydragnn_amd.utils.time_utils import Timer, gather_timers
+
+    Timer.reset()
+    names = ["common"] + (["only_rank1_a", "only_rank1_b"] if rank == 1 else ["zz_rank0"])
+    for n in names:
+        t = Timer(n)
+        t.start()
+        t.stop()
+    Timer.timers_local["common"] = float(rank + 1)
+    st = gather_timers()
+    assert set(st) == {"common", "only_rank1_a", "only_rank1_b", "zz_rank0"}
+    mn, mx, avg, calls = st["common"]
+    assert (mn, mx, avg, calls) == (1.0, 2.0, 1.5, 2)
+    assert st["only_rank1_a"][3] == 1 and st["zz_rank0"][3] == 1
+
+
+def _filecount_body(rank, world):
+    from hydragnn_amd.data.lsms import check_same_count_across_ranks
+
+    assert check_same_count_across_ranks(7, "same") == 7
+    try:
+        check_same_count_across_ranks(7 + rank, "differs")
+    except RuntimeError as e:
+        assert "ranks disagree" in str(e)
+    else:
+        raise AssertionError("mismatched file counts not detected")
+
+
 def _train_body(rank, world, workdir):
     from graph_train_util import unittest_train_model
 
@@ -305,6 +336,14 @@ def test_syncbatchnorm_matches_full_batch():
 
 def test_metric_reductions():
     run_ranks("_reduce_body")
+
+
+def test_timer_reduction_with_rank_specific_timers():
+    run_ranks("_timers_body")
+
+
+def test_raw_file_count_check():
+    run_ranks("_filecount_body")
 
 
 def test_task_parallel_multibranch_four_ranks():

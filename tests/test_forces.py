@@ -63,3 +63,23 @@ def test_captured_force_step_matches_eager_gpu():
         le = float(eager(store, idx)[0])
         lg = float(graph(store, idx)[0])
         assert abs(le - lg) <= 1e-3 * max(1.0, abs(le)), (le, lg)
+
+
+def test_force_test_returns_samples_and_dump(tmp_path, monkeypatch):
+    """``test()`` on a force run returns per-graph energy samples (head 0) and, with
+    HYDRAGNN_DUMP_TESTDATA=1, per-sample energy/force records (ref ``train_validate_test.py:642-705``)."""
+    from hydragnn_amd.data.graph import collate
+    from hydragnn_amd.train.train_validate_test import test as run_test
+
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("HYDRAGNN_DUMP_TESTDATA", "1")
+    samples = _samples(8)
+    loader = [collate(samples[:4]), collate(samples[4:])]
+    m = _model("PAINN")
+    err, _, true, pred = run_test(loader, m, 0, compute_grad_energy=True)
+    assert true[0].shape == (8, 1) and pred[0].shape == (8, 1)
+    assert torch.allclose(true[0].view(-1), torch.stack([s.energy.reshape(()) for s in samples]).float())
+    recs = torch.load(tmp_path / "testdata_rank0.pt", weights_only=True)
+    assert len(recs) == 8
+    assert recs[0]["forces_pred"].numel() == samples[0].num_nodes * 3
+    assert abs(recs[3]["energy_pred"] - float(pred[0][3])) < 1e-5
