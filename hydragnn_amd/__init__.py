@@ -10,4 +10,4 @@ __version__ = "0.1.0"
 
 from . import _native  # noqa: F401
 from .run_prediction import run_prediction  # noqa: F401
-from .run_training import run_training  # noqa: F401
+from .run_training import run_training, train_model  # noqa: F401

@@ -34,14 +34,19 @@ from .graph import Graph
 DEFAULT_DATASET_IDS = {"ani1x": 0, "qm7x": 1, "mptrj": 2, "alexandria": 3, "transition1x": 4, "omat24": 5}
 
 
+COMM_SELF = "self"  # the MPI.COMM_SELF analogue: a writer/reader used by one rank alone
+
+
 def _rank_world(group=None):
+    if group == COMM_SELF:
+        return 0, 1
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
 
 
 def _allgather_obj(obj, group=None):
-    if not (dist.is_available() and dist.is_initialized()):
+    if group == COMM_SELF or not (dist.is_available() and dist.is_initialized()):
         return [obj]
     from ..parallel.distributed import host_group
 
@@ -51,7 +56,7 @@ def _allgather_obj(obj, group=None):
 
 
 def _barrier(group=None):
-    if dist.is_available() and dist.is_initialized():
+    if group != COMM_SELF and dist.is_available() and dist.is_initialized():
         from ..parallel.distributed import host_group
 
         dist.barrier(group=group or host_group())
@@ -422,12 +427,36 @@ class AbstractRawDataset(AbstractBaseDataset):
                                                              replace=False))]
         self.dataset = proc.process(samples)
 
+    @classmethod
+    def from_samples(cls, samples, config, dist=False):
+        """Raw samples already in memory (a generator's output: ``x`` = all node feature
+        columns, ``y`` = all graph feature columns, ``pos``) -> the same normalise + process
+        pipeline as raw files (the reference's in-script ``transform_input_to_data_object_base``
+        datasets, e.g. ``examples/ising_model/train_ising.py``).  With ``dist`` each rank
+        passes its own shard and the min/max normalisation is reduced over ranks."""
+        from .lsms import RawDataLoader
+        from .serialized import SerializedDataLoader
+
+        self = cls.__new__(cls)
+        AbstractBaseDataset.__init__(self)
+        ds = dict(config["Dataset"])
+        ds.setdefault("format", "unit_test")
+        ds.setdefault("path", {})
+        loader = RawDataLoader(ds, dist=dist)
+        loader.dataset_list = [loader.scale_features_by_num_nodes(list(samples))]
+        loader.normalize_dataset()
+        self.minmax_node_feature = loader.minmax_node_feature
+        self.minmax_graph_feature = loader.minmax_graph_feature
+        self.dataset = SerializedDataLoader(config, dist=dist).process(loader.dataset_list[0])
+        return self
+
     @staticmethod
     def _collect(loader):
         for split, raw_path in loader.path_dictionary.items():
             files = sorted(f for f in os.listdir(raw_path) if f != ".DS_Store")
             ds = [loader._read(os.path.join(raw_path, f)) for f in files
                   if os.path.isfile(os.path.join(raw_path, f))]
+            ds = [d for d in ds if d is not None]
             loader.dataset_list.append(loader.scale_features_by_num_nodes(ds))
             loader.serial_data_name_list.append(split)
 

@@ -31,8 +31,16 @@ def dataset_loading_and_splitting(config):
 
 
 def create_dataloaders(trainset, valset, testset, batch_size, train_sampler_shuffle=True, val_sampler_shuffle=True,
-                       test_sampler_shuffle=True, group=None, oversampling=False, num_samples=None):
+                       test_sampler_shuffle=True, group=None, oversampling=False, num_samples=None, local=False):
+    """``local=True``: every rank already holds its own shard (multidataset subsets), so
+    the samplers shuffle the local data without sharding it again across ranks."""
     ns = num_samples or (None, None, None)
+    if local:
+        from .loader import _ShuffleSampler
+
+        return tuple(GraphDataLoader(ds, batch_size, sampler=_ShuffleSampler(len(ds), sh))
+                     for ds, sh in ((trainset, train_sampler_shuffle), (valset, val_sampler_shuffle),
+                                    (testset, test_sampler_shuffle)))
     tr = GraphDataLoader(trainset, batch_size, sampler=make_sampler(trainset, train_sampler_shuffle, group,
                                                                     oversampling, ns[0]))
     va = GraphDataLoader(valset, batch_size, sampler=make_sampler(valset, val_sampler_shuffle, group, oversampling,

@@ -112,37 +112,99 @@ def read_lsms(filepath, node_feature_dim, node_feature_col, graph_feature_dim, g
 
 
 def read_cfg(filepath, node_feature_dim, node_feature_col, graph_feature_dim, graph_feature_col):
-    """Minimal AtomEye extended-CFG reader (positions, per-atom auxiliary columns, energy comment)."""
+    """AtomEye extended-CFG reader (reference ``utils/datasets/cfgdataset.py:31-89`` via
+    ``ase.io.cfg.read_cfg``; ase is not available here, the format is parsed directly).
+
+    Layout: ``Number of particles = N``; ``A = <scale> Angstrom``; ``H0(i,j) = v``;
+    ``.NO_VELOCITY.``; ``entry_count``; ``auxiliary[k] = name``; then per species a mass
+    line, a symbol line and that species' rows ``s1 s2 s3 aux...`` (reduced coordinates).
+    Returns x = [Z, mass, aux columns...] (the reference's node matrix ``numbers, masses,
+    c_peratom, fx, fy, fz``), cartesian ``pos = s @ (A * H0)``, the cell, and ``y`` from
+    the sibling ``.bulk`` file's graph columns when it exists (else the ``# energy``
+    comment, else empty)."""
+    from .elements import atomic_number
+
+    if not filepath.endswith(".cfg"):
+        return None  # companion files (.bulk) and anything else in the directory
     with open(filepath) as f:
         lines = [l.strip() for l in f if l.strip()]
-    n = int(lines[0].split("=")[1])
+    n = None
+    scale = 1.0
     H = np.zeros((3, 3))
-    aux = []
-    energy = 0.0
-    body = []
-    for l in lines[1:]:
-        if l.startswith("H0("):
-            k = l.split("=")[0].strip()
-            i, j = int(k[3]) - 1, int(k[5]) - 1
+    n_aux = 0
+    energy = None
+    mass, z = 0.0, 0
+    rows = []
+    for l in lines:
+        key = l.split("=")[0].strip()
+        if key.startswith("Number of particles"):
+            n = int(l.split("=")[1].split()[0])
+        elif key == "A":
+            scale = float(l.split("=")[1].split()[0])
+        elif key.startswith("H0("):
+            i, j = int(key[3]) - 1, int(key[5]) - 1
             H[i, j] = float(l.split("=")[1].split()[0])
-        elif l.startswith("auxiliary["):
-            aux.append(l.split("=")[1].strip())
-        elif l.startswith("#") and "energy" in l.lower():
-            energy = float(l.split("=")[-1])
-        elif l[0].isdigit() or l[0] == "-" or l[0] == ".":
-            body.append(l.split())
-    rows = [r for r in body if len(r) >= 3 + len(aux)]
-    frac = np.array([[float(v) for v in r[:3]] for r in rows[:n]])
-    pos = frac @ H
-    extra = np.array([[float(v) for v in r[3:]] for r in rows[:n]]) if aux else np.zeros((n, 0))
-    cols = np.concatenate([np.zeros((n, 1)), np.zeros((n, 1)), pos, extra], axis=1)
-    xs = []
-    for item in range(len(node_feature_dim)):
-        for ic in range(node_feature_dim[item]):
-            xs.append(cols[:, node_feature_col[item] + ic])
-    x = np.stack(xs, 1) if xs else np.zeros((n, 0))
+        elif key.startswith("auxiliary["):
+            n_aux += 1
+        elif key in ("entry_count", "R", "eta") or key.startswith((".", "Transform(")):
+            continue
+        elif l.startswith("#"):
+            if "energy" in l.lower() and "=" in l:
+                energy = float(l.split("=")[-1])
+        else:
+            tok = l.split()
+            if len(tok) == 1:
+                try:
+                    mass = float(tok[0])
+                except ValueError:
+                    z = atomic_number(tok[0])
+                continue
+            if len(tok) >= 3 + n_aux:
+                rows.append([float(z), mass] + [float(v) for v in tok[:3 + n_aux]])
+    assert n is not None and len(rows) == n, f"{filepath}: expected {n} atoms, parsed {len(rows)}"
+    arr = np.asarray(rows, dtype=np.float64)
+    cell = H * scale
+    pos = arr[:, 2:5] @ cell
+    x = np.concatenate([arr[:, :2], arr[:, 5:]], 1)
+    bulk = os.path.splitext(filepath)[0] + ".bulk"
+    gf = []
+    if os.path.exists(bulk):
+        with open(bulk) as f:
+            vals = f.readline().split()
+        for item in range(len(graph_feature_dim)):
+            for ic in range(graph_feature_dim[item]):
+                gf.append(float(vals[graph_feature_col[item] + ic]))
+    elif energy is not None:
+        gf = [energy]
     return Graph(x=torch.tensor(x, dtype=torch.float32), pos=torch.tensor(pos, dtype=torch.float32),
-                 y=torch.tensor([energy], dtype=torch.float32), cell=torch.tensor(H, dtype=torch.float32))
+                 y=torch.tensor(gf, dtype=torch.float32), cell=torch.tensor(cell, dtype=torch.float32),
+                 pbc=torch.tensor([True, True, True]))
+
+
+def write_cfg(filepath, numbers, masses, frac, cell, aux=None, aux_names=(), energy=None):
+    """Write an extended CFG file (species-grouped, reduced coordinates) that ``read_cfg``
+    and AtomEye/ase read; ``aux`` [N, K] per-atom auxiliary columns."""
+    from .elements import element_symbol
+
+    numbers = np.asarray(numbers)
+    aux = np.zeros((len(numbers), 0)) if aux is None else np.asarray(aux)
+    with open(filepath, "w") as f:
+        f.write(f"Number of particles = {len(numbers)}\n")
+        if energy is not None:
+            f.write(f"# energy = {energy:.10f}\n")
+        f.write("A = 1.0 Angstrom (basic length-scale)\n")
+        for i in range(3):
+            for j in range(3):
+                f.write(f"H0({i + 1},{j + 1}) = {cell[i][j]:.10f} A\n")
+        f.write(".NO_VELOCITY.\n")
+        f.write(f"entry_count = {3 + aux.shape[1]}\n")
+        for k, name in enumerate(aux_names):
+            f.write(f"auxiliary[{k}] = {name}\n")
+        for zz in sorted(set(numbers.tolist())):
+            sel = np.nonzero(numbers == zz)[0]
+            f.write(f"{float(masses[sel[0]]):.6f}\n{element_symbol(int(zz))}\n")
+            for i in sel:
+                f.write(" ".join(f"{v:.10f}" for v in list(frac[i]) + list(aux[i])) + "\n")
 
 
 def read_xyz(filepath, node_feature_dim=(), node_feature_col=(), graph_feature_dim=(1,), graph_feature_col=(0,)):
@@ -249,6 +311,7 @@ class RawDataLoader:
                     for sub in sorted(os.listdir(full)):
                         if os.path.isfile(os.path.join(full, sub)):
                             dataset.append(self._read(os.path.join(full, sub)))
+            dataset = [d for d in dataset if d is not None]  # readers skip files of other kinds
             dataset = self.scale_features_by_num_nodes(dataset)
             fname = self.raw_dataset_name + (".pkl" if split == "total" else f"_{split}.pkl")
             self.dataset_list.append(dataset)

@@ -8,8 +8,13 @@ optional resume -> ``train_validate_test`` -> ``save_model`` -> timers.
 On a GPU the splits are moved into HBM (``DeviceGraphStore``) and training
 batches run through the hipGraph-captured ``TrainStep`` (set
 ``HYDRAGNN_CAPTURE=0`` for eager, ``HYDRAGNN_DEVICE_DATA=0`` for the host
-loader path).  Force training (``compute_grad_energy``) uses the eager
-double-backward path.
+loader path).  Force training (``compute_grad_energy``) captures the double
+backward too (energy + force loss masked over the padded bucket).
+
+``train_model(config, train_loader, val_loader, test_loader)`` is the same pipeline
+from loaders the caller built (the reference examples' low-level sequence
+``update_config -> create_model_config -> get_distributed_model -> select_optimizer ->
+train_validate_test -> save_model``, e.g. ``examples/ising_model/train_ising.py``).
 """
 import json
 import os
@@ -56,6 +61,16 @@ def _(config: dict, use_deepspeed=False):
     setup_log(get_log_name_config(config))
     setup_ddp()
     train_loader, val_loader, test_loader = dataset_loading_and_splitting(config=config)
+    return train_model(config, train_loader, val_loader, test_loader)
+
+
+def train_model(config, train_loader, val_loader, test_loader, log_name=None):
+    """Train from prebuilt host loaders (any dataset class: serialized, pickle, columnar,
+    DistDataset); ``update_config`` is applied here.  ``log_name`` defaults to the
+    config-derived name (configs without a Dataset section must pass one).  Returns the
+    (DDP-wrapped) model."""
+    verbosity = config["Verbosity"]["level"]
+    setup_ddp()
     config = update_config(config, train_loader, val_loader, test_loader)
     vis = config.get("Visualization", {})
     plot_init_solution = vis.get("plot_init_solution", False)
@@ -69,7 +84,7 @@ def _(config: dict, use_deepspeed=False):
 
     set_precision(nn_cfg["Training"].get("precision", "fp32"))
     model = create_model_config(config=nn_cfg, verbosity=verbosity)
-    log_name = get_log_name_config(config)
+    log_name = log_name or get_log_name_config(config)
     model = get_distributed_model(model, verbosity, sync_batch_norm=nn_cfg["Architecture"].get("SyncBatchNorm", False),
                                   find_unused_parameters=True)
     optimizer = select_optimizer(model, nn_cfg["Training"]["Optimizer"])

@@ -279,3 +279,32 @@ def merge_config(a, b):
         else:
             result[k] = copy.deepcopy(v)
     return result
+
+
+def merge_pna_deg(deg_list):
+    """Merge per-dataset PNA in-degree histograms of different lengths into one (reference
+    ``examples/multidataset/train.py:214-232``, multi-dataset setup C21): each histogram is
+    resampled onto the shortest length with a cubic interpolating spline over [0, 1] and the
+    resampled histograms are summed (truncated to int64)."""
+    from scipy.interpolate import make_interp_spline
+
+    degs = [np.asarray(d, dtype=np.float64) for d in deg_list if d is not None]
+    assert degs, "merge_pna_deg: no histograms"
+    mlen = min(len(d) for d in degs)
+    out = np.zeros(mlen)
+    grid = np.linspace(0, 1, num=mlen)
+    for d in degs:
+        k = min(3, len(d) - 1)
+        out += make_interp_spline(np.linspace(0, 1, num=len(d)), d, k=k)(grid) if k > 0 else d[:mlen]
+    return out.astype(np.int64).tolist()
+
+
+def proportional_process_list(ndata_list, world_size):
+    """Ranks per dataset in proportion to dataset sizes (ceil, then the largest share gives
+    back the excess) — the reference's multidataset rank assignment (``train.py:206-212``)."""
+    nd = np.asarray(ndata_list, dtype=np.float64)
+    pl = np.ceil(nd / nd.sum() * world_size).astype(np.int64)
+    imax = int(np.argmax(pl))
+    pl[imax] -= int(pl.sum()) - world_size
+    assert pl.min() >= 1, f"not enough ranks ({world_size}) for {len(nd)} datasets"
+    return pl.tolist()

@@ -107,3 +107,49 @@ def test_lsms_raw_dataset(tmp_path):
     d = ds[0]
     assert d.edge_index.shape[0] == 2 and d.y.shape[1] == 1 and d.x.shape[1] == 1
     assert float(d.edge_attr.max()) <= 1.0 + 1e-6
+
+
+def test_cfg_roundtrip_and_bulk(tmp_path):
+    """Extended-CFG writer/reader (reference CFGDataset via ase.io.cfg): species blocks,
+    reduced coordinates, aux columns, .bulk graph features; non-.cfg files are skipped."""
+    import numpy as np
+
+    from hydragnn_amd.data.lsms import read_cfg, write_cfg
+
+    rng = np.random.default_rng(0)
+    cell = np.diag([5.0, 6.0, 7.0]) + 0.3 * np.eye(3)[[1, 2, 0]]
+    numbers = np.array([28, 41, 28, 28, 41])
+    masses = np.array([58.693, 92.906, 58.693, 58.693, 92.906])
+    frac = rng.random((5, 3))
+    aux = rng.normal(size=(5, 4))
+    write_cfg(str(tmp_path / "a.cfg"), numbers, masses, frac, cell, aux, ("c", "fx", "fy", "fz"), energy=-3.5)
+    (tmp_path / "a.bulk").write_text("5 -3.5 181.25\n")
+    d = read_cfg(str(tmp_path / "a.cfg"), [1, 1, 1, 3], [0, 1, 2, 3], [1], [2])
+    order = np.argsort(numbers, kind="stable")  # the writer groups atoms by species
+    assert torch.allclose(d.x[:, 0], torch.tensor(numbers[order], dtype=torch.float32))
+    assert torch.allclose(d.x[:, 1], torch.tensor(masses[order], dtype=torch.float32))
+    assert torch.allclose(d.x[:, 2:], torch.tensor(aux[order], dtype=torch.float32), atol=1e-6)
+    assert torch.allclose(d.pos, torch.tensor(frac[order] @ cell, dtype=torch.float32), atol=1e-5)
+    assert float(d.y[0]) == 181.25 and torch.allclose(d.cell, torch.tensor(cell, dtype=torch.float32))
+    assert read_cfg(str(tmp_path / "a.bulk"), [1], [0], [1], [0]) is None
+
+
+def test_xyz_reader_symbols(tmp_path):
+    from hydragnn_amd.data.lsms import read_xyz
+
+    (tmp_path / "m.xyz").write_text("3\n-1.5 2.0\nO 0 0 0\nH 0.96 0 0\nH -0.24 0.93 0\n")
+    d = read_xyz(str(tmp_path / "m.xyz"), [1], [0], [1], [1])
+    assert d.x[:, 0].tolist() == [8.0, 1.0, 1.0] and float(d.y[0]) == 2.0
+
+
+def test_merge_pna_deg_and_process_list():
+    from hydragnn_amd.utils.config_utils import merge_pna_deg, proportional_process_list
+
+    a = [0, 10, 40, 30, 10, 5]
+    # a single histogram is reproduced up to the reference's int truncation of the spline values
+    assert all(abs(x - y) <= 1 for x, y in zip(merge_pna_deg([a]), a))
+    m = merge_pna_deg([a, [0, 20, 60, 20]])
+    assert len(m) == 4 and m[0] == 0 and sum(m) > 0
+    assert proportional_process_list([100, 100], 3) == [1, 2]
+    assert proportional_process_list([1000, 10, 10], 8) == [6, 1, 1]
+    assert sum(proportional_process_list([5, 7, 11], 16)) == 16

@@ -12,15 +12,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EX = os.path.join(ROOT, "examples")
 
 
-def _run(script, args, tmp_path, nproc=1, timeout=600):
+def _run(script, args, tmp_path, nproc=1, timeout=300):
     env = dict(os.environ, HYDRAGNN_DEVICE_DATA="0", OMP_NUM_THREADS="2")
     if nproc == 1:
         cmd = [sys.executable, os.path.join(EX, script), "--workdir", str(tmp_path)] + args
         env["HYDRAGNN_MASTER_PORT"] = str(29000 + (abs(hash(script + str(args))) % 2000))
     else:
+        # torchrun's MASTER_PORT must win: an inherited HYDRAGNN_MASTER_PORT (conftest gives each
+        # xdist worker one, and the worker may hold a process group on it) would override it
+        env.pop("HYDRAGNN_MASTER_PORT", None)
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", f"--master-port={31000 + abs(hash(script)) % 2000}",
-               os.path.join(EX, script)] + args
+               os.path.join(EX, script), "--workdir", str(tmp_path)] + args
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r.stdout
@@ -80,3 +83,40 @@ def test_multibranch_task_parallel_three_ranks(tmp_path):
 def test_lsms(tmp_path):
     r = _result(_run("lsms/lsms.py", ["--num_samples", "300", "--num_epoch", "2"], tmp_path))
     assert len(r["task_errors"]) == 3
+
+
+@pytest.mark.parametrize("fmt", ["pickle", "columnar"])
+def test_ising_model(fmt, tmp_path):
+    """Reference ``examples/ising_model``: generated configurations -> raw pipeline ->
+    pickle / columnar stores -> train_model."""
+    r = _result(_run("ising_model/train_ising.py", ["--histogram_cutoff", "8", "--num_epoch", "1", "--format", fmt],
+                     tmp_path))
+    assert len(r["task_errors"]) == 2 and r["test_error"] == r["test_error"]
+
+
+def test_ising_model_ddstore_two_ranks(tmp_path):
+    _run("ising_model/train_ising.py", ["--histogram_cutoff", "8", "--num_epoch", "1", "--ddstore"], tmp_path,
+         nproc=2)
+
+
+@pytest.mark.parametrize("cfg,fmt", [("NiNb_EAM_multitask.json", "--pickle"),
+                                     ("NiNb_EAM_bulk_multitask.json", "--adios")])
+def test_eam(cfg, fmt, tmp_path):
+    """Reference ``examples/eam``: EAM CFG files -> CFGDataset -> serialized/columnar store."""
+    r = _result(_run("eam/eam.py", ["--inputfile", cfg, "--num_samples", "40", "--num_epoch", "1", fmt], tmp_path))
+    assert len(r["task_errors"]) == (2 if "bulk" not in cfg else 3)
+
+
+def test_multidataset_single_rank(tmp_path):
+    r = _result(_run("multidataset/train.py", ["--multi_model_list", "ANI1x", "--prepare_samples", "40",
+                                               "--num_epoch", "1"], tmp_path))
+    assert r["datasets"] == ["ANI1x"]
+
+
+def test_multidataset_three_ranks_and_ddstore(tmp_path):
+    """Reference ``examples/multidataset --multi``: ranks split over two stores in proportion
+    to their sizes, merged PNA histograms; then the same stores through ``--ddstore``."""
+    _run("multidataset/train.py", ["--multi_model_list", "ANI1x,QM7-X", "--prepare_samples", "40", "--num_epoch", "1"],
+         tmp_path, nproc=3)
+    _run("multidataset/train.py", ["--multi_model_list", "ANI1x,QM7-X", "--num_epoch", "1", "--ddstore"], tmp_path,
+         nproc=2)
