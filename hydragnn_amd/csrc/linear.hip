@@ -61,18 +61,15 @@ __device__ __forceinline__ void wg_load(const float* __restrict__ base, int ld, 
 }
 
 // part layout: [S][O*I + O]   (dW partial, then db partial)
+// smem: 2 buffers x (dY, X) x 32 rows x 64 floats = 32 KB; reused for the wave fold afterwards
 template <bool VY, bool VX>
-__global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restrict__ dY, int ldy,
-                                                            const float* __restrict__ X, int ldx,
-                                                            float* __restrict__ part, int with_bias, int M, int O,
-                                                            int I, int rows_per_block, int tiles_i) {
-  // 2 buffers x (dY, X) x 32 rows x 64 floats = 32 KB; reused for the wave fold afterwards
-  __shared__ float4 smem[2 * 2 * kWC * 16];
+__device__ __forceinline__ void wgrad_partial_body(float4* smem, const float* __restrict__ dY, int ldy,
+                                                   const float* __restrict__ X, int ldx, float* __restrict__ part,
+                                                   int with_bias, int M, int O, int I, int rows_per_block,
+                                                   int tiles_i, int tile, int s) {
   float4* Ys = smem;                  // [2][kWC][16]
   float4* Xs = smem + 2 * kWC * 16;   // [2][kWC][16]
-  const int tile = blockIdx.x;
   const int to0 = (tile / tiles_i) * kWT, ti0 = (tile % tiles_i) * kWT;
-  const int s = blockIdx.y;
   const int r0 = s * rows_per_block, r1 = min(M, r0 + rows_per_block);
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
@@ -169,6 +166,16 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
   }
 }
 
+template <bool VY, bool VX>
+__global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restrict__ dY, int ldy,
+                                                            const float* __restrict__ X, int ldx,
+                                                            float* __restrict__ part, int with_bias, int M, int O,
+                                                            int I, int rows_per_block, int tiles_i) {
+  __shared__ float4 smem[2 * 2 * kWC * 16];
+  wgrad_partial_body<VY, VX>(smem, dY, ldy, X, ldx, part, with_bias, M, O, I, rows_per_block, tiles_i, blockIdx.x,
+                             blockIdx.y);
+}
+
 // out[j] = sum_s part[s * ld + j]; block = 64 outputs x 16 waves splitting s; fixed order
 constexpr int kSpWaves = 16;
 __global__ void __launch_bounds__(64 * kSpWaves) sum_partials_kernel(const float* __restrict__ part,
@@ -250,8 +257,182 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
   return {dW, db};
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Grouped (deferred) weight gradients: every tall linear of a backward pass records
+// (dY, X, W.grad, b.grad) instead of launching its own wgrad pair; after backward ONE
+// partial launch covers all of them (each workgroup looks up its problem in the kernarg
+// table) and ONE reduce launch sums the slab partials in a fixed order and writes or
+// accumulates into the gradient tensors.  Replaces 2 launches per linear (~33 pairs per
+// GPS+PNAPlus step) with 2 per step, and the merged grid fills the chip.
+constexpr int kWgMaxP = 24;
+
+struct WgProb {
+  const float* dy;
+  const float* x;
+  float* dw;
+  float* db;  // nullptr: no bias
+  int64_t part_off;  // float offset of this problem's [S][ld] partials in the workspace
+  int ldy, ldx, M, O, I, tiles_i, S, rpb;
+  int wg0;    // first partial-kernel workgroup of this problem
+  int rwg0;   // first reduce-kernel workgroup
+  int vec;    // bit0: dY float4 path, bit1: X float4 path
+  int accumulate;
+};
+
+struct WgArgs {
+  WgProb p[kWgMaxP];
+  float* ws;  // slab partials of all problems
+  int n;
+};
+
+typedef __attribute__((address_space(4))) const WgArgs KWgArgs;
+typedef __attribute__((address_space(4))) const WgProb KWgProb;
+
+__device__ __forceinline__ int wg_find(KWgArgs* A, int b, bool reduce) {
+  int pi = 0;
+  for (int j = 1; j < A->n; ++j)
+    if (b >= (reduce ? A->p[j].rwg0 : A->p[j].wg0)) pi = j;
+  return pi;
+}
+
+__global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
+  __shared__ float4 smem[2 * 2 * kWC * 16];
+  KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = blockIdx.x;
+  const int pi = wg_find(A, b, false);
+  KWgProb& P = A->p[pi];
+  const int local = b - P.wg0;
+  const int tiles = ((P.O + kWT - 1) / kWT) * P.tiles_i;
+  const int tile = local % tiles, s = local / tiles;
+  float* part = A->ws + P.part_off;
+  const int wb = P.db != nullptr ? 1 : 0;
+  switch (P.vec) {
+    case 3: wgrad_partial_body<true, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+    case 1: wgrad_partial_body<true, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+    case 2: wgrad_partial_body<false, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+    default: wgrad_partial_body<false, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+  }
+}
+
+// reduce: 256 outputs per workgroup, 4 waves x 64 lanes; wave w sums slabs w, w+4, ... in a
+// fixed order, the 4 wave sums are folded in a fixed order through LDS.
+__global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
+  __shared__ float red[4][64];
+  KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = blockIdx.x;
+  const int pi = wg_find(A, b, true);
+  KWgProb& P = A->p[pi];
+  const float* part = A->ws + P.part_off;
+  const int64_t nw = (int64_t)P.O * P.I;
+  const int64_t n = nw + (P.db != nullptr ? P.O : 0);
+  const int64_t ld = nw + P.O;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int S = P.S;
+  for (int sub = 0; sub < 4; ++sub) {  // 4 x 64 outputs per workgroup
+    const int64_t j = (int64_t)(b - P.rwg0) * 256 + sub * 64 + lane;
+    float a0 = 0.f, a1 = 0.f;
+    if (j < n) {
+      int s = w;
+      for (; s + 4 < S; s += 8) {
+        a0 += part[(int64_t)s * ld + j];
+        a1 += part[(int64_t)(s + 4) * ld + j];
+      }
+      if (s < S) a0 += part[(int64_t)s * ld + j];
+    }
+    red[w][lane] = a0 + a1;
+    __syncthreads();
+    if (w == 0 && j < n) {
+      const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      float* dst = j < nw ? P.dw + j : P.db + (j - nw);
+      *dst = P.accumulate ? *dst + v : v;
+    }
+    __syncthreads();
+  }
+}
+
+static int wgrad_slabs(int64_t M, int tiles) {
+  int S = (int)std::min<int64_t>(ceil_div(M, kWC), std::max(1, 512 / tiles));
+  return std::max(S, 1);
+}
+
+void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList dWs, at::TensorList dbs,
+                          at::IntArrayRef accumulate) {
+  const int64_t n = (int64_t)dYs.size();
+  HY_CHECK(Xs.size() == (size_t)n && dWs.size() == (size_t)n && dbs.size() == (size_t)n &&
+               accumulate.size() == (size_t)n,
+           "linear_wgrad_grouped: list lengths differ");
+  for (int64_t c0 = 0; c0 < n; c0 += kWgMaxP) {
+    const int cnt = (int)std::min<int64_t>(kWgMaxP, n - c0);
+    WgArgs a{};
+    a.n = cnt;
+    std::vector<at::Tensor> keep;
+    int64_t part_total = 0;
+    int wg = 0, rwg = 0;
+    for (int q = 0; q < cnt; ++q) {
+      const int64_t k = c0 + q;
+      auto dY = dYs[k].stride(1) == 1 ? dYs[k] : dYs[k].contiguous();
+      auto X = Xs[k].stride(1) == 1 ? Xs[k] : Xs[k].contiguous();
+      keep.push_back(dY);
+      keep.push_back(X);
+      HY_CHECK(dY.is_cuda() && X.is_cuda() && dY.scalar_type() == at::kFloat && X.scalar_type() == at::kFloat,
+               "linear_wgrad_grouped: fp32 GPU operands");
+      HY_CHECK(dY.dim() == 2 && X.dim() == 2 && dY.size(0) == X.size(0), "wgrad expects dY [M,O], X [M,I]");
+      const int64_t M = dY.size(0);
+      const int O = (int)dY.size(1), I = (int)X.size(1);
+      const auto& dW = dWs[k];
+      HY_CHECK(dW.is_contiguous() && dW.scalar_type() == at::kFloat && dW.numel() == (int64_t)O * I,
+               "linear_wgrad_grouped: dW must be a contiguous fp32 [O, I]");
+      const bool hb = dbs[k].defined() && dbs[k].numel() > 0;
+      if (hb)
+        HY_CHECK(dbs[k].is_contiguous() && dbs[k].numel() == O && dbs[k].scalar_type() == at::kFloat,
+                 "linear_wgrad_grouped: db must be a contiguous fp32 [O]");
+      HY_CHECK(M > 0, "linear_wgrad_grouped: empty problem");
+      WgProb& P = a.p[q];
+      P.dy = dY.data_ptr<float>();
+      P.x = X.data_ptr<float>();
+      P.dw = dW.data_ptr<float>();
+      P.db = hb ? dbs[k].data_ptr<float>() : nullptr;
+      P.ldy = (int)dY.stride(0);
+      P.ldx = (int)X.stride(0);
+      P.M = (int)M;
+      P.O = O;
+      P.I = I;
+      P.tiles_i = ceil_div(I, kWT);
+      const int tiles = ceil_div(O, kWT) * P.tiles_i;
+      int S = wgrad_slabs(M, tiles);
+      int rpb = (int)((M + S - 1) / S);
+      rpb = ceil_div(rpb, kWC) * kWC;
+      S = ceil_div(M, rpb);
+      P.S = S;
+      P.rpb = rpb;
+      P.part_off = part_total;
+      part_total += (int64_t)S * ((int64_t)O * I + O);
+      P.wg0 = wg;
+      wg += tiles * S;
+      P.rwg0 = rwg;
+      rwg += ceil_div((int64_t)O * I + (hb ? O : 0), 256);
+      auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+      const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
+      const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);
+      P.vec = (vy ? 1 : 0) | (vx ? 2 : 0);
+      P.accumulate = accumulate[k] ? 1 : 0;
+    }
+    auto ws = at::empty({part_total}, dYs[c0].options());
+    a.ws = ws.data_ptr<float>();
+    wgrad_grouped_partial_kernel<<<wg, 256, 0, stream()>>>(a);
+    wgrad_grouped_reduce_kernel<<<rwg, 256, 0, stream()>>>(a);
+  }
+}
+
 }  // namespace hy
 
-TORCH_LIBRARY_FRAGMENT(hydra, m) { m.def("linear_wgrad(Tensor dY, Tensor X, bool with_bias) -> (Tensor, Tensor)"); }
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("linear_wgrad(Tensor dY, Tensor X, bool with_bias) -> (Tensor, Tensor)");
+  m.def("linear_wgrad_grouped(Tensor[] dYs, Tensor[] Xs, Tensor(a!)[] dWs, Tensor(b!)[] dbs, int[] accumulate) -> ()");
+}
 
-TORCH_LIBRARY_IMPL(hydra, CUDA, m) { m.impl("linear_wgrad", hy::linear_wgrad); }
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("linear_wgrad", hy::linear_wgrad);
+  m.impl("linear_wgrad_grouped", hy::linear_wgrad_grouped);
+}

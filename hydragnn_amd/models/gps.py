@@ -20,6 +20,7 @@ from ..ops.attention import segment_attention
 from ..ops.linear import ACT_RELU, linear
 from ..ops.norm import norm_add
 from ..ops.rng import dropout as rng_dropout, new_salt
+from ..ops.streams import Fork
 from .layers import BatchNorm, Linear
 
 
@@ -123,12 +124,16 @@ class GPSConv(nn.Module):
         nv = ctx.get("num_valid")
         tr = self.training
         hs = []
+        # the attention branch runs on a side stream, concurrently with the local MPNN
+        # (forward AND backward; ops/streams.py)
+        with Fork(inv, ctx.attn_seg_id, ctx.attn_seg_ptr) as fork:
+            h = self.attn(inv, ctx.attn_seg_id, ctx.attn_seg_ptr)
+            h_att = norm_add(h, self.norm2, nv, residual=inv, p=self.dropout, salt=self._salts[1], training=tr)
         if self.conv is not None:
             h, equiv = self.conv(inv, equiv, ctx)
             # BN1(dropout(h) + x): one fused launch each way on the GPU
             hs.append(norm_add(h, self.norm1, nv, residual=inv, p=self.dropout, salt=self._salts[0], training=tr))
-        h = self.attn(inv, ctx.attn_seg_id, ctx.attn_seg_ptr)
-        hs.append(norm_add(h, self.norm2, nv, residual=inv, p=self.dropout, salt=self._salts[1], training=tr))
+        hs.append(fork.join(h_att))
         out = hs[0] if len(hs) == 1 else hs[0] + hs[1]
         lin1, act, _, lin2, _ = self.mlp
         if isinstance(act, nn.ReLU):  # bias + ReLU in the GEMM epilogue

@@ -87,11 +87,90 @@ class _MM(torch.autograd.Function):
         return (None, None, db if want_b else None, dres, *grads)
 
 
+# ---- deferred weight gradients -------------------------------------------------------
+# Inside ``deferred_wgrad()`` (the training engine wraps its backward in it) the tall
+# linears do not launch their own split-K weight-gradient pair: they record
+# (dY, X, W, b) and return no dW/db; on exit ONE grouped launch pair computes every
+# recorded weight gradient and writes / accumulates it into ``W.grad`` / ``b.grad``
+# (csrc/linear.hip, ``linear_wgrad_grouped``), then runs the parameters'
+# post-accumulate-grad hooks (the bucketed all-reduce of the captured step).
+_defer = {"on": False, "items": []}
+
+
+def _can_defer(W, b):
+    return _defer["on"] and not torch.is_grad_enabled() and isinstance(W, torch.nn.Parameter) and \
+        (b is None or isinstance(b, torch.nn.Parameter))
+
+
+class deferred_wgrad:
+    def __init__(self, enabled=True):
+        self.enabled = enabled and os.environ.get("HYDRA_DEFER_WGRAD", "1") == "1"
+
+    def __enter__(self):
+        self.prev = _defer["on"]
+        _defer["on"] = self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        _defer["on"] = self.prev
+        if exc[0] is None:
+            flush_deferred_wgrads()
+        else:
+            _defer["items"].clear()
+        return False
+
+
+def flush_deferred_wgrads():
+    items, _defer["items"] = _defer["items"], []
+    if not items:
+        return
+    # one launch covers problems with distinct outputs; a parameter recorded twice (shared
+    # weights) goes to a later launch so its accumulation is ordered
+    rounds = []
+    for it in items:
+        for r in rounds:
+            if all(it[2] is not o[2] for o in r):
+                r.append(it)
+                break
+        else:
+            rounds.append([it])
+    touched = []
+    for r in rounds:
+        dys, xs, dws, dbs, acc = [], [], [], [], []
+        for dy, x, W, b in r:
+            a = W.grad is not None
+            if W.grad is None:
+                W.grad = torch.empty_like(W)
+            if b is not None and b.grad is None:
+                b.grad = torch.empty_like(b)
+                assert not a, "bias grad missing while weight grad exists"
+            dys.append(dy)
+            xs.append(x)
+            dws.append(W.grad)
+            dbs.append(b.grad if b is not None else torch.empty(0, device=dy.device))
+            acc.append(1 if a else 0)
+            touched += [W] + ([b] if b is not None else [])
+        _native.ops().linear_wgrad_grouped(dys, xs, dws, dbs, acc)
+    seen = set()
+    for p in touched:
+        if id(p) not in seen:
+            seen.add(id(p))
+            _run_post_hooks(p)
+
+
+def _run_post_hooks(p):
+    hooks = getattr(p, "_post_accumulate_grad_hooks", None)
+    if hooks:
+        for h in hooks.values():
+            h(p)
+
+
 class _TallLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.params = (W, b)
         return F.linear(x, W, b)
 
     @staticmethod
@@ -99,6 +178,10 @@ class _TallLinear(torch.autograd.Function):
         x, W = ctx.saved_tensors
         dx = dy @ W if ctx.needs_input_grad[0] else None
         dW = db = None
+        Wp, bp = ctx.params
+        if ctx.needs_input_grad[1] and (not ctx.has_b or ctx.needs_input_grad[2]) and _can_defer(Wp, bp):
+            _defer["items"].append((dy, x, Wp, bp))
+            return dx, None, None
         if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
             dW, db = _native.ops().linear_wgrad(dy, x, ctx.has_b)
             if not ctx.has_b:
@@ -116,6 +199,7 @@ class _TallLinearSum(torch.autograd.Function):
         ctx.save_for_backward(*xs, *ws)
         ctx.k = len(xs)
         ctx.has_b = b is not None
+        ctx.params = (b, tuple(ws))
         y = F.linear(xs[0], ws[0], b)
         for x, w in zip(xs[1:], ws[1:]):
             y = torch.addmm(y, x, w.t())
@@ -127,6 +211,14 @@ class _TallLinearSum(torch.autograd.Function):
         xs, ws = t[:ctx.k], t[ctx.k:]
         grads = []
         db = None
+        bp, wps = ctx.params
+        if all(ctx.needs_input_grad[2 + 2 * j] for j in range(ctx.k)) and \
+                (not ctx.has_b or ctx.needs_input_grad[0]) and all(_can_defer(w, None) for w in wps) and \
+                _can_defer(wps[0], bp) and len({id(w) for w in wps}) == len(wps):
+            for j, (x, w) in enumerate(zip(xs, ws)):
+                _defer["items"].append((dy, x, wps[j], bp if j == 0 else None))
+                grads += [dy @ w if ctx.needs_input_grad[1 + 2 * j] else None, None]
+            return (None, *grads)
         for j, (x, w) in enumerate(zip(xs, ws)):
             dx = dy @ w if ctx.needs_input_grad[1 + 2 * j] else None
             dW = None
@@ -149,6 +241,7 @@ class _EngineSumF32(_TallLinearSum):
         ctx.save_for_backward(*xs, *ws)
         ctx.k = len(xs)
         ctx.has_b = b is not None
+        ctx.params = (b, tuple(ws))
         return _native.ops().mm_fwd([_row_contig(x) for x in xs], [_row_contig(w) for w in ws], b, None, 0, 0)
 
 

@@ -204,13 +204,20 @@ class TrainStep:
         return self._backward_impl(loss, sync)
 
     def _backward_impl(self, loss, sync=True):
+        from ..ops.linear import deferred_wgrad
+
+        # tall-linear weight gradients are deferred and computed by one grouped launch pair
+        # at the end of backward (ops/linear.py); their grad hooks (bucket all-reduces) fire then
+        defer = self.sync is not None or self.flat_grads is not None
         if self.sync is not None:
             if sync:
                 self.sync.begin()
-            loss.backward()
+            with deferred_wgrad(defer):
+                loss.backward()
             self.sync.finish()
             return
-        loss.backward()
+        with deferred_wgrad(defer):
+            loss.backward()
         if self.flat_grads is not None:
             self.flat_grads.gather()
 

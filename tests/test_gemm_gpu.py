@@ -102,3 +102,30 @@ def test_mm_deterministic_split_k():
         linear(x, W).sum().backward()
         outs.append(W.grad.clone())
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+def test_wgrad_grouped_matches_torch():
+    """Grouped deferred weight gradients (csrc/linear.hip ``linear_wgrad_grouped``): several
+    problems of different shapes / strides in one launch pair, write and accumulate modes."""
+    import hydragnn_amd._native as nat
+
+    torch.manual_seed(11)
+    shapes = [(2311, 64, 64, True), (23105, 64, 7, True), (37, 5, 130, False), (2311, 192, 64, True),
+              (4000, 33, 66, False), (1, 3, 3, True)]
+    dys, xs, dws, dbs, acc, ref_w, ref_b = [], [], [], [], [], [], []
+    for k, (M, O, I, hb) in enumerate(shapes):
+        dy = torch.randn(M, O + 3, device=DEV)[:, 1:O + 1]  # strided (column-sliced) operand
+        x = torch.randn(M, I, device=DEV)
+        a = k % 2
+        dw = torch.randn(O, I, device=DEV) if a else torch.empty(O, I, device=DEV)
+        db = (torch.randn(O, device=DEV) if a else torch.empty(O, device=DEV)) if hb else torch.empty(0, device=DEV)
+        ref_w.append(dy.double().t() @ x.double() + (dw.double() if a else 0))
+        ref_b.append(dy.double().sum(0) + (db.double() if a else 0) if hb else None)
+        dys.append(dy), xs.append(x), dws.append(dw), dbs.append(db), acc.append(a)
+    nat.ops().linear_wgrad_grouped(dys, xs, dws, dbs, acc)
+    for k, (M, O, I, hb) in enumerate(shapes):
+        tol = dict(rtol=1e-4, atol=1e-3 * max(1.0, (M / 1000) ** 0.5))
+        torch.testing.assert_close(dws[k].double(), ref_w[k], **tol)
+        if hb:
+            torch.testing.assert_close(dbs[k].double(), ref_b[k], **tol)
+

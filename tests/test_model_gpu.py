@@ -112,3 +112,25 @@ def test_ci_pna_trajectory_cpu_vs_gpu_captured():
     d_gpu = max(abs(a - b) for a, b in zip(lc, lg))
     d_64 = max(abs(a - b) for a, b in zip(lc, l64))
     assert d_gpu <= 10 * d_64 + 1e-5 * scale, (d_gpu, d_64, lc, lg)
+
+
+def test_deferred_wgrad_grads_match_per_linear():
+    """GPS+PNAPlus parameter gradients with the deferred grouped weight-gradient launch
+    (ops/linear.deferred_wgrad) equal the per-linear split-K path."""
+    from hydragnn_amd.ops.linear import deferred_wgrad
+
+    samples = oc20_like(12, seed=5)
+    m1 = _model(samples).cuda()
+    m2 = copy.deepcopy(m1)
+    s = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
+    idx = list(range(12))
+    grads = []
+    for m, on in ((m1, False), (m2, True)):
+        b = s.batch(idx)
+        loss, _ = batch_loss(m, m(b), b)
+        with deferred_wgrad(on):
+            loss.backward()
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        torch.testing.assert_close(grads[1][n], grads[0][n], rtol=1e-4, atol=1e-5, msg=n)
