@@ -266,6 +266,7 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
 // accumulates into the gradient tensors.  Replaces 2 launches per linear (~33 pairs per
 // GPS+PNAPlus step) with 2 per step, and the merged grid fills the chip.
 constexpr int kWgMaxP = 24;
+constexpr int kWgMaxSlabs = 64;
 
 struct WgProb {
   const float* dy;
@@ -315,8 +316,10 @@ __global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
   }
 }
 
-// reduce: 256 outputs per workgroup, 4 waves x 64 lanes; wave w sums slabs w, w+4, ... in a
-// fixed order, the 4 wave sums are folded in a fixed order through LDS.
+// reduce: 64 outputs per workgroup; the 4 waves split the problem's slabs (wave w takes
+// slabs w, w+4, ...) with 8 independent accumulators each, so a wave keeps 8 coalesced
+// 256-byte loads in flight (the pass is latency-bound otherwise); the per-wave sums are
+// folded in a fixed order through LDS -> deterministic.
 __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
   __shared__ float red[4][64];
   KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -328,32 +331,24 @@ __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
   const int64_t n = nw + (P.db != nullptr ? P.O : 0);
   const int64_t ld = nw + P.O;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)(b - P.rwg0) * 64 + lane;
+  const int64_t jc = j < n ? j : n - 1;  // loads stay in range; result discarded
   const int S = P.S;
-  for (int sub = 0; sub < 4; ++sub) {  // 4 x 64 outputs per workgroup
-    const int64_t j = (int64_t)(b - P.rwg0) * 256 + sub * 64 + lane;
-    float a0 = 0.f, a1 = 0.f;
-    if (j < n) {
-      int s = w;
-      for (; s + 4 < S; s += 8) {
-        a0 += part[(int64_t)s * ld + j];
-        a1 += part[(int64_t)(s + 4) * ld + j];
-      }
-      if (s < S) a0 += part[(int64_t)s * ld + j];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s0 = w; s0 < S; s0 += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int s = s0 + 4 * u;
+      if (s < S) acc[u] += part[(int64_t)s * ld + jc];
     }
-    red[w][lane] = a0 + a1;
-    __syncthreads();
-    if (w == 0 && j < n) {
-      const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-      float* dst = j < nw ? P.dw + j : P.db + (j - nw);
-      *dst = P.accumulate ? *dst + v : v;
-    }
-    __syncthreads();
   }
-}
-
-static int wgrad_slabs(int64_t M, int tiles) {
-  int S = (int)std::min<int64_t>(ceil_div(M, kWC), std::max(1, 512 / tiles));
-  return std::max(S, 1);
+  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (w == 0 && j < n) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float* dst = j < nw ? P.dw + j : P.db + (j - nw);
+    *dst = P.accumulate ? *dst + v : v;
+  }
 }
 
 void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList dWs, at::TensorList dbs,
@@ -369,6 +364,17 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
     std::vector<at::Tensor> keep;
     int64_t part_total = 0;
     int wg = 0, rwg = 0;
+    // rows per slab: 256 when the merged grid still has >= 1024 workgroups, else halve
+    // (down to one 32-row LDS chunk) until it does
+    int rps = 256;
+    for (; rps > kWC; rps /= 2) {
+      int64_t tot = 0;
+      for (int q = 0; q < cnt; ++q) {
+        const auto& dY = dYs[c0 + q];
+        tot += (int64_t)ceil_div(dY.size(1), kWT) * ceil_div(Xs[c0 + q].size(1), kWT) * ceil_div(dY.size(0), rps);
+      }
+      if (tot >= 1024) break;
+    }
     for (int q = 0; q < cnt; ++q) {
       const int64_t k = c0 + q;
       auto dY = dYs[k].stride(1) == 1 ? dYs[k] : dYs[k].contiguous();
@@ -400,10 +406,9 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.I = I;
       P.tiles_i = ceil_div(I, kWT);
       const int tiles = ceil_div(O, kWT) * P.tiles_i;
-      int S = wgrad_slabs(M, tiles);
-      int rpb = (int)((M + S - 1) / S);
-      rpb = ceil_div(rpb, kWC) * kWC;
-      S = ceil_div(M, rpb);
+      // at most kWgMaxSlabs slabs per problem: the reduce pass reads S partial tiles
+      const int rpb = std::max(rps, ceil_div(ceil_div(M, kWgMaxSlabs), kWC) * kWC);
+      const int S = ceil_div(M, rpb);
       P.S = S;
       P.rpb = rpb;
       P.part_off = part_total;
@@ -411,7 +416,7 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.wg0 = wg;
       wg += tiles * S;
       P.rwg0 = rwg;
-      rwg += ceil_div((int64_t)O * I + (hb ? O : 0), 256);
+      rwg += ceil_div((int64_t)O * I + (hb ? O : 0), 64);
       auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
       const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
       const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);

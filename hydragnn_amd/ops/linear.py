@@ -219,15 +219,22 @@ class _TallLinearSum(torch.autograd.Function):
                 _defer["items"].append((dy, x, wps[j], bp if j == 0 else None))
                 grads += [dy @ w if ctx.needs_input_grad[1 + 2 * j] else None, None]
             return (None, *grads)
+        # non-leaf weights (e.g. the PNA weight-prep outputs): all k weight gradients of this
+        # sum in ONE grouped launch pair (they share dY)
+        need_w = [bool(ctx.needs_input_grad[2 + 2 * j]) for j in range(ctx.k)]
+        want_b = ctx.has_b and ctx.needs_input_grad[0]
+        dws = [torch.empty(w.shape, device=w.device, dtype=w.dtype) if (need_w[j] or (want_b and j == 0)) else None
+               for j, w in enumerate(ws)]
+        if want_b:
+            db = torch.empty(ws[0].shape[0], device=dy.device, dtype=dy.dtype)
+        sel = [j for j in range(ctx.k) if dws[j] is not None]
+        if sel:
+            _native.ops().linear_wgrad_grouped(
+                [dy] * len(sel), [xs[j] for j in sel], [dws[j] for j in sel],
+                [db if (want_b and j == 0) else torch.empty(0, device=dy.device) for j in sel], [0] * len(sel))
         for j, (x, w) in enumerate(zip(xs, ws)):
             dx = dy @ w if ctx.needs_input_grad[1 + 2 * j] else None
-            dW = None
-            want_b = ctx.has_b and j == 0 and ctx.needs_input_grad[0]
-            if ctx.needs_input_grad[2 + 2 * j] or want_b:
-                dW, dbj = _native.ops().linear_wgrad(dy, x, want_b)
-                if want_b:
-                    db = dbj
-            grads += [dx, dW]
+            grads += [dx, dws[j] if need_w[j] else None]
         return (db, *grads)
 
 
