@@ -17,16 +17,29 @@ MAX_L = 8
 
 
 class _Radial(torch.autograd.Function):
+    """Outputs: the L per-layer r_l then the L per-layer G_l, each its own output, so
+    the backward receives one gradient per layer (returning the stacked [L, E, F]
+    tensors and indexing them made autograd build each layer's gradient as
+    zeros(L, E, F) + slice copy + add: 18 launches / 120 us per OC20 step)."""
+
     @staticmethod
     def forward(ctx, dist, freq, Wemb, bemb, Wlin, cutoff, exponent):
         R, Gt = _native.ops().radial_fwd(dist, freq, Wemb, bemb, Wlin, cutoff, exponent)
         ctx.save_for_backward(R, dist, freq, Wemb, Wlin)
         ctx.cfg = (cutoff, exponent)
-        return R, Gt
+        ctx.L = R.shape[0]
+        return (*R.unbind(0), *Gt.unbind(0))
 
     @staticmethod
-    def backward(ctx, dR, dG):
+    def backward(ctx, *grads):
         R, dist, freq, Wemb, Wlin = ctx.saved_tensors
+        L = ctx.L
+
+        def stack(gs, like):
+            return torch.stack([g if g is not None else torch.zeros_like(like[0]) for g in gs])
+
+        dR = stack(grads[:L], R)
+        dG = stack(grads[L:], R)
         ddist, dfreq, dWemb, dbemb, dWlin = _native.ops().radial_bwd(dR, dG, R, dist, freq, Wemb, Wlin, *ctx.cfg)
         return ddist, dfreq, dWemb, dbemb, dWlin, None, None
 
@@ -47,6 +60,7 @@ def radial_features(dist, basis, convs):
     Wemb = torch.stack([c.rbf_emb[0].weight for c in convs])
     bemb = torch.stack([c.rbf_emb[0].bias for c in convs])
     Wlin = torch.stack([c.rbf_lin.weight for c in convs])
-    R, Gt = _Radial.apply(dist.contiguous(), basis.freq, Wemb, bemb, Wlin, float(basis.cutoff),
-                          int(basis.envelope.p - 1))
-    return [(R[i], Gt[i]) for i in range(len(convs))]
+    outs = _Radial.apply(dist.contiguous(), basis.freq, Wemb, bemb, Wlin, float(basis.cutoff),
+                         int(basis.envelope.p - 1))
+    L = len(convs)
+    return [(outs[i], outs[L + i]) for i in range(L)]

@@ -31,8 +31,43 @@ import torch
 from ..parallel.ddp import BucketedGradSync, DistributedDataParallel
 
 
+_LOSS_KIND = {"mse": 0, "mae": 1, "rmse": 2, "smooth_l1": 3}
+
+
+class _FusedMaskedLoss(torch.autograd.Function):
+    """One HIP launch forward, one backward (csrc/loss.hip) for the masked losses of a
+    padded batch; the composite below stays the CPU / double-backward path."""
+
+    @staticmethod
+    def forward(ctx, pred, target, mask, kind):
+        from .. import _native
+
+        out = _native.ops().masked_loss_fwd(pred, target, mask, kind)
+        ctx.save_for_backward(pred, target, mask, out)
+        ctx.kind = kind
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        pred, target, mask, out = ctx.saved_tensors
+        return _native.ops().masked_loss_bwd(g.reshape(1), pred, target, mask, out, ctx.kind), None, None, None
+
+
+def _fused_loss_ok(kind, pred, target, mask):
+    from ..ops.pna import fused
+
+    return (kind in _LOSS_KIND and pred.is_cuda and pred.dtype == torch.float32 and target.dtype == torch.float32
+            and fused("loss") and pred.dim() >= 1 and pred.shape == target.shape
+            and (mask is None or mask.numel() == pred.shape[0]))
+
+
 def masked_loss(kind, pred, target, mask=None, var=None):
     """Reference loss functions restricted to rows where ``mask`` is true."""
+    if _fused_loss_ok(kind, pred, target, mask):
+        return _FusedMaskedLoss.apply(pred.contiguous(), target.contiguous(),
+                                      None if mask is None else mask.contiguous(), _LOSS_KIND[kind])
     if mask is None:
         if kind == "mse":
             return torch.nn.functional.mse_loss(pred, target)
@@ -75,7 +110,9 @@ def batch_loss(module, pred, batch):
         mask = batch.get("graph_mask") if module.head_type[ih] == "graph" else batch.get("node_mask")
         v = None if var is None else var[ih]
         l = masked_loss(module.loss_function_type, pred[ih], batch.targets[ih], mask, v)
-        tot = tot + l * module.loss_weights[ih]
+        w = module.loss_weights[ih]
+        lw = l if (not torch.is_tensor(w) and w == 1.0) else l * w
+        tot = lw if ih == 0 else tot + lw
         tasks.append(l)
     return tot, tasks
 

@@ -131,3 +131,23 @@ def test_native_store_assemble_matches_torch(padded):
     if padded:
         assert torch.equal(a.node_mask, b.node_mask) and torch.equal(a.graph_mask, b.graph_mask)
     assert np.isfinite(a.pos.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("kind", ["mse", "mae", "rmse", "smooth_l1"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_fused_masked_loss_matches_composite(kind, masked):
+    """csrc/loss.hip (one launch each way) vs the torch composite of train/step.masked_loss."""
+    from hydragnn_amd.ops.pna import composite_mode
+    from hydragnn_amd.train.step import masked_loss
+
+    torch.manual_seed(7)
+    pred = torch.randn(333, 3, device="cuda", requires_grad=True)
+    target = torch.randn(333, 3, device="cuda")
+    mask = (torch.rand(333, device="cuda") > 0.3) if masked else None
+    l1 = masked_loss(kind, pred, target, mask)
+    (g1,) = torch.autograd.grad(l1 * 1.7, pred)
+    with composite_mode(True):
+        l2 = masked_loss(kind, pred, target, mask)
+        (g2,) = torch.autograd.grad(l2 * 1.7, pred)
+    torch.testing.assert_close(l1, l2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(g1, g2, rtol=1e-5, atol=1e-7)
