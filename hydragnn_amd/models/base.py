@@ -299,13 +299,53 @@ class Base(nn.Module):
         return inv, equiv, ctx
 
     def _branch_ids(self, data):
+        """Branch ids present in the batch, known on the host; ``None`` for a statically
+        padded (captured) batch without host ids: every branch is then evaluated densely
+        and selected per graph on the device (``_decode_dense``, no host sync)."""
         ids = data.get("dataset_ids_host")
         if ids is not None:
             return list(ids)
         dn = data.get("dataset_name")
         if dn is None:
             return [0]
+        if data.get("graph_mask") is not None:
+            return None
         return [int(i) for i in torch.unique(dn).tolist()]
+
+    def branch_names(self):
+        return sorted((k for k in self.graph_shared.keys()), key=lambda k: int(k.split("-")[1])) \
+            if len(self.graph_shared) else [f"branch-{i}" for i in range(self.num_branches)]
+
+    def dense_decode_ok(self):
+        """Capturable multi-branch decode: graph heads and shared-MLP node heads (a ``conv``
+        node head's BatchNorm would see every branch's nodes)."""
+        return "node" not in self.config_heads or self.config_heads["node"][0]["architecture"]["type"] != "conv"
+
+    def _decode_dense(self, x, x_graph, equiv, ctx):
+        """Every branch head on every graph / node, selected per row by its dataset id
+        (``torch.where`` on the device): the static-shape decode of the captured step.
+        Rows of a branch see exactly the computation of ``decode`` (heads are row-wise);
+        padding rows (dataset id -1) get zeros."""
+        data = ctx.data
+        dn = data.dataset_name.view(-1)
+        dn_node = dn.index_select(0, data.batch)
+        outputs, outputs_var = [], []
+        for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
+            width = head_dim * (1 + self.var_output)
+            rows, ids = (x_graph, dn) if t == "graph" else (x, dn_node)
+            out = rows.new_zeros((rows.shape[0], width))
+            for bt in self.branch_names():
+                ID = int(bt.split("-")[1])
+                if t == "graph":
+                    ob = sequential_chain(x_graph, self.graph_shared[bt], headloc[bt])
+                else:
+                    ob = headloc[bt](x=x, batch=data.batch)
+                out = torch.where((ids == ID).unsqueeze(1), ob, out)
+            outputs.append(out[:, :head_dim])
+            outputs_var.append(out[:, head_dim:] ** 2)
+        if self.var_output:
+            return outputs, outputs_var
+        return outputs
 
     def decode(self, x, equiv, ctx):
         data = ctx.data
@@ -319,6 +359,8 @@ class Base(nn.Module):
         if nb > 1 and data.get("branch_graph_ranges") is not None:
             return self._decode_ranges(x, x_graph, equiv, ctx)
         ids = self._branch_ids(data) if nb > 1 else [0]
+        if ids is None:
+            return self._decode_dense(x, x_graph, equiv, ctx)
         G = x_graph.shape[0]
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
             if t == "graph":

@@ -256,6 +256,19 @@ class MultiheadDecoderBlock(nn.Module):
         data = ctx.data
         outs = []
         granges, nranges = data.get("branch_graph_ranges"), data.get("branch_node_ranges")
+        if self.num_branches > 1 and ids is None:
+            # statically padded (captured) batch: every branch densely, selected per row
+            dn = data.dataset_name.view(-1)
+            dn_node = dn.index_select(0, data.batch)
+            names = sorted(self.heads_NN[0].keys(), key=lambda k: int(k.split("-")[1]))
+            for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
+                feats, rid = (gfeat, dn) if t == "graph" else (node_features, dn_node)
+                out = feats.new_zeros(feats.shape[0], hd)
+                for bt in names:
+                    x = self.graph_shared[bt](feats) if (t == "graph" and self.nonlinear) else feats
+                    out = torch.where((rid == int(bt.split("-")[1])).unsqueeze(1), hn[bt](x)[:, :hd], out)
+                outs.append(out)
+            return outs
         if self.num_branches > 1 and granges is not None and len(granges) > 1:
             # store batches are grouped by branch: contiguous slices, no masks / host syncs
             for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
@@ -363,11 +376,12 @@ class MACEStack(Base):
         self.multihead_decoders.append(dec(n == 1, o3.Irreps([(self.num_elements, 0, 1)])))
         for i in range(n):
             last = i == n - 1
-            self.graph_convs.append(self._apply_global_attn(self.get_conv(H, H, first_layer=i == 0, last_layer=last)))
+            self.graph_convs.append(self._apply_global_attn(self.get_conv(H, H, first_layer=i == 0, last_layer=last,
+                                                                          layer=i)))
             self.feature_layers.append(nn.Identity())
             self.multihead_decoders.append(dec(last, final if last else hidden))
 
-    def get_conv(self, input_dim, output_dim, first_layer=False, last_layer=False):
+    def get_conv(self, input_dim, output_dim, first_layer=False, last_layer=False, layer=0):
         hidden_dim = output_dim if input_dim == 1 else input_dim
         node_feats = o3.Irreps.natural(input_dim, 0 if first_layer else self.node_max_ell)
         hidden = o3.Irreps.natural(hidden_dim, self.node_max_ell)
@@ -381,8 +395,10 @@ class MACEStack(Base):
         n_edge = self.hidden_dim if (self.use_global_attn and self.is_edge_model) else self.num_bessel
         inter = InteractionBlock(node_feats, self.edge_attrs_irreps, n_edge, interaction, hidden,
                                  self.avg_num_neighbors)
-        prod = EquivariantProductBasisBlock(self.max_ell, hidden, self.correlation[0], hidden_dim, self.num_elements,
-                                            use_sc=True)
+        # per-layer correlation order (reference MACEStack.py: ``correlation`` may be a list, one
+        # entry per interaction layer; a scalar applies to all)
+        corr = self.correlation[min(layer, len(self.correlation) - 1)]
+        prod = EquivariantProductBasisBlock(self.max_ell, hidden, corr, hidden_dim, self.num_elements, use_sc=True)
         sizing = o3.O3Linear(hidden, output)
         return MACELayer(inter, prod, sizing, output.count(0, 1))
 
@@ -397,8 +413,11 @@ class MACEStack(Base):
             pos = pos - seg.gather(seg.segment_mean(pos, ctx.graph_si), ctx.graph_si)
         vec, dist = edge_vectors_and_lengths(pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
         node_attrs, elem = process_node_attributes(data.x)
-        ctx.node_attributes, ctx.elem = node_attrs, elem
-        node_feats = self.node_embedding(node_attrs)
+        # element-indexed weight tables are gathered, not multiplied by the one-hot: the node
+        # embedding and every symmetric contraction use the element SegIndex (the one-hot
+        # only feeds the first linear read-out, as in the reference)
+        ctx.node_attributes, ctx.elem = node_attrs, o3.element_index(elem, self.num_elements)
+        node_feats = self.node_embedding.lookup(ctx.elem)
         ea = o3.spherical_harmonics(self.max_ell, vec)
         if self.use_edge_attr:
             ea = torch.cat([data.edge_attr, ea], 1)

@@ -184,6 +184,21 @@ def wigner_3j(l1, l2, l3):
 
 
 # ----------------------------------------------------------------------------- layers
+def element_index(elem, num_elements):
+    """SegIndex grouping nodes by element (CSR over ``num_elements`` segments with a stable
+    sort permutation) so per-element weight tables are *gathered* (``seg.gather``: an
+    embedding lookup whose backward is a deterministic segment-sum) instead of multiplying
+    a materialised [N, num_elements] one-hot.  Device-only ops (no host sync): capturable."""
+    from . import segment as seg
+
+    elem = elem.view(-1)
+    counts = torch.zeros(num_elements, dtype=torch.float32, device=elem.device).index_add_(
+        0, elem.long(), torch.ones(elem.shape[0], dtype=torch.float32, device=elem.device))  # exact integer sums
+    rowptr = torch.cat([counts.new_zeros(1), counts.cumsum(0)]).to(torch.int32)
+    perm = torch.sort(elem, stable=True).indices.to(torch.int32)
+    return seg.SegIndex(elem.to(torch.int32), rowptr, perm, num_elements)
+
+
 class O3Linear(nn.Module):
     """e3nn ``o3.Linear`` semantics: per (l, p) channel mixing, N(0,1) weights scaled by
     1/sqrt(fan_in) in the forward ("element" path normalisation), no bias."""
@@ -202,6 +217,23 @@ class O3Linear(nn.Module):
                 numel += mi * mo
         self.weight = nn.Parameter(torch.randn(numel))
         self.sl_in, self.sl_out = irreps_in.slices(), irreps_out.slices()
+
+    def lookup(self, elem_si):
+        """forward(one_hot(elem)) for a single scalar input block (the MACE node embedding):
+        one row gather of the weight table per node."""
+        from . import segment as seg
+
+        (mi, li, _), = self.irreps_in.blocks
+        assert li == 0 and all(l == 0 for _, l, _ in self.irreps_out.blocks), "lookup: scalar irreps only"
+        cols = []
+        for io in range(len(self.irreps_out.blocks)):
+            W = None
+            for ii, o, off, m_in, mo, a in self.paths:
+                if o == io:
+                    W = self.weight[off:off + m_in * mo].view(m_in, mo) * a
+            cols.append(W if W is not None else self.weight.new_zeros(mi, self.irreps_out.blocks[io][0]))
+        table = torch.cat(cols, 1) if len(cols) > 1 else cols[0]
+        return seg.gather(table, elem_si)
 
     def forward(self, x):
         N = x.shape[0]
@@ -411,7 +443,11 @@ class Contraction(nn.Module):
                 # per-element weights: one-hot(elem) @ W as a GEMM (its backward is a GEMM too,
                 # not a sort-based index_put), then one (N*H, K) x (K, M d^nu) GEMM
                 Wt = self.weights[nu - 1]
-                if elem.dim() == 2:  # one-hot [N, num_elements]
+                if not torch.is_tensor(elem):  # element SegIndex: per-node row gather of the table
+                    from . import segment as seg
+
+                    W = seg.gather(Wt.reshape(Wt.shape[0], -1), elem).view(N, K, H)
+                elif elem.dim() == 2:  # one-hot / soft assignment [N, num_elements]
                     W = (elem @ Wt.reshape(Wt.shape[0], -1)).view(N, K, H)
                 else:
                     W = Wt[elem]
@@ -436,8 +472,9 @@ class SymmetricContraction(nn.Module):
                                            for _, l, _ in irreps_out.blocks])
 
     def forward(self, x, elem):
-        """``elem``: element indices [N] or a one-hot / soft assignment [N, num_elements]."""
+        """``elem``: an element SegIndex (``element_index``), element indices [N], or a
+        one-hot / soft assignment [N, num_elements]."""
         N = x.shape[0]
-        if elem.dim() == 1:
-            elem = torch.nn.functional.one_hot(elem.long(), self.contractions[0].weights[0].shape[0]).to(x.dtype)
+        if torch.is_tensor(elem) and elem.dim() == 1:
+            elem = element_index(elem, self.contractions[0].weights[0].shape[0])
         return torch.cat([c(x, elem).reshape(N, -1) for c in self.contractions], -1)

@@ -188,9 +188,7 @@ class TrainStep:
         self.mode = mode
         dev = next(self.module.parameters()).device
         self.device = dev
-        if mode == "graph" and getattr(self.module, "num_branches", 1) > 1:
-            # multi-branch decode routes graphs by their (host-known) branch ranges, which
-            # change from batch to batch: such models step eagerly
+        if mode == "graph" and getattr(self.module, "num_branches", 1) > 1 and not self._capture_multibranch():
             self.mode = mode = "eager"
         if world > 1 and mode == "eager" and not isinstance(model, DistributedDataParallel):
             self.model = DistributedDataParallel(model)
@@ -222,6 +220,22 @@ class TrainStep:
         self.graphs = {}
         self.pool = None
         self.B = None
+
+    def _capture_multibranch(self):
+        """Multi-branch models capture with a dense decode (every branch head on every row,
+        per-row select on the device; ``Base._decode_dense``); conv node heads cannot (their
+        BatchNorm would see other branches' nodes).  The dense decode multiplies the head
+        work by the branch count, which pays for launch-bound models (MACE multibranch:
+        2.4x over eager on MI355X) but not for GEMM-bound ones (the SC25 EGNN-866 with 3 x 889
+        node heads: captured 30.6 vs eager 30.1 ms/step), so ``HYDRA_MULTIBRANCH_CAPTURE=auto``
+        captures models below 8M parameters; 1 / 0 force it."""
+        m = self.module
+        if not (hasattr(m, "dense_decode_ok") and m.dense_decode_ok()):
+            return False
+        flag = os.environ.get("HYDRA_MULTIBRANCH_CAPTURE", "auto")
+        if flag in ("0", "1"):
+            return flag == "1"
+        return sum(p.numel() for p in m.parameters()) < 8_000_000
 
     # ------------------------------------------------------------------ eager
     def _zero(self):

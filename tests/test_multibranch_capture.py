@@ -1,0 +1,76 @@
+"""Multi-branch models on the captured (statically padded) training step.
+
+The reference decodes a multi-dataset batch by masking graphs per branch
+(``Base.py:482-560``); the host-side branch ranges used by the eager store path change
+from batch to batch, so the captured step decodes densely instead: every branch head on
+every row, selected per row by the dataset id on the device (``Base._decode_dense``).
+Checks: padded step (the CPU twin of the captured step) == eager step, on CPU for
+EGNN / SchNet / MACE, and captured == eager on the GPU."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from hydragnn_amd.data.device_store import DeviceGraphStore
+from hydragnn_amd.data.synthetic import oc20_like
+from hydragnn_amd.models.create import create_model
+from hydragnn_amd.train.step import TrainStep
+
+NB = 3
+
+
+def _data(n=18):
+    s = oc20_like(n, seed=20, radius=5.0, max_neighbours=8, pe_dim=2, min_atoms=5, max_atoms=10)
+    for i, g in enumerate(s):
+        g.dataset_name = torch.tensor([[i % NB]])
+        g.x = torch.randint(1, 9, (g.x.shape[0], 1)).float()
+        g.y = torch.cat([g.y.view(-1)[:1], torch.sin(g.pos[:, 0])])
+        g.y_loc = torch.tensor([[0, 1, 1 + g.num_nodes]])
+    return s
+
+
+def _model(mt):
+    heads = {"graph": [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                                  "num_headlayers": 1, "dim_headlayers": [8]}}
+                       for b in range(NB)],
+             "node": [{"type": f"branch-{b}", "architecture": {"num_headlayers": 1, "dim_headlayers": [8],
+                                                                 "type": "mlp"}} for b in range(NB)]}
+    torch.manual_seed(0)
+    return create_model(mt, 1, 12, [1, 1], 2, "", "multihead", 1, ["graph", "node"], heads, "relu", "mse",
+                        [1.0, 1.0], 2, use_gpu=False, edge_dim=None, dropout=0.0, radius=5.0, num_radial=5,
+                        num_gaussians=8, num_filters=12, max_neighbours=8, envelope_exponent=5, max_ell=1,
+                        node_max_ell=1, avg_num_neighbors=5.0, correlation=2)
+
+
+def _compare(mt, dev, tol):
+    samples = _data()
+    m1 = _model(mt).to(dev)
+    m2 = copy.deepcopy(m1)
+    store = DeviceGraphStore(samples, dev, head_types=["graph", "node"], head_dims=[1, 1])
+    eager = TrainStep(m1, lr=1e-3, mode="eager")
+    cap = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=256)
+    assert cap.mode == "graph"
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        idx = list(rng.choice(len(samples), 6, replace=False))
+        le, lc = float(eager(store, idx)[0]), float(cap(store, idx)[0])
+        assert abs(le - lc) <= tol * max(1.0, abs(le)), (le, lc)
+
+
+@pytest.mark.parametrize("mt", ["EGNN", "SchNet", "MACE"])
+def test_multibranch_padded_step_equals_eager(mt):
+    _compare(mt, "cpu", 1e-4)
+
+
+def test_multibranch_capture_policy(monkeypatch):
+    m = _model("EGNN")
+    assert TrainStep(m, mode="graph").mode == "graph"  # small model: dense capture
+    monkeypatch.setenv("HYDRA_MULTIBRANCH_CAPTURE", "0")
+    assert TrainStep(m, mode="graph").mode == "eager"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mt", ["EGNN", "MACE"])
+def test_multibranch_captured_step_equals_eager_gpu(mt):
+    _compare(mt, "cuda", 2e-3)

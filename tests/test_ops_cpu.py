@@ -103,3 +103,42 @@ def test_fused_adamw_cpu_matches_torch():
         ob.step()
     for x, y in zip(a, b):
         torch.testing.assert_close(x, y)
+
+
+def test_mace_element_lookup_equals_one_hot():
+    """Element-indexed tables gathered through an element SegIndex == the one-hot GEMMs
+    (node embedding and symmetric contraction), forward and backward."""
+    from hydragnn_amd.ops import o3
+
+    torch.manual_seed(0)
+    elem = torch.randint(0, 118, (57,))
+    oh = torch.nn.functional.one_hot(elem, 118).float()
+    si = o3.element_index(elem, 118)
+    lin = o3.O3Linear(o3.Irreps([(118, 0, 1)]), o3.Irreps([(16, 0, 1)]))
+    a, b = lin.lookup(si), lin(oh)
+    torch.testing.assert_close(a, b)
+    g = torch.randn_like(a)
+    ga = torch.autograd.grad(a, lin.weight, g)[0]
+    gb = torch.autograd.grad(lin(oh), lin.weight, g)[0]
+    torch.testing.assert_close(ga, gb)
+    sc = o3.SymmetricContraction(1, o3.Irreps([(8, 0, 1), (8, 1, -1)]), 3, 8, 118)
+    x = torch.randn(57, 8, 4, requires_grad=True)
+    ya, yb = sc(x, si), sc(x, oh)
+    torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5)
+    w = sc.contractions[0].weights[0]
+    gy = torch.randn_like(ya)
+    torch.testing.assert_close(torch.autograd.grad(ya, w, gy)[0], torch.autograd.grad(sc(x, oh), w, gy)[0],
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_mace_per_layer_correlation():
+    from hydragnn_amd.data.synthetic import oc20_like
+    from hydragnn_amd.models.create import create_model
+
+    heads = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                             "num_headlayers": 1, "dim_headlayers": [8]}}]}
+    m = create_model("MACE", 1, 8, [1], 0, "", "", 0, ["graph"], heads, "relu", "mse", [1.0], 3, use_gpu=False,
+                     radius=5.0, num_radial=4, max_ell=1, node_max_ell=1, avg_num_neighbors=4.0,
+                     correlation=[3, 2, 1], envelope_exponent=5)
+    corrs = [c.prod.symmetric_contractions.contractions[0].correlation for c in m.graph_convs]
+    assert corrs == [3, 2, 1]

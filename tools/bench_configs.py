@@ -7,6 +7,7 @@
                        forces = -dE/dpos (compute_grad_energy, double backward), batch 32
   5a multibranch_egnn  SC25 multibranch shape: EGNN hidden 866 x 4, 5 branches, graph energy +
                        node force heads (3 x 889), batch 128, branch routing by dataset_name
+                       (captured step: dense per-row branch select)
   5b multibranch_mace  the BASELINE.json variant of config 5 with MACE (hidden 64, l_max 2,
                        correlation 2, 3 layers), 5 branches, batch 32
 
@@ -124,7 +125,14 @@ def run(name, steps, warmup, dev):
         def step(idx):
             return ts(store, idx)[0]
     else:
-        ts = TrainStep(model, lr=1e-3, mode="eager")
+        # captured step (multi-branch models decode densely; SchNet's in-forward radius
+        # graph has a data-dependent edge count and steps eagerly)
+        mode = os.environ.get("BENCH_MODE", "eager" if not getattr(model, "capturable", True) else "graph")
+        nbk = 512 if name.startswith("multibranch") else 256
+        ts = TrainStep(model, lr=1e-3, mode=mode, node_bucket=nbk, edge_bucket=8 * nbk)
+        ts.prepare(store, B)
+        if ts.mode == "graph":
+            ts.precapture(store, B)
 
         def step(idx):
             return ts(store, idx)[0]
