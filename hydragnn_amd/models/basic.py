@@ -8,6 +8,7 @@ import torch
 from torch import nn
 
 from ..ops import segment as seg
+from ..ops.pna import fused
 from .base import Base
 from .layers import Linear
 
@@ -42,6 +43,36 @@ class SAGEConv(nn.Module):
         return self.lin_l(agg) + self.lin_r(inv), equiv
 
 
+class _MFBanks(torch.autograd.Function):
+    """Per-node degree bank (csrc/conv_misc.hip): each node multiplies only its own bank
+    forward and input-gradient; the weight gradient is one GEMM against the gradient
+    scattered into its degree column block."""
+
+    @staticmethod
+    def forward(ctx, h, x, Wl, bl, Wr, rowptr, maxd):
+        from .. import _native
+
+        out = _native.ops().mf_fwd(h, x, Wl, bl, Wr, rowptr, maxd)
+        ctx.save_for_backward(h, x, Wl, Wr, rowptr)
+        ctx.maxd, ctx.has_b = maxd, bl is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        h, x, Wl, Wr, rowptr = ctx.saved_tensors
+        D1 = ctx.maxd + 1
+        N, O = g.shape
+        dh, dx = _native.ops().mf_dgrad(g, Wl, Wr, rowptr, ctx.maxd, h.shape[1])
+        d = (rowptr[1:] - rowptr[:-1]).clamp(max=ctx.maxd).long()
+        gexp = g.new_zeros(N, D1, O).scatter_(1, d.view(-1, 1, 1).expand(-1, 1, O), g.view(N, 1, O)).view(N, D1 * O)
+        dWl = gexp.t() @ h
+        dWr = gexp.t() @ x
+        dbl = gexp.sum(0) if ctx.has_b else None
+        return dh, dx, dWl, dbl, dWr, None, None
+
+
 class MFConv(nn.Module):
     """Degree-specific weights: out_i = W_l[d_i] sum_j x_j + W_r[d_i] x_i, d_i = min(deg_i, max_degree).
 
@@ -58,10 +89,13 @@ class MFConv(nn.Module):
 
     def forward(self, inv, equiv, ctx):
         h = seg.segment_sum(seg.gather(inv, ctx.src_si), ctx.dst_si)
-        deg = ctx.dst_si.degree().to(inv.device).clamp(max=self.max_degree).long()
         Wl = torch.cat([l.weight for l in self.lins_l], 0)
         Wr = torch.cat([l.weight for l in self.lins_r], 0)
         bl = torch.cat([l.bias for l in self.lins_l], 0) if self.lins_l[0].bias is not None else None
+        if inv.is_cuda and inv.dtype == torch.float32 and fused("mfconv"):
+            return _MFBanks.apply(h.contiguous(), inv.contiguous(), Wl, bl, Wr, ctx.dst_si.rowptr,
+                                  self.max_degree), equiv
+        deg = ctx.dst_si.degree().to(inv.device).clamp(max=self.max_degree).long()
         y = torch.nn.functional.linear(h, Wl, bl) + torch.nn.functional.linear(inv, Wr)
         D1, O = self.max_degree + 1, self.out_channels
         y = y.view(-1, D1, O)

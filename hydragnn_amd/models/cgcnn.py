@@ -12,10 +12,32 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import _native
 from ..ops import segment as seg
 from ..ops.linear import linear
+from ..ops.pna import fused
 from .layers import Linear
 from .base import Base
+
+
+class _CGGate(torch.autograd.Function):
+    """sum_{e->i} sigmoid(z_e) softplus(s_e) in one launch (csrc/conv_misc.hip); backward:
+    one launch for the per-edge gate gradients + one by-source CSR segment sum."""
+
+    @staticmethod
+    def forward(ctx, nb, et, bias, dst_si, src_si):
+        out = _native.ops().cg_gate_fwd(nb, et, bias, dst_si.rowptr, src_si.index)
+        ctx.save_for_backward(nb, et, bias)
+        ctx.si = (dst_si, src_si)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nb, et, bias = ctx.saved_tensors
+        dst_si, src_si = ctx.si
+        G, dnd = _native.ops().cg_gate_bwd(g, nb, et, bias, dst_si.rowptr, src_si.index)
+        dnb = torch.cat([dnd, seg.segment_sum(G, src_si)], 1)
+        return dnb, (G if et is not None else None), (G.sum(0) if bias is not None else None), None, None
 
 
 class CGConv(nn.Module):
@@ -34,10 +56,16 @@ class CGConv(nn.Module):
         # node blocks: [f_i | s_i | f_j | s_j]
         Wn = torch.cat([Wf[:, :C], Ws[:, :C], Wf[:, C:2 * C], Ws[:, C:2 * C]], 0)
         nb = linear(x, Wn)
-        ij = seg.gather(nb[:, :2 * C], ctx.dst_si) + seg.gather(nb[:, 2 * C:], ctx.src_si)
         bias = None
         if self.lin_f.bias is not None:
             bias = torch.cat([self.lin_f.bias, self.lin_s.bias])
+        if x.is_cuda and x.dtype == torch.float32 and fused("cggate"):
+            et = None
+            if self.dim and ctx.edge_attr is not None:
+                et = linear(ctx.edge_attr, torch.cat([Wf[:, 2 * C:], Ws[:, 2 * C:]], 0), bias).contiguous()
+            m = _CGGate.apply(nb.contiguous(), et, bias if et is None else None, ctx.dst_si, ctx.src_si)
+            return x + m, equiv
+        ij = seg.gather(nb[:, :2 * C], ctx.dst_si) + seg.gather(nb[:, 2 * C:], ctx.src_si)
         if self.dim and ctx.edge_attr is not None:
             ij = ij + linear(ctx.edge_attr, torch.cat([Wf[:, 2 * C:], Ws[:, 2 * C:]], 0), bias)
         elif bias is not None:

@@ -20,11 +20,40 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import _native
 from ..ops import rng as _rng
 from ..ops import segment as seg
 from ..ops.linear import linear
+from ..ops.pna import fused
 from .base import Base
 from .layers import BatchNorm, Linear
+
+
+class _GATFused(torch.autograd.Function):
+    """Fused GATv2 softmax-aggregate (csrc/gat.hip): one launch forward, one backward
+    (+ one by-source CSR segment-sum for dxl)."""
+
+    @staticmethod
+    def forward(ctx, xl, xr, ge, gself, att, dst_si, src_si, H, slope, self_loop, rng, salt, p):
+        out, ml = _native.ops().gat_fwd(xl, xr, ge, gself, att, dst_si.rowptr, src_si.index, H, slope, self_loop,
+                                        rng, salt, p)
+        ctx.save_for_backward(xl, xr, ge, gself, att, ml, rng)
+        ctx.cfg = (dst_si, src_si, H, slope, self_loop, salt, p)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xl, xr, ge, gself, att, ml, rng = ctx.saved_tensors
+        dst_si, src_si, H, slope, self_loop, salt, p = ctx.cfg
+        P, dge, dxr, dxl_self, dgself, datt = _native.ops().gat_bwd(dout, xl, xr, ge, gself, att, dst_si.rowptr,
+                                                                    src_si.index, ml, H, slope, self_loop, rng,
+                                                                    salt, p)
+        dxl = seg.segment_sum(P, src_si) + dxl_self
+        return (dxl, dxr, dge if ge is not None else None, dgself if gself is not None else None,
+                datt.sum(0).view_as(att), None, None, None, None, None, None, None, None)
+
+
+_GAT_MAX_C = 32  # wider heads would spill registers in the fused kernel
 
 
 class GATv2Conv(nn.Module):
@@ -67,9 +96,23 @@ class GATv2Conv(nn.Module):
         lr = linear(x, W, b)  # one node GEMM for both projections
         xl, xr = lr[:, :H * C], lr[:, H * C:]
         dst_si, src_si = ctx.dst_si, ctx.src_si
+        e = ctx.edge_attr if self.lin_edge is not None else None
+        if x.is_cuda and x.dtype == torch.float32 and fused("gat") and C <= _GAT_MAX_C:
+            ge = linear(e, self.lin_edge.weight).contiguous() if e is not None else None
+            gself = linear(seg.segment_mean(e, dst_si), self.lin_edge.weight).contiguous() \
+                if (e is not None and self.add_self_loops) else None
+            drop = self.training and self.dropout > 0
+            out = _GATFused.apply(xl, xr, ge, gself, self.att.reshape(-1).contiguous(), dst_si, src_si, H,
+                                  float(self.negative_slope), bool(self.add_self_loops),
+                                  _rng.counter(x.device) if drop else None, int(self._salt),
+                                  float(self.dropout) if drop else 0.0)
+            out = out.view(N, H, C)
+            out = out.reshape(N, H * C) if self.concat else out.mean(1)
+            if self.bias is not None:
+                out = out + self.bias
+            return out, equiv
         xl_j = seg.gather(xl, src_si)
         g = xl_j + seg.gather(xr, dst_si)
-        e = ctx.edge_attr if self.lin_edge is not None else None
         if e is not None:
             g = g + linear(e, self.lin_edge.weight)
         s = (F.leaky_relu(g, self.negative_slope).view(-1, H, C) * self.att).sum(-1)  # [E, H]

@@ -30,6 +30,9 @@ def assign_salts(model):
         if hasattr(m, "_salts"):
             m._salts = list(range(k + 1, k + 1 + len(m._salts)))
             k += len(m._salts)
+        if hasattr(m, "_salt"):  # single-site modules (GATv2Conv)
+            m._salt = k + 1
+            k += 1
 
 
 def _key(device):
