@@ -18,6 +18,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   (N>1: launched by torch.distributed.run, one rank per GPU)
 """
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -65,6 +66,7 @@ def _spawn(args):
 
 
 def main():
+    faulthandler.enable()  # a native crash prints the Python stack of every thread
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_spawn(args))

@@ -807,9 +807,77 @@ at::Tensor attn_bwd(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tens
   return dqkv;
 }
 
+// ---- split backward: the dQ pass and the dK/dV pass as separate ops, so the caller can
+// run them on two streams (they only share read-only inputs); attn_bwd_combine sums the
+// split partials (or concatenates the S == 1 outputs) into dqkv.
+at::Tensor attn_bwd_delta(const at::Tensor& dO_, const at::Tensor& O, int64_t H) {
+  auto dO = dO_.contiguous();
+  HY_CHECK_CUDA(dO);
+  const int64_t N = O.size(0);
+  const int D = (int)(O.size(1) / H);
+  auto delta = at::empty({H, N}, O.options());
+  if (N > 0)
+    attn_delta_kernel<<<ceil_div(N * H, 256), 256, 0, stream()>>>(dO.data_ptr<float>(), O.data_ptr<float>(),
+                                                                   delta.data_ptr<float>(), (int)N, (int)H, D);
+  return delta;
+}
+
+// which = 0: dQ partials [S, N, F]; which = 1: dK|dV partials [S, N, 2F]
+at::Tensor attn_bwd_part(const at::Tensor& dO_, const at::Tensor& qkv, const at::Tensor& LSE, const at::Tensor& delta,
+                         const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t H, double scale,
+                         int64_t max_span, int64_t splits, int64_t which) {
+  auto dO = dO_.contiguous();
+  HY_CHECK_CUDA(dO);
+  const int64_t N = qkv.size(0);
+  const int64_t F = qkv.size(1) / 3;
+  const int D = (int)(F / H);
+  const int ld = (int)qkv.stride(0);
+  const float* base = qkv.data_ptr<float>();
+  const int S = attn_splits(N, H, D, max_span > 0 ? max_span : N, splits);
+  dim3 grid(ceil_div(N, 64), H, S);
+  if (which == 0) {
+    auto pq = at::empty({(int64_t)S, N, F}, qkv.options());
+    if (N > 0)
+      HY_ATTN_DISPATCH(D, {
+        HY_DQ(kD)(base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(),
+                  delta.data_ptr<float>(), pq.data_ptr<float>(), (int)F, N * F, seg_id.data_ptr<int>(),
+                  seg_ptr.data_ptr<int>(), (int)N, (int)H, S, (float)scale);
+      });
+    return pq;
+  }
+  auto pkv = at::empty({(int64_t)S, N, 2 * F}, qkv.options());
+  if (N > 0)
+    HY_ATTN_DISPATCH(D, {
+      HY_DKV(kD)(base, base + F, base + 2 * F, ld, dO.data_ptr<float>(), LSE.data_ptr<float>(),
+                 delta.data_ptr<float>(), pkv.data_ptr<float>(), pkv.data_ptr<float>() + F, (int)(2 * F), N * 2 * F,
+                 seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), (int)N, (int)H, S, (float)scale);
+    });
+  return pkv;
+}
+
+at::Tensor attn_bwd_combine(const at::Tensor& pq, const at::Tensor& pkv) {
+  HY_CHECK(pq.dim() == 3 && pkv.dim() == 3 && pq.size(1) == pkv.size(1) && pkv.size(2) == 2 * pq.size(2),
+           "attn_bwd_combine: partial shapes");
+  const int64_t N = pq.size(1), F = pq.size(2);
+  HY_CHECK(F % 4 == 0, "attention hidden must be a multiple of 4");
+  auto dqkv = at::empty({N, 3 * F}, pq.options());
+  const int F4 = (int)(F / 4);
+  if (N > 0)
+    attn_bwd_sum_kernel<<<ceil_div(N * 3 * F4, 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(pq.data_ptr<float>()), (int)pq.size(0),
+        reinterpret_cast<const float4*>(pkv.data_ptr<float>()), (int)pkv.size(0),
+        reinterpret_cast<float4*>(dqkv.data_ptr<float>()), N, F4);
+  return dqkv;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("attn_bwd_delta(Tensor dO, Tensor O, int H) -> Tensor");
+  m.def(
+      "attn_bwd_part(Tensor dO, Tensor qkv, Tensor LSE, Tensor delta, Tensor seg_id, Tensor seg_ptr, int H, "
+      "float scale, int max_span, int splits, int which) -> Tensor");
+  m.def("attn_bwd_combine(Tensor pq, Tensor pkv) -> Tensor");
   m.def(
       "attn_fwd(Tensor qkv, Tensor seg_id, Tensor seg_ptr, int H, float scale, int max_span, int splits) "
       "-> (Tensor, Tensor)");
@@ -819,6 +887,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("attn_bwd_delta", hy::attn_bwd_delta);
+  m.impl("attn_bwd_part", hy::attn_bwd_part);
+  m.impl("attn_bwd_combine", hy::attn_bwd_combine);
   m.impl("attn_fwd", hy::attn_fwd);
   m.impl("attn_bwd", hy::attn_bwd);
 }

@@ -11,6 +11,7 @@ names follow ``torch.nn.MultiheadAttention`` (``attn.in_proj_weight``,
 (``norm1.module.*``) so state dicts keep the reference layout.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -21,6 +22,8 @@ from ..ops.linear import ACT_RELU, linear
 from ..ops.norm import norm_add
 from ..ops.rng import dropout as rng_dropout, new_salt
 from ..ops.streams import Fork
+
+_GPS_FORK = os.environ.get("HYDRA_GPS_FORK", "1") == "1"  # attention branch on a side stream
 from .layers import BatchNorm, Linear
 
 
@@ -126,7 +129,7 @@ class GPSConv(nn.Module):
         hs = []
         # the attention branch runs on a side stream, concurrently with the local MPNN
         # (forward AND backward; ops/streams.py)
-        with Fork(inv, ctx.attn_seg_id, ctx.attn_seg_ptr) as fork:
+        with Fork(inv, ctx.attn_seg_id, ctx.attn_seg_ptr, enable=_GPS_FORK) as fork:
             h = self.attn(inv, ctx.attn_seg_id, ctx.attn_seg_ptr)
             h_att = norm_add(h, self.norm2, nv, residual=inv, p=self.dropout, salt=self._salts[1], training=tr)
         if self.conv is not None:

@@ -14,6 +14,7 @@ import os
 import torch
 
 from .. import _native
+from . import streams as _streams
 from . import pna as _pna_mode
 
 
@@ -86,8 +87,25 @@ class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dO):
         qkv, O, LSE, seg_id, seg_ptr = ctx.saved_tensors
-        dqkv = _native.ops().attn_bwd(dO, qkv, O, LSE, seg_id, seg_ptr, ctx.heads, ctx.scale, ctx.span, _SPLITS)
-        return dqkv, None, None, None, None
+        ops = _native.ops()
+        # HYDRA_ATTN_BWD_FORK=1: dQ and dK/dV passes on two streams.  Off by default: measured
+        # on MI355X (OC20 GPS headline) it loses to forking the whole attention branch
+        # (13.3k vs 15.6k graphs/s), and the two cannot nest (hipGraph capture of a fork
+        # from an already-forked stream crashed at capture end on ROCm 7).
+        nested = _streams.enabled(qkv) and torch.cuda.current_stream(qkv.device) == _streams.side_stream(qkv.device)
+        if not _streams.enabled(qkv) or nested or os.environ.get("HYDRA_ATTN_BWD_FORK", "0") != "1":
+            dqkv = ops.attn_bwd(dO, qkv, O, LSE, seg_id, seg_ptr, ctx.heads, ctx.scale, ctx.span, _SPLITS)
+            return dqkv, None, None, None, None
+        # the dQ and dK/dV passes only share read-only inputs: dK/dV on a second side stream,
+        # concurrently with dQ (each ~50 us and below the chip's width for GPS shapes)
+        dO = dO.contiguous()
+        delta = ops.attn_bwd_delta(dO, O, ctx.heads)
+        args = (dO, qkv, LSE, delta, seg_id, seg_ptr, ctx.heads, ctx.scale, ctx.span, _SPLITS)
+        with _streams.Fork(*args[:6], slot=1) as fork:
+            pkv = ops.attn_bwd_part(*args, 1)
+        pq = ops.attn_bwd_part(*args, 0)
+        fork.join(pkv)
+        return ops.attn_bwd_combine(pq, pkv), None, None, None, None
 
 
 def segment_attention(qkv, heads, seg_id, seg_ptr, scale=None):

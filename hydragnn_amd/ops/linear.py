@@ -253,6 +253,7 @@ class _EngineSumF32(_TallLinearSum):
 
 
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+ENGINE_SUM_MAX_ROWS = 8192  # fp32 multi-input sums above this use the library GEMM pair
 BIG_GEMM = 1 << 30  # M*N*K above which bf16 maps go to the library's large-tile kernels
 
 
@@ -296,7 +297,10 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
         flat = []
         for x, w in zip(xs, ws):
             flat += [x, w]
-        y = _EngineSumF32.apply(b, *flat)
+        # fp32 concat-linear: the engine's one-launch forward wins on node-sized inputs; on
+        # edge-sized ones (PNAPlus radial term, 23k x 65 -> 64) the library GEMM + addmm pair
+        # is ~2x faster on MI355X (30-40 us vs ~14 us, profiles/r2_rocprof_headline_sequence.txt)
+        y = (_EngineSumF32 if xs[0].shape[0] < ENGINE_SUM_MAX_ROWS else _TallLinearSum).apply(b, *flat)
     else:
         y = F.linear(xs[0], ws[0], b)
         for x, w in zip(xs[1:], ws[1:]):

@@ -22,8 +22,10 @@ def enabled(t):
     return t.is_cuda and os.environ.get("HYDRA_BRANCH_STREAMS", "1") == "1"
 
 
-def side_stream(device):
-    key = torch.device(device).index
+def side_stream(device, slot=0):
+    """Cached side stream ``slot`` of ``device`` (slot 0: branch forks; slot 1: the
+    attention backward's dK/dV pass, which forks again from inside a side branch)."""
+    key = (torch.device(device).index, slot)
     s = _side.get(key)
     if s is None:
         s = torch.cuda.Stream(device=device)
@@ -35,12 +37,12 @@ class Fork:
     """``with Fork(x) as f: <side-branch code>``; after the block ``f.join(*outs)`` makes
     the current stream wait for the side branch and keeps its outputs alive for it."""
 
-    def __init__(self, *inputs):
+    def __init__(self, *inputs, slot=0, enable=True):
         self.inputs = [t for t in inputs if torch.is_tensor(t)]
-        self.on = bool(self.inputs) and enabled(self.inputs[0])
+        self.on = enable and bool(self.inputs) and enabled(self.inputs[0])
         if self.on:
             self.main = torch.cuda.current_stream(self.inputs[0].device)
-            self.side = side_stream(self.inputs[0].device)
+            self.side = side_stream(self.inputs[0].device, slot)
 
     def __enter__(self):
         if self.on:
