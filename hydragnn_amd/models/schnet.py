@@ -74,8 +74,11 @@ class SCFStack(Base):
     is_edge_model = True
 
     @property
-    def capturable(self):  # the in-forward radius graph has a data-dependent edge count
-        return bool(self.use_edge_attr or (self.use_global_attn and self.is_edge_model))
+    def capturable(self):
+        # the in-forward radius graph has a data-dependent edge count; without equivariant
+        # position updates it equals the batch's own radius graph (built by the preprocessing
+        # with the same radius / max_neighbours / index cap), which a padded batch provides
+        return bool(self.use_edge_attr or (self.use_global_attn and self.is_edge_model) or not self.equivariance)
 
     def __init__(self, input_args, conv_args, num_filters, edge_dim, num_gaussians, radius, *args,
                  max_neighbours=None, **kwargs):
@@ -116,12 +119,18 @@ class SCFStack(Base):
         stack = self
         cache = {}
 
+        # statically padded (captured) batch, fixed positions: the interaction graph is the
+        # batch's radius graph (same radius / max_neighbours / index cap as the in-forward
+        # builder, SCFStack.py:175-190), so the step has static shapes
+        static_graph = data.get("graph_mask") is not None and not self.equivariance
+
         def layer_graph(conv, p):
-            if with_edges:  # data edges, no PBC shifts (reference overrides shifts with zeros)
+            if with_edges or static_graph:  # data edges, no PBC shifts (reference overrides shifts with zeros)
                 if "g" not in cache:
                     _, d = edge_vectors_and_lengths(p, ctx.dst_si, ctx.src_si, None)
                     d = d.view(-1)
-                    cache["g"] = (ctx.dst_si, ctx.src_si, d, stack.distance_expansion(d), ctx.edge_attr)
+                    cache["g"] = (ctx.dst_si, ctx.src_si, d, stack.distance_expansion(d),
+                                  ctx.edge_attr if with_edges else None)
                 return cache["g"]
             key = "g" if not conv.equivariant and "static" in cache else None
             if key is not None:

@@ -237,6 +237,7 @@ class BucketedGradSync:
         self.works = []
         self.active = False
         self.next = 0
+        self.counted = set()
         self.comm = torch.cuda.Stream(device=dev, priority=-1) if dev.type == "cuda" else None
         for p in self.params:
             p.register_post_accumulate_grad_hook(self._hook)
@@ -263,11 +264,19 @@ class BucketedGradSync:
         self.launched = [False] * len(self.buckets)
         self.works = []
         self.next = 0
+        self.counted = set()
 
     def _hook(self, p):
         if not self.active:
             return
         bi = self.bucket_of[p]
+        if id(p) in self.counted:
+            # a second gradient contribution (a parameter used by both a deferred grouped
+            # weight gradient and an ordinary op): fine until its bucket has been reduced
+            if self.launched[bi]:
+                raise RuntimeError("gradient contribution arrived after its bucket was all-reduced")
+            return
+        self.counted.add(id(p))
         self.pending[bi] -= 1
         # launch in bucket-index order only: every rank then issues the identical
         # collective sequence whatever order its autograd engine finished buckets in

@@ -22,7 +22,13 @@ NB = 3
 
 def _data(n=18):
     s = oc20_like(n, seed=20, radius=5.0, max_neighbours=8, pe_dim=2, min_atoms=5, max_atoms=10)
+    from hydragnn_amd.data.transforms import radius_graph
+
     for i, g in enumerate(s):
+        # the models' own radius / cap (index policy): SchNet's captured step uses these edges
+        g.edge_index = radius_graph(g.pos, 5.0, max_num_neighbors=8)
+        g.edge_attr = None
+        g.sort_edges_by_dst()
         g.dataset_name = torch.tensor([[i % NB]])
         g.x = torch.randint(1, 9, (g.x.shape[0], 1)).float()
         g.y = torch.cat([g.y.view(-1)[:1], torch.sin(g.pos[:, 0])])
