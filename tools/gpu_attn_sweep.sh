@@ -1,0 +1,8 @@
+#!/bin/bash
+# headline bench over attention split counts (and the LDS forward variant)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for envs in "HYDRA_ATTN_SPLITS=0" "HYDRA_ATTN_SPLITS=2" "HYDRA_ATTN_SPLITS=3" "HYDRA_ATTN_SPLITS=8" "HYDRA_ATTN_SPLITS=12" "HYDRA_ATTN_SPLITS=16" "HYDRA_ATTN_LDS=1"; do
+  env $envs timeout -k 10 120 python bench.py --steps 30 --warmup 10 > gpurun_out/sweep.log 2>&1 || { echo "[$envs] failed"; tail -5 gpurun_out/sweep.log; exit 1; }
+  echo "[$envs] $(tail -1 gpurun_out/sweep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done
