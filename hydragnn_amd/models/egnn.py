@@ -19,11 +19,37 @@ Parameter names follow the reference (``edge_mlp.0``, ``node_mlp.2``,
 import torch
 from torch import nn
 
+from .. import _native
 from ..ops import segment as seg
 from ..ops.geometry import edge_vectors_and_lengths
 from ..ops.linear import linear
+from ..ops.pna import fused
 from .layers import Linear
 from .base import Base
+
+
+class _EdgeGatherAct(torch.autograd.Function):
+    """act(A[src] + B[dst] + r w + b (+ e-term)) in one pass (csrc/conv_misc.hip); backward:
+    one pass for dz / dr, CSR segment sums for dA / dB, a GEMV for dw."""
+
+    @staticmethod
+    def forward(ctx, ab, r, w, b, et, src_si, dst_si, act):
+        out = _native.ops().edge_gather_act_fwd(ab, src_si.index, dst_si.index, r, w, b, et, act)
+        ctx.save_for_backward(ab, r, w, b, et)
+        ctx.cfg = (src_si, dst_si, act)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ab, r, w, b, et = ctx.saved_tensors
+        src_si, dst_si, act = ctx.cfg
+        dz, dr = _native.ops().edge_gather_act_bwd(g, ab, src_si.index, dst_si.index, r, w, b, et, act)
+        dab = torch.cat([seg.segment_sum(dz, src_si), seg.segment_sum(dz, dst_si)], 1)
+        dw = dz.t() @ r
+        return dab, dr.view_as(r), dw, dz.sum(0), (dz if et is not None else None), None, None, None
+
+
+_ACT_CODE = {nn.ReLU: 1, nn.SiLU: 2}
 
 
 def split_concat_linear(lin, widths):
@@ -74,11 +100,17 @@ class E_GCL(nn.Module):
         Wb = split_concat_linear(l0, ws)
         # [x_row | x_col] blocks at node level (one GEMM), gathered per edge
         ab = linear(x, torch.cat([Wb[0], Wb[1]], 0))
-        h = seg.gather(ab[:, :l0.out_features], src_si) + seg.gather(ab[:, l0.out_features:], dst_si)
-        h = h + radial * Wb[2].view(1, -1) + l0.bias
-        if len(ws) == 4:
-            h = h + linear(edge_attr, Wb[3])
-        h = self.edge_mlp[1](h)
+        act_code = _ACT_CODE.get(type(self.edge_mlp[1]))
+        if x.is_cuda and x.dtype == torch.float32 and fused("egnn") and act_code is not None:
+            et = linear(edge_attr, Wb[3]).contiguous() if len(ws) == 4 else None
+            h = _EdgeGatherAct.apply(ab.contiguous(), radial.reshape(-1).contiguous(), Wb[2].reshape(-1).contiguous(),
+                                     l0.bias, et, src_si, dst_si, act_code)
+        else:
+            h = seg.gather(ab[:, :l0.out_features], src_si) + seg.gather(ab[:, l0.out_features:], dst_si)
+            h = h + radial * Wb[2].view(1, -1) + l0.bias
+            if len(ws) == 4:
+                h = h + linear(edge_attr, Wb[3])
+            h = self.edge_mlp[1](h)
         out = self.edge_mlp[3](self.edge_mlp[2](h))
         if self.attention:
             out = out * self.att_mlp(out)

@@ -254,7 +254,7 @@ class _EngineSumF32(_TallLinearSum):
 
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
 ENGINE_SUM_MAX_ROWS = 8192  # fp32 multi-input sums above this use the library GEMM pair
-BIG_GEMM = 1 << 30  # M*N*K above which bf16 maps go to the library's large-tile kernels
+BIG_GEMM = int(os.environ.get("HYDRA_BF16_LIBRARY_MIN", str(1 << 30)))  # M*N*K above which bf16 maps use the library
 
 
 def _engine_ok(tensors):

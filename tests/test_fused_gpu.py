@@ -245,3 +245,41 @@ def test_fused_mfconv_banks_match_composite():
             assert (a is None or not a.abs().sum()) and (c is None or not c.abs().sum())
             continue
         torch.testing.assert_close(a, c, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("edge,act", [(False, "relu"), (True, "silu")])
+def test_fused_egnn_edge_stage_matches_composite(edge, act):
+    """EGNN edge_mlp first stage act(A[src] + B[dst] + r w + b (+ e-term)) fused (one pass
+    each way, csrc/conv_misc.hip) vs the composite; full E_GCL layer outputs and grads."""
+    from torch import nn
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.data.synthetic import oc20_like
+    from hydragnn_amd.models.egnn import E_GCL
+    from hydragnn_amd.models.layers import Ctx
+    from hydragnn_amd.ops.pna import composite_mode
+
+    torch.manual_seed(3)
+    samples = oc20_like(6, seed=4, radius=5.0, max_neighbours=10, pe_dim=2, min_atoms=20, max_atoms=40)
+    b = DeviceGraphStore(samples, "cuda").batch(list(range(6)))
+    H = 40
+    layer = E_GCL(H, H, H, edge_attr_dim=2 if edge else 0, act_fn=nn.ReLU() if act == "relu" else nn.SiLU(),
+                  equivariant=True).cuda()
+    x = torch.randn(b.num_nodes, H, device="cuda", requires_grad=True)
+    pos = b.pos.clone().requires_grad_(True)
+    ctx = Ctx(dst_si=b.dst_si, src_si=b.src_si,
+              edge_attr=torch.rand(b.edge_index.shape[1], 2, device="cuda") if edge else None)
+    params = [x, pos] + list(layer.parameters())
+    o1 = layer(x, pos, ctx)
+    gx, gp = torch.randn_like(o1[0]), torch.randn_like(o1[1])
+    g1 = torch.autograd.grad(o1, params, (gx, gp), allow_unused=True)
+    with composite_mode(True):
+        o2 = layer(x, pos, ctx)
+        g2 = torch.autograd.grad(o2, params, (gx, gp), allow_unused=True)
+    for a, c in zip(o1, o2):
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-4)
+    for a, c in zip(g1, g2):
+        if a is None or c is None:
+            assert a is None and c is None
+            continue
+        torch.testing.assert_close(a, c, rtol=1e-3, atol=2e-4)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel summary of one bench_configs config: $1 = config, $2 = precision
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_cfg_$1_$2
+rm -rf $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d $OUT -o run -- python3 tools/bench_configs.py $1 --steps 10 --warmup 5 --precision $2 > ${OUT}.log 2>&1 || exit $?
+DB=$(find $OUT -name "*.db" | head -1)
+python3 tools/rocpd_summary.py $DB --top 40 > ${OUT}_summary.txt
+grep metric ${OUT}.log | cut -c1-200
+head -30 ${OUT}_summary.txt | cut -c1-160
