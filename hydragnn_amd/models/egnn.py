@@ -45,7 +45,7 @@ class _EdgeGatherAct(torch.autograd.Function):
         src_si, dst_si, act = ctx.cfg
         dz, dr = _native.ops().edge_gather_act_bwd(g, ab, src_si.index, dst_si.index, r, w, b, et, act)
         dab = torch.cat([seg.segment_sum(dz, src_si), seg.segment_sum(dz, dst_si)], 1)
-        dw = dz.t() @ r
+        dw = (r.view(1, -1) @ dz).view(-1)  # row-vector GEMV (the dz^T r form ran at 4 workgroups)
         return dab, dr.view_as(r), dw, dz.sum(0), (dz if et is not None else None), None, None, None
 
 

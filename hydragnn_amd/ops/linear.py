@@ -284,6 +284,11 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
         y = F.linear(xs[0].to(torch.bfloat16), ws[0].to(torch.bfloat16),
                      None if b is None else b.to(torch.bfloat16)).float()
         return torch.relu(y) if act == ACT_RELU else y
+    if engine and _state["prec"] == 1 and min(min(w.shape) for w in ws) < 16:
+        # very narrow maps (EGNN coord_mlp's 866 -> 1, the 1 -> 866 edge-attribute term): the
+        # engine's 32x32 tiles waste >90% of the MFMA work and write the [E, 866] side tile by
+        # tile (~600 us per call measured for 36k rows); these are bandwidth-bound, fp32 library
+        engine = False
     if engine and _state["prec"] == 1:
         flat = []
         for x, w in zip(xs, ws):
