@@ -25,6 +25,12 @@ struct VecT<4> {
   static __device__ __forceinline__ T add(T a, T b) { return f4add(a, b); }
 };
 template <>
+struct VecT<2> {
+  using T = float2;
+  static __device__ __forceinline__ T zero() { return make_float2(0.f, 0.f); }
+  static __device__ __forceinline__ T add(T a, T b) { return make_float2(a.x + b.x, a.y + b.y); }
+};
+template <>
 struct VecT<1> {
   using T = float;
   static __device__ __forceinline__ T zero() { return 0.f; }
@@ -35,6 +41,10 @@ template <typename T>
 __device__ __forceinline__ T shfl_xor_t(T v, int o);
 template <>
 __device__ __forceinline__ float shfl_xor_t<float>(float v, int o) { return __shfl_xor(v, o, 64); }
+template <>
+__device__ __forceinline__ float2 shfl_xor_t<float2>(float2 v, int o) {
+  return make_float2(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64));
+}
 template <>
 __device__ __forceinline__ float4 shfl_xor_t<float4>(float4 v, int o) {
   return make_float4(__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64), __shfl_xor(v.z, o, 64), __shfl_xor(v.w, o, 64));
@@ -79,7 +89,9 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
     for (int o = 1; o < KS; o <<= 1) a = V::add(a, shfl_xor_t<T>(a, o * tpr));
     if (k != 0) continue;
     if constexpr (MEAN) {
-      if constexpr (VEC == 4) a = f4scale(a, inv); else a *= inv;
+      if constexpr (VEC == 4) a = f4scale(a, inv);
+      else if constexpr (VEC == 2) a = make_float2(a.x * inv, a.y * inv);
+      else a *= inv;
     }
     reinterpret_cast<T*>(out + (int64_t)r * F)[v] = a;
   }
@@ -162,7 +174,10 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
     pp = perm->data_ptr<int>();
   }
   const bool v4 = (F % 4 == 0);
-  auto g = row_geom(N, v4 ? F : F * 4);
+  // wide odd-multiple-of-2 rows (the SC25 EGNN's 866 channels): float2 loads halve the
+  // per-column dependent load chains of the scalar path
+  const bool v2 = !v4 && (F % 2 == 0) && F >= 128;
+  auto g = row_geom(N, v4 ? F : (v2 ? F * 2 : F * 4));
   // KS row streams per segment, as long as one segment's threads stay inside a wave
   const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);
   const int rpb = 256 / (g.tpr * ks);
@@ -174,6 +189,8 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   if (ks == 4) HY_SEG_SUM(VEC, MEAN, 4); else if (ks == 2) HY_SEG_SUM(VEC, MEAN, 2); else HY_SEG_SUM(VEC, MEAN, 1)
   if (v4) {
     if (mean) { HY_SEG_SUM_KS(4, true); } else { HY_SEG_SUM_KS(4, false); }
+  } else if (v2) {
+    if (mean) { HY_SEG_SUM_KS(2, true); } else { HY_SEG_SUM_KS(2, false); }
   } else {
     if (mean) { HY_SEG_SUM_KS(1, true); } else { HY_SEG_SUM_KS(1, false); }
   }

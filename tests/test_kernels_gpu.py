@@ -36,7 +36,7 @@ def test_native_loaded():
     assert _native.load(), _native._error
 
 
-@pytest.mark.parametrize("F", [1, 3, 8, 64, 130])
+@pytest.mark.parametrize("F", [1, 3, 8, 64, 130, 866])
 def test_segment_sum_gather(F):
     dst_si, src_si, E = _graph()
     x = torch.randn(E, F, dtype=torch.float32)
