@@ -338,35 +338,48 @@ __global__ void __launch_bounds__(256) pna_wprep_fwd_kernel(const float* __restr
                                                             const float* __restrict__ encb, float* __restrict__ Wab,
                                                             float* __restrict__ Wr, float* __restrict__ Wd,
                                                             float* __restrict__ bc, int F, int d) {
+  // one thread per output element (Wab copy, then the Wr / Wd / bc dot products of length F
+  // over L1/L2-resident operands, fixed sequential order).  The round-1 form (one wave per
+  // dot, 2048 workgroups) cost ~19 us on the conv branch's critical path for F = 64.
   const int ld = 3 * F, le = d + F;
-  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t idx = tid; idx < 2 * F * F; idx += nthreads) {
-    const int r = (int)(idx / F), c = (int)(idx % F);
-    Wab[idx] = W[(r % F) * ld + (r / F) * F + c];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nab = 2LL * F * F, nr = (int64_t)F * F, nd = (int64_t)F * d;
+  if (t < nab) {
+    const int r = (int)(t / F), c = (int)(t % F);
+    Wab[t] = W[(r % F) * ld + (r / F) * F + c];
+    return;
   }
-  // dot products: Wr (F*F), Wd (F*d), bc (F) -- one wave each
-  const int64_t nd = (int64_t)F * F + (int64_t)F * d + F;
-  const int64_t nwaves = nthreads / 64;
-  for (int64_t q = tid / 64; q < nd; q += nwaves) {
-    float v;
-    float* dst;
-    if (q < F * F) {
-      const int o = (int)(q / F), c = (int)(q % F);
-      v = wave_dot(W + o * ld + 2 * F, 1, encW + d + c, le, F);
-      dst = Wr + q;
-    } else if (q < (int64_t)F * F + F * d) {
-      const int64_t k = q - F * F;
-      const int o = (int)(k / d), c = (int)(k % d);
-      v = wave_dot(W + o * ld + 2 * F, 1, encW + c, le, F);
-      dst = Wd + k;
-    } else {
-      const int o = (int)(q - F * F - (int64_t)F * d);
-      v = wave_dot(W + o * ld + 2 * F, 1, encb, 1, F) + b[o];
-      dst = bc + o;
-    }
-    if (lane_id() == 0) *dst = v;
+  int64_t q = t - nab;
+  if (q >= nr + nd + F) return;
+  const float* wrow;
+  const float* col;
+  int stride;
+  float* dst;
+  float v = 0.f;
+  if (q < nr) {
+    const int o = (int)(q / F), c = (int)(q % F);
+    wrow = W + o * ld + 2 * F;
+    col = encW + d + c;
+    stride = le;
+    dst = Wr + q;
+  } else if (q < nr + nd) {
+    const int64_t k = q - nr;
+    const int o = (int)(k / d), c = (int)(k % d);
+    wrow = W + o * ld + 2 * F;
+    col = encW + c;
+    stride = le;
+    dst = Wd + k;
+  } else {
+    const int o = (int)(q - nr - nd);
+    wrow = W + o * ld + 2 * F;
+    col = encb;
+    stride = 1;
+    dst = bc + o;
+    v = b[o];
   }
+  float acc = 0.f;
+  for (int k = 0; k < F; ++k) acc = fmaf(wrow[k], col[(int64_t)k * stride], acc);
+  *dst = acc + v;
 }
 
 // Backward of pna_wprep_fwd: dW [F,3F], db [F], dencW [F, d+F], dencb [F].
@@ -427,8 +440,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pna_wprep_fwd(const a
   const int d = (int)encW.size(1) - F;
   auto Wab = at::empty({2 * F, F}, W.options()), Wr = at::empty({F, F}, W.options());
   auto Wd = at::empty({F, d}, W.options()), bc = at::empty({F}, W.options());
-  const int64_t total = (int64_t)F * F + (int64_t)F * d + F;
-  pna_wprep_fwd_kernel<<<wprep_grid(total), 256, 0, stream()>>>(W.data_ptr<float>(), b.data_ptr<float>(),
+  const int64_t total = 2LL * F * F + (int64_t)F * F + (int64_t)F * d + F;  // one thread per output
+  pna_wprep_fwd_kernel<<<ceil_div(total, 256), 256, 0, stream()>>>(W.data_ptr<float>(), b.data_ptr<float>(),
                                                                encW.data_ptr<float>(), encb.data_ptr<float>(),
                                                                Wab.data_ptr<float>(), Wr.data_ptr<float>(),
                                                                Wd.data_ptr<float>(), bc.data_ptr<float>(), F, d);

@@ -1,7 +1,7 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "segment" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/seg2_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "segment or weight_prep" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/seg2_tests.log 2>&1
 rc=$?
 tail -2 gpurun_out/seg2_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
