@@ -80,8 +80,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
     # (RCCL refuses duplicate devices); the driver's N-GPU runs use RCCL ("nccl").
-    backend = os.environ.get("BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    backend = os.environ.get("BENCH_BACKEND", "nccl" if local_world <= ndev else "gloo")
     use_pg = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ  # 1-rank torchrun runs keep the PG
     if use_pg:
         torch.cuda.set_device(local % ndev)
@@ -89,7 +90,7 @@ def main():
             from hydragnn_amd.parallel.distributed import rccl_env
 
             rccl_env()
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local % ndev}"))
         else:
             dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local % ndev}")
