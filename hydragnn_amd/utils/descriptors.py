@@ -136,6 +136,4 @@ class atomicdescriptors:
         return torch.tensor(self.atom_embeddings[str(int(atomtype))])
 
 
-def generate_graphdata_from_smilestr(*args, **kwargs):
-    """SMILES -> graph (reference ``smiles_utils.py:18-127``) requires RDKit, not available here."""
-    raise ImportError("generate_graphdata_from_smilestr needs RDKit, which is not installed in this environment")
+from .smiles import generate_graphdata_from_smilestr, get_node_attribute_name  # noqa: E402,F401  (RDKit-free)
