@@ -120,3 +120,57 @@ def test_multidataset_three_ranks_and_ddstore(tmp_path):
          tmp_path, nproc=3)
     _run("multidataset/train.py", ["--multi_model_list", "ANI1x,QM7-X", "--num_epoch", "1", "--ddstore"], tmp_path,
          nproc=2)
+
+
+_FAMILIES = ["qm7x", "ani1_x", "transition1x", "open_molecules_2025", "mptrj", "alexandria", "open_materials_2024",
+             "open_catalyst_2022", "open_direct_air_capture_2023"]
+
+
+@pytest.mark.parametrize("family", _FAMILIES)
+def test_atomistic_family(family, tmp_path):
+    """Every dataset-family driver (examples/atomistic.py) trains EGNN end to end; energy and
+    forces configs alternate across the families."""
+    task = "forces" if _FAMILIES.index(family) % 2 else "energy"
+    n = "12" if family == "open_direct_air_capture_2023" else "30"
+    r = _result(_run(f"{family}/train.py", ["--inputfile", f"{family}_{task}.json", "--num_samples", n,
+                                             "--num_epoch", "1"], tmp_path))
+    assert r["test_error"] == r["test_error"]
+
+
+@pytest.mark.parametrize("family", ["qm7x", "mptrj", "open_catalyst_2022"])
+def test_atomistic_forces_are_gradients(family):
+    """The synthetic potential's analytic forces equal -dE/dpos (central differences)."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, EX)
+    import atomistic as A
+
+    fam = A.FAMILIES[family]
+    rng = np.random.default_rng(3)
+    g = A.make_sample(rng, fam)
+    pos = g.pos.double().numpy()
+    z = g.x[:, 0].long().numpy()
+    cell = g.cell.double().numpy() if g.get("cell") is not None else None
+
+    def energy(p):
+        if cell is not None:
+            ei, sh = A.radius_graph_pbc(torch.from_numpy(p), torch.from_numpy(cell), list(fam.pbc_axes), fam.radius,
+                                        max_num_neighbors=10 ** 6)
+            src, dst = ei[0].numpy(), ei[1].numpy()
+            vec = p[dst] - p[src] + sh.numpy().astype(np.float64)
+        else:
+            r = np.linalg.norm(p[:, None] - p[None], axis=-1)
+            dst, src = np.nonzero((r < fam.radius) & (r > 0))
+            vec = p[dst] - p[src]
+        return A._energy_forces(z, p, src, dst, vec)
+
+    e0, f0 = energy(pos)
+    # recompute f0 in float64 (the sample stores float32)
+    for a, k in [(0, 0), (len(pos) // 2, 1), (len(pos) - 1, 2)]:
+        h = 1e-5
+        pp, pm = pos.copy(), pos.copy()
+        pp[a, k] += h
+        pm[a, k] -= h
+        fd = -(energy(pp)[0] - energy(pm)[0]) / (2 * h)
+        assert abs(fd - f0[a, k]) < 1e-4 * max(1.0, abs(fd)), (a, k, fd, f0[a, k])
