@@ -174,3 +174,12 @@ def test_atomistic_forces_are_gradients(family):
         pm[a, k] -= h
         fd = -(energy(pp)[0] - energy(pm)[0]) / (2 * h)
         assert abs(fd - f0[a, k]) < 1e-4 * max(1.0, abs(fd)), (a, k, fd, f0[a, k])
+
+
+@pytest.mark.parametrize("script", ["ogb/train_gap.py", "csce/train_gap.py", "zinc/zinc.py",
+                                    "dftb_uv_spectrum/train_smooth_uv_spectrum.py",
+                                    "dftb_uv_spectrum/train_discrete_uv_spectrum.py"])
+def test_smiles_examples(script, tmp_path):
+    """SMILES-table examples (RDKit-free reader) train end to end through the low-level API."""
+    r = _result(_run(script, ["--num_samples", "48", "--num_epoch", "1"], tmp_path))
+    assert r["test_error"] == r["test_error"] and r["num_train"] > 0

@@ -406,3 +406,46 @@ def test_radial_features(E, F, K, L):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
     for a, b in zip(g_h, g_r):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * max(1.0, float(b.abs().max())))
+
+
+@pytest.mark.parametrize("scope", ["batch", "graph"])
+@pytest.mark.parametrize("mag", [1.0, 30.0])
+def test_attention_mfma_forward_fp32_accuracy(scope, mag):
+    """The MFMA forward (D = 8, two-term fp16 splits) against an fp64 reference: its error must
+    stay at fp32 level (not fp16/bf16 level), including large-magnitude logits."""
+    from hydragnn_amd import _native
+
+    H, D = 8, 8
+    torch.manual_seed(int(mag))
+    ptr = torch.tensor([0, 37, 100, 101, 900, 2000])
+    N = 2051
+    seg_id, seg_ptr = make_segments(N, scope, ptr=ptr, num_valid=2000)
+    qkv = torch.randn(N, 3 * H * D) * torch.tensor([mag] * (2 * H * D) + [1.0] * (H * D))
+    ref = attention_reference(qkv.double(), H, seg_id)
+    O, LSE = _native.ops().attn_fwd(qkv.to(DEV), seg_id.to(DEV), seg_ptr.to(DEV), H, 1.0 / D ** 0.5, N, 0)
+    err = (O.cpu().double() - ref).abs().max().item()
+    # fp32 baseline: the same attention in plain fp32 torch (at mag 30 the logits reach ~1e3
+    # and fp32 itself is off by ~3e-4 there)
+    err32 = (attention_reference(qkv, H, seg_id).double() - ref).abs().max().item()
+    assert err < 2.0 * err32 + 2e-6, (err, err32)
+    # the LSE the backward consumes: natural log-sum-exp of the scaled logits
+    q = qkv[:, :H * D].double().view(N, H, D).transpose(0, 1)
+    k = qkv[:, H * D:2 * H * D].double().view(N, H, D).transpose(0, 1)
+    s = (q @ k.transpose(1, 2)) / D ** 0.5
+    s = s.masked_fill(~(seg_id.view(-1, 1) == seg_id.view(1, -1)).unsqueeze(0), float("-inf"))
+    lse_ref = torch.logsumexp(s, -1)
+    assert (LSE.cpu().double() - lse_ref).abs().max().item() < 1e-4 * max(1.0, mag)
+
+
+def test_attention_valu_forward_kernels():
+    """HYDRA_ATTN_MFMA=0 (VALU sk forward) and HYDRA_ATTN_V3=1 (v3 kernels) in subprocesses."""
+    import subprocess
+    import sys
+
+    code = ("import torch, sys; sys.path.insert(0, '.'); from tests.test_kernels_gpu import test_attention_key_splits;"
+            "[test_attention_key_splits(s, sc) for s in (1, 5) for sc in ('batch', 'graph')]; print('ok')")
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
+    for extra in ({"HYDRA_ATTN_MFMA": "0"}, {"HYDRA_ATTN_MFMA": "0", "HYDRA_ATTN_V3": "1"}):
+        env = dict(__import__("os").environ, **extra)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120, cwd=root)
+        assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stderr[-2000:])
