@@ -40,6 +40,10 @@ def base_parser(description, default_config):
     ap.add_argument("--pe_dim", type=int, default=None)
     ap.add_argument("--workdir", default=None, help="where logs/ and serialized_dataset/ go (default: cwd)")
     ap.add_argument("--seed", type=int, default=0)
+    # hyper-parameter overrides (the HPO drivers' search space)
+    ap.add_argument("--hidden_dim", type=int, default=None)
+    ap.add_argument("--num_conv_layers", type=int, default=None)
+    ap.add_argument("--learning_rate", type=float, default=None)
     return ap
 
 
@@ -61,6 +65,20 @@ def load_config(here, args):
         arch["global_attn_type"] = args.global_attn_type
     if args.pe_dim is not None:
         arch["pe_dim"] = args.pe_dim
+    apply_hparams(config, args)
+    return config
+
+
+def apply_hparams(config, args):
+    arch = config["NeuralNetwork"]["Architecture"]
+    if getattr(args, "hidden_dim", None) is not None:
+        arch["hidden_dim"] = args.hidden_dim
+    if getattr(args, "num_conv_layers", None) is not None:
+        arch["num_conv_layers"] = args.num_conv_layers
+    if getattr(args, "learning_rate", None) is not None:
+        config["NeuralNetwork"]["Training"]["Optimizer"]["learning_rate"] = args.learning_rate
+    if getattr(args, "mpnn_type", None):
+        arch["mpnn_type"] = args.mpnn_type
     return config
 
 

@@ -111,6 +111,10 @@ def main(argv=None):
     ap.add_argument("--prepare_samples", type=int, default=200, help="samples per generated store")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--hidden_dim", type=int, default=None)
+    ap.add_argument("--num_conv_layers", type=int, default=None)
+    ap.add_argument("--learning_rate", type=float, default=None)
+    ap.add_argument("--mpnn_type", default=None)
     args = ap.parse_args(argv)
     assert not (args.shmem and args.ddstore), "Cannot use both ddstore and shmem"
     args.mpnn_type = args.global_attn_engine = args.global_attn_type = args.pe_dim = None

@@ -84,6 +84,9 @@ class TrialScheduler:
                     os.makedirs(d, exist_ok=True)
                     env = dict(os.environ, **self.env,
                                HIP_VISIBLE_DEVICES=",".join(str(g) for g in self.slots[s]))
+                    # each trial's torchrun owns its rendezvous port: an inherited port override
+                    # would put concurrent trials on one port
+                    env.pop("HYDRAGNN_MASTER_PORT", None)
                     cmd = create_launch_command(self.script, list(args) + ["--workdir", d], self.g, next(port))
                     log = open(os.path.join(d, "trial.log"), "w")
                     p = subprocess.Popen(cmd, cwd=d, env=env, stdout=log, stderr=subprocess.STDOUT, text=True)

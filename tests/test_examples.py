@@ -183,3 +183,21 @@ def test_smiles_examples(script, tmp_path):
     """SMILES-table examples (RDKit-free reader) train end to end through the low-level API."""
     r = _result(_run(script, ["--num_samples", "48", "--num_epoch", "1"], tmp_path))
     assert r["test_error"] == r["test_error"] and r["num_train"] > 0
+
+
+def test_qm9_hpo_random_search(tmp_path):
+    """examples/qm9_hpo: random search, trials as torchrun children on disjoint slots."""
+    out = _run("qm9_hpo/qm9_hpo.py", ["--trials", "2", "--gpus", "2", "--num_epoch", "1", "--num_samples", "40"],
+               tmp_path, timeout=600)
+    r = _result(out)
+    assert r["n_ok"] == 2 and r["best_test_error"] == r["best_test_error"]
+
+
+def test_multidataset_deepspeed_zero(tmp_path):
+    """examples/multidataset_deepspeed --zero_opt: the GFM driver on ZeRO-1, two ranks."""
+    out = _run("multidataset_deepspeed/train.py", ["--zero_opt", "--num_epoch", "1", "--num_samples", "24",
+                                                   "--prepare_samples", "50"], tmp_path, nproc=2, timeout=600)
+    r = _result(out)
+    assert r["test_error"] == r["test_error"]
+    cfg = json.load(open(os.path.join(str(tmp_path), "deepspeed_derived_config_rank0.json")))
+    assert cfg["NeuralNetwork"]["Training"]["Optimizer"]["use_zero_redundancy"] is True
