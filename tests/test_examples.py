@@ -201,3 +201,13 @@ def test_multidataset_deepspeed_zero(tmp_path):
     assert r["test_error"] == r["test_error"]
     cfg = json.load(open(os.path.join(str(tmp_path), "deepspeed_derived_config_rank0.json")))
     assert cfg["NeuralNetwork"]["Training"]["Optimizer"]["use_zero_redundancy"] is True
+
+
+def test_multidataset_inference_reproduces_test_error(tmp_path):
+    """examples/multidataset/inference.py on a freshly trained GFM log: same test error as training."""
+    tr = _result(_run("multidataset/train.py", ["--adios", "--modelname", "ANI1x", "--num_epoch", "1",
+                                                "--num_samples", "30", "--prepare_samples", "60"], tmp_path))
+    out = _run("multidataset/inference.py", ["--log", "GFM", "--datasets", "ANI1x"], tmp_path)
+    inf = _result(out)
+    assert abs(inf["test_error"] - tr["test_error"]) < 1e-5 * max(1.0, tr["test_error"])
+    assert inf["graphs_per_s"] > 0
