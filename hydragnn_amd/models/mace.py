@@ -193,6 +193,42 @@ class _ScalarLinear(nn.Module):
         return self.lin(x)
 
 
+class _PerNodeMLP(nn.Module):
+    """``mlp_per_node`` MACE read-out (reference ``blocks.py:770-900``, Linear/NonLinear
+    MLPNode with ``num_mlp = num_nodes``): graphs of a fixed size, one MLP per node slot.
+    The first layer is the slot's o3.Linear to scalars, i.e. a linear map of the scalar
+    channels (the only block an irreps -> n x 0e map can use); every layer runs for all
+    slots at once as one batched product over stacked weights [slots, in, out] instead
+    of the reference's per-slot Python loop with index lists."""
+
+    def __init__(self, input_irreps, dims, act, num_nodes):
+        super().__init__()
+        assert num_nodes is not None and num_nodes > 0, "num_nodes must be positive integer for MLP"
+        self.num_nodes = num_nodes
+        self.n_scalar = input_irreps.count(0, 1)
+        self.act = act
+        self.weights = nn.ParameterList()
+        self.biases = nn.ParameterList()
+        fan = [self.n_scalar] + list(dims)
+        for i in range(len(dims)):
+            w = torch.empty(num_nodes, fan[i], fan[i + 1])
+            for k in range(num_nodes):
+                nn.init.kaiming_uniform_(w[k].T, a=5 ** 0.5)
+            self.weights.append(nn.Parameter(w))
+            # the o3.Linear first layer has no bias
+            self.biases.append(nn.Parameter(torch.zeros(num_nodes, fan[i + 1]), requires_grad=i > 0))
+
+    def forward(self, x):
+        nn_ = self.num_nodes
+        G = x.shape[0] // nn_
+        h = x[:, :self.n_scalar].reshape(G, nn_, -1).transpose(0, 1)  # [slots, G, F]
+        # o3.Linear normalisation of the scalar block: 1/sqrt(fan_in)
+        h = torch.baddbmm(self.biases[0].unsqueeze(1), h, self.weights[0]) / self.n_scalar ** 0.5
+        for i in range(1, len(self.weights)):
+            h = torch.baddbmm(self.biases[i].unsqueeze(1), self.act(h), self.weights[i])
+        return h.transpose(0, 1).reshape(G * nn_, -1)
+
+
 class MultiheadDecoderBlock(nn.Module):
     """Linear (intermediate) or non-linear (last) MACE read-out over all heads
     (reference ``blocks.py:417-767``)."""
@@ -235,7 +271,9 @@ class MultiheadDecoderBlock(nn.Module):
                     if a["type"] == "conv":
                         raise ValueError("Node-level convolutional layers are not supported in MACE")
                     if a["type"] == "mlp_per_node":
-                        raise ValueError("mlp_per_node heads are not supported for MACE in this build")
+                        dims = (list(a["dim_headlayers"]) if nonlinear else []) + [head_dims[ih]]
+                        hn[b["type"]] = _PerNodeMLP(input_irreps, dims, act, num_nodes)
+                        continue
                     if nonlinear:
                         dh = a["dim_headlayers"]
                         layers = [_ScalarLinear(input_irreps, dh[0]), act]

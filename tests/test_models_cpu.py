@@ -148,3 +148,39 @@ def test_multibranch_range_decode_matches_mask_decode(node_type):
         slow = m(b)
     for a, c in zip(fast, slow):
         torch.testing.assert_close(a, c)
+
+
+def test_mace_mlp_per_node_head():
+    """MACE node head of type mlp_per_node (fixed-size graphs, one MLP per node slot;
+    reference blocks.py:770-900): shapes, gradients, and slot independence (changing one
+    slot's weights changes only that slot's outputs)."""
+    from hydragnn_amd.data.synthetic import oc20_like
+
+    nn_ = 7
+    s = oc20_like(3, seed=5, radius=5.0, max_neighbours=8, pe_dim=4, min_atoms=nn_, max_atoms=nn_)
+    for g in s:
+        g.edge_attr = torch.ones(g.edge_index.shape[1], 1)
+        g.x = torch.randint(1, 9, (g.x.shape[0], 1)).float()
+    heads = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                             "num_headlayers": 1, "dim_headlayers": [8]}}],
+             "node": [{"type": "branch-0", "architecture": {"num_headlayers": 2, "dim_headlayers": [8, 8],
+                                                            "type": "mlp_per_node"}}]}
+    torch.manual_seed(0)
+    m = create_model("MACE", 1, 12, [1, 1], 0, "", "", 0, ["graph", "node"], heads, "relu", "mse", [1.0, 1.0], 2,
+                     use_gpu=False, radius=5.0, max_neighbours=8, num_radial=5, envelope_exponent=5, max_ell=2,
+                     node_max_ell=1, avg_num_neighbors=5.0, correlation=2, dropout=0.0, num_nodes=nn_)
+    b = collate(s)
+    pred = m(b)
+    assert pred[1].shape == (3 * nn_, 1)
+    sum(p.pow(2).mean() for p in pred).backward()
+    from hydragnn_amd.models.mace import _PerNodeMLP
+
+    heads_pn = [mod for mod in m.modules() if isinstance(mod, _PerNodeMLP)]
+    assert heads_pn and all(w.grad is not None for h in heads_pn for w in h.weights)
+    with torch.no_grad():
+        y0 = m(b)[1].view(3, nn_)
+        for h in heads_pn:
+            h.weights[-1][2].add_(1.0)
+        y1 = m(b)[1].view(3, nn_)
+    changed = (y1 - y0).abs().sum(0) > 0
+    assert changed[2] and not changed[[0, 1, 3, 4, 5, 6]].any()

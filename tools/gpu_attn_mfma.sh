@@ -1,0 +1,12 @@
+#!/bin/bash
+# MFMA attention forward: numerics tests, standalone timing (VALU vs MFMA), headline bench A/B
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "attention" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/attn_tests.log 2>&1
+rc=$?; tail -15 gpurun_out/attn_tests.log; [ $rc -ne 0 ] && exit $rc
+for cfg in "HYDRA_ATTN_MFMA=0" "HYDRA_ATTN_MFMA=1"; do
+  echo "== $cfg"; env $cfg timeout -k 10 120 python3 tools/bench_attn.py 2311 8 8 2>&1 | grep splits || exit 1
+done
+for cfg in "HYDRA_ATTN_MFMA=0" "HYDRA_ATTN_MFMA=1"; do
+  echo "== bench $cfg"; env $cfg timeout -k 10 180 python3 bench.py --steps 30 --warmup 5 2>&1 | tail -1 | cut -c1-220 || exit 1
+done
