@@ -1360,11 +1360,16 @@ static bool attn_v3(int D) {
   }();
   return v && D <= 16;
 }
-// MFMA forward (D = 8) is the default; HYDRA_ATTN_MFMA=0 selects the VALU kernels.
+// MFMA forward (D = 8) is opt-in (HYDRA_ATTN_MFMA=1).  Measured on MI355X at the OC20
+// shape (N 2311, H 8, standalone, rocprofv3): the MFMA kernel itself takes 35 us at 3-6
+// key splits (50 us at 1) plus 5 us for the K/V split pass and 5 us for the combine,
+// against 34-42 us for the whole VALU sk forward; headline step 2.02 vs 2.01 ms.  At
+// D = 8 the matrix work per score is tiny and the VALU still carries the softmax and
+// the fp16 splitting of P, so the matrix cores do not pay for the extra passes.
 static bool attn_mfma() {
   static const bool v = [] {
     const char* e = std::getenv("HYDRA_ATTN_MFMA");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }

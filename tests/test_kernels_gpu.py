@@ -411,8 +411,21 @@ def test_radial_features(E, F, K, L):
 @pytest.mark.parametrize("scope", ["batch", "graph"])
 @pytest.mark.parametrize("mag", [1.0, 30.0])
 def test_attention_mfma_forward_fp32_accuracy(scope, mag):
-    """The MFMA forward (D = 8, two-term fp16 splits) against an fp64 reference: its error must
-    stay at fp32 level (not fp16/bf16 level), including large-magnitude logits."""
+    """The MFMA forward (D = 8, two-term fp16 splits; opt-in HYDRA_ATTN_MFMA=1, run in a
+    subprocess) against an fp64 reference: its error must stay at fp32 level (not fp16/bf16
+    level), including large-magnitude logits."""
+    import os
+    import subprocess
+    import sys
+
+    if os.environ.get("HYDRA_ATTN_MFMA") != "1":
+        code = ("import sys; sys.path.insert(0, '.'); from tests.test_kernels_gpu import "
+                f"test_attention_mfma_forward_fp32_accuracy as t; t({scope!r}, {mag!r}); print('ok')")
+        env = dict(os.environ, HYDRA_ATTN_MFMA="1")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+        return
     from hydragnn_amd import _native
 
     H, D = 8, 8
@@ -438,14 +451,14 @@ def test_attention_mfma_forward_fp32_accuracy(scope, mag):
 
 
 def test_attention_valu_forward_kernels():
-    """HYDRA_ATTN_MFMA=0 (VALU sk forward) and HYDRA_ATTN_V3=1 (v3 kernels) in subprocesses."""
+    """HYDRA_ATTN_MFMA=1 (MFMA forward) and HYDRA_ATTN_V3=1 (v3 kernels) in subprocesses."""
     import subprocess
     import sys
 
     code = ("import torch, sys; sys.path.insert(0, '.'); from tests.test_kernels_gpu import test_attention_key_splits;"
             "[test_attention_key_splits(s, sc) for s in (1, 5) for sc in ('batch', 'graph')]; print('ok')")
     root = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
-    for extra in ({"HYDRA_ATTN_MFMA": "0"}, {"HYDRA_ATTN_MFMA": "0", "HYDRA_ATTN_V3": "1"}):
+    for extra in ({"HYDRA_ATTN_MFMA": "1"}, {"HYDRA_ATTN_MFMA": "0", "HYDRA_ATTN_V3": "1"}):
         env = dict(__import__("os").environ, **extra)
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120, cwd=root)
         assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stderr[-2000:])
