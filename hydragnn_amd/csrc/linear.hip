@@ -430,14 +430,229 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Small-K concat-linear forward for edge-sized rows (fp32):
+//   y[r, f] = b[f] + sum_j sum_k x_j[r, k] W_j[f, k]     (1-3 inputs, sum K <= 188)
+// e.g. the PNAPlus edge term C = r Wr^T + edge_attr Wd^T + bc over ~23k edges, K = 65,
+// F = 64.  The library path (bias broadcast copy + GEMM + addmm) cost ~32 us per layer on
+// MI355X (three launches, an intermediate written and re-read); this is one pass: a
+// 256-thread workgroup stages a 64-row x K tile of the inputs and the transposed
+// K x 64 weight tile in LDS, each thread computes a 4 x 4 block (float4 weight reads,
+// broadcast input reads) and writes 4 float4 rows (coalesced 256 B per row).
+constexpr int kElK = 188;  // (KMAX + 4) floats per staged row
+struct ElArgs {
+  const float* x[3];
+  int ldx[3];
+  const float* w[3];
+  int k[3];
+  int wt;  // 1: w[0] is stored [K, F] (y = x @ W, the dgrad of a linear), single input
+  int nin;
+  const float* b;
+  float* y;
+  int rows, F;
+};
+
+template <int KMAX>
+__global__ void __launch_bounds__(256) edge_linear_fwd_kernel(ElArgs a) {
+  // row stride: float4-aligned, and rows 4 banks apart (XS % 64 == 4) so the four rows a
+  // wave reads per k-step hit disjoint banks
+  constexpr int XS = (KMAX + 63) / 64 * 64 + 4;
+  __shared__ __attribute__((aligned(16))) float Xs[64][XS];
+  __shared__ __attribute__((aligned(16))) float Wt[KMAX][64];
+  const int r0 = blockIdx.x * 64, f0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  // staging: every thread owns one row (r = tid / 4) and a strided set of 4-wide column
+  // groups; the loads of a group batch are all issued before their LDS stores (a
+  // load -> store loop paid one L2 latency per element)
+  const int sr = tid >> 2, sq = tid & 3;
+  int K = 0;
+  for (int j = 0; j < a.nin; ++j) {
+    const int kj = a.k[j];
+    const float* xr = a.x[j] + (int64_t)min(r0 + sr, a.rows - 1) * a.ldx[j];
+    const float* wr = a.w[j] + (int64_t)min(f0 + sr, a.F - 1) * kj;
+    const bool vec = !a.wt && ((kj | a.ldx[j]) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.x[j]) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(a.w[j]) & 15) == 0;
+    if (vec) {
+      const int n4 = kj >> 2;
+      for (int m0 = sq; m0 < n4; m0 += 16) {
+        float4 xv[4], wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = min(m0 + 4 * u, n4 - 1);
+          xv[u] = reinterpret_cast<const float4*>(xr)[m];
+          wv[u] = reinterpret_cast<const float4*>(wr)[m];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = m0 + 4 * u;
+          if (m < n4) {
+            const int c = K + 4 * m;
+            *reinterpret_cast<float4*>(&Xs[sr][c]) = xv[u];
+            Wt[c][sr] = wv[u].x;
+            Wt[c + 1][sr] = wv[u].y;
+            Wt[c + 2][sr] = wv[u].z;
+            Wt[c + 3][sr] = wv[u].w;
+          }
+        }
+      }
+    } else {
+      for (int c0 = sq; c0 < kj; c0 += 32) {
+        float xv[8], wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = min(c0 + 4 * u, kj - 1);
+          xv[u] = xr[c];
+          wv[u] = a.wt ? a.w[j][(int64_t)c * a.F + min(f0 + sr, a.F - 1)] : wr[c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = c0 + 4 * u;
+          if (c < kj) {
+            Xs[sr][K + c] = xv[u];
+            Wt[K + c][sr] = wv[u];
+          }
+        }
+      }
+    }
+    K += kj;
+  }
+  const int K4 = (K + 3) & ~3;
+  for (int idx = tid; idx < 64 * (K4 - K); idx += 256) {  // zero the k tail up to a multiple of 4
+    const int r = idx / (K4 - K), c = K + idx % (K4 - K);
+    Xs[r][c] = 0.f;
+    Wt[c][r] = 0.f;
+  }
+  __syncthreads();
+  const int cg = tid & 15, rg = tid >> 4;  // 4 cols (cg*4..), 4 rows (rg*4..)
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
+  for (int k = 0; k < K4; k += 4) {
+    float4 w[4], x[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) w[kk] = *reinterpret_cast<const float4*>(&Wt[k + kk][cg * 4]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const float4*>(&Xs[rg * 4 + i][k]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        acc[i][0] = fmaf(xv[kk], w[kk].x, acc[i][0]);
+        acc[i][1] = fmaf(xv[kk], w[kk].y, acc[i][1]);
+        acc[i][2] = fmaf(xv[kk], w[kk].z, acc[i][2]);
+        acc[i][3] = fmaf(xv[kk], w[kk].w, acc[i][3]);
+      }
+    }
+  }
+  const int f = f0 + cg * 4;
+  float bb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bb[q] = (a.b != nullptr && f + q < a.F) ? a.b[f + q] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + rg * 4 + i;
+    if (r >= a.rows) continue;
+    float* yr = a.y + (int64_t)r * a.F;
+    if (f + 3 < a.F && (a.F & 3) == 0) {
+      *reinterpret_cast<float4*>(yr + f) =
+          make_float4(acc[i][0] + bb[0], acc[i][1] + bb[1], acc[i][2] + bb[2], acc[i][3] + bb[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (f + q < a.F) yr[f + q] = acc[i][q] + bb[q];
+    }
+  }
+}
+
+static void edge_linear_launch(ElArgs& a, int K, int64_t rows, int64_t F) {
+  const dim3 grid(ceil_div(rows, 64), ceil_div(F, 64));
+  if (K <= 64)  // ~33 KB of LDS: 4 workgroups per CU
+    edge_linear_fwd_kernel<64><<<grid, 256, 0, stream()>>>(a);
+  else if (K <= 128)  // ~66 KB: 2 workgroups per CU (the PNAPlus+GPS edge term, K = 128)
+    edge_linear_fwd_kernel<128><<<grid, 256, 0, stream()>>>(a);
+  else
+    edge_linear_fwd_kernel<kElK><<<grid, 256, 0, stream()>>>(a);
+}
+
+// dX = dY @ W for a linear y = x W^T with W [F, K], dY [rows, F] (row stride any) -> [rows, K]
+at::Tensor edge_linear_dgrad(const at::Tensor& dy, const at::Tensor& W_) {
+  HY_CHECK_CUDA(dy);
+  HY_CHECK_F32(dy);
+  auto W = W_.contiguous();
+  HY_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && W.dim() == 2 && W.size(0) == dy.size(1),
+           "edge_linear_dgrad: shapes");
+  const int64_t rows = dy.size(0), Fin = W.size(0), Kout = W.size(1);
+  HY_CHECK(Fin >= 1 && Fin <= kElK, "edge_linear_dgrad: dY width must be in [1, 188]");
+  auto y = at::empty({rows, Kout}, dy.options());
+  if (rows == 0 || Kout == 0) return y;
+  ElArgs a{};
+  a.nin = 1;
+  a.x[0] = dy.data_ptr<float>();
+  a.ldx[0] = (int)dy.stride(0);
+  a.w[0] = W.data_ptr<float>();
+  a.k[0] = (int)Fin;
+  a.wt = 1;
+  a.y = y.data_ptr<float>();
+  a.rows = (int)rows;
+  a.F = (int)Kout;
+  edge_linear_launch(a, (int)Fin, rows, Kout);
+  return y;
+}
+
+at::Tensor edge_linear_fwd(const std::vector<at::Tensor>& xs, const std::vector<at::Tensor>& ws,
+                           const c10::optional<at::Tensor>& b) {
+  HY_CHECK(!xs.empty() && xs.size() <= 3 && xs.size() == ws.size(), "edge_linear_fwd: 1-3 (x, W) pairs");
+  ElArgs a{};
+  a.nin = (int)xs.size();
+  const int64_t rows = xs[0].size(0);
+  const int64_t F = ws[0].size(0);
+  int K = 0;
+  std::vector<at::Tensor> keep;
+  for (int j = 0; j < a.nin; ++j) {
+    HY_CHECK_CUDA(xs[j]);
+    HY_CHECK_F32(xs[j]);
+    HY_CHECK(xs[j].dim() == 2 && xs[j].size(0) == rows && xs[j].stride(1) == 1, "edge_linear_fwd: x rows");
+    auto w = ws[j].contiguous();
+    keep.push_back(w);
+    HY_CHECK(w.dim() == 2 && w.size(0) == F && w.size(1) == xs[j].size(1), "edge_linear_fwd: W shape");
+    a.x[j] = xs[j].data_ptr<float>();
+    a.ldx[j] = (int)xs[j].stride(0);
+    a.w[j] = w.data_ptr<float>();
+    a.k[j] = (int)w.size(1);
+    K += a.k[j];
+  }
+  HY_CHECK(K >= 1 && K <= kElK, "edge_linear_fwd: total K must be in [1, 188], got ", K);
+  at::Tensor bc;
+  if (b.has_value() && b->defined()) {
+    bc = b->contiguous();
+    HY_CHECK(bc.numel() == F, "edge_linear_fwd: bias");
+    a.b = bc.data_ptr<float>();
+  }
+  auto y = at::empty({rows, F}, xs[0].options());
+  if (rows == 0 || F == 0) return y;
+  a.y = y.data_ptr<float>();
+  a.rows = (int)rows;
+  a.F = (int)F;
+  edge_linear_launch(a, K, rows, F);
+  return y;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("linear_wgrad(Tensor dY, Tensor X, bool with_bias) -> (Tensor, Tensor)");
+  m.def("edge_linear_fwd(Tensor[] xs, Tensor[] ws, Tensor? b) -> Tensor");
+  m.def("edge_linear_dgrad(Tensor dy, Tensor W) -> Tensor");
   m.def("linear_wgrad_grouped(Tensor[] dYs, Tensor[] Xs, Tensor(a!)[] dWs, Tensor(b!)[] dbs, int[] accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("linear_wgrad", hy::linear_wgrad);
+  m.impl("edge_linear_fwd", hy::edge_linear_fwd);
+  m.impl("edge_linear_dgrad", hy::edge_linear_dgrad);
   m.impl("linear_wgrad_grouped", hy::linear_wgrad_grouped);
 }

@@ -462,3 +462,35 @@ def test_attention_valu_forward_kernels():
         env = dict(__import__("os").environ, **extra)
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120, cwd=root)
         assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stderr[-2000:])
+
+
+@pytest.mark.parametrize("shapes,F,rows", [([64, 1], 64, 23117), ([6], 64, 1000), ([3, 5, 7], 100, 130),
+                                           ([124, 64], 96, 777), ([1], 1, 65)])
+def test_edge_linear_fwd(shapes, F, rows):
+    """One-pass small-K concat-linear (csrc/linear.hip) vs fp32 torch, incl. a strided input."""
+    from hydragnn_amd import _native
+
+    torch.manual_seed(rows)
+    big = torch.randn(rows, sum(shapes) + 3, device=DEV)
+    xs, off = [], 0
+    for k in shapes:
+        xs.append(big[:, off:off + k])  # row stride > width (column slices of one buffer)
+        off += k
+    ws = [torch.randn(F, k, device=DEV) for k in shapes]
+    b = torch.randn(F, device=DEV)
+    y = _native.ops().edge_linear_fwd(xs, ws, b)
+    ref = sum(x.double() @ w.double().t() for x, w in zip(xs, ws)) + b.double()
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-4)
+    y0 = _native.ops().edge_linear_fwd(xs, ws, None)
+    torch.testing.assert_close(y0.double(), ref - b.double(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("F,K,rows", [(64, 64, 23117), (64, 1, 999), (100, 37, 130)])
+def test_edge_linear_dgrad(F, K, rows):
+    from hydragnn_amd import _native
+
+    torch.manual_seed(F + K)
+    dy = torch.randn(rows, F + 2, device=DEV)[:, 1:F + 1]  # strided rows
+    W = torch.randn(F, K, device=DEV)
+    out = _native.ops().edge_linear_dgrad(dy, W)
+    torch.testing.assert_close(out.double(), dy.double() @ W.double(), rtol=1e-5, atol=1e-4)

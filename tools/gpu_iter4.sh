@@ -1,0 +1,11 @@
+#!/bin/bash
+# edge linear + wprep: kernel tests, PNA model parity, headline bench + rocprof
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_parity_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/iter4_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/iter4_tests.log; [ $rc -ne 0 ] && exit $rc
+for cfg in "HYDRA_EDGE_LINEAR=0" "HYDRA_EDGE_LINEAR=1"; do
+  echo "== bench $cfg"; env $cfg timeout -k 10 180 python3 bench.py --steps 30 --warmup 5 2>&1 | tail -1 | cut -c1-200 || exit 1
+done
+bash tools/gpu_prof_bench.sh head4
