@@ -66,7 +66,12 @@ def _task_parallel(config, datasets, args):
     from hydragnn_amd.utils.print_utils import setup_log
 
     setup_ddp()
-    bid, group, lists = branch_groups([len(d) for d in datasets])
+    if args.use_devicemesh:
+        from hydragnn_amd.models.multitask import branch_groups_mesh
+
+        bid, group, lists = branch_groups_mesh(len(datasets))
+    else:
+        bid, group, lists = branch_groups([len(d) for d in datasets])
     mine = datasets[bid]
     tr, va, te = split(mine, config["NeuralNetwork"]["Training"]["perc_train"], seed=args.seed)
     proc = SerializedDataLoader(config)
@@ -95,6 +100,8 @@ def main(argv=None):
     ap.add_argument("--num_datasets", type=int, default=None, help="default: number of branches in the config")
     ap.add_argument("--task_parallel", action="store_true")
     ap.add_argument("--nosync", action="store_true")
+    ap.add_argument("--use_devicemesh", action="store_true",
+                    help="task parallel: branch groups from a 2-D device mesh (equal rank split)")
     ap.add_argument("--oversampling", action="store_true")
     ap.add_argument("--oversampling_num_samples", type=int, default=None)
     args = ap.parse_args(argv)

@@ -388,6 +388,19 @@ class DistDataset(AbstractBaseDataset):
             s.x = s.x[:, self.var_config["input_node_features"]]
         return s
 
+    def epoch_begin(self):
+        """Start of a data epoch (reference DDStore ``epoch_begin``: opens the MPI one-sided
+        access epoch).  Shared-memory segments need no fence; remote segments are mapped
+        lazily on first access."""
+        self.epochs = getattr(self, "epochs", 0) + 1
+
+    def epoch_end(self):
+        """End of a data epoch (DDStore ``epoch_end``): unmap the other ranks' segments so
+        the mappings (and their page-cache residency in this process) do not accumulate
+        across epochs; the local segment stays."""
+        for name in [n for n in self.handles if n != self.segname]:
+            self.ops.shm_store_close(self.handles.pop(name))
+
     def close(self):
         for name, h in list(self.handles.items()):
             self.ops.shm_store_close(h)

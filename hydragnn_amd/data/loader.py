@@ -84,27 +84,63 @@ class GraphDataLoader:
         return batch
 
     def __iter__(self):
-        if self.num_workers == 0:
+        nw = self.num_workers
+        if nw == 0 and os.environ.get("HYDRAGNN_CUSTOM_DATALOADER", "0") == "1":
+            nw = 1  # the reference's HydraDataLoader: threaded prefetch even without workers
+        if nw == 0:
             for b in self._batches():
                 yield self._make(b)
             return
-        q = queue.Queue(maxsize=self.prefetch)
-        stop = object()
-
-        def worker(chunks):
-            for b in chunks:
-                q.put(self._make(b))
-            q.put(stop)
-
+        # nw collate threads, worker w builds batches w, w + nw, ...; consumed in order
         batches = list(self._batches())
-        t = threading.Thread(target=worker, args=(batches,), daemon=True)
-        t.start()
-        while True:
-            item = q.get()
-            if item is stop:
-                break
-            yield item
-        t.join()
+        qs = [queue.Queue(maxsize=max(1, self.prefetch // nw + 1)) for _ in range(nw)]
+
+        def worker(w):
+            apply_worker_affinity(w)
+            for k in range(w, len(batches), nw):
+                qs[w].put(self._make(batches[k]))
+
+        ts = [threading.Thread(target=worker, args=(w,), daemon=True) for w in range(nw)]
+        for t in ts:
+            t.start()
+        for k in range(len(batches)):
+            yield qs[k % nw].get()
+        for t in ts:
+            t.join()
+
+
+def parse_omp_places(places):
+    """CPU list of an ``OMP_PLACES`` string such as ``{0:4},{8:4}`` or ``{0,1,2},{5}``."""
+    cpus = []
+    for part in (places or "").replace("},", "}|").split("|"):
+        part = part.strip().strip("{}")
+        if not part:
+            continue
+        if ":" in part:
+            start, n = part.split(":")[:2]
+            cpus += list(range(int(start), int(start) + int(n)))
+        else:
+            cpus += [int(c) for c in part.split(",") if c.strip()]
+    return cpus
+
+
+def apply_worker_affinity(wid):
+    """Pin the calling loader thread to its core window (reference ``HydraDataLoader.worker_init``,
+    ``load_data.py:118-150``): ``HYDRAGNN_AFFINITY_WIDTH`` cores (default 2) starting at
+    ``HYDRAGNN_AFFINITY_OFFSET + width * wid`` of the process's allowed set (or of
+    ``OMP_PLACES`` with ``HYDRAGNN_AFFINITY=OMP``).  Only when HYDRAGNN_AFFINITY is set;
+    returns the applied set (None when unchanged)."""
+    mode = os.environ.get("HYDRAGNN_AFFINITY")
+    if mode is None or not hasattr(os, "sched_setaffinity"):
+        return None
+    width = int(os.environ.get("HYDRAGNN_AFFINITY_WIDTH", "2"))
+    offset = int(os.environ.get("HYDRAGNN_AFFINITY_OFFSET", "0"))
+    cpus = parse_omp_places(os.environ.get("OMP_PLACES")) if mode == "OMP" else sorted(os.sched_getaffinity(0))
+    mask = set(cpus[width * wid + offset:width * (wid + 1) + offset])
+    if not mask:
+        return None
+    os.sched_setaffinity(0, mask)  # tid 0 = this thread
+    return mask
 
 
 class DeviceGraphLoader:

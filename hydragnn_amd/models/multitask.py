@@ -119,6 +119,27 @@ class MultiTaskModelMP(nn.Module):
         return self.module.energy_force_loss(*a, **k)
 
 
+def branch_groups_mesh(num_branches, device_type=None):
+    """Device-mesh variant of :func:`branch_groups` (reference ``examples/multibranch/
+    train.py:216-252``, ``--use_devicemesh``): a 2-D ``init_device_mesh`` of shape
+    (branches, world // branches); the first mesh coordinate is the branch id, the
+    second dimension's group (ranks of one branch) is the branch group.  Equal split,
+    so ``world`` must be a multiple of the branch count.
+
+    Returns (branch_id_of_this_rank, this_branch_group, rank_lists)."""
+    from torch.distributed.device_mesh import init_device_mesh
+
+    world = dist.get_world_size()
+    assert world % num_branches == 0, f"device mesh: world {world} is not a multiple of {num_branches} branches"
+    if device_type is None:
+        device_type = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    mesh = init_device_mesh(device_type, (num_branches, world // num_branches), mesh_dim_names=("branch", "replica"))
+    bid = mesh.get_coordinate()[0]
+    per = world // num_branches
+    lists = [list(range(b * per, (b + 1) * per)) for b in range(num_branches)]
+    return bid, mesh["replica"].get_group(), lists
+
+
 def branch_groups(sizes, world=None, rank=None):
     """Assign ranks to branches proportionally to ``sizes`` (e.g. dataset sizes; every branch
     gets >= 1 rank) and create one process group per branch (reference

@@ -104,6 +104,28 @@ def gather_tensor_ranks(head_values):
     return torch.cat([t[: int(s)] for t, s in zip(lst, sizes)], 0)
 
 
+def _ddstore_epochs(fn):
+    """``HYDRAGNN_USE_ddstore=1``: bracket the pass over a DistDataset-backed loader with the
+    store's ``epoch_begin`` / ``epoch_end`` (reference ``train_validate_test.py:468-472,
+    577-581, 634-638``)."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(loader, *a, **kw):
+        ds = getattr(loader, "dataset", None)
+        use = bool(int(os.getenv("HYDRAGNN_USE_ddstore", "0"))) and hasattr(ds, "epoch_begin")
+        if use:
+            ds.epoch_begin()
+        try:
+            return fn(loader, *a, **kw)
+        finally:
+            if use:
+                ds.epoch_end()
+
+    return wrapped
+
+
+@_ddstore_epochs
 def train(loader, model, opt, verbosity, profiler=None, use_deepspeed=False, compute_grad_energy=False,
           step_engine=None):
     module = _module(model)
@@ -180,6 +202,7 @@ def _eval_batches(loader, nbatch):
 
 
 @torch.no_grad()
+@_ddstore_epochs
 def validate(loader, model, verbosity, reduce_ranks=True, compute_grad_energy=False):
     module = _module(model)
     device = next(module.parameters()).device
@@ -240,6 +263,7 @@ def _dump_samples(records, data, pred, module):
 
 
 @torch.no_grad()
+@_ddstore_epochs
 def test(loader, model, verbosity, reduce_ranks=True, return_samples=True, compute_grad_energy=False):
     """Test-set error (+ per-head true/pred samples).
 

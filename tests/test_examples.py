@@ -211,3 +211,11 @@ def test_multidataset_inference_reproduces_test_error(tmp_path):
     inf = _result(out)
     assert abs(inf["test_error"] - tr["test_error"]) < 1e-5 * max(1.0, tr["test_error"])
     assert inf["graphs_per_s"] > 0
+
+
+def test_multibranch_task_parallel_device_mesh(tmp_path):
+    """--use_devicemesh: branch groups from a 2-D device mesh (2 branches x 2 replicas)."""
+    _run("multibranch/train.py", ["--task_parallel", "--use_devicemesh", "--num_datasets", "2", "--num_samples", "40",
+                                  "--num_epoch", "1"], tmp_path, nproc=4)
+    logs = os.listdir(os.path.join(tmp_path, "logs"))
+    assert sum(1 for d in logs if "_branch" in d) == 2

@@ -64,3 +64,59 @@ def test_hpo_scheduler_two_slots(tmp_path):
                                    fixed_args=["--num_samples", "30", "--num_epoch", "1"])
     assert all(r["returncode"] == 0 for r in res), [open(r["log"]).read()[-2000:] for r in res]
     assert best is not None and val == val
+
+
+def test_loader_threads_affinity_and_custom_flag(monkeypatch):
+    """HYDRAGNN_NUM_WORKERS collate threads keep the batch order; HYDRAGNN_AFFINITY pins
+    each worker thread to its core window (reference HydraDataLoader.worker_init)."""
+    import os
+    import threading
+
+    from hydragnn_amd.data import loader as L
+    from hydragnn_amd.data.synthetic import oc20_like
+
+    samples = oc20_like(10, seed=1, pe_dim=2, min_atoms=4, max_atoms=8)
+    ref = [b.num_graphs for b in L.GraphDataLoader(samples, 3, shuffle=False, num_workers=0)]
+    got = [b.num_graphs for b in L.GraphDataLoader(samples, 3, shuffle=False, num_workers=3)]
+    assert got == ref
+    monkeypatch.setenv("HYDRAGNN_CUSTOM_DATALOADER", "1")
+    assert [b.num_graphs for b in L.GraphDataLoader(samples, 3, shuffle=False, num_workers=0)] == ref
+    assert L.parse_omp_places("{0:2},{4:2}") == [0, 1, 4, 5] and L.parse_omp_places("{1,3},{7}") == [1, 3, 7]
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) >= 2:
+        monkeypatch.setenv("HYDRAGNN_AFFINITY", "1")
+        monkeypatch.setenv("HYDRAGNN_AFFINITY_WIDTH", "1")
+        out = {}
+
+        def run():
+            out["mask"] = L.apply_worker_affinity(1)
+            out["now"] = os.sched_getaffinity(0)
+
+        t = threading.Thread(target=run)
+        t.start()
+        t.join()
+        assert out["mask"] == {allowed[1]} and out["now"] == {allowed[1]}
+        assert sorted(os.sched_getaffinity(0)) == allowed  # the main thread is untouched
+
+
+def test_ddstore_epoch_hooks(monkeypatch):
+    """HYDRAGNN_USE_ddstore=1 brackets train/validate/test passes with the store's
+    epoch_begin / epoch_end (reference train_validate_test.py:468-472)."""
+    from hydragnn_amd.train.train_validate_test import _ddstore_epochs
+
+    calls = []
+
+    class DS:
+        def epoch_begin(self):
+            calls.append("b")
+
+        def epoch_end(self):
+            calls.append("e")
+
+    class Loader:
+        dataset = DS()
+
+    f = _ddstore_epochs(lambda loader, x: calls.append(x) or x)
+    assert f(Loader(), 1) == 1 and calls == [1]
+    monkeypatch.setenv("HYDRAGNN_USE_ddstore", "1")
+    assert f(Loader(), 2) == 2 and calls == [1, "b", 2, "e"]
