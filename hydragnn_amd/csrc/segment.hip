@@ -55,12 +55,29 @@ __device__ __forceinline__ float4 shfl_xor_t<float4>(float4 v, int o) {
 // interleaved row streams per column group, folded by a fixed xor butterfly (deterministic)
 // — so a hub node with 70 in-edges (torch_cluster "index" caps make low-index atoms the
 // source of every neighbourhood) costs ~70/KS dependent loads instead of 70.
-template <int VEC, bool MEAN, int KS>
+//
+// GM = true: gather-multiply-sum  out[n] = sum_e w[row] * x[gidx[row]] (row = perm[e] or e),
+// the CFConv / continuous-filter message + aggregation in one pass (no [E, F] message
+// tensor): x is the node table, w the per-edge filter rows.
+template <typename T>
+__device__ __forceinline__ T vmul(T a, T b);
+template <>
+__device__ __forceinline__ float4 vmul<float4>(float4 a, float4 b) {
+  return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+template <>
+__device__ __forceinline__ float2 vmul<float2>(float2 a, float2 b) { return make_float2(a.x * b.x, a.y * b.y); }
+template <>
+__device__ __forceinline__ float vmul<float>(float a, float b) { return a * b; }
+
+template <int VEC, bool MEAN, int KS, bool GM = false>
 __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ x,
                                                       const int* __restrict__ rowptr,
                                                       const int* __restrict__ perm,
                                                       float* __restrict__ out, int N, int F,
-                                                      int tpr, int rpb) {
+                                                      int tpr, int rpb,
+                                                      const float* __restrict__ w = nullptr,
+                                                      const int* __restrict__ gidx = nullptr) {
   using V = VecT<VEC>;
   using T = typename V::T;
   const int tg = tpr * KS;
@@ -77,12 +94,23 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
     for (; e + KS < end; e += 2 * KS) {
       const int r0 = perm ? perm[e] : e;
       const int r1 = perm ? perm[e + KS] : e + KS;
-      a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
-      a1 = V::add(a1, reinterpret_cast<const T*>(x + (int64_t)r1 * F)[v]);
+      if constexpr (GM) {
+        a0 = V::add(a0, vmul(reinterpret_cast<const T*>(w + (int64_t)r0 * F)[v],
+                             reinterpret_cast<const T*>(x + (int64_t)gidx[r0] * F)[v]));
+        a1 = V::add(a1, vmul(reinterpret_cast<const T*>(w + (int64_t)r1 * F)[v],
+                             reinterpret_cast<const T*>(x + (int64_t)gidx[r1] * F)[v]));
+      } else {
+        a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
+        a1 = V::add(a1, reinterpret_cast<const T*>(x + (int64_t)r1 * F)[v]);
+      }
     }
     if (e < end) {
       const int r0 = perm ? perm[e] : e;
-      a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
+      if constexpr (GM)
+        a0 = V::add(a0, vmul(reinterpret_cast<const T*>(w + (int64_t)r0 * F)[v],
+                             reinterpret_cast<const T*>(x + (int64_t)gidx[r0] * F)[v]));
+      else
+        a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
     }
     T a = V::add(a0, a1);
 #pragma unroll
@@ -154,6 +182,22 @@ __global__ void __launch_bounds__(256) gather_arg_kernel(const float* __restrict
   out[t] = a >= 0 ? x[(int64_t)a * F + (t % F)] : 0.f;
 }
 
+// out[e, :] = x[ia[e], :] * y[ib[e], :]   (the filter gradient of gather-multiply-sum)
+template <int VEC>
+__global__ void __launch_bounds__(256) gather_mul2_kernel(const float* __restrict__ x, const int* __restrict__ ia,
+                                                          const float* __restrict__ y, const int* __restrict__ ib,
+                                                          float* __restrict__ out, int E, int F, int tpr, int rpb) {
+  using T = typename VecT<VEC>::T;
+  const int r = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int c = threadIdx.x % tpr;
+  if (r >= E) return;
+  const int64_t a = ia[r], b = ib[r];
+  const int nv = F / VEC;
+  for (int v = c; v < nv; v += tpr)
+    reinterpret_cast<T*>(out + (int64_t)r * F)[v] =
+        vmul(reinterpret_cast<const T*>(x + a * F)[v], reinterpret_cast<const T*>(y + b * F)[v]);
+}
+
 // ---------------------------------------------------------------- host side
 
 static at::Tensor as2d(const at::Tensor& x) { return x.dim() == 1 ? x.unsqueeze(1) : x; }
@@ -200,6 +244,70 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   }
 #undef HY_SEG_SUM_KS
 #undef HY_SEG_SUM
+  return x_.dim() == 1 ? out.squeeze(1) : out;
+}
+
+// out[n] = sum over the rowptr segment n (rows through perm) of w[row] * x[gidx[row]]
+at::Tensor gather_mul_sum(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& gidx,
+                          const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm, int64_t N) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous(), w = as2d(w_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_F32(w);
+  HY_CHECK_I32(gidx);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(rowptr.numel() == N + 1, "rowptr must have N+1 entries");
+  HY_CHECK(w.size(1) == x.size(1) && gidx.numel() == w.size(0), "gather_mul_sum: shapes");
+  const int F = (int)x.size(1);
+  auto out = at::empty({N, F}, x.options());
+  if (N == 0 || F == 0) return out;
+  const int* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    HY_CHECK_I32(*perm);
+    pp = perm->data_ptr<int>();
+  }
+  const bool v4 = (F % 4 == 0);
+  auto g = row_geom(N, v4 ? F : F * 4);
+  const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);
+  const int rpb = 256 / (g.tpr * ks);
+  const int blocks = (int)std::max<int64_t>(1, (N + rpb - 1) / rpb);
+#define HY_GMS(VEC, KS)                                                                                  \
+  seg_sum_kernel<VEC, false, KS, true><<<blocks, 256, 0, stream()>>>(                                    \
+      x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, out.data_ptr<float>(), (int)N, F, g.tpr, rpb,     \
+      w.data_ptr<float>(), gidx.data_ptr<int>())
+  if (v4) {
+    if (ks == 4) HY_GMS(4, 4); else if (ks == 2) HY_GMS(4, 2); else HY_GMS(4, 1);
+  } else {
+    if (ks == 4) HY_GMS(1, 4); else if (ks == 2) HY_GMS(1, 2); else HY_GMS(1, 1);
+  }
+#undef HY_GMS
+  return x_.dim() == 1 ? out.squeeze(1) : out;
+}
+
+at::Tensor gather_mul2(const at::Tensor& x_, const at::Tensor& ia, const at::Tensor& y_, const at::Tensor& ib) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous(), y = as2d(y_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_F32(y);
+  HY_CHECK_I32(ia);
+  HY_CHECK_I32(ib);
+  HY_CHECK(x.size(1) == y.size(1) && ia.numel() == ib.numel(), "gather_mul2: shapes");
+  const int64_t E = ia.numel();
+  const int F = (int)x.size(1);
+  auto out = at::empty({E, F}, x.options());
+  if (E == 0 || F == 0) return out;
+  const bool v4 = (F % 4 == 0);
+  auto g = row_geom(E, v4 ? F : F * 4);
+  const int rpb = 256 / g.tpr;
+  const int blocks = (int)std::max<int64_t>(1, (E + rpb - 1) / rpb);
+  if (v4)
+    gather_mul2_kernel<4><<<blocks, 256, 0, stream()>>>(x.data_ptr<float>(), ia.data_ptr<int>(), y.data_ptr<float>(),
+                                                        ib.data_ptr<int>(), out.data_ptr<float>(), (int)E, F, g.tpr,
+                                                        rpb);
+  else
+    gather_mul2_kernel<1><<<blocks, 256, 0, stream()>>>(x.data_ptr<float>(), ia.data_ptr<int>(), y.data_ptr<float>(),
+                                                        ib.data_ptr<int>(), out.data_ptr<float>(), (int)E, F, g.tpr,
+                                                        rpb);
   return x_.dim() == 1 ? out.squeeze(1) : out;
 }
 
@@ -280,6 +388,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
   m.def("scatter_arg(Tensor g, Tensor arg, int E) -> Tensor");
   m.def("gather_arg(Tensor x, Tensor arg) -> Tensor");
+  m.def("gather_mul_sum(Tensor x, Tensor w, Tensor gidx, Tensor rowptr, Tensor? perm, int N) -> Tensor");
+  m.def("gather_mul2(Tensor x, Tensor ia, Tensor y, Tensor ib) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
@@ -288,4 +398,6 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("seg_minmax", hy::seg_minmax);
   m.impl("scatter_arg", hy::scatter_arg);
   m.impl("gather_arg", hy::gather_arg);
+  m.impl("gather_mul_sum", hy::gather_mul_sum);
+  m.impl("gather_mul2", hy::gather_mul2);
 }

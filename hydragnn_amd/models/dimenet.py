@@ -191,7 +191,7 @@ class InteractionPPBlock(nn.Module):
         x_kj = self.act(self.lin_kj(x)) * self.lin_rbf2(self.lin_rbf1(rbf))
         x_kj = self.act(self.lin_down(x_kj))
         sbf = self.lin_sbf2(self.lin_sbf1(sbf))
-        x_kj = seg.segment_sum(seg.gather(x_kj, kj_si) * sbf, ji_si)
+        x_kj = seg.gather_mul_sum(x_kj, sbf, kj_si, ji_si)  # triplet gather * sbf -> sum, one pass
         h = x_ji + self.act(self.lin_up(x_kj))
         for layer in self.layers_before_skip:
             h = layer(h)

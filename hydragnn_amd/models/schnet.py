@@ -63,7 +63,7 @@ class CFConv(nn.Module):
             coord_diff, _ = edge_vectors_and_lengths(pos, dst_si, src_si, None, normalize=True, eps=1.0)
             trans = (coord_diff * self.coord_mlp(W)).clamp(-100.0, 100.0)
             pos = pos + seg.segment_mean(trans, src_si)
-        x = seg.segment_sum(seg.gather(x, src_si) * W, dst_si)
+        x = seg.gather_mul_sum(x, W, src_si, dst_si)  # gather * filter -> segment sum, one pass
         return self.lin2(x), pos
 
     def __repr__(self):

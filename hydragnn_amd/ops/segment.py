@@ -196,6 +196,54 @@ class _SegMinMax(torch.autograd.Function):
         return _ScatterArg.apply(g, arg, ctx.E), None, None
 
 
+class _GatherMulSum(torch.autograd.Function):
+    """out[n] = sum_{rows e of segment n of ssi} w[e] * x[gsi.index[e]] — gather, multiply by
+    a per-row filter and segment-sum in one pass (csrc/segment.hip).  The op family
+    {gather_mul_sum, gather_mul2} is closed under differentiation, so any derivative
+    order stays on the native path:
+        d/dw  = gather_mul2(x, gsi, g, ssi)
+        d/dx  = gather_mul_sum(g, w, ssi, gsi)"""
+
+    @staticmethod
+    def forward(ctx, x, w, gsi, ssi):
+        ctx.gsi, ctx.ssi = gsi, ssi
+        ctx.save_for_backward(x, w)
+        if _use_native(x) and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2:
+            return _native.ops().gather_mul_sum(x, w, gsi.index, ssi.rowptr, ssi.perm, ssi.num_segments)
+        return _cpu_segment_sum(x.index_select(0, gsi.index64.to(x.device)) * w, ssi)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        dx = _GatherMulSum.apply(g, w, ctx.ssi, ctx.gsi) if ctx.needs_input_grad[0] else None
+        dw = _GatherMul2.apply(x, ctx.gsi, g, ctx.ssi) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
+class _GatherMul2(torch.autograd.Function):
+    """out[e] = x[asi.index[e]] * y[bsi.index[e]]."""
+
+    @staticmethod
+    def forward(ctx, x, asi, y, bsi):
+        ctx.asi, ctx.bsi = asi, bsi
+        ctx.save_for_backward(x, y)
+        if _use_native(x) and x.dtype == torch.float32 and y.dtype == torch.float32 and x.dim() == 2:
+            return _native.ops().gather_mul2(x, asi.index, y, bsi.index)
+        return x.index_select(0, asi.index64.to(x.device)) * y.index_select(0, bsi.index64.to(y.device))
+
+    @staticmethod
+    def backward(ctx, go):
+        x, y = ctx.saved_tensors
+        dx = _GatherMulSum.apply(y, go, ctx.bsi, ctx.asi) if ctx.needs_input_grad[0] else None
+        dy = _GatherMulSum.apply(x, go, ctx.asi, ctx.bsi) if ctx.needs_input_grad[2] else None
+        return dx, None, dy, None
+
+
+def gather_mul_sum(x, w, gsi, ssi):
+    """``segment_sum(gather(x, gsi) * w, ssi)`` without the [E, F] message tensor."""
+    return _GatherMulSum.apply(x, w, gsi, ssi)
+
+
 # ------------------------------------------------------------------ public API
 
 def gather(x, si):

@@ -494,3 +494,30 @@ def test_edge_linear_dgrad(F, K, rows):
     W = torch.randn(F, K, device=DEV)
     out = _native.ops().edge_linear_dgrad(dy, W)
     torch.testing.assert_close(out.double(), dy.double() @ W.double(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("F", [8, 64, 3])
+def test_gather_mul_sum_native(F):
+    """Native gather-multiply-segment-sum (+ its gradient ops, incl. a double backward) vs the
+    fp32 CPU composite."""
+    from hydragnn_amd.ops import segment as seg
+
+    torch.manual_seed(F)
+    N, E = 300, 2500
+    src = torch.randint(0, N, (E,))
+    dst = torch.sort(torch.randint(0, N, (E,))).values
+    x = torch.randn(N, F)
+    w = torch.randn(E, F)
+
+    def run(dev):
+        gsi = seg.SegIndex.from_index(src.to(dev), N)
+        ssi = seg.SegIndex.from_index(dst.to(dev), N, sorted_=True)
+        xx = x.to(dev).requires_grad_()
+        ww = w.to(dev).requires_grad_()
+        out = seg.gather_mul_sum(xx, ww, gsi, ssi)
+        gx, gw = torch.autograd.grad(out.pow(2).sum(), (xx, ww), create_graph=True)
+        (ggx,) = torch.autograd.grad(gw.pow(2).sum() + gx.sum(), xx)
+        return [t.detach().cpu() for t in (out, gx, gw, ggx)]
+
+    for a, b in zip(run(DEV), run("cpu")):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)

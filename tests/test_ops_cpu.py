@@ -142,3 +142,22 @@ def test_mace_per_layer_correlation():
                      correlation=[3, 2, 1], envelope_exponent=5)
     corrs = [c.prod.symmetric_contractions.contractions[0].correlation for c in m.graph_convs]
     assert corrs == [3, 2, 1]
+
+
+def test_gather_mul_sum_matches_composite_and_twice_differentiable():
+    """gather_mul_sum == segment_sum(gather(x) * w) and its closed derivative family passes
+    gradcheck and gradgradcheck in fp64 (the force-training double backward)."""
+    from hydragnn_amd.ops import segment as seg
+
+    torch.manual_seed(0)
+    N, E, F = 7, 23, 3
+    src = torch.randint(0, N, (E,))
+    dst = torch.sort(torch.randint(0, N, (E,))).values
+    gsi = seg.SegIndex.from_index(src, N)
+    ssi = seg.SegIndex.from_index(dst, N, sorted_=True)
+    x = torch.randn(N, F, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(E, F, dtype=torch.float64, requires_grad=True)
+    ref = torch.zeros(N, F, dtype=torch.float64).index_add_(0, dst, x[src] * w)
+    torch.testing.assert_close(seg.gather_mul_sum(x, w, gsi, ssi), ref)
+    torch.autograd.gradcheck(lambda a, b: seg.gather_mul_sum(a, b, gsi, ssi), (x, w))
+    torch.autograd.gradgradcheck(lambda a, b: seg.gather_mul_sum(a, b, gsi, ssi), (x, w))
