@@ -124,8 +124,8 @@ def test_example_config_keys(config_file):
     with open(os.path.join(ROOT, "examples", config_file)) as f:
         config = json.load(f)
     assert "NeuralNetwork" in config
-    if "Dataset" not in config:  # GFM multidataset configs: the driver supplies the data section
-        assert "multidataset" in config_file, config_file
+    if "Dataset" not in config:  # GFM multidataset / SMILES-table configs: the driver supplies the data section
+        assert any(k in config_file for k in ("multidataset", "ogb", "csce", "dftb", "zinc")), config_file
         config["Dataset"] = {"name": "GFM", "node_features": {}, "graph_features": {}}
     # the reference lists num_nodes too, but its check is a no-op (``for input in category``) and
     # its own lsms.json has no num_nodes; it pins the Dataset keys on lsms.json only; the generator-driven examples
