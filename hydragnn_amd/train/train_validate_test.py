@@ -104,6 +104,24 @@ def gather_tensor_ranks(head_values):
     return torch.cat([t[: int(s)] for t, s in zip(lst, sizes)], 0)
 
 
+def _sync_running_stats(model):
+    """Broadcast rank 0's BatchNorm running statistics (and any other buffers) once per
+    epoch.  torch DDP (the reference's wrapper) broadcasts buffers before every forward;
+    the captured step keeps them rank-local inside the step graph, so without this the
+    ranks' eval-mode statistics would drift apart.  One collective per buffer per epoch."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    if hasattr(model, "head_pg"):  # MultiTaskModelMP: decoder buffers are branch-local
+        return
+    module = _module(model)
+    with torch.no_grad():
+        for b in module.buffers():
+            if b.is_floating_point():
+                dist.broadcast(b, src=0)
+
+
 def _ddstore_epochs(fn):
     """``HYDRAGNN_USE_ddstore=1``: bracket the pass over a DistDataset-backed loader with the
     store's ``epoch_begin`` / ``epoch_end`` (reference ``train_validate_test.py:468-472,
@@ -425,6 +443,7 @@ def train_validate_test(model, optimizer, train_loader, val_loader, test_loader,
             tr.disable()
             if epoch == 0:
                 tr.reset()
+        _sync_running_stats(model)
         t_train = time.time() - t0
         sk = getattr(getattr(optimizer, "optim", optimizer), "skipped_steps", None)
         if sk is not None:

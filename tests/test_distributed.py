@@ -312,6 +312,24 @@ def _task_parallel_body(rank, world):
         torch.testing.assert_close(alldec[r], dec)
 
 
+
+def _bnsync_body(rank, world):
+    """Rank-local BN running statistics are made identical (rank 0's) once per epoch."""
+    from hydragnn_amd.models.layers import BatchNorm
+    from hydragnn_amd.train.train_validate_test import _sync_running_stats
+
+    m = torch.nn.Sequential(BatchNorm(4))
+    m.train()
+    m(torch.randn(16, 4) * (rank + 1) + rank)
+    _sync_running_stats(m)
+    rm = [b.clone() for b in m.buffers() if b.is_floating_point()]
+    for t in rm:
+        allv = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        for v in allv[1:]:
+            torch.testing.assert_close(v, allv[0])
+
+
 # ---------------------------------------------------------------------------- tests
 
 def test_ddp_bucketed_allreduce_matches_full_batch():
@@ -353,3 +371,7 @@ def test_task_parallel_multibranch_four_ranks():
 @pytest.mark.slow
 def test_run_training_two_ranks(tmp_path):
     run_ranks("_train_body", args=(str(tmp_path),))
+
+
+def test_bn_running_stats_synced_per_epoch():
+    run_ranks("_bnsync_body")
