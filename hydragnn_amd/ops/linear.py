@@ -278,6 +278,7 @@ class _EngineSumF32(_TallLinearSum):
 
 
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+BF16_MIN_MACS = int(os.environ.get("HYDRA_BF16_MIN_MACS", str(1 << 26)))
 ENGINE_SUM_MAX_ROWS = 8192  # fp32 multi-input sums above this use the library GEMM pair
 BIG_GEMM = int(os.environ.get("HYDRA_BF16_LIBRARY_MIN", str(1 << 30)))  # M*N*K above which bf16 maps use the library
 
@@ -302,19 +303,26 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     ws = [p[1] for p in pairs]
     engine = len(pairs) <= 3 and _engine_ok(xs + ws) and xs[0].shape[0] > 0 and \
         (residual is None or (residual.is_cuda and residual.dtype == torch.float32))
-    if engine and _state["prec"] == 1 and len(pairs) == 1 and residual is None and \
+    # bf16 precision pays only where the GEMM is big enough to be compute-bound: below
+    # BF16_MIN_MACS (QM9-sized SchNet maps, ~1-20 M MACs) the launch-bound library fp32
+    # path is faster than rounding into the MFMA engine (measured on MI355X: QM9 SchNet
+    # 72.5 k graphs/s fp32 vs 44.9 k with every map on the bf16 engine), and fp32 is the
+    # more accurate of the two, so small maps stay fp32 in bf16 mode
+    bf16 = _state["prec"] == 1 and \
+        sum(x.shape[0] * w.shape[0] * w.shape[1] for x, w in zip(xs, ws)) >= BF16_MIN_MACS
+    if engine and bf16 and len(pairs) == 1 and residual is None and \
             xs[0].shape[0] * ws[0].shape[0] * ws[0].shape[1] >= BIG_GEMM:
         # big dense maps (e.g. the SC25 EGNN's 866-wide edge/node MLPs): the library's tuned
         # 256x256-tile bf16 MFMA GEMMs (hipBLASLt), bf16 in / fp32 accumulate, fp32 out
         y = F.linear(xs[0].to(torch.bfloat16), ws[0].to(torch.bfloat16),
                      None if b is None else b.to(torch.bfloat16)).float()
         return torch.relu(y) if act == ACT_RELU else y
-    if engine and _state["prec"] == 1 and min(min(w.shape) for w in ws) < 16:
+    if engine and bf16 and min(min(w.shape) for w in ws) < 16:
         # very narrow maps (EGNN coord_mlp's 866 -> 1, the 1 -> 866 edge-attribute term): the
         # engine's 32x32 tiles waste >90% of the MFMA work and write the [E, 866] side tile by
         # tile (~600 us per call measured for 36k rows); these are bandwidth-bound, fp32 library
         engine = False
-    if engine and _state["prec"] == 1:
+    if engine and bf16:
         flat = []
         for x, w in zip(xs, ws):
             flat += [_row_contig(x), _row_contig(w)]
