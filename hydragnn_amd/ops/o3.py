@@ -101,8 +101,35 @@ def create_irreps_string(n, ell):
 
 
 # ----------------------------------------------------------------------------- spherical harmonics
+class _SHFused(torch.autograd.Function):
+    """One-launch real SH of [E, 3] edge vectors (csrc/sphharm.hip, l <= 4); the backward
+    re-evaluates the recurrences in forward-mode dual numbers (one launch).  Double
+    backward (force training) takes the composite path via ``composite_mode``."""
+
+    @staticmethod
+    def forward(ctx, vec, lmax, normalize, eps):
+        from .. import _native
+
+        ctx.save_for_backward(vec)
+        ctx.cfg = (lmax, normalize, eps)
+        return _native.ops().sh_fwd(vec, lmax, eps, normalize)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        (vec,) = ctx.saved_tensors
+        lmax, normalize, eps = ctx.cfg
+        return _native.ops().sh_bwd(g, vec, lmax, eps, normalize), None, None, None
+
+
 def spherical_harmonics(lmax, vec, normalize=True, eps=0.0):
     """Real SH, component normalisation, [..., (lmax+1)^2] with m = -l..l per l."""
+    from .pna import fused
+
+    if (vec.is_cuda and vec.dtype == torch.float32 and vec.dim() == 2 and vec.shape[1] == 3 and 0 <= lmax <= 4
+            and fused("sh")):
+        return _SHFused.apply(vec.contiguous(), int(lmax), bool(normalize), float(eps))
     if normalize:
         vec = vec / (torch.linalg.vector_norm(vec, dim=-1, keepdim=True) + eps)
     x, y, z = vec[..., 0], vec[..., 1], vec[..., 2]

@@ -521,3 +521,26 @@ def test_gather_mul_sum_native(F):
 
     for a, b in zip(run(DEV), run("cpu")):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("lmax", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("normalize", [True, False])
+def test_spherical_harmonics_native(lmax, normalize):
+    """One-launch SH kernel (+ dual-number backward) vs the fp64 composite recurrences."""
+    from hydragnn_amd.ops import o3
+
+    torch.manual_seed(lmax)
+    v = torch.randn(3000, 3, dtype=torch.float64)
+    v[0] = 0.0  # zero vector: finite output and gradient with eps
+    eps = 1e-9
+    vd = v.clone().requires_grad_()
+    ref = o3.spherical_harmonics(lmax, vd, normalize=normalize, eps=eps)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    vg = v.float().to(DEV).requires_grad_()
+    out = o3.spherical_harmonics(lmax, vg, normalize=normalize, eps=eps)
+    out.backward(g.float().to(DEV))
+    scale = 1.0 if normalize else float(v.norm(dim=1).max()) ** lmax
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5 * scale)
+    sel = slice(1, None)  # the zero vector's gradient is eps-dominated
+    torch.testing.assert_close(vg.grad.double().cpu()[sel], vd.grad[sel], rtol=1e-3, atol=1e-3 * max(1.0, scale))
