@@ -29,6 +29,7 @@ import torch
 from torch import nn
 
 from ..ops import segment as seg
+from ..ops import geometry as _geo
 from ..ops.geometry import edge_vectors_and_lengths
 from ..ops.pna import degree_scalers, pna_avg_deg
 from .layers import Linear
@@ -36,13 +37,12 @@ from .base import Base
 
 
 def sinc_expansion(edge_dist, num_radial, cutoff):
-    n = torch.arange(num_radial, device=edge_dist.device, dtype=edge_dist.dtype) + 1
-    return torch.sin(edge_dist * n * math.pi / cutoff) / edge_dist
+    """[E, 1] distances -> [E, num_radial] (one launch on the GPU, ops/geometry.py)."""
+    return _geo.sinc_expansion(edge_dist.reshape(-1), num_radial, cutoff)
 
 
 def cosine_cutoff(edge_dist, cutoff):
-    return torch.where(edge_dist < cutoff, 0.5 * (torch.cos(math.pi * edge_dist / cutoff) + 1),
-                       torch.zeros((), device=edge_dist.device, dtype=edge_dist.dtype))
+    return _geo.cosine_cutoff(edge_dist, cutoff, masked=True)
 
 
 class rbf_BasisLayer(nn.Module):

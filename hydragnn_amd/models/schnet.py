@@ -19,7 +19,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops import segment as seg
-from ..ops.geometry import GaussianSmearing, edge_vectors_and_lengths
+from ..ops.geometry import GaussianSmearing, cosine_cutoff, edge_vectors_and_lengths
 from ..ops.radius import interaction_graph
 from .layers import Linear
 from .base import Base
@@ -55,7 +55,7 @@ class CFConv(nn.Module):
         pos = equiv
         g = ctx.layer_graph(self, pos)  # (dst_si, src_si, dist, rbf, edge_attr)
         dst_si, src_si, dist, rbf, eattr = g
-        C = 0.5 * (torch.cos(dist * math.pi / self.cutoff) + 1.0)
+        C = cosine_cutoff(dist, self.cutoff, masked=False)  # one launch on the GPU
         h = rbf if eattr is None else torch.cat([rbf, eattr], -1)
         W = self.nn(h) * C.view(-1, 1)
         x = self.lin1(inv)

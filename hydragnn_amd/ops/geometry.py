@@ -71,6 +71,34 @@ class BesselBasis(torch.nn.Module):
         return self.envelope(d) * torch.sin(self.freq * d)
 
 
+class _EdgeBasis(torch.autograd.Function):
+    """One-launch radial bases (csrc/edge_basis.hip); first derivative native, higher orders
+    via the composite path (``composite_mode``)."""
+
+    @staticmethod
+    def forward(ctx, d, off, K, kind, a, b, masked):
+        from .. import _native
+
+        ctx.save_for_backward(d, off)
+        ctx.cfg = (K, kind, a, b, masked)
+        return _native.ops().edge_basis_fwd(d, off, K, kind, a, b, masked)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        d, off = ctx.saved_tensors
+        K, kind, a, b, masked = ctx.cfg
+        dd = _native.ops().edge_basis_bwd(g, d, off, K, kind, a, b, masked).view(d.shape)
+        return dd, None, None, None, None, None, None
+
+
+def _basis_native(d):
+    from .pna import fused
+
+    return d.is_cuda and d.dtype == torch.float32 and fused("radial")
+
+
 class GaussianSmearing(torch.nn.Module):
     def __init__(self, start=0.0, stop=5.0, num_gaussians=50):
         super().__init__()
@@ -79,16 +107,28 @@ class GaussianSmearing(torch.nn.Module):
         self.register_buffer("offset", offset)
 
     def forward(self, dist):
+        if _basis_native(dist) and self.offset.dtype == torch.float32:
+            return _EdgeBasis.apply(dist.reshape(-1), self.offset, self.offset.numel(), 0, float(self.coeff), 0.0,
+                                    False)
         dist = dist.view(-1, 1) - self.offset.view(1, -1)
         return torch.exp(self.coeff * dist.pow(2))
 
 
 def sinc_expansion(edge_dist, edge_size, cutoff):
     """sin(n*pi*d/c)/d, n=1..edge_size (PAINN)."""
+    if _basis_native(edge_dist) and edge_dist.dim() == 1:
+        return _EdgeBasis.apply(edge_dist, None, int(edge_size), 1, math.pi / cutoff, 0.0, False)
     n = torch.arange(edge_size, device=edge_dist.device, dtype=edge_dist.dtype) + 1
     return torch.sin(edge_dist.unsqueeze(-1) * n * math.pi / cutoff) / edge_dist.unsqueeze(-1)
 
 
-def cosine_cutoff(edge_dist, cutoff):
+def cosine_cutoff(edge_dist, cutoff, masked=True):
+    """0.5 (cos(pi d / c) + 1), zero beyond the cutoff when ``masked`` (PAINN); SchNet's
+    CFConv uses the unmasked form."""
+    if _basis_native(edge_dist):
+        return _EdgeBasis.apply(edge_dist.reshape(-1), None, 1, 2, math.pi / cutoff, float(cutoff),
+                                bool(masked)).view(edge_dist.shape)
+    if not masked:
+        return 0.5 * (torch.cos(edge_dist * math.pi / cutoff) + 1.0)
     return torch.where(edge_dist < cutoff, 0.5 * (torch.cos(math.pi * edge_dist / cutoff) + 1),
                        torch.zeros_like(edge_dist))

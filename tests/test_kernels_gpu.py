@@ -546,3 +546,32 @@ def test_spherical_harmonics_native(lmax, normalize):
     out.backward(g.float().to(DEV))
     sel = slice(1, None)  # the zero vector's gradient is eps-dominated
     torch.testing.assert_close(vg.grad.double().cpu()[sel], vd.grad[sel], rtol=1e-3, atol=1e-3 * max(1.0, scale))
+
+
+def test_edge_basis_native():
+    """Gaussian smearing, sinc expansion and cosine cutoff kernels (fwd + d/dd) vs fp64 torch."""
+    import math
+
+    from hydragnn_amd.ops import geometry as geo
+
+    torch.manual_seed(7)
+    d = torch.rand(5000, dtype=torch.float64) * 6.0 + 0.05
+    gs = geo.GaussianSmearing(0.0, 5.0, 50).to(DEV)
+    cases = [
+        (lambda t: gs(t), lambda t: torch.exp(gs.coeff * (t.view(-1, 1) - gs.offset.double().cpu().view(1, -1)) ** 2)),
+        (lambda t: geo.sinc_expansion(t, 8, 5.0),
+         lambda t: torch.sin(t.unsqueeze(-1) * (torch.arange(8, dtype=t.dtype) + 1) * math.pi / 5.0) / t.unsqueeze(-1)),
+        (lambda t: geo.cosine_cutoff(t, 5.0, masked=True),
+         lambda t: torch.where(t < 5.0, 0.5 * (torch.cos(math.pi * t / 5.0) + 1), torch.zeros_like(t))),
+        (lambda t: geo.cosine_cutoff(t, 5.0, masked=False), lambda t: 0.5 * (torch.cos(math.pi * t / 5.0) + 1)),
+    ]
+    for f_gpu, f_ref in cases:
+        dr = d.clone().requires_grad_()
+        ref = f_ref(dr)
+        g = torch.randn_like(ref)
+        ref.backward(g)
+        dg = d.float().to(DEV).requires_grad_()
+        out = f_gpu(dg)
+        out.backward(g.float().to(DEV))
+        torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(dg.grad.double().cpu(), dr.grad, rtol=1e-3, atol=1e-3)
