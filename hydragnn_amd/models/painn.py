@@ -23,7 +23,6 @@ vec_embed_out: Lin on the channel dim).  Deliberate fix: every Linear acting on 
 vector state (U, V, vec_embed_out) is bias-free here; the reference's biases add the
 same offset to all three Cartesian components and break rotation equivariance.
 """
-import math
 
 import torch
 from torch import nn
