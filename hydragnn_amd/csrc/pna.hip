@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
     const float* __restrict__ C, const float* __restrict__ G, const int* __restrict__ src,
     const int* __restrict__ rowptr, const int* __restrict__ amin, const int* __restrict__ amax,
     float* __restrict__ dpre, float* __restrict__ dG, float* __restrict__ dA, int N, int F, float avg_log,
-    float avg_lin, int tpr, int rpb) {
+    float avg_lin, int tpr, int rpb, int ldda) {
   const int n = blockIdx.x * rpb + threadIdx.x / tpr;
   const int c = threadIdx.x % tpr;
   if (n >= N) return;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
       st<VEC>(dpre + (int64_t)e * F + f0, dp);
       if (dG) st<VEC>(dG + (int64_t)e * F + f0, dg);
     }
-    st<VEC>(dA + (int64_t)n * F + f0, da);
+    st<VEC>(dA + (int64_t)n * ldda + f0, da);
   }
 }
 
@@ -289,7 +289,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_bwd(const at::Tensor& dZ_, co
   const float* Gp = opt_edge_ptr(G_, E, F, "G");
   auto dpre = at::empty({E, F}, Z.options());
   auto dG = Gp ? at::empty({E, F}, Z.options()) : at::empty({0}, Z.options());
-  auto dA = at::empty({N, F}, Z.options());
+  // dA is written into the left half of a [N, 2F] buffer: the caller's seg_sum_out fills the
+  // right half (dB), so dAB needs no concatenation
+  auto dA = at::empty({N, 2 * F}, Z.options());
   if (N == 0) return {dpre, dG, dA};
   const int ldab = (int)AB.stride(0);
   const bool v4 = (F % 4 == 0) && (ldab % 4 == 0) &&
@@ -300,13 +302,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_bwd(const at::Tensor& dZ_, co
         dZ.data_ptr<float>(), Z.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp,
         Gp, src.data_ptr<int>(), rowptr.data_ptr<int>(), amin.data_ptr<int>(),
         amax.data_ptr<int>(), dpre.data_ptr<float>(), Gp ? dG.data_ptr<float>() : nullptr, dA.data_ptr<float>(), N, F,
-        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block, 2 * F);
   else
     pna_bwd_kernel<1><<<g.blocks, 256, 0, stream()>>>(
         dZ.data_ptr<float>(), Z.data_ptr<float>(), AB.data_ptr<float>(), ldab, Cp,
         Gp, src.data_ptr<int>(), rowptr.data_ptr<int>(), amin.data_ptr<int>(),
         amax.data_ptr<int>(), dpre.data_ptr<float>(), Gp ? dG.data_ptr<float>() : nullptr, dA.data_ptr<float>(), N, F,
-        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block);
+        (float)avg_log, (float)avg_lin, g.tpr, g.rows_per_block, 2 * F);
   return {dpre, dG, dA};
 }
 

@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
                                                       float* __restrict__ out, int N, int F,
                                                       int tpr, int rpb,
                                                       const float* __restrict__ w = nullptr,
-                                                      const int* __restrict__ gidx = nullptr) {
+                                                      const int* __restrict__ gidx = nullptr, int ldo = 0) {
   using V = VecT<VEC>;
   using T = typename V::T;
   const int tg = tpr * KS;
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
       else if constexpr (VEC == 2) a = make_float2(a.x * inv, a.y * inv);
       else a *= inv;
     }
-    reinterpret_cast<T*>(out + (int64_t)r * F)[v] = a;
+    reinterpret_cast<T*>(out + (int64_t)r * (ldo > 0 ? ldo : F))[v] = a;
   }
 }
 
@@ -245,6 +245,43 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
 #undef HY_SEG_SUM_KS
 #undef HY_SEG_SUM
   return x_.dim() == 1 ? out.squeeze(1) : out;
+}
+
+// seg_sum into a caller-provided [N, F] view with row stride out.stride(0) (e.g. the right
+// half of a concatenated gradient buffer: no separate torch.cat launch)
+void seg_sum_out(const at::Tensor& x_, const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm,
+                 at::Tensor out) {
+  HY_CHECK_CUDA(x_);
+  auto x = as2d(x_).contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK_F32(out);
+  HY_CHECK_I32(rowptr);
+  const int64_t N = out.size(0);
+  const int F = (int)x.size(1);
+  HY_CHECK(out.dim() == 2 && out.size(1) == F && out.stride(1) == 1 && rowptr.numel() == N + 1,
+           "seg_sum_out: shapes");
+  const int ldo = (int)out.stride(0);
+  if (N == 0 || F == 0) return;
+  const int* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    HY_CHECK_I32(*perm);
+    pp = perm->data_ptr<int>();
+  }
+  const bool v4 = (F % 4 == 0) && (ldo % 4 == 0) && (reinterpret_cast<uintptr_t>(out.data_ptr<float>()) % 16 == 0);
+  auto g = row_geom(N, v4 ? F : F * 4);
+  const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);
+  const int rpb = 256 / (g.tpr * ks);
+  const int blocks = (int)std::max<int64_t>(1, (N + rpb - 1) / rpb);
+#define HY_SSO(VEC, KS)                                                                                          \
+  seg_sum_kernel<VEC, false, KS><<<blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp,  \
+                                                               out.data_ptr<float>(), (int)N, F, g.tpr, rpb,     \
+                                                               nullptr, nullptr, ldo)
+  if (v4) {
+    if (ks == 4) HY_SSO(4, 4); else if (ks == 2) HY_SSO(4, 2); else HY_SSO(4, 1);
+  } else {
+    if (ks == 4) HY_SSO(1, 4); else if (ks == 2) HY_SSO(1, 2); else HY_SSO(1, 1);
+  }
+#undef HY_SSO
 }
 
 // out[n] = sum over the rowptr segment n (rows through perm) of w[row] * x[gidx[row]]
@@ -390,6 +427,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("gather_arg(Tensor x, Tensor arg) -> Tensor");
   m.def("gather_mul_sum(Tensor x, Tensor w, Tensor gidx, Tensor rowptr, Tensor? perm, int N) -> Tensor");
   m.def("gather_mul2(Tensor x, Tensor ia, Tensor y, Tensor ib) -> Tensor");
+  m.def("seg_sum_out(Tensor x, Tensor rowptr, Tensor? perm, Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
@@ -400,4 +438,5 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gather_arg", hy::gather_arg);
   m.impl("gather_mul_sum", hy::gather_mul_sum);
   m.impl("gather_mul2", hy::gather_mul2);
+  m.impl("seg_sum_out", hy::seg_sum_out);
 }

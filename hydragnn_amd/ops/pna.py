@@ -116,10 +116,11 @@ class _PNAFused(torch.autograd.Function):
     def backward(ctx, dZ):
         Z, AB, C, G, amin, amax = ctx.saved_tensors
         F = Z.shape[1] // 17
-        dpre, dG, dA = _native.ops().pna_bwd(dZ, Z, AB, C, G, ctx.src_si.index, ctx.dst_si.rowptr, amin,
-                                             amax, ctx.avg[0], ctx.avg[1])
-        dB = _native.ops().seg_sum(dpre, ctx.src_si.rowptr, ctx.src_si.perm, ctx.src_si.num_segments, False)
-        dAB = torch.cat([dA, dB], dim=1)
+        # pna_bwd writes dA into the left half of a [N, 2F] buffer; dB (segment sum of the edge
+        # gradient over sources) lands in the right half: no concatenation launch
+        dpre, dG, dAB = _native.ops().pna_bwd(dZ, Z, AB, C, G, ctx.src_si.index, ctx.dst_si.rowptr, amin,
+                                              amax, ctx.avg[0], ctx.avg[1])
+        _native.ops().seg_sum_out(dpre, ctx.src_si.rowptr, ctx.src_si.perm, dAB[:, F:])
         dx = dZ[:, :F]
         dC = dpre if ctx.has_C else None
         dG = dG if ctx.has_G else None
