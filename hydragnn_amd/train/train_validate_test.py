@@ -71,8 +71,20 @@ def _loss(module, pred, data, compute_grad_energy):
 
 @torch.no_grad()
 def reduce_values_ranks(local_tensor):
+    """Rank average of an error metric; ``HYDRAGNN_AGGR_BACKEND=mpi`` reduces on the host
+    (gloo host group, reference ``reduce_values_ranks_mpi``), any value other than
+    torch / mpi keeps the rank-local metric."""
+    backend = os.getenv("HYDRAGNN_AGGR_BACKEND", "torch")
+    if backend not in ("torch", "mpi"):
+        return local_tensor
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         t = local_tensor.clone()
+        if backend == "mpi":
+            from ..parallel.distributed import host_group
+
+            h = t.detach().cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=host_group())
+            return h.to(local_tensor.device) / dist.get_world_size()
         if not t.is_cuda and dist.get_backend() != "gloo":
             from ..parallel.distributed import host_group
 

@@ -19,11 +19,23 @@ from .model import update_multibranch_heads
 
 
 def _allreduce(t, op):
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        from ..parallel.distributed import comm_reduce
+    """Cross-rank reduction of a dataset statistic.  ``HYDRAGNN_AGGR_BACKEND`` (reference
+    ``graph_samples_checks_and_updates.py:33,436``, ``model.py:194,208``): "torch" (default,
+    the process group), "mpi" (host-side reduction: the gloo host group, this framework's
+    MPI replacement), anything else: rank-local value (no reduction)."""
+    backend = os.getenv("HYDRAGNN_AGGR_BACKEND", "torch")
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1) or \
+            backend not in ("torch", "mpi"):
+        return t
+    if backend == "mpi":
+        from ..parallel.distributed import host_group
 
-        return comm_reduce(t, op)
-    return t
+        h = t.detach().cpu().clone()
+        dist.all_reduce(h, op=op, group=host_group())
+        return h.to(t.device)
+    from ..parallel.distributed import comm_reduce
+
+    return comm_reduce(t, op)
 
 
 def check_if_graph_size_variable(train_loader, val_loader, test_loader):

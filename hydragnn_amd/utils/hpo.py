@@ -29,6 +29,9 @@ from ..parallel.distributed import parse_slurm_nodelist
 
 
 def read_node_list():
+    """Nodes of the allocation.  The reference decodes ``SLURM_NODELIST`` per machine
+    (``HYDRAGNN_SYSTEM`` = frontier / perlmutter fixed-width prefixes); the bracket-range
+    parser here is prefix- and width-generic, so ``HYDRAGNN_SYSTEM`` needs no value."""
     nl = os.environ.get("SLURM_NODELIST", socket.gethostname())
     nodes = parse_slurm_nodelist(nl)
     return nodes, ",".join(nodes)

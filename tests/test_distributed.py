@@ -330,6 +330,23 @@ def _bnsync_body(rank, world):
             torch.testing.assert_close(v, allv[0])
 
 
+
+def _aggr_backend_body(rank, world):
+    """HYDRAGNN_AGGR_BACKEND: torch / mpi reduce across ranks, anything else stays local."""
+    import os
+
+    from hydragnn_amd.train.train_validate_test import reduce_values_ranks
+    from hydragnn_amd.utils.config_utils import _allreduce
+
+    v = torch.tensor([float(rank + 1)])
+    for backend, want in (("torch", 1.5), ("mpi", 1.5), ("local", float(rank + 1))):
+        os.environ["HYDRAGNN_AGGR_BACKEND"] = backend
+        assert float(reduce_values_ranks(v)) == want, backend
+        s = _allreduce(torch.tensor([rank + 1]), dist.ReduceOp.SUM)
+        assert int(s) == (3 if backend != "local" else rank + 1), backend
+    os.environ.pop("HYDRAGNN_AGGR_BACKEND")
+
+
 # ---------------------------------------------------------------------------- tests
 
 def test_ddp_bucketed_allreduce_matches_full_batch():
@@ -375,3 +392,7 @@ def test_run_training_two_ranks(tmp_path):
 
 def test_bn_running_stats_synced_per_epoch():
     run_ranks("_bnsync_body")
+
+
+def test_aggr_backend_flag():
+    run_ranks("_aggr_backend_body")
