@@ -19,6 +19,7 @@ import numbers
 import numpy as np
 import torch
 
+from .. import _native
 from ..ops.segment import SegIndex
 
 # keys whose leading dim is the edge count
@@ -154,7 +155,11 @@ class GraphBatch(Graph):
         ptr = s["ptr"]
         s["graph_si"] = SegIndex(s["batch"].to(torch.int32), ptr.to(torch.int32), None, G)
         ei = s.get("edge_index")
-        if ei is not None:
+        if ei is not None and ei.device.type == "cpu" and _native.available():
+            drow, srow, sperm = _native.ops().csr_from_edges(ei[0], ei[1], N)
+            s["dst_si"] = SegIndex(ei[1].to(torch.int32), drow, None, N)
+            s["src_si"] = SegIndex(ei[0].to(torch.int32), srow, sperm, N)
+        elif ei is not None:
             src, dst = ei[0], ei[1]
             dev = ei.device
             cnt = torch.bincount(dst, minlength=N)
@@ -235,8 +240,11 @@ def collate(samples, build_csr=True):
             for s in samples:
                 s.sort_edges_by_dst()
             vals = [s.get(k) for s in samples]
-            off = ptr[:-1].tolist()
-            out[k] = torch.cat([v + o for v, o in zip(vals, off)], dim=1) if G > 1 else vals[0].clone()
+            if _native.available() and all(v.device.type == "cpu" for v in vals):
+                out[k] = _native.ops().collate_edges(vals, torch.tensor(nn, dtype=torch.long))
+            else:
+                off = ptr[:-1].tolist()
+                out[k] = torch.cat([v + o for v, o in zip(vals, off)], dim=1) if G > 1 else vals[0].clone()
         elif torch.is_tensor(v0):
             if v0.dim() == 0:
                 out[k] = torch.stack(vals)
