@@ -10,7 +10,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_C.so")
+# HYDRA_NATIVE_LIB: load an alternative build of the library (A/B experiments with
+# compile-time variants); default is the in-tree _C.so
+LIB_PATH = os.environ.get("HYDRA_NATIVE_LIB") or os.path.join(_HERE, "_C.so")
 
 _loaded = False
 _error = None

@@ -69,7 +69,10 @@ __device__ __forceinline__ void set_el<1>(float& v, int, float x) {
 // cover one row (V channels each, coalesced along the row) and the block covers
 // 256/tpr rows per step.  Channel groups beyond tpr*V loop.
 constexpr int kBlk = 256;
-constexpr int kRows = 4;  // rows per thread per slab, all loads issued before use
+#ifndef HY_BN_ROWS
+#define HY_BN_ROWS 4
+#endif
+constexpr int kRows = HY_BN_ROWS;  // rows per thread per slab, all loads issued before use
 
 struct Geo {
   int tpr, rpb, ngrp, slab;  // threads per row, rows per block-step, channel groups (C / V), rows per block
