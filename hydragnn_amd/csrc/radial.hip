@@ -95,13 +95,19 @@ __global__ void __launch_bounds__(256) radial_fwd_kernel(const float* __restrict
 
 // part layout per workgroup: [L][F][2K+1] (dWemb k, dWlin k, dbemb) then [K] dfreq.
 // Block: 64 edges, wave w owns the 16 edges w*16 .. w*16+15; lanes own features.
+// per-layer gradient bases: autograd hands the backward one [E, F] gradient per layer
+// output; reading them in place avoids stacking them into [L, E, F] (two copy launches)
+struct RadPtrs {
+  const float* p[kRadMaxL];
+};
+
 // ONE pass over (R, dR, dG): per (f-chunk, layer) the wave's 16 rows are loaded
 // at once (one latency round); each lane accumulates its features' weight
 // gradients (folded over the 4 waves in LDS, fixed order) AND its share of every
 // edge's input-side term  sum_f dr W_emb[f,k] + dg W_lin[f,k]  in registers
 // (16 x K accumulators), which are wave-reduced once at the end.
 template <int K>
-__global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict__ dR, const float* __restrict__ dG,
+__global__ void __launch_bounds__(256) radial_bwd_kernel(RadPtrs dR, RadPtrs dG,
                                                          const float* __restrict__ R,
                                                          const float* __restrict__ dist, int64_t E,
                                                          const float* __restrict__ freq,
@@ -154,10 +160,10 @@ __global__ void __launch_bounds__(256) radial_bwd_kernel(const float* __restrict
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         const int el = min(w * kPer + i, ne - 1);
-        const int64_t o = ((int64_t)l * E + e0 + el) * F + fc;
-        vr[i] = R[o];
-        vd[i] = dR[o];
-        vg[i] = dG[o];
+        const int64_t ol = (e0 + el) * F + fc;
+        vr[i] = R[(int64_t)l * E * F + ol];
+        vd[i] = dR.p[l][ol];
+        vg[i] = dG.p[l][ol];
       }
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
@@ -309,14 +315,29 @@ std::tuple<at::Tensor, at::Tensor> radial_fwd(const at::Tensor& dist_, const at:
 
 // returns ddist [E], dfreq [K], dWemb [L,F,K], dbemb [L,F], dWlin [L,F,K]
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bwd(
-    const at::Tensor& dR_, const at::Tensor& dG_, const at::Tensor& R, const at::Tensor& dist_,
-    const at::Tensor& freq_, const at::Tensor& Wemb, const at::Tensor& Wlin, double cutoff, int64_t exponent) {
-  auto dR = dR_.contiguous(), dG = dG_.contiguous(), dist = dist_.contiguous(), freq = freq_.contiguous();
+    const std::vector<at::Tensor>& dR_, const std::vector<at::Tensor>& dG_, const at::Tensor& R,
+    const at::Tensor& dist_, const at::Tensor& freq_, const at::Tensor& Wemb, const at::Tensor& Wlin, double cutoff,
+    int64_t exponent) {
+  auto dist = dist_.contiguous(), freq = freq_.contiguous();
   const int64_t E = dist.numel(), K = freq.numel(), L = Wemb.size(0), F = Wemb.size(1);
   HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL, "radial_bwd: 1 <= K <= 8, 1 <= L <= 8");
   check_w(Wemb, L, F, K, "Wemb");
   check_w(Wlin, L, F, K, "Wlin");
-  HY_CHECK(dR.sizes() == R.sizes() && dG.sizes() == R.sizes() && R.is_contiguous(), "radial_bwd: grad shapes");
+  HY_CHECK(R.dim() == 3 && R.size(0) == L && R.size(1) == E && R.size(2) == F && R.is_contiguous(),
+           "radial_bwd: R must be contiguous [L, E, F]");
+  HY_CHECK((int64_t)dR_.size() == L && (int64_t)dG_.size() == L, "radial_bwd: one dR and one dG per layer");
+  std::vector<at::Tensor> keep;  // contiguous copies (normally none) stay alive until launch
+  RadPtrs pr{}, pg{};
+  for (int64_t l = 0; l < L; ++l) {
+    for (int which = 0; which < 2; ++which) {
+      const at::Tensor& t = which == 0 ? dR_[l] : dG_[l];
+      HY_CHECK(t.dim() == 2 && t.size(0) == E && t.size(1) == F && t.scalar_type() == at::kFloat && t.is_cuda(),
+               "radial_bwd: per-layer gradients must be float [E, F] on the GPU");
+      at::Tensor c = t.contiguous();
+      keep.push_back(c);
+      (which == 0 ? pr : pg).p[l] = c.data_ptr<float>();
+    }
+  }
   const int64_t per = 2 * K + 1;
   const int64_t ld = L * F * per + K;
   const int nb = std::max(1, ceil_div(E, kRadBwdEdges));
@@ -326,7 +347,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
   if (E > 0) {
     const auto ev = make_env(cutoff, exponent);
 #define HY_RAD_BWD(KK)                                                                                              \
-  radial_bwd_kernel<KK><<<nb, 256, 0, stream()>>>(dR.data_ptr<float>(), dG.data_ptr<float>(), R.data_ptr<float>(), \
+  radial_bwd_kernel<KK><<<nb, 256, 0, stream()>>>(pr, pg, R.data_ptr<float>(),                                   \
                                                   dist.data_ptr<float>(), E, freq.data_ptr<float>(),               \
                                                   Wemb.data_ptr<float>(), Wlin.data_ptr<float>(), (int)L, (int)F,   \
                                                   ev, ddist.data_ptr<float>(), part.data_ptr<float>(), ld)
@@ -362,7 +383,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "radial_fwd(Tensor dist, Tensor freq, Tensor Wemb, Tensor bemb, Tensor Wlin, float cutoff, int exponent) -> "
       "(Tensor, Tensor)");
   m.def(
-      "radial_bwd(Tensor dR, Tensor dG, Tensor R, Tensor dist, Tensor freq, Tensor Wemb, Tensor Wlin, float cutoff, "
+      "radial_bwd(Tensor[] dR, Tensor[] dG, Tensor R, Tensor dist, Tensor freq, Tensor Wemb, Tensor Wlin, float cutoff, "
       "int exponent) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
 }
 

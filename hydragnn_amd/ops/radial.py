@@ -35,11 +35,11 @@ class _Radial(torch.autograd.Function):
         R, dist, freq, Wemb, Wlin = ctx.saved_tensors
         L = ctx.L
 
-        def stack(gs, like):
-            return torch.stack([g if g is not None else torch.zeros_like(like[0]) for g in gs])
+        def fill(gs):  # per-layer gradients, read in place by the kernel (no stacking copy)
+            return [g if g is not None else torch.zeros_like(R[0]) for g in gs]
 
-        dR = stack(grads[:L], R)
-        dG = stack(grads[L:], R)
+        dR = fill(grads[:L])
+        dG = fill(grads[L:])
         ddist, dfreq, dWemb, dbemb, dWlin = _native.ops().radial_bwd(dR, dG, R, dist, freq, Wemb, Wlin, *ctx.cfg)
         return ddist, dfreq, dWemb, dbemb, dWlin, None, None
 

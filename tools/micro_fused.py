@@ -72,7 +72,7 @@ def main():
     R, Gt = ops.radial_fwd(dist, freq, We, be, Wl, 10.0, 5)
     dR, dG = torch.randn_like(R), torch.randn_like(Gt)
     print(f"radial_fwd {graph_us(lambda: ops.radial_fwd(dist, freq, We, be, Wl, 10.0, 5), reps):8.2f} us", flush=True)
-    print(f"radial_bwd {graph_us(lambda: ops.radial_bwd(dR, dG, R, dist, freq, We, Wl, 10.0, 5), reps):8.2f} us",
+    print(f"radial_bwd {graph_us(lambda: ops.radial_bwd(list(dR.unbind(0)), list(dG.unbind(0)), R, dist, freq, We, Wl, 10.0, 5), reps):8.2f} us",
           flush=True)
     z = torch.zeros(256, device=dev)
     print(f"floor fill(256) {graph_us(lambda: z.fill_(1.0), reps):8.2f} us", flush=True)
