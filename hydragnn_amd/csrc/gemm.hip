@@ -373,15 +373,11 @@ __global__ void __launch_bounds__(256) mm_kernel(MMArgs args_) {
 
 // ----------------------------------------------------------------------------- host side
 
-static at::Tensor& ticket_buffer(const at::Tensor& like, int64_t need) {
-  // zero-initialised once; every reducer resets its tickets, so it stays zero between launches
-  static std::vector<at::Tensor> bufs(64);
-  const int dev = like.get_device();
-  at::Tensor& b = bufs[dev];
-  if (!b.defined() || b.numel() < need) {
-    b = at::zeros({std::max<int64_t>(need, 1 << 16)}, like.options().dtype(at::kInt));
-  }
-  return b;
+// Tickets of one launch: allocated from the caching allocator on the CURRENT stream and
+// zeroed in-stream (a memset node when captured), so two launches on different streams
+// (e.g. the GPS attention branch's backward beside the local MPNN's) never share counters.
+static at::Tensor ticket_buffer(const at::Tensor& like, int64_t need) {
+  return at::zeros({need}, like.options().dtype(at::kInt));
 }
 
 struct ProbBuilder {
@@ -465,7 +461,11 @@ static void launch(ProbBuilder& pb, const at::Tensor& like, bool bf16) {
   at::Tensor ws;
   if (pb.ws_floats > 0) ws = at::empty({pb.ws_floats}, like.options().dtype(at::kFloat));
   int* tk = nullptr;
-  if (pb.tickets > 0) tk = ticket_buffer(like, pb.tickets).data_ptr<int>();
+  at::Tensor tkbuf;
+  if (pb.tickets > 0) {
+    tkbuf = ticket_buffer(like, pb.tickets);
+    tk = tkbuf.data_ptr<int>();
+  }
   for (int q = 0; q < pb.args.nprob; ++q) {
     MMProb& p = pb.args.p[q];
     if (p.split > 1) {

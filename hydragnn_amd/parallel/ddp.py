@@ -206,7 +206,13 @@ class BucketedGradSync:
         order = list(reversed(self.params))
         total = sum(p.numel() for p in order)
         dev = order[0].device
-        self.flat = torch.zeros(total, device=dev, dtype=order[0].dtype)
+        # one extra trailing element: the step guard slot.  It rides in the last bucket, so
+        # after the all-reduce it holds sum_r loss_r / world — finite iff EVERY rank's loss is
+        # finite, the same value on every rank (ranks skip or apply the update together)
+        self.flat = torch.zeros(total + 1, device=dev, dtype=order[0].dtype)
+        self.total = total
+        self.guard = self.flat[total:total + 1]
+        self._loss = None
         nbytes = total * self.flat.element_size()
         if bucket_cap_mb is None:
             # small GNN models: a few buckets so the first all-reduce starts mid-backward; large
@@ -228,6 +234,8 @@ class BucketedGradSync:
             off += p.numel()
         if cur:
             self.buckets.append((start, off, cur))
+        s_, e_, ps_ = self.buckets[-1]
+        self.buckets[-1] = (s_, e_ + 1, ps_)  # + the guard slot
         self.bucket_of = {}
         for bi, (_, _, ps) in enumerate(self.buckets):
             for p in ps:
@@ -257,6 +265,10 @@ class BucketedGradSync:
         self.flat.zero_()
 
     # -- sync protocol: begin() before backward, finish() after it
+    def set_loss(self, loss):
+        """The step's loss: packed into the guard slot with the last bucket."""
+        self._loss = loss
+
     def begin(self):
         # HYDRA_GRADSYNC_FORCE=1 exercises the collective path on a 1-rank group (tests)
         self.active = self.world > 1 or (dist.is_initialized() and os.environ.get("HYDRA_GRADSYNC_FORCE") == "1")
@@ -288,6 +300,10 @@ class BucketedGradSync:
         s, e, ps = self.buckets[bi]
         gs = [p.grad.reshape(-1) if p.grad is not None else
               torch.zeros(p.numel(), device=self.flat.device, dtype=self.flat.dtype) for p in ps]
+        if e == self.total + 1:
+            loss = self._loss
+            gs.append(loss.detach().reshape(1).to(self.flat.dtype) if loss is not None else
+                      torch.zeros(1, device=self.flat.device, dtype=self.flat.dtype))
         out = self.flat[s:e]
         if len(gs) == 1:
             out.copy_(gs[0])

@@ -77,13 +77,43 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
 
     # ------------------------------------------------------------------ step
     def _pack_grads(self):
-        for p in self.all_params:
-            if p.grad is None:
-                continue
+        """Copy every local gradient into ``flat_grad``; slices of parameters without a
+        gradient this step are ZEROED (never left over from an earlier step).  Returns the
+        per-parameter "has a gradient" flags (float, one per parameter)."""
+        used = torch.zeros(len(self.all_params), device=self.flat.device, dtype=self.flat.dtype)
+        for i, p in enumerate(self.all_params):
             o = self.offset[p]
             view = self.flat_grad[o:o + p.numel()]
+            if p.grad is None:
+                view.zero_()
+                continue
+            used[i] = 1.0
             if p.grad.data_ptr() != view.data_ptr():
                 view.copy_(p.grad.reshape(-1))
+        return used
+
+    def _unused(self, used):
+        """Parameters with no gradient on ANY rank (the reference's per-parameter ZeRO and
+        torch optimizers skip them: no weight decay, no moment update)."""
+        if self.world > 1 and self.reduce_grads:
+            dist.all_reduce(used, group=self.group)
+        flags = used.tolist()
+        return [p for p, f in zip(self.all_params, flags) if f == 0.0]
+
+    def _frozen_slices(self, unused):
+        """(lo, hi) ranges of this rank's shard that belong to globally unused parameters."""
+        lo0 = self.rank * self.S
+        out = []
+        for p in unused:
+            a = max(self.offset[p], lo0)
+            b = min(self.offset[p] + p.numel(), lo0 + self.S)
+            if a < b:
+                out.append((a - lo0, b - lo0))
+        return out
+
+    def _shard_state(self):
+        st = self.optim.state.get(self.shard, {}) if self.optim is not None else {}
+        return [t for t in st.values() if torch.is_tensor(t) and t.numel() == self.S]
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -92,28 +122,41 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
             for g in self.optim.param_groups:
                 g["lr"] = self.param_groups[0]["lr"]
         if self.elementwise:
-            self._pack_grads()
+            used = self._pack_grads()
             lo = self.rank * self.S
             if self.world > 1 and self.reduce_grads:
                 if _gloo(self.group):
-                    dist.all_reduce(self.flat_grad, group=self.group)
-                    self.shard.grad.copy_(self.flat_grad[lo:lo + self.S])
+                    # reduce a copy: flat_grad keeps only this step's local gradients
+                    red = self.flat_grad.clone()
+                    dist.all_reduce(red, group=self.group)
+                    self.shard.grad.copy_(red[lo:lo + self.S])
                 else:
                     dist.reduce_scatter_tensor(self.shard.grad, self.flat_grad, group=self.group)
                 self.shard.grad.mul_(1.0 / self.world)
             else:
                 self.shard.grad.copy_(self.flat_grad[lo:lo + self.S])
+            frozen = self._frozen_slices(self._unused(used))
+            saved = []
+            if frozen:
+                for a, b in frozen:
+                    saved.append([self.shard.data[a:b].clone()] + [t[a:b].clone() for t in self._shard_state()])
             self.optim.step()
+            for (a, b), vals in zip(frozen, saved):
+                self.shard.data[a:b].copy_(vals[0])
+                for t, v in zip(self._shard_state(), vals[1:]):
+                    t[a:b].copy_(v)
             if self.world > 1:
                 self._all_gather_flat()
             return loss
         if self.world > 1 and self.reduce_grads:
-            self._pack_grads()
-            dist.all_reduce(self.flat_grad, group=self.group)
-            self.flat_grad.mul_(1.0 / self.world)
+            used = self._pack_grads()
+            red = self.flat_grad.clone() if _gloo(self.group) else self.flat_grad
+            dist.all_reduce(red, group=self.group)
+            red.mul_(1.0 / self.world)
+            unused = {id(p) for p in self._unused(used)}
             for p in self.all_params:
                 o = self.offset[p]
-                p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+                p.grad = None if id(p) in unused else red[o:o + p.numel()].view_as(p)
         if self.optim is not None:
             self.optim.step()
         if self.world > 1:
@@ -172,8 +215,22 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
         return [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
 
     def load_state_dict(self, state):
+        layout = state.get("layout", "param")
+        mine_layout = "flat" if self.elementwise else "param"
+        if layout != mine_layout:
+            raise ValueError(f"ZeRO checkpoint layout '{layout}' does not match this optimizer's '{mine_layout}'")
         shards = state.get("shards", [])
-        if self.optim is not None:
-            mine = shards[self.rank] if len(shards) == self.world else (shards[0] if shards else None)
+        if shards and len(shards) not in (1, self.world):
+            raise ValueError(f"ZeRO checkpoint holds {len(shards)} shards; this run has world size {self.world}")
+        if self.elementwise and shards and len(shards) != self.world:
+            raise ValueError("flat-layout ZeRO state is sharded by world size: re-shard from a consolidated "
+                             f"checkpoint of world size {self.world}")
+        if self.optim is not None and shards:
+            mine = shards[self.rank] if len(shards) == self.world else shards[0]
             if mine is not None:
+                if self.elementwise:
+                    for st in mine.get("state", {}).values():
+                        for t in st.values():
+                            if torch.is_tensor(t) and t.dim() == 1 and t.numel() not in (1, self.S):
+                                raise ValueError(f"ZeRO shard state of length {t.numel()} != shard size {self.S}")
                 self.optim.load_state_dict(mine)

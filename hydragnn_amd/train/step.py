@@ -261,6 +261,7 @@ class TrainStep:
         # at the end of backward (ops/linear.py); their grad hooks (bucket all-reduces) fire then
         defer = self.sync is not None or self.flat_grads is not None
         if self.sync is not None:
+            self.sync.set_loss(loss)
             if sync:
                 self.sync.begin()
             with deferred_wgrad(defer):
@@ -347,11 +348,24 @@ class TrainStep:
         return loss.detach(), [t.detach() for t in tasks]
 
     def _set_guard(self, loss):
-        """NaN/Inf step guard: optimizers that support it skip the update on the device."""
+        """NaN/Inf step guard: optimizers that support it skip the update on the device.
+
+        The guard must be the SAME value on every rank: gradients are all-reduced, so one
+        rank's NaN reaches every rank's gradients.  The captured path uses the all-reduced
+        guard slot of the gradient buffer (sum of the ranks' losses); the eager DDP path
+        all-reduces a copy of the loss."""
+        g = loss.detach()
+        if self.sync is not None:
+            g = self.sync.guard
+        elif self.world > 1 and isinstance(self.model, DistributedDataParallel):
+            import torch.distributed as dist
+
+            g = g.reshape(1).clone()
+            dist.all_reduce(g, group=self.model.process_group)
         if hasattr(self.opt, "guard"):
-            self.opt.guard = loss.detach()
+            self.opt.guard = g
         elif hasattr(getattr(self.opt, "optim", None), "guard"):  # ZeRO wrapper
-            self.opt.optim.guard = loss.detach()
+            self.opt.optim.guard = g
 
     def _opt_state_tensors(self):
         out = []

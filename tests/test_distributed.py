@@ -164,6 +164,40 @@ def _trainstep_body(rank, world):
     assert torch.equal(allg[0], allg[1]), "averaged gradients differ across ranks"
 
 
+def _nan_guard_body(rank, world):
+    """One rank's NaN loss must make EVERY rank skip the update (the all-reduced gradient
+    carries the NaN to all ranks): parameters stay bit-identical across ranks and
+    unchanged; the next finite step updates all ranks together."""
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.train.step import TrainStep
+
+    samples, model = _store_model()
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])
+    step = TrainStep(model, lr=1e-2, mode="graph", world=world, node_bucket=64, edge_bucket=512)
+    step.prepare(store, 4)
+    orig = step._loss
+    poison = {"on": True}
+
+    def _loss(batch):
+        loss, tasks = orig(batch)
+        if poison["on"] and rank == 1:
+            loss = loss * float("nan")
+        return loss, tasks
+
+    step._loss = _loss
+    p0 = torch.cat([p.detach().reshape(-1) for p in step.module.parameters()]).clone()
+    step(store, [4 * rank + k for k in range(4)])
+    p1 = torch.cat([p.detach().reshape(-1) for p in step.module.parameters()])
+    assert torch.equal(p0, p1), "a rank applied the update of a step with a non-finite loss"
+    poison["on"] = False
+    step(store, [4 * rank + k for k in range(4)])
+    p2 = torch.cat([p.detach().reshape(-1) for p in step.module.parameters()])
+    assert not torch.equal(p1, p2) and torch.isfinite(p2).all()
+    allp = [torch.empty_like(p2) for _ in range(world)]
+    dist.all_gather(allp, p2)
+    assert torch.equal(allp[0], allp[1]), "ranks diverged after a guarded step"
+
+
 def _zero_body(rank, world):
     from hydragnn_amd.parallel.zero import ZeroRedundancyOptimizer
 
@@ -200,6 +234,50 @@ def _zero_body(rank, world):
         opt.step()
     for a, b in zip(sh.parameters(), ref.parameters()):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def _zero_unused_body(rank, world):
+    """A head used only on alternating steps (multibranch batches missing a branch): its
+    stale gradient must never be re-applied, and while it has no gradient on any rank it
+    gets no update at all (no weight decay / moments), as with per-parameter optimizers.
+    Per-parameter ownership matches torch AdamW exactly; the flat layout shares one step
+    counter per shard (bias correction), so there the skipped parameter is checked to be
+    frozen on its skipped steps and every other parameter to match exactly."""
+    from hydragnn_amd.parallel.zero import ZeroRedundancyOptimizer
+
+    for elementwise in (True, False):
+        for reduce in (False, True):
+            torch.manual_seed(11)
+            ref, sh = _mlp(), _mlp()
+            sh.load_state_dict(ref.state_dict())
+            mk = lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.1)  # noqa: E731
+            opt_ref = mk(ref.parameters())
+            opt = ZeroRedundancyOptimizer(list(sh.parameters()), mk, reduce_grads=reduce, elementwise=elementwise)
+            nparam = len(list(ref.parameters()))
+            for it in range(6):
+                g = [[torch.randn_like(p) for p in ref.parameters()] for _ in range(world)]
+                skip = it % 2 == 1  # the last bias ("a branch head") has no gradient on odd steps
+                for i, p in enumerate(ref.parameters()):
+                    p.grad = None if (skip and i == nparam - 1) else (
+                        sum(g[r][i] for r in range(world)) / world if reduce else g[0][i].clone())
+                for i, p in enumerate(sh.parameters()):
+                    p.grad = None if (skip and i == nparam - 1) else (g[rank][i].clone() if reduce else g[0][i].clone())
+                before = list(sh.parameters())[-1].detach().clone()
+                opt_ref.step()
+                opt.step()
+                if skip:
+                    assert torch.equal(list(sh.parameters())[-1], before), "unused parameter was updated"
+                opt_ref.zero_grad(set_to_none=True)
+                opt.zero_grad(set_to_none=True)
+            pairs = list(zip(sh.parameters(), ref.parameters()))
+            if elementwise:
+                pairs = pairs[:-1]
+            for a, b in pairs:
+                torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+            st = opt.state_dict()
+            bad = dict(st, layout="param" if elementwise else "flat")
+            with pytest.raises(ValueError):
+                opt.load_state_dict(bad)
 
 
 def _syncbn_body(rank, world):
@@ -363,6 +441,14 @@ def test_bucketed_grad_sync_matches_rank_average():
 
 def test_zero1_matches_adamw():
     run_ranks("_zero_body")
+
+
+def test_nan_guard_is_global():
+    run_ranks("_nan_guard_body")
+
+
+def test_zero1_unused_parameters():
+    run_ranks("_zero_unused_body")
 
 
 def test_syncbatchnorm_matches_full_batch():
