@@ -265,7 +265,7 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
 // table) and ONE reduce launch sums the slab partials in a fixed order and writes or
 // accumulates into the gradient tensors.  Replaces 2 launches per linear (~33 pairs per
 // GPS+PNAPlus step) with 2 per step, and the merged grid fills the chip.
-constexpr int kWgMaxP = 24;
+constexpr int kWgMaxP = 40;  // 40 x 88 B of kernel arguments (< 4 KB)
 constexpr int kWgMaxSlabs = 64;
 
 struct WgProb {

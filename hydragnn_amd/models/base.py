@@ -286,6 +286,9 @@ class Base(nn.Module):
         keep = data.get("node_mask")  # statically padded batch: keep dummy rows at zero
         if keep is not None:
             inv = _zero_rows(inv, keep)
+        fused = self._fused_encode(inv, equiv, ctx)
+        if fused is not None:
+            return fused
         for conv, bn in zip(self.graph_convs, self.feature_layers):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
             if isinstance(self.activation_function, torch.nn.ReLU) and isinstance(bn, BatchNorm):
@@ -297,6 +300,11 @@ class Base(nn.Module):
             if keep is not None:
                 inv = _zero_rows(inv, keep)
         return inv, equiv, ctx
+
+    def _fused_encode(self, inv, equiv, ctx):
+        """Stacks with a whole-encoder fused GPU path return (inv, equiv, ctx) here; None
+        runs the layer-by-layer module path."""
+        return None
 
     def _branch_ids(self, data):
         """Branch ids present in the batch, known on the host; ``None`` for a statically

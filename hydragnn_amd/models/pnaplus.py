@@ -130,6 +130,15 @@ class PNAPlusStack(Base):
             ctx.rbf = self.rbf(dist)
         return x, pos, ctx
 
+    def _fused_encode(self, inv, equiv, ctx):
+        # GPS + PNAPlus training on the GPU: the whole conv stack in one autograd function
+        # over csrc/gps_fused.hip (ops/gps_encoder.py)
+        from ..ops import gps_encoder
+
+        if self.use_global_attn and gps_encoder.eligible(self, inv, ctx):
+            return gps_encoder.encode(self, inv, ctx), equiv, ctx
+        return None
+
     def _stack_convs(self):
         out = []
         for c in self.graph_convs:

@@ -1,0 +1,334 @@
+"""Fused GPS(PNAPlus) encoder: the whole conv stack as ONE autograd function over the
+kernels of ``csrc/gps_fused.hip`` (plus the PNA, attention, edge-linear and weight-prep
+kernels it shares with the unfused path).
+
+Reference computation per layer (``globalAtt/gps.py:103-152`` around
+``PNAPlusStack.py:228-279``, then ``Base.py:466``)::
+
+    h_att = BN2(drop(MHA(x)) + x)
+    h_loc = BN1(drop(lin(post_nn(PNA(x)))) + x)
+    out   = h_loc + h_att
+    z3    = drop(W2 drop(relu(W1 out + b1)) + b2) + out
+    x'    = relu(BN4(BN3(z3)))            (rows >= num_valid -> 0)
+
+Kernel schedule per layer (forward): wprep, node GEMM [AB | qkv] (+ previous layer's
+BN3/BN4 finalise + apply in its prologue), {side stream: attention, o-proj + BN2 stats},
+edge linear, PNA aggregate, post/lin GEMM chain + BN1 stats, {join} BN1/BN2 apply + MLP
+chain + BN3 stats.  Backward mirrors it (mlp, {side: BN2 + o-proj dgrad, attention},
+BN1 + lin/post dgrad, PNA, edge dgrad, {join} node dgrad + previous pair statistics), with
+every weight gradient of the stack in ONE grouped launch pair at the end.
+
+BN4 o BN3 is a single per-column affine map: BN4's batch statistics are derived from
+BN3's (mean4 = beta3, var4 = gamma3^2 var3 / (var3 + eps3)), and its backward is closed-
+form (``csrc/gps_fused.hip``, "BN3 -> BN4 pair").  Mathematically identical to the
+reference; numerically equal to fp32 rounding.
+
+Used in GPU training mode when every layer matches the pattern (``eligible``); CPU,
+eval, double-backward (composite mode) and any other configuration run the module path.
+``HYDRA_UNFUSED=gpsfused`` switches it off.
+"""
+import torch
+
+from .. import _native
+from . import pna as _mode
+from . import streams as _streams
+
+NREP = 8
+SITES = 11  # fwd BN1 (2) + BN2 (2) + BN3 (2) + bwd pair (2) + bwd BN1/BN2 (3)
+NSAVED = 7
+
+
+def _bn(m):
+    return m.module if hasattr(m, "module") else m
+
+
+def _bn_ok(m, F):
+    b = _bn(m)
+    return (isinstance(b, torch.nn.BatchNorm1d) and b.affine and b.momentum is not None and b.training
+            and b.num_features == F)
+
+
+def eligible(model, x, ctx):
+    """True when the fused encoder reproduces ``Base.encode`` for this model and batch."""
+    from ..models.gps import GPSConv, MultiheadAttention
+    from ..models.pnaplus import PNAConvFused
+    from ..ops.attention import segment_attention  # noqa: F401
+
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and _mode.fused("gpsfused")
+            and _mode.fused("attn") and _mode.fused("pna") and model.training):
+        return False
+    F = x.shape[1]
+    if F not in (32, 64) or model.conv_checkpointing:
+        return False
+    if not isinstance(model.activation_function, torch.nn.ReLU):
+        return False
+    rad = ctx.get("radial")
+    if rad is None or ctx.get("edge_attr") is None or ctx.edge_attr.shape[1] + F > 188:
+        return False
+    if ctx.dst_si is None or ctx.dst_si.perm is not None or ctx.get("attn_seg_id") is None:
+        return False
+    for conv, bn in zip(model.graph_convs, model.feature_layers):
+        if not isinstance(conv, GPSConv) or not isinstance(conv.attn, MultiheadAttention):
+            return False
+        c = conv.conv
+        if not (isinstance(c, PNAConvFused) and c.plus and c.edge_dim is not None and id(c) in rad):
+            return False
+        if c.F_in != F or c.F_out != F or not hasattr(c, "edge_encoder"):
+            return False
+        if not isinstance(conv.mlp[1], torch.nn.ReLU):
+            return False
+        if any(n is None or not _bn_ok(n, F) for n in (conv.norm1, conv.norm2, conv.norm3)) or not _bn_ok(bn, F):
+            return False
+        D = F // conv.heads
+        if D not in (4, 8, 16, 32, 64) or conv.attn.in_proj_bias is None:
+            return False
+    return True
+
+
+def _layer_params(conv, bn4):
+    c = conv.conv
+    at = conv.attn
+    n1, n2, n3, n4 = _bn(conv.norm1), _bn(conv.norm2), _bn(conv.norm3), _bn(bn4)
+    lin1, _, _, lin2, _ = conv.mlp
+    return [at.in_proj_weight, at.in_proj_bias, at.out_proj.weight, at.out_proj.bias,
+            c.pre_nns[0][0].weight, c.pre_nns[0][0].bias, c.edge_encoder.weight, c.edge_encoder.bias,
+            c.post_nns[0][0].weight, c.post_nns[0][0].bias, c.lin.weight, c.lin.bias,
+            n1.weight, n1.bias, n2.weight, n2.bias, n3.weight, n3.bias, n4.weight, n4.bias,
+            lin1.weight, lin1.bias, lin2.weight, lin2.bias]
+
+
+NP = 24
+
+
+class _Cfg:
+    pass
+
+
+def encode(model, x0, ctx):
+    """Run the fused encoder: returns x_L (the input of the decoder heads)."""
+    from . import rng as _rng
+    from .attention import _SPLITS, _max_span
+
+    cfg = _Cfg()
+    convs = list(model.graph_convs)
+    cfg.L = len(convs)
+    cfg.F = x0.shape[1]
+    cfg.bns = [(_bn(c.norm1), _bn(c.norm2), _bn(c.norm3), _bn(b)) for c, b in zip(convs, model.feature_layers)]
+    cfg.salts = [list(c._salts) for c in convs]
+    cfg.p = float(convs[0].dropout) if model.training else 0.0
+    cfg.rng = _rng.counter(x0.device) if cfg.p > 0 else None
+    cfg.heads = convs[0].heads
+    cfg.scale = 1.0 / float(cfg.F // cfg.heads) ** 0.5
+    cfg.sid, cfg.sptr = ctx.attn_seg_id, ctx.attn_seg_ptr
+    cfg.span = _max_span(x0.shape[0], cfg.sptr)
+    cfg.splits = _SPLITS
+    cfg.dst, cfg.src = ctx.dst_si, ctx.src_si
+    cfg.avg = [(float(c.conv.avg_deg["log"]), float(c.conv.avg_deg["lin"])) for c in convs]
+    nv = ctx.get("num_valid")
+    if nv is not None:
+        from .norm import _as_nv
+
+        nv = _as_nv(nv, x0.device)
+    cfg.nv = nv
+    cfg.side = _streams.enabled(x0)
+    flat = []
+    for c in convs:
+        r, G = ctx.radial[id(c.conv)]
+        flat += [r.contiguous(), G.contiguous()]
+    for c, b in zip(convs, model.feature_layers):
+        flat += _layer_params(c, b)
+    return _GPSEncoder.apply(cfg, x0.contiguous(), ctx.edge_attr.contiguous(), *flat)
+
+
+class _Side:
+    """Fork/join of the attention branch onto the cached side stream (capture-safe)."""
+
+    def __init__(self, dev, on):
+        self.on = on
+        if on:
+            self.main = torch.cuda.current_stream(dev)
+            self.side = _streams.side_stream(dev)
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            self._c = torch.cuda.stream(self.side)
+            self._c.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._c.__exit__(*exc)
+        return False
+
+    def used(self, *ts):  # main-stream tensors read on the side stream
+        if self.on:
+            for t in ts:
+                if t is not None:
+                    t.record_stream(self.side)
+
+    def join(self, *ts):  # side-stream results read on the main stream
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in ts:
+                if t is not None:
+                    t.record_stream(self.main)
+
+
+def _bn_state(b):
+    track = b.track_running_stats and b.running_mean is not None
+    return ((b.running_mean if track else None), (b.running_var if track else None),
+            (b.num_batches_tracked if track and b.num_batches_tracked is not None else None),
+            float(b.momentum), float(b.eps))
+
+
+class _GPSEncoder(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, x0, e, *flat):
+        ops = _native.ops()
+        L, F = cfg.L, cfg.F
+        radial = flat[:2 * L]
+        prm = [flat[2 * L + NP * l: 2 * L + NP * (l + 1)] for l in range(L)]
+        dev = x0.device
+        acc = torch.empty(L, NREP * SITES * F, device=dev, dtype=torch.float64)
+        saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
+        nv, rng, p = cfg.nv, cfg.rng, cfg.p
+        st = []
+        z3 = None
+        for l in range(L):
+            (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
+             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2) = prm[l]
+            r, G = radial[2 * l], radial[2 * l + 1]
+            s0, s1, s2, s3 = cfg.salts[l]
+            Wab, Wr, Wd, bc = ops.pna_wprep_fwd(Wpre, bpre, Wenc, benc)
+            if l == 0:
+                x, AB, qkv = ops.gf_node_fwd(x0, Wab, Win, bin_, nv, None, None, [], None, None, None, None, None,
+                                             None, 0.0, 0.0, 0.0, 0.0, acc)
+            else:
+                _, _, n3p, n4p = cfg.bns[l - 1]
+                rm3, rv3, nb3, m3, e3 = _bn_state(n3p)
+                rm4, rv4, nb4, m4, e4 = _bn_state(n4p)
+                pp = prm[l - 1]
+                x, AB, qkv = ops.gf_node_fwd(z3, Wab, Win, bin_, nv, acc[l - 1], saved[l - 1],
+                                             [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3, rm4, rv4, nb4,
+                                             m3, e3, m4, e4, None)
+            side = _Side(dev, cfg.side)
+            with side:
+                side.used(qkv, x)
+                O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
+                z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
+            C = ops.edge_linear_fwd([r, e], [Wr, Wd], bc)
+            Z, amin, amax = ops.pna_fwd(x, AB, C, G, cfg.src.index, cfg.dst.rowptr, cfg.avg[l][0], cfg.avg[l][1])
+            pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
+            side.join(O, LSE, z2)
+            n1, n2, _, _ = cfg.bns[l]
+            rm1, rv1, nb1, m1, e1 = _bn_state(n1)
+            rm2, rv2, nb2, m2, e2 = _bn_state(n2)
+            out, md, z3 = ops.gf_mlp_fwd(z1, z2, acc[l], saved[l], [g1, b1n, g2, b2n], rm1, rv1, nb1, rm2, rv2, nb2,
+                                         m1, e1, m2, e2, W1, b1, W2, b2, rng, s2, s3, p, nv)
+            st.append(dict(x=x, AB=AB, qkv=qkv, O=O, LSE=LSE, z2=z2, C=C, Z=Z, amin=amin, amax=amax, p=pl, z1=z1,
+                           out=out, md=md, z3=z3, Wab=Wab, Wr=Wr, Wd=Wd))
+        _, _, n3, n4 = cfg.bns[L - 1]
+        rm3, rv3, nb3, m3, e3 = _bn_state(n3)
+        rm4, rv4, nb4, m4, e4 = _bn_state(n4)
+        pp = prm[L - 1]
+        xL = ops.gf_final_fwd(z3, acc[L - 1], saved[L - 1], [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3, rm4, rv4,
+                              nb4, m3, e3, m4, e4, nv)
+        ctx.cfg = cfg
+        ctx.st = st
+        ctx.acc, ctx.saved = acc, saved
+        ctx.save_for_backward(x0, e, xL, *flat)
+        return xL
+
+    @staticmethod
+    def backward(ctx, dxL):
+        ops = _native.ops()
+        cfg = ctx.cfg
+        L, F = cfg.L, cfg.F
+        x0, e, xL, *flat = ctx.saved_tensors
+        radial = flat[:2 * L]
+        prm = [flat[2 * L + NP * l: 2 * L + NP * (l + 1)] for l in range(L)]
+        acc, saved, st = ctx.acc, ctx.saved, ctx.st
+        nv, rng, p = cfg.nv, cfg.rng, cfg.p
+        dev = x0.device
+        g = ops.gf_pair_stats_bwd(dxL, xL, st[L - 1]["z3"], saved[L - 1], acc[L - 1], nv)
+        empty = torch.empty(0, device=dev, dtype=torch.float32)
+        dys, xs, dws, dbs = [], [], [], []
+
+        def item(dy, x, W, with_bias):
+            dW = torch.empty(W.shape, device=dev, dtype=torch.float32)
+            db = torch.empty(W.shape[0], device=dev, dtype=torch.float32) if with_bias else None
+            dys.append(dy)
+            xs.append(x)
+            dws.append(dW)
+            dbs.append(db if db is not None else empty)
+            return dW, db
+
+        grads = [None] * len(flat)
+        de = None
+        dx0 = None
+        wg = []  # per layer: (dWab, (dWr, dbc), dWd)
+        for l in reversed(range(L)):
+            s = st[l]
+            (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
+             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2) = prm[l]
+            s0, s1, s2, s3 = cfg.salts[l]
+            n1, n2, n3, n4 = cfg.bns[l]
+            dg, dpre, dout, dw3, db3, dw4, db4 = ops.gf_mlp_bwd(g, s["z3"], acc[l], saved[l], g3, g4, float(n3.eps),
+                                                               float(n4.eps), s["md"], W2, W1, s["z1"], s["z2"], rng,
+                                                               s2, s3, p, nv)
+            side = _Side(dev, cfg.side)
+            with side:
+                side.used(dout)
+                dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
+                dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span,
+                                    cfg.splits)
+            dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
+                                                         nv)
+            dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], radial[2 * l + 1], cfg.src.index, cfg.dst.rowptr,
+                                      s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
+            ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
+            dr = dE @ s["Wr"]
+            de = dE @ s["Wd"] if de is None else torch.addmm(de, dE, s["Wd"])
+            side.join(dz2, da, dO, dqkv, dw2n, db2n)
+            if l > 0:
+                sp = st[l - 1]
+                g = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], sp["z3"], saved[l - 1], acc[l - 1],
+                                    nv)
+            else:
+                dx0 = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], None, None, None, nv)
+            base = 2 * L + NP * l
+            grads[2 * l] = dr
+            grads[2 * l + 1] = dG
+            gw = {}
+            gw["Win"] = item(dqkv, s["x"], Win, True)
+            gw["Wo"] = item(da, s["O"], Wo, True)
+            gw["Wab"] = item(dAB, s["x"], s["Wab"], False)
+            gw["Wr"] = item(dE, radial[2 * l], s["Wr"], True)
+            gw["Wd"] = item(dE, e, s["Wd"], False)
+            gw["Wpost"] = item(dp, s["Z"], Wpost, True)
+            gw["Wlin"] = item(dq, s["p"], Wlin, True)
+            gw["W1"] = item(dpre, s["out"], W1, True)
+            gw["W2"] = item(dg, s["md"], W2, True)
+            wg.append((l, gw))
+            grads[base + 12], grads[base + 13] = dw1n, db1n
+            grads[base + 14], grads[base + 15] = dw2n, db2n
+            grads[base + 16], grads[base + 17] = dw3, db3
+            grads[base + 18], grads[base + 19] = dw4, db4
+        # every weight gradient of the stack: one grouped launch pair
+        ops.linear_wgrad_grouped(dys, xs, dws, dbs, [0] * len(dys))
+        for l, gw in wg:
+            base = 2 * L + NP * l
+            Wpre, Wenc, benc = prm[l][4], prm[l][6], prm[l][7]
+            dWpre, dbpre, dWenc, dbenc = ops.pna_wprep_bwd(gw["Wab"][0], gw["Wr"][0], gw["Wd"][0], gw["Wr"][1], Wpre,
+                                                           Wenc, benc)
+            grads[base + 0], grads[base + 1] = gw["Win"]
+            grads[base + 2], grads[base + 3] = gw["Wo"]
+            grads[base + 4], grads[base + 5] = dWpre, dbpre
+            grads[base + 6], grads[base + 7] = dWenc, dbenc
+            grads[base + 8], grads[base + 9] = gw["Wpost"]
+            grads[base + 10], grads[base + 11] = gw["Wlin"]
+            grads[base + 20], grads[base + 21] = gw["W1"]
+            grads[base + 22], grads[base + 23] = gw["W2"]
+        ctx.st = None
+        return (None, dx0, de, *grads)
