@@ -201,7 +201,9 @@ struct NodeFwd {
   const float* bin;     // [3F]
   float* x;             // [N, F] out
   float* AB;            // [N, 2F] out
-  float* qkv;           // [N, 3F] out
+  float* qkv;           // [N, 3F] out (or null: packed attention operands instead)
+  float* pk[6];         // Q, K, V in the pair / quad layouts of csrc/attention8.hip (8-wide heads)
+  int Nq;               // packed row count (N rounded up to 16)
   const int* nvp;
   int N;
   double* zero_buf;     // accumulators to clear (layer 0) or null
@@ -255,6 +257,23 @@ __global__ void __launch_bounds__(256) node_fwd_kernel(NodeFwd a) {
     f4v acc = tile_mma<true>(xs, LD, W, F, 0, F, 0);
     const int col = ab ? n0 + i : n0 - 2 * F + i;
     const float bias = ab ? 0.f : a.bin[col];
+    if (!ab && a.qkv == nullptr) {
+      // packed attention operands: which = Q/K/V, head h, lane d (rows up to Nq: padding rows
+      // hold the bias, finite)
+      const int which = col / F, hd = col % F, h = hd >> 3, d = hd & 7;
+      float* pr = a.pk[2 * which];
+      float* qd = a.pk[2 * which + 1];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * g + r;
+        if (row < a.Nq) {
+          const float v = acc[r] + bias;
+          pr[((int64_t)h * a.Nq + row) * 8 + 2 * (d & 3) + (d >> 2)] = v;
+          qd[(((int64_t)h * (a.Nq >> 2) + (row >> 2)) * 8 + d) * 4 + (row & 3)] = v;
+        }
+      }
+      continue;
+    }
     float* out = ab ? a.AB : a.qkv;
     const int ldo = ab ? 2 * F : 3 * F;
 #pragma unroll
@@ -916,6 +935,136 @@ __global__ void __launch_bounds__(256) node_bwd_kernel(NodeBwd a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Edge rows (E ~ 10 x N): the PNAPlus edge term C = r Wr^T + e Wd^T + bc and its dgrad
+// dr = dC Wr (optionally masked by r > 0, the ReLU of the radial embedding) and
+// de (+)= dC Wd, accumulated in place over the layers (one launch each way per layer,
+// replacing GEMM + addmm + copy library calls).
+struct EdgeFwd {
+  const float* r;   // [E, F]
+  const float* e;   // [E, D]
+  const float* Wr;  // [F, F]
+  const float* Wd;  // [F, D]
+  const float* bc;  // [F]
+  float* C;         // [E, F]
+  int E;
+};
+
+template <int F, int D>
+__global__ void __launch_bounds__(256) edge_fwd_kernel(EdgeFwd a) {
+  constexpr int K = F + D, LD = K + 4;
+  __shared__ __attribute__((aligned(16))) float xs[BM * LD];
+  const int row0 = blockIdx.x * BM;
+  for (int idx = threadIdx.x; idx < BM * K / 4; idx += 256) {
+    const int rr = idx / (K / 4), c = (idx % (K / 4)) * 4, row = row0 + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < a.E)
+      v = c < F ? *reinterpret_cast<const float4*>(a.r + (int64_t)row * F + c)
+                : *reinterpret_cast<const float4*>(a.e + (int64_t)row * D + (c - F));
+    *reinterpret_cast<float4*>(xs + rr * LD + c) = v;
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  for (int t = w; t < F / 16; t += 4) {
+    const int n0 = 16 * t, col = n0 + i;
+    f4v acc = tile_mma<true>(xs, LD, a.Wr + (int64_t)n0 * F, F, 0, F, 0);
+    acc += tile_mma<true>(xs + F, LD, a.Wd + (int64_t)n0 * D, D, 0, D, 0);
+    const float bias = a.bc[col];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * g + r;
+      if (row < a.E) a.C[(int64_t)row * F + col] = acc[r] + bias;
+    }
+  }
+}
+
+struct EdgeBwd {
+  const float* dC;   // [E, F]
+  const float* Wr;   // [F, F]
+  const float* Wd;   // [F, D]
+  const float* rmask;  // [E, F] or null: dr *= (rmask > 0)
+  float* dr;         // [E, F]
+  float* de;         // [E, D]
+  int accumulate;    // de += (else =)
+  int E;
+  // optional radial-basis gradient: drbf (+)= dr Wemb + dG Wlin  ([E, K], K <= 16)
+  const float* dG;   // [E, F]
+  const float* Wemb; // [F, K]
+  const float* Wlin; // [F, K]
+  float* drbf;
+  int K;
+  int rbf_acc;
+};
+
+template <int F, int D>
+__global__ void __launch_bounds__(256) edge_bwd_kernel(EdgeBwd a) {
+  constexpr int LD = F + 4, LD2 = 2 * F + 4;
+  __shared__ __attribute__((aligned(16))) float gs[BM * LD];
+  __shared__ __attribute__((aligned(16))) float rs[BM * LD2];  // [dr masked | dG] for drbf
+  const int row0 = blockIdx.x * BM;
+  for (int idx = threadIdx.x; idx < BM * F / 4; idx += 256) {
+    const int rr = idx / (F / 4), c = (idx % (F / 4)) * 4, row = row0 + rr;
+    *reinterpret_cast<float4*>(gs + rr * LD + c) =
+        row < a.E ? *reinterpret_cast<const float4*>(a.dC + (int64_t)row * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  constexpr int T = (F + D) / 16;
+  for (int t = w; t < T; t += 4) {
+    const int n0 = 16 * t;
+    const bool isr = n0 < F;
+    const int col = (isr ? n0 : n0 - F) + i;
+    f4v acc = isr ? tile_mma<false>(gs, LD, a.Wr, F, 0, F, n0) : tile_mma<false>(gs, LD, a.Wd, D, 0, F, n0 - F);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * g + r;
+      if (row >= a.E) continue;
+      if (isr) {
+        const int64_t o = (int64_t)row * F + col;
+        const float v = (a.rmask == nullptr || a.rmask[o] > 0.f) ? acc[r] : 0.f;
+        a.dr[o] = v;
+        rs[(4 * g + r) * LD2 + col] = v;
+      } else {
+        const int64_t o = (int64_t)row * D + col;
+        a.de[o] = a.accumulate ? a.de[o] + acc[r] : acc[r];
+      }
+    }
+  }
+  if (a.drbf == nullptr) return;
+  // rows past E were skipped above: keep their LDS rows zero
+  for (int idx = threadIdx.x; idx < BM * F; idx += 256) {
+    const int rr = idx / F, c = idx % F, row = row0 + rr;
+    rs[rr * LD2 + F + c] = row < a.E ? a.dG[(int64_t)row * F + c] : 0.f;
+    if (row >= a.E) rs[rr * LD2 + c] = 0.f;
+  }
+  __syncthreads();
+  if (w == 0) {
+    f4v acc = f4z();
+    for (int kb = 0; kb < 2 * F; kb += 16) {
+      const float4 xa = *reinterpret_cast<const float4*>(rs + i * LD2 + kb + 4 * g);
+      const int k = kb + 4 * g;
+      const float* Wsrc = k < F ? a.Wemb + (int64_t)k * a.K : a.Wlin + (int64_t)(k - F) * a.K;
+      const bool ok = i < a.K;
+      const float b0 = ok ? Wsrc[i] : 0.f, b1 = ok ? Wsrc[a.K + i] : 0.f;
+      const float b2 = ok ? Wsrc[2 * a.K + i] : 0.f, b3 = ok ? Wsrc[3 * a.K + i] : 0.f;
+      acc = mfma(xa.x, b0, acc);
+      acc = mfma(xa.y, b1, acc);
+      acc = mfma(xa.z, b2, acc);
+      acc = mfma(xa.w, b3, acc);
+    }
+    if (i < a.K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * g + r;
+        if (row < a.E) {
+          float* o = a.drbf + (int64_t)row * a.K + i;
+          *o = a.rbf_acc ? *o + acc[r] : acc[r];
+        }
+      }
+    }
+  }
+}
+
 // ====================================================================================
 // host side
 static Drop mk_drop(const c10::optional<at::Tensor>& rng, int64_t salt, double p) {
@@ -981,15 +1130,33 @@ std::vector<at::Tensor> gf_node_fwd(const at::Tensor& src, const at::Tensor& Wab
                                     const c10::optional<at::Tensor>& rv3, const c10::optional<at::Tensor>& nbt3,
                                     const c10::optional<at::Tensor>& rm4, const c10::optional<at::Tensor>& rv4,
                                     const c10::optional<at::Tensor>& nbt4, double mom3, double eps3, double mom4,
-                                    double eps4, const c10::optional<at::Tensor>& zero_buf) {
+                                    double eps4, const c10::optional<at::Tensor>& zero_buf, bool packed) {
   const int64_t N = src.size(0), F = src.size(1);
   chk(src, N, F, "src");
   chk(Wab, 2 * F, F, "Wab");
   chk(Win, 3 * F, F, "Win");
-  auto x = at::empty({N, F}, src.options()), AB = at::empty({N, 2 * F}, src.options()),
-       qkv = at::empty({N, 3 * F}, src.options());
-  if (N == 0) return {x, AB, qkv};
+  auto x = at::empty({N, F}, src.options()), AB = at::empty({N, 2 * F}, src.options());
+  const int64_t H8 = F / 8, Nq = (N + 15) / 16 * 16;
+  std::vector<at::Tensor> pk;
+  at::Tensor qkv;
+  if (packed) {
+    HY_CHECK(F % 8 == 0, "gf_node_fwd: packed attention operands need 8-wide heads");
+    for (int j = 0; j < 3; ++j) {
+      pk.push_back(at::empty({H8, Nq, 8}, src.options()));
+      pk.push_back(at::empty({H8, Nq / 4, 8, 4}, src.options()));
+    }
+  } else {
+    qkv = at::empty({N, 3 * F}, src.options());
+  }
+  std::vector<at::Tensor> ret = {x, AB};
+  if (packed)
+    ret.insert(ret.end(), pk.begin(), pk.end());
+  else
+    ret.push_back(qkv);
+  if (N == 0) return ret;
   NodeFwd a{};
+  a.Nq = (int)Nq;
+  for (int j = 0; j < 6; ++j) a.pk[j] = packed ? pk[j].data_ptr<float>() : nullptr;
   a.src = src.data_ptr<float>();
   a.has_prev = prev_acc.has_value() && prev_acc->defined();
   if (a.has_prev) {
@@ -1004,13 +1171,13 @@ std::vector<at::Tensor> gf_node_fwd(const at::Tensor& src, const at::Tensor& Wab
   a.bin = bin.data_ptr<float>();
   a.x = x.data_ptr<float>();
   a.AB = AB.data_ptr<float>();
-  a.qkv = qkv.data_ptr<float>();
+  a.qkv = packed ? nullptr : qkv.data_ptr<float>();
   a.nvp = nvptr(nv);
   a.N = (int)N;
   a.zero_buf = optp<double>(zero_buf);
   a.zero_n = a.zero_buf ? zero_buf->numel() : 0;
-  HY_GF_DISPATCH(F, node_fwd_kernel, ceil_div(N, BM), 256, a);
-  return {x, AB, qkv};
+  HY_GF_DISPATCH(F, node_fwd_kernel, ceil_div(Nq, BM), 256, a);
+  return ret;
 }
 
 at::Tensor gf_oproj_fwd(const at::Tensor& o, const at::Tensor& Wo, const at::Tensor& bo, const at::Tensor& x,
@@ -1109,6 +1276,77 @@ at::Tensor gf_final_fwd(const at::Tensor& z3, const at::Tensor& acc, const at::T
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(N * F / 4, 256), 1024));
   HY_GF_DISPATCH(F, final_fwd_kernel, blocks, 256, a);
   return x;
+}
+
+#define HY_GF_EDGE(F, D, KERN, GRID, ARGS)                                          \
+  do {                                                                              \
+    if ((F) == 64 && (D) == 64)                                                     \
+      KERN<64, 64><<<(GRID), 256, 0, stream()>>>(ARGS);                             \
+    else if ((F) == 32 && (D) == 32)                                                \
+      KERN<32, 32><<<(GRID), 256, 0, stream()>>>(ARGS);                             \
+    else                                                                            \
+      HY_CHECK(false, "gps_fused edge kernels: (F, D) = (64, 64) or (32, 32)");     \
+  } while (0)
+
+at::Tensor gf_edge_fwd(const at::Tensor& r, const at::Tensor& e, const at::Tensor& Wr, const at::Tensor& Wd,
+                       const at::Tensor& bc) {
+  const int64_t E = r.size(0), F = r.size(1), D = e.size(1);
+  chk(r, E, F, "r");
+  chk(e, E, D, "e");
+  chk(Wr, F, F, "Wr");
+  chk(Wd, F, D, "Wd");
+  auto C = at::empty({E, F}, r.options());
+  if (E == 0) return C;
+  EdgeFwd a{r.data_ptr<float>(), e.data_ptr<float>(), Wr.data_ptr<float>(), Wd.data_ptr<float>(),
+            bc.data_ptr<float>(), C.data_ptr<float>(), (int)E};
+  HY_GF_EDGE(F, D, edge_fwd_kernel, ceil_div(E, BM), a);
+  return C;
+}
+
+// dr = dC Wr (* [rmask > 0]); de = dC Wd, or de += dC Wd in place when de_acc is given
+std::vector<at::Tensor> gf_edge_bwd(const at::Tensor& dC_, const at::Tensor& Wr, const at::Tensor& Wd,
+                                    const c10::optional<at::Tensor>& rmask, const c10::optional<at::Tensor>& de_acc,
+                                    const c10::optional<at::Tensor>& dG, const c10::optional<at::Tensor>& Wemb,
+                                    const c10::optional<at::Tensor>& Wlin, const c10::optional<at::Tensor>& drbf_acc,
+                                    int64_t K) {
+  at::Tensor dC = dC_.contiguous();
+  const int64_t E = dC.size(0), F = dC.size(1), D = Wd.size(1);
+  chk(Wr, F, F, "Wr");
+  chk(Wd, F, D, "Wd");
+  auto dr = at::empty({E, F}, dC.options());
+  const bool acc = de_acc.has_value() && de_acc->defined();
+  at::Tensor de = acc ? *de_acc : at::empty({E, D}, dC.options());
+  if (acc) chk(de, E, D, "de");
+  const bool want_rbf = K > 0;
+  const bool racc = drbf_acc.has_value() && drbf_acc->defined();
+  at::Tensor drbf = racc ? *drbf_acc : (want_rbf ? at::empty({E, K}, dC.options()) : at::empty({0}, dC.options()));
+  if (want_rbf) {
+    HY_CHECK(K <= 16 && dG.has_value() && Wemb.has_value() && Wlin.has_value(), "gf_edge_bwd: radial operands");
+    chk(*dG, E, F, "dG");
+    chk(*Wemb, F, K, "Wemb");
+    chk(*Wlin, F, K, "Wlin");
+    chk(drbf, E, K, "drbf");
+  }
+  if (E == 0) return {dr, de, drbf};
+  EdgeBwd a{};
+  a.dC = dC.data_ptr<float>();
+  a.Wr = Wr.data_ptr<float>();
+  a.Wd = Wd.data_ptr<float>();
+  a.rmask = optp<float>(rmask);
+  a.dr = dr.data_ptr<float>();
+  a.de = de.data_ptr<float>();
+  a.accumulate = acc ? 1 : 0;
+  a.E = (int)E;
+  if (want_rbf) {
+    a.dG = dG->data_ptr<float>();
+    a.Wemb = Wemb->data_ptr<float>();
+    a.Wlin = Wlin->data_ptr<float>();
+    a.drbf = drbf.data_ptr<float>();
+    a.K = (int)K;
+    a.rbf_acc = racc ? 1 : 0;
+  }
+  HY_GF_EDGE(F, D, edge_bwd_kernel, ceil_div(E, BM), a);
+  return {dr, de, drbf};
 }
 
 // ---- backward ops -------------------------------------------------------------------
@@ -1240,7 +1478,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "gf_node_fwd(Tensor src, Tensor Wab, Tensor Win, Tensor bin, Tensor? nv, Tensor? prev_acc, Tensor(h!)? prev_saved, "
       "Tensor[] prev_bn, Tensor(a!)? rm3, Tensor(b!)? rv3, Tensor(c!)? nbt3, Tensor(d!)? rm4, Tensor(e!)? rv4, "
-      "Tensor(f!)? nbt4, float mom3, float eps3, float mom4, float eps4, Tensor(g!)? zero_buf) -> Tensor[]");
+      "Tensor(f!)? nbt4, float mom3, float eps3, float mom4, float eps4, Tensor(g!)? zero_buf, bool packed) -> Tensor[]");
   m.def(
       "gf_oproj_fwd(Tensor o, Tensor Wo, Tensor bo, Tensor x, Tensor(a!) acc, Tensor? rng, int salt, float p, "
       "Tensor? nv) -> Tensor");
@@ -1256,6 +1494,10 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "gf_final_fwd(Tensor z3, Tensor acc, Tensor(a!) saved, Tensor[] bn, Tensor(b!)? rm3, Tensor(c!)? rv3, "
       "Tensor(d!)? nbt3, Tensor(e!)? rm4, Tensor(f!)? rv4, Tensor(g!)? nbt4, float mom3, float eps3, float mom4, "
       "float eps4, Tensor? nv) -> Tensor");
+  m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
+  m.def(
+      "gf_edge_bwd(Tensor dC, Tensor Wr, Tensor Wd, Tensor? rmask, Tensor(a!)? de_acc, Tensor? dG, Tensor? Wemb, "
+      "Tensor? Wlin, Tensor(b!)? drbf_acc, int K) -> Tensor[]");
   m.def("gf_pair_stats_bwd(Tensor dx, Tensor x, Tensor z3, Tensor saved, Tensor(a!) acc, Tensor? nv) -> Tensor");
   m.def(
       "gf_mlp_bwd(Tensor g, Tensor z3, Tensor(a!) acc, Tensor saved, Tensor g3, Tensor g4, float eps3, float eps4, "
@@ -1278,6 +1520,8 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gf_post_fwd", hy::gf::gf_post_fwd);
   m.impl("gf_mlp_fwd", hy::gf::gf_mlp_fwd);
   m.impl("gf_final_fwd", hy::gf::gf_final_fwd);
+  m.impl("gf_edge_fwd", hy::gf::gf_edge_fwd);
+  m.impl("gf_edge_bwd", hy::gf::gf_edge_bwd);
   m.impl("gf_pair_stats_bwd", hy::gf::gf_pair_stats_bwd);
   m.impl("gf_mlp_bwd", hy::gf::gf_mlp_bwd);
   m.impl("gf_loc_bwd", hy::gf::gf_loc_bwd);

@@ -313,6 +313,120 @@ std::tuple<at::Tensor, at::Tensor> radial_fwd(const at::Tensor& dist_, const at:
   return {R, Gt};
 }
 
+// Variant for the fused GPS encoder (ops/gps_encoder.py): per-layer weight pointers (no
+// [L, F, K] stacking copies) and the basis itself written out, rbf [E, K] and its derivative
+// w.r.t. the learnable frequencies drbf/dfreq [E, K] = u(x) cos(freq_k x) x, so that every
+// radial parameter gradient becomes a row-reduction (dW = dY^T X) of the encoder's grouped
+// weight-gradient launch: dW_emb = (dr * [r > 0])^T rbf, dW_lin = dG^T rbf, and
+// dfreq = diag(drbf^T drbf/dfreq).
+struct RadW {
+  const float* we[kRadMaxL];
+  const float* be[kRadMaxL];
+  const float* wl[kRadMaxL];
+  float* R[kRadMaxL];
+  float* G[kRadMaxL];
+};
+
+template <int K>
+__global__ void __launch_bounds__(256) radial_fwd_multi_kernel(const float* __restrict__ dist, int64_t E,
+                                                               const float* __restrict__ freq, RadW W, int L, int F,
+                                                               RadEnv ev, float* __restrict__ rbf,
+                                                               float* __restrict__ drdf) {
+  __shared__ float rb[kRadFwdEdges][K];
+  const int64_t e0 = (int64_t)blockIdx.x * kRadFwdEdges;
+  const int ne = (int)min<int64_t>(kRadFwdEdges, E - e0);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < ne * K) {
+    const int el = threadIdx.x / K, k = threadIdx.x % K;
+    const float x = dist[e0 + el] * ev.inv_c;
+    float u, du;
+    envelope(ev, x, u, du);
+    float sn, cs;
+    sincosf(freq[k] * x, &sn, &cs);
+    const float v = u * sn;
+    rb[el][k] = v;
+    rbf[(e0 + el) * K + k] = v;
+    if (drdf) drdf[(e0 + el) * K + k] = u * cs * x;
+  }
+  __syncthreads();
+  for (int f = lane; f < F; f += 64) {
+    for (int l = 0; l < L; ++l) {
+      float we[K], wl[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        we[k] = W.we[l][(int64_t)f * K + k];
+        wl[k] = W.wl[l][(int64_t)f * K + k];
+      }
+      const float b0 = W.be[l][f];
+      for (int el = w; el < ne; el += 4) {
+        float r = b0, g = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          r = fmaf(we[k], rb[el][k], r);
+          g = fmaf(wl[k], rb[el][k], g);
+        }
+        const int64_t o = (e0 + el) * F + f;
+        W.R[l][o] = fmaxf(r, 0.f);
+        W.G[l][o] = g;
+      }
+    }
+  }
+}
+
+// returns [rbf [E, K], drbf/dfreq [E, K] (empty unless want_dfreq), R_0..R_{L-1}, G_0..G_{L-1}]
+std::vector<at::Tensor> radial_fwd_multi(const at::Tensor& dist_, const at::Tensor& freq_,
+                                         const std::vector<at::Tensor>& Wemb, const std::vector<at::Tensor>& bemb,
+                                         const std::vector<at::Tensor>& Wlin, double cutoff, int64_t exponent,
+                                         bool want_dfreq) {
+  auto dist = dist_.contiguous(), freq = freq_.contiguous();
+  const int64_t E = dist.numel(), K = freq.numel(), L = (int64_t)Wemb.size();
+  HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL && (int64_t)bemb.size() == L &&
+               (int64_t)Wlin.size() == L,
+           "radial_fwd_multi: 1 <= K <= 8, 1 <= L <= 8, one (Wemb, bemb, Wlin) per layer");
+  const int64_t F = Wemb[0].size(0);
+  RadW W{};
+  std::vector<at::Tensor> out;
+  auto rbf = at::empty({E, K}, dist.options());
+  auto drdf = want_dfreq ? at::empty({E, K}, dist.options()) : at::empty({0}, dist.options());
+  out.push_back(rbf);
+  out.push_back(drdf);
+  std::vector<at::Tensor> Rs, Gs;
+  for (int64_t l = 0; l < L; ++l) {
+    HY_CHECK(Wemb[l].is_contiguous() && Wemb[l].size(0) == F && Wemb[l].size(1) == K && Wlin[l].is_contiguous() &&
+                 Wlin[l].sizes() == Wemb[l].sizes() && bemb[l].is_contiguous() && bemb[l].numel() == F,
+             "radial_fwd_multi: per-layer weights [F, K], bias [F]");
+    W.we[l] = Wemb[l].data_ptr<float>();
+    W.be[l] = bemb[l].data_ptr<float>();
+    W.wl[l] = Wlin[l].data_ptr<float>();
+    Rs.push_back(at::empty({E, F}, dist.options()));
+    Gs.push_back(at::empty({E, F}, dist.options()));
+    W.R[l] = Rs.back().data_ptr<float>();
+    W.G[l] = Gs.back().data_ptr<float>();
+  }
+  out.insert(out.end(), Rs.begin(), Rs.end());
+  out.insert(out.end(), Gs.begin(), Gs.end());
+  if (E == 0) return out;
+  const auto ev = make_env(cutoff, exponent);
+  const dim3 grid(ceil_div(E, kRadFwdEdges));
+  float* dp = want_dfreq ? drdf.data_ptr<float>() : nullptr;
+#define HY_RAD_FWDM(KK)                                                                                        \
+  radial_fwd_multi_kernel<KK><<<grid, 256, 0, stream()>>>(dist.data_ptr<float>(), E, freq.data_ptr<float>(), W, \
+                                                          (int)L, (int)F, ev, rbf.data_ptr<float>(), dp)
+  switch (K) {
+    case 1: HY_RAD_FWDM(1); break;
+    case 2: HY_RAD_FWDM(2); break;
+    case 3: HY_RAD_FWDM(3); break;
+    case 4: HY_RAD_FWDM(4); break;
+    case 5: HY_RAD_FWDM(5); break;
+    case 6: HY_RAD_FWDM(6); break;
+    case 7: HY_RAD_FWDM(7); break;
+    case 8: HY_RAD_FWDM(8); break;
+    default: HY_CHECK(false, "radial_fwd_multi: unsupported basis size ", K);
+  }
+#undef HY_RAD_FWDM
+  return out;
+}
+
 // returns ddist [E], dfreq [K], dWemb [L,F,K], dbemb [L,F], dWlin [L,F,K]
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bwd(
     const std::vector<at::Tensor>& dR_, const std::vector<at::Tensor>& dG_, const at::Tensor& R,
@@ -383,6 +497,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "radial_fwd(Tensor dist, Tensor freq, Tensor Wemb, Tensor bemb, Tensor Wlin, float cutoff, int exponent) -> "
       "(Tensor, Tensor)");
   m.def(
+      "radial_fwd_multi(Tensor dist, Tensor freq, Tensor[] Wemb, Tensor[] bemb, Tensor[] Wlin, float cutoff, "
+      "int exponent, bool want_dfreq) -> Tensor[]");
+  m.def(
       "radial_bwd(Tensor[] dR, Tensor[] dG, Tensor R, Tensor dist, Tensor freq, Tensor Wemb, Tensor Wlin, float cutoff, "
       "int exponent) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
 }
@@ -390,4 +507,5 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radial_fwd", hy::radial_fwd);
   m.impl("radial_bwd", hy::radial_bwd);
+  m.impl("radial_fwd_multi", hy::radial_fwd_multi);
 }

@@ -120,15 +120,20 @@ class PNAPlusStack(Base):
         x, pos, ctx = super()._embedding(data)
         assert data.pos is not None, "PNA+ requires node positions (data.pos) to be set."
         _, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
-        dist = dist.squeeze(-1)
-        convs = self._stack_convs()
-        if fused_ok(dist, self.rbf, convs):
-            # Bessel basis + every layer's rbf_emb/rbf_lin in one launch (ops/radial.py)
-            ctx.radial = {id(c): rg for c, rg in zip(convs, radial_features(dist, self.rbf, convs))}
-            ctx.rbf, ctx.rbf_basis, ctx.dist = None, self.rbf, dist
-        else:
-            ctx.rbf = self.rbf(dist)
+        ctx.dist = dist.squeeze(-1)
+        ctx.rbf_basis, ctx.rbf, ctx.radial = self.rbf, None, None
         return x, pos, ctx
+
+    def _materialize_radial(self, ctx):
+        """Radial features of the module path (the fused encoder computes its own)."""
+        if ctx.get("radial") is not None or ctx.get("rbf") is not None:
+            return
+        convs = self._stack_convs()
+        if fused_ok(ctx.dist, self.rbf, convs):
+            # Bessel basis + every layer's rbf_emb/rbf_lin in one launch (ops/radial.py)
+            ctx.radial = {id(c): rg for c, rg in zip(convs, radial_features(ctx.dist, self.rbf, convs))}
+        else:
+            ctx.rbf = self.rbf(ctx.dist)
 
     def _fused_encode(self, inv, equiv, ctx):
         # GPS + PNAPlus training on the GPU: the whole conv stack in one autograd function
@@ -137,6 +142,7 @@ class PNAPlusStack(Base):
 
         if self.use_global_attn and gps_encoder.eligible(self, inv, ctx):
             return gps_encoder.encode(self, inv, ctx), equiv, ctx
+        self._materialize_radial(ctx)
         return None
 
     def _stack_convs(self):

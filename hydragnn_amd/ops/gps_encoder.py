@@ -62,8 +62,14 @@ def eligible(model, x, ctx):
         return False
     if not isinstance(model.activation_function, torch.nn.ReLU):
         return False
-    rad = ctx.get("radial")
-    if rad is None or ctx.get("edge_attr") is None or ctx.edge_attr.shape[1] + F > 188:
+    from .radial import MAX_K, MAX_L
+
+    dist = ctx.get("dist")
+    if dist is None or dist.requires_grad or not dist.is_cuda or ctx.get("rbf_basis") is None:
+        return False  # the radial basis is computed inside the encoder (no force training)
+    if ctx.rbf_basis.freq.numel() > MAX_K or len(model.graph_convs) > MAX_L or not _mode.fused("radial"):
+        return False
+    if ctx.get("edge_attr") is None or ctx.edge_attr.shape[1] + F > 188:
         return False
     if ctx.dst_si is None or ctx.dst_si.perm is not None or ctx.get("attn_seg_id") is None:
         return False
@@ -71,7 +77,7 @@ def eligible(model, x, ctx):
         if not isinstance(conv, GPSConv) or not isinstance(conv.attn, MultiheadAttention):
             return False
         c = conv.conv
-        if not (isinstance(c, PNAConvFused) and c.plus and c.edge_dim is not None and id(c) in rad):
+        if not (isinstance(c, PNAConvFused) and c.plus and c.edge_dim is not None):
             return False
         if c.F_in != F or c.F_out != F or not hasattr(c, "edge_encoder"):
             return False
@@ -94,10 +100,11 @@ def _layer_params(conv, bn4):
             c.pre_nns[0][0].weight, c.pre_nns[0][0].bias, c.edge_encoder.weight, c.edge_encoder.bias,
             c.post_nns[0][0].weight, c.post_nns[0][0].bias, c.lin.weight, c.lin.bias,
             n1.weight, n1.bias, n2.weight, n2.bias, n3.weight, n3.bias, n4.weight, n4.bias,
-            lin1.weight, lin1.bias, lin2.weight, lin2.bias]
+            lin1.weight, lin1.bias, lin2.weight, lin2.bias,
+            c.rbf_emb[0].weight, c.rbf_emb[0].bias, c.rbf_lin.weight]
 
 
-NP = 24
+NP = 27
 
 
 class _Cfg:
@@ -131,13 +138,18 @@ def encode(model, x0, ctx):
         nv = _as_nv(nv, x0.device)
     cfg.nv = nv
     cfg.side = _streams.enabled(x0)
+    # 8-wide heads: MFMA attention (csrc/attention8.hip) on operands the node kernel packs
+    cfg.a8 = cfg.F // cfg.heads == 8 and _mode.fused("attn8")
+    # edge-row GEMMs (C forward, dr/de dgrad) on the MFMA tile kernels when the edge width
+    # equals the hidden width (the GPS edge embedding)
+    cfg.edge_mfma = ctx.edge_attr.shape[1] == cfg.F and _mode.fused("edgemfma")
+    basis = ctx.rbf_basis
+    cfg.cutoff, cfg.exponent = float(basis.cutoff), int(basis.envelope.p - 1)
     flat = []
-    for c in convs:
-        r, G = ctx.radial[id(c.conv)]
-        flat += [r.contiguous(), G.contiguous()]
     for c, b in zip(convs, model.feature_layers):
         flat += _layer_params(c, b)
-    return _GPSEncoder.apply(cfg, x0.contiguous(), ctx.edge_attr.contiguous(), *flat)
+    return _GPSEncoder.apply(cfg, x0.contiguous(), ctx.edge_attr.contiguous(), ctx.dist.contiguous(), basis.freq,
+                             *flat)
 
 
 class _Side:
@@ -184,12 +196,16 @@ def _bn_state(b):
 
 class _GPSEncoder(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg, x0, e, *flat):
+    def forward(ctx, cfg, x0, e, dist, freq, *flat):
         ops = _native.ops()
         L, F = cfg.L, cfg.F
-        radial = flat[:2 * L]
-        prm = [flat[2 * L + NP * l: 2 * L + NP * (l + 1)] for l in range(L)]
+        prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
         dev = x0.device
+        # Bessel basis + every layer's radial embedding / gate in one launch; the basis and its
+        # frequency derivative are kept for the weight gradients
+        ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
+                                  cfg.cutoff, cfg.exponent, bool(freq.requires_grad))
+        rbf, drdf, Rl, Gl = ro[0], ro[1], ro[2:2 + L], ro[2 + L:2 + 2 * L]
         acc = torch.empty(L, NREP * SITES * F, device=dev, dtype=torch.float64)
         saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
@@ -197,27 +213,33 @@ class _GPSEncoder(torch.autograd.Function):
         z3 = None
         for l in range(L):
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
-             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2) = prm[l]
-            r, G = radial[2 * l], radial[2 * l + 1]
+             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2, _, _, _) = prm[l]
+            r, G = Rl[l], Gl[l]
             s0, s1, s2, s3 = cfg.salts[l]
             Wab, Wr, Wd, bc = ops.pna_wprep_fwd(Wpre, bpre, Wenc, benc)
             if l == 0:
-                x, AB, qkv = ops.gf_node_fwd(x0, Wab, Win, bin_, nv, None, None, [], None, None, None, None, None,
-                                             None, 0.0, 0.0, 0.0, 0.0, acc)
+                outs = ops.gf_node_fwd(x0, Wab, Win, bin_, nv, None, None, [], None, None, None, None, None,
+                                       None, 0.0, 0.0, 0.0, 0.0, acc, cfg.a8)
             else:
                 _, _, n3p, n4p = cfg.bns[l - 1]
                 rm3, rv3, nb3, m3, e3 = _bn_state(n3p)
                 rm4, rv4, nb4, m4, e4 = _bn_state(n4p)
                 pp = prm[l - 1]
-                x, AB, qkv = ops.gf_node_fwd(z3, Wab, Win, bin_, nv, acc[l - 1], saved[l - 1],
-                                             [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3, rm4, rv4, nb4,
-                                             m3, e3, m4, e4, None)
+                outs = ops.gf_node_fwd(z3, Wab, Win, bin_, nv, acc[l - 1], saved[l - 1],
+                                       [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3, rm4, rv4, nb4,
+                                       m3, e3, m4, e4, None, cfg.a8)
+            x, AB = outs[0], outs[1]
+            pk = outs[2:] if cfg.a8 else None
+            qkv = None if cfg.a8 else outs[2]
             side = _Side(dev, cfg.side)
             with side:
-                side.used(qkv, x)
-                O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
+                side.used(x, *(pk if cfg.a8 else [qkv]))
+                if cfg.a8:
+                    O, LSE = ops.attn8_fwd(pk[0], pk[2], pk[5], cfg.sid, cfg.sptr, x.shape[0], cfg.scale, cfg.splits)
+                else:
+                    O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
                 z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
-            C = ops.edge_linear_fwd([r, e], [Wr, Wd], bc)
+            C = ops.gf_edge_fwd(r, e, Wr, Wd, bc) if cfg.edge_mfma else ops.edge_linear_fwd([r, e], [Wr, Wd], bc)
             Z, amin, amax = ops.pna_fwd(x, AB, C, G, cfg.src.index, cfg.dst.rowptr, cfg.avg[l][0], cfg.avg[l][1])
             pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
             side.join(O, LSE, z2)
@@ -226,7 +248,7 @@ class _GPSEncoder(torch.autograd.Function):
             rm2, rv2, nb2, m2, e2 = _bn_state(n2)
             out, md, z3 = ops.gf_mlp_fwd(z1, z2, acc[l], saved[l], [g1, b1n, g2, b2n], rm1, rv1, nb1, rm2, rv2, nb2,
                                          m1, e1, m2, e2, W1, b1, W2, b2, rng, s2, s3, p, nv)
-            st.append(dict(x=x, AB=AB, qkv=qkv, O=O, LSE=LSE, z2=z2, C=C, Z=Z, amin=amin, amax=amax, p=pl, z1=z1,
+            st.append(dict(x=x, AB=AB, qkv=qkv, pk=pk, O=O, LSE=LSE, z2=z2, C=C, Z=Z, amin=amin, amax=amax, p=pl, z1=z1,
                            out=out, md=md, z3=z3, Wab=Wab, Wr=Wr, Wd=Wd))
         _, _, n3, n4 = cfg.bns[L - 1]
         rm3, rv3, nb3, m3, e3 = _bn_state(n3)
@@ -237,6 +259,8 @@ class _GPSEncoder(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.st = st
         ctx.acc, ctx.saved = acc, saved
+        ctx.radial = (rbf, drdf, Rl, Gl)
+        ctx.freq_grad = bool(freq.requires_grad)
         ctx.save_for_backward(x0, e, xL, *flat)
         return xL
 
@@ -246,8 +270,9 @@ class _GPSEncoder(torch.autograd.Function):
         cfg = ctx.cfg
         L, F = cfg.L, cfg.F
         x0, e, xL, *flat = ctx.saved_tensors
-        radial = flat[:2 * L]
-        prm = [flat[2 * L + NP * l: 2 * L + NP * (l + 1)] for l in range(L)]
+        prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
+        rbf, drdf, Rl, Gl = ctx.radial
+        K = rbf.shape[1]
         acc, saved, st = ctx.acc, ctx.saved, ctx.st
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
         dev = x0.device
@@ -266,12 +291,13 @@ class _GPSEncoder(torch.autograd.Function):
 
         grads = [None] * len(flat)
         de = None
+        drbf = None
         dx0 = None
         wg = []  # per layer: (dWab, (dWr, dbc), dWd)
         for l in reversed(range(L)):
             s = st[l]
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
-             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2) = prm[l]
+             g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2, Wemb, bemb, Wrl) = prm[l]
             s0, s1, s2, s3 = cfg.salts[l]
             n1, n2, n3, n4 = cfg.bns[l]
             dg, dpre, dout, dw3, db3, dw4, db4 = ops.gf_mlp_bwd(g, s["z3"], acc[l], saved[l], g3, g4, float(n3.eps),
@@ -281,15 +307,20 @@ class _GPSEncoder(torch.autograd.Function):
             with side:
                 side.used(dout)
                 dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
-                dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span,
-                                    cfg.splits)
+                if cfg.a8:
+                    pk = s["pk"]
+                    dqkv = ops.attn8_bwd(dO, s["O"], s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid, cfg.sptr,
+                                         cfg.scale, cfg.splits)
+                else:
+                    dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale,
+                                        cfg.span, cfg.splits)
             dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
                                                          nv)
-            dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], radial[2 * l + 1], cfg.src.index, cfg.dst.rowptr,
+            dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], Gl[l], cfg.src.index, cfg.dst.rowptr,
                                       s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
             ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
-            dr = dE @ s["Wr"]
-            de = dE @ s["Wd"] if de is None else torch.addmm(de, dE, s["Wd"])
+            # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch
+            dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
             side.join(dz2, da, dO, dqkv, dw2n, db2n)
             if l > 0:
                 sp = st[l - 1]
@@ -297,14 +328,14 @@ class _GPSEncoder(torch.autograd.Function):
                                     nv)
             else:
                 dx0 = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], None, None, None, nv)
-            base = 2 * L + NP * l
-            grads[2 * l] = dr
-            grads[2 * l + 1] = dG
+            base = NP * l
             gw = {}
+            gw["Wemb"] = item(dr, rbf, Wemb, True)
+            gw["Wrl"] = item(dG, rbf, Wrl, False)
             gw["Win"] = item(dqkv, s["x"], Win, True)
             gw["Wo"] = item(da, s["O"], Wo, True)
             gw["Wab"] = item(dAB, s["x"], s["Wab"], False)
-            gw["Wr"] = item(dE, radial[2 * l], s["Wr"], True)
+            gw["Wr"] = item(dE, Rl[l], s["Wr"], True)
             gw["Wd"] = item(dE, e, s["Wd"], False)
             gw["Wpost"] = item(dp, s["Z"], Wpost, True)
             gw["Wlin"] = item(dq, s["p"], Wlin, True)
@@ -315,10 +346,15 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 14], grads[base + 15] = dw2n, db2n
             grads[base + 16], grads[base + 17] = dw3, db3
             grads[base + 18], grads[base + 19] = dw4, db4
-        # every weight gradient of the stack: one grouped launch pair
+        dfreq_w = item(drbf, drdf, torch.empty(K, K, device=dev), False)[0] if ctx.freq_grad else None
+        # every weight gradient of the stack (incl. the radial basis and its frequencies): one
+        # grouped launch pair
         ops.linear_wgrad_grouped(dys, xs, dws, dbs, [0] * len(dys))
+        dfreq = torch.diagonal(dfreq_w).contiguous() if dfreq_w is not None else None
         for l, gw in wg:
-            base = 2 * L + NP * l
+            base = NP * l
+            grads[base + 24], grads[base + 25] = gw["Wemb"]
+            grads[base + 26] = gw["Wrl"][0]
             Wpre, Wenc, benc = prm[l][4], prm[l][6], prm[l][7]
             dWpre, dbpre, dWenc, dbenc = ops.pna_wprep_bwd(gw["Wab"][0], gw["Wr"][0], gw["Wd"][0], gw["Wr"][1], Wpre,
                                                            Wenc, benc)
@@ -331,4 +367,5 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 20], grads[base + 21] = gw["W1"]
             grads[base + 22], grads[base + 23] = gw["W2"]
         ctx.st = None
-        return (None, dx0, de, *grads)
+        ctx.radial = None
+        return (None, dx0, de, None, dfreq, *grads)

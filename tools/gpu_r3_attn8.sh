@@ -1,0 +1,14 @@
+#!/bin/bash
+# MFMA attention (8-wide heads): numerics, microbench, fused encoder tests, headline bench + profile
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_attention8_gpu.py > gpurun_out/r3_attn8_tests.log 2>&1
+rc=$?; tail -15 gpurun_out/r3_attn8_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 tools/bench_attn8.py > gpurun_out/r3_attn8_bench.log 2>&1 || exit $?
+cat gpurun_out/r3_attn8_bench.log | grep -v amdgpu.ids
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gps_fused_gpu.py > gpurun_out/r3_fused_tests2.log 2>&1
+rc=$?; tail -5 gpurun_out/r3_fused_tests2.log; [ $rc -eq 0 ] || exit $rc
+HYDRA_STEP_TIMING=1 timeout -k 10 240 python3 bench.py --steps 50 --warmup 10 > gpurun_out/r3_attn8_headline.log 2>&1 || exit $?
+tail -1 gpurun_out/r3_attn8_headline.log | cut -c1-400
+bash tools/gpu_prof_bench.sh r3_attn8
