@@ -69,35 +69,6 @@ __device__ __forceinline__ int wave_max_i(int v) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Segment bounds of this lane's row i (rows >= N: empty), the wave's union [lo, hi) and
-// intersection [ilo, ihi) of row ranges, and split s of S of the union (16-aligned).
-struct Span {
-  int b, e;       // this row's segment
-  int lo, hi;     // wave union
-  int ilo, ihi;   // wave intersection (tiles inside it need no mask)
-  int cb, ce;     // this split
-};
-
-__device__ __forceinline__ Span span_of(int row, int N, const int* seg_id, const int* seg_ptr, int S, int s) {
-  Span sp;
-  sp.b = N;
-  sp.e = 0;
-  if (row < N) {
-    const int sg = seg_id[row];
-    sp.b = seg_ptr[sg];
-    sp.e = seg_ptr[sg + 1];
-  }
-  sp.lo = uni(wave_min_i(sp.b)) & ~15;  // tiles start 16-aligned (the quad layout groups rows by 4)
-  sp.hi = uni(wave_max_i(sp.e));
-  sp.ilo = uni(wave_max_i(row < N ? sp.b : 0));
-  sp.ihi = uni(wave_min_i(row < N ? sp.e : N));
-  const int L = max(sp.hi - sp.lo, 0);
-  const int C = (((L + S - 1) / S) + 15) / 16 * 16;
-  sp.cb = uni(min(sp.lo + s * C, max(sp.hi, sp.lo)));
-  sp.ce = uni(min(sp.hi, sp.cb + C));
-  return sp;
-}
-
 // ------------------------------------------------------------------------------------ fwd
 // grid (ceil(N/64), H, S); wave w: queries 64 bx + 16 w + i.
 // part: [S][H][N][10] = (m, l, o[8]) in log2 units (S > 1); else O [N, 8H] and LSE2 [H][Nq]
@@ -124,89 +95,142 @@ __device__ __forceinline__ KV8 ld_kv(const float* __restrict__ Kp, const float* 
   return t;
 }
 
+template <int RT>
 __global__ void __launch_bounds__(256) attn8_fwd_kernel(const float* __restrict__ Qp, const float* __restrict__ Kp,
                                                         const float* __restrict__ Vq, int N, int Nq, int H,
                                                         const int* __restrict__ seg_id,
                                                         const int* __restrict__ seg_ptr, int S, float qscale,
                                                         float* __restrict__ part, float* __restrict__ O,
                                                         float* __restrict__ LSE2) {
+  // RT row tiles (16 queries each) per wave: every K/V fragment feeds RT independent chains
   const int h = blockIdx.y, sp_ = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int q = blockIdx.x * 64 + 16 * w + i;
-  const Span sp = span_of(q, N, seg_id, seg_ptr, S, sp_);
-  const int qc = min(q, Nq - 1);
-  const float2 bq = ld2(Qp + ((int64_t)h * Nq + qc) * 8 + 2 * g);
-  const float bq0 = bq.x * qscale, bq1 = bq.y * qscale;
-  const float vone = (i == 8) ? 1.f : 0.f;
-  auto masked = [&](int k0) { return !(k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce); };
-  auto mask_tile = [&](f4v& s, int k0, float neg) {
+  const int qbase = blockIdx.x * 64 * RT + 16 * RT * w;
+  int q[RT], sb[RT], se[RT];
+  float bq0[RT], bq1[RT];
+  int lo = N, hi = 0, ilo = 0, ihi = N;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = k0 + 4 * g + r;
-      if (key < sp.b || key >= sp.e || key >= sp.ce) s[r] = neg;
+  for (int t = 0; t < RT; ++t) {
+    q[t] = qbase + 16 * t + i;
+    sb[t] = N;
+    se[t] = 0;
+    if (q[t] < N) {
+      const int sg = seg_id[q[t]];
+      sb[t] = seg_ptr[sg];
+      se[t] = seg_ptr[sg + 1];
     }
-  };
+    lo = min(lo, sb[t]);
+    hi = max(hi, se[t]);
+    ilo = max(ilo, q[t] < N ? sb[t] : 0);
+    ihi = min(ihi, q[t] < N ? se[t] : N);
+    const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(q[t], Nq - 1)) * 8 + 2 * g);
+    bq0[t] = bq.x * qscale;
+    bq1[t] = bq.y * qscale;
+  }
+  lo = uni(wave_min_i(lo)) & ~15;
+  hi = uni(wave_max_i(hi));
+  ilo = uni(wave_max_i(ilo));
+  ihi = uni(wave_min_i(ihi));
+  const int L = max(hi - lo, 0);
+  const int C = (((L + S - 1) / S) + 15) / 16 * 16;
+  const int cb = uni(min(lo + sp_ * C, max(hi, lo))), ce = uni(min(hi, cb + C));
+  const float vone = (i == 8) ? 1.f : 0.f;
+  auto full_tile = [&](int k0) { return k0 >= ilo && k0 + 16 <= ihi && k0 + 16 <= ce; };
   // pass 1: row max
-  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  float m[RT];
   {
-    float2 k0r = ld2(Kp + ((int64_t)h * Nq + min(sp.cb, Nq - 16) + i) * 8 + 2 * g);
-    float2 k1r = ld2(Kp + ((int64_t)h * Nq + min(sp.cb + 16, Nq - 16) + i) * 8 + 2 * g);
-    for (int k0 = sp.cb; k0 < sp.ce; k0 += 16) {
-      const float2 kn = ld2(Kp + ((int64_t)h * Nq + min(k0 + 32, Nq - 16) + i) * 8 + 2 * g);
-      f4v s = mfma(k0r.x, bq0, f4z());
-      s = mfma(k0r.y, bq1, s);
-      if (masked(k0)) mask_tile(s, k0, -INFINITY);
+    float mx[RT][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], s[r]);
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx[t][r] = -INFINITY;
+    float2 k0r = ld2(Kp + ((int64_t)h * Nq + min(cb, Nq - 16) + i) * 8 + 2 * g);
+    float2 k1r = ld2(Kp + ((int64_t)h * Nq + min(cb + 16, Nq - 16) + i) * 8 + 2 * g);
+    for (int k0 = cb; k0 < ce; k0 += 16) {
+      const float2 kn = ld2(Kp + ((int64_t)h * Nq + min(k0 + 32, Nq - 16) + i) * 8 + 2 * g);
+      const bool full = full_tile(k0);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        f4v s = mfma(k0r.x, bq0[t], f4z());
+        s = mfma(k0r.y, bq1[t], s);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 4 * g + r;
+          const bool ok = full || (key >= sb[t] && key < se[t] && key < ce);
+          mx[t][r] = fmaxf(mx[t][r], ok ? s[r] : -INFINITY);
+        }
+      }
       k0r = k1r;
       k1r = kn;
     }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) m[t] = wmax16(fmaxf(fmaxf(mx[t][0], mx[t][1]), fmaxf(mx[t][2], mx[t][3])));
   }
-  const float m = wmax16(fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3])));
-  const bool live = m > -INFINITY;
-  const float negm = live ? -m : 0.f;
-  // pass 2: p = exp2(s - m), O^T += Vx^T P^T (row 8 of O^T = l)
-  // (control flow stays wave-uniform: every lane supplies A-operand rows of V to the
-  // whole tile; rows of dead queries are fully masked, p = 0)
-  f4v o = f4z();
+  // pass 2: p = exp2(s - m), O^T += Vx^T P^T (row 8 of O^T = l); control flow stays
+  // wave-uniform (every lane supplies A-operand rows of V; dead queries are fully masked)
+  f4v o[RT];
+  float negm[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    o[t] = f4z();
+    negm[t] = m[t] > -INFINITY ? -m[t] : 0.f;
+  }
   {
-    KV8 t0 = ld_kv(Kp, Vq, h, Nq, sp.cb, i, g, vone);
-    KV8 t1 = ld_kv(Kp, Vq, h, Nq, sp.cb + 16, i, g, vone);
-    for (int k0 = sp.cb; k0 < sp.ce; k0 += 16) {
+    KV8 t0 = ld_kv(Kp, Vq, h, Nq, cb, i, g, vone);
+    KV8 t1 = ld_kv(Kp, Vq, h, Nq, cb + 16, i, g, vone);
+    for (int k0 = cb; k0 < ce; k0 += 16) {
       const KV8 tn = ld_kv(Kp, Vq, h, Nq, k0 + 32, i, g, vone);
-      f4v s = mfma(t0.k.x, bq0, f4v{negm, negm, negm, negm});
-      s = mfma(t0.k.y, bq1, s);
-      if (masked(k0)) mask_tile(s, k0, -INFINITY);
-      o = mfma(t0.v.x, fexp2(s[0]), o);
-      o = mfma(t0.v.y, fexp2(s[1]), o);
-      o = mfma(t0.v.z, fexp2(s[2]), o);
-      o = mfma(t0.v.w, fexp2(s[3]), o);
+      const bool full = full_tile(k0);
+      f4v s[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(t0.k.x, bq0[t], f4v{negm[t], negm[t], negm[t], negm[t]});
+        s[t] = mfma(t0.k.y, bq1[t], s[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 4 * g + r;
+          const bool ok = full || (key >= sb[t] && key < se[t] && key < ce);
+          p[r] = ok ? fexp2(s[t][r]) : 0.f;
+        }
+        o[t] = mfma(t0.v.x, p[0], o[t]);
+        o[t] = mfma(t0.v.y, p[1], o[t]);
+        o[t] = mfma(t0.v.z, p[2], o[t]);
+        o[t] = mfma(t0.v.w, p[3], o[t]);
+      }
       t0 = t1;
       t1 = tn;
     }
   }
-  // o: lane (i, g) rows 4g + r of O^T for query i: g = 0, 1 -> d 0..7, g = 2, r = 0 -> l
-  const float l = __shfl(o[0], 32 + i, 64);
-  if (q >= N) {
-    if (S == 1 && g == 2 && q < Nq) LSE2[(int64_t)h * Nq + q] = 0.f;
-    return;
-  }
-  if (S == 1) {
-    if (g < 2) {
-      const float inv = l > 0.f ? 1.f / l : 0.f;
-      float4 v = make_float4(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
-      *reinterpret_cast<float4*>(O + (int64_t)q * 8 * H + h * 8 + 4 * g) = v;
-    } else if (g == 2) {
-      LSE2[(int64_t)h * Nq + q] = l > 0.f ? m + __log2f(l) : -INFINITY;
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    // o: lane (i, g) rows 4g + r of O^T for query i: g = 0, 1 -> d 0..7, g = 2, r = 0 -> l
+    const float l = __shfl(o[t][0], 32 + i, 64);
+    const int qq = q[t];
+    if (qq >= N) {
+      if (S == 1 && g == 2 && qq < Nq) LSE2[(int64_t)h * Nq + qq] = 0.f;
+      continue;
     }
-    return;
-  }
-  float* P = part + (((int64_t)sp_ * H + h) * N + q) * 10;
-  if (g < 2) {
-    *reinterpret_cast<float4*>(P + 2 + 4 * g) = make_float4(o[0], o[1], o[2], o[3]);
-  } else if (g == 2) {
-    P[0] = live ? m : -INFINITY;
-    P[1] = l;
+    if (S == 1) {
+      if (g < 2) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        float4 v = make_float4(o[t][0] * inv, o[t][1] * inv, o[t][2] * inv, o[t][3] * inv);
+        *reinterpret_cast<float4*>(O + (int64_t)qq * 8 * H + h * 8 + 4 * g) = v;
+      } else if (g == 2) {
+        LSE2[(int64_t)h * Nq + qq] = l > 0.f ? m[t] + __log2f(l) : -INFINITY;
+      }
+      continue;
+    }
+    float* P = part + (((int64_t)sp_ * H + h) * N + qq) * 10;
+    if (g < 2) {
+      *reinterpret_cast<float4*>(P + 2 + 4 * g) = make_float4(o[t][0], o[t][1], o[t][2], o[t][3]);
+    } else if (g == 2) {
+      P[0] = m[t] > -INFINITY ? m[t] : -INFINITY;
+      P[1] = l;
+    }
   }
 }
 
@@ -263,6 +287,47 @@ __device__ __forceinline__ DQ8 ld_dq(const float* __restrict__ Kp, const float* 
   return t;
 }
 
+// Span of RT row tiles of a wave (rows base + 16 t + i): per-row segments, wave union /
+// intersection, split range (as span_of)
+template <int RT>
+struct SpanR {
+  int b[RT], e[RT], row[RT];
+  int ilo, ihi, cb, ce;
+};
+
+template <int RT>
+__device__ __forceinline__ SpanR<RT> span_rt(int base, int i, int N, const int* seg_id, const int* seg_ptr, int S,
+                                              int s) {
+  SpanR<RT> sp;
+  int lo = N, hi = 0, ilo = 0, ihi = N;
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int r = base + 16 * t + i;
+    sp.row[t] = r;
+    sp.b[t] = N;
+    sp.e[t] = 0;
+    if (r < N) {
+      const int sg = seg_id[r];
+      sp.b[t] = seg_ptr[sg];
+      sp.e[t] = seg_ptr[sg + 1];
+    }
+    lo = min(lo, sp.b[t]);
+    hi = max(hi, sp.e[t]);
+    ilo = max(ilo, r < N ? sp.b[t] : 0);
+    ihi = min(ihi, r < N ? sp.e[t] : N);
+  }
+  lo = uni(wave_min_i(lo)) & ~15;
+  hi = uni(wave_max_i(hi));
+  sp.ilo = uni(wave_max_i(ilo));
+  sp.ihi = uni(wave_min_i(ihi));
+  const int L = max(hi - lo, 0);
+  const int C = (((L + S - 1) / S) + 15) / 16 * 16;
+  sp.cb = uni(min(lo + s * C, max(hi, lo)));
+  sp.ce = uni(min(hi, sp.cb + C));
+  return sp;
+}
+
+template <int RT>
 __global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
     const float* __restrict__ Qp, const float* __restrict__ Kp, const float* __restrict__ Kq,
     const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ LSE2,
@@ -271,40 +336,61 @@ __global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
     int64_t sstride) {
   const int h = blockIdx.y, sp_ = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int q = blockIdx.x * 64 + 16 * w + i;
-  const Span sp = span_of(q, N, seg_id, seg_ptr, S, sp_);
-  const int qc = min(q, Nq - 1);
-  const float2 bq = ld2(Qp + ((int64_t)h * Nq + qc) * 8 + 2 * g);
-  const float2 bo = ld2(dOp + ((int64_t)h * Nq + qc) * 8 + 2 * g);
-  const float bq0 = bq.x * qscale, bq1 = bq.y * qscale;
-  const float nlse = q < N ? -LSE2[(int64_t)h * Nq + q] : 0.f;
-  const float ndl = q < N ? -delta[(int64_t)h * Nq + q] : 0.f;
-  f4v dq = f4z();
+  const SpanR<RT> sp = span_rt<RT>(blockIdx.x * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
+  float bq0[RT], bq1[RT], bo0[RT], bo1[RT], nlse[RT], ndl[RT];
+  f4v dq[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int q = sp.row[t], qc = min(q, Nq - 1);
+    const float2 bq = ld2(Qp + ((int64_t)h * Nq + qc) * 8 + 2 * g);
+    const float2 bo = ld2(dOp + ((int64_t)h * Nq + qc) * 8 + 2 * g);
+    bq0[t] = bq.x * qscale;
+    bq1[t] = bq.y * qscale;
+    bo0[t] = bo.x;
+    bo1[t] = bo.y;
+    nlse[t] = q < N ? -LSE2[(int64_t)h * Nq + q] : 0.f;
+    ndl[t] = q < N ? -delta[(int64_t)h * Nq + q] : 0.f;
+    dq[t] = f4z();
+  }
   DQ8 t0 = ld_dq(Kp, Kq, Vp, h, Nq, sp.cb, i, g), t1 = ld_dq(Kp, Kq, Vp, h, Nq, sp.cb + 16, i, g);
   for (int k0 = sp.cb; k0 < sp.ce; k0 += 16) {
     const DQ8 tn = ld_dq(Kp, Kq, Vp, h, Nq, k0 + 32, i, g);
-    f4v s = mfma(t0.k.x, bq0, f4v{nlse, nlse, nlse, nlse});
-    s = mfma(t0.k.y, bq1, s);
-    f4v dp = mfma(t0.v.x, bo.x, f4v{ndl, ndl, ndl, ndl});
-    dp = mfma(t0.v.y, bo.y, dp);
     const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
-    float ds[4];
+    f4v s[RT], dp[RT];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = k0 + 4 * g + r;
-      const bool ok = full || (key >= sp.b && key < sp.e && key < sp.ce);
-      ds[r] = ok ? fexp2(s[r]) * dp[r] : 0.f;
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(t0.k.x, bq0[t], f4v{nlse[t], nlse[t], nlse[t], nlse[t]});
+      dp[t] = mfma(t0.v.x, bo0[t], f4v{ndl[t], ndl[t], ndl[t], ndl[t]});
     }
-    dq = mfma(t0.kt.x, ds[0], dq);
-    dq = mfma(t0.kt.y, ds[1], dq);
-    dq = mfma(t0.kt.z, ds[2], dq);
-    dq = mfma(t0.kt.w, ds[3], dq);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(t0.k.y, bq1[t], s[t]);
+      dp[t] = mfma(t0.v.y, bo1[t], dp[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 4 * g + r;
+        const bool ok = full || (key >= sp.b[t] && key < sp.e[t] && key < sp.ce);
+        ds[r] = ok ? fexp2(s[t][r]) * dp[t][r] : 0.f;
+      }
+      dq[t] = mfma(t0.kt.x, ds[0], dq[t]);
+      dq[t] = mfma(t0.kt.y, ds[1], dq[t]);
+      dq[t] = mfma(t0.kt.z, ds[2], dq[t]);
+      dq[t] = mfma(t0.kt.w, ds[3], dq[t]);
+    }
     t0 = t1;
     t1 = tn;
   }
-  if (q < N && g < 2) {
-    *reinterpret_cast<float4*>(out + sp_ * sstride + (int64_t)q * ldo + h * 8 + 4 * g) =
-        make_float4(dq[0] * scale, dq[1] * scale, dq[2] * scale, dq[3] * scale);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int q = sp.row[t];
+    if (q < N && g < 2) {
+      *reinterpret_cast<float4*>(out + sp_ * sstride + (int64_t)q * ldo + h * 8 + 4 * g) =
+          make_float4(dq[t][0] * scale, dq[t][1] * scale, dq[t][2] * scale, dq[t][3] * scale);
+    }
   }
 }
 
@@ -337,6 +423,7 @@ __device__ __forceinline__ KV8b ld_kvb(const float* __restrict__ Qp, const float
   return t;
 }
 
+template <int RT>
 __global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
     const float* __restrict__ Qp, const float* __restrict__ Qq, const float* __restrict__ Kp,
     const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ dOq,
@@ -345,45 +432,71 @@ __global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
     float* __restrict__ out, int ldo, int64_t sstride) {
   const int h = blockIdx.y, sp_ = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int k = blockIdx.x * 64 + 16 * w + i;
-  const Span sp = span_of(k, N, seg_id, seg_ptr, S, sp_);  // keys and queries share segments
-  const int kc = min(k, Nq - 1);
-  const float2 bk = ld2(Kp + ((int64_t)h * Nq + kc) * 8 + 2 * g);
-  const float2 bv = ld2(Vp + ((int64_t)h * Nq + kc) * 8 + 2 * g);
-  const float bk0 = bk.x * qscale, bk1 = bk.y * qscale;
-  f4v dk = f4z(), dv = f4z();
+  // keys and queries share segments: the key rows' spans are the query ranges to visit
+  const SpanR<RT> sp = span_rt<RT>(blockIdx.x * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
+  float bk0[RT], bk1[RT], bv0[RT], bv1[RT];
+  f4v dk[RT], dv[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int kc = min(sp.row[t], Nq - 1);
+    const float2 bk = ld2(Kp + ((int64_t)h * Nq + kc) * 8 + 2 * g);
+    const float2 bv = ld2(Vp + ((int64_t)h * Nq + kc) * 8 + 2 * g);
+    bk0[t] = bk.x * qscale;
+    bk1[t] = bk.y * qscale;
+    bv0[t] = bv.x;
+    bv1[t] = bv.y;
+    dk[t] = f4z();
+    dv[t] = f4z();
+  }
   KV8b t0 = ld_kvb(Qp, Qq, dOp, dOq, LSE2, delta, h, Nq, sp.cb, i, g);
   KV8b t1 = ld_kvb(Qp, Qq, dOp, dOq, LSE2, delta, h, Nq, sp.cb + 16, i, g);
   for (int q0 = sp.cb; q0 < sp.ce; q0 += 16) {
     const KV8b tn = ld_kvb(Qp, Qq, dOp, dOq, LSE2, delta, h, Nq, q0 + 32, i, g);
-    f4v s = mfma(t0.q.x, bk0, f4v{-t0.lse.x, -t0.lse.y, -t0.lse.z, -t0.lse.w});
-    s = mfma(t0.q.y, bk1, s);
-    f4v dp = mfma(t0.o.x, bv.x, f4v{-t0.dl.x, -t0.dl.y, -t0.dl.z, -t0.dl.w});
-    dp = mfma(t0.o.y, bv.y, dp);
     const bool full = q0 >= sp.ilo && q0 + 16 <= sp.ihi && q0 + 16 <= sp.ce;
-    float p[4], ds[4];
+    const f4v nl = f4v{-t0.lse.x, -t0.lse.y, -t0.lse.z, -t0.lse.w};
+    const f4v nd = f4v{-t0.dl.x, -t0.dl.y, -t0.dl.z, -t0.dl.w};
+    f4v s[RT], dp[RT];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qq = q0 + 4 * g + r;
-      const bool ok = full || (qq >= sp.b && qq < sp.e && qq < sp.ce);
-      p[r] = ok ? fexp2(s[r]) : 0.f;
-      ds[r] = p[r] * dp[r];
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(t0.q.x, bk0[t], nl);
+      dp[t] = mfma(t0.o.x, bv0[t], nd);
     }
-    dv = mfma(t0.ot.x, p[0], dv);
-    dv = mfma(t0.ot.y, p[1], dv);
-    dv = mfma(t0.ot.z, p[2], dv);
-    dv = mfma(t0.ot.w, p[3], dv);
-    dk = mfma(t0.qt.x, ds[0], dk);
-    dk = mfma(t0.qt.y, ds[1], dk);
-    dk = mfma(t0.qt.z, ds[2], dk);
-    dk = mfma(t0.qt.w, ds[3], dk);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(t0.q.y, bk1[t], s[t]);
+      dp[t] = mfma(t0.o.y, bv1[t], dp[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + 4 * g + r;
+        const bool ok = full || (qq >= sp.b[t] && qq < sp.e[t] && qq < sp.ce);
+        p[r] = ok ? fexp2(s[t][r]) : 0.f;
+        ds[r] = p[r] * dp[t][r];
+      }
+      dv[t] = mfma(t0.ot.x, p[0], dv[t]);
+      dk[t] = mfma(t0.qt.x, ds[0], dk[t]);
+      dv[t] = mfma(t0.ot.y, p[1], dv[t]);
+      dk[t] = mfma(t0.qt.y, ds[1], dk[t]);
+      dv[t] = mfma(t0.ot.z, p[2], dv[t]);
+      dk[t] = mfma(t0.qt.z, ds[2], dk[t]);
+      dv[t] = mfma(t0.ot.w, p[3], dv[t]);
+      dk[t] = mfma(t0.qt.w, ds[3], dk[t]);
+    }
     t0 = t1;
     t1 = tn;
   }
-  if (k < N && g < 2) {
-    float* o = out + sp_ * sstride + (int64_t)k * ldo + h * 8 + 4 * g;
-    *reinterpret_cast<float4*>(o) = make_float4(dk[0] * scale, dk[1] * scale, dk[2] * scale, dk[3] * scale);
-    *reinterpret_cast<float4*>(o + 8 * H) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int k = sp.row[t];
+    if (k < N && g < 2) {
+      float* o = out + sp_ * sstride + (int64_t)k * ldo + h * 8 + 4 * g;
+      *reinterpret_cast<float4*>(o) =
+          make_float4(dk[t][0] * scale, dk[t][1] * scale, dk[t][2] * scale, dk[t][3] * scale);
+      *reinterpret_cast<float4*>(o + 8 * H) = make_float4(dv[t][0], dv[t][1], dv[t][2], dv[t][3]);
+    }
   }
 }
 
@@ -436,10 +549,12 @@ __global__ void __launch_bounds__(256) attn8_delta_pack_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------------------ host
+constexpr int kRT = 2;  // row tiles per wave
+
 static int pick_splits(int N, int H, int64_t splits) {
   if (splits > 0) return (int)splits;
   // >= ~5 waves per SIMD over 256 CUs x 4 SIMDs: blocks x H x S x 4 waves >= 5120
-  const int blocks = ceil_div(N, 64) * H;
+  const int blocks = ceil_div(N, 64 * kRT) * H;
   int S = 1;
   while (S < 16 && (int64_t)blocks * S * 4 < 5120 && N / (S * 2) >= 128) S *= 2;
   return S;
@@ -484,15 +599,15 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
   if (N == 0) return {O, L};
   const int S = pick_splits((int)N, (int)H, splits);
   const float qs = (float)scale * kLog2e;
-  dim3 grid(ceil_div(N, 64), H, S);
+  dim3 grid(ceil_div(N, 64 * kRT), H, S);
   if (S == 1) {
-    attn8_fwd_kernel<<<grid, 256, 0, stream()>>>(Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(),
+    attn8_fwd_kernel<kRT><<<grid, 256, 0, stream()>>>(Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(),
                                                  (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
                                                  seg_ptr.data_ptr<int>(), 1, qs, nullptr, O.data_ptr<float>(),
                                                  L.data_ptr<float>());
   } else {
     auto part = at::empty({S, H, N, 10}, opt);
-    attn8_fwd_kernel<<<grid, 256, 0, stream()>>>(Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(),
+    attn8_fwd_kernel<kRT><<<grid, 256, 0, stream()>>>(Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(),
                                                  (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
                                                  seg_ptr.data_ptr<int>(), S, qs, part.data_ptr<float>(), nullptr,
                                                  nullptr);
@@ -520,25 +635,25 @@ at::Tensor attn8_bwd(const at::Tensor& dO_, const at::Tensor& O, const at::Tenso
       dOp.data_ptr<float>(), dOq.data_ptr<float>());
   const int S = pick_splits((int)N, (int)H, splits);
   const float qs = (float)scale * kLog2e;
-  dim3 grid(ceil_div(N, 64), H, S);
+  dim3 grid(ceil_div(N, 64 * kRT), H, S);
   const int F = (int)(8 * H);
   if (S == 1) {
-    attn8_bwd_dq_kernel<<<grid, 256, 0, stream()>>>(
+    attn8_bwd_dq_kernel<kRT><<<grid, 256, 0, stream()>>>(
         Qp.data_ptr<float>(), Kp.data_ptr<float>(), Kq.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
         LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
         seg_ptr.data_ptr<int>(), 1, (float)scale, qs, dqkv.data_ptr<float>(), 3 * F, 0);
-    attn8_bwd_dkv_kernel<<<grid, 256, 0, stream()>>>(
+    attn8_bwd_dkv_kernel<kRT><<<grid, 256, 0, stream()>>>(
         Qp.data_ptr<float>(), Qq.data_ptr<float>(), Kp.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
         dOq.data_ptr<float>(), LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H,
         seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), 1, (float)scale, qs, dqkv.data_ptr<float>() + F, 3 * F, 0);
     return dqkv;
   }
   auto pq = at::empty({S, N, F}, opt), pkv = at::empty({S, N, 2 * F}, opt);
-  attn8_bwd_dq_kernel<<<grid, 256, 0, stream()>>>(
+  attn8_bwd_dq_kernel<kRT><<<grid, 256, 0, stream()>>>(
       Qp.data_ptr<float>(), Kp.data_ptr<float>(), Kq.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
       LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
       seg_ptr.data_ptr<int>(), S, (float)scale, qs, pq.data_ptr<float>(), F, N * F);
-  attn8_bwd_dkv_kernel<<<grid, 256, 0, stream()>>>(
+  attn8_bwd_dkv_kernel<kRT><<<grid, 256, 0, stream()>>>(
       Qp.data_ptr<float>(), Qq.data_ptr<float>(), Kp.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
       dOq.data_ptr<float>(), LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H,
       seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), S, (float)scale, qs, pkv.data_ptr<float>(), 2 * F,

@@ -512,17 +512,24 @@ __global__ void __launch_bounds__(256) mlp_fwd_kernel(MlpFwd a) {
 
 // ------------------------------------------------------------------------------------
 // Forward 5 (after the last layer): x_L = relu(A z3 + B), rows >= nv -> 0.
+// With a graph CSR (gptr [G+1]) the same launch also mean-pools x_L per graph
+// (reference Base.py:478 global_mean_pool): workgroups [0, G) pool one graph each
+// (recomputing its rows' x on the fly), the rest write x_L row-parallel.
 struct FinalFwd {
   const float* z3;
   PairFin pf;
   float* x;
   const int* nvp;
   int N;
+  const int* gptr;  // [G + 1] or null
+  int G;
+  float* pooled;    // [G, F]
 };
 
 template <int F>
 __global__ void __launch_bounds__(256) final_fwd_kernel(FinalFwd a) {
   __shared__ float cA[F], cB[F];
+  __shared__ float red[256 / F][F];
   const int nv = a.nvp ? min(*a.nvp, a.N) : a.N;
   if (threadIdx.x < F) {
     float A, B;
@@ -535,8 +542,26 @@ __global__ void __launch_bounds__(256) final_fwd_kernel(FinalFwd a) {
     }
   }
   __syncthreads();
+  if ((int)blockIdx.x < a.G) {
+    constexpr int RPP = 256 / F;  // rows per pass
+    const int gb = a.gptr[blockIdx.x], ge = a.gptr[blockIdx.x + 1];
+    const int c = threadIdx.x % F, rl = threadIdx.x / F;
+    float acc = 0.f;
+    for (int row = gb + rl; row < ge; row += RPP)
+      if (row < nv) acc += fmaxf(cA[c] * a.z3[(int64_t)row * F + c] + cB[c], 0.f);
+    red[rl][c] = acc;
+    __syncthreads();
+    if (threadIdx.x < F) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < RPP; ++q) t += red[q][threadIdx.x];
+      a.pooled[(int64_t)blockIdx.x * F + threadIdx.x] = t / (float)max(ge - gb, 1);
+    }
+    return;
+  }
   const int64_t total = (int64_t)a.N * F / 4;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+  const int64_t nb = (int64_t)gridDim.x - a.G;
+  for (int64_t t = ((int64_t)blockIdx.x - a.G) * 256 + threadIdx.x; t < total; t += nb * 256) {
     const int row = (int)(t / (F / 4)), c = (int)(t % (F / 4)) * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row < nv) {
@@ -561,7 +586,7 @@ __global__ void __launch_bounds__(256) final_fwd_kernel(FinalFwd a) {
 
 // Pair statistics of the last layer: g = dxL * [xL > 0] -> S1, S2 (site [NREP][2][F]).
 struct PairStatsBwd {
-  const float* dx;
+  const float* dx;     // [N, F] or null
   const float* x;      // relu output (mask)
   const float* z3;
   const float* saved;  // layer's [S_N][F]
@@ -569,6 +594,9 @@ struct PairStatsBwd {
   double* site;
   const int* nvp;
   int N;
+  const float* dpool;  // [G, F] gradient of the per-graph mean pool, or null
+  const int* gidx;     // [N] graph of each row
+  const int* gptr;     // [G + 1]
 };
 
 template <int F>
@@ -585,7 +613,12 @@ __global__ void __launch_bounds__(256) pair_stats_bwd_kernel(PairStatsBwd a) {
       const int row = row0 + 4 * gq + r;
       if (row < a.N) {
         const int64_t o = (int64_t)row * F + col;
-        const float gv = (row < nv && a.x[o] > 0.f) ? a.dx[o] : 0.f;
+        float up = a.dx ? a.dx[o] : 0.f;
+        if (a.dpool) {
+          const int gi = a.gidx[row];
+          up += a.dpool[(int64_t)gi * F + col] / (float)max(a.gptr[gi + 1] - a.gptr[gi], 1);
+        }
+        const float gv = (row < nv && a.x[o] > 0.f) ? up : 0.f;
         a.g[o] = gv;
         if (row < nv) {
           s1 += gv;
@@ -1065,6 +1098,97 @@ __global__ void __launch_bounds__(256) edge_bwd_kernel(EdgeBwd a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// GPS input embeddings (reference Base.py:229-243, _embedding):
+//   node: x0 = node_lin(cat[node_emb(x), pos_emb(pe)]),  rows >= nv -> 0
+//   edge: e  = edge_lin(cat[edge_emb(edge_attr), rel_pos_emb(rel_pe)])
+// all bias-free: y = [A Wa^T | B Wb^T] Wl^T with narrow A, B (1-16 columns).  One launch
+// per embedding: the [M, 2F] concat tile is built in LDS (kept for the weight gradient
+// dWl = dy^T ab) and multiplied on the spot.  Backward: dab = dy Wl (one launch); the three
+// weight gradients are rows of the encoder's grouped reduction.
+struct EmbFwd {
+  const float* A;   // [M, ka]
+  const float* B;   // [M, kb]
+  const float* Wa;  // [F, ka]
+  const float* Wb;  // [F, kb]
+  const float* Wl;  // [F, 2F]
+  float* y;         // [M, F]
+  float* ab;        // [M, 2F]
+  int ka, kb, M;
+  const int* nvp;   // rows >= *nvp -> 0 (node embedding of a padded batch) or null
+};
+
+template <int F>
+__global__ void __launch_bounds__(256) emb_fwd_kernel(EmbFwd a) {
+  constexpr int LD = 2 * F + 4;
+  __shared__ __attribute__((aligned(16))) float abs_[BM * LD];
+  __shared__ float in[BM][33];  // [A | B] of the tile, <= 16 + 16 columns
+  const int row0 = blockIdx.x * BM;
+  const int kt = a.ka + a.kb;
+  for (int idx = threadIdx.x; idx < BM * kt; idx += 256) {
+    const int r = idx / kt, c = idx % kt, row = row0 + r;
+    float v = 0.f;
+    if (row < a.M) v = c < a.ka ? a.A[(int64_t)row * a.ka + c] : a.B[(int64_t)row * a.kb + (c - a.ka)];
+    in[r][c] = v;
+  }
+  __syncthreads();
+  // first stage (K <= 16): plain fp32 dot products, one output per thread-iteration
+  for (int idx = threadIdx.x; idx < BM * 2 * F; idx += 256) {
+    const int r = idx / (2 * F), c = idx % (2 * F);
+    float acc = 0.f;
+    if (c < F) {
+      for (int k = 0; k < a.ka; ++k) acc = fmaf(in[r][k], a.Wa[c * a.ka + k], acc);
+    } else {
+      for (int k = 0; k < a.kb; ++k) acc = fmaf(in[r][a.ka + k], a.Wb[(c - F) * a.kb + k], acc);
+    }
+    abs_[r * LD + c] = acc;
+    const int row = row0 + r;
+    if (row < a.M) a.ab[(int64_t)row * 2 * F + c] = acc;
+  }
+  __syncthreads();
+  const int nv = a.nvp ? min(*a.nvp, a.M) : a.M;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  for (int t = w; t < F / 16; t += 4) {
+    const int n0 = 16 * t, col = n0 + i;
+    f4v acc = tile_mma<true>(abs_, LD, a.Wl + (int64_t)n0 * 2 * F, 2 * F, 0, 2 * F, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * g + r;
+      if (row < a.M) a.y[(int64_t)row * F + col] = row < nv ? acc[r] : 0.f;
+    }
+  }
+}
+
+struct EmbBwd {
+  const float* dy;  // [M, F]
+  const float* Wl;  // [F, 2F]
+  float* dab;       // [M, 2F]
+  int M;
+};
+
+template <int F>
+__global__ void __launch_bounds__(256) emb_bwd_kernel(EmbBwd a) {
+  constexpr int LD = F + 4;
+  __shared__ __attribute__((aligned(16))) float gs[BM * LD];
+  const int row0 = blockIdx.x * BM;
+  for (int idx = threadIdx.x; idx < BM * F / 4; idx += 256) {
+    const int r = idx / (F / 4), c = (idx % (F / 4)) * 4, row = row0 + r;
+    *reinterpret_cast<float4*>(gs + r * LD + c) =
+        row < a.M ? *reinterpret_cast<const float4*>(a.dy + (int64_t)row * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  for (int t = w; t < 2 * F / 16; t += 4) {
+    const int n0 = 16 * t, col = n0 + i;
+    f4v acc = tile_mma<false>(gs, LD, a.Wl, 2 * F, 0, F, n0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * g + r;
+      if (row < a.M) a.dab[(int64_t)row * 2 * F + col] = acc[r];
+    }
+  }
+}
+
 // ====================================================================================
 // host side
 static Drop mk_drop(const c10::optional<at::Tensor>& rng, int64_t salt, double p) {
@@ -1254,16 +1378,21 @@ std::vector<at::Tensor> gf_mlp_fwd(const at::Tensor& z1, const at::Tensor& z2, c
   return {out, md, z3};
 }
 
-at::Tensor gf_final_fwd(const at::Tensor& z3, const at::Tensor& acc, const at::Tensor& saved,
-                        const std::vector<at::Tensor>& bn, const c10::optional<at::Tensor>& rm3,
-                        const c10::optional<at::Tensor>& rv3, const c10::optional<at::Tensor>& nbt3,
-                        const c10::optional<at::Tensor>& rm4, const c10::optional<at::Tensor>& rv4,
-                        const c10::optional<at::Tensor>& nbt4, double mom3, double eps3, double mom4, double eps4,
-                        const c10::optional<at::Tensor>& nv) {
+std::vector<at::Tensor> gf_final_fwd(const at::Tensor& z3, const at::Tensor& acc, const at::Tensor& saved,
+                                     const std::vector<at::Tensor>& bn, const c10::optional<at::Tensor>& rm3,
+                                     const c10::optional<at::Tensor>& rv3, const c10::optional<at::Tensor>& nbt3,
+                                     const c10::optional<at::Tensor>& rm4, const c10::optional<at::Tensor>& rv4,
+                                     const c10::optional<at::Tensor>& nbt4, double mom3, double eps3, double mom4,
+                                     double eps4, const c10::optional<at::Tensor>& nv,
+                                     const c10::optional<at::Tensor>& gptr) {
   const int64_t N = z3.size(0), F = z3.size(1);
   chk(z3, N, F, "z3");
   HY_CHECK(bn.size() == 4, "gf_final_fwd: bn = [w3, b3, w4, b4]");
   auto x = at::empty({N, F}, z3.options());
+  const bool pool = gptr.has_value() && gptr->defined();
+  const int64_t G = pool ? gptr->numel() - 1 : 0;
+  if (pool) HY_CHECK(gptr->scalar_type() == at::kInt && gptr->is_contiguous(), "gf_final_fwd: gptr int32");
+  auto pooled = at::empty({G, F}, z3.options());
   FinalFwd a{};
   a.z3 = z3.data_ptr<float>();
   a.pf.site = site_ptr(acc, 2, (int)F);
@@ -1273,9 +1402,12 @@ at::Tensor gf_final_fwd(const at::Tensor& z3, const at::Tensor& acc, const at::T
   a.x = x.data_ptr<float>();
   a.nvp = nvptr(nv);
   a.N = (int)N;
+  a.gptr = pool ? gptr->data_ptr<int>() : nullptr;
+  a.G = (int)G;
+  a.pooled = pool ? pooled.data_ptr<float>() : nullptr;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(N * F / 4, 256), 1024));
-  HY_GF_DISPATCH(F, final_fwd_kernel, blocks, 256, a);
-  return x;
+  HY_GF_DISPATCH(F, final_fwd_kernel, blocks + (int)G, 256, a);
+  return {x, pooled};
 }
 
 #define HY_GF_EDGE(F, D, KERN, GRID, ARGS)                                          \
@@ -1349,18 +1481,61 @@ std::vector<at::Tensor> gf_edge_bwd(const at::Tensor& dC_, const at::Tensor& Wr,
   return {dr, de, drbf};
 }
 
+std::vector<at::Tensor> gf_embed_fwd(const at::Tensor& A_, const at::Tensor& B_, const at::Tensor& Wa,
+                                     const at::Tensor& Wb, const at::Tensor& Wl, const c10::optional<at::Tensor>& nv) {
+  at::Tensor A = A_.contiguous(), B = B_.contiguous();
+  const int64_t M = A.size(0), F = Wl.size(0), ka = A.size(1), kb = B.size(1);
+  HY_CHECK(B.size(0) == M && ka >= 1 && kb >= 1 && ka <= 16 && kb <= 16 && A.scalar_type() == at::kFloat &&
+               B.scalar_type() == at::kFloat,
+           "gf_embed_fwd: inputs [M, 1..16] fp32");
+  chk(Wa, F, ka, "Wa");
+  chk(Wb, F, kb, "Wb");
+  chk(Wl, F, 2 * F, "Wl");
+  auto y = at::empty({M, F}, A.options()), ab = at::empty({M, 2 * F}, A.options());
+  if (M == 0) return {y, ab};
+  EmbFwd a{A.data_ptr<float>(), B.data_ptr<float>(), Wa.data_ptr<float>(), Wb.data_ptr<float>(), Wl.data_ptr<float>(),
+           y.data_ptr<float>(), ab.data_ptr<float>(), (int)ka, (int)kb, (int)M, nvptr(nv)};
+  HY_GF_DISPATCH(F, emb_fwd_kernel, ceil_div(M, BM), 256, a);
+  return {y, ab};
+}
+
+at::Tensor gf_embed_bwd(const at::Tensor& dy_, const at::Tensor& Wl) {
+  at::Tensor dy = dy_.contiguous();
+  const int64_t M = dy.size(0), F = dy.size(1);
+  chk(Wl, F, 2 * F, "Wl");
+  auto dab = at::empty({M, 2 * F}, dy.options());
+  if (M == 0) return dab;
+  EmbBwd a{dy.data_ptr<float>(), Wl.data_ptr<float>(), dab.data_ptr<float>(), (int)M};
+  HY_GF_DISPATCH(F, emb_bwd_kernel, ceil_div(M, BM), 256, a);
+  return dab;
+}
+
 // ---- backward ops -------------------------------------------------------------------
-at::Tensor gf_pair_stats_bwd(const at::Tensor& dx, const at::Tensor& x, const at::Tensor& z3, const at::Tensor& saved,
-                             const at::Tensor& acc, const c10::optional<at::Tensor>& nv) {
+at::Tensor gf_pair_stats_bwd(const c10::optional<at::Tensor>& dx, const at::Tensor& x, const at::Tensor& z3,
+                             const at::Tensor& saved, const at::Tensor& acc, const c10::optional<at::Tensor>& nv,
+                             const c10::optional<at::Tensor>& dpool, const c10::optional<at::Tensor>& gidx,
+                             const c10::optional<at::Tensor>& gptr) {
   const int64_t N = z3.size(0), F = z3.size(1);
   chk(z3, N, F, "z3");
   chk(x, N, F, "x");
-  at::Tensor d = dx.contiguous();
-  chk(d, N, F, "dx");
+  at::Tensor d;
+  if (dx.has_value() && dx->defined()) {
+    d = dx->contiguous();
+    chk(d, N, F, "dx");
+  }
+  at::Tensor dp;
+  if (dpool.has_value() && dpool->defined()) {
+    dp = dpool->contiguous();
+    HY_CHECK(gidx.has_value() && gptr.has_value() && gidx->scalar_type() == at::kInt && gidx->numel() == N &&
+                 gptr->scalar_type() == at::kInt && dp.size(0) == gptr->numel() - 1 && dp.size(1) == F,
+             "gf_pair_stats_bwd: pooled gradient needs graph index / pointers");
+  }
   auto g = at::empty({N, F}, z3.options());
   if (N == 0) return g;
-  PairStatsBwd a{d.data_ptr<float>(), x.data_ptr<float>(), z3.data_ptr<float>(), saved.data_ptr<float>(),
-                 g.data_ptr<float>(), site_ptr(acc, 3, (int)F), nvptr(nv), (int)N};
+  PairStatsBwd a{d.defined() ? d.data_ptr<float>() : nullptr, x.data_ptr<float>(), z3.data_ptr<float>(),
+                 saved.data_ptr<float>(), g.data_ptr<float>(), site_ptr(acc, 3, (int)F), nvptr(nv), (int)N,
+                 dp.defined() ? dp.data_ptr<float>() : nullptr, dp.defined() ? gidx->data_ptr<int>() : nullptr,
+                 dp.defined() ? gptr->data_ptr<int>() : nullptr};
   HY_GF_DISPATCH(F, pair_stats_bwd_kernel, ceil_div(N, BM), 256, a);
   return g;
 }
@@ -1493,12 +1668,16 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "gf_final_fwd(Tensor z3, Tensor acc, Tensor(a!) saved, Tensor[] bn, Tensor(b!)? rm3, Tensor(c!)? rv3, "
       "Tensor(d!)? nbt3, Tensor(e!)? rm4, Tensor(f!)? rv4, Tensor(g!)? nbt4, float mom3, float eps3, float mom4, "
-      "float eps4, Tensor? nv) -> Tensor");
+      "float eps4, Tensor? nv, Tensor? gptr) -> Tensor[]");
+  m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor[]");
+  m.def("gf_embed_bwd(Tensor dy, Tensor Wl) -> Tensor");
   m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
   m.def(
       "gf_edge_bwd(Tensor dC, Tensor Wr, Tensor Wd, Tensor? rmask, Tensor(a!)? de_acc, Tensor? dG, Tensor? Wemb, "
       "Tensor? Wlin, Tensor(b!)? drbf_acc, int K) -> Tensor[]");
-  m.def("gf_pair_stats_bwd(Tensor dx, Tensor x, Tensor z3, Tensor saved, Tensor(a!) acc, Tensor? nv) -> Tensor");
+  m.def(
+      "gf_pair_stats_bwd(Tensor? dx, Tensor x, Tensor z3, Tensor saved, Tensor(a!) acc, Tensor? nv, Tensor? dpool, "
+      "Tensor? gidx, Tensor? gptr) -> Tensor");
   m.def(
       "gf_mlp_bwd(Tensor g, Tensor z3, Tensor(a!) acc, Tensor saved, Tensor g3, Tensor g4, float eps3, float eps4, "
       "Tensor md, Tensor W2, Tensor W1, Tensor z1, Tensor z2, Tensor? rng, int salt2, int salt3, float p, Tensor? nv) "
@@ -1520,6 +1699,8 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gf_post_fwd", hy::gf::gf_post_fwd);
   m.impl("gf_mlp_fwd", hy::gf::gf_mlp_fwd);
   m.impl("gf_final_fwd", hy::gf::gf_final_fwd);
+  m.impl("gf_embed_fwd", hy::gf::gf_embed_fwd);
+  m.impl("gf_embed_bwd", hy::gf::gf_embed_bwd);
   m.impl("gf_edge_fwd", hy::gf::gf_edge_fwd);
   m.impl("gf_edge_bwd", hy::gf::gf_edge_bwd);
   m.impl("gf_pair_stats_bwd", hy::gf::gf_pair_stats_bwd);

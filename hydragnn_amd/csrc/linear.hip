@@ -297,6 +297,67 @@ __device__ __forceinline__ int wg_find(KWgArgs* A, int b, bool reduce) {
   return pi;
 }
 
+// Narrow problems (I <= 16: radial-basis, embedding and frequency weights over E rows): a
+// 64 x 64 register tile would waste >= 75% of its FMAs, so the lane owns one output row o
+// (64 per workgroup) and all I columns; waves stride the slab's rows (4 in flight each),
+// folded in a fixed order through LDS.  Same partial layout as wgrad_partial_body.
+constexpr int kWgNarrow = 16;
+
+__device__ __forceinline__ void wgrad_narrow_body(float4* smem, const float* __restrict__ dY, int ldy,
+                                                  const float* __restrict__ X, int ldx, float* __restrict__ part,
+                                                  int with_bias, int M, int O, int I, int rows_per_block, int tile,
+                                                  int s) {
+  constexpr int ST = kWgNarrow + 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = tile * 64 + lane, oc = min(o, O - 1);
+  const int r0 = s * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float* xs = reinterpret_cast<float*>(smem);  // [64 rows][ST]: the chunk's X rows, broadcast reads
+  float acc[kWgNarrow], bacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < kWgNarrow; ++k) acc[k] = 0.f;
+  for (int c0 = r0; c0 < r1; c0 += 64) {
+    const int nrow = min(64, r1 - c0);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 64 * kWgNarrow; idx += 256) {
+      const int c = idx / kWgNarrow, k = idx % kWgNarrow;
+      xs[c * ST + k] = (c < nrow && k < I) ? X[(int64_t)(c0 + min(c, nrow - 1)) * ldx + min(k, I - 1)] : 0.f;
+    }
+    // this wave's 16 rows of the chunk: all dY loads in flight before the FMAs
+    float y[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int c = w * 16 + u;
+      const float v = dY[(int64_t)(c0 + min(c, nrow - 1)) * ldy + oc];
+      y[u] = c < nrow ? v : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float* xr = xs + (w * 16 + u) * ST;
+      bacc += y[u];
+#pragma unroll
+      for (int k = 0; k < kWgNarrow; ++k) acc[k] = fmaf(y[u], xr[k], acc[k]);
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4][64][ST]
+#pragma unroll
+  for (int k = 0; k < kWgNarrow; ++k) red[(w * 64 + lane) * ST + k] = acc[k];
+  red[(w * 64 + lane) * ST + kWgNarrow] = bacc;
+  __syncthreads();
+  float* P = part + (int64_t)s * ((int64_t)O * I + O);
+  for (int idx = threadIdx.x; idx < 64 * ST; idx += 256) {
+    const int ol = idx / ST, k = idx % ST, oo = tile * 64 + ol;
+    if (oo >= O) continue;
+    const float v = ((red[(0 * 64 + ol) * ST + k] + red[(1 * 64 + ol) * ST + k]) + red[(2 * 64 + ol) * ST + k]) +
+                    red[(3 * 64 + ol) * ST + k];
+    if (k < I)
+      P[(int64_t)oo * I + k] = v;
+    else if (k == kWgNarrow && with_bias)
+      P[(int64_t)O * I + oo] = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
   __shared__ float4 smem[2 * 2 * kWC * 16];
   KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -308,6 +369,10 @@ __global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
   const int tile = local % tiles, s = local / tiles;
   float* part = A->ws + P.part_off;
   const int wb = P.db != nullptr ? 1 : 0;
+  if (P.vec & 4) {
+    wgrad_narrow_body(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, tile, s);
+    return;
+  }
   switch (P.vec) {
     case 3: wgrad_partial_body<true, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
     case 1: wgrad_partial_body<true, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
@@ -404,7 +469,8 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.M = (int)M;
       P.O = O;
       P.I = I;
-      P.tiles_i = ceil_div(I, kWT);
+      const bool narrow = I <= kWgNarrow;
+      P.tiles_i = narrow ? 1 : ceil_div(I, kWT);
       const int tiles = ceil_div(O, kWT) * P.tiles_i;
       // at most kWgMaxSlabs slabs per problem: the reduce pass reads S partial tiles
       const int rpb = std::max(rps, ceil_div(ceil_div(M, kWgMaxSlabs), kWC) * kWC);
@@ -420,7 +486,7 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
       const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
       const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);
-      P.vec = (vy ? 1 : 0) | (vx ? 2 : 0);
+      P.vec = (vy ? 1 : 0) | (vx ? 2 : 0) | (narrow ? 4 : 0);
       P.accumulate = accumulate[k] ? 1 : 0;
     }
     auto ws = at::empty({part_total}, dYs[c0].options());

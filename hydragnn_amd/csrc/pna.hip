@@ -237,6 +237,17 @@ static const float* opt_edge_ptr(const c10::optional<at::Tensor>& t, int64_t E, 
   return t->data_ptr<float>();
 }
 
+// One wave per node (lane = feature, 4-byte gathers) for F = 64 instead of 16 lanes x
+// float4: 4x the waves in flight for the latency-bound edge gathers (OC20 GPS step on
+// MI355X: 1.438 vs 1.457 ms, tools/gpu_r3_iter.sh).  HYDRA_PNA_WAVE=0 restores float4 lanes.
+static bool pna_wave_per_node(int F) {
+  static const int on = [] {
+    const char* e = std::getenv("HYDRA_PNA_WAVE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return on && F == 64;
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_fwd(const at::Tensor& x, const at::Tensor& AB,
                                                        const c10::optional<at::Tensor>& C_,
                                                        const c10::optional<at::Tensor>& G_,
@@ -259,7 +270,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_fwd(const at::Tensor& x, cons
   if (N == 0) return {Z, amin, amax};
   const int ldab = (int)AB.stride(0);
   const bool v4 = (F % 4 == 0) && (ldab % 4 == 0) &&
-                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0);
+                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0) && !pna_wave_per_node(F);
   auto g = row_geom(N, v4 ? F : 4 * F);
   if (v4)
     pna_fwd_kernel<4><<<g.blocks, 256, 0, stream()>>>(
@@ -295,7 +306,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_bwd(const at::Tensor& dZ_, co
   if (N == 0) return {dpre, dG, dA};
   const int ldab = (int)AB.stride(0);
   const bool v4 = (F % 4 == 0) && (ldab % 4 == 0) &&
-                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0);
+                  (reinterpret_cast<uintptr_t>(AB.data_ptr<float>()) % 16 == 0) && !pna_wave_per_node(F);
   auto g = row_geom(N, v4 ? F : 4 * F);
   if (v4)
     pna_bwd_kernel<4><<<g.blocks, 256, 0, stream()>>>(

@@ -272,9 +272,22 @@ class Base(nn.Module):
         else:
             ctx.edge_attr = None
         if self.use_global_attn:
+            if self._gps_embed_lazy(data):
+                # a whole-encoder fused path may absorb the embedding (``_fused_encode``);
+                # ``_materialize_embed`` runs the module embedding otherwise
+                ctx.gps_lazy, ctx.edge_attr_raw = True, ctx.edge_attr
+                ctx.edge_attr = None
+                return None, data.pos, ctx
             x = self._gps_embed(data, ctx, ctx.edge_attr)
             return x, data.pos, ctx
         return data.x, data.pos, ctx
+
+    def _gps_embed_lazy(self, data):
+        return False
+
+    def _materialize_embed(self, ctx):
+        ctx.gps_lazy = False
+        return self._gps_embed(ctx.data, ctx, ctx.edge_attr_raw)
 
     def _run_conv(self, conv, inv, equiv, ctx):
         if self.conv_checkpointing and self.training:
@@ -284,11 +297,13 @@ class Base(nn.Module):
     def encode(self, data):
         inv, equiv, ctx = self._embedding(data)
         keep = data.get("node_mask")  # statically padded batch: keep dummy rows at zero
-        if keep is not None:
-            inv = _zero_rows(inv, keep)
         fused = self._fused_encode(inv, equiv, ctx)
         if fused is not None:
             return fused
+        if ctx.get("gps_lazy"):
+            inv = self._materialize_embed(ctx)
+        if keep is not None:
+            inv = _zero_rows(inv, keep)
         for conv, bn in zip(self.graph_convs, self.feature_layers):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
             if isinstance(self.activation_function, torch.nn.ReLU) and isinstance(bn, BatchNorm):
@@ -358,7 +373,9 @@ class Base(nn.Module):
     def decode(self, x, equiv, ctx):
         data = ctx.data
         gsi = ctx.graph_si
-        if gsi is None:
+        if ctx.get("pooled") is not None:
+            x_graph = ctx.pooled  # pooled by a fused encoder
+        elif gsi is None:
             x_graph = x.mean(dim=0, keepdim=True)
         else:
             x_graph = seg.segment_mean(x, gsi)

@@ -135,13 +135,18 @@ class PNAPlusStack(Base):
         else:
             ctx.rbf = self.rbf(ctx.dist)
 
-    def _fused_encode(self, inv, equiv, ctx):
-        # GPS + PNAPlus training on the GPU: the whole conv stack in one autograd function
-        # over csrc/gps_fused.hip (ops/gps_encoder.py)
+    def _gps_embed_lazy(self, data):
         from ..ops import gps_encoder
 
-        if self.use_global_attn and gps_encoder.eligible(self, inv, ctx):
-            return gps_encoder.encode(self, inv, ctx), equiv, ctx
+        return gps_encoder.pre_eligible(self, data)
+
+    def _fused_encode(self, inv, equiv, ctx):
+        # GPS + PNAPlus training on the GPU: embedding + radial basis + the whole conv stack in
+        # one autograd function over csrc/gps_fused.hip (ops/gps_encoder.py)
+        from ..ops import gps_encoder
+
+        if self.use_global_attn and ctx.get("gps_lazy") and gps_encoder.eligible(self, ctx):
+            return gps_encoder.encode(self, ctx), equiv, ctx
         self._materialize_radial(ctx)
         return None
 

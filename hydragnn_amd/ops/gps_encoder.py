@@ -48,16 +48,26 @@ def _bn_ok(m, F):
             and b.num_features == F)
 
 
-def eligible(model, x, ctx):
+def pre_eligible(model, data):
+    """Cheap checks before the embedding runs (the fused path absorbs the GPS embedding)."""
+    x = data.get("x")
+    return (model.training and x is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+            and model.input_dim and 1 <= x.shape[1] <= 16 and data.get("pe") is not None
+            and data.pe.shape[1] <= 16 and model.is_edge_model and model.use_edge_attr
+            and data.get("edge_attr") is not None and data.edge_attr.dim() == 2 and data.edge_attr.shape[1] <= 16
+            and data.get("rel_pe") is not None and data.rel_pe.shape[1] <= 16
+            and not (data.x.requires_grad or data.pe.requires_grad or data.edge_attr.requires_grad)
+            and _mode.fused("gpsfused") and model.hidden_dim in (32, 64))
+
+
+def eligible(model, ctx):
     """True when the fused encoder reproduces ``Base.encode`` for this model and batch."""
     from ..models.gps import GPSConv, MultiheadAttention
     from ..models.pnaplus import PNAConvFused
-    from ..ops.attention import segment_attention  # noqa: F401
 
-    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and _mode.fused("gpsfused")
-            and _mode.fused("attn") and _mode.fused("pna") and model.training):
+    if not (_mode.fused("gpsfused") and _mode.fused("attn") and _mode.fused("pna") and model.training):
         return False
-    F = x.shape[1]
+    F = model.hidden_dim
     if F not in (32, 64) or model.conv_checkpointing:
         return False
     if not isinstance(model.activation_function, torch.nn.ReLU):
@@ -69,8 +79,7 @@ def eligible(model, x, ctx):
         return False  # the radial basis is computed inside the encoder (no force training)
     if ctx.rbf_basis.freq.numel() > MAX_K or len(model.graph_convs) > MAX_L or not _mode.fused("radial"):
         return False
-    if ctx.get("edge_attr") is None or ctx.edge_attr.shape[1] + F > 188:
-        return False
+
     if ctx.dst_si is None or ctx.dst_si.perm is not None or ctx.get("attn_seg_id") is None:
         return False
     for conv, bn in zip(model.graph_convs, model.feature_layers):
@@ -111,15 +120,17 @@ class _Cfg:
     pass
 
 
-def encode(model, x0, ctx):
+def encode(model, ctx):
     """Run the fused encoder: returns x_L (the input of the decoder heads)."""
     from . import rng as _rng
     from .attention import _SPLITS, _max_span
 
+    data = ctx.data
+    x0 = data.x
     cfg = _Cfg()
     convs = list(model.graph_convs)
     cfg.L = len(convs)
-    cfg.F = x0.shape[1]
+    cfg.F = model.hidden_dim
     cfg.bns = [(_bn(c.norm1), _bn(c.norm2), _bn(c.norm3), _bn(b)) for c, b in zip(convs, model.feature_layers)]
     cfg.salts = [list(c._salts) for c in convs]
     cfg.p = float(convs[0].dropout) if model.training else 0.0
@@ -140,16 +151,23 @@ def encode(model, x0, ctx):
     cfg.side = _streams.enabled(x0)
     # 8-wide heads: MFMA attention (csrc/attention8.hip) on operands the node kernel packs
     cfg.a8 = cfg.F // cfg.heads == 8 and _mode.fused("attn8")
-    # edge-row GEMMs (C forward, dr/de dgrad) on the MFMA tile kernels when the edge width
-    # equals the hidden width (the GPS edge embedding)
-    cfg.edge_mfma = ctx.edge_attr.shape[1] == cfg.F and _mode.fused("edgemfma")
+
     basis = ctx.rbf_basis
     cfg.cutoff, cfg.exponent = float(basis.cutoff), int(basis.envelope.p - 1)
     flat = []
     for c, b in zip(convs, model.feature_layers):
         flat += _layer_params(c, b)
-    return _GPSEncoder.apply(cfg, x0.contiguous(), ctx.edge_attr.contiguous(), ctx.dist.contiguous(), basis.freq,
-                             *flat)
+    emb = [model.node_emb.weight, model.pos_emb.weight, model.node_lin.weight,
+           model.edge_emb.weight, model.rel_pos_emb.weight, model.edge_lin.weight]
+    ins = [data.x.float().contiguous(), data.pe.contiguous(), ctx.edge_attr_raw.contiguous(), data.rel_pe.contiguous()]
+    gsi = ctx.get("graph_si")
+    cfg.gptr = gsi.rowptr if (gsi is not None and gsi.rowptr.dtype == torch.int32
+                              and gsi.index.dtype == torch.int32 and gsi.rowptr.is_cuda) else None
+    cfg.gidx = gsi.index if cfg.gptr is not None else None
+    xL, pooled = _GPSEncoder.apply(cfg, ctx.dist.contiguous(), basis.freq, *ins, *emb, *flat)
+    if cfg.gptr is not None:
+        ctx.pooled = pooled  # per-graph mean of x_L (Base.decode), pooled inside the final launch
+    return xL
 
 
 class _Side:
@@ -196,11 +214,14 @@ def _bn_state(b):
 
 class _GPSEncoder(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg, x0, e, dist, freq, *flat):
+    def forward(ctx, cfg, dist, freq, xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, *flat):
         ops = _native.ops()
         L, F = cfg.L, cfg.F
         prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
-        dev = x0.device
+        dev = xin.device
+        # GPS input embeddings (node rows >= num_valid -> 0), one launch each
+        x0, ab_n = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
+        e, ab_e = ops.gf_embed_fwd(eattr, rpe, Wee, Wrp, Wel, None)
         # Bessel basis + every layer's radial embedding / gate in one launch; the basis and its
         # frequency derivative are kept for the weight gradients
         ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
@@ -239,7 +260,7 @@ class _GPSEncoder(torch.autograd.Function):
                 else:
                     O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
                 z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
-            C = ops.gf_edge_fwd(r, e, Wr, Wd, bc) if cfg.edge_mfma else ops.edge_linear_fwd([r, e], [Wr, Wd], bc)
+            C = ops.gf_edge_fwd(r, e, Wr, Wd, bc)
             Z, amin, amax = ops.pna_fwd(x, AB, C, G, cfg.src.index, cfg.dst.rowptr, cfg.avg[l][0], cfg.avg[l][1])
             pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
             side.join(O, LSE, z2)
@@ -254,29 +275,34 @@ class _GPSEncoder(torch.autograd.Function):
         rm3, rv3, nb3, m3, e3 = _bn_state(n3)
         rm4, rv4, nb4, m4, e4 = _bn_state(n4)
         pp = prm[L - 1]
-        xL = ops.gf_final_fwd(z3, acc[L - 1], saved[L - 1], [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3, rm4, rv4,
-                              nb4, m3, e3, m4, e4, nv)
+        xL, pooled = ops.gf_final_fwd(z3, acc[L - 1], saved[L - 1], [pp[16], pp[17], pp[18], pp[19]], rm3, rv3, nb3,
+                                      rm4, rv4, nb4, m3, e3, m4, e4, nv, cfg.gptr)
+        ctx.set_materialize_grads(False)
         ctx.cfg = cfg
         ctx.st = st
         ctx.acc, ctx.saved = acc, saved
         ctx.radial = (rbf, drdf, Rl, Gl)
+        ctx.emb = (ab_n, ab_e, e)
         ctx.freq_grad = bool(freq.requires_grad)
-        ctx.save_for_backward(x0, e, xL, *flat)
-        return xL
+        ctx.save_for_backward(xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, xL, *flat)
+        return xL, pooled
 
     @staticmethod
-    def backward(ctx, dxL):
+    def backward(ctx, dxL, dpool):
         ops = _native.ops()
         cfg = ctx.cfg
         L, F = cfg.L, cfg.F
-        x0, e, xL, *flat = ctx.saved_tensors
+        xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, xL, *flat = ctx.saved_tensors
         prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
         rbf, drdf, Rl, Gl = ctx.radial
+        ab_n, ab_e, e = ctx.emb
         K = rbf.shape[1]
         acc, saved, st = ctx.acc, ctx.saved, ctx.st
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
-        dev = x0.device
-        g = ops.gf_pair_stats_bwd(dxL, xL, st[L - 1]["z3"], saved[L - 1], acc[L - 1], nv)
+        dev = xin.device
+        if dpool is not None and cfg.gptr is None:
+            dpool = None
+        g = ops.gf_pair_stats_bwd(dxL, xL, st[L - 1]["z3"], saved[L - 1], acc[L - 1], nv, dpool, cfg.gidx, cfg.gptr)
         empty = torch.empty(0, device=dev, dtype=torch.float32)
         dys, xs, dws, dbs = [], [], [], []
 
@@ -347,6 +373,12 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 16], grads[base + 17] = dw3, db3
             grads[base + 18], grads[base + 19] = dw4, db4
         dfreq_w = item(drbf, drdf, torch.empty(K, K, device=dev), False)[0] if ctx.freq_grad else None
+        # embeddings: d[ab] = dy Wl, then their three weight gradients per embedding
+        dab_n = ops.gf_embed_bwd(dx0, Wnl)
+        dab_e = ops.gf_embed_bwd(de, Wel)
+        emb_g = [item(dx0, ab_n, Wnl, False)[0], item(dab_n[:, :F], xin, Wne, False)[0],
+                 item(dab_n[:, F:], pe, Wpe, False)[0], item(de, ab_e, Wel, False)[0],
+                 item(dab_e[:, :F], eattr, Wee, False)[0], item(dab_e[:, F:], rpe, Wrp, False)[0]]
         # every weight gradient of the stack (incl. the radial basis and its frequencies): one
         # grouped launch pair
         ops.linear_wgrad_grouped(dys, xs, dws, dbs, [0] * len(dys))
@@ -368,4 +400,6 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 22], grads[base + 23] = gw["W2"]
         ctx.st = None
         ctx.radial = None
-        return (None, dx0, de, None, dfreq, *grads)
+        ctx.emb = None
+        return (None, None, dfreq, None, None, None, None, emb_g[1], emb_g[2], emb_g[0], emb_g[4], emb_g[5], emb_g[3],
+                *grads)

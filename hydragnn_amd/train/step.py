@@ -209,7 +209,9 @@ class TrainStep:
                 self.model = self.module
             elif world > 1:
                 _broadcast_state(self.module)
-            cap = bucket_cap_mb if world > 1 else 1e9
+            # one bucket on a single rank unless asked otherwise (the 1-rank RCCL check,
+            # tools/gradsync_check.py, uses several to exercise the in-graph bucket order)
+            cap = bucket_cap_mb if (world > 1 or bucket_cap_mb is not None) else 1e9
             self.sync = BucketedGradSync(params, bucket_cap_mb=cap)
         elif not isinstance(self.model, DistributedDataParallel):
             self.flat_grads = FlatGrads(params)

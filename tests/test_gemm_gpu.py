@@ -110,8 +110,10 @@ def test_wgrad_grouped_matches_torch():
     import hydragnn_amd._native as nat
 
     torch.manual_seed(11)
+    # (I <= 16 problems take the narrow path: one lane per output row, all I columns)
     shapes = [(2311, 64, 64, True), (23105, 64, 7, True), (37, 5, 130, False), (2311, 192, 64, True),
-              (4000, 33, 66, False), (1, 3, 3, True)]
+              (4000, 33, 66, False), (1, 3, 3, True), (24571, 130, 16, True), (9001, 6, 6, False),
+              (24576, 64, 1, False)]
     dys, xs, dws, dbs, acc, ref_w, ref_b = [], [], [], [], [], [], []
     for k, (M, O, I, hb) in enumerate(shapes):
         dy = torch.randn(M, O + 3, device=DEV)[:, 1:O + 1]  # strided (column-sliced) operand
