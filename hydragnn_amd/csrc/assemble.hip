@@ -42,13 +42,34 @@ struct AsmArgs {
   int Np, Ep, Gp, padded, pos_field;
 };
 
-__device__ __forceinline__ void copy_row(const AsmFields& F, int out_row, int in_row, bool valid) {
-  const int r = valid ? in_row : 0;
-  for (int f = 0; f < F.n; ++f) {
-    const int w = F.width[f];
-    const float* s = F.src[f] + (int64_t)r * w;
-    float* d = F.dst[f] + (int64_t)out_row * w;
-    for (int c = 0; c < w; ++c) d[c] = valid ? s[c] : 0.f;
+// Field copies element-parallel: consecutive threads take consecutive (row, column)
+// elements, 4 independent loads in flight per thread before the stores.  (The first
+// version copied one row per thread, field by field: a chain of dependent load -> store
+// pairs, ~20 us per step for the OC20 batch on MI355X.)
+__device__ __forceinline__ void copy_field(const float* __restrict__ s, float* __restrict__ d, int w,
+                                           const int* __restrict__ rows, int nrows, int nvalid_rows, int tid,
+                                           int stride, int padpos = -1) {
+  const int64_t total = (int64_t)nrows * w;
+  for (int64_t base = tid; base < total; base += 4LL * stride) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t idx = base + (int64_t)u * stride;
+      v[u] = 0.f;
+      if (idx < total) {
+        const int r = (int)(idx / w), c = (int)(idx % w);
+        const int row = rows ? rows[r] : r;
+        if (r < nvalid_rows && row >= 0)
+          v[u] = s[(int64_t)row * w + c];
+        else if (padpos >= 0 && c == 0)  // positions of padding atoms: distinct and finite
+          v[u] = 2.f * ((float)(r - padpos) + 1.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t idx = base + (int64_t)u * stride;
+      if (idx < total) d[idx] = v[u];
+    }
   }
 }
 
@@ -56,32 +77,26 @@ __global__ void __launch_bounds__(256) assemble_kernel(AsmArgs a) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int stride = gridDim.x * blockDim.x;
   const int nvalid = a.scal[0], gvalid = a.scal[1];
-  // nodes
+  const int big = 1 << 30;
+  for (int f = 0; f < a.node.n; ++f)
+    copy_field(a.node.src[f], a.node.dst[f], a.node.width[f], a.node_rows, a.Np, big, tid, stride,
+               f == a.pos_field ? nvalid : -1);
+  for (int f = 0; f < a.edge.n; ++f)
+    copy_field(a.edge.src[f], a.edge.dst[f], a.edge.width[f], a.edge_rows, a.Ep, big, tid, stride);
+  for (int f = 0; f < a.graph.n; ++f)
+    copy_field(a.graph.src[f], a.graph.dst[f], a.graph.width[f], a.sidx, a.Gp, a.padded ? gvalid : big, tid,
+               stride);
   for (int n = tid; n < a.Np; n += stride) {
-    const int row = a.node_rows[n];
-    const bool valid = !a.padded || row >= 0;
-    copy_row(a.node, n, row, valid);
-    if (!valid && a.pos_field >= 0) {
-      float* d = a.node.dst[a.pos_field] + (int64_t)n * a.node.width[a.pos_field];
-      d[0] = 2.f * ((float)(n - nvalid) + 1.f);
-    }
-    a.nmask[n] = valid;
+    a.nmask[n] = !a.padded || a.node_rows[n] >= 0;
     a.batch_l[n] = a.batch[n];
   }
-  // edges
   for (int e = tid; e < a.Ep; e += stride) {
-    const int row = a.edge_rows[e];
-    copy_row(a.edge, e, row, !a.padded || row >= 0);
     a.edge_index[e] = a.src[e];
     a.edge_index[(int64_t)a.Ep + e] = a.dst[e];
   }
-  // graphs
   for (int g = tid; g <= a.Gp; g += stride) {
     a.ptr_l[g] = a.gptr[g];
-    if (g == a.Gp) break;
-    const bool valid = !a.padded || g < gvalid;
-    copy_row(a.graph, g, a.sidx[g], valid);
-    a.gmask[g] = valid;
+    if (g < a.Gp) a.gmask[g] = !a.padded || g < gvalid;
   }
 }
 
@@ -136,7 +151,11 @@ std::vector<at::Tensor> store_assemble(const at::Tensor& plan, int64_t Np, int64
   a.Gp = (int)Gp;
   a.padded = padded ? 1 : 0;
   a.pos_field = (int)pos_field;
-  const int64_t work = std::max<int64_t>(std::max(Np, Ep), Gp + 1);
+  int64_t work = std::max<int64_t>(std::max(Np, Ep), Gp + 1);
+  int64_t we = 0, wn = 0;
+  for (int f = 0; f < a.edge.n; ++f) we += a.edge.width[f];
+  for (int f = 0; f < a.node.n; ++f) wn += a.node.width[f];
+  work = std::max<int64_t>(work, std::max(Ep * we, Np * wn) / 16);
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(work, 256)), 2048);
   assemble_kernel<<<blocks, 256, 0, stream()>>>(a);
   outs.push_back(edge_index);

@@ -618,50 +618,120 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
 }
 
 // dqkv [N, 24H] from dO [N, 8H] (and O, LSE2 of the forward)
-at::Tensor attn8_bwd(const at::Tensor& dO_, const at::Tensor& O, const at::Tensor& LSE2, const at::Tensor& Qp,
-                     const at::Tensor& Qq, const at::Tensor& Kp, const at::Tensor& Kq, const at::Tensor& Vp,
-                     const at::Tensor& seg_id, const at::Tensor& seg_ptr, double scale, int64_t splits) {
+// Backward in parts (the dQ and dK/dV passes are independent given delta; running them
+// on two streams measured slower in the GPS step, see ops/gps_encoder.py):
+//   prep: delta = rowsum(dO * O) + packed dO   ->  [delta, dOp, dOq]
+//   dq:   per-split dQ partials [S, N, F]       (S == 1: written straight into dqkv[:, :F])
+//   dkv:  per-split dK|dV partials [S, N, 2F]   (S == 1: straight into dqkv[:, F:])
+//   sum:  dqkv = [sum_s dQ | sum_s dKV]         (skipped when S == 1)
+std::vector<at::Tensor> attn8_bwd_prep(const at::Tensor& dO_, const at::Tensor& O, int64_t Nq, int64_t H) {
   at::Tensor dO = dO_.contiguous();
-  const int64_t H = Qp.size(0), Nq = Qp.size(1), N = dO.size(0);
-  HY_CHECK(dO.size(1) == 8 * H && O.is_contiguous() && O.sizes() == dO.sizes() && LSE2.numel() == H * Nq,
-           "attn8_bwd: shapes");
-  chk_seg(seg_id, seg_ptr, N);
+  const int64_t N = dO.size(0);
+  HY_CHECK(dO.dim() == 2 && dO.size(1) == 8 * H && O.is_contiguous() && O.sizes() == dO.sizes() && Nq >= N &&
+               Nq % 16 == 0,
+           "attn8_bwd_prep: shapes");
   auto opt = dO.options();
-  auto dqkv = at::empty({N, 24 * H}, opt);
-  if (N == 0) return dqkv;
   auto delta = at::empty({H, Nq}, opt), dOp = at::empty({H, Nq, 8}, opt), dOq = at::empty({H, Nq / 4, 8, 4}, opt);
-  attn8_delta_pack_kernel<<<ceil_div(Nq * H, 256), 256, 0, stream()>>>(
-      dO.data_ptr<float>(), O.data_ptr<float>(), (int)N, (int)Nq, (int)H, delta.data_ptr<float>(),
-      dOp.data_ptr<float>(), dOq.data_ptr<float>());
+  if (Nq * H > 0)
+    attn8_delta_pack_kernel<<<ceil_div(Nq * H, 256), 256, 0, stream()>>>(
+        dO.data_ptr<float>(), O.data_ptr<float>(), (int)N, (int)Nq, (int)H, delta.data_ptr<float>(),
+        dOp.data_ptr<float>(), dOq.data_ptr<float>());
+  return {delta, dOp, dOq};
+}
+
+static void chk_bwd(const at::Tensor& Qp, const at::Tensor& LSE2, const at::Tensor& delta, const at::Tensor& dOp,
+                    int64_t N) {
+  const int64_t H = Qp.size(0), Nq = Qp.size(1);
+  HY_CHECK(Qp.dim() == 3 && Qp.size(2) == 8 && Nq >= N && Nq % 16 == 0 && LSE2.numel() == H * Nq &&
+               delta.numel() == H * Nq && dOp.sizes() == Qp.sizes(),
+           "attn8_bwd: operand shapes");
+}
+
+// out: [S, N, F] partials (S > 1) or the dqkv buffer [N, 3F] (S == 1)
+at::Tensor attn8_bwd_dq(const at::Tensor& Qp, const at::Tensor& Kp, const at::Tensor& Kq, const at::Tensor& Vp,
+                        const at::Tensor& dOp, const at::Tensor& LSE2, const at::Tensor& delta,
+                        const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N, double scale, int64_t splits,
+                        const c10::optional<at::Tensor>& dqkv) {
+  chk_bwd(Qp, LSE2, delta, dOp, N);
+  chk_seg(seg_id, seg_ptr, N);
+  const int64_t H = Qp.size(0), Nq = Qp.size(1), F = 8 * H;
   const int S = pick_splits((int)N, (int)H, splits);
-  const float qs = (float)scale * kLog2e;
-  dim3 grid(ceil_div(N, 64 * kRT), H, S);
-  const int F = (int)(8 * H);
+  at::Tensor out;
   if (S == 1) {
-    attn8_bwd_dq_kernel<kRT><<<grid, 256, 0, stream()>>>(
-        Qp.data_ptr<float>(), Kp.data_ptr<float>(), Kq.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
-        LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
-        seg_ptr.data_ptr<int>(), 1, (float)scale, qs, dqkv.data_ptr<float>(), 3 * F, 0);
-    attn8_bwd_dkv_kernel<kRT><<<grid, 256, 0, stream()>>>(
-        Qp.data_ptr<float>(), Qq.data_ptr<float>(), Kp.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
-        dOq.data_ptr<float>(), LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H,
-        seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), 1, (float)scale, qs, dqkv.data_ptr<float>() + F, 3 * F, 0);
-    return dqkv;
+    HY_CHECK(dqkv.has_value() && dqkv->is_contiguous() && dqkv->size(0) == N && dqkv->size(1) == 3 * F,
+             "attn8_bwd_dq: S == 1 writes into dqkv [N, 3F]");
+    out = *dqkv;
+  } else {
+    out = at::empty({S, N, F}, Qp.options());
   }
-  auto pq = at::empty({S, N, F}, opt), pkv = at::empty({S, N, 2 * F}, opt);
+  if (N == 0) return out;
+  dim3 grid(ceil_div(N, 64 * kRT), H, S);
   attn8_bwd_dq_kernel<kRT><<<grid, 256, 0, stream()>>>(
       Qp.data_ptr<float>(), Kp.data_ptr<float>(), Kq.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
       LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H, seg_id.data_ptr<int>(),
-      seg_ptr.data_ptr<int>(), S, (float)scale, qs, pq.data_ptr<float>(), F, N * F);
+      seg_ptr.data_ptr<int>(), S, (float)scale, (float)scale * kLog2e, out.data_ptr<float>(),
+      S == 1 ? (int)(3 * F) : (int)F, S == 1 ? 0 : N * F);
+  return out;
+}
+
+at::Tensor attn8_bwd_dkv(const at::Tensor& Qp, const at::Tensor& Qq, const at::Tensor& Kp, const at::Tensor& Vp,
+                         const at::Tensor& dOp, const at::Tensor& dOq, const at::Tensor& LSE2, const at::Tensor& delta,
+                         const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N, double scale, int64_t splits,
+                         const c10::optional<at::Tensor>& dqkv) {
+  chk_bwd(Qp, LSE2, delta, dOp, N);
+  chk_seg(seg_id, seg_ptr, N);
+  const int64_t H = Qp.size(0), Nq = Qp.size(1), F = 8 * H;
+  HY_CHECK(Qq.numel() == Qp.numel() && dOq.numel() == dOp.numel(), "attn8_bwd_dkv: quad operand shapes");
+  const int S = pick_splits((int)N, (int)H, splits);
+  at::Tensor out;
+  if (S == 1) {
+    HY_CHECK(dqkv.has_value() && dqkv->is_contiguous() && dqkv->size(0) == N && dqkv->size(1) == 3 * F,
+             "attn8_bwd_dkv: S == 1 writes into dqkv [N, 3F]");
+    out = *dqkv;
+  } else {
+    out = at::empty({S, N, 2 * F}, Qp.options());
+  }
+  if (N == 0) return out;
+  dim3 grid(ceil_div(N, 64 * kRT), H, S);
   attn8_bwd_dkv_kernel<kRT><<<grid, 256, 0, stream()>>>(
       Qp.data_ptr<float>(), Qq.data_ptr<float>(), Kp.data_ptr<float>(), Vp.data_ptr<float>(), dOp.data_ptr<float>(),
       dOq.data_ptr<float>(), LSE2.data_ptr<float>(), delta.data_ptr<float>(), (int)N, (int)Nq, (int)H,
-      seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), S, (float)scale, qs, pkv.data_ptr<float>(), 2 * F,
-      N * 2 * F);
-  attn8_bwd_sum_kernel<<<ceil_div(N * 3 * (F / 4), 256), 256, 0, stream()>>>(
-      reinterpret_cast<const float4*>(pq.data_ptr<float>()), S, reinterpret_cast<const float4*>(pkv.data_ptr<float>()),
-      S, reinterpret_cast<float4*>(dqkv.data_ptr<float>()), (int)N, F);
+      seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), S, (float)scale, (float)scale * kLog2e,
+      out.data_ptr<float>() + (S == 1 ? F : 0), S == 1 ? (int)(3 * F) : (int)(2 * F), S == 1 ? 0 : N * 2 * F);
+  return out;
+}
+
+at::Tensor attn8_bwd_sum(const at::Tensor& pq, const at::Tensor& pkv) {
+  HY_CHECK(pq.dim() == 3 && pkv.dim() == 3 && pq.is_contiguous() && pkv.is_contiguous() && pq.size(1) == pkv.size(1) &&
+               pkv.size(2) == 2 * pq.size(2) && pq.size(2) % 4 == 0,
+           "attn8_bwd_sum: partials [Sq, N, F] and [Skv, N, 2F]");
+  const int64_t N = pq.size(1), F = pq.size(2);
+  auto dqkv = at::empty({N, 3 * F}, pq.options());
+  if (N > 0)
+    attn8_bwd_sum_kernel<<<ceil_div(N * 3 * (F / 4), 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(pq.data_ptr<float>()), (int)pq.size(0),
+        reinterpret_cast<const float4*>(pkv.data_ptr<float>()), (int)pkv.size(0),
+        reinterpret_cast<float4*>(dqkv.data_ptr<float>()), (int)N, (int)F);
   return dqkv;
+}
+
+// single-stream composition of the parts
+at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor& LSE2, const at::Tensor& Qp,
+                     const at::Tensor& Qq, const at::Tensor& Kp, const at::Tensor& Kq, const at::Tensor& Vp,
+                     const at::Tensor& seg_id, const at::Tensor& seg_ptr, double scale, int64_t splits) {
+  const int64_t H = Qp.size(0), Nq = Qp.size(1), N = dO.size(0);
+  auto pre = attn8_bwd_prep(dO, O, Nq, H);
+  const int S = pick_splits((int)N, (int)H, splits);
+  if (S == 1) {
+    auto dqkv = at::empty({N, 24 * H}, dO.options());
+    attn8_bwd_dq(Qp, Kp, Kq, Vp, pre[1], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, dqkv);
+    attn8_bwd_dkv(Qp, Qq, Kp, Vp, pre[1], pre[2], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, dqkv);
+    return dqkv;
+  }
+  auto pq = attn8_bwd_dq(Qp, Kp, Kq, Vp, pre[1], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, c10::nullopt);
+  auto pkv = attn8_bwd_dkv(Qp, Qq, Kp, Vp, pre[1], pre[2], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits,
+                           c10::nullopt);
+  return attn8_bwd_sum(pq, pkv);
 }
 
 }  // namespace a8

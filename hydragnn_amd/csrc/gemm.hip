@@ -405,11 +405,6 @@ static void set_seg(MMSeg& g, const float* A, const float* Am, int64_t sam, int6
 }
 
 static int pick_split(int64_t tiles, int kchunks) {
-  static const int forced = [] {
-    const char* e = std::getenv("HYDRA_MM_SPLIT");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced > 0) return std::min(forced, std::max(1, kchunks));
   // The in-launch reduction costs agent-scope release fences, which are cheap only while few
   // workgroups run (measured, tools/bench_mm.py: +17 us on a 292-workgroup grid): split only
   // deep-K problems with a narrow grid (weight gradients), one group of chunks per wave.

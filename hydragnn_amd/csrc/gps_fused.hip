@@ -1103,9 +1103,11 @@ __global__ void __launch_bounds__(256) edge_bwd_kernel(EdgeBwd a) {
 //   node: x0 = node_lin(cat[node_emb(x), pos_emb(pe)]),  rows >= nv -> 0
 //   edge: e  = edge_lin(cat[edge_emb(edge_attr), rel_pos_emb(rel_pe)])
 // all bias-free: y = [A Wa^T | B Wb^T] Wl^T with narrow A, B (1-16 columns).  One launch
-// per embedding: the [M, 2F] concat tile is built in LDS (kept for the weight gradient
-// dWl = dy^T ab) and multiplied on the spot.  Backward: dab = dy Wl (one launch); the three
-// weight gradients are rows of the encoder's grouped reduction.
+// per embedding: the [M, 2F] concat tile is built in LDS and multiplied on the spot.
+// Backward needs no per-row pass at all: with the narrow products Ta = dy^T A [F, ka] and
+// Tb = dy^T B [F, kb] (two rows of the encoder's grouped weight-gradient launch),
+//   dWl = [Ta Wa^T | Tb Wb^T],  dWa = Wl[:, :F]^T Ta,  dWb = Wl[:, F:]^T Tb
+// (gf_finish below), so neither the [M, 2F] concat nor d[concat] is ever written.
 struct EmbFwd {
   const float* A;   // [M, ka]
   const float* B;   // [M, kb]
@@ -1113,7 +1115,6 @@ struct EmbFwd {
   const float* Wb;  // [F, kb]
   const float* Wl;  // [F, 2F]
   float* y;         // [M, F]
-  float* ab;        // [M, 2F]
   int ka, kb, M;
   const int* nvp;   // rows >= *nvp -> 0 (node embedding of a padded batch) or null
 };
@@ -1142,8 +1143,6 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(EmbFwd a) {
       for (int k = 0; k < a.kb; ++k) acc = fmaf(in[r][a.ka + k], a.Wb[(c - F) * a.kb + k], acc);
     }
     abs_[r * LD + c] = acc;
-    const int row = row0 + r;
-    if (row < a.M) a.ab[(int64_t)row * 2 * F + c] = acc;
   }
   __syncthreads();
   const int nv = a.nvp ? min(*a.nvp, a.M) : a.M;
@@ -1159,34 +1158,116 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(EmbFwd a) {
   }
 }
 
-struct EmbBwd {
-  const float* dy;  // [M, F]
-  const float* Wl;  // [F, 2F]
-  float* dab;       // [M, 2F]
-  int M;
+// ------------------------------------------------------------------------------------
+// Weight-gradient epilogue of the encoder (one launch after the grouped wgrad reduction):
+//   * per layer, the backward of pna_wprep_fwd (csrc/pna.hip): dW [F, 3F], db, dencW, dencb
+//     from dWab, dWr, dWd, dbc;
+//   * per embedding, dWl / dWa / dWb from the narrow products Ta, Tb (see EmbFwd);
+//   * dfreq = diag(drbf^T drbf/dfreq).
+// One thread per output element, dot products of length <= 3F with 4 partial sums.
+constexpr int kFinMaxL = 8;
+struct FinWprep {
+  const float *dWab, *dWr, *dWd, *dbc, *W, *encW, *encb;
+  float *dW, *db, *dencW, *dencb;
+};
+struct FinEmb {
+  const float *Ta, *Tb, *Wa, *Wb, *Wl;
+  float *dWa, *dWb, *dWl;
+  int ka, kb;
+};
+struct Finish {
+  FinWprep wp[kFinMaxL];
+  FinEmb em[2];
+  const float* dfw;  // [K, K] or null
+  float* dfreq;      // [K]
+  int L, ne, F, d, K;
+  int64_t per_l, per_e[2], total;
 };
 
-template <int F>
-__global__ void __launch_bounds__(256) emb_bwd_kernel(EmbBwd a) {
-  constexpr int LD = F + 4;
-  __shared__ __attribute__((aligned(16))) float gs[BM * LD];
-  const int row0 = blockIdx.x * BM;
-  for (int idx = threadIdx.x; idx < BM * F / 4; idx += 256) {
-    const int r = idx / (F / 4), c = (idx % (F / 4)) * 4, row = row0 + r;
-    *reinterpret_cast<float4*>(gs + r * LD + c) =
-        row < a.M ? *reinterpret_cast<const float4*>(a.dy + (int64_t)row * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  for (int t = w; t < 2 * F / 16; t += 4) {
-    const int n0 = 16 * t, col = n0 + i;
-    f4v acc = tile_mma<false>(gs, LD, a.Wl, 2 * F, 0, F, n0);
+__device__ __forceinline__ float fin_dot(const float* __restrict__ a, int sa, const float* __restrict__ b, int sb,
+                                         int n) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    float x[8], y[8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = row0 + 4 * g + r;
-      if (row < a.M) a.dab[(int64_t)row * 2 * F + col] = acc[r];
+    for (int u = 0; u < 8; ++u) {
+      x[u] = a[(int64_t)(k + u) * sa];
+      y[u] = b[(int64_t)(k + u) * sb];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 4) {
+      a0 = fmaf(x[u], y[u], a0);
+      a1 = fmaf(x[u + 1], y[u + 1], a1);
+      a2 = fmaf(x[u + 2], y[u + 2], a2);
+      a3 = fmaf(x[u + 3], y[u + 3], a3);
     }
   }
+  for (; k < n; ++k) a0 = fmaf(a[(int64_t)k * sa], b[(int64_t)k * sb], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+
+__global__ void __launch_bounds__(256) finish_kernel(Finish a) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.total) return;
+  const int F = a.F, d = a.d, ld = 3 * F, le = d + F;
+  if (t < a.L * a.per_l) {
+    const FinWprep& w = a.wp[t / a.per_l];
+    int64_t q = t % a.per_l;
+    if (q < 2 * F * F) {  // dW[:, :2F] <- dWab (row blocks [W_i; W_j])
+      const int o = (int)(q / (2 * F)), c = (int)(q % (2 * F));
+      w.dW[o * ld + c] = w.dWab[((c / F) * F + o) * F + (c % F)];
+      return;
+    }
+    q -= 2 * F * F;
+    if (q < F) {
+      w.db[q] = w.dbc[q];
+      return;
+    }
+    q -= F;
+    if (q < F * F) {  // dW_e[o, j] = dWr[o,:] . encW[j, d:] + dWd[o,:] . encW[j, :d] + dbc[o] encb[j]
+      const int o = (int)(q / F), j = (int)(q % F);
+      float v = fin_dot(w.dWr + o * F, 1, w.encW + j * le + d, 1, F) + w.dbc[o] * w.encb[j];
+      if (d > 0) v += fin_dot(w.dWd + o * d, 1, w.encW + j * le, 1, d);
+      w.dW[o * ld + 2 * F + j] = v;
+      return;
+    }
+    q -= F * F;
+    if (q < (int64_t)F * le) {  // dencW[j, c] = sum_o W_e[o, j] [dWd | dWr][o, c]
+      const int j = (int)(q / le), c = (int)(q % le);
+      w.dencW[q] = c < d ? fin_dot(w.W + 2 * F + j, ld, w.dWd + c, d, F)
+                         : fin_dot(w.W + 2 * F + j, ld, w.dWr + (c - d), F, F);
+      return;
+    }
+    q -= (int64_t)F * le;
+    w.dencb[q] = fin_dot(w.W + 2 * F + q, ld, w.dbc, 1, F);
+    return;
+  }
+  t -= a.L * a.per_l;
+  for (int m = 0; m < a.ne; ++m) {
+    if (t >= a.per_e[m]) {
+      t -= a.per_e[m];
+      continue;
+    }
+    const FinEmb& e = a.em[m];
+    if (t < 2 * F * F) {  // dWl[o, c]
+      const int o = (int)(t / (2 * F)), c = (int)(t % (2 * F));
+      e.dWl[t] = c < F ? fin_dot(e.Ta + o * e.ka, 1, e.Wa + c * e.ka, 1, e.ka)
+                       : fin_dot(e.Tb + o * e.kb, 1, e.Wb + (c - F) * e.kb, 1, e.kb);
+      return;
+    }
+    t -= 2 * F * F;
+    if (t < F * e.ka) {  // dWa[c, k] = sum_o Wl[o, c] Ta[o, k]
+      const int c = (int)(t / e.ka), k = (int)(t % e.ka);
+      e.dWa[t] = fin_dot(e.Wl + c, 2 * F, e.Ta + k, e.ka, F);
+      return;
+    }
+    t -= F * e.ka;
+    const int c = (int)(t / e.kb), k = (int)(t % e.kb);  // dWb[c, k] = sum_o Wl[o, F + c] Tb[o, k]
+    e.dWb[t] = fin_dot(e.Wl + F + c, 2 * F, e.Tb + k, e.kb, F);
+    return;
+  }
+  if (t < a.K) a.dfreq[t] = a.dfw[t * a.K + t];
 }
 
 // ====================================================================================
@@ -1481,8 +1562,8 @@ std::vector<at::Tensor> gf_edge_bwd(const at::Tensor& dC_, const at::Tensor& Wr,
   return {dr, de, drbf};
 }
 
-std::vector<at::Tensor> gf_embed_fwd(const at::Tensor& A_, const at::Tensor& B_, const at::Tensor& Wa,
-                                     const at::Tensor& Wb, const at::Tensor& Wl, const c10::optional<at::Tensor>& nv) {
+at::Tensor gf_embed_fwd(const at::Tensor& A_, const at::Tensor& B_, const at::Tensor& Wa, const at::Tensor& Wb,
+                        const at::Tensor& Wl, const c10::optional<at::Tensor>& nv) {
   at::Tensor A = A_.contiguous(), B = B_.contiguous();
   const int64_t M = A.size(0), F = Wl.size(0), ka = A.size(1), kb = B.size(1);
   HY_CHECK(B.size(0) == M && ka >= 1 && kb >= 1 && ka <= 16 && kb <= 16 && A.scalar_type() == at::kFloat &&
@@ -1491,23 +1572,71 @@ std::vector<at::Tensor> gf_embed_fwd(const at::Tensor& A_, const at::Tensor& B_,
   chk(Wa, F, ka, "Wa");
   chk(Wb, F, kb, "Wb");
   chk(Wl, F, 2 * F, "Wl");
-  auto y = at::empty({M, F}, A.options()), ab = at::empty({M, 2 * F}, A.options());
-  if (M == 0) return {y, ab};
+  auto y = at::empty({M, F}, A.options());
+  if (M == 0) return y;
   EmbFwd a{A.data_ptr<float>(), B.data_ptr<float>(), Wa.data_ptr<float>(), Wb.data_ptr<float>(), Wl.data_ptr<float>(),
-           y.data_ptr<float>(), ab.data_ptr<float>(), (int)ka, (int)kb, (int)M, nvptr(nv)};
+           y.data_ptr<float>(), (int)ka, (int)kb, (int)M, nvptr(nv)};
   HY_GF_DISPATCH(F, emb_fwd_kernel, ceil_div(M, BM), 256, a);
-  return {y, ab};
+  return y;
 }
 
-at::Tensor gf_embed_bwd(const at::Tensor& dy_, const at::Tensor& Wl) {
-  at::Tensor dy = dy_.contiguous();
-  const int64_t M = dy.size(0), F = dy.size(1);
-  chk(Wl, F, 2 * F, "Wl");
-  auto dab = at::empty({M, 2 * F}, dy.options());
-  if (M == 0) return dab;
-  EmbBwd a{dy.data_ptr<float>(), Wl.data_ptr<float>(), dab.data_ptr<float>(), (int)M};
-  HY_GF_DISPATCH(F, emb_bwd_kernel, ceil_div(M, BM), 256, a);
-  return dab;
+// wp: 7 tensors per layer (dWab, dWr, dWd, dbc, W_pre, encW, encb); em: 5 per embedding
+// (Ta, Tb, Wa, Wb, Wl).  Returns per layer [dW_pre, db_pre, dencW, dencb], then per embedding
+// [dWa, dWb, dWl], then dfreq (when dfw is given).
+std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::vector<at::Tensor>& em,
+                                  const c10::optional<at::Tensor>& dfw) {
+  HY_CHECK(wp.size() % 7 == 0 && wp.size() / 7 <= (size_t)kFinMaxL && em.size() % 5 == 0 && em.size() <= 10,
+           "gf_finish: 7 tensors per layer (<= 8 layers), 5 per embedding (<= 2)");
+  Finish a{};
+  a.L = (int)(wp.size() / 7);
+  a.ne = (int)(em.size() / 5);
+  const at::Tensor& ref = a.L ? wp[4] : em[4];
+  const int64_t F = a.L ? wp[4].size(0) : em[4].size(0);
+  a.F = (int)F;
+  a.d = a.L ? (int)(wp[5].size(1) - F) : 0;
+  std::vector<at::Tensor> out;
+  auto opt = ref.options();
+  for (int l = 0; l < a.L; ++l) {
+    const at::Tensor* t = &wp[7 * l];
+    for (int u = 0; u < 7; ++u) HY_CHECK(t[u].is_contiguous() && t[u].scalar_type() == at::kFloat, "gf_finish: wp");
+    HY_CHECK(t[0].numel() == 2 * F * F && t[1].numel() == F * F && t[2].numel() == F * a.d && t[3].numel() == F &&
+                 t[4].size(0) == F && t[4].size(1) == 3 * F && t[5].size(0) == F && t[5].size(1) == F + a.d &&
+                 t[6].numel() == F,
+             "gf_finish: weight-prep shapes");
+    auto dW = at::empty_like(t[4]), db = at::empty({F}, opt), dencW = at::empty_like(t[5]), dencb = at::empty({F}, opt);
+    a.wp[l] = FinWprep{t[0].data_ptr<float>(), t[1].data_ptr<float>(), t[2].data_ptr<float>(), t[3].data_ptr<float>(),
+                       t[4].data_ptr<float>(), t[5].data_ptr<float>(), t[6].data_ptr<float>(), dW.data_ptr<float>(),
+                       db.data_ptr<float>(), dencW.data_ptr<float>(), dencb.data_ptr<float>()};
+    out.insert(out.end(), {dW, db, dencW, dencb});
+  }
+  a.per_l = 3 * F * F + 2 * F + F * (F + a.d);
+  a.total = a.L * a.per_l;
+  for (int m = 0; m < a.ne; ++m) {
+    const at::Tensor* t = &em[5 * m];
+    for (int u = 0; u < 5; ++u) HY_CHECK(t[u].is_contiguous() && t[u].scalar_type() == at::kFloat, "gf_finish: em");
+    const int64_t ka = t[2].size(1), kb = t[3].size(1);
+    HY_CHECK(t[0].numel() == F * ka && t[1].numel() == F * kb && t[2].size(0) == F && t[3].size(0) == F &&
+                 t[4].size(0) == F && t[4].size(1) == 2 * F,
+             "gf_finish: embedding shapes");
+    auto dWa = at::empty_like(t[2]), dWb = at::empty_like(t[3]), dWl = at::empty_like(t[4]);
+    a.em[m] = FinEmb{t[0].data_ptr<float>(), t[1].data_ptr<float>(), t[2].data_ptr<float>(), t[3].data_ptr<float>(),
+                     t[4].data_ptr<float>(), dWa.data_ptr<float>(), dWb.data_ptr<float>(), dWl.data_ptr<float>(),
+                     (int)ka, (int)kb};
+    a.per_e[m] = 2 * F * F + F * ka + F * kb;
+    a.total += a.per_e[m];
+    out.insert(out.end(), {dWa, dWb, dWl});
+  }
+  if (dfw.has_value() && dfw->defined()) {
+    HY_CHECK(dfw->dim() == 2 && dfw->size(0) == dfw->size(1) && dfw->is_contiguous(), "gf_finish: dfw [K, K]");
+    a.K = (int)dfw->size(0);
+    auto dfreq = at::empty({a.K}, opt);
+    a.dfw = dfw->data_ptr<float>();
+    a.dfreq = dfreq.data_ptr<float>();
+    a.total += a.K;
+    out.push_back(dfreq);
+  }
+  if (a.total > 0) finish_kernel<<<ceil_div(a.total, 256), 256, 0, stream()>>>(a);
+  return out;
 }
 
 // ---- backward ops -------------------------------------------------------------------
@@ -1669,8 +1798,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "gf_final_fwd(Tensor z3, Tensor acc, Tensor(a!) saved, Tensor[] bn, Tensor(b!)? rm3, Tensor(c!)? rv3, "
       "Tensor(d!)? nbt3, Tensor(e!)? rm4, Tensor(f!)? rv4, Tensor(g!)? nbt4, float mom3, float eps3, float mom4, "
       "float eps4, Tensor? nv, Tensor? gptr) -> Tensor[]");
-  m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor[]");
-  m.def("gf_embed_bwd(Tensor dy, Tensor Wl) -> Tensor");
+  m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor");
+  m.def("gf_finish(Tensor[] wp, Tensor[] em, Tensor? dfw) -> Tensor[]");
   m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
   m.def(
       "gf_edge_bwd(Tensor dC, Tensor Wr, Tensor Wd, Tensor? rmask, Tensor(a!)? de_acc, Tensor? dG, Tensor? Wemb, "
@@ -1700,7 +1829,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gf_mlp_fwd", hy::gf::gf_mlp_fwd);
   m.impl("gf_final_fwd", hy::gf::gf_final_fwd);
   m.impl("gf_embed_fwd", hy::gf::gf_embed_fwd);
-  m.impl("gf_embed_bwd", hy::gf::gf_embed_bwd);
+  m.impl("gf_finish", hy::gf::gf_finish);
   m.impl("gf_edge_fwd", hy::gf::gf_edge_fwd);
   m.impl("gf_edge_bwd", hy::gf::gf_edge_bwd);
   m.impl("gf_pair_stats_bwd", hy::gf::gf_pair_stats_bwd);

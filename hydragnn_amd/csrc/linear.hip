@@ -512,7 +512,6 @@ struct ElArgs {
   int ldx[3];
   const float* w[3];
   int k[3];
-  int wt;  // 1: w[0] is stored [K, F] (y = x @ W, the dgrad of a linear), single input
   int nin;
   const float* b;
   float* y;
@@ -537,7 +536,7 @@ __global__ void __launch_bounds__(256) edge_linear_fwd_kernel(ElArgs a) {
     const int kj = a.k[j];
     const float* xr = a.x[j] + (int64_t)min(r0 + sr, a.rows - 1) * a.ldx[j];
     const float* wr = a.w[j] + (int64_t)min(f0 + sr, a.F - 1) * kj;
-    const bool vec = !a.wt && ((kj | a.ldx[j]) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.x[j]) & 15) == 0 &&
+    const bool vec = ((kj | a.ldx[j]) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.x[j]) & 15) == 0 &&
                      (reinterpret_cast<uintptr_t>(a.w[j]) & 15) == 0;
     if (vec) {
       const int n4 = kj >> 2;
@@ -569,7 +568,7 @@ __global__ void __launch_bounds__(256) edge_linear_fwd_kernel(ElArgs a) {
         for (int u = 0; u < 8; ++u) {
           const int c = min(c0 + 4 * u, kj - 1);
           xv[u] = xr[c];
-          wv[u] = a.wt ? a.w[j][(int64_t)c * a.F + min(f0 + sr, a.F - 1)] : wr[c];
+          wv[u] = wr[c];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -644,31 +643,6 @@ static void edge_linear_launch(ElArgs& a, int K, int64_t rows, int64_t F) {
     edge_linear_fwd_kernel<kElK><<<grid, 256, 0, stream()>>>(a);
 }
 
-// dX = dY @ W for a linear y = x W^T with W [F, K], dY [rows, F] (row stride any) -> [rows, K]
-at::Tensor edge_linear_dgrad(const at::Tensor& dy, const at::Tensor& W_) {
-  HY_CHECK_CUDA(dy);
-  HY_CHECK_F32(dy);
-  auto W = W_.contiguous();
-  HY_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && W.dim() == 2 && W.size(0) == dy.size(1),
-           "edge_linear_dgrad: shapes");
-  const int64_t rows = dy.size(0), Fin = W.size(0), Kout = W.size(1);
-  HY_CHECK(Fin >= 1 && Fin <= kElK, "edge_linear_dgrad: dY width must be in [1, 188]");
-  auto y = at::empty({rows, Kout}, dy.options());
-  if (rows == 0 || Kout == 0) return y;
-  ElArgs a{};
-  a.nin = 1;
-  a.x[0] = dy.data_ptr<float>();
-  a.ldx[0] = (int)dy.stride(0);
-  a.w[0] = W.data_ptr<float>();
-  a.k[0] = (int)Fin;
-  a.wt = 1;
-  a.y = y.data_ptr<float>();
-  a.rows = (int)rows;
-  a.F = (int)Kout;
-  edge_linear_launch(a, (int)Fin, rows, Kout);
-  return y;
-}
-
 at::Tensor edge_linear_fwd(const std::vector<at::Tensor>& xs, const std::vector<at::Tensor>& ws,
                            const c10::optional<at::Tensor>& b) {
   HY_CHECK(!xs.empty() && xs.size() <= 3 && xs.size() == ws.size(), "edge_linear_fwd: 1-3 (x, W) pairs");
@@ -712,13 +686,11 @@ at::Tensor edge_linear_fwd(const std::vector<at::Tensor>& xs, const std::vector<
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("linear_wgrad(Tensor dY, Tensor X, bool with_bias) -> (Tensor, Tensor)");
   m.def("edge_linear_fwd(Tensor[] xs, Tensor[] ws, Tensor? b) -> Tensor");
-  m.def("edge_linear_dgrad(Tensor dy, Tensor W) -> Tensor");
   m.def("linear_wgrad_grouped(Tensor[] dYs, Tensor[] Xs, Tensor(a!)[] dWs, Tensor(b!)[] dbs, int[] accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("linear_wgrad", hy::linear_wgrad);
   m.impl("edge_linear_fwd", hy::edge_linear_fwd);
-  m.impl("edge_linear_dgrad", hy::edge_linear_dgrad);
   m.impl("linear_wgrad_grouped", hy::linear_wgrad_grouped);
 }

@@ -62,6 +62,12 @@ __device__ __forceinline__ void stage_seg(const float* __restrict__ src, int cnt
   }
 }
 
+// csrc/loss.hip loss_term (0 mse, 1 mae, 2 rmse, 3 smooth_l1)
+__device__ __forceinline__ float loss_term_hl(int kind, float d) {
+  const float a = fabsf(d);
+  return kind == 1 ? a : (kind == 3 ? (a < 1.f ? 0.5f * d * d : a - 0.5f) : d * d);
+}
+
 __device__ __forceinline__ int max_width(const MlpArgs& a) {
   int m = 1;
   for (int l = 0; l <= a.n; ++l) m = max(m, a.dims[l]);
@@ -326,6 +332,303 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> mlp_bwd
   return {dx, dWs, dbs};
 }
 
+// ------------------------------------------------------------------------------------
+// Head + loss in one workgroup (the training step's graph-level decoder, Base.py:_multihead
+// followed by Base.loss_hpweighted's masked loss, csrc/loss.hip):
+//   forward : pred = MLP(x), loss = masked mean of loss_term(pred - target)
+//   backward: dpred = g dloss/dpred, then the chain backward with COMPLETE weight
+//             gradients (all rows are in the workgroup: no partials, no sum pass).
+// For the ~32 pooled rows of a training batch the old path was 7 launches (MLP fwd,
+// loss fwd, grad seed fill, loss bwd, MLP bwd, partial sum, copy), ~70 us of serial
+// dependent launches between the encoder's forward and backward; this is 2.
+// One 1024-thread workgroup; everything lives in LDS: W per layer natural [o][i],
+// X [G][D0], every layer's activation A [G][S] and two dY buffers [G][md].
+// The backward launch recomputes the (tiny) forward chain instead of reading it back.
+constexpr int kHlThreads = 1024;
+constexpr size_t kHlMaxLds = 150 * 1024;
+
+// LDS layout shared by both kernels.  Every row stride is odd (W rows I+1, activation rows
+// S|1, X rows D0+1 or D0+2) so lanes walking a column never collide on a bank, and lanes
+// walking a row read consecutive words.
+struct HlLds {
+  int nw, xs, as, dy, md, ldx, lda;
+  int woff[kMlpMaxLayers + 1];
+  __host__ __device__ HlLds(const MlpArgs& a, int G, int mw) {
+    md = mw + 1;
+    int o = 0;
+    for (int l = 0; l < a.n; ++l) {
+      woff[l] = o;
+      o += a.dims[l + 1] * (a.dims[l] + 1);
+    }
+    woff[a.n] = o;
+    nw = o;
+    ldx = a.dims[0] + 1 + (a.dims[0] % 2 ? 1 : 0);
+    lda = a.aoff[a.n] | 1;
+    xs = G * ldx;
+    as = G * lda;
+    dy = G * md;
+  }
+  __host__ __device__ size_t bytes() const { return sizeof(float) * ((size_t)nw + xs + as + 2 * (size_t)dy); }
+};
+
+// all weights (row stride I+1) and the input rows into LDS, 8 loads in flight per thread
+__device__ void hl_stage(const MlpArgs& a, const HlLds& L, const float* __restrict__ x, int G, float* WS, float* XS) {
+  for (int l = 0; l <= a.n; ++l) {
+    const bool isx = l == a.n;
+    const int I = isx ? a.dims[0] : a.dims[l], cnt = isx ? G * a.dims[0] : a.dims[l + 1] * a.dims[l];
+    const int ld = isx ? L.ldx : I + 1;
+    const float* __restrict__ src = isx ? x : a.W[l];
+    float* dst = isx ? XS : WS + L.woff[l];
+    for (int base = threadIdx.x; base < cnt; base += 8 * kHlThreads) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = src[min(base + k * kHlThreads, cnt - 1)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = base + k * kHlThreads;
+        if (idx < cnt) dst[(idx / I) * ld + idx % I] = v[k];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// forward chain into AS; lanes over outputs o (W rows conflict-free, input reads broadcast)
+__device__ void hl_chain(const MlpArgs& a, const HlLds& L, int G, const float* WS, const float* XS, float* AS) {
+  for (int l = 0; l < a.n; ++l) {
+    const int I = a.dims[l], O = a.dims[l + 1];
+    const float* in = l == 0 ? XS : AS + a.aoff[l - 1];
+    const int ldi = l == 0 ? L.ldx : L.lda;
+    const float* Wl = WS + L.woff[l];
+    const float* __restrict__ bb = a.b[l];
+    for (int idx = threadIdx.x; idx < G * O; idx += kHlThreads) {
+      const int o = idx % O, r = idx / O;
+      const float* xr = in + r * ldi;
+      const float* wr = Wl + o * (I + 1);
+      float a0 = bb[o], a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int i = 0;
+      for (; i + 4 <= I; i += 4) {
+        a0 = fmaf(xr[i], wr[i], a0);
+        a1 = fmaf(xr[i + 1], wr[i + 1], a1);
+        a2 = fmaf(xr[i + 2], wr[i + 2], a2);
+        a3 = fmaf(xr[i + 3], wr[i + 3], a3);
+      }
+      for (; i < I; ++i) a0 = fmaf(xr[i], wr[i], a0);
+      float v = (a0 + a1) + (a2 + a3);
+      if (a.relu[l]) v = fmaxf(v, 0.f);
+      AS[r * L.lda + a.aoff[l] + o] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// out: [loss, count]; pred [G, Do]
+__global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* __restrict__ x, int G, MlpArgs a,
+                                                                   const float* __restrict__ target,
+                                                                   const bool* __restrict__ mask, int kind,
+                                                                   float* __restrict__ out, float* __restrict__ pred) {
+  extern __shared__ float sm[];
+  const HlLds L(a, G, max_width(a));
+  float* WS = sm;
+  float* XS = WS + L.nw;
+  float* AS = XS + L.xs;
+  hl_stage(a, L, x, G, WS, XS);
+  hl_chain(a, L, G, WS, XS, AS);
+  const int S = L.lda, Do = a.dims[a.n], po = a.aoff[a.n - 1];
+  __shared__ double red[kHlThreads / 64][2];
+  double s = 0.0, c = 0.0;
+  for (int idx = threadIdx.x; idx < G * Do; idx += kHlThreads) {
+    const int r = idx / Do, o = idx % Do;
+    const float p = AS[r * S + po + o];
+    pred[idx] = p;
+    if (mask == nullptr || mask[r]) {
+      s += (double)loss_term_hl(kind, p - target[idx]);
+      c += 1.0;
+    }
+  }
+  // fixed-order reduction: wave shuffle tree, then wave 0 over the per-wave sums
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    c += __shfl_xor(c, off);
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[w][0] = s;
+    red[w][1] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ts = 0.0, tc = 0.0;
+    for (int k = 0; k < kHlThreads / 64; ++k) {
+      ts += red[k][0];
+      tc += red[k][1];
+    }
+    double l = ts / (tc > 0.0 ? tc : 1.0);
+    if (kind == 2) l = sqrt(l);
+    out[0] = (float)l;
+    out[1] = (float)tc;
+  }
+}
+
+// grads: [dW_0 | db_0 | dW_1 | db_1 | ...] (goff), dx [G, D0]
+__global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* __restrict__ gout,
+                                                                   const float* __restrict__ x, int G, MlpArgs a,
+                                                                   const float* __restrict__ target,
+                                                                   const bool* __restrict__ mask, int kind,
+                                                                   const float* __restrict__ fwd,
+                                                                   float* __restrict__ grads, float* __restrict__ dx) {
+  extern __shared__ float sm[];
+  const HlLds L(a, G, max_width(a));
+  float* WS = sm;
+  float* XS = WS + L.nw;
+  float* AS = XS + L.xs;
+  float* DY = AS + L.as;
+  float* DY2 = DY + L.dy;
+  const int md = L.md;
+  hl_stage(a, L, x, G, WS, XS);
+  hl_chain(a, L, G, WS, XS, AS);
+  const int n = a.n, S = L.lda, Do = a.dims[n], po = a.aoff[n - 1];
+  {
+    const float g = gout[0], den = fwd[1] > 0.f ? fwd[1] : 1.f, lv = fwd[0];
+    const bool rl = a.relu[n - 1];
+    for (int idx = threadIdx.x; idx < G * Do; idx += kHlThreads) {
+      const int r = idx / Do, o = idx % Do;
+      const float p = AS[r * S + po + o];
+      float v = 0.f;
+      if (mask == nullptr || mask[r]) {
+        const float d = p - target[idx];
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        switch (kind) {
+          case 1: v = sgn / den; break;
+          case 3: v = (fabsf(d) < 1.f ? d : sgn) / den; break;
+          case 2: v = lv > 0.f ? d / (den * lv) : 0.f; break;
+          default: v = 2.f * d / den; break;
+        }
+        v *= g;
+      }
+      DY[r * md + o] = (rl && p <= 0.f) ? 0.f : v;
+    }
+  }
+  __syncthreads();
+  for (int l = n - 1; l >= 0; --l) {
+    const int I = a.dims[l], O = a.dims[l + 1];
+    const float* ain = l == 0 ? XS : AS + a.aoff[l - 1];
+    const int lda = l == 0 ? L.ldx : S;
+    const float* Wl = WS + L.woff[l];
+    const int ldw = I + 1;
+    float* gl = grads + a.goff[l];
+    // dW[o, i] = sum_r dy[r, o] ain[r, i] (lanes over i: ain contiguous, dy broadcast); db[o]
+    for (int idx = threadIdx.x; idx < O * I + O; idx += kHlThreads) {
+      float a0 = 0.f, a1 = 0.f;
+      if (idx < O * I) {
+        const int o = idx / I, i = idx % I;
+        int r = 0;
+        for (; r + 2 <= G; r += 2) {
+          a0 = fmaf(DY[r * md + o], ain[r * lda + i], a0);
+          a1 = fmaf(DY[(r + 1) * md + o], ain[(r + 1) * lda + i], a1);
+        }
+        if (r < G) a0 = fmaf(DY[r * md + o], ain[r * lda + i], a0);
+      } else {
+        const int o = idx - O * I;
+        for (int r = 0; r < G; ++r) a0 += DY[r * md + o];
+      }
+      gl[idx] = a0 + a1;
+    }
+    // da[r, i] = sum_o dy[r, o] W[o, i], masked by ReLU'(ain) for the previous layer
+    const bool msk = l > 0 && a.relu[l - 1];
+    for (int idx = threadIdx.x; idx < G * I; idx += kHlThreads) {
+      const int r = idx / I, i = idx % I;
+      float a0 = 0.f, a1 = 0.f;
+      if (!msk || ain[r * lda + i] > 0.f) {
+        const float* dy = DY + r * md;
+        int o = 0;
+        for (; o + 2 <= O; o += 2) {
+          a0 = fmaf(dy[o], Wl[o * ldw + i], a0);
+          a1 = fmaf(dy[o + 1], Wl[(o + 1) * ldw + i], a1);
+        }
+        if (o < O) a0 = fmaf(dy[o], Wl[o * ldw + i], a0);
+      }
+      if (l == 0)
+        dx[idx] = a0 + a1;
+      else
+        DY2[r * md + i] = a0 + a1;
+    }
+    __syncthreads();
+    float* t = DY;
+    DY = DY2;
+    DY2 = t;
+  }
+}
+
+static size_t hl_lds(const MlpArgs& a, int G) { return HlLds(a, G, host_max_width(a)).bytes(); }
+
+static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::optional<at::Tensor>& mask,
+                      const MlpArgs& a, int64_t kind) {
+  const int64_t G = x.size(0);
+  HY_CHECK(kind >= 0 && kind <= 3, "head_loss: unknown loss kind");
+  HY_CHECK(target.is_contiguous() && target.scalar_type() == at::kFloat && target.numel() == G * a.dims[a.n],
+           "head_loss: target must be contiguous fp32 [G, out]");
+  if (mask.has_value() && mask->defined())
+    HY_CHECK(mask->scalar_type() == at::kBool && mask->is_contiguous() && mask->numel() == G,
+             "head_loss: bool mask [G]");
+  HY_CHECK(G >= 1 && hl_lds(a, (int)G) <= kHlMaxLds, "head_loss: rows x widths exceed one workgroup's LDS");
+  static bool once = [] {
+    hipFuncSetAttribute((const void*)head_loss_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)kHlMaxLds);
+    hipFuncSetAttribute((const void*)head_loss_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)kHlMaxLds);
+    return true;
+  }();
+  (void)once;
+}
+
+// returns [stats [2] = (loss, kept count), pred [G, out]]
+std::vector<at::Tensor> head_loss_fwd(const at::Tensor& x_, at::TensorList Ws_, at::TensorList bs_,
+                                      at::IntArrayRef relu, const at::Tensor& target,
+                                      const c10::optional<at::Tensor>& mask, int64_t kind) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK(x.dim() == 2, "head_loss: x must be [G, D]");
+  std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
+  auto a = make_args(x, Ws, bs, relu.vec());
+  hl_checks(x, target, mask, a, kind);
+  const int64_t G = x.size(0);
+  auto stats = at::empty({2}, x.options());
+  auto pred = at::empty({G, a.dims[a.n]}, x.options());
+  const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
+  head_loss_fwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
+      x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),
+      pred.data_ptr<float>());
+  return {stats, pred};
+}
+
+// returns [dx, dW_0, db_0, dW_1, db_1, ...]
+std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& x_, at::TensorList Ws_,
+                                      at::TensorList bs_, at::IntArrayRef relu, const at::Tensor& target,
+                                      const c10::optional<at::Tensor>& mask, const at::Tensor& stats, int64_t kind) {
+  auto x = x_.contiguous();
+  std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
+  auto a = make_args(x, Ws, bs, relu.vec());
+  hl_checks(x, target, mask, a, kind);
+  HY_CHECK(gout.numel() == 1 && gout.scalar_type() == at::kFloat && gout.is_contiguous() && stats.numel() == 2,
+           "head_loss_bwd: scalar upstream gradient and the forward's stats");
+  const int64_t G = x.size(0);
+  auto flat = at::empty({a.goff[a.n]}, x.options());
+  auto dx = at::empty_like(x);
+  const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
+  head_loss_bwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
+      gout.data_ptr<float>(), x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind,
+      stats.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>());
+  std::vector<at::Tensor> out{dx};
+  for (int l = 0; l < a.n; ++l) {
+    const int O = a.dims[l + 1], I = a.dims[l];
+    out.push_back(flat.narrow(0, a.goff[l], O * I).view({O, I}));
+    out.push_back(flat.narrow(0, a.goff[l] + O * I, O));
+  }
+  return out;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
@@ -333,9 +636,17 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "mlp_bwd(Tensor dout, Tensor x, Tensor acts, Tensor[] Ws, Tensor[] bs, int[] relu) -> "
       "(Tensor, Tensor[], Tensor[])");
+  m.def(
+      "head_loss_fwd(Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, int kind) -> "
+      "Tensor[]");
+  m.def(
+      "head_loss_bwd(Tensor gout, Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, "
+      "Tensor stats, int kind) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("mlp_fwd", hy::mlp_fwd);
   m.impl("mlp_bwd", hy::mlp_bwd);
+  m.impl("head_loss_fwd", hy::head_loss_fwd);
+  m.impl("head_loss_bwd", hy::head_loss_bwd);
 }

@@ -239,14 +239,8 @@ static const float* opt_edge_ptr(const c10::optional<at::Tensor>& t, int64_t E, 
 
 // One wave per node (lane = feature, 4-byte gathers) for F = 64 instead of 16 lanes x
 // float4: 4x the waves in flight for the latency-bound edge gathers (OC20 GPS step on
-// MI355X: 1.438 vs 1.457 ms, tools/gpu_r3_iter.sh).  HYDRA_PNA_WAVE=0 restores float4 lanes.
-static bool pna_wave_per_node(int F) {
-  static const int on = [] {
-    const char* e = std::getenv("HYDRA_PNA_WAVE");
-    return e ? std::atoi(e) : 1;
-  }();
-  return on && F == 64;
-}
+// MI355X: 1.438 vs 1.457 ms with the float4 layout, tools/gpu_r3_iter.sh).
+static bool pna_wave_per_node(int F) { return F == 64; }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> pna_fwd(const at::Tensor& x, const at::Tensor& AB,
                                                        const c10::optional<at::Tensor>& C_,

@@ -327,18 +327,46 @@ struct RadW {
   float* G[kRadMaxL];
 };
 
+// edge geometry for the in-kernel distance (null pos: the distances are given)
+struct RadGeom {
+  const float* pos;     // [N, 3]
+  const int* dst;       // [E] receiver
+  const int* src;       // [E] sender
+  const float* shifts;  // [E, 3] or null
+};
+
 template <int K>
-__global__ void __launch_bounds__(256) radial_fwd_multi_kernel(const float* __restrict__ dist, int64_t E,
-                                                               const float* __restrict__ freq, RadW W, int L, int F,
-                                                               RadEnv ev, float* __restrict__ rbf,
+__global__ void __launch_bounds__(256) radial_fwd_multi_kernel(const float* __restrict__ dist, RadGeom geo,
+                                                               int64_t E, const float* __restrict__ freq, RadW W,
+                                                               int L, int F, RadEnv ev, float* __restrict__ rbf,
                                                                float* __restrict__ drdf) {
   __shared__ float rb[kRadFwdEdges][K];
+  __shared__ float dl[kRadFwdEdges];
   const int64_t e0 = (int64_t)blockIdx.x * kRadFwdEdges;
   const int ne = (int)min<int64_t>(kRadFwdEdges, E - e0);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < ne) {
+    const int64_t e = e0 + threadIdx.x;
+    float d;
+    if (geo.pos) {  // |pos[dst] - pos[src] + shift| (geometry.py edge_vectors_and_lengths)
+      const float* pd = geo.pos + 3 * (int64_t)geo.dst[e];
+      const float* ps = geo.pos + 3 * (int64_t)geo.src[e];
+      float vx = pd[0] - ps[0], vy = pd[1] - ps[1], vz = pd[2] - ps[2];
+      if (geo.shifts) {
+        vx += geo.shifts[3 * e];
+        vy += geo.shifts[3 * e + 1];
+        vz += geo.shifts[3 * e + 2];
+      }
+      d = sqrtf(fmaf(vx, vx, fmaf(vy, vy, vz * vz)));
+    } else {
+      d = dist[e];
+    }
+    dl[threadIdx.x] = d;
+  }
+  __syncthreads();
   if (threadIdx.x < ne * K) {
     const int el = threadIdx.x / K, k = threadIdx.x % K;
-    const float x = dist[e0 + el] * ev.inv_c;
+    const float x = dl[el] * ev.inv_c;
     float u, du;
     envelope(ev, x, u, du);
     float sn, cs;
@@ -374,20 +402,50 @@ __global__ void __launch_bounds__(256) radial_fwd_multi_kernel(const float* __re
 }
 
 // returns [rbf [E, K], drbf/dfreq [E, K] (empty unless want_dfreq), R_0..R_{L-1}, G_0..G_{L-1}]
-std::vector<at::Tensor> radial_fwd_multi(const at::Tensor& dist_, const at::Tensor& freq_,
+// Distances either given (dist [E]) or computed in the kernel from pos [N, 3], dst/src [E]
+// int32 and optional shifts [E, 3] (no separate gather / subtract / norm launches).
+std::vector<at::Tensor> radial_fwd_multi(const c10::optional<at::Tensor>& dist_, const at::Tensor& freq_,
                                          const std::vector<at::Tensor>& Wemb, const std::vector<at::Tensor>& bemb,
                                          const std::vector<at::Tensor>& Wlin, double cutoff, int64_t exponent,
-                                         bool want_dfreq) {
-  auto dist = dist_.contiguous(), freq = freq_.contiguous();
-  const int64_t E = dist.numel(), K = freq.numel(), L = (int64_t)Wemb.size();
+                                         bool want_dfreq, const c10::optional<at::Tensor>& pos_,
+                                         const c10::optional<at::Tensor>& dst_, const c10::optional<at::Tensor>& src_,
+                                         const c10::optional<at::Tensor>& shifts_) {
+  auto freq = freq_.contiguous();
+  RadGeom geo{nullptr, nullptr, nullptr, nullptr};
+  at::Tensor dist, pos, dsti, srci, shifts;
+  int64_t E;
+  if (pos_.has_value() && pos_->defined()) {
+    pos = pos_->contiguous();
+    HY_CHECK(dst_.has_value() && src_.has_value(), "radial_fwd_multi: pos needs dst and src");
+    dsti = dst_->contiguous();
+    srci = src_->contiguous();
+    E = dsti.numel();
+    HY_CHECK(pos.is_cuda() && pos.scalar_type() == at::kFloat && pos.dim() == 2 && pos.size(1) == 3 &&
+                 dsti.scalar_type() == at::kInt && srci.scalar_type() == at::kInt && srci.numel() == E,
+             "radial_fwd_multi: pos float [N, 3], dst/src int32 [E]");
+    geo.pos = pos.data_ptr<float>();
+    geo.dst = dsti.data_ptr<int>();
+    geo.src = srci.data_ptr<int>();
+    if (shifts_.has_value() && shifts_->defined()) {
+      shifts = shifts_->contiguous();
+      HY_CHECK(shifts.scalar_type() == at::kFloat && shifts.numel() == 3 * E, "radial_fwd_multi: shifts [E, 3]");
+      geo.shifts = shifts.data_ptr<float>();
+    }
+  } else {
+    HY_CHECK(dist_.has_value() && dist_->defined(), "radial_fwd_multi: dist or pos required");
+    dist = dist_->contiguous();
+    E = dist.numel();
+  }
+  const auto fopt = freq.options();
+  const int64_t K = freq.numel(), L = (int64_t)Wemb.size();
   HY_CHECK(K >= 1 && K <= kRadMaxK && L >= 1 && L <= kRadMaxL && (int64_t)bemb.size() == L &&
                (int64_t)Wlin.size() == L,
            "radial_fwd_multi: 1 <= K <= 8, 1 <= L <= 8, one (Wemb, bemb, Wlin) per layer");
   const int64_t F = Wemb[0].size(0);
   RadW W{};
   std::vector<at::Tensor> out;
-  auto rbf = at::empty({E, K}, dist.options());
-  auto drdf = want_dfreq ? at::empty({E, K}, dist.options()) : at::empty({0}, dist.options());
+  auto rbf = at::empty({E, K}, fopt);
+  auto drdf = want_dfreq ? at::empty({E, K}, fopt) : at::empty({0}, fopt);
   out.push_back(rbf);
   out.push_back(drdf);
   std::vector<at::Tensor> Rs, Gs;
@@ -398,8 +456,8 @@ std::vector<at::Tensor> radial_fwd_multi(const at::Tensor& dist_, const at::Tens
     W.we[l] = Wemb[l].data_ptr<float>();
     W.be[l] = bemb[l].data_ptr<float>();
     W.wl[l] = Wlin[l].data_ptr<float>();
-    Rs.push_back(at::empty({E, F}, dist.options()));
-    Gs.push_back(at::empty({E, F}, dist.options()));
+    Rs.push_back(at::empty({E, F}, fopt));
+    Gs.push_back(at::empty({E, F}, fopt));
     W.R[l] = Rs.back().data_ptr<float>();
     W.G[l] = Gs.back().data_ptr<float>();
   }
@@ -410,8 +468,9 @@ std::vector<at::Tensor> radial_fwd_multi(const at::Tensor& dist_, const at::Tens
   const dim3 grid(ceil_div(E, kRadFwdEdges));
   float* dp = want_dfreq ? drdf.data_ptr<float>() : nullptr;
 #define HY_RAD_FWDM(KK)                                                                                        \
-  radial_fwd_multi_kernel<KK><<<grid, 256, 0, stream()>>>(dist.data_ptr<float>(), E, freq.data_ptr<float>(), W, \
-                                                          (int)L, (int)F, ev, rbf.data_ptr<float>(), dp)
+  radial_fwd_multi_kernel<KK><<<grid, 256, 0, stream()>>>(dist.defined() ? dist.data_ptr<float>() : nullptr, geo, E, \
+                                                          freq.data_ptr<float>(), W, (int)L, (int)F, ev,            \
+                                                          rbf.data_ptr<float>(), dp)
   switch (K) {
     case 1: HY_RAD_FWDM(1); break;
     case 2: HY_RAD_FWDM(2); break;
@@ -497,8 +556,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "radial_fwd(Tensor dist, Tensor freq, Tensor Wemb, Tensor bemb, Tensor Wlin, float cutoff, int exponent) -> "
       "(Tensor, Tensor)");
   m.def(
-      "radial_fwd_multi(Tensor dist, Tensor freq, Tensor[] Wemb, Tensor[] bemb, Tensor[] Wlin, float cutoff, "
-      "int exponent, bool want_dfreq) -> Tensor[]");
+      "radial_fwd_multi(Tensor? dist, Tensor freq, Tensor[] Wemb, Tensor[] bemb, Tensor[] Wlin, float cutoff, "
+      "int exponent, bool want_dfreq, Tensor? pos=None, Tensor? dst=None, Tensor? src=None, Tensor? shifts=None) "
+      "-> Tensor[]");
   m.def(
       "radial_bwd(Tensor[] dR, Tensor[] dG, Tensor R, Tensor dist, Tensor freq, Tensor Wemb, Tensor Wlin, float cutoff, "
       "int exponent) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");

@@ -220,11 +220,7 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   const bool v4 = (F % 4 == 0);
   // wide odd-multiple-of-2 rows (the SC25 EGNN's 866 channels): float2 loads halve the
   // per-column dependent load chains of the scalar path
-  static const bool v2_on = [] {
-    const char* e = std::getenv("HYDRA_SEG_VEC2");
-    return e == nullptr || e[0] != '0';
-  }();
-  const bool v2 = v2_on && !v4 && (F % 2 == 0) && F >= 128;
+  const bool v2 = !v4 && (F % 2 == 0) && F >= 128;
   auto g = row_geom(N, v4 ? F : (v2 ? F * 2 : F * 4));
   // KS row streams per segment, as long as one segment's threads stay inside a wave
   const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);

@@ -491,6 +491,36 @@ class Base(nn.Module):
         tr.stop("branch_forward")
         return out
 
+    def fused_train_loss(self, data):
+        """Training forward + loss for a model whose decoder is ONE graph-level MLP head
+        with a plain masked loss: returns ``(loss, [loss])`` (``train.step.batch_loss``
+        form) with the head and the loss as one forward and one backward launch
+        (``ops.mlp.head_loss``), or None when the model / batch does not qualify."""
+        from ..ops import mlp as _mlp
+
+        if not (self.training and self.num_heads == 1 and self.head_type[0] == "graph" and self.num_branches == 1
+                and not self.var_output and self.loss_weights[0] == 1.0 and data.get("targets") is not None
+                and data.get("graph_si") is not None and self._dev_type() == "cuda"):
+            return None
+        target = data.targets[0]
+        mask = data.get("graph_mask")
+        G = target.shape[0]
+        if target.dim() != 2 or target.shape[1] != self.head_dims[0] or target.dtype != torch.float32:
+            return None
+        if mask is not None and (mask.dtype != torch.bool or mask.numel() != G):
+            return None
+        layers = _mlp.head_loss_layers([self.graph_shared["branch-0"], self.heads_NN[0]["branch-0"]], G,
+                                       self.hidden_dim, self.loss_function_type)
+        if layers is None or layers[-1][0].weight.shape[0] != self.head_dims[0]:
+            return None
+        _rng.advance(next(self.parameters()).device)
+        x, equiv, ctx = self.encode(data)
+        x_graph = ctx.pooled if ctx.get("pooled") is not None else seg.segment_mean(x, ctx.graph_si)
+        if x_graph.shape[0] != G or x_graph.shape[1] != self.hidden_dim:
+            raise RuntimeError("fused_train_loss: pooled features do not match the targets")
+        loss, _ = _mlp.head_loss(x_graph, layers, target, mask, self.loss_function_type)
+        return loss, [loss]
+
     # ------------------------------------------------------------------ losses
     def loss(self, pred, value, head_index):
         var = None

@@ -119,13 +119,23 @@ class PNAPlusStack(Base):
     def _embedding(self, data):
         x, pos, ctx = super()._embedding(data)
         assert data.pos is not None, "PNA+ requires node positions (data.pos) to be set."
-        _, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
-        ctx.dist = dist.squeeze(-1)
+        ctx.geom = (data.pos, data.get("edge_shifts"))
+        if ctx.get("gps_lazy") and not data.pos.requires_grad:
+            ctx.dist = None  # the fused encoder computes the distances inside its radial launch
+        else:
+            ctx.dist = self._edge_dist(ctx)
         ctx.rbf_basis, ctx.rbf, ctx.radial = self.rbf, None, None
         return x, pos, ctx
 
+    @staticmethod
+    def _edge_dist(ctx):
+        pos, shifts = ctx.geom
+        return edge_vectors_and_lengths(pos, ctx.dst_si, ctx.src_si, shifts)[1].squeeze(-1)
+
     def _materialize_radial(self, ctx):
         """Radial features of the module path (the fused encoder computes its own)."""
+        if ctx.get("dist") is None:
+            ctx.dist = self._edge_dist(ctx)
         if ctx.get("radial") is not None or ctx.get("rbf") is not None:
             return
         convs = self._stack_convs()

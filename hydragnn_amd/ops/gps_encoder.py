@@ -74,9 +74,16 @@ def eligible(model, ctx):
         return False
     from .radial import MAX_K, MAX_L
 
-    dist = ctx.get("dist")
-    if dist is None or dist.requires_grad or not dist.is_cuda or ctx.get("rbf_basis") is None:
+    dist, geom = ctx.get("dist"), ctx.get("geom")
+    if dist is None:
+        if geom is None or geom[0].requires_grad or geom[0].dtype != torch.float32 or not geom[0].is_cuda:
+            return False
+        if ctx.src_si is None or ctx.src_si.index.dtype != torch.int32 or ctx.dst_si.index.dtype != torch.int32:
+            return False
+    elif dist.requires_grad or not dist.is_cuda:
         return False  # the radial basis is computed inside the encoder (no force training)
+    if ctx.get("rbf_basis") is None:
+        return False
     if ctx.rbf_basis.freq.numel() > MAX_K or len(model.graph_convs) > MAX_L or not _mode.fused("radial"):
         return False
 
@@ -164,7 +171,15 @@ def encode(model, ctx):
     cfg.gptr = gsi.rowptr if (gsi is not None and gsi.rowptr.dtype == torch.int32
                               and gsi.index.dtype == torch.int32 and gsi.rowptr.is_cuda) else None
     cfg.gidx = gsi.index if cfg.gptr is not None else None
-    xL, pooled = _GPSEncoder.apply(cfg, ctx.dist.contiguous(), basis.freq, *ins, *emb, *flat)
+    if ctx.get("dist") is None:  # distances computed inside the radial launch
+        pos, shifts = ctx.geom
+        cfg.geom = (pos.contiguous(), cfg.dst.index, cfg.src.index,
+                    shifts.float().contiguous() if shifts is not None else None)
+        dist = None
+    else:
+        cfg.geom = None
+        dist = ctx.dist.contiguous()
+    xL, pooled = _GPSEncoder.apply(cfg, dist, basis.freq, *ins, *emb, *flat)
     if cfg.gptr is not None:
         ctx.pooled = pooled  # per-graph mean of x_L (Base.decode), pooled inside the final launch
     return xL
@@ -220,12 +235,13 @@ class _GPSEncoder(torch.autograd.Function):
         prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
         dev = xin.device
         # GPS input embeddings (node rows >= num_valid -> 0), one launch each
-        x0, ab_n = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
-        e, ab_e = ops.gf_embed_fwd(eattr, rpe, Wee, Wrp, Wel, None)
-        # Bessel basis + every layer's radial embedding / gate in one launch; the basis and its
-        # frequency derivative are kept for the weight gradients
+        x0 = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
+        e = ops.gf_embed_fwd(eattr, rpe, Wee, Wrp, Wel, None)
+        # edge distances + Bessel basis + every layer's radial embedding / gate in one launch;
+        # the basis and its frequency derivative are kept for the weight gradients
+        geo = cfg.geom if cfg.geom is not None else (None, None, None, None)
         ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
-                                  cfg.cutoff, cfg.exponent, bool(freq.requires_grad))
+                                  cfg.cutoff, cfg.exponent, bool(freq.requires_grad), *geo)
         rbf, drdf, Rl, Gl = ro[0], ro[1], ro[2:2 + L], ro[2 + L:2 + 2 * L]
         acc = torch.empty(L, NREP * SITES * F, device=dev, dtype=torch.float64)
         saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
@@ -282,7 +298,7 @@ class _GPSEncoder(torch.autograd.Function):
         ctx.st = st
         ctx.acc, ctx.saved = acc, saved
         ctx.radial = (rbf, drdf, Rl, Gl)
-        ctx.emb = (ab_n, ab_e, e)
+        ctx.emb = e
         ctx.freq_grad = bool(freq.requires_grad)
         ctx.save_for_backward(xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, xL, *flat)
         return xL, pooled
@@ -295,7 +311,7 @@ class _GPSEncoder(torch.autograd.Function):
         xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, xL, *flat = ctx.saved_tensors
         prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
         rbf, drdf, Rl, Gl = ctx.radial
-        ab_n, ab_e, e = ctx.emb
+        e = ctx.emb
         K = rbf.shape[1]
         acc, saved, st = ctx.acc, ctx.saved, ctx.st
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
@@ -307,8 +323,9 @@ class _GPSEncoder(torch.autograd.Function):
         dys, xs, dws, dbs = [], [], [], []
 
         def item(dy, x, W, with_bias):
-            dW = torch.empty(W.shape, device=dev, dtype=torch.float32)
-            db = torch.empty(W.shape[0], device=dev, dtype=torch.float32) if with_bias else None
+            shape = W if isinstance(W, tuple) else W.shape
+            dW = torch.empty(shape, device=dev, dtype=torch.float32)
+            db = torch.empty(shape[0], device=dev, dtype=torch.float32) if with_bias else None
             dys.append(dy)
             xs.append(x)
             dws.append(dW)
@@ -347,6 +364,9 @@ class _GPSEncoder(torch.autograd.Function):
             ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
             # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch
             dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+            # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
+            # MI355X: the attention passes are throughput-bound once they overlap the local
+            # branch, 209 vs 200 us per layer)
             side.join(dz2, da, dO, dqkv, dw2n, db2n)
             if l > 0:
                 sp = st[l - 1]
@@ -372,28 +392,27 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 14], grads[base + 15] = dw2n, db2n
             grads[base + 16], grads[base + 17] = dw3, db3
             grads[base + 18], grads[base + 19] = dw4, db4
-        dfreq_w = item(drbf, drdf, torch.empty(K, K, device=dev), False)[0] if ctx.freq_grad else None
-        # embeddings: d[ab] = dy Wl, then their three weight gradients per embedding
-        dab_n = ops.gf_embed_bwd(dx0, Wnl)
-        dab_e = ops.gf_embed_bwd(de, Wel)
-        emb_g = [item(dx0, ab_n, Wnl, False)[0], item(dab_n[:, :F], xin, Wne, False)[0],
-                 item(dab_n[:, F:], pe, Wpe, False)[0], item(de, ab_e, Wel, False)[0],
-                 item(dab_e[:, :F], eattr, Wee, False)[0], item(dab_e[:, F:], rpe, Wrp, False)[0]]
+        dfreq_w = item(drbf, drdf, (K, K), False)[0] if ctx.freq_grad else None
+        # embeddings: only the narrow products dy^T [A | B] (see csrc/gps_fused.hip, EmbFwd)
+        tn = [item(dx0, xin, (F, xin.shape[1]), False)[0], item(dx0, pe, (F, pe.shape[1]), False)[0]]
+        te = [item(de, eattr, (F, eattr.shape[1]), False)[0], item(de, rpe, (F, rpe.shape[1]), False)[0]]
         # every weight gradient of the stack (incl. the radial basis and its frequencies): one
         # grouped launch pair
         ops.linear_wgrad_grouped(dys, xs, dws, dbs, [0] * len(dys))
-        dfreq = torch.diagonal(dfreq_w).contiguous() if dfreq_w is not None else None
+        # weight-prep backward of every layer, embedding weights and dfreq: one launch
+        wp = []
         for l, gw in wg:
+            wp += [gw["Wab"][0], gw["Wr"][0], gw["Wd"][0], gw["Wr"][1], prm[l][4], prm[l][6], prm[l][7]]
+        fin = ops.gf_finish(wp, [tn[0], tn[1], Wne, Wpe, Wnl, te[0], te[1], Wee, Wrp, Wel], dfreq_w)
+        dfreq = fin[4 * L + 6] if dfreq_w is not None else None
+        emb_g = fin[4 * L: 4 * L + 6]  # node dWa, dWb, dWl, edge dWa, dWb, dWl
+        for k, (l, gw) in enumerate(wg):
             base = NP * l
             grads[base + 24], grads[base + 25] = gw["Wemb"]
             grads[base + 26] = gw["Wrl"][0]
-            Wpre, Wenc, benc = prm[l][4], prm[l][6], prm[l][7]
-            dWpre, dbpre, dWenc, dbenc = ops.pna_wprep_bwd(gw["Wab"][0], gw["Wr"][0], gw["Wd"][0], gw["Wr"][1], Wpre,
-                                                           Wenc, benc)
             grads[base + 0], grads[base + 1] = gw["Win"]
             grads[base + 2], grads[base + 3] = gw["Wo"]
-            grads[base + 4], grads[base + 5] = dWpre, dbpre
-            grads[base + 6], grads[base + 7] = dWenc, dbenc
+            grads[base + 4], grads[base + 5], grads[base + 6], grads[base + 7] = fin[4 * k: 4 * k + 4]
             grads[base + 8], grads[base + 9] = gw["Wpost"]
             grads[base + 10], grads[base + 11] = gw["Wlin"]
             grads[base + 20], grads[base + 21] = gw["W1"]
@@ -401,5 +420,4 @@ class _GPSEncoder(torch.autograd.Function):
         ctx.st = None
         ctx.radial = None
         ctx.emb = None
-        return (None, None, dfreq, None, None, None, None, emb_g[1], emb_g[2], emb_g[0], emb_g[4], emb_g[5], emb_g[3],
-                *grads)
+        return (None, None, dfreq, None, None, None, None, *emb_g, *grads)

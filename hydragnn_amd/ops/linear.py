@@ -198,16 +198,9 @@ def _edge_linear_ok(xs, ws, b):
             and (b is None or b.dtype == torch.float32))
 
 
-_EDGE_DGRAD = os.environ.get("HYDRA_EDGE_DGRAD", "0") == "1"
-
-
 def _dgrad(dy, w):
-    """dX = dY @ W of an edge-sized linear.  HYDRA_EDGE_DGRAD=1 routes it through the
-    edge-linear kernel; measured on MI355X (OC20 GPS step, 23k x 64 @ 64 x 64) it is
-    9.5 us per call, on par with the library GEMM, so the library stays the default."""
-    if _EDGE_DGRAD and dy.is_cuda and dy.dtype == torch.float32 and w.dtype == torch.float32 and dy.dim() == 2 \
-            and dy.stride(1) == 1 and dy.shape[1] <= 188:
-        return _native.ops().edge_linear_dgrad(dy, w)
+    """dX = dY @ W of an edge-sized linear (library GEMM: the edge-linear kernel measured
+    on par, 9.5 us per call at 23k x 64 @ 64 x 64 on MI355X, and was removed)."""
     return dy @ w
 
 

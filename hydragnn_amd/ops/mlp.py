@@ -77,3 +77,61 @@ def sequential_chain(x, *seqs):
     for s in seqs:
         x = s(x)
     return x
+
+
+# ---------------------------------------------------------------- head + loss
+HL_MAX_LDS = 150 * 1024
+_KIND = {"mse": 0, "mae": 1, "rmse": 2, "smooth_l1": 3}
+
+
+def _hl_lds(G, dims):
+    """LDS footprint of ``csrc/mlp.hip`` head_loss kernels (HlLds)."""
+    w = sum((dims[i] + 1) * dims[i + 1] for i in range(len(dims) - 1))
+    md = max(dims) + 1
+    ldx = dims[0] + 1 + dims[0] % 2
+    return 4 * (w + G * ldx + G * (sum(dims[1:]) | 1) + 2 * G * md)
+
+
+def head_loss_layers(seqs, G, in_dim, kind):
+    """[(Linear, relu)] when ``seqs`` + a masked ``kind`` loss over G rows fit the one-
+    workgroup head+loss kernels, else None."""
+    if kind not in _KIND or not _mode.fused("headloss") or not _mode.fused("mlp") or G < 1:
+        return None
+    layers = _chain(seqs)
+    if not layers or len(layers) > MAX_LAYERS:
+        return None
+    dims = [in_dim] + [m.weight.shape[0] for m, _ in layers]
+    if max(dims) > MAX_DIM or _hl_lds(G, dims) > HL_MAX_LDS:
+        return None
+    if any(m.weight.dtype != torch.float32 or not m.weight.is_cuda for m, _ in layers):
+        return None
+    return layers
+
+
+class _HeadLoss(torch.autograd.Function):
+    """loss = masked_loss(MLP(x), target) as one forward and one backward launch."""
+
+    @staticmethod
+    def forward(ctx, x, target, mask, kind, relu, *params):
+        stats, pred = _native.ops().head_loss_fwd(x, params[0::2], params[1::2], relu, target, mask, kind)
+        ctx.save_for_backward(x, target, mask, stats, *params)
+        ctx.kind, ctx.relu = kind, relu
+        ctx.mark_non_differentiable(pred)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for pred
+        return stats[0], pred
+
+    @staticmethod
+    def backward(ctx, g, _gpred):
+        x, target, mask, stats, *params = ctx.saved_tensors
+        out = _native.ops().head_loss_bwd(g.reshape(1).contiguous(), x, params[0::2], params[1::2], ctx.relu, target,
+                                          mask, stats, ctx.kind)
+        return (out[0], None, None, None, None, *out[1:])
+
+
+def head_loss(x, layers, target, mask, kind):
+    """(loss, pred) of a masked-loss graph head over the pooled features ``x``."""
+    params = []
+    for m, _ in layers:
+        params += [m.weight, m.bias]
+    return _HeadLoss.apply(x.contiguous(), target.contiguous(), None if mask is None else mask.contiguous(),
+                           _KIND[kind], [int(r) for _, r in layers], *params)

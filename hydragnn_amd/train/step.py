@@ -267,13 +267,23 @@ class TrainStep:
             if sync:
                 self.sync.begin()
             with deferred_wgrad(defer):
-                loss.backward()
+                loss.backward(self._seed(loss))
             self.sync.finish()
             return
         with deferred_wgrad(defer):
-            loss.backward()
+            loss.backward(self._seed(loss))
         if self.flat_grads is not None:
             self.flat_grads.gather()
+
+    def _seed(self, loss):
+        """The backward seed d loss / d loss = 1 as a persistent tensor (an implicit seed is
+        a fill launch inside every captured step)."""
+        one = getattr(self, "_one", None)
+        if one is None or one.device != loss.device or one.dtype != loss.dtype or one.shape != loss.shape:
+            if torch.cuda.is_available() and loss.is_cuda and torch.cuda.is_current_stream_capturing():
+                return None  # never allocate inside a capture; the warm-up run has created it
+            one = self._one = torch.ones_like(loss, memory_format=torch.contiguous_format)
+        return one
 
     def eager(self, store, indices):
         batch = store.batch(indices)
@@ -338,6 +348,10 @@ class TrainStep:
             with composite_mode(True):  # every op on the pos -> E path must be twice differentiable
                 pred = self.model(batch)
                 return self.module.energy_force_loss(pred, batch)
+        if self.model is self.module and hasattr(self.module, "fused_train_loss"):
+            out = self.module.fused_train_loss(batch)  # single graph head: head + loss fused
+            if out is not None:
+                return out
         pred = self.model(batch)
         return batch_loss(self.module, pred, batch)
 

@@ -1,0 +1,53 @@
+"""Fused graph head + masked loss (``ops/mlp.py`` _HeadLoss over ``csrc/mlp.hip``
+head_loss_fwd/bwd, one workgroup each way) == plain fp32 PyTorch: Linear/ReLU chain, masked
+mean loss over kept rows, autograd gradients of the input and of every weight."""
+import pytest
+import torch
+
+from hydragnn_amd.ops import mlp as _mlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_loss(kind, pred, target, mask):
+    keep = mask.view(-1, 1) if mask is not None else torch.ones_like(pred, dtype=torch.bool)
+    d = (pred - target)[keep.expand_as(pred)]
+    if kind == "mae":
+        return d.abs().mean()
+    if kind == "smooth_l1":
+        a = d.abs()
+        return torch.where(a < 1.0, 0.5 * d * d, a - 0.5).mean()
+    l = (d * d).mean()
+    return l.sqrt() if kind == "rmse" else l
+
+
+@pytest.mark.parametrize("kind", ["mae", "mse", "rmse", "smooth_l1"])
+@pytest.mark.parametrize("G,dims,masked", [(33, [64, 50, 50, 50, 25, 1], True), (1, [32, 16, 1], False),
+                                           (100, [64, 64, 3], True)])
+def test_head_loss_matches_torch(kind, G, dims, masked):
+    dev = torch.device("cuda")
+    torch.manual_seed(G + len(dims))
+    lins = [torch.nn.Linear(dims[i], dims[i + 1]).to(dev) for i in range(len(dims) - 1)]
+    seq = []
+    for i, l in enumerate(lins):
+        seq.append(l)
+        if i < len(lins) - 1:
+            seq.append(torch.nn.ReLU())
+    seq = torch.nn.Sequential(*seq)
+    x = torch.randn(G, dims[0], device=dev, requires_grad=True)
+    target = torch.randn(G, dims[-1], device=dev)
+    mask = (torch.arange(G, device=dev) < max(1, G - 2)) if masked else None
+    layers = _mlp.head_loss_layers([seq], G, dims[0], kind)
+    assert layers is not None
+    loss, pred = _mlp.head_loss(x, layers, target, mask, kind)
+    gx, *gw = torch.autograd.grad(loss * 1.7, [x] + [p for l in lins for p in (l.weight, l.bias)])
+
+    xr = x.detach().clone().requires_grad_(True)
+    pr = seq(xr)
+    lr = _ref_loss(kind, pr, target, mask)
+    gxr, *gwr = torch.autograd.grad(lr * 1.7, [xr] + [p for l in lins for p in (l.weight, l.bias)])
+    torch.testing.assert_close(pred, pr.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss, lr.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gx, gxr, rtol=1e-4, atol=1e-6)
+    for a, b in zip(gw, gwr):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
