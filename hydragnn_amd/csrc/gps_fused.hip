@@ -1175,13 +1175,16 @@ struct FinEmb {
   float *dWa, *dWb, *dWl;
   int ka, kb;
 };
+// workgroups are assigned to jobs on the host (a job's parameters are then uniform across
+// the workgroup: scalar loads, not per-lane loads from the kernarg segment)
 struct Finish {
   FinWprep wp[kFinMaxL];
   FinEmb em[2];
   const float* dfw;  // [K, K] or null
   float* dfreq;      // [K]
   int L, ne, F, d, K;
-  int64_t per_l, per_e[2], total;
+  int per_l, per_e[2];
+  int blk_l, blk_e[2], blk_f;  // workgroups per layer job / per embedding job / dfreq
 };
 
 __device__ __forceinline__ float fin_dot(const float* __restrict__ a, int sa, const float* __restrict__ b, int sb,
@@ -1208,14 +1211,14 @@ __device__ __forceinline__ float fin_dot(const float* __restrict__ a, int sa, co
 }
 
 __global__ void __launch_bounds__(256) finish_kernel(Finish a) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.total) return;
+  int b = blockIdx.x;
   const int F = a.F, d = a.d, ld = 3 * F, le = d + F;
-  if (t < a.L * a.per_l) {
-    const FinWprep& w = a.wp[t / a.per_l];
-    int64_t q = t % a.per_l;
+  if (b < a.L * a.blk_l) {
+    const FinWprep& w = a.wp[b / a.blk_l];
+    int q = (b % a.blk_l) * 256 + threadIdx.x;
+    if (q >= a.per_l) return;
     if (q < 2 * F * F) {  // dW[:, :2F] <- dWab (row blocks [W_i; W_j])
-      const int o = (int)(q / (2 * F)), c = (int)(q % (2 * F));
+      const int o = q / (2 * F), c = q % (2 * F);
       w.dW[o * ld + c] = w.dWab[((c / F) * F + o) * F + (c % F)];
       return;
     }
@@ -1226,48 +1229,50 @@ __global__ void __launch_bounds__(256) finish_kernel(Finish a) {
     }
     q -= F;
     if (q < F * F) {  // dW_e[o, j] = dWr[o,:] . encW[j, d:] + dWd[o,:] . encW[j, :d] + dbc[o] encb[j]
-      const int o = (int)(q / F), j = (int)(q % F);
+      const int o = q / F, j = q % F;
       float v = fin_dot(w.dWr + o * F, 1, w.encW + j * le + d, 1, F) + w.dbc[o] * w.encb[j];
       if (d > 0) v += fin_dot(w.dWd + o * d, 1, w.encW + j * le, 1, d);
       w.dW[o * ld + 2 * F + j] = v;
       return;
     }
     q -= F * F;
-    if (q < (int64_t)F * le) {  // dencW[j, c] = sum_o W_e[o, j] [dWd | dWr][o, c]
-      const int j = (int)(q / le), c = (int)(q % le);
+    if (q < F * le) {  // dencW[j, c] = sum_o W_e[o, j] [dWd | dWr][o, c]
+      const int j = q / le, c = q % le;
       w.dencW[q] = c < d ? fin_dot(w.W + 2 * F + j, ld, w.dWd + c, d, F)
                          : fin_dot(w.W + 2 * F + j, ld, w.dWr + (c - d), F, F);
       return;
     }
-    q -= (int64_t)F * le;
+    q -= F * le;
     w.dencb[q] = fin_dot(w.W + 2 * F + q, ld, w.dbc, 1, F);
     return;
   }
-  t -= a.L * a.per_l;
+  b -= a.L * a.blk_l;
   for (int m = 0; m < a.ne; ++m) {
-    if (t >= a.per_e[m]) {
-      t -= a.per_e[m];
+    if (b >= a.blk_e[m]) {
+      b -= a.blk_e[m];
       continue;
     }
     const FinEmb& e = a.em[m];
+    int t = b * 256 + threadIdx.x;
+    if (t >= a.per_e[m]) return;
     if (t < 2 * F * F) {  // dWl[o, c]
-      const int o = (int)(t / (2 * F)), c = (int)(t % (2 * F));
+      const int o = t / (2 * F), c = t % (2 * F);
       e.dWl[t] = c < F ? fin_dot(e.Ta + o * e.ka, 1, e.Wa + c * e.ka, 1, e.ka)
                        : fin_dot(e.Tb + o * e.kb, 1, e.Wb + (c - F) * e.kb, 1, e.kb);
       return;
     }
     t -= 2 * F * F;
     if (t < F * e.ka) {  // dWa[c, k] = sum_o Wl[o, c] Ta[o, k]
-      const int c = (int)(t / e.ka), k = (int)(t % e.ka);
+      const int c = t / e.ka, k = t % e.ka;
       e.dWa[t] = fin_dot(e.Wl + c, 2 * F, e.Ta + k, e.ka, F);
       return;
     }
     t -= F * e.ka;
-    const int c = (int)(t / e.kb), k = (int)(t % e.kb);  // dWb[c, k] = sum_o Wl[o, F + c] Tb[o, k]
+    const int c = t / e.kb, k = t % e.kb;  // dWb[c, k] = sum_o Wl[o, F + c] Tb[o, k]
     e.dWb[t] = fin_dot(e.Wl + F + c, 2 * F, e.Tb + k, e.kb, F);
     return;
   }
-  if (t < a.K) a.dfreq[t] = a.dfw[t * a.K + t];
+  if (threadIdx.x < a.K) a.dfreq[threadIdx.x] = a.dfw[threadIdx.x * a.K + threadIdx.x];
 }
 
 // ====================================================================================
@@ -1609,8 +1614,9 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
                        db.data_ptr<float>(), dencW.data_ptr<float>(), dencb.data_ptr<float>()};
     out.insert(out.end(), {dW, db, dencW, dencb});
   }
-  a.per_l = 3 * F * F + 2 * F + F * (F + a.d);
-  a.total = a.L * a.per_l;
+  a.per_l = (int)(3 * F * F + 2 * F + F * (F + a.d));
+  a.blk_l = ceil_div(a.per_l, 256);
+  int blocks = a.L * a.blk_l;
   for (int m = 0; m < a.ne; ++m) {
     const at::Tensor* t = &em[5 * m];
     for (int u = 0; u < 5; ++u) HY_CHECK(t[u].is_contiguous() && t[u].scalar_type() == at::kFloat, "gf_finish: em");
@@ -1622,8 +1628,9 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
     a.em[m] = FinEmb{t[0].data_ptr<float>(), t[1].data_ptr<float>(), t[2].data_ptr<float>(), t[3].data_ptr<float>(),
                      t[4].data_ptr<float>(), dWa.data_ptr<float>(), dWb.data_ptr<float>(), dWl.data_ptr<float>(),
                      (int)ka, (int)kb};
-    a.per_e[m] = 2 * F * F + F * ka + F * kb;
-    a.total += a.per_e[m];
+    a.per_e[m] = (int)(2 * F * F + F * ka + F * kb);
+    a.blk_e[m] = ceil_div(a.per_e[m], 256);
+    blocks += a.blk_e[m];
     out.insert(out.end(), {dWa, dWb, dWl});
   }
   if (dfw.has_value() && dfw->defined()) {
@@ -1632,10 +1639,11 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
     auto dfreq = at::empty({a.K}, opt);
     a.dfw = dfw->data_ptr<float>();
     a.dfreq = dfreq.data_ptr<float>();
-    a.total += a.K;
+    HY_CHECK(a.K <= 256, "gf_finish: dfw [K, K] with K <= 256");
+    blocks += 1;
     out.push_back(dfreq);
   }
-  if (a.total > 0) finish_kernel<<<ceil_div(a.total, 256), 256, 0, stream()>>>(a);
+  if (blocks > 0) finish_kernel<<<blocks, 256, 0, stream()>>>(a);
   return out;
 }
 

@@ -344,109 +344,186 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> mlp_bwd
 // One 1024-thread workgroup; everything lives in LDS: W per layer natural [o][i],
 // X [G][D0], every layer's activation A [G][S] and two dY buffers [G][md].
 // The backward launch recomputes the (tiny) forward chain instead of reading it back.
+typedef float f4v_hl __attribute__((ext_vector_type(4)));
 constexpr int kHlThreads = 1024;
+constexpr int kHlWaves = kHlThreads / 64;
+constexpr int kHlBatch = 16;  // staged loads in flight per thread
 constexpr size_t kHlMaxLds = 150 * 1024;
 
-// LDS layout shared by both kernels.  Every row stride is odd (W rows I+1, activation rows
-// S|1, X rows D0+1 or D0+2) so lanes walking a column never collide on a bank, and lanes
-// walking a row read consecutive words.
-struct HlLds {
-  int nw, xs, as, dy, md, ldx, lda;
-  int woff[kMlpMaxLayers + 1];
-  __host__ __device__ HlLds(const MlpArgs& a, int G, int mw) {
-    md = mw + 1;
-    int o = 0;
-    for (int l = 0; l < a.n; ++l) {
-      woff[l] = o;
-      o += a.dims[l + 1] * (a.dims[l] + 1);
-    }
-    woff[a.n] = o;
-    nw = o;
-    ldx = a.dims[0] + 1 + (a.dims[0] % 2 ? 1 : 0);
-    lda = a.aoff[a.n] | 1;
-    xs = G * ldx;
-    as = G * lda;
-    dy = G * md;
-  }
-  __host__ __device__ size_t bytes() const { return sizeof(float) * ((size_t)nw + xs + as + 2 * (size_t)dy); }
+// Every layer product runs on v_mfma_f32_16x16x4f32 (exact fp32): a 16x16 output tile per
+// wave, operands read straight from LDS.  (A VALU form, one output per lane, needed two LDS
+// reads per FMA and was LDS-issue bound: ~6 us per 33 x 50 x 64 layer.)  Every LDS matrix
+// is [rows padded to 16][cols padded to 16, + 1] with zeroed padding, so tiles never need
+// bounds checks and reads along either dimension are bank-conflict free (odd row stride).
+__device__ __host__ __forceinline__ int hl_r16(int v) { return (v + 15) / 16 * 16; }
+__device__ __host__ __forceinline__ int hl_ld(int cols) { return hl_r16(cols) + 1; }
+
+struct HlLayout {  // float offsets into the dynamic LDS block
+  int w[kMlpMaxLayers];      // W_l   [r16(O)][ld(I)]
+  int act[kMlpMaxLayers];    // A_l   [Gp][ld(O)]   (layer l's output)
+  int x, dy, dy2, total, Gp, ldy;
 };
 
-// all weights (row stride I+1) and the input rows into LDS, 8 loads in flight per thread
-__device__ void hl_stage(const MlpArgs& a, const HlLds& L, const float* __restrict__ x, int G, float* WS, float* XS) {
-  for (int l = 0; l <= a.n; ++l) {
-    const bool isx = l == a.n;
-    const int I = isx ? a.dims[0] : a.dims[l], cnt = isx ? G * a.dims[0] : a.dims[l + 1] * a.dims[l];
-    const int ld = isx ? L.ldx : I + 1;
-    const float* __restrict__ src = isx ? x : a.W[l];
-    float* dst = isx ? XS : WS + L.woff[l];
-    for (int base = threadIdx.x; base < cnt; base += 8 * kHlThreads) {
-      float v[8];
+__device__ __host__ inline HlLayout hl_layout(const MlpArgs& a, int G) {
+  HlLayout L{};
+  L.Gp = hl_r16(G);
+  int o = 0, mw = a.dims[0];
+  for (int l = 0; l < a.n; ++l) {
+    L.w[l] = o;
+    o += hl_r16(a.dims[l + 1]) * hl_ld(a.dims[l]);
+    mw = a.dims[l + 1] > mw ? a.dims[l + 1] : mw;
+  }
+  L.x = o;
+  o += L.Gp * hl_ld(a.dims[0]);
+  for (int l = 0; l < a.n; ++l) {
+    L.act[l] = o;
+    o += L.Gp * hl_ld(a.dims[l + 1]);
+  }
+  L.ldy = hl_ld(mw);
+  L.dy = o;
+  o += L.Gp * L.ldy;
+  L.dy2 = o;
+  o += L.Gp * L.ldy;
+  L.total = o;
+  return L;
+}
+
+__device__ __forceinline__ f4v_hl hl_mfma(float a, float b, f4v_hl c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// zero the whole block, then every weight, the input rows and (backward) the saved
+// activations in ONE pass over a flat index (kHlBatch loads in flight per thread before the
+// stores).  The segment table is built in LDS: a per-lane search through the kernel-argument
+// arrays compiles to per-lane loads from the kernarg segment, a memory round trip per probe.
+constexpr int kHlSegs = 2 * kMlpMaxLayers + 1;
+struct HlSegTab {
+  const float* src[kHlSegs];
+  int beg[kHlSegs + 1];
+  int width[kHlSegs], ld[kHlSegs], dst[kHlSegs];
+  int n;
+};
+
+__device__ void hl_stage(const MlpArgs& a, const HlLayout& L, const float* __restrict__ x,
+                         const float* __restrict__ acts, int G, float* sm) {
+  __shared__ HlSegTab T;
+  for (int e = threadIdx.x; e < L.total; e += kHlThreads) sm[e] = 0.f;
+  if (threadIdx.x == 0) {
+    int k = 0, b = 0;
+    for (int l = 0; l < a.n; ++l, ++k) {
+      T.src[k] = a.W[l];
+      T.beg[k] = b;
+      T.width[k] = a.dims[l];
+      T.ld[k] = hl_ld(a.dims[l]);
+      T.dst[k] = L.w[l];
+      b += a.dims[l] * a.dims[l + 1];
+    }
+    T.src[k] = x;
+    T.beg[k] = b;
+    T.width[k] = a.dims[0];
+    T.ld[k] = hl_ld(a.dims[0]);
+    T.dst[k] = L.x;
+    b += G * a.dims[0];
+    ++k;
+    if (acts) {  // acts [G, S]: layer l's block of columns -> A_l
+      for (int l = 0; l < a.n; ++l, ++k) {
+        T.src[k] = acts + a.aoff[l];  // strided rows: handled by the S-wide flat index below
+        T.beg[k] = b;
+        T.width[k] = a.dims[l + 1];
+        T.ld[k] = hl_ld(a.dims[l + 1]);
+        T.dst[k] = L.act[l];
+        b += G * a.dims[l + 1];
+      }
+    }
+    T.beg[k] = b;
+    T.n = k;
+  }
+  __syncthreads();
+  const int total = T.beg[T.n], ns = T.n, nplain = a.n + 1, S = a.aoff[a.n];
+  for (int base = threadIdx.x; base < total; base += kHlBatch * kHlThreads) {
+    float v[kHlBatch];
+    int sg[kHlBatch];
+    int q = 0;  // idx grows with k: the segment search resumes where the last one stopped
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = src[min(base + k * kHlThreads, cnt - 1)];
+    for (int k = 0; k < kHlBatch; ++k) {
+      const int idx = min(base + k * kHlThreads, total - 1);
+      while (q + 1 < ns && idx >= T.beg[q + 1]) ++q;
+      sg[k] = q;
+      const int e = idx - T.beg[q];
+      // activation segments read rows of the [G, S] image (row stride S, not the width)
+      v[k] = q < nplain ? T.src[q][e] : T.src[q][(e / T.width[q]) * S + e % T.width[q]];
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int idx = base + k * kHlThreads;
-        if (idx < cnt) dst[(idx / I) * ld + idx % I] = v[k];
+    for (int k = 0; k < kHlBatch; ++k) {
+      const int idx = base + k * kHlThreads;
+      if (idx < total) {
+        const int q = sg[k], e = idx - T.beg[q], w = T.width[q];
+        sm[T.dst[q] + (e / w) * T.ld[q] + e % w] = v[k];
       }
     }
   }
   __syncthreads();
 }
 
-// forward chain into AS; lanes over outputs o (W rows conflict-free, input reads broadcast)
-__device__ void hl_chain(const MlpArgs& a, const HlLds& L, int G, const float* WS, const float* XS, float* AS) {
+// forward chain: A_l = act(A_{l-1} W_l^T + b_l), tiles of 16 rows x 16 outputs per wave;
+// padding rows/columns stay exactly zero; rows < G, columns < O also go to the global acts
+__device__ void hl_chain(const MlpArgs& a, const HlLayout& L, int G, float* sm, float* __restrict__ acts) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  const int S = a.aoff[a.n];
   for (int l = 0; l < a.n; ++l) {
     const int I = a.dims[l], O = a.dims[l + 1];
-    const float* in = l == 0 ? XS : AS + a.aoff[l - 1];
-    const int ldi = l == 0 ? L.ldx : L.lda;
-    const float* Wl = WS + L.woff[l];
+    const float* in = sm + (l == 0 ? L.x : L.act[l - 1]);
+    const int ldi = hl_ld(I), ldo = hl_ld(O);
+    const float* W = sm + L.w[l];
+    float* out = sm + L.act[l];
+    const int ct = hl_r16(O) / 16, tiles = (L.Gp / 16) * ct, K4 = (I + 3) / 4;
     const float* __restrict__ bb = a.b[l];
-    for (int idx = threadIdx.x; idx < G * O; idx += kHlThreads) {
-      const int o = idx % O, r = idx / O;
-      const float* xr = in + r * ldi;
-      const float* wr = Wl + o * (I + 1);
-      float a0 = bb[o], a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      int i = 0;
-      for (; i + 4 <= I; i += 4) {
-        a0 = fmaf(xr[i], wr[i], a0);
-        a1 = fmaf(xr[i + 1], wr[i + 1], a1);
-        a2 = fmaf(xr[i + 2], wr[i + 2], a2);
-        a3 = fmaf(xr[i + 3], wr[i + 3], a3);
+    for (int t = wv; t < tiles; t += kHlWaves) {
+      const int r0 = (t / ct) * 16, c0 = (t % ct) * 16;
+      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
+      const float* ap = in + (r0 + li) * ldi + lg;
+      const float* bp = W + (c0 + li) * ldi + lg;
+      for (int k = 0; k < K4; ++k) acc = hl_mfma(ap[4 * k], bp[4 * k], acc);
+      const int col = c0 + li;
+      const float bias = col < O ? bb[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 4 * lg + r;
+        float v = acc[r] + bias;
+        if (a.relu[l]) v = fmaxf(v, 0.f);
+        const bool live = row < G && col < O;
+        out[row * ldo + col] = live ? v : 0.f;
+        if (live && acts) acts[(int64_t)row * S + a.aoff[l] + col] = v;
       }
-      for (; i < I; ++i) a0 = fmaf(xr[i], wr[i], a0);
-      float v = (a0 + a1) + (a2 + a3);
-      if (a.relu[l]) v = fmaxf(v, 0.f);
-      AS[r * L.lda + a.aoff[l] + o] = v;
     }
     __syncthreads();
   }
 }
 
-// out: [loss, count]; pred [G, Do]
+// out: [loss, count]; pred [G, Do]; acts [G, S] (every layer's output, for the backward)
 __global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* __restrict__ x, int G, MlpArgs a,
                                                                    const float* __restrict__ target,
                                                                    const bool* __restrict__ mask, int kind,
-                                                                   float* __restrict__ out, float* __restrict__ pred) {
+                                                                   float* __restrict__ out, float* __restrict__ pred,
+                                                                   float* __restrict__ acts) {
   extern __shared__ float sm[];
-  const HlLds L(a, G, max_width(a));
-  float* WS = sm;
-  float* XS = WS + L.nw;
-  float* AS = XS + L.xs;
-  hl_stage(a, L, x, G, WS, XS);
-  hl_chain(a, L, G, WS, XS, AS);
-  const int S = L.lda, Do = a.dims[a.n], po = a.aoff[a.n - 1];
-  __shared__ double red[kHlThreads / 64][2];
+  const HlLayout L = hl_layout(a, G);
+  hl_stage(a, L, x, nullptr, G, sm);
+  hl_chain(a, L, G, sm, acts);
+  const int Do = a.dims[a.n], ldo = hl_ld(Do);
+  const float* P = sm + L.act[a.n - 1];
+  __shared__ double red[kHlWaves][2];
   double s = 0.0, c = 0.0;
   for (int idx = threadIdx.x; idx < G * Do; idx += kHlThreads) {
     const int r = idx / Do, o = idx % Do;
-    const float p = AS[r * S + po + o];
+    const float p = P[r * ldo + o];
     pred[idx] = p;
     if (mask == nullptr || mask[r]) {
       s += (double)loss_term_hl(kind, p - target[idx]);
       c += 1.0;
     }
   }
-  // fixed-order reduction: wave shuffle tree, then wave 0 over the per-wave sums
+  // fixed-order reduction: wave shuffle tree, then thread 0 over the per-wave sums
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off);
     c += __shfl_xor(c, off);
@@ -459,7 +536,7 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* 
   __syncthreads();
   if (threadIdx.x == 0) {
     double ts = 0.0, tc = 0.0;
-    for (int k = 0; k < kHlThreads / 64; ++k) {
+    for (int k = 0; k < kHlWaves; ++k) {
       ts += red[k][0];
       tc += red[k][1];
     }
@@ -472,28 +549,28 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* 
 
 // grads: [dW_0 | db_0 | dW_1 | db_1 | ...] (goff), dx [G, D0]
 __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* __restrict__ gout,
-                                                                   const float* __restrict__ x, int G, MlpArgs a,
+                                                                   const float* __restrict__ x,
+                                                                   const float* __restrict__ acts, int G, MlpArgs a,
                                                                    const float* __restrict__ target,
                                                                    const bool* __restrict__ mask, int kind,
                                                                    const float* __restrict__ fwd,
                                                                    float* __restrict__ grads, float* __restrict__ dx) {
   extern __shared__ float sm[];
-  const HlLds L(a, G, max_width(a));
-  float* WS = sm;
-  float* XS = WS + L.nw;
-  float* AS = XS + L.xs;
-  float* DY = AS + L.as;
-  float* DY2 = DY + L.dy;
-  const int md = L.md;
-  hl_stage(a, L, x, G, WS, XS);
-  hl_chain(a, L, G, WS, XS, AS);
-  const int n = a.n, S = L.lda, Do = a.dims[n], po = a.aoff[n - 1];
+  const HlLayout L = hl_layout(a, G);
+  hl_stage(a, L, x, acts, G, sm);
+  const int n = a.n, Do = a.dims[n];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  float* DY = sm + L.dy;
+  float* DY2 = sm + L.dy2;
+  const int ldy = L.ldy;
   {
     const float g = gout[0], den = fwd[1] > 0.f ? fwd[1] : 1.f, lv = fwd[0];
     const bool rl = a.relu[n - 1];
+    const float* P = sm + L.act[n - 1];
+    const int ldo = hl_ld(Do);
     for (int idx = threadIdx.x; idx < G * Do; idx += kHlThreads) {
       const int r = idx / Do, o = idx % Do;
-      const float p = AS[r * S + po + o];
+      const float p = P[r * ldo + o];
       float v = 0.f;
       if (mask == nullptr || mask[r]) {
         const float d = p - target[idx];
@@ -506,52 +583,64 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
         }
         v *= g;
       }
-      DY[r * md + o] = (rl && p <= 0.f) ? 0.f : v;
+      DY[r * ldy + o] = (rl && p <= 0.f) ? 0.f : v;
     }
   }
   __syncthreads();
   for (int l = n - 1; l >= 0; --l) {
     const int I = a.dims[l], O = a.dims[l + 1];
-    const float* ain = l == 0 ? XS : AS + a.aoff[l - 1];
-    const int lda = l == 0 ? L.ldx : S;
-    const float* Wl = WS + L.woff[l];
-    const int ldw = I + 1;
+    const float* ain = sm + (l == 0 ? L.x : L.act[l - 1]);
+    const int lda = hl_ld(I);
+    const float* W = sm + L.w[l];
     float* gl = grads + a.goff[l];
-    // dW[o, i] = sum_r dy[r, o] ain[r, i] (lanes over i: ain contiguous, dy broadcast); db[o]
-    for (int idx = threadIdx.x; idx < O * I + O; idx += kHlThreads) {
-      float a0 = 0.f, a1 = 0.f;
-      if (idx < O * I) {
-        const int o = idx / I, i = idx % I;
-        int r = 0;
-        for (; r + 2 <= G; r += 2) {
-          a0 = fmaf(DY[r * md + o], ain[r * lda + i], a0);
-          a1 = fmaf(DY[(r + 1) * md + o], ain[(r + 1) * lda + i], a1);
-        }
-        if (r < G) a0 = fmaf(DY[r * md + o], ain[r * lda + i], a0);
-      } else {
-        const int o = idx - O * I;
-        for (int r = 0; r < G; ++r) a0 += DY[r * md + o];
+    // dW = DY^T A_in: 16 x 16 (o, i) tiles, K = the rows (DY rows >= G are zero)
+    const int ti = hl_r16(I) / 16, to = hl_r16(O) / 16;
+    for (int t = wv; t < to * ti; t += kHlWaves) {
+      const int o0 = (t / ti) * 16, i0 = (t % ti) * 16;
+      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
+      const float* ap = DY + lg * ldy + o0 + li;
+      const float* bp = ain + lg * lda + i0 + li;
+      for (int k = 0; k < L.Gp / 4; ++k) acc = hl_mfma(ap[4 * k * ldy], bp[4 * k * lda], acc);
+      const int i = i0 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + 4 * lg + r;
+        if (o < O && i < I) gl[o * I + i] = acc[r];
       }
-      gl[idx] = a0 + a1;
     }
-    // da[r, i] = sum_o dy[r, o] W[o, i], masked by ReLU'(ain) for the previous layer
-    const bool msk = l > 0 && a.relu[l - 1];
-    for (int idx = threadIdx.x; idx < G * I; idx += kHlThreads) {
-      const int r = idx / I, i = idx % I;
+    // db[o] = sum_r dy[r, o]
+    for (int o = threadIdx.x; o < O; o += kHlThreads) {
       float a0 = 0.f, a1 = 0.f;
-      if (!msk || ain[r * lda + i] > 0.f) {
-        const float* dy = DY + r * md;
-        int o = 0;
-        for (; o + 2 <= O; o += 2) {
-          a0 = fmaf(dy[o], Wl[o * ldw + i], a0);
-          a1 = fmaf(dy[o + 1], Wl[(o + 1) * ldw + i], a1);
-        }
-        if (o < O) a0 = fmaf(dy[o], Wl[o * ldw + i], a0);
+      int r = 0;
+      for (; r + 2 <= G; r += 2) {
+        a0 += DY[r * ldy + o];
+        a1 += DY[(r + 1) * ldy + o];
       }
-      if (l == 0)
-        dx[idx] = a0 + a1;
-      else
-        DY2[r * md + i] = a0 + a1;
+      if (r < G) a0 += DY[r * ldy + o];
+      gl[O * I + o] = a0 + a1;
+    }
+    // da = DY W (K = O; DY columns >= O and W rows >= O are zero), masked by ReLU'(A_in)
+    const bool msk = l > 0 && a.relu[l - 1];
+    const int K4 = (O + 3) / 4;
+    for (int t = wv; t < (L.Gp / 16) * ti; t += kHlWaves) {
+      const int r0 = (t / ti) * 16, i0 = (t % ti) * 16;
+      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
+      const float* ap = DY + (r0 + li) * ldy + lg;
+      const float* bp = W + lg * lda + i0 + li;
+      for (int k = 0; k < K4; ++k) acc = hl_mfma(ap[4 * k], bp[4 * k * lda], acc);
+      const int col = i0 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 4 * lg + r;
+        float v = acc[r];
+        if (msk && !(ain[row * lda + col] > 0.f)) v = 0.f;
+        const bool live = row < G && col < I;
+        if (l == 0) {
+          if (live) dx[row * I + col] = v;
+        } else {
+          DY2[row * ldy + col] = live ? v : 0.f;
+        }
+      }
     }
     __syncthreads();
     float* t = DY;
@@ -560,7 +649,7 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
   }
 }
 
-static size_t hl_lds(const MlpArgs& a, int G) { return HlLds(a, G, host_max_width(a)).bytes(); }
+static size_t hl_lds(const MlpArgs& a, int G) { return sizeof(float) * (size_t)hl_layout(a, G).total; }
 
 static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::optional<at::Tensor>& mask,
                       const MlpArgs& a, int64_t kind) {
@@ -582,7 +671,7 @@ static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::
   (void)once;
 }
 
-// returns [stats [2] = (loss, kept count), pred [G, out]]
+// returns [stats [2] = (loss, kept count), pred [G, out], acts [G, sum of widths]]
 std::vector<at::Tensor> head_loss_fwd(const at::Tensor& x_, at::TensorList Ws_, at::TensorList bs_,
                                       at::IntArrayRef relu, const at::Tensor& target,
                                       const c10::optional<at::Tensor>& mask, int64_t kind) {
@@ -596,17 +685,19 @@ std::vector<at::Tensor> head_loss_fwd(const at::Tensor& x_, at::TensorList Ws_, 
   const int64_t G = x.size(0);
   auto stats = at::empty({2}, x.options());
   auto pred = at::empty({G, a.dims[a.n]}, x.options());
+  auto acts = at::empty({G, a.aoff[a.n]}, x.options());
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
   head_loss_fwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
       x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),
-      pred.data_ptr<float>());
-  return {stats, pred};
+      pred.data_ptr<float>(), acts.data_ptr<float>());
+  return {stats, pred, acts};
 }
 
 // returns [dx, dW_0, db_0, dW_1, db_1, ...]
-std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& x_, at::TensorList Ws_,
-                                      at::TensorList bs_, at::IntArrayRef relu, const at::Tensor& target,
-                                      const c10::optional<at::Tensor>& mask, const at::Tensor& stats, int64_t kind) {
+std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& x_, const at::Tensor& acts,
+                                      at::TensorList Ws_, at::TensorList bs_, at::IntArrayRef relu,
+                                      const at::Tensor& target, const c10::optional<at::Tensor>& mask,
+                                      const at::Tensor& stats, int64_t kind) {
   auto x = x_.contiguous();
   std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
   auto a = make_args(x, Ws, bs, relu.vec());
@@ -614,11 +705,13 @@ std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& 
   HY_CHECK(gout.numel() == 1 && gout.scalar_type() == at::kFloat && gout.is_contiguous() && stats.numel() == 2,
            "head_loss_bwd: scalar upstream gradient and the forward's stats");
   const int64_t G = x.size(0);
+  HY_CHECK(acts.is_contiguous() && acts.size(0) == G && acts.size(1) == a.aoff[a.n], "head_loss_bwd: acts shape");
   auto flat = at::empty({a.goff[a.n]}, x.options());
   auto dx = at::empty_like(x);
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
   head_loss_bwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
-      gout.data_ptr<float>(), x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind,
+      gout.data_ptr<float>(), x.data_ptr<float>(), acts.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp,
+      (int)kind,
       stats.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>());
   std::vector<at::Tensor> out{dx};
   for (int l = 0; l < a.n; ++l) {
@@ -640,8 +733,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "head_loss_fwd(Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, int kind) -> "
       "Tensor[]");
   m.def(
-      "head_loss_bwd(Tensor gout, Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, "
-      "Tensor stats, int kind) -> Tensor[]");
+      "head_loss_bwd(Tensor gout, Tensor x, Tensor acts, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, "
+      "Tensor? mask, Tensor stats, int kind) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

@@ -85,11 +85,14 @@ _KIND = {"mse": 0, "mae": 1, "rmse": 2, "smooth_l1": 3}
 
 
 def _hl_lds(G, dims):
-    """LDS footprint of ``csrc/mlp.hip`` head_loss kernels (HlLds)."""
-    w = sum((dims[i] + 1) * dims[i + 1] for i in range(len(dims) - 1))
-    md = max(dims) + 1
-    ldx = dims[0] + 1 + dims[0] % 2
-    return 4 * (w + G * ldx + G * (sum(dims[1:]) | 1) + 2 * G * md)
+    """LDS footprint of ``csrc/mlp.hip`` head_loss kernels (hl_layout): every matrix is
+    [rows padded to 16][cols padded to 16, + 1]."""
+    r16 = lambda v: (v + 15) // 16 * 16
+    ld = lambda c: r16(c) + 1
+    Gp = r16(G)
+    w = sum(r16(dims[i + 1]) * ld(dims[i]) for i in range(len(dims) - 1))
+    acts = sum(Gp * ld(d) for d in dims[1:])
+    return 4 * (w + Gp * ld(dims[0]) + acts + 2 * Gp * ld(max(dims)))
 
 
 def head_loss_layers(seqs, G, in_dim, kind):
@@ -113,8 +116,8 @@ class _HeadLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, target, mask, kind, relu, *params):
-        stats, pred = _native.ops().head_loss_fwd(x, params[0::2], params[1::2], relu, target, mask, kind)
-        ctx.save_for_backward(x, target, mask, stats, *params)
+        stats, pred, acts = _native.ops().head_loss_fwd(x, params[0::2], params[1::2], relu, target, mask, kind)
+        ctx.save_for_backward(x, acts, target, mask, stats, *params)
         ctx.kind, ctx.relu = kind, relu
         ctx.mark_non_differentiable(pred)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for pred
@@ -122,9 +125,9 @@ class _HeadLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _gpred):
-        x, target, mask, stats, *params = ctx.saved_tensors
-        out = _native.ops().head_loss_bwd(g.reshape(1).contiguous(), x, params[0::2], params[1::2], ctx.relu, target,
-                                          mask, stats, ctx.kind)
+        x, acts, target, mask, stats, *params = ctx.saved_tensors
+        out = _native.ops().head_loss_bwd(g.reshape(1).contiguous(), x, acts, params[0::2], params[1::2], ctx.relu,
+                                          target, mask, stats, ctx.kind)
         return (out[0], None, None, None, None, *out[1:])
 
 

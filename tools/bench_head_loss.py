@@ -1,0 +1,43 @@
+"""Micro-benchmark of the one-workgroup head+loss kernels (csrc/mlp.hip) against the
+multi-launch path (fused MLP + masked loss): per-call time for several row counts and
+chain shapes.  GPU only."""
+import torch
+
+from hydragnn_amd import _native
+from hydragnn_amd.ops import mlp as _mlp
+
+
+def bench(fn, it=200):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+def main():
+    dev = torch.device("cuda")
+    ops = _native.ops()
+    for G, dims in [(33, [64, 50, 50, 50, 25, 1]), (1, [64, 50, 50, 50, 25, 1]), (8, [64, 50, 50, 50, 25, 1]),
+                    (33, [64, 1]), (33, [64, 50, 1]), (33, [8, 8, 1])]:
+        Ws = [torch.randn(dims[i + 1], dims[i], device=dev) * 0.1 for i in range(len(dims) - 1)]
+        bs = [torch.randn(dims[i + 1], device=dev) * 0.1 for i in range(len(dims) - 1)]
+        relu = [1] * (len(dims) - 2) + [0]
+        x = torch.randn(G, dims[0], device=dev)
+        t = torch.randn(G, dims[-1], device=dev)
+        m = torch.ones(G, dtype=torch.bool, device=dev)
+        stats, pred, acts = ops.head_loss_fwd(x, Ws, bs, relu, t, m, 1)
+        g = torch.ones(1, device=dev)
+        tf = bench(lambda: ops.head_loss_fwd(x, Ws, bs, relu, t, m, 1))
+        tb = bench(lambda: ops.head_loss_bwd(g, x, acts, Ws, bs, relu, t, m, stats, 1))
+        to = bench(lambda: ops.mlp_fwd(x, Ws, bs, relu))
+        print(f"G {G:4d} dims {dims}: head_loss fwd {tf:7.1f} us  bwd {tb:7.1f} us   (mlp_fwd {to:6.1f} us)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
