@@ -101,12 +101,39 @@ def build(jobs=None, force=False, verbose=True):
     return OUT
 
 
+ASAN_OUT = os.path.join(PKG, "_C_host_asan.so")
+
+
+def build_asan(verbose=True):
+    """Sanitizer flavour of the HOST C++ sources (collate.cpp, shm_store.cpp): g++ with
+    -fsanitize=address,undefined into ``_C_host_asan.so``.  GPU code is never
+    sanitized (not available on this pool); load this library alone, in a process started
+    with ``LD_PRELOAD`` of the ASan/UBSan runtimes (tests/test_host_asan.py)."""
+    inc, lib, abi = _torch_paths()
+    srcs = sorted(glob.glob(os.path.join(HERE, "*.cpp")))
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", "-fsanitize=address,undefined",
+           "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           "-Wno-deprecated-declarations", f"-I{HERE}", f"-I{sysconfig.get_paths()['include']}"] + \
+        [f"-I{p}" for p in inc] + srcs + ["-o", ASAN_OUT, f"-L{lib}", "-ltorch", "-ltorch_cpu", "-lc10",
+                                           f"-Wl,-rpath,{lib}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[hydragnn_amd] built {ASAN_OUT} (host sources, ASan + UBSan)")
+    return ASAN_OUT
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="build the sanitized host-code library instead")
     a = ap.parse_args()
     try:
+        if a.asan:
+            build_asan()
+            sys.exit(0)
         build(a.j, a.force)
     except RuntimeError as e:
         print(e, file=sys.stderr)

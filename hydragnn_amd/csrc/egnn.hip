@@ -1,0 +1,526 @@
+// EGNN (E_GCL) edge / node kernels for the bf16 wide-layer path (SC25 EGNN-866,
+// reference hydragnn/models/EGCLStack.py:175-289).  The GEMMs run on the MFMA engine
+// (bgemm.hip); these kernels are the memory-bound pieces between them, each one pass:
+//
+//   gather_fwd : h1[e] = relu(AB[src_e, :H] + AB[dst_e, Hp:Hp+H] + |d_e| w_r + sum_j ea_ej w_j + b1)
+//                (the edge_mlp[0] Linear over cat[x_row, x_col, radial, edge_attr], with its
+//                x blocks evaluated at node level), edge geometry d_e = pos[dst]-pos[src],
+//                cd_e = d_e / (|d_e| + 1), and the bf16 per-edge scalar row [|d|, ea.., 1]
+//   agg_fwd    : agg[n] = sum_{e: src_e = n} m[e] (bf16 rows, fp32 sums) and the coordinate
+//                update pos'[n] = pos[n] + cw * mean_{e: src_e = n} clamp(cd_e tanh(s_e), +-100)
+//   coord_bwd  : d(pos') -> ds_e, dcd_e; dc1 = ds_e wc2 * relu'(c1) (bf16), dwc2 partials
+//   edge_bwd   : dAB (by-source and by-destination CSR sums of dh1, bf16), d|d_e|, the
+//                per-edge position gradient and the column partials of dw_r / dw_j / db1
+//   pos_bwd    : dpos[n] = dpos'[n] + sum_{dst_e = n} dvec_e - sum_{src_e = n} dvec_e
+//
+// One wave per edge row or node; each lane owns 4 consecutive channels (8-byte bf16 /
+// 16-byte fp32 accesses), looping over the padded width Hp in steps of 256.  Column
+// reductions over edges go to per-block partial rows reduced by bg_slab_reduce (no
+// atomics).  Edges are stored sorted by destination (dst CSR is the identity order);
+// the source CSR carries a permutation.
+#include "common.h"
+
+namespace hy {
+namespace eg {
+
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf2v v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float lo_bf(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float4 ld_bf4(const uint16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y));
+}
+__device__ __forceinline__ void st_bf4(uint16_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2(a, b), pack2(c, d));
+}
+
+constexpr int MAXS = 4;  // per-edge scalar features: |d| + up to 3 edge attributes
+
+struct GatherFwd {
+  const float* AB;  // [N, 2Hp]
+  const int* src;   // [E]
+  const int* dst;   // [E]
+  const float* pos; // [N, 3]
+  const float* ea;  // [E, nea] or null
+  const float* W0;  // edge_mlp[0].weight [H, ld0]; scalar columns at c0 .. c0 + nea
+  const float* b1;  // [H]
+  int ld0, c0, nea, H, Hp, E;
+  uint16_t* h1;     // [E, Hp] (ones lane at H)
+  float* geo;       // [E, 4]: cd.xyz, |d|
+  uint16_t* sc;     // [E, 128]: |d|, ea..., 1 at 1 + nea
+};
+
+__global__ __launch_bounds__(256) void gather_fwd_kernel(GatherFwd p) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (e >= p.E) return;
+  const int s = p.src[e], d = p.dst[e];
+  const float vx = p.pos[d * 3] - p.pos[s * 3], vy = p.pos[d * 3 + 1] - p.pos[s * 3 + 1],
+              vz = p.pos[d * 3 + 2] - p.pos[s * 3 + 2];
+  const float L = sqrtf(vx * vx + vy * vy + vz * vz);
+  float sv[MAXS] = {L, 0.f, 0.f, 0.f};
+  for (int j = 0; j < p.nea; ++j) sv[1 + j] = p.ea[(int64_t)e * p.nea + j];
+  if (lane == 0) {
+    const float inv = 1.f / (L + 1.f);
+    *reinterpret_cast<float4*>(p.geo + (int64_t)e * 4) = make_float4(vx * inv, vy * inv, vz * inv, L);
+  }
+  if (lane < 32) {  // scalar row: 4 bf16 per lane over 128 columns
+    float t[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = lane * 4 + r;
+      t[r] = c <= p.nea ? sv[c < MAXS ? c : 0] : (c == p.nea + 1 ? 1.f : 0.f);
+    }
+    st_bf4(p.sc + (int64_t)e * 128 + lane * 4, t[0], t[1], t[2], t[3]);
+  }
+  const float* ar = p.AB + (int64_t)s * 2 * p.Hp;
+  const float* br = p.AB + (int64_t)d * 2 * p.Hp + p.Hp;
+  uint16_t* out = p.h1 + (int64_t)e * p.Hp;
+  for (int k = lane * 4; k < p.Hp; k += 256) {
+    float v[4];
+    if (k + 3 < p.H) {
+      const float4 a = *reinterpret_cast<const float4*>(ar + k), b = *reinterpret_cast<const float4*>(br + k);
+      v[0] = a.x + b.x; v[1] = a.y + b.y; v[2] = a.z + b.z; v[3] = a.w + b.w;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (k + r < p.H) ? ar[k + r] + br[k + r] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kk = k + r;
+      if (kk < p.H) {
+        float z = v[r] + p.b1[kk];
+        const float* wrow = p.W0 + (int64_t)kk * p.ld0 + p.c0;
+        for (int j = 0; j <= p.nea; ++j) z += sv[j] * wrow[j];
+        v[r] = fmaxf(z, 0.f);
+      } else {
+        v[r] = kk == p.H ? 1.f : 0.f;
+      }
+    }
+    st_bf4(out + k, v[0], v[1], v[2], v[3]);
+  }
+}
+
+struct AggFwd {
+  const uint16_t* m;  // [E, Hp]
+  const int* srp;     // [N + 1] source CSR
+  const int* sperm;   // [E] (null: identity)
+  const float* pos;   // [N, 3]
+  const float* geo;   // [E, 4]
+  const float* s;     // [E] coord_mlp output (pre-tanh), null: no coordinate update
+  float cw;
+  int N, Hp;
+  uint16_t* agg;      // [N, Hp]
+  float* pos_out;     // [N, 3]
+};
+
+__global__ __launch_bounds__(256) void agg_fwd_kernel(AggFwd p) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= p.N) return;
+  const int b = p.srp[n], eN = p.srp[n + 1];
+  for (int k = lane * 4; k < p.Hp; k += 256) {
+    float4 acc = f4zero();
+    int i = b;
+    for (; i + 1 < eN; i += 2) {
+      const int e0 = p.sperm ? p.sperm[i] : i, e1 = p.sperm ? p.sperm[i + 1] : i + 1;
+      const float4 x0 = ld_bf4(p.m + (int64_t)e0 * p.Hp + k), x1 = ld_bf4(p.m + (int64_t)e1 * p.Hp + k);
+      acc = f4add(acc, f4add(x0, x1));
+    }
+    if (i < eN) acc = f4add(acc, ld_bf4(p.m + (int64_t)(p.sperm ? p.sperm[i] : i) * p.Hp + k));
+    st_bf4(p.agg + (int64_t)n * p.Hp + k, acc.x, acc.y, acc.z, acc.w);
+  }
+  if (p.s && lane < 3) {
+    float t = 0.f;
+    for (int i = b; i < eN; ++i) {
+      const int e = p.sperm ? p.sperm[i] : i;
+      const float u = p.geo[(int64_t)e * 4 + lane] * tanhf(p.s[e]);
+      t += fminf(fmaxf(u, -100.f), 100.f);
+    }
+    const int cnt = eN - b;
+    p.pos_out[n * 3 + lane] = p.pos[n * 3 + lane] + p.cw * t / (float)(cnt > 0 ? cnt : 1);
+  }
+}
+
+constexpr int EPB = 64;  // edges per block (16 per wave) for the column-partial kernels
+
+struct CoordBwd {
+  const float* dpos;  // [N, 3] gradient of pos'
+  const int* src;     // [E]
+  const int* srp;     // [N + 1]
+  const float* geo;   // [E, 4]
+  const float* s;     // [E]
+  const uint16_t* c1; // [E, Hp]
+  const float* wc2;   // [H]
+  float cw;
+  int E, H, Hp;
+  uint16_t* dc1;      // [E, Hp]
+  float* dcd;         // [E, 3]
+  float* part;        // [nblk, Hp]: sum_e ds_e c1[e]
+};
+
+__global__ __launch_bounds__(256) void coord_bwd_kernel(CoordBwd p) {
+  __shared__ float red[4][1024];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int e0 = blockIdx.x * EPB + w * (EPB / 4);
+  float pa[4][4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pa[it][r] = 0.f;
+  for (int i = 0; i < EPB / 4; ++i) {
+    const int e = e0 + i;
+    if (e >= p.E) break;
+    const int n = p.src[e];
+    const int cnt = p.srp[n + 1] - p.srp[n];
+    const float sc = p.cw / (float)(cnt > 0 ? cnt : 1);
+    const float4 g = *reinterpret_cast<const float4*>(p.geo + (int64_t)e * 4);
+    const float t = tanhf(p.s[e]);
+    const float cd[3] = {g.x, g.y, g.z};
+    float dt = 0.f, dcd[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float u = cd[c] * t;
+      const float dtr = (u >= -100.f && u <= 100.f) ? sc * p.dpos[n * 3 + c] : 0.f;
+      dt += dtr * cd[c];
+      dcd[c] = dtr * t;
+    }
+    const float ds = dt * (1.f - t * t);
+    if (lane < 3) p.dcd[(int64_t)e * 3 + lane] = dcd[lane];
+    const uint16_t* crow = p.c1 + (int64_t)e * p.Hp;
+    uint16_t* orow = p.dc1 + (int64_t)e * p.Hp;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 4 + it * 256;
+      if (k >= p.Hp) break;
+      const float4 c = ld_bf4(crow + k);
+      float o[4];
+      const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float wv = (k + r < p.H) ? p.wc2[k + r] : 0.f;
+        o[r] = cv[r] > 0.f ? ds * wv : 0.f;
+        pa[it][r] += ds * cv[r];
+      }
+      st_bf4(orow + k, o[0], o[1], o[2], o[3]);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int k = lane * 4 + it * 256;
+    if (k < 1024) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][k + r] = pa[it][r];
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < p.Hp; k += 256)
+    p.part[(int64_t)blockIdx.x * p.Hp + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+struct EdgeBwd {
+  const uint16_t* dh1;  // [E, Hp]
+  const int* srp;       // [N + 1] source CSR
+  const int* sperm;     // [E]
+  const int* drp;       // [N + 1] destination CSR (identity order)
+  const float* geo;     // [E, 4]
+  const float* dcd;     // [E, 3] or null
+  const float* W0;      // radial weight column at c0 (row stride ld0)
+  int ld0, c0, N, H, Hp;
+  uint16_t* dAB;        // [N, 2Hp]
+  float* dvec;          // [E, 3]
+};
+
+// one wave per node: by-source sum -> dAB[:, :Hp], by-destination sum -> dAB[:, Hp:], and
+// for each edge of the destination list its d|d| and position gradient.
+__global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwd p) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= p.N) return;
+  {
+    const int b = p.srp[n], eN = p.srp[n + 1];
+    for (int k = lane * 4; k < p.Hp; k += 256) {
+      float4 acc = f4zero();
+      for (int i = b; i < eN; ++i) {
+        const int e = p.sperm ? p.sperm[i] : i;
+        acc = f4add(acc, ld_bf4(p.dh1 + (int64_t)e * p.Hp + k));
+      }
+      st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + k, acc.x, acc.y, acc.z, acc.w);
+    }
+  }
+  const int b = p.drp[n], eN = p.drp[n + 1];
+  // radial weights of this lane's channels
+  float wr[4][4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = lane * 4 + it * 256 + r;
+      wr[it][r] = k < p.H ? p.W0[(int64_t)k * p.ld0 + p.c0] : 0.f;
+    }
+  float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+  for (int e = b; e < eN; ++e) {
+    const uint16_t* row = p.dh1 + (int64_t)e * p.Hp;
+    float dr = 0.f;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 4 + it * 256;
+      if (k < p.Hp) {
+        const float4 x = ld_bf4(row + k);
+        acc[it] = f4add(acc[it], x);
+        dr += x.x * wr[it][0] + x.y * wr[it][1] + x.z * wr[it][2] + x.w * wr[it][3];
+      }
+    }
+    dr = wave_sum(dr);
+    if (lane < 3) {
+      // d = pos[dst] - pos[src]; |d| = L; cd = d / (L + 1)
+      const float4 g = *reinterpret_cast<const float4*>(p.geo + (int64_t)e * 4);
+      const float L = g.w, s1 = L + 1.f;
+      const float dc[3] = {g.x * s1, g.y * s1, g.z * s1};  // the vector d
+      float gv = 0.f;
+      if (L > 0.f) {
+        gv = dr * dc[lane] / L;
+        if (p.dcd) {
+          const float q0 = p.dcd[(int64_t)e * 3], q1 = p.dcd[(int64_t)e * 3 + 1], q2 = p.dcd[(int64_t)e * 3 + 2];
+          const float dot = q0 * dc[0] + q1 * dc[1] + q2 * dc[2];
+          const float qc = lane == 0 ? q0 : (lane == 1 ? q1 : q2);
+          gv += qc / s1 - dc[lane] * dot / (L * s1 * s1);
+        }
+      }
+      p.dvec[(int64_t)e * 3 + lane] = gv;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int k = lane * 4 + it * 256;
+    if (k < p.Hp) st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + p.Hp + k, acc[it].x, acc[it].y, acc[it].z, acc[it].w);
+  }
+}
+
+__global__ void pos_bwd_kernel(const float* __restrict__ dpos_out, const float* __restrict__ dvec,
+                               const int* __restrict__ srp, const int* __restrict__ sperm, const int* __restrict__ drp,
+                               int N, float* __restrict__ dpos) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = t / 3, c = t % 3;
+  if (n >= N) return;
+  float v = dpos_out ? dpos_out[n * 3 + c] : 0.f;
+  for (int e = drp[n]; e < drp[n + 1]; ++e) v += dvec[(int64_t)e * 3 + c];
+  for (int i = srp[n]; i < srp[n + 1]; ++i) v -= dvec[(int64_t)(sperm ? sperm[i] : i) * 3 + c];
+  dpos[n * 3 + c] = v;
+}
+
+// out[e] = g[idx[e], :H] * (gate[e] > 0) as padded bf16 (the non-equivariant layer's
+// dZ2 = dagg[src] * relu'(m): no coordinate GEMM to carry the gather in its epilogue)
+__global__ __launch_bounds__(256) void gather_gate_kernel(const float* __restrict__ g, int ldg,
+                                                          const int* __restrict__ idx,
+                                                          const uint16_t* __restrict__ gate, int E, int H, int Hp,
+                                                          uint16_t* __restrict__ out) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (e >= E) return;
+  const float* row = g + (int64_t)idx[e] * ldg;
+  for (int k = lane * 4; k < Hp; k += 256) {
+    const float4 q = ld_bf4(gate + (int64_t)e * Hp + k);
+    const float qv[4] = {q.x, q.y, q.z, q.w};
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (k + r < H && qv[r] > 0.f) ? row[k + r] : 0.f;
+    st_bf4(out + (int64_t)e * Hp + k, v[0], v[1], v[2], v[3]);
+  }
+}
+
+}  // namespace eg
+
+using namespace eg;
+
+static const int* iptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<int>() : nullptr; }
+static const uint16_t* cbf(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+static uint16_t* wbf(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+static void chk_rows(const at::Tensor& t, int64_t rows, int64_t cols, at::ScalarType dt, const char* name) {
+  HY_CHECK(t.is_cuda() && t.scalar_type() == dt && t.is_contiguous() && t.dim() == 2 && t.size(0) == rows &&
+               t.size(1) == cols,
+           name, ": expected contiguous [", rows, ", ", cols, "]");
+}
+
+// returns nothing; writes h1, geo, sc
+void egnn_gather_fwd(const at::Tensor& AB, const at::Tensor& src, const at::Tensor& dst, const at::Tensor& pos,
+                     const c10::optional<at::Tensor>& ea, const at::Tensor& W0, int64_t c0, const at::Tensor& b1,
+                     const at::Tensor& h1, const at::Tensor& geo, const at::Tensor& sc) {
+  const int64_t E = src.numel(), N = pos.size(0), Hp = h1.size(1), H = b1.numel();
+  HY_CHECK(H < Hp && Hp % 256 != 1, "egnn_gather_fwd: H < Hp");
+  chk_rows(AB, N, 2 * Hp, at::kFloat, "AB");
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(dst);
+  HY_CHECK(dst.numel() == E, "egnn_gather_fwd: dst length");
+  chk_rows(pos, N, 3, at::kFloat, "pos");
+  chk_rows(h1, E, Hp, at::kBFloat16, "h1");
+  chk_rows(geo, E, 4, at::kFloat, "geo");
+  chk_rows(sc, E, 128, at::kBFloat16, "sc");
+  HY_CHECK(W0.scalar_type() == at::kFloat && W0.stride(1) == 1 && W0.size(0) == H, "egnn_gather_fwd: W0");
+  GatherFwd p{};
+  p.AB = AB.data_ptr<float>();
+  p.src = src.data_ptr<int>();
+  p.dst = dst.data_ptr<int>();
+  p.pos = pos.data_ptr<float>();
+  if (ea.has_value() && ea->numel()) {
+    HY_CHECK(ea->scalar_type() == at::kFloat && ea->is_contiguous() && ea->size(0) == E && ea->dim() == 2 &&
+                 ea->size(1) < MAXS,
+             "egnn_gather_fwd: edge attributes");
+    p.ea = ea->data_ptr<float>();
+    p.nea = (int)ea->size(1);
+  }
+  HY_CHECK(c0 + 1 + p.nea <= W0.size(1), "egnn_gather_fwd: W0 scalar columns");
+  p.W0 = W0.data_ptr<float>();
+  p.ld0 = (int)W0.stride(0);
+  p.c0 = (int)c0;
+  p.b1 = b1.data_ptr<float>();
+  p.H = (int)H;
+  p.Hp = (int)Hp;
+  p.E = (int)E;
+  p.h1 = wbf(h1);
+  p.geo = geo.data_ptr<float>();
+  p.sc = wbf(sc);
+  if (E) gather_fwd_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(p);
+}
+
+void egnn_agg_fwd(const at::Tensor& m, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
+                  const at::Tensor& pos, const at::Tensor& geo, const c10::optional<at::Tensor>& s, double cw,
+                  const at::Tensor& agg, const at::Tensor& pos_out) {
+  const int64_t N = pos.size(0), E = m.size(0), Hp = m.size(1);
+  chk_rows(m, E, Hp, at::kBFloat16, "m");
+  chk_rows(agg, N, Hp, at::kBFloat16, "agg");
+  chk_rows(pos, N, 3, at::kFloat, "pos");
+  chk_rows(pos_out, N, 3, at::kFloat, "pos_out");
+  chk_rows(geo, E, 4, at::kFloat, "geo");
+  HY_CHECK_I32(srp);
+  HY_CHECK(srp.numel() == N + 1, "egnn_agg_fwd: srp length");
+  AggFwd p{};
+  p.m = cbf(m);
+  p.srp = srp.data_ptr<int>();
+  p.sperm = iptr(sperm);
+  p.pos = pos.data_ptr<float>();
+  p.geo = geo.data_ptr<float>();
+  p.s = s.has_value() ? s->data_ptr<float>() : nullptr;
+  p.cw = (float)cw;
+  p.N = (int)N;
+  p.Hp = (int)Hp;
+  p.agg = wbf(agg);
+  p.pos_out = pos_out.data_ptr<float>();
+  if (N) agg_fwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(p);
+}
+
+// returns the number of partial rows written to part ([nblk, Hp])
+int64_t egnn_coord_bwd(const at::Tensor& dpos, const at::Tensor& src, const at::Tensor& srp, const at::Tensor& geo,
+                       const at::Tensor& s, const at::Tensor& c1, const at::Tensor& wc2, double cw, const at::Tensor& dc1,
+                       const at::Tensor& dcd, const at::Tensor& part) {
+  const int64_t E = c1.size(0), Hp = c1.size(1), H = wc2.numel(), N = dpos.size(0);
+  HY_CHECK(Hp <= 1024, "egnn_coord_bwd: Hp <= 1024");
+  chk_rows(dpos, N, 3, at::kFloat, "dpos");
+  chk_rows(geo, E, 4, at::kFloat, "geo");
+  chk_rows(dc1, E, Hp, at::kBFloat16, "dc1");
+  chk_rows(dcd, E, 3, at::kFloat, "dcd");
+  HY_CHECK(s.numel() == E && src.numel() == E && srp.numel() == N + 1, "egnn_coord_bwd: lengths");
+  const int64_t nblk = (E + EPB - 1) / EPB;
+  HY_CHECK(part.scalar_type() == at::kFloat && part.numel() >= nblk * Hp, "egnn_coord_bwd: part");
+  CoordBwd p{};
+  p.dpos = dpos.data_ptr<float>();
+  p.src = src.data_ptr<int>();
+  p.srp = srp.data_ptr<int>();
+  p.geo = geo.data_ptr<float>();
+  p.s = s.data_ptr<float>();
+  p.c1 = cbf(c1);
+  p.wc2 = wc2.data_ptr<float>();
+  p.cw = (float)cw;
+  p.E = (int)E;
+  p.H = (int)H;
+  p.Hp = (int)Hp;
+  p.dc1 = wbf(dc1);
+  p.dcd = dcd.data_ptr<float>();
+  p.part = part.data_ptr<float>();
+  if (E) coord_bwd_kernel<<<(int)nblk, 256, 0, stream()>>>(p);
+  return nblk;
+}
+
+void egnn_edge_bwd(const at::Tensor& dh1, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
+                   const at::Tensor& drp, const at::Tensor& geo, const c10::optional<at::Tensor>& dcd,
+                   const at::Tensor& W0, int64_t c0, int64_t H, const at::Tensor& dAB, const at::Tensor& dvec) {
+  const int64_t E = dh1.size(0), Hp = dh1.size(1), N = srp.numel() - 1;
+  HY_CHECK(Hp <= 1024 && H < Hp, "egnn_edge_bwd: H < Hp <= 1024");
+  chk_rows(dh1, E, Hp, at::kBFloat16, "dh1");
+  chk_rows(dAB, N, 2 * Hp, at::kBFloat16, "dAB");
+  chk_rows(dvec, E, 3, at::kFloat, "dvec");
+  chk_rows(geo, E, 4, at::kFloat, "geo");
+  HY_CHECK(drp.numel() == N + 1, "egnn_edge_bwd: drp length");
+  HY_CHECK(W0.scalar_type() == at::kFloat && W0.stride(1) == 1 && W0.size(0) == H && c0 < W0.size(1),
+           "egnn_edge_bwd: W0");
+  EdgeBwd p{};
+  p.dh1 = cbf(dh1);
+  p.srp = srp.data_ptr<int>();
+  p.sperm = iptr(sperm);
+  p.drp = drp.data_ptr<int>();
+  p.geo = geo.data_ptr<float>();
+  p.dcd = dcd.has_value() ? dcd->data_ptr<float>() : nullptr;
+  p.W0 = W0.data_ptr<float>();
+  p.ld0 = (int)W0.stride(0);
+  p.c0 = (int)c0;
+  p.N = (int)N;
+  p.H = (int)H;
+  p.Hp = (int)Hp;
+  p.dAB = wbf(dAB);
+  p.dvec = dvec.data_ptr<float>();
+  if (N) edge_bwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(p);
+}
+
+void egnn_pos_bwd(const c10::optional<at::Tensor>& dpos_out, const at::Tensor& dvec, const at::Tensor& srp,
+                  const c10::optional<at::Tensor>& sperm, const at::Tensor& drp, const at::Tensor& dpos) {
+  const int64_t N = srp.numel() - 1;
+  chk_rows(dpos, N, 3, at::kFloat, "dpos");
+  if (dpos_out.has_value()) chk_rows(*dpos_out, N, 3, at::kFloat, "dpos_out");
+  if (N)
+    pos_bwd_kernel<<<ceil_div(N * 3, 256), 256, 0, stream()>>>(
+        dpos_out.has_value() ? dpos_out->data_ptr<float>() : nullptr, dvec.data_ptr<float>(), srp.data_ptr<int>(),
+        iptr(sperm), drp.data_ptr<int>(), (int)N, dpos.data_ptr<float>());
+}
+
+void egnn_gather_gate(const at::Tensor& g, const at::Tensor& idx, const at::Tensor& gate, int64_t H,
+                      const at::Tensor& out) {
+  const int64_t E = gate.size(0), Hp = gate.size(1);
+  chk_rows(gate, E, Hp, at::kBFloat16, "gate");
+  chk_rows(out, E, Hp, at::kBFloat16, "out");
+  HY_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(1) >= H, "egnn_gather_gate: g");
+  HY_CHECK_I32(idx);
+  HY_CHECK(idx.numel() == E, "egnn_gather_gate: idx length");
+  if (E)
+    gather_gate_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(g.data_ptr<float>(), (int)g.stride(0),
+                                                             idx.data_ptr<int>(), cbf(gate), (int)E, (int)H, (int)Hp,
+                                                             wbf(out));
+}
+
+}  // namespace hy
+
+TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def(
+      "egnn_gather_fwd(Tensor AB, Tensor src, Tensor dst, Tensor pos, Tensor? ea, Tensor W0, int c0, Tensor b1, "
+      "Tensor h1, Tensor geo, Tensor sc) -> ()");
+  m.def(
+      "egnn_agg_fwd(Tensor m, Tensor srp, Tensor? sperm, Tensor pos, Tensor geo, Tensor? s, float cw, Tensor agg, "
+      "Tensor pos_out) -> ()");
+  m.def(
+      "egnn_coord_bwd(Tensor dpos, Tensor src, Tensor srp, Tensor geo, Tensor s, Tensor c1, Tensor wc2, float cw, "
+      "Tensor dc1, Tensor dcd, Tensor part) -> int");
+  m.def(
+      "egnn_edge_bwd(Tensor dh1, Tensor srp, Tensor? sperm, Tensor drp, Tensor geo, Tensor? dcd, Tensor W0, int c0, "
+      "int H, Tensor dAB, Tensor dvec) -> ()");
+  m.def("egnn_gather_gate(Tensor g, Tensor idx, Tensor gate, int H, Tensor out) -> ()");
+  m.def("egnn_pos_bwd(Tensor? dpos_out, Tensor dvec, Tensor srp, Tensor? sperm, Tensor drp, Tensor dpos) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("egnn_gather_fwd", hy::egnn_gather_fwd);
+  m.impl("egnn_agg_fwd", hy::egnn_agg_fwd);
+  m.impl("egnn_coord_bwd", hy::egnn_coord_bwd);
+  m.impl("egnn_edge_bwd", hy::egnn_edge_bwd);
+  m.impl("egnn_pos_bwd", hy::egnn_pos_bwd);
+  m.impl("egnn_gather_gate", hy::egnn_gather_gate);
+}

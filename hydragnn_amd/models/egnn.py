@@ -167,6 +167,19 @@ class EGCLStack(Base):
     def _conv_head_kwargs(self):
         return {"last_layer": False, "edge_dim": self.edge_embed_dim}
 
+    def _fused_encode(self, inv, equiv, ctx):
+        # bf16 precision on the GPU: the whole wide E_GCL stack on the MFMA engine
+        # (ops/egnn_wide.py over csrc/bgemm.hip + csrc/egnn.hip)
+        from ..ops import egnn_wide
+
+        if self.training is not None and egnn_wide.eligible(self, ctx):
+            x, pos = egnn_wide.encode(self, ctx)
+            keep = ctx.data.get("node_mask")
+            if keep is not None:
+                x = x * keep.view(-1, 1).to(x.dtype)
+            return x, pos, ctx
+        return None
+
     def _embedding(self, data):
         x, pos, ctx = super()._embedding(data)
         if not self.use_global_attn and not self.edge_dim:

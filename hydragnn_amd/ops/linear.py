@@ -1,17 +1,15 @@
-"""Linear layers on the MFMA GEMM engine (``csrc/gemm.hip``).
+"""Linear layers: library / fused-engine fp32 paths and the bf16 MFMA engine.
 
-Forward: ``Y = act(sum_p X_p W_p^T + b) (+ residual)`` — one launch, the
-concat-linear blocks ``X_p`` never concatenated, bias / ReLU / residual in the
-epilogue.  Backward: ONE launch producing every ``dX_p``, every ``dW_p`` and
-``db`` (split-K weight gradients reduced inside the launch), with the ReLU
-derivative applied while staging ``dY``.  Compare the library path it
-replaces: GEMM + bias/act elementwise kernels forward, and dgrad GEMM +
-wgrad-partial + partial-sum (+ act-backward) backward — 4-6 launches per layer.
+``linear_act`` computes ``act(sum_p X_p W_p^T + b) (+ residual)``.
 
 Precision (``set_precision`` / ``Training.precision``):
-* ``"fp32"`` (default; the reference's numerics): v_mfma_f32_16x16x4_f32, exact fp32;
-* ``"bf16"``: v_mfma_f32_16x16x32_bf16 — operands rounded to bf16 as they are
-  staged into LDS, fp32 accumulation, fp32 storage and master weights.
+* ``"fp32"`` (default; the reference's numerics): library GEMM forward + data gradient,
+  split-K weight-gradient kernel (csrc/linear.hip, deferred + grouped inside the training
+  engine's backward), and the one-launch concat-linear forward of csrc/gemm.hip
+  (v_mfma_f32_16x16x4_f32, exact fp32) for node-sized multi-input sums;
+* ``"bf16"``: single-input maps above ``BF16_MIN_MACS`` run on the bf16 MFMA engine
+  (csrc/bgemm.hip via ``ops.bgemm.BF16Linear``): operands rounded to bf16, fp32
+  accumulation, fp32 storage and master weights.  Narrow or small maps stay fp32.
 
 CPU tensors, non-fp32 dtypes and composite mode (double backward for force
 training) use ``F.linear``.
@@ -55,36 +53,6 @@ class precision:
 
 def _row_contig(t):
     return t if (t.stride(-1) == 1 or t.shape[-1] == 1) else t.contiguous()
-
-
-class _MM(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, act, prec, b, residual, *xw):
-        xs, ws = list(xw[0::2]), list(xw[1::2])
-        y = _native.ops().mm_fwd(xs, ws, b, residual, act, prec)
-        ctx.act, ctx.prec = act, prec
-        ctx.has_b, ctx.has_res = b is not None, residual is not None
-        ctx.n = len(xs)
-        ctx.save_for_backward(*xs, *ws, *( [y] if act == ACT_RELU else []))
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        t = ctx.saved_tensors
-        n = ctx.n
-        xs, ws = list(t[:n]), list(t[n:2 * n])
-        y = t[2 * n] if ctx.act == ACT_RELU else None
-        need_dx = [int(ctx.needs_input_grad[4 + 2 * j]) for j in range(n)]
-        need_dw = any(ctx.needs_input_grad[5 + 2 * j] for j in range(n))
-        want_b = ctx.has_b and ctx.needs_input_grad[2]
-        outs = _native.ops().mm_bwd(dy.contiguous() if y is not None else _row_contig(dy), y, xs, ws, need_dx, need_dw, want_b, ctx.prec)
-        dxs, dws, db = outs[:n], outs[n:2 * n], outs[2 * n]
-        grads = []
-        for j in range(n):
-            grads.append(dxs[j] if need_dx[j] else None)
-            grads.append(dws[j] if ctx.needs_input_grad[5 + 2 * j] else None)
-        dres = dy if ctx.has_res and ctx.needs_input_grad[3] else None
-        return (None, None, db if want_b else None, dres, *grads)
 
 
 # ---- deferred weight gradients -------------------------------------------------------
@@ -273,7 +241,6 @@ class _EngineSumF32(_TallLinearSum):
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
 BF16_MIN_MACS = int(os.environ.get("HYDRA_BF16_MIN_MACS", str(1 << 26)))
 ENGINE_SUM_MAX_ROWS = 8192  # fp32 multi-input sums above this use the library GEMM pair
-BIG_GEMM = int(os.environ.get("HYDRA_BF16_LIBRARY_MIN", str(1 << 30)))  # M*N*K above which bf16 maps use the library
 
 
 def _engine_ok(tensors):
@@ -284,7 +251,8 @@ def _engine_ok(tensors):
 def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     """``act(sum_k x_k @ W_k^T + b) (+ residual)`` for 1-3 (x_k, W_k) pairs.
 
-    bf16 precision: the MFMA engine for forward and backward.  fp32: measured on MI355X
+    bf16 precision: single-input maps above BF16_MIN_MACS run on the bf16 MFMA engine
+    (csrc/bgemm.hip, ``ops.bgemm.BF16Linear``).  fp32: measured on MI355X
     (tools/bench_mm.py, profiles/r2_bench_mm.log) the library GEMM is faster for the
     plain single-input forward and the dgrad of these shapes, and the engine's in-launch
     split-K reduction loses to a separate reduce launch whenever the grid has more than a
@@ -303,23 +271,14 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     # more accurate of the two, so small maps stay fp32 in bf16 mode
     bf16 = _state["prec"] == 1 and \
         sum(x.shape[0] * w.shape[0] * w.shape[1] for x, w in zip(xs, ws)) >= BF16_MIN_MACS
-    if engine and bf16 and len(pairs) == 1 and residual is None and \
-            xs[0].shape[0] * ws[0].shape[0] * ws[0].shape[1] >= BIG_GEMM:
-        # big dense maps (e.g. the SC25 EGNN's 866-wide edge/node MLPs): the library's tuned
-        # 256x256-tile bf16 MFMA GEMMs (hipBLASLt), bf16 in / fp32 accumulate, fp32 out
-        y = F.linear(xs[0].to(torch.bfloat16), ws[0].to(torch.bfloat16),
-                     None if b is None else b.to(torch.bfloat16)).float()
-        return torch.relu(y) if act == ACT_RELU else y
-    if engine and bf16 and min(min(w.shape) for w in ws) < 16:
-        # very narrow maps (EGNN coord_mlp's 866 -> 1, the 1 -> 866 edge-attribute term): the
-        # engine's 32x32 tiles waste >90% of the MFMA work and write the [E, 866] side tile by
-        # tile (~600 us per call measured for 36k rows); these are bandwidth-bound, fp32 library
-        engine = False
-    if engine and bf16:
-        flat = []
-        for x, w in zip(xs, ws):
-            flat += [_row_contig(x), _row_contig(w)]
-        return _MM.apply(act, _state["prec"], b, None if residual is None else _row_contig(residual), *flat)
+    if engine and bf16 and len(pairs) == 1 and residual is None and min(ws[0].shape) >= 16:
+        # wide maps (the SC25 EGNN decoder heads, 866 -> 889 -> ...): the bf16 MFMA engine
+        # of csrc/bgemm.hip (padded bf16 operands, fp32 accumulate, fused bias/ReLU,
+        # split-row weight gradient with the bias gradient from the ones lane)
+        from . import bgemm
+
+        return bgemm.bf16_linear(xs[0], ws[0], b, act)
+    # narrow maps (e.g. an 866 -> 1 projection) and multi-input sums stay on the fp32 path
     tall = engine and xs[0].shape[0] >= MIN_ROWS and torch.is_grad_enabled() and \
         any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
     if len(pairs) == 1:

@@ -1,0 +1,109 @@
+"""bf16 MFMA GEMM engine (csrc/bgemm.hip) against plain-torch fp32 references computed on
+the same bf16-rounded operands."""
+import pytest
+import torch
+
+from hydragnn_amd.ops import bgemm as bg
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def _rb(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, tol=2e-2):
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= tol * ref, f"max err {err} vs ref scale {ref}"
+
+
+@pytest.mark.parametrize("M", [1, 200, 1000, 4097, 20000])
+@pytest.mark.parametrize("bm", [64, 128, 256, 1064, 1128, 1256])
+def test_nt_plain(M, bm):
+    torch.manual_seed(0)
+    K, Np, N = 192, 256, 250
+    A, B = _rb(M, K), _rb(Np, K, scale=0.1)
+    bias = torch.randn(N, device=dev)
+    outf = torch.empty(M, N, device=dev)
+    outb = torch.empty(M, Np, device=dev, dtype=torch.bfloat16)
+    bg.nt(A, B, K, N, bias=bias, act=1, outf=outf, outb=outb, ones_col=N, bm=bm)
+    ref = torch.relu(A.float() @ B.float()[:N].T + bias)
+    _close(outf, ref, 1e-3)
+    _close(outb[:, :N].float(), ref)
+    assert (outb[:, N].float() == 1).all() and (outb[:, N + 1:].float() == 0).all()
+
+
+def test_nt_epilogues():
+    torch.manual_seed(1)
+    M, K1, K2, Np, N, R = 3000, 128, 192, 384, 300, 700
+    A, A2, B = _rb(M, K1), _rb(M, K2), _rb(Np, K1 + K2, scale=0.1)
+    gate = _rb(M, Np)
+    addg = torch.randn(R, N + 4, device=dev)
+    idx = torch.randint(0, R, (M,), device=dev, dtype=torch.int32)
+    rowvec = torch.randn(N, device=dev)
+    rowdot = torch.zeros(M, device=dev)
+    outf = torch.randn(M, N, device=dev)
+    prev = outf.clone()
+    bg.nt(A, B, K1 + K2, N, A2=A2, k1=K1, gate=gate, addg=addg, addg_idx=idx, outf=outf, beta=1.0, rowvec=rowvec,
+          rowdot=rowdot)
+    z = torch.cat([A, A2], 1).float() @ B.float()[:N].T + addg[idx.long(), :N]
+    z = z * (gate[:, :N].float() > 0)
+    _close(outf - prev, z, 1e-3)
+    _close(rowdot, z @ rowvec, 1e-3)
+
+
+@pytest.mark.parametrize("M", [64, 1000, 35000])
+def test_tn_reduce(M):
+    torch.manual_seed(2)
+    Np, K1, K2 = 256, 128, 256
+    G, X, X2 = _rb(M, Np), _rb(M, K1), _rb(M, K2)
+    N, K = 250, K1 + 200
+    out = torch.randn(N, K, device=dev)
+    prev = out.clone()
+    bias = torch.randn(N, device=dev)
+    bprev = bias.clone()
+    bg.wgrad(G, X, Np, K1 + K2, [(out, 0, bias, 5)], X2=X2, kc1=K1, beta=1.0)
+    full = G.float().T @ torch.cat([X, X2], 1).float()
+    _close(out - prev, full[:N, :K], 1e-3)
+    _close(bias - bprev, full[:N, 5], 1e-3)
+
+
+def test_cast_weights_and_pad():
+    torch.manual_seed(3)
+    W = torch.randn(866, 889, device=dev)
+    (wb, wt), = bg.weight_images([W])
+    assert wb.shape == (896, 896) and wt.shape == (896, 896)
+    assert torch.equal(wb[:866, :889], W.to(torch.bfloat16))
+    assert torch.equal(wt[:889, :866], W.T.to(torch.bfloat16))
+    assert (wb[866:].float() == 0).all() and (wb[:, 889:].float() == 0).all()
+    x = torch.randn(100, 866, device=dev)
+    g = _rb(100, 896)
+    xb = bg.cast_pad(x, 896, gate=g)
+    ref = x * (g[:, :866].float() > 0)
+    assert torch.equal(xb[:, :866], ref.to(torch.bfloat16))
+    assert (xb[:, 866].float() == 1).all() and (xb[:, 867:].float() == 0).all()
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_bf16_linear_grad(act):
+    torch.manual_seed(4)
+    M, K, N = 5000, 866, 889
+    x = torch.randn(M, K, device=dev, requires_grad=True)
+    W = (torch.randn(N, K, device=dev) * 0.03).requires_grad_()
+    b = torch.randn(N, device=dev, requires_grad=True)
+    y = bg.bf16_linear(x, W, b, act)
+    gy = torch.randn(M, N, device=dev)
+    y.backward(gy)
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_()
+    Wr = W.detach().to(torch.bfloat16).float().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    yr = xr @ Wr.T + br
+    if act == 1:
+        yr = torch.relu(yr)
+    yr.backward(gy)
+    _close(y, yr, 1e-3)
+    _close(x.grad, xr.grad, 2e-2)
+    _close(W.grad, Wr.grad, 2e-2)
+    _close(b.grad, br.grad, 2e-2)

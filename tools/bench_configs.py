@@ -148,11 +148,18 @@ def run(name, steps, warmup, dev):
                 step(draw())
             torch.cuda.synchronize()
         print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=45), flush=True)
+    mark = os.environ.get("HYDRA_PROFILE_MARK") == "1"
+    if mark:  # spin kernels bracket the timed steps: rocpd_summary.py --between spin_kernel
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = step(draw())
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if mark:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     nodes = float(np.mean([s.num_nodes for s in samples]))
     return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
             "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
