@@ -84,6 +84,11 @@ struct NTArgs {
   const float* rowvec; // rowdot[m] += sum_n act(v)[m, n] * rowvec[n]
   float* rowdot;
   int tiles_n;
+  // branch-grouped mode (multi-branch heads): row m uses weight image B + bid[m] * bsB and
+  // bias + bid[m] * bsbias; bid is non-decreasing (rows sorted by branch)
+  const int* bid;
+  int64_t bsB;
+  int bsbias;
 };
 
 constexpr int BN = 128, BK = 64;
@@ -92,20 +97,21 @@ __device__ __forceinline__ int a_off(int row, int c) { return row * 128 + ((c ^ 
 
 // acc[i][j][r] = C[m = mb + i*16 + fr][n = nb + j*16 + 4*fg + r]
 template <int NJ>
-__device__ __forceinline__ void nt_epilogue(const NTArgs& p, f4v (&acc)[4][NJ], int mb, int nb, int fr, int fg) {
+__device__ __forceinline__ void nt_epilogue(const NTArgs& p, f4v (&acc)[4][NJ], int mb, int nb, int fr, int fg,
+                                            const float* bias, int br) {
   const bool fvec = (p.ldf & 3) == 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = mb + i * 16 + fr;
-    const bool mv = m < p.M;
+    const bool mv = m < p.M && (br < 0 || p.bid[m] == br);
     float rd = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int n = nb + j * 16 + 4 * fg;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias) {
+      if (bias) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (n + r < p.N) ? p.bias[n + r] : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] += (n + r < p.N) ? bias[n + r] : 0.f;
       }
       if (p.addg && mv) {
         const int src = p.addg_idx ? p.addg_idx[m] : m;
@@ -183,6 +189,13 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (wg / p.tiles_n) * BM, n0 = (wg % p.tiles_n) * BN;
   const int KT = p.K / BK;
+  // branch range of this row tile (rows sorted by branch): one pass per branch present
+  int br0 = -1, br1 = -1;
+  if (p.bid) {
+    br0 = p.bid[m0];
+    br1 = p.bid[min(m0 + BM, p.M) - 1];
+  }
+  const uint16_t* Bw = p.B;
 
   uint4 ra[ACH], rb[BCH];
   auto load = [&](int kt) {
@@ -199,7 +212,7 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       const int i = tid + j * NTH, row = i >> 3, c = i & 7;
-      rb[j] = *reinterpret_cast<const uint4*>(p.B + (int64_t)(n0 + row) * p.ldb + kt * BK + c * 8);
+      rb[j] = *reinterpret_cast<const uint4*>(Bw + (int64_t)(n0 + row) * p.ldb + kt * BK + c * 8);
     }
   };
   auto store = [&](int buf) {
@@ -216,6 +229,9 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
     }
   };
 
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int br = br0; br <= br1; ++br) {
+  Bw = p.bid ? p.B + (int64_t)br * p.bsB : p.B;
   f4v acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -225,7 +241,6 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
   load(0);
   store(0);
   __syncthreads();
-  const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) load(kt + 1);
@@ -248,7 +263,9 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
     __syncthreads();
   }
 
-  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg);
+  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg,
+                  p.bias ? p.bias + (p.bid ? (int64_t)br * p.bsbias : 0) : nullptr, br);
+  }
 }
 
 // glds variant: A and B tiles copied global -> LDS by global_load_lds (16 bytes per lane,
@@ -336,7 +353,7 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
-  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg);
+  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg, p.bias, -1);
 }
 
 // ------------------------------------------------------------------------------ TN GEMM
@@ -346,7 +363,9 @@ struct TNArgs {
   const uint16_t* X2;  // [M, ldx2]: output cols k >= kc1 (k - kc1), may be null
   int ldg, ldx, ldx2, kc1;
   int M, Np, Kp, rows_per_split, tiles_k, tiles_nk;
-  float* slab;         // [S][Np][Kp]
+  float* slab;         // [S][Np][Kp]  ([nb][S][Np][Kp] when grouped)
+  const int* boff;     // branch row offsets [nb + 1] (grouped: per-branch G^T X), or null
+  int splits;
 };
 
 __device__ __forceinline__ int t_off(int m, int c16) {
@@ -368,8 +387,15 @@ __global__ __launch_bounds__(256) void tn_kernel(TNArgs p) {
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int split = wg / p.tiles_nk, t = wg % p.tiles_nk;
   const int n0 = (t / p.tiles_k) * 128, k0 = (t % p.tiles_k) * 128;
-  const int r0 = split * p.rows_per_split;
-  const int r1 = min(p.M, r0 + p.rows_per_split);
+  int r0 = split * p.rows_per_split;
+  int r1 = min(p.M, r0 + p.rows_per_split);
+  if (p.boff) {  // split index = branch * splits + s over that branch's rows
+    const int br = split / p.splits, sp = split % p.splits;
+    const int b0 = p.boff[br], b1 = p.boff[br + 1];
+    const int chunk = ((b1 - b0 + p.splits - 1) / p.splits + 63) / 64 * 64;
+    r0 = b0 + sp * chunk;
+    r1 = min(b1, r0 + chunk);
+  }
   const int KT = (r1 - r0 + 63) / 64;
   const uint16_t* Xs;
   int ldx, kk;
@@ -561,7 +587,7 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
            const c10::optional<at::Tensor>& addg, const c10::optional<at::Tensor>& addg_idx,
            const c10::optional<at::Tensor>& outf, double beta, const c10::optional<at::Tensor>& outb,
            int64_t ones_col, const c10::optional<at::Tensor>& rowvec, const c10::optional<at::Tensor>& rowdot,
-           int64_t bm_) {
+           int64_t bm_, const c10::optional<at::Tensor>& bid, int64_t bsB, int64_t bsbias) {
   // bm_ = tile rows (64 / 128 / 256) + 1000 for the glds-staged variant
   const bool glds = bm_ >= 1000;
   const int64_t bm = bm_ % 1000;
@@ -631,6 +657,13 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
     p.rowvec = rowvec->data_ptr<float>();
     p.rowdot = rowdot->data_ptr<float>();
   }
+  if (bid.has_value()) {
+    HY_CHECK_I32(*bid);
+    HY_CHECK(bid->numel() >= M && !glds, "bg_nt: grouped mode needs bid [M] (register-staged kernel)");
+    p.bid = bid->data_ptr<int>();
+    p.bsB = bsB;
+    p.bsbias = (int)bsbias;
+  }
   if (M == 0) return;
   p.tiles_n = (int)(Np / 128);
   if (glds) {
@@ -651,7 +684,7 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
 
 // slab[S][Np][Kp] = split-M partial sums of G^T [X | X2]
 void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Tensor>& X2, int64_t kc1,
-           int64_t Np, int64_t Kp, const at::Tensor& slab, int64_t splits) {
+           int64_t Np, int64_t Kp, const at::Tensor& slab, int64_t splits, const c10::optional<at::Tensor>& boff) {
   check_bf(G, "G");
   check_bf(X, "X");
   const int64_t M = G.size(0);
@@ -671,7 +704,14 @@ void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Ten
   } else {
     HY_CHECK(kc1 == Kp && X.size(1) >= Kp, "bg_tn: X narrower than Kp");
   }
-  HY_CHECK(slab.scalar_type() == at::kFloat && slab.is_contiguous() && slab.numel() >= splits * Np * Kp,
+  int64_t groups = 1;
+  if (boff.has_value()) {
+    HY_CHECK_I32(*boff);
+    groups = boff->numel() - 1;
+    p.boff = boff->data_ptr<int>();
+  }
+  p.splits = (int)splits;
+  HY_CHECK(slab.scalar_type() == at::kFloat && slab.is_contiguous() && slab.numel() >= groups * splits * Np * Kp,
            "bg_tn: slab");
   p.M = (int)M;
   p.Np = (int)Np;
@@ -680,7 +720,7 @@ void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Ten
   p.tiles_k = (int)(Kp / 128);
   p.tiles_nk = (int)((Np / 128) * p.tiles_k);
   p.slab = slab.data_ptr<float>();
-  const int grid = (int)(p.tiles_nk * splits);
+  const int grid = (int)(p.tiles_nk * splits * groups);
   tn_kernel<<<grid, 256, 0, stream()>>>(p);
 }
 
@@ -776,8 +816,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "bg_nt(Tensor A, Tensor? A2, int k1, Tensor B, int K, int N, Tensor? bias, int act, Tensor? gate, Tensor? addg, "
       "Tensor? addg_idx, Tensor? outf, float beta, Tensor? outb, int ones_col, Tensor? rowvec, Tensor? rowdot, "
-      "int bm) -> ()");
-  m.def("bg_tn(Tensor G, Tensor X, Tensor? X2, int kc1, int Np, int Kp, Tensor slab, int splits) -> ()");
+      "int bm, Tensor? bid=None, int bsB=0, int bsbias=0) -> ()");
+  m.def("bg_tn(Tensor G, Tensor X, Tensor? X2, int kc1, int Np, int Kp, Tensor slab, int splits, Tensor? boff=None) -> ()");
   m.def(
       "bg_slab_reduce(Tensor slab, int S, int Np, int Kp, int n0, int k0, int N, int K, Tensor out, float beta, int bias_col, "
       "Tensor? bias_out) -> ()");

@@ -101,7 +101,7 @@ def build(jobs=None, force=False, verbose=True):
     return OUT
 
 
-ASAN_OUT = os.path.join(PKG, "_C_host_asan.so")
+ASAN_OUT = os.path.join(BUILD, "_C_host_asan.so")  # build dir: host-only, never shipped to the GPU box
 
 
 def build_asan(verbose=True):
@@ -110,6 +110,7 @@ def build_asan(verbose=True):
     sanitized (not available on this pool); load this library alone, in a process started
     with ``LD_PRELOAD`` of the ASan/UBSan runtimes (tests/test_host_asan.py)."""
     inc, lib, abi = _torch_paths()
+    os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(HERE, "*.cpp")))
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", "-fsanitize=address,undefined",
            "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",

@@ -94,6 +94,134 @@ __global__ void __launch_bounds__(256) tp_uvu_bwd_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- fused convolution
+// MACE message + aggregation in one pass (reference blocks.py:354-387):
+//   out[n] = sum_{e: dst_e = n} TP(x1[src_e], Y_e, w_e)
+// one wave per destination node (edges are destination-sorted: the node's edges are
+// one contiguous range), lanes over channels; neither the gathered [E, ld1] operand nor
+// the [E, out] message tensor exists.  Backward: d x1 by a source-CSR pass (one wave
+// per source node, atomic-free), dY / dw by an edge pass reading go[dst_e].
+__global__ void __launch_bounds__(256) tp_conv_fwd_kernel(const float* __restrict__ x1, int ld1,
+                                                          const float* __restrict__ y, int ld2,
+                                                          const float* __restrict__ w, int ldw,
+                                                          const int* __restrict__ ins, int nins,
+                                                          const float* __restrict__ cg, const int* __restrict__ src,
+                                                          const int* __restrict__ drp, float* __restrict__ out,
+                                                          int ldo, int N) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int e0 = drp[n], e1 = drp[n + 1];
+  for (int t = 0; t < nins; ++t) {
+    const int* r = ins + t * kInsCols;
+    const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const float* C = cg + r[8];
+    for (int u = lane; u < m; u += 64) {
+      float acc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int e = e0; e < e1; ++e) {
+        const float* a = x1 + (int64_t)src[e] * ld1 + r[4] + u * d1;
+        const float* yb = y + (int64_t)e * ld2 + r[5];
+        const float wu = w[(int64_t)e * ldw + r[6] + u];
+        float av[7], yv[7];
+        for (int i = 0; i < d1; ++i) av[i] = a[i];
+        for (int j = 0; j < d2; ++j) yv[j] = yb[j];
+        for (int k = 0; k < d3; ++k) {
+          float s = 0.f;
+          for (int i = 0; i < d1; ++i)
+            for (int j = 0; j < d2; ++j) s = fmaf(C[(i * d2 + j) * d3 + k] * av[i], yv[j], s);
+          acc[k] = fmaf(wu, s, acc[k]);
+        }
+      }
+      float* o = out + (int64_t)n * ldo + r[7] + u * d3;
+      for (int k = 0; k < d3; ++k) o[k] = acc[k];
+    }
+  }
+}
+
+// gx1[j] = sum_{e: src_e = j} w_e * C^T(go[dst_e], Y_e)   (gx1 zero-initialised)
+__global__ void __launch_bounds__(256) tp_conv_bwd_x_kernel(const float* __restrict__ go, int ldo,
+                                                            const float* __restrict__ y, int ld2,
+                                                            const float* __restrict__ w, int ldw,
+                                                            const int* __restrict__ ins, int nins,
+                                                            const float* __restrict__ cg,
+                                                            const int* __restrict__ dst, const int* __restrict__ srp,
+                                                            const int* __restrict__ sperm, float* __restrict__ gx1,
+                                                            int ld1, int N) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int b = srp[n], eN = srp[n + 1];
+  for (int t = 0; t < nins; ++t) {
+    const int* r = ins + t * kInsCols;
+    const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const float* C = cg + r[8];
+    for (int u = lane; u < m; u += 64) {
+      float ga[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int q = b; q < eN; ++q) {
+        const int e = sperm ? sperm[q] : q;
+        const float* g = go + (int64_t)dst[e] * ldo + r[7] + u * d3;
+        const float* yb = y + (int64_t)e * ld2 + r[5];
+        const float wu = w[(int64_t)e * ldw + r[6] + u];
+        float gv[7];
+        for (int k = 0; k < d3; ++k) gv[k] = g[k];
+        for (int i = 0; i < d1; ++i) {
+          float acc = 0.f;
+          for (int j = 0; j < d2; ++j) {
+            float s = 0.f;
+            for (int k = 0; k < d3; ++k) s = fmaf(C[(i * d2 + j) * d3 + k], gv[k], s);
+            acc = fmaf(s, yb[j], acc);
+          }
+          ga[i] = fmaf(wu, acc, ga[i]);
+        }
+      }
+      float* o = gx1 + (int64_t)n * ld1 + r[4] + u * d1;
+      for (int i = 0; i < d1; ++i) o[i] += ga[i];
+    }
+  }
+}
+
+// per edge: gw[e] and gy[e] (gy zero-initialised) from x1[src_e] and go[dst_e]
+__global__ void __launch_bounds__(256) tp_conv_bwd_e_kernel(const float* __restrict__ go, int ldo,
+                                                            const float* __restrict__ x1, int ld1,
+                                                            const float* __restrict__ y, int ld2,
+                                                            const float* __restrict__ w, int ldw,
+                                                            const int* __restrict__ ins, int nins,
+                                                            const float* __restrict__ cg, const int* __restrict__ src,
+                                                            const int* __restrict__ dst, float* __restrict__ gy,
+                                                            float* __restrict__ gw, int64_t E) {
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= E) return;
+  const int sn = src[e], dn = dst[e];
+  for (int t = 0; t < nins; ++t) {
+    const int* r = ins + t * kInsCols;
+    const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const float* yb = y + e * ld2 + r[5];
+    const float* C = cg + r[8];
+    float gyl[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int u = lane; u < m; u += 64) {
+      const float* a = x1 + (int64_t)sn * ld1 + r[4] + u * d1;
+      const float* g = go + (int64_t)dn * ldo + r[7] + u * d3;
+      const float wu = w[e * ldw + r[6] + u];
+      float gwu = 0.f;
+      for (int i = 0; i < d1; ++i) {
+        const float ai = a[i];
+        for (int j = 0; j < d2; ++j) {
+          float s = 0.f;
+          for (int k = 0; k < d3; ++k) s = fmaf(C[(i * d2 + j) * d3 + k], g[k], s);
+          gwu = fmaf(s * ai, yb[j], gwu);
+          gyl[j] = fmaf(wu * ai, s, gyl[j]);
+        }
+      }
+      gw[e * ldw + r[6] + u] = gwu;
+    }
+    for (int j = 0; j < d2; ++j) {
+      const float v = wave_sum(gyl[j]);
+      if (lane == 0) gy[e * ld2 + r[5] + j] += v;
+    }
+  }
+}
+
 static void check_ins(const at::Tensor& ins, const at::Tensor& cg) {
   HY_CHECK(ins.device().is_cuda() && ins.scalar_type() == at::kInt && ins.dim() == 2 && ins.size(1) == kInsCols,
            "tp_uvu: instruction table must be int32 [n, 9] on the GPU");
@@ -134,14 +262,66 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> tp_uvu_bwd(const at::Tensor& go_,
   return {gx1, gy, gw};
 }
 
+at::Tensor tp_conv_fwd(const at::Tensor& x1, const at::Tensor& y, const at::Tensor& w, const at::Tensor& ins,
+                       const at::Tensor& cg, const at::Tensor& src, const at::Tensor& drp, int64_t out_dim) {
+  HY_CHECK(x1.is_cuda() && x1.is_contiguous() && y.is_contiguous() && w.is_contiguous(), "tp_conv: contiguous");
+  HY_CHECK_F32(x1);
+  HY_CHECK_F32(y);
+  HY_CHECK_F32(w);
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(drp);
+  check_ins(ins, cg);
+  const int64_t N = drp.numel() - 1, E = y.size(0);
+  HY_CHECK(x1.size(0) == N && w.size(0) == E && src.numel() == E, "tp_conv: shapes");
+  auto out = at::empty({N, out_dim}, x1.options());
+  if (N == 0) return out;
+  tp_conv_fwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(
+      x1.data_ptr<float>(), (int)x1.size(1), y.data_ptr<float>(), (int)y.size(1), w.data_ptr<float>(),
+      (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0), cg.data_ptr<float>(), src.data_ptr<int>(),
+      drp.data_ptr<int>(), out.data_ptr<float>(), (int)out_dim, (int)N);
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> tp_conv_bwd(const at::Tensor& go_, const at::Tensor& x1,
+                                                           const at::Tensor& y, const at::Tensor& w,
+                                                           const at::Tensor& ins, const at::Tensor& cg,
+                                                           const at::Tensor& src, const at::Tensor& dst,
+                                                           const at::Tensor& srp,
+                                                           const c10::optional<at::Tensor>& sperm) {
+  auto go = go_.contiguous();
+  check_ins(ins, cg);
+  const int64_t N = x1.size(0), E = y.size(0);
+  HY_CHECK(srp.numel() == N + 1 && dst.numel() == E && go.size(0) == N, "tp_conv_bwd: shapes");
+  auto gx1 = at::zeros_like(x1), gy = at::zeros_like(y), gw = at::empty_like(w);
+  if (N)
+    tp_conv_bwd_x_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(
+        go.data_ptr<float>(), (int)go.size(1), y.data_ptr<float>(), (int)y.size(1), w.data_ptr<float>(),
+        (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0), cg.data_ptr<float>(), dst.data_ptr<int>(),
+        srp.data_ptr<int>(), sperm.has_value() ? sperm->data_ptr<int>() : nullptr, gx1.data_ptr<float>(),
+        (int)x1.size(1), (int)N);
+  if (E)
+    tp_conv_bwd_e_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(
+        go.data_ptr<float>(), (int)go.size(1), x1.data_ptr<float>(), (int)x1.size(1), y.data_ptr<float>(),
+        (int)y.size(1), w.data_ptr<float>(), (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0),
+        cg.data_ptr<float>(), src.data_ptr<int>(), dst.data_ptr<int>(), gy.data_ptr<float>(), gw.data_ptr<float>(),
+        E);
+  return {gx1, gy, gw};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("tp_conv_fwd(Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, Tensor src, Tensor drp, int out_dim) -> Tensor");
+  m.def(
+      "tp_conv_bwd(Tensor go, Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, Tensor src, Tensor dst, Tensor srp, "
+      "Tensor? sperm) -> (Tensor, Tensor, Tensor)");
   m.def("tp_uvu_fwd(Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, int out_dim) -> Tensor");
   m.def("tp_uvu_bwd(Tensor go, Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("tp_uvu_fwd", hy::tp_uvu_fwd);
+  m.impl("tp_conv_fwd", hy::tp_conv_fwd);
+  m.impl("tp_conv_bwd", hy::tp_conv_bwd);
   m.impl("tp_uvu_bwd", hy::tp_uvu_bwd);
 }

@@ -253,8 +253,10 @@ class DeviceGraphStore:
         edge_index, batch_l, ptr_l, nmask, gmask = outs[nn_ + ne + ng:]
         return fields, targets, edge_index, batch_l, ptr_l, nmask, gmask
 
-    def assemble(self, dev_buf, lay, host_ids=None):
-        """Build a GraphBatch from a packed device plan (device ops only; graph-capturable)."""
+    def assemble(self, dev_buf, lay, host_ids=None, branch_sorted=False):
+        """Build a GraphBatch from a packed device plan (device ops only; graph-capturable).
+        ``branch_sorted``: the sample indices were ordered by ``branch_order`` (graphs, and so
+        nodes, grouped by branch id, padding last): enables branch-grouped decoding."""
         if dev_buf.is_cuda and self.dataset_name is None:
             views = []
             o = 0
@@ -281,9 +283,9 @@ class DeviceGraphStore:
                 s["graph_mask"] = gmask
                 s["node_mask"] = nmask
             return b
-        return self._assemble_torch(dev_buf, lay, host_ids)
+        return self._assemble_torch(dev_buf, lay, host_ids, branch_sorted)
 
-    def _assemble_torch(self, dev_buf, lay, host_ids=None):
+    def _assemble_torch(self, dev_buf, lay, host_ids=None, branch_sorted=False):
         """Plain-torch assembly: the CPU path, multi-branch batches, and the oracle of the
         native kernel's tests."""
         views = []
@@ -360,6 +362,7 @@ class DeviceGraphStore:
             if lay.padded:
                 dn = torch.where(gmask, dn, torch.full_like(dn, -1))
             s["dataset_name"] = dn.view(-1, 1)
+            s["branch_sorted"] = bool(branch_sorted)
             if host_ids is not None:
                 s["dataset_ids_host"] = host_ids
         return b
@@ -392,7 +395,7 @@ class DeviceGraphStore:
             ranges = (gr, nr)
         lay = self.layout(indices, Np, Ep, Gp)
         dev = self.upload(indices, lay)
-        b = self.assemble(dev, lay, host_ids)
+        b = self.assemble(dev, lay, host_ids, branch_sorted=True)
         if ranges is not None:
             b._store["branch_graph_ranges"], b._store["branch_node_ranges"] = ranges
         return b

@@ -70,12 +70,35 @@ def _legendre(lmax, t):
     return p
 
 
+class _TripletSBF(torch.autograd.Function):
+    """Triplet angle + spherical basis in one HIP pass each way (csrc/dimenet.hip):
+    sbf[t] from vec[e_ji], vec[e_kj]; backward returns d vec (analytic)."""
+
+    @staticmethod
+    def forward(ctx, vec, kj, ji, layer):
+        from .. import _native
+
+        ctx.save_for_backward(vec, kj, ji)
+        ctx.layer = layer
+        return _native.ops().dimenet_sbf_fwd(vec, kj, ji, layer.zeros, layer.norm, layer.cutoff, layer.exponent)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        vec, kj, ji = ctx.saved_tensors
+        L = ctx.layer
+        dvec = _native.ops().dimenet_sbf_bwd(g.contiguous(), vec, kj, ji, L.zeros, L.norm, L.cutoff, L.exponent)
+        return dvec, None, None, None
+
+
 class SphericalBasisLayer(nn.Module):
     def __init__(self, num_spherical, num_radial, cutoff=5.0, envelope_exponent=5):
         super().__init__()
         assert num_radial <= 64
         self.num_spherical, self.num_radial = num_spherical, num_radial
         self.cutoff = float(cutoff)
+        self.exponent = int(envelope_exponent)
         self.envelope = Envelope(envelope_exponent)
         z = bessel_zeros(num_spherical, num_radial)
         norm = np.zeros_like(z)
@@ -97,6 +120,16 @@ class SphericalBasisLayer(nn.Module):
         P = _legendre(n - 1, t)
         cbf = torch.stack([math.sqrt((2 * l + 1) / (4 * math.pi)) * P[l] for l in range(n)], 1).to(dist.dtype)
         return (seg.gather(rbf.reshape(-1, n * k), idx_kj).view(-1, n, k) * cbf.view(-1, n, 1)).reshape(-1, n * k)
+
+    def native_ok(self, vec):
+        from ..ops.pna import fused
+
+        return vec.is_cuda and vec.dtype == torch.float32 and fused("sbf") and self.num_spherical <= 8 and \
+            self.num_radial <= 8
+
+    def from_vectors(self, vec, kj_si, ji_si):
+        """sbf directly from edge vectors (the GPU path: angle + basis in one kernel)."""
+        return _TripletSBF.apply(vec.contiguous(), kj_si.index, ji_si.index, self)
 
 
 # ----------------------------------------------------------------------------- triplets
@@ -285,13 +318,16 @@ class DIMEStack(Base):
         ctx.kj_si = seg.SegIndex.from_index(idx_kj, E, sorted_=False)
         ctx.ji_si = seg.SegIndex.from_index(idx_ji, E, sorted_=True)
         vec, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
+        d = dist.view(-1)
+        ctx.rbf = self.rbf(d)
+        if self.sbf.native_ok(vec):
+            ctx.sbf = self.sbf.from_vectors(vec, ctx.kj_si, ctx.ji_si)
+            return x, pos, ctx
         pos_ji = seg.gather(vec, ctx.ji_si)
         pos_ki = seg.gather(vec, ctx.kj_si) + pos_ji
         a = (pos_ji * pos_ki).sum(-1)
         b = torch.linalg.cross(pos_ji, pos_ki).norm(dim=-1)
         angle = torch.atan2(b, a)
-        d = dist.view(-1)
-        ctx.rbf = self.rbf(d)
         ctx.sbf = self.sbf(d, angle, ctx.kj_si)
         return x, pos, ctx
 

@@ -151,8 +151,8 @@ class InteractionBlock(nn.Module):
         up = self.linear_up(h)
         down = self.linear_down(h)
         w = self.conv_tp_weights(torch.cat([edge_feats, seg.gather(down, src_si), seg.gather(down, dst_si)], -1))
-        mji = self.conv_tp(seg.gather(up, src_si), edge_attrs, w)
-        msg = self.linear(seg.segment_sum(mji, dst_si)) / self.avg_num_neighbors
+        # gather -> uvu tensor product -> segment sum, fused on the GPU (one launch each way)
+        msg = self.linear(self.conv_tp.conv(up, edge_attrs, w, src_si, dst_si)) / self.avg_num_neighbors
         return _to_channels(msg, self.target_irreps), sc
 
 

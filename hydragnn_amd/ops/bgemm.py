@@ -156,3 +156,133 @@ class BF16Linear(torch.autograd.Function):
 
 def bf16_linear(x, W, b=None, act=0):
     return BF16Linear.apply(x, W, b, act)
+
+
+# ---------------------------------------------------------------- branch-grouped heads
+def _chain_layers(seq):
+    """[(Linear, relu_after)] of a Sequential made of Linear (+bias) and ReLU, else None."""
+    out = []
+    for m in seq:
+        if isinstance(m, torch.nn.Linear) and m.bias is not None:
+            out.append([m, False])
+        elif isinstance(m, torch.nn.ReLU) and out and not out[-1][1]:
+            out[-1][1] = True
+        else:
+            return None
+    return out
+
+
+def branch_offsets(bid, nb):
+    """Row offsets [nb + 1] (int32, on the device, no host sync) of rows sorted by branch."""
+    cnt = (bid.view(-1, 1) == torch.arange(nb, device=bid.device, dtype=bid.dtype).view(1, -1)).sum(0)
+    return torch.cat([torch.zeros(1, device=bid.device, dtype=torch.int64), torch.cumsum(cnt, 0)]).to(torch.int32)
+
+
+class _BranchMLP(torch.autograd.Function):
+    """Per-branch MLP chains over rows sorted by branch: every layer is ONE grouped NT GEMM
+    (each row tile runs against its branch's weight image; a tile straddling a branch
+    boundary runs once per branch present) and its weight gradients ONE grouped TN GEMM
+    over each branch's own rows.  Replaces the captured step's dense decode (every branch
+    head on every row, then a per-row select)."""
+
+    @staticmethod
+    def forward(ctx, x, bid, boff, dims, relu, nb, *params):
+        M = x.shape[0]
+        L = len(dims) - 1
+        dev = x.device
+        kps = [pad128(d) for d in dims]  # padded width of each layer's input / output
+        imgs, imgTs, biases = [], [], []
+        srcs, d, dt = [], [], []
+        for l in range(L):
+            img = torch.empty((nb, kps[l + 1], kps[l]), device=dev, dtype=torch.bfloat16)
+            imgT = torch.empty((nb, kps[l], kps[l + 1]), device=dev, dtype=torch.bfloat16)
+            for b in range(nb):
+                srcs.append(params[(l * 2) * nb + b])
+                d.append(img[b])
+                dt.append(imgT[b])
+            imgs.append(img)
+            imgTs.append(imgT)
+            biases.append(torch.stack([params[(l * 2 + 1) * nb + b] for b in range(nb)]).contiguous())
+        _native.ops().bg_cast_weights(srcs, d, dt)
+        h = cast_pad(x, kps[0])
+        hs = [h]
+        out = None
+        for l in range(L):
+            last = l == L - 1
+            Np = kps[l + 1]
+            if last:
+                out = torch.empty((M, dims[-1]), device=dev, dtype=torch.float32)
+                _native.ops().bg_nt(h, None, kps[l], imgs[l][0], kps[l], dims[l + 1], biases[l], int(relu[l]), None,
+                                    None, None, out, 0.0, None, -1, None, None, 128, bid, imgs[l][0].numel(),
+                                    dims[l + 1])
+            else:
+                hn = torch.empty((M, Np), device=dev, dtype=torch.bfloat16)
+                _native.ops().bg_nt(h, None, kps[l], imgs[l][0], kps[l], dims[l + 1], biases[l], int(relu[l]), None,
+                                    None, None, None, 0.0, hn, dims[l + 1], None, None, 128, bid, imgs[l][0].numel(),
+                                    dims[l + 1])
+                h = hn
+                hs.append(h)
+        ctx.save_for_backward(bid, boff, *hs)
+        ctx.imgTs, ctx.dims, ctx.relu, ctx.nb, ctx.kps = imgTs, dims, relu, nb, kps
+        ctx.shapes = [tuple(p.shape) for p in params]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        bid, boff, *hs = ctx.saved_tensors
+        dims, relu, nb, kps, imgTs = ctx.dims, ctx.relu, ctx.nb, ctx.kps, ctx.imgTs
+        L = len(dims) - 1
+        M = dout.shape[0]
+        dev = dout.device
+        grads = [None] * (2 * L * nb)
+        # gradient at the last pre-activation
+        g = cast_pad(dout, kps[L], gate=None, ones=False) if not relu[L - 1] else None
+        if g is None:
+            raise NotImplementedError("branch MLP ending in an activation")
+        dx = None
+        S = splits_for(max(1, M // nb), (kps[L] // 128) * (kps[L - 1] // 128))
+        for l in range(L - 1, -1, -1):
+            Np, Kp = kps[l + 1], kps[l]
+            slab = _slab(dev, nb * S * Np * Kp)
+            _native.ops().bg_tn(g, hs[l], None, Kp, Np, Kp, slab, S, boff)
+            for b in range(nb):
+                dW = torch.empty((dims[l + 1], dims[l]), device=dev, dtype=torch.float32)
+                db = torch.empty(dims[l + 1], device=dev, dtype=torch.float32)
+                _native.ops().bg_slab_reduce(slab[b * S * Np * Kp:], S, Np, Kp, 0, 0, dims[l + 1], dims[l], dW, 0.0,
+                                             dims[l], db)
+                grads[(l * 2) * nb + b] = dW
+                grads[(l * 2 + 1) * nb + b] = db
+            if l > 0:
+                gn = torch.empty((M, Kp), device=dev, dtype=torch.bfloat16)
+                _native.ops().bg_nt(g, None, Np, imgTs[l][0], Np, dims[l], None, 0, hs[l] if relu[l - 1] else None,
+                                    None, None, None, 0.0, gn, -1, None, None, 128, bid, imgTs[l][0].numel(), 0)
+                g = gn
+            elif ctx.needs_input_grad[0]:
+                dx = torch.empty((M, dims[0]), device=dev, dtype=torch.float32)
+                _native.ops().bg_nt(g, None, Np, imgTs[0][0], Np, dims[0], None, 0, None, None, None, dx, 0.0, None,
+                                    -1, None, None, 128, bid, imgTs[0][0].numel(), 0)
+        ctx.imgTs = None
+        return (dx, None, None, None, None, None, *grads)
+
+
+def branch_mlp(x, seqs, bid, boff):
+    """Rows of ``x`` (sorted by branch id ``bid``, int32, values in [0, len(seqs))) through
+    their branch's Linear/ReLU chain ``seqs[bid]``; None when the chains do not qualify."""
+    chains = [_chain_layers(s) for s in seqs]
+    if any(c is None for c in chains) or len({len(c) for c in chains}) != 1:
+        return None
+    c0 = chains[0]
+    dims = [x.shape[1]] + [m.out_features for m, _ in c0]
+    relu = [r for _, r in c0]
+    for c in chains:
+        if [m.out_features for m, _ in c] != dims[1:] or [r for _, r in c] != relu or \
+                c[0][0].in_features != dims[0]:
+            return None
+    if relu[-1] or min(dims[1:]) < 1:
+        return None
+    nb = len(seqs)
+    params = []
+    for l in range(len(c0)):
+        params += [chains[b][l][0].weight for b in range(nb)]
+        params += [chains[b][l][0].bias for b in range(nb)]
+    return _BranchMLP.apply(x, bid, boff, dims, relu, nb, *params)

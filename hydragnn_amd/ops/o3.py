@@ -349,6 +349,29 @@ class _TPUVU(torch.autograd.Function):
         return g1, g2, gw, None, None, None
 
 
+class _TPConv(torch.autograd.Function):
+    """Fused MACE convolution: out[n] = sum_{e: dst_e = n} TP(x1[src_e], Y_e, w_e)
+    (csrc/equivariant.hip tp_conv_*; first-order autograd)."""
+
+    @staticmethod
+    def forward(ctx, x1, y, w, ins, cg, out_dim, src_si, dst_si):
+        from .. import _native
+
+        ctx.save_for_backward(x1, y, w, ins, cg)
+        ctx.si = (src_si, dst_si)
+        return _native.ops().tp_conv_fwd(x1, y, w, ins, cg, src_si.index, dst_si.rowptr, out_dim)
+
+    @staticmethod
+    def backward(ctx, go):
+        from .. import _native
+
+        x1, y, w, ins, cg = ctx.saved_tensors
+        src_si, dst_si = ctx.si
+        g1, gy, gw = _native.ops().tp_conv_bwd(go, x1, y, w, ins, cg, src_si.index, dst_si.index, src_si.rowptr,
+                                               src_si.perm)
+        return g1, gy, gw, None, None, None, None, None
+
+
 class TensorProductUVU(nn.Module):
     """Channel-wise ("uvu") tensor product with per-edge external weights:
     out[e, u, m3] (block k) = sqrt(2 l3 + 1) sum_v w[e, k, u, v] sum_{m1 m2} C[m1 m2 m3] x1[e, u, m1] x2[e, v, m2]."""
@@ -389,6 +412,18 @@ class TensorProductUVU(nn.Module):
         if x1.is_cuda and self.native_ok and x1.dtype == torch.float32 and _mode.fused("tp"):
             return _TPUVU.apply(x1, x2, w, self._ins, self._cg, self.irreps_out.dim)
         return self.forward_reference(x1, x2, w)
+
+    def conv(self, x1_nodes, x2, w, src_si, dst_si):
+        """sum over each destination's edges of TP(x1_nodes[src], x2, w) (MACE message +
+        aggregation): one fused kernel on the GPU, gather / TP / segment-sum otherwise."""
+        from . import pna as _mode
+        from . import segment as seg
+
+        if x1_nodes.is_cuda and self.native_ok and x1_nodes.dtype == torch.float32 and _mode.fused("tp") and \
+                dst_si.perm is None:
+            return _TPConv.apply(x1_nodes.contiguous(), x2.contiguous(), w.contiguous(), self._ins, self._cg,
+                                 self.irreps_out.dim, src_si, dst_si)
+        return seg.segment_sum(self(seg.gather(x1_nodes, src_si), x2, w), dst_si)
 
     def forward_reference(self, x1, x2, w):
         E = x1.shape[0]

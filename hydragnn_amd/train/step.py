@@ -357,7 +357,7 @@ class TrainStep:
 
     def _body_fwd_bwd(self, store, cap, sync=True):
         self._zero()
-        batch = store.assemble(cap.dev_plan, cap.lay)
+        batch = store.assemble(cap.dev_plan, cap.lay, branch_sorted=store.dataset_name is not None)
         loss, tasks = self._loss(batch)
         self._backward(loss, sync=sync)
         self._set_guard(loss)
@@ -496,6 +496,9 @@ class TrainStep:
 
     def __call__(self, store, indices):
         if self.mode == "graph":
+            if store.dataset_name is not None:
+                # graphs grouped by branch (padding last): branch-grouped head GEMMs
+                indices = store.branch_order(indices)[0]
             if self.device.type == "cuda":
                 return self.graph_step(store, indices)
             return self.padded_step(store, indices)

@@ -323,6 +323,39 @@ def test_tp_uvu_native_matches_reference(lmax_node, lmax_sh):
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("lmax_node,lmax_sh", [(1, 2), (2, 3)])
+def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh):
+    """Fused MACE convolution (gather x1[src] -> uvu TP -> segment sum by dst, one launch
+    each way) == segment_sum(TP(gather)) reference, values and all three gradients."""
+    from hydragnn_amd.ops import o3
+    from hydragnn_amd.ops import segment as seg
+
+    torch.manual_seed(7 + lmax_node)
+    ir1 = o3.Irreps.natural(32, lmax_node)
+    ir2 = o3.Irreps.sh(lmax_sh)
+    out_ir, ins = o3.tp_uvu_instructions(ir1, ir2, o3.Irreps.natural(1, 3))
+    tp = o3.TensorProductUVU(ir1, ir2, out_ir, ins).to(DEV)
+    N, E = 90, 700
+    src = torch.randint(0, N, (E,))
+    dst = torch.sort(torch.randint(0, N, (E,))).values
+    src_si = seg.SegIndex.from_index(src.to(DEV), N, sorted_=False)
+    dst_si = seg.SegIndex.from_index(dst.to(DEV), N, sorted_=True)
+    x1 = torch.randn(N, ir1.dim, device=DEV, requires_grad=True)
+    y = torch.randn(E, ir2.dim, device=DEV, requires_grad=True)
+    w = torch.randn(E, tp.weight_numel, device=DEV, requires_grad=True)
+    out = tp.conv(x1, y, w, src_si, dst_si)
+    xr, yr, wr = [t.detach().double().cpu().requires_grad_() for t in (x1, y, w)]
+    tp64 = o3.TensorProductUVU(ir1, ir2, out_ir, ins).double()
+    ref = torch.zeros(N, out.shape[1], dtype=torch.float64).index_add_(
+        0, dst, tp64.forward_reference(xr[src], yr, wr))
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(ref)
+    out.backward(g.float().to(DEV))
+    ref.backward(g)
+    for a, b in zip((x1, y, w), (xr, yr, wr)):
+        torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("G,dims,relus", [(33, [64, 50, 50, 50, 25, 1], [1, 1, 1, 1, 0]),
                                           (203, [7, 128, 3], [1, 0]), (1, [16, 8], [1])])
 def test_fused_mlp_chain(G, dims, relus):
