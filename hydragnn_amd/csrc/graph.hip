@@ -465,6 +465,98 @@ std::tuple<at::Tensor, at::Tensor> triplets(const at::Tensor& edge_index, const 
   return {kj, ji};
 }
 
+
+// ------------------------------------------------------------------ static-capacity radius graph
+// Capturable in-forward radius graph (SchNet rebuilds its interaction graph inside forward,
+// reference SCFStack.py:121-134 / 175-190): no host synchronisation, fixed output shapes.
+// Valid receivers i (node_mask) take the first `cap` sources j of their own graph (index
+// order, torch_cluster semantics) with |p_i - p_j| <= r, j != i.  Edges are written
+// receiver-sorted at rowptr[i] (a device exclusive scan of the counts); slots
+// [rowptr[N], E_cap) become self-edges of the `dummy` (padding) node, so every segment
+// op of the padded batch runs over static shapes and padding never reaches a valid node.
+__global__ void rs_count_kernel(const float* __restrict__ pos, const int64_t* __restrict__ node_graph,
+                                const int64_t* __restrict__ gptr, const bool* __restrict__ mask, int N, float r2,
+                                int cap, int* __restrict__ counts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  int c = 0;
+  if (!mask || mask[i]) {
+    const int64_t g = node_graph[i];
+    const float xi = pos[3 * i], yi = pos[3 * i + 1], zi = pos[3 * i + 2];
+    for (int64_t j = gptr[g]; j < gptr[g + 1] && c < cap; ++j) {
+      if (j == i || (mask && !mask[j])) continue;
+      const float dx = pos[3 * j] - xi, dy = pos[3 * j + 1] - yi, dz = pos[3 * j + 2] - zi;
+      if (dx * dx + dy * dy + dz * dz <= r2) ++c;
+    }
+  }
+  counts[i] = c;
+}
+
+__global__ void rs_fill_kernel(const float* __restrict__ pos, const int64_t* __restrict__ node_graph,
+                               const int64_t* __restrict__ gptr, const bool* __restrict__ mask, int N, float r2,
+                               int cap, const int* __restrict__ rowptr, int64_t Ecap, int dummy, int* __restrict__ src,
+                               int* __restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < N) {
+    const int i = (int)t;
+    if (!mask || mask[i]) {
+      const int64_t g = node_graph[i];
+      const float xi = pos[3 * i], yi = pos[3 * i + 1], zi = pos[3 * i + 2];
+      int q = rowptr[i];
+      const int q1 = rowptr[i + 1];
+      for (int64_t j = gptr[g]; j < gptr[g + 1] && q < q1; ++j) {
+        if (j == i || (mask && !mask[j])) continue;
+        const float dx = pos[3 * j] - xi, dy = pos[3 * j + 1] - yi, dz = pos[3 * j + 2] - zi;
+        if (dx * dx + dy * dy + dz * dz <= r2) {
+          src[q] = (int)j;
+          dst[q] = i;
+          ++q;
+        }
+      }
+    }
+  }
+  // padding slots
+  const int64_t e0 = rowptr[N];
+  for (int64_t e = e0 + t; e < Ecap; e += (int64_t)gridDim.x * blockDim.x) {
+    src[e] = dummy;
+    dst[e] = dummy;
+  }
+}
+
+at::Tensor radius_static_count(const at::Tensor& pos_, const at::Tensor& node_graph, const at::Tensor& gptr,
+                               const c10::optional<at::Tensor>& mask, double r, int64_t cap) {
+  HY_CHECK_CUDA(pos_);
+  auto pos = pos_.to(at::kFloat).contiguous();
+  HY_CHECK(node_graph.scalar_type() == at::kLong && gptr.scalar_type() == at::kLong, "radius_static: int64 batch/ptr");
+  const int N = (int)pos.size(0);
+  auto counts = at::empty({N}, pos.options().dtype(at::kInt));
+  if (mask.has_value()) HY_CHECK(mask->scalar_type() == at::kBool && mask->numel() == N, "radius_static: mask [N] bool");
+  if (N)
+    rs_count_kernel<<<ceil_div(N, 256), 256, 0, stream()>>>(pos.data_ptr<float>(), node_graph.data_ptr<int64_t>(),
+                                                           gptr.data_ptr<int64_t>(),
+                                                           mask.has_value() ? mask->data_ptr<bool>() : nullptr, N,
+                                                           (float)(r * r), (int)cap, counts.data_ptr<int>());
+  return counts;
+}
+
+std::tuple<at::Tensor, at::Tensor> radius_static_fill(const at::Tensor& pos_, const at::Tensor& node_graph,
+                                                      const at::Tensor& gptr, const c10::optional<at::Tensor>& mask,
+                                                      double r, int64_t cap, const at::Tensor& rowptr, int64_t Ecap,
+                                                      int64_t dummy) {
+  auto pos = pos_.to(at::kFloat).contiguous();
+  const int N = (int)pos.size(0);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(rowptr.numel() == N + 1 && Ecap >= (int64_t)N * cap && dummy >= 0 && dummy < N, "radius_static_fill: sizes");
+  auto src = at::empty({Ecap}, rowptr.options()), dst = at::empty({Ecap}, rowptr.options());
+  const int blocks = std::max(ceil_div(N, 256), 64);
+  rs_fill_kernel<<<blocks, 256, 0, stream()>>>(pos.data_ptr<float>(), node_graph.data_ptr<int64_t>(),
+                                               gptr.data_ptr<int64_t>(),
+                                               mask.has_value() ? mask->data_ptr<bool>() : nullptr, N,
+                                               (float)(r * r), (int)cap, rowptr.data_ptr<int>(), Ecap, (int)dummy,
+                                               src.data_ptr<int>(), dst.data_ptr<int>());
+  return {src, dst};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
@@ -472,6 +564,10 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "radius_graph(Tensor pos, Tensor node_graph, Tensor gptr, float r, int max_nb, bool loop, bool nearest, "
       "Tensor? cell, Tensor? reps) -> (Tensor, Tensor)");
   m.def("triplets(Tensor edge_index, Tensor rowptr) -> (Tensor, Tensor)");
+  m.def("radius_static_count(Tensor pos, Tensor node_graph, Tensor gptr, Tensor? mask, float r, int cap) -> Tensor");
+  m.def(
+      "radius_static_fill(Tensor pos, Tensor node_graph, Tensor gptr, Tensor? mask, float r, int cap, Tensor rowptr, "
+      "int Ecap, int dummy) -> (Tensor, Tensor)");
   m.def(
       "radius_graph_cells(Tensor pos, Tensor node_graph, Tensor grid, Tensor geo, Tensor off, float r, int max_nb, "
       "bool loop, bool nearest, bool periodic) -> (Tensor, Tensor)");
@@ -480,5 +576,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radius_graph", hy::radius_graph);
   m.impl("triplets", hy::triplets);
+  m.impl("radius_static_count", hy::radius_static_count);
+  m.impl("radius_static_fill", hy::radius_static_fill);
   m.impl("radius_graph_cells", hy::radius_graph_cells);
 }

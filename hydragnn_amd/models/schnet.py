@@ -20,7 +20,7 @@ from torch import nn
 
 from ..ops import segment as seg
 from ..ops.geometry import GaussianSmearing, cosine_cutoff, edge_vectors_and_lengths
-from ..ops.radius import interaction_graph
+from ..ops.radius import interaction_graph, interaction_graph_static
 from .layers import Linear
 from .base import Base
 
@@ -75,10 +75,9 @@ class SCFStack(Base):
 
     @property
     def capturable(self):
-        # the in-forward radius graph has a data-dependent edge count; without equivariant
-        # position updates it equals the batch's own radius graph (built by the preprocessing
-        # with the same radius / max_neighbours / index cap), which a padded batch provides
-        return bool(self.use_edge_attr or (self.use_global_attn and self.is_edge_model) or not self.equivariance)
+        # a statically padded batch rebuilds the in-forward radius graph with fixed capacity
+        # (ops.radius.interaction_graph_static: no host sync), equivariant layers included
+        return True
 
     def __init__(self, input_args, conv_args, num_filters, edge_dim, num_gaussians, radius, *args,
                  max_neighbours=None, **kwargs):
@@ -119,13 +118,23 @@ class SCFStack(Base):
         stack = self
         cache = {}
 
-        # statically padded (captured) batch, fixed positions: the interaction graph is the
-        # batch's radius graph (same radius / max_neighbours / index cap as the in-forward
-        # builder, SCFStack.py:175-190), so the step has static shapes
-        static_graph = data.get("graph_mask") is not None and not self.equivariance
+        # statically padded (captured) batch: the in-forward radius graph (SCFStack.py:175-190)
+        # is rebuilt on the device with a fixed edge capacity, so the step has static shapes
+        static_graph = data.get("graph_mask") is not None
 
         def layer_graph(conv, p):
-            if with_edges or static_graph:  # data edges, no PBC shifts (reference overrides shifts with zeros)
+            if static_graph and not with_edges:
+                key = "g" if not conv.equivariant else None
+                if key is not None and "g" in cache:
+                    return cache["g"]
+                dst_si, src_si = interaction_graph_static(p, data, stack.radius, stack.max_neighbours)
+                _, d = edge_vectors_and_lengths(p, dst_si, src_si, None)
+                d = d.view(-1)
+                g = (dst_si, src_si, d, stack.distance_expansion(d), None)
+                if not conv.equivariant:
+                    cache["g"] = g
+                return g
+            if with_edges:  # data edges, no PBC shifts (reference overrides shifts with zeros)
                 if "g" not in cache:
                     _, d = edge_vectors_and_lengths(p, ctx.dst_si, ctx.src_si, None)
                     d = d.view(-1)

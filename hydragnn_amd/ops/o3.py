@@ -523,6 +523,36 @@ class Contraction(nn.Module):
         return out  # [N, H, 2L+1]
 
 
+class _SymConNative(torch.autograd.Function):
+    """csrc/symcon.hip: the whole product basis (every L, every nu) in one launch each
+    way; per-element weight gradients by a CSR segment sum over the element index."""
+
+    @staticmethod
+    def forward(ctx, x, elem_si, ents, grps, out_cols, shapes, *weights):
+        from .. import _native
+
+        ne = weights[0].shape[0]
+        Wcat = torch.cat([w for w in weights], 1).contiguous()  # [ne, Ktot, H]
+        ctx.save_for_backward(x, Wcat, ents, grps)
+        ctx.elem_si, ctx.shapes, ctx.ne = elem_si, shapes, ne
+        return _native.ops().symcon_fwd(x.contiguous(), elem_si.index, Wcat, ents, grps, out_cols)
+
+    @staticmethod
+    def backward(ctx, gout):
+        from .. import _native
+        from . import segment as seg
+
+        x, Wcat, ents, grps = ctx.saved_tensors
+        dx, dWn = _native.ops().symcon_bwd(gout, x, ctx.elem_si.index, Wcat, ents, grps)
+        N, Ktot, H = dWn.shape
+        dW = seg.segment_sum(dWn.view(N, Ktot * H), ctx.elem_si).view(ctx.ne, Ktot, H)
+        grads, o = [], 0
+        for K in ctx.shapes:
+            grads.append(dW[:, o:o + K])
+            o += K
+        return (dx, None, None, None, None, None, *grads)
+
+
 class SymmetricContraction(nn.Module):
     """MACE product basis: per output irrep L of ``irreps_out``, sum_{nu<=correlation}
     sum_k W_{nu,k}(element) U_{nu,k} . x^{(x) nu}, channel-wise."""
@@ -530,8 +560,47 @@ class SymmetricContraction(nn.Module):
     def __init__(self, lmax_in, irreps_out, correlation, num_features, num_elements):
         super().__init__()
         self.irreps_out = irreps_out
+        self.correlation = correlation
         self.contractions = nn.ModuleList([Contraction(lmax_in, l, correlation, num_features, num_elements)
                                            for _, l, _ in irreps_out.blocks])
+        self._tables = None
+
+    def _native_tables(self, H, dev):
+        """Entry table of the non-zero U coefficients (i0, i1, i2, weight row, value bits)
+        grouped by output column (base, 2L+1, M, first, end), for csrc/symcon.hip."""
+        if self._tables is not None and self._tables[0].device == dev and self._tables[3] == H:
+            return self._tables
+        ents, grps = [], []
+        koff, base = 0, 0
+        for c in self.contractions:
+            L = c.L
+            ks = []
+            for nu in range(1, c.correlation + 1):
+                ks.append(koff)
+                koff += getattr(c, f"U_{nu}").shape[-1]
+            for M in range(2 * L + 1):
+                e0 = len(ents)
+                for nu in range(1, c.correlation + 1):
+                    U = getattr(c, f"U_{nu}")[M]  # [d]*nu + [K]
+                    nz = torch.nonzero(U.abs() > 1e-12)
+                    for row in nz.tolist():
+                        idx, k = row[:-1], row[-1]
+                        v = float(U[tuple(row)])
+                        i = idx + [-1] * (3 - len(idx))
+                        ents.append([i[0], i[1], i[2], ks[nu - 1] + k, v])
+                grps.append([base, 2 * L + 1, M, e0, len(ents)])
+            base += H * (2 * L + 1)
+        e = torch.tensor([r[:4] for r in ents], dtype=torch.int32).view(-1, 4)
+        vals = torch.tensor([r[4] for r in ents], dtype=torch.float32).view(-1, 1).view(torch.int32)
+        self._tables = (torch.cat([e, vals], 1).contiguous().to(dev), torch.tensor(grps, dtype=torch.int32).to(dev),
+                        base, H)
+        return self._tables
+
+    def native_ok(self, x, elem):
+        from . import pna as _mode
+
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and x.shape[2] <= 16 and
+                self.correlation <= 3 and _mode.fused("symcon") and not torch.is_tensor(elem))
 
     def forward(self, x, elem):
         """``elem``: an element SegIndex (``element_index``), element indices [N], or a
@@ -539,4 +608,8 @@ class SymmetricContraction(nn.Module):
         N = x.shape[0]
         if torch.is_tensor(elem) and elem.dim() == 1:
             elem = element_index(elem, self.contractions[0].weights[0].shape[0])
+        if self.native_ok(x, elem):
+            ents, grps, cols, _ = self._native_tables(x.shape[1], x.device)
+            weights = [w for c in self.contractions for w in c.weights]
+            return _SymConNative.apply(x, elem, ents, grps, cols, [w.shape[1] for w in weights], *weights)
         return torch.cat([c(x, elem).reshape(N, -1) for c in self.contractions], -1)

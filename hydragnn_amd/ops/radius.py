@@ -94,6 +94,49 @@ def interaction_graph(pos, batch, r, max_num_neighbors=32):
     return csr_views(ei, pos.shape[0])
 
 
+def interaction_graph_static(pos, data, r, max_num_neighbors=None):
+    """In-forward radius graph of a statically padded batch with FIXED shapes and no host
+    synchronisation (capturable; csrc/graph.hip ``radius_static_*``): each valid receiver
+    keeps the first ``max_num_neighbors`` sources of its graph within ``r`` (index order,
+    torch_cluster semantics); the edge list has capacity ``N * cap``, unused slots are
+    self-edges of the last (padding) node.  Returns (dst_si, src_si)."""
+    from .. import _native
+
+    N = pos.shape[0]
+    cap = 32 if max_num_neighbors is None else int(max_num_neighbors)
+    Ecap = N * cap
+    mask = data.get("node_mask")
+    mask = None if mask is None else mask.view(-1).bool()
+    batch, ptr = data.batch.long(), data.ptr.long()
+    dummy = N - 1
+    p = pos.detach()
+    if p.is_cuda:
+        counts = _native.ops().radius_static_count(p, batch, ptr, mask, float(r), cap)
+        rowptr = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0, dtype=torch.int32)])
+        src, dst = _native.ops().radius_static_fill(p, batch, ptr, mask, float(r), cap, rowptr, Ecap, dummy)
+    else:  # CPU twin (padded_step tests): identical edge order
+        d = torch.cdist(p.float(), p.float())
+        m = (d <= r) & (batch.view(-1, 1) == batch.view(1, -1))
+        m.fill_diagonal_(False)
+        if mask is not None:
+            m &= mask.view(-1, 1) & mask.view(1, -1)
+        keep = m & (torch.cumsum(m.to(torch.int32), dim=1) <= cap)
+        dst_v, src_v = keep.nonzero(as_tuple=True)
+        counts = keep.sum(1).to(torch.int32)
+        rowptr = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0, dtype=torch.int32)])
+        E = dst_v.numel()
+        src = torch.full((Ecap,), dummy, dtype=torch.int32)
+        dst = torch.full((Ecap,), dummy, dtype=torch.int32)
+        src[:E], dst[:E] = src_v.int(), dst_v.int()
+    drp = rowptr.clone()
+    drp[N] = Ecap  # the padding slots belong to the last (padding) receiver
+    scnt = torch.zeros(N, dtype=torch.int32, device=src.device).index_add_(
+        0, src.long(), torch.ones(Ecap, dtype=torch.int32, device=src.device))
+    srp = torch.cat([scnt.new_zeros(1), torch.cumsum(scnt, 0, dtype=torch.int32)])
+    sperm = torch.sort(src, stable=True).indices.to(torch.int32)
+    return SegIndex(dst, drp, None, N), SegIndex(src, srp, sperm, N)
+
+
 def radius_graph_cells(pos, batch, r, max_num_neighbors=None, loop=False, cap_policy="index", cell=None):
     """Cell-list (binned) HIP radius graph (``csrc/graph.hip`` ``radius_graph_cells``): O(N) for
     large structures, same output as ``radius_graph_device`` (edge set, cap policies, CSR order

@@ -83,3 +83,30 @@ def test_force_test_returns_samples_and_dump(tmp_path, monkeypatch):
     assert len(recs) == 8
     assert recs[0]["forces_pred"].numel() == samples[0].num_nodes * 3
     assert abs(recs[3]["energy_pred"] - float(pred[0][3])) < 1e-5
+
+
+@pytest.mark.parametrize("equivariance", [False, True])
+def test_schnet_static_inforward_graph_padded_equals_eager(equivariance):
+    """SchNet's in-forward radius graph (SCFStack.py:175-190) in the padded (capturable)
+    step is rebuilt with a fixed edge capacity on the device (ops.radius
+    .interaction_graph_static); the step equals the eager step (dynamic builder)."""
+    samples = _samples()
+    heads = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                             "num_headlayers": 1, "dim_headlayers": [8]}}]}
+    for s in samples:
+        s.y = s.energy.view(-1, 1) if "energy" in s else s.y.view(-1, 1)
+        s.y_loc = torch.tensor([[0, 1]])
+    m1 = create_model("SchNet", 1, 16, [1], 0, "", "", 0, ["graph"], heads, "relu", "mae", [1.0], 3,
+                      num_gaussians=10, num_filters=16, radius=3.0, max_neighbours=4, dropout=0.0,
+                      equivariance=equivariance)
+    m2 = copy.deepcopy(m1)
+    assert m1.capturable
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])
+    eager = TrainStep(m1, lr=1e-3, mode="eager")
+    padded = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=512)
+    rng = np.random.default_rng(1)
+    for _ in range(3):
+        idx = list(rng.choice(len(store), 4, replace=False))
+        le = float(eager(store, idx)[0])
+        lp = float(padded(store, idx)[0])
+        assert abs(le - lp) <= 1e-4 * max(1.0, abs(le)), (le, lp)

@@ -284,3 +284,33 @@ def test_cell_list_radius_graph_large_structure_linear_time():
         want = want[want != i]
         got = ei[0][ei[1] == i].sort().values
         assert torch.equal(got, want.sort().values)
+
+
+@pytest.mark.gpu
+def test_static_radius_graph_gpu_matches_cpu_twin():
+    """Capturable in-forward radius graph (csrc/graph.hip radius_static_*): same edges,
+    CSR views and padding layout as the CPU twin, no host sync (fixed capacity)."""
+    from hydragnn_amd.ops.radius import interaction_graph_static
+
+    g = torch.Generator().manual_seed(3)
+    sizes = [7, 12, 1, 9]
+    pos = torch.cat([torch.rand(n, 3, generator=g) * 3 for n in sizes] + [torch.zeros(3, 3)])
+    batch = torch.cat([torch.full((n,), i) for i, n in enumerate(sizes)] + [torch.full((3,), len(sizes))])
+    ptr = torch.tensor([0] + list(np.cumsum(sizes + [3])))
+    mask = torch.cat([torch.ones(sum(sizes), dtype=torch.bool), torch.zeros(3, dtype=torch.bool)])
+
+    class D(dict):
+        def get(self, k, d=None):
+            return dict.get(self, k, d)
+
+    def data(dev):
+        d = D(node_mask=mask.to(dev))
+        d.batch, d.ptr = batch.to(dev), ptr.to(dev)
+        return d
+
+    a_dst, a_src = interaction_graph_static(pos, data("cpu"), 1.5, 4)
+    b_dst, b_src = interaction_graph_static(pos.cuda(), data("cuda"), 1.5, 4)
+    for x, y in [(a_dst.index, b_dst.index), (a_dst.rowptr, b_dst.rowptr), (a_src.index, b_src.index),
+                 (a_src.rowptr, b_src.rowptr), (a_src.perm, b_src.perm)]:
+        assert torch.equal(x, y.cpu())
+    assert a_dst.index.numel() == pos.shape[0] * 4

@@ -356,6 +356,36 @@ def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh):
         torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("correlation,lmax_out", [(2, 1), (3, 1), (3, 2)])
+def test_symmetric_contraction_native(correlation, lmax_out):
+    """MACE product basis kernel (csrc/symcon.hip) == the torch Horner path (fp64 CPU),
+    outputs, d x and the per-element weight gradients."""
+    from hydragnn_amd.ops import o3
+
+    torch.manual_seed(correlation * 10 + lmax_out)
+    H, ne, N = 32, 5, 300
+    irreps_out = o3.Irreps.natural(H, lmax_out)
+    sc = o3.SymmetricContraction(2, irreps_out, correlation, H, ne)
+    elem = torch.randint(0, ne, (N,))
+    x = torch.randn(N, H, 9)
+    sc64 = o3.SymmetricContraction(2, irreps_out, correlation, H, ne).double()
+    sc64.load_state_dict(sc.state_dict())
+    scg = sc.to(DEV)
+    xg = x.to(DEV).requires_grad_()
+    esi = o3.element_index(elem.to(DEV), ne)
+    assert scg.native_ok(xg, esi)
+    out = scg(xg, esi)
+    xr = x.double().requires_grad_()
+    ref = sc64(xr, elem)
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(ref)
+    out.backward(g.float().to(DEV))
+    ref.backward(g)
+    torch.testing.assert_close(xg.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-3)
+    for a, b in zip(scg.parameters(), sc64.parameters()):
+        torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("G,dims,relus", [(33, [64, 50, 50, 50, 25, 1], [1, 1, 1, 1, 0]),
                                           (203, [7, 128, 3], [1, 0]), (1, [16, 8], [1])])
 def test_fused_mlp_chain(G, dims, relus):
