@@ -275,7 +275,7 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void nt_kernel(NTArgs p) {
 // The next tile's copies stay in flight across the barrier: counted vmcnt + raw s_barrier
 // (a __syncthreads would drain them).  Rows past M read a clamped valid row (masked in
 // the epilogue).
-template <int BM, int WN>
+template <int BM, int WN, bool GR>
 __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
   constexpr int WM = BM / 64;
   constexpr int NW = WM * WN;
@@ -291,6 +291,12 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
   const int m0 = (wg / p.tiles_n) * BM, n0 = (wg % p.tiles_n) * BN;
   const int KT = p.K / BK;
   const int lr = lane >> 3, ls = lane & 7;  // row within the 8-row group, LDS slot
+  int br0 = -1, br1 = -1;  // branch-grouped mode: one pass per branch present in the tile
+  if constexpr (GR) {
+    br0 = p.bid[m0];
+    br1 = p.bid[min(m0 + BM, p.M) - 1];
+  }
+  const uint16_t* Bw = p.B;
 
   auto issue = [&](int kt, int buf) {
     const uint16_t* As;
@@ -310,19 +316,21 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
     for (int j = 0; j < BI; ++j) {
       const int row = (wid * BI + j) * 8 + lr;
       const int c = ls ^ ((row >> 1) & 7);
-      __builtin_amdgcn_global_load_lds(p.B + (int64_t)(n0 + row) * p.ldb + kt * BK + c * 8,
+      __builtin_amdgcn_global_load_lds(Bw + (int64_t)(n0 + row) * p.ldb + kt * BK + c * 8,
                                        (__attribute__((address_space(3))) void*)(s + ABYTES + (wid * BI + j) * 1024),
                                        16, 0, 0);
     }
   };
 
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int br = br0; br <= br1; ++br) {
+  if constexpr (GR) Bw = p.B + (int64_t)br * p.bsB;
   f4v acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  const int fr = lane & 15, fg = lane >> 4;
   issue(0, 0);
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
@@ -353,7 +361,9 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
-  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg, p.bias, -1);
+  nt_epilogue<NJ>(p, acc, m0 + wm * 64, n0 + wn * NJ * 16, fr, fg,
+                  p.bias ? p.bias + (GR ? (int64_t)br * p.bsbias : 0) : nullptr, GR ? br : -1);
+  }
 }
 
 // ------------------------------------------------------------------------------ TN GEMM
@@ -659,7 +669,7 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
   }
   if (bid.has_value()) {
     HY_CHECK_I32(*bid);
-    HY_CHECK(bid->numel() >= M && !glds, "bg_nt: grouped mode needs bid [M] (register-staged kernel)");
+    HY_CHECK(bid->numel() >= M, "bg_nt: grouped mode needs bid [M]");
     p.bid = bid->data_ptr<int>();
     p.bsB = bsB;
     p.bsbias = (int)bsbias;
@@ -667,9 +677,16 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
   if (M == 0) return;
   p.tiles_n = (int)(Np / 128);
   if (glds) {
-    if (bm == 256) ntg_kernel<256, 2><<<ceil_div(M, 256) * p.tiles_n, 512, 0, stream()>>>(p);
-    else if (bm == 128) ntg_kernel<128, 2><<<ceil_div(M, 128) * p.tiles_n, 256, 0, stream()>>>(p);
-    else ntg_kernel<64, 4><<<ceil_div(M, 64) * p.tiles_n, 256, 0, stream()>>>(p);
+    if (p.bid) {
+      HY_CHECK(bm == 64, "bg_nt: grouped glds mode uses the 64-row tile");
+      ntg_kernel<64, 4, true><<<ceil_div(M, 64) * p.tiles_n, 256, 0, stream()>>>(p);
+    } else if (bm == 256) {
+      ntg_kernel<256, 2, false><<<ceil_div(M, 256) * p.tiles_n, 512, 0, stream()>>>(p);
+    } else if (bm == 128) {
+      ntg_kernel<128, 2, false><<<ceil_div(M, 128) * p.tiles_n, 256, 0, stream()>>>(p);
+    } else {
+      ntg_kernel<64, 4, false><<<ceil_div(M, 64) * p.tiles_n, 256, 0, stream()>>>(p);
+    }
     return;
   }
   if (bm == 256) {

@@ -16,6 +16,7 @@ import torch
 from .. import _native
 
 ACT = {"none": 0, "relu": 1, "silu": 2}
+GEMM_TILE = 1064  # NT kernel: 64-row tile, global_load_lds staging (1000 + rows; 64/128/256 = register staging)
 
 
 def pad64(k):
@@ -65,11 +66,9 @@ def nt(A, B, K, N, *, A2=None, k1=None, bias=None, act=0, gate=None, addg=None, 
     [Np, >=K] padded bf16 weight image; writes ``outf`` (fp32, first N columns) and/or
     ``outb`` (padded bf16, all Np columns)."""
     if bm is None:
-        # >= ~2 workgroups per CU: big row counts take the 256-row tile (half the B
-        # traffic), node-sized ones the 64-row tile
-        tiles_n = B.shape[0] // 128
-        M = A.shape[0]
-        bm = 256 if (M + 255) // 256 * tiles_n >= 512 else (128 if (M + 127) // 128 * tiles_n >= 512 else 64)
+        # the glds-staged 64-row tile measured fastest on every EGNN shape on MI355X
+        # (profiles/r3_bench_bgemm.log: 752 TF/s at 35k x 896 x 896 vs 571 for hipBLASLt)
+        bm = GEMM_TILE
     _native.ops().bg_nt(A, A2, K if k1 is None else k1, B, K, N, bias, act, gate, addg, addg_idx, outf, beta, outb,
                         ones_col, rowvec, rowdot, bm)
 
@@ -213,12 +212,12 @@ class _BranchMLP(torch.autograd.Function):
             if last:
                 out = torch.empty((M, dims[-1]), device=dev, dtype=torch.float32)
                 _native.ops().bg_nt(h, None, kps[l], imgs[l][0], kps[l], dims[l + 1], biases[l], int(relu[l]), None,
-                                    None, None, out, 0.0, None, -1, None, None, 128, bid, imgs[l][0].numel(),
+                                    None, None, out, 0.0, None, -1, None, None, GEMM_TILE, bid, imgs[l][0].numel(),
                                     dims[l + 1])
             else:
                 hn = torch.empty((M, Np), device=dev, dtype=torch.bfloat16)
                 _native.ops().bg_nt(h, None, kps[l], imgs[l][0], kps[l], dims[l + 1], biases[l], int(relu[l]), None,
-                                    None, None, None, 0.0, hn, dims[l + 1], None, None, 128, bid, imgs[l][0].numel(),
+                                    None, None, None, 0.0, hn, dims[l + 1], None, None, GEMM_TILE, bid, imgs[l][0].numel(),
                                     dims[l + 1])
                 h = hn
                 hs.append(h)
@@ -255,12 +254,12 @@ class _BranchMLP(torch.autograd.Function):
             if l > 0:
                 gn = torch.empty((M, Kp), device=dev, dtype=torch.bfloat16)
                 _native.ops().bg_nt(g, None, Np, imgTs[l][0], Np, dims[l], None, 0, hs[l] if relu[l - 1] else None,
-                                    None, None, None, 0.0, gn, -1, None, None, 128, bid, imgTs[l][0].numel(), 0)
+                                    None, None, None, 0.0, gn, -1, None, None, GEMM_TILE, bid, imgTs[l][0].numel(), 0)
                 g = gn
             elif ctx.needs_input_grad[0]:
                 dx = torch.empty((M, dims[0]), device=dev, dtype=torch.float32)
                 _native.ops().bg_nt(g, None, Np, imgTs[0][0], Np, dims[0], None, 0, None, None, None, dx, 0.0, None,
-                                    -1, None, None, 128, bid, imgTs[0][0].numel(), 0)
+                                    -1, None, None, GEMM_TILE, bid, imgTs[0][0].numel(), 0)
         ctx.imgTs = None
         return (dx, None, None, None, None, None, *grads)
 

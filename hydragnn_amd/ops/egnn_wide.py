@@ -26,6 +26,7 @@ from . import bgemm as bg
 
 
 ENABLED = True  # module switch (tests compare against the module-by-module bf16 path)
+DEBUG = None  # dict: backward records the position gradient entering each layer (tests)
 
 
 def eligible(model, ctx):
@@ -234,6 +235,8 @@ class _EGNNWide(torch.autograd.Function):
                 dpos_in = torch.empty((N, 3), device=dev, dtype=torch.float32)
                 ops.egnn_pos_bwd(dpos, dvec, src.rowptr, src.perm, dst.rowptr, dpos_in)
                 dpos = dpos_in
+                if DEBUG is not None:
+                    DEBUG[li] = dpos_in.clone()
             for j in range(L["np"]):
                 grads[offs[li] + j] = g[j]
         ctx.saved = ctx.imgs = None

@@ -111,7 +111,8 @@ def test_bf16_linear_grad(act):
 
 def test_branch_mlp_matches_per_branch():
     """Branch-grouped head GEMMs (rows sorted by branch, tiles straddling branch boundaries,
-    an empty branch) against per-branch fp32 evaluation."""
+    an empty branch) against per-branch evaluation with the same bf16 rounding points
+    (BF16Linear layer by layer), and loosely against fp32."""
     torch.manual_seed(5)
     nb, dims = 4, [200, 150, 150, 3]
     seqs = []
@@ -129,20 +130,39 @@ def test_branch_mlp_matches_per_branch():
     (y * G).sum().backward()
     gx = x.grad.clone()
     gw = [[p.grad.clone() for p in s.parameters()] for s in seqs]
-    for s in seqs:
-        s.zero_grad()
-    x.grad = None
-    ref = torch.cat([seqs[b](x[boff[b]:boff[b + 1]]) for b in range(nb)])
-    (ref * G).sum().backward()
+
+    def run_ref(bf16):
+        for s in seqs:
+            s.zero_grad()
+        x.grad = None
+        outs = []
+        for b in range(nb):
+            h = x[boff[b]:boff[b + 1]]
+            mods = list(seqs[b])
+            for i in range(0, len(mods), 2):
+                lin = mods[i]
+                act = 1 if i + 1 < len(mods) else 0
+                if bf16:
+                    h = bg.bf16_linear(h, lin.weight, lin.bias, act)
+                else:
+                    h = lin(h)
+                    h = torch.relu(h) if act else h
+            outs.append(h)
+        ref = torch.cat(outs)
+        (ref * G).sum().backward()
+        return ref.detach(), x.grad.clone(), [[p.grad.clone() for p in s.parameters()] for s in seqs]
 
     def rel(a, b):
         return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
-    assert rel(y, ref) < 1e-2
-    assert rel(gx, x.grad) < 2e-2
-    for b, s in enumerate(seqs):
-        for g, p in zip(gw[b], s.parameters()):
+    rb, gxb, gwb = run_ref(True)
+    rf, gxf, gwf = run_ref(False)
+    assert rel(y, rb) < 2e-3 and rel(y, rf) < 1e-2
+    assert rel(gx, gxb) < 5e-3, rel(gx, gxb)
+    assert rel(gx, gxf) < 1e-1
+    for b in range(nb):
+        for g, r in zip(gw[b], gwb[b]):
             if sizes[b] == 0:
                 assert g.abs().max().item() == 0.0
             else:
-                assert rel(g, p.grad) < 2e-2, (b, p.shape, rel(g, p.grad))
+                assert rel(g, r) < 5e-3, (b, g.shape, rel(g, r))

@@ -16,7 +16,9 @@ def _graph(n=60, seed=0):
     g = torch.Generator().manual_seed(seed)
     pos = torch.rand(n, 3, generator=g) * 4.0
     d = torch.cdist(pos, pos)
-    src, dst = torch.nonzero((d < 2.5) & (d > 0), as_tuple=True)
+    src, dst = torch.nonzero(d < 2.5, as_tuple=True)
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
     order = torch.argsort(dst * n + src)
     src, dst = src[order], dst[order]
     return pos, src, dst
