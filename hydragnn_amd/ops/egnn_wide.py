@@ -165,6 +165,8 @@ class _EGNNWide(torch.autograd.Function):
                 x_out = torch.empty((N, Ho), device=dev, dtype=torch.float32)
             bg.nt(n1, im["n2"], Hp, Ho, bias=p[7], act=1, outb=xn, ones_col=Ho, outf=x_out)
             saved.append(dict(xb=xb, h1=h1, geo=geo, sc=sc, m=m, s=s, c1=c1, agg=agg, n1=n1, xn=xn))
+            if DEBUG is not None:
+                DEBUG[("s", li)], DEBUG[("geo", li)] = s, geo
             xb, pos_l = xn, pos_n
         ctx.plan, ctx.imgs, ctx.saved, ctx.params = plan, imgs, saved, params
         ctx.mark_non_differentiable(pos_l)
@@ -214,6 +216,8 @@ class _EGNNWide(torch.autograd.Function):
                 ops.bg_slab_reduce(part, nblk, 1, Hp, 0, 0, 1, H, g[10], 0.0, -1, None)
                 bg.wgrad(dc1, S["m"], Hp, Hp, [(g[8], 0, g[9], H)])
                 bg.nt(dc1, im["c1T"], Hp, H, addg=dagg, addg_idx=src.index, gate=S["m"], outb=dZ2)
+                if DEBUG is not None:
+                    DEBUG[("dc1", li)] = dc1
                 del dc1
             else:
                 ops.egnn_gather_gate(dagg, src.index, S["m"], H, dZ2)
