@@ -490,24 +490,37 @@ __global__ __launch_bounds__(256) void tn_kernel(TNArgs p) {
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Np, int Kp, int n0, int k0, int N, int K,
                                    float* __restrict__ out, int ldo, int ldk, float beta, int bias_col,
                                    float* __restrict__ bias_out) {
-  const int64_t total = (int64_t)N * (K + 1);
+  // threads [0, N * KQ): 4 consecutive columns each (16-byte slab loads, 4 slabs in flight);
+  // threads [N * KQ, N * KQ + N): the bias column
+  const int KQ = (K + 3) / 4;
+  const int64_t total = (int64_t)N * KQ + (bias_out && bias_col >= 0 ? N : 0);
   const int64_t stride = (int64_t)Np * Kp;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int n = (int)(e / (K + 1)), k = (int)(e % (K + 1));
-    int kc = k0 + k;
-    if (k == K) {
-      if (bias_col < 0 || !bias_out) continue;
-      kc = bias_col;
-    }
-    const float* s = slab + (int64_t)(n0 + n) * Kp + kc;
-    float v = 0.f;
-    for (int i = 0; i < S; ++i) v += s[i * stride];
-    if (k == K) {
+    if (e >= (int64_t)N * KQ) {
+      const int n = (int)(e - (int64_t)N * KQ);
+      const float* sp = slab + (int64_t)(n0 + n) * Kp + bias_col;
+      float v = 0.f;
+      for (int i = 0; i < S; ++i) v += sp[i * stride];
       bias_out[n] = v + (beta != 0.f ? beta * bias_out[n] : 0.f);
-    } else {
-      float* o = out + (int64_t)n * ldo + (int64_t)k * ldk;
-      *o = v + (beta != 0.f ? beta * *o : 0.f);
+      continue;
     }
+    const int n = (int)(e / KQ), k = (int)(e % KQ) * 4;
+    const float* sp = slab + (int64_t)(n0 + n) * Kp + k0 + k;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int i = 0;
+    for (; i + 3 < S; i += 4) {
+      const float4 a0 = *reinterpret_cast<const float4*>(sp + i * stride);
+      const float4 a1 = *reinterpret_cast<const float4*>(sp + (i + 1) * stride);
+      const float4 a2 = *reinterpret_cast<const float4*>(sp + (i + 2) * stride);
+      const float4 a3 = *reinterpret_cast<const float4*>(sp + (i + 3) * stride);
+      acc = f4add(acc, f4add(f4add(a0, a1), f4add(a2, a3)));
+    }
+    for (; i < S; ++i) acc = f4add(acc, *reinterpret_cast<const float4*>(sp + i * stride));
+    const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+    float* o = out + (int64_t)n * ldo + (int64_t)k * ldk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (k + r < K) o[r * ldk] = v[r] + (beta != 0.f ? beta * o[r * ldk] : 0.f);
   }
 }
 
@@ -745,14 +758,14 @@ void bg_slab_reduce(const at::Tensor& slab, int64_t S, int64_t Np, int64_t Kp, i
                     const at::Tensor& out, double beta, int64_t bias_col, const c10::optional<at::Tensor>& bias_out) {
   HY_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) >= N && out.size(1) >= K,
            "bg_slab_reduce: out");
-  HY_CHECK(n0 + N <= Np && k0 + K <= Kp && bias_col < Kp, "bg_slab_reduce: bounds");
+  HY_CHECK(n0 + N <= Np && k0 + K <= Kp && bias_col < Kp && Kp % 4 == 0 && k0 % 4 == 0, "bg_slab_reduce: bounds");
   float* bo = nullptr;
   if (bias_out.has_value()) {
     HY_CHECK(bias_out->scalar_type() == at::kFloat && bias_out->is_contiguous() && bias_out->numel() >= N,
              "bg_slab_reduce: bias_out");
     bo = bias_out->data_ptr<float>();
   }
-  const int64_t total = N * (K + 1);
+  const int64_t total = N * ((K + 3) / 4) + N;
   const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   slab_reduce_kernel<<<blocks, 256, 0, stream()>>>(slab.data_ptr<float>(), (int)S, (int)Np, (int)Kp, (int)n0,
                                                    (int)k0, (int)N, (int)K, out.data_ptr<float>(), (int)out.stride(0),

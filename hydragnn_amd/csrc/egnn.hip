@@ -54,53 +54,68 @@ struct GatherFwd {
   uint16_t* sc;     // [E, 128]: |d|, ea..., 1 at 1 + nea
 };
 
+constexpr int GE = 32;  // edges per block (8 per wave) of the gather kernel
+
+// One wave per edge row, 32 edges per block: the radial / edge-attribute weight columns
+// and the bias are staged once per block in LDS (the strided W0 columns are never read per
+// element); each lane owns channels 4l + 256 t (t < 4), all 8 row loads issued together.
 __global__ __launch_bounds__(256) void gather_fwd_kernel(GatherFwd p) {
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (e >= p.E) return;
-  const int s = p.src[e], d = p.dst[e];
-  const float vx = p.pos[d * 3] - p.pos[s * 3], vy = p.pos[d * 3 + 1] - p.pos[s * 3 + 1],
-              vz = p.pos[d * 3 + 2] - p.pos[s * 3 + 2];
-  const float L = sqrtf(vx * vx + vy * vy + vz * vz);
-  float sv[MAXS] = {L, 0.f, 0.f, 0.f};
-  for (int j = 0; j < p.nea; ++j) sv[1 + j] = p.ea[(int64_t)e * p.nea + j];
-  if (lane == 0) {
-    const float inv = 1.f / (L + 1.f);
-    *reinterpret_cast<float4*>(p.geo + (int64_t)e * 4) = make_float4(vx * inv, vy * inv, vz * inv, L);
+  __shared__ float wl[MAXS + 1][1024];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int k = threadIdx.x; k < p.Hp; k += 256) {
+    const bool v = k < p.H;
+    wl[MAXS][k] = v ? p.b1[k] : 0.f;
+    for (int j = 0; j <= p.nea; ++j) wl[j][k] = v ? p.W0[(int64_t)k * p.ld0 + p.c0 + j] : 0.f;
   }
-  if (lane < 32) {  // scalar row: 4 bf16 per lane over 128 columns
-    float t[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = lane * 4 + r;
-      t[r] = c <= p.nea ? sv[c < MAXS ? c : 0] : (c == p.nea + 1 ? 1.f : 0.f);
+  __syncthreads();
+  for (int i = 0; i < GE / 4; ++i) {
+    const int e = blockIdx.x * GE + w * (GE / 4) + i;
+    if (e >= p.E) break;
+    const int s = p.src[e], d = p.dst[e];
+    const float vx = p.pos[d * 3] - p.pos[s * 3], vy = p.pos[d * 3 + 1] - p.pos[s * 3 + 1],
+                vz = p.pos[d * 3 + 2] - p.pos[s * 3 + 2];
+    const float L = sqrtf(vx * vx + vy * vy + vz * vz);
+    float sv[MAXS] = {L, 0.f, 0.f, 0.f};
+    for (int j = 0; j < p.nea; ++j) sv[1 + j] = p.ea[(int64_t)e * p.nea + j];
+    if (lane == 0) {
+      const float inv = 1.f / (L + 1.f);
+      *reinterpret_cast<float4*>(p.geo + (int64_t)e * 4) = make_float4(vx * inv, vy * inv, vz * inv, L);
     }
-    st_bf4(p.sc + (int64_t)e * 128 + lane * 4, t[0], t[1], t[2], t[3]);
-  }
-  const float* ar = p.AB + (int64_t)s * 2 * p.Hp;
-  const float* br = p.AB + (int64_t)d * 2 * p.Hp + p.Hp;
-  uint16_t* out = p.h1 + (int64_t)e * p.Hp;
-  for (int k = lane * 4; k < p.Hp; k += 256) {
-    float v[4];
-    if (k + 3 < p.H) {
-      const float4 a = *reinterpret_cast<const float4*>(ar + k), b = *reinterpret_cast<const float4*>(br + k);
-      v[0] = a.x + b.x; v[1] = a.y + b.y; v[2] = a.z + b.z; v[3] = a.w + b.w;
-    } else {
+    if (lane < 32) {  // scalar row: 4 bf16 per lane over 128 columns
+      float t[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (k + r < p.H) ? ar[k + r] + br[k + r] : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        const int c = lane * 4 + r;
+        t[r] = c <= p.nea ? sv[c < MAXS ? c : 0] : (c == p.nea + 1 ? 1.f : 0.f);
+      }
+      st_bf4(p.sc + (int64_t)e * 128 + lane * 4, t[0], t[1], t[2], t[3]);
     }
+    const float* ar = p.AB + (int64_t)s * 2 * p.Hp;
+    const float* br = p.AB + (int64_t)d * 2 * p.Hp + p.Hp;
+    uint16_t* out = p.h1 + (int64_t)e * p.Hp;
+    float4 av[4], bv[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int kk = k + r;
-      if (kk < p.H) {
-        float z = v[r] + p.b1[kk];
-        const float* wrow = p.W0 + (int64_t)kk * p.ld0 + p.c0;
-        for (int j = 0; j <= p.nea; ++j) z += sv[j] * wrow[j];
-        v[r] = fmaxf(z, 0.f);
-      } else {
-        v[r] = kk == p.H ? 1.f : 0.f;
+    for (int t = 0; t < 4; ++t) {
+      const int k = lane * 4 + t * 256;
+      if (k < p.Hp) {  // AB pad columns are zero (padded weight images)
+        av[t] = *reinterpret_cast<const float4*>(ar + k);
+        bv[t] = *reinterpret_cast<const float4*>(br + k);
       }
     }
-    st_bf4(out + k, v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = lane * 4 + t * 256;
+      if (k >= p.Hp) continue;
+      float v[4] = {av[t].x + bv[t].x, av[t].y + bv[t].y, av[t].z + bv[t].z, av[t].w + bv[t].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = k + r;
+        float z = v[r] + wl[MAXS][kk] + sv[0] * wl[0][kk];
+        for (int j = 1; j <= p.nea; ++j) z += sv[j] * wl[j][kk];
+        v[r] = kk < p.H ? fmaxf(z, 0.f) : (kk == p.H ? 1.f : 0.f);
+      }
+      st_bf4(out + k, v[0], v[1], v[2], v[3]);
+    }
   }
 }
 
@@ -117,20 +132,46 @@ struct AggFwd {
   float* pos_out;     // [N, 3]
 };
 
+// sum of bf16 rows e in [b, eN) (through perm) into 4 float4 accumulators per lane
+// (channels 4l + 256 t), two rows in flight
+__device__ __forceinline__ void rows_sum(const uint16_t* __restrict__ X, int Hp, const int* __restrict__ perm, int b,
+                                         int eN, int lane, float4 (&acc)[4]) {
+  int i = b;
+  for (; i + 1 < eN; i += 2) {
+    const int e0 = perm ? perm[i] : i, e1 = perm ? perm[i + 1] : i + 1;
+    float4 x0[4], x1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = lane * 4 + t * 256;
+      if (k < Hp) {
+        x0[t] = ld_bf4(X + (int64_t)e0 * Hp + k);
+        x1[t] = ld_bf4(X + (int64_t)e1 * Hp + k);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (lane * 4 + t * 256 < Hp) acc[t] = f4add(acc[t], f4add(x0[t], x1[t]));
+  }
+  if (i < eN) {
+    const int e0 = perm ? perm[i] : i;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = lane * 4 + t * 256;
+      if (k < Hp) acc[t] = f4add(acc[t], ld_bf4(X + (int64_t)e0 * Hp + k));
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void agg_fwd_kernel(AggFwd p) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (n >= p.N) return;
   const int b = p.srp[n], eN = p.srp[n + 1];
-  for (int k = lane * 4; k < p.Hp; k += 256) {
-    float4 acc = f4zero();
-    int i = b;
-    for (; i + 1 < eN; i += 2) {
-      const int e0 = p.sperm ? p.sperm[i] : i, e1 = p.sperm ? p.sperm[i + 1] : i + 1;
-      const float4 x0 = ld_bf4(p.m + (int64_t)e0 * p.Hp + k), x1 = ld_bf4(p.m + (int64_t)e1 * p.Hp + k);
-      acc = f4add(acc, f4add(x0, x1));
-    }
-    if (i < eN) acc = f4add(acc, ld_bf4(p.m + (int64_t)(p.sperm ? p.sperm[i] : i) * p.Hp + k));
-    st_bf4(p.agg + (int64_t)n * p.Hp + k, acc.x, acc.y, acc.z, acc.w);
+  float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+  rows_sum(p.m, p.Hp, p.sperm, b, eN, lane, acc);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int k = lane * 4 + t * 256;
+    if (k < p.Hp) st_bf4(p.agg + (int64_t)n * p.Hp + k, acc[t].x, acc[t].y, acc[t].z, acc[t].w);
   }
   if (p.s && lane < 3) {
     float t = 0.f;
@@ -191,11 +232,17 @@ __global__ __launch_bounds__(256) void coord_bwd_kernel(CoordBwd p) {
     if (lane < 3) p.dcd[(int64_t)e * 3 + lane] = dcd[lane];
     const uint16_t* crow = p.c1 + (int64_t)e * p.Hp;
     uint16_t* orow = p.dc1 + (int64_t)e * p.Hp;
+    float4 cr[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {  // the whole row in flight at once
+      const int k = lane * 4 + it * 256;
+      if (k < p.Hp) cr[it] = ld_bf4(crow + k);
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int k = lane * 4 + it * 256;
       if (k >= p.Hp) break;
-      const float4 c = ld_bf4(crow + k);
+      const float4 c = cr[it];
       float o[4];
       const float cv[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
@@ -239,14 +286,12 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwd p) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (n >= p.N) return;
   {
-    const int b = p.srp[n], eN = p.srp[n + 1];
-    for (int k = lane * 4; k < p.Hp; k += 256) {
-      float4 acc = f4zero();
-      for (int i = b; i < eN; ++i) {
-        const int e = p.sperm ? p.sperm[i] : i;
-        acc = f4add(acc, ld_bf4(p.dh1 + (int64_t)e * p.Hp + k));
-      }
-      st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + k, acc.x, acc.y, acc.z, acc.w);
+    float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+    rows_sum(p.dh1, p.Hp, p.sperm, p.srp[n], p.srp[n + 1], lane, acc);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = lane * 4 + t * 256;
+      if (k < p.Hp) st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + k, acc[t].x, acc[t].y, acc[t].z, acc[t].w);
     }
   }
   const int b = p.drp[n], eN = p.drp[n + 1];
@@ -260,16 +305,27 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwd p) {
       wr[it][r] = k < p.H ? p.W0[(int64_t)k * p.ld0 + p.c0] : 0.f;
     }
   float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+  float4 nx[4];
+  auto ld_row = [&](int e, float4 (&x)[4]) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 4 + it * 256;
+      if (k < p.Hp) x[it] = ld_bf4(p.dh1 + (int64_t)e * p.Hp + k);
+    }
+  };
+  if (b < eN) ld_row(b, nx);
   for (int e = b; e < eN; ++e) {
-    const uint16_t* row = p.dh1 + (int64_t)e * p.Hp;
+    float4 x[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) x[it] = nx[it];
+    if (e + 1 < eN) ld_row(e + 1, nx);  // next row in flight while this one reduces
     float dr = 0.f;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int k = lane * 4 + it * 256;
       if (k < p.Hp) {
-        const float4 x = ld_bf4(row + k);
-        acc[it] = f4add(acc[it], x);
-        dr += x.x * wr[it][0] + x.y * wr[it][1] + x.z * wr[it][2] + x.w * wr[it][3];
+        acc[it] = f4add(acc[it], x[it]);
+        dr += x[it].x * wr[it][0] + x[it].y * wr[it][1] + x[it].z * wr[it][2] + x[it].w * wr[it][3];
       }
     }
     dr = wave_sum(dr);
@@ -381,7 +437,8 @@ void egnn_gather_fwd(const at::Tensor& AB, const at::Tensor& src, const at::Tens
   p.h1 = wbf(h1);
   p.geo = geo.data_ptr<float>();
   p.sc = wbf(sc);
-  if (E) gather_fwd_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(p);
+  HY_CHECK(Hp <= 1024, "egnn_gather_fwd: Hp <= 1024");
+  if (E) gather_fwd_kernel<<<ceil_div(E, GE), 256, 0, stream()>>>(p);
 }
 
 void egnn_agg_fwd(const at::Tensor& m, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
@@ -394,7 +451,7 @@ void egnn_agg_fwd(const at::Tensor& m, const at::Tensor& srp, const c10::optiona
   chk_rows(pos_out, N, 3, at::kFloat, "pos_out");
   chk_rows(geo, E, 4, at::kFloat, "geo");
   HY_CHECK_I32(srp);
-  HY_CHECK(srp.numel() == N + 1, "egnn_agg_fwd: srp length");
+  HY_CHECK(srp.numel() == N + 1 && Hp <= 1024, "egnn_agg_fwd: srp length, Hp <= 1024");
   AggFwd p{};
   p.m = cbf(m);
   p.srp = srp.data_ptr<int>();

@@ -88,11 +88,9 @@ def _slab(dev, numel):
 
 
 def splits_for(M, tiles):
-    """Row splits of a weight-gradient product: ~2 workgroups per CU, >= 2 K-steps each."""
-    s = max(1, min(64, (512 + tiles - 1) // tiles))
-    while s > 1 and M / s < 128:
-        s //= 2
-    return s
+    """Row splits of a weight-gradient product: ~1.5 workgroups per CU and >= 8 K-steps
+    (512 rows) per split (fewer slabs for the reduce to read)."""
+    return max(1, min(64, (384 + tiles - 1) // tiles, M // 512))
 
 
 def wgrad(G, X, Np, Kp, outs, *, X2=None, kc1=None, beta=0.0):

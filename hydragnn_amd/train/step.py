@@ -237,6 +237,14 @@ class TrainStep:
         flag = os.environ.get("HYDRA_MULTIBRANCH_CAPTURE", "auto")
         if flag in ("0", "1"):
             return flag == "1"
+        from ..ops.linear import get_precision
+
+        # bf16: shared-MLP node heads decode branch-grouped (ops.bgemm.branch_mlp: each row
+        # through its own branch only), so the captured step wins at any size (EGNN-866:
+        # 9.2 ms captured vs 12.1 ms eager on MI355X, profiles/r3_bench_multibranch_egnn.log)
+        nh = getattr(m, "config_heads", {}).get("node")
+        if get_precision() == "bf16" and (nh is None or nh[0]["architecture"].get("type") == "mlp"):
+            return True
         return sum(p.numel() for p in m.parameters()) < 8_000_000
 
     # ------------------------------------------------------------------ eager
