@@ -425,6 +425,39 @@ def _aggr_backend_body(rank, world):
     os.environ.pop("HYDRAGNN_AGGR_BACKEND")
 
 
+def _multibranch_capture_body(rank, world):
+    """Captured-step (statically padded, dense / grouped multi-branch decode, bucketed
+    gradient sync) on 4 ranks == the rank average of the eager per-branch-range gradients."""
+    import copy
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_multibranch_capture import _data, _model
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.train.step import TrainStep, batch_loss
+
+    samples = _data(24)
+    model = _model("EGNN")
+    ref = copy.deepcopy(model)
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph", "node"], head_dims=[1, 1])
+    step = TrainStep(model, lr=0.0, mode="graph", world=world, node_bucket=64, edge_bucket=256,
+                     bucket_cap_mb=0.004)
+    assert step.mode == "graph" and len(step.sync.buckets) > 1
+    idx = [6 * rank + k for k in range(6)]
+    step(store, idx)
+    batch = store.batch(idx)  # eager: branch-sorted ranges decode
+    loss, _ = batch_loss(ref, ref(batch), batch)
+    loss.backward()
+    local = torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel())
+                       for p in ref.parameters() if p.requires_grad])
+    allg = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(allg, local)
+    want = sum(allg) / world
+    got = torch.cat([p.grad.reshape(-1) for p in step.module.parameters() if p.requires_grad])
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-5)
+
+
 # ---------------------------------------------------------------------------- tests
 
 def test_ddp_bucketed_allreduce_matches_full_batch():
@@ -465,6 +498,10 @@ def test_timer_reduction_with_rank_specific_timers():
 
 def test_raw_file_count_check():
     run_ranks("_filecount_body")
+
+
+def test_captured_multibranch_four_ranks_matches_eager():
+    run_ranks("_multibranch_capture_body", world=4)
 
 
 def test_task_parallel_multibranch_four_ranks():
