@@ -356,13 +356,12 @@ class Base(nn.Module):
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
             width = head_dim * (1 + self.var_output)
             rows, ids = (x_graph, dn) if t == "graph" else (x, dn_node)
-            if t != "graph":
-                ob = self._grouped_node_heads(headloc, x, ids, data)
-                if ob is not None:
-                    out = _zero_rows(ob, ids >= 0)
-                    outputs.append(out[:, :head_dim])
-                    outputs_var.append(out[:, head_dim:] ** 2)
-                    continue
+            ob = self._grouped_heads(t, headloc, rows, ids, data)
+            if ob is not None:
+                out = _zero_rows(ob, ids >= 0)
+                outputs.append(out[:, :head_dim])
+                outputs_var.append(out[:, head_dim:] ** 2)
+                continue
             out = rows.new_zeros((rows.shape[0], width))
             for bt in self.branch_names():
                 ID = int(bt.split("-")[1])
@@ -377,24 +376,30 @@ class Base(nn.Module):
             return outputs, outputs_var
         return outputs
 
-    def _grouped_node_heads(self, headloc, x, ids, data):
-        """bf16 precision, rows grouped by branch: every branch's shared-MLP node head in
-        one branch-grouped GEMM per layer (``ops.bgemm.branch_mlp``) instead of every head
-        on every row; None when not applicable."""
+    def _grouped_heads(self, t, headloc, rows, ids, data):
+        """bf16 precision, rows grouped by branch: every branch's head chain (graph heads:
+        shared MLP + head MLP; node heads: the shared-MLP node head) in one branch-grouped
+        GEMM per layer (``ops.bgemm.branch_mlp``) instead of every head on every row; None
+        when not applicable."""
         from ..ops.linear import get_precision
 
-        if not (x.is_cuda and get_precision() == "bf16" and data.get("branch_sorted")):
+        if not (rows.is_cuda and get_precision() == "bf16" and data.get("branch_sorted")):
             return None
-        nt = self.config_heads["node"][0]["architecture"]["type"]
         names = self.branch_names()
-        if nt != "mlp" or [int(b.split("-")[1]) for b in names] != list(range(len(names))):
+        if [int(b.split("-")[1]) for b in names] != list(range(len(names))):
             return None
+        if t == "graph":
+            chains = [list(self.graph_shared[bt]) + list(headloc[bt]) for bt in names]
+        else:
+            if self.config_heads["node"][0]["architecture"]["type"] != "mlp":
+                return None
+            chains = [list(headloc[bt].mlp[0]) for bt in names]
         from ..ops import bgemm
 
         nb = len(names)
         bid = torch.where(ids < 0, torch.full_like(ids, nb - 1), ids).to(torch.int32)
         boff = bgemm.branch_offsets(bid, nb)
-        return bgemm.branch_mlp(x, [headloc[bt].mlp[0] for bt in names], bid, boff)
+        return bgemm.branch_mlp(rows, chains, bid, boff)
 
     def decode(self, x, equiv, ctx):
         data = ctx.data

@@ -80,3 +80,33 @@ def test_multibranch_capture_policy(monkeypatch):
 @pytest.mark.parametrize("mt", ["EGNN", "MACE"])
 def test_multibranch_captured_step_equals_eager_gpu(mt):
     _compare(mt, "cuda", 2e-3)
+
+
+@pytest.mark.gpu
+def test_multibranch_bf16_grouped_heads_captured_vs_eager_gpu():
+    """bf16: the captured step decodes branch-grouped (ops.bgemm.branch_mlp for graph and
+    node heads, rows sorted by branch) on the wide-EGNN encoder; the eager step decodes
+    per-branch ranges with BF16Linear.  Same losses within bf16 tolerance."""
+    from hydragnn_amd.ops.linear import precision
+
+    heads = {"graph": [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 32,
+                                                                  "num_headlayers": 2, "dim_headlayers": [160, 160]}}
+                       for b in range(NB)],
+             "node": [{"type": f"branch-{b}", "architecture": {"num_headlayers": 2, "dim_headlayers": [160, 160],
+                                                                 "type": "mlp"}} for b in range(NB)]}
+    with precision("bf16"):
+        torch.manual_seed(0)
+        m1 = create_model("EGNN", 1, 128, [1, 1], 2, "", "multihead", 1, ["graph", "node"], heads, "relu", "mse",
+                          [1.0, 1.0], 2, edge_dim=None, dropout=0.0, radius=5.0, max_neighbours=8,
+                          equivariance=True).cuda()
+        m2 = copy.deepcopy(m1)
+        samples = _data()
+        store = DeviceGraphStore(samples, "cuda", head_types=["graph", "node"], head_dims=[1, 1])
+        eager = TrainStep(m1, lr=1e-3, mode="eager")
+        cap = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=256)
+        assert cap.mode == "graph"
+        rng = np.random.default_rng(0)
+        for _ in range(4):
+            idx = list(rng.choice(len(samples), 6, replace=False))
+            le, lc = float(eager(store, idx)[0]), float(cap(store, idx)[0])
+            assert abs(le - lc) <= 3e-2 * max(1.0, abs(le)), (le, lc)

@@ -11,4 +11,4 @@ for cap in 0 1; do
 done
 timeout -k 10 300 python3 -u tools/bench_configs.py multibranch_egnn --steps 10 --warmup 3 --precision fp32 > gpurun_out/egnn_fp32.log 2>&1 || exit $?
 echo "fp32 $(grep metric gpurun_out/egnn_fp32.log | cut -c1-260)"
-HYDRA_MULTIBRANCH_CAPTURE=${1:-0} bash tools/gpu_prof_cfg.sh multibranch_egnn bf16 || exit $?
+HYDRA_MULTIBRANCH_CAPTURE=${1:-auto} bash tools/gpu_prof_cfg.sh multibranch_egnn bf16 || exit $?
