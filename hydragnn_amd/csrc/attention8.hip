@@ -328,7 +328,7 @@ __device__ __forceinline__ SpanR<RT> span_rt(int base, int i, int N, const int* 
 }
 
 template <int RT>
-__global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
+__device__ __forceinline__ void attn8_bwd_dq_body(int bx, 
     const float* __restrict__ Qp, const float* __restrict__ Kp, const float* __restrict__ Kq,
     const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ LSE2,
     const float* __restrict__ delta, int N, int Nq, int H, const int* __restrict__ seg_id,
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
     int64_t sstride) {
   const int h = blockIdx.y, sp_ = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const SpanR<RT> sp = span_rt<RT>(blockIdx.x * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
+  const SpanR<RT> sp = span_rt<RT>(bx * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
   float bq0[RT], bq1[RT], bo0[RT], bo1[RT], nlse[RT], ndl[RT];
   f4v dq[RT];
 #pragma unroll
@@ -394,6 +394,17 @@ __global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
   }
 }
 
+template <int RT>
+__global__ void __launch_bounds__(256) attn8_bwd_dq_kernel(
+    const float* __restrict__ Qp, const float* __restrict__ Kp, const float* __restrict__ Kq,
+    const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ LSE2,
+    const float* __restrict__ delta, int N, int Nq, int H, const int* __restrict__ seg_id,
+    const int* __restrict__ seg_ptr, int S, float scale, float qscale, float* __restrict__ out, int ldo,
+    int64_t sstride) {
+  attn8_bwd_dq_body<RT>(blockIdx.x, Qp, Kp, Kq, Vp, dOp, LSE2, delta, N, Nq, H, seg_id, seg_ptr, S, scale, qscale, out, ldo, sstride);
+}
+
+
 // dK/dV pass: grid (ceil(N/64) key blocks, H, S over queries).  Outputs dK (x scale) at
 // out + s * sstride + k * ldo + h * 8 and dV at the same + 8H.  Operands two tiles ahead in
 // flight, as in the dQ pass.
@@ -424,7 +435,7 @@ __device__ __forceinline__ KV8b ld_kvb(const float* __restrict__ Qp, const float
 }
 
 template <int RT>
-__global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
+__device__ __forceinline__ void attn8_bwd_dkv_body(int bx, 
     const float* __restrict__ Qp, const float* __restrict__ Qq, const float* __restrict__ Kp,
     const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ dOq,
     const float* __restrict__ LSE2, const float* __restrict__ delta, int N, int Nq, int H,
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
   const int h = blockIdx.y, sp_ = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
   // keys and queries share segments: the key rows' spans are the query ranges to visit
-  const SpanR<RT> sp = span_rt<RT>(blockIdx.x * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
+  const SpanR<RT> sp = span_rt<RT>(bx * 64 * RT + 16 * RT * w, i, N, seg_id, seg_ptr, S, sp_);
   float bk0[RT], bk1[RT], bv0[RT], bv1[RT];
   f4v dk[RT], dv[RT];
 #pragma unroll
@@ -500,7 +511,44 @@ __global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
   }
 }
 
+template <int RT>
+__global__ void __launch_bounds__(256) attn8_bwd_dkv_kernel(
+    const float* __restrict__ Qp, const float* __restrict__ Qq, const float* __restrict__ Kp,
+    const float* __restrict__ Vp, const float* __restrict__ dOp, const float* __restrict__ dOq,
+    const float* __restrict__ LSE2, const float* __restrict__ delta, int N, int Nq, int H,
+    const int* __restrict__ seg_id, const int* __restrict__ seg_ptr, int S, float scale, float qscale,
+    float* __restrict__ out, int ldo, int64_t sstride) {
+  attn8_bwd_dkv_body<RT>(blockIdx.x, Qp, Qq, Kp, Vp, dOp, dOq, LSE2, delta, N, Nq, H, seg_id, seg_ptr, S, scale, qscale, out, ldo, sstride);
+}
+
+
 // dqkv [N, 3F] = [sum_s dQ_s | sum_s dKV_s] over split partials (fixed order)
+// dQ and dK/dV passes in ONE launch: blocks [0, nbq) run the dQ body, the rest the dK/dV
+// body (they only share read-only inputs).  Each pass alone leaves most of the chip idle
+// in its tail; one grid lets the two overlap without a second stream.
+struct A8Bwd {
+  const float *Qp, *Qq, *Kp, *Kq, *Vp, *dOp, *dOq, *LSE2, *delta;
+  int N, Nq, H;
+  const int *seg_id, *seg_ptr;
+  int S;
+  float scale, qscale;
+  float *out_q, *out_kv;
+  int ldq, ldkv;
+  int64_t sq, skv;
+  int nbq;
+};
+
+template <int RT>
+__global__ void __launch_bounds__(256) attn8_bwd_fused_kernel(A8Bwd a) {
+  if ((int)blockIdx.x < a.nbq) {
+    attn8_bwd_dq_body<RT>(blockIdx.x, a.Qp, a.Kp, a.Kq, a.Vp, a.dOp, a.LSE2, a.delta, a.N, a.Nq, a.H, a.seg_id,
+                          a.seg_ptr, a.S, a.scale, a.qscale, a.out_q, a.ldq, a.sq);
+  } else {
+    attn8_bwd_dkv_body<RT>(blockIdx.x - a.nbq, a.Qp, a.Qq, a.Kp, a.Vp, a.dOp, a.dOq, a.LSE2, a.delta, a.N, a.Nq,
+                           a.H, a.seg_id, a.seg_ptr, a.S, a.scale, a.qscale, a.out_kv, a.ldkv, a.skv);
+  }
+}
+
 __global__ void __launch_bounds__(256) attn8_bwd_sum_kernel(const float4* __restrict__ pq, int Sq,
                                                             const float4* __restrict__ pkv, int Skv,
                                                             float4* __restrict__ dqkv, int N, int F) {
@@ -715,23 +763,55 @@ at::Tensor attn8_bwd_sum(const at::Tensor& pq, const at::Tensor& pkv) {
   return dqkv;
 }
 
-// single-stream composition of the parts
+// single-stream composition: prep, ONE fused dQ + dK/dV launch, partial sum
 at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor& LSE2, const at::Tensor& Qp,
                      const at::Tensor& Qq, const at::Tensor& Kp, const at::Tensor& Kq, const at::Tensor& Vp,
                      const at::Tensor& seg_id, const at::Tensor& seg_ptr, double scale, int64_t splits) {
-  const int64_t H = Qp.size(0), Nq = Qp.size(1), N = dO.size(0);
+  const int64_t H = Qp.size(0), Nq = Qp.size(1), N = dO.size(0), F = 8 * H;
   auto pre = attn8_bwd_prep(dO, O, Nq, H);
+  chk_bwd(Qp, LSE2, pre[0], pre[1], N);
+  chk_seg(seg_id, seg_ptr, N);
+  HY_CHECK(Qq.numel() == Qp.numel() && pre[2].numel() == pre[1].numel(), "attn8_bwd: quad operand shapes");
   const int S = pick_splits((int)N, (int)H, splits);
+  at::Tensor dqkv, pq, pkv;
+  A8Bwd a{};
   if (S == 1) {
-    auto dqkv = at::empty({N, 24 * H}, dO.options());
-    attn8_bwd_dq(Qp, Kp, Kq, Vp, pre[1], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, dqkv);
-    attn8_bwd_dkv(Qp, Qq, Kp, Vp, pre[1], pre[2], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, dqkv);
-    return dqkv;
+    dqkv = at::empty({N, 3 * F}, dO.options());
+    a.out_q = dqkv.data_ptr<float>();
+    a.out_kv = dqkv.data_ptr<float>() + F;
+    a.ldq = a.ldkv = (int)(3 * F);
+  } else {
+    pq = at::empty({S, N, F}, dO.options());
+    pkv = at::empty({S, N, 2 * F}, dO.options());
+    a.out_q = pq.data_ptr<float>();
+    a.out_kv = pkv.data_ptr<float>();
+    a.ldq = (int)F;
+    a.ldkv = (int)(2 * F);
+    a.sq = N * F;
+    a.skv = N * 2 * F;
   }
-  auto pq = attn8_bwd_dq(Qp, Kp, Kq, Vp, pre[1], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits, c10::nullopt);
-  auto pkv = attn8_bwd_dkv(Qp, Qq, Kp, Vp, pre[1], pre[2], LSE2, pre[0], seg_id, seg_ptr, N, scale, splits,
-                           c10::nullopt);
-  return attn8_bwd_sum(pq, pkv);
+  if (N == 0) return S == 1 ? dqkv : at::zeros({N, 3 * F}, dO.options());
+  a.Qp = Qp.data_ptr<float>();
+  a.Qq = Qq.data_ptr<float>();
+  a.Kp = Kp.data_ptr<float>();
+  a.Kq = Kq.data_ptr<float>();
+  a.Vp = Vp.data_ptr<float>();
+  a.dOp = pre[1].data_ptr<float>();
+  a.dOq = pre[2].data_ptr<float>();
+  a.LSE2 = LSE2.data_ptr<float>();
+  a.delta = pre[0].data_ptr<float>();
+  a.N = (int)N;
+  a.Nq = (int)Nq;
+  a.H = (int)H;
+  a.seg_id = seg_id.data_ptr<int>();
+  a.seg_ptr = seg_ptr.data_ptr<int>();
+  a.S = S;
+  a.scale = (float)scale;
+  a.qscale = (float)scale * kLog2e;
+  a.nbq = ceil_div(N, 64 * kRT);
+  dim3 grid(2 * a.nbq, H, S);
+  attn8_bwd_fused_kernel<kRT><<<grid, 256, 0, stream()>>>(a);
+  return S == 1 ? dqkv : attn8_bwd_sum(pq, pkv);
 }
 
 }  // namespace a8

@@ -389,9 +389,13 @@ class Base(nn.Module):
         if [int(b.split("-")[1]) for b in names] != list(range(len(names))):
             return None
         if t == "graph":
-            chains = [list(self.graph_shared[bt]) + list(headloc[bt]) for bt in names]
+            shared = getattr(self, "graph_shared", None)
+            if shared is None or any(bt not in shared or bt not in headloc for bt in names):
+                return None
+            chains = [list(shared[bt]) + list(headloc[bt]) for bt in names]
         else:
-            if self.config_heads["node"][0]["architecture"]["type"] != "mlp":
+            if self.config_heads["node"][0]["architecture"]["type"] != "mlp" or \
+                    any(bt not in headloc or not hasattr(headloc[bt], "mlp") for bt in names):
                 return None
             chains = [list(headloc[bt].mlp[0]) for bt in names]
         from ..ops import bgemm
@@ -532,6 +536,10 @@ class Base(nn.Module):
         if not (self.training and self.num_heads == 1 and self.head_type[0] == "graph" and self.num_branches == 1
                 and not self.var_output and self.loss_weights[0] == 1.0 and data.get("targets") is not None
                 and data.get("graph_si") is not None and self._dev_type() == "cuda"):
+            return None
+        # stacks with their own decoder (MACE readouts) or forward do not qualify
+        if type(self).forward is not Base.forward or type(self).decode is not Base.decode or \
+                "branch-0" not in getattr(self, "graph_shared", {}):
             return None
         target = data.targets[0]
         mask = data.get("graph_mask")

@@ -129,7 +129,7 @@ def interaction_graph_static(pos, data, r, max_num_neighbors=None):
         dst = torch.full((Ecap,), dummy, dtype=torch.int32)
         src[:E], dst[:E] = src_v.int(), dst_v.int()
     drp = rowptr.clone()
-    drp[N] = Ecap  # the padding slots belong to the last (padding) receiver
+    drp[N:].fill_(Ecap)  # the padding slots belong to the last (padding) receiver (device fill: capturable)
     scnt = torch.zeros(N, dtype=torch.int32, device=src.device).index_add_(
         0, src.long(), torch.ones(Ecap, dtype=torch.int32, device=src.device))
     srp = torch.cat([scnt.new_zeros(1), torch.cumsum(scnt, 0, dtype=torch.int32)])
