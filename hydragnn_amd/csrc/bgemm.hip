@@ -487,9 +487,14 @@ __global__ __launch_bounds__(256) void tn_kernel(TNArgs p) {
 
 // out[n][k] (n < N, k < K) = beta * out + sum_s slab[s][n0 + n][k];  bias_out[n] likewise
 // from slab column bias_col.
+// blockIdx.y = group (the per-branch problems of a grouped weight gradient): slab, out and
+// bias_out advance by gslab / gout / gbias elements per group
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Np, int Kp, int n0, int k0, int N, int K,
                                    float* __restrict__ out, int ldo, int ldk, float beta, int bias_col,
-                                   float* __restrict__ bias_out) {
+                                   float* __restrict__ bias_out, int64_t gslab, int64_t gout, int64_t gbias) {
+  slab += blockIdx.y * gslab;
+  out += blockIdx.y * gout;
+  if (bias_out) bias_out += blockIdx.y * gbias;
   // threads [0, N * KQ): 4 consecutive columns each (16-byte slab loads, 4 slabs in flight);
   // threads [N * KQ, N * KQ + N): the bias column
   const int KQ = (K + 3) / 4;
@@ -755,7 +760,8 @@ void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Ten
 }
 
 void bg_slab_reduce(const at::Tensor& slab, int64_t S, int64_t Np, int64_t Kp, int64_t n0, int64_t k0, int64_t N, int64_t K,
-                    const at::Tensor& out, double beta, int64_t bias_col, const c10::optional<at::Tensor>& bias_out) {
+                    const at::Tensor& out, double beta, int64_t bias_col, const c10::optional<at::Tensor>& bias_out,
+                    int64_t groups) {
   HY_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) >= N && out.size(1) >= K,
            "bg_slab_reduce: out");
   HY_CHECK(n0 + N <= Np && k0 + K <= Kp && bias_col < Kp && Kp % 4 == 0 && k0 % 4 == 0, "bg_slab_reduce: bounds");
@@ -765,11 +771,14 @@ void bg_slab_reduce(const at::Tensor& slab, int64_t S, int64_t Np, int64_t Kp, i
              "bg_slab_reduce: bias_out");
     bo = bias_out->data_ptr<float>();
   }
+  // groups > 1: out is [groups, N, K] (contiguous per group), bias_out [groups, N]
+  HY_CHECK(groups >= 1 && (groups == 1 || (out.numel() >= groups * N * K && slab.numel() >= groups * S * Np * Kp)),
+           "bg_slab_reduce: groups");
   const int64_t total = N * ((K + 3) / 4) + N;
   const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
-  slab_reduce_kernel<<<blocks, 256, 0, stream()>>>(slab.data_ptr<float>(), (int)S, (int)Np, (int)Kp, (int)n0,
-                                                   (int)k0, (int)N, (int)K, out.data_ptr<float>(), (int)out.stride(0),
-                                                   (int)out.stride(1), (float)beta, (int)bias_col, bo);
+  slab_reduce_kernel<<<dim3(blocks, (unsigned)groups), 256, 0, stream()>>>(
+      slab.data_ptr<float>(), (int)S, (int)Np, (int)Kp, (int)n0, (int)k0, (int)N, (int)K, out.data_ptr<float>(),
+      (int)out.stride(0), (int)out.stride(1), (float)beta, (int)bias_col, bo, S * Np * Kp, N * K, N);
 }
 
 void bg_cast_pad(const at::Tensor& x, const at::Tensor& out, const c10::optional<at::Tensor>& gate, int64_t ones_col) {
@@ -850,7 +859,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("bg_tn(Tensor G, Tensor X, Tensor? X2, int kc1, int Np, int Kp, Tensor slab, int splits, Tensor? boff=None) -> ()");
   m.def(
       "bg_slab_reduce(Tensor slab, int S, int Np, int Kp, int n0, int k0, int N, int K, Tensor out, float beta, int bias_col, "
-      "Tensor? bias_out) -> ()");
+      "Tensor? bias_out, int groups=1) -> ()");
   m.def("bg_cast_pad(Tensor x, Tensor out, Tensor? gate, int ones_col) -> ()");
   m.def("bg_cast_weights(Tensor[] srcs, Tensor[] dsts, Tensor[] dstTs) -> ()");
 }

@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
                                                       float* __restrict__ out, int N, int F,
                                                       int tpr, int rpb,
                                                       const float* __restrict__ w = nullptr,
-                                                      const int* __restrict__ gidx = nullptr, int ldo = 0) {
+                                                      const int* __restrict__ gidx = nullptr, int ldo = 0,
+                                                      const int* __restrict__ row_limit = nullptr) {
   using V = VecT<VEC>;
   using T = typename V::T;
   const int tg = tpr * KS;
@@ -85,7 +86,10 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
   const int lt = threadIdx.x % tg;
   const int c = lt % tpr, k = lt / tpr;
   if (r >= N) return;
-  const int beg = rowptr[r], end = rowptr[r + 1];
+  // row_limit (device scalar, e.g. the padded batch's valid-node count): rows past it are
+  // padding; the padding graph's long tail segment is then empty instead of serial work
+  const int end = row_limit ? min(rowptr[r + 1], *row_limit) : rowptr[r + 1];
+  const int beg = min(rowptr[r], end);
   const int nv = F / VEC;
   const float inv = MEAN ? 1.f / (float)max(end - beg, 1) : 1.f;
   for (int v = c; v < nv; v += tpr) {
@@ -203,7 +207,7 @@ __global__ void __launch_bounds__(256) gather_mul2_kernel(const float* __restric
 static at::Tensor as2d(const at::Tensor& x) { return x.dim() == 1 ? x.unsqueeze(1) : x; }
 
 at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm,
-                   int64_t N, bool mean) {
+                   int64_t N, bool mean, const c10::optional<at::Tensor>& limit) {
   HY_CHECK_CUDA(x_);
   auto x = as2d(x_).contiguous();
   HY_CHECK_F32(x);
@@ -217,6 +221,13 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
     HY_CHECK_I32(*perm);
     pp = perm->data_ptr<int>();
   }
+  const int* lim = nullptr;
+  if (limit.has_value() && limit->defined()) {
+    HY_CHECK(limit->is_cuda() && limit->scalar_type() == at::kInt && limit->numel() == 1,
+             "seg_sum: limit must be a device int32 scalar");
+    HY_CHECK(!pp, "seg_sum: a row limit needs rows in segment order (no perm)");
+    lim = limit->data_ptr<int>();
+  }
   const bool v4 = (F % 4 == 0);
   // wide odd-multiple-of-2 rows (the SC25 EGNN's 866 channels): float2 loads halve the
   // per-column dependent load chains of the scalar path
@@ -228,7 +239,8 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   const int blocks = (int)std::max<int64_t>(1, (N + rpb - 1) / rpb);
 #define HY_SEG_SUM(VEC, MEAN, KS)                                                                              \
   seg_sum_kernel<VEC, MEAN, KS><<<blocks, 256, 0, stream()>>>(x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, \
-                                                              out.data_ptr<float>(), N, F, g.tpr, rpb)
+                                                              out.data_ptr<float>(), N, F, g.tpr, rpb, nullptr,  \
+                                                              nullptr, 0, lim)
 #define HY_SEG_SUM_KS(VEC, MEAN) \
   if (ks == 4) HY_SEG_SUM(VEC, MEAN, 4); else if (ks == 2) HY_SEG_SUM(VEC, MEAN, 2); else HY_SEG_SUM(VEC, MEAN, 1)
   if (v4) {
@@ -416,7 +428,7 @@ at::Tensor gather_arg(const at::Tensor& x_, const at::Tensor& arg) {
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("seg_sum(Tensor x, Tensor rowptr, Tensor? perm, int N, bool mean) -> Tensor");
+  m.def("seg_sum(Tensor x, Tensor rowptr, Tensor? perm, int N, bool mean, Tensor? limit=None) -> Tensor");
   m.def("gather_rows(Tensor x, Tensor idx) -> Tensor");
   m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
   m.def("scatter_arg(Tensor g, Tensor arg, int E) -> Tensor");

@@ -413,7 +413,8 @@ class Base(nn.Module):
         elif gsi is None:
             x_graph = x.mean(dim=0, keepdim=True)
         else:
-            x_graph = seg.segment_mean(x, gsi)
+            # padded batch: padding rows are zero; the limit skips the padding graph's tail
+            x_graph = seg.segment_mean(x, gsi, limit=data.get("num_valid"))
         outputs, outputs_var = [], []
         nb = self.num_branches
         if nb > 1 and data.get("branch_graph_ranges") is not None:

@@ -242,13 +242,14 @@ class _BranchMLP(torch.autograd.Function):
             Np, Kp = kps[l + 1], kps[l]
             slab = _slab(dev, nb * S * Np * Kp)
             _native.ops().bg_tn(g, hs[l], None, Kp, Np, Kp, slab, S, boff)
+            # every branch's weight and bias gradient in ONE grouped reduce launch
+            dW = torch.empty((nb, dims[l + 1], dims[l]), device=dev, dtype=torch.float32)
+            db = torch.empty((nb, dims[l + 1]), device=dev, dtype=torch.float32)
+            _native.ops().bg_slab_reduce(slab, S, Np, Kp, 0, 0, dims[l + 1], dims[l], dW.view(-1, dims[l]), 0.0,
+                                         dims[l], db.view(-1), nb)
             for b in range(nb):
-                dW = torch.empty((dims[l + 1], dims[l]), device=dev, dtype=torch.float32)
-                db = torch.empty(dims[l + 1], device=dev, dtype=torch.float32)
-                _native.ops().bg_slab_reduce(slab[b * S * Np * Kp:], S, Np, Kp, 0, 0, dims[l + 1], dims[l], dW, 0.0,
-                                             dims[l], db)
-                grads[(l * 2) * nb + b] = dW
-                grads[(l * 2 + 1) * nb + b] = db
+                grads[(l * 2) * nb + b] = dW[b]
+                grads[(l * 2 + 1) * nb + b] = db[b]
             if l > 0:
                 gn = torch.empty((M, Kp), device=dev, dtype=torch.bfloat16)
                 _native.ops().bg_nt(g, None, Np, imgTs[l][0], Np, dims[l], None, 0, hs[l] if relu[l - 1] else None,

@@ -125,18 +125,19 @@ class _Gather(torch.autograd.Function):
 
 class _SegSum(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, si):
+    def forward(ctx, x, si, limit=None):
         ctx.si = si
         if _use_native(x) and x.dtype == torch.float32:
             tail = x.shape[1:]
+            lim = limit if (limit is not None and si.perm is None and limit.dtype == torch.int32) else None
             out = _native.ops().seg_sum(x.reshape(x.shape[0], _width(tail)), si.rowptr, si.perm, si.num_segments,
-                                        False)
+                                        False, lim)
             return out.view((si.num_segments,) + tuple(tail))
         return _cpu_segment_sum(x, si)
 
     @staticmethod
     def backward(ctx, g):
-        return _Gather.apply(g, ctx.si), None
+        return _Gather.apply(g, ctx.si), None, None
 
 
 class _ScatterArg(torch.autograd.Function):
@@ -251,12 +252,15 @@ def gather(x, si):
     return _Gather.apply(x, si)
 
 
-def segment_sum(x, si):
-    return _SegSum.apply(x, si)
+def segment_sum(x, si, limit=None):
+    """``limit`` (optional device int32 scalar): rows at or past it are padding and skipped
+    (their values must be zero for the result to be exact; the GPU kernel then does no
+    serial work on the padding graph's long segment)."""
+    return _SegSum.apply(x, si, limit)
 
 
-def segment_mean(x, si):
-    s = _SegSum.apply(x, si)
+def segment_mean(x, si, limit=None):
+    s = _SegSum.apply(x, si, limit)
     deg = si.degree(s.dtype).clamp(min=1.0).to(s.device)
     return s / deg.view(-1, *([1] * (s.dim() - 1)))
 
