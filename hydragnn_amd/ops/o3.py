@@ -419,7 +419,7 @@ class TensorProductUVU(nn.Module):
         from . import pna as _mode
         from . import segment as seg
 
-        if x1_nodes.is_cuda and self.native_ok and x1_nodes.dtype == torch.float32 and _mode.fused("tp") and \
+        if x1_nodes.is_cuda and self.native_ok and x1_nodes.dtype == torch.float32 and _mode.fused("tpconv") and \
                 dst_si.perm is None:
             return _TPConv.apply(x1_nodes.contiguous(), x2.contiguous(), w.contiguous(), self._ins, self._cg,
                                  self.irreps_out.dim, src_si, dst_si)

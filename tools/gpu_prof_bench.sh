@@ -12,3 +12,4 @@ python3 tools/rocpd_summary.py $DB --between spin_kernel --steps 20 --top 60 > $
 python3 tools/rocpd_summary.py $DB --between spin_kernel --sequence 400 > ${OUT}_seq.txt
 tail -3 ${OUT}.log
 head -3 ${OUT}_summary.txt
+rm -rf $OUT

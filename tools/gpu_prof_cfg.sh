@@ -11,3 +11,4 @@ DB=$(find $OUT -name "*.db" | head -1)
 python3 tools/rocpd_summary.py $DB --between spin_kernel --steps 10 --top 40 > ${OUT}_summary.txt
 grep metric ${OUT}.log | cut -c1-200
 head -30 ${OUT}_summary.txt | cut -c1-160
+rm -rf $OUT  # the trace db stays on the box (gpurun_out is copied back only under 64 MiB)
