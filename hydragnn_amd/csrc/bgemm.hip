@@ -25,9 +25,10 @@
 //    Both operands are [M, *] row-major: the reduction index is the row, so fragments
 //    are read with ds_read_b64_tr_b16 (hardware 4x16 transpose) from a 256-byte-row LDS
 //    image with a 32-byte XOR swizzle (slot ^ (m & 3 | (m >> 3 & 1) << 2)), conflict-free
-//    for the transposed reads.  Split over M (rows) to fill the chip; a reduce kernel sums
-//    the slabs into the fp32 parameter gradient (masked, strided, optional accumulate) and
-//    extracts the bias gradient from the ones lane.
+//    for the transposed reads.  Split over M (rows) to fill the chip; the last split block
+//    of each tile to finish (device-scope arrival counter) sums the tile's slabs in split
+//    order — deterministic — into the fp32 parameter gradients (masked, strided, optional
+//    accumulate) and extracts the bias gradient from the ones lane: no reduce launch.
 //  * cast kernels: fp32 activation -> padded bf16 (+ ones lane, optional relu' gate), and
 //    a batched weight caster writing W and W^T padded bf16 images in one launch.
 //
@@ -367,6 +368,16 @@ __global__ __launch_bounds__(BM / 64 * WN * 64) void ntg_kernel(NTArgs p) {
 }
 
 // ------------------------------------------------------------------------------ TN GEMM
+// one destination of a fused weight-gradient reduce: out[n - n0][(k - k0) * ldk] for the
+// slab rectangle [n0, n0 + N) x [k0, k0 + K), bias_out[n - n0] from slab column bias_col;
+// group g (grouped products) writes at out + g * gout, bias_out + g * gbias
+struct TNOut {
+  float* out;
+  float* bias_out;
+  int ldo, ldk, n0, k0, N, K, bias_col;
+  int64_t gout, gbias;
+};
+
 struct TNArgs {
   const uint16_t* G;   // [M, ldg]: output rows n
   const uint16_t* X;   // [M, ldx]: output cols k < kc1
@@ -376,6 +387,12 @@ struct TNArgs {
   float* slab;         // [S][Np][Kp]  ([nb][S][Np][Kp] when grouped)
   const int* boff;     // branch row offsets [nb + 1] (grouped: per-branch G^T X), or null
   int splits;
+  // fused reduce: the last split block of each tile to finish (per-tile arrival counter)
+  // sums the S slab tiles in split order (deterministic) into up to 3 output rectangles
+  int* counters;       // [groups * tiles_nk] zero on entry, left zero on exit; null: slab only
+  int nout;
+  float beta;
+  TNOut outs[3];
 };
 
 __device__ __forceinline__ int t_off(int m, int c16) {
@@ -483,6 +500,48 @@ __global__ __launch_bounds__(256) void tn_kernel(TNArgs p) {
       *reinterpret_cast<float4*>(out + (int64_t)n * p.Kp + k) =
           make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     }
+  if (!p.counters) return;
+  // last-arriver fixup: release the slab tile (device scope: the L2 of another XCD), count
+  // the arrival; the block that completes the tile reduces it
+  __shared__ int last;
+  const int S = p.splits, grp = p.boff ? split / p.splits : 0;
+  const int cid = grp * p.tiles_nk + t;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(p.counters + cid, 1) == S - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const float* base = p.slab + (int64_t)grp * S * p.Np * p.Kp;
+  const int64_t stride = (int64_t)p.Np * p.Kp;
+  for (int idx = tid; idx < 128 * 32; idx += 256) {
+    const int n = n0 + (idx >> 5), k = k0 + (idx & 31) * 4;
+    const float* sp = base + (int64_t)n * p.Kp + k;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s2 = 0; s2 < S; ++s2) {
+      const float4 v = *reinterpret_cast<const float4*>(sp + s2 * stride);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const float av[4] = {a.x, a.y, a.z, a.w};
+    for (int d = 0; d < p.nout; ++d) {
+      const TNOut& o = p.outs[d];
+      if (n < o.n0 || n >= o.n0 + o.N) continue;
+      const int64_t row = n - o.n0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = k + r;
+        if (kk >= o.k0 && kk < o.k0 + o.K) {
+          float* q = o.out + grp * o.gout + row * o.ldo + (int64_t)(kk - o.k0) * o.ldk;
+          *q = av[r] + (p.beta != 0.f ? p.beta * *q : 0.f);
+        }
+        if (kk == o.bias_col && o.bias_out) {
+          float* q = o.bias_out + grp * o.gbias + row;
+          *q = av[r] + (p.beta != 0.f ? p.beta * *q : 0.f);
+        }
+      }
+    }
+  }
+  if (tid == 0) p.counters[cid] = 0;  // ready for the next product on this stream
 }
 
 // out[n][k] (n < N, k < K) = beta * out + sum_s slab[s][n0 + n][k];  bias_out[n] likewise
@@ -719,7 +778,9 @@ void bg_nt(const at::Tensor& A, const c10::optional<at::Tensor>& A2, int64_t k1,
 
 // slab[S][Np][Kp] = split-M partial sums of G^T [X | X2]
 void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Tensor>& X2, int64_t kc1,
-           int64_t Np, int64_t Kp, const at::Tensor& slab, int64_t splits, const c10::optional<at::Tensor>& boff) {
+           int64_t Np, int64_t Kp, const at::Tensor& slab, int64_t splits, const c10::optional<at::Tensor>& boff,
+           at::TensorList outs, const c10::List<c10::optional<at::Tensor>>& bias_outs, at::IntArrayRef meta,
+           double beta, const c10::optional<at::Tensor>& counters) {
   check_bf(G, "G");
   check_bf(X, "X");
   const int64_t M = G.size(0);
@@ -755,6 +816,44 @@ void bg_tn(const at::Tensor& G, const at::Tensor& X, const c10::optional<at::Ten
   p.tiles_k = (int)(Kp / 128);
   p.tiles_nk = (int)((Np / 128) * p.tiles_k);
   p.slab = slab.data_ptr<float>();
+  // fused reduce destinations: meta = (n0, k0, N, K, bias_col) per output (per group when
+  // grouped: the output view is [groups * N, K], the bias [groups * N])
+  HY_CHECK(outs.size() <= 3 && (int64_t)bias_outs.size() == (int64_t)outs.size() &&
+               (int64_t)meta.size() == 5 * (int64_t)outs.size(),
+           "bg_tn: at most 3 outputs with (n0, k0, N, K, bias_col) each");
+  if (!outs.empty()) {
+    HY_CHECK(counters.has_value() && counters->scalar_type() == at::kInt && counters->is_cuda() &&
+                 counters->numel() >= groups * p.tiles_nk,
+             "bg_tn: fused reduce needs an int32 counter buffer (zeroed) of groups * tiles");
+    p.counters = counters->data_ptr<int>();
+    p.nout = (int)outs.size();
+    p.beta = (float)beta;
+    for (size_t d = 0; d < outs.size(); ++d) {
+      const at::Tensor& o = outs[d];
+      TNOut& t = p.outs[d];
+      HY_CHECK(o.scalar_type() == at::kFloat && o.dim() == 2 && o.is_cuda(), "bg_tn: outputs fp32 2-D");
+      t.out = o.data_ptr<float>();
+      t.ldo = (int)o.stride(0);
+      t.ldk = (int)o.stride(1);
+      t.n0 = (int)meta[5 * d];
+      t.k0 = (int)meta[5 * d + 1];
+      t.N = (int)meta[5 * d + 2];
+      t.K = (int)meta[5 * d + 3];
+      t.bias_col = (int)meta[5 * d + 4];
+      HY_CHECK(o.size(0) >= groups * t.N && o.size(1) >= t.K, "bg_tn: output view smaller than (groups * N, K)");
+      HY_CHECK(t.n0 >= 0 && t.k0 >= 0 && t.n0 + t.N <= Np && t.k0 + t.K <= Kp && t.bias_col < Kp,
+               "bg_tn: output rectangle outside the product");
+      t.gout = groups > 1 ? (int64_t)t.N * t.ldo : 0;
+      HY_CHECK(groups == 1 || o.is_contiguous(), "bg_tn: grouped outputs are contiguous [groups * N, K]");
+      const c10::optional<at::Tensor> bo = bias_outs.get(d);
+      if (bo.has_value()) {
+        HY_CHECK(bo->scalar_type() == at::kFloat && bo->is_contiguous() && bo->numel() >= groups * t.N,
+                 "bg_tn: bias_out");
+        t.bias_out = bo->data_ptr<float>();
+        t.gbias = groups > 1 ? t.N : 0;
+      }
+    }
+  }
   const int grid = (int)(p.tiles_nk * splits * groups);
   tn_kernel<<<grid, 256, 0, stream()>>>(p);
 }
@@ -856,7 +955,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "bg_nt(Tensor A, Tensor? A2, int k1, Tensor B, int K, int N, Tensor? bias, int act, Tensor? gate, Tensor? addg, "
       "Tensor? addg_idx, Tensor? outf, float beta, Tensor? outb, int ones_col, Tensor? rowvec, Tensor? rowdot, "
       "int bm, Tensor? bid=None, int bsB=0, int bsbias=0) -> ()");
-  m.def("bg_tn(Tensor G, Tensor X, Tensor? X2, int kc1, int Np, int Kp, Tensor slab, int splits, Tensor? boff=None) -> ()");
+  m.def(
+      "bg_tn(Tensor G, Tensor X, Tensor? X2, int kc1, int Np, int Kp, Tensor slab, int splits, Tensor? boff, "
+      "Tensor[] outs, Tensor?[] bias_outs, int[] meta, float beta, Tensor? counters) -> ()");
   m.def(
       "bg_slab_reduce(Tensor slab, int S, int Np, int Kp, int n0, int k0, int N, int K, Tensor out, float beta, int bias_col, "
       "Tensor? bias_out, int groups=1) -> ()");

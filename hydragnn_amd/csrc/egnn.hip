@@ -6,15 +6,16 @@
 //                (the edge_mlp[0] Linear over cat[x_row, x_col, radial, edge_attr], with its
 //                x blocks evaluated at node level), edge geometry d_e = pos[dst]-pos[src],
 //                cd_e = d_e / (|d_e| + 1), and the bf16 per-edge scalar row [|d|, ea.., 1]
-//   agg_fwd    : agg[n] = sum_{e: src_e = n} m[e] (bf16 rows, fp32 sums) and the coordinate
-//                update pos'[n] = pos[n] + cw * mean_{e: src_e = n} clamp(cd_e tanh(s_e), +-100)
+//   csr_rows   : agg[n] = sum_{e: src_e = n} m[e] forward; dAB = by-source | by-destination
+//                sums of dh1 backward (bf16 rows, fp32 sums, one block per (node, part))
+//   pos_fwd    : pos'[n] = pos[n] + cw * mean_{e: src_e = n} clamp(cd_e tanh(s_e), +-100)
 //   coord_bwd  : d(pos') -> ds_e, dcd_e; dc1 = ds_e wc2 * relu'(c1) (bf16), dwc2 partials
-//   edge_bwd   : dAB (by-source and by-destination CSR sums of dh1, bf16), d|d_e|, the
-//                per-edge position gradient and the column partials of dw_r / dw_j / db1
-//   pos_bwd    : dpos[n] = dpos'[n] + sum_{dst_e = n} dvec_e - sum_{src_e = n} dvec_e
+//   pos_bwd    : dpos[n] = dpos'[n] + sum_{dst_e = n} dvec_e - sum_{src_e = n} dvec_e, the
+//                per-edge dvec_e rebuilt inline from geo, dcd and dr_e = d loss / d|d_e|
+//                (dr comes from the row-dot epilogue of the dh1 GEMM, bgemm.hip)
 //
-// One wave per edge row or node; each lane owns 4 consecutive channels (8-byte bf16 /
-// 16-byte fp32 accesses), looping over the padded width Hp in steps of 256.  Column
+// Edge-row kernels: one wave per edge row; each lane owns 4 consecutive channels (8-byte
+// bf16 / 16-byte fp32 accesses), looping over the padded width Hp in steps of 256.  Column
 // reductions over edges go to per-block partial rows reduced by bg_slab_reduce (no
 // atomics).  Edges are stored sorted by destination (dst CSR is the identity order);
 // the source CSR carries a permutation.
@@ -119,73 +120,7 @@ __global__ __launch_bounds__(256) void gather_fwd_kernel(GatherFwd p) {
   }
 }
 
-struct AggFwd {
-  const uint16_t* m;  // [E, Hp]
-  const int* srp;     // [N + 1] source CSR
-  const int* sperm;   // [E] (null: identity)
-  const float* pos;   // [N, 3]
-  const float* geo;   // [E, 4]
-  const float* s;     // [E] coord_mlp output (pre-tanh), null: no coordinate update
-  float cw;
-  int N, Hp;
-  uint16_t* agg;      // [N, Hp]
-  float* pos_out;     // [N, 3]
-};
-
-// sum of bf16 rows e in [b, eN) (through perm) into 4 float4 accumulators per lane
-// (channels 4l + 256 t), two rows in flight
-__device__ __forceinline__ void rows_sum(const uint16_t* __restrict__ X, int Hp, const int* __restrict__ perm, int b,
-                                         int eN, int lane, float4 (&acc)[4]) {
-  int i = b;
-  for (; i + 1 < eN; i += 2) {
-    const int e0 = perm ? perm[i] : i, e1 = perm ? perm[i + 1] : i + 1;
-    float4 x0[4], x1[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = lane * 4 + t * 256;
-      if (k < Hp) {
-        x0[t] = ld_bf4(X + (int64_t)e0 * Hp + k);
-        x1[t] = ld_bf4(X + (int64_t)e1 * Hp + k);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (lane * 4 + t * 256 < Hp) acc[t] = f4add(acc[t], f4add(x0[t], x1[t]));
-  }
-  if (i < eN) {
-    const int e0 = perm ? perm[i] : i;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = lane * 4 + t * 256;
-      if (k < Hp) acc[t] = f4add(acc[t], ld_bf4(X + (int64_t)e0 * Hp + k));
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void agg_fwd_kernel(AggFwd p) {
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (n >= p.N) return;
-  const int b = p.srp[n], eN = p.srp[n + 1];
-  float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-  rows_sum(p.m, p.Hp, p.sperm, b, eN, lane, acc);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int k = lane * 4 + t * 256;
-    if (k < p.Hp) st_bf4(p.agg + (int64_t)n * p.Hp + k, acc[t].x, acc[t].y, acc[t].z, acc[t].w);
-  }
-  if (p.s && lane < 3) {
-    float t = 0.f;
-    for (int i = b; i < eN; ++i) {
-      const int e = p.sperm ? p.sperm[i] : i;
-      const float u = p.geo[(int64_t)e * 4 + lane] * tanhf(p.s[e]);
-      t += fminf(fmaxf(u, -100.f), 100.f);
-    }
-    const int cnt = eN - b;
-    p.pos_out[n * 3 + lane] = p.pos[n * 3 + lane] + p.cw * t / (float)(cnt > 0 ? cnt : 1);
-  }
-}
-
-constexpr int EPB = 64;  // edges per block (16 per wave) for the column-partial kernels
+constexpr int EPB = 32;  // edges per block (8 per wave) for the column-partial kernels
 
 struct CoordBwd {
   const float* dpos;  // [N, 3] gradient of pos'
@@ -267,105 +202,6 @@ __global__ __launch_bounds__(256) void coord_bwd_kernel(CoordBwd p) {
     p.part[(int64_t)blockIdx.x * p.Hp + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
 }
 
-struct EdgeBwd {
-  const uint16_t* dh1;  // [E, Hp]
-  const int* srp;       // [N + 1] source CSR
-  const int* sperm;     // [E]
-  const int* drp;       // [N + 1] destination CSR (identity order)
-  const float* geo;     // [E, 4]
-  const float* dcd;     // [E, 3] or null
-  const float* W0;      // radial weight column at c0 (row stride ld0)
-  int ld0, c0, N, H, Hp;
-  uint16_t* dAB;        // [N, 2Hp]
-  float* dvec;          // [E, 3]
-};
-
-// one wave per node: by-source sum -> dAB[:, :Hp], by-destination sum -> dAB[:, Hp:], and
-// for each edge of the destination list its d|d| and position gradient.
-__global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwd p) {
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (n >= p.N) return;
-  {
-    float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-    rows_sum(p.dh1, p.Hp, p.sperm, p.srp[n], p.srp[n + 1], lane, acc);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = lane * 4 + t * 256;
-      if (k < p.Hp) st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + k, acc[t].x, acc[t].y, acc[t].z, acc[t].w);
-    }
-  }
-  const int b = p.drp[n], eN = p.drp[n + 1];
-  // radial weights of this lane's channels
-  float wr[4][4];
-#pragma unroll
-  for (int it = 0; it < 4; ++it)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = lane * 4 + it * 256 + r;
-      wr[it][r] = k < p.H ? p.W0[(int64_t)k * p.ld0 + p.c0] : 0.f;
-    }
-  float4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-  float4 nx[4];
-  auto ld_row = [&](int e, float4 (&x)[4]) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int k = lane * 4 + it * 256;
-      if (k < p.Hp) x[it] = ld_bf4(p.dh1 + (int64_t)e * p.Hp + k);
-    }
-  };
-  if (b < eN) ld_row(b, nx);
-  for (int e = b; e < eN; ++e) {
-    float4 x[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) x[it] = nx[it];
-    if (e + 1 < eN) ld_row(e + 1, nx);  // next row in flight while this one reduces
-    float dr = 0.f;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int k = lane * 4 + it * 256;
-      if (k < p.Hp) {
-        acc[it] = f4add(acc[it], x[it]);
-        dr += x[it].x * wr[it][0] + x[it].y * wr[it][1] + x[it].z * wr[it][2] + x[it].w * wr[it][3];
-      }
-    }
-    dr = wave_sum(dr);
-    if (lane < 3) {
-      // d = pos[dst] - pos[src]; |d| = L; cd = d / (L + 1)
-      const float4 g = *reinterpret_cast<const float4*>(p.geo + (int64_t)e * 4);
-      const float L = g.w, s1 = L + 1.f;
-      const float dc[3] = {g.x * s1, g.y * s1, g.z * s1};  // the vector d
-      float gv = 0.f;
-      if (L > 0.f) {
-        gv = dr * dc[lane] / L;
-        if (p.dcd) {
-          const float q0 = p.dcd[(int64_t)e * 3], q1 = p.dcd[(int64_t)e * 3 + 1], q2 = p.dcd[(int64_t)e * 3 + 2];
-          const float dot = q0 * dc[0] + q1 * dc[1] + q2 * dc[2];
-          const float qc = lane == 0 ? q0 : (lane == 1 ? q1 : q2);
-          gv += qc / s1 - dc[lane] * dot / (L * s1 * s1);
-        }
-      }
-      p.dvec[(int64_t)e * 3 + lane] = gv;
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int k = lane * 4 + it * 256;
-    if (k < p.Hp) st_bf4(p.dAB + (int64_t)n * 2 * p.Hp + p.Hp + k, acc[it].x, acc[it].y, acc[it].z, acc[it].w);
-  }
-}
-
-__global__ void pos_bwd_kernel(const float* __restrict__ dpos_out, const float* __restrict__ dvec,
-                               const int* __restrict__ srp, const int* __restrict__ sperm, const int* __restrict__ drp,
-                               int N, float* __restrict__ dpos) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = t / 3, c = t % 3;
-  if (n >= N) return;
-  float v = dpos_out ? dpos_out[n * 3 + c] : 0.f;
-  for (int e = drp[n]; e < drp[n + 1]; ++e) v += dvec[(int64_t)e * 3 + c];
-  for (int i = srp[n]; i < srp[n + 1]; ++i) v -= dvec[(int64_t)(sperm ? sperm[i] : i) * 3 + c];
-  dpos[n * 3 + c] = v;
-}
-
 // out[e] = g[idx[e], :H] * (gate[e] > 0) as padded bf16 (the non-equivariant layer's
 // dZ2 = dagg[src] * relu'(m): no coordinate GEMM to carry the gather in its epilogue)
 __global__ __launch_bounds__(256) void gather_gate_kernel(const float* __restrict__ g, int ldg,
@@ -382,6 +218,110 @@ __global__ __launch_bounds__(256) void gather_gate_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = (k + r < H && qv[r] > 0.f) ? row[k + r] : 0.f;
     st_bf4(out + (int64_t)e * Hp + k, v[0], v[1], v[2], v[3]);
+  }
+}
+
+// ---------------------------------------------------------------- CSR row sums (bf16 rows)
+// out[n, off_p + k] = sum_{i in segment n of CSR p} X[perm_p ? perm_p[i] : i, k]; one 256-thread
+// block per (node, part), wave q owns channels [256 q, 256 q + 256) (4 per lane), 4 rows in
+// flight: ~16 waves per SIMD on the EGNN shapes instead of one wave per node.
+struct CsrParts {
+  const uint16_t* X;
+  int Hp;
+  const int* rp[2];
+  const int* perm[2];
+  int off[2];
+  uint16_t* out;
+  int ldo;
+};
+
+__global__ __launch_bounds__(256) void csr_rows_kernel(CsrParts p) {
+  const int n = blockIdx.x, part = blockIdx.y, lane = threadIdx.x & 63;
+  const int k = (threadIdx.x >> 6) * 256 + lane * 4;
+  if (k >= p.Hp) return;
+  const int* rp = p.rp[part];
+  const int* pm = p.perm[part];
+  const int b = rp[n], eN = rp[n + 1];
+  float4 a0 = f4zero(), a1 = f4zero();
+  int i = b;
+  for (; i + 3 < eN; i += 4) {
+    const int e0 = pm ? pm[i] : i, e1 = pm ? pm[i + 1] : i + 1, e2 = pm ? pm[i + 2] : i + 2,
+              e3 = pm ? pm[i + 3] : i + 3;
+    const float4 x0 = ld_bf4(p.X + (int64_t)e0 * p.Hp + k), x1 = ld_bf4(p.X + (int64_t)e1 * p.Hp + k);
+    const float4 x2 = ld_bf4(p.X + (int64_t)e2 * p.Hp + k), x3 = ld_bf4(p.X + (int64_t)e3 * p.Hp + k);
+    a0 = f4add(a0, f4add(x0, x1));
+    a1 = f4add(a1, f4add(x2, x3));
+  }
+  for (; i < eN; ++i) a0 = f4add(a0, ld_bf4(p.X + (int64_t)(pm ? pm[i] : i) * p.Hp + k));
+  const float4 a = f4add(a0, a1);
+  st_bf4(p.out + (int64_t)n * p.ldo + p.off[part] + k, a.x, a.y, a.z, a.w);
+}
+
+// pos'[n] = pos[n] + cw * mean_{e: src_e = n} clamp(cd_e tanh(s_e), +-100)   (wave per node,
+// lanes stride the node's edges)
+__global__ __launch_bounds__(256) void pos_fwd_kernel(const float* __restrict__ pos, const float* __restrict__ geo,
+                                                      const float* __restrict__ s, const int* __restrict__ srp,
+                                                      const int* __restrict__ sperm, float cw, int N,
+                                                      float* __restrict__ pos_out) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  const int b = srp[n], eN = srp[n + 1];
+  float a[3] = {0.f, 0.f, 0.f};
+  for (int i = b + lane; i < eN; i += 64) {
+    const int e = sperm ? sperm[i] : i;
+    const float4 g = *reinterpret_cast<const float4*>(geo + (int64_t)e * 4);
+    const float t = tanhf(s[e]);
+    a[0] += fminf(fmaxf(g.x * t, -100.f), 100.f);
+    a[1] += fminf(fmaxf(g.y * t, -100.f), 100.f);
+    a[2] += fminf(fmaxf(g.z * t, -100.f), 100.f);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) a[c] = wave_sum(a[c]);
+  if (lane < 3) {
+    const int cnt = eN - b;
+    const float v = lane == 0 ? a[0] : (lane == 1 ? a[1] : a[2]);
+    pos_out[n * 3 + lane] = pos[n * 3 + lane] + cw * v / (float)(cnt > 0 ? cnt : 1);
+  }
+}
+
+// per-edge position gradient d loss / d vec_e (vec = pos[dst] - pos[src]) from the radial
+// gradient dr_e (|vec| feeds edge_mlp[0]) and dcd_e (normalised difference of the update)
+__device__ __forceinline__ float dvec_c(const float* geo, const float* dr, const float* dcd, int64_t e, int c) {
+  const float4 g = *reinterpret_cast<const float4*>(geo + e * 4);
+  const float L = g.w, s1 = L + 1.f;
+  if (!(L > 0.f)) return 0.f;
+  const float d[3] = {g.x * s1, g.y * s1, g.z * s1};
+  float v = dr[e] * d[c] / L;
+  if (dcd) {
+    const float q0 = dcd[e * 3], q1 = dcd[e * 3 + 1], q2 = dcd[e * 3 + 2];
+    const float dot = q0 * d[0] + q1 * d[1] + q2 * d[2];
+    const float qc = c == 0 ? q0 : (c == 1 ? q1 : q2);
+    v += qc / s1 - d[c] * dot / (L * s1 * s1);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void pos_bwd_kernel(const float* __restrict__ dpos_out,
+                                                      const float* __restrict__ geo, const float* __restrict__ dr,
+                                                      const float* __restrict__ dcd, const int* __restrict__ srp,
+                                                      const int* __restrict__ sperm, const int* __restrict__ drp,
+                                                      int N, float* __restrict__ dpos) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  float a[3] = {0.f, 0.f, 0.f};
+  for (int e = drp[n] + lane; e < drp[n + 1]; e += 64)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a[c] += dvec_c(geo, dr, dcd, e, c);
+  for (int i = srp[n] + lane; i < srp[n + 1]; i += 64) {
+    const int e = sperm ? sperm[i] : i;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a[c] -= dvec_c(geo, dr, dcd, e, c);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) a[c] = wave_sum(a[c]);
+  if (lane < 3) {
+    const float v = lane == 0 ? a[0] : (lane == 1 ? a[1] : a[2]);
+    dpos[n * 3 + lane] = v + (dpos_out ? dpos_out[n * 3 + lane] : 0.f);
   }
 }
 
@@ -441,32 +381,6 @@ void egnn_gather_fwd(const at::Tensor& AB, const at::Tensor& src, const at::Tens
   if (E) gather_fwd_kernel<<<ceil_div(E, GE), 256, 0, stream()>>>(p);
 }
 
-void egnn_agg_fwd(const at::Tensor& m, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
-                  const at::Tensor& pos, const at::Tensor& geo, const c10::optional<at::Tensor>& s, double cw,
-                  const at::Tensor& agg, const at::Tensor& pos_out) {
-  const int64_t N = pos.size(0), E = m.size(0), Hp = m.size(1);
-  chk_rows(m, E, Hp, at::kBFloat16, "m");
-  chk_rows(agg, N, Hp, at::kBFloat16, "agg");
-  chk_rows(pos, N, 3, at::kFloat, "pos");
-  chk_rows(pos_out, N, 3, at::kFloat, "pos_out");
-  chk_rows(geo, E, 4, at::kFloat, "geo");
-  HY_CHECK_I32(srp);
-  HY_CHECK(srp.numel() == N + 1 && Hp <= 1024, "egnn_agg_fwd: srp length, Hp <= 1024");
-  AggFwd p{};
-  p.m = cbf(m);
-  p.srp = srp.data_ptr<int>();
-  p.sperm = iptr(sperm);
-  p.pos = pos.data_ptr<float>();
-  p.geo = geo.data_ptr<float>();
-  p.s = s.has_value() ? s->data_ptr<float>() : nullptr;
-  p.cw = (float)cw;
-  p.N = (int)N;
-  p.Hp = (int)Hp;
-  p.agg = wbf(agg);
-  p.pos_out = pos_out.data_ptr<float>();
-  if (N) agg_fwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(p);
-}
-
 // returns the number of partial rows written to part ([nblk, Hp])
 int64_t egnn_coord_bwd(const at::Tensor& dpos, const at::Tensor& src, const at::Tensor& srp, const at::Tensor& geo,
                        const at::Tensor& s, const at::Tensor& c1, const at::Tensor& wc2, double cw, const at::Tensor& dc1,
@@ -499,47 +413,6 @@ int64_t egnn_coord_bwd(const at::Tensor& dpos, const at::Tensor& src, const at::
   return nblk;
 }
 
-void egnn_edge_bwd(const at::Tensor& dh1, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
-                   const at::Tensor& drp, const at::Tensor& geo, const c10::optional<at::Tensor>& dcd,
-                   const at::Tensor& W0, int64_t c0, int64_t H, const at::Tensor& dAB, const at::Tensor& dvec) {
-  const int64_t E = dh1.size(0), Hp = dh1.size(1), N = srp.numel() - 1;
-  HY_CHECK(Hp <= 1024 && H < Hp, "egnn_edge_bwd: H < Hp <= 1024");
-  chk_rows(dh1, E, Hp, at::kBFloat16, "dh1");
-  chk_rows(dAB, N, 2 * Hp, at::kBFloat16, "dAB");
-  chk_rows(dvec, E, 3, at::kFloat, "dvec");
-  chk_rows(geo, E, 4, at::kFloat, "geo");
-  HY_CHECK(drp.numel() == N + 1, "egnn_edge_bwd: drp length");
-  HY_CHECK(W0.scalar_type() == at::kFloat && W0.stride(1) == 1 && W0.size(0) == H && c0 < W0.size(1),
-           "egnn_edge_bwd: W0");
-  EdgeBwd p{};
-  p.dh1 = cbf(dh1);
-  p.srp = srp.data_ptr<int>();
-  p.sperm = iptr(sperm);
-  p.drp = drp.data_ptr<int>();
-  p.geo = geo.data_ptr<float>();
-  p.dcd = dcd.has_value() ? dcd->data_ptr<float>() : nullptr;
-  p.W0 = W0.data_ptr<float>();
-  p.ld0 = (int)W0.stride(0);
-  p.c0 = (int)c0;
-  p.N = (int)N;
-  p.H = (int)H;
-  p.Hp = (int)Hp;
-  p.dAB = wbf(dAB);
-  p.dvec = dvec.data_ptr<float>();
-  if (N) edge_bwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(p);
-}
-
-void egnn_pos_bwd(const c10::optional<at::Tensor>& dpos_out, const at::Tensor& dvec, const at::Tensor& srp,
-                  const c10::optional<at::Tensor>& sperm, const at::Tensor& drp, const at::Tensor& dpos) {
-  const int64_t N = srp.numel() - 1;
-  chk_rows(dpos, N, 3, at::kFloat, "dpos");
-  if (dpos_out.has_value()) chk_rows(*dpos_out, N, 3, at::kFloat, "dpos_out");
-  if (N)
-    pos_bwd_kernel<<<ceil_div(N * 3, 256), 256, 0, stream()>>>(
-        dpos_out.has_value() ? dpos_out->data_ptr<float>() : nullptr, dvec.data_ptr<float>(), srp.data_ptr<int>(),
-        iptr(sperm), drp.data_ptr<int>(), (int)N, dpos.data_ptr<float>());
-}
-
 void egnn_gather_gate(const at::Tensor& g, const at::Tensor& idx, const at::Tensor& gate, int64_t H,
                       const at::Tensor& out) {
   const int64_t E = gate.size(0), Hp = gate.size(1);
@@ -554,6 +427,72 @@ void egnn_gather_gate(const at::Tensor& g, const at::Tensor& idx, const at::Tens
                                                              wbf(out));
 }
 
+// CSR row sums of bf16 rows into column blocks of out (one or two CSR parts)
+void egnn_csr_rows(const at::Tensor& X, const at::Tensor& rp0, const c10::optional<at::Tensor>& perm0, int64_t off0,
+                   const c10::optional<at::Tensor>& rp1, const c10::optional<at::Tensor>& perm1, int64_t off1,
+                   const at::Tensor& out) {
+  const int64_t E = X.size(0), Hp = X.size(1), N = rp0.numel() - 1;
+  chk_rows(X, E, Hp, at::kBFloat16, "X");
+  HY_CHECK(Hp % 4 == 0 && Hp <= 1024, "egnn_csr_rows: Hp % 4 == 0, <= 1024");
+  HY_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.stride(1) == 1 && out.size(0) == N &&
+               out.size(1) >= off0 + Hp && out.stride(0) % 4 == 0,
+           "egnn_csr_rows: out");
+  HY_CHECK_I32(rp0);
+  HY_CHECK(!perm0.has_value() || perm0->numel() == E, "egnn_csr_rows: perm0 length");
+  CsrParts p{};
+  p.X = cbf(X);
+  p.Hp = (int)Hp;
+  p.rp[0] = rp0.data_ptr<int>();
+  p.perm[0] = iptr(perm0);
+  p.off[0] = (int)off0;
+  int parts = 1;
+  if (rp1.has_value()) {
+    HY_CHECK_I32(*rp1);
+    HY_CHECK(rp1->numel() == N + 1 && out.size(1) >= off1 + Hp && (!perm1.has_value() || perm1->numel() == E),
+             "egnn_csr_rows: second part");
+    p.rp[1] = rp1->data_ptr<int>();
+    p.perm[1] = iptr(perm1);
+    p.off[1] = (int)off1;
+    parts = 2;
+  }
+  p.out = wbf(out);
+  p.ldo = (int)out.stride(0);
+  if (N) csr_rows_kernel<<<dim3((unsigned)N, parts), 256, 0, stream()>>>(p);
+}
+
+void egnn_pos_fwd(const at::Tensor& pos, const at::Tensor& geo, const at::Tensor& s, const at::Tensor& srp,
+                  const c10::optional<at::Tensor>& sperm, double cw, const at::Tensor& pos_out) {
+  const int64_t N = pos.size(0);
+  chk_rows(pos, N, 3, at::kFloat, "pos");
+  chk_rows(pos_out, N, 3, at::kFloat, "pos_out");
+  chk_rows(geo, s.numel(), 4, at::kFloat, "geo");
+  HY_CHECK_I32(srp);
+  HY_CHECK(srp.numel() == N + 1 && s.scalar_type() == at::kFloat, "egnn_pos_fwd: srp / s");
+  if (N)
+    pos_fwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(pos.data_ptr<float>(), geo.data_ptr<float>(),
+                                                               s.data_ptr<float>(), srp.data_ptr<int>(), iptr(sperm),
+                                                               (float)cw, (int)N, pos_out.data_ptr<float>());
+}
+
+void egnn_pos_bwd(const c10::optional<at::Tensor>& dpos_out, const at::Tensor& geo, const at::Tensor& dr,
+                   const c10::optional<at::Tensor>& dcd, const at::Tensor& srp, const c10::optional<at::Tensor>& sperm,
+                   const at::Tensor& drp, const at::Tensor& dpos) {
+  const int64_t N = srp.numel() - 1;
+  chk_rows(dpos, N, 3, at::kFloat, "dpos");
+  HY_CHECK(dr.scalar_type() == at::kFloat && dr.numel() == geo.size(0), "egnn_pos_bwd: dr [E]");
+  chk_rows(geo, dr.numel(), 4, at::kFloat, "geo");
+  HY_CHECK_I32(srp);
+  HY_CHECK_I32(drp);
+  HY_CHECK(drp.numel() == N + 1, "egnn_pos_bwd: drp");
+  if (dcd.has_value()) chk_rows(*dcd, dr.numel(), 3, at::kFloat, "dcd");
+  if (dpos_out.has_value()) chk_rows(*dpos_out, N, 3, at::kFloat, "dpos_out");
+  if (N)
+    pos_bwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(
+        dpos_out.has_value() ? dpos_out->data_ptr<float>() : nullptr, geo.data_ptr<float>(), dr.data_ptr<float>(),
+        dcd.has_value() ? dcd->data_ptr<float>() : nullptr, srp.data_ptr<int>(), iptr(sperm), drp.data_ptr<int>(),
+        (int)N, dpos.data_ptr<float>());
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
@@ -561,23 +500,23 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "egnn_gather_fwd(Tensor AB, Tensor src, Tensor dst, Tensor pos, Tensor? ea, Tensor W0, int c0, Tensor b1, "
       "Tensor h1, Tensor geo, Tensor sc) -> ()");
   m.def(
-      "egnn_agg_fwd(Tensor m, Tensor srp, Tensor? sperm, Tensor pos, Tensor geo, Tensor? s, float cw, Tensor agg, "
-      "Tensor pos_out) -> ()");
-  m.def(
       "egnn_coord_bwd(Tensor dpos, Tensor src, Tensor srp, Tensor geo, Tensor s, Tensor c1, Tensor wc2, float cw, "
       "Tensor dc1, Tensor dcd, Tensor part) -> int");
-  m.def(
-      "egnn_edge_bwd(Tensor dh1, Tensor srp, Tensor? sperm, Tensor drp, Tensor geo, Tensor? dcd, Tensor W0, int c0, "
-      "int H, Tensor dAB, Tensor dvec) -> ()");
   m.def("egnn_gather_gate(Tensor g, Tensor idx, Tensor gate, int H, Tensor out) -> ()");
-  m.def("egnn_pos_bwd(Tensor? dpos_out, Tensor dvec, Tensor srp, Tensor? sperm, Tensor drp, Tensor dpos) -> ()");
+  m.def(
+      "egnn_csr_rows(Tensor X, Tensor rp0, Tensor? perm0, int off0, Tensor? rp1, Tensor? perm1, int off1, Tensor out) "
+      "-> ()");
+  m.def("egnn_pos_fwd(Tensor pos, Tensor geo, Tensor s, Tensor srp, Tensor? sperm, float cw, Tensor pos_out) -> ()");
+  m.def(
+      "egnn_pos_bwd(Tensor? dpos_out, Tensor geo, Tensor dr, Tensor? dcd, Tensor srp, Tensor? sperm, Tensor drp, "
+      "Tensor dpos) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("egnn_gather_fwd", hy::egnn_gather_fwd);
-  m.impl("egnn_agg_fwd", hy::egnn_agg_fwd);
   m.impl("egnn_coord_bwd", hy::egnn_coord_bwd);
-  m.impl("egnn_edge_bwd", hy::egnn_edge_bwd);
-  m.impl("egnn_pos_bwd", hy::egnn_pos_bwd);
   m.impl("egnn_gather_gate", hy::egnn_gather_gate);
+  m.impl("egnn_csr_rows", hy::egnn_csr_rows);
+  m.impl("egnn_pos_fwd", hy::egnn_pos_fwd);
+  m.impl("egnn_pos_bwd", hy::egnn_pos_bwd);
 }

@@ -9,7 +9,7 @@ product ``dY^T X`` then carries the bias gradient in its column ``K``.
 ``BF16Linear`` is the bf16-precision ``linear`` for wide maps (>= ``BF16_MIN_MACS``):
 fp32 in / fp32 out at the module boundary, bf16 MFMA inside (operands rounded to bf16,
 fp32 accumulation), backward = one data-gradient NT GEMM and one split-M weight-gradient
-TN GEMM + slab reduce (bias gradient from the ones lane).
+TN GEMM whose last-arriving split block reduces each tile (bias gradient from the ones lane).
 """
 import torch
 
@@ -87,6 +87,32 @@ def _slab(dev, numel):
     return s
 
 
+_counters = {}
+
+
+def _counter_buf(dev, n):
+    """Per-tile arrival counters of the fused TN reduce (zero between products: the last
+    block of each tile resets its counter).  Shared by every product on one stream."""
+    key = (dev, torch.cuda.current_stream(dev).stream_id)
+    c = _counters.get(key)
+    if c is None or c.numel() < n:
+        c = torch.zeros(max(n, 1 << 14), device=dev, dtype=torch.int32)
+        _counters[key] = c
+    return c
+
+
+def tn_reduce(G, X, Np, Kp, slab, S, outs, *, X2=None, kc1=None, boff=None, beta=0.0):
+    """``slab = G^T [X | X2]`` split over rows, reduced in the same launch into ``outs``:
+    (out, n0, k0, N, K, bias_out or None, bias_col) per destination (up to 3)."""
+    groups = 1 if boff is None else boff.numel() - 1
+    cnt = _counter_buf(G.device, groups * (Np // 128) * (Kp // 128))
+    meta = []
+    for o in outs:
+        meta += [o[1], o[2], o[3], o[4], o[6]]
+    _native.ops().bg_tn(G, X, X2, Kp if kc1 is None else kc1, Np, Kp, slab, S, boff, [o[0] for o in outs],
+                        [o[5] for o in outs], meta, beta, cnt)
+
+
 def splits_for(M, tiles):
     """Row splits of a weight-gradient product: ~1.5 workgroups per CU and >= 8 K-steps
     (512 rows) per split (fewer slabs for the reduce to read)."""
@@ -99,12 +125,12 @@ def wgrad(G, X, Np, Kp, outs, *, X2=None, kc1=None, beta=0.0):
     M = G.shape[0]
     S = splits_for(M, (Np // 128) * (Kp // 128))
     slab = _slab(G.device, S * Np * Kp)
-    _native.ops().bg_tn(G, X, X2, Kp if kc1 is None else kc1, Np, Kp, slab, S)
+    dst = []
     for o in outs:
         out, n0, bias_out, bias_col = o[:4]
         k0 = o[4] if len(o) > 4 else 0
-        _native.ops().bg_slab_reduce(slab, S, Np, Kp, n0, k0, out.shape[0], out.shape[1], out, beta, bias_col,
-                                     bias_out)
+        dst.append((out, n0, k0, out.shape[0], out.shape[1], bias_out, bias_col))
+    tn_reduce(G, X, Np, Kp, slab, S, dst, X2=X2, kc1=kc1, beta=beta)
 
 
 def _accum_grad(p, g):
@@ -241,12 +267,11 @@ class _BranchMLP(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             Np, Kp = kps[l + 1], kps[l]
             slab = _slab(dev, nb * S * Np * Kp)
-            _native.ops().bg_tn(g, hs[l], None, Kp, Np, Kp, slab, S, boff)
-            # every branch's weight and bias gradient in ONE grouped reduce launch
+            # every branch's weight and bias gradient in the same grouped launch
             dW = torch.empty((nb, dims[l + 1], dims[l]), device=dev, dtype=torch.float32)
             db = torch.empty((nb, dims[l + 1]), device=dev, dtype=torch.float32)
-            _native.ops().bg_slab_reduce(slab, S, Np, Kp, 0, 0, dims[l + 1], dims[l], dW.view(-1, dims[l]), 0.0,
-                                         dims[l], db.view(-1), nb)
+            tn_reduce(g, hs[l], Np, Kp, slab, S, [(dW.view(-1, dims[l]), 0, 0, dims[l + 1], dims[l], db.view(-1),
+                                                   dims[l])], boff=boff)
             for b in range(nb):
                 grads[(l * 2) * nb + b] = dW[b]
                 grads[(l * 2 + 1) * nb + b] = db[b]

@@ -8,7 +8,7 @@ to 128 with the ones lane at column H, F = input width, Kx = pad128(F)):
            h1   = relu(AB[src] + AB[dst] + ...)   egnn_gather_fwd            bf16 [E, Hp]
            m    = relu(h1 W2^T + b2)              NT  (edge GEMM)            bf16 [E, Hp]
            c1   = relu(m Wc1^T + bc1), s = c1 wc2 NT + row-dot epilogue     (equivariant)
-           agg, pos' = CSR-by-source sums          egnn_agg_fwd
+           agg, pos' = CSR-by-source sums          egnn_csr_rows / egnn_pos_fwd
            n1   = relu([x | agg] Wn1^T + bn1)     NT, K-concatenated A       bf16 [N, Hp]
            x'   = relu(n1 Wn2^T + bn2)            NT                         bf16 (+fp32 last)
   backward the dual chain: relu'-gated casts, NT data gradients with gather-add and
@@ -156,7 +156,9 @@ class _EGNNWide(torch.autograd.Function):
                 bg.nt(m, im["c1"], Hp, H, bias=p[9], act=1, outb=c1, rowvec=p[10].reshape(-1), rowdot=s)
             agg = torch.empty((N, Hp), device=dev, dtype=torch.bfloat16)
             pos_n = torch.empty_like(pos_l) if L["eq"] else pos_l
-            ops.egnn_agg_fwd(m, src.rowptr, src.perm, pos_l, geo, s, L["cw"], agg, pos_n)
+            ops.egnn_csr_rows(m, src.rowptr, src.perm, 0, None, None, 0, agg)
+            if L["eq"]:
+                ops.egnn_pos_fwd(pos_l, geo, s, src.rowptr, src.perm, L["cw"], pos_n)
             n1 = torch.empty((N, Hp), device=dev, dtype=torch.bfloat16)
             bg.nt(xb, im["n1"], Kx + Hp, H, A2=agg, k1=Kx, bias=p[5], act=1, outb=n1, ones_col=H)
             last = li == len(plan.layers) - 1
@@ -210,7 +212,7 @@ class _EGNNWide(torch.autograd.Function):
                 dpo = dpos if dpos is not None else torch.zeros((N, 3), device=dev, dtype=torch.float32)
                 dc1 = torch.empty((E, Hp), device=dev, dtype=torch.bfloat16)
                 dcd = torch.empty((E, 3), device=dev, dtype=torch.float32)
-                part = torch.empty(((E + 63) // 64) * Hp, device=dev, dtype=torch.float32)
+                part = torch.empty(((E + 31) // 32) * Hp, device=dev, dtype=torch.float32)
                 nblk = ops.egnn_coord_bwd(dpo, src.index, src.rowptr, S["geo"], S["s"], S["c1"],
                                           p[10].reshape(-1), L["cw"], dc1, dcd, part)
                 ops.bg_slab_reduce(part, nblk, 1, Hp, 0, 0, 1, H, g[10], 0.0, -1, None)
@@ -223,12 +225,16 @@ class _EGNNWide(torch.autograd.Function):
                 ops.egnn_gather_gate(dagg, src.index, S["m"], H, dZ2)
             bg.wgrad(dZ2, S["h1"], Hp, Hp, [(g[2], 0, g[3], H)])
             dh1 = torch.empty((E, Hp), device=dev, dtype=torch.bfloat16)
-            bg.nt(dZ2, im["w2T"], Hp, H, gate=S["h1"], outb=dh1)
+            dr = None  # d loss / d|d_e| (the radial input of edge_mlp[0]), from the fp32 epilogue
+            if li > 0:
+                dr = torch.zeros(E, device=dev, dtype=torch.float32)
+                bg.nt(dZ2, im["w2T"], Hp, H, gate=S["h1"], outb=dh1, rowvec=p[0][:, 2 * F].contiguous(), rowdot=dr)
+            else:
+                bg.nt(dZ2, im["w2T"], Hp, H, gate=S["h1"], outb=dh1)
             del dZ2
-            # edge MLP first layer (node-level blocks, per-edge scalars) and geometry
+            # edge MLP first layer: node-level blocks are by-source / by-destination CSR sums
             dAB = torch.empty((N, 2 * Hp), device=dev, dtype=torch.bfloat16)
-            dvec = torch.empty((E, 3), device=dev, dtype=torch.float32)
-            ops.egnn_edge_bwd(dh1, src.rowptr, src.perm, dst.rowptr, S["geo"], dcd, p[0], 2 * F, H, dAB, dvec)
+            ops.egnn_csr_rows(dh1, src.rowptr, src.perm, 0, dst.rowptr, None, Hp, dAB)
             ns = plan.nea + 1
             bg.wgrad(dh1, S["sc"], Hp, 128, [(g[0][:, 2 * F:2 * F + ns], 0, g[1], ns)])
             del dh1
@@ -237,7 +243,7 @@ class _EGNNWide(torch.autograd.Function):
                 dx = dxa[:, :F]
                 bg.nt(dAB, im["abT"], 2 * Hp, F, outf=dx, beta=1.0)
                 dpos_in = torch.empty((N, 3), device=dev, dtype=torch.float32)
-                ops.egnn_pos_bwd(dpos, dvec, src.rowptr, src.perm, dst.rowptr, dpos_in)
+                ops.egnn_pos_bwd(dpos, S["geo"], dr, dcd, src.rowptr, src.perm, dst.rowptr, dpos_in)
                 dpos = dpos_in
                 if DEBUG is not None:
                     DEBUG[li] = dpos_in.clone()

@@ -70,6 +70,29 @@ def test_tn_reduce(M):
     _close(bias - bprev, full[:N, 5], 1e-3)
 
 
+def test_tn_fused_reduce_multi_out_deterministic():
+    """two destination rectangles + transposed (strided) output; the per-tile arrival
+    counters are left at zero and repeated products are bitwise identical (fixed split order)"""
+    torch.manual_seed(5)
+    M, Np, Kp = 20000, 384, 256
+    G, X = _rb(M, Np), _rb(M, Kp)
+    full = G.float().T @ X.float()
+    a = torch.empty(100, 200, device=dev)
+    bt = torch.empty(120, 130, device=dev).T  # [130, 120] view with ldk != 1
+    ba = torch.empty(100, device=dev)
+    bg.wgrad(G, X, Np, Kp, [(a, 0, ba, 200), (bt, 250, None, -1, 100)])
+    _close(a, full[:100, :200], 1e-3)
+    _close(ba, full[:100, 200], 1e-3)
+    _close(bt, full[250:380, 100:220], 1e-3)
+    first = a.clone()
+    for _ in range(3):
+        bg.wgrad(G, X, Np, Kp, [(a, 0, ba, 200), (bt, 250, None, -1, 100)])
+        assert torch.equal(a, first)
+    torch.cuda.synchronize()
+    for c in bg._counters.values():
+        assert int(c.abs().sum()) == 0
+
+
 def test_cast_weights_and_pad():
     torch.manual_seed(3)
     W = torch.randn(866, 889, device=dev)
