@@ -121,10 +121,9 @@ class RadialEmbeddingBlock(nn.Module):
 def _to_channels(x, irreps):
     """flat e3nn layout (blocks of [H, 2l+1], equal H) -> [N, H, sum(2l+1)]."""
     N = x.shape[0]
-    out = []
-    for (a, b), (m, l, _) in zip(irreps.slices(), irreps.blocks):
-        out.append(x[:, a:b].reshape(N, m, 2 * l + 1))
-    return torch.cat(out, -1)
+    parts = torch.split(x, [b - a for a, b in irreps.slices()], 1) if len(irreps.blocks) > 1 else [x]
+    out = [t.reshape(N, m, 2 * l + 1) for t, (m, l, _) in zip(parts, irreps.blocks)]
+    return torch.cat(out, -1) if len(out) > 1 else out[0]
 
 
 class InteractionBlock(nn.Module):
@@ -179,7 +178,9 @@ class MACELayer(nn.Module):
         h = torch.cat([inv, equiv], 1)
         m, sc = self.inter(h, ctx.edge_attributes, ctx.edge_features, ctx.dst_si, ctx.src_si)
         h = self.sizing(self.prod(m, sc, ctx.elem))
-        return h[:, :self.n_scalars_out], h[:, self.n_scalars_out:]
+        # one split (backward: one concat) instead of two slices (a zero-fill + copy each)
+        inv, equiv = h.split([self.n_scalars_out, h.shape[1] - self.n_scalars_out], 1)
+        return inv, equiv
 
 
 class _ScalarLinear(nn.Module):
@@ -221,7 +222,8 @@ class _PerNodeMLP(nn.Module):
     def forward(self, x):
         nn_ = self.num_nodes
         G = x.shape[0] // nn_
-        h = x[:, :self.n_scalar].reshape(G, nn_, -1).transpose(0, 1)  # [slots, G, F]
+        xs = x if x.shape[1] == self.n_scalar else x[:, :self.n_scalar]
+        h = xs.reshape(G, nn_, -1).transpose(0, 1)  # [slots, G, F]
         # o3.Linear normalisation of the scalar block: 1/sqrt(fan_in)
         h = torch.baddbmm(self.biases[0].unsqueeze(1), h, self.weights[0]) / self.n_scalar ** 0.5
         for i in range(1, len(self.weights)):
@@ -287,9 +289,82 @@ class MultiheadDecoderBlock(nn.Module):
                 raise ValueError("Unknown head type" + head_type[ih])
             self.heads_NN.append(hn)
 
+    def _chain_steps(self, mods):
+        """Sequential head modules -> [(W [out, in], bias | None, act | None)], or None when
+        a module is not a plain linear map / activation (e.g. ``mlp_per_node``)."""
+        steps = []
+        for m in mods:
+            if isinstance(m, nn.Linear):
+                steps.append([m.weight, m.bias, None, 1.0])
+            elif isinstance(m, _ScalarLinear):
+                lin = m.lin
+                if len(lin.paths) != 1 or lin.paths[0][0] != 0 or lin.irreps_in.blocks[0][1] != 0:
+                    return None
+                # raw weight view; the (branch-independent) path normalisation is applied once
+                # to the stacked product instead of once per branch weight
+                _, _, _, mi, mo, a = lin.paths[0]
+                steps.append([lin.weight.view(mi, mo).t(), None, None, a])
+                continue
+            elif steps and steps[-1][2] is None and not isinstance(m, (nn.Sequential, _PerNodeMLP)):
+                steps[-1][2] = m
+            else:
+                return None
+        return steps
+
+    def _stacked_dense(self, names, gfeat, sc, dn, dn_node):
+        """Dense multi-branch decode with the branches STACKED: per layer one GEMM over all
+        branches (the first layer's weights concatenated along the output, later layers one
+        batched product), then one per-row gather of the row's own branch.  Same values as
+        evaluating every branch head on every row and selecting with ``torch.where`` (the
+        reference decode ``blocks.py:417-767`` per branch), at a launch count independent of
+        the branch count.  None when the heads are not plain MLP chains."""
+        nb = len(names)
+        if [int(b.split("-")[1]) for b in names] != list(range(nb)):
+            return None
+        outs = []
+        for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
+            chains = []
+            for bt in names:
+                mods = list(hn[bt]) if isinstance(hn[bt], nn.Sequential) else None
+                if mods is None:
+                    return None
+                if t == "graph" and self.nonlinear:
+                    mods = list(self.graph_shared[bt]) + mods
+                st = self._chain_steps(mods)
+                if st is None:
+                    return None
+                chains.append(st)
+            shapes = [[(tuple(s[0].shape), s[1] is None, type(s[2]), s[3]) for s in c] for c in chains]
+            if any(s != shapes[0] for s in shapes):
+                return None
+            x, rid = (gfeat, dn) if t == "graph" else (sc, dn_node)
+            R = x.shape[0]
+            h = None
+            for li in range(len(chains[0])):
+                Ws = [c[li][0] for c in chains]
+                bs = [c[li][1] for c in chains]
+                act, scale = chains[0][li][2], chains[0][li][3]
+                out_dim = Ws[0].shape[0]
+                if li == 0:  # shared input: one GEMM against the branch-concatenated weights
+                    xs = x * scale if scale != 1.0 else x
+                    y = torch.nn.functional.linear(xs, torch.cat(Ws, 0), None if bs[0] is None else torch.cat(bs, 0))
+                    h = y.view(R, nb, out_dim).transpose(0, 1)
+                else:
+                    hs = h * scale if scale != 1.0 else h
+                    W = torch.stack(Ws, 0).transpose(1, 2)
+                    h = torch.bmm(hs, W) if bs[0] is None else torch.baddbmm(torch.stack(bs, 0).unsqueeze(1), hs, W)
+                if act is not None:
+                    h = act(h)
+            h = h[:, :, :hd]
+            sel = h.gather(0, rid.clamp(min=0).view(1, R, 1).expand(1, R, hd)).squeeze(0)
+            outs.append(torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype, device=sel.device)))
+        return outs
+
     def forward(self, node_features, ctx, ids):
         gsi = ctx.graph_si
-        sc = node_features[:, :self.input_scalar_dim]
+        # the read-outs only use the scalar channels; the stack hands over just those
+        sc = node_features if node_features.shape[1] == self.input_scalar_dim else \
+            node_features[:, :self.input_scalar_dim]
         gfeat = sc.mean(0, keepdim=True) if gsi is None else seg.segment_mean(sc, gsi)
         data = ctx.data
         outs = []
@@ -299,6 +374,9 @@ class MultiheadDecoderBlock(nn.Module):
             dn = data.dataset_name.view(-1)
             dn_node = dn.index_select(0, data.batch)
             names = sorted(self.heads_NN[0].keys(), key=lambda k: int(k.split("-")[1]))
+            stacked = self._stacked_dense(names, gfeat, sc, dn, dn_node)
+            if stacked is not None:
+                return stacked
             for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
                 feats, rid = (gfeat, dn) if t == "graph" else (node_features, dn_node)
                 out = feats.new_zeros(feats.shape[0], hd)
@@ -485,7 +563,7 @@ class MACEStack(Base):
         outputs = self.multihead_decoders[0](ctx.node_attributes, ctx, ids)
         for conv, readout in zip(self.graph_convs, self.multihead_decoders[1:]):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
-            out = readout(torch.cat([inv, equiv], 1), ctx, ids)
+            out = readout(inv, ctx, ids)  # read-outs map the scalar block only
             outputs = [a + b for a, b in zip(outputs, out)]
         return outputs
 

@@ -66,15 +66,32 @@ class PainnMessage(nn.Module):
         if edge_dim is not None:
             self.edge_filter = nn.Sequential(Linear(edge_dim, F), nn.SiLU(), Linear(F, 3 * F))
 
+    def _edge_terms(self, ctx):
+        """Layer-independent edge terms — sinc basis, cosine cutoff, d̂/d as [E, 3, 1] —
+        computed once per forward and shared by every message layer (the reference
+        recomputes them per layer, ``PAINNStack.py:228-236``; same values)."""
+        key = ("painn_edge", self.num_radial, float(self.cutoff))
+        cache = ctx.get("_painn_cache")
+        if cache is None:
+            cache = {}
+            ctx._painn_cache = cache
+        if key not in cache:
+            d = ctx.edge_dist
+            cache[key] = (sinc_expansion(d, self.num_radial, self.cutoff), cosine_cutoff(d, self.cutoff),
+                          (ctx.edge_diff / d).unsqueeze(-1))
+        return cache[key]
+
     def forward(self, s, v, ctx):
         F = self.node_size
-        d = ctx.edge_dist
-        W = self.filter_layer(sinc_expansion(d, self.num_radial, self.cutoff)) * cosine_cutoff(d, self.cutoff)
+        rbf, cut, unit = self._edge_terms(ctx)
+        W = self.filter_layer(rbf) * cut
         if ctx.edge_attr is not None and self.edge_dim is not None:
             W = W * self.edge_filter(ctx.edge_attr)
         out = W * seg.gather(self.scalar_message_mlp(s), ctx.dst_si)
-        g_v, g_e, m_s = out[:, :F], out[:, F:2 * F], out[:, 2 * F:]
-        m_v = seg.gather(v, ctx.dst_si) * g_v.unsqueeze(1) + g_e.unsqueeze(1) * (ctx.edge_diff / d).unsqueeze(-1)
+        # one split (backward: one concat) instead of three slices (a zero-fill + copy each,
+        # at every order of differentiation under force training)
+        g_v, g_e, m_s = out.split(F, 1)
+        m_v = seg.gather(v, ctx.dst_si) * g_v.unsqueeze(1) + g_e.unsqueeze(1) * unit
         s = s + seg.segment_sum(m_s, ctx.src_si)
         v = v + seg.segment_sum(m_v, ctx.src_si)
         return s, v
@@ -111,9 +128,9 @@ class PainnUpdate(nn.Module):
         a = self.update_mlp(torch.cat((safe_vector_norm(Vv, 1), s), dim=-1))
         inner = (Uv * Vv).sum(1)
         if self.last_layer:
-            a_sv, a_ss = a[:, :F], a[:, F:]
+            a_sv, a_ss = a.split(F, 1)
             return s + a_sv * inner + a_ss, v
-        a_vv, a_sv, a_ss = a[:, :F], a[:, F:2 * F], a[:, 2 * F:]
+        a_vv, a_sv, a_ss = a.split(F, 1)
         return s + a_sv * inner + a_ss, v + a_vv.unsqueeze(1) * Uv
 
 

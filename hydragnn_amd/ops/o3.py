@@ -244,6 +244,24 @@ class O3Linear(nn.Module):
                 numel += mi * mo
         self.weight = nn.Parameter(torch.randn(numel))
         self.sl_in, self.sl_out = irreps_in.slices(), irreps_out.slices()
+        # per-element path normalisation: ONE multiply of the whole weight vector per forward
+        # and one split into path views (per-path slices would cost a zero-fill + copy each
+        # in backward, and a multiply each way per path)
+        scale = torch.empty(numel)
+        for _, _, off, mi, mo, a in self.paths:
+            scale[off:off + mi * mo] = a
+        self.register_buffer("wscale", scale, persistent=False)
+
+    def path_weights(self):
+        """[mi, mo] normalised weight of every path (views of one scaled vector)."""
+        if not self.paths:
+            return []
+        w = self.weight * self.wscale
+        if len(self.paths) == 1:
+            _, _, _, mi, mo, _ = self.paths[0]
+            return [w.view(mi, mo)]
+        return [t.view(mi, mo) for t, (_, _, _, mi, mo, _) in
+                zip(torch.split(w, [p[3] * p[4] for p in self.paths]), self.paths)]
 
     def lookup(self, elem_si):
         """forward(one_hot(elem)) for a single scalar input block (the MACE node embedding):
@@ -253,11 +271,12 @@ class O3Linear(nn.Module):
         (mi, li, _), = self.irreps_in.blocks
         assert li == 0 and all(l == 0 for _, l, _ in self.irreps_out.blocks), "lookup: scalar irreps only"
         cols = []
+        ws = self.path_weights()
         for io in range(len(self.irreps_out.blocks)):
             W = None
-            for ii, o, off, m_in, mo, a in self.paths:
+            for (ii, o, off, m_in, mo, a), Wp in zip(self.paths, ws):
                 if o == io:
-                    W = self.weight[off:off + m_in * mo].view(m_in, mo) * a
+                    W = Wp
             cols.append(W if W is not None else self.weight.new_zeros(mi, self.irreps_out.blocks[io][0]))
         table = torch.cat(cols, 1) if len(cols) > 1 else cols[0]
         return seg.gather(table, elem_si)
@@ -265,11 +284,17 @@ class O3Linear(nn.Module):
     def forward(self, x):
         N = x.shape[0]
         outs = [None] * len(self.irreps_out.blocks)
-        for ii, io, off, mi, mo, a in self.paths:
+        # input blocks by ONE split (backward: one concat; per-block slices would zero-fill
+        # and copy a full-width gradient each); a scalar-only input may be just its first block
+        sizes = [b - a for a, b in self.sl_in]
+        if x.shape[1] == sizes[0] and all(p[0] == 0 for p in self.paths):
+            xs = [x]
+        else:
+            xs = torch.split(x, sizes, 1) if len(sizes) > 1 else [x]
+        for (ii, io, off, mi, mo, a), W in zip(self.paths, self.path_weights()):
             l = self.irreps_in.blocks[ii][1]
             d = 2 * l + 1
-            xi = x[:, self.sl_in[ii][0]:self.sl_in[ii][1]].reshape(N, mi, d)
-            W = self.weight[off:off + mi * mo].view(mi, mo) * a
+            xi = xs[ii].reshape(N, mi, d)
             if d == 1:  # scalars: a plain [N, mi] x [mi, mo] GEMM
                 y = (xi.reshape(N, mi) @ W).view(N, mo, 1)
             else:  # one (N*d, mi) x (mi, mo) GEMM instead of an N-batched tiny bmm
@@ -281,7 +306,7 @@ class O3Linear(nn.Module):
             if o is None:
                 o = x.new_zeros(N, mo, 2 * lo + 1)
             res.append(o.reshape(N, -1))
-        return torch.cat(res, -1)
+        return res[0] if len(res) == 1 else torch.cat(res, -1)
 
 
 def _silu_2mom():

@@ -110,3 +110,41 @@ def test_multibranch_bf16_grouped_heads_captured_vs_eager_gpu():
             idx = list(rng.choice(len(samples), 6, replace=False))
             le, lc = float(eager(store, idx)[0]), float(cap(store, idx)[0])
             assert abs(le - lc) <= 3e-2 * max(1.0, abs(le)), (le, lc)
+
+
+def test_mace_stacked_dense_decode_matches_branch_loop(monkeypatch):
+    """MACE's dense multi-branch read-out runs the branches stacked (one GEMM per layer for
+    all branches + a per-row gather); gradients equal the per-branch torch.where loop."""
+    from hydragnn_amd.models.mace import MultiheadDecoderBlock
+
+    samples = _data()
+    m = _model("MACE")
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph", "node"], head_dims=[1, 1])
+    ts = TrainStep(m, lr=1e-3, mode="eager")
+    idx = store.branch_order(list(range(7)))[0]
+    Np, Ep = ts.bucket_of(*store.sizes_of(idx))
+    lay = store.layout(idx, Np=Np, Ep=Ep, Gp=len(idx) + 1)
+    buf = store.upload(idx, lay)
+    calls = []
+    orig = MultiheadDecoderBlock._stacked_dense
+
+    def spy(self, *a):
+        out = orig(self, *a)
+        calls.append(out is not None)
+        return out
+
+    def run():
+        m.zero_grad(set_to_none=True)
+        loss, _ = ts._loss(store.assemble(buf, lay, branch_sorted=True))
+        loss.backward()
+        return float(loss), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    monkeypatch.setattr(MultiheadDecoderBlock, "_stacked_dense", spy)
+    l1, g1 = run()
+    assert calls and all(calls)
+    monkeypatch.setattr(MultiheadDecoderBlock, "_stacked_dense", lambda self, *a: None)
+    l2, g2 = run()
+    assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l2))
+    assert g1.keys() == g2.keys()
+    for k in g1:
+        torch.testing.assert_close(g1[k], g2[k], rtol=1e-4, atol=1e-6, msg=k)
