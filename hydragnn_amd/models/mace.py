@@ -365,7 +365,9 @@ class MultiheadDecoderBlock(nn.Module):
         # the read-outs only use the scalar channels; the stack hands over just those
         sc = node_features if node_features.shape[1] == self.input_scalar_dim else \
             node_features[:, :self.input_scalar_dim]
-        gfeat = sc.mean(0, keepdim=True) if gsi is None else seg.segment_mean(sc, gsi)
+        # padded batch: the limit skips the padding graph's (long, all-zero) segment
+        gfeat = sc.mean(0, keepdim=True) if gsi is None else \
+            seg.segment_mean(sc, gsi, limit=ctx.data.get("num_valid"))
         data = ctx.data
         outs = []
         granges, nranges = data.get("branch_graph_ranges"), data.get("branch_node_ranges")
@@ -526,7 +528,10 @@ class MACEStack(Base):
         if ctx.graph_si is None:
             pos = pos - pos.mean(0, keepdim=True)
         else:
-            pos = pos - seg.gather(seg.segment_mean(pos, ctx.graph_si), ctx.graph_si)
+            # (padded batch: the padding graph's rows are skipped by the limit; its nodes keep
+            # their raw positions, a common shift that leaves every padding distance unchanged)
+            pos = pos - seg.gather(seg.segment_mean(pos, ctx.graph_si, limit=data.get("num_valid")),
+                                   ctx.graph_si)
         vec, dist = edge_vectors_and_lengths(pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
         node_attrs, elem = process_node_attributes(data.x)
         # element-indexed weight tables are gathered, not multiplied by the one-hot: the node

@@ -11,6 +11,8 @@ fp32 in / fp32 out at the module boundary, bf16 MFMA inside (operands rounded to
 fp32 accumulation), backward = one data-gradient NT GEMM and one split-M weight-gradient
 TN GEMM whose last-arriving split block reduces each tile (bias gradient from the ones lane).
 """
+import os
+
 import torch
 
 from .. import _native
@@ -88,6 +90,7 @@ def _slab(dev, numel):
 
 
 _counters = {}
+_FUSED_TN_REDUCE = os.environ.get("HYDRA_TN_FUSED_REDUCE", "0") == "1"
 
 
 def _counter_buf(dev, n):
@@ -105,6 +108,15 @@ def tn_reduce(G, X, Np, Kp, slab, S, outs, *, X2=None, kc1=None, boff=None, beta
     """``slab = G^T [X | X2]`` split over rows, reduced in the same launch into ``outs``:
     (out, n0, k0, N, K, bias_out or None, bias_col) per destination (up to 3)."""
     groups = 1 if boff is None else boff.numel() - 1
+    if not _FUSED_TN_REDUCE:
+        # measured on MI355X (EGNN-866 bf16, profiles/r3_rocprof_cfg_multibranch_egnn_bf16_*):
+        # the in-launch last-arriver reduce made tn_kernel 4.6x slower (30 -> 138 us per call,
+        # device-scope release/acquire per split block under load) than the GEMM + one
+        # slab_reduce launch per destination (12 us), so the separate reduce is the default
+        _native.ops().bg_tn(G, X, X2, Kp if kc1 is None else kc1, Np, Kp, slab, S, boff, [], [], [], 0.0, None)
+        for out, n0, k0, N, K, bias_out, bias_col in outs:
+            _native.ops().bg_slab_reduce(slab, S, Np, Kp, n0, k0, N, K, out, beta, bias_col, bias_out, groups)
+        return
     cnt = _counter_buf(G.device, groups * (Np // 128) * (Kp // 128))
     meta = []
     for o in outs:

@@ -226,6 +226,32 @@ def element_index(elem, num_elements):
     return seg.SegIndex(elem.to(torch.int32), rowptr, perm, num_elements)
 
 
+class _IrrepsLinear(torch.autograd.Function):
+    """Native o3.Linear (csrc/irreps_linear.hip): forward and input gradient are the same
+    column-table kernel in two orientations; the weight gradient is a split node reduction
+    (first-order; composite mode runs the torch path)."""
+
+    @staticmethod
+    def forward(ctx, x, W, fwd, bwd, jobs, maxd, wscale):
+        from .. import _native
+
+        x = x.contiguous()
+        ctx.save_for_backward(x, W)
+        ctx.tabs = (bwd, jobs, maxd, wscale)
+        return _native.ops().irreps_linear(x, W, fwd[0], fwd[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        x, W = ctx.saved_tensors
+        bwd, jobs, maxd, wscale = ctx.tabs
+        g = g.contiguous()
+        dx = _native.ops().irreps_linear(g, W, bwd[0], bwd[1]) if ctx.needs_input_grad[0] else None
+        dW = _native.ops().irreps_linear_wgrad(x, g, jobs, wscale, maxd) if ctx.needs_input_grad[1] else None
+        return dx, dW, None, None, None, None, None
+
+
 class O3Linear(nn.Module):
     """e3nn ``o3.Linear`` semantics: per (l, p) channel mixing, N(0,1) weights scaled by
     1/sqrt(fan_in) in the forward ("element" path normalisation), no bias."""
@@ -251,6 +277,58 @@ class O3Linear(nn.Module):
         for _, _, off, mi, mo, a in self.paths:
             scale[off:off + mi * mo] = a
         self.register_buffer("wscale", scale, persistent=False)
+
+    # ---- native (HIP) path: csrc/irreps_linear.hip, one launch forward, two backward
+    def _native_tables(self, dev):
+        t = getattr(self, "_ntabs", None)
+        if t is not None and t[0] == dev:
+            return t[1]
+        import numpy as np
+
+        def bits(a):
+            return int(np.array([a], dtype=np.float32).view(np.int32)[0])
+
+        def orient(transposed):
+            # column table over the orientation's OUTPUT columns, paths grouped by output block
+            oblocks = self.irreps_in.blocks if transposed else self.irreps_out.blocks
+            osl = self.sl_in if transposed else self.sl_out
+            prow, cols = [], []
+            for ob, (m, l, _) in enumerate(oblocks):
+                d = 2 * l + 1
+                p0 = len(prow)
+                for ii, io, off, mi, mo, a in self.paths:
+                    if (ii if transposed else io) != ob:
+                        continue
+                    if transposed:  # dX: reduce over o, weight index off + i * mo + o
+                        prow.append([self.sl_out[io][0], mo, off, 1, mo, d, bits(a)])
+                    else:
+                        prow.append([self.sl_in[ii][0], mi, off, mo, 1, d, bits(a)])
+                p1 = len(prow)
+                for u in range(m):
+                    for c in range(d):
+                        cols.append([p0, p1, u, c])
+                assert len(cols) == osl[ob][1]
+            return (torch.tensor(prow, dtype=torch.int32, device=dev).reshape(-1, 7),
+                    torch.tensor(cols, dtype=torch.int32, device=dev).reshape(-1, 4))
+
+        jobs = []
+        for ii, io, off, mi, mo, a in self.paths:
+            d = 2 * self.irreps_in.blocks[ii][1] + 1
+            for i0 in range(0, mi, 64):
+                for o0 in range(0, mo, 64):
+                    jobs.append([self.sl_in[ii][0], self.sl_out[io][0], mi, mo, d, off, i0, o0])
+        fwd, bwd = orient(False), orient(True)
+        tabs = (fwd, bwd, torch.tensor(jobs, dtype=torch.int32, device=dev).reshape(-1, 8),
+                max([2 * l + 1 for _, l, _ in self.irreps_in.blocks] + [1]))
+        self._ntabs = (dev, tabs)
+        return tabs
+
+    def native_ok(self, x):
+        from . import pna as _mode
+
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == self.irreps_in.dim
+                and 0 < x.shape[1] <= 1024 and len(self.paths) > 0 and self.irreps_in.lmax <= 4
+                and _mode.fused("o3linear"))
 
     def path_weights(self):
         """[mi, mo] normalised weight of every path (views of one scaled vector)."""
@@ -279,9 +357,16 @@ class O3Linear(nn.Module):
                     W = Wp
             cols.append(W if W is not None else self.weight.new_zeros(mi, self.irreps_out.blocks[io][0]))
         table = torch.cat(cols, 1) if len(cols) > 1 else cols[0]
+        if table.is_cuda:  # backward = one GEMM over the element one-hot (few, long segments)
+            return elem_si.onehot_t(table.dtype).t() @ table
         return seg.gather(table, elem_si)
 
     def forward(self, x):
+        from .linear import linear
+
+        if self.native_ok(x):
+            fwd, bwd, jobs, maxd = self._native_tables(x.device)
+            return _IrrepsLinear.apply(x, self.weight, fwd, bwd, jobs, maxd, self.wscale)
         N = x.shape[0]
         outs = [None] * len(self.irreps_out.blocks)
         # input blocks by ONE split (backward: one concat; per-block slices would zero-fill
@@ -296,9 +381,9 @@ class O3Linear(nn.Module):
             d = 2 * l + 1
             xi = xs[ii].reshape(N, mi, d)
             if d == 1:  # scalars: a plain [N, mi] x [mi, mo] GEMM
-                y = (xi.reshape(N, mi) @ W).view(N, mo, 1)
+                y = linear(xi.reshape(N, mi), W.t()).view(N, mo, 1)
             else:  # one (N*d, mi) x (mi, mo) GEMM instead of an N-batched tiny bmm
-                y = (xi.transpose(1, 2).reshape(N * d, mi) @ W).view(N, d, mo).transpose(1, 2)
+                y = linear(xi.transpose(1, 2).reshape(N * d, mi), W.t()).view(N, d, mo).transpose(1, 2)
             outs[io] = y if outs[io] is None else outs[io] + y
         res = []
         for io, (mo, lo, _) in enumerate(self.irreps_out.blocks):
@@ -329,9 +414,13 @@ class FullyConnectedNet(nn.Module):
         self.weights = nn.ParameterList([nn.Parameter(torch.randn(a, b)) for a, b in zip(dims[:-1], dims[1:])])
 
     def forward(self, x):
+        from .linear import linear
+
         n = len(self.weights)
         for i, W in enumerate(self.weights):
-            x = x @ W / math.sqrt(W.shape[0])
+            # edge-sized rows: the weight gradient (K = edges) takes the split-K wgrad kernel
+            # of ops.linear on the GPU instead of a library GEMM with a handful of workgroups
+            x = linear(x, W.t()) / math.sqrt(W.shape[0])
             if i < n - 1:
                 x = torch.nn.functional.silu(x) * _SILU_C
         return x
@@ -570,7 +659,10 @@ class _SymConNative(torch.autograd.Function):
         x, Wcat, ents, grps = ctx.saved_tensors
         dx, dWn = _native.ops().symcon_bwd(gout, x, ctx.elem_si.index, Wcat, ents, grps)
         N, Ktot, H = dWn.shape
-        dW = seg.segment_sum(dWn.view(N, Ktot * H), ctx.elem_si).view(ctx.ne, Ktot, H)
+        # per-element reduction over nodes: few, long segments (every node of an element,
+        # padding nodes included) -> one GEMM with the element one-hot (a CSR walk of the
+        # longest segment was 80+ us per layer on MI355X)
+        dW = (ctx.elem_si.onehot_t(dWn.dtype) @ dWn.view(N, Ktot * H)).view(ctx.ne, Ktot, H)
         grads, o = [], 0
         for K in ctx.shapes:
             grads.append(dW[:, o:o + K])

@@ -23,7 +23,7 @@ from .. import _native
 class SegIndex:
     """Row -> segment mapping with a CSR view (all index tensors int32)."""
 
-    __slots__ = ("index", "rowptr", "perm", "num_segments", "_deg", "_index64")
+    __slots__ = ("index", "rowptr", "perm", "num_segments", "_deg", "_index64", "_onehot_t")
 
     def __init__(self, index, rowptr, perm, num_segments):
         self.index = index
@@ -32,10 +32,21 @@ class SegIndex:
         self.num_segments = int(num_segments)
         self._deg = None
         self._index64 = None
+        self._onehot_t = None
 
     @property
     def num_rows(self):
         return self.index.numel()
+
+    def onehot_t(self, dtype=torch.float32):
+        """[num_segments, rows] 0/1 matrix, built once per index: a segment sum over FEW,
+        LONG segments (element-indexed weight tables: a handful of elements over every node
+        of the batch) is then one GEMM instead of a serial walk down each segment."""
+        if self._onehot_t is None or self._onehot_t.dtype != dtype:
+            oh = torch.zeros(self.num_segments, self.num_rows, device=self.index.device, dtype=dtype)
+            oh.scatter_(0, self.index64.view(1, -1), 1.0)
+            self._onehot_t = oh
+        return self._onehot_t
 
     @property
     def index64(self):
