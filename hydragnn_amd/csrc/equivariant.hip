@@ -101,6 +101,113 @@ __global__ void __launch_bounds__(256) tp_uvu_bwd_kernel(const float* __restrict
 // one contiguous range), lanes over channels; neither the gathered [E, ld1] operand nor
 // the [E, out] message tensor exists.  Backward: d x1 by a source-CSR pass (one wave
 // per source node, atomic-free), dY / dw by an edge pass reading go[dst_e].
+// Every (l1, l2, l3) instruction body is compiled with its degrees as template constants
+// (dispatched by a wave-uniform switch): the per-lane operand and accumulator arrays then
+// live in VGPRs with every loop unrolled.  (Runtime-sized loops over fixed-size arrays put
+// them in scratch memory: 440-590 us per launch at MACE-multibranch size on MI355X, vs.
+// the einsum/bmm composite's ~60 us per call.)
+#define HY_TP_LCASES(X)                                                                                   \
+  X(0, 0, 0) X(0, 1, 1) X(0, 2, 2) X(0, 3, 3) X(1, 0, 1) X(1, 1, 0) X(1, 1, 1) X(1, 1, 2) X(1, 2, 1)      \
+  X(1, 2, 2) X(1, 2, 3) X(1, 3, 2) X(1, 3, 3) X(2, 0, 2) X(2, 1, 1) X(2, 1, 2) X(2, 1, 3) X(2, 2, 0)      \
+  X(2, 2, 1) X(2, 2, 2) X(2, 2, 3) X(2, 3, 1) X(2, 3, 2) X(2, 3, 3) X(3, 0, 3) X(3, 1, 2) X(3, 1, 3)      \
+  X(3, 2, 1) X(3, 2, 2) X(3, 2, 3) X(3, 3, 0) X(3, 3, 1) X(3, 3, 2) X(3, 3, 3)
+
+__device__ __forceinline__ int tp_lcode(int l1, int l2, int l3) { return (l1 * 4 + l2) * 4 + l3; }
+
+// out[n, u, :] = sum_{e in dst segment} w[e, u] * C(x1[src_e, u, :], Y_e)
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void conv_fwd_body(const float* __restrict__ x1, int ld1, const float* __restrict__ y,
+                                              int ld2, const float* __restrict__ w, int ldw,
+                                              const int* __restrict__ src, int e0, int e1, const int* r,
+                                              const float* __restrict__ C, int u, float* __restrict__ o) {
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  float acc[D3];
+#pragma unroll
+  for (int k = 0; k < D3; ++k) acc[k] = 0.f;
+  for (int e = e0; e < e1; ++e) {
+    const float* a = x1 + (int64_t)src[e] * ld1 + r[4] + u * D1;
+    const float* yb = y + (int64_t)e * ld2 + r[5];
+    const float wu = w[(int64_t)e * ldw + r[6] + u];
+    float av[D1], yv[D2];
+#pragma unroll
+    for (int i = 0; i < D1; ++i) av[i] = a[i] * wu;
+#pragma unroll
+    for (int j = 0; j < D2; ++j) yv[j] = yb[j];
+#pragma unroll
+    for (int i = 0; i < D1; ++i)
+#pragma unroll
+      for (int j = 0; j < D2; ++j) {
+        const float p = av[i] * yv[j];
+#pragma unroll
+        for (int k = 0; k < D3; ++k) acc[k] = fmaf(C[(i * D2 + j) * D3 + k], p, acc[k]);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < D3; ++k) o[k] = acc[k];
+}
+
+// gx1[n, u, :] += sum_{e in src segment} w[e, u] * C^T(go[dst_e, u, :], Y_e)
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void conv_bwdx_body(const float* __restrict__ go, int ldo, const float* __restrict__ y,
+                                               int ld2, const float* __restrict__ w, int ldw,
+                                               const int* __restrict__ dst, const int* __restrict__ sperm, int b,
+                                               int eN, const int* r, const float* __restrict__ C, int u,
+                                               float* __restrict__ o) {
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  float ga[D1];
+#pragma unroll
+  for (int i = 0; i < D1; ++i) ga[i] = 0.f;
+  for (int q = b; q < eN; ++q) {
+    const int e = sperm ? sperm[q] : q;
+    const float* g = go + (int64_t)dst[e] * ldo + r[7] + u * D3;
+    const float* yb = y + (int64_t)e * ld2 + r[5];
+    const float wu = w[(int64_t)e * ldw + r[6] + u];
+    float gv[D3], yv[D2];
+#pragma unroll
+    for (int k = 0; k < D3; ++k) gv[k] = g[k] * wu;
+#pragma unroll
+    for (int j = 0; j < D2; ++j) yv[j] = yb[j];
+#pragma unroll
+    for (int i = 0; i < D1; ++i)
+#pragma unroll
+      for (int j = 0; j < D2; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < D3; ++k) s = fmaf(C[(i * D2 + j) * D3 + k], gv[k], s);
+        ga[i] = fmaf(s, yv[j], ga[i]);
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < D1; ++i) o[i] += ga[i];
+}
+
+// per edge and channel: gw[e, u]; gY partial sums (reduced over the channels by the caller)
+template <int L1, int L2, int L3>
+__device__ __forceinline__ float conv_bwde_body(const float* __restrict__ a, const float* __restrict__ g,
+                                                const float* __restrict__ yb, float wu,
+                                                const float* __restrict__ C, float* gyl) {
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  float av[D1], gv[D3], yv[D2];
+#pragma unroll
+  for (int i = 0; i < D1; ++i) av[i] = a[i];
+#pragma unroll
+  for (int k = 0; k < D3; ++k) gv[k] = g[k];
+#pragma unroll
+  for (int j = 0; j < D2; ++j) yv[j] = yb[j];
+  float gwu = 0.f;
+#pragma unroll
+  for (int i = 0; i < D1; ++i)
+#pragma unroll
+    for (int j = 0; j < D2; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < D3; ++k) s = fmaf(C[(i * D2 + j) * D3 + k], gv[k], s);
+      gwu = fmaf(s * av[i], yv[j], gwu);
+      gyl[j] = fmaf(wu * av[i], s, gyl[j]);
+    }
+  return gwu;
+}
+
 __global__ void __launch_bounds__(256) tp_conv_fwd_kernel(const float* __restrict__ x1, int ld1,
                                                           const float* __restrict__ y, int ld2,
                                                           const float* __restrict__ w, int ldw,
@@ -114,26 +221,20 @@ __global__ void __launch_bounds__(256) tp_conv_fwd_kernel(const float* __restric
   const int e0 = drp[n], e1 = drp[n + 1];
   for (int t = 0; t < nins; ++t) {
     const int* r = ins + t * kInsCols;
-    const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
     const float* C = cg + r[8];
     for (int u = lane; u < m; u += 64) {
-      float acc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int e = e0; e < e1; ++e) {
-        const float* a = x1 + (int64_t)src[e] * ld1 + r[4] + u * d1;
-        const float* yb = y + (int64_t)e * ld2 + r[5];
-        const float wu = w[(int64_t)e * ldw + r[6] + u];
-        float av[7], yv[7];
-        for (int i = 0; i < d1; ++i) av[i] = a[i];
-        for (int j = 0; j < d2; ++j) yv[j] = yb[j];
-        for (int k = 0; k < d3; ++k) {
-          float s = 0.f;
-          for (int i = 0; i < d1; ++i)
-            for (int j = 0; j < d2; ++j) s = fmaf(C[(i * d2 + j) * d3 + k] * av[i], yv[j], s);
-          acc[k] = fmaf(wu, s, acc[k]);
-        }
+      float* o = out + (int64_t)n * ldo + r[7] + u * (2 * r[2] + 1);
+      switch (code) {
+#define HY_X(a, b, c)                                                             \
+  case (a * 4 + b) * 4 + c:                                                       \
+    conv_fwd_body<a, b, c>(x1, ld1, y, ld2, w, ldw, src, e0, e1, r, C, u, o); \
+    break;
+        HY_TP_LCASES(HY_X)
+#undef HY_X
+        default:
+          break;
       }
-      float* o = out + (int64_t)n * ldo + r[7] + u * d3;
-      for (int k = 0; k < d3; ++k) o[k] = acc[k];
     }
   }
 }
@@ -153,29 +254,20 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_x_kernel(const float* __restr
   const int b = srp[n], eN = srp[n + 1];
   for (int t = 0; t < nins; ++t) {
     const int* r = ins + t * kInsCols;
-    const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
     const float* C = cg + r[8];
     for (int u = lane; u < m; u += 64) {
-      float ga[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int q = b; q < eN; ++q) {
-        const int e = sperm ? sperm[q] : q;
-        const float* g = go + (int64_t)dst[e] * ldo + r[7] + u * d3;
-        const float* yb = y + (int64_t)e * ld2 + r[5];
-        const float wu = w[(int64_t)e * ldw + r[6] + u];
-        float gv[7];
-        for (int k = 0; k < d3; ++k) gv[k] = g[k];
-        for (int i = 0; i < d1; ++i) {
-          float acc = 0.f;
-          for (int j = 0; j < d2; ++j) {
-            float s = 0.f;
-            for (int k = 0; k < d3; ++k) s = fmaf(C[(i * d2 + j) * d3 + k], gv[k], s);
-            acc = fmaf(s, yb[j], acc);
-          }
-          ga[i] = fmaf(wu, acc, ga[i]);
-        }
+      float* o = gx1 + (int64_t)n * ld1 + r[4] + u * (2 * r[0] + 1);
+      switch (code) {
+#define HY_X(a, b_, c)                                                                      \
+  case (a * 4 + b_) * 4 + c:                                                                \
+    conv_bwdx_body<a, b_, c>(go, ldo, y, ld2, w, ldw, dst, sperm, b, eN, r, C, u, o); \
+    break;
+        HY_TP_LCASES(HY_X)
+#undef HY_X
+        default:
+          break;
       }
-      float* o = gx1 + (int64_t)n * ld1 + r[4] + u * d1;
-      for (int i = 0; i < d1; ++i) o[i] += ga[i];
     }
   }
 }
@@ -196,6 +288,7 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_e_kernel(const float* __restr
   for (int t = 0; t < nins; ++t) {
     const int* r = ins + t * kInsCols;
     const int d1 = 2 * r[0] + 1, d2 = 2 * r[1] + 1, d3 = 2 * r[2] + 1, m = r[3];
+    const int code = tp_lcode(r[0], r[1], r[2]);
     const float* yb = y + e * ld2 + r[5];
     const float* C = cg + r[8];
     float gyl[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -204,20 +297,26 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_e_kernel(const float* __restr
       const float* g = go + (int64_t)dn * ldo + r[7] + u * d3;
       const float wu = w[e * ldw + r[6] + u];
       float gwu = 0.f;
-      for (int i = 0; i < d1; ++i) {
-        const float ai = a[i];
-        for (int j = 0; j < d2; ++j) {
-          float s = 0.f;
-          for (int k = 0; k < d3; ++k) s = fmaf(C[(i * d2 + j) * d3 + k], g[k], s);
-          gwu = fmaf(s * ai, yb[j], gwu);
-          gyl[j] = fmaf(wu * ai, s, gyl[j]);
-        }
+      switch (code) {
+#define HY_X(a_, b_, c_)                                              \
+  case (a_ * 4 + b_) * 4 + c_:                                        \
+    gwu = conv_bwde_body<a_, b_, c_>(a, g, yb, wu, C, gyl);           \
+    break;
+        HY_TP_LCASES(HY_X)
+#undef HY_X
+        default:
+          break;
       }
       gw[e * ldw + r[6] + u] = gwu;
     }
-    for (int j = 0; j < d2; ++j) {
-      const float v = wave_sum(gyl[j]);
-      if (lane == 0) gy[e * ld2 + r[5] + j] += v;
+    // gyl is indexed with compile-time constants inside each case body; the reduction
+    // below walks the (uniform) runtime width
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      if (j < d2) {
+        const float v = wave_sum(gyl[j]);
+        if (lane == 0) gy[e * ld2 + r[5] + j] += v;
+      }
     }
   }
 }

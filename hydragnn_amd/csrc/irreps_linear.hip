@@ -138,8 +138,15 @@ __global__ void il_wreduce_kernel(const float* __restrict__ slab, int S, int64_t
                                   const float* __restrict__ scale, float* __restrict__ dW) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= numel) return;
-  float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * numel + k];
+  // 8 independent partial chains keep 8 slab loads in flight (the order of the final
+  // combine is fixed: deterministic)
+  float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= S; s += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) part[u] += slab[(int64_t)(s + u) * numel + k];
+  for (; s < S; ++s) part[0] += slab[(int64_t)s * numel + k];
+  const float acc = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
   dW[k] = acc * scale[k];
 }
 
@@ -185,9 +192,9 @@ at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const
   auto dW = at::empty({numel}, x.options());
   if (numel == 0) return dW;
   if (N == 0 || J == 0) return dW.zero_();
-  // splits: ~256 workgroups over the chip, at least NCH nodes each, at most 16 (the reduce
+  // splits: ~256 workgroups over the chip, at least NCH nodes each, at most 64 (the reduce
   // reads every split's slab)
-  int64_t S = std::max<int64_t>(1, std::min<int64_t>({ceil_div(256, J), ceil_div(N, NCH), (int64_t)16}));
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>({ceil_div(256, J), ceil_div(N, NCH), (int64_t)64}));
   const int64_t per = ceil_div(N, S);
   S = ceil_div(N, per);
   // every split writes every weight element of every path (partial tiles mask their pad)

@@ -481,7 +481,11 @@ class MACEStack(Base):
         H = self.hidden_dim
         self.sh_irreps = o3.Irreps.sh(self.max_ell)
         if self.use_edge_attr:
-            self.edge_attrs_irreps = (o3.Irreps([(self.edge_dim, 0, 1)]) + self.sh_irreps).simplify()
+            # every edge-attribute scalar is its own 1x0e block (not merged with Y_0 into one
+            # multi-channel 0e block): the uvu product is the same function class (one weight
+            # per (u, v) either way), and single-channel blocks keep the fused HIP convolution
+            # (csrc/equivariant.hip) applicable
+            self.edge_attrs_irreps = o3.Irreps([(1, 0, 1)] * self.edge_dim) + self.sh_irreps
         else:
             self.edge_attrs_irreps = self.sh_irreps
         hidden = o3.Irreps.natural(H, self.node_max_ell)

@@ -508,7 +508,8 @@ class TensorProductUVU(nn.Module):
 
         # native (HIP) path tables: the second operand carries one channel per l (spherical
         # harmonics), which is the case the fused kernel implements (csrc/equivariant.hip)
-        self.native_ok = all(m2 == 1 for _, _, m2 in self.woff) and irreps2.lmax <= 3
+        # (the fused kernels compile every (l1, l2, l3) body with l <= 3)
+        self.native_ok = all(m2 == 1 for _, _, m2 in self.woff) and max(irreps1.lmax, irreps2.lmax, irreps_out.lmax) <= 3
         rows, cgs, cgoff = [], [], 0
         so = irreps_out.slices()
         for (i, j, k), (off, m1, m2) in zip(instructions, self.woff):
