@@ -147,7 +147,9 @@ def run(name, steps, warmup, dev):
             for _ in range(3):
                 step(draw())
             torch.cuda.synchronize()
-        print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=45), flush=True)
+        # BENCH_OP_SORT=count: the most frequently launched ops first (launch-bound steps)
+        key = "count" if os.environ.get("BENCH_OP_SORT") == "count" else "self_device_time_total"
+        print(prof.key_averages().table(sort_by=key, row_limit=70), flush=True)
     mark = os.environ.get("HYDRA_PROFILE_MARK") == "1"
     if mark:  # spin kernels bracket the timed steps: rocpd_summary.py --between spin_kernel
         torch.cuda._sleep(1000)

@@ -14,4 +14,5 @@ bash tools/gpu_r3_cfgs.sh || exit $?
 HYDRA_STEP_TIMING=1 timeout -k 10 240 python3 bench.py --steps 50 --warmup 10 > gpurun_out/headline_bench.log 2>&1 || exit $?
 tail -1 gpurun_out/headline_bench.log | cut -c1-600
 bash tools/gpu_prof_bench.sh r3_headline || exit $?
+bash tools/gpu_pmc_l2.sh || exit $?
 exit $rc
