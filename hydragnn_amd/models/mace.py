@@ -118,9 +118,29 @@ class RadialEmbeddingBlock(nn.Module):
 
 
 # ----------------------------------------------------------------------------- blocks
+_PERM_CACHE = {}
+
+
 def _to_channels(x, irreps):
-    """flat e3nn layout (blocks of [H, 2l+1], equal H) -> [N, H, sum(2l+1)]."""
+    """flat e3nn layout (blocks of [H, 2l+1], equal H) -> [N, H, sum(2l+1)].
+
+    The map is a fixed column permutation: on the GPU ONE column gather (backward: one
+    index-add) instead of per-block reshapes + concat (whose backward copies every
+    non-contiguous block gradient)."""
     N = x.shape[0]
+    if x.is_cuda and len(irreps.blocks) > 1:
+        key = (tuple(irreps.blocks), x.device)
+        perm = _PERM_CACHE.get(key)
+        if perm is None:
+            H = irreps.blocks[0][0]
+            cols = []
+            for u in range(H):
+                for (a, b), (m, l, _) in zip(irreps.slices(), irreps.blocks):
+                    d = 2 * l + 1
+                    cols += [a + u * d + c for c in range(d)]
+            perm = torch.tensor(cols, dtype=torch.long, device=x.device)
+            _PERM_CACHE[key] = perm
+        return x.index_select(1, perm).view(N, irreps.blocks[0][0], -1)
     parts = torch.split(x, [b - a for a, b in irreps.slices()], 1) if len(irreps.blocks) > 1 else [x]
     out = [t.reshape(N, m, 2 * l + 1) for t, (m, l, _) in zip(parts, irreps.blocks)]
     return torch.cat(out, -1) if len(out) > 1 else out[0]
@@ -143,6 +163,11 @@ class InteractionBlock(nn.Module):
         self.conv_tp_weights = o3.FullyConnectedNet([num_edge_feats + 2 * n_down] + 3 * [n_down]
                                                     + [self.conv_tp.weight_numel])
         self.linear = o3.O3Linear(irreps_mid.simplify(), target_irreps)
+        # the radial MLP's last 1/sqrt(fan_in) and the 1/avg_num_neighbors normalisation are
+        # constants on a chain that is linear in them (w -> TP -> segment sum -> linear):
+        # folded into the output linear's path scales instead of two elementwise passes
+        self.conv_tp_weights.defer_last_scale = True
+        self.linear.wscale.mul_(self.conv_tp_weights.last_scale() / avg_num_neighbors)
         self.skip_linear = o3.O3Linear(node_feats_irreps, hidden_irreps)
 
     def forward(self, h, edge_attrs, edge_feats, dst_si, src_si):
@@ -151,7 +176,7 @@ class InteractionBlock(nn.Module):
         down = self.linear_down(h)
         w = self.conv_tp_weights(torch.cat([edge_feats, seg.gather(down, src_si), seg.gather(down, dst_si)], -1))
         # gather -> uvu tensor product -> segment sum, fused on the GPU (one launch each way)
-        msg = self.linear(self.conv_tp.conv(up, edge_attrs, w, src_si, dst_si)) / self.avg_num_neighbors
+        msg = self.linear(self.conv_tp.conv(up, edge_attrs, w, src_si, dst_si))  # scales folded (init)
         return _to_channels(msg, self.target_irreps), sc
 
 
@@ -339,7 +364,8 @@ class MultiheadDecoderBlock(nn.Module):
                 return None
             x, rid = (gfeat, dn) if t == "graph" else (sc, dn_node)
             R = x.shape[0]
-            h = None
+            h = None  # [nb, features, R]: weights multiply from the LEFT, so the weight
+            # gradients come out in the parameters' own layout (no per-parameter copies)
             for li in range(len(chains[0])):
                 Ws = [c[li][0] for c in chains]
                 bs = [c[li][1] for c in chains]
@@ -348,15 +374,15 @@ class MultiheadDecoderBlock(nn.Module):
                 if li == 0:  # shared input: one GEMM against the branch-concatenated weights
                     xs = x * scale if scale != 1.0 else x
                     y = torch.nn.functional.linear(xs, torch.cat(Ws, 0), None if bs[0] is None else torch.cat(bs, 0))
-                    h = y.view(R, nb, out_dim).transpose(0, 1)
+                    h = y.t().view(nb, out_dim, R)
                 else:
                     hs = h * scale if scale != 1.0 else h
-                    W = torch.stack(Ws, 0).transpose(1, 2)
-                    h = torch.bmm(hs, W) if bs[0] is None else torch.baddbmm(torch.stack(bs, 0).unsqueeze(1), hs, W)
+                    W = torch.stack(Ws, 0)
+                    h = torch.bmm(W, hs) if bs[0] is None else torch.baddbmm(torch.stack(bs, 0).unsqueeze(2), W, hs)
                 if act is not None:
                     h = act(h)
-            h = h[:, :, :hd]
-            sel = h.gather(0, rid.clamp(min=0).view(1, R, 1).expand(1, R, hd)).squeeze(0)
+            h = h[:, :hd, :].permute(2, 0, 1)  # [R, nb, hd]
+            sel = h.gather(1, rid.clamp(min=0).view(R, 1, 1).expand(R, 1, hd)).squeeze(1)
             outs.append(torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype, device=sel.device)))
         return outs
 

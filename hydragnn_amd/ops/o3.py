@@ -404,6 +404,36 @@ def _silu_2mom():
 _SILU_C = _silu_2mom()
 
 
+class _TallMM(torch.autograd.Function):
+    """x @ W for edge-sized x and a [in, out] weight: the weight gradient x^T dY (K = edges)
+    takes the split-K wgrad kernel of csrc/linear.hip, written straight in the weight's
+    layout (a library GEMM picks a handful of workgroups for this shape)."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return x @ W
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        x, W = ctx.saved_tensors
+        dx = g @ W.t() if ctx.needs_input_grad[0] else None
+        dW = _native.ops().linear_wgrad(x, g.contiguous(), False)[0] if ctx.needs_input_grad[1] else None
+        return dx, dW
+
+
+def _mm_tall(x, W):
+    from . import pna as _mode
+    from .linear import MIN_ROWS
+
+    if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[0] >= MIN_ROWS and \
+            _mode.fused("linear") and torch.is_grad_enabled():
+        return _TallMM.apply(x, W)
+    return x @ W
+
+
 class FullyConnectedNet(nn.Module):
     """e3nn ``nn.FullyConnectedNet`` with silu: no biases, N(0,1) weights, 1/sqrt(fan_in),
     second-moment-normalised activation between layers."""
@@ -412,17 +442,28 @@ class FullyConnectedNet(nn.Module):
         super().__init__()
         self.dims = list(dims)
         self.weights = nn.ParameterList([nn.Parameter(torch.randn(a, b)) for a, b in zip(dims[:-1], dims[1:])])
+        # True: the last layer's 1/sqrt(fan_in) is left to the consumer (a linear one folds it
+        # into its own constants: the MACE convolution's output linear)
+        self.defer_last_scale = False
+
+    def last_scale(self):
+        """The constant the last layer's output still needs with ``defer_last_scale``: its
+        1/sqrt(fan_in) times the previous activation's normalisation."""
+        return (_SILU_C if len(self.weights) > 1 else 1.0) / math.sqrt(self.weights[-1].shape[0])
 
     def forward(self, x):
-        from .linear import linear
-
+        # the activation normalisation C and the next layer's 1/sqrt(fan_in) are ONE multiply
+        # of the pre-activation (same values as scaling after each step)
         n = len(self.weights)
+        carry = 1.0
         for i, W in enumerate(self.weights):
-            # edge-sized rows: the weight gradient (K = edges) takes the split-K wgrad kernel
-            # of ops.linear on the GPU instead of a library GEMM with a handful of workgroups
-            x = linear(x, W.t()) / math.sqrt(W.shape[0])
+            x = _mm_tall(x, W)
+            s = carry / math.sqrt(W.shape[0])
             if i < n - 1:
-                x = torch.nn.functional.silu(x) * _SILU_C
+                x = torch.nn.functional.silu(x * s)
+                carry = _SILU_C
+            elif not self.defer_last_scale:
+                x = x * s  # (deferred: s == last_scale(), applied by the consumer)
         return x
 
 

@@ -193,6 +193,13 @@ class BucketedGradSync:
     compute stream while RCCL moves the bucket over xGMI; ``finish`` joins the comm
     stream back before the optimizer reads the buffer.
 
+    Difference from the reference, by design: after ``finish`` EVERY parameter holds a
+    gradient (zeros where the step produced none), because a captured graph cannot vary
+    the optimizer's parameter set per step.  Fused AdamW therefore applies weight decay and
+    moment decay to parameters unused in a step (e.g. heads of branches absent from a
+    batch), where torch optimizers and the reference skip ``grad is None``.  The eager
+    path (and ZeRO, ``zero.py``) keep the reference semantics.
+
     Captured inside ``torch.cuda.graph`` the event fork/join becomes graph edges, so
     the replayed step is ONE graph launch whose collective nodes run concurrently
     with the remaining backward kernels.  On CPU tensors (gloo) the same code issues

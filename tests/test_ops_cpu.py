@@ -161,3 +161,24 @@ def test_gather_mul_sum_matches_composite_and_twice_differentiable():
     torch.testing.assert_close(seg.gather_mul_sum(x, w, gsi, ssi), ref)
     torch.autograd.gradcheck(lambda a, b: seg.gather_mul_sum(a, b, gsi, ssi), (x, w))
     torch.autograd.gradgradcheck(lambda a, b: seg.gather_mul_sum(a, b, gsi, ssi), (x, w))
+
+
+def test_fcn_folded_scales_match_definition():
+    """e3nn FullyConnectedNet: x W_i / sqrt(fan_i), silu * C between layers.  The folded
+    forward (C and the next 1/sqrt(fan) as one multiply; optionally the last scale left to
+    the consumer) gives the same values."""
+    import math
+
+    from hydragnn_amd.ops import o3
+
+    torch.manual_seed(0)
+    f = o3.FullyConnectedNet([10, 8, 8, 8, 6])
+    x = torch.randn(5, 10)
+    h = x
+    for i, W in enumerate(f.weights):
+        h = h @ W / math.sqrt(W.shape[0])
+        if i < 3:
+            h = torch.nn.functional.silu(h) * o3._SILU_C
+    torch.testing.assert_close(f(x), h)
+    f.defer_last_scale = True
+    torch.testing.assert_close(f(x) * f.last_scale(), h)
