@@ -336,7 +336,20 @@ class MultiheadDecoderBlock(nn.Module):
                 return None
         return steps
 
-    def _stacked_dense(self, names, gfeat, sc, dn, dn_node):
+    @staticmethod
+    def _row_select(ctx, rid, tag):
+        """(gather index [R, 1, 1] int64, valid-row mask [R, 1]) of a row -> branch id vector,
+        built once per forward and shared by every read-out (padding rows: id -1 -> 0, masked)."""
+        cache = ctx.get("_mace_rowsel")
+        if cache is None:
+            cache = {}
+            ctx._mace_rowsel = cache
+        key = (tag, rid.shape[0])
+        if key not in cache:
+            cache[key] = (rid.clamp(min=0).view(-1, 1, 1), (rid >= 0).to(torch.float32).view(-1, 1))
+        return cache[key]
+
+    def _stacked_dense(self, names, gfeat, sc, dn, dn_node, ctx=None):
         """Dense multi-branch decode with the branches STACKED: per layer one GEMM over all
         branches (the first layer's weights concatenated along the output, later layers one
         batched product), then one per-row gather of the row's own branch.  Same values as
@@ -382,8 +395,14 @@ class MultiheadDecoderBlock(nn.Module):
                 if act is not None:
                     h = act(h)
             h = h[:, :hd, :].permute(2, 0, 1)  # [R, nb, hd]
-            sel = h.gather(1, rid.clamp(min=0).view(R, 1, 1).expand(R, 1, hd)).squeeze(1)
-            outs.append(torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype, device=sel.device)))
+            if ctx is not None:
+                idx, valid = self._row_select(ctx, rid, t)
+                sel = h.gather(1, idx.expand(R, 1, hd)).squeeze(1)
+                outs.append(sel * valid.to(sel.dtype))
+            else:
+                sel = h.gather(1, rid.clamp(min=0).view(R, 1, 1).expand(R, 1, hd)).squeeze(1)
+                outs.append(torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype,
+                                                                                  device=sel.device)))
         return outs
 
     def forward(self, node_features, ctx, ids):
@@ -400,9 +419,11 @@ class MultiheadDecoderBlock(nn.Module):
         if self.num_branches > 1 and ids is None:
             # statically padded (captured) batch: every branch densely, selected per row
             dn = data.dataset_name.view(-1)
-            dn_node = dn.index_select(0, data.batch)
+            dn_node = ctx.get("_mace_dn_node")
+            if dn_node is None:  # once per forward (shared by every read-out)
+                dn_node = ctx._mace_dn_node = dn.index_select(0, data.batch)
             names = sorted(self.heads_NN[0].keys(), key=lambda k: int(k.split("-")[1]))
-            stacked = self._stacked_dense(names, gfeat, sc, dn, dn_node)
+            stacked = self._stacked_dense(names, gfeat, sc, dn, dn_node, ctx)
             if stacked is not None:
                 return stacked
             for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
