@@ -167,7 +167,7 @@ class InteractionBlock(nn.Module):
         # constants on a chain that is linear in them (w -> TP -> segment sum -> linear):
         # folded into the output linear's path scales instead of two elementwise passes
         self.conv_tp_weights.defer_last_scale = True
-        self.linear.wscale.mul_(self.conv_tp_weights.last_scale() / avg_num_neighbors)
+        self.linear.scale_paths(self.conv_tp_weights.last_scale() / avg_num_neighbors)
         self.skip_linear = o3.O3Linear(node_feats_irreps, hidden_irreps)
 
     def forward(self, h, edge_attrs, edge_feats, dst_si, src_si):

@@ -278,6 +278,13 @@ class O3Linear(nn.Module):
             scale[off:off + mi * mo] = a
         self.register_buffer("wscale", scale, persistent=False)
 
+    def scale_paths(self, f):
+        """Multiply every path normalisation by the constant ``f`` (a scale folded in from a
+        neighbouring linear op); keeps the torch scale vector and the native tables in step."""
+        self.paths = [(ii, io, off, mi, mo, a * f) for ii, io, off, mi, mo, a in self.paths]
+        self.wscale.mul_(f)
+        self._ntabs = None
+
     # ---- native (HIP) path: csrc/irreps_linear.hip, one launch forward, two backward
     def _native_tables(self, dev):
         t = getattr(self, "_ntabs", None)
