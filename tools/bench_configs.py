@@ -2,7 +2,7 @@
 (``bench.py`` is the driver's headline: config 4, OC20 PNAPlus + GPS).
 
   2  qm9_schnet        QM9-shaped molecules, SchNet 4 layers, graph energy head, batch 64
-                       (in-forward radius graph -> eager step)
+                       (in-forward radius graph, static capacity: captured step)
   3  md17_painn_forces MD17-shaped frames, PAINN (equivariant), node energy head, energy +
                        forces = -dE/dpos (compute_grad_energy, double backward), batch 32
   5a multibranch_egnn  SC25 multibranch shape: EGNN hidden 866 x 4, 5 branches, graph energy +
