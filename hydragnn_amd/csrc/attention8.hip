@@ -90,8 +90,9 @@ __device__ __forceinline__ KV8 ld_kv(const float* __restrict__ Kp, const float* 
   KV8 t;
   const int kc = min(k0, Nq - 16);  // prefetches past the split stay in bounds
   t.k = ld2(Kp + ((int64_t)h * Nq + kc + i) * 8 + 2 * g);
-  t.v = make_float4(vone, vone, vone, vone);
-  if (i < 8) t.v = ld4(Vq + (((int64_t)h * (Nq >> 2) + (kc >> 2) + g) * 8 + i) * 4);
+  // branch-free (a load under an exec branch makes the compiler drain vmcnt there)
+  const float4 v = ld4(Vq + (((int64_t)h * (Nq >> 2) + (kc >> 2) + g) * 8 + (i & 7)) * 4);
+  t.v = i < 8 ? v : make_float4(vone, vone, vone, vone);
   return t;
 }
 
@@ -282,8 +283,9 @@ __device__ __forceinline__ DQ8 ld_dq(const float* __restrict__ Kp, const float* 
   const int kc = min(k0, Nq - 16);
   t.k = ld2(Kp + ((int64_t)h * Nq + kc + i) * 8 + 2 * g);
   t.v = ld2(Vp + ((int64_t)h * Nq + kc + i) * 8 + 2 * g);
-  t.kt = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (i < 8) t.kt = ld4(Kq + (((int64_t)h * (Nq >> 2) + (kc >> 2) + g) * 8 + i) * 4);
+  // lanes i >= 8 load a duplicate column: rows 8..15 of dQ^T are junk and never stored
+  // (branch- and select-free: either makes the compiler wait for the load right away)
+  t.kt = ld4(Kq + (((int64_t)h * (Nq >> 2) + (kc >> 2) + g) * 8 + (i & 7)) * 4);
   return t;
 }
 
@@ -349,7 +351,7 @@ __device__ __forceinline__ void attn8_bwd_dq_body(int bx,
     bo0[t] = bo.x;
     bo1[t] = bo.y;
     nlse[t] = q < N ? -LSE2[(int64_t)h * Nq + q] : 0.f;
-    ndl[t] = q < N ? -delta[(int64_t)h * Nq + q] : 0.f;
+    ndl[t] = q < N ? delta[(int64_t)h * Nq + q] : 0.f;  // delta buffer holds -delta
     dq[t] = f4z();
   }
   DQ8 t0 = ld_dq(Kp, Kq, Vp, h, Nq, sp.cb, i, g), t1 = ld_dq(Kp, Kq, Vp, h, Nq, sp.cb + 16, i, g);
@@ -422,13 +424,9 @@ __device__ __forceinline__ KV8b ld_kvb(const float* __restrict__ Qp, const float
   const int qc = min(q0, Nq - 16);
   t.q = ld2(Qp + ((int64_t)h * Nq + qc + i) * 8 + 2 * g);
   t.o = ld2(dOp + ((int64_t)h * Nq + qc + i) * 8 + 2 * g);
-  t.qt = make_float4(0.f, 0.f, 0.f, 0.f);
-  t.ot = t.qt;
-  if (i < 8) {
-    const int64_t qo = (((int64_t)h * (Nq >> 2) + (qc >> 2) + g) * 8 + i) * 4;
-    t.qt = ld4(Qq + qo);
-    t.ot = ld4(dOq + qo);
-  }
+  const int64_t qo = (((int64_t)h * (Nq >> 2) + (qc >> 2) + g) * 8 + (i & 7)) * 4;
+  t.qt = ld4(Qq + qo);  // lanes i >= 8: duplicate columns (rows 8..15 of dK^T / dV^T unused)
+  t.ot = ld4(dOq + qo);
   t.lse = ld4(LSE2 + (int64_t)h * Nq + qc + 4 * g);
   t.dl = ld4(delta + (int64_t)h * Nq + qc + 4 * g);
   return t;
@@ -465,7 +463,7 @@ __device__ __forceinline__ void attn8_bwd_dkv_body(int bx,
     const KV8b tn = ld_kvb(Qp, Qq, dOp, dOq, LSE2, delta, h, Nq, q0 + 32, i, g);
     const bool full = q0 >= sp.ilo && q0 + 16 <= sp.ihi && q0 + 16 <= sp.ce;
     const f4v nl = f4v{-t0.lse.x, -t0.lse.y, -t0.lse.z, -t0.lse.w};
-    const f4v nd = f4v{-t0.dl.x, -t0.dl.y, -t0.dl.z, -t0.dl.w};
+    const f4v nd = f4v{t0.dl.x, t0.dl.y, t0.dl.z, t0.dl.w};  // delta buffer holds -delta
     f4v s[RT], dp[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -593,11 +591,424 @@ __global__ void __launch_bounds__(256) attn8_delta_pack_kernel(const float* __re
     pair[pair_idx(h, Nq, n, d)] = v;
     quad[quad_idx(h, Nq, n, d)] = v;
   }
-  delta[(int64_t)h * Nq + n] = a;
+  delta[(int64_t)h * Nq + n] = -a;  // stored negated: the MFMA accumulator seed of dP - delta
+}
+
+// ------------------------------------------------------------------- v2: one launch each way
+// The grid-split kernels above leave a combine (fwd) / partial-sum (bwd) launch behind and
+// run the forward in two passes over the keys (exact row max first).  v2:
+//   * a workgroup = W waves on the SAME RT query (or key) row tiles, each wave a 1/W slice
+//     of the other index; the W partial results meet in LDS and are merged in a fixed
+//     order at the end of the launch (deterministic, no partial buffers, no extra launch);
+//   * forward in ONE pass with a deferred-rescale softmax: scores are shifted by a running
+//     per-row reference m (exact max of the keys seen when it was last moved) that only
+//     moves when a score exceeds it by more than kTau (p <= 2^kTau, l stays far from fp32
+//     overflow); the check is 3 VALU ops per tile, the rescale (cross-lane max, o *= 2^dm)
+//     runs on the few tiles that raise a row's max by > kTau, so the score MFMAs run once
+//     per tile instead of twice.  Results equal the two-pass kernel to fp32 rounding;
+//   * lean tile bodies (the loops are issue-bound, not MFMA-bound, when written plainly):
+//     operands come through buffer loads whose lane offset is a loop-invariant VGPR and
+//     whose tile offset is a scalar (no per-tile 64-bit address VALU), two operand buffers
+//     are reloaded in place right after use (a register copy of an in-flight load would
+//     force a vmcnt drain), MFMA accumulator seeds (-m, -LSE, -delta) stay in persistent
+//     registers, the forward stores -LSE2 and the backward prep -delta so no tile negates;
+//     lanes i >= 8 load duplicate columns (rows 8..15 of the d-major products are junk and
+//     never stored) instead of selecting zeros, and the forward's row sum l is VALU adds.
+// Contract: the v2 forward returns NL = -LSE2 (rows Nq > q >= N: 0), which the v2 backward
+// consumes; the grid kernels keep LSE2.
+constexpr float kTau = 8.f;
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc mk_rsrc(const float* p, int nfloats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
+}
+__device__ __forceinline__ float2 bl2(Rsrc r, int vo, int so) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+__device__ __forceinline__ float4 bl4(Rsrc r, int vo, int so) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+__device__ __forceinline__ float max4(f4v s) { return fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3])); }
+
+// Byte offsets inside one head's [Nq][8] pair / [Nq/4][8][4] quad block: a 16-row tile at
+// row k0 starts at k0 * 32 bytes in both layouts; lane (i, g) reads
+//   pair: row k0 + i, float2 at 2g        -> (8 i + 2 g) * 4
+//   quad: rows k0 + 4g .. +3, column i&7   -> (32 g + 4 (i & 7)) * 4
+__device__ __forceinline__ int off_pair(int i, int g) { return (8 * i + 2 * g) * 4; }
+__device__ __forceinline__ int off_quad(int i, int g) { return (32 * g + 4 * (i & 7)) * 4; }
+
+template <int RT, int W>
+__global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restrict__ Qp,
+                                                            const float* __restrict__ Kp,
+                                                            const float* __restrict__ Vq, int N, int Nq, int H,
+                                                            const int* __restrict__ seg_id,
+                                                            const int* __restrict__ seg_ptr, float qscale,
+                                                            float* __restrict__ O, float* __restrict__ NL) {
+  __shared__ float red[W][RT][16][10];  // per wave and query: (m, l, o[8])
+  const int h = blockIdx.y;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int qbase = blockIdx.x * 16 * RT;
+  const SpanR<RT> sp = span_rt<RT>(qbase, i, N, seg_id, seg_ptr, W, w);
+  const Rsrc rk = mk_rsrc(Kp + (int64_t)h * Nq * 8, Nq * 8), rv = mk_rsrc(Vq + (int64_t)h * Nq * 8, Nq * 8);
+  const int ok_ = off_pair(i, g), ov_ = off_quad(i, g);
+  float bq0[RT], bq1[RT], m[RT], l[RT], thr[RT];
+  f4v o[RT], cin[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(sp.row[t], Nq - 1)) * 8 + 2 * g);
+    bq0[t] = bq.x * qscale;
+    bq1[t] = bq.y * qscale;
+    m[t] = -INFINITY;
+    thr[t] = -INFINITY;  // unset reference: any valid score moves it
+    l[t] = 0.f;
+    o[t] = f4z();
+    cin[t] = f4z();
+  }
+  // one key tile: S^T (shifted by the row references), mask, deferred rescale, O^T += V^T P^T.
+  // Tiles past the slice end (k0 >= ce, the odd tail of the 2-tile loop) are fully masked.
+  auto tile = [&](float2 kk, float4 vv, int k0) {
+    const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
+    f4v s[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(kk.x, bq0[t], cin[t]);
+      s[t] = mfma(kk.y, bq1[t], s[t]);
+    }
+    if (!full) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 4 * g + r;
+          if (!(key >= sp.b[t] && key < sp.e[t] && key < sp.ce)) s[t][r] = -INFINITY;
+        }
+    }
+    bool trig = false;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) trig |= max4(s[t]) > thr[t];
+    if (__any(trig)) {  // wave-uniform: move the row references, rescale o and l
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const float base = -cin[t][0];
+        const float mn = fmaxf(m[t], wmax16(max4(s[t])) + base);
+        if (mn > -INFINITY) {
+          const float f = fexp2(m[t] - mn), sh = mn - base;
+          o[t] = o[t] * f;
+          l[t] *= f;
+          s[t] = s[t] - f4v{sh, sh, sh, sh};
+          m[t] = mn;
+          thr[t] = kTau;
+          cin[t] = f4v{-mn, -mn, -mn, -mn};
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const float p0 = fexp2(s[t][0]), p1 = fexp2(s[t][1]), p2 = fexp2(s[t][2]), p3 = fexp2(s[t][3]);
+      o[t] = mfma(vv.x, p0, o[t]);
+      o[t] = mfma(vv.y, p1, o[t]);
+      o[t] = mfma(vv.z, p2, o[t]);
+      o[t] = mfma(vv.w, p3, o[t]);
+      l[t] += (p0 + p1) + (p2 + p3);
+    }
+  };
+  // load order pinned by scheduling barriers: the loop header is entered with the same
+  // in-flight sequence (ka va kb vb) from the preheader and from the latch, so the compiler's
+  // wait before the first tile is vmcnt(2), not a drain
+  const int cmax = (Nq - 16) * 32;
+  float2 ka = bl2(rk, ok_, min(sp.cb * 32, cmax));
+  float4 va = bl4(rv, ov_, min(sp.cb * 32, cmax));
+  __builtin_amdgcn_sched_barrier(0);
+  float2 kb = bl2(rk, ok_, min(sp.cb * 32 + 512, cmax));
+  float4 vb = bl4(rv, ov_, min(sp.cb * 32 + 512, cmax));
+  __builtin_amdgcn_sched_barrier(0);
+  for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
+    tile(ka, va, k0);
+    ka = bl2(rk, ok_, min(k0 * 32 + 1024, cmax));
+    va = bl4(rv, ov_, min(k0 * 32 + 1024, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+    tile(kb, vb, k0 + 16);
+    kb = bl2(rk, ok_, min(k0 * 32 + 1536, cmax));
+    vb = bl4(rv, ov_, min(k0 * 32 + 1536, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // o: lane (i, g) rows 4g + r of O^T for query i (g = 0, 1 -> d 0..7); l: this lane's
+  // 4-key share of the row sum -> total over the 4 lane groups
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    float lt = l[t] + __shfl_xor(l[t], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (g < 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][t][i][2 + 4 * g + r] = o[t][r];
+    } else if (g == 2) {
+      red[w][t][i][0] = m[t];
+      red[w][t][i][1] = lt;
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < RT * 128; idx += 64 * W) {
+    const int t = idx >> 7, qi = (idx >> 3) & 15, d = idx & 7;
+    const int qq = qbase + 16 * t + qi;
+    float M = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < W; ++v) M = fmaxf(M, red[v][t][qi][0]);
+    float lsum = 0.f, a = 0.f;
+    if (M > -INFINITY) {
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const float f = fexp2(red[v][t][qi][0] - M);
+        lsum = fmaf(red[v][t][qi][1], f, lsum);
+        a = fmaf(red[v][t][qi][2 + d], f, a);
+      }
+    }
+    if (qq < N) {
+      O[(int64_t)qq * 8 * H + h * 8 + d] = lsum > 0.f ? a * (1.f / lsum) : 0.f;
+      if (d == 0) NL[(int64_t)h * Nq + qq] = lsum > 0.f ? -(M + __log2f(lsum)) : INFINITY;
+    } else if (qq < Nq && d == 0) {
+      NL[(int64_t)h * Nq + qq] = 0.f;
+    }
+  }
+}
+
+// Backward v2: blocks [0, nbq) produce dQ for RT query tiles (W waves split the keys),
+// the rest dK | dV for RT key tiles (W waves split the queries); per-wave partials are
+// summed in LDS in wave order and written straight into dqkv [N, 3F].
+struct A8Bwd2 {
+  const float *Qp, *Qq, *Kp, *Kq, *Vp, *dOp, *dOq, *NL, *ndelta;
+  int N, Nq, H;
+  const int *seg_id, *seg_ptr;
+  float scale, qscale;
+  float* dqkv;
+  int nbq;
+};
+
+template <int RT, int W>
+__device__ __forceinline__ void attn8_bwd2_dq(const A8Bwd2& a, int bx, float* red) {
+  const int h = blockIdx.y;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int N = a.N, Nq = a.Nq;
+  const int base = bx * 16 * RT;
+  const SpanR<RT> sp = span_rt<RT>(base, i, N, a.seg_id, a.seg_ptr, W, w);
+  const int64_t hb = (int64_t)h * Nq * 8;
+  const Rsrc rk = mk_rsrc(a.Kp + hb, Nq * 8), rv = mk_rsrc(a.Vp + hb, Nq * 8), rkt = mk_rsrc(a.Kq + hb, Nq * 8);
+  const int op = off_pair(i, g), oq = off_quad(i, g);
+  float bq0[RT], bq1[RT], bo0[RT], bo1[RT];
+  f4v dq[RT], cs[RT], cd[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int q = sp.row[t], qc = min(q, Nq - 1);
+    const float2 bq = ld2(a.Qp + hb + (int64_t)qc * 8 + 2 * g);
+    const float2 bo = ld2(a.dOp + hb + (int64_t)qc * 8 + 2 * g);
+    bq0[t] = bq.x * a.qscale;
+    bq1[t] = bq.y * a.qscale;
+    bo0[t] = bo.x;
+    bo1[t] = bo.y;
+    const float nl = q < N ? a.NL[(int64_t)h * Nq + q] : 0.f;
+    const float nd = q < N ? a.ndelta[(int64_t)h * Nq + q] : 0.f;
+    cs[t] = f4v{nl, nl, nl, nl};
+    cd[t] = f4v{nd, nd, nd, nd};
+    dq[t] = f4z();
+  }
+  auto tile = [&](float2 kk, float2 vv, float4 kt, int k0) {
+    const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
+    f4v s[RT], dp[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(kk.x, bq0[t], cs[t]);
+      dp[t] = mfma(vv.x, bo0[t], cd[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(kk.y, bq1[t], s[t]);
+      dp[t] = mfma(vv.y, bo1[t], dp[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[r] = fexp2(s[t][r]) * dp[t][r];
+      if (!full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 4 * g + r;
+          if (!(key >= sp.b[t] && key < sp.e[t] && key < sp.ce)) ds[r] = 0.f;
+        }
+      }
+      dq[t] = mfma(kt.x, ds[0], dq[t]);
+      dq[t] = mfma(kt.y, ds[1], dq[t]);
+      dq[t] = mfma(kt.z, ds[2], dq[t]);
+      dq[t] = mfma(kt.w, ds[3], dq[t]);
+    }
+  };
+  const int cmax = (Nq - 16) * 32;
+  int o0 = min(sp.cb * 32, cmax), o1 = min(sp.cb * 32 + 512, cmax);
+  float2 ka = bl2(rk, op, o0), va = bl2(rv, op, o0);
+  float4 ta = bl4(rkt, oq, o0);
+  __builtin_amdgcn_sched_barrier(0);
+  float2 kb = bl2(rk, op, o1), vb = bl2(rv, op, o1);
+  float4 tb = bl4(rkt, oq, o1);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
+    tile(ka, va, ta, k0);
+    o0 = min(k0 * 32 + 1024, cmax);
+    ka = bl2(rk, op, o0);
+    va = bl2(rv, op, o0);
+    ta = bl4(rkt, oq, o0);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(kb, vb, tb, k0 + 16);
+    o1 = min(k0 * 32 + 1536, cmax);
+    kb = bl2(rk, op, o1);
+    vb = bl2(rv, op, o1);
+    tb = bl4(rkt, oq, o1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // red [W][RT][16 rows][8]: dQ^T rows 4g + r (g < 2) of column i
+  if (g < 2) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((w * RT + t) * 16 + i) * 8 + 4 * g + r] = dq[t][r];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < RT * 128; idx += 64 * W) {
+    const int t = idx >> 7, qi = (idx >> 3) & 15, d = idx & 7;
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < W; ++u) v += red[((u * RT + t) * 16 + qi) * 8 + d];
+    const int q = base + 16 * t + qi;
+    if (q < N) a.dqkv[(int64_t)q * 24 * a.H + h * 8 + d] = v * a.scale;
+  }
+}
+
+template <int RT, int W>
+__device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* red) {
+  const int h = blockIdx.y;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int N = a.N, Nq = a.Nq;
+  const int base = bx * 16 * RT;
+  // keys and queries share segments: the key rows' spans are the query ranges to visit
+  const SpanR<RT> sp = span_rt<RT>(base, i, N, a.seg_id, a.seg_ptr, W, w);
+  const int64_t hb = (int64_t)h * Nq * 8;
+  const Rsrc rq = mk_rsrc(a.Qp + hb, Nq * 8), ro = mk_rsrc(a.dOp + hb, Nq * 8);
+  const Rsrc rqt = mk_rsrc(a.Qq + hb, Nq * 8), rot = mk_rsrc(a.dOq + hb, Nq * 8);
+  const Rsrc rl = mk_rsrc(a.NL + (int64_t)h * Nq, Nq), rd = mk_rsrc(a.ndelta + (int64_t)h * Nq, Nq);
+  const int op = off_pair(i, g), oq = off_quad(i, g), os = 16 * g;
+  float bk0[RT], bk1[RT], bv0[RT], bv1[RT];
+  f4v dk[RT], dv[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int kc = min(sp.row[t], Nq - 1);
+    const float2 bk = ld2(a.Kp + hb + (int64_t)kc * 8 + 2 * g);
+    const float2 bv = ld2(a.Vp + hb + (int64_t)kc * 8 + 2 * g);
+    bk0[t] = bk.x * a.qscale;
+    bk1[t] = bk.y * a.qscale;
+    bv0[t] = bv.x;
+    bv1[t] = bv.y;
+    dk[t] = f4z();
+    dv[t] = f4z();
+  }
+  struct T6 {
+    float2 q, o;
+    float4 qt, ot, nl, nd;
+  };
+  auto load = [&](int q0) {
+    const int ob = min(q0 * 32, (Nq - 16) * 32), os_ = min(q0 * 4, (Nq - 16) * 4);
+    T6 x;
+    x.q = bl2(rq, op, ob);
+    x.o = bl2(ro, op, ob);
+    x.qt = bl4(rqt, oq, ob);
+    x.ot = bl4(rot, oq, ob);
+    x.nl = bl4(rl, os, os_);
+    x.nd = bl4(rd, os, os_);
+    return x;
+  };
+  auto tile = [&](const T6& x, int q0) {
+    const bool full = q0 >= sp.ilo && q0 + 16 <= sp.ihi && q0 + 16 <= sp.ce;
+    const f4v nl = f4v{x.nl.x, x.nl.y, x.nl.z, x.nl.w}, nd = f4v{x.nd.x, x.nd.y, x.nd.z, x.nd.w};
+    f4v s[RT], dp[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(x.q.x, bk0[t], nl);
+      dp[t] = mfma(x.o.x, bv0[t], nd);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      s[t] = mfma(x.q.y, bk1[t], s[t]);
+      dp[t] = mfma(x.o.y, bv1[t], dp[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = fexp2(s[t][r]);
+      if (!full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = q0 + 4 * g + r;
+          if (!(qq >= sp.b[t] && qq < sp.e[t] && qq < sp.ce)) p[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[r] = p[r] * dp[t][r];
+      dv[t] = mfma(x.ot.x, p[0], dv[t]);
+      dk[t] = mfma(x.qt.x, ds[0], dk[t]);
+      dv[t] = mfma(x.ot.y, p[1], dv[t]);
+      dk[t] = mfma(x.qt.y, ds[1], dk[t]);
+      dv[t] = mfma(x.ot.z, p[2], dv[t]);
+      dk[t] = mfma(x.qt.z, ds[2], dk[t]);
+      dv[t] = mfma(x.ot.w, p[3], dv[t]);
+      dk[t] = mfma(x.qt.w, ds[3], dk[t]);
+    }
+  };
+  T6 xa = load(sp.cb);
+  __builtin_amdgcn_sched_barrier(0);
+  T6 xb = load(sp.cb + 16);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int q0 = sp.cb; q0 < sp.ce; q0 += 32) {
+    tile(xa, q0);
+    xa = load(q0 + 32);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(xb, q0 + 16);
+    xb = load(q0 + 48);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // red [W][RT][16 rows][16]: (dK^T | dV^T) rows 4g + r (g < 2) of column i
+  if (g < 2) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[((w * RT + t) * 16 + i) * 16 + 4 * g + r] = dk[t][r];
+        red[((w * RT + t) * 16 + i) * 16 + 8 + 4 * g + r] = dv[t][r];
+      }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < RT * 256; idx += 64 * W) {
+    const int t = idx >> 8, ki = (idx >> 4) & 15, c = idx & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < W; ++u) v += red[((u * RT + t) * 16 + ki) * 16 + c];
+    const int k = base + 16 * t + ki;
+    if (k < N) {
+      const int F = 8 * a.H;
+      // dK at column F + 8h + d (x scale), dV at 2F + 8h + d
+      a.dqkv[(int64_t)k * 3 * F + (c < 8 ? F : 2 * F) + h * 8 + (c & 7)] = c < 8 ? v * a.scale : v;
+    }
+  }
+}
+
+template <int RT, int W>
+__global__ void __launch_bounds__(64 * W) attn8_bwd2_kernel(A8Bwd2 a) {
+  __shared__ float red[W * RT * 16 * 16];
+  if ((int)blockIdx.x < a.nbq)
+    attn8_bwd2_dq<RT, W>(a, blockIdx.x, red);
+  else
+    attn8_bwd2_dkv<RT, W>(a, blockIdx.x - a.nbq, red);
 }
 
 // ------------------------------------------------------------------------------------ host
-constexpr int kRT = 2;  // row tiles per wave
+constexpr int kRT = 2;  // row tiles per wave (grid-split kernels)
 
 static int pick_splits(int N, int H, int64_t splits) {
   if (splits > 0) return (int)splits;
@@ -606,6 +1017,108 @@ static int pick_splits(int N, int H, int64_t splits) {
   int S = 1;
   while (S < 16 && (int64_t)blocks * S * 4 < 5120 && N / (S * 2) >= 128) S *= 2;
   return S;
+}
+
+// v2 launch shape.  One row tile per wave (RT = 1: more rows per wave raised the register
+// count and lowered occupancy, measured slower); W, the waves that split one (row tile,
+// head) unit's key (query) range, is picked per launch so that the whole grid is resident
+// at once: with every unit of equal work, a grid of 1.25 "rounds" of resident workgroups
+// runs as two (the first round finishes together, then a quarter-full chip runs the rest),
+// which cost ~30% at the OC20 shape.  Cost model: rounds x tiles per wave, with the
+// resident workgroups per CU from the occupancy API (registers / LDS of each instantiation).
+// splits < 0 forces W = -splits (sweeps and tests).
+struct Occ {
+  int cus = 0;
+  int fwd[9] = {0}, bwd[9] = {0};
+};
+
+template <int W>
+static int occ_of(const void* f) {
+  int nb = 0;
+  HY_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * W, 0) == hipSuccess, "attn8: occupancy query");
+  return std::max(nb, 1);
+}
+
+static const Occ& occ() {
+  static Occ o = [] {
+    Occ r;
+    int dev = 0;
+    HY_CHECK(hipGetDevice(&dev) == hipSuccess, "attn8: hipGetDevice");
+    hipDeviceProp_t pr;
+    HY_CHECK(hipGetDeviceProperties(&pr, dev) == hipSuccess, "attn8: device properties");
+    r.cus = pr.multiProcessorCount;
+#define HY_OCC(W)                                                          \
+  r.fwd[W] = occ_of<W>((const void*)attn8_fwd2_kernel<1, W>);            \
+  r.bwd[W] = occ_of<W>((const void*)attn8_bwd2_kernel<1, W>);
+    HY_OCC(2) HY_OCC(3) HY_OCC(4) HY_OCC(5) HY_OCC(6) HY_OCC(8)
+#undef HY_OCC
+    return r;
+  }();
+  return o;
+}
+
+static int pick_w(int nwg, int ntiles, const int* per_cu, int cus) {
+  static const int cand[] = {2, 3, 4, 5, 6, 8};
+  int best = 8;
+  double bc = 1e30;
+  for (int W : cand) {
+    const int slots = std::max(per_cu[W], 1) * cus;
+    const double c = (double)ceil_div(nwg, slots) * (double)ceil_div(ntiles, W) + 0.01 * W;
+    if (c < bc) {
+      bc = c;
+      best = W;
+    }
+  }
+  return best;
+}
+
+template <int W>
+static void fwd2_go(const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H, const int* sid,
+                    const int* sptr, float qs, float* O, float* L) {
+  dim3 grid(ceil_div(Nq, 16), H);
+  attn8_fwd2_kernel<1, W><<<grid, 64 * W, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
+}
+
+static void launch_fwd2(int var, const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H,
+                        const int* sid, const int* sptr, float qs, float* O, float* L) {
+  const Occ& o = occ();
+  const int W = var > 0 ? var : pick_w(ceil_div(Nq, 16) * H, ceil_div(N, 16), o.fwd, o.cus);
+  switch (W) {
+    case 2: fwd2_go<2>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 3: fwd2_go<3>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 4: fwd2_go<4>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 5: fwd2_go<5>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 6: fwd2_go<6>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    default: fwd2_go<8>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+  }
+}
+
+template <int W>
+static void bwd2_go(A8Bwd2 b) {
+  b.nbq = ceil_div(b.Nq, 16);
+  dim3 grid(2 * b.nbq, b.H);
+  attn8_bwd2_kernel<1, W><<<grid, 64 * W, 0, stream()>>>(b);
+}
+
+static void launch_bwd2(int var, const A8Bwd2& b) {
+  const Occ& o = occ();
+  const int W = var > 0 ? var : pick_w(2 * ceil_div(b.Nq, 16) * b.H, ceil_div(b.N, 16), o.bwd, o.cus);
+  switch (W) {
+    case 2: bwd2_go<2>(b); break;
+    case 3: bwd2_go<3>(b); break;
+    case 4: bwd2_go<4>(b); break;
+    case 5: bwd2_go<5>(b); break;
+    case 6: bwd2_go<6>(b); break;
+    default: bwd2_go<8>(b); break;
+  }
+}
+
+// chosen W of the v2 kernels for a shape (tools / tests)
+std::vector<int64_t> attn8_v2_shape(int64_t N, int64_t H) {
+  const Occ& o = occ();
+  const int Nq = (int)((N + 15) / 16 * 16);
+  return {pick_w(ceil_div(Nq, 16) * (int)H, ceil_div(N, 16), o.fwd, o.cus),
+          pick_w(2 * ceil_div(Nq, 16) * (int)H, ceil_div(N, 16), o.bwd, o.cus), o.cus, o.fwd[6], o.bwd[6]};
 }
 
 static void chk_seg(const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N) {
@@ -645,8 +1158,13 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
   auto opt = Qp.options();
   auto O = at::empty({N, 8 * H}, opt), L = at::empty({H, Nq}, opt);
   if (N == 0) return {O, L};
-  const int S = pick_splits((int)N, (int)H, splits);
   const float qs = (float)scale * kLog2e;
+  if (splits <= 0) {  // v2: one launch, in-workgroup key split (variant -splits, 0 = default)
+    launch_fwd2((int)(-splits), Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(), (int)N, (int)Nq,
+                (int)H, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), qs, O.data_ptr<float>(), L.data_ptr<float>());
+    return {O, L};
+  }
+  const int S = pick_splits((int)N, (int)H, splits);
   dim3 grid(ceil_div(N, 64 * kRT), H, S);
   if (S == 1) {
     attn8_fwd_kernel<kRT><<<grid, 256, 0, stream()>>>(Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(),
@@ -772,6 +1290,30 @@ at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor
   chk_bwd(Qp, LSE2, pre[0], pre[1], N);
   chk_seg(seg_id, seg_ptr, N);
   HY_CHECK(Qq.numel() == Qp.numel() && pre[2].numel() == pre[1].numel(), "attn8_bwd: quad operand shapes");
+  if (splits <= 0) {
+    auto dqkv = at::empty({N, 3 * F}, dO.options());
+    if (N == 0) return dqkv;
+    A8Bwd2 b{};
+    b.Qp = Qp.data_ptr<float>();
+    b.Qq = Qq.data_ptr<float>();
+    b.Kp = Kp.data_ptr<float>();
+    b.Kq = Kq.data_ptr<float>();
+    b.Vp = Vp.data_ptr<float>();
+    b.dOp = pre[1].data_ptr<float>();
+    b.dOq = pre[2].data_ptr<float>();
+    b.NL = LSE2.data_ptr<float>();  // v2 forward: -LSE2
+    b.ndelta = pre[0].data_ptr<float>();
+    b.N = (int)N;
+    b.Nq = (int)Nq;
+    b.H = (int)H;
+    b.seg_id = seg_id.data_ptr<int>();
+    b.seg_ptr = seg_ptr.data_ptr<int>();
+    b.scale = (float)scale;
+    b.qscale = (float)scale * kLog2e;
+    b.dqkv = dqkv.data_ptr<float>();
+    launch_bwd2((int)(-splits), b);
+    return dqkv;
+  }
   const int S = pick_splits((int)N, (int)H, splits);
   at::Tensor dqkv, pq, pkv;
   A8Bwd a{};
@@ -819,6 +1361,7 @@ at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("attn8_pack(Tensor qkv, int H) -> Tensor[]");
+  m.def("attn8_v2_shape(int N, int H) -> int[]", hy::a8::attn8_v2_shape);
   m.def(
       "attn8_fwd(Tensor Qp, Tensor Kp, Tensor Vq, Tensor seg_id, Tensor seg_ptr, int N, float scale, int splits) -> "
       "Tensor[]");

@@ -2,7 +2,9 @@
 reference of the same segment-masked multi-head softmax attention: forward output and
 the gradients of q, k and v, for batch scope (one segment plus a padding segment) and
 graph scope (many small segments), at row counts that are and are not multiples of 16
-and for forced key/query split counts (the combine and partial-sum paths)."""
+for the single-launch v2 kernels (splits <= 0: in-workgroup key/query split, one-pass
+deferred-rescale softmax; variants -1..-4 are other (row tiles, waves) shapes) and for
+forced grid split counts (splits > 0: the combine and partial-sum paths)."""
 import math
 
 import pytest
@@ -26,7 +28,7 @@ def _segments(N, scope, dev):
 
 @pytest.mark.parametrize("N", [37, 300, 2560])
 @pytest.mark.parametrize("scope", ["batch", "graph"])
-@pytest.mark.parametrize("splits", [0, 1, 3])
+@pytest.mark.parametrize("splits", [0, -2, -3, -5, -8, 1, 3])
 def test_attn8_matches_reference(N, scope, splits):
     torch.manual_seed(N + splits)
     dev = torch.device("cuda")
@@ -44,3 +46,28 @@ def test_attn8_matches_reference(N, scope, splits):
     ref.backward(dO.double().cpu())
     dqkv = ops.attn8_bwd(dO, O, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, sc, splits)
     torch.testing.assert_close(dqkv.double().cpu(), x.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_attn8_v2_large_scores_rescale():
+    """Scores that grow along the key order force the deferred-rescale path many times
+    (every row's reference moves by > 8 log2 units several times within one wave's slice)."""
+    torch.manual_seed(7)
+    dev = torch.device("cuda")
+    N, H = 700, 8
+    ops = _native.ops()
+    qkv = torch.randn(N, 24 * H, device=dev)
+    ramp = torch.linspace(0.0, 12.0, N, device=dev).unsqueeze(1)
+    qkv[:, 8 * H:16 * H] *= ramp  # keys grow with their index
+    qkv[:, :8 * H] = qkv[:, :8 * H].abs() + 1.0
+    qkv[:, 8 * H:16 * H] = qkv[:, 8 * H:16 * H].abs()
+    sid, sptr = make_segments(N, "batch", num_valid=N - 3, device=dev)
+    sc = 1.0 / math.sqrt(8)
+    Qp, Qq, Kp, Kq, Vp, Vq = ops.attn8_pack(qkv, H)
+    O, L2 = ops.attn8_fwd(Qp, Kp, Vq, sid, sptr, N, sc, 0)
+    x = qkv.double().cpu().requires_grad_()
+    ref = attention_reference(x, H, sid.cpu(), sc)
+    torch.testing.assert_close(O.double().cpu(), ref.detach(), rtol=2e-5, atol=2e-5)
+    dO = torch.randn(N, 8 * H, device=dev)
+    ref.backward(dO.double().cpu())
+    dqkv = ops.attn8_bwd(dO, O, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, sc, 0)
+    torch.testing.assert_close(dqkv.double().cpu(), x.grad, rtol=1e-4, atol=2e-4)

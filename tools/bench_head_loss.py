@@ -1,10 +1,14 @@
 """Micro-benchmark of the one-workgroup head+loss kernels (csrc/mlp.hip) against the
 multi-launch path (fused MLP + masked loss): per-call time for several row counts and
 chain shapes.  GPU only."""
+import os
+import sys
+
 import torch
 
-from hydragnn_amd import _native
-from hydragnn_amd.ops import mlp as _mlp
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hydragnn_amd import _native  # noqa: E402
+from hydragnn_amd.ops import mlp as _mlp  # noqa: E402,F401
 
 
 def bench(fn, it=200):
