@@ -1020,57 +1020,13 @@ static int pick_splits(int N, int H, int64_t splits) {
 }
 
 // v2 launch shape.  One row tile per wave (RT = 1: more rows per wave raised the register
-// count and lowered occupancy, measured slower); W, the waves that split one (row tile,
-// head) unit's key (query) range, is picked per launch so that the whole grid is resident
-// at once: with every unit of equal work, a grid of 1.25 "rounds" of resident workgroups
-// runs as two (the first round finishes together, then a quarter-full chip runs the rest),
-// which cost ~30% at the OC20 shape.  Cost model: rounds x tiles per wave, with the
-// resident workgroups per CU from the occupancy API (registers / LDS of each instantiation).
+// count and lowered occupancy, measured slower); W waves split one (row tile, head) unit's
+// key (query) range.  Measured at the OC20 shape (Nq 2560, 8 heads, MI355X): W = 8 is the
+// fastest both ways (fwd 31.3 us vs 31.4-41.9 for W = 2..6; bwd 85.3 vs 87.4-109), an
+// occupancy-driven choice (fill exactly one round of resident workgroups) was slower; short
+// key ranges (graph scope, small batches) use fewer waves so no wave runs empty.
 // splits < 0 forces W = -splits (sweeps and tests).
-struct Occ {
-  int cus = 0;
-  int fwd[9] = {0}, bwd[9] = {0};
-};
-
-template <int W>
-static int occ_of(const void* f) {
-  int nb = 0;
-  HY_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * W, 0) == hipSuccess, "attn8: occupancy query");
-  return std::max(nb, 1);
-}
-
-static const Occ& occ() {
-  static Occ o = [] {
-    Occ r;
-    int dev = 0;
-    HY_CHECK(hipGetDevice(&dev) == hipSuccess, "attn8: hipGetDevice");
-    hipDeviceProp_t pr;
-    HY_CHECK(hipGetDeviceProperties(&pr, dev) == hipSuccess, "attn8: device properties");
-    r.cus = pr.multiProcessorCount;
-#define HY_OCC(W)                                                          \
-  r.fwd[W] = occ_of<W>((const void*)attn8_fwd2_kernel<1, W>);            \
-  r.bwd[W] = occ_of<W>((const void*)attn8_bwd2_kernel<1, W>);
-    HY_OCC(2) HY_OCC(3) HY_OCC(4) HY_OCC(5) HY_OCC(6) HY_OCC(8)
-#undef HY_OCC
-    return r;
-  }();
-  return o;
-}
-
-static int pick_w(int nwg, int ntiles, const int* per_cu, int cus) {
-  static const int cand[] = {2, 3, 4, 5, 6, 8};
-  int best = 8;
-  double bc = 1e30;
-  for (int W : cand) {
-    const int slots = std::max(per_cu[W], 1) * cus;
-    const double c = (double)ceil_div(nwg, slots) * (double)ceil_div(ntiles, W) + 0.01 * W;
-    if (c < bc) {
-      bc = c;
-      best = W;
-    }
-  }
-  return best;
-}
+static int pick_w(int ntiles) { return ntiles >= 32 ? 8 : (ntiles >= 12 ? 4 : 2); }
 
 template <int W>
 static void fwd2_go(const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H, const int* sid,
@@ -1081,8 +1037,7 @@ static void fwd2_go(const float* Qp, const float* Kp, const float* Vq, int N, in
 
 static void launch_fwd2(int var, const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H,
                         const int* sid, const int* sptr, float qs, float* O, float* L) {
-  const Occ& o = occ();
-  const int W = var > 0 ? var : pick_w(ceil_div(Nq, 16) * H, ceil_div(N, 16), o.fwd, o.cus);
+  const int W = var > 0 ? var : pick_w(ceil_div(N, 16));
   switch (W) {
     case 2: fwd2_go<2>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
     case 3: fwd2_go<3>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
@@ -1101,8 +1056,7 @@ static void bwd2_go(A8Bwd2 b) {
 }
 
 static void launch_bwd2(int var, const A8Bwd2& b) {
-  const Occ& o = occ();
-  const int W = var > 0 ? var : pick_w(2 * ceil_div(b.Nq, 16) * b.H, ceil_div(b.N, 16), o.bwd, o.cus);
+  const int W = var > 0 ? var : pick_w(ceil_div(b.N, 16));
   switch (W) {
     case 2: bwd2_go<2>(b); break;
     case 3: bwd2_go<3>(b); break;
@@ -1115,10 +1069,9 @@ static void launch_bwd2(int var, const A8Bwd2& b) {
 
 // chosen W of the v2 kernels for a shape (tools / tests)
 std::vector<int64_t> attn8_v2_shape(int64_t N, int64_t H) {
-  const Occ& o = occ();
-  const int Nq = (int)((N + 15) / 16 * 16);
-  return {pick_w(ceil_div(Nq, 16) * (int)H, ceil_div(N, 16), o.fwd, o.cus),
-          pick_w(2 * ceil_div(Nq, 16) * (int)H, ceil_div(N, 16), o.bwd, o.cus), o.cus, o.fwd[6], o.bwd[6]};
+  (void)H;
+  const int W = pick_w(ceil_div(N, 16));
+  return {W, W};
 }
 
 static void chk_seg(const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N) {

@@ -6,25 +6,20 @@
 // 64x64 gradient becomes 1-4 workgroups walking 20k+ rows (rocprof on MI355X:
 // 30-105 us per call with 1-4 WGs busy on a 256-CU chip).  Here the reduction
 // dimension is split instead:
-//   pass 1: workgroup (tile, slab) owns a 64x64 output tile and a slab of >=128
-//           rows.  The slab streams through LDS in 32-row chunks, double
-//           buffered: all 256 threads issue the float4 loads of chunk c+1 before
-//           computing chunk c, so one HBM/L2 latency covers 32 rows (the first
-//           version, one row pair in flight per wave, was latency-bound at
-//           ~17 us per call).  Each lane owns an 8x8 register block of the
-//           output (2 ds_read_b128 of dY + 2 of X feed 64 FMAs, 8 distinct
-//           addresses per wave instruction -> broadcast, no bank conflicts);
-//           waves take interleaved rows of the chunk, their accumulators are
-//           folded in a fixed order through a padded LDS image, and the
-//           partial tile (+ bias column sums) is written coalesced;
+//   pass 1: workgroup (tile, slab) owns a 64x64 output tile and a slab of rows.  The
+//           slab streams through LDS in 32-row chunks, double buffered: all 256
+//           threads issue the float4 loads of chunk c+1 before computing chunk c, so
+//           one HBM/L2 latency covers 32 rows.  The products run on the fp32 matrix
+//           cores (exact fp32, v_mfma_f32_16x16x4_f32), each wave a 32x32 quarter of
+//           the tile, and each wave writes its partial tile (+ bias column sums);
 //   pass 2: the S slab partials are summed in a fixed order, 4 waves per
 //           64-output group (deterministic: no float atomics).
-// fp32 in / fp32 accumulate: FMA-bound at the VALU rate, which on gfx950 equals
-// the f32-MFMA rate, so the register-blocked VALU form loses nothing to MFMA.
+// Narrow problems (I <= 16) keep a VALU form (a 16-wide MFMA tile would be mostly padding).
 #include "common.h"
 
 namespace hy {
 
+typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int kWT = 64;  // output tile edge
 
 constexpr int kWC = 32;  // rows per LDS chunk
@@ -60,108 +55,226 @@ __device__ __forceinline__ void wg_load(const float* __restrict__ base, int ld, 
   }
 }
 
+// Same chunk staging through buffer loads whose descriptor covers exactly the slab's rows:
+// rows past the slab end read as zeros (hardware range check), columns past ncol read the
+// next row's values (or zeros past the buffer), which only feed output columns that are
+// never stored.  No select on loaded values: a select right after the load makes the
+// compiler wait for it there, serialising the next-chunk prefetch with this chunk's MFMAs.
+typedef __amdgpu_buffer_rsrc_t WgRsrc;
+__device__ __forceinline__ WgRsrc wg_rsrc(const float* base, int ld, int r0, int r1) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)r0 * ld), (short)0, max(r1 - r0, 0) * ld * 4,
+                                           0x00020000);
+}
+template <bool VEC>
+__device__ __forceinline__ void wg_load_b(WgRsrc rs, int ld, int col0, int rrel, int t, float4 (&r)[2]) {
+  const int c = col0 + (t & 15) * 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = rrel + (t >> 4) + 16 * h;
+    const int vo = (row * ld + c) * 4;
+    if constexpr (VEC) {
+      r[h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
+    } else {
+      r[h].x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0));
+      r[h].y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 4, 0, 0));
+      r[h].z = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 8, 0, 0));
+      r[h].w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo + 12, 0, 0));
+    }
+  }
+}
+
 // part layout: [S][O*I + O]   (dW partial, then db partial)
-// smem: 2 buffers x (dY, X) x 32 rows x 64 floats = 32 KB; reused for the wave fold afterwards
+// smem: 2 buffers x (dY, X) x 32 rows x kLdsW floats (row-major chunks, 80 KB... see below)
+//
+// MFMA form (v_mfma_f32_16x16x4_f32, exact fp32): wave w owns the 32 x 32 output quarter
+// (o half w >> 1, i half w & 1) of the workgroup's 64 x 64 tile as 2 x 2 accumulator tiles;
+// per 4-row k-step a lane reads one dY value per o block and one X value per i block
+// (row 4s + g of the chunk, column i) and issues 4 independent MFMAs.  The staged rows use a
+// stride of 80 floats (== 16 mod 32 banks): the two row groups a ds_read_b32 lane group
+// touches land on disjoint bank halves.  Each wave writes its own partial outputs straight
+// from the accumulators (no cross-wave fold); the bias column sums ride along as two VALU
+// adds per k-step on the waves that hold i block 0.  (The VALU 8x8-register-block form
+// before this ran at ~20 % of the fp32 peak on the grouped OC20 step: 87 us.)
+constexpr int kLdsW = 80;
+
 template <bool VY, bool VX>
 __device__ __forceinline__ void wgrad_partial_body(float4* smem, const float* __restrict__ dY, int ldy,
                                                    const float* __restrict__ X, int ldx, float* __restrict__ part,
                                                    int with_bias, int M, int O, int I, int rows_per_block,
                                                    int tiles_i, int tile, int s) {
-  float4* Ys = smem;                  // [2][kWC][16]
-  float4* Xs = smem + 2 * kWC * 16;   // [2][kWC][16]
+  float* Ys = reinterpret_cast<float*>(smem);  // [2][kWC][kLdsW]
+  float* Xs = Ys + 2 * kWC * kLdsW;            // [2][kWC][kLdsW]
   const int to0 = (tile / tiles_i) * kWT, ti0 = (tile % tiles_i) * kWT;
   const int r0 = s * rows_per_block, r1 = min(M, r0 + rows_per_block);
   const int t = threadIdx.x;
-  const int lane = t & 63, w = t >> 6;
-  const int obq = (lane >> 3) * 2, ibq = (lane & 7) * 2;  // float4 column index of this lane's 8-block
-  const bool bias_lane = with_bias && ti0 == 0 && (lane & 7) == 0;
-  float acc[8][8];
+  const int lane = t & 63, w = t >> 6, i = lane & 15, g = lane >> 4;
+  const int ob = (w >> 1) * 32, ib = (w & 1) * 32;  // this wave's quarter of the tile
+  const bool bias_w = with_bias && ti0 == 0 && (w & 1) == 0;
+  f4v acc[2][2];
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = 0.f;
-  float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < 2; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+  float bacc0 = 0.f, bacc1 = 0.f;
   const int nch = (r1 - r0 + kWC - 1) / kWC;
   float4 ry[2], rx[2];
-  if (nch > 0) {
-    wg_load<VY>(dY, ldy, to0, O, r0, r1, t, ry);
-    wg_load<VX>(X, ldx, ti0, I, r0, r1, t, rx);
+  auto stage = [&](int b) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      Ys[((t >> 4) + 16 * h) * 16 + (t & 15)] = ry[h];
-      Xs[((t >> 4) + 16 * h) * 16 + (t & 15)] = rx[h];
+      const int row = (t >> 4) + 16 * h, c4 = (t & 15) * 4;
+      *reinterpret_cast<float4*>(Ys + (b * kWC + row) * kLdsW + c4) = ry[h];
+      *reinterpret_cast<float4*>(Xs + (b * kWC + row) * kLdsW + c4) = rx[h];
     }
+  };
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
+  if (nch > 0) {
+    wg_load_b<VY>(rsy, ldy, to0, 0, t, ry);
+    wg_load_b<VX>(rsx, ldx, ti0, 0, t, rx);
+    stage(0);
   }
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int b = c & 1;
     const bool more = c + 1 < nch;
-    if (more) {  // issue the next chunk's global loads before computing this one
-      wg_load<VY>(dY, ldy, to0, O, r0 + (c + 1) * kWC, r1, t, ry);
-      wg_load<VX>(X, ldx, ti0, I, r0 + (c + 1) * kWC, r1, t, rx);
+    if (more) {  // issue the next chunk's loads before computing this one
+      wg_load_b<VY>(rsy, ldy, to0, (c + 1) * kWC, t, ry);
+      wg_load_b<VX>(rsx, ldx, ti0, (c + 1) * kWC, t, rx);
     }
-    const float4* yb = Ys + b * kWC * 16;
-    const float4* xb = Xs + b * kWC * 16;
-#pragma unroll 2
-    for (int rr = w; rr < kWC; rr += 4) {
-      const float4 y0 = yb[rr * 16 + obq], y1 = yb[rr * 16 + obq + 1];
-      const float4 x0 = xb[rr * 16 + ibq], x1 = xb[rr * 16 + ibq + 1];
-      const float ya[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-      const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const float* yb = Ys + b * kWC * kLdsW + ob + i;
+    const float* xb = Xs + b * kWC * kLdsW + ib + i;
 #pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[a][q] = fmaf(ya[a], xa[q], acc[a][q]);
-      if (bias_lane) {
-#pragma unroll
-        for (int a = 0; a < 8; ++a) bacc[a] += ya[a];
+    for (int ks = 0; ks < kWC / 4; ++ks) {
+      const int row = 4 * ks + g;
+      const float a0 = yb[row * kLdsW], a1 = yb[row * kLdsW + 16];
+      const float b0 = xb[row * kLdsW], b1 = xb[row * kLdsW + 16];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      if (bias_w) {
+        bacc0 += a0;
+        bacc1 += a1;
       }
     }
-    if (more) {
-      float4* yn = Ys + (b ^ 1) * kWC * 16;
-      float4* xn = Xs + (b ^ 1) * kWC * 16;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        yn[((t >> 4) + 16 * h) * 16 + (t & 15)] = ry[h];
-        xn[((t >> 4) + 16 * h) * 16 + (t & 15)] = rx[h];
-      }
-    }
+    if (more) stage(b ^ 1);
     __syncthreads();
   }
-  // fold the 4 wave accumulators in a fixed order through LDS ([lane][65] padding)
-  float* red = reinterpret_cast<float*>(smem);
-  for (int step = 0; step < 4; ++step) {
-    if (w == step) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float v = acc[a][q] + (step > 0 ? red[lane * 65 + a * 8 + q] : 0.f);
-          red[lane * 65 + a * 8 + q] = v;
-        }
-    }
-    __syncthreads();
-  }
-  // coalesced write of the 64x64 partial tile
+  // D layout: lane (i, g) holds rows 4g + r (o) of column i (i) of each 16 x 16 tile
   float* P = part + (int64_t)s * ((int64_t)O * I + O);
-  for (int idx = t; idx < kWT * kWT; idx += 256) {
-    const int oo = idx >> 6, ii = idx & 63;
-    const int o = to0 + oo, i = ti0 + ii;
-    if (o < O && i < I) P[(int64_t)o * I + i] = red[((oo >> 3) * 8 + (ii >> 3)) * 65 + (oo & 7) * 8 + (ii & 7)];
-  }
-  if (with_bias && ti0 == 0) {
-    __syncthreads();
-    if (bias_lane) {
 #pragma unroll
-      for (int a = 0; a < 8; ++a) red[(w * 8 + (lane >> 3)) * 8 + a] = bacc[a];
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = to0 + ob + 16 * x + 4 * g + r, ii = ti0 + ib + 16 * y + i;
+        if (o < O && ii < I) P[(int64_t)o * I + ii] = acc[x][y][r];
+      }
+  if (bias_w) {  // rows 4s + g of the chunk went to lane group g: fold the 4 groups
+    bacc0 += __shfl_xor(bacc0, 16, 64);
+    bacc0 += __shfl_xor(bacc0, 32, 64);
+    bacc1 += __shfl_xor(bacc1, 16, 64);
+    bacc1 += __shfl_xor(bacc1, 32, 64);
+    if (g == 0) {
+      const int o0 = to0 + ob + i, o1 = o0 + 16;
+      if (o0 < O) P[(int64_t)O * I + o0] = bacc0;
+      if (o1 < O) P[(int64_t)O * I + o1] = bacc1;
     }
-    __syncthreads();
-    if (t < 64) {
-      const int kb = t >> 3, a = t & 7;  // o = kb*8 + a
-      const float v = red[(0 * 8 + kb) * 8 + a] + red[(1 * 8 + kb) * 8 + a] + red[(2 * 8 + kb) * 8 + a] +
-                      red[(3 * 8 + kb) * 8 + a];
-      const int o = to0 + t;
-      if (o < O) P[(int64_t)O * I + o] = v;
+  }
+}
+
+// LDS-DMA form of the same product (both operands 16-byte vectorisable): chunks are copied
+// global -> LDS by buffer_load_dwordx4 ... lds (no staging registers, no ds_write pass)
+// into a 3-stage ring, two chunks in flight while one is computed: the register-staged form
+// above keeps only the next chunk in flight, ~0.5 us of MFMA work against ~1.5 us of load
+// latency per chunk.  One wave instruction fills a 4-row x 64-column group (1 KB, lane-
+// linear); groups are kGS = 264 floats apart, and k-step s of lane group g reads row
+// s % 4 of group 2g + s / 4, so the two row groups of a ds_read_b32 lane group sit 528
+// floats (16 banks) apart: conflict-free.  Rows past the slab read zeros (descriptor range);
+// the next chunks' copies stay in flight across the barrier (counted vmcnt + raw s_barrier).
+constexpr int kGS = 264, kGrp = kWC / 4, kStageF = 2 * kGrp * kGS, kNS = 3;
+
+__device__ __forceinline__ void wgrad_glds_body(float* lds, const float* __restrict__ dY, int ldy,
+                                                const float* __restrict__ X, int ldx, float* __restrict__ part,
+                                                int with_bias, int M, int O, int I, int rows_per_block, int tiles_i,
+                                                int tile, int s) {
+  const int to0 = (tile / tiles_i) * kWT, ti0 = (tile % tiles_i) * kWT;
+  const int r0 = s * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6, i = lane & 15, g = lane >> 4;
+  const int ob = (w >> 1) * 32, ib = (w & 1) * 32;
+  const bool bias_w = with_bias && ti0 == 0 && (w & 1) == 0;
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
+  // this lane's source element in group w * 2 + j of a chunk: row 4 grp + lane / 16, 4 columns
+  const int lr = lane >> 4, lc = (lane & 15) * 4;
+  auto issue = [&](int c, int st) {
+    float* sb = lds + st * kStageF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int grp = w * 2 + j, row = 4 * grp + lr;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsy, (__attribute__((address_space(3))) void*)(sb + grp * kGS), 16, (row * ldy + to0 + lc) * 4,
+          c * kWC * ldy * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsx, (__attribute__((address_space(3))) void*)(sb + (kGrp + grp) * kGS), 16, (row * ldx + ti0 + lc) * 4,
+          c * kWC * ldx * 4, 0, 0);
+    }
+  };
+  f4v acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+  float bacc0 = 0.f, bacc1 = 0.f;
+  const int nch = (r1 - r0 + kWC - 1) / kWC;
+  if (nch > 0) issue(0, 0);
+  if (nch > 1) issue(1, 1);
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // chunk c landed (c + 1 may be in flight)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's copies of chunk c landed; chunk c - 1 consumed
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 2 < nch) issue(c + 2, (c + 2) % kNS);
+    const float* yb = lds + (c % kNS) * kStageF + ob + i;
+    const float* xb = lds + (c % kNS) * kStageF + kGrp * kGS + ib + i;
+#pragma unroll
+    for (int ks = 0; ks < kWC / 4; ++ks) {
+      const int off = (2 * g + (ks >> 2)) * kGS + (ks & 3) * 64;
+      const float a0 = yb[off], a1 = yb[off + 16];
+      const float b0 = xb[off], b1 = xb[off + 16];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      if (bias_w) {
+        bacc0 += a0;
+        bacc1 += a1;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* P = part + (int64_t)s * ((int64_t)O * I + O);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = to0 + ob + 16 * x + 4 * g + r, ii = ti0 + ib + 16 * y + i;
+        if (o < O && ii < I) P[(int64_t)o * I + ii] = acc[x][y][r];
+      }
+  if (bias_w) {
+    bacc0 += __shfl_xor(bacc0, 16, 64);
+    bacc0 += __shfl_xor(bacc0, 32, 64);
+    bacc1 += __shfl_xor(bacc1, 16, 64);
+    bacc1 += __shfl_xor(bacc1, 32, 64);
+    if (g == 0) {
+      const int o0 = to0 + ob + i, o1 = o0 + 16;
+      if (o0 < O) P[(int64_t)O * I + o0] = bacc0;
+      if (o1 < O) P[(int64_t)O * I + o1] = bacc1;
     }
   }
 }
@@ -171,7 +284,7 @@ __global__ void __launch_bounds__(256) wgrad_partial_kernel(const float* __restr
                                                             const float* __restrict__ X, int ldx,
                                                             float* __restrict__ part, int with_bias, int M, int O,
                                                             int I, int rows_per_block, int tiles_i) {
-  __shared__ float4 smem[2 * 2 * kWC * 16];
+  __shared__ float4 smem[2 * 2 * kWC * kLdsW / 4];
   wgrad_partial_body<VY, VX>(smem, dY, ldy, X, ldx, part, with_bias, M, O, I, rows_per_block, tiles_i, blockIdx.x,
                              blockIdx.y);
 }
@@ -315,21 +428,23 @@ __device__ __forceinline__ void wgrad_narrow_body(float4* smem, const float* __r
   float acc[kWgNarrow], bacc = 0.f;
 #pragma unroll
   for (int k = 0; k < kWgNarrow; ++k) acc[k] = 0.f;
+  // buffer loads over exactly the slab's rows: rows past it read as zeros; X columns past I
+  // (and dY columns past O) only feed outputs that are never stored (no selects on loads)
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
   for (int c0 = r0; c0 < r1; c0 += 64) {
-    const int nrow = min(64, r1 - c0);
     __syncthreads();
-    for (int idx = threadIdx.x; idx < 64 * kWgNarrow; idx += 256) {
-      const int c = idx / kWgNarrow, k = idx % kWgNarrow;
-      xs[c * ST + k] = (c < nrow && k < I) ? X[(int64_t)(c0 + min(c, nrow - 1)) * ldx + min(k, I - 1)] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 64 * kWgNarrow / 256; ++q) {
+      const int idx = threadIdx.x + 256 * q, c = idx / kWgNarrow, k = idx % kWgNarrow;
+      xs[c * ST + k] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rsx, ((c0 - r0 + c) * ldx + min(k, I - 1)) * 4, 0, 0));
     }
     // this wave's 16 rows of the chunk: all dY loads in flight before the FMAs
     float y[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int c = w * 16 + u;
-      const float v = dY[(int64_t)(c0 + min(c, nrow - 1)) * ldy + oc];
-      y[u] = c < nrow ? v : 0.f;
-    }
+    for (int u = 0; u < 16; ++u)
+      y[u] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rsy, ((c0 - r0 + w * 16 + u) * ldy + oc) * 4, 0, 0));
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -358,8 +473,16 @@ __device__ __forceinline__ void wgrad_narrow_body(float4* smem, const float* __r
   }
 }
 
-__global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
-  __shared__ float4 smem[2 * 2 * kWC * 16];
+// One launch for every vectorisable problem: wide ones (I > 16) on the LDS-DMA MFMA body,
+// narrow ones on the VALU body.  The LDS ring (3 workgroups per CU) bounds the occupancy
+// either way, so the narrow body's registers cost nothing, and narrow workgroups fill the
+// wide ones' tail.  Problems with an operand that is not 16-byte vectorisable go to a
+// second launch on the register-staged MFMA body (its scalar-load variants would otherwise
+// set this kernel's register count).
+template <bool FALLBACK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+wgrad_grouped_partial_kernel(WgArgs) {
+  __shared__ float4 smem[(FALLBACK ? 2 * 2 * kWC * kLdsW : kNS * kStageF) / 4];
   KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int b = blockIdx.x;
   const int pi = wg_find(A, b, false);
@@ -369,24 +492,27 @@ __global__ void __launch_bounds__(256) wgrad_grouped_partial_kernel(WgArgs) {
   const int tile = local % tiles, s = local / tiles;
   float* part = A->ws + P.part_off;
   const int wb = P.db != nullptr ? 1 : 0;
-  if (P.vec & 4) {
-    wgrad_narrow_body(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, tile, s);
-    return;
-  }
-  switch (P.vec) {
-    case 3: wgrad_partial_body<true, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
-    case 1: wgrad_partial_body<true, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
-    case 2: wgrad_partial_body<false, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
-    default: wgrad_partial_body<false, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+  if constexpr (!FALLBACK) {
+    if (P.vec & 4)
+      wgrad_narrow_body(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, tile, s);
+    else
+      wgrad_glds_body(reinterpret_cast<float*>(smem), P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb,
+                      P.tiles_i, tile, s);
+  } else {
+    switch (P.vec & 3) {
+      case 1: wgrad_partial_body<true, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+      case 2: wgrad_partial_body<false, true>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+      default: wgrad_partial_body<false, false>(smem, P.dy, P.ldy, P.x, P.ldx, part, wb, P.M, P.O, P.I, P.rpb, P.tiles_i, tile, s); break;
+    }
   }
 }
 
-// reduce: 64 outputs per workgroup; the 4 waves split the problem's slabs (wave w takes
-// slabs w, w+4, ...) with 8 independent accumulators each, so a wave keeps 8 coalesced
-// 256-byte loads in flight (the pass is latency-bound otherwise); the per-wave sums are
-// folded in a fixed order through LDS -> deterministic.
+// reduce: one output per thread, 256 consecutive outputs per workgroup (coalesced 1 KB
+// per slab row); each thread walks all S slabs of its output with 8 independent
+// accumulators in flight and folds them in a fixed order -> deterministic.  (The first
+// form, 64 outputs per workgroup with the slabs split over 4 waves and folded through LDS,
+// launched ~5,900 tiny workgroups for the OC20 step and took 33 us.)
 __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
-  __shared__ float red[4][64];
   KWgArgs* A = (KWgArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int b = blockIdx.x;
   const int pi = wg_find(A, b, true);
@@ -395,25 +521,21 @@ __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
   const int64_t nw = (int64_t)P.O * P.I;
   const int64_t n = nw + (P.db != nullptr ? P.O : 0);
   const int64_t ld = nw + P.O;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t j = (int64_t)(b - P.rwg0) * 64 + lane;
-  const int64_t jc = j < n ? j : n - 1;  // loads stay in range; result discarded
+  const int64_t j = (int64_t)(b - P.rwg0) * 256 + threadIdx.x;
+  if (j >= n) return;
   const int S = P.S;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int s0 = w; s0 < S; s0 += 32) {
+  int s0 = 0;
+  for (; s0 + 8 <= S; s0 += 8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int s = s0 + 4 * u;
-      if (s < S) acc[u] += part[(int64_t)s * ld + jc];
-    }
+    for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(s0 + u) * ld + j];
   }
-  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  __syncthreads();
-  if (w == 0 && j < n) {
-    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-    float* dst = j < nw ? P.dw + j : P.db + (j - nw);
-    *dst = P.accumulate ? *dst + v : v;
-  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (s0 + u < S) acc[u] += part[(int64_t)(s0 + u) * ld + j];
+  const float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  float* dst = j < nw ? P.dw + j : P.db + (j - nw);
+  *dst = P.accumulate ? *dst + v : v;
 }
 
 void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList dWs, at::TensorList dbs,
@@ -424,21 +546,22 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
            "linear_wgrad_grouped: list lengths differ");
   for (int64_t c0 = 0; c0 < n; c0 += kWgMaxP) {
     const int cnt = (int)std::min<int64_t>(kWgMaxP, n - c0);
-    WgArgs a{};
+    WgArgs a{};  // every problem: the reduce launch
     a.n = cnt;
     std::vector<at::Tensor> keep;
     int64_t part_total = 0;
-    int wg = 0, rwg = 0;
-    // rows per slab: 256 when the merged grid still has >= 1024 workgroups, else halve
-    // (down to one 32-row LDS chunk) until it does
-    int rps = 256;
+    int wg = 0, wg_fb = 0, rwg = 0;
+    // rows per slab: the largest power of two (<= 1024) that still gives the merged grid
+    // >= 768 workgroups (3 per CU: the MFMA body is latency-, not issue-bound, so a CU
+    // wants a few resident workgroups), down to one 32-row LDS chunk
+    int rps = 1024;
     for (; rps > kWC; rps /= 2) {
       int64_t tot = 0;
       for (int q = 0; q < cnt; ++q) {
         const auto& dY = dYs[c0 + q];
         tot += (int64_t)ceil_div(dY.size(1), kWT) * ceil_div(Xs[c0 + q].size(1), kWT) * ceil_div(dY.size(0), rps);
       }
-      if (tot >= 1024) break;
+      if (tot >= 768) break;
     }
     for (int q = 0; q < cnt; ++q) {
       const int64_t k = c0 + q;
@@ -470,28 +593,42 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.O = O;
       P.I = I;
       const bool narrow = I <= kWgNarrow;
+      auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+      const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
+      const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);
       P.tiles_i = narrow ? 1 : ceil_div(I, kWT);
       const int tiles = ceil_div(O, kWT) * P.tiles_i;
-      // at most kWgMaxSlabs slabs per problem: the reduce pass reads S partial tiles
-      const int rpb = std::max(rps, ceil_div(ceil_div(M, kWgMaxSlabs), kWC) * kWC);
+      // at most kWgMaxSlabs slabs per problem: the reduce pass reads S partial tiles.  Narrow
+      // problems are latency-bound (one dY row per lane per load, partials of O x (I+1)
+      // floats): short 128-row slabs, up to 4x as many
+      const int rpb = narrow ? std::max(128, ceil_div(ceil_div(M, 4 * kWgMaxSlabs), 64) * 64)
+                             : std::max(rps, ceil_div(ceil_div(M, kWgMaxSlabs), kWC) * kWC);
       const int S = ceil_div(M, rpb);
       P.S = S;
       P.rpb = rpb;
       P.part_off = part_total;
       part_total += (int64_t)S * ((int64_t)O * I + O);
-      P.wg0 = wg;
-      wg += tiles * S;
+      const bool fb = !narrow && (!vy || !vx);
+      int& wgc = fb ? wg_fb : wg;
+      P.wg0 = wgc;
+      wgc += tiles * S;
       P.rwg0 = rwg;
-      rwg += ceil_div((int64_t)O * I + (hb ? O : 0), 64);
-      auto al16 = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
-      const bool vy = (dY.stride(0) & 3) == 0 && (O & 3) == 0 && al16(dY);
-      const bool vx = (X.stride(0) & 3) == 0 && (I & 3) == 0 && al16(X);
+      rwg += ceil_div((int64_t)O * I + (hb ? O : 0), 256);
       P.vec = (vy ? 1 : 0) | (vx ? 2 : 0) | (narrow ? 4 : 0);
       P.accumulate = accumulate[k] ? 1 : 0;
     }
     auto ws = at::empty({part_total}, dYs[c0].options());
     a.ws = ws.data_ptr<float>();
-    wgrad_grouped_partial_kernel<<<wg, 256, 0, stream()>>>(a);
+    // per-launch problem tables (wg_find scans p[0..n) for the owning problem)
+    WgArgs am{}, af{};
+    am.ws = af.ws = a.ws;
+    for (int q = 0; q < cnt; ++q) {
+      const WgProb& P = a.p[q];
+      WgArgs& t = (!(P.vec & 4) && (P.vec & 3) != 3) ? af : am;
+      t.p[t.n++] = P;
+    }
+    if (wg > 0) wgrad_grouped_partial_kernel<false><<<wg, 256, 0, stream()>>>(am);
+    if (wg_fb > 0) wgrad_grouped_partial_kernel<true><<<wg_fb, 256, 0, stream()>>>(af);
     wgrad_grouped_reduce_kernel<<<rwg, 256, 0, stream()>>>(a);
   }
 }

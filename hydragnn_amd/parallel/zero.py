@@ -14,7 +14,12 @@ MI355X design — flat, element-sharded, two collectives per step:
   parameter vector, i.e. the same as one all-reduce (vs. the reference's
   all-reduce + world_size broadcasts);
 * element-wise optimizers (SGD/Adam/AdamW/Adadelta/Adagrad/Adamax/RMSprop) are
-  exactly the unsharded update.  Optimizers with per-tensor statistics
+  exactly the unsharded update, with one documented difference for parameters that get
+  no gradient on any rank in a step: their slice of the shard (values and moment
+  state) is restored after the inner step, as torch skips them, but the shard's single
+  ``step`` counter still advances, so when such a parameter is used again its Adam
+  bias correction counts every step rather than its own updates (torch keeps a
+  per-parameter step).  Optimizers with per-tensor statistics
   (FusedLAMB's trust ratio) use per-parameter ownership instead (greedy by size)
   with the same all-gather of owner slices.
 
@@ -79,26 +84,35 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
     def _pack_grads(self):
         """Copy every local gradient into ``flat_grad``; slices of parameters without a
         gradient this step are ZEROED (never left over from an earlier step).  Returns the
-        per-parameter "has a gradient" flags (float, one per parameter)."""
-        used = torch.zeros(len(self.all_params), device=self.flat.device, dtype=self.flat.dtype)
-        for i, p in enumerate(self.all_params):
+        per-parameter "has a gradient" flags as a host list (whether ``p.grad`` is None is
+        known on the host: no device round trip, so the step stays capturable)."""
+        used = []
+        for p in self.all_params:
             o = self.offset[p]
             view = self.flat_grad[o:o + p.numel()]
             if p.grad is None:
                 view.zero_()
+                used.append(0.0)
                 continue
-            used[i] = 1.0
+            used.append(1.0)
             if p.grad.data_ptr() != view.data_ptr():
                 view.copy_(p.grad.reshape(-1))
         return used
 
     def _unused(self, used):
         """Parameters with no gradient on ANY rank (the reference's per-parameter ZeRO and
-        torch optimizers skip them: no weight decay, no moment update)."""
+        torch optimizers skip them: no weight decay, no moment update).  Only the eager
+        ``reduce_grads`` path needs the other ranks' flags (one small all-reduce + a host
+        read; that path is never captured).  Without it every rank already holds averaged
+        gradients (DDP wrapper / the captured step's bucketed all-reduce, which attaches a
+        gradient to every parameter), so the local flags are the global ones."""
+        if all(f == 1.0 for f in used):
+            return []
         if self.world > 1 and self.reduce_grads:
-            dist.all_reduce(used, group=self.group)
-        flags = used.tolist()
-        return [p for p, f in zip(self.all_params, flags) if f == 0.0]
+            t = torch.tensor(used, device=self.flat.device, dtype=self.flat.dtype)
+            dist.all_reduce(t, group=self.group)
+            used = t.tolist()
+        return [p for p, f in zip(self.all_params, used) if f == 0.0]
 
     def _frozen_slices(self, unused):
         """(lo, hi) ranges of this rank's shard that belong to globally unused parameters."""

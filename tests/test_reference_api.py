@@ -52,6 +52,31 @@ def test_optimizers(workdir, opt, use_zero):
     _sweep(workdir, "ci", Optimizer={"type": opt, "use_zero_redundancy": use_zero, "learning_rate": 0.01})
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["AdamW", "Adam"])
+def test_zero_on_captured_step_gpu(workdir, opt):
+    """ZeRO-1 inside the hipGraph-captured training step (run_training's default GPU path):
+    the optimizer's per-step bookkeeping must not read the device (a host sync during
+    stream capture fails), and the captured replays must train."""
+    from hydragnn_amd.parallel.zero import ZeroRedundancyOptimizer
+    from hydragnn_amd.train.step import TrainStep
+
+    seen = {}
+    orig = TrainStep.__init__
+
+    def spy(self, model, *a, **k):
+        orig(self, model, *a, **k)
+        seen["mode"] = self.mode
+        seen["zero"] = isinstance(self.opt, ZeroRedundancyOptimizer)
+
+    TrainStep.__init__ = spy
+    try:
+        _sweep(workdir, "ci", Optimizer={"type": opt, "use_zero_redundancy": True, "learning_rate": 0.01})
+    finally:
+        TrainStep.__init__ = orig
+    assert seen == {"mode": "graph", "zero": True}
+
+
 @pytest.mark.parametrize("loss", ["mse", "mae", "rmse", "GaussianNLLLoss"])
 def test_loss_functions(workdir, loss):
     _sweep(workdir, "ci_multihead" if loss == "GaussianNLLLoss" else "ci", loss_function_type=loss)
