@@ -67,6 +67,9 @@ def _spawn(args):
 
 def main():
     faulthandler.enable()  # a native crash prints the Python stack of every thread
+    # host phase timers of the captured step (perf_counter only, no device sync): reported
+    # as config.host_phases_ms (plan, slot_wait = host ahead of the GPU, replay)
+    os.environ.setdefault("HYDRA_STEP_TIMING", "1")
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_spawn(args))
@@ -150,6 +153,8 @@ def main():
         store.plan(idx, lay_, np.empty(lay_.total, dtype=np.int32))
     plan_ms = 1000.0 * (time.perf_counter() - hp) / 20
     host = 0.0  # host time spent issuing steps (index plan + upload + replay launch)
+    if step.host_times is not None:
+        step.host_times.clear()  # phases of the timed steps only
     t0 = time.perf_counter()
     for _ in range(args.steps):
         h0 = time.perf_counter()

@@ -212,12 +212,14 @@ __device__ __forceinline__ void wgrad_glds_body(float* lds, const float* __restr
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int grp = w * 2 + j, row = 4 * grp + lr;
+      // the chunk offset goes into the VGPR offset, not soffset: the descriptor's range check
+      // (rows past the slab read zeros) covers the VGPR + instruction offset only
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsy, (__attribute__((address_space(3))) void*)(sb + grp * kGS), 16, (row * ldy + to0 + lc) * 4,
-          c * kWC * ldy * 4, 0, 0);
+          rsy, (__attribute__((address_space(3))) void*)(sb + grp * kGS), 16, ((c * kWC + row) * ldy + to0 + lc) * 4,
+          0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsx, (__attribute__((address_space(3))) void*)(sb + (kGrp + grp) * kGS), 16, (row * ldx + ti0 + lc) * 4,
-          c * kWC * ldx * 4, 0, 0);
+          rsx, (__attribute__((address_space(3))) void*)(sb + (kGrp + grp) * kGS), 16,
+          ((c * kWC + row) * ldx + ti0 + lc) * 4, 0, 0, 0);
     }
   };
   f4v acc[2][2];

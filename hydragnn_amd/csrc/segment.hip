@@ -225,7 +225,8 @@ at::Tensor seg_sum(const at::Tensor& x_, const at::Tensor& rowptr, const c10::op
   if (limit.has_value() && limit->defined()) {
     HY_CHECK(limit->is_cuda() && limit->scalar_type() == at::kInt && limit->numel() == 1,
              "seg_sum: limit must be a device int32 scalar");
-    HY_CHECK(!pp, "seg_sum: a row limit needs rows in segment order (no perm)");
+    // with a perm the limit bounds positions in the permuted order (the caller's padding
+    // rows must sit at the tail of that order, e.g. the static radius graph's source view)
     lim = limit->data_ptr<int>();
   }
   const bool v4 = (F % 4 == 0);
@@ -294,7 +295,8 @@ void seg_sum_out(const at::Tensor& x_, const at::Tensor& rowptr, const c10::opti
 
 // out[n] = sum over the rowptr segment n (rows through perm) of w[row] * x[gidx[row]]
 at::Tensor gather_mul_sum(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& gidx,
-                          const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm, int64_t N) {
+                          const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm, int64_t N,
+                          const c10::optional<at::Tensor>& limit) {
   HY_CHECK_CUDA(x_);
   auto x = as2d(x_).contiguous(), w = as2d(w_).contiguous();
   HY_CHECK_F32(x);
@@ -311,6 +313,12 @@ at::Tensor gather_mul_sum(const at::Tensor& x_, const at::Tensor& w_, const at::
     HY_CHECK_I32(*perm);
     pp = perm->data_ptr<int>();
   }
+  const int* lim = nullptr;
+  if (limit.has_value() && limit->defined()) {
+    HY_CHECK(limit->is_cuda() && limit->scalar_type() == at::kInt && limit->numel() == 1,
+             "gather_mul_sum: limit must be a device int32 scalar");
+    lim = limit->data_ptr<int>();  // CSR positions at or past it are padding: skipped
+  }
   const bool v4 = (F % 4 == 0);
   auto g = row_geom(N, v4 ? F : F * 4);
   const int ks = g.tpr <= 16 ? 4 : (g.tpr <= 32 ? 2 : 1);
@@ -319,7 +327,7 @@ at::Tensor gather_mul_sum(const at::Tensor& x_, const at::Tensor& w_, const at::
 #define HY_GMS(VEC, KS)                                                                                  \
   seg_sum_kernel<VEC, false, KS, true><<<blocks, 256, 0, stream()>>>(                                    \
       x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, out.data_ptr<float>(), (int)N, F, g.tpr, rpb,     \
-      w.data_ptr<float>(), gidx.data_ptr<int>())
+      w.data_ptr<float>(), gidx.data_ptr<int>(), 0, lim)
   if (v4) {
     if (ks == 4) HY_GMS(4, 4); else if (ks == 2) HY_GMS(4, 2); else HY_GMS(4, 1);
   } else {
@@ -433,7 +441,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
   m.def("scatter_arg(Tensor g, Tensor arg, int E) -> Tensor");
   m.def("gather_arg(Tensor x, Tensor arg) -> Tensor");
-  m.def("gather_mul_sum(Tensor x, Tensor w, Tensor gidx, Tensor rowptr, Tensor? perm, int N) -> Tensor");
+  m.def("gather_mul_sum(Tensor x, Tensor w, Tensor gidx, Tensor rowptr, Tensor? perm, int N, Tensor? limit=None) -> Tensor");
   m.def("gather_mul2(Tensor x, Tensor ia, Tensor y, Tensor ib) -> Tensor");
   m.def("seg_sum_out(Tensor x, Tensor rowptr, Tensor? perm, Tensor(a!) out) -> ()");
 }

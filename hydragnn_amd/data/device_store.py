@@ -28,6 +28,8 @@ extra attention segment), padded edges are spread over the padded nodes
 and the device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked
 reductions.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -101,6 +103,8 @@ class DeviceGraphStore:
             self.dataset_name_dev = torch.from_numpy(self.dataset_name).to(self.device)
         self._ring = []
         self._ring_pos = 0
+        self.slot_wait_s = 0.0  # host seconds spent waiting for a pinned plan slot (the GPU is behind)
+        self.phase_s = {}  # host seconds per upload phase (plan, copy call incl. event record)
 
     def __len__(self):
         return self.num_samples
@@ -125,8 +129,31 @@ class DeviceGraphStore:
             Np, Ep, Gp = N, E, G
         return Layout(Np, Ep, Gp, padded, self.attn_scope)
 
+    def _native_plan_args(self):
+        t = getattr(self, "_plan_t", None)
+        if t is None:
+            c = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))  # noqa: E731
+            t = self._plan_t = (c(self.n_nodes), c(self.n_edges), c(self.node_off), c(self.edge_off),
+                                c(self.src_local), c(self.dst_local), c(self.sperm_local))
+        return t
+
     def plan(self, indices, lay, out=None):
-        """Fill the packed int32 plan for ``indices`` (numpy view ``out`` of size lay.total)."""
+        """Fill the packed int32 plan for ``indices`` (numpy view ``out`` of size lay.total):
+        native C++ (``csrc/collate.cpp`` store_plan) when the library is loaded, else the
+        numpy reference ``plan_numpy`` (identical values; tests/test_store_plan.py)."""
+        from .. import _native
+
+        if out is None:
+            out = np.empty(lay.total, dtype=np.int32)
+        if _native.available():
+            idx = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int64))
+            _native.ops().store_plan(idx, *self._native_plan_args(), torch.from_numpy(out), lay.Np, lay.Ep, lay.Gp,
+                                     bool(lay.padded), lay.attn_scope == "batch")
+            return out
+        return self.plan_numpy(indices, lay, out)
+
+    def plan_numpy(self, indices, lay, out=None):
+        """numpy reference of ``plan`` (the oracle of the native builder)."""
         idx = np.asarray(indices, dtype=np.int64)
         G = idx.size
         n = self.n_nodes[idx]
@@ -196,7 +223,9 @@ class DeviceGraphStore:
             slot = self._ring[self._ring_pos % ring]
             self._ring_pos += 1
         if slot[1] is not None:
+            t0 = time.perf_counter()
             slot[1].synchronize()  # the async copy that last read this pinned buffer is done
+            self.slot_wait_s += time.perf_counter() - t0
         if slot[0] is None or slot[0].numel() < n:
             slot[0] = torch.empty(max(n, 1 << 16), dtype=torch.int32, pin_memory=cuda)
         slot[1] = torch.cuda.Event() if cuda else None
@@ -206,7 +235,9 @@ class DeviceGraphStore:
         """plan() into a pinned buffer and copy it (async) to ``dev_buf`` (or a new device tensor)."""
         slot = self._slot(lay.total)
         host = slot[0][:lay.total]
+        t0 = time.perf_counter()
         self.plan(indices, lay, host.numpy())
+        t1 = time.perf_counter()
         if self.device.type == "cuda":
             if dev_buf is None:
                 dev_buf = host.to(self.device, non_blocking=True)
@@ -218,6 +249,9 @@ class DeviceGraphStore:
                 dev_buf = host.clone()
             else:
                 dev_buf[:lay.total].copy_(host)
+        ph = self.phase_s
+        ph["plan"] = ph.get("plan", 0.0) + (t1 - t0)
+        ph["copy"] = ph.get("copy", 0.0) + (time.perf_counter() - t1)
         return dev_buf
 
     # ------------------------------------------------------------------ device side

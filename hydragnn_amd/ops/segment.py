@@ -23,13 +23,17 @@ from .. import _native
 class SegIndex:
     """Row -> segment mapping with a CSR view (all index tensors int32)."""
 
-    __slots__ = ("index", "rowptr", "perm", "num_segments", "_deg", "_index64", "_onehot_t")
+    __slots__ = ("index", "rowptr", "perm", "num_segments", "limit", "_deg", "_index64", "_onehot_t")
 
-    def __init__(self, index, rowptr, perm, num_segments):
+    def __init__(self, index, rowptr, perm, num_segments, limit=None):
         self.index = index
         self.rowptr = rowptr
         self.perm = perm
         self.num_segments = int(num_segments)
+        # optional device int32 scalar: CSR positions at or past it are padding (their rows
+        # contribute zero / are never read): the native segment sums stop there, so a padded
+        # tail owned by one segment is not summed serially (static in-forward radius graph)
+        self.limit = limit
         self._deg = None
         self._index64 = None
         self._onehot_t = None
@@ -61,8 +65,9 @@ class SegIndex:
 
     def to(self, device):
         p = None if self.perm is None else self.perm.to(device, non_blocking=True)
+        lim = None if self.limit is None else self.limit.to(device, non_blocking=True)
         return SegIndex(self.index.to(device, non_blocking=True), self.rowptr.to(device, non_blocking=True), p,
-                        self.num_segments)
+                        self.num_segments, lim)
 
     @staticmethod
     def from_index(index, num_segments, sorted_=False):
@@ -140,7 +145,9 @@ class _SegSum(torch.autograd.Function):
         ctx.si = si
         if _use_native(x) and x.dtype == torch.float32:
             tail = x.shape[1:]
-            lim = limit if (limit is not None and si.perm is None and limit.dtype == torch.int32) else None
+            lim = limit if limit is not None else si.limit
+            if lim is not None and not (lim.dtype == torch.int32 and (si.perm is None or si.limit is lim)):
+                lim = None
             out = _native.ops().seg_sum(x.reshape(x.shape[0], _width(tail)), si.rowptr, si.perm, si.num_segments,
                                         False, lim)
             return out.view((si.num_segments,) + tuple(tail))
@@ -221,7 +228,7 @@ class _GatherMulSum(torch.autograd.Function):
         ctx.gsi, ctx.ssi = gsi, ssi
         ctx.save_for_backward(x, w)
         if _use_native(x) and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2:
-            return _native.ops().gather_mul_sum(x, w, gsi.index, ssi.rowptr, ssi.perm, ssi.num_segments)
+            return _native.ops().gather_mul_sum(x, w, gsi.index, ssi.rowptr, ssi.perm, ssi.num_segments, ssi.limit)
         return _cpu_segment_sum(x.index_select(0, gsi.index64.to(x.device)) * w, ssi)
 
     @staticmethod

@@ -28,7 +28,10 @@ def side_stream(device, slot=0):
     key = (torch.device(device).index, slot)
     s = _side.get(key)
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        # HYDRA_SIDE_PRIORITY: priority of the side-branch stream (torch convention: lower is
+        # higher priority; 0 = default).  The captured step records branch priorities only
+        # if the runtime keeps them per graph node (tools/gpu_r4_iter.sh A/B).
+        s = torch.cuda.Stream(device=device, priority=int(os.environ.get("HYDRA_SIDE_PRIORITY", "0")))
         _side[key] = s
     return s
 

@@ -166,13 +166,36 @@ def _broadcast_state(module):
 
 
 class _Captured:
+    """One captured bucket: two step graphs that differ only in the pinned host buffer their
+    first node (an H2D memcpy of the packed plan into ``dev_plan``) reads.  Steps alternate
+    between them, so the host writes the next step's plan into the buffer the PREVIOUS
+    graph read while the current one runs.  (A separate ``copy_`` call per step blocked the
+    host until the queued graph finished on ROCm — 0.41 ms per OC20 step — and left the GPU
+    idle while the next replay was being issued.)"""
+
     def __init__(self):
-        self.g_fwd_bwd = None
+        self.graphs = [None, None]
+        self.pinned = [None, None]
+        self.done = [None, None]  # event after the last replay that read pinned[j]
+        self.losses = [None, None]
+        self.taskss = [None, None]
+        self.next = 0
         self.g_opt = None
         self.dev_plan = None
-        self.loss = None
-        self.tasks = None
         self.lay = None
+
+    # the most recently replayed graph's outputs (and graph 0 for callers that want one)
+    @property
+    def g_fwd_bwd(self):
+        return self.graphs[0]
+
+    @property
+    def loss(self):
+        return self.losses[self.next ^ 1]
+
+    @property
+    def tasks(self):
+        return self.taskss[self.next ^ 1]
 
 
 class TrainStep:
@@ -425,7 +448,11 @@ class TrainStep:
         Np, Ep = key
         cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap.dev_plan = torch.empty(cap.lay.total, dtype=torch.int32, device=self.device)
-        store.upload(indices, cap.lay, cap.dev_plan)
+        cap.pinned = [torch.empty(cap.lay.total, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        store.plan(indices, cap.lay, cap.pinned[0].numpy())
+        cap.pinned[1].copy_(cap.pinned[0])
+        cap.dev_plan.copy_(cap.pinned[0])
+        torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -440,21 +467,34 @@ class TrainStep:
                 self._body_fwd_bwd(store, cap, sync=False)
                 self.opt.step()
         torch.cuda.current_stream().wait_stream(s)
-        pool = torch.cuda.graph_pool_handle()
-        cap.g_fwd_bwd = torch.cuda.CUDAGraph()
         split = self.world > 1 and not self._graph_collectives()
-        with torch.cuda.graph(cap.g_fwd_bwd, pool=pool):
-            cap.loss, cap.tasks = self._body_fwd_bwd(store, cap, sync=not split)
-            if not split:
-                self.opt.step()
-        if split:  # gloo rehearsal on one GPU: [fwd+bwd] -> eager all-reduce -> [optimizer]
-            cap.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(cap.g_opt, pool=pool):
-                self.opt.step()
+        for j in range(2):
+            pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+                cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)  # first node: H2D of the plan
+                cap.losses[j], cap.taskss[j] = self._body_fwd_bwd(store, cap, sync=not split)
+                if not split:
+                    self.opt.step()
+            cap.graphs[j] = g
+            cap.done[j] = torch.cuda.Event()
+            if split and j == 0:  # gloo rehearsal on one GPU: [fwd+bwd] -> eager all-reduce -> [optimizer]
+                cap.g_opt = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(cap.g_opt, pool=pool):
+                    self.opt.step()
         self.graphs[key] = cap
         torch.cuda.synchronize()
         self._restore(snap)
         return cap
+
+    def _capture_stream(self):
+        """Stream the step graphs are captured on (HYDRA_CAPTURE_PRIORITY: its priority, torch
+        convention, lower = higher; default 0 = a normal-priority private stream)."""
+        s = getattr(self, "_cap_stream", None)
+        if s is None:
+            s = self._cap_stream = torch.cuda.Stream(device=self.device,
+                                                     priority=int(os.environ.get("HYDRA_CAPTURE_PRIORITY", "0")))
+        return s
 
     def graph_step(self, store, indices):
         N, E = store.sizes_of(indices)
@@ -464,15 +504,23 @@ class TrainStep:
             cap = self._capture(store, indices, key)
             # the capture warm-up already trained on this batch; replay once more as the step
         tm = self.host_times
+        j = cap.next
+        cap.next ^= 1
         t0 = time.perf_counter() if tm is not None else 0.0
+        ev = cap.done[j]
+        ev.synchronize()  # the replay that last read pinned[j] (two steps back) is done
+        tw = time.perf_counter() if tm is not None else 0.0
         lay = store.layout(indices, Np=cap.lay.Np, Ep=cap.lay.Ep, Gp=cap.lay.Gp)
-        store.upload(indices, lay, cap.dev_plan)
+        assert lay.total == cap.lay.total
+        store.plan(indices, lay, cap.pinned[j].numpy())
         if tm is not None:
             t1 = time.perf_counter()
-        cap.g_fwd_bwd.replay()
+        cap.graphs[j].replay()
+        ev.record()
         if tm is not None:
             t2 = time.perf_counter()
-            tm["plan+upload"] = tm.get("plan+upload", 0.0) + (t1 - t0)
+            tm["plan"] = tm.get("plan", 0.0) + (t1 - tw)
+            tm["slot_wait"] = tm.get("slot_wait", 0.0) + (tw - t0)
             tm["replay"] = tm.get("replay", 0.0) + (t2 - t1)
             tm["n"] = tm.get("n", 0) + 1
         if cap.g_opt is not None:
@@ -481,7 +529,7 @@ class TrainStep:
             self.sync.flat.mul_(1.0 / self.world)
             dist.all_reduce(self.sync.flat)
             cap.g_opt.replay()
-        return cap.loss, cap.tasks
+        return cap.losses[j], cap.taskss[j]
 
     def _graph_collectives(self):
         """Collectives can live inside the captured graph only on RCCL ("nccl")."""

@@ -98,7 +98,7 @@ def test_schnet_static_inforward_graph_padded_equals_eager(equivariance):
         s.y_loc = torch.tensor([[0, 1]])
     m1 = create_model("SchNet", 1, 16, [1], 0, "", "", 0, ["graph"], heads, "relu", "mae", [1.0], 3,
                       num_gaussians=10, num_filters=16, radius=3.0, max_neighbours=4, dropout=0.0,
-                      equivariance=equivariance)
+                      equivariance=equivariance, use_gpu=False)
     m2 = copy.deepcopy(m1)
     assert m1.capturable
     store = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])

@@ -558,3 +558,46 @@ def test_edge_basis_native():
         out.backward(g.float().to(DEV))
         torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(dg.grad.double().cpu(), dr.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_gather_mul_sum_slack_limit():
+    """Static-capacity radius graph (ops/radius.interaction_graph_static): the slack slots
+    past the real edges all belong to the last (padding) receiver.  With the CSR limit the
+    native gather-multiply-sum skips them: rows before it match the reference exactly, and
+    the launch time does not grow with the slack (it summed the slack serially before)."""
+    import time
+
+    torch.manual_seed(5)
+    N, F, deg = 2048, 64, 8
+    E = N * deg
+    src = torch.randint(0, N - 1, (E,), dtype=torch.int32)
+    dst = torch.arange(N - 1, dtype=torch.int32).repeat_interleave(deg)[:E]
+    dst = torch.cat([dst, torch.full((E - dst.numel(),), N - 1, dtype=torch.int32)])
+    x = torch.randn(N, F, device=DEV)
+
+    def build(slack):
+        s_src = torch.cat([src, torch.full((slack,), N - 1, dtype=torch.int32)]).to(DEV)
+        s_dst = torch.cat([dst, torch.full((slack,), N - 1, dtype=torch.int32)]).to(DEV)
+        cnt = torch.bincount(dst.long(), minlength=N).to(torch.int32)
+        rp = torch.cat([cnt.new_zeros(1), torch.cumsum(cnt, 0, dtype=torch.int32)]).to(DEV)
+        lim = rp[N:N + 1].clone()
+        rp[N] = E + slack
+        w = torch.randn(E + slack, F, device=DEV)
+        w[E:] = 1.0
+        return seg.SegIndex(s_src, rp.clone(), None, N), seg.SegIndex(s_dst, rp, None, N, lim), w
+
+    gsi0, ssi0, w0 = build(0)
+    ref = seg.gather_mul_sum(x, w0, gsi0, ssi0)
+    times = {}
+    for slack in (0, 400_000):
+        gsi, ssi, w = build(slack)
+        w[:E] = w0[:E]
+        out = seg.gather_mul_sum(x, w, gsi, ssi)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(50):
+            seg.gather_mul_sum(x, w, gsi, ssi)
+        torch.cuda.synchronize()
+        times[slack] = (time.perf_counter() - t) / 50
+    assert times[400_000] < 2.0 * times[0] + 20e-6, times
