@@ -87,10 +87,18 @@ def _task_parallel(config, datasets, args):
     sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.5, patience=5, min_lr=1e-5)
     if dist.get_rank() == 0:
         save_config(config, log_name)
+    engine = None
+    if not args.nosync:
+        # GPU: HBM-resident branch shard + captured step with both gradient syncs in the graph
+        from hydragnn_amd.run_training import make_step_engine
+
+        engine, (tl, vl, tel) = make_step_engine(config, model, opt, (tl, vl, tel))
     ctx = model.no_sync() if args.nosync else contextlib.nullcontext()
     with ctx:
         train_validate_test(model, opt, tl, vl, tel, get_summary_writer(log_name), sched, config["NeuralNetwork"],
-                            log_name, config["Verbosity"]["level"])
+                            log_name, config["Verbosity"]["level"],
+                            compute_grad_energy=config["NeuralNetwork"]["Training"].get("compute_grad_energy", False),
+                            step_engine=engine)
     save_model(model, opt, log_name)  # -> <log_name>_branch<B>.pk, rank 0 of every branch group
     return {"branch": bid, "ranks": lists}
 

@@ -99,11 +99,31 @@ __device__ __forceinline__ float dropv(const DropCfg& d, uint32_t idx, float v) 
 
 // Column statistics of a 16x16 tile (this lane: rows row0 + 4g + r, column c) over
 // rows < nv, folded over the 4 lane groups and added to replica (blockIdx.x % NREP).
-// site: [NREP][NS][F] doubles; s = stat index (NS stats per site).
+// site: [NREP][NS][F] entries of 3 x 64-bit words; s = stat index (NS stats per site).
+//
+// Deterministic accumulation: a block's partial v is split into exact fixed-point words
+// (integer part, fraction bits 2^-1..2^-32, 2^-33..2^-64) and each word is added with an
+// INTEGER atomic.  Integer sums do not depend on the order the workgroups arrive in, so the
+// statistics are bitwise reproducible run to run; fp64 atomics were not.
+// Range |v| < 2^62, resolution 2^-64 (backward sums of small gradients keep full relative
+// precision down to ~1e-19).
+typedef unsigned long long u64;
+constexpr double kTwo32 = 4294967296.0;
+
+__device__ __forceinline__ void fx_add(u64* q, double v) {
+  const double fl = floor(v);
+  const double f = (v - fl) * kTwo32;  // [0, 2^32), exact
+  const double fh = floor(f);
+  atomicAdd(q, (u64)(long long)fl);
+  atomicAdd(q + 1, (u64)fh);
+  atomicAdd(q + 2, (u64)((f - fh) * kTwo32));
+}
+
 __device__ __forceinline__ void col_sum_add(double v, double* site, int NS, int s, int F, int c) {
   v += __shfl_xor(v, 16, 64);
   v += __shfl_xor(v, 32, 64);
-  if ((threadIdx.x & 63) < 16) unsafeAtomicAdd(site + ((blockIdx.x & (NREP - 1)) * NS + s) * F + c, v);
+  if ((threadIdx.x & 63) < 16)
+    fx_add(reinterpret_cast<u64*>(site) + 3 * (((blockIdx.x & (NREP - 1)) * NS + s) * F + c), v);
 }
 
 __device__ __forceinline__ void stats2(const f4v& v, int row0, int nv, double* site, int F, int c) {
@@ -122,10 +142,16 @@ __device__ __forceinline__ void stats2(const f4v& v, int row0, int nv, double* s
 }
 
 __device__ __forceinline__ double site_sum(const double* site, int NS, int s, int F, int c) {
-  double t = 0.0;
+  const u64* q = reinterpret_cast<const u64*>(site);
+  u64 I = 0, H = 0, L = 0;  // exact integer sums over the replicas (wrap-around = two's complement)
 #pragma unroll
-  for (int r = 0; r < NREP; ++r) t += site[(r * NS + s) * F + c];
-  return t;
+  for (int r = 0; r < NREP; ++r) {
+    const u64* e = q + 3 * ((r * NS + s) * F + c);
+    I += e[0];
+    H += e[1];
+    L += e[2];
+  }
+  return (double)(long long)I + (double)H * (1.0 / kTwo32) + (double)L * (1.0 / (kTwo32 * kTwo32));
 }
 
 // BN parameters of one site (affine weight/bias, running stats, batches counter)
@@ -1323,13 +1349,14 @@ static void chk(const at::Tensor& t, int64_t r, int64_t c, const char* n) {
            "gps_fused: ", n, " must be a contiguous fp32 GPU tensor [", r, ", ", c, "]");
 }
 
-// pair site / stats helpers: `acc` is one layer's fp64 accumulator block
-// [fwd1 | fwd2 | fwd3 | bwd pair | bwd12] = NREP x (2 + 2 + 2 + 2 + 3) x F doubles.
+// pair site / stats helpers: `acc` is one layer's accumulator block
+// [fwd1 | fwd2 | fwd3 | bwd pair | bwd12] = NREP x (2 + 2 + 2 + 2 + 3) x F statistics of
+// three 64-bit fixed-point words each (col_sum_add), held in a float64 tensor.
 constexpr int kSiteStride = NREP * 11;
 static double* site_ptr(const at::Tensor& acc, int which, int F) {
   // which: 0 fwd BN1, 1 fwd BN2, 2 fwd BN3, 3 bwd pair, 4 bwd BN1/BN2
   static const int off[5] = {0, 2, 4, 6, 8};
-  return acc.data_ptr<double>() + (int64_t)NREP * off[which] * F;
+  return acc.data_ptr<double>() + 3 * (int64_t)NREP * off[which] * F;  // 3 words per statistic
 }
 
 // ---- forward ops --------------------------------------------------------------------

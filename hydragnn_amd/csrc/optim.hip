@@ -16,12 +16,17 @@ struct TensorRef {
   float* m;
   float* v;
   int64_t n;
+  float* step;        // this parameter's step count (device scalar, torch's per-param "step")
+  const float* used;  // optional usage flag (> 0: the parameter took part in this step); a
+                      // parameter with flag 0 is skipped entirely (value, moments, step), as
+                      // torch optimizers skip grad-is-None parameters
 };
 
 constexpr int kChunk = 2048;
 
-// state: [0] = step (advanced by step_incr_kernel after the update), [1] = lr,
-// [2] = number of steps skipped by the non-finite guard.
+// state: [0] = unused, [1] = lr, [2] = number of steps skipped by the non-finite guard.
+// Per-parameter step counts live in the TensorRefs (advanced by step_incr_kernel after the
+// update, so every block of a tensor reads the same count).
 // guard (optional): the step's loss; a NaN/Inf loss skips the whole update on the device
 // (no host sync, capture-safe) and is counted in state[2] (SURVEY §5.3 step guard).
 __device__ __forceinline__ bool guard_bad(const float* guard) { return guard && !isfinite(*guard); }
@@ -33,7 +38,8 @@ __global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict_
   if (guard_bad(guard)) return;
   const int2 bt = blocks[blockIdx.x];
   const TensorRef r = refs[bt.x];
-  const float step = state[0] + 1.f;  // this step's count (state[0] is updated by a follow-up kernel)
+  if (r.used && !(*r.used > 0.f)) return;
+  const float step = *r.step + 1.f;  // this step's count (advanced by a follow-up kernel)
   const float lr = state[1];
   const float bc1 = 1.f - powf(beta1, step);
   const float bc2 = 1.f - powf(beta2, step);
@@ -56,12 +62,17 @@ __global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict_
   }
 }
 
-__global__ void step_incr_kernel(float* state, const float* guard, int has_skip) {
+__global__ void __launch_bounds__(256) step_incr_kernel(const TensorRef* __restrict__ refs, int nt, float* state,
+                                                        const float* guard, int has_skip) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
   if (guard_bad(guard)) {
-    if (has_skip) state[2] += 1.f;
+    if (t == 0 && has_skip) state[2] += 1.f;
     return;
   }
-  state[0] += 1.f;
+  if (t >= nt) return;
+  const TensorRef r = refs[t];
+  if (r.used && !(*r.used > 0.f)) return;
+  *r.step += 1.f;
 }
 
 void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tensor& state, double beta1,
@@ -73,7 +84,7 @@ void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tens
     gp = guard->data_ptr<float>();
   }
   HY_CHECK_CUDA(refs);
-  HY_CHECK(refs.scalar_type() == at::kByte, "refs must be a uint8 blob");
+  HY_CHECK(refs.scalar_type() == at::kByte && refs.numel() % sizeof(TensorRef) == 0, "refs must be a TensorRef blob");
   HY_CHECK_I32(blocks);
   HY_CHECK_F32(state);
   const int nblocks = (int)(blocks.numel() / 2);
@@ -82,7 +93,9 @@ void adamw_step(const at::Tensor& refs, const at::Tensor& blocks, const at::Tens
                                               reinterpret_cast<const int2*>(blocks.data_ptr<int>()),
                                               state.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
                                               (float)wd, adamw ? 1 : 0, (float)grad_scale, gp);
-  step_incr_kernel<<<1, 1, 0, stream()>>>(state.data_ptr<float>(), gp, state.numel() > 2 ? 1 : 0);
+  const int nt = (int)(refs.numel() / (int64_t)sizeof(TensorRef));
+  step_incr_kernel<<<ceil_div(nt, 256), 256, 0, stream()>>>(reinterpret_cast<const TensorRef*>(refs.data_ptr<uint8_t>()),
+                                                            nt, state.data_ptr<float>(), gp, state.numel() > 2 ? 1 : 0);
 }
 
 }  // namespace hy

@@ -339,6 +339,32 @@ class Base(nn.Module):
         return sorted((k for k in self.graph_shared.keys()), key=lambda k: int(k.split("-")[1])) \
             if len(self.graph_shared) else [f"branch-{i}" for i in range(self.num_branches)]
 
+    def branch_param_groups(self):
+        """Per-branch decoder parameters (graph shared MLP + every head's branch module), in
+        branch id order: the usage groups of the captured multi-branch step (a branch absent
+        from a batch leaves its group's parameters untouched, as torch skips grad-is-None)."""
+        if "graph_shared" not in self._modules:
+            return []
+        groups = []
+        for bt in self.branch_names():
+            ps = []
+            if bt in getattr(self, "graph_shared", {}):
+                ps += list(self.graph_shared[bt].parameters())
+            for headloc in self.heads_NN:
+                if bt in headloc:
+                    ps += list(headloc[bt].parameters())
+            groups.append([p for p in ps if p.requires_grad])
+        return groups
+
+    def _note_branch_presence(self, dn):
+        """Write this batch's per-branch presence (device, no host sync) into the persistent
+        buffer the captured step packs as usage flags (``BucketedGradSync.set_flags``)."""
+        buf = getattr(self, "_branch_presence", None)
+        if buf is None:
+            return
+        ids = torch.tensor([int(b.split("-")[1]) for b in self.branch_names()], device=dn.device, dtype=dn.dtype)
+        buf.copy_((dn.view(1, -1) == ids.view(-1, 1)).any(1).to(buf.dtype))
+
     def dense_decode_ok(self):
         """Capturable multi-branch decode: graph heads and shared-MLP node heads (a ``conv``
         node head's BatchNorm would see every branch's nodes)."""
@@ -351,6 +377,7 @@ class Base(nn.Module):
         padding rows (dataset id -1) get zeros."""
         data = ctx.data
         dn = data.dataset_name.view(-1)
+        self._note_branch_presence(dn)
         dn_node = dn.index_select(0, data.batch)
         outputs, outputs_var = [], []
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):

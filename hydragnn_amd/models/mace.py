@@ -501,6 +501,12 @@ def process_node_attributes(x, num_elements=NUM_ELEMENTS):
 class MACEStack(Base):
     is_edge_model = True
 
+
+    def branch_param_groups(self):
+        """No per-branch usage groups: the multi-branch read-outs are STACKED (one weight
+        tensor holds every branch, ``_decode_stacked``), so a parameter is always used."""
+        return []
+
     def __init__(self, input_args, conv_args, r_max, radial_type, distance_transform, num_bessel, edge_dim, max_ell,
                  node_max_ell, avg_num_neighbors, num_polynomial_cutoff, correlation, *args, **kwargs):
         self.max_ell = max_ell

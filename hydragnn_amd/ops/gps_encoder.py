@@ -243,7 +243,9 @@ class _GPSEncoder(torch.autograd.Function):
         ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
                                   cfg.cutoff, cfg.exponent, bool(freq.requires_grad), *geo)
         rbf, drdf, Rl, Gl = ro[0], ro[1], ro[2:2 + L], ro[2 + L:2 + 2 * L]
-        acc = torch.empty(L, NREP * SITES * F, device=dev, dtype=torch.float64)
+        # BN statistics sites: 3 fixed-point 64-bit words per statistic (deterministic integer
+        # atomics, csrc/gps_fused.hip col_sum_add); zeroed by the first node launch
+        acc = torch.empty(L, 3 * NREP * SITES * F, device=dev, dtype=torch.float64)
         saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
         st = []

@@ -28,6 +28,15 @@ class FusedAdamW(torch.optim.Optimizer):
         # the device (captured into the step graph, no host sync) and is counted
         self.guard = None
         self._skipped_cpu = 0
+        # optional per-parameter usage flags (device scalars, > 0 = used this step): set by
+        # the captured training step for parameters that a step may not reach (heads of
+        # branches absent from a batch), which then keep torch's skip-if-no-grad semantics
+        self._flags = {}
+
+    def set_usage_flags(self, flags):
+        """``{param: 1-element device tensor view}``; rebuilds the tables at the next step."""
+        self._flags = dict(flags)
+        self._tables = None
 
     def _init_state(self):
         for group in self.param_groups:
@@ -48,22 +57,25 @@ class FusedAdamW(torch.optim.Optimizer):
                 st = self.state[p]
                 n = p.numel()
                 assert p.is_contiguous() and p.grad.is_contiguous()
-                refs.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), n))
+                step = st["step"]
+                if not (torch.is_tensor(step) and step.is_cuda and step.dtype == torch.float32 and step.numel() == 1):
+                    step = st["step"] = torch.full((), float(step), dtype=torch.float32, device=p.device)
+                fl = self._flags.get(p)
+                refs.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), n,
+                             step.data_ptr(), 0 if fl is None else fl.data_ptr()))
                 for c in range((n + 2047) // 2048):
                     blocks.append((ti, c))
             if not ps:
                 tables.append(None)
                 continue
-            # TensorRef {float* p; const float* g; float* m; float* v; int64 n;} = 40 bytes
-            blob = b"".join(struct.pack("<QQQQq", *r) for r in refs)
-            assert len(blob) == 40 * len(refs) and struct.unpack_from("<QQQQq", blob, 40 * (len(refs) - 1)) == refs[-1]
+            # TensorRef {float* p; const float* g; float* m; float* v; int64 n; float* step;
+            #            const float* used;} = 56 bytes
+            blob = b"".join(struct.pack("<QQQQqQQ", *r) for r in refs)
+            assert len(blob) == 56 * len(refs) and struct.unpack_from("<QQQQqQQ", blob, 56 * (len(refs) - 1)) == refs[-1]
             dev = ps[0].device
             rb = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
             bt = torch.tensor(blocks, dtype=torch.int32).view(-1).to(dev)
-            step0 = float(self.state[ps[0]]["step"])
-            state = torch.tensor([step0, group["lr"], 0.0], dtype=torch.float32, device=dev)
-            for p in ps:
-                self.state[p]["step"] = state[0]  # shared view: checkpoints see the live count
+            state = torch.tensor([0.0, group["lr"], 0.0], dtype=torch.float32, device=dev)
             tables.append([rb, bt, state, group["lr"], tuple(p.grad.data_ptr() for p in ps), ps])
         self._tables = tables
 
@@ -77,6 +89,9 @@ class FusedAdamW(torch.optim.Optimizer):
                     return False
                 continue
             if tuple(p.grad.data_ptr() for p in ps) != t[4]:
+                return False
+            # a checkpoint load / state replacement swaps the per-parameter step tensors
+            if any(not torch.is_tensor(self.state[p].get("step")) or not self.state[p]["step"].is_cuda for p in ps):
                 return False
         return True
 
@@ -127,6 +142,9 @@ class FusedAdamW(torch.optim.Optimizer):
             lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
             for p in group["params"]:
                 if p.grad is None:
+                    continue
+                fl = self._flags.get(p)
+                if fl is not None and not float(fl.reshape(-1)[0]) > 0.0:
                     continue
                 st = self.state[p]
                 st["step"] += 1

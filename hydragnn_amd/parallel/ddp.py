@@ -193,12 +193,14 @@ class BucketedGradSync:
     compute stream while RCCL moves the bucket over xGMI; ``finish`` joins the comm
     stream back before the optimizer reads the buffer.
 
-    Difference from the reference, by design: after ``finish`` EVERY parameter holds a
-    gradient (zeros where the step produced none), because a captured graph cannot vary
-    the optimizer's parameter set per step.  Fused AdamW therefore applies weight decay and
-    moment decay to parameters unused in a step (e.g. heads of branches absent from a
-    batch), where torch optimizers and the reference skip ``grad is None``.  The eager
-    path (and ZeRO, ``zero.py``) keep the reference semantics.
+    After ``finish`` EVERY parameter holds a gradient (zeros where the step produced none),
+    because a captured graph cannot vary the optimizer's parameter set per step.  Parameters
+    a step may not reach (heads of branches absent from a batch) get torch's skip-if-no-grad
+    semantics back through USAGE FLAGS: ``nflags`` extra slots after the guard slot carry a
+    per-group "used this step" value that the model writes on the device (``set_flags``); it
+    rides in the last bucket, so after the all-reduce a flag is > 0 iff some rank used the
+    group (the reference's DDP ``find_unused_parameters`` + torch AdamW skip), and fused AdamW
+    skips flagged-off parameters entirely (``FusedAdamW.set_usage_flags``).
 
     Captured inside ``torch.cuda.graph`` the event fork/join becomes graph edges, so
     the replayed step is ONE graph launch whose collective nodes run concurrently
@@ -206,7 +208,7 @@ class BucketedGradSync:
     async collectives and waits for them in ``finish``.
     """
 
-    def __init__(self, params, process_group=None, bucket_cap_mb=None, min_buckets=2):
+    def __init__(self, params, process_group=None, bucket_cap_mb=None, min_buckets=2, nflags=0):
         self.params = [p for p in params if p.requires_grad]
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -216,9 +218,12 @@ class BucketedGradSync:
         # one extra trailing element: the step guard slot.  It rides in the last bucket, so
         # after the all-reduce it holds sum_r loss_r / world — finite iff EVERY rank's loss is
         # finite, the same value on every rank (ranks skip or apply the update together)
-        self.flat = torch.zeros(total + 1, device=dev, dtype=order[0].dtype)
+        self.nflags = int(nflags)
+        self.flat = torch.zeros(total + 1 + self.nflags, device=dev, dtype=order[0].dtype)
         self.total = total
         self.guard = self.flat[total:total + 1]
+        self.flags = self.flat[total + 1:total + 1 + self.nflags]  # usage flags (after the reduce)
+        self._flag_src = None
         self._loss = None
         nbytes = total * self.flat.element_size()
         if bucket_cap_mb is None:
@@ -242,7 +247,7 @@ class BucketedGradSync:
         if cur:
             self.buckets.append((start, off, cur))
         s_, e_, ps_ = self.buckets[-1]
-        self.buckets[-1] = (s_, e_ + 1, ps_)  # + the guard slot
+        self.buckets[-1] = (s_, e_ + 1 + self.nflags, ps_)  # + the guard slot (+ usage flags)
         self.bucket_of = {}
         for bi, (_, _, ps) in enumerate(self.buckets):
             for p in ps:
@@ -276,6 +281,10 @@ class BucketedGradSync:
         """The step's loss: packed into the guard slot with the last bucket."""
         self._loss = loss
 
+    def set_flags(self, src):
+        """Device tensor [nflags] of this step's per-group usage (packed with the last bucket)."""
+        self._flag_src = src
+
     def begin(self):
         # HYDRA_GRADSYNC_FORCE=1 exercises the collective path on a 1-rank group (tests)
         self.active = self.world > 1 or (dist.is_initialized() and os.environ.get("HYDRA_GRADSYNC_FORCE") == "1")
@@ -307,10 +316,14 @@ class BucketedGradSync:
         s, e, ps = self.buckets[bi]
         gs = [p.grad.reshape(-1) if p.grad is not None else
               torch.zeros(p.numel(), device=self.flat.device, dtype=self.flat.dtype) for p in ps]
-        if e == self.total + 1:
+        if e == self.total + 1 + self.nflags:
             loss = self._loss
             gs.append(loss.detach().reshape(1).to(self.flat.dtype) if loss is not None else
                       torch.zeros(1, device=self.flat.device, dtype=self.flat.dtype))
+            if self.nflags:
+                f = self._flag_src
+                gs.append(f.detach().reshape(-1).to(self.flat.dtype) if f is not None else
+                          torch.ones(self.nflags, device=self.flat.device, dtype=self.flat.dtype))
         out = self.flat[s:e]
         if len(gs) == 1:
             out.copy_(gs[0])
@@ -330,6 +343,13 @@ class BucketedGradSync:
         self.comm.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.comm):
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+
+    def eager_reduce(self):
+        """Average the packed flat buffer over the group with one blocking all-reduce (the
+        split gloo rehearsal of the captured step: collectives outside the graph)."""
+        if self.world > 1:
+            self.flat.mul_(1.0 / self.world)
+            dist.all_reduce(self.flat, group=self.group)
 
     def finish(self):
         """Flush buckets never completed (parameters without a gradient), join the comm
@@ -411,3 +431,55 @@ def convert_sync_batchnorm(model, group=None):
             bn = m.module
             m.forward = SyncBatchNorm(bn, group).forward
     return model
+
+
+class MultiGradSync:
+    """Several :class:`BucketedGradSync` over disjoint parameter subsets, each on its own
+    process group and comm stream, driven as one (the captured task-parallel step,
+    reference ``MultiTaskModelMP.py:172-276``: the shared encoder all-reduces over WORLD,
+    each branch decoder over its branch group).  Inside the step graph the two bucket
+    streams become two sets of collective nodes overlapping the rest of backward.
+
+    The first sync is the global one: it carries the step guard (loss) and the usage
+    flags, so every rank takes the same skip decision.  All syncs share ONE comm stream:
+    two communicators' kernels in flight at once can deadlock when one rank's GPU runs
+    them in the other order; on a shared stream every rank issues its branch group's
+    buckets, then the world's, in the same autograd order."""
+
+    def __init__(self, syncs):
+        self.syncs = list(syncs)
+        for s in self.syncs[1:]:
+            s.comm = self.syncs[0].comm
+        self.guard = self.syncs[0].guard
+        self.nflags = self.syncs[0].nflags
+        self.flags = self.syncs[0].flags
+
+    def set_loss(self, loss):
+        self.syncs[0].set_loss(loss)
+
+    def set_flags(self, src):
+        self.syncs[0].set_flags(src)
+
+    def begin(self):
+        for s in self.syncs:
+            s.begin()
+
+    def finish(self):
+        for s in self.syncs:
+            s.finish()
+
+    def release(self):
+        for s in self.syncs:
+            s.release()
+
+    def attach(self):
+        for s in self.syncs:
+            s.attach()
+
+    def zero(self):
+        for s in self.syncs:
+            s.zero()
+
+    def eager_reduce(self):
+        for s in self.syncs:
+            s.eager_reduce()

@@ -53,6 +53,26 @@ def _device_path_enabled(config):
     return flag == 2 or (torch.cuda.is_available() and flag == 1)
 
 
+def make_step_engine(config, model, optimizer, loaders):
+    """On a GPU: move the split loaders into HBM (``DeviceGraphStore``) and build the
+    captured ``TrainStep`` for ``model`` (plain, DDP-wrapped, or task-parallel
+    ``MultiTaskModelMP``: encoder synced over WORLD, the branch decoder over its branch
+    group, both inside the step graph).  Returns ``(engine | None, loaders)``."""
+    if not _device_path_enabled(config):
+        return None, loaders
+    nn_cfg = config["NeuralNetwork"]
+    module = model.module if hasattr(model, "module") else model
+    loaders = to_device_loaders(tuple(loaders), get_device(), module.head_type, module.head_dims,
+                                attn_scope=getattr(module, "attn_scope", "batch"))
+    mode = "graph" if (int(os.getenv("HYDRAGNN_CAPTURE", "1")) == 1 and getattr(module, "capturable", True)) \
+        else "eager"
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer,
+                       compute_grad_energy=nn_cfg["Training"].get("compute_grad_energy", False))
+    engine.prepare(loaders[0].store, loaders[0].batch_size)
+    return engine, tuple(loaders)
+
+
 @run_training.register
 def _(config: dict, use_deepspeed=False):
     assert not use_deepspeed, "DeepSpeed is not part of hydragnn_amd (ZeRO-1 via Optimizer.use_zero_redundancy)"
@@ -103,18 +123,8 @@ def train_model(config, train_loader, val_loader, test_loader, log_name=None):
         trainer_state = load_trainer_state(nn_cfg["Training"]["startfrom"]) or {}
         restore_trainer_state(trainer_state, scheduler)
     compute_grad_energy = nn_cfg["Training"].get("compute_grad_energy", False)
-    engine = None
-    if _device_path_enabled(config):
-        module = model.module if hasattr(model, "module") else model
-        train_loader, val_loader, test_loader = to_device_loaders(
-            (train_loader, val_loader, test_loader), get_device(), module.head_type, module.head_dims,
-            attn_scope=getattr(module, "attn_scope", "batch"))
-        mode = "graph" if (int(os.getenv("HYDRAGNN_CAPTURE", "1")) == 1
-                           and getattr(module, "capturable", True)) else "eager"
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        engine = TrainStep(model, mode=mode, world=world, optimizer=optimizer,
-                           compute_grad_energy=compute_grad_energy)
-        engine.prepare(train_loader.store, train_loader.batch_size)
+    engine, (train_loader, val_loader, test_loader) = make_step_engine(
+        config, model, optimizer, (train_loader, val_loader, test_loader))
     from .parallel.zero import ZeroRedundancyOptimizer
 
     if isinstance(optimizer, ZeroRedundancyOptimizer) and hasattr(model, "_sync_enabled") and \

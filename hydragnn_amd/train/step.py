@@ -28,7 +28,7 @@ import time
 import numpy as np
 import torch
 
-from ..parallel.ddp import BucketedGradSync, DistributedDataParallel
+from ..parallel.ddp import BucketedGradSync, DistributedDataParallel, MultiGradSync
 
 
 _LOSS_KIND = {"mse": 0, "mae": 1, "rmse": 2, "smooth_l1": 3}
@@ -148,13 +148,19 @@ class FlatGrads:
             p.grad = None
 
     def gather(self):
-        gs = []
+        gs, none = [], []
         for p in self.params:
             g = p.grad
+            if g is None:
+                none.append(p)
             gs.append(torch.zeros(p.numel(), device=self.flat.device, dtype=self.flat.dtype) if g is None
                       else g.reshape(-1))
         torch.cat(gs, out=self.flat)
         self.attach()
+        # parameters the step did not reach keep grad None (torch / reference semantics: the
+        # optimizer skips them — no weight or moment decay for absent branch heads)
+        for p in none:
+            p.grad = None
 
 
 def _broadcast_state(module):
@@ -204,16 +210,21 @@ class TrainStep:
         # compute_grad_energy: energy + force loss with forces = -dE/dpos (double backward,
         # reference Base.energy_force_loss); the whole step — including the create_graph
         # backward through the segment ops — is captured like any other step
+        from ..models.multitask import MultiTaskModelMP
+
         self.forces = compute_grad_energy
         self.model = model
-        self.module = model.module if isinstance(model, DistributedDataParallel) else model
+        # task parallel (SC25 "TP1"): encoder synced over WORLD, this rank's branch decoder
+        # over its branch group (two communicators, both in the captured step)
+        self.taskpar = model if isinstance(model, MultiTaskModelMP) else None
+        self.module = model.module if isinstance(model, (DistributedDataParallel, MultiTaskModelMP)) else model
         self.world = world
         self.mode = mode
         dev = next(self.module.parameters()).device
         self.device = dev
         if mode == "graph" and getattr(self.module, "num_branches", 1) > 1 and not self._capture_multibranch():
             self.mode = mode = "eager"
-        if world > 1 and mode == "eager" and not isinstance(model, DistributedDataParallel):
+        if world > 1 and mode == "eager" and not isinstance(model, DistributedDataParallel) and self.taskpar is None:
             self.model = DistributedDataParallel(model)
             self.module = self.model.module
         params = [p for p in self.module.parameters() if p.requires_grad]
@@ -230,13 +241,37 @@ class TrainStep:
             if isinstance(self.model, DistributedDataParallel):
                 self.model._sync_enabled = False  # the wrapper's own hooks stand down
                 self.model = self.module
+            elif self.taskpar is not None:
+                self.taskpar.encoder._sync_enabled = False
+                self.taskpar.decoder._sync_enabled = False
+                self.model = self.module
             elif world > 1:
                 _broadcast_state(self.module)
             # one bucket on a single rank unless asked otherwise (the 1-rank RCCL check,
             # tools/gradsync_check.py, uses several to exercise the in-graph bucket order)
             cap = bucket_cap_mb if (world > 1 or bucket_cap_mb is not None) else 1e9
-            self.sync = BucketedGradSync(params, bucket_cap_mb=cap)
-        elif not isinstance(self.model, DistributedDataParallel):
+            # task parallel: every rank holds only its own branch (present by construction)
+            groups = self._usage_groups(params) if self.taskpar is None else []
+            if self.taskpar is not None:
+                tp = self.taskpar
+                enc_ids = {id(p) for p in tp.encoder.module.parameters()}
+                enc = [p for p in params if id(p) in enc_ids]
+                dec = [p for p in params if id(p) not in enc_ids]
+                self.sync = MultiGradSync([BucketedGradSync(enc, process_group=tp.shared_pg, bucket_cap_mb=cap),
+                                           BucketedGradSync(dec, process_group=tp.head_pg, bucket_cap_mb=cap)])
+            else:
+                self.sync = BucketedGradSync(params, bucket_cap_mb=cap, nflags=len(groups))
+            if groups:
+                # branch heads absent from a batch keep torch's skip-if-no-grad semantics: the
+                # model writes per-branch presence on the device, the sync all-reduces it with
+                # the gradients, fused AdamW skips flagged-off parameters
+                m = self.module
+                m._branch_presence = torch.ones(len(groups), device=dev, dtype=torch.float32)
+                self.sync.set_flags(m._branch_presence)
+                if hasattr(optimizer, "set_usage_flags"):
+                    optimizer.set_usage_flags({p: self.sync.flags[k:k + 1] for k, ps in enumerate(groups)
+                                               for p in ps})
+        elif not isinstance(self.model, DistributedDataParallel) and self.taskpar is None:
             self.flat_grads = FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket
         self.max_graphs = max_graphs
@@ -245,6 +280,14 @@ class TrainStep:
         self.graphs = {}
         self.pool = None
         self.B = None
+
+    def _usage_groups(self, params):
+        """Per-branch parameter groups of a multi-branch model (captured dense decode)."""
+        m = self.module
+        if getattr(m, "num_branches", 1) <= 1 or not hasattr(m, "branch_param_groups"):
+            return []
+        ids = {id(p) for p in params}
+        return [[p for p in g if id(p) in ids] for g in m.branch_param_groups()]
 
     def _capture_multibranch(self):
         """Multi-branch models capture with a dense decode (every branch head on every row,
@@ -274,7 +317,7 @@ class TrainStep:
     def _zero(self):
         if self.sync is not None:
             self.sync.release()
-        elif isinstance(self.model, DistributedDataParallel):
+        elif isinstance(self.model, DistributedDataParallel) or self.taskpar is not None:
             self.model.zero_grad()
         else:
             self.flat_grads.release()
@@ -409,6 +452,11 @@ class TrainStep:
 
             g = g.reshape(1).clone()
             dist.all_reduce(g, group=self.model.process_group)
+        elif self.world > 1 and self.taskpar is not None:  # eager task parallel: world group
+            import torch.distributed as dist
+
+            g = g.reshape(1).clone()
+            dist.all_reduce(g, group=self.taskpar.shared_pg)
         if hasattr(self.opt, "guard"):
             self.opt.guard = g
         elif hasattr(getattr(self.opt, "optim", None), "guard"):  # ZeRO wrapper
@@ -423,10 +471,9 @@ class TrainStep:
         return out
 
     def _snapshot(self):
+        # optimizer state tensors include the per-parameter step counts (FusedAdamW)
         ts = list(self.module.parameters()) + list(self.module.buffers()) + self._opt_state_tensors()
-        tables = [t for t in (getattr(self.opt, "_tables", None) or []) if t is not None]
-        return {"pairs": [(t, t.detach().clone()) for t in ts], "ids": {id(t) for t in ts},
-                "steps": [float(t[2][0]) for t in tables]}
+        return {"pairs": [(t, t.detach().clone()) for t in ts], "ids": {id(t) for t in ts}}
 
     @torch.no_grad()
     def _restore(self, snap):
@@ -435,9 +482,6 @@ class TrainStep:
         for t in self._opt_state_tensors():  # created during warm-up -> fresh (zero) state
             if id(t) not in snap["ids"]:
                 t.zero_()
-        tables = [t for t in (getattr(self.opt, "_tables", None) or []) if t is not None]
-        for i, t in enumerate(tables):
-            t[2][0].fill_(snap["steps"][i] if i < len(snap["steps"]) else 0.0)
 
     def _capture(self, store, indices, key):
         """Warm up + capture one bucket.  Parameters, buffers and optimizer state are
@@ -453,7 +497,10 @@ class TrainStep:
         cap.pinned[1].copy_(cap.pinned[0])
         cap.dev_plan.copy_(cap.pinned[0])
         torch.cuda.synchronize()
-        s = torch.cuda.Stream()
+        # warm-up on the capture stream itself: the parameters' AccumulateGrad nodes are then
+        # created on the stream the captured backward runs on (a warm-up on a different stream
+        # left them there, and autograd warned of a stream mismatch on every later backward)
+        s = self._capture_stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             # warm-up (allocator, kernels, autograd buffers) on real data.  No collective
@@ -524,10 +571,7 @@ class TrainStep:
             tm["replay"] = tm.get("replay", 0.0) + (t2 - t1)
             tm["n"] = tm.get("n", 0) + 1
         if cap.g_opt is not None:
-            import torch.distributed as dist
-
-            self.sync.flat.mul_(1.0 / self.world)
-            dist.all_reduce(self.sync.flat)
+            self.sync.eager_reduce()
             cap.g_opt.replay()
         return cap.losses[j], cap.taskss[j]
 

@@ -14,6 +14,7 @@ import socket
 import sys
 import traceback
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -391,6 +392,50 @@ def _task_parallel_body(rank, world):
 
 
 
+def _task_parallel_captured_body(rank, world):
+    """TrainStep drives MultiTaskModelMP in graph mode (statically padded step, the CPU twin
+    of the captured one): encoder gradients all-reduced over WORLD, the branch decoder's over
+    its branch group, both through the step's bucketed sync — equal to the eager wrapper
+    (two DDP communicators) after several AdamW steps."""
+    import copy
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_multibranch_capture import _data, _model
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.models.multitask import MultiTaskModelMP, branch_groups
+    from hydragnn_amd.parallel.ddp import MultiGradSync
+    from hydragnn_amd.train.step import TrainStep
+
+    bid, group, lists = branch_groups([2, 2])
+    samples = _data(16)
+    for g in samples:
+        g.dataset_name = torch.tensor([[bid]])
+    base = _model("EGNN")
+    m_e = MultiTaskModelMP(copy.deepcopy(base), bid, group)
+    m_g = MultiTaskModelMP(base, bid, group)
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph", "node"], head_dims=[1, 1])
+    eager = TrainStep(m_e, lr=1e-2, mode="eager", world=world)
+    cap = TrainStep(m_g, lr=1e-2, mode="graph", world=world, node_bucket=64, edge_bucket=256,
+                    bucket_cap_mb=0.004)
+    assert cap.mode == "graph" and isinstance(cap.sync, MultiGradSync)
+    assert len(cap.sync.syncs[0].buckets) > 1
+    rng = np.random.default_rng(rank)
+    for _ in range(3):
+        idx = list(rng.choice(len(samples), 5, replace=False))
+        le, lc = float(eager(store, idx)[0]), float(cap(store, idx)[0])
+        assert abs(le - lc) <= 1e-4 * max(1.0, abs(le)), (le, lc)
+    for (n, pe), (_, pg) in zip(m_e.named_parameters(), m_g.named_parameters()):
+        torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-5, msg=n)
+    enc = torch.cat([p.detach().reshape(-1) for n, p in m_g.named_parameters()
+                     if not n.startswith(("graph_shared", "heads_NN"))])
+    allenc = [torch.empty_like(enc) for _ in range(world)]
+    dist.all_gather(allenc, enc)  # the encoder stays identical on every rank
+    for t in allenc[1:]:
+        torch.testing.assert_close(t, allenc[0])
+
+
 def _bnsync_body(rank, world):
     """Rank-local BN running statistics are made identical (rank 0's) once per epoch."""
     from hydragnn_amd.models.layers import BatchNorm
@@ -506,6 +551,10 @@ def test_captured_multibranch_four_ranks_matches_eager():
 
 def test_task_parallel_multibranch_four_ranks():
     run_ranks("_task_parallel_body", world=4)
+
+
+def test_task_parallel_captured_step_four_ranks():
+    run_ranks("_task_parallel_captured_body", world=4)
 
 
 @pytest.mark.slow

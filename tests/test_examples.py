@@ -12,8 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EX = os.path.join(ROOT, "examples")
 
 
-def _run(script, args, tmp_path, nproc=1, timeout=300):
-    env = dict(os.environ, HYDRAGNN_DEVICE_DATA="0", OMP_NUM_THREADS="2")
+def _run(script, args, tmp_path, nproc=1, timeout=300, device_data="0"):
+    env = dict(os.environ, HYDRAGNN_DEVICE_DATA=device_data, OMP_NUM_THREADS="2")
     if nproc == 1:
         cmd = [sys.executable, os.path.join(EX, script), "--workdir", str(tmp_path)] + args
         env["HYDRAGNN_MASTER_PORT"] = str(29000 + (abs(hash(script + str(args))) % 2000))
@@ -73,8 +73,12 @@ def test_multibranch_data_parallel(tmp_path):
     assert len(r["task_errors"]) == 2
 
 
-def test_multibranch_task_parallel_three_ranks(tmp_path):
-    _run("multibranch/train.py", ["--task_parallel", "--num_samples", "40", "--num_epoch", "1"], tmp_path, nproc=3)
+@pytest.mark.parametrize("device_data", ["0", "2"])
+def test_multibranch_task_parallel_three_ranks(tmp_path, device_data):
+    """device_data=2: the store + statically padded TrainStep path (the CPU twin of the
+    captured step) drives MultiTaskModelMP with its two bucketed gradient syncs."""
+    _run("multibranch/train.py", ["--task_parallel", "--num_samples", "40", "--num_epoch", "1"], tmp_path, nproc=3,
+         device_data=device_data)
     logs = os.listdir(os.path.join(tmp_path, "logs"))
     assert sum(1 for d in logs if "_branch" in d) == 3
 

@@ -14,11 +14,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_captured_rccl_gradsync_one_rank():
+@pytest.mark.parametrize("mode", ["ddp", "taskpar"])
+def test_captured_rccl_gradsync_one_rank(mode):
+    """``taskpar``: MultiTaskModelMP in the captured step (encoder + branch-group syncs)."""
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gradsync_check.py")], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=300)
+    extra = ["--taskpar"] if mode == "taskpar" else []
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gradsync_check.py")] + extra, cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
     print(r.stdout[-3000:])
     print(r.stderr[-3000:])
     assert r.returncode == 0 and "GRADSYNC_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -45,6 +45,8 @@ def main():
                             pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=8.0, max_neighbours=10,
                             dropout=0.0).to(dev)
 
+    if "--taskpar" in sys.argv:
+        sys.exit(taskpar(dev, samples, deg))
     store = DeviceGraphStore(samples, dev, head_types=["graph"], head_dims=[1])
     batches = [list(range(0, 8)), list(range(8, 16)), list(range(16, 24)), list(range(0, 8))]
     out = {}
@@ -69,6 +71,61 @@ def main():
     ok = same and out["synced"]["launched_at_capture"] >= 2 and out["plain"]["launched_at_capture"] == 0
     print("GRADSYNC_OK" if ok else "GRADSYNC_FAIL", flush=True)
     sys.exit(0 if ok else 1)
+
+
+def taskpar(dev, samples, deg):
+    """``--taskpar``: TrainStep drives MultiTaskModelMP (branch 0 of 2) in graph mode — two
+    bucketed syncs (encoder over WORLD, decoder over a 1-rank branch group created with
+    ``new_group``), their all-reduces recorded into the captured step on one comm stream —
+    and must equal the same pruned model stepped without any sync, bit for bit."""
+    import copy
+
+    import torch
+    import torch.distributed as dist
+
+    from hydragnn_amd.data.device_store import DeviceGraphStore
+    from hydragnn_amd.models.create import create_model
+    from hydragnn_amd.models.multitask import MultiTaskModelMP, prune_branches
+    from hydragnn_amd.train.step import TrainStep
+
+    for g in samples:
+        g.dataset_name = torch.tensor([[0]])
+    hd = {"graph": [{"type": f"branch-{b}", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 16,
+                                                              "num_headlayers": 1, "dim_headlayers": [16]}}
+                    for b in range(2)]}
+    torch.manual_seed(0)
+    base = create_model("PNAPlus", 4, 64, [1], 8, "GPS", "multihead", 8, ["graph"], hd, "relu", "mae", [1.0], 3,
+                        pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=8.0, max_neighbours=10,
+                        dropout=0.0).to(dev)
+    plain = copy.deepcopy(base)
+    prune_branches(plain, 0)
+    store = DeviceGraphStore(samples, dev, head_types=["graph"], head_dims=[1])
+    batches = [list(range(0, 8)), list(range(8, 16)), list(range(16, 24)), list(range(0, 8))]
+    group = dist.new_group([0])
+    out = {}
+    for tag, model, force in (("taskpar", MultiTaskModelMP(base, 0, group), "1"), ("plain", plain, "0")):
+        os.environ["HYDRA_GRADSYNC_FORCE"] = force
+        step = TrainStep(model, lr=1e-3, mode="graph", world=1, bucket_cap_mb=0.05)
+        assert step.mode == "graph"
+        syncs = getattr(step.sync, "syncs", [step.sync])
+        launched = []
+        for k, s in enumerate(syncs):
+            s._launch = lambda bi, o=s._launch, k=k: (launched.append((k, bi)), o(bi))[1]
+        step.prepare(store, 8)
+        losses = [float(step(store, b)[0]) for b in batches]
+        torch.cuda.synchronize()
+        out[tag] = dict(losses=losses, recorded=launched, captured=len(step.graphs),
+                        params=torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu())
+    same = torch.equal(out["taskpar"]["params"], out["plain"]["params"])
+    groups_recorded = sorted({k for k, _ in out["taskpar"]["recorded"]})
+    res = {"mode": "taskpar", "losses_taskpar": out["taskpar"]["losses"], "losses_plain": out["plain"]["losses"],
+           "allreduces_recorded": len(out["taskpar"]["recorded"]), "communicators": groups_recorded,
+           "graphs": out["taskpar"]["captured"], "params_bitwise_equal": same}
+    print(json.dumps(res), flush=True)
+    dist.destroy_process_group()
+    ok = same and groups_recorded == [0, 1] and out["taskpar"]["captured"] >= 1 and not out["plain"]["recorded"]
+    print("GRADSYNC_OK" if ok else "GRADSYNC_FAIL", flush=True)
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
