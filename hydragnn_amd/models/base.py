@@ -639,9 +639,15 @@ class Base(nn.Module):
         node_energy_pred = pred[0]
         graph_energy_pred = seg.segment_sum(node_energy_pred, data.graph_si).squeeze(-1).float()
         graph_energy_true = data.energy.reshape(graph_energy_pred.shape).float()
-        forces_pred = torch.autograd.grad(graph_energy_pred, data.pos, grad_outputs=torch.ones_like(graph_energy_pred),
-                                          retain_graph=graph_energy_pred.requires_grad and create_graph,
-                                          create_graph=create_graph)[0]
+        from ..ops.painn_force import input_grads_only
+
+        # forces need input gradients only: native twice-differentiable ops skip their weight
+        # gradients in this pass (the parameter gradients come from the loss backward)
+        with input_grads_only():
+            forces_pred = torch.autograd.grad(graph_energy_pred, data.pos,
+                                              grad_outputs=torch.ones_like(graph_energy_pred),
+                                              retain_graph=graph_energy_pred.requires_grad and create_graph,
+                                              create_graph=create_graph)[0]
         assert forces_pred is not None, "No gradients were found for data.pos."
         return graph_energy_pred, graph_energy_true, -forces_pred.float(), data.forces.float()
 

@@ -201,6 +201,18 @@ class PAINNStack(_EqStackBase):
         self.radius = radius
         super().__init__(input_args, conv_args, *args, **kwargs)
 
+    def _fused_encode(self, inv, equiv, ctx):
+        """Native twice-differentiable encoder (ops/painn_force.py): geometry, message and
+        per-layer node chains as closed op families with explicit first and second
+        derivatives (force training without the composite op-by-op graph)."""
+        from ..ops import painn_force
+
+        if not painn_force.model_ok(self, ctx):
+            return None
+        if ctx.get("gps_lazy"):
+            return None
+        return painn_force.painn_encode(self, inv, ctx)
+
     def get_conv(self, input_dim, output_dim, last_layer=False, edge_dim=None):
         hidden = output_dim if input_dim == 1 else input_dim
         assert hidden > 1, "PainnNet requires more than one hidden dimension between input_dim and output_dim."

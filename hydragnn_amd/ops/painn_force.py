@@ -1,0 +1,584 @@
+"""Native twice-differentiable PAINN (reference ``hydragnn/models/PAINNStack.py:194-319``)
+for force training (``Base.energy_force_loss``, ``Base.py:582-636``).
+
+A force step differentiates the energy twice: forces = -dE/dpos with ``create_graph``, then
+the loss gradient w.r.t. the parameters through that backward graph.  Op by op (the torch
+composite) a PAINN step is ~1,300 launches.  Here the model is three op families, each a
+closed set of native ops with explicit first AND second derivatives:
+
+* ``EdgeGeom``: pos -> per-edge basis [sinc(n pi d / c)/d * cut(d) | cut(d)] and d̂/d
+  (``PAINNStack.py:228-236``; the reference's d̂/d quirk kept).  Backward: one node-parallel
+  pass over both CSR views (incoming edges add, outgoing subtract); its backward: the
+  per-edge Jacobian-vector product plus the second-derivative term w.r.t. pos.
+* ``Msg``: the PAINN message + CSR-by-source segment sums, residual included
+  (``PAINNStack.py:194-263``): W_e = [W_f | b_f] basis_e, o = W_e * phi[dst], s += sum o_s,
+  v += sum v[dst] o_v + o_e d̂/d.  Backward: one dst-CSR pass; its backward (the VJP's VJP,
+  derived in ``_msg_vvjp``): one src-CSR pass + one dst-CSR pass.
+* node chains (``ops.rowprog``): update + adapters + activation/mask + the next layer's
+  scalar-message MLP as ONE row program per layer; first and second derivative programs
+  are generated from it (dual + reverse).
+
+In the force pass (``input_grads_only``) the first backward skips the weight-gradient
+work: forces need only input gradients, and the parameter gradients come from the second
+backward.  Weight-gradient outputs of the first-order backward ops are marked
+non-differentiable (a third derivative through them is not supported).
+
+CPU: every op runs its torch twin (the same formulas as the kernels, vectorised);
+``tests/test_painn_force.py`` checks them with fp64 ``gradcheck`` / ``gradgradcheck``.
+"""
+import contextlib
+import math
+
+import torch
+
+from . import rowprog as rp
+
+_state = {"inputs_only": False}
+
+
+@contextlib.contextmanager
+def input_grads_only(enabled=True):
+    """First backward of a force step: input gradients only (no weight gradients)."""
+    prev = _state["inputs_only"]
+    _state["inputs_only"] = enabled
+    try:
+        yield
+    finally:
+        _state["inputs_only"] = prev
+
+
+def _scatter(n, idx, val):
+    out = torch.zeros((n,) + tuple(val.shape[1:]), dtype=val.dtype, device=val.device)
+    return out.index_add_(0, idx, val)
+
+
+# ============================================================================ edge geometry
+def _radial(L, R, a, cutoff, eps):
+    """f [E, R+1], f' and f'' w.r.t. L; q, q', q'' of q(L) = 1 / ((L + eps) L)."""
+    inside = (L < cutoff).to(L.dtype)
+    k = torch.arange(1, R + 1, device=L.device, dtype=L.dtype) * a
+    Lc = L.unsqueeze(1)
+    sn, cs = torch.sin(k * Lc), torch.cos(k * Lc)
+    g = sn / Lc
+    g1 = k * cs / Lc - sn / Lc ** 2
+    g2 = -k * k * sn / Lc - 2 * k * cs / Lc ** 2 + 2 * sn / Lc ** 3
+    cut = 0.5 * (torch.cos(a * L) + 1) * inside
+    cut1 = -0.5 * a * torch.sin(a * L) * inside
+    cut2 = -0.5 * a * a * torch.cos(a * L) * inside
+    c0, c1, c2 = cut.unsqueeze(1), cut1.unsqueeze(1), cut2.unsqueeze(1)
+    f = torch.cat([g * c0, c0], 1)
+    f1 = torch.cat([g1 * c0 + g * c1, c1], 1)
+    f2 = torch.cat([g2 * c0 + 2 * g1 * c1 + g * c2, c2], 1)
+    D = L * L + eps * L
+    q = 1.0 / D
+    dD = 2 * L + eps
+    q1 = -dD / D ** 2
+    q2 = (-2 * D + 2 * dD * dD) / D ** 3
+    return f, f1, f2, q, q1, q2
+
+
+def _geom_vec(pos, dst, src, shifts):
+    vec = pos[dst] - pos[src]
+    if shifts is not None:
+        vec = vec + shifts
+    return vec
+
+
+class _GeomCfg:
+    __slots__ = ("R", "a", "cutoff", "eps", "dst", "src", "N", "dst_si", "src_si", "shifts")
+
+
+def _geom_fwd(cfg, pos):
+    vec = _geom_vec(pos, cfg.dst, cfg.src, cfg.shifts)
+    L = vec.norm(dim=1)
+    f, _, _, q, _, _ = _radial(L, cfg.R, cfg.a, cfg.cutoff, cfg.eps)
+    return f, vec * q.unsqueeze(1)
+
+
+def _geom_vjp(cfg, pos, gB, gU):
+    vec = _geom_vec(pos, cfg.dst, cfg.src, cfg.shifts)
+    L = vec.norm(dim=1)
+    f, f1, _, q, q1, _ = _radial(L, cfg.R, cfg.a, cfg.cutoff, cfg.eps)
+    A = (gB * f1).sum(1)
+    u = (gU * vec).sum(1)
+    gv = ((A + u * q1) / L).unsqueeze(1) * vec + gU * q.unsqueeze(1)
+    return _scatter(cfg.N, cfg.dst, gv) - _scatter(cfg.N, cfg.src, gv)
+
+
+def _geom_vvjp(cfg, pos, gB, gU, hpos, need_g, need_pos):
+    """Backward of _geom_vjp: (grad gB, grad gU, grad pos) for the upstream hpos."""
+    vec = _geom_vec(pos, cfg.dst, cfg.src, cfg.shifts)
+    L = vec.norm(dim=1)
+    f, f1, f2, q, q1, q2 = _radial(L, cfg.R, cfg.a, cfg.cutoff, cfg.eps)
+    hv = hpos[cfg.dst] - hpos[cfg.src]
+    t = (vec * hv).sum(1)
+    hB = hU = gp = None
+    if need_g:
+        hB = f1 * (t / L).unsqueeze(1)
+        hU = hv * q.unsqueeze(1) + vec * (q1 * t / L).unsqueeze(1)
+    if need_pos:
+        A = (gB * f1).sum(1)
+        A1 = (gB * f2).sum(1)
+        u = (gU * vec).sum(1)
+        w = (gU * hv).sum(1)
+        c_vec = (A1 + u * q2) * t / L ** 2 - (A + u * q1) * t / L ** 3 + q1 * w / L
+        gvec = c_vec.unsqueeze(1) * vec + (q1 * t / L).unsqueeze(1) * gU + ((A + u * q1) / L).unsqueeze(1) * hv
+        gp = _scatter(cfg.N, cfg.dst, gvec) - _scatter(cfg.N, cfg.src, gvec)
+    return hB, hU, gp
+
+
+def _native_ok(t):
+    return False  # device kernels: csrc/painn_force.hip (wired in once built)
+
+
+class _Geom(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pos, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(pos)
+        return _geom_fwd(cfg, pos)
+
+    @staticmethod
+    def backward(ctx, gB, gU):
+        (pos,) = ctx.saved_tensors
+        E = ctx.cfg.dst.numel()
+        if gB is None:
+            gB = torch.zeros(E, ctx.cfg.R + 1, dtype=pos.dtype, device=pos.device)
+        if gU is None:
+            gU = torch.zeros(E, 3, dtype=pos.dtype, device=pos.device)
+        return _GeomBwd.apply(gB, gU, pos, ctx.cfg), None
+
+
+class _GeomBwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gB, gU, pos, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(gB, gU, pos)
+        return _geom_vjp(cfg, pos, gB, gU)
+
+    @staticmethod
+    def backward(ctx, hpos):
+        gB, gU, pos = ctx.saved_tensors
+        hB, hU, gp = _geom_vvjp(ctx.cfg, pos, gB, gU, hpos, ctx.needs_input_grad[0] or ctx.needs_input_grad[1],
+                                ctx.needs_input_grad[2])
+        return hB, hU, gp, None
+
+
+def edge_geometry(pos, dst_si, src_si, num_radial, cutoff, shifts=None, eps=1e-9):
+    """(basis [E, R+1] = [sinc_n(d) * cut(d) | cut(d)], d̂ / d [E, 3]) for PAINN."""
+    cfg = _GeomCfg()
+    cfg.R, cfg.a, cfg.cutoff, cfg.eps = int(num_radial), math.pi / float(cutoff), float(cutoff), float(eps)
+    cfg.dst, cfg.src = dst_si.index64, src_si.index64
+    cfg.dst_si, cfg.src_si = dst_si, src_si
+    cfg.N = pos.shape[0]
+    cfg.shifts = shifts
+    return _Geom.apply(pos, cfg)
+
+
+# ============================================================================ message
+class _MsgCfg:
+    __slots__ = ("dst", "src", "N", "F", "R", "dst_si", "src_si")
+
+
+def _msg_w(Bas, W, b):
+    R = W.shape[1]
+    return Bas[:, :R] @ W.t() + Bas[:, R:R + 1] * b.view(1, -1)
+
+
+def _msg_fwd(cfg, s, v, phi, Bas, Un, W, b):
+    F = cfg.F
+    w = _msg_w(Bas, W, b)
+    o = w * phi[cfg.dst]
+    ov, oe, os_ = o[:, :F], o[:, F:2 * F], o[:, 2 * F:]
+    mv = v[cfg.dst] * ov.unsqueeze(1) + oe.unsqueeze(1) * Un.unsqueeze(2)
+    return s + _scatter(cfg.N, cfg.src, os_), v + _scatter(cfg.N, cfg.src, mv)
+
+
+def _msg_vjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, need_w):
+    """-> (g_v total, g_phi, g_Bas, g_Un, g_W, g_b); g_s = Gs (identity, returned by the caller)."""
+    F, R = cfg.F, cfg.R
+    dst, src = cfg.dst, cfg.src
+    w = _msg_w(Bas, W, b)
+    P = phi[dst]
+    o = w * P
+    Gs_e, Gv_e = Gs[src], Gv[src]
+    Vj = v[dst]
+    go = torch.cat([(Gv_e * Vj).sum(1), (Gv_e * Un.unsqueeze(2)).sum(1), Gs_e], 1)
+    g_phi = _scatter(cfg.N, dst, go * w)
+    g_v = Gv + _scatter(cfg.N, dst, Gv_e * o[:, :F].unsqueeze(1))
+    gw = go * P
+    g_Bas = torch.cat([gw @ W, (gw * b.view(1, -1)).sum(1, keepdim=True)], 1)
+    g_Un = (Gv_e * o[:, F:2 * F].unsqueeze(1)).sum(2)
+    g_W = g_b = None
+    if need_w:
+        g_W = gw.t() @ Bas[:, :R]
+        g_b = (gw * Bas[:, R:R + 1]).sum(0)
+    return g_v, g_phi, g_Bas, g_Un, g_W, g_b
+
+
+def _msg_vvjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, Hv, Hphi, HBas, HUn, HW, Hb, need):
+    """Backward of _msg_vjp for the upstream (Hv, Hphi, HBas, HUn, HW, Hb) (None = zero).
+    need: flags for (Gs, Gv, v, phi, Bas, Un, W, b).  Derivation: with a = [sum_c Gv_c Hv[dst]_c,
+    sum_c Gv_c HUn_c, 0], bb = [sum_c Gv_c v[dst]_c, sum_c Gv_c Un_c, Gs] (bb = the VJP's go),
+    w' = W HBas + HW Bas and o' = w' P + w HP, the VJP's contraction with the upstream is
+    Hv.Gv + sum_e a.o + bb.o'; its gradients are taken term by term."""
+    F, R = cfg.F, cfg.R
+    dst, src = cfg.dst, cfg.src
+    E = Bas.shape[0]
+    z3 = lambda: torch.zeros(E, 3 * F, dtype=Bas.dtype, device=Bas.device)  # noqa: E731
+    w = _msg_w(Bas, W, b)
+    P = phi[dst]
+    HP = Hphi[dst] if Hphi is not None else None
+    o = w * P
+    wp = _msg_w(HBas, W, b) if HBas is not None else z3()
+    if HW is not None or Hb is not None:
+        wp = wp + _msg_w(Bas, HW if HW is not None else torch.zeros_like(W), Hb if Hb is not None else torch.zeros_like(b))
+    op = wp * P + (w * HP if HP is not None else 0)
+    Gs_e, Gv_e = Gs[src], Gv[src]
+    Vj = v[dst]
+    HVj = Hv[dst] if Hv is not None else None
+    out = [None] * 8
+    # (1) gradients w.r.t. the VJP's upstream (Gs, Gv): J applied to the tangent
+    if need[0]:
+        out[0] = _scatter(cfg.N, src, op[:, 2 * F:])
+    if need[1]:
+        t = Vj * op[:, :F].unsqueeze(1) + op[:, F:2 * F].unsqueeze(1) * Un.unsqueeze(2)
+        if HVj is not None:
+            t = t + HVj * o[:, :F].unsqueeze(1)
+        if HUn is not None:
+            t = t + o[:, F:2 * F].unsqueeze(1) * HUn.unsqueeze(2)
+        gGv = _scatter(cfg.N, src, t)
+        out[1] = gGv + Hv if Hv is not None else gGv
+    # (2) second-order terms
+    a = torch.cat([(Gv_e * HVj).sum(1) if HVj is not None else torch.zeros_like(Gs_e),
+                   (Gv_e * HUn.unsqueeze(2)).sum(1) if HUn is not None else torch.zeros_like(Gs_e),
+                   torch.zeros_like(Gs_e)], 1)
+    bb = torch.cat([(Gv_e * Vj).sum(1), (Gv_e * Un.unsqueeze(2)).sum(1), Gs_e], 1)
+    if need[2]:
+        out[2] = _scatter(cfg.N, dst, Gv_e * op[:, :F].unsqueeze(1))
+    if need[3]:
+        out[3] = _scatter(cfg.N, dst, a * w + bb * wp)
+    gw2 = a * P + (bb * HP if HP is not None else 0)
+    bP = bb * P
+    if need[4]:
+        gB = torch.cat([gw2 @ W, (gw2 * b.view(1, -1)).sum(1, keepdim=True)], 1)
+        if HW is not None:
+            gB[:, :R] += bP @ HW
+        if Hb is not None:
+            gB[:, R] += (bP * Hb.view(1, -1)).sum(1)
+        out[4] = gB
+    if need[5]:
+        out[5] = (Gv_e * op[:, F:2 * F].unsqueeze(1)).sum(2)
+    if need[6] or need[7]:
+        gW = gw2.t() @ Bas[:, :R]
+        gb = (gw2 * Bas[:, R:R + 1]).sum(0)
+        if HBas is not None:
+            gW = gW + bP.t() @ HBas[:, :R]
+            gb = gb + (bP * HBas[:, R:R + 1]).sum(0)
+        out[6], out[7] = gW, gb
+    return out
+
+
+class _Msg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, v, phi, Bas, Un, W, b, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(v, phi, Bas, Un, W, b)
+        return _msg_fwd(cfg, s, v, phi, Bas, Un, W, b)
+
+    @staticmethod
+    def backward(ctx, Gs, Gv):
+        v, phi, Bas, Un, W, b = ctx.saved_tensors
+        if Gs is None:
+            Gs = torch.zeros_like(phi[:, :ctx.cfg.F])
+        if Gv is None:
+            Gv = torch.zeros_like(v)
+        need_w = not _state["inputs_only"] and (ctx.needs_input_grad[5] or ctx.needs_input_grad[6])
+        g_v, g_phi, g_Bas, g_Un, g_W, g_b = _MsgBwd.apply(Gs, Gv, v, phi, Bas, Un, W, b, ctx.cfg, need_w)
+        return Gs, g_v, g_phi, g_Bas, g_Un, g_W, g_b, None
+
+
+class _MsgBwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Gs, Gv, v, phi, Bas, Un, W, b, cfg, need_w):
+        ctx.cfg = cfg
+        ctx.save_for_backward(Gs, Gv, v, phi, Bas, Un, W, b)
+        out = _msg_vjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, need_w)
+        if need_w:
+            ctx.mark_non_differentiable(out[4], out[5])
+        return out
+
+    @staticmethod
+    def backward(ctx, Hv, Hphi, HBas, HUn, HW, Hb):
+        Gs, Gv, v, phi, Bas, Un, W, b = ctx.saved_tensors
+        need = ctx.needs_input_grad[:8]
+        g = _msg_vvjp(ctx.cfg, Gs, Gv, v, phi, Bas, Un, W, b, Hv, Hphi, HBas, HUn, None, None, need)
+        return (*g, None, None)
+
+
+def painn_message(s, v, phi, Bas, Un, W, b, dst_si, src_si):
+    """s + sum_src o_s, v + sum_src (v[dst] o_v + o_e d̂/d) with o = ([W | b] basis) * phi[dst]."""
+    cfg = _MsgCfg()
+    cfg.dst, cfg.src = dst_si.index64, src_si.index64
+    cfg.dst_si, cfg.src_si = dst_si, src_si
+    cfg.N, cfg.F, cfg.R = s.shape[0], s.shape[1], W.shape[1]
+    return _Msg.apply(s, v, phi, Bas, Un, W, b, cfg)
+
+
+# ============================================================================ node chains
+class ChainProg:
+    """A compiled node chain: forward program + generated VJP / VVJP programs."""
+
+    def __init__(self, prog, ins, outs, weights):
+        self.prog, self.ins, self.outs, self.weights = prog, list(ins), list(outs), list(weights)
+        # first order: reverse of the forward program
+        self.gouts = [rp.Val(o.w, o.nc, name=f"g{o.name}") for o in self.outs]
+        vjp, self.vjp_res, self.vjp_wg = rp.reverse(prog, dict(zip(self.outs, self.gouts)), self.ins)
+        vjp_in, self.vjp_in_res, _ = rp.reverse(prog, dict(zip(self.outs, self.gouts)), self.ins, want_weights=False)
+        # backward programs recompute the forward values they read (cheap row-local work)
+        wg_reads = [r[3] for r in self.vjp_wg if r[0] == "w"] + [r[4] for r in self.vjp_wg if r[0] == "w"] + \
+            [r[2] for r in self.vjp_wg if r[0] == "b"]
+        self.vjp = rp.concat_pruned(prog.ins, vjp.ins, keep_out=wg_reads)
+        self.vjp_in = rp.concat_pruned(prog.ins, vjp_in.ins)
+        # second order: reverse of the dual program seeded on the output tangents
+        self.hins = [rp.Val(x.w, x.nc, name=f"h{x.name}") for x in self.ins]
+        self.dual, tan = rp.dual(prog, dict(zip(self.ins, self.hins)))
+        self.touts = [tan.get(o.base.id) for o in self.outs]
+        seeds = {t: g for t, g in zip(self.touts, self.gouts) if t is not None}
+        vvjp, self.vvjp_res, self.vvjp_wg = rp.reverse(self.dual, seeds, self.ins)
+        wg_reads = [r[3] for r in self.vvjp_wg if r[0] == "w"] + [r[4] for r in self.vvjp_wg if r[0] == "w"] + \
+            [r[2] for r in self.vvjp_wg if r[0] == "b"]
+        self.vvjp = rp.concat_pruned(self.dual.ins, vvjp.ins, keep_out=[t for t in self.touts if t is not None] +
+                                     wg_reads)
+
+
+def _run(cp, prog, env_in, mask, N, wg=None):
+    env = {v.base.id: t.reshape(N, -1) for v, t in env_in.items()}
+    rp.run_torch(prog, env, cp.weights_t, mask, N)
+    grads = None
+    if wg is not None:
+        grads = rp.wgrads_torch(wg, env, N, cp.weights_t, [None] * len(cp.weights_t))
+    return env, grads
+
+
+class _Chain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cp, mask, n_in, *args):
+        xs, ws = args[:n_in], args[n_in:]
+        N = xs[0].shape[0]
+        cp.weights_t = ws
+        env, _ = _run(cp, cp.prog, dict(zip(cp.ins, xs)), mask, N)
+        outs = [env[o.base.id].view(N, o.nc, o.w) if o.nc == 3 else env[o.base.id] for o in cp.outs]
+        ctx.cp, ctx.mask, ctx.n_in = cp, mask, n_in
+        ctx.save_for_backward(*xs, *ws)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        cp, n_in = ctx.cp, ctx.n_in
+        saved = ctx.saved_tensors
+        xs, ws = saved[:n_in], saved[n_in:]
+        gouts = [g if g is not None else torch.zeros(xs[0].shape[0], o.nc * o.w, dtype=xs[0].dtype,
+                                                     device=xs[0].device)
+                 for g, o in zip(gouts, cp.outs)]
+        need_w = not _state["inputs_only"] and any(ctx.needs_input_grad[3 + n_in:])
+        res = _ChainBwd.apply(cp, ctx.mask, n_in, len(gouts), need_w, *gouts, *xs, *ws)
+        gx, gw = res[:n_in], res[n_in:]
+        return (None, None, None, *gx, *(gw if need_w else [None] * len(ws)))
+
+
+class _ChainBwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cp, mask, n_in, n_out, need_w, *args):
+        gouts, xs, ws = args[:n_out], args[n_out:n_out + n_in], args[n_out + n_in:]
+        N = xs[0].shape[0]
+        cp.weights_t = ws
+        prog = cp.vjp if need_w else cp.vjp_in
+        env, grads = _run(cp, prog, {**dict(zip(cp.ins, xs)), **dict(zip(cp.gouts, gouts))}, mask, N,
+                          cp.vjp_wg if need_w else None)
+        gx = []
+        res = cp.vjp_res if need_w else cp.vjp_in_res
+        for x, t in zip(cp.ins, xs):
+            a = res[x]
+            gx.append(_slot(env, a, N).reshape(t.shape) if a is not None else torch.zeros_like(t))
+        gw = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)] if need_w else \
+            [torch.zeros(0, dtype=xs[0].dtype, device=xs[0].device) for _ in ws]
+        ctx.mark_non_differentiable(*gw)
+        ctx.cp, ctx.mask, ctx.n_in, ctx.n_out = cp, mask, n_in, n_out
+        ctx.save_for_backward(*gouts, *xs, *ws)
+        return (*gx, *gw)
+
+    @staticmethod
+    def backward(ctx, *hs):
+        cp, n_in, n_out = ctx.cp, ctx.n_in, ctx.n_out
+        saved = ctx.saved_tensors
+        gouts, xs, ws = saved[:n_out], saved[n_out:n_out + n_in], saved[n_out + n_in:]
+        N = xs[0].shape[0]
+        hx = [h if h is not None else torch.zeros_like(x) for h, x in zip(hs[:n_in], xs)]
+        cp.weights_t = ws
+        env_in = {**dict(zip(cp.ins, xs)), **dict(zip(cp.hins, hx)), **dict(zip(cp.gouts, gouts))}
+        env, grads = _run(cp, cp.vvjp, env_in, ctx.mask, N, cp.vvjp_wg)
+        g_gouts = []
+        for t, g in zip(cp.touts, gouts):
+            g_gouts.append(env[t.id].reshape(g.shape) if t is not None else torch.zeros_like(g))
+        g_xs = []
+        for x, t in zip(cp.ins, xs):
+            a = cp.vvjp_res[x]
+            g_xs.append(_slot(env, a, N).reshape(t.shape) if a is not None else torch.zeros_like(t))
+        g_ws = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)]
+        return (None, None, None, None, None, *g_gouts, *g_xs, *g_ws)
+
+
+def _slot(env, v, N):
+    t = env[v.base.id]
+    if v.full:
+        return t
+    return t.view(N, v.base.nc, v.base.w)[:, :, v.c0:v.c0 + v.w].reshape(N, -1)
+
+
+def run_chain(cp, mask, xs, ws):
+    """Outputs of the chain ``cp`` for inputs ``xs`` (vectors as [N, 3, w]) and weights ``ws``
+    (aligned with the chain's weight list)."""
+    return _Chain.apply(cp, mask, len(xs), *xs, *ws)
+
+
+# ============================================================================ PAINN model
+def _act_name(m):
+    for name, cls in (("relu", torch.nn.ReLU), ("silu", torch.nn.SiLU), ("tanh", torch.nn.Tanh),
+                      ("sigmoid", torch.nn.Sigmoid), ("identity", torch.nn.Identity)):
+        if isinstance(m, cls):
+            return name
+    return None
+
+
+def model_ok(model, ctx):
+    """The native path covers PAINNStack without global attention, edge-feature filters or
+    activation checkpointing, with a supported activation (``HYDRA_UNFUSED=painn`` turns it
+    off; it is NOT affected by ``composite_mode``: it is itself twice differentiable)."""
+    from .pna import _state as _mode_state
+
+    if "painn" in _mode_state["off"] or model.use_global_attn or model.conv_checkpointing:
+        return False
+    if _act_name(model.activation_function) is None:
+        return False
+    data = ctx.data
+    if data.pos is None or ctx.dst_si is None or ctx.src_si is None:
+        return False
+    for conv in model.graph_convs:
+        msg = conv.message
+        if msg.edge_dim is not None and ctx.get("edge_attr") is not None:
+            return False
+    return True
+
+
+class _ChainBuilder:
+    """Row-program builder that maps program weights to module parameters."""
+
+    def __init__(self):
+        self.P = rp.Prog()
+        self.params = []
+
+    def W(self, lin):
+        pid = len(self.params)
+        self.params.append(lin.weight)
+        bid = None
+        if lin.bias is not None:
+            bid = len(self.params)
+            self.params.append(lin.bias)
+        return rp.Weight(pid, lin.weight.shape[0], lin.weight.shape[1], bid)
+
+    def linear(self, xs, lin, name=""):
+        return self.P.lin(xs, self.W(lin), name=name)
+
+    def mlp2(self, x, seq, act_mid, name):
+        """Linear - act - Linear (scalar_message_mlp / node_embed_out)."""
+        h = self.P.act(self.linear([(x, 0)], seq[0], name=f"{name}.0"), act_mid, name=f"{name}.a")
+        return self.linear([(h, 0)], seq[2], name=name)
+
+
+def _phi_prog(layer, F, mask):
+    """Layer-0 prologue: phi = scalar_message_mlp(mask(x))."""
+    cb = _ChainBuilder()
+    s = cb.P.input(F, 1, "s0")
+    x = cb.P.mask(s, name="s0m") if mask else s
+    phi = cb.mlp2(x, layer.message.scalar_message_mlp, "silu", "phi0")
+    cb.P.outputs = [phi]
+    return ChainProg(cb.P, [s], [phi], [None] * len(cb.params)), cb.params
+
+
+def _layer_prog(layer, next_layer, act, mask):
+    """update -> node_embed_out -> activation (+ mask) [-> vec_embed_out, next phi]."""
+    upd = layer.update
+    F = upd.update_V.weight.shape[1]
+    cb = _ChainBuilder()
+    P = cb.P
+    s = P.input(F, 1, "s")
+    v = P.input(F, 3, "v")
+    Uv = cb.linear([(v, 0)], getattr(upd, upd._u), name="Uv")
+    Vv = cb.linear([(v, 0)], upd.update_V, name="Vv")
+    n = P.norm3(Vv, name="nVv")
+    a1 = P.act(cb.linear([(n, 0), (s, F)], upd.update_mlp[0], name="a1p"), "silu", name="a1")
+    a = cb.linear([(a1, 0)], upd.update_mlp[2], name="a")
+    inner = P.dot3(Uv, Vv, name="inner")
+    if upd.last_layer:
+        s2 = P.add(s, P.mul(a.slice(0, F), inner), a.slice(F, F), name="s2")
+        v2 = None
+    else:
+        s2 = P.add(s, P.mul(a.slice(F, F), inner), a.slice(2 * F, F), name="s2")
+        v2 = P.add(v, P.mul(a.slice(0, F), Uv), name="v2")
+    s3 = cb.mlp2(s2, layer.node_embed_out, "tanh", "s3")
+    so = P.act(s3, act, name="so_a")
+    if mask:
+        so = P.mask(so, name="so")
+    outs = [so]
+    if v2 is not None:
+        outs.append(cb.linear([(v2, 0)], layer.vec_embed_out, name="v3"))
+    if next_layer is not None:
+        outs.append(cb.mlp2(so, next_layer.message.scalar_message_mlp, "silu", "phi"))
+    P.outputs = outs
+    return ChainProg(P, [s, v], outs, [None] * len(cb.params)), cb.params
+
+
+def _programs(model, mask):
+    key = ("painn_progs", bool(mask), _act_name(model.activation_function))
+    cache = model.__dict__.setdefault("_native_force_progs", {})
+    if key not in cache:
+        layers = list(model.graph_convs)
+        act = _act_name(model.activation_function)
+        F0 = layers[0].update.update_V.weight.shape[1]
+        progs = [_phi_prog(layers[0], F0, mask)]
+        for i, layer in enumerate(layers):
+            nxt = layers[i + 1] if i + 1 < len(layers) else None
+            progs.append(_layer_prog(layer, nxt, act, mask))
+        cache[key] = progs
+    return cache[key]
+
+
+def painn_encode(model, inv, ctx):
+    """Native PAINN encoder: (node features, vector features, ctx), the same values as the
+    layer-by-layer composite (``Base.encode`` over ``_EqLayer``)."""
+    data = ctx.data
+    keep = data.get("node_mask")
+    mask = keep.to(inv.dtype) if keep is not None else None
+    layers = list(model.graph_convs)
+    msg0 = layers[0].message
+    B, U = edge_geometry(data.pos, ctx.dst_si, ctx.src_si, msg0.num_radial, msg0.cutoff,
+                         shifts=data.get("edge_shifts"))
+    progs = _programs(model, mask is not None)
+    cp, params = progs[0]
+    s = inv
+    (phi,) = run_chain(cp, mask, [s], params)
+    v = torch.zeros(s.shape[0], 3, s.shape[1], device=s.device, dtype=s.dtype)
+    for i, layer in enumerate(layers):
+        flt = layer.message.filter_layer
+        s1, v1 = painn_message(s, v, phi, B, U, flt.weight, flt.bias, ctx.dst_si, ctx.src_si)
+        cp, params = progs[i + 1]
+        outs = run_chain(cp, mask, [s1, v1], params)
+        s = outs[0]
+        if len(outs) > 1 and cp.outs[1].nc == 3:
+            v = outs[1]
+            phi = outs[2] if len(outs) > 2 else None
+        else:
+            v = v1
+            phi = outs[1] if len(outs) > 1 else None
+    return s, v, ctx
