@@ -394,6 +394,7 @@ struct WgProb {
   int rwg0;   // first reduce-kernel workgroup
   int vec;    // bit0: dY float4 path, bit1: X float4 path
   int accumulate;
+  int ldw;    // row stride of dW (a column block of a wider weight gradient: ldw > I)
 };
 
 struct WgArgs {
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
   for (int u = 0; u < 8; ++u)
     if (s0 + u < S) acc[u] += part[(int64_t)(s0 + u) * ld + j];
   const float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  float* dst = j < nw ? P.dw + j : P.db + (j - nw);
+  float* dst = j < nw ? P.dw + (j / P.I) * P.ldw + (j % P.I) : P.db + (j - nw);
   *dst = P.accumulate ? *dst + v : v;
 }
 
@@ -577,8 +578,9 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       const int64_t M = dY.size(0);
       const int O = (int)dY.size(1), I = (int)X.size(1);
       const auto& dW = dWs[k];
-      HY_CHECK(dW.is_contiguous() && dW.scalar_type() == at::kFloat && dW.numel() == (int64_t)O * I,
-               "linear_wgrad_grouped: dW must be a contiguous fp32 [O, I]");
+      HY_CHECK(dW.scalar_type() == at::kFloat && dW.numel() == (int64_t)O * I &&
+                   (dW.is_contiguous() || (dW.dim() == 2 && dW.stride(1) == 1 && dW.size(0) == O)),
+               "linear_wgrad_grouped: dW must be fp32 [O, I] with unit column stride");
       const bool hb = dbs[k].defined() && dbs[k].numel() > 0;
       if (hb)
         HY_CHECK(dbs[k].is_contiguous() && dbs[k].numel() == O && dbs[k].scalar_type() == at::kFloat,
@@ -588,6 +590,7 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.dy = dY.data_ptr<float>();
       P.x = X.data_ptr<float>();
       P.dw = dW.data_ptr<float>();
+      P.ldw = (dW.dim() == 2 && !dW.is_contiguous()) ? (int)dW.stride(0) : I;
       P.db = hb ? dbs[k].data_ptr<float>() : nullptr;
       P.ldy = (int)dY.stride(0);
       P.ldx = (int)X.stride(0);

@@ -213,6 +213,13 @@ class PAINNStack(_EqStackBase):
             return None
         return painn_force.painn_encode(self, inv, ctx)
 
+    def decode(self, x, equiv, ctx):
+        # the native encoder fused a single node MLP head into its last node chain
+        e = ctx.get("native_node_head")
+        if e is not None:
+            return [e]
+        return super().decode(x, equiv, ctx)
+
     def get_conv(self, input_dim, output_dim, last_layer=False, edge_dim=None):
         hidden = output_dim if input_dim == 1 else input_dim
         assert hidden > 1, "PainnNet requires more than one hidden dimension between input_dim and output_dim."

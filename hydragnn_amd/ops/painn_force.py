@@ -87,6 +87,10 @@ def _geom_vec(pos, dst, src, shifts):
 class _GeomCfg:
     __slots__ = ("R", "a", "cutoff", "eps", "dst", "src", "N", "dst_si", "src_si", "shifts")
 
+    def csr_args(self):
+        d, s_ = self.dst_si, self.src_si
+        return (d.index, s_.index, d.rowptr, d.perm, s_.rowptr, s_.perm)
+
 
 def _geom_fwd(cfg, pos):
     vec = _geom_vec(pos, cfg.dst, cfg.src, cfg.shifts)
@@ -127,8 +131,14 @@ def _geom_vvjp(cfg, pos, gB, gU, hpos, need_g, need_pos):
     return hB, hU, gp
 
 
-def _native_ok(t):
-    return False  # device kernels: csrc/painn_force.hip (wired in once built)
+def _ops():
+    from .. import _native
+
+    return _native.ops()
+
+
+def _c(t):
+    return t if t is None or t.is_contiguous() else t.contiguous()
 
 
 class _Geom(torch.autograd.Function):
@@ -136,6 +146,10 @@ class _Geom(torch.autograd.Function):
     def forward(ctx, pos, cfg):
         ctx.cfg = cfg
         ctx.save_for_backward(pos)
+        if _device(pos):
+            d, s_ = cfg.csr_args()[:2]
+            B, U = _ops().painn_geom_fwd(_c(pos), _c(cfg.shifts), d, s_, cfg.R, cfg.a, cfg.cutoff, cfg.eps)
+            return B, U
         return _geom_fwd(cfg, pos)
 
     @staticmethod
@@ -154,13 +168,22 @@ class _GeomBwd(torch.autograd.Function):
     def forward(ctx, gB, gU, pos, cfg):
         ctx.cfg = cfg
         ctx.save_for_backward(gB, gU, pos)
+        if _device(pos):
+            return _ops().painn_geom_vjp(_c(pos), _c(cfg.shifts), *cfg.csr_args(), _c(gB), _c(gU), cfg.R, cfg.a,
+                                         cfg.cutoff, cfg.eps)
         return _geom_vjp(cfg, pos, gB, gU)
 
     @staticmethod
     def backward(ctx, hpos):
         gB, gU, pos = ctx.saved_tensors
-        hB, hU, gp = _geom_vvjp(ctx.cfg, pos, gB, gU, hpos, ctx.needs_input_grad[0] or ctx.needs_input_grad[1],
-                                ctx.needs_input_grad[2])
+        cfg = ctx.cfg
+        need_g = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        need_pos = ctx.needs_input_grad[2]
+        if _device(pos):
+            hB, hU, gp = _ops().painn_geom_vvjp(_c(pos), _c(cfg.shifts), *cfg.csr_args(), _c(gB), _c(gU), _c(hpos),
+                                                cfg.R, cfg.a, cfg.cutoff, cfg.eps, need_g, need_pos)
+            return (hB if need_g else None), (hU if need_g else None), (gp if need_pos else None), None
+        hB, hU, gp = _geom_vvjp(cfg, pos, gB, gU, hpos, need_g, need_pos)
         return hB, hU, gp, None
 
 
@@ -178,6 +201,10 @@ def edge_geometry(pos, dst_si, src_si, num_radial, cutoff, shifts=None, eps=1e-9
 # ============================================================================ message
 class _MsgCfg:
     __slots__ = ("dst", "src", "N", "F", "R", "dst_si", "src_si")
+
+    def csr_args(self):
+        d, s_ = self.dst_si, self.src_si
+        return (d.index, s_.index, d.rowptr, d.perm, s_.rowptr, s_.perm)
 
 
 def _msg_w(Bas, W, b):
@@ -284,6 +311,9 @@ class _Msg(torch.autograd.Function):
     def forward(ctx, s, v, phi, Bas, Un, W, b, cfg):
         ctx.cfg = cfg
         ctx.save_for_backward(v, phi, Bas, Un, W, b)
+        if _device(s):
+            s1, v1 = _ops().painn_msg_fwd(_c(s), _c(v), _c(phi), _c(Bas), _c(Un), _c(W), _c(b), *cfg.csr_args())
+            return s1, v1
         return _msg_fwd(cfg, s, v, phi, Bas, Un, W, b)
 
     @staticmethod
@@ -303,7 +333,14 @@ class _MsgBwd(torch.autograd.Function):
     def forward(ctx, Gs, Gv, v, phi, Bas, Un, W, b, cfg, need_w):
         ctx.cfg = cfg
         ctx.save_for_backward(Gs, Gv, v, phi, Bas, Un, W, b)
-        out = _msg_vjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, need_w)
+        if _device(v):
+            out = _ops().painn_msg_vjp(_c(Gs), _c(Gv), _c(v), _c(phi), _c(Bas), _c(Un), _c(W), _c(b),
+                                       *cfg.csr_args(), need_w)
+            out = list(out)
+            if not need_w:
+                out[4] = out[5] = None
+        else:
+            out = _msg_vjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, need_w)
         if need_w:
             ctx.mark_non_differentiable(out[4], out[5])
         return out
@@ -312,7 +349,13 @@ class _MsgBwd(torch.autograd.Function):
     def backward(ctx, Hv, Hphi, HBas, HUn, HW, Hb):
         Gs, Gv, v, phi, Bas, Un, W, b = ctx.saved_tensors
         need = ctx.needs_input_grad[:8]
-        g = _msg_vvjp(ctx.cfg, Gs, Gv, v, phi, Bas, Un, W, b, Hv, Hphi, HBas, HUn, None, None, need)
+        if _device(v):
+            g = _ops().painn_msg_vvjp(_c(Gs), _c(Gv), _c(v), _c(phi), _c(Bas), _c(Un), _c(W), _c(b),
+                                      *ctx.cfg.csr_args(), _c(Hv), _c(Hphi), _c(HBas), _c(HUn),
+                                      [int(x) for x in need])
+            g = [t if n else None for t, n in zip(g, need)]
+        else:
+            g = _msg_vvjp(ctx.cfg, Gs, Gv, v, phi, Bas, Un, W, b, Hv, Hphi, HBas, HUn, None, None, need)
         return (*g, None, None)
 
 
@@ -331,6 +374,7 @@ class ChainProg:
 
     def __init__(self, prog, ins, outs, weights):
         self.prog, self.ins, self.outs, self.weights = prog, list(ins), list(outs), list(weights)
+        self.dev = {}  # (mode, device) -> _DevMode
         # first order: reverse of the forward program
         self.gouts = [rp.Val(o.w, o.nc, name=f"g{o.name}") for o in self.outs]
         vjp, self.vjp_res, self.vjp_wg = rp.reverse(prog, dict(zip(self.outs, self.gouts)), self.ins)
@@ -361,14 +405,134 @@ def _run(cp, prog, env_in, mask, N, wg=None):
     return env, grads
 
 
+def _device(t):
+    from .. import _native
+
+    return t.is_cuda and t.dtype == torch.float32 and _native.available()
+
+
+class _DevMode:
+    """One program lowered for the interpreter: tables on the device + external roots."""
+
+    def __init__(self, prog, ext_roots, n_weights, wg, dev):
+        ins, bufs, width, where = rp.compile_device(prog, ext_roots, n_weights)
+        self.ins = torch.from_numpy(ins).to(dev)
+        self.bufs = torch.from_numpy(bufs).to(dev)
+        self.width = width
+        self.where = where
+        self.bufs_np = bufs
+        self.ext = list(ext_roots)
+        self.rounds = rp.wgrad_rounds(wg) if wg else []
+
+
+def _dev_mode(cp, mode, dev):
+    key = (mode, str(dev))
+    dm = cp.dev.get(key)
+    if dm is None:
+        nW = len(cp.weights)
+        if mode == "fwd":
+            prog, ext, wg = cp.prog, cp.ins + [o.base for o in cp.outs], None
+        elif mode == "vjp_in":
+            prog, wg = cp.vjp_in, None
+            ext = cp.ins + cp.gouts + [a.base for a in cp.vjp_in_res.values() if a is not None]
+        elif mode == "vjp":
+            prog, wg = cp.vjp, cp.vjp_wg
+            ext = cp.ins + cp.gouts + [a.base for a in cp.vjp_res.values() if a is not None]
+        else:
+            prog, wg = cp.vvjp, cp.vvjp_wg
+            ext = cp.ins + cp.hins + cp.gouts + [t for t in cp.touts if t is not None] + \
+                [a.base for a in cp.vvjp_res.values() if a is not None]
+        seen, uniq = set(), []
+        for v in ext:
+            if v.id not in seen:
+                seen.add(v.id)
+                uniq.append(v)
+        dm = _DevMode(prog, uniq, nW, wg, dev)
+        cp.dev[key] = dm
+    return dm
+
+
+def _dev_exec(cp, mode, N, mask, feeds, ws):
+    """Run program ``mode`` on the device.  feeds: {root Val: tensor}; returns a getter
+    Val -> [N, nc * w] view (external tensor or workspace slot) and the workspace."""
+    from .. import _native
+
+    x0 = next(iter(feeds.values()))
+    dm = _dev_mode(cp, mode, x0.device)
+    tens = {}
+    ptrs = [w if w.is_contiguous() else w.contiguous() for w in ws]
+    for v in dm.ext:
+        t = feeds.get(v)
+        if t is None:
+            t = torch.empty(N, v.nc * v.w, device=x0.device, dtype=torch.float32)
+        t = t.reshape(N, v.nc * v.w)
+        if not t.is_contiguous():
+            t = t.contiguous()
+        tens[v.id] = t
+        ptrs.append(t)
+    wsb = torch.empty(max(N * dm.width, 1), device=x0.device, dtype=torch.float32)
+    _native.ops().rowprog_run(dm.ins, dm.bufs, wsb, mask, ptrs, N)
+
+    def get(v):
+        b = v.base
+        if b.id in tens:
+            t = tens[b.id]
+        else:
+            k = dm.where[b.id]
+            off = int(dm.bufs_np[k][1]) * N
+            t = wsb[off:off + N * b.nc * b.w].view(N, b.nc * b.w)
+        if v.full:
+            return t
+        return t.view(N, b.nc, b.w)[:, :, v.c0:v.c0 + v.w].reshape(N, -1) if b.nc == 1 else \
+            t.view(N, b.nc, b.w)[:, :, v.c0:v.c0 + v.w]
+
+    return get, dm
+
+
+def _dev_wgrads(dm, get, N, ws):
+    """Weight gradients of a device run: one grouped MFMA launch pair per round."""
+    from .. import _native
+
+    grads = [None] * len(ws)
+    covered = {}
+    for (pid, k0, G, X, bias, acc) in (dm.rounds[0] if dm.rounds else []):
+        covered.setdefault(pid, 0)
+        covered[pid] += X.w
+    for pid, K in covered.items():
+        grads[pid] = torch.empty_like(ws[pid]) if K == ws[pid].shape[1] else torch.zeros_like(ws[pid])
+    for rnd in dm.rounds:
+        dys, xs, dws, dbs, accs = [], [], [], [], []
+        for (pid, k0, G, X, bias, acc) in rnd:
+            g, x = get(G), get(X)
+            if G.nc == 3:
+                g = g.reshape(N, 3, G.w).reshape(N * 3, G.w) if g.is_contiguous() else \
+                    g.reshape(N * 3, G.w)
+                x = x.reshape(N * 3, X.w) if x.is_contiguous() else x.reshape(N * 3, X.w)
+            if grads[pid] is None:
+                grads[pid] = torch.zeros_like(ws[pid])
+            if bias is not None and grads[bias] is None:
+                grads[bias] = torch.empty_like(ws[bias])
+            dys.append(g)
+            xs.append(x)
+            dws.append(grads[pid][:, k0:k0 + X.w])
+            dbs.append(grads[bias] if bias is not None else torch.empty(0, device=g.device))
+            accs.append(1 if acc else 0)
+        _native.ops().linear_wgrad_grouped(dys, xs, dws, dbs, accs)
+    return grads
+
+
 class _Chain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cp, mask, n_in, *args):
         xs, ws = args[:n_in], args[n_in:]
         N = xs[0].shape[0]
-        cp.weights_t = ws
-        env, _ = _run(cp, cp.prog, dict(zip(cp.ins, xs)), mask, N)
-        outs = [env[o.base.id].view(N, o.nc, o.w) if o.nc == 3 else env[o.base.id] for o in cp.outs]
+        if _device(xs[0]):
+            get, _ = _dev_exec(cp, "fwd", N, mask, dict(zip(cp.ins, xs)), ws)
+            outs = [get(o).reshape(N, o.nc, o.w) if o.nc == 3 else get(o) for o in cp.outs]
+        else:
+            cp.weights_t = ws
+            env, _ = _run(cp, cp.prog, dict(zip(cp.ins, xs)), mask, N)
+            outs = [_slot(env, o, N).reshape(N, o.nc, o.w) if o.nc == 3 else _slot(env, o, N) for o in cp.outs]
         ctx.cp, ctx.mask, ctx.n_in = cp, mask, n_in
         ctx.save_for_backward(*xs, *ws)
         return tuple(outs)
@@ -378,8 +542,8 @@ class _Chain(torch.autograd.Function):
         cp, n_in = ctx.cp, ctx.n_in
         saved = ctx.saved_tensors
         xs, ws = saved[:n_in], saved[n_in:]
-        gouts = [g if g is not None else torch.zeros(xs[0].shape[0], o.nc * o.w, dtype=xs[0].dtype,
-                                                     device=xs[0].device)
+        gouts = [g.contiguous() if g is not None else
+                 torch.zeros(xs[0].shape[0], o.nc * o.w, dtype=xs[0].dtype, device=xs[0].device)
                  for g, o in zip(gouts, cp.outs)]
         need_w = not _state["inputs_only"] and any(ctx.needs_input_grad[3 + n_in:])
         res = _ChainBwd.apply(cp, ctx.mask, n_in, len(gouts), need_w, *gouts, *xs, *ws)
@@ -392,15 +556,16 @@ class _ChainBwd(torch.autograd.Function):
     def forward(ctx, cp, mask, n_in, n_out, need_w, *args):
         gouts, xs, ws = args[:n_out], args[n_out:n_out + n_in], args[n_out + n_in:]
         N = xs[0].shape[0]
-        cp.weights_t = ws
-        prog = cp.vjp if need_w else cp.vjp_in
-        env, grads = _run(cp, prog, {**dict(zip(cp.ins, xs)), **dict(zip(cp.gouts, gouts))}, mask, N,
-                          cp.vjp_wg if need_w else None)
-        gx = []
         res = cp.vjp_res if need_w else cp.vjp_in_res
-        for x, t in zip(cp.ins, xs):
-            a = res[x]
-            gx.append(_slot(env, a, N).reshape(t.shape) if a is not None else torch.zeros_like(t))
+        feeds = {**dict(zip(cp.ins, xs)), **dict(zip(cp.gouts, gouts))}
+        if _device(xs[0]):
+            get, dm = _dev_exec(cp, "vjp" if need_w else "vjp_in", N, mask, feeds, ws)
+            grads = _dev_wgrads(dm, get, N, ws) if need_w else None
+        else:
+            cp.weights_t = ws
+            env, grads = _run(cp, cp.vjp if need_w else cp.vjp_in, feeds, mask, N, cp.vjp_wg if need_w else None)
+            get = lambda v: _slot(env, v, N)  # noqa: E731
+        gx = [get(res[x]).reshape(t.shape) if res[x] is not None else torch.zeros_like(t) for x, t in zip(cp.ins, xs)]
         gw = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)] if need_w else \
             [torch.zeros(0, dtype=xs[0].dtype, device=xs[0].device) for _ in ws]
         ctx.mark_non_differentiable(*gw)
@@ -414,17 +579,18 @@ class _ChainBwd(torch.autograd.Function):
         saved = ctx.saved_tensors
         gouts, xs, ws = saved[:n_out], saved[n_out:n_out + n_in], saved[n_out + n_in:]
         N = xs[0].shape[0]
-        hx = [h if h is not None else torch.zeros_like(x) for h, x in zip(hs[:n_in], xs)]
-        cp.weights_t = ws
-        env_in = {**dict(zip(cp.ins, xs)), **dict(zip(cp.hins, hx)), **dict(zip(cp.gouts, gouts))}
-        env, grads = _run(cp, cp.vvjp, env_in, ctx.mask, N, cp.vvjp_wg)
-        g_gouts = []
-        for t, g in zip(cp.touts, gouts):
-            g_gouts.append(env[t.id].reshape(g.shape) if t is not None else torch.zeros_like(g))
-        g_xs = []
-        for x, t in zip(cp.ins, xs):
-            a = cp.vvjp_res[x]
-            g_xs.append(_slot(env, a, N).reshape(t.shape) if a is not None else torch.zeros_like(t))
+        hx = [h.contiguous() if h is not None else torch.zeros_like(x) for h, x in zip(hs[:n_in], xs)]
+        feeds = {**dict(zip(cp.ins, xs)), **dict(zip(cp.hins, hx)), **dict(zip(cp.gouts, gouts))}
+        if _device(xs[0]):
+            get, dm = _dev_exec(cp, "vvjp", N, ctx.mask, feeds, ws)
+            grads = _dev_wgrads(dm, get, N, ws)
+        else:
+            cp.weights_t = ws
+            env, grads = _run(cp, cp.vvjp, feeds, ctx.mask, N, cp.vvjp_wg)
+            get = lambda v: _slot(env, v, N)  # noqa: E731
+        g_gouts = [get(t).reshape(g.shape) if t is not None else torch.zeros_like(g) for t, g in zip(cp.touts, gouts)]
+        g_xs = [get(cp.vvjp_res[x]).reshape(t.shape) if cp.vvjp_res[x] is not None else torch.zeros_like(t)
+                for x, t in zip(cp.ins, xs)]
         g_ws = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)]
         return (None, None, None, None, None, *g_gouts, *g_xs, *g_ws)
 
@@ -506,8 +672,24 @@ def _phi_prog(layer, F, mask):
     return ChainProg(cb.P, [s], [phi], [None] * len(cb.params)), cb.params
 
 
-def _layer_prog(layer, next_layer, act, mask):
-    """update -> node_embed_out -> activation (+ mask) [-> vec_embed_out, next phi]."""
+def _head_seq(model):
+    """The node-level MLP head (``MLPNode`` 'mlp': Linear/activation chain) when the model
+    has exactly one node head and one branch, else None."""
+    if model.num_heads != 1 or model.head_type[0] != "node" or getattr(model, "num_branches", 1) != 1 or \
+            model.var_output:
+        return None
+    head = model.heads_NN[0]["branch-0"]
+    if getattr(head, "node_type", None) != "mlp":
+        return None
+    seq = list(head.mlp[0])
+    for m in seq:
+        if not isinstance(m, torch.nn.Linear) and _act_name(m) is None:
+            return None
+    return seq
+
+
+def _layer_prog(layer, next_layer, act, mask, head=None):
+    """update -> node_embed_out -> activation (+ mask) [-> vec_embed_out, next phi | node head]."""
     upd = layer.update
     F = upd.update_V.weight.shape[1]
     cb = _ChainBuilder()
@@ -535,6 +717,12 @@ def _layer_prog(layer, next_layer, act, mask):
         outs.append(cb.linear([(v2, 0)], layer.vec_embed_out, name="v3"))
     if next_layer is not None:
         outs.append(cb.mlp2(so, next_layer.message.scalar_message_mlp, "silu", "phi"))
+    elif head is not None:
+        h = so
+        for k, m in enumerate(head):
+            h = cb.linear([(h, 0)], m, name=f"head{k}") if isinstance(m, torch.nn.Linear) else \
+                P.act(h, _act_name(m), name=f"head{k}a")
+        outs.append(h)
     P.outputs = outs
     return ChainProg(P, [s, v], outs, [None] * len(cb.params)), cb.params
 
@@ -547,9 +735,10 @@ def _programs(model, mask):
         act = _act_name(model.activation_function)
         F0 = layers[0].update.update_V.weight.shape[1]
         progs = [_phi_prog(layers[0], F0, mask)]
+        head = _head_seq(model)
         for i, layer in enumerate(layers):
             nxt = layers[i + 1] if i + 1 < len(layers) else None
-            progs.append(_layer_prog(layer, nxt, act, mask))
+            progs.append(_layer_prog(layer, nxt, act, mask, head if nxt is None else None))
         cache[key] = progs
     return cache[key]
 
@@ -581,4 +770,6 @@ def painn_encode(model, inv, ctx):
         else:
             v = v1
             phi = outs[1] if len(outs) > 1 else None
+    if phi is not None and i == len(layers) - 1:
+        ctx.native_node_head = phi  # the fused node head's output (PAINNStack.decode)
     return s, v, ctx

@@ -616,3 +616,98 @@ def wgrads_torch(wg, env, N, weights, grads):
                 grads[pid] = torch.zeros_like(weights[pid])
             grads[pid] += g.sum(0)
     return grads
+
+
+# ----------------------------------------------------------------------------- device compile
+INS_INTS = 32
+
+
+def compile_device(prog, ext_roots, n_weights):
+    """Lower ``prog`` to the interpreter's tables (csrc/rowprog.hip).
+
+    ext_roots: root Vals held in external tensors, in pointer-table order after the
+    ``n_weights`` weight pointers.  Every other root the program touches is a workspace
+    slot.  Returns (ins int32 [n, INS_INTS], bufs int32 [nb, 4], ws width per row,
+    {root id: (kind, index)})."""
+    import numpy as np
+
+    ext = {v.id: k for k, v in enumerate(ext_roots)}
+    bufs, where = [], {}
+    prefix = [0]
+
+    def buf(v):
+        b = v.base
+        if b.id not in where:
+            if b.id in ext:
+                where[b.id] = len(bufs)
+                bufs.append((1, n_weights + ext[b.id], b.w, b.nc))
+            else:
+                where[b.id] = len(bufs)
+                bufs.append((0, prefix[0], b.w, b.nc))
+                prefix[0] += b.w * b.nc
+        return where[b.id]
+
+    def opnd(v):
+        if v is None:
+            return [-1, 0, 0, 0]
+        return [buf(v), v.c0, v.w, v.nc]
+
+    rows = []
+    for ins in prog.ins:
+        r = [0] * INS_INTS
+        if ins[0] == "lin":
+            _, y, xs, trans, bias, acc = ins
+            assert 1 <= len(xs) <= 2, "LIN with more than two K blocks"
+            W = xs[0][1]
+            assert all(t[1] is W for t in xs), "K blocks of one LIN share one weight"
+            r[0], r[4] = 1, int(acc)
+            r[5:9] = opnd(y)
+            r[9:13] = opnd(xs[0][0])
+            r[13:17] = opnd(xs[1][0] if len(xs) > 1 else None)
+            r[21], r[22] = W.pid, W.K
+            r[23] = xs[0][2]
+            r[24] = xs[1][2] if len(xs) > 1 else 0
+            r[25] = bias if bias is not None else -1
+            r[26] = int(trans)
+        else:
+            _, op, y, a, b, c, arg, coef, acc = ins
+            r[0], r[1], r[2] = 0, op, arg
+            r[3] = int(np.array([coef], dtype=np.float32).view(np.int32)[0])
+            r[4] = int(acc)
+            r[5:9] = opnd(y)
+            r[9:13] = opnd(a)
+            r[13:17] = opnd(b)
+            r[17:21] = opnd(c)
+        rows.append(r)
+    ins = np.asarray(rows, dtype=np.int32).reshape(-1, INS_INTS)
+    return ins, np.asarray(bufs, dtype=np.int32).reshape(-1, 4), prefix[0], where
+
+
+def wgrad_rounds(wg):
+    """Group weight-gradient records into launch rounds: within a round every destination
+    (weight column block) is distinct; a later record on a destination accumulates onto the
+    earlier round's result.  Bias records ride with the k0 = 0 weight record of the same
+    adjoint.  Returns [[(pid, k0, G, X, bias_pid | None, accumulate)]], {pid: covered}."""
+    bias_of = {}
+    for rec in wg:
+        if rec[0] == "b":
+            bias_of.setdefault(rec[2].id, []).append(rec[1])
+    seen = {}
+    rounds = []
+    # records carrying a bias first: the bias is written (not accumulated) in its first round
+    ws_ = [r for r in wg if r[0] == "w"]
+    ws_ = [r for r in ws_ if r[2] == 0 and bias_of.get(r[3].id)] + \
+        [r for r in ws_ if not (r[2] == 0 and bias_of.get(r[3].id))]
+    for rec in ws_:
+        _, pid, k0, G, X, trans = rec
+        assert trans, "weight gradients of x W products are not generated"
+        key = (pid, k0)
+        r = seen.get(key, 0)
+        seen[key] = r + 1
+        bias = None
+        if k0 == 0 and bias_of.get(G.id):
+            bias = bias_of[G.id].pop(0)
+        while len(rounds) <= r:
+            rounds.append([])
+        rounds[r].append((pid, k0, G, X, bias, r > 0))
+    return rounds

@@ -336,18 +336,27 @@ class TrainStep:
         # tall-linear weight gradients are deferred and computed by one grouped launch pair
         # at the end of backward (ops/linear.py); their grad hooks (bucket all-reduces) fire then
         defer = self.sync is not None or self.flat_grads is not None
+        # force steps: only the parameters are backward targets (the positions' second-order
+        # gradient terms are never formed)
+        inputs = self._train_params() if self.forces else None
         if self.sync is not None:
             self.sync.set_loss(loss)
             if sync:
                 self.sync.begin()
             with deferred_wgrad(defer):
-                loss.backward(self._seed(loss))
+                torch.autograd.backward(loss, self._seed(loss), inputs=inputs)
             self.sync.finish()
             return
         with deferred_wgrad(defer):
-            loss.backward(self._seed(loss))
+            torch.autograd.backward(loss, self._seed(loss), inputs=inputs)
         if self.flat_grads is not None:
             self.flat_grads.gather()
+
+    def _train_params(self):
+        ps = getattr(self, "_tparams", None)
+        if ps is None:
+            ps = self._tparams = [p for p in self.module.parameters() if p.requires_grad]
+        return ps
 
     def _seed(self, loss):
         """The backward seed d loss / d loss = 1 as a persistent tensor (an implicit seed is

@@ -192,3 +192,111 @@ def test_native_painn_force_step_equals_composite():
     assert gn.keys() == gr.keys()
     for k in gr:
         torch.testing.assert_close(gn[k], gr[k], rtol=1e-8, atol=1e-10, msg=k)
+
+
+def _emulate(ins, bufs, width, ptrs, N, mask):
+    """numpy model of csrc/rowprog.hip over the lowered tables (addressing + semantics)."""
+    ws = np.zeros(max(N * width, 1))
+
+    def opd(o):
+        b = o[0]
+        if b < 0:
+            return None
+        typ, idx, wr, ncr = bufs[b]
+        base = ws[idx * N: idx * N + N * wr * ncr] if typ == 0 else ptrs[idx]
+        return (base.reshape(N, ncr, wr), o[1], o[2], o[3])
+
+    def view(d):
+        arr, c0, w, nc = d
+        return arr[:, :, c0:c0 + w]
+
+    act = rp._act
+    for I in ins:
+        y = opd(I[5:9])
+        Y = view(y)
+        if I[0] == 1:
+            xs = [opd(I[9:13]), opd(I[13:17])]
+            W = ptrs[I[21]].reshape(-1, I[22])
+            r = 0
+            for x, k0 in zip(xs, (I[23], I[24])):
+                if x is None:
+                    continue
+                X = view(x)
+                if I[26]:
+                    r = r + np.einsum("nck,ok->nco", X, W[:, k0:k0 + X.shape[2]])
+                else:
+                    r = r + np.einsum("nco,ok->nck", X, W[:, k0:k0 + Y.shape[2]])
+            if I[25] >= 0:
+                r = r + ptrs[I[25]].reshape(1, 1, -1)
+            Y[...] = Y + r if I[4] else r
+            continue
+        op, arg, acc = I[1], I[2], I[4]
+        coef = np.array([I[3]], dtype=np.int32).view(np.float32)[0]
+        A, B, C = (view(d) if d is not None else None for d in (opd(I[9:13]), opd(I[13:17]), opd(I[17:21])))
+        if op == rp.E_ZERO:
+            Y[...] = 0
+            continue
+        if op == rp.E_COPY:
+            r = A
+        elif op == rp.E_MUL:
+            r = A * B
+        elif op == rp.E_MUL3:
+            r = A * B * C
+        elif op == rp.E_ACT:
+            r = act(torch.from_numpy(np.ascontiguousarray(A)), arg >> 2, arg & 3).numpy()
+            if B is not None:
+                r = r * B
+            if C is not None:
+                r = r * C
+        elif op == rp.E_DOT3:
+            r = (A * B).sum(1, keepdims=True)
+            if C is not None:
+                r = r * C
+        elif op == rp.E_NORM3:
+            r = np.sqrt((A * A).sum(1, keepdims=True))
+        elif op == rp.E_SINV:
+            r = np.where(A > 0, 1.0 / np.where(A > 0, A, 1.0), 0.0)
+        elif op == rp.E_MASK:
+            r = A * (mask.reshape(N, 1, 1) if mask is not None else 1.0)
+        r = np.broadcast_to(r * coef, Y.shape)
+        Y[...] = Y + r if acc else r
+    return ws
+
+
+@pytest.mark.parametrize("mode", ["fwd", "vjp_in", "vjp", "vvjp"])
+def test_rowprog_lowering_matches_twin(mode):
+    """The tables the interpreter kernel runs (rowprog.compile_device), executed by a numpy
+    model of the kernel, reproduce the torch twin of every program mode."""
+    F, Fo, N = 3, 4, 5
+    cp, shapes = _chain_prog(F, Fo, False, act="silu")
+    g = torch.Generator().manual_seed(5)
+    ws = [torch.randn(*sh, generator=g, dtype=DT) * 0.5 for sh in shapes]
+    xs = [torch.randn(N, F, generator=g, dtype=DT), torch.randn(N, 3, F, generator=g, dtype=DT)]
+    gouts = [torch.randn(N, o.nc * o.w, generator=g, dtype=DT) for o in cp.outs]
+    hins = [torch.randn_like(x) for x in xs]
+    mask = torch.tensor([1, 0, 1, 1, 1], dtype=DT)
+    feeds = dict(zip(cp.ins, xs))
+    if mode == "fwd":
+        prog, wanted = cp.prog, [o.base for o in cp.outs]
+    elif mode in ("vjp_in", "vjp"):
+        feeds.update(zip(cp.gouts, gouts))
+        res = cp.vjp_in_res if mode == "vjp_in" else cp.vjp_res
+        prog, wanted = (cp.vjp_in if mode == "vjp_in" else cp.vjp), [a.base for a in res.values() if a is not None]
+    else:
+        feeds.update(zip(cp.gouts, gouts))
+        feeds.update(zip(cp.hins, hins))
+        prog = cp.vvjp
+        wanted = [t for t in cp.touts if t is not None] + [a.base for a in cp.vvjp_res.values() if a is not None]
+    ext = list(feeds.keys()) + [v for v in wanted if v not in feeds]
+    ins, bufs, width, where = rp.compile_device(prog, ext, len(ws))
+    ptrs = [w.numpy().copy() for w in ws]
+    for v in ext:
+        t = feeds.get(v)
+        ptrs.append(t.reshape(N, -1).numpy().copy() if t is not None else np.zeros((N, v.nc * v.w)))
+    _emulate(ins, bufs, width, ptrs, N, mask.numpy())
+    cp.weights_t = ws
+    env, _ = pf._run(cp, prog, feeds, mask, N)
+    for k, v in enumerate(ext):
+        if v in feeds:
+            continue
+        np.testing.assert_allclose(ptrs[len(ws) + k], env[v.id].numpy(), rtol=1e-12, atol=1e-12)
