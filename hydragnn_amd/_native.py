@@ -50,6 +50,10 @@ class _SyncOps:
         op = getattr(self._ns, name)
 
         def run(*args, **kwargs):
+            if _TRACE:  # HYDRA_DEBUG_SYNC=2: name every native op (and its tensor shapes) before it launches
+                shapes = [tuple(a.shape) + ((str(a.dtype)[6:], tuple(a.stride())),) for a in args
+                          if isinstance(a, torch.Tensor)]
+                print(f"[hydra op] {name} {shapes}", flush=True)
             out = op(*args, **kwargs)
             if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
                 try:
@@ -61,8 +65,11 @@ class _SyncOps:
         return run
 
 
+_TRACE = os.environ.get("HYDRA_DEBUG_SYNC", "0") == "2"
+
+
 def debug_sync():
-    return os.environ.get("HYDRA_DEBUG_SYNC", "0") == "1"
+    return os.environ.get("HYDRA_DEBUG_SYNC", "0") in ("1", "2")
 
 
 def ops():

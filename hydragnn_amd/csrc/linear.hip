@@ -57,13 +57,17 @@ __device__ __forceinline__ void wg_load(const float* __restrict__ base, int ld, 
 
 // Same chunk staging through buffer loads whose descriptor covers exactly the slab's rows:
 // rows past the slab end read as zeros (hardware range check), columns past ncol read the
-// next row's values (or zeros past the buffer), which only feed output columns that are
-// never stored.  No select on loaded values: a select right after the load makes the
+// next row's values (or zeros past the slab's last valid element), which only feed output
+// columns that are never stored.  No select on loaded values: a select right after the load makes the
 // compiler wait for it there, serialising the next-chunk prefetch with this chunk's MFMAs.
 typedef __amdgpu_buffer_rsrc_t WgRsrc;
-__device__ __forceinline__ WgRsrc wg_rsrc(const float* base, int ld, int r0, int r1) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)r0 * ld), (short)0, max(r1 - r0, 0) * ld * 4,
-                                           0x00020000);
+// The range ends at the LAST row's last valid column (not after a full row stride): an
+// operand that is a column slice of a wider tensor (offset c0 > 0) would otherwise let the
+// over-wide tile reads of its last row run up to c0 floats past the end of the storage —
+// an unmapped page when the allocation ends there (observed: illegal address on MI355X).
+__device__ __forceinline__ WgRsrc wg_rsrc(const float* base, int ld, int r0, int r1, int ncols) {
+  const int n = r1 > r0 ? ((r1 - r0 - 1) * ld + ncols) * 4 : 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)r0 * ld), (short)0, n, 0x00020000);
 }
 template <bool VEC>
 __device__ __forceinline__ void wg_load_b(WgRsrc rs, int ld, int col0, int rrel, int t, float4 (&r)[2]) {
@@ -126,7 +130,7 @@ __device__ __forceinline__ void wgrad_partial_body(float4* smem, const float* __
       *reinterpret_cast<float4*>(Xs + (b * kWC + row) * kLdsW + c4) = rx[h];
     }
   };
-  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1, O), rsx = wg_rsrc(X, ldx, r0, r1, I);
   if (nch > 0) {
     wg_load_b<VY>(rsy, ldy, to0, 0, t, ry);
     wg_load_b<VX>(rsx, ldx, ti0, 0, t, rx);
@@ -204,7 +208,7 @@ __device__ __forceinline__ void wgrad_glds_body(float* lds, const float* __restr
   const int lane = t & 63, w = t >> 6, i = lane & 15, g = lane >> 4;
   const int ob = (w >> 1) * 32, ib = (w & 1) * 32;
   const bool bias_w = with_bias && ti0 == 0 && (w & 1) == 0;
-  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1, O), rsx = wg_rsrc(X, ldx, r0, r1, I);
   // this lane's source element in group w * 2 + j of a chunk: row 4 grp + lane / 16, 4 columns
   const int lr = lane >> 4, lc = (lane & 15) * 4;
   auto issue = [&](int c, int st) {
@@ -380,7 +384,7 @@ std::tuple<at::Tensor, at::Tensor> linear_wgrad(const at::Tensor& dY_, const at:
 // table) and ONE reduce launch sums the slab partials in a fixed order and writes or
 // accumulates into the gradient tensors.  Replaces 2 launches per linear (~33 pairs per
 // GPS+PNAPlus step) with 2 per step, and the merged grid fills the chip.
-constexpr int kWgMaxP = 40;  // 40 x 88 B of kernel arguments (< 4 KB)
+constexpr int kWgMaxP = 36;  // 36 x 96 B of kernel arguments + hidden arguments < 4 KB
 constexpr int kWgMaxSlabs = 64;
 
 struct WgProb {
@@ -433,7 +437,7 @@ __device__ __forceinline__ void wgrad_narrow_body(float4* smem, const float* __r
   for (int k = 0; k < kWgNarrow; ++k) acc[k] = 0.f;
   // buffer loads over exactly the slab's rows: rows past it read as zeros; X columns past I
   // (and dY columns past O) only feed outputs that are never stored (no selects on loads)
-  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1), rsx = wg_rsrc(X, ldx, r0, r1);
+  const WgRsrc rsy = wg_rsrc(dY, ldy, r0, r1, O), rsx = wg_rsrc(X, ldx, r0, r1, I);
   for (int c0 = r0; c0 < r1; c0 += 64) {
     __syncthreads();
 #pragma unroll

@@ -343,7 +343,7 @@ class _MsgBwd(torch.autograd.Function):
             out = _msg_vjp(cfg, Gs, Gv, v, phi, Bas, Un, W, b, need_w)
         if need_w:
             ctx.mark_non_differentiable(out[4], out[5])
-        return out
+        return tuple(out)
 
     @staticmethod
     def backward(ctx, Hv, Hphi, HBas, HUn, HW, Hb):

@@ -496,6 +496,9 @@ class TrainStep:
         """Warm up + capture one bucket.  Parameters, buffers and optimizer state are
         restored afterwards, so the warm-up iterations do not count as training steps."""
         torch.cuda.synchronize()
+        if store.dataset_name is not None:
+            # the warm-up must see the branch-grouped row order the replayed steps use
+            indices = store.branch_order(indices)[0]
         snap = self._snapshot()
         cap = _Captured()
         Np, Ep = key
