@@ -348,7 +348,12 @@ __device__ void wacc_store(const Rows<RM> (&A)[NC], int F, int R, float* __restr
   for (int k = threadIdx.x; k < n; k += 256) part[k] = lds[k];
 }
 
-// VJP over the dst-CSR: g_phi, g_v (= Gv + gather sums), g_basis, g_unit (+ W partials)
+// VJP over the dst-CSR: g_phi, g_v (= Gv + gather sums), g_basis, g_unit (+ W partials).
+// One wave per destination node; incoming edges in batches of kEB whose index / basis /
+// source-row loads are all issued before any of them is used (the per-edge dependent load
+// chain src -> Gv[src] was the whole cost: ~3 us per edge at one edge per step).
+constexpr int kEB = 4;
+
 template <int RM, int NC>
 __global__ void __launch_bounds__(256) msg_vjp_kernel(Msg M, const float* __restrict__ Gs,
                                                       const float* __restrict__ Gv, float* __restrict__ gphi,
@@ -357,7 +362,6 @@ __global__ void __launch_bounds__(256) msg_vjp_kernel(Msg M, const float* __rest
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int F = M.F, R1 = M.R + 1;
-  const int nodes_per_iter = gridDim.x * 4;
   Rows<RM> acc[NC], Wr[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -367,63 +371,86 @@ __global__ void __launch_bounds__(256) msg_vjp_kernel(Msg M, const float* __rest
       for (int r = 0; r < RM; ++r) acc[c].w[q][r] = 0.f;
     load_rows<RM>(M, min(lane + 64 * c, F - 1), Wr[c]);
   }
-  for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < M.N; j += nodes_per_iter) {
-    float aphi[NC][3], av[NC][3];
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j < M.N) {
+    float aphi[NC][3], av[NC][3], P[NC][3], V[NC][3];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
+    for (int c = 0; c < NC; ++c) {
+      const int f = min(lane + 64 * c, F - 1);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) aphi[c][q] = av[c][q] = 0.f;
-    const float* P = M.phi + (int64_t)j * 3 * F;
-    const float* V = M.v + (int64_t)j * 3 * F;
-    for (int p = M.din.ptr[j]; p < M.din.ptr[j + 1]; ++p) {
-      const int e = edge_at(M.din, p), n = M.src[e];
-      float bs[RM];
-      load_basis<RM>(M, M.basis + (int64_t)e * R1, bs);
-      const float* U = M.unit + 3 * (int64_t)e;
-      const float U0 = U[0], U1 = U[1], U2 = U[2];
-      float pb[RM], pu[3] = {0.f, 0.f, 0.f};
+      for (int q = 0; q < 3; ++q) {
+        aphi[c][q] = av[c][q] = 0.f;
+        P[c][q] = M.phi[(int64_t)j * 3 * F + q * F + f];
+        V[c][q] = M.v[(int64_t)j * 3 * F + q * F + f];
+      }
+    }
+    const int pb = M.din.ptr[j], pe = M.din.ptr[j + 1];
+    for (int p0 = pb; p0 < pe; p0 += kEB) {
+      int e[kEB], n[kEB];
+      float bs[kEB][RM], U[kEB][3], g[kEB][NC][4];
 #pragma unroll
-      for (int r = 0; r < RM; ++r) pb[r] = 0.f;
+      for (int b = 0; b < kEB; ++b) e[b] = edge_at(M.din, min(p0 + b, pe - 1));
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int f = lane + 64 * c;
-        if (f >= F) continue;
-        float w[3];
-        filt<RM>(Wr[c], bs, w);
-        const float* G = Gv + (int64_t)n * 3 * F;
-        const float g0 = G[f], g1 = G[F + f], g2 = G[2 * F + f];
-        const float go[3] = {g0 * V[f] + g1 * V[F + f] + g2 * V[2 * F + f], g0 * U0 + g1 * U1 + g2 * U2,
-                             Gs[(int64_t)n * F + f]};
-        const float Pv[3] = {P[f], P[F + f], P[2 * F + f]};
+      for (int b = 0; b < kEB; ++b) n[b] = M.src[e[b]];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) aphi[c][q] += go[q] * w[q];
-        const float ov = w[0] * Pv[0], oe = w[1] * Pv[1];
-        av[c][0] += g0 * ov;
-        av[c][1] += g1 * ov;
-        av[c][2] += g2 * ov;
-        pu[0] += g0 * oe;
-        pu[1] += g1 * oe;
-        pu[2] += g2 * oe;
+      for (int b = 0; b < kEB; ++b) {
+        load_basis<RM>(M, M.basis + (int64_t)e[b] * R1, bs[b]);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float gw = go[q] * Pv[q];
+        for (int q = 0; q < 3; ++q) U[b][q] = M.unit[3 * (int64_t)e[b] + q];
 #pragma unroll
-          for (int r = 0; r < RM; ++r) {
-            pb[r] += Wr[c].w[q][r] * gw;
-            acc[c].w[q][r] += gw * bs[r];
-          }
+        for (int c = 0; c < NC; ++c) {
+          const int f = min(lane + 64 * c, F - 1);
+          const float* G = Gv + (int64_t)n[b] * 3 * F;
+          g[b][c][0] = G[f];
+          g[b][c][1] = G[F + f];
+          g[b][c][2] = G[2 * F + f];
+          g[b][c][3] = Gs[(int64_t)n[b] * F + f];
         }
       }
 #pragma unroll
-      for (int r = 0; r < RM; ++r) {
-        if (r >= R1) continue;
-        const float t = wave_sum(pb[r]);
-        if (lane == 0) gbas[(int64_t)e * R1 + r] = t;
-      }
+      for (int b = 0; b < kEB; ++b) {
+        if (p0 + b >= pe) break;  // uniform
+        float pbv[RM], pu[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const float t = wave_sum(pu[q]);
-        if (lane == 0) gun[3 * (int64_t)e + q] = t;
+        for (int r = 0; r < RM; ++r) pbv[r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (lane + 64 * c >= F) continue;
+          float w[3];
+          filt<RM>(Wr[c], bs[b], w);
+          const float g0 = g[b][c][0], g1 = g[b][c][1], g2 = g[b][c][2];
+          const float go[3] = {g0 * V[c][0] + g1 * V[c][1] + g2 * V[c][2], g0 * U[b][0] + g1 * U[b][1] + g2 * U[b][2],
+                               g[b][c][3]};
+#pragma unroll
+          for (int q = 0; q < 3; ++q) aphi[c][q] += go[q] * w[q];
+          const float ov = w[0] * P[c][0], oe = w[1] * P[c][1];
+          av[c][0] += g0 * ov;
+          av[c][1] += g1 * ov;
+          av[c][2] += g2 * ov;
+          pu[0] += g0 * oe;
+          pu[1] += g1 * oe;
+          pu[2] += g2 * oe;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const float gw = go[q] * P[c][q];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+              pbv[r] += Wr[c].w[q][r] * gw;
+              acc[c].w[q][r] += gw * bs[b][r];
+            }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (r >= R1) continue;
+          const float t = wave_sum(pbv[r]);
+          if (lane == 0) gbas[(int64_t)e[b] * R1 + r] = t;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const float t = wave_sum(pu[q]);
+          if (lane == 0) gun[3 * (int64_t)e[b] + q] = t;
+        }
       }
     }
 #pragma unroll
@@ -544,7 +571,6 @@ __global__ void __launch_bounds__(256) msg_vvjp_dst_kernel(Msg M, Tan T, const f
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int F = M.F, R1 = M.R + 1;
-  const int nodes_per_iter = gridDim.x * 4;
   Rows<RM> acc[NC], Wr[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -554,90 +580,106 @@ __global__ void __launch_bounds__(256) msg_vvjp_dst_kernel(Msg M, Tan T, const f
       for (int r = 0; r < RM; ++r) acc[c].w[q][r] = 0.f;
     load_rows<RM>(M, min(lane + 64 * c, F - 1), Wr[c]);
   }
-  for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < M.N; j += nodes_per_iter) {
-    float aphi[NC][3], av[NC][3];
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j < M.N) {
+    float aphi[NC][3], av[NC][3], P[NC][3], HP[NC][3], V[NC][3], HV[NC][3];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
+    for (int c = 0; c < NC; ++c) {
+      const int f = min(lane + 64 * c, F - 1);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) aphi[c][q] = av[c][q] = 0.f;
-    const float* P = M.phi + (int64_t)j * 3 * F;
-    const float* V = M.v + (int64_t)j * 3 * F;
-    for (int p = M.din.ptr[j]; p < M.din.ptr[j + 1]; ++p) {
-      const int e = edge_at(M.din, p), n = M.src[e];
-      float bs[RM], hb[RM];
-      load_basis<RM>(M, M.basis + (int64_t)e * R1, bs);
-      if (T.Hbas)
-        load_basis<RM>(M, T.Hbas + (int64_t)e * R1, hb);
-      else
-#pragma unroll
-        for (int r = 0; r < RM; ++r) hb[r] = 0.f;
-      const float* U = M.unit + 3 * (int64_t)e;
-      const float U0 = U[0], U1 = U[1], U2 = U[2];
-      float HU0 = 0.f, HU1 = 0.f, HU2 = 0.f;
-      if (T.Hun) {
-        HU0 = T.Hun[3 * (int64_t)e];
-        HU1 = T.Hun[3 * (int64_t)e + 1];
-        HU2 = T.Hun[3 * (int64_t)e + 2];
+      for (int q = 0; q < 3; ++q) {
+        const int64_t o = (int64_t)j * 3 * F + q * F + f;
+        aphi[c][q] = av[c][q] = 0.f;
+        P[c][q] = M.phi[o];
+        V[c][q] = M.v[o];
+        HP[c][q] = T.Hphi ? T.Hphi[o] : 0.f;
+        HV[c][q] = T.Hv ? T.Hv[o] : 0.f;
       }
-      float pb[RM], pu[3] = {0.f, 0.f, 0.f};
+    }
+    const int pb = M.din.ptr[j], pe = M.din.ptr[j + 1];
+    for (int p0 = pb; p0 < pe; p0 += kEB) {
+      int e[kEB], n[kEB];
+      float bs[kEB][RM], hb[kEB][RM], U[kEB][3], HU[kEB][3], g[kEB][NC][4];
 #pragma unroll
-      for (int r = 0; r < RM; ++r) pb[r] = 0.f;
+      for (int b = 0; b < kEB; ++b) e[b] = edge_at(M.din, min(p0 + b, pe - 1));
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int f = lane + 64 * c;
-        if (f >= F) continue;
-        float w[3], wp[3];
-        filt<RM>(Wr[c], bs, w);
-        filt<RM>(Wr[c], hb, wp);
-        const float* G = Gv + (int64_t)n * 3 * F;
-        const float g0 = G[f], g1 = G[F + f], g2 = G[2 * F + f];
-        float HV0 = 0.f, HV1 = 0.f, HV2 = 0.f;
-        if (T.Hv) {
-          const float* HV = T.Hv + (int64_t)j * 3 * F;
-          HV0 = HV[f];
-          HV1 = HV[F + f];
-          HV2 = HV[2 * F + f];
-        }
-        const float a[3] = {g0 * HV0 + g1 * HV1 + g2 * HV2, g0 * HU0 + g1 * HU1 + g2 * HU2, 0.f};
-        const float bb[3] = {g0 * V[f] + g1 * V[F + f] + g2 * V[2 * F + f], g0 * U0 + g1 * U1 + g2 * U2,
-                             Gs[(int64_t)n * F + f]};
-        float Pv[3], HP[3], op[3];
+      for (int b = 0; b < kEB; ++b) n[b] = M.src[e[b]];
+#pragma unroll
+      for (int b = 0; b < kEB; ++b) {
+        load_basis<RM>(M, M.basis + (int64_t)e[b] * R1, bs[b]);
+        if (T.Hbas)
+          load_basis<RM>(M, T.Hbas + (int64_t)e[b] * R1, hb[b]);
+        else
+#pragma unroll
+          for (int r = 0; r < RM; ++r) hb[b][r] = 0.f;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          Pv[q] = P[q * F + f];
-          HP[q] = T.Hphi ? T.Hphi[(int64_t)j * 3 * F + q * F + f] : 0.f;
-          op[q] = wp[q] * Pv[q] + w[q] * HP[q];
-          aphi[c][q] += a[q] * w[q] + bb[q] * wp[q];
+          U[b][q] = M.unit[3 * (int64_t)e[b] + q];
+          HU[b][q] = T.Hun ? T.Hun[3 * (int64_t)e[b] + q] : 0.f;
         }
-        av[c][0] += g0 * op[0];
-        av[c][1] += g1 * op[0];
-        av[c][2] += g2 * op[0];
-        pu[0] += g0 * op[1];
-        pu[1] += g1 * op[1];
-        pu[2] += g2 * op[1];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float gw2 = a[q] * Pv[q] + bb[q] * HP[q], bP = bb[q] * Pv[q];
+        for (int c = 0; c < NC; ++c) {
+          const int f = min(lane + 64 * c, F - 1);
+          const float* G = Gv + (int64_t)n[b] * 3 * F;
+          g[b][c][0] = G[f];
+          g[b][c][1] = G[F + f];
+          g[b][c][2] = G[2 * F + f];
+          g[b][c][3] = Gs[(int64_t)n[b] * F + f];
+        }
+      }
 #pragma unroll
-          for (int r = 0; r < RM; ++r) {
-            pb[r] += Wr[c].w[q][r] * gw2;
-            acc[c].w[q][r] += gw2 * bs[r] + bP * hb[r];
+      for (int b = 0; b < kEB; ++b) {
+        if (p0 + b >= pe) break;  // uniform
+        float pbv[RM], pu[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RM; ++r) pbv[r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (lane + 64 * c >= F) continue;
+          float w[3], wp[3];
+          filt<RM>(Wr[c], bs[b], w);
+          filt<RM>(Wr[c], hb[b], wp);
+          const float g0 = g[b][c][0], g1 = g[b][c][1], g2 = g[b][c][2];
+          const float a[3] = {g0 * HV[c][0] + g1 * HV[c][1] + g2 * HV[c][2],
+                              g0 * HU[b][0] + g1 * HU[b][1] + g2 * HU[b][2], 0.f};
+          const float bb[3] = {g0 * V[c][0] + g1 * V[c][1] + g2 * V[c][2], g0 * U[b][0] + g1 * U[b][1] + g2 * U[b][2],
+                               g[b][c][3]};
+          float op[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            op[q] = wp[q] * P[c][q] + w[q] * HP[c][q];
+            aphi[c][q] += a[q] * w[q] + bb[q] * wp[q];
+          }
+          av[c][0] += g0 * op[0];
+          av[c][1] += g1 * op[0];
+          av[c][2] += g2 * op[0];
+          pu[0] += g0 * op[1];
+          pu[1] += g1 * op[1];
+          pu[2] += g2 * op[1];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const float gw2 = a[q] * P[c][q] + bb[q] * HP[c][q], bP = bb[q] * P[c][q];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+              pbv[r] += Wr[c].w[q][r] * gw2;
+              acc[c].w[q][r] += gw2 * bs[b][r] + bP * hb[b][r];
+            }
           }
         }
+        if (gbas)
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            if (r >= R1) continue;
+            const float t = wave_sum(pbv[r]);
+            if (lane == 0) gbas[(int64_t)e[b] * R1 + r] = t;
+          }
+        if (gun)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const float t = wave_sum(pu[q]);
+            if (lane == 0) gun[3 * (int64_t)e[b] + q] = t;
+          }
       }
-      if (gbas)
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
-          if (r >= R1) continue;
-          const float t = wave_sum(pb[r]);
-          if (lane == 0) gbas[(int64_t)e * R1 + r] = t;
-        }
-      if (gun)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float t = wave_sum(pu[q]);
-          if (lane == 0) gun[3 * (int64_t)e + q] = t;
-        }
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -746,7 +788,7 @@ pf::Msg msg(const at::Tensor& s, const at::Tensor& v, const at::Tensor& phi, con
   } while (0)
 
 int grid_nodes(int64_t N) { return std::max(1, ceil_div(N, 4)); }
-int grid_stride(int64_t N) { return std::max(1, std::min(ceil_div(N, 4), 128)); }
+int grid_stride(int64_t N) { return std::max(1, ceil_div(N, 4)); }  // one node per wave
 size_t wlds(int64_t F, int64_t R) { return (size_t)3 * F * (R + 1) * sizeof(float); }
 }  // namespace
 

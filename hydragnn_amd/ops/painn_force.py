@@ -414,11 +414,16 @@ def _device(t):
 class _DevMode:
     """One program lowered for the interpreter: tables on the device + external roots."""
 
-    def __init__(self, prog, ext_roots, n_weights, wg, dev):
-        ins, bufs, width, where = rp.compile_device(prog, ext_roots, n_weights)
+    def __init__(self, prog, ext_roots, inputs, n_weights, wg, dev):
+        keep = []
+        for rec in (wg or []):
+            keep += [rec[3].base, rec[4].base] if rec[0] == "w" else [rec[2].base]
+        ins, bufs, width, lds_w, where = rp.compile_device(prog, ext_roots, n_weights, inputs=inputs,
+                                                           keep_global=keep)
         self.ins = torch.from_numpy(ins).to(dev)
         self.bufs = torch.from_numpy(bufs).to(dev)
         self.width = width
+        self.lds_w = lds_w
         self.where = where
         self.bufs_np = bufs
         self.ext = list(ext_roots)
@@ -432,22 +437,26 @@ def _dev_mode(cp, mode, dev):
         nW = len(cp.weights)
         if mode == "fwd":
             prog, ext, wg = cp.prog, cp.ins + [o.base for o in cp.outs], None
+            inputs = cp.ins
         elif mode == "vjp_in":
             prog, wg = cp.vjp_in, None
             ext = cp.ins + cp.gouts + [a.base for a in cp.vjp_in_res.values() if a is not None]
+            inputs = cp.ins + cp.gouts
         elif mode == "vjp":
             prog, wg = cp.vjp, cp.vjp_wg
             ext = cp.ins + cp.gouts + [a.base for a in cp.vjp_res.values() if a is not None]
+            inputs = cp.ins + cp.gouts
         else:
             prog, wg = cp.vvjp, cp.vvjp_wg
             ext = cp.ins + cp.hins + cp.gouts + [t for t in cp.touts if t is not None] + \
                 [a.base for a in cp.vvjp_res.values() if a is not None]
+            inputs = cp.ins + cp.hins + cp.gouts
         seen, uniq = set(), []
         for v in ext:
             if v.id not in seen:
                 seen.add(v.id)
                 uniq.append(v)
-        dm = _DevMode(prog, uniq, nW, wg, dev)
+        dm = _DevMode(prog, uniq, inputs, nW, wg, dev)
         cp.dev[key] = dm
     return dm
 
@@ -471,7 +480,7 @@ def _dev_exec(cp, mode, N, mask, feeds, ws):
         tens[v.id] = t
         ptrs.append(t)
     wsb = torch.empty(max(N * dm.width, 1), device=x0.device, dtype=torch.float32)
-    _native.ops().rowprog_run(dm.ins, dm.bufs, wsb, mask, ptrs, N)
+    _native.ops().rowprog_run(dm.ins, wsb, mask, ptrs, N, dm.lds_w)
 
     def get(v):
         b = v.base
@@ -479,6 +488,7 @@ def _dev_exec(cp, mode, N, mask, feeds, ws):
             t = tens[b.id]
         else:
             k = dm.where[b.id]
+            assert int(dm.bufs_np[k][0]) in (rp.B_WS, rp.B_LDS_WS), f"{b} has no global home"
             off = int(dm.bufs_np[k][1]) * N
             t = wsb[off:off + N * b.nc * b.w].view(N, b.nc * b.w)
         if v.full:

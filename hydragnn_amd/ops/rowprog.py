@@ -619,41 +619,146 @@ def wgrads_torch(wg, env, N, weights, grads):
 
 
 # ----------------------------------------------------------------------------- device compile
-INS_INTS = 32
+INS_INTS = 64
+OPD_INTS = 12  # per operand: present, global kind, global index, gld, LDS offset, lld, cs, c0, w, nc
 
 
-def compile_device(prog, ext_roots, n_weights):
+LDS_FLOATS = 160 * 1024 // 4  # one workgroup per CU may take all of it
+BUF_INTS = 6
+# buffer kinds of the interpreter: global workspace, external pointer, LDS only,
+# LDS + global-workspace mirror, LDS + external-pointer mirror
+B_WS, B_PTR, B_LDS, B_LDS_WS, B_LDS_PTR = range(5)
+
+
+def _substitute(prog, old_root, new_root):
+    """Reads of ``old_root`` (and its slices) -> ``new_root`` in a copy of the instruction list."""
+    def sub(v):
+        if v is None or v.base is not old_root:
+            return v
+        return new_root if v.full else new_root.slice(v.c0, v.w)
+
+    out = []
+    for ins in prog:
+        if ins[0] == "lin":
+            _, y, xs, trans, bias, acc = ins
+            out.append(("lin", y, [(sub(x), W, k0) for x, W, k0 in xs], trans, bias, acc))
+        else:
+            _, op, y, a, b, c, arg, coef, acc = ins
+            out.append(("ew", op, y, sub(a), sub(b), sub(c), arg, coef, acc))
+    return out
+
+
+def compile_device(prog, ext_roots, n_weights, inputs=(), keep_global=(), lds_budget=None):
     """Lower ``prog`` to the interpreter's tables (csrc/rowprog.hip).
 
     ext_roots: root Vals held in external tensors, in pointer-table order after the
-    ``n_weights`` weight pointers.  Every other root the program touches is a workspace
-    slot.  Returns (ins int32 [n, INS_INTS], bufs int32 [nb, 4], ws width per row,
-    {root id: (kind, index)})."""
+    ``n_weights`` weight pointers.  ``inputs`` (ext roots the program only reads) are staged
+    into LDS by a copy right before their first use; every value lives in the workgroup's
+    LDS for its live range (first-fit by liveness), mirrored to its global home when it is
+    an external output or ``keep_global`` (read later by the weight-gradient launch).
+    Values that do not fit stay in the global workspace.  Returns (ins int32 [n, INS_INTS],
+    bufs int32 [nb, BUF_INTS], global workspace floats per row, LDS floats per row,
+    {root id: buffer index})."""
     import numpy as np
 
     ext = {v.id: k for k, v in enumerate(ext_roots)}
+    inp = {v.id for v in inputs}
+    keep = {v.id for v in keep_global}
+    ins_list = list(prog.ins)
+    if lds_budget is None:
+        # floats per row of the 16-row block; the program itself (+ staged copies) is staged
+        # into LDS too: reserve room for it (ints, generous for the input copies)
+        lds_budget = max(0, (LDS_FLOATS - (len(ins_list) + 16) * INS_INTS) // 16)
+    # stage read-only external inputs through LDS
+    shadows = {}
+    for v in ext_roots:
+        if v.id not in inp:
+            continue
+        first = None
+        for k, ins in enumerate(ins_list):
+            if any(t.base is v for t in _reads(ins)):
+                first = k
+                break
+        if first is None:
+            continue
+        sh = Val(v.w, v.nc, name=f"lds({v.name})")
+        rest = _substitute(ins_list[first:], v, sh)
+        ins_list = ins_list[:first] + [("ew", E_COPY, sh, v, None, None, 0, 1.0, False)] + rest
+        shadows[sh.id] = v.id
+    # liveness of every root (first write .. last read)
+    first_w, last_r, roots = {}, {}, {}
+    for k, ins in enumerate(ins_list):
+        y = _writes(ins).base
+        roots[y.id] = y
+        first_w.setdefault(y.id, k)
+        last_r.setdefault(y.id, k)
+        for t in _reads(ins):
+            roots[t.base.id] = t.base
+            last_r[t.base.id] = max(last_r.get(t.base.id, k), k)
+    # first-fit LDS allocation in instruction order (a slot is reused only after its last
+    # reader finished: instructions are separated by a barrier)
+    lds_off, free, top = {}, [], 0
+    active = []
+    for k, ins in enumerate(ins_list):
+        still = []
+        for rid, off, size in active:
+            if last_r[rid] < k:
+                free.append((off, size))
+            else:
+                still.append((rid, off, size))
+        active = still
+        y = _writes(ins).base
+        if y.id in lds_off or first_w[y.id] != k:
+            continue  # a value gets its LDS slot at its first write, or never
+        size = y.nc * y.w + 1  # odd row stride: MFMA A-operand reads hit distinct banks
+        free.sort()
+        slot = None
+        for q, (off, sz) in enumerate(free):
+            if sz >= size:
+                slot = off
+                free[q] = (off + size, sz - size)
+                if free[q][1] == 0:
+                    free.pop(q)
+                break
+        if slot is None and top + size <= lds_budget:
+            slot = top
+            top += size
+        if slot is not None:
+            lds_off[y.id] = slot
+            active.append((y.id, slot, size))
     bufs, where = [], {}
     prefix = [0]
 
     def buf(v):
         b = v.base
-        if b.id not in where:
-            if b.id in ext:
-                where[b.id] = len(bufs)
-                bufs.append((1, n_weights + ext[b.id], b.w, b.nc))
-            else:
-                where[b.id] = len(bufs)
-                bufs.append((0, prefix[0], b.w, b.nc))
-                prefix[0] += b.w * b.nc
+        if b.id in where:
+            return where[b.id]
+        lo = lds_off.get(b.id, -1)
+        if b.id in ext:
+            kind = B_PTR if lo < 0 else B_LDS_PTR
+            g = n_weights + ext[b.id]
+        elif lo >= 0 and b.id not in keep:
+            kind, g = B_LDS, 0
+        else:
+            kind = B_WS if lo < 0 else B_LDS_WS
+            g = prefix[0]
+            prefix[0] += b.w * b.nc
+        where[b.id] = len(bufs)
+        bufs.append((kind, g, b.w, b.nc, lo, 0))
         return where[b.id]
 
     def opnd(v):
+        """Operand descriptor embedded in the instruction (no table lookup on the device):
+        [present, global kind (0 none, 1 workspace, 2 pointer), global index, global row
+        stride, LDS offset (-1 none), LDS row stride, component stride, c0, w, nc]."""
         if v is None:
-            return [-1, 0, 0, 0]
-        return [buf(v), v.c0, v.w, v.nc]
+            return [0] * OPD_INTS
+        kind, g, w, nc, lo, _ = bufs[buf(v)]
+        gk = {B_WS: 1, B_LDS_WS: 1, B_PTR: 2, B_LDS_PTR: 2}.get(kind, 0)
+        return [1, gk, g if gk else 0, nc * w, lo, nc * w + 1, w, v.c0, v.w, v.nc, 0, 0]
 
     rows = []
-    for ins in prog.ins:
+    for ins in ins_list:
         r = [0] * INS_INTS
         if ins[0] == "lin":
             _, y, xs, trans, bias, acc = ins
@@ -661,26 +766,23 @@ def compile_device(prog, ext_roots, n_weights):
             W = xs[0][1]
             assert all(t[1] is W for t in xs), "K blocks of one LIN share one weight"
             r[0], r[4] = 1, int(acc)
-            r[5:9] = opnd(y)
-            r[9:13] = opnd(xs[0][0])
-            r[13:17] = opnd(xs[1][0] if len(xs) > 1 else None)
-            r[21], r[22] = W.pid, W.K
-            r[23] = xs[0][2]
-            r[24] = xs[1][2] if len(xs) > 1 else 0
-            r[25] = bias if bias is not None else -1
-            r[26] = int(trans)
+            ops_ = [y, xs[0][0], xs[1][0] if len(xs) > 1 else None, None]
+            r[56], r[57] = W.pid, W.K
+            r[58] = xs[0][2]
+            r[59] = xs[1][2] if len(xs) > 1 else 0
+            r[60] = bias if bias is not None else -1
+            r[61] = int(trans)
         else:
             _, op, y, a, b, c, arg, coef, acc = ins
             r[0], r[1], r[2] = 0, op, arg
             r[3] = int(np.array([coef], dtype=np.float32).view(np.int32)[0])
             r[4] = int(acc)
-            r[5:9] = opnd(y)
-            r[9:13] = opnd(a)
-            r[13:17] = opnd(b)
-            r[17:21] = opnd(c)
+            ops_ = [y, a, b, c]
+        for q, v in enumerate(ops_):
+            r[8 + OPD_INTS * q: 8 + OPD_INTS * (q + 1)] = opnd(v)
         rows.append(r)
     ins = np.asarray(rows, dtype=np.int32).reshape(-1, INS_INTS)
-    return ins, np.asarray(bufs, dtype=np.int32).reshape(-1, 4), prefix[0], where
+    return ins, np.asarray(bufs, dtype=np.int32).reshape(-1, BUF_INTS), prefix[0], top, where
 
 
 def wgrad_rounds(wg):

@@ -194,47 +194,63 @@ def test_native_painn_force_step_equals_composite():
         torch.testing.assert_close(gn[k], gr[k], rtol=1e-8, atol=1e-10, msg=k)
 
 
-def _emulate(ins, bufs, width, ptrs, N, mask):
-    """numpy model of csrc/rowprog.hip over the lowered tables (addressing + semantics)."""
+def _emulate(ins, bufs, width, ptrs, N, mask, lds_w=0):
+    """numpy model of csrc/rowprog.hip over the lowered instructions (embedded operand
+    descriptors; the LDS of all row blocks modelled as one [N, lds_w] array, values with a
+    global home written to both)."""
     ws = np.zeros(max(N * width, 1))
+    lds = np.full((N, max(lds_w, 1)), np.nan)  # unwritten LDS reads poison the results
+    O = rp.OPD_INTS
 
-    def opd(o):
-        b = o[0]
-        if b < 0:
+    def opd(I, q):
+        d = I[8 + O * q: 8 + O * (q + 1)]
+        if not d[0]:
             return None
-        typ, idx, wr, ncr = bufs[b]
-        base = ws[idx * N: idx * N + N * wr * ncr] if typ == 0 else ptrs[idx]
-        return (base.reshape(N, ncr, wr), o[1], o[2], o[3])
+        _, gk, gi, gld, lo, lld, cs, c0, w, nc = d[:10]
+        ncr = gld // cs
+        g = None
+        if gk == 1:
+            g = ws[gi * N: gi * N + N * gld].reshape(N, ncr, cs)
+        elif gk == 2:
+            g = ptrs[gi].reshape(N, ncr, cs)
+        loc = lds[:, lo:lo + gld].reshape(N, ncr, cs) if lo >= 0 else None
+        return (loc if loc is not None else g, c0, w, nc, g if loc is not None else None)
 
     def view(d):
-        arr, c0, w, nc = d
+        arr, c0, w, nc, _ = d
         return arr[:, :, c0:c0 + w]
+
+    def mirror(d):
+        if d[4] is not None:
+            d[4][:, :, d[1]:d[1] + d[2]] = d[0][:, :, d[1]:d[1] + d[2]]
 
     act = rp._act
     for I in ins:
-        y = opd(I[5:9])
+        y = opd(I, 0)
         Y = view(y)
         if I[0] == 1:
-            xs = [opd(I[9:13]), opd(I[13:17])]
-            W = ptrs[I[21]].reshape(-1, I[22])
+            xs = [opd(I, 1), opd(I, 2)]
+            W = ptrs[I[56]].reshape(-1, I[57])
             r = 0
-            for x, k0 in zip(xs, (I[23], I[24])):
+            for x, k0 in zip(xs, (I[58], I[59])):
                 if x is None:
                     continue
                 X = view(x)
-                if I[26]:
+                if I[61]:
                     r = r + np.einsum("nck,ok->nco", X, W[:, k0:k0 + X.shape[2]])
                 else:
                     r = r + np.einsum("nco,ok->nck", X, W[:, k0:k0 + Y.shape[2]])
-            if I[25] >= 0:
-                r = r + ptrs[I[25]].reshape(1, 1, -1)
+            if I[60] >= 0:
+                r = r + ptrs[I[60]].reshape(1, 1, -1)
             Y[...] = Y + r if I[4] else r
+            mirror(y)
             continue
         op, arg, acc = I[1], I[2], I[4]
         coef = np.array([I[3]], dtype=np.int32).view(np.float32)[0]
-        A, B, C = (view(d) if d is not None else None for d in (opd(I[9:13]), opd(I[13:17]), opd(I[17:21])))
+        A, B, C = (view(d) if d is not None else None for d in (opd(I, 1), opd(I, 2), opd(I, 3)))
         if op == rp.E_ZERO:
             Y[...] = 0
+            mirror(y)
             continue
         if op == rp.E_COPY:
             r = A
@@ -260,11 +276,13 @@ def _emulate(ins, bufs, width, ptrs, N, mask):
             r = A * (mask.reshape(N, 1, 1) if mask is not None else 1.0)
         r = np.broadcast_to(r * coef, Y.shape)
         Y[...] = Y + r if acc else r
+        mirror(y)
     return ws
 
 
+@pytest.mark.parametrize("budget", [2400, 40, 0])
 @pytest.mark.parametrize("mode", ["fwd", "vjp_in", "vjp", "vvjp"])
-def test_rowprog_lowering_matches_twin(mode):
+def test_rowprog_lowering_matches_twin(mode, budget):
     """The tables the interpreter kernel runs (rowprog.compile_device), executed by a numpy
     model of the kernel, reproduce the torch twin of every program mode."""
     F, Fo, N = 3, 4, 5
@@ -288,12 +306,13 @@ def test_rowprog_lowering_matches_twin(mode):
         prog = cp.vvjp
         wanted = [t for t in cp.touts if t is not None] + [a.base for a in cp.vvjp_res.values() if a is not None]
     ext = list(feeds.keys()) + [v for v in wanted if v not in feeds]
-    ins, bufs, width, where = rp.compile_device(prog, ext, len(ws))
+    ins, bufs, width, lds_w, where = rp.compile_device(prog, ext, len(ws), inputs=list(feeds.keys()),
+                                                       lds_budget=budget)
     ptrs = [w.numpy().copy() for w in ws]
     for v in ext:
         t = feeds.get(v)
         ptrs.append(t.reshape(N, -1).numpy().copy() if t is not None else np.zeros((N, v.nc * v.w)))
-    _emulate(ins, bufs, width, ptrs, N, mask.numpy())
+    _emulate(ins, bufs, width, ptrs, N, mask.numpy(), lds_w)
     cp.weights_t = ws
     env, _ = pf._run(cp, prog, feeds, mask, N)
     for k, v in enumerate(ext):
