@@ -21,6 +21,8 @@
 // (linear.hip linear_wgrad_grouped) over all of them.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace hy {
 namespace rpg {
 
@@ -30,7 +32,6 @@ constexpr int kMaxPtr = 48;
 constexpr int kInsInts = 64;
 constexpr int kOpdInts = 12;
 constexpr int kBM = 16;         // rows per workgroup (one per wave for element-wise work)
-constexpr int kThreads = 1024;  // 16 waves: every 16x16 output tile of a LIN in flight at once
 
 enum { E_COPY = 0, E_MUL, E_MUL3, E_ACT, E_DOT3, E_NORM3, E_SINV, E_MASK, E_ZERO };
 
@@ -41,8 +42,16 @@ struct Args {
   int lds_w;       // LDS floats per row
   float* ws;
   const float* mask;  // [N] 0/1 or null
+  long long* dbg;     // optional per-instruction cycle stamps of workgroup 0 (profiling)
   float* p[kMaxPtr];
 };
+
+// explicit address spaces: pointers that come out of the kernel-argument table are generic
+// to the compiler, and generic accesses become FLAT instructions (global-like latency even
+// for LDS, and both wait counters)
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(3))) float lfloat;
+__device__ __forceinline__ gfloat* G(const float* p) { return (gfloat*)(p); }
 
 // operand: LDS part (int offsets into the block's LDS: ds_read / ds_write) and/or a global
 // home (absolute rows)
@@ -51,33 +60,46 @@ struct Opd {
   int loff, lld, gld, cs, c0, w, nc;
 };
 
-__device__ __forceinline__ Opd opd(const Args& A, const int* o) {
+// An instruction lives in one VGPR: lane t holds field t.  Fields are broadcast to SGPRs
+// (v_readlane) at their use, not all 64 up front (that spilled SGPRs into VGPR lanes).
+struct Ins {
+  int v;
+  __device__ __forceinline__ int operator[](int t) const { return __builtin_amdgcn_readlane(v, t); }
+};
+
+__device__ __forceinline__ Opd opd(const Args& A, const Ins& I, int o) {
   Opd d;
-  d.nc = o[0] ? o[9] : 0;
-  d.gb = o[1] == 1 ? A.ws + (int64_t)o[2] * A.N : (o[1] == 2 ? A.p[o[2]] : nullptr);
-  d.gld = o[3];
-  d.loff = o[4];
-  d.lld = o[5];
-  d.cs = o[6];
-  d.c0 = o[7];
-  d.w = o[8];
+  d.nc = I[o] ? I[o + 9] : 0;
+  const int gk = I[o + 1];
+  d.gb = gk == 1 ? A.ws + (int64_t)I[o + 2] * A.N : (gk == 2 ? A.p[I[o + 2]] : nullptr);
+  d.gld = I[o + 3];
+  d.loff = I[o + 4];
+  d.lld = I[o + 5];
+  d.cs = I[o + 6];
+  d.c0 = I[o + 7];
+  d.w = I[o + 8];
   return d;
 }
 
-__device__ __forceinline__ float rd(const float* smem, const Opd& d, int i, int row, int c, int f) {
+// The two homes are read by DIFFERENT instructions: a plain ternary lets the compiler select
+// the address and issue one FLAT load, which waits like a global load even when it hits LDS
+// (measured ~2 us per element-wise instruction); the global path is a non-temporal load,
+// which cannot be merged with the ds_read.
+__device__ __forceinline__ float rd(lfloat* smem, const Opd& d, int i, int row, int c, int f) {
   const int o = (d.nc == 1 ? 0 : c) * d.cs + d.c0 + f;
-  return d.loff >= 0 ? smem[kBM * d.loff + i * d.lld + o] : d.gb[(int64_t)row * d.gld + o];
+  if (d.loff >= 0) return smem[kBM * d.loff + i * d.lld + o];
+  return G(d.gb)[(int64_t)row * d.gld + o];
 }
 
-__device__ __forceinline__ void wr(float* smem, const Opd& d, int i, int row, int c, int f, float v, int acc) {
+__device__ __forceinline__ void wr(lfloat* smem, const Opd& d, int i, int row, int c, int f, float v, int acc) {
   const int o = c * d.cs + d.c0 + f;
   if (d.loff >= 0) {
-    float& p = smem[kBM * d.loff + i * d.lld + o];
+    lfloat& p = smem[kBM * d.loff + i * d.lld + o];
     v = acc ? p + v : v;
     p = v;
-    if (d.gb) d.gb[(int64_t)row * d.gld + o] = v;
+    if (d.gb) G(d.gb)[(int64_t)row * d.gld + o] = v;
   } else {
-    float* p = d.gb + (int64_t)row * d.gld + o;
+    gfloat* p = G(d.gb) + (int64_t)row * d.gld + o;
     *p = acc ? *p + v : v;
   }
 }
@@ -112,71 +134,199 @@ __device__ __forceinline__ float act(int kind, int order, float x) {
   }
 }
 
-__device__ void run_ew(const Args& A, const int* I, int r0, float* smem) {
-  const int op = I[1], arg = I[2], acc = I[4];
-  const float coef = __int_as_float(I[3]);
-  const Opd y = opd(A, I + 8), a = opd(A, I + 8 + kOpdInts), b = opd(A, I + 8 + 2 * kOpdInts),
-            c = opd(A, I + 8 + 3 * kOpdInts);
-  const int ync = (op == E_DOT3 || op == E_NORM3) ? 1 : y.nc;
-  const int i = threadIdx.x >> 6, lane = threadIdx.x & 63, row = r0 + i;  // one row per wave
-  if (row >= A.N) return;
-  for (int cc = 0; cc < ync; ++cc)
-    for (int f = lane; f < y.w; f += 64) {
-      float r;
-      switch (op) {
-        case E_ZERO: r = 0.f; break;
-        case E_COPY: r = rd(smem, a, i, row, cc, f); break;
-        case E_MUL: r = rd(smem, a, i, row, cc, f) * rd(smem, b, i, row, cc, f); break;
-        case E_MUL3: r = rd(smem, a, i, row, cc, f) * rd(smem, b, i, row, cc, f) * rd(smem, c, i, row, cc, f); break;
-        case E_ACT: {
-          r = act(arg >> 2, arg & 3, rd(smem, a, i, row, cc, f));
-          if (b.nc) r *= rd(smem, b, i, row, cc, f);
-          if (c.nc) r *= rd(smem, c, i, row, cc, f);
-          break;
-        }
-        case E_DOT3: {
+// element-wise instruction: the opcode (and activation kind/order) dispatch happens ONCE
+// per instruction, outside the element loop; FAST = every operand is an LDS value (the
+// lowering guarantees it whenever the values fit), so the element loop has no home checks.
+struct LOpd {  // LDS-only operand view
+  int base, lld, cs, c0, nc;
+};
+__device__ __forceinline__ LOpd lopd(const Opd& d) { return LOpd{kBM * d.loff + d.c0, d.lld, d.cs, d.c0, d.nc}; }
+__device__ __forceinline__ float lrd(const lfloat* smem, const LOpd& d, int i, int c, int f) {
+  return smem[d.base + i * d.lld + (d.nc == 1 ? 0 : c) * d.cs + f];
+}
+
+template <int OP, int KIND, int ORD>
+__device__ __forceinline__ float ew_op(float a, float b, float c, bool hb, bool hc) {
+  if constexpr (OP == E_COPY) return a;
+  if constexpr (OP == E_MUL) return a * b;
+  if constexpr (OP == E_MUL3) return a * b * c;
+  if constexpr (OP == E_SINV) return a > 0.f ? 1.f / a : 0.f;
+  if constexpr (OP == E_ACT) {
+    float r = act(KIND, ORD, a);
+    if (hb) r *= b;
+    if (hc) r *= c;
+    return r;
+  }
+  return 0.f;
+}
+
+template <int NT, int OP, int KIND, int ORD>
+__device__ void ew_fast(const Args& A, const Opd& y, const Opd& a, const Opd& b, const Opd& c, float coef, int acc,
+                        int r0, lfloat* smem) {
+  const int lane = threadIdx.x & 63;
+  const LOpd la = lopd(a), lb = lopd(b), lc = lopd(c);
+  const bool hb = b.nc != 0, hc = c.nc != 0;
+  const int ync = (OP == E_DOT3 || OP == E_NORM3) ? 1 : y.nc;
+  const int ybase = kBM * y.loff + y.c0;
+  for (int i = threadIdx.x >> 6; i < kBM; i += NT / 64) {
+    const int row = r0 + i;
+    if (row >= A.N) break;
+    const float m = (OP == E_MASK) ? (A.mask ? G(A.mask)[row] : 1.f) : 1.f;
+    for (int cc = 0; cc < ync; ++cc)
+      for (int f = lane; f < y.w; f += 64) {
+        float r;
+        if constexpr (OP == E_ZERO) {
+          r = 0.f;
+        } else if constexpr (OP == E_DOT3) {
           r = 0.f;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) r += rd(smem, a, i, row, q, f) * rd(smem, b, i, row, q, f);
-          if (c.nc) r *= rd(smem, c, i, row, 0, f);
-          break;
-        }
-        case E_NORM3: {
+          for (int q = 0; q < 3; ++q) r += lrd(smem, la, i, q, f) * lrd(smem, lb, i, q, f);
+          if (hc) r *= lrd(smem, lc, i, 0, f);
+          r *= coef;
+        } else if constexpr (OP == E_NORM3) {
           float s2 = 0.f;
 #pragma unroll
           for (int q = 0; q < 3; ++q) {
-            const float v = rd(smem, a, i, row, q, f);
+            const float v = lrd(smem, la, i, q, f);
             s2 += v * v;
           }
-          r = sqrtf(s2);
-          break;
+          r = sqrtf(s2) * coef;
+        } else if constexpr (OP == E_MASK) {
+          r = lrd(smem, la, i, cc, f) * m * coef;
+        } else {
+          const float va = lrd(smem, la, i, cc, f);
+          const float vb = (OP == E_MUL || OP == E_MUL3 || hb) ? lrd(smem, lb, i, cc, f) : 0.f;
+          const float vc = (OP == E_MUL3 || hc) ? lrd(smem, lc, i, cc, f) : 0.f;
+          r = ew_op<OP, KIND, ORD>(va, vb, vc, hb, hc) * coef;
         }
-        case E_SINV: {
-          const float v = rd(smem, a, i, row, cc, f);
-          r = v > 0.f ? 1.f / v : 0.f;
-          break;
-        }
-        case E_MASK: r = rd(smem, a, i, row, cc, f) * (A.mask ? A.mask[row] : 1.f); break;
-        default: r = 0.f;
+        lfloat& p = smem[ybase + i * y.lld + cc * y.cs + f];
+        const float v = acc ? p + r : r;
+        p = v;
+        if (y.gb) G(y.gb)[(int64_t)row * y.gld + cc * y.cs + y.c0 + f] = v;
       }
-      if (op != E_ZERO) r *= coef;
-      wr(smem, y, i, row, cc, f, r, acc);
-    }
+  }
 }
 
-__device__ __forceinline__ float ldB(const float* W, int ldw, int k0, int trans, int k, int n) {
+// general path (some operand lives in global memory): per-element home checks
+template <int NT>
+__device__ void ew_slow(const Args& A, const Ins& I, int r0, lfloat* smem) {
+  const int op = I[1], arg = I[2], acc = I[4];
+  const float coef = __int_as_float(I[3]);
+  const Opd y = opd(A, I, 8), a = opd(A, I, 8 + kOpdInts), b = opd(A, I, 8 + 2 * kOpdInts),
+            c = opd(A, I, 8 + 3 * kOpdInts);
+  const int ync = (op == E_DOT3 || op == E_NORM3) ? 1 : y.nc;
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x >> 6; i < kBM; i += NT / 64) {
+    const int row = r0 + i;
+    if (row >= A.N) break;
+    for (int cc = 0; cc < ync; ++cc)
+      for (int f = lane; f < y.w; f += 64) {
+        float r;
+        switch (op) {
+          case E_ZERO: r = 0.f; break;
+          case E_COPY: r = rd(smem, a, i, row, cc, f); break;
+          case E_MUL: r = rd(smem, a, i, row, cc, f) * rd(smem, b, i, row, cc, f); break;
+          case E_MUL3: r = rd(smem, a, i, row, cc, f) * rd(smem, b, i, row, cc, f) * rd(smem, c, i, row, cc, f); break;
+          case E_ACT: {
+            r = act(arg >> 2, arg & 3, rd(smem, a, i, row, cc, f));
+            if (b.nc) r *= rd(smem, b, i, row, cc, f);
+            if (c.nc) r *= rd(smem, c, i, row, cc, f);
+            break;
+          }
+          case E_DOT3: {
+            r = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) r += rd(smem, a, i, row, q, f) * rd(smem, b, i, row, q, f);
+            if (c.nc) r *= rd(smem, c, i, row, 0, f);
+            break;
+          }
+          case E_NORM3: {
+            float s2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+              const float v = rd(smem, a, i, row, q, f);
+              s2 += v * v;
+            }
+            r = sqrtf(s2);
+            break;
+          }
+          case E_SINV: {
+            const float v = rd(smem, a, i, row, cc, f);
+            r = v > 0.f ? 1.f / v : 0.f;
+            break;
+          }
+          case E_MASK: r = rd(smem, a, i, row, cc, f) * (A.mask ? G(A.mask)[row] : 1.f); break;
+          default: r = 0.f;
+        }
+        if (op != E_ZERO) r *= coef;
+        wr(smem, y, i, row, cc, f, r, acc);
+      }
+  }
+}
+
+template <int NT>
+__device__ void run_ew(const Args& A, const Ins& I, int r0, lfloat* smem) {
+  if (!I[5]) {  // lowering flag: not every operand is an LDS value
+    ew_slow<NT>(A, I, r0, smem);
+    return;
+  }
+  const int op = I[1], arg = I[2], acc = I[4];
+  const float coef = __int_as_float(I[3]);
+  const Opd y = opd(A, I, 8), a = opd(A, I, 8 + kOpdInts), b = opd(A, I, 8 + 2 * kOpdInts),
+            c = opd(A, I, 8 + 3 * kOpdInts);
+#define HY_EW(OPC, K, O) ew_fast<NT, OPC, K, O>(A, y, a, b, c, coef, acc, r0, smem)
+  switch (op) {
+    case E_ZERO: HY_EW(E_ZERO, 0, 0); break;
+    case E_COPY: HY_EW(E_COPY, 0, 0); break;
+    case E_MUL: HY_EW(E_MUL, 0, 0); break;
+    case E_MUL3: HY_EW(E_MUL3, 0, 0); break;
+    case E_DOT3: HY_EW(E_DOT3, 0, 0); break;
+    case E_NORM3: HY_EW(E_NORM3, 0, 0); break;
+    case E_SINV: HY_EW(E_SINV, 0, 0); break;
+    case E_MASK: HY_EW(E_MASK, 0, 0); break;
+    case E_ACT:
+      switch (arg) {
+        case 0: HY_EW(E_ACT, 0, 0); break;
+        case 1: HY_EW(E_ACT, 0, 1); break;
+        case 2: HY_EW(E_ACT, 0, 2); break;
+        case 4: HY_EW(E_ACT, 1, 0); break;
+        case 5: HY_EW(E_ACT, 1, 1); break;
+        case 6: HY_EW(E_ACT, 1, 2); break;
+        case 8: HY_EW(E_ACT, 2, 0); break;
+        case 9: HY_EW(E_ACT, 2, 1); break;
+        case 10: HY_EW(E_ACT, 2, 2); break;
+        case 12: HY_EW(E_ACT, 3, 0); break;
+        case 13: HY_EW(E_ACT, 3, 1); break;
+        case 14: HY_EW(E_ACT, 3, 2); break;
+        case 16: HY_EW(E_ACT, 4, 0); break;
+        case 17: HY_EW(E_ACT, 4, 1); break;
+        case 18: HY_EW(E_ACT, 4, 2); break;
+        default: break;
+      }
+      break;
+    default: break;
+  }
+#undef HY_EW
+}
+
+__device__ __forceinline__ float ldB(const gfloat* W, int ldw, int k0, int trans, int k, int n) {
   return trans ? W[(int64_t)n * ldw + k0 + k] : W[(int64_t)k * ldw + k0 + n];
 }
 
-// 16x16 output tile (component c, columns n0..n0+15) of one LIN: 16 K-steps of operand
-// loads issued together per round (one global latency per 64 K for the weights; A from LDS)
-__device__ void run_lin(const Args& A, const int* I, int r0, float* smem) {
+// 16x16 output tile (component c, columns n0..n0+15) of one LIN.  FAST (every A operand
+// is an LDS value, flagged at lowering): per 64-deep K round the 16 weight loads are issued
+// back to back with clamped, always-valid indices (no branch between them: a home check or
+// a select there made the compiler wait out one full memory latency per K-step), then the
+// 16 A values come from LDS (zeroed past K), then 16 MFMAs.  Rows past N only feed output
+// rows that are never stored.
+template <int NT, bool FAST>
+__device__ void run_lin(const Args& A, const Ins& I, int r0, lfloat* smem) {
   const int acc = I[4];
-  const Opd y = opd(A, I + 8), x0 = opd(A, I + 8 + kOpdInts), x1 = opd(A, I + 8 + 2 * kOpdInts);
-  const float* W = A.p[I[56]];
+  const Opd y = opd(A, I, 8), x0 = opd(A, I, 8 + kOpdInts), x1 = opd(A, I, 8 + 2 * kOpdInts);
+  const gfloat* W = G(A.p[I[56]]);
   const int ldw = I[57], k0a = I[58], k0b = I[59], trans = I[61];
   const float* bias = I[60] >= 0 ? A.p[I[60]] : nullptr;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = kThreads >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = NT >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int ntn = (y.w + 15) >> 4, tiles = y.nc * ntn;
   const int arow = r0 + i;
@@ -184,20 +334,34 @@ __device__ void run_lin(const Args& A, const int* I, int r0, float* smem) {
   for (int tile = wv; tile < tiles; tile += nw) {
     const int c = tile / ntn, n0 = (tile % ntn) * 16, n = n0 + i;
     const bool nok = n < y.w;
+    const int nc_ = min(n, y.w - 1);
     f4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
     for (int blk = 0; blk < 2; ++blk) {
       const Opd& x = blk == 0 ? x0 : x1;
       if (!x.nc) continue;
       const int k0 = blk == 0 ? k0a : k0b;
       const int K = x.w;
+      const int xb = kBM * x.loff + i * x.lld + (x.nc == 1 ? 0 : c) * x.cs + x.c0;
       for (int kb = 0; kb < K; kb += 64) {
         float av[16], bv[16];
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-          const int k = kb + 4 * s + g;
-          const bool kok = k < K;
-          bv[s] = (nok && kok) ? ldB(W, ldw, k0, trans, k, n) : 0.f;
-          av[s] = (rok && kok) ? rd(smem, x, i, arow, c, k) : 0.f;
+          const int kc = min(kb + 4 * s + g, K - 1);
+          bv[s] = trans ? W[(int64_t)nc_ * ldw + k0 + kc] : W[(int64_t)kc * ldw + k0 + nc_];
+        }
+        if constexpr (FAST) {
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int k = kb + 4 * s + g;
+            const float v = smem[xb + min(k, K - 1)];
+            av[s] = k < K ? v : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int k = kb + 4 * s + g;
+            av[s] = (rok && k < K) ? rd(smem, x, i, arow, c, k) : 0.f;
+          }
         }
 #pragma unroll
         for (int s = 0; s < 16; s += 2) {
@@ -208,7 +372,7 @@ __device__ void run_lin(const Args& A, const int* I, int r0, float* smem) {
     }
     const f4v s = a0 + a1;
     if (nok) {
-      const float bb = bias ? bias[n] : 0.f;
+      const float bb = bias ? G(bias)[n] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int il = 4 * g + r, row = r0 + il;
@@ -219,30 +383,50 @@ __device__ void run_lin(const Args& A, const int* I, int r0, float* smem) {
 }
 
 // the program is staged into LDS first (after the activation area): every instruction was
-// a scalar-cache miss to L2 on a CU that runs one workgroup; its fields are then read from
-// LDS (broadcast) and made wave-uniform with readfirstlane
-__global__ void __launch_bounds__(kThreads) rowprog_kernel(Args A) {
-  extern __shared__ float smem[];
+// a scalar-cache miss to L2 on a CU that runs one workgroup.  Each lane then reads ONE field
+// of the next instruction (one LDS read per instruction, prefetched a step ahead) and the
+// fields are broadcast from their lanes (v_readlane -> SGPRs); reading the 64 fields one by
+// one cost ~2 us per instruction (measured, tools/bench_rowprog.py)
+template <int NT>
+__global__ void __launch_bounds__(NT) rowprog_kernel(Args A) {
+  extern __shared__ float smem_[];
+  lfloat* smem = (lfloat*)smem_;
   const int r0 = blockIdx.x * kBM;
-  int* prog = reinterpret_cast<int*>(smem + kBM * A.lds_w);
-  for (int t = threadIdx.x; t < A.nins * kInsInts; t += kThreads) prog[t] = A.ins[t];
+  __attribute__((address_space(3))) int* prog = (__attribute__((address_space(3))) int*)(smem + kBM * A.lds_w);
+  const __attribute__((address_space(1))) int* gins = (const __attribute__((address_space(1))) int*)A.ins;
+  for (int t = threadIdx.x; t < A.nins * kInsInts; t += NT) prog[t] = gins[t];
   __syncthreads();
-  int I[kInsInts];
+  const int lane = threadIdx.x & 63;
+  int nxt = prog[lane];  // lane t holds field t of the next instruction (one LDS read per lane)
   for (int q = 0; q < A.nins; ++q) {
-#pragma unroll
-    for (int t = 0; t < kInsInts; ++t) I[t] = __builtin_amdgcn_readfirstlane(prog[q * kInsInts + t]);
-    if (I[0] == 1)
-      run_lin(A, I, r0, smem);
-    else
-      run_ew(A, I, r0, smem);
-    __syncthreads();
+    const Ins I{nxt};
+    if (q + 1 < A.nins) nxt = prog[(q + 1) * kInsInts + lane];
+    const bool stamp = A.dbg && blockIdx.x == 0 && threadIdx.x == 0;
+    long long t0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    long long t1 = t0;
+    if (I[0] == 1) {
+      if (I[5])
+        run_lin<NT, true>(A, I, r0, smem);
+      else
+        run_lin<NT, false>(A, I, r0, smem);
+    } else
+      run_ew<NT>(A, I, r0, smem);
+    long long t2 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    if (!I[6]) __syncthreads();  // the lowering elides barriers between same-thread element-wise steps
+    if (stamp) {
+      const long long t3 = (long long)__builtin_amdgcn_s_memtime();
+      A.dbg[4 * q] = t0;
+      A.dbg[4 * q + 1] = t1;
+      A.dbg[4 * q + 2] = t2;
+      A.dbg[4 * q + 3] = t3;
+    }
   }
 }
 
 }  // namespace rpg
 
 void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::optional<at::Tensor>& mask,
-                 at::TensorList ptrs, int64_t N, int64_t lds_w) {
+                 at::TensorList ptrs, int64_t N, int64_t lds_w, const c10::optional<at::Tensor>& dbg) {
   HY_CHECK(prog.is_cuda() && prog.scalar_type() == at::kInt && prog.is_contiguous(), "rowprog: program");
   HY_CHECK(prog.numel() % rpg::kInsInts == 0, "rowprog: program size");
   HY_CHECK((int64_t)ptrs.size() <= rpg::kMaxPtr, "rowprog: too many pointers");
@@ -254,6 +438,12 @@ void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::option
   HY_CHECK(lds_w >= 0, "rowprog: LDS width");
   a.ws = ws.numel() ? ws.data_ptr<float>() : nullptr;
   a.mask = nullptr;
+  a.dbg = nullptr;
+  if (dbg.has_value() && dbg->defined()) {
+    HY_CHECK(dbg->is_cuda() && dbg->scalar_type() == at::kLong && dbg->numel() >= 4 * (prog.numel() / rpg::kInsInts),
+             "rowprog: dbg must be int64 [4 * nins]");
+    a.dbg = reinterpret_cast<long long*>(dbg->data_ptr<int64_t>());
+  }
   if (mask.has_value() && mask->defined()) {
     HY_CHECK(mask->is_cuda() && mask->scalar_type() == at::kFloat && mask->numel() == N, "rowprog: mask [N] fp32");
     a.mask = mask->data_ptr<float>();
@@ -267,19 +457,32 @@ void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::option
   if (N == 0 || a.nins == 0) return;
   const size_t lds = (size_t)lds_w * rpg::kBM * sizeof(float) + (size_t)prog.numel() * sizeof(int);
   HY_CHECK(lds <= 160 * 1024, "rowprog: activations + program exceed the 160 KiB LDS");
-  if (lds > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)rpg::rowprog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
+  // workgroup size: every wave decodes every instruction on the CU's one scalar unit, so
+  // fewer waves cost less per instruction; HYDRA_ROWPROG_THREADS picks 256 / 512 / 1024
+  static int nt = [] {
+    const char* e = std::getenv("HYDRA_ROWPROG_THREADS");
+    const int v = e ? std::atoi(e) : 256;
+    return (v == 1024 || v == 512) ? v : 256;
+  }();
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)rpg::rowprog_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)rpg::rowprog_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)rpg::rowprog_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
   }
-  rpg::rowprog_kernel<<<ceil_div(N, rpg::kBM), rpg::kThreads, lds, stream()>>>(a);
+  const int grid = ceil_div(N, rpg::kBM);
+  if (nt == 1024)
+    rpg::rowprog_kernel<1024><<<grid, 1024, lds, stream()>>>(a);
+  else if (nt == 512)
+    rpg::rowprog_kernel<512><<<grid, 512, lds, stream()>>>(a);
+  else
+    rpg::rowprog_kernel<256><<<grid, 256, lds, stream()>>>(a);
 }
 
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("rowprog_run(Tensor prog, Tensor(a!) ws, Tensor? mask, Tensor(b!)[] ptrs, int N, int lds_w) -> ()");
+  m.def("rowprog_run(Tensor prog, Tensor(a!) ws, Tensor? mask, Tensor(b!)[] ptrs, int N, int lds_w, Tensor(c!)? dbg=None) -> ()");
 }
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) { m.impl("rowprog_run", hy::rowprog_run); }

@@ -685,6 +685,42 @@ def compile_device(prog, ext_roots, n_weights, inputs=(), keep_global=(), lds_bu
         rest = _substitute(ins_list[first:], v, sh)
         ins_list = ins_list[:first] + [("ew", E_COPY, sh, v, None, None, 0, 1.0, False)] + rest
         shadows[sh.id] = v.id
+    # barrier elision: the interpreter maps element (row, component, column f) of an
+    # element-wise instruction to wave row % waves, lane f % 64 (all components in that
+    # thread), so an element-wise instruction may follow another without a barrier when
+    # every value it reads that was written since the last barrier was written by the same
+    # threads: same root, column offsets congruent mod 64.  LINs read across rows and
+    # columns: barriers around them always.
+    nb = len(ins_list)
+    no_bar = [False] * nb
+    group = [0] * nb
+    g_id, written = 0, {}
+
+    def _w_off(ins):
+        y = _writes(ins)
+        return y.base.id, y.c0
+
+    for k, ins in enumerate(ins_list):
+        if k > 0:
+            prev = ins_list[k - 1]
+            ok = prev[0] == "ew" and ins[0] == "ew"
+            if ok:
+                for t in _reads(ins):
+                    offs = written.get(t.base.id)
+                    if offs is not None and any((o - t.c0) % 64 for o in offs):
+                        ok = False
+                        break
+            if ok:
+                no_bar[k - 1] = True
+            else:
+                g_id += 1
+                written = {}
+        group[k] = g_id
+        r_, o_ = _w_off(ins)
+        written.setdefault(r_, []).append(o_)
+    group_start = {}
+    for k in range(nb):
+        group_start.setdefault(group[k], k)
     # liveness of every root (first write .. last read)
     first_w, last_r, roots = {}, {}, {}
     for k, ins in enumerate(ins_list):
@@ -701,8 +737,9 @@ def compile_device(prog, ext_roots, n_weights, inputs=(), keep_global=(), lds_bu
     active = []
     for k, ins in enumerate(ins_list):
         still = []
+        g0 = group_start[group[k]]  # within a barrier-free group other threads may still read
         for rid, off, size in active:
-            if last_r[rid] < k:
+            if last_r[rid] < g0:
                 free.append((off, size))
             else:
                 still.append((rid, off, size))
@@ -767,6 +804,8 @@ def compile_device(prog, ext_roots, n_weights, inputs=(), keep_global=(), lds_bu
             assert all(t[1] is W for t in xs), "K blocks of one LIN share one weight"
             r[0], r[4] = 1, int(acc)
             ops_ = [y, xs[0][0], xs[1][0] if len(xs) > 1 else None, None]
+            # fast-path flag: every A operand is an LDS value (the destination may be anywhere)
+            r[5] = int(all(t is None or bufs[buf(t)][4] >= 0 for t in ops_[1:3]))
             r[56], r[57] = W.pid, W.K
             r[58] = xs[0][2]
             r[59] = xs[1][2] if len(xs) > 1 else 0
@@ -778,6 +817,9 @@ def compile_device(prog, ext_roots, n_weights, inputs=(), keep_global=(), lds_bu
             r[3] = int(np.array([coef], dtype=np.float32).view(np.int32)[0])
             r[4] = int(acc)
             ops_ = [y, a, b, c]
+            # fast-path flag: every operand (incl. the destination) is an LDS value
+            r[5] = int(all(t is None or bufs[buf(t)][4] >= 0 for t in ops_))
+        r[6] = int(no_bar[len(rows)])  # no barrier after this instruction
         for q, v in enumerate(ops_):
             r[8 + OPD_INTS * q: 8 + OPD_INTS * (q + 1)] = opnd(v)
         rows.append(r)
