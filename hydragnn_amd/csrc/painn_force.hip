@@ -467,27 +467,35 @@ __global__ void __launch_bounds__(256) msg_vjp_kernel(Msg M, const float* __rest
   if (wpart) wacc_store<RM, NC>(acc, F, M.R, wpart + (int64_t)blockIdx.x * 3 * F * R1, lds);
 }
 
-// fixed-order sum of the workgroup partials into W grad [3F][R] and b grad [3F]
+// fixed-order sum of the workgroup partials into W grad [3F][R] and b grad [3F]: a block
+// owns 64 outputs; its 4 waves sum interleaved quarters of the partials (8 loads in flight
+// per lane), folded through LDS in a fixed order (one partial row per node quartet made a
+// one-thread-per-output walk over ~256 rows a 19 us dependent-load chain)
 __global__ void __launch_bounds__(256) wpart_reduce_kernel(const float* __restrict__ part, int nparts, int F, int R,
                                                            float* __restrict__ gW, float* __restrict__ gb) {
+  __shared__ float red[4][64];
   const int R1 = R + 1, n = 3 * F * R1;
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= n) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int p = 0;
-  for (; p + 4 <= nparts; p += 4) {
-    a0 += part[(int64_t)p * n + k];
-    a1 += part[(int64_t)(p + 1) * n + k];
-    a2 += part[(int64_t)(p + 2) * n + k];
-    a3 += part[(int64_t)(p + 3) * n + k];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (k < n) {
+    int p = w;
+    for (; p + 28 < nparts; p += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += part[(int64_t)(p + 4 * u) * n + k];
+    }
+    for (int u = 0; p < nparts; p += 4, ++u) a[u & 7] += part[(int64_t)p * n + k];
   }
-  for (; p < nparts; ++p) a0 += part[(int64_t)p * n + k];
-  const float t = (a0 + a1) + (a2 + a3);
-  const int m = k / R1, r = k % R1;
-  if (r < R)
-    gW[(int64_t)m * R + r] = t;
-  else
-    gb[m] = t;
+  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (w == 0 && k < n) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    const int m = k / R1, r = k % R1;
+    if (r < R)
+      gW[(int64_t)m * R + r] = t;
+    else
+      gb[m] = t;
+  }
 }
 
 // ---- double backward: (1) src-CSR pass -> gradients of the VJP's upstream (Gs, Gv)
@@ -884,7 +892,7 @@ std::vector<at::Tensor> painn_msg_vjp(const at::Tensor& Gs, const at::Tensor& Gv
   if (need_w) {
     const int n = 3 * M.F * (M.R + 1);
     if (M.N)
-      pf::wpart_reduce_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(part.data_ptr<float>(), grid, M.F, M.R,
+      pf::wpart_reduce_kernel<<<ceil_div(n, 64), 256, 0, stream()>>>(part.data_ptr<float>(), grid, M.F, M.R,
                                                                        gW.data_ptr<float>(), gb.data_ptr<float>());
     else {
       gW.zero_();
@@ -934,7 +942,7 @@ std::vector<at::Tensor> painn_msg_vvjp(const at::Tensor& Gs, const at::Tensor& G
   if (nw) {
     const int n = 3 * (int)F * ((int)R + 1);
     if (N)
-      pf::wpart_reduce_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(part.data_ptr<float>(), grid, (int)F, (int)R,
+      pf::wpart_reduce_kernel<<<ceil_div(n, 64), 256, 0, stream()>>>(part.data_ptr<float>(), grid, (int)F, (int)R,
                                                                        out[6].data_ptr<float>(),
                                                                        out[7].data_ptr<float>());
     else {

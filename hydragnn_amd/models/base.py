@@ -362,7 +362,11 @@ class Base(nn.Module):
         buf = getattr(self, "_branch_presence", None)
         if buf is None:
             return
-        ids = torch.tensor([int(b.split("-")[1]) for b in self.branch_names()], device=dn.device, dtype=dn.dtype)
+        # branch-id table built once (the capture warm-up runs first: no H2D copy inside capture)
+        ids = self.__dict__.get("_branch_ids_t")
+        if ids is None or ids.device != dn.device or ids.dtype != dn.dtype:
+            ids = torch.tensor([int(b.split("-")[1]) for b in self.branch_names()], device=dn.device, dtype=dn.dtype)
+            self.__dict__["_branch_ids_t"] = ids
         buf.copy_((dn.view(1, -1) == ids.view(-1, 1)).any(1).to(buf.dtype))
 
     def dense_decode_ok(self):

@@ -105,16 +105,30 @@ def flush_deferred_wgrads():
     touched = []
     for r in rounds:
         dys, xs, dws, dbs, acc = [], [], [], [], []
-        for dy, x, W, b in r:
-            a = W.grad is not None
-            if W.grad is None:
+        for it in r:
+            dy, x, W, b = it[:4]
+            k0 = it[4] if len(it) > 4 else 0  # column block [k0, k0 + K) of W (row programs)
+            K = x.shape[1]
+            full = k0 == 0 and K == W.shape[1]
+            aw = W.grad is not None
+            abx = b is not None and b.grad is not None
+            if not aw and not abx and full:
+                # first contribution to both: written, not accumulated
                 W.grad = torch.empty_like(W)
-            if b is not None and b.grad is None:
-                b.grad = torch.empty_like(b)
-                assert not a, "bias grad missing while weight grad exists"
+                if b is not None:
+                    b.grad = torch.empty_like(b)
+                a = False
+            else:
+                # a column block of a wider weight (the rest may get no contribution), or one
+                # of the pair already holds earlier rounds: zero-fill what is missing, accumulate
+                if not aw:
+                    W.grad = torch.zeros_like(W)
+                if b is not None and b.grad is None:
+                    b.grad = torch.zeros_like(b)
+                a = True
             dys.append(dy)
             xs.append(x)
-            dws.append(W.grad)
+            dws.append(W.grad if full else W.grad[:, k0:k0 + K])
             dbs.append(b.grad if b is not None else torch.empty(0, device=dy.device))
             acc.append(1 if a else 0)
             touched += [W] + ([b] if b is not None else [])

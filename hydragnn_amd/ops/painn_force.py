@@ -480,7 +480,7 @@ def _dev_exec(cp, mode, N, mask, feeds, ws):
         tens[v.id] = t
         ptrs.append(t)
     wsb = torch.empty(max(N * dm.width, 1), device=x0.device, dtype=torch.float32)
-    _native.ops().rowprog_run(dm.ins, wsb, mask, ptrs, N, dm.lds_w)
+    _native.ops().rowprog_run(dm.ins, wsb, mask, ptrs, N, dm.lds_w, None, len(ws))
 
     def get(v):
         b = v.base
@@ -497,6 +497,28 @@ def _dev_exec(cp, mode, N, mask, feeds, ws):
             t.view(N, b.nc, b.w)[:, :, v.c0:v.c0 + v.w]
 
     return get, dm
+
+
+def _defer_ok(ws):
+    from .linear import _defer
+
+    return _defer["on"] and not torch.is_grad_enabled() and all(isinstance(w, torch.nn.Parameter) for w in ws)
+
+
+def _dev_wgrads_defer(dm, get, N, ws):
+    """Record a device run's weight-gradient products with the backward's deferred grouped
+    weight-gradient launch (ops/linear.py deferred_wgrad): every row program of the
+    backward, first- and second-order, shares one launch pair per round, accumulating in
+    place into ``.grad`` (no per-program launches, no autograd accumulation adds)."""
+    from .linear import _defer
+
+    for rnd in dm.rounds:
+        for (pid, k0, G, X, bias, acc) in rnd:
+            g, x = get(G), get(X)
+            if G.nc == 3:
+                g = g.reshape(N * 3, G.w)
+                x = x.reshape(N * 3, X.w)
+            _defer["items"].append((g, x, ws[pid], ws[bias] if bias is not None else None, k0))
 
 
 def _dev_wgrads(dm, get, N, ws):
@@ -558,6 +580,8 @@ class _Chain(torch.autograd.Function):
         need_w = not _state["inputs_only"] and any(ctx.needs_input_grad[3 + n_in:])
         res = _ChainBwd.apply(cp, ctx.mask, n_in, len(gouts), need_w, *gouts, *xs, *ws)
         gx, gw = res[:n_in], res[n_in:]
+        if need_w and gw and gw[0].numel() == 0 and ws[0].numel() != 0:  # deferred to the grouped flush
+            need_w = False
         return (None, None, None, *gx, *(gw if need_w else [None] * len(ws)))
 
 
@@ -568,17 +592,24 @@ class _ChainBwd(torch.autograd.Function):
         N = xs[0].shape[0]
         res = cp.vjp_res if need_w else cp.vjp_in_res
         feeds = {**dict(zip(cp.ins, xs)), **dict(zip(cp.gouts, gouts))}
+        deferred = False
         if _device(xs[0]):
             get, dm = _dev_exec(cp, "vjp" if need_w else "vjp_in", N, mask, feeds, ws)
-            grads = _dev_wgrads(dm, get, N, ws) if need_w else None
+            if need_w and _defer_ok(ws):
+                _dev_wgrads_defer(dm, get, N, ws)
+                grads, deferred = [None] * len(ws), True
+            else:
+                grads = _dev_wgrads(dm, get, N, ws) if need_w else None
         else:
             cp.weights_t = ws
             env, grads = _run(cp, cp.vjp if need_w else cp.vjp_in, feeds, mask, N, cp.vjp_wg if need_w else None)
             get = lambda v: _slot(env, v, N)  # noqa: E731
         gx = [get(res[x]).reshape(t.shape) if res[x] is not None else torch.zeros_like(t) for x, t in zip(cp.ins, xs)]
-        gw = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)] if need_w else \
-            [torch.zeros(0, dtype=xs[0].dtype, device=xs[0].device) for _ in ws]
+        gw = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)] if (need_w and not deferred) \
+            else [torch.zeros(0, dtype=xs[0].dtype, device=xs[0].device) for _ in ws]
         ctx.mark_non_differentiable(*gw)
+        ctx.deferred = deferred
+        ctx.params = list(ws)  # the Parameter objects themselves (deferred weight gradients)
         ctx.cp, ctx.mask, ctx.n_in, ctx.n_out = cp, mask, n_in, n_out
         ctx.save_for_backward(*gouts, *xs, *ws)
         return (*gx, *gw)
@@ -593,7 +624,11 @@ class _ChainBwd(torch.autograd.Function):
         feeds = {**dict(zip(cp.ins, xs)), **dict(zip(cp.hins, hx)), **dict(zip(cp.gouts, gouts))}
         if _device(xs[0]):
             get, dm = _dev_exec(cp, "vvjp", N, ctx.mask, feeds, ws)
-            grads = _dev_wgrads(dm, get, N, ws)
+            if _defer_ok(ctx.params):
+                _dev_wgrads_defer(dm, get, N, ctx.params)
+                grads = [None] * len(ws)
+            else:
+                grads = _dev_wgrads(dm, get, N, ws)
         else:
             cp.weights_t = ws
             env, grads = _run(cp, cp.vvjp, feeds, ctx.mask, N, cp.vvjp_wg)
@@ -601,7 +636,8 @@ class _ChainBwd(torch.autograd.Function):
         g_gouts = [get(t).reshape(g.shape) if t is not None else torch.zeros_like(g) for t, g in zip(cp.touts, gouts)]
         g_xs = [get(cp.vvjp_res[x]).reshape(t.shape) if cp.vvjp_res[x] is not None else torch.zeros_like(t)
                 for x, t in zip(cp.ins, xs)]
-        g_ws = [g if g is not None else torch.zeros_like(w) for g, w in zip(grads, ws)]
+        g_ws = [g if g is not None else (None if _defer_ok(ctx.params) else torch.zeros_like(w))
+                for g, w in zip(grads, ws)]
         return (None, None, None, None, None, *g_gouts, *g_xs, *g_ws)
 
 

@@ -26,17 +26,17 @@ def run(name, build, N=1024, F=64, reps=20):
     wsb = torch.empty(max(N * width, 1), device=dev)
     ptrs = wts + [xt, ot]
     for _ in range(3):
-        _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w)
+        _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w, None, len(wts))
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w)
+        _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w, None, len(wts))
     e1.record()
     torch.cuda.synchronize()
     us = 1000 * e0.elapsed_time(e1) / reps
     dbg = torch.zeros(4 * len(ins), dtype=torch.int64, device=dev)
-    _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w, dbg)
+    _native.ops().rowprog_run(tins, wsb, None, ptrs, N, lds_w, dbg, len(wts))
     torch.cuda.synchronize()
     d = dbg.view(-1, 4).cpu().double()
     dec, run, bar = (d[:, 1] - d[:, 0]).mean(), (d[:, 2] - d[:, 1]).mean(), (d[:, 3] - d[:, 2]).mean()
