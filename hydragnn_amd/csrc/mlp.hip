@@ -22,6 +22,9 @@
 // widths <= 128, G <= 1024 rows, weights <= ~150 KB of LDS.
 #include "common.h"
 
+#include <cstdlib>
+#include <string>
+
 namespace hy {
 
 constexpr int kMlpMaxLayers = 8;
@@ -360,22 +363,34 @@ __device__ __host__ __forceinline__ int hl_ld(int cols) { return hl_r16(cols) + 
 
 struct HlLayout {  // float offsets into the dynamic LDS block
   int w[kMlpMaxLayers];      // W_l   [r16(O)][ld(I)]
+  int b[kMlpMaxLayers];      // b_l   [r16(O)]
   int act[kMlpMaxLayers];    // A_l   [Gp][ld(O)]   (layer l's output)
-  int x, dy, dy2, total, Gp, ldy;
+  int x, dy, dy2, tg, mk, total, Gp, ldy;  // tg: target [G][Do]; mk: row mask [Gp] (1 / 0)
 };
 
-__device__ __host__ inline HlLayout hl_layout(const MlpArgs& a, int G) {
-  HlLayout L{};
+// Every head kernel is instantiated per layer count NL (1..kMlpMaxLayers): the layer loops
+// unroll, each layer's widths / offsets are compile-time-indexed (registers and hoisted
+// kernel-argument loads instead of a dependent load chain at every layer), and the layout is
+// computed by every thread (a runtime-indexed struct would live in scratch memory).
+template <int NL>
+__device__ __host__ inline void hl_layout_into(HlLayout& L, const MlpArgs& a, int G) {
   L.Gp = hl_r16(G);
   int o = 0, mw = a.dims[0];
-  for (int l = 0; l < a.n; ++l) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     L.w[l] = o;
     o += hl_r16(a.dims[l + 1]) * hl_ld(a.dims[l]);
     mw = a.dims[l + 1] > mw ? a.dims[l + 1] : mw;
   }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    L.b[l] = o;
+    o += hl_r16(a.dims[l + 1]);
+  }
   L.x = o;
   o += L.Gp * hl_ld(a.dims[0]);
-  for (int l = 0; l < a.n; ++l) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     L.act[l] = o;
     o += L.Gp * hl_ld(a.dims[l + 1]);
   }
@@ -384,7 +399,17 @@ __device__ __host__ inline HlLayout hl_layout(const MlpArgs& a, int G) {
   o += L.Gp * L.ldy;
   L.dy2 = o;
   o += L.Gp * L.ldy;
+  L.tg = o;
+  o += G * a.dims[NL];
+  L.mk = o;
+  o += L.Gp;
   L.total = o;
+}
+
+template <int NL>
+__device__ __host__ inline HlLayout hl_layout(const MlpArgs& a, int G) {
+  HlLayout L{};
+  hl_layout_into<NL>(L, a, G);
   return L;
 }
 
@@ -392,98 +417,99 @@ __device__ __forceinline__ f4v_hl hl_mfma(float a, float b, f4v_hl c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// zero the whole block, then every weight, the input rows and (backward) the saved
-// activations in ONE pass over a flat index (kHlBatch loads in flight per thread before the
-// stores).  The segment table is built in LDS: a per-lane search through the kernel-argument
-// arrays compiles to per-lane loads from the kernarg segment, a memory round trip per probe.
-constexpr int kHlSegs = 2 * kMlpMaxLayers + 1;
-struct HlSegTab {
-  const float* src[kHlSegs];
-  int beg[kHlSegs + 1];
-  int width[kHlSegs], ld[kHlSegs], dst[kHlSegs];
-  int n;
-};
+// sum over k-steps 0..K4-1 of mfma(ap[k sa], bp[k sb]): the LDS reads of 8 steps are
+// issued together (one latency per group instead of one per step) and two accumulators
+// alternate (dependent-accumulator latency); steps past K4 read nothing and add zero
+__device__ __forceinline__ f4v_hl hl_dot(const float* ap, int sa, const float* bp, int sb, int K4) {
+  f4v_hl a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  for (int k = 0; k < K4; k += 8) {
+    float x[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = k + j < K4;
+      x[j] = ok ? ap[(k + j) * sa] : 0.f;
+      y[j] = ok ? bp[(k + j) * sb] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      a0 = hl_mfma(x[j], y[j], a0);
+      a1 = hl_mfma(x[j + 1], y[j + 1], a1);
+    }
+  }
+  return a0 + a1;
+}
 
+// workgroup barrier that waits for this wave's LDS traffic only: the global stores of
+// activations / gradients stay in flight (nothing in these kernels reads them back), where
+// __syncthreads' release fence would drain them at every layer
+// optional cycle stamps (tools/bench_head_loss.py --stamps): thread 0 records the shader
+// clock at phase boundaries into dbg[i]
+__device__ __forceinline__ void hl_stamp(long long* dbg, int i) {
+  if (dbg != nullptr && threadIdx.x == 0) dbg[i] = (long long)__builtin_amdgcn_s_memtime();
+}
+
+__device__ __forceinline__ void hl_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Zero the whole block, then copy every weight and bias, the input rows, the targets and
+// (backward) the saved activations straight into it with LDS-DMA (global_load_lds_dword: no
+// staging registers, no ds_write pass): one wave instruction per (matrix row, 64-column
+// chunk), rows dealt round-robin to the waves (continuing across matrices), every copy in
+// flight together, so staging costs ~one memory latency and nothing later in the kernel
+// reads global memory.  The matrix loop is unrolled over the layers (NL): its parameters
+// are compile-time kernel-argument offsets, loaded once, not searched per row.
+template <int NL>
 __device__ void hl_stage(const MlpArgs& a, const HlLayout& L, const float* __restrict__ x,
-                         const float* __restrict__ acts, int G, float* sm) {
-  __shared__ HlSegTab T;
+                         const float* __restrict__ acts, const float* __restrict__ target,
+                         const bool* __restrict__ mask, int G, float* sm) {
   for (int e = threadIdx.x; e < L.total; e += kHlThreads) sm[e] = 0.f;
-  if (threadIdx.x == 0) {
-    int k = 0, b = 0;
-    for (int l = 0; l < a.n; ++l, ++k) {
-      T.src[k] = a.W[l];
-      T.beg[k] = b;
-      T.width[k] = a.dims[l];
-      T.ld[k] = hl_ld(a.dims[l]);
-      T.dst[k] = L.w[l];
-      b += a.dims[l] * a.dims[l + 1];
-    }
-    T.src[k] = x;
-    T.beg[k] = b;
-    T.width[k] = a.dims[0];
-    T.ld[k] = hl_ld(a.dims[0]);
-    T.dst[k] = L.x;
-    b += G * a.dims[0];
-    ++k;
-    if (acts) {  // acts [G, S]: layer l's block of columns -> A_l
-      for (int l = 0; l < a.n; ++l, ++k) {
-        T.src[k] = acts + a.aoff[l];  // strided rows: handled by the S-wide flat index below
-        T.beg[k] = b;
-        T.width[k] = a.dims[l + 1];
-        T.ld[k] = hl_ld(a.dims[l + 1]);
-        T.dst[k] = L.act[l];
-        b += G * a.dims[l + 1];
-      }
-    }
-    T.beg[k] = b;
-    T.n = k;
-  }
-  __syncthreads();
-  const int total = T.beg[T.n], ns = T.n, nplain = a.n + 1, S = a.aoff[a.n];
-  for (int base = threadIdx.x; base < total; base += kHlBatch * kHlThreads) {
-    float v[kHlBatch];
-    int sg[kHlBatch];
-    int q = 0;  // idx grows with k: the segment search resumes where the last one stopped
+  hl_sync();  // zero fill done before any copy lands
+  // the row mask (bool -> 1 / 0; padding rows stay 0)
+  for (int r = threadIdx.x; r < G; r += kHlThreads) sm[L.mk + r] = (mask == nullptr || mask[r]) ? 1.f : 0.f;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  int base = 0;  // rows dealt so far (wave-uniform)
+  auto rows = [&](const float* src, int n, int width, int sld, int dst, int dld) {
+    // this wave's rows r = (wv - base) mod kHlWaves, + kHlWaves, ...
+    for (int r = (wv - base % kHlWaves + kHlWaves) % kHlWaves; r < n; r += kHlWaves)
+      for (int c0 = 0; c0 < width; c0 += 64)
+        if (c0 + lane < width)
+          __builtin_amdgcn_global_load_lds(
+              (__attribute__((address_space(1))) void*)(src + (int64_t)r * sld + c0 + lane),
+              (__attribute__((address_space(3))) void*)(sm + dst + r * dld + c0), 4, 0, 0);
+    base += n;
+  };
 #pragma unroll
-    for (int k = 0; k < kHlBatch; ++k) {
-      const int idx = min(base + k * kHlThreads, total - 1);
-      while (q + 1 < ns && idx >= T.beg[q + 1]) ++q;
-      sg[k] = q;
-      const int e = idx - T.beg[q];
-      // activation segments read rows of the [G, S] image (row stride S, not the width)
-      v[k] = q < nplain ? T.src[q][e] : T.src[q][(e / T.width[q]) * S + e % T.width[q]];
-    }
+  for (int l = 0; l < NL; ++l) rows(a.W[l], a.dims[l + 1], a.dims[l], a.dims[l], L.w[l], hl_ld(a.dims[l]));
 #pragma unroll
-    for (int k = 0; k < kHlBatch; ++k) {
-      const int idx = base + k * kHlThreads;
-      if (idx < total) {
-        const int q = sg[k], e = idx - T.beg[q], w = T.width[q];
-        sm[T.dst[q] + (e / w) * T.ld[q] + e % w] = v[k];
-      }
-    }
+  for (int l = 0; l < NL; ++l) rows(a.b[l], 1, a.dims[l + 1], 0, L.b[l], 0);
+  rows(x, G, a.dims[0], a.dims[0], L.x, hl_ld(a.dims[0]));
+  rows(target, G, a.dims[NL], a.dims[NL], L.tg, a.dims[NL]);
+  if (acts) {  // acts [G, S]: layer l's block of columns -> A_l
+#pragma unroll
+    for (int l = 0; l < NL; ++l) rows(acts + a.aoff[l], G, a.dims[l + 1], a.aoff[NL], L.act[l], hl_ld(a.dims[l + 1]));
   }
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  hl_sync();
 }
 
 // forward chain: A_l = act(A_{l-1} W_l^T + b_l), tiles of 16 rows x 16 outputs per wave;
 // padding rows/columns stay exactly zero; rows < G, columns < O also go to the global acts
-__device__ void hl_chain(const MlpArgs& a, const HlLayout& L, int G, float* sm, float* __restrict__ acts) {
+template <int NL>
+__device__ void hl_chain(const MlpArgs& a, const HlLayout& L, int G, float* sm, float* __restrict__ acts,
+                         long long* dbg = nullptr) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
-  const int S = a.aoff[a.n];
-  for (int l = 0; l < a.n; ++l) {
+  const int S = a.aoff[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     const int I = a.dims[l], O = a.dims[l + 1];
     const float* in = sm + (l == 0 ? L.x : L.act[l - 1]);
     const int ldi = hl_ld(I), ldo = hl_ld(O);
     const float* W = sm + L.w[l];
     float* out = sm + L.act[l];
     const int ct = hl_r16(O) / 16, tiles = (L.Gp / 16) * ct, K4 = (I + 3) / 4;
-    const float* __restrict__ bb = a.b[l];
+    const float* bb = sm + L.b[l];
     for (int t = wv; t < tiles; t += kHlWaves) {
       const int r0 = (t / ct) * 16, c0 = (t % ct) * 16;
-      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = in + (r0 + li) * ldi + lg;
-      const float* bp = W + (c0 + li) * ldi + lg;
-      for (int k = 0; k < K4; ++k) acc = hl_mfma(ap[4 * k], bp[4 * k], acc);
+      const f4v_hl acc = hl_dot(in + (r0 + li) * ldi + lg, 4, W + (c0 + li) * ldi + lg, 4, K4);
       const int col = c0 + li;
       const float bias = col < O ? bb[col] : 0.f;
 #pragma unroll
@@ -496,30 +522,56 @@ __device__ void hl_chain(const MlpArgs& a, const HlLayout& L, int G, float* sm, 
         if (live && acts) acts[(int64_t)row * S + a.aoff[l] + col] = v;
       }
     }
-    __syncthreads();
+    hl_sync();
+    hl_stamp(dbg, 3 + l);
   }
 }
 
-// out: [loss, count]; pred [G, Do]; acts [G, S] (every layer's output, for the backward)
-__global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* __restrict__ x, int G, MlpArgs a,
-                                                                   const float* __restrict__ target,
-                                                                   const bool* __restrict__ mask, int kind,
-                                                                   float* __restrict__ out, float* __restrict__ pred,
-                                                                   float* __restrict__ acts) {
-  extern __shared__ float sm[];
-  const HlLayout L = hl_layout(a, G);
-  hl_stage(a, L, x, nullptr, G, sm);
-  hl_chain(a, L, G, sm, acts);
-  const int Do = a.dims[a.n], ldo = hl_ld(Do);
-  const float* P = sm + L.act[a.n - 1];
+// pred [G, Do] and the masked loss of the staged chain's output; thread 0 writes out =
+// [loss, count] and every thread returns them (for the fused backward)
+// fixed-order workgroup sum of two doubles: wave shuffle tree, then one thread over the
+// per-wave sums; every thread returns the totals
+__device__ __forceinline__ double2 hl_block_sum2(double s, double c) {
   __shared__ double red[kHlWaves][2];
+  __shared__ double res[2];
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    c += __shfl_xor(c, off);
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[w][0] = s;
+    red[w][1] = c;
+  }
+  hl_sync();
+  if (threadIdx.x == 0) {
+    double ts = 0.0, tc = 0.0;
+    for (int k = 0; k < kHlWaves; ++k) {
+      ts += red[k][0];
+      tc += red[k][1];
+    }
+    res[0] = ts;
+    res[1] = tc;
+  }
+  hl_sync();
+  return make_double2(res[0], res[1]);
+}
+
+template <int NL>
+__device__ float2 hl_loss(const MlpArgs& a, const HlLayout& L, int G, const float* sm,
+                          const float* __restrict__ target, const bool* __restrict__ mask, int kind,
+                          float* __restrict__ out, float* __restrict__ pred) {
+  const int Do = a.dims[NL], ldo = hl_ld(Do);
+  const float* P = sm + L.act[NL - 1];
+  __shared__ double red[kHlWaves][2];
+  __shared__ float res[2];
   double s = 0.0, c = 0.0;
   for (int idx = threadIdx.x; idx < G * Do; idx += kHlThreads) {
     const int r = idx / Do, o = idx % Do;
     const float p = P[r * ldo + o];
     pred[idx] = p;
-    if (mask == nullptr || mask[r]) {
-      s += (double)loss_term_hl(kind, p - target[idx]);
+    if (sm[L.mk + r] != 0.f) {
+      s += (double)loss_term_hl(kind, p - sm[L.tg + idx]);
       c += 1.0;
     }
   }
@@ -533,7 +585,7 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* 
     red[w][0] = s;
     red[w][1] = c;
   }
-  __syncthreads();
+  hl_sync();
   if (threadIdx.x == 0) {
     double ts = 0.0, tc = 0.0;
     for (int k = 0; k < kHlWaves; ++k) {
@@ -542,29 +594,41 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* 
     }
     double l = ts / (tc > 0.0 ? tc : 1.0);
     if (kind == 2) l = sqrt(l);
-    out[0] = (float)l;
-    out[1] = (float)tc;
+    out[0] = res[0] = (float)l;
+    out[1] = res[1] = (float)tc;
   }
+  hl_sync();
+  return make_float2(res[0], res[1]);
 }
 
-// grads: [dW_0 | db_0 | dW_1 | db_1 | ...] (goff), dx [G, D0]
-__global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* __restrict__ gout,
-                                                                   const float* __restrict__ x,
-                                                                   const float* __restrict__ acts, int G, MlpArgs a,
+// out: [loss, count]; pred [G, Do]; acts [G, S] (every layer's output, for the backward)
+template <int NL>
+__global__ void __launch_bounds__(kHlThreads) head_loss_fwd_kernel(const float* __restrict__ x, int G, MlpArgs a,
                                                                    const float* __restrict__ target,
                                                                    const bool* __restrict__ mask, int kind,
-                                                                   const float* __restrict__ fwd,
-                                                                   float* __restrict__ grads, float* __restrict__ dx) {
+                                                                   float* __restrict__ out, float* __restrict__ pred,
+                                                                   float* __restrict__ acts) {
   extern __shared__ float sm[];
-  const HlLayout L = hl_layout(a, G);
-  hl_stage(a, L, x, acts, G, sm);
-  const int n = a.n, Do = a.dims[n];
+  const HlLayout L = hl_layout<NL>(a, G);
+  hl_stage<NL>(a, L, x, nullptr, target, mask, G, sm);
+  hl_chain<NL>(a, L, G, sm, acts);
+  hl_loss<NL>(a, L, G, sm, target, mask, kind, out, pred);
+}
+
+// backward of the staged chain (every activation in LDS) and the loss with upstream gradient
+// g, loss value lv and kept count cnt.  grads: [dW_0 | db_0 | dW_1 | db_1 | ...] (goff),
+// dx [G, D0]
+template <int NL>
+__device__ void hl_backward(const MlpArgs& a, const HlLayout& L, int G, float* sm, const float* __restrict__ target,
+                            const bool* __restrict__ mask, int kind, float g, float lv, float cnt,
+                            float* __restrict__ grads, float* __restrict__ dx, long long* dbg = nullptr) {
+  const int n = NL, Do = a.dims[n];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
   float* DY = sm + L.dy;
   float* DY2 = sm + L.dy2;
   const int ldy = L.ldy;
   {
-    const float g = gout[0], den = fwd[1] > 0.f ? fwd[1] : 1.f, lv = fwd[0];
+    const float den = cnt > 0.f ? cnt : 1.f;
     const bool rl = a.relu[n - 1];
     const float* P = sm + L.act[n - 1];
     const int ldo = hl_ld(Do);
@@ -572,8 +636,8 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
       const int r = idx / Do, o = idx % Do;
       const float p = P[r * ldo + o];
       float v = 0.f;
-      if (mask == nullptr || mask[r]) {
-        const float d = p - target[idx];
+      if (sm[L.mk + r] != 0.f) {
+        const float d = p - sm[L.tg + idx];
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
         switch (kind) {
           case 1: v = sgn / den; break;
@@ -586,7 +650,8 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
       DY[r * ldy + o] = (rl && p <= 0.f) ? 0.f : v;
     }
   }
-  __syncthreads();
+  hl_sync();
+#pragma unroll
   for (int l = n - 1; l >= 0; --l) {
     const int I = a.dims[l], O = a.dims[l + 1];
     const float* ain = sm + (l == 0 ? L.x : L.act[l - 1]);
@@ -597,10 +662,7 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
     const int ti = hl_r16(I) / 16, to = hl_r16(O) / 16;
     for (int t = wv; t < to * ti; t += kHlWaves) {
       const int o0 = (t / ti) * 16, i0 = (t % ti) * 16;
-      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = DY + lg * ldy + o0 + li;
-      const float* bp = ain + lg * lda + i0 + li;
-      for (int k = 0; k < L.Gp / 4; ++k) acc = hl_mfma(ap[4 * k * ldy], bp[4 * k * lda], acc);
+      const f4v_hl acc = hl_dot(DY + lg * ldy + o0 + li, 4 * ldy, ain + lg * lda + i0 + li, 4 * lda, L.Gp / 4);
       const int i = i0 + li;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -608,26 +670,25 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
         if (o < O && i < I) gl[o * I + i] = acc[r];
       }
     }
-    // db[o] = sum_r dy[r, o]
-    for (int o = threadIdx.x; o < O; o += kHlThreads) {
-      float a0 = 0.f, a1 = 0.f;
-      int r = 0;
-      for (; r + 2 <= G; r += 2) {
-        a0 += DY[r * ldy + o];
-        a1 += DY[(r + 1) * ldy + o];
-      }
-      if (r < G) a0 += DY[r * ldy + o];
-      gl[O * I + o] = a0 + a1;
+    // db[o] = sum_r dy[r, o]: 16 lanes per column (rows part, part + 16, ...), folded by a
+    // fixed xor tree
+    for (int c0 = 0; c0 < O; c0 += kHlThreads / 16) {
+      const int o = c0 + (threadIdx.x >> 4), part = threadIdx.x & 15;
+      float v = 0.f;
+      if (o < O)
+        for (int r = part; r < G; r += 16) v += DY[r * ldy + o];
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 1);
+      if (part == 0 && o < O) gl[O * I + o] = v;
     }
     // da = DY W (K = O; DY columns >= O and W rows >= O are zero), masked by ReLU'(A_in)
     const bool msk = l > 0 && a.relu[l - 1];
     const int K4 = (O + 3) / 4;
     for (int t = wv; t < (L.Gp / 16) * ti; t += kHlWaves) {
       const int r0 = (t / ti) * 16, i0 = (t % ti) * 16;
-      f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = DY + (r0 + li) * ldy + lg;
-      const float* bp = W + lg * lda + i0 + li;
-      for (int k = 0; k < K4; ++k) acc = hl_mfma(ap[4 * k], bp[4 * k * lda], acc);
+      const f4v_hl acc = hl_dot(DY + (r0 + li) * ldy + lg, 4, W + lg * lda + i0 + li, 4 * lda, K4);
       const int col = i0 + li;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -642,14 +703,181 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* 
         }
       }
     }
-    __syncthreads();
+    hl_sync();
+    hl_stamp(dbg, 20 + l);
     float* t = DY;
     DY = DY2;
     DY2 = t;
   }
 }
 
-static size_t hl_lds(const MlpArgs& a, int G) { return sizeof(float) * (size_t)hl_layout(a, G).total; }
+template <int NL>
+__global__ void __launch_bounds__(kHlThreads) head_loss_bwd_kernel(const float* __restrict__ gout,
+                                                                   const float* __restrict__ x,
+                                                                   const float* __restrict__ acts, int G, MlpArgs a,
+                                                                   const float* __restrict__ target,
+                                                                   const bool* __restrict__ mask, int kind,
+                                                                   const float* __restrict__ fwd,
+                                                                   float* __restrict__ grads, float* __restrict__ dx) {
+  extern __shared__ float sm[];
+  const HlLayout L = hl_layout<NL>(a, G);
+  hl_stage<NL>(a, L, x, acts, target, mask, G, sm);
+  hl_backward<NL>(a, L, G, sm, target, mask, kind, gout[0], fwd[0], fwd[1], grads, dx);
+}
+
+// forward, loss and the backward for a unit upstream gradient in ONE launch: the chain's
+// activations never leave LDS and the backward launch (a second staging of every weight and
+// activation) disappears from the step; _HeadLoss.backward scales by g unless g is the
+// training step's unit seed
+template <int NL>
+__global__ void __launch_bounds__(kHlThreads) head_loss_fused_kernel(const float* __restrict__ x, int G, MlpArgs a,
+                                                                     const float* __restrict__ target,
+                                                                     const bool* __restrict__ mask, int kind,
+                                                                     float* __restrict__ out,
+                                                                     float* __restrict__ pred,
+                                                                     float* __restrict__ grads,
+                                                                     float* __restrict__ dx, long long* dbg) {
+  hl_stamp(dbg, 0);
+  extern __shared__ float sm[];
+  const HlLayout L = hl_layout<NL>(a, G);
+  hl_stamp(dbg, 1);
+  hl_stage<NL>(a, L, x, nullptr, target, mask, G, sm);
+  hl_stamp(dbg, 2);
+  hl_chain<NL>(a, L, G, sm, nullptr, dbg);
+  const float2 lc = hl_loss<NL>(a, L, G, sm, target, mask, kind, out, pred);
+  hl_stamp(dbg, 19);
+  hl_backward<NL>(a, L, G, sm, target, mask, kind, 1.f, lc.x, lc.y, grads, dx, dbg);
+  hl_stamp(dbg, 31);
+}
+
+// ------------------------------------------------------------------------------------
+// Row-split head + loss + backward (the training path, ops/mlp.py _HeadLoss fused): one
+// workgroup per kHlRows rows.  A single workgroup runs every layer on ONE CU's matrix cores
+// (a 33-row x 64-wide layer is ~1.5k MFMA cycles there, and the backward twice that), so the
+// one-workgroup kernels above spend most of their time MFMA-bound on a nearly idle chip.
+// Rows are independent through the forward chain, the loss terms and the backward's dgrad
+// chain; only the weight gradients (sums over rows) and the loss (a mean) couple the
+// workgroups: each writes its dW/db partial slab and loss partial, draws an agent-scope
+// ticket, and the last arriver sums the slabs in workgroup order (deterministic) and writes
+// the loss.  Every workgroup counts the kept elements of the whole batch itself (the loss
+// normalisation), so no other cross-workgroup step exists.  RMSE's dpred = d / (n lv) needs
+// the global loss lv: the workgroups seed d / n and the reducer rescales dW, db and dx by 1/lv.
+constexpr int kHlRows = 16;
+
+__device__ __forceinline__ bool hl_arrive(int* counter, int expected) {
+  __shared__ int flag;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int tk = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (tk == expected - 1);
+  }
+  __syncthreads();
+  if (!flag) return false;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *counter = 0;  // reset for the next launch (every ticket of this launch is drawn)
+  }
+  __syncthreads();
+  return true;
+}
+
+template <int NL>
+__global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
+    const float* __restrict__ x, int G, MlpArgs a, const float* __restrict__ target, const bool* __restrict__ mask,
+    int kind, float* __restrict__ out, float* __restrict__ pred, float* __restrict__ grads, float* __restrict__ dx,
+    float* __restrict__ part, double* __restrict__ lpart, int* __restrict__ cnt, long long* dbg) {
+  hl_stamp(dbg, 0);
+  extern __shared__ float sm[];
+  const int R = gridDim.x, b = blockIdx.x, row0 = b * kHlRows, Gl = min(kHlRows, G - row0);
+  const int Do = a.dims[NL], D0 = a.dims[0], nw = a.goff[NL];
+  const HlLayout L = hl_layout<NL>(a, Gl);
+  // kept elements of the whole batch (loads issued ahead of the staging wait)
+  double kc = 0.0;
+  for (int r = threadIdx.x; r < G; r += kHlThreads) kc += (mask == nullptr || mask[r]) ? (double)Do : 0.0;
+  hl_stamp(dbg, 1);
+  hl_stage<NL>(a, L, x + (int64_t)row0 * D0, nullptr, target + (int64_t)row0 * Do,
+               mask == nullptr ? nullptr : mask + row0, Gl, sm);
+  hl_stamp(dbg, 2);
+  hl_chain<NL>(a, L, Gl, sm, nullptr, dbg);
+  const float* P = sm + L.act[NL - 1];
+  const int ldo = hl_ld(Do);
+  double ls = 0.0;
+  for (int idx = threadIdx.x; idx < Gl * Do; idx += kHlThreads) {
+    const int r = idx / Do, o = idx % Do;
+    const float p = P[r * ldo + o];
+    pred[(int64_t)row0 * Do + idx] = p;
+    if (sm[L.mk + r] != 0.f) ls += (double)loss_term_hl(kind, p - sm[L.tg + idx]);
+  }
+  const double2 tot = hl_block_sum2(ls, kc);
+  hl_stamp(dbg, 19);
+  // lv = 1: RMSE's 1 / lv is applied by the reducer
+  hl_backward<NL>(a, L, Gl, sm, target, mask, kind, 1.f, 1.f, (float)tot.y, part + (int64_t)b * nw,
+                  dx + (int64_t)row0 * D0, dbg);
+  if (threadIdx.x == 0) lpart[b] = tot.x;
+  if (!hl_arrive(cnt, R)) return;
+  __shared__ float scale_s;
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < R; ++k) t += lpart[k];
+    const double tc = tot.y;
+    double l = t / (tc > 0.0 ? tc : 1.0);
+    float sc = 1.f;
+    if (kind == 2) {
+      l = sqrt(l);
+      sc = l > 0.0 ? (float)(1.0 / l) : 0.f;
+    }
+    out[0] = (float)l;
+    out[1] = (float)tc;
+    scale_s = sc;
+  }
+  __syncthreads();
+  const float sc = scale_s;
+  for (int e = threadIdx.x; e < nw; e += kHlThreads) {
+    float v = 0.f;
+    for (int k = 0; k < R; ++k) v += part[(int64_t)k * nw + e];
+    grads[e] = v * sc;
+  }
+  if (kind == 2)
+    for (int e = threadIdx.x; e < G * D0; e += kHlThreads) dx[e] *= sc;
+  hl_stamp(dbg, 31);
+}
+
+#define HL_NL_SWITCH(n, F)                                        \
+  switch (n) {                                                    \
+    case 1: F(1); break;                                          \
+    case 2: F(2); break;                                          \
+    case 3: F(3); break;                                          \
+    case 4: F(4); break;                                          \
+    case 5: F(5); break;                                          \
+    case 6: F(6); break;                                          \
+    case 7: F(7); break;                                          \
+    case 8: F(8); break;                                          \
+    default: HY_CHECK(false, "head_loss: 1..8 layers");           \
+  }
+static_assert(kMlpMaxLayers == 8, "HL_NL_SWITCH covers 1..8 layers");
+
+static size_t hl_lds(const MlpArgs& a, int G) {
+  size_t r = 0;
+#define HL_LDS(N) r = sizeof(float) * (size_t)hl_layout<N>(a, G).total
+  HL_NL_SWITCH(a.n, HL_LDS)
+#undef HL_LDS
+  return r;
+}
+
+template <int N>
+static void hl_attrs() {
+  hipFuncSetAttribute((const void*)head_loss_fwd_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)kHlMaxLds);
+  hipFuncSetAttribute((const void*)head_loss_bwd_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)kHlMaxLds);
+  hipFuncSetAttribute((const void*)head_loss_fused_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)kHlMaxLds);
+  hipFuncSetAttribute((const void*)head_loss_rows_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)kHlMaxLds);
+}
 
 static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::optional<at::Tensor>& mask,
                       const MlpArgs& a, int64_t kind) {
@@ -662,10 +890,14 @@ static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::
              "head_loss: bool mask [G]");
   HY_CHECK(G >= 1 && hl_lds(a, (int)G) <= kHlMaxLds, "head_loss: rows x widths exceed one workgroup's LDS");
   static bool once = [] {
-    hipFuncSetAttribute((const void*)head_loss_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)kHlMaxLds);
-    hipFuncSetAttribute((const void*)head_loss_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)kHlMaxLds);
+    hl_attrs<1>();
+    hl_attrs<2>();
+    hl_attrs<3>();
+    hl_attrs<4>();
+    hl_attrs<5>();
+    hl_attrs<6>();
+    hl_attrs<7>();
+    hl_attrs<8>();
     return true;
   }();
   (void)once;
@@ -687,9 +919,13 @@ std::vector<at::Tensor> head_loss_fwd(const at::Tensor& x_, at::TensorList Ws_, 
   auto pred = at::empty({G, a.dims[a.n]}, x.options());
   auto acts = at::empty({G, a.aoff[a.n]}, x.options());
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
-  head_loss_fwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
-      x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),
-      pred.data_ptr<float>(), acts.data_ptr<float>());
+  const size_t lds = hl_lds(a, (int)G);
+#define HL_FWD(N)                                                                                                \
+  head_loss_fwd_kernel<N><<<1, kHlThreads, lds, stream()>>>(x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), \
+                                                            mp, (int)kind, stats.data_ptr<float>(),                 \
+                                                            pred.data_ptr<float>(), acts.data_ptr<float>())
+  HL_NL_SWITCH(a.n, HL_FWD)
+#undef HL_FWD
   return {stats, pred, acts};
 }
 
@@ -709,11 +945,75 @@ std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& 
   auto flat = at::empty({a.goff[a.n]}, x.options());
   auto dx = at::empty_like(x);
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
-  head_loss_bwd_kernel<<<1, kHlThreads, hl_lds(a, (int)G), stream()>>>(
-      gout.data_ptr<float>(), x.data_ptr<float>(), acts.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp,
-      (int)kind,
-      stats.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>());
+  const size_t lds = hl_lds(a, (int)G);
+#define HL_BWD(N)                                                                                               \
+  head_loss_bwd_kernel<N><<<1, kHlThreads, lds, stream()>>>(                                                    \
+      gout.data_ptr<float>(), x.data_ptr<float>(), acts.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), \
+      mp, (int)kind, stats.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>())
+  HL_NL_SWITCH(a.n, HL_BWD)
+#undef HL_BWD
   std::vector<at::Tensor> out{dx};
+  for (int l = 0; l < a.n; ++l) {
+    const int O = a.dims[l + 1], I = a.dims[l];
+    out.push_back(flat.narrow(0, a.goff[l], O * I).view({O, I}));
+    out.push_back(flat.narrow(0, a.goff[l] + O * I, O));
+  }
+  return out;
+}
+
+// returns [stats [2], pred [G, out], dx, dW_0, db_0, dW_1, db_1, ...] (gradients of the loss
+// itself, upstream gradient 1)
+std::vector<at::Tensor> head_loss_fused(const at::Tensor& x_, at::TensorList Ws_, at::TensorList bs_,
+                                        at::IntArrayRef relu, const at::Tensor& target,
+                                        const c10::optional<at::Tensor>& mask, int64_t kind,
+                                        const c10::optional<at::Tensor>& dbg) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK(x.dim() == 2, "head_loss: x must be [G, D]");
+  std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
+  auto a = make_args(x, Ws, bs, relu.vec());
+  hl_checks(x, target, mask, a, kind);
+  long long* dp = nullptr;
+  if (dbg.has_value() && dbg->defined()) {
+    HY_CHECK(dbg->is_cuda() && dbg->scalar_type() == at::kLong && dbg->is_contiguous() && dbg->numel() >= 32,
+             "head_loss_fused: dbg must be int64 [>= 32]");
+    dp = (long long*)dbg->data_ptr<int64_t>();
+  }
+  const int64_t G = x.size(0);
+  auto stats = at::empty({2}, x.options());
+  auto pred = at::empty({G, a.dims[a.n]}, x.options());
+  auto flat = at::empty({a.goff[a.n]}, x.options());
+  auto dx = at::empty_like(x);
+  const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
+  // row-split launch (head_loss_rows_kernel); HYDRA_HEADLOSS_ROWS=0: the one-workgroup kernel
+  static const bool rows_split = [] {
+    const char* e = std::getenv("HYDRA_HEADLOSS_ROWS");
+    return e == nullptr || std::string(e) != "0";
+  }();
+  if (rows_split) {
+    const int R = (int)ceil_div(G, (int64_t)kHlRows);
+    const size_t lds = hl_lds(a, (int)std::min<int64_t>(G, kHlRows));
+    auto part = at::empty({(int64_t)R * a.goff[a.n]}, x.options());
+    auto lpart = at::empty({R}, x.options().dtype(at::kDouble));
+    auto cnt = at::zeros({1}, x.options().dtype(at::kInt));
+#define HL_ROWS(N)                                                                                              \
+  head_loss_rows_kernel<N><<<R, kHlThreads, lds, stream()>>>(                                                   \
+      x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),         \
+      pred.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(),             \
+      lpart.data_ptr<double>(), cnt.data_ptr<int>(), dp)
+    HL_NL_SWITCH(a.n, HL_ROWS)
+#undef HL_ROWS
+  } else {
+    const size_t lds = hl_lds(a, (int)G);
+#define HL_FUSED(N)                                                                                            \
+  head_loss_fused_kernel<N><<<1, kHlThreads, lds, stream()>>>(                                                 \
+      x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),        \
+      pred.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>(), dp)
+    HL_NL_SWITCH(a.n, HL_FUSED)
+#undef HL_FUSED
+  }
+  std::vector<at::Tensor> out{stats, pred, dx};
   for (int l = 0; l < a.n; ++l) {
     const int O = a.dims[l + 1], I = a.dims[l];
     out.push_back(flat.narrow(0, a.goff[l], O * I).view({O, I}));
@@ -735,6 +1035,10 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "head_loss_bwd(Tensor gout, Tensor x, Tensor acts, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, "
       "Tensor? mask, Tensor stats, int kind) -> Tensor[]");
+  m.def(
+      "head_loss_fused(Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, int kind, "
+      "Tensor? dbg=None) -> "
+      "Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
@@ -742,4 +1046,5 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("mlp_bwd", hy::mlp_bwd);
   m.impl("head_loss_fwd", hy::head_loss_fwd);
   m.impl("head_loss_bwd", hy::head_loss_bwd);
+  m.impl("head_loss_fused", hy::head_loss_fused);
 }

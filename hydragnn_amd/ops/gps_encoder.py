@@ -27,6 +27,8 @@ Used in GPU training mode when every layer matches the pattern (``eligible``); C
 eval, double-backward (composite mode) and any other configuration run the module path.
 ``HYDRA_UNFUSED=gpsfused`` switches it off.
 """
+import os
+
 import torch
 
 from .. import _native
@@ -339,6 +341,14 @@ class _GPSEncoder(torch.autograd.Function):
         drbf = None
         dx0 = None
         wg = []  # per layer: (dWab, (dWr, dbc), dWd)
+        # layer l's weight gradients are launched on a third stream as soon as its backward
+        # is enqueued, overlapping layer l-1's latency-bound backward (the last layer's,
+        # plus the embeddings', stay on the main stream at the end)
+        wside = cfg.side and os.environ.get("HYDRA_WGRAD_OVERLAP", "1") == "1"
+        if wside:
+            wmain = torch.cuda.current_stream(dev)
+            wstream = _streams.side_stream(dev, 2)
+        lo = 0
         for l in reversed(range(L)):
             s = st[l]
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
@@ -390,6 +400,11 @@ class _GPSEncoder(torch.autograd.Function):
             gw["W1"] = item(dpre, s["out"], W1, True)
             gw["W2"] = item(dg, s["md"], W2, True)
             wg.append((l, gw))
+            if wside and l > 0:
+                wstream.wait_stream(wmain)
+                with torch.cuda.stream(wstream):
+                    ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+                lo = len(dys)
             grads[base + 12], grads[base + 13] = dw1n, db1n
             grads[base + 14], grads[base + 15] = dw2n, db2n
             grads[base + 16], grads[base + 17] = dw3, db3
@@ -400,7 +415,9 @@ class _GPSEncoder(torch.autograd.Function):
         te = [item(de, eattr, (F, eattr.shape[1]), False)[0], item(de, rpe, (F, rpe.shape[1]), False)[0]]
         # every weight gradient of the stack (incl. the radial basis and its frequencies): one
         # grouped launch pair
-        ops.linear_wgrad_grouped(dys, xs, dws, dbs, [0] * len(dys))
+        ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+        if wside:
+            wmain.wait_stream(wstream)  # (dys/xs/dws hold every operand alive until here)
         # weight-prep backward of every layer, embedding weights and dfreq: one launch
         wp = []
         for l, gw in wg:

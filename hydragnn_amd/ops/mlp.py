@@ -6,6 +6,8 @@ GPU a chain of up to 8 Linear(+ReLU) layers of width <= 128 over <= 1024 rows is
 one forward and two backward launches; anything else (CPU, other activations,
 composite/double-backward mode) runs the modules as written.
 """
+import os
+
 import torch
 from torch import nn
 
@@ -90,9 +92,10 @@ def _hl_lds(G, dims):
     r16 = lambda v: (v + 15) // 16 * 16
     ld = lambda c: r16(c) + 1
     Gp = r16(G)
-    w = sum(r16(dims[i + 1]) * ld(dims[i]) for i in range(len(dims) - 1))
+    w = sum(r16(dims[i + 1]) * ld(dims[i]) + r16(dims[i + 1]) for i in range(len(dims) - 1))
     acts = sum(Gp * ld(d) for d in dims[1:])
-    return 4 * (w + Gp * ld(dims[0]) + acts + 2 * Gp * ld(max(dims)))
+    # + targets [G][out] and the row mask [Gp]
+    return 4 * (w + Gp * ld(dims[0]) + acts + 2 * Gp * ld(max(dims)) + G * dims[-1] + Gp)
 
 
 def head_loss_layers(seqs, G, in_dim, kind):
@@ -111,30 +114,60 @@ def head_loss_layers(seqs, G, in_dim, kind):
     return layers
 
 
+def mark_unit_seed(t):
+    """Declare ``t`` a persistent all-ones backward seed (the training step's d loss / d loss):
+    a fused head+loss whose upstream gradient IS this tensor returns its precomputed
+    gradients without a scaling launch."""
+    t._hydra_unit_seed = True
+    return t
+
+
 class _HeadLoss(torch.autograd.Function):
-    """loss = masked_loss(MLP(x), target) as one forward and one backward launch."""
+    """loss = masked_loss(MLP(x), target) as one forward and one backward launch; with
+    ``fused`` (training), the forward launch also computes every gradient for a unit
+    upstream gradient (``head_loss_fused``) and the backward only scales them by ``g`` —
+    nothing at all when ``g`` is the step's unit seed (``mark_unit_seed``)."""
 
     @staticmethod
-    def forward(ctx, x, target, mask, kind, relu, *params):
+    def forward(ctx, x, target, mask, kind, relu, fused, *params):
+        ctx.fused = fused
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for pred
+        if fused:
+            out = _native.ops().head_loss_fused(x, params[0::2], params[1::2], relu, target, mask, kind)
+            stats, pred = out[0], out[1]
+            ctx.grads = out[2:]
+            ctx.mark_non_differentiable(pred)
+            return stats[0], pred
         stats, pred, acts = _native.ops().head_loss_fwd(x, params[0::2], params[1::2], relu, target, mask, kind)
         ctx.save_for_backward(x, acts, target, mask, stats, *params)
         ctx.kind, ctx.relu = kind, relu
         ctx.mark_non_differentiable(pred)
-        ctx.set_materialize_grads(False)  # no zero-filled gradient for pred
         return stats[0], pred
 
     @staticmethod
     def backward(ctx, g, _gpred):
+        if ctx.fused:
+            grads = ctx.grads
+            ctx.grads = None
+            if g is None:
+                return (None,) * (6 + len(grads) - 1)
+            if not getattr(g, "_hydra_unit_seed", False):
+                grads = [t * g for t in grads]
+            return (grads[0], None, None, None, None, None, *grads[1:])
         x, acts, target, mask, stats, *params = ctx.saved_tensors
         out = _native.ops().head_loss_bwd(g.reshape(1).contiguous(), x, acts, params[0::2], params[1::2], ctx.relu,
                                           target, mask, stats, ctx.kind)
-        return (out[0], None, None, None, None, *out[1:])
+        return (out[0], None, None, None, None, None, *out[1:])
 
 
-def head_loss(x, layers, target, mask, kind):
-    """(loss, pred) of a masked-loss graph head over the pooled features ``x``."""
+def head_loss(x, layers, target, mask, kind, fused=None):
+    """(loss, pred) of a masked-loss graph head over the pooled features ``x``.  ``fused``
+    (default: when grad mode is on; ``HYDRA_HEADLOSS_FUSED=0`` disables): gradients computed
+    inside the forward launch (see ``_HeadLoss``)."""
     params = []
     for m, _ in layers:
         params += [m.weight, m.bias]
+    if fused is None:
+        fused = torch.is_grad_enabled() and os.environ.get("HYDRA_HEADLOSS_FUSED", "1") == "1"
     return _HeadLoss.apply(x.contiguous(), target.contiguous(), None if mask is None else mask.contiguous(),
-                           _KIND[kind], [int(r) for _, r in layers], *params)
+                           _KIND[kind], [int(r) for _, r in layers], bool(fused), *params)

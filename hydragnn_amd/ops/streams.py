@@ -24,7 +24,8 @@ def enabled(t):
 
 def side_stream(device, slot=0):
     """Cached side stream ``slot`` of ``device`` (slot 0: branch forks; slot 1: the
-    attention backward's dK/dV pass, which forks again from inside a side branch)."""
+    attention backward's dK/dV pass, which forks again from inside a side branch;
+    slot 2: the fused GPS backward's per-layer weight gradients)."""
     key = (torch.device(device).index, slot)
     s = _side.get(key)
     if s is None:

@@ -366,6 +366,9 @@ class TrainStep:
             if torch.cuda.is_available() and loss.is_cuda and torch.cuda.is_current_stream_capturing():
                 return None  # never allocate inside a capture; the warm-up run has created it
             one = self._one = torch.ones_like(loss, memory_format=torch.contiguous_format)
+            from ..ops.mlp import mark_unit_seed
+
+            mark_unit_seed(one)
         return one
 
     def eager(self, store, indices):

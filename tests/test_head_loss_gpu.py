@@ -21,10 +21,11 @@ def _ref_loss(kind, pred, target, mask):
     return l.sqrt() if kind == "rmse" else l
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("kind", ["mae", "mse", "rmse", "smooth_l1"])
 @pytest.mark.parametrize("G,dims,masked", [(33, [64, 50, 50, 50, 25, 1], True), (1, [32, 16, 1], False),
                                            (100, [64, 64, 3], True)])
-def test_head_loss_matches_torch(kind, G, dims, masked):
+def test_head_loss_matches_torch(kind, G, dims, masked, fused):
     dev = torch.device("cuda")
     torch.manual_seed(G + len(dims))
     lins = [torch.nn.Linear(dims[i], dims[i + 1]).to(dev) for i in range(len(dims) - 1)]
@@ -39,7 +40,7 @@ def test_head_loss_matches_torch(kind, G, dims, masked):
     mask = (torch.arange(G, device=dev) < max(1, G - 2)) if masked else None
     layers = _mlp.head_loss_layers([seq], G, dims[0], kind)
     assert layers is not None
-    loss, pred = _mlp.head_loss(x, layers, target, mask, kind)
+    loss, pred = _mlp.head_loss(x, layers, target, mask, kind, fused=fused)
     gx, *gw = torch.autograd.grad(loss * 1.7, [x] + [p for l in lins for p in (l.weight, l.bias)])
 
     xr = x.detach().clone().requires_grad_(True)
@@ -51,3 +52,29 @@ def test_head_loss_matches_torch(kind, G, dims, masked):
     torch.testing.assert_close(gx, gxr, rtol=1e-4, atol=1e-6)
     for a, b in zip(gw, gwr):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+def test_head_loss_fused_unit_seed():
+    """The fused path returns its in-forward gradients unscaled for a marked unit seed (the
+    training step's), and scales them for any other upstream gradient."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    dims = [64, 50, 25, 1]
+    seq = torch.nn.Sequential(torch.nn.Linear(64, 50), torch.nn.ReLU(), torch.nn.Linear(50, 25), torch.nn.ReLU(),
+                              torch.nn.Linear(25, 1)).to(dev)
+    params = list(seq.parameters())
+    x = torch.randn(33, dims[0], device=dev, requires_grad=True)
+    target = torch.randn(33, 1, device=dev)
+    layers = _mlp.head_loss_layers([seq], 33, 64, "mae")
+    ref = None
+    for seed in (_mlp.mark_unit_seed(torch.ones((), device=dev)), torch.ones((), device=dev),
+                 torch.full((), 2.0, device=dev)):
+        for p in params + [x]:
+            p.grad = None
+        loss, _ = _mlp.head_loss(x, layers, target, None, "mae", fused=True)
+        torch.autograd.backward(loss, seed)
+        got = [x.grad.clone()] + [p.grad.clone() for p in params]
+        if ref is None:
+            ref = got
+        for a, b in zip(got, ref):
+            torch.testing.assert_close(a, b * float(seed), rtol=1e-6, atol=1e-7)

@@ -39,8 +39,23 @@ def main():
         g = torch.ones(1, device=dev)
         tf = bench(lambda: ops.head_loss_fwd(x, Ws, bs, relu, t, m, 1))
         tb = bench(lambda: ops.head_loss_bwd(g, x, acts, Ws, bs, relu, t, m, stats, 1))
+        tu = bench(lambda: ops.head_loss_fused(x, Ws, bs, relu, t, m, 1))
         to = bench(lambda: ops.mlp_fwd(x, Ws, bs, relu))
-        print(f"G {G:4d} dims {dims}: head_loss fwd {tf:7.1f} us  bwd {tb:7.1f} us   (mlp_fwd {to:6.1f} us)", flush=True)
+        dbg = torch.zeros(32, dtype=torch.int64, device=dev)
+        ops.head_loss_fused(x, Ws, bs, relu, t, m, 1, dbg)
+        torch.cuda.synchronize()
+        st = dbg.cpu().tolist()
+        n = len(dims) - 1
+        marks = [("start", 0), ("layout", 1), ("stage", 2)] + [(f"fwd{l}", 3 + l) for l in range(n)] + \
+                [("loss", 19)] + [(f"bwd{l}", 20 + l) for l in reversed(range(n))] + [("end", 31)]
+        prev = st[0]
+        txt = []
+        for name, i in marks:
+            txt.append(f"{name} +{st[i] - prev}")
+            prev = st[i]
+        print("   stamps (shader clocks, s_memtime): " + ", ".join(txt), flush=True)
+        print(f"G {G:4d} dims {dims}: head_loss fwd {tf:7.1f} us  bwd {tb:7.1f} us  fused fwd+bwd {tu:7.1f} us"
+              f"   (mlp_fwd {to:6.1f} us)", flush=True)
 
 
 if __name__ == "__main__":

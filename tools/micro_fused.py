@@ -74,6 +74,19 @@ def main():
     print(f"radial_fwd {graph_us(lambda: ops.radial_fwd(dist, freq, We, be, Wl, 10.0, 5), reps):8.2f} us", flush=True)
     print(f"radial_bwd {graph_us(lambda: ops.radial_bwd(list(dR.unbind(0)), list(dG.unbind(0)), R, dist, freq, We, Wl, 10.0, 5), reps):8.2f} us",
           flush=True)
+    Ee = 26624  # edges of the headline batch (1664 row blocks of 16)
+    r = torch.randn(Ee, F, device=dev)
+    e = torch.randn(Ee, F, device=dev)
+    Wr, Wd = torch.randn(F, F, device=dev) * 0.1, torch.randn(F, F, device=dev) * 0.1
+    bc = torch.randn(F, device=dev)
+    print(f"gf_edge_fwd E={Ee} {graph_us(lambda: ops.gf_edge_fwd(r, e, Wr, Wd, bc), reps):8.2f} us", flush=True)
+    dC, dGe = torch.randn(Ee, F, device=dev), torch.randn(Ee, F, device=dev)
+    Wemb, Wrl = torch.randn(F, K, device=dev), torch.randn(F, K, device=dev)
+    de = torch.zeros(Ee, F, device=dev)
+    drbf = torch.zeros(Ee, K, device=dev)
+    print(f"gf_edge_bwd E={Ee} {graph_us(lambda: ops.gf_edge_bwd(dC, Wr, Wd, r, de, dGe, Wemb, Wrl, drbf, K), reps):8.2f} us",
+          flush=True)
+    print(f"copy [E,F] {graph_us(lambda: r.clone(), reps):8.2f} us", flush=True)
     z = torch.zeros(256, device=dev)
     print(f"floor fill(256) {graph_us(lambda: z.fill_(1.0), reps):8.2f} us", flush=True)
 
