@@ -1010,7 +1010,15 @@ struct EdgeFwd {
 };
 
 template <int F, int D>
+__device__ __forceinline__ void edge_fwd_body(const EdgeFwd& a);
+
+template <int F, int D>
 __global__ void __launch_bounds__(256) edge_fwd_kernel(EdgeFwd a) {
+  edge_fwd_body<F, D>(a);
+}
+
+template <int F, int D>
+__device__ __forceinline__ void edge_fwd_body(const EdgeFwd& a) {
   constexpr int K = F + D, LD = K + 4;
   __shared__ __attribute__((aligned(16))) float xs[BM * LD];
   const int row0 = blockIdx.x * BM;
@@ -1035,6 +1043,27 @@ __global__ void __launch_bounds__(256) edge_fwd_kernel(EdgeFwd a) {
       if (row < a.E) a.C[(int64_t)row * F + col] = acc[r] + bias;
     }
   }
+}
+
+// Every layer's edge term in ONE launch (blockIdx.y = layer), the 16-row body above per
+// workgroup.  (A 64-row form with the layer's [Wr | Wd] staged in LDS ran slower, 35.6 vs
+// 3 x 10.3 us on MI355X: 67 KB of LDS left 2 workgroups per CU and nothing overlapped the
+// staging loads.)
+constexpr int kEdgeMaxL = 8;
+struct EdgeFwdMulti {
+  const float* r[kEdgeMaxL];   // [E, F] per layer
+  const float* e;              // [E, D]
+  const float* Wr[kEdgeMaxL];  // [F, F]
+  const float* Wd[kEdgeMaxL];  // [F, D]
+  const float* bc[kEdgeMaxL];  // [F]
+  float* C[kEdgeMaxL];         // [E, F]
+  int E;
+};
+
+template <int F, int D>
+__global__ void __launch_bounds__(256) edge_fwd_multi_kernel(EdgeFwdMulti m) {
+  const int l = blockIdx.y;
+  edge_fwd_body<F, D>(EdgeFwd{m.r[l], m.e, m.Wr[l], m.Wd[l], m.bc[l], m.C[l], m.E});
 }
 
 struct EdgeBwd {
@@ -1149,7 +1178,8 @@ template <int F>
 __global__ void __launch_bounds__(256) emb_fwd_kernel(EmbFwd a) {
   constexpr int LD = 2 * F + 4;
   __shared__ __attribute__((aligned(16))) float abs_[BM * LD];
-  __shared__ float in[BM][33];  // [A | B] of the tile, <= 16 + 16 columns
+  __shared__ float in[BM][33];       // [A | B] of the tile, <= 16 + 16 columns
+  __shared__ float wab[2 * F][17];   // [Wa ; Wb] rows (<= 16 columns each), staged with the tile
   const int row0 = blockIdx.x * BM;
   const int kt = a.ka + a.kb;
   for (int idx = threadIdx.x; idx < BM * kt; idx += 256) {
@@ -1158,15 +1188,24 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(EmbFwd a) {
     if (row < a.M) v = c < a.ka ? a.A[(int64_t)row * a.ka + c] : a.B[(int64_t)row * a.kb + (c - a.ka)];
     in[r][c] = v;
   }
+  // (the first-stage weights were read from global memory inside the dot loops below: a
+  // dependent L2 round trip per k, ~10 us of the edge embedding's 14)
+  for (int idx = threadIdx.x; idx < F * kt; idx += 256) {
+    const int c = idx / kt, k = idx % kt;
+    if (k < a.ka)
+      wab[c][k] = a.Wa[c * a.ka + k];
+    else
+      wab[F + c][k - a.ka] = a.Wb[c * a.kb + (k - a.ka)];
+  }
   __syncthreads();
   // first stage (K <= 16): plain fp32 dot products, one output per thread-iteration
   for (int idx = threadIdx.x; idx < BM * 2 * F; idx += 256) {
     const int r = idx / (2 * F), c = idx % (2 * F);
     float acc = 0.f;
     if (c < F) {
-      for (int k = 0; k < a.ka; ++k) acc = fmaf(in[r][k], a.Wa[c * a.ka + k], acc);
+      for (int k = 0; k < a.ka; ++k) acc = fmaf(in[r][k], wab[c][k], acc);
     } else {
-      for (int k = 0; k < a.kb; ++k) acc = fmaf(in[r][a.ka + k], a.Wb[(c - F) * a.kb + k], acc);
+      for (int k = 0; k < a.kb; ++k) acc = fmaf(in[r][a.ka + k], wab[c][k], acc);
     }
     abs_[r * LD + c] = acc;
   }
@@ -1533,6 +1572,37 @@ std::vector<at::Tensor> gf_final_fwd(const at::Tensor& z3, const at::Tensor& acc
       HY_CHECK(false, "gps_fused edge kernels: (F, D) = (64, 64) or (32, 32)");     \
   } while (0)
 
+// [C_0, C_1, ...] = r_l Wr_l^T + e Wd_l^T + bc_l for every layer, one launch
+std::vector<at::Tensor> gf_edge_fwd_multi(at::TensorList rs, const at::Tensor& e, at::TensorList Wrs,
+                                          at::TensorList Wds, at::TensorList bcs) {
+  const int L = (int)rs.size();
+  HY_CHECK(L >= 1 && L <= kEdgeMaxL && (int)Wrs.size() == L && (int)Wds.size() == L && (int)bcs.size() == L,
+           "gf_edge_fwd_multi: 1..8 layers");
+  const int64_t E = rs[0].size(0), F = rs[0].size(1), D = e.size(1);
+  chk(e, E, D, "e");
+  EdgeFwdMulti a{};
+  a.e = e.data_ptr<float>();
+  a.E = (int)E;
+  std::vector<at::Tensor> out;
+  for (int l = 0; l < L; ++l) {
+    chk(rs[l], E, F, "r");
+    chk(Wrs[l], F, F, "Wr");
+    chk(Wds[l], F, D, "Wd");
+    HY_CHECK(bcs[l].is_contiguous() && bcs[l].numel() == F, "gf_edge_fwd_multi: bc [F]");
+    auto C = at::empty({E, F}, e.options());
+    a.r[l] = rs[l].data_ptr<float>();
+    a.Wr[l] = Wrs[l].data_ptr<float>();
+    a.Wd[l] = Wds[l].data_ptr<float>();
+    a.bc[l] = bcs[l].data_ptr<float>();
+    a.C[l] = C.data_ptr<float>();
+    out.push_back(C);
+  }
+  if (E == 0) return out;
+  const dim3 grid((unsigned)ceil_div(E, (int64_t)BM), (unsigned)L);
+  HY_GF_EDGE(F, D, edge_fwd_multi_kernel, grid, a);
+  return out;
+}
+
 at::Tensor gf_edge_fwd(const at::Tensor& r, const at::Tensor& e, const at::Tensor& Wr, const at::Tensor& Wd,
                        const at::Tensor& bc) {
   const int64_t E = r.size(0), F = r.size(1), D = e.size(1);
@@ -1836,6 +1906,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor");
   m.def("gf_finish(Tensor[] wp, Tensor[] em, Tensor? dfw) -> Tensor[]");
   m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
+  m.def("gf_edge_fwd_multi(Tensor[] r, Tensor e, Tensor[] Wr, Tensor[] Wd, Tensor[] bc) -> Tensor[]");
   m.def(
       "gf_edge_bwd(Tensor dC, Tensor Wr, Tensor Wd, Tensor? rmask, Tensor(a!)? de_acc, Tensor? dG, Tensor? Wemb, "
       "Tensor? Wlin, Tensor(b!)? drbf_acc, int K) -> Tensor[]");
@@ -1866,6 +1937,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gf_embed_fwd", hy::gf::gf_embed_fwd);
   m.impl("gf_finish", hy::gf::gf_finish);
   m.impl("gf_edge_fwd", hy::gf::gf_edge_fwd);
+  m.impl("gf_edge_fwd_multi", hy::gf::gf_edge_fwd_multi);
   m.impl("gf_edge_bwd", hy::gf::gf_edge_bwd);
   m.impl("gf_pair_stats_bwd", hy::gf::gf_pair_stats_bwd);
   m.impl("gf_mlp_bwd", hy::gf::gf_mlp_bwd);

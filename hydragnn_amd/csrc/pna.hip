@@ -340,11 +340,36 @@ __device__ __forceinline__ float wave_dot(const float* __restrict__ a, int sa, c
   return wave_sum(acc);
 }
 
+__device__ __forceinline__ void wprep_fwd_body(const float* __restrict__ W, const float* __restrict__ b,
+                                               const float* __restrict__ encW, const float* __restrict__ encb,
+                                               float* __restrict__ Wab, float* __restrict__ Wr, float* __restrict__ Wd,
+                                               float* __restrict__ bc, int F, int d);
+
 __global__ void __launch_bounds__(256) pna_wprep_fwd_kernel(const float* __restrict__ W, const float* __restrict__ b,
                                                             const float* __restrict__ encW,
                                                             const float* __restrict__ encb, float* __restrict__ Wab,
                                                             float* __restrict__ Wr, float* __restrict__ Wd,
                                                             float* __restrict__ bc, int F, int d) {
+  wprep_fwd_body(W, b, encW, encb, Wab, Wr, Wd, bc, F, d);
+}
+
+// every layer of a stack in one launch (blockIdx.y = layer): the fused GPS encoder prepares
+// all its layers' weights up front
+constexpr int kWprepMaxL = 8;
+struct WprepMulti {
+  const float *W[kWprepMaxL], *b[kWprepMaxL], *encW[kWprepMaxL], *encb[kWprepMaxL];
+  float *Wab[kWprepMaxL], *Wr[kWprepMaxL], *Wd[kWprepMaxL], *bc[kWprepMaxL];
+};
+
+__global__ void __launch_bounds__(256) pna_wprep_fwd_multi_kernel(WprepMulti m, int F, int d) {
+  const int l = blockIdx.y;
+  wprep_fwd_body(m.W[l], m.b[l], m.encW[l], m.encb[l], m.Wab[l], m.Wr[l], m.Wd[l], m.bc[l], F, d);
+}
+
+__device__ __forceinline__ void wprep_fwd_body(const float* __restrict__ W, const float* __restrict__ b,
+                                               const float* __restrict__ encW, const float* __restrict__ encb,
+                                               float* __restrict__ Wab, float* __restrict__ Wr, float* __restrict__ Wd,
+                                               float* __restrict__ bc, int F, int d) {
   // one thread per output element (Wab copy, then the Wr / Wd / bc dot products of length F
   // over L1/L2-resident operands, fixed sequential order).  The round-1 form (one wave per
   // dot, 2048 workgroups) cost ~19 us on the conv branch's critical path for F = 64.
@@ -473,6 +498,41 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pna_wprep_fwd(const a
   return {Wab, Wr, Wd, bc};
 }
 
+// [Wab_0, Wr_0, Wd_0, bc_0, Wab_1, ...] for every layer, one launch
+std::vector<at::Tensor> pna_wprep_fwd_multi(at::TensorList Ws, at::TensorList bs, at::TensorList encWs,
+                                            at::TensorList encbs) {
+  const int L = (int)Ws.size();
+  HY_CHECK(L >= 1 && L <= kWprepMaxL && (int)bs.size() == L && (int)encWs.size() == L && (int)encbs.size() == L,
+           "pna_wprep_fwd_multi: 1..8 layers of (W, b, encW, encb)");
+  const int F = (int)Ws[0].size(0);
+  const int d = (int)encWs[0].size(1) - F;
+  WprepMulti m{};
+  std::vector<at::Tensor> out, keep;
+  for (int l = 0; l < L; ++l) {
+    HY_CHECK_CUDA(Ws[l]);
+    auto W = Ws[l].contiguous(), b = bs[l].contiguous(), encW = encWs[l].contiguous(), encb = encbs[l].contiguous();
+    HY_CHECK_F32(W); HY_CHECK_F32(b); HY_CHECK_F32(encW); HY_CHECK_F32(encb);
+    HY_CHECK(W.dim() == 2 && W.size(0) == F && W.size(1) == 3 * F, "pna_wprep: W must be [F, 3F] (same F per layer)");
+    HY_CHECK(encW.dim() == 2 && encW.size(0) == F && encW.size(1) == F + d, "pna_wprep: encW must be [F, d+F]");
+    HY_CHECK(b.numel() == F && encb.numel() == F, "pna_wprep: biases must have F entries");
+    auto Wab = at::empty({2 * F, F}, W.options()), Wr = at::empty({F, F}, W.options());
+    auto Wd = at::empty({F, d}, W.options()), bc = at::empty({F}, W.options());
+    m.W[l] = W.data_ptr<float>();
+    m.b[l] = b.data_ptr<float>();
+    m.encW[l] = encW.data_ptr<float>();
+    m.encb[l] = encb.data_ptr<float>();
+    m.Wab[l] = Wab.data_ptr<float>();
+    m.Wr[l] = Wr.data_ptr<float>();
+    m.Wd[l] = Wd.data_ptr<float>();
+    m.bc[l] = bc.data_ptr<float>();
+    keep.insert(keep.end(), {W, b, encW, encb});
+    out.insert(out.end(), {Wab, Wr, Wd, bc});
+  }
+  const int64_t total = 2LL * F * F + (int64_t)F * F + (int64_t)F * d + F;
+  pna_wprep_fwd_multi_kernel<<<dim3((unsigned)ceil_div(total, 256), (unsigned)L), 256, 0, stream()>>>(m, F, d);
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pna_wprep_bwd(const at::Tensor& dWab_, const at::Tensor& dWr_,
                                                                          const at::Tensor& dWd_, const at::Tensor& dbc_,
                                                                          const at::Tensor& W_, const at::Tensor& encW_,
@@ -502,6 +562,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "pna_bwd(Tensor dZ, Tensor Z, Tensor AB, Tensor? C, Tensor? G, Tensor src, Tensor rowptr, Tensor amin, "
       "Tensor amax, float avg_log, float avg_lin) -> (Tensor, Tensor, Tensor)");
   m.def("pna_wprep_fwd(Tensor W, Tensor b, Tensor encW, Tensor encb) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("pna_wprep_fwd_multi(Tensor[] W, Tensor[] b, Tensor[] encW, Tensor[] encb) -> Tensor[]");
   m.def(
       "pna_wprep_bwd(Tensor dWab, Tensor dWr, Tensor dWd, Tensor dbc, Tensor W, Tensor encW, Tensor encb) -> "
       "(Tensor, Tensor, Tensor, Tensor)");
@@ -511,5 +572,6 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("pna_fwd", hy::pna_fwd);
   m.impl("pna_bwd", hy::pna_bwd);
   m.impl("pna_wprep_fwd", hy::pna_wprep_fwd);
+  m.impl("pna_wprep_fwd_multi", hy::pna_wprep_fwd_multi);
   m.impl("pna_wprep_bwd", hy::pna_wprep_bwd);
 }

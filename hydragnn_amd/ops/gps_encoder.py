@@ -252,12 +252,23 @@ class _GPSEncoder(torch.autograd.Function):
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
         st = []
         z3 = None
+        # the PNAPlus edge term C = r Wr^T + e Wd^T + bc depends on no node state: every layer's
+        # is computed up front, where the chip is otherwise idle, instead of inside the local
+        # branch of its layer (the critical path of the layer's two-stream fork; concurrent
+        # with the attention kernels the edge launch took ~3x its standalone time)
+        hoist = os.environ.get("HYDRA_EDGE_HOIST", "1") == "1"
+        if hoist:
+            pw = ops.pna_wprep_fwd_multi([q[4] for q in prm], [q[5] for q in prm], [q[6] for q in prm],
+                                         [q[7] for q in prm])
+            preps = [pw[4 * l: 4 * l + 4] for l in range(L)]
+        Cs = ops.gf_edge_fwd_multi(list(Rl), e, [q[1] for q in preps], [q[2] for q in preps],
+                                   [q[3] for q in preps]) if hoist else None
         for l in range(L):
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
              g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2, _, _, _) = prm[l]
             r, G = Rl[l], Gl[l]
             s0, s1, s2, s3 = cfg.salts[l]
-            Wab, Wr, Wd, bc = ops.pna_wprep_fwd(Wpre, bpre, Wenc, benc)
+            Wab, Wr, Wd, bc = preps[l] if hoist else ops.pna_wprep_fwd(Wpre, bpre, Wenc, benc)
             if l == 0:
                 outs = ops.gf_node_fwd(x0, Wab, Win, bin_, nv, None, None, [], None, None, None, None, None,
                                        None, 0.0, 0.0, 0.0, 0.0, acc, cfg.a8)
@@ -280,7 +291,7 @@ class _GPSEncoder(torch.autograd.Function):
                 else:
                     O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
                 z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
-            C = ops.gf_edge_fwd(r, e, Wr, Wd, bc)
+            C = Cs[l] if hoist else ops.gf_edge_fwd(r, e, Wr, Wd, bc)
             Z, amin, amax = ops.pna_fwd(x, AB, C, G, cfg.src.index, cfg.dst.rowptr, cfg.avg[l][0], cfg.avg[l][1])
             pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
             side.join(O, LSE, z2)
@@ -374,8 +385,16 @@ class _GPSEncoder(torch.autograd.Function):
             dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], Gl[l], cfg.src.index, cfg.dst.rowptr,
                                       s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
             ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
-            # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch
-            dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+            # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch.
+            # Nothing of the layer chain reads them (only weight gradients and the embedding /
+            # radial backward at the end): with the weight-gradient stream it runs there, off
+            # the local branch's critical path
+            if wside:
+                wstream.wait_stream(wmain)
+                with torch.cuda.stream(wstream):
+                    dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+            else:
+                dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
             # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
             # MI355X: the attention passes are throughput-bound once they overlap the local
             # branch, 209 vs 200 us per layer)
@@ -409,6 +428,12 @@ class _GPSEncoder(torch.autograd.Function):
             grads[base + 14], grads[base + 15] = dw2n, db2n
             grads[base + 16], grads[base + 17] = dw3, db3
             grads[base + 18], grads[base + 19] = dw4, db4
+        if wside:
+            # the edge backward's outputs (and the overlapped weight gradients) join the main stream
+            wmain.wait_stream(wstream)
+            for t in (dr, de, drbf):
+                if t is not None:
+                    t.record_stream(wmain)
         dfreq_w = item(drbf, drdf, (K, K), False)[0] if ctx.freq_grad else None
         # embeddings: only the narrow products dy^T [A | B] (see csrc/gps_fused.hip, EmbFwd)
         tn = [item(dx0, xin, (F, xin.shape[1]), False)[0], item(dx0, pe, (F, pe.shape[1]), False)[0]]
@@ -416,8 +441,6 @@ class _GPSEncoder(torch.autograd.Function):
         # every weight gradient of the stack (incl. the radial basis and its frequencies): one
         # grouped launch pair
         ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
-        if wside:
-            wmain.wait_stream(wstream)  # (dys/xs/dws hold every operand alive until here)
         # weight-prep backward of every layer, embedding weights and dfreq: one launch
         wp = []
         for l, gw in wg:

@@ -128,3 +128,32 @@ def test_fused_encoder_bitwise_reproducible():
             assert torch.equal(a.grad, b.grad), n
     for (n, a), (_, b) in zip(model.named_buffers(), twin.named_buffers()):
         assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("F,E", [(64, 26624), (64, 1000), (32, 77)])
+def test_edge_fwd_multi_and_wprep_multi_match_torch(F, E):
+    """One-launch edge terms / weight preps of every layer (csrc/gps_fused.hip
+    edge_fwd_multi_kernel, csrc/pna.hip pna_wprep_fwd_multi) == fp32 torch and == the
+    per-layer launches."""
+    from hydragnn_amd import _native
+
+    ops = _native.ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(F + E)
+    L, d = 3, F
+    rs = [torch.randn(E, F, generator=g).to(dev) for _ in range(L)]
+    e = torch.randn(E, d, generator=g).to(dev)
+    Ws = [(torch.randn(F, 3 * F, generator=g) * 0.1).to(dev) for _ in range(L)]
+    bs = [torch.randn(F, generator=g).to(dev) for _ in range(L)]
+    encW = [(torch.randn(F, d + F, generator=g) * 0.1).to(dev) for _ in range(L)]
+    encb = [torch.randn(F, generator=g).to(dev) for _ in range(L)]
+    pw = ops.pna_wprep_fwd_multi(Ws, bs, encW, encb)
+    Cs = ops.gf_edge_fwd_multi(rs, e, pw[1::4], pw[2::4], pw[3::4])
+    for l in range(L):
+        one = ops.pna_wprep_fwd(Ws[l], bs[l], encW[l], encb[l])
+        for a, b in zip(pw[4 * l:4 * l + 4], one):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+        Wr, Wd, bc = one[1], one[2], one[3]
+        ref = rs[l].double() @ Wr.double().t() + e.double() @ Wd.double().t() + bc.double()
+        torch.testing.assert_close(Cs[l].double(), ref, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(Cs[l], ops.gf_edge_fwd(rs[l], e, Wr, Wd, bc), rtol=1e-5, atol=1e-5)
