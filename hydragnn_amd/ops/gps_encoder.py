@@ -352,14 +352,14 @@ class _GPSEncoder(torch.autograd.Function):
         drbf = None
         dx0 = None
         wg = []  # per layer: (dWab, (dWr, dbc), dWd)
-        # layer l's weight gradients are launched on a third stream as soon as its backward
-        # is enqueued, overlapping layer l-1's latency-bound backward (the last layer's,
-        # plus the embeddings', stay on the main stream at the end)
+        # layer l's weight gradients are launched on a third stream during layer l-1's
+        # backward (the last layer's, plus the embeddings', stay on the main stream at the end)
         wside = cfg.side and os.environ.get("HYDRA_WGRAD_OVERLAP", "1") == "1"
         if wside:
             wmain = torch.cuda.current_stream(dev)
             wstream = _streams.side_stream(dev, 2)
         lo = 0
+        edge_ev = None
         for l in reversed(range(L)):
             s = st[l]
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
@@ -382,6 +382,14 @@ class _GPSEncoder(torch.autograd.Function):
                                         cfg.span, cfg.splits)
             dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
                                                          nv)
+            if wside and lo < len(dys):
+                # the previous layer's weight gradients: enqueued here so they run beside this
+                # layer's attention backward (long, matrix-core bound) rather than beside the
+                # short node / MLP / delta kernels that lead into it (the critical path)
+                wstream.wait_stream(wmain)
+                with torch.cuda.stream(wstream):
+                    ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+                lo = len(dys)
             dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], Gl[l], cfg.src.index, cfg.dst.rowptr,
                                       s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
             ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
@@ -389,11 +397,18 @@ class _GPSEncoder(torch.autograd.Function):
             # Nothing of the layer chain reads them (only weight gradients and the embedding /
             # radial backward at the end): with the weight-gradient stream it runs there, off
             # the local branch's critical path
-            if wside:
+            # (the first layer's runs on the main stream, which has nothing else to do until the
+            # attention branch joins, while the side stream is still busy with layer 1's weight
+            # gradients; it waits only for the previous edge launch, through an event)
+            if wside and l > 0:
                 wstream.wait_stream(wmain)
                 with torch.cuda.stream(wstream):
                     dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+                edge_ev = torch.cuda.Event()
+                edge_ev.record(wstream)
             else:
+                if wside and edge_ev is not None:
+                    wmain.wait_event(edge_ev)
                 dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
             # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
             # MI355X: the attention passes are throughput-bound once they overlap the local
@@ -419,11 +434,6 @@ class _GPSEncoder(torch.autograd.Function):
             gw["W1"] = item(dpre, s["out"], W1, True)
             gw["W2"] = item(dg, s["md"], W2, True)
             wg.append((l, gw))
-            if wside and l > 0:
-                wstream.wait_stream(wmain)
-                with torch.cuda.stream(wstream):
-                    ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
-                lo = len(dys)
             grads[base + 12], grads[base + 13] = dw1n, db1n
             grads[base + 14], grads[base + 15] = dw2n, db2n
             grads[base + 16], grads[base + 17] = dw3, db3

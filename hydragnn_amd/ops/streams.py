@@ -32,7 +32,9 @@ def side_stream(device, slot=0):
         # HYDRA_SIDE_PRIORITY: priority of the side-branch stream (torch convention: lower is
         # higher priority; 0 = default).  The captured step records branch priorities only
         # if the runtime keeps them per graph node (tools/gpu_r4_iter.sh A/B).
-        s = torch.cuda.Stream(device=device, priority=int(os.environ.get("HYDRA_SIDE_PRIORITY", "0")))
+        # HYDRA_WGRAD_PRIORITY: the same for slot 2 (weight gradients / edge backward)
+        env = "HYDRA_WGRAD_PRIORITY" if slot == 2 else "HYDRA_SIDE_PRIORITY"
+        s = torch.cuda.Stream(device=device, priority=int(os.environ.get(env, "0")))
         _side[key] = s
     return s
 
