@@ -1235,6 +1235,42 @@ at::Tensor attn8_bwd_sum(const at::Tensor& pq, const at::Tensor& pkv) {
 }
 
 // single-stream composition: prep, ONE fused dQ + dK/dV launch, partial sum
+// v2 backward from operands packed by the producer of dO (csrc/gps_fused.hip att_bwd with O):
+// -delta [H, Nq], dO in the pair / quad layouts [H, Nq, 8]
+at::Tensor attn8_bwd_packed(const at::Tensor& ndelta, const at::Tensor& dOp, const at::Tensor& dOq,
+                            const at::Tensor& LSE2, const at::Tensor& Qp, const at::Tensor& Qq, const at::Tensor& Kp,
+                            const at::Tensor& Kq, const at::Tensor& Vp, const at::Tensor& seg_id,
+                            const at::Tensor& seg_ptr, int64_t N, double scale) {
+  const int64_t H = Qp.size(0), Nq = Qp.size(1), F = 8 * H;
+  chk_bwd(Qp, LSE2, ndelta, dOp, N);
+  chk_seg(seg_id, seg_ptr, N);
+  HY_CHECK(Qq.numel() == Qp.numel() && dOq.numel() == dOp.numel() && dOp.is_contiguous() && dOq.is_contiguous() &&
+               ndelta.is_contiguous(),
+           "attn8_bwd_packed: operand shapes");
+  auto dqkv = at::empty({N, 3 * F}, Qp.options());
+  if (N == 0) return dqkv;
+  A8Bwd2 b{};
+  b.Qp = Qp.data_ptr<float>();
+  b.Qq = Qq.data_ptr<float>();
+  b.Kp = Kp.data_ptr<float>();
+  b.Kq = Kq.data_ptr<float>();
+  b.Vp = Vp.data_ptr<float>();
+  b.dOp = dOp.data_ptr<float>();
+  b.dOq = dOq.data_ptr<float>();
+  b.NL = LSE2.data_ptr<float>();  // v2 forward: -LSE2
+  b.ndelta = ndelta.data_ptr<float>();
+  b.N = (int)N;
+  b.Nq = (int)Nq;
+  b.H = (int)H;
+  b.seg_id = seg_id.data_ptr<int>();
+  b.seg_ptr = seg_ptr.data_ptr<int>();
+  b.scale = (float)scale;
+  b.qscale = (float)scale * kLog2e;
+  b.dqkv = dqkv.data_ptr<float>();
+  launch_bwd2(0, b);
+  return dqkv;
+}
+
 at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor& LSE2, const at::Tensor& Qp,
                      const at::Tensor& Qq, const at::Tensor& Kp, const at::Tensor& Kq, const at::Tensor& Vp,
                      const at::Tensor& seg_id, const at::Tensor& seg_ptr, double scale, int64_t splits) {
@@ -1321,10 +1357,14 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "attn8_bwd(Tensor dO, Tensor O, Tensor LSE2, Tensor Qp, Tensor Qq, Tensor Kp, Tensor Kq, Tensor Vp, "
       "Tensor seg_id, Tensor seg_ptr, float scale, int splits) -> Tensor");
+  m.def(
+      "attn8_bwd_packed(Tensor ndelta, Tensor dOp, Tensor dOq, Tensor LSE2, Tensor Qp, Tensor Qq, Tensor Kp, "
+      "Tensor Kq, Tensor Vp, Tensor seg_id, Tensor seg_ptr, int N, float scale) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("attn8_pack", hy::a8::attn8_pack);
   m.impl("attn8_fwd", hy::a8::attn8_fwd);
   m.impl("attn8_bwd", hy::a8::attn8_bwd);
+  m.impl("attn8_bwd_packed", hy::a8::attn8_bwd_packed);
 }

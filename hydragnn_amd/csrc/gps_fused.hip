@@ -884,7 +884,21 @@ struct AttBwd {
   Drop drop1;
   const int* nvp;
   int N;
+  // 8-wide-head attention backward operands written here instead of dO (csrc/attention8.hip
+  // attn8_delta_pack, folded into this epilogue): -delta[h][q] = -sum_d dO O, dO in the
+  // "pair" and "quad" layouts; rows N..Nq zero
+  const float* O;
+  float *ndelta, *dOp, *dOq;
+  int Nq;
 };
+
+// attention8.hip operand layouts of one head (element d of row n)
+__device__ __forceinline__ int64_t a8_pair_idx(int h, int Nq, int n, int d) {
+  return ((int64_t)h * Nq + n) * 8 + 2 * (d & 3) + (d >> 2);
+}
+__device__ __forceinline__ int64_t a8_quad_idx(int h, int Nq, int n, int d) {
+  return (((int64_t)h * (Nq >> 2) + (n >> 2)) * 8 + d) * 4 + (n & 3);
+}
 
 template <int F>
 __global__ void __launch_bounds__(256) att_bwd_kernel(AttBwd a) {
@@ -917,10 +931,30 @@ __global__ void __launch_bounds__(256) att_bwd_kernel(AttBwd a) {
   for (int t = w; t < F / 16; t += 4) {
     const int n0 = 16 * t, col = n0 + i;
     f4v acc = tile_mma<false>(das, LD, a.Wo, F, 0, F, n0);
+    if (a.dOp == nullptr) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = row0 + 4 * g + r;
-      if (row < a.N) a.dO[(int64_t)row * F + col] = acc[r];
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * g + r;
+        if (row < a.N) a.dO[(int64_t)row * F + col] = acc[r];
+      }
+    } else {
+      // a 16-column tile holds two heads (lanes i < 8, i >= 8): delta by an xor tree over
+      // the 8 lanes of a head
+      const int h = col >> 3, d = col & 7;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * g + r;
+        const float v = row < a.N ? acc[r] : 0.f;
+        float pd = row < a.N ? v * a.O[(int64_t)row * F + col] : 0.f;
+        pd += __shfl_xor(pd, 1);
+        pd += __shfl_xor(pd, 2);
+        pd += __shfl_xor(pd, 4);
+        if (row < a.Nq) {
+          a.dOp[a8_pair_idx(h, a.Nq, row, d)] = v;
+          a.dOq[a8_quad_idx(h, a.Nq, row, d)] = v;
+          if (d == 0) a.ndelta[(int64_t)h * a.Nq + row] = -pd;
+        }
+      }
     }
   }
 }
@@ -1834,17 +1868,34 @@ std::vector<at::Tensor> gf_loc_bwd(const at::Tensor& dout, const at::Tensor& z1,
 std::vector<at::Tensor> gf_att_bwd(const at::Tensor& dout, const at::Tensor& z2, const at::Tensor& acc,
                                    const at::Tensor& saved, const at::Tensor& gamma2, const at::Tensor& Wo,
                                    const c10::optional<at::Tensor>& rng, int64_t salt1, double p,
-                                   const c10::optional<at::Tensor>& nv) {
+                                   const c10::optional<at::Tensor>& nv, const c10::optional<at::Tensor>& O) {
   const int64_t N = z2.size(0), F = z2.size(1);
   chk(dout, N, F, "dout");
   auto o = z2.options();
-  auto dz2 = at::empty({N, F}, o), da = at::empty({N, F}, o), dO = at::empty({N, F}, o), dw2 = at::empty({F}, o),
-       db2 = at::empty({F}, o);
+  const bool packed = O.has_value() && O->defined();
+  auto dz2 = at::empty({N, F}, o), da = at::empty({N, F}, o), dw2 = at::empty({F}, o), db2 = at::empty({F}, o);
+  auto dO = packed ? at::empty({0}, o) : at::empty({N, F}, o);
   AttBwd a{dout.data_ptr<float>(), z2.data_ptr<float>(), site_ptr(acc, 4, (int)F), saved.data_ptr<float>(),
            gamma2.data_ptr<float>(), BNG{dw2.data_ptr<float>(), db2.data_ptr<float>()}, Wo.data_ptr<float>(),
-           dz2.data_ptr<float>(), da.data_ptr<float>(), dO.data_ptr<float>(), mk_drop(rng, salt1, p), nvptr(nv),
-           (int)N};
+           dz2.data_ptr<float>(), da.data_ptr<float>(), packed ? nullptr : dO.data_ptr<float>(),
+           mk_drop(rng, salt1, p), nvptr(nv), (int)N};
+  at::Tensor ndelta, dOp, dOq;
+  if (packed) {
+    // with O: the 8-wide-head attention backward operands (heads H = F / 8, rows Nq = 16k)
+    HY_CHECK(F % 8 == 0, "gf_att_bwd: packed attention operands need 8-wide heads");
+    chk(*O, N, F, "O");
+    const int64_t H = F / 8, Nq = ceil_div(N, (int64_t)BM) * BM;
+    ndelta = at::empty({H, Nq}, o);
+    dOp = at::empty({H, Nq, 8}, o);
+    dOq = at::empty({H, Nq, 8}, o);
+    a.O = O->data_ptr<float>();
+    a.ndelta = ndelta.data_ptr<float>();
+    a.dOp = dOp.data_ptr<float>();
+    a.dOq = dOq.data_ptr<float>();
+    a.Nq = (int)Nq;
+  }
   HY_GF_DISPATCH(F, att_bwd_kernel, std::max(1, ceil_div(N, BM)), 256, a);
+  if (packed) return {dz2, da, dO, dw2, db2, ndelta, dOp, dOq};
   return {dz2, da, dO, dw2, db2};
 }
 
@@ -1922,7 +1973,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "int salt0, float p, Tensor? nv) -> Tensor[]");
   m.def(
       "gf_att_bwd(Tensor dout, Tensor z2, Tensor acc, Tensor saved, Tensor gamma2, Tensor Wo, Tensor? rng, int salt1, "
-      "float p, Tensor? nv) -> Tensor[]");
+      "float p, Tensor? nv, Tensor? O=None) -> Tensor[]");
   m.def(
       "gf_node_bwd(Tensor dAB, Tensor dqkv, Tensor Wab, Tensor Win, Tensor dZ, Tensor dz1, Tensor dz2, Tensor x, "
       "Tensor? z3p, Tensor? savedp, Tensor(a!)? accp, Tensor? nv) -> Tensor");

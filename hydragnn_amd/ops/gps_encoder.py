@@ -236,33 +236,48 @@ class _GPSEncoder(torch.autograd.Function):
         L, F = cfg.L, cfg.F
         prm = [flat[NP * l: NP * (l + 1)] for l in range(L)]
         dev = xin.device
-        # GPS input embeddings (node rows >= num_valid -> 0), one launch each
-        x0 = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
-        e = ops.gf_embed_fwd(eattr, rpe, Wee, Wrp, Wel, None)
-        # edge distances + Bessel basis + every layer's radial embedding / gate in one launch;
-        # the basis and its frequency derivative are kept for the weight gradients
-        geo = cfg.geom if cfg.geom is not None else (None, None, None, None)
-        ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
-                                  cfg.cutoff, cfg.exponent, bool(freq.requires_grad), *geo)
-        rbf, drdf, Rl, Gl = ro[0], ro[1], ro[2:2 + L], ro[2 + L:2 + 2 * L]
-        # BN statistics sites: 3 fixed-point 64-bit words per statistic (deterministic integer
-        # atomics, csrc/gps_fused.hip col_sum_add); zeroed by the first node launch
-        acc = torch.empty(L, 3 * NREP * SITES * F, device=dev, dtype=torch.float64)
-        saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
         nv, rng, p = cfg.nv, cfg.rng, cfg.p
-        st = []
-        z3 = None
         # the PNAPlus edge term C = r Wr^T + e Wd^T + bc depends on no node state: every layer's
-        # is computed up front, where the chip is otherwise idle, instead of inside the local
-        # branch of its layer (the critical path of the layer's two-stream fork; concurrent
-        # with the attention kernels the edge launch took ~3x its standalone time)
+        # is computed up front (one launch) instead of inside the local branch of its layer
+        # (the critical path of the layer's two-stream fork; concurrent with the attention
+        # kernels the per-layer edge launch took ~3x its standalone time)
         hoist = os.environ.get("HYDRA_EDGE_HOIST", "1") == "1"
         if hoist:
             pw = ops.pna_wprep_fwd_multi([q[4] for q in prm], [q[5] for q in prm], [q[6] for q in prm],
                                          [q[7] for q in prm])
             preps = [pw[4 * l: 4 * l + 4] for l in range(L)]
+        # the edge chain (edge embedding -> radial basis / per-layer embeddings -> edge terms)
+        # feeds only the local branches: on a third stream it overlaps the node embedding, the
+        # first node launch and the first attention; the main stream joins it just before the
+        # first PNA aggregation
+        eside = hoist and cfg.side and os.environ.get("HYDRA_EDGE_SIDE", "1") == "1"
+        geo = cfg.geom if cfg.geom is not None else (None, None, None, None)
+        if eside:
+            emain = torch.cuda.current_stream(dev)
+            estream = _streams.side_stream(dev, 2)
+            estream.wait_stream(emain)
+            ectx = torch.cuda.stream(estream)
+            ectx.__enter__()
+        # edge embedding, then edge distances + Bessel basis + every layer's radial embedding /
+        # gate in one launch (the basis and its frequency derivative are kept for the weight
+        # gradients), then every layer's edge term
+        e = ops.gf_embed_fwd(eattr, rpe, Wee, Wrp, Wel, None)
+        ro = ops.radial_fwd_multi(dist, freq, [q[24] for q in prm], [q[25] for q in prm], [q[26] for q in prm],
+                                  cfg.cutoff, cfg.exponent, bool(freq.requires_grad), *geo)
+        rbf, drdf, Rl, Gl = ro[0], ro[1], ro[2:2 + L], ro[2 + L:2 + 2 * L]
         Cs = ops.gf_edge_fwd_multi(list(Rl), e, [q[1] for q in preps], [q[2] for q in preps],
                                    [q[3] for q in preps]) if hoist else None
+        if eside:
+            ectx.__exit__(None, None, None)
+        edge_pending = eside
+        # GPS node input embedding (rows >= num_valid -> 0)
+        x0 = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
+        # BN statistics sites: 3 fixed-point 64-bit words per statistic (deterministic integer
+        # atomics, csrc/gps_fused.hip col_sum_add); zeroed by the first node launch
+        acc = torch.empty(L, 3 * NREP * SITES * F, device=dev, dtype=torch.float64)
+        saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
+        st = []
+        z3 = None
         for l in range(L):
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
              g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2, _, _, _) = prm[l]
@@ -291,6 +306,12 @@ class _GPSEncoder(torch.autograd.Function):
                 else:
                     O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
                 z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
+            if edge_pending:  # join the edge chain (its outputs live on in the main stream)
+                emain.wait_stream(estream)
+                for t in [e, rbf, drdf, *Rl, *Gl, *Cs]:
+                    if t is not None:
+                        t.record_stream(emain)
+                edge_pending = False
             C = Cs[l] if hoist else ops.gf_edge_fwd(r, e, Wr, Wd, bc)
             Z, amin, amax = ops.pna_fwd(x, AB, C, G, cfg.src.index, cfg.dst.rowptr, cfg.avg[l][0], cfg.avg[l][1])
             pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
@@ -372,12 +393,22 @@ class _GPSEncoder(torch.autograd.Function):
             side = _Side(dev, cfg.side)
             with side:
                 side.used(dout)
-                dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
-                if cfg.a8:
+                if cfg.a8 and cfg.splits <= 0:
+                    # the attention backward's operands (-delta, dO in the pair / quad layouts)
+                    # come out of the output-projection backward's epilogue: no packing launch
+                    pk = s["pk"]
+                    dz2, da, _, dw2n, db2n, nd, dOp, dOq = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng,
+                                                                          s1, p, nv, s["O"])
+                    dqkv = ops.attn8_bwd_packed(nd, dOp, dOq, s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid,
+                                                cfg.sptr, s["x"].shape[0], cfg.scale)
+                    dO = None
+                elif cfg.a8:
+                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
                     pk = s["pk"]
                     dqkv = ops.attn8_bwd(dO, s["O"], s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid, cfg.sptr,
                                          cfg.scale, cfg.splits)
                 else:
+                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
                     dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale,
                                         cfg.span, cfg.splits)
             dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
@@ -397,18 +428,25 @@ class _GPSEncoder(torch.autograd.Function):
             # Nothing of the layer chain reads them (only weight gradients and the embedding /
             # radial backward at the end): with the weight-gradient stream it runs there, off
             # the local branch's critical path
-            # (the first layer's runs on the main stream, which has nothing else to do until the
-            # attention branch joins, while the side stream is still busy with layer 1's weight
-            # gradients; it waits only for the previous edge launch, through an event)
             if wside and l > 0:
                 wstream.wait_stream(wmain)
                 with torch.cuda.stream(wstream):
                     dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
                 edge_ev = torch.cuda.Event()
                 edge_ev.record(wstream)
+            elif wside:
+                # the first layer's: the weight-gradient stream is still busy with layer 1's
+                # weight gradients, so a fourth stream runs it beside the attention backward,
+                # behind the previous edge launch (accumulated de / drbf) through an event
+                e3 = _streams.side_stream(dev, 3)
+                e3.wait_stream(wmain)
+                if edge_ev is not None:
+                    e3.wait_event(edge_ev)
+                with torch.cuda.stream(e3):
+                    dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+                edge_ev = torch.cuda.Event()
+                edge_ev.record(e3)
             else:
-                if wside and edge_ev is not None:
-                    wmain.wait_event(edge_ev)
                 dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
             # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
             # MI355X: the attention passes are throughput-bound once they overlap the local
@@ -441,6 +479,8 @@ class _GPSEncoder(torch.autograd.Function):
         if wside:
             # the edge backward's outputs (and the overlapped weight gradients) join the main stream
             wmain.wait_stream(wstream)
+            if edge_ev is not None:
+                wmain.wait_event(edge_ev)
             for t in (dr, de, drbf):
                 if t is not None:
                     t.record_stream(wmain)

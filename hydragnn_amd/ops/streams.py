@@ -25,7 +25,8 @@ def enabled(t):
 def side_stream(device, slot=0):
     """Cached side stream ``slot`` of ``device`` (slot 0: branch forks; slot 1: the
     attention backward's dK/dV pass, which forks again from inside a side branch;
-    slot 2: the fused GPS backward's per-layer weight gradients)."""
+    slot 2: the fused GPS encoder's edge chain (forward) and per-layer weight gradients /
+    edge backward (backward); slot 3: the first layer's edge backward)."""
     key = (torch.device(device).index, slot)
     s = _side.get(key)
     if s is None:
@@ -33,7 +34,7 @@ def side_stream(device, slot=0):
         # higher priority; 0 = default).  The captured step records branch priorities only
         # if the runtime keeps them per graph node (tools/gpu_r4_iter.sh A/B).
         # HYDRA_WGRAD_PRIORITY: the same for slot 2 (weight gradients / edge backward)
-        env = "HYDRA_WGRAD_PRIORITY" if slot == 2 else "HYDRA_SIDE_PRIORITY"
+        env = "HYDRA_WGRAD_PRIORITY" if slot >= 2 else "HYDRA_SIDE_PRIORITY"
         s = torch.cuda.Stream(device=device, priority=int(os.environ.get(env, "0")))
         _side[key] = s
     return s
