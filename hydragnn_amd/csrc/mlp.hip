@@ -23,7 +23,10 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 
 namespace hy {
 
@@ -996,7 +999,19 @@ std::vector<at::Tensor> head_loss_fused(const at::Tensor& x_, at::TensorList Ws_
     const size_t lds = hl_lds(a, (int)std::min<int64_t>(G, kHlRows));
     auto part = at::empty({(int64_t)R * a.goff[a.n]}, x.options());
     auto lpart = at::empty({R}, x.options().dtype(at::kDouble));
-    auto cnt = at::zeros({1}, x.options().dtype(at::kInt));
+    // the ticket counter: persistent per (device, stream) — launches on one stream never
+    // overlap, and the reducer resets it to zero (an at::zeros here was a fill launch on the
+    // step's critical path)
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, at::Tensor> counters;
+    at::Tensor cnt;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto key = std::make_pair((int)x.get_device(), stream());
+      auto it = counters.find(key);
+      if (it == counters.end()) it = counters.emplace(key, at::zeros({1}, x.options().dtype(at::kInt))).first;
+      cnt = it->second;
+    }
 #define HL_ROWS(N)                                                                                              \
   head_loss_rows_kernel<N><<<R, kHlThreads, lds, stream()>>>(                                                   \
       x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),         \

@@ -493,12 +493,12 @@ void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::option
   if (N == 0 || a.nins == 0) return;
   const size_t lds = (size_t)lds_w * rpg::kBM * sizeof(float) + (size_t)prog.numel() * sizeof(int);
   HY_CHECK(lds <= 160 * 1024, "rowprog: activations + program exceed the 160 KiB LDS");
-  // workgroup size: every wave decodes every instruction on the CU's one scalar unit, so
-  // fewer waves cost less per instruction; HYDRA_ROWPROG_THREADS picks 256 / 512 / 1024
+  // workgroup size (HYDRA_ROWPROG_THREADS: 256 / 512 / 1024).  md17 PAINN forces on MI355X:
+  // 512 -> 11.36k, 1024 -> 11.27k, 256 -> 9.85k graphs/s (tools/gpu_ab_rowprog.sh)
   static int nt = [] {
     const char* e = std::getenv("HYDRA_ROWPROG_THREADS");
-    const int v = e ? std::atoi(e) : 256;
-    return (v == 1024 || v == 512) ? v : 256;
+    const int v = e ? std::atoi(e) : 512;
+    return (v == 1024 || v == 256) ? v : 512;
   }();
   static bool attr = false;
   if (!attr) {
