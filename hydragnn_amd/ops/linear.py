@@ -88,47 +88,70 @@ class deferred_wgrad:
         return False
 
 
+def _span(it):
+    k0 = it[4] if len(it) > 4 else 0  # column block [k0, k0 + K) of W (row programs)
+    return k0, k0 + it[1].shape[1]
+
+
+def _conflict(a, b):
+    """Two deferred problems write the same output elements (same weight columns / bias)."""
+    if a[2] is b[2]:
+        (a0, a1), (b0, b1) = _span(a), _span(b)
+        if a0 < b1 and b0 < a1:
+            return True
+    return a[3] is not None and a[3] is b[3]
+
+
 def flush_deferred_wgrads():
     items, _defer["items"] = _defer["items"], []
     if not items:
         return
-    # one launch covers problems with distinct outputs; a parameter recorded twice (shared
-    # weights) goes to a later launch so its accumulation is ordered
+    # one launch covers problems with disjoint outputs (column blocks of one weight included);
+    # a weight / bias recorded twice (shared weights) goes to a later launch so its
+    # accumulation is ordered
     rounds = []
     for it in items:
         for r in rounds:
-            if all(it[2] is not o[2] for o in r):
+            if not any(_conflict(it, o) for o in r):
                 r.append(it)
                 break
         else:
             rounds.append([it])
     touched = []
     for r in rounds:
+        # a weight without a gradient yet whose column blocks in this launch cover all its
+        # columns is written directly (no zero fill, no accumulation)
+        cover = {}
+        for it in r:
+            cover.setdefault(id(it[2]), [it[2], []])[1].append(_span(it))
+        fresh = set()
+        for key, (W, spans) in cover.items():
+            if W.grad is None:
+                spans = sorted(spans)
+                pos = 0
+                for a0, a1 in spans:
+                    if a0 != pos:
+                        break
+                    pos = a1
+                if pos == W.shape[1]:
+                    fresh.add(key)
         dys, xs, dws, dbs, acc = [], [], [], [], []
         for it in r:
             dy, x, W, b = it[:4]
-            k0 = it[4] if len(it) > 4 else 0  # column block [k0, k0 + K) of W (row programs)
-            K = x.shape[1]
-            full = k0 == 0 and K == W.shape[1]
-            aw = W.grad is not None
-            abx = b is not None and b.grad is not None
-            if not aw and not abx and full:
-                # first contribution to both: written, not accumulated
-                W.grad = torch.empty_like(W)
-                if b is not None:
-                    b.grad = torch.empty_like(b)
-                a = False
-            else:
-                # a column block of a wider weight (the rest may get no contribution), or one
-                # of the pair already holds earlier rounds: zero-fill what is missing, accumulate
-                if not aw:
-                    W.grad = torch.zeros_like(W)
-                if b is not None and b.grad is None:
-                    b.grad = torch.zeros_like(b)
-                a = True
+            k0, k1 = _span(it)
+            full = k0 == 0 and k1 == W.shape[1]
+            a = not (id(W) in fresh and (b is None or b.grad is None))
+            if W.grad is None:
+                W.grad = torch.empty_like(W) if id(W) in fresh else torch.zeros_like(W)
+            if b is not None and b.grad is None:
+                b.grad = torch.empty_like(b) if not a else torch.zeros_like(b)
+            if a and id(W) in fresh:
+                # (a fresh weight block paired with an already-accumulating bias: the block's
+                # columns must start from zero too)
+                W.grad[:, k0:k1].zero_()
             dys.append(dy)
             xs.append(x)
-            dws.append(W.grad if full else W.grad[:, k0:k0 + K])
+            dws.append(W.grad if full else W.grad[:, k0:k1])
             dbs.append(b.grad if b is not None else torch.empty(0, device=dy.device))
             acc.append(1 if a else 0)
             touched += [W] + ([b] if b is not None else [])
