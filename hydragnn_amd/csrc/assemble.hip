@@ -173,12 +173,175 @@ std::vector<at::Tensor> store_assemble(const at::Tensor& plan, int64_t Np, int64
   return outs;
 }
 
+// ------------------------------------------------------------------------------------
+// Device-side batch plan (the captured step's per-step upload shrinks from the whole packed
+// plan, ~0.6 MB for an OC20 batch, to the G sample ids): the same 13 arrays, with the same
+// values, as the host builder (csrc/collate.cpp store_plan), expanded from per-sample tables
+// that live in HBM with the dataset:
+//   nn, ne [S]; noff, eoff [S]; sl, dl, pl [E_tot] (local src / dst / src-sort permutation);
+//   dcum, scum [N_tot] (per-sample local dst- / src-CSR row starts).
+// Every workgroup scans the G per-graph node / edge counts in LDS (G <= kPlanMaxG), then
+// threads fill a flat index over nodes, edges and graphs; padded nodes / edges follow the
+// host's closed forms (padded edge j: dst = N + floor(j pn / pe), src = N + (that + 1) mod pn,
+// stable source order by counting).
+constexpr int kPlanMaxG = 4096;
+struct PlanTabs {
+  const int *nn, *ne, *noff, *eoff, *sl, *dl, *pl, *dcum, *scum;
+};
+struct PlanOut {
+  int *node_rows, *erows, *src, *dst, *sperm, *rowptr, *srowptr, *batch, *gptr, *aseg_id, *aseg_ptr, *sidx, *scal;
+};
+
+__device__ __forceinline__ int64_t ceil_q(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+__global__ void __launch_bounds__(256) plan_expand_kernel(const int* __restrict__ seed, PlanTabs t, PlanOut o, int Np,
+                                                          int Ep, int Gp, int padded, int batch_scope) {
+  __shared__ int pn[kPlanMaxG + 1], pe[kPlanMaxG + 1];
+  const int G = seed[0];
+  const int* idx = seed + 1;
+  for (int g = threadIdx.x; g < G; g += 256) {
+    const int s = idx[g];
+    pn[g + 1] = t.nn[s];
+    pe[g + 1] = t.ne[s];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int a = 0, b = 0;
+    pn[0] = 0;
+    pe[0] = 0;
+    for (int g = 1; g <= G; ++g) {
+      a += pn[g];
+      b += pe[g];
+      pn[g] = a;
+      pe[g] = b;
+    }
+  }
+  __syncthreads();
+  const int N = pn[G], E = pe[G];
+  const int64_t pnn = (int64_t)Np - N, pee = (int64_t)Ep - E;
+  // padded-edge counts below a padded node offset q (closed forms of the host's bincounts)
+  auto dcount = [&](int64_t q) -> int64_t { return pee > 0 ? ceil_q(q * pee, pnn) : 0; };  // dst < N + q
+  auto scount = [&](int64_t q) -> int64_t {  // src < N + q
+    if (pee == 0 || q <= 0) return 0;
+    return dcount(q - 1) + (pee - dcount(pnn - 1));
+  };
+  auto find = [&](const int* ptr, int v) {  // g with ptr[g] <= v < ptr[g + 1]
+    int lo = 0, hi = G;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (ptr[mid] <= v) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  const int64_t total = (int64_t)Np + Ep + Gp + 1;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    if (q < Np) {
+      const int n = (int)q;
+      if (n < N) {
+        const int g = find(pn, n), s = idx[g], r = n - pn[g], nr = t.noff[s] + r;
+        o.node_rows[n] = nr;
+        o.batch[n] = g;
+        o.rowptr[n] = pe[g] + t.dcum[nr];
+        o.srowptr[n] = pe[g] + t.scum[nr];
+        o.aseg_id[n] = batch_scope ? 0 : g;
+      } else {
+        const int64_t qq = n - N;
+        o.node_rows[n] = -1;
+        o.batch[n] = G;
+        o.rowptr[n] = (int)(E + dcount(qq));
+        o.srowptr[n] = (int)(E + scount(qq));
+        o.aseg_id[n] = batch_scope ? 1 : G;
+      }
+    } else if (q < (int64_t)Np + Ep) {
+      const int k = (int)(q - Np);
+      if (k < E) {
+        const int g = find(pe, k), s = idx[g], er = t.eoff[s] + (k - pe[g]);
+        o.erows[k] = er;
+        o.src[k] = t.sl[er] + pn[g];
+        o.dst[k] = t.dl[er] + pn[g];
+        o.sperm[k] = t.pl[er] + pe[g];
+      } else {
+        const int64_t j = k - E, pd = j * pnn / pee;
+        o.erows[k] = -1;
+        o.dst[k] = (int)(N + pd);
+        o.src[k] = (int)(N + (pd + 1) % pnn);
+        // the j-th padded edge in source order: its source bucket qb (scount(qb) <= j), then the
+        // bucket's edges in index order (those with pd == qb - 1 mod pn)
+        int64_t lo = 0, hi = pnn;
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (scount(mid) <= j) lo = mid; else hi = mid;
+        }
+        const int64_t pdb = lo == 0 ? pnn - 1 : lo - 1;
+        o.sperm[k] = (int)(E + dcount(pdb) + (j - scount(lo)));
+      }
+    } else {
+      const int g = (int)(q - Np - Ep);
+      const int v = g <= G ? pn[g] : Np;
+      o.gptr[g] = v;
+      if (!batch_scope) o.aseg_ptr[g] = v;
+      if (g < Gp) o.sidx[g] = g < G ? idx[g] : 0;
+      if (g == 0) {
+        o.rowptr[Np] = Ep;
+        o.srowptr[Np] = Ep;
+        if (batch_scope) {
+          o.aseg_ptr[0] = 0;
+          o.aseg_ptr[1] = N;
+          o.aseg_ptr[2] = Np;
+        }
+        o.scal[0] = N;
+        o.scal[1] = G;
+        o.scal[2] = E;
+        o.scal[3] = 0;
+      }
+    }
+  }
+}
+
+// out: the packed plan [13 segments] of a (Np, Ep, Gp) layout; seed: [G, idx[0..G)] (int32,
+// device); tabs: nn, ne, noff, eoff, sl, dl, pl, dcum, scum (int32, device)
+void store_plan_expand(const at::Tensor& seed, at::TensorList tabs, at::Tensor out, int64_t Np, int64_t Ep, int64_t Gp,
+                       bool padded, bool batch_scope) {
+  HY_CHECK_CUDA(seed);
+  HY_CHECK_I32(seed);
+  HY_CHECK_I32(out);
+  HY_CHECK(tabs.size() == 9, "store_plan_expand: 9 per-sample tables");
+  for (const auto& x : tabs) HY_CHECK(x.is_cuda() && x.scalar_type() == at::kInt && x.is_contiguous(),
+                                      "store_plan_expand: int32 device tables");
+  HY_CHECK(Gp <= kPlanMaxG && seed.numel() >= Gp + 1 && out.is_contiguous(), "store_plan_expand: Gp / seed size");
+  const int64_t na = batch_scope ? 3 : Gp + 1;
+  const int64_t sizes[13] = {Np, Ep, Ep, Ep, Ep, Np + 1, Np + 1, Np, Gp + 1, Np, na, Gp, 4};
+  int64_t tot = 0;
+  for (int k = 0; k < 13; ++k) tot += sizes[k];
+  HY_CHECK(out.numel() >= tot, "store_plan_expand: out smaller than the layout");
+  int* p = out.data_ptr<int>();
+  int* v[13];
+  for (int k = 0; k < 13; ++k) {
+    v[k] = p;
+    p += sizes[k];
+  }
+  PlanTabs t{tabs[0].data_ptr<int>(), tabs[1].data_ptr<int>(), tabs[2].data_ptr<int>(), tabs[3].data_ptr<int>(),
+             tabs[4].data_ptr<int>(), tabs[5].data_ptr<int>(), tabs[6].data_ptr<int>(), tabs[7].data_ptr<int>(),
+             tabs[8].data_ptr<int>()};
+  PlanOut o{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12]};
+  const int64_t work = Np + Ep + Gp + 1;
+  const int blocks = (int)std::min<int64_t>(ceil_div(work, (int64_t)256), 1024);
+  plan_expand_kernel<<<blocks, 256, 0, stream()>>>(seed.data_ptr<int>(), t, o, (int)Np, (int)Ep, (int)Gp,
+                                                   padded ? 1 : 0, batch_scope ? 1 : 0);
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "store_assemble(Tensor plan, int Np, int Ep, int Gp, bool padded, int[] offs, Tensor[] node_src, "
       "Tensor[] edge_src, Tensor[] graph_src, int pos_field) -> Tensor[]");
+  m.def(
+      "store_plan_expand(Tensor seed, Tensor[] tabs, Tensor(a!) out, int Np, int Ep, int Gp, bool padded, "
+      "bool batch_scope) -> ()");
 }
 
-TORCH_LIBRARY_IMPL(hydra, CUDA, m) { m.impl("store_assemble", hy::store_assemble); }
+TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("store_assemble", hy::store_assemble);
+  m.impl("store_plan_expand", hy::store_plan_expand);
+}

@@ -838,10 +838,25 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
   }
   __syncthreads();
   const float sc = scale_s;
-  for (int e = threadIdx.x; e < nw; e += kHlThreads) {
-    float v = 0.f;
-    for (int k = 0; k < R; ++k) v += part[(int64_t)k * nw + e];
-    grads[e] = v * sc;
+  // 4 elements per thread per pass with all their slab loads in flight (a load -> add chain
+  // per element paid one memory latency each)
+  for (int e0 = threadIdx.x; e0 < nw; e0 += 4 * kHlThreads) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < R; ++k) {
+      float t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * kHlThreads;
+        t[u] = e < nw ? part[(int64_t)k * nw + e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] += t[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * kHlThreads;
+      if (e < nw) grads[e] = v[u] * sc;
+    }
   }
   if (kind == 2)
     for (int e = threadIdx.x; e < G * D0; e += kHlThreads) dx[e] *= sc;

@@ -28,6 +28,7 @@ extra attention segment), padded edges are spread over the padded nodes
 and the device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked
 reductions.
 """
+import os
 import time
 
 import numpy as np
@@ -151,6 +152,61 @@ class DeviceGraphStore:
                                      bool(lay.padded), lay.attn_scope == "batch")
             return out
         return self.plan_numpy(indices, lay, out)
+
+    # ------------------------------------------------------------------ device-side plan
+    def device_plan_ok(self, lay):
+        """The captured step can expand the plan on the device (csrc/assemble.hip
+        store_plan_expand) from the sample ids alone."""
+        from .. import _native
+
+        return (self.device.type == "cuda" and lay.Gp <= 4096 and _native.available()
+                and os.environ.get("HYDRA_DEVICE_PLAN", "1") == "1")
+
+    def _dev_plan_tabs(self):
+        t = getattr(self, "_dplan", None)
+        if t is None:
+            S = self.num_samples
+            i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(self.device)  # noqa: E731
+            Ntot, Etot = int(self.node_off[-1]), int(self.edge_off[-1])
+            e_sample = np.repeat(np.arange(S), self.n_edges)
+            n_sample = np.repeat(np.arange(S), self.n_nodes)
+            # per-sample local CSR row starts: every earlier sample's edges come first globally
+            gd = self.dst_local + self.node_off[:-1][e_sample]
+            gs = self.src_local + self.node_off[:-1][e_sample]
+            dc = np.zeros(Ntot + 1, dtype=np.int64)
+            np.cumsum(np.bincount(gd, minlength=Ntot), out=dc[1:])
+            sc = np.zeros(Ntot + 1, dtype=np.int64)
+            np.cumsum(np.bincount(gs, minlength=Ntot), out=sc[1:])
+            base = self.edge_off[:-1][n_sample]
+            t = self._dplan = [i32(self.n_nodes), i32(self.n_edges), i32(self.node_off[:-1]), i32(self.edge_off[:-1]),
+                               i32(self.src_local), i32(self.dst_local), i32(self.sperm_local), i32(dc[:-1] - base),
+                               i32(sc[:-1] - base)]
+            assert Etot == self.src_local.size
+        return t
+
+    def seed(self, indices, lay, out):
+        """Host part of the device-side plan: out[0] = G, out[1 + g] = sample id (int32 view of
+        ``lay.Gp + 1`` entries); the layout must hold the batch (as for ``plan``)."""
+        idx = np.asarray(indices, dtype=np.int64)
+        G = idx.size
+        N, E = self.sizes_of(idx)
+        if N > lay.Np or E > lay.Ep or G > lay.Gp or (lay.padded and (N + 2 > lay.Np or G + 1 > lay.Gp)):
+            raise ValueError("seed: batch exceeds the layout")
+        if G and (idx.min() < 0 or idx.max() >= self.num_samples):
+            raise ValueError("seed: sample index out of range")
+        out[0] = G
+        out[1:1 + G] = idx
+        out[1 + G:] = 0
+        return out
+
+    def plan_device(self, seed, lay, out):
+        """Expand ``seed`` (device int32, see ``seed``) into the packed plan ``out`` on the device:
+        the same values as ``plan`` (tests/test_device_plan_gpu.py)."""
+        from .. import _native
+
+        _native.ops().store_plan_expand(seed, self._dev_plan_tabs(), out, lay.Np, lay.Ep, lay.Gp, bool(lay.padded),
+                                        lay.attn_scope == "batch")
+        return out
 
     def plan_numpy(self, indices, lay, out=None):
         """numpy reference of ``plan`` (the oracle of the native builder)."""

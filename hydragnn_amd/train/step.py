@@ -188,6 +188,8 @@ class _Captured:
         self.next = 0
         self.g_opt = None
         self.dev_plan = None
+        self.dev_seed = None
+        self.seeded = False
         self.lay = None
 
     # the most recently replayed graph's outputs (and graph 0 for callers that want one)
@@ -507,10 +509,20 @@ class TrainStep:
         Np, Ep = key
         cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap.dev_plan = torch.empty(cap.lay.total, dtype=torch.int32, device=self.device)
-        cap.pinned = [torch.empty(cap.lay.total, dtype=torch.int32, pin_memory=True) for _ in range(2)]
-        store.plan(indices, cap.lay, cap.pinned[0].numpy())
+        # device-side plan: the step uploads only [G, sample ids] and expands the plan in the
+        # graph (csrc/assemble.hip store_plan_expand) instead of copying the ~0.6 MB host plan
+        cap.seeded = hasattr(store, "device_plan_ok") and store.device_plan_ok(cap.lay)
+        n_up = cap.lay.Gp + 1 if cap.seeded else cap.lay.total
+        cap.pinned = [torch.empty(n_up, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        if cap.seeded:
+            cap.dev_seed = torch.empty(n_up, dtype=torch.int32, device=self.device)
+            store.seed(indices, cap.lay, cap.pinned[0].numpy())
+            cap.dev_seed.copy_(cap.pinned[0])
+            store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan)
+        else:
+            store.plan(indices, cap.lay, cap.pinned[0].numpy())
+            cap.dev_plan.copy_(cap.pinned[0])
         cap.pinned[1].copy_(cap.pinned[0])
-        cap.dev_plan.copy_(cap.pinned[0])
         torch.cuda.synchronize()
         # warm-up on the capture stream itself: the parameters' AccumulateGrad nodes are then
         # created on the stream the captured backward runs on (a warm-up on a different stream
@@ -534,7 +546,11 @@ class TrainStep:
             pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
-                cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)  # first node: H2D of the plan
+                if cap.seeded:  # first nodes: H2D of the sample ids, device-side plan
+                    cap.dev_seed.copy_(cap.pinned[j], non_blocking=True)
+                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan)
+                else:  # first node: H2D of the plan
+                    cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)
                 cap.losses[j], cap.taskss[j] = self._body_fwd_bwd(store, cap, sync=not split)
                 if not split:
                     self.opt.step()
@@ -574,7 +590,10 @@ class TrainStep:
         tw = time.perf_counter() if tm is not None else 0.0
         lay = store.layout(indices, Np=cap.lay.Np, Ep=cap.lay.Ep, Gp=cap.lay.Gp)
         assert lay.total == cap.lay.total
-        store.plan(indices, lay, cap.pinned[j].numpy())
+        if cap.seeded:
+            store.seed(indices, lay, cap.pinned[j].numpy())
+        else:
+            store.plan(indices, lay, cap.pinned[j].numpy())
         if tm is not None:
             t1 = time.perf_counter()
         cap.graphs[j].replay()
