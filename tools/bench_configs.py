@@ -163,9 +163,21 @@ def run(name, steps, warmup, dev):
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
     nodes = float(np.mean([s.num_nodes for s in samples]))
+    dtype = get_precision()
+    if dtype == "bf16":
+        # label honestly: "bf16" only if bf16 MFMA kernels (csrc/bgemm.hip) actually ran in a
+        # step (maps below the bf16 size threshold stay fp32, e.g. every QM9 SchNet map)
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step(draw())
+            torch.cuda.synchronize()
+        kn = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+        nbf = sum(1 for n in kn if "bg::" in n)  # csrc/bgemm.hip kernels (namespace hy::bg)
+        dtype = "bf16" if nbf else "fp32 (bf16 requested; every map below the bf16 size threshold)"
     return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
             "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
-            "params": sum(p.numel() for p in model.parameters()), "dtype": get_precision(), "final_loss": float(loss),
+            "params": sum(p.numel() for p in model.parameters()), "dtype": dtype, "final_loss": float(loss),
             "data": "synthetic", "mode": ts.mode}
 
 
