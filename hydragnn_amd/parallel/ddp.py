@@ -312,10 +312,20 @@ class BucketedGradSync:
             self._launch(self.next)
             self.next += 1
 
+    def _zeros(self, n):
+        """A read-only all-zero source of n elements: slices of one persistent buffer (a
+        per-step torch.zeros was a fill launch per parameter without a gradient)."""
+        z = getattr(self, "_zsrc", None)
+        if z is None or z.numel() < n:
+            if self.flat.is_cuda and torch.cuda.is_current_stream_capturing():
+                return torch.zeros(n, device=self.flat.device, dtype=self.flat.dtype)
+            z = self._zsrc = torch.zeros(max(n, max(p.numel() for p in self.params)), device=self.flat.device,
+                                         dtype=self.flat.dtype)
+        return z[:n]
+
     def _pack(self, bi):
         s, e, ps = self.buckets[bi]
-        gs = [p.grad.reshape(-1) if p.grad is not None else
-              torch.zeros(p.numel(), device=self.flat.device, dtype=self.flat.dtype) for p in ps]
+        gs = [p.grad.reshape(-1) if p.grad is not None else self._zeros(p.numel()) for p in ps]
         if e == self.total + 1 + self.nflags:
             loss = self._loss
             gs.append(loss.detach().reshape(1).to(self.flat.dtype) if loss is not None else
