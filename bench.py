@@ -45,6 +45,8 @@ def parse():
                     help="graph: capture fwd+bwd+optimizer in a hipGraph (static padded shapes)")
     ap.add_argument("--profile-json", default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: the GPS attention products on bf16 MFMA (fp32 accumulate / softmax)")
     return ap.parse_args()
 
 
@@ -103,6 +105,9 @@ def main():
     from hydragnn_amd.models.create import create_model
     from hydragnn_amd.train.step import TrainStep
 
+    from hydragnn_amd.ops.linear import set_precision
+
+    set_precision(args.precision)
     samples = oc20_like(args.dataset_size, seed=1000 + rank + args.seed, radius=10.0, max_neighbours=10,
                         pe_dim=args.pe_dim)
     deg = degree_histogram(samples, max_degree=10).to(torch.float64)
@@ -187,7 +192,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.precision,
             "data": "synthetic (OC20-S2EF-shaped graphs, random-init weights)",
             "config": {
                 "model": f"PNAPlus+GPS hidden{args.hidden} x{args.layers} layers, {args.heads} heads, pe_dim {args.pe_dim}",
@@ -198,6 +203,8 @@ def main():
                 "avg_atoms_per_graph": round(nodes, 1),
                 "radius": 10.0,
                 "max_neighbours": 10,
+                "precision_scope": ("GPS attention products on bf16 MFMA (fp32 accumulate and softmax); "
+                                    "every other product fp32") if args.precision == "bf16" else "fp32 throughout",
                 "attn_scope": args.attn_scope,
                 "mode": args.mode,
                 "final_loss": float(loss) if loss is not None else None,

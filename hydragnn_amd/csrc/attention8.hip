@@ -26,6 +26,8 @@
 //          summed over 16 rows.
 #include "common.h"
 
+#include <type_traits>
+
 namespace hy {
 namespace a8 {
 
@@ -630,6 +632,28 @@ __device__ __forceinline__ float4 bl4(Rsrc r, int vo, int so) {
 }
 __device__ __forceinline__ float max4(f4v s) { return fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3])); }
 
+// bf16 mode (precision "bf16"): every product on v_mfma_f32_16x16x16_bf16 (fp32 accumulate).
+// Lane (i, g) supplies A[i][4g .. 4g+3] / B[4g .. 4g+3][i].  D = 8 contractions (S = Q K^T,
+// dP = dO V^T) use lane groups 0, 1 only — each reads one float4 of the pair layout, d in the
+// order {0, 4, 1, 5} / {2, 6, 3, 7}, the same for both operands — and zeros in groups 2, 3; the
+// 16-key / 16-query contractions (O, dQ, dK, dV) take a quad-layout float4 and the four
+// probabilities / dS values of the score accumulator, exactly as the fp32 path's four k-steps.
+typedef short s4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s4v pk4(float a, float b, float c, float d) {
+  typedef __bf16 b4v __attribute__((ext_vector_type(4)));
+  const b4v v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  return __builtin_bit_cast(s4v, v);
+}
+__device__ __forceinline__ s4v pk4(float4 v) { return pk4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ s4v pk4z(float4 v, bool live) {  // zero in lane groups 2, 3
+  return live ? pk4(v) : s4v{0, 0, 0, 0};
+}
+__device__ __forceinline__ f4v mfma_bf(s4v a, s4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// pair-layout float4 of row k0 + i for the D = 8 bf16 contractions (lane groups 0, 1)
+__device__ __forceinline__ int off_pair4(int i, int g) { return (8 * i + 4 * (g & 1)) * 4; }
+
 // Byte offsets inside one head's [Nq][8] pair / [Nq/4][8][4] quad block: a 16-row tile at
 // row k0 starts at k0 * 32 bytes in both layouts; lane (i, g) reads
 //   pair: row k0 + i, float2 at 2g        -> (8 i + 2 g) * 4
@@ -637,7 +661,7 @@ __device__ __forceinline__ float max4(f4v s) { return fmaxf(fmaxf(s[0], s[1]), f
 __device__ __forceinline__ int off_pair(int i, int g) { return (8 * i + 2 * g) * 4; }
 __device__ __forceinline__ int off_quad(int i, int g) { return (32 * g + 4 * (i & 7)) * 4; }
 
-template <int RT, int W>
+template <int RT, int W, bool BF = false>
 __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restrict__ Qp,
                                                             const float* __restrict__ Kp,
                                                             const float* __restrict__ Vq, int N, int Nq, int H,
@@ -650,14 +674,21 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
   const int qbase = blockIdx.x * 16 * RT;
   const SpanR<RT> sp = span_rt<RT>(qbase, i, N, seg_id, seg_ptr, W, w);
   const Rsrc rk = mk_rsrc(Kp + (int64_t)h * Nq * 8, Nq * 8), rv = mk_rsrc(Vq + (int64_t)h * Nq * 8, Nq * 8);
-  const int ok_ = off_pair(i, g), ov_ = off_quad(i, g);
+  const int ok_ = BF ? off_pair4(i, g) : off_pair(i, g), ov_ = off_quad(i, g);
+  const bool lo2 = g < 2;
   float bq0[RT], bq1[RT], m[RT], l[RT], thr[RT];
+  s4v qb[RT];
   f4v o[RT], cin[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(sp.row[t], Nq - 1)) * 8 + 2 * g);
-    bq0[t] = bq.x * qscale;
-    bq1[t] = bq.y * qscale;
+    if constexpr (BF) {
+      float4 q4 = ld4(Qp + ((int64_t)h * Nq + min(sp.row[t], Nq - 1)) * 8 + 4 * (g & 1));
+      qb[t] = pk4z(make_float4(q4.x * qscale, q4.y * qscale, q4.z * qscale, q4.w * qscale), lo2);
+    } else {
+      const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(sp.row[t], Nq - 1)) * 8 + 2 * g);
+      bq0[t] = bq.x * qscale;
+      bq1[t] = bq.y * qscale;
+    }
     m[t] = -INFINITY;
     thr[t] = -INFINITY;  // unset reference: any valid score moves it
     l[t] = 0.f;
@@ -666,13 +697,19 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
   }
   // one key tile: S^T (shifted by the row references), mask, deferred rescale, O^T += V^T P^T.
   // Tiles past the slice end (k0 >= ce, the odd tail of the 2-tile loop) are fully masked.
-  auto tile = [&](float2 kk, float4 vv, int k0) {
+  auto tile = [&](auto kk, float4 vv, int k0) {
     const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
     f4v s[RT];
+    if constexpr (BF) {
+      const s4v ka = pk4z(kk, lo2);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      s[t] = mfma(kk.x, bq0[t], cin[t]);
-      s[t] = mfma(kk.y, bq1[t], s[t]);
+      for (int t = 0; t < RT; ++t) s[t] = mfma_bf(ka, qb[t], cin[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(kk.x, bq0[t], cin[t]);
+        s[t] = mfma(kk.y, bq1[t], s[t]);
+      }
     }
     if (!full) {
 #pragma unroll
@@ -705,10 +742,14 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const float p0 = fexp2(s[t][0]), p1 = fexp2(s[t][1]), p2 = fexp2(s[t][2]), p3 = fexp2(s[t][3]);
-      o[t] = mfma(vv.x, p0, o[t]);
-      o[t] = mfma(vv.y, p1, o[t]);
-      o[t] = mfma(vv.z, p2, o[t]);
-      o[t] = mfma(vv.w, p3, o[t]);
+      if constexpr (BF) {
+        o[t] = mfma_bf(pk4(vv), pk4(p0, p1, p2, p3), o[t]);
+      } else {
+        o[t] = mfma(vv.x, p0, o[t]);
+        o[t] = mfma(vv.y, p1, o[t]);
+        o[t] = mfma(vv.z, p2, o[t]);
+        o[t] = mfma(vv.w, p3, o[t]);
+      }
       l[t] += (p0 + p1) + (p2 + p3);
     }
   };
@@ -716,19 +757,22 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
   // in-flight sequence (ka va kb vb) from the preheader and from the latch, so the compiler's
   // wait before the first tile is vmcnt(2), not a drain
   const int cmax = (Nq - 16) * 32;
-  float2 ka = bl2(rk, ok_, min(sp.cb * 32, cmax));
+  auto ldk = [&](int off) {
+    if constexpr (BF) return bl4(rk, ok_, off); else return bl2(rk, ok_, off);
+  };
+  auto ka = ldk(min(sp.cb * 32, cmax));
   float4 va = bl4(rv, ov_, min(sp.cb * 32, cmax));
   __builtin_amdgcn_sched_barrier(0);
-  float2 kb = bl2(rk, ok_, min(sp.cb * 32 + 512, cmax));
+  auto kb = ldk(min(sp.cb * 32 + 512, cmax));
   float4 vb = bl4(rv, ov_, min(sp.cb * 32 + 512, cmax));
   __builtin_amdgcn_sched_barrier(0);
   for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
     tile(ka, va, k0);
-    ka = bl2(rk, ok_, min(k0 * 32 + 1024, cmax));
+    ka = ldk(min(k0 * 32 + 1024, cmax));
     va = bl4(rv, ov_, min(k0 * 32 + 1024, cmax));
     __builtin_amdgcn_sched_barrier(0);
     tile(kb, vb, k0 + 16);
-    kb = bl2(rk, ok_, min(k0 * 32 + 1536, cmax));
+    kb = ldk(min(k0 * 32 + 1536, cmax));
     vb = bl4(rv, ov_, min(k0 * 32 + 1536, cmax));
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -783,7 +827,7 @@ struct A8Bwd2 {
   int nbq;
 };
 
-template <int RT, int W>
+template <int RT, int W, bool BF>
 __device__ __forceinline__ void attn8_bwd2_dq(const A8Bwd2& a, int bx, float* red) {
   const int h = blockIdx.y;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
@@ -792,36 +836,53 @@ __device__ __forceinline__ void attn8_bwd2_dq(const A8Bwd2& a, int bx, float* re
   const SpanR<RT> sp = span_rt<RT>(base, i, N, a.seg_id, a.seg_ptr, W, w);
   const int64_t hb = (int64_t)h * Nq * 8;
   const Rsrc rk = mk_rsrc(a.Kp + hb, Nq * 8), rv = mk_rsrc(a.Vp + hb, Nq * 8), rkt = mk_rsrc(a.Kq + hb, Nq * 8);
-  const int op = off_pair(i, g), oq = off_quad(i, g);
+  const int op = BF ? off_pair4(i, g) : off_pair(i, g), oq = off_quad(i, g);
+  const bool lo2 = g < 2;
   float bq0[RT], bq1[RT], bo0[RT], bo1[RT];
+  s4v qb[RT], ob[RT];
   f4v dq[RT], cs[RT], cd[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const int q = sp.row[t], qc = min(q, Nq - 1);
-    const float2 bq = ld2(a.Qp + hb + (int64_t)qc * 8 + 2 * g);
-    const float2 bo = ld2(a.dOp + hb + (int64_t)qc * 8 + 2 * g);
-    bq0[t] = bq.x * a.qscale;
-    bq1[t] = bq.y * a.qscale;
-    bo0[t] = bo.x;
-    bo1[t] = bo.y;
+    if constexpr (BF) {
+      const float4 q4 = ld4(a.Qp + hb + (int64_t)qc * 8 + 4 * (g & 1));
+      qb[t] = pk4z(make_float4(q4.x * a.qscale, q4.y * a.qscale, q4.z * a.qscale, q4.w * a.qscale), lo2);
+      ob[t] = pk4z(ld4(a.dOp + hb + (int64_t)qc * 8 + 4 * (g & 1)), lo2);
+    } else {
+      const float2 bq = ld2(a.Qp + hb + (int64_t)qc * 8 + 2 * g);
+      const float2 bo = ld2(a.dOp + hb + (int64_t)qc * 8 + 2 * g);
+      bq0[t] = bq.x * a.qscale;
+      bq1[t] = bq.y * a.qscale;
+      bo0[t] = bo.x;
+      bo1[t] = bo.y;
+    }
     const float nl = q < N ? a.NL[(int64_t)h * Nq + q] : 0.f;
     const float nd = q < N ? a.ndelta[(int64_t)h * Nq + q] : 0.f;
     cs[t] = f4v{nl, nl, nl, nl};
     cd[t] = f4v{nd, nd, nd, nd};
     dq[t] = f4z();
   }
-  auto tile = [&](float2 kk, float2 vv, float4 kt, int k0) {
+  auto tile = [&](auto kk, auto vv, float4 kt, int k0) {
     const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
     f4v s[RT], dp[RT];
+    if constexpr (BF) {
+      const s4v ka = pk4z(kk, lo2), va = pk4z(vv, lo2);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      s[t] = mfma(kk.x, bq0[t], cs[t]);
-      dp[t] = mfma(vv.x, bo0[t], cd[t]);
-    }
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma_bf(ka, qb[t], cs[t]);
+        dp[t] = mfma_bf(va, ob[t], cd[t]);
+      }
+    } else {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      s[t] = mfma(kk.y, bq1[t], s[t]);
-      dp[t] = mfma(vv.y, bo1[t], dp[t]);
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(kk.x, bq0[t], cs[t]);
+        dp[t] = mfma(vv.x, bo0[t], cd[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(kk.y, bq1[t], s[t]);
+        dp[t] = mfma(vv.y, bo1[t], dp[t]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -835,31 +896,40 @@ __device__ __forceinline__ void attn8_bwd2_dq(const A8Bwd2& a, int bx, float* re
           if (!(key >= sp.b[t] && key < sp.e[t] && key < sp.ce)) ds[r] = 0.f;
         }
       }
-      dq[t] = mfma(kt.x, ds[0], dq[t]);
-      dq[t] = mfma(kt.y, ds[1], dq[t]);
-      dq[t] = mfma(kt.z, ds[2], dq[t]);
-      dq[t] = mfma(kt.w, ds[3], dq[t]);
+      if constexpr (BF) {
+        dq[t] = mfma_bf(pk4(kt), pk4(ds[0], ds[1], ds[2], ds[3]), dq[t]);
+      } else {
+        dq[t] = mfma(kt.x, ds[0], dq[t]);
+        dq[t] = mfma(kt.y, ds[1], dq[t]);
+        dq[t] = mfma(kt.z, ds[2], dq[t]);
+        dq[t] = mfma(kt.w, ds[3], dq[t]);
+      }
     }
   };
   const int cmax = (Nq - 16) * 32;
+  auto ldp = [&](Rsrc r, int off) {
+    if constexpr (BF) return bl4(r, op, off); else return bl2(r, op, off);
+  };
   int o0 = min(sp.cb * 32, cmax), o1 = min(sp.cb * 32 + 512, cmax);
-  float2 ka = bl2(rk, op, o0), va = bl2(rv, op, o0);
+  auto ka = ldp(rk, o0);
+  auto va = ldp(rv, o0);
   float4 ta = bl4(rkt, oq, o0);
   __builtin_amdgcn_sched_barrier(0);
-  float2 kb = bl2(rk, op, o1), vb = bl2(rv, op, o1);
+  auto kb = ldp(rk, o1);
+  auto vb = ldp(rv, o1);
   float4 tb = bl4(rkt, oq, o1);
   __builtin_amdgcn_sched_barrier(0);
   for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
     tile(ka, va, ta, k0);
     o0 = min(k0 * 32 + 1024, cmax);
-    ka = bl2(rk, op, o0);
-    va = bl2(rv, op, o0);
+    ka = ldp(rk, o0);
+    va = ldp(rv, o0);
     ta = bl4(rkt, oq, o0);
     __builtin_amdgcn_sched_barrier(0);
     tile(kb, vb, tb, k0 + 16);
     o1 = min(k0 * 32 + 1536, cmax);
-    kb = bl2(rk, op, o1);
-    vb = bl2(rv, op, o1);
+    kb = ldp(rk, o1);
+    vb = ldp(rv, o1);
     tb = bl4(rkt, oq, o1);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -881,7 +951,7 @@ __device__ __forceinline__ void attn8_bwd2_dq(const A8Bwd2& a, int bx, float* re
   }
 }
 
-template <int RT, int W>
+template <int RT, int W, bool BF>
 __device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* red) {
   const int h = blockIdx.y;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
@@ -893,30 +963,42 @@ __device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* r
   const Rsrc rq = mk_rsrc(a.Qp + hb, Nq * 8), ro = mk_rsrc(a.dOp + hb, Nq * 8);
   const Rsrc rqt = mk_rsrc(a.Qq + hb, Nq * 8), rot = mk_rsrc(a.dOq + hb, Nq * 8);
   const Rsrc rl = mk_rsrc(a.NL + (int64_t)h * Nq, Nq), rd = mk_rsrc(a.ndelta + (int64_t)h * Nq, Nq);
-  const int op = off_pair(i, g), oq = off_quad(i, g), os = 16 * g;
+  const int op = BF ? off_pair4(i, g) : off_pair(i, g), oq = off_quad(i, g), os = 16 * g;
+  const bool lo2 = g < 2;
   float bk0[RT], bk1[RT], bv0[RT], bv1[RT];
+  s4v kb4[RT], vb4[RT];
   f4v dk[RT], dv[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const int kc = min(sp.row[t], Nq - 1);
-    const float2 bk = ld2(a.Kp + hb + (int64_t)kc * 8 + 2 * g);
-    const float2 bv = ld2(a.Vp + hb + (int64_t)kc * 8 + 2 * g);
-    bk0[t] = bk.x * a.qscale;
-    bk1[t] = bk.y * a.qscale;
-    bv0[t] = bv.x;
-    bv1[t] = bv.y;
+    if constexpr (BF) {
+      const float4 k4 = ld4(a.Kp + hb + (int64_t)kc * 8 + 4 * (g & 1));
+      kb4[t] = pk4z(make_float4(k4.x * a.qscale, k4.y * a.qscale, k4.z * a.qscale, k4.w * a.qscale), lo2);
+      vb4[t] = pk4z(ld4(a.Vp + hb + (int64_t)kc * 8 + 4 * (g & 1)), lo2);
+    } else {
+      const float2 bk = ld2(a.Kp + hb + (int64_t)kc * 8 + 2 * g);
+      const float2 bv = ld2(a.Vp + hb + (int64_t)kc * 8 + 2 * g);
+      bk0[t] = bk.x * a.qscale;
+      bk1[t] = bk.y * a.qscale;
+      bv0[t] = bv.x;
+      bv1[t] = bv.y;
+    }
     dk[t] = f4z();
     dv[t] = f4z();
   }
+  typedef typename std::conditional<BF, float4, float2>::type PT;
   struct T6 {
-    float2 q, o;
+    PT q, o;
     float4 qt, ot, nl, nd;
+  };
+  auto ldp = [&](Rsrc r, int off) {
+    if constexpr (BF) return bl4(r, op, off); else return bl2(r, op, off);
   };
   auto load = [&](int q0) {
     const int ob = min(q0 * 32, (Nq - 16) * 32), os_ = min(q0 * 4, (Nq - 16) * 4);
     T6 x;
-    x.q = bl2(rq, op, ob);
-    x.o = bl2(ro, op, ob);
+    x.q = ldp(rq, ob);
+    x.o = ldp(ro, ob);
     x.qt = bl4(rqt, oq, ob);
     x.ot = bl4(rot, oq, ob);
     x.nl = bl4(rl, os, os_);
@@ -927,15 +1009,24 @@ __device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* r
     const bool full = q0 >= sp.ilo && q0 + 16 <= sp.ihi && q0 + 16 <= sp.ce;
     const f4v nl = f4v{x.nl.x, x.nl.y, x.nl.z, x.nl.w}, nd = f4v{x.nd.x, x.nd.y, x.nd.z, x.nd.w};
     f4v s[RT], dp[RT];
+    if constexpr (BF) {
+      const s4v qa = pk4z(x.q, lo2), oa = pk4z(x.o, lo2);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      s[t] = mfma(x.q.x, bk0[t], nl);
-      dp[t] = mfma(x.o.x, bv0[t], nd);
-    }
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma_bf(qa, kb4[t], nl);
+        dp[t] = mfma_bf(oa, vb4[t], nd);
+      }
+    } else {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      s[t] = mfma(x.q.y, bk1[t], s[t]);
-      dp[t] = mfma(x.o.y, bv1[t], dp[t]);
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(x.q.x, bk0[t], nl);
+        dp[t] = mfma(x.o.x, bv0[t], nd);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        s[t] = mfma(x.q.y, bk1[t], s[t]);
+        dp[t] = mfma(x.o.y, bv1[t], dp[t]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -951,14 +1042,19 @@ __device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* r
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) ds[r] = p[r] * dp[t][r];
-      dv[t] = mfma(x.ot.x, p[0], dv[t]);
-      dk[t] = mfma(x.qt.x, ds[0], dk[t]);
-      dv[t] = mfma(x.ot.y, p[1], dv[t]);
-      dk[t] = mfma(x.qt.y, ds[1], dk[t]);
-      dv[t] = mfma(x.ot.z, p[2], dv[t]);
-      dk[t] = mfma(x.qt.z, ds[2], dk[t]);
-      dv[t] = mfma(x.ot.w, p[3], dv[t]);
-      dk[t] = mfma(x.qt.w, ds[3], dk[t]);
+      if constexpr (BF) {
+        dv[t] = mfma_bf(pk4(x.ot), pk4(p[0], p[1], p[2], p[3]), dv[t]);
+        dk[t] = mfma_bf(pk4(x.qt), pk4(ds[0], ds[1], ds[2], ds[3]), dk[t]);
+      } else {
+        dv[t] = mfma(x.ot.x, p[0], dv[t]);
+        dk[t] = mfma(x.qt.x, ds[0], dk[t]);
+        dv[t] = mfma(x.ot.y, p[1], dv[t]);
+        dk[t] = mfma(x.qt.y, ds[1], dk[t]);
+        dv[t] = mfma(x.ot.z, p[2], dv[t]);
+        dk[t] = mfma(x.qt.z, ds[2], dk[t]);
+        dv[t] = mfma(x.ot.w, p[3], dv[t]);
+        dk[t] = mfma(x.qt.w, ds[3], dk[t]);
+      }
     }
   };
   T6 xa = load(sp.cb);
@@ -998,13 +1094,13 @@ __device__ __forceinline__ void attn8_bwd2_dkv(const A8Bwd2& a, int bx, float* r
   }
 }
 
-template <int RT, int W>
+template <int RT, int W, bool BF = false>
 __global__ void __launch_bounds__(64 * W) attn8_bwd2_kernel(A8Bwd2 a) {
   __shared__ float red[W * RT * 16 * 16];
   if ((int)blockIdx.x < a.nbq)
-    attn8_bwd2_dq<RT, W>(a, blockIdx.x, red);
+    attn8_bwd2_dq<RT, W, BF>(a, blockIdx.x, red);
   else
-    attn8_bwd2_dkv<RT, W>(a, blockIdx.x - a.nbq, red);
+    attn8_bwd2_dkv<RT, W, BF>(a, blockIdx.x - a.nbq, red);
 }
 
 // ------------------------------------------------------------------------------------ host
@@ -1028,43 +1124,60 @@ static int pick_splits(int N, int H, int64_t splits) {
 // splits < 0 forces W = -splits (sweeps and tests).
 static int pick_w(int ntiles) { return ntiles >= 32 ? 8 : (ntiles >= 12 ? 4 : 2); }
 
-template <int W>
+template <int W, bool BF>
 static void fwd2_go(const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H, const int* sid,
                     const int* sptr, float qs, float* O, float* L) {
   dim3 grid(ceil_div(Nq, 16), H);
-  attn8_fwd2_kernel<1, W><<<grid, 64 * W, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
+  attn8_fwd2_kernel<1, W, BF><<<grid, 64 * W, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
+}
+
+template <bool BF>
+static void launch_fwd2_p(int var, const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H,
+                          const int* sid, const int* sptr, float qs, float* O, float* L) {
+  const int W = var > 0 ? var : pick_w(ceil_div(N, 16));
+  switch (W) {
+    case 2: fwd2_go<2, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 3: fwd2_go<3, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 4: fwd2_go<4, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 5: fwd2_go<5, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    case 6: fwd2_go<6, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+    default: fwd2_go<8, BF>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
+  }
 }
 
 static void launch_fwd2(int var, const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H,
-                        const int* sid, const int* sptr, float qs, float* O, float* L) {
-  const int W = var > 0 ? var : pick_w(ceil_div(N, 16));
-  switch (W) {
-    case 2: fwd2_go<2>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-    case 3: fwd2_go<3>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-    case 4: fwd2_go<4>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-    case 5: fwd2_go<5>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-    case 6: fwd2_go<6>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-    default: fwd2_go<8>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L); break;
-  }
+                        const int* sid, const int* sptr, float qs, float* O, float* L, bool bf16 = false) {
+  if (bf16)
+    launch_fwd2_p<true>(var, Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
+  else
+    launch_fwd2_p<false>(var, Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
 }
 
-template <int W>
+template <int W, bool BF>
 static void bwd2_go(A8Bwd2 b) {
   b.nbq = ceil_div(b.Nq, 16);
   dim3 grid(2 * b.nbq, b.H);
-  attn8_bwd2_kernel<1, W><<<grid, 64 * W, 0, stream()>>>(b);
+  attn8_bwd2_kernel<1, W, BF><<<grid, 64 * W, 0, stream()>>>(b);
 }
 
-static void launch_bwd2(int var, const A8Bwd2& b) {
+template <bool BF>
+static void launch_bwd2_p(int var, const A8Bwd2& b) {
   const int W = var > 0 ? var : pick_w(ceil_div(b.N, 16));
   switch (W) {
-    case 2: bwd2_go<2>(b); break;
-    case 3: bwd2_go<3>(b); break;
-    case 4: bwd2_go<4>(b); break;
-    case 5: bwd2_go<5>(b); break;
-    case 6: bwd2_go<6>(b); break;
-    default: bwd2_go<8>(b); break;
+    case 2: bwd2_go<2, BF>(b); break;
+    case 3: bwd2_go<3, BF>(b); break;
+    case 4: bwd2_go<4, BF>(b); break;
+    case 5: bwd2_go<5, BF>(b); break;
+    case 6: bwd2_go<6, BF>(b); break;
+    default: bwd2_go<8, BF>(b); break;
   }
+}
+
+static void launch_bwd2(int var, const A8Bwd2& b, bool bf16 = false) {
+  if (bf16)
+    launch_bwd2_p<true>(var, b);
+  else
+    launch_bwd2_p<false>(var, b);
 }
 
 // chosen W of the v2 kernels for a shape (tools / tests)
@@ -1102,7 +1215,8 @@ std::vector<at::Tensor> attn8_pack(const at::Tensor& qkv_, int64_t H) {
 
 std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, const at::Tensor& Vq,
                                   const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N, double scale,
-                                  int64_t splits) {
+                                  int64_t splits, bool bf16) {
+  HY_CHECK(!bf16 || splits <= 0, "attn8_fwd: bf16 MFMA mode is the v2 (one-launch) kernel only");
   const int64_t H = Qp.size(0), Nq = Qp.size(1);
   HY_CHECK(Qp.is_contiguous() && Kp.is_contiguous() && Vq.is_contiguous() && Qp.size(2) == 8 && Nq % 16 == 0 &&
                Nq >= N && Kp.sizes() == Qp.sizes() && Vq.numel() == Qp.numel(),
@@ -1114,7 +1228,8 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
   const float qs = (float)scale * kLog2e;
   if (splits <= 0) {  // v2: one launch, in-workgroup key split (variant -splits, 0 = default)
     launch_fwd2((int)(-splits), Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(), (int)N, (int)Nq,
-                (int)H, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), qs, O.data_ptr<float>(), L.data_ptr<float>());
+                (int)H, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), qs, O.data_ptr<float>(), L.data_ptr<float>(),
+                bf16);
     return {O, L};
   }
   const int S = pick_splits((int)N, (int)H, splits);
@@ -1240,7 +1355,7 @@ at::Tensor attn8_bwd_sum(const at::Tensor& pq, const at::Tensor& pkv) {
 at::Tensor attn8_bwd_packed(const at::Tensor& ndelta, const at::Tensor& dOp, const at::Tensor& dOq,
                             const at::Tensor& LSE2, const at::Tensor& Qp, const at::Tensor& Qq, const at::Tensor& Kp,
                             const at::Tensor& Kq, const at::Tensor& Vp, const at::Tensor& seg_id,
-                            const at::Tensor& seg_ptr, int64_t N, double scale) {
+                            const at::Tensor& seg_ptr, int64_t N, double scale, bool bf16) {
   const int64_t H = Qp.size(0), Nq = Qp.size(1), F = 8 * H;
   chk_bwd(Qp, LSE2, ndelta, dOp, N);
   chk_seg(seg_id, seg_ptr, N);
@@ -1267,7 +1382,7 @@ at::Tensor attn8_bwd_packed(const at::Tensor& ndelta, const at::Tensor& dOp, con
   b.scale = (float)scale;
   b.qscale = (float)scale * kLog2e;
   b.dqkv = dqkv.data_ptr<float>();
-  launch_bwd2(0, b);
+  launch_bwd2(0, b, bf16);
   return dqkv;
 }
 
@@ -1352,14 +1467,14 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("attn8_pack(Tensor qkv, int H) -> Tensor[]");
   m.def("attn8_v2_shape(int N, int H) -> int[]", hy::a8::attn8_v2_shape);
   m.def(
-      "attn8_fwd(Tensor Qp, Tensor Kp, Tensor Vq, Tensor seg_id, Tensor seg_ptr, int N, float scale, int splits) -> "
-      "Tensor[]");
+      "attn8_fwd(Tensor Qp, Tensor Kp, Tensor Vq, Tensor seg_id, Tensor seg_ptr, int N, float scale, int splits, "
+      "bool bf16=False) -> Tensor[]");
   m.def(
       "attn8_bwd(Tensor dO, Tensor O, Tensor LSE2, Tensor Qp, Tensor Qq, Tensor Kp, Tensor Kq, Tensor Vp, "
       "Tensor seg_id, Tensor seg_ptr, float scale, int splits) -> Tensor");
   m.def(
       "attn8_bwd_packed(Tensor ndelta, Tensor dOp, Tensor dOq, Tensor LSE2, Tensor Qp, Tensor Qq, Tensor Kp, "
-      "Tensor Kq, Tensor Vp, Tensor seg_id, Tensor seg_ptr, int N, float scale) -> Tensor");
+      "Tensor Kq, Tensor Vp, Tensor seg_id, Tensor seg_ptr, int N, float scale, bool bf16=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

@@ -160,6 +160,10 @@ def encode(model, ctx):
     cfg.side = _streams.enabled(x0)
     # 8-wide heads: MFMA attention (csrc/attention8.hip) on operands the node kernel packs
     cfg.a8 = cfg.F // cfg.heads == 8 and _mode.fused("attn8")
+    # precision "bf16": the attention products on bf16 MFMA (fp32 accumulate, fp32 softmax)
+    from .linear import get_precision
+
+    cfg.bf16 = cfg.a8 and cfg.splits <= 0 and get_precision() == "bf16"
 
     basis = ctx.rbf_basis
     cfg.cutoff, cfg.exponent = float(basis.cutoff), int(basis.envelope.p - 1)
@@ -302,7 +306,8 @@ class _GPSEncoder(torch.autograd.Function):
             with side:
                 side.used(x, *(pk if cfg.a8 else [qkv]))
                 if cfg.a8:
-                    O, LSE = ops.attn8_fwd(pk[0], pk[2], pk[5], cfg.sid, cfg.sptr, x.shape[0], cfg.scale, cfg.splits)
+                    O, LSE = ops.attn8_fwd(pk[0], pk[2], pk[5], cfg.sid, cfg.sptr, x.shape[0], cfg.scale, cfg.splits,
+                                           cfg.bf16)
                 else:
                     O, LSE = ops.attn_fwd(qkv, cfg.sid, cfg.sptr, cfg.heads, cfg.scale, cfg.span, cfg.splits)
                 z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
@@ -400,7 +405,7 @@ class _GPSEncoder(torch.autograd.Function):
                     dz2, da, _, dw2n, db2n, nd, dOp, dOq = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng,
                                                                           s1, p, nv, s["O"])
                     dqkv = ops.attn8_bwd_packed(nd, dOp, dOq, s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid,
-                                                cfg.sptr, s["x"].shape[0], cfg.scale)
+                                                cfg.sptr, s["x"].shape[0], cfg.scale, cfg.bf16)
                     dO = None
                 elif cfg.a8:
                     dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)

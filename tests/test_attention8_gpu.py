@@ -71,3 +71,43 @@ def test_attn8_v2_large_scores_rescale():
     ref.backward(dO.double().cpu())
     dqkv = ops.attn8_bwd(dO, O, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, sc, 0)
     torch.testing.assert_close(dqkv.double().cpu(), x.grad, rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("N", [37, 300, 2560])
+@pytest.mark.parametrize("scope", ["batch", "graph"])
+def test_attn8_bf16_mfma_close_to_reference(N, scope):
+    """bf16 MFMA mode of the v2 kernels (precision "bf16": operands rounded to bf16, fp32
+    accumulate and softmax): forward output and q / k / v gradients within bf16 rounding of
+    the float64 reference (relative to each tensor's scale)."""
+    torch.manual_seed(N + 7)
+    dev = torch.device("cuda")
+    H = 8
+    ops = _native.ops()
+    qkv = (torch.randn(N, 24 * H, device=dev) * 1.5).contiguous()
+    sid, sptr = _segments(N, scope, dev)
+    sc = 1.0 / math.sqrt(8)
+    Qp, Qq, Kp, Kq, Vp, Vq = ops.attn8_pack(qkv, H)
+    O, L2 = ops.attn8_fwd(Qp, Kp, Vq, sid, sptr, N, sc, 0, True)
+    x = qkv.double().cpu().requires_grad_()
+    ref = attention_reference(x, H, sid.cpu(), sc)
+    err = (O.double().cpu() - ref.detach()).abs().max().item()
+    assert err < 3e-2 * ref.abs().max().item(), err
+    dO = torch.randn(N, 8 * H, device=dev)
+    ref.backward(dO.double().cpu())
+    # the packed backward operands (-delta, dO in the pair / quad layouts), as gf_att_bwd writes them
+    Nq = Qp.shape[1]
+    dOp, dOq = ops.attn8_pack(torch.cat([dO, dO, dO], 1).contiguous(), H)[:2]
+    nd = torch.zeros(H, Nq, device=dev)
+    nd[:, :N] = -(dO * O).view(N, H, 8).sum(-1).t()
+    dqkv = ops.attn8_bwd_packed(nd, dOp, dOq, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, N, sc, True)
+    g = x.grad
+    for blk in range(3):
+        a, b = dqkv[:, blk * 8 * H:(blk + 1) * 8 * H].double().cpu(), g[:, blk * 8 * H:(blk + 1) * 8 * H]
+        err = (a - b).abs().max().item()
+        assert err < 4e-2 * b.abs().max().item(), (blk, err, b.abs().max().item())
+    # the fp32 mode of the same packed entry point matches the reference tightly
+    O32, L32 = ops.attn8_fwd(Qp, Kp, Vq, sid, sptr, N, sc, 0)
+    nd32 = torch.zeros(H, Nq, device=dev)
+    nd32[:, :N] = -(dO * O32).view(N, H, 8).sum(-1).t()
+    dq32 = ops.attn8_bwd_packed(nd32, dOp, dOq, L32, Qp, Qq, Kp, Kq, Vp, sid, sptr, N, sc)
+    torch.testing.assert_close(dq32.double().cpu(), g, rtol=1e-4, atol=1e-4)
