@@ -494,7 +494,7 @@ void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::option
   const size_t lds = (size_t)lds_w * rpg::kBM * sizeof(float) + (size_t)prog.numel() * sizeof(int);
   HY_CHECK(lds <= 160 * 1024, "rowprog: activations + program exceed the 160 KiB LDS");
   // workgroup size (HYDRA_ROWPROG_THREADS: 256 / 512 / 1024).  md17 PAINN forces on MI355X:
-  // 512 -> 11.36k, 1024 -> 11.27k, 256 -> 9.85k graphs/s (tools/gpu_ab_rowprog.sh)
+  // 512 -> 11.36k, 1024 -> 11.27k, 256 -> 9.85k graphs/s (tools/gpu_ab_env.sh)
   static int nt = [] {
     const char* e = std::getenv("HYDRA_ROWPROG_THREADS");
     const int v = e ? std::atoi(e) : 512;

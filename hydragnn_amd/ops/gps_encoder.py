@@ -11,12 +11,21 @@ Reference computation per layer (``globalAtt/gps.py:103-152`` around
     z3    = drop(W2 drop(relu(W1 out + b1)) + b2) + out
     x'    = relu(BN4(BN3(z3)))            (rows >= num_valid -> 0)
 
-Kernel schedule per layer (forward): wprep, node GEMM [AB | qkv] (+ previous layer's
-BN3/BN4 finalise + apply in its prologue), {side stream: attention, o-proj + BN2 stats},
-edge linear, PNA aggregate, post/lin GEMM chain + BN1 stats, {join} BN1/BN2 apply + MLP
-chain + BN3 stats.  Backward mirrors it (mlp, {side: BN2 + o-proj dgrad, attention},
-BN1 + lin/post dgrad, PNA, edge dgrad, {join} node dgrad + previous pair statistics), with
-every weight gradient of the stack in ONE grouped launch pair at the end.
+Stream schedule (all captured into the step graph as parallel branches):
+
+* prologue: every layer's weight prep (one launch); on a third stream the edge chain
+  (edge embedding, radial basis + every layer's radial embedding, every layer's edge term
+  C = r Wr^T + e Wd^T + bc in one launch) beside the node embedding and the first layer;
+* forward per layer: node GEMM [AB | qkv] (+ previous layer's BN3/BN4 finalise + apply in
+  its prologue), {side stream: attention, o-proj + BN2 stats}, PNA aggregate (joins the
+  edge chain once), post/lin GEMM chain + BN1 stats, {join} BN1/BN2 apply + MLP chain + BN3
+  stats;
+* backward per layer: mlp, {side: BN2 + o-proj dgrad whose epilogue packs the attention
+  operands, attention}, BN1 + lin/post dgrad, [third stream: the previous layer's weight
+  gradients, one grouped launch pair, beside this layer's attention], PNA, [third stream:
+  edge dgrad (the first layer's on a fourth)], {join} node dgrad + previous pair statistics;
+  the first layer's and the embeddings' weight gradients close the backward on the main
+  stream.
 
 BN4 o BN3 is a single per-column affine map: BN4's batch statistics are derived from
 BN3's (mean4 = beta3, var4 = gamma3^2 var3 / (var3 + eps3)), and its backward is closed-
