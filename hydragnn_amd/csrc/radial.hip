@@ -549,9 +549,90 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> radial_bw
   return {ddist, dfreq, dWemb, dbemb, dWlin};
 }
 
+// ---------------------------------------------------------------- MACE radial embedding
+// out[e, k] = sqrt(2/rc) sin(w_k r)/r * env(r/rc) [r < rc], env(u) = 1 - (p+1)(p+2)/2 u^p +
+// p(p+2) u^(p+1) - p(p+1)/2 u^(p+2): reference mace_utils/modules/radial.py:23-63 (BesselBasis),
+// :98-130 (PolynomialCutoff), blocks.py:148-162 (RadialEmbeddingBlock).  As torch ops the
+// basis + cutoff is ~15 elementwise launches over [E, K]; here one launch writes it, and the
+// backward (edge-length gradient, first order) is one more.
+struct MaceRadial {
+  float pref, rc, p;
+  __device__ __forceinline__ void env(float r, float& e, float& de) const {
+    if (!(r < rc)) { e = 0.f; de = 0.f; return; }
+    const float u = r / rc;
+    const float up = powf(u, p - 1.f);  // u^(p-1); u > 0 for a real edge
+    const float a = 0.5f * (p + 1.f) * (p + 2.f), b = p * (p + 2.f), c = 0.5f * p * (p + 1.f);
+    const float u_p = up * u;
+    e = 1.f - a * u_p + b * u_p * u - c * u_p * u * u;
+    de = (-a * p * up + b * (p + 1.f) * u_p - c * (p + 2.f) * u_p * u) / rc;
+  }
+};
+
+__global__ void __launch_bounds__(256) mace_radial_fwd_kernel(const float* __restrict__ r, const float* __restrict__ w,
+                                                              float* __restrict__ out, int E, int K, MaceRadial m) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)E * K) return;
+  const int e = (int)(t / K), k = (int)(t % K);
+  const float x = r[e];
+  float en, den;
+  m.env(x, en, den);
+  out[t] = m.pref * sinf(w[k] * x) / x * en;
+}
+
+__global__ void __launch_bounds__(256) mace_radial_bwd_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                                                              const float* __restrict__ w, float* __restrict__ dr,
+                                                              int E, int K, MaceRadial m) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float x = r[e];
+  float en, den;
+  m.env(x, en, den);
+  const float inv = 1.f / x;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float s, c;
+    sincosf(w[k] * x, &s, &c);
+    const float b = s * inv;                        // sin(w r)/r
+    const float db = (w[k] * c - b) * inv;          // d/dr sin(w r)/r
+    acc += g[(int64_t)e * K + k] * (db * en + b * den);
+  }
+  dr[e] = m.pref * acc;
+}
+
+at::Tensor mace_radial_fwd(const at::Tensor& r_, const at::Tensor& w, double rc, double p) {
+  HY_CHECK_CUDA(r_);
+  auto r = r_.contiguous();
+  HY_CHECK_F32(r);
+  HY_CHECK_F32(w);
+  const int E = (int)r.numel(), K = (int)w.numel();
+  auto out = at::empty({E, K}, r.options());
+  MaceRadial m{(float)std::sqrt(2.0 / rc), (float)rc, (float)p};
+  if ((int64_t)E * K > 0)
+    mace_radial_fwd_kernel<<<ceil_div((int64_t)E * K, 256), 256, 0, stream()>>>(
+        r.data_ptr<float>(), w.contiguous().data_ptr<float>(), out.data_ptr<float>(), E, K, m);
+  return out;
+}
+
+at::Tensor mace_radial_bwd(const at::Tensor& g_, const at::Tensor& r_, const at::Tensor& w, double rc, double p) {
+  HY_CHECK_CUDA(g_);
+  auto g = g_.contiguous(), r = r_.contiguous();
+  HY_CHECK_F32(g);
+  HY_CHECK_F32(r);
+  const int E = (int)r.numel(), K = (int)w.numel();
+  HY_CHECK(g.numel() == (int64_t)E * K, "mace_radial_bwd: gradient shape");
+  auto dr = at::empty_like(r);
+  MaceRadial m{(float)std::sqrt(2.0 / rc), (float)rc, (float)p};
+  if (E > 0)
+    mace_radial_bwd_kernel<<<ceil_div((int64_t)E, 256), 256, 0, stream()>>>(
+        g.data_ptr<float>(), r.data_ptr<float>(), w.contiguous().data_ptr<float>(), dr.data_ptr<float>(), E, K, m);
+  return dr;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("mace_radial_fwd(Tensor r, Tensor w, float rc, float p) -> Tensor");
+  m.def("mace_radial_bwd(Tensor g, Tensor r, Tensor w, float rc, float p) -> Tensor");
   m.def(
       "radial_fwd(Tensor dist, Tensor freq, Tensor Wemb, Tensor bemb, Tensor Wlin, float cutoff, int exponent) -> "
       "(Tensor, Tensor)");
@@ -568,4 +649,6 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radial_fwd", hy::radial_fwd);
   m.impl("radial_bwd", hy::radial_bwd);
   m.impl("radial_fwd_multi", hy::radial_fwd_multi);
+  m.impl("mace_radial_fwd", hy::mace_radial_fwd);
+  m.impl("mace_radial_bwd", hy::mace_radial_bwd);
 }

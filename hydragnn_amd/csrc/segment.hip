@@ -166,6 +166,101 @@ __global__ void __launch_bounds__(256) seg_minmax_kernel(const float* __restrict
   arg[t] = besti;
 }
 
+// PNA degree-scaler aggregation of a per-row message table in one pass (the PNAEq message,
+// reference PNAEqStack.py:59-66 / :310-387 over PyG DegreeScalerAggregation with aggregators
+// [mean, min, max, std] and any of the 5 scalers incl. inverse_linear): one thread per
+// (segment, column) walks the segment's rows once for sum, sum of squares and the two
+// extrema, then writes out[n, s*4F + k*F + f] = scaler_s(deg_n) * agg_k for every scaler.
+// The composite it replaces (ops.pna.pna_aggregate_composite) takes 4 reductions, a
+// sqrt/clamp/mask chain, two cats and S multiplies.  Scaler codes are packed 3 bits each
+// (0 identity, 1 amplification, 2 attenuation, 3 linear, 4 inverse_linear).
+__device__ __forceinline__ float pna_scaler(int code, float d, float avg_log, float avg_lin) {
+  switch (code) {
+    case 0: return 1.f;
+    case 1: return logf(d + 1.f) / avg_log;
+    case 2: return avg_log / logf(d + 1.f);
+    case 3: return d / avg_lin;
+    default: return avg_lin / d;
+  }
+}
+
+struct PnaAggArgs {
+  const float* x;
+  const int* rowptr;
+  const int* perm;
+  float* out;    // [N, S*4F]
+  float* stat;   // [N, 2F]: mean, std (0 where masked)
+  int* arg;      // [N, 2F]: row of the min / max (-1 for an empty segment)
+  const float* g;  // backward: dL/dout
+  float* dx;       // backward: [E, F]
+  int N, F, S, codes;
+  float avg_log, avg_lin, eps, sqrt_eps;
+};
+
+__global__ void __launch_bounds__(256) seg_pna_agg_kernel(PnaAggArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.N * a.F) return;
+  const int F = a.F, n = (int)(t / F), f = (int)(t % F);
+  const int beg = a.rowptr[n], end = a.rowptr[n + 1];
+  float s = 0.f, s2 = 0.f, mn = INFINITY, mx = -INFINITY;
+  int imn = -1, imx = -1;
+  for (int e = beg; e < end; ++e) {
+    const int row = a.perm ? a.perm[e] : e;
+    const float v = a.x[(int64_t)row * F + f];
+    s += v;
+    s2 += v * v;
+    if (v < mn) { mn = v; imn = row; }
+    if (v > mx) { mx = v; imx = row; }
+  }
+  const float d = (float)max(end - beg, 1);
+  const float mean = s / d;
+  float sd = sqrtf(fmaxf(s2 / d - mean * mean, a.eps));
+  if (sd <= a.sqrt_eps) sd = 0.f;
+  if (imn < 0) { mn = 0.f; mx = 0.f; }
+  const float agg[4] = {mean, mn, mx, sd};
+  float* o = a.out + (int64_t)n * a.S * 4 * F + f;
+  for (int si = 0; si < a.S; ++si) {
+    const float sc = pna_scaler((a.codes >> (3 * si)) & 7, d, a.avg_log, a.avg_lin);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[(si * 4 + k) * F] = agg[k] * sc;
+  }
+  a.stat[(int64_t)n * 2 * F + f] = mean;
+  a.stat[(int64_t)n * 2 * F + F + f] = sd;
+  a.arg[(int64_t)n * 2 * F + f] = imn;
+  a.arg[(int64_t)n * 2 * F + F + f] = imx;
+}
+
+// dx[row, f] = Gmean/d + Gstd (x - mean)/(d std) + [row == argmin] Gmin + [row == argmax] Gmax
+// with G_k = sum_s scaler_s(d) g[n, s*4F + k*F + f]: the same (segment, column) threads
+// fold the scalers once and write every row of the segment (rows partition the segments,
+// so each dx element is written exactly once, without atomics).
+__global__ void __launch_bounds__(256) seg_pna_agg_bwd_kernel(PnaAggArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.N * a.F) return;
+  const int F = a.F, n = (int)(t / F), f = (int)(t % F);
+  const int beg = a.rowptr[n], end = a.rowptr[n + 1];
+  if (end <= beg) return;
+  const float d = (float)(end - beg);
+  float G[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* gp = a.g + (int64_t)n * a.S * 4 * F + f;
+  for (int si = 0; si < a.S; ++si) {
+    const float sc = pna_scaler((a.codes >> (3 * si)) & 7, d, a.avg_log, a.avg_lin);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) G[k] += sc * gp[(si * 4 + k) * F];
+  }
+  const float mean = a.stat[(int64_t)n * 2 * F + f], sd = a.stat[(int64_t)n * 2 * F + F + f];
+  const int imn = a.arg[(int64_t)n * 2 * F + f], imx = a.arg[(int64_t)n * 2 * F + F + f];
+  const float gm = G[0] / d, gs = sd > 0.f ? G[3] / (d * sd) : 0.f;
+  for (int e = beg; e < end; ++e) {
+    const int row = a.perm ? a.perm[e] : e;
+    const float v = a.x[(int64_t)row * F + f];
+    float r = gm + gs * (v - mean);
+    if (row == imn) r += G[1];
+    if (row == imx) r += G[2];
+    a.dx[(int64_t)row * F + f] = r;
+  }
+}
+
 // out[E, F] = 0; out[arg[n,f], f] = g[n,f]   (segments are disjoint -> no conflicts)
 __global__ void __launch_bounds__(256) scatter_arg_kernel(const float* __restrict__ g,
                                                           const int* __restrict__ arg,
@@ -433,9 +528,75 @@ at::Tensor gather_arg(const at::Tensor& x_, const at::Tensor& arg) {
   return out;
 }
 
+static PnaAggArgs pna_agg_args(const at::Tensor& x, const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm,
+                               int64_t S, int64_t codes, double avg_log, double avg_lin) {
+  HY_CHECK_CUDA(x);
+  HY_CHECK_F32(x);
+  HY_CHECK(x.dim() == 2 && x.is_contiguous(), "seg_pna_agg: x must be a contiguous [E, F] table");
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(S >= 1 && S <= 8, "seg_pna_agg: 1..8 scalers");
+  PnaAggArgs a{};
+  a.x = x.data_ptr<float>();
+  a.rowptr = rowptr.data_ptr<int>();
+  if (perm.has_value() && perm->defined()) {
+    HY_CHECK_I32(*perm);
+    HY_CHECK(perm->numel() == x.size(0), "seg_pna_agg: perm must list every row");
+    a.perm = perm->data_ptr<int>();
+  }
+  a.N = (int)(rowptr.numel() - 1);
+  a.F = (int)x.size(1);
+  a.S = (int)S;
+  a.codes = (int)codes;
+  a.avg_log = (float)avg_log;
+  a.avg_lin = (float)avg_lin;
+  return a;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> seg_pna_agg(const at::Tensor& x, const at::Tensor& rowptr,
+                                                           const c10::optional<at::Tensor>& perm, int64_t S,
+                                                           int64_t codes, double avg_log, double avg_lin, double eps,
+                                                           double sqrt_eps) {
+  auto a = pna_agg_args(x, rowptr, perm, S, codes, avg_log, avg_lin);
+  a.eps = (float)eps;
+  a.sqrt_eps = (float)sqrt_eps;
+  auto out = at::empty({a.N, 4 * S * a.F}, x.options());
+  auto stat = at::empty({a.N, 2 * a.F}, x.options());
+  auto arg = at::empty({a.N, 2 * a.F}, x.options().dtype(at::kInt));
+  a.out = out.data_ptr<float>();
+  a.stat = stat.data_ptr<float>();
+  a.arg = arg.data_ptr<int>();
+  const int64_t tot = (int64_t)a.N * a.F;
+  if (tot > 0) seg_pna_agg_kernel<<<ceil_div(tot, 256), 256, 0, stream()>>>(a);
+  return {out, stat, arg};
+}
+
+at::Tensor seg_pna_agg_bwd(const at::Tensor& g_, const at::Tensor& x, const at::Tensor& rowptr,
+                           const c10::optional<at::Tensor>& perm, const at::Tensor& stat, const at::Tensor& arg,
+                           int64_t S, int64_t codes, double avg_log, double avg_lin) {
+  auto a = pna_agg_args(x, rowptr, perm, S, codes, avg_log, avg_lin);
+  auto g = g_.contiguous();
+  HY_CHECK_F32(g);
+  HY_CHECK(g.size(0) == a.N && g.size(1) == 4 * S * a.F, "seg_pna_agg_bwd: gradient shape");
+  HY_CHECK(stat.size(0) == a.N && stat.size(1) == 2 * a.F && arg.size(1) == 2 * a.F, "seg_pna_agg_bwd: saved shapes");
+  // every row belongs to exactly one segment (rowptr[N] == E, SegIndex invariant): each
+  // dx row is written by its segment's threads, no zero fill
+  auto dx = at::empty_like(x);
+  a.g = g.data_ptr<float>();
+  a.stat = const_cast<float*>(stat.data_ptr<float>());
+  a.arg = const_cast<int*>(arg.data_ptr<int>());
+  a.dx = dx.data_ptr<float>();
+  const int64_t tot = (int64_t)a.N * a.F;
+  if (tot > 0) seg_pna_agg_bwd_kernel<<<ceil_div(tot, 256), 256, 0, stream()>>>(a);
+  return dx;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("seg_pna_agg(Tensor x, Tensor rowptr, Tensor? perm, int S, int codes, float avg_log, float avg_lin, "
+        "float eps, float sqrt_eps) -> (Tensor, Tensor, Tensor)");
+  m.def("seg_pna_agg_bwd(Tensor g, Tensor x, Tensor rowptr, Tensor? perm, Tensor stat, Tensor arg, int S, "
+        "int codes, float avg_log, float avg_lin) -> Tensor");
   m.def("seg_sum(Tensor x, Tensor rowptr, Tensor? perm, int N, bool mean, Tensor? limit=None) -> Tensor");
   m.def("gather_rows(Tensor x, Tensor idx) -> Tensor");
   m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
@@ -455,4 +616,6 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gather_mul_sum", hy::gather_mul_sum);
   m.impl("gather_mul2", hy::gather_mul2);
   m.impl("seg_sum_out", hy::seg_sum_out);
+  m.impl("seg_pna_agg", hy::seg_pna_agg);
+  m.impl("seg_pna_agg_bwd", hy::seg_pna_agg_bwd);
 }

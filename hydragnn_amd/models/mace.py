@@ -21,8 +21,10 @@ import torch
 from torch import nn
 from torch.nn import ModuleDict, ModuleList, Sequential
 
+from .. import _native
 from ..ops import o3
 from ..ops import segment as seg
+from ..ops.pna import fused
 from ..ops.geometry import edge_vectors_and_lengths
 from .base import Base
 from .layers import Linear
@@ -84,6 +86,20 @@ class PolynomialCutoff(nn.Module):
         return env * (x < self.r_max)
 
 
+class _MaceRadial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, w, rc, p):
+        ctx.save_for_backward(r, w)
+        ctx.cfg = (float(rc), float(p))
+        return _native.ops().mace_radial_fwd(r, w, *ctx.cfg)
+
+    @staticmethod
+    def backward(ctx, g):
+        r, w = ctx.saved_tensors
+        dr = _native.ops().mace_radial_bwd(g, r, w, *ctx.cfg) if ctx.needs_input_grad[0] else None
+        return dr, None, None, None
+
+
 class RadialEmbeddingBlock(nn.Module):
     def __init__(self, r_max, num_bessel, num_polynomial_cutoff, radial_type="bessel", distance_transform=None):
         super().__init__()
@@ -111,6 +127,12 @@ class RadialEmbeddingBlock(nn.Module):
     def forward(self, edge_lengths, z_src=None, z_dst=None):
         """(reference ``blocks.py:148-162``): the cutoff acts on the raw length, the basis on
         the (optionally) transformed one."""
+        bf = self.bessel_fn
+        if (self.distance_transform is None and isinstance(bf, MACEBesselBasis) and edge_lengths.is_cuda
+                and edge_lengths.dtype == torch.float32 and not bf.bessel_weights.requires_grad and fused("radial")):
+            # basis x cutoff in one HIP launch (csrc/radial.hip mace_radial_fwd), first order
+            return _MaceRadial.apply(edge_lengths.reshape(-1), bf.bessel_weights, self.cutoff_fn.r_max,
+                                     self.cutoff_fn.p)
         cutoff = self.cutoff_fn(edge_lengths)
         if self.distance_transform is not None:
             edge_lengths = self.distance_transform(edge_lengths, z_src, z_dst)

@@ -30,7 +30,7 @@ from torch import nn
 from ..ops import segment as seg
 from ..ops import geometry as _geo
 from ..ops.geometry import edge_vectors_and_lengths
-from ..ops.pna import degree_scalers, pna_avg_deg
+from ..ops.pna import degree_scalers, pna_aggregate, pna_avg_deg
 from .layers import Linear
 from .base import Base
 
@@ -252,6 +252,10 @@ class PNAEqMessage(nn.Module):
                                                 Linear(F, 3 * F))
 
     def _aggregate(self, m, si):
+        if m.is_cuda:
+            # one HIP pass each way for [mean, min, max, std] x 5 scalers (csrc/segment.hip
+            # seg_pna_agg); composite fallback inside for double backward / other sets
+            return pna_aggregate(m, si, self.avg_deg, self.aggregators, self.scalers)
         aggs = []
         for a in self.aggregators:
             if a == "mean":

@@ -102,6 +102,47 @@ def pna_aggregate_composite(m, dst_si, avg_deg, aggregators=("mean", "min", "max
     return torch.cat([out * s for s in degree_scalers(deg, avg_deg, scalers)], dim=-1)
 
 
+_SCALER_CODE = {"identity": 0, "amplification": 1, "attenuation": 2, "linear": 3, "inverse_linear": 4}
+_STD_EPS = 1e-5
+
+
+class _PNAAggFused(torch.autograd.Function):
+    """[mean, min, max, std] x scalers of a per-row table in one HIP pass each way
+    (``csrc/segment.hip`` seg_pna_agg / seg_pna_agg_bwd); first-order only."""
+
+    @staticmethod
+    def forward(ctx, m, si, S, codes, avg_log, avg_lin):
+        out, stat, arg = _native.ops().seg_pna_agg(m, si.rowptr, si.perm, S, codes, avg_log, avg_lin, _STD_EPS,
+                                                   _STD_EPS ** 0.5)
+        ctx.save_for_backward(m, stat, arg)
+        ctx.si, ctx.cfg = si, (S, codes, avg_log, avg_lin)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        m, stat, arg = ctx.saved_tensors
+        dm = _native.ops().seg_pna_agg_bwd(g.contiguous(), m, ctx.si.rowptr, ctx.si.perm, stat, arg, *ctx.cfg)
+        return dm, None, None, None, None, None
+
+
+def pna_aggregate(m, si, avg_deg, aggregators=("mean", "min", "max", "std"),
+                  scalers=("identity", "amplification", "attenuation", "linear")):
+    """Degree-scaler aggregation [N, len(aggr)*len(scalers)*F] of a per-row table ``m``
+    over ``si`` (sorted or permuted CSR).  GPU fp32 with the [mean, min, max, std]
+    aggregator set: one fused kernel each way; otherwise (CPU, other aggregators, double
+    backward) the composite."""
+    if (m.is_cuda and fused("pna") and m.dtype == torch.float32 and m.dim() == 2
+            and tuple(aggregators) == ("mean", "min", "max", "std") and 1 <= len(scalers) <= 8):
+        codes = 0
+        for i, s in enumerate(scalers):
+            if s not in _SCALER_CODE:
+                raise ValueError(f"unknown PNA scaler {s}")
+            codes |= _SCALER_CODE[s] << (3 * i)
+        return _PNAAggFused.apply(m.contiguous(), si, len(scalers), codes, float(avg_deg["log"]),
+                                  float(avg_deg["lin"]))
+    return pna_aggregate_composite(m, si, avg_deg, aggregators, scalers)
+
+
 class _PNAFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, AB, C, G, dst_si, src_si, avg_log, avg_lin):
