@@ -195,8 +195,11 @@ struct PlanOut {
 __device__ __forceinline__ int64_t ceil_q(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 __global__ void __launch_bounds__(256) plan_expand_kernel(const int* __restrict__ seed, PlanTabs t, PlanOut o, int Np,
-                                                          int Ep, int Gp, int padded, int batch_scope) {
+                                                          int Ep, int Gp, int padded, int batch_scope,
+                                                          int64_t* __restrict__ rng) {
   __shared__ int pn[kPlanMaxG + 1], pe[kPlanMaxG + 1];
+  // the step's dropout-counter advance rides along (ops/rng.py fold_next_advance)
+  if (rng != nullptr && blockIdx.x == 0 && threadIdx.x == 0) rng[0] += 1;
   const int G = seed[0];
   const int* idx = seed + 1;
   for (int g = threadIdx.x; g < G; g += 256) {
@@ -301,7 +304,12 @@ __global__ void __launch_bounds__(256) plan_expand_kernel(const int* __restrict_
 // out: the packed plan [13 segments] of a (Np, Ep, Gp) layout; seed: [G, idx[0..G)] (int32,
 // device); tabs: nn, ne, noff, eoff, sl, dl, pl, dcum, scum (int32, device)
 void store_plan_expand(const at::Tensor& seed, at::TensorList tabs, at::Tensor out, int64_t Np, int64_t Ep, int64_t Gp,
-                       bool padded, bool batch_scope) {
+                       bool padded, bool batch_scope, const c10::optional<at::Tensor>& rng) {
+  int64_t* rp = nullptr;
+  if (rng.has_value() && rng->defined()) {
+    HY_CHECK(rng->is_cuda() && rng->scalar_type() == at::kLong && rng->numel() >= 1, "store_plan_expand: rng int64");
+    rp = rng->data_ptr<int64_t>();
+  }
   HY_CHECK_CUDA(seed);
   HY_CHECK_I32(seed);
   HY_CHECK_I32(out);
@@ -327,7 +335,7 @@ void store_plan_expand(const at::Tensor& seed, at::TensorList tabs, at::Tensor o
   const int64_t work = Np + Ep + Gp + 1;
   const int blocks = (int)std::min<int64_t>(ceil_div(work, (int64_t)256), 1024);
   plan_expand_kernel<<<blocks, 256, 0, stream()>>>(seed.data_ptr<int>(), t, o, (int)Np, (int)Ep, (int)Gp,
-                                                   padded ? 1 : 0, batch_scope ? 1 : 0);
+                                                   padded ? 1 : 0, batch_scope ? 1 : 0, rp);
 }
 
 }  // namespace hy
@@ -338,7 +346,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "Tensor[] edge_src, Tensor[] graph_src, int pos_field) -> Tensor[]");
   m.def(
       "store_plan_expand(Tensor seed, Tensor[] tabs, Tensor(a!) out, int Np, int Ep, int Gp, bool padded, "
-      "bool batch_scope) -> ()");
+      "bool batch_scope, Tensor(b!)? rng=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

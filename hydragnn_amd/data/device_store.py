@@ -199,13 +199,14 @@ class DeviceGraphStore:
         out[1 + G:] = 0
         return out
 
-    def plan_device(self, seed, lay, out):
+    def plan_device(self, seed, lay, out, rng=None):
         """Expand ``seed`` (device int32, see ``seed``) into the packed plan ``out`` on the device:
-        the same values as ``plan`` (tests/test_device_plan_gpu.py)."""
+        the same values as ``plan`` (tests/test_device_plan_gpu.py).  ``rng``: an int64 device
+        counter the launch also advances by one (the step's dropout counter)."""
         from .. import _native
 
         _native.ops().store_plan_expand(seed, self._dev_plan_tabs(), out, lay.Np, lay.Ep, lay.Gp, bool(lay.padded),
-                                        lay.attn_scope == "batch")
+                                        lay.attn_scope == "batch", rng)
         return out
 
     def plan_numpy(self, indices, lay, out=None):

@@ -58,8 +58,26 @@ def counter(device):
     return ent[0]
 
 
+_folded = set()
+
+
+def fold_next_advance(device):
+    """The next ``advance`` on ``device`` is already done by a launch that precedes it in the
+    same stream (the captured step's device-side plan expansion increments the counter)."""
+    _folded.add(_key(device))
+
+
+def clear_fold(device):
+    _folded.discard(_key(device))
+
+
 def advance(device):
-    """Advance the device counter (one tiny kernel; capturable)."""
+    """Advance the device counter (one tiny kernel; capturable) — or nothing, when a preceding
+    launch already did (``fold_next_advance``)."""
+    k = _key(device)
+    if k in _folded:
+        _folded.discard(k)
+        return
     _native.ops().rng_advance(counter(device))
 
 

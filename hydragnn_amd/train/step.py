@@ -548,10 +548,17 @@ class TrainStep:
             with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                 if cap.seeded:  # first nodes: H2D of the sample ids, device-side plan
                     cap.dev_seed.copy_(cap.pinned[j], non_blocking=True)
-                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan)
+                    # the plan launch also advances the dropout counter (the model's per-step
+                    # advance is folded into it: one launch less in the step)
+                    from ..ops import rng as _rngmod
+
+                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan, rng=_rngmod.counter(self.device))
+                    _rngmod.fold_next_advance(self.device)
                 else:  # first node: H2D of the plan
                     cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)
                 cap.losses[j], cap.taskss[j] = self._body_fwd_bwd(store, cap, sync=not split)
+                if cap.seeded:
+                    _rngmod.clear_fold(self.device)
                 if not split:
                     self.opt.step()
             cap.graphs[j] = g
