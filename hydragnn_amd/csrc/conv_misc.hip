@@ -312,9 +312,77 @@ std::tuple<at::Tensor, at::Tensor> edge_gather_act_bwd(const at::Tensor& g_, con
   return {dz, dr};
 }
 
+
+// MACE FullyConnectedNet hidden activation y = silu(s x) (the e3nn second-moment
+// normalisation and the next layer's 1/sqrt(fan_in) folded into one scale s, reference
+// e3nn nn.FullyConnectedNet used by mace_utils/modules/blocks.py:354-387): one launch each
+// way instead of a scale + silu (+ their two backward launches).
+__global__ void __launch_bounds__(256) scaled_silu_fwd_kernel(const float4* __restrict__ x, float4* __restrict__ y,
+                                                              int64_t n4, float s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = x[i];
+  float* a = reinterpret_cast<float*>(&v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float z = a[k] * s;
+    a[k] = z / (1.f + __expf(-z));
+  }
+  y[i] = v;
+}
+
+__global__ void __launch_bounds__(256) scaled_silu_bwd_kernel(const float4* __restrict__ g,
+                                                              const float4* __restrict__ x, float4* __restrict__ dx,
+                                                              int64_t n4, float s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = x[i];
+  const float4 gv = g[i];
+  float* a = reinterpret_cast<float*>(&v);
+  const float* b = reinterpret_cast<const float*>(&gv);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float z = a[k] * s;
+    const float sg = 1.f / (1.f + __expf(-z));
+    a[k] = b[k] * s * sg * (1.f + z * (1.f - sg));
+  }
+  dx[i] = v;
+}
+
+at::Tensor scaled_silu_fwd(const at::Tensor& x_, double s) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK(x.numel() % 4 == 0, "scaled_silu: numel must be a multiple of 4");
+  auto y = at::empty_like(x);
+  const int64_t n4 = x.numel() / 4;
+  if (n4 > 0)
+    scaled_silu_fwd_kernel<<<ceil_div(n4, 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(x.data_ptr<float>()), reinterpret_cast<float4*>(y.data_ptr<float>()), n4,
+        (float)s);
+  return y;
+}
+
+at::Tensor scaled_silu_bwd(const at::Tensor& g_, const at::Tensor& x_, double s) {
+  HY_CHECK_CUDA(g_);
+  auto g = g_.contiguous(), x = x_.contiguous();
+  HY_CHECK_F32(g);
+  HY_CHECK_F32(x);
+  HY_CHECK(g.numel() == x.numel() && x.numel() % 4 == 0, "scaled_silu_bwd: shapes");
+  auto dx = at::empty_like(x);
+  const int64_t n4 = x.numel() / 4;
+  if (n4 > 0)
+    scaled_silu_bwd_kernel<<<ceil_div(n4, 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(g.data_ptr<float>()), reinterpret_cast<const float4*>(x.data_ptr<float>()),
+        reinterpret_cast<float4*>(dx.data_ptr<float>()), n4, (float)s);
+  return dx;
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("scaled_silu_fwd(Tensor x, float s) -> Tensor");
+  m.def("scaled_silu_bwd(Tensor g, Tensor x, float s) -> Tensor");
   m.def(
       "edge_gather_act_fwd(Tensor ab, Tensor src, Tensor dst, Tensor r, Tensor w, Tensor b, Tensor? et, int act) -> "
       "Tensor");
@@ -328,6 +396,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("scaled_silu_fwd", hy::scaled_silu_fwd);
+  m.impl("scaled_silu_bwd", hy::scaled_silu_bwd);
   m.impl("edge_gather_act_fwd", hy::edge_gather_act_fwd);
   m.impl("edge_gather_act_bwd", hy::edge_gather_act_bwd);
   m.impl("cg_gate_fwd", hy::cg_gate_fwd);

@@ -431,6 +431,33 @@ class _TallMM(torch.autograd.Function):
         return dx, dW
 
 
+class _ScaledSilu(torch.autograd.Function):
+    """silu(s x) in one HIP launch each way (csrc/conv_misc.hip scaled_silu_*); first order."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        from .. import _native
+
+        ctx.save_for_backward(x)
+        ctx.s = s
+        return _native.ops().scaled_silu_fwd(x, s)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        (x,) = ctx.saved_tensors
+        return _native.ops().scaled_silu_bwd(g, x, ctx.s), None
+
+
+def scaled_silu(x, s):
+    from . import pna as _mode
+
+    if x.is_cuda and x.dtype == torch.float32 and x.numel() % 4 == 0 and _mode.fused("mlp"):
+        return _ScaledSilu.apply(x.contiguous(), float(s))
+    return torch.nn.functional.silu(x * s)
+
+
 def _mm_tall(x, W):
     from . import pna as _mode
     from .linear import MIN_ROWS
@@ -467,7 +494,7 @@ class FullyConnectedNet(nn.Module):
             x = _mm_tall(x, W)
             s = carry / math.sqrt(W.shape[0])
             if i < n - 1:
-                x = torch.nn.functional.silu(x * s)
+                x = scaled_silu(x, s)
                 carry = _SILU_C
             elif not self.defer_last_scale:
                 x = x * s  # (deferred: s == last_scale(), applied by the consumer)

@@ -542,6 +542,11 @@ class TrainStep:
                 self.opt.step()
         torch.cuda.current_stream().wait_stream(s)
         split = self.world > 1 and not self._graph_collectives()
+        from ..ops import rng as _rngmod
+
+        # the dropout counter must exist before capture (created lazily by the first dropout
+        # otherwise, and a model without dropout never made it: its H2D init cannot be captured)
+        rng_ctr = _rngmod.counter(self.device)
         for j in range(2):
             pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
@@ -550,9 +555,7 @@ class TrainStep:
                     cap.dev_seed.copy_(cap.pinned[j], non_blocking=True)
                     # the plan launch also advances the dropout counter (the model's per-step
                     # advance is folded into it: one launch less in the step)
-                    from ..ops import rng as _rngmod
-
-                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan, rng=_rngmod.counter(self.device))
+                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan, rng=rng_ctr)
                     _rngmod.fold_next_advance(self.device)
                 else:  # first node: H2D of the plan
                     cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)

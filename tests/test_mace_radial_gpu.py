@@ -32,3 +32,21 @@ def test_mace_radial_matches_composite(K, p, rc):
         comp = blk(rd.detach())
     assert not isinstance(comp.grad_fn, _MaceRadial)
     torch.testing.assert_close(comp, out.detach(), rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("shape,s", [((2048, 64), 0.125), ((37, 12), 1.7)])
+def test_scaled_silu_matches_torch(shape, s):
+    """FullyConnectedNet hidden activation silu(s x) (csrc/conv_misc.hip scaled_silu_*)."""
+    from hydragnn_amd.ops.o3 import _ScaledSilu, scaled_silu
+
+    g = torch.Generator().manual_seed(shape[0])
+    x = torch.randn(shape, generator=g, dtype=torch.float64) * 4
+    go = torch.randn(shape, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.silu(xr * s).backward(go)
+    xd = x.float().cuda().requires_grad_(True)
+    y = scaled_silu(xd, s)
+    assert isinstance(y.grad_fn, _ScaledSilu._backward_cls)
+    y.backward(go.float().cuda())
+    torch.testing.assert_close(y.double().cpu(), torch.nn.functional.silu(x * s), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xd.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-5)
