@@ -193,7 +193,7 @@ struct PnaAggArgs {
   int* arg;      // [N, 2F]: row of the min / max (-1 for an empty segment)
   const float* g;  // backward: dL/dout
   float* dx;       // backward: [E, F]
-  int N, F, S, codes, E;
+  int N, F, S, codes;
   float avg_log, avg_lin, eps, sqrt_eps;
 };
 
@@ -239,8 +239,6 @@ __global__ void __launch_bounds__(256) seg_pna_agg_bwd_kernel(PnaAggArgs a) {
   if (t >= (int64_t)a.N * a.F) return;
   const int F = a.F, n = (int)(t / F), f = (int)(t % F);
   const int beg = a.rowptr[n], end = a.rowptr[n + 1];
-  // rows past rowptr[N] belong to no segment (did not reach the output): zero gradient
-  for (int e = a.rowptr[a.N] + n; e < a.E; e += a.N) a.dx[(int64_t)(a.perm ? a.perm[e] : e) * F + f] = 0.f;
   if (end <= beg) return;
   const float d = (float)(end - beg);
   float G[4] = {0.f, 0.f, 0.f, 0.f};
@@ -548,7 +546,6 @@ static PnaAggArgs pna_agg_args(const at::Tensor& x, const at::Tensor& rowptr, co
   }
   a.N = (int)(rowptr.numel() - 1);
   a.F = (int)x.size(1);
-  a.E = (int)x.size(0);
   a.S = (int)S;
   a.codes = (int)codes;
   a.avg_log = (float)avg_log;
@@ -582,9 +579,9 @@ at::Tensor seg_pna_agg_bwd(const at::Tensor& g_, const at::Tensor& x, const at::
   HY_CHECK_F32(g);
   HY_CHECK(g.size(0) == a.N && g.size(1) == 4 * S * a.F, "seg_pna_agg_bwd: gradient shape");
   HY_CHECK(stat.size(0) == a.N && stat.size(1) == 2 * a.F && arg.size(1) == 2 * a.F, "seg_pna_agg_bwd: saved shapes");
-  // every dx row is written once: by its segment's threads, or zeroed by the tail loop when
-  // it lies past rowptr[N] (no zero-fill launch)
-  auto dx = at::empty_like(x);
+  // zero-filled: a padded batch's permutation need not list every padding row (rows no
+  // segment owns get zero gradient, as in the composite's gather / arg-scatter)
+  auto dx = at::zeros_like(x);
   a.g = g.data_ptr<float>();
   a.stat = const_cast<float*>(stat.data_ptr<float>());
   a.arg = const_cast<int*>(arg.data_ptr<int>());
