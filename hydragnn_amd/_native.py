@@ -25,12 +25,34 @@ def load():
     if not os.path.exists(LIB_PATH):
         _error = f"{LIB_PATH} not found (run `python -m hydragnn_amd.csrc.build`)"
         return False
+    stale = _stale_reason()
+    if stale:
+        _error = stale
+        return False
     try:
         torch.ops.load_library(LIB_PATH)
         _loaded = True
     except Exception as e:  # pragma: no cover - depends on the build
         _error = f"failed to load {LIB_PATH}: {e}"
     return _loaded
+
+
+def _stale_reason():
+    """The in-tree library must match the sources it was built from (``_C.so.srchash``,
+    written by ``csrc/build.py``); an alternative library (HYDRA_NATIVE_LIB) is not checked."""
+    if os.environ.get("HYDRA_NATIVE_LIB"):
+        return None
+    from .csrc import build as _b
+
+    side = LIB_PATH + ".srchash"
+    if not os.path.exists(side):
+        return f"{LIB_PATH} has no source digest ({side}): rebuild with `python -m hydragnn_amd.csrc.build`"
+    with open(side) as fh:
+        built = fh.read().strip()
+    if built != _b.source_digest():
+        return (f"{LIB_PATH} is stale: the native sources changed since it was built "
+                "(run `python -m hydragnn_amd.csrc.build`)")
+    return None
 
 
 def available():

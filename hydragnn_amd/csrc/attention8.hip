@@ -26,6 +26,8 @@
 //          summed over 16 rows.
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace hy {
@@ -631,6 +633,16 @@ __device__ __forceinline__ float4 bl4(Rsrc r, int vo, int so) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
 }
 __device__ __forceinline__ float max4(f4v s) { return fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3])); }
+// max of 4 accumulator values as a v_max3_f32 chain: fmaxf on an MFMA result makes the
+// compiler canonicalise every operand first (one v_max x, x each); the scores here are never
+// signalling NaNs, so the raw instruction is exact
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max4r(f4v s) { return vmax3(vmax3(s[0], s[1], s[2]), s[3], s[3]); }
+
 
 // bf16 mode (precision "bf16"): every product on v_mfma_f32_16x16x16_bf16 (fp32 accumulate).
 // Lane (i, g) supplies A[i][4g .. 4g+3] / B[4g .. 4g+3][i].  D = 8 contractions (S = Q K^T,
@@ -804,6 +816,143 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
         const float f = fexp2(red[v][t][qi][0] - M);
         lsum = fmaf(red[v][t][qi][1], f, lsum);
         a = fmaf(red[v][t][qi][2 + d], f, a);
+      }
+    }
+    if (qq < N) {
+      O[(int64_t)qq * 8 * H + h * 8 + d] = lsum > 0.f ? a * (1.f / lsum) : 0.f;
+      if (d == 0) NL[(int64_t)h * Nq + qq] = lsum > 0.f ? -(M + __log2f(lsum)) : INFINITY;
+    } else if (qq < Nq && d == 0) {
+      NL[(int64_t)h * Nq + qq] = 0.f;
+    }
+  }
+}
+
+// v2 forward on quad-block MFMAs (fp32).  Measured on MI355X (tools/mfma_rate.hip): an f32
+// MFMA and f32 VALU work of the same SIMD do NOT overlap (4 x 16x16x4 + 16 v_fma take the SUM
+// of their times), and v_mfma_f32_4x4x1_16b_f32 retires 512 FLOP in ~10 cycles against the
+// 16x16x4's 2,048 in 32.  The P.V product of an 8-wide head wastes half of every 16x16x4
+// (only 8 of its 16 output rows are real), so here it runs as 4x4x1_16b blocks instead:
+// block b = 4g + i/4 of lane (i, g) owns queries 4(i/4)..+3 x dims 4dh..+3 and sums over its
+// lane group's keys 4g + r (r = the instruction), so the A operand is the lane's OWN
+// probability p[r] (no shuffles) and the B operand comes straight from the quad layout
+// (keys 4g..4g+3 of dim 4dh + i%4: one float4 per d half).  2 x 4 independent 10-cycle MFMAs
+// replace 4 dependent 32-cycle ones; the 4 lane groups' partial O are summed once per slice.
+// VALU per tile is kept minimal (it adds to the MFMA time): the -m seed is rebuilt from one
+// register, the score maximum runs on raw v_max3_f32.
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __restrict__ Qp,
+                                                             const float* __restrict__ Kp,
+                                                             const float* __restrict__ Vq, int N, int Nq, int H,
+                                                             const int* __restrict__ seg_id,
+                                                             const int* __restrict__ seg_ptr, float qscale,
+                                                             float* __restrict__ O, float* __restrict__ NL) {
+  __shared__ float red[W][16][10];
+  const int h = blockIdx.y;
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int qbase = blockIdx.x * 16;
+  const SpanR<1> sp = span_rt<1>(qbase, i, N, seg_id, seg_ptr, W, w);
+  const Rsrc rk = mk_rsrc(Kp + (int64_t)h * Nq * 8, Nq * 8), rv = mk_rsrc(Vq + (int64_t)h * Nq * 8, Nq * 8);
+  // K pair fragment of row k0 + i; V quad float4s of keys k0 + 4g..+3, dims i%4 and 4 + i%4
+  const int ok_ = off_pair(i, g), ov0 = (32 * g + 4 * (i & 3)) * 4, ov1 = ov0 + 64;
+  const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(sp.row[0], Nq - 1)) * 8 + 2 * g);
+  const float bq0 = bq.x * qscale, bq1 = bq.y * qscale;
+  float m = -INFINITY, thr = -INFINITY, l = 0.f, negm = 0.f;
+  f4v o0 = f4z(), o1 = f4z();  // 4x4 blocks: rows = queries 4(i/4)+r, cols = dims (4dh + c)
+  auto tile = [&](float2 kk, float4 va, float4 vb, int k0) {
+    const f4v cin = f4v{negm, negm, negm, negm};
+    f4v s = mfma(kk.x, bq0, cin);
+    s = mfma(kk.y, bq1, s);
+    const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
+    if (!full) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 4 * g + r;
+        if (!(key >= sp.b[0] && key < sp.e[0] && key < sp.ce)) s[r] = -INFINITY;
+      }
+    }
+    const float mx = max4r(s);
+    if (__any(mx > thr)) {  // move the row reference (rare), rescale o and l
+      const float mn = fmaxf(m, wmax16(mx) - negm);
+      if (mn > -INFINITY) {
+        const float f = fexp2(m - mn), sh = mn + negm;
+        o0 = o0 * f;
+        o1 = o1 * f;
+        l *= f;
+        s = s - f4v{sh, sh, sh, sh};
+        m = mn;
+        thr = kTau;
+        negm = -mn;
+      }
+    }
+    const float p0 = fexp2(s[0]), p1 = fexp2(s[1]), p2 = fexp2(s[2]), p3 = fexp2(s[3]);
+    o0 = mfma4(p0, va.x, o0);
+    o1 = mfma4(p0, vb.x, o1);
+    o0 = mfma4(p1, va.y, o0);
+    o1 = mfma4(p1, vb.y, o1);
+    o0 = mfma4(p2, va.z, o0);
+    o1 = mfma4(p2, vb.z, o1);
+    o0 = mfma4(p3, va.w, o0);
+    o1 = mfma4(p3, vb.w, o1);
+    l += (p0 + p1) + (p2 + p3);
+  };
+  const int cmax = (Nq - 16) * 32;
+  float2 ka = bl2(rk, ok_, min(sp.cb * 32, cmax));
+  float4 va0 = bl4(rv, ov0, min(sp.cb * 32, cmax)), va1 = bl4(rv, ov1, min(sp.cb * 32, cmax));
+  __builtin_amdgcn_sched_barrier(0);
+  float2 kb = bl2(rk, ok_, min(sp.cb * 32 + 512, cmax));
+  float4 vb0 = bl4(rv, ov0, min(sp.cb * 32 + 512, cmax)), vb1 = bl4(rv, ov1, min(sp.cb * 32 + 512, cmax));
+  __builtin_amdgcn_sched_barrier(0);
+  for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
+    tile(ka, va0, va1, k0);
+    ka = bl2(rk, ok_, min(k0 * 32 + 1024, cmax));
+    va0 = bl4(rv, ov0, min(k0 * 32 + 1024, cmax));
+    va1 = bl4(rv, ov1, min(k0 * 32 + 1024, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+    tile(kb, vb0, vb1, k0 + 16);
+    kb = bl2(rk, ok_, min(k0 * 32 + 1536, cmax));
+    vb0 = bl4(rv, ov0, min(k0 * 32 + 1536, cmax));
+    vb1 = bl4(rv, ov1, min(k0 * 32 + 1536, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // sum the 4 lane groups' partial blocks and row sums; lanes of group 0 hold the slice's O
+  float lt = l + __shfl_xor(l, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    o0[r] += __shfl_xor(o0[r], 16, 64);
+    o0[r] += __shfl_xor(o0[r], 32, 64);
+    o1[r] += __shfl_xor(o1[r], 16, 64);
+    o1[r] += __shfl_xor(o1[r], 32, 64);
+  }
+  if (g == 0) {
+    // lane i: block i/4, column c = i%4, rows r: query 4(i/4) + r, dims c and 4 + c
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[w][4 * (i >> 2) + r][2 + (i & 3)] = o0[r];
+      red[w][4 * (i >> 2) + r][6 + (i & 3)] = o1[r];
+    }
+  } else if (g == 1) {
+    red[w][i][0] = m;
+    red[w][i][1] = lt;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 128; idx += 64 * W) {
+    const int qi = idx >> 3, d = idx & 7;
+    const int qq = qbase + qi;
+    float M = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < W; ++v) M = fmaxf(M, red[v][qi][0]);
+    float lsum = 0.f, a = 0.f;
+    if (M > -INFINITY) {
+#pragma unroll
+      for (int v = 0; v < W; ++v) {
+        const float f = fexp2(red[v][qi][0] - M);
+        lsum = fmaf(red[v][qi][1], f, lsum);
+        a = fmaf(red[v][qi][2 + d], f, a);
       }
     }
     if (qq < N) {
@@ -1103,6 +1252,778 @@ __global__ void __launch_bounds__(64 * W) attn8_bwd2_kernel(A8Bwd2 a) {
     attn8_bwd2_dkv<RT, W, BF>(a, blockIdx.x - a.nbq, red);
 }
 
+// ----------------------------------------------------- v3: persistent, cost-balanced (batch scope)
+// The v2 grids are (row tiles x heads) workgroups of W waves: at the OC20 shape that is
+// 1,160-1,264 workgroups for 1,024 resident slots, so the chip runs a full round and then a
+// second round on a fraction of its CUs (profiled: 4-5 of 8 waves per SIMD resident on
+// average over the launch).  v3 launches ONE 16-wave workgroup per CU and deals the work
+// out by cost:
+//   * a UNIT is one (head, 16-row tile) of the outer index (queries for the forward and the
+//     dQ pass, keys for the dK/dV pass); its cost is the number of 16-wide tiles of the other
+//     index in its segment span.  Units are ordered head-major, tile-minor, and their costs
+//     have a closed form for the batch-scope layouts (one segment [0, N), or the valid
+//     segment [0, nv) + the padding segment [nv, N), nv read on the device);
+//   * workgroup b owns the whole units whose flattened start is nearest to b * T / G
+//     (T = total cost): no unit is split across workgroups (no inter-workgroup hand-off), and
+//     the makespan is within half a unit of T / G;
+//   * the workgroup takes its units in GROUPS of up to R consecutive units of one head and
+//     one span type (R = 5 forward, 3 dQ and dK/dV: register budget of 4 waves per SIMD).  Every wave of the workgroup owns a
+//     1/16 slice of the group's span and runs it for ALL units of the group: each K/V (or
+//     Q/dO) fragment it loads feeds R independent MFMA chains (R x less operand traffic than
+//     one tile per wave, and R chains of instruction-level parallelism).  The 16 per-wave
+//     partial results of a unit meet in LDS and are merged in wave order (deterministic).
+// (A first v3 split each workgroup's tile range contiguously over its waves, one unit per
+// wave at a time: 4 waves per SIMD streaming private key ranges spent 42 % of their cycles
+// waiting on loads and ran the forward in 35 us against v2's 31 us.)
+// The backward flattens [dQ units | dK/dV units] with tile weights 2 : 3 (8 vs 12 MFMAs).
+// Tile bodies as v2 (fp32 16x16x4 MFMA, deferred-rescale softmax, accumulator-seeded LSE).
+constexpr int kNW3 = 16;   // waves per v3 workgroup
+// group-size caps (register budget of 4 waves per SIMD): RF forward, RQ dQ, RK dK/dV
+
+// closed-form unit costs of a batch-scope layout (segments [0, nv) and [nv, N))
+struct BPlan {
+  int N, nv, nqt, nvt, bnd, cv, ca, cp, plo, Tq;
+  __device__ __forceinline__ void init(int N_, int nv_) {
+    N = N_;
+    nv = min(max(nv_, 0), N_);
+    nqt = (N + 15) >> 4;
+    bnd = (nv < N && (nv & 15)) ? 1 : 0;        // one tile holds rows of both segments
+    nvt = nv == N ? nqt : (nv >> 4);            // tiles whose rows are all valid
+    cv = (nv + 15) >> 4;                        // span [0, nv)
+    ca = nqt;                                   // span [0, N)
+    plo = nv >> 4;                              // padding span starts at tile nv / 16
+    cp = nqt - plo;                             // span [16 plo, N)
+    Tq = pre(nqt);
+  }
+  // arithmetic selects: a select of two fields lets the compiler select their ADDRESSES,
+  // which pins the whole plan in (LDS-promoted) private memory
+  __device__ __forceinline__ int cost(int t) const {
+    const int v = t < nvt ? 1 : 0, a = (bnd && t == nvt) ? 1 : 0;
+    return cp + v * (cv - cp) + a * (ca - cp);
+  }
+  // 0 valid, 1 boundary, 2 padding (units of one type share span and masks)
+  __device__ __forceinline__ int type(int t) const { return t < nvt ? 0 : ((bnd && t == nvt) ? 1 : 2); }
+  __device__ __forceinline__ int lo(int t) const { return (t < nvt + bnd ? 0 : 16) * plo; }
+  __device__ __forceinline__ int pre(int t) const {
+    if (t <= nvt) return t * cv;
+    int p = nvt * cv, r = t - nvt;
+    if (bnd) {
+      p += ca;
+      r -= 1;
+    }
+    return p + r * cp;
+  }
+  // y in [0, Tq) -> (tile t, tile k of its span)
+  __device__ __forceinline__ void decode(int y, int& t, int& k) const {
+    const int a = nvt * cv;
+    if (y < a) {
+      t = y / cv;
+      k = y - t * cv;
+      return;
+    }
+    y -= a;
+    if (bnd) {
+      if (y < ca) {
+        t = nvt;
+        k = y;
+        return;
+      }
+      y -= ca;
+    }
+    t = nvt + bnd + y / cp;
+    k = y - (t - nvt - bnd) * cp;
+  }
+  // segment span of row r (empty for r >= N) and the intersection [ilo, ihi) over the
+  // valid rows of tile t (empty when the tile holds rows of both segments)
+  __device__ __forceinline__ void row_span(int r, int& b, int& e) const {
+    b = r < nv ? 0 : (r < N ? nv : N);
+    e = r < nv ? nv : (r < N ? N : 0);
+  }
+  __device__ __forceinline__ void tile_isect(int t, int& ilo, int& ihi) const {
+    const int ty = type(t);
+    ilo = ty == 0 ? 0 : nv;
+    ihi = ty == 0 ? nv : (ty == 1 ? nv : N);
+  }
+};
+
+// the unit boundary nearest to tile j of the flattened tile space of one or two unit kinds
+// (tiles [0, D) of kind 0, [D, 2D) of kind 1; D = H * Tq): returns a unit index
+__device__ __forceinline__ int nearest_unit(BPlan P, int D, int H, int j, int ntiles) {
+  if (j >= ntiles) return (ntiles / D) * H * P.nqt;
+  const int kind = j < D ? 0 : 1, jj = j - kind * D;
+  const int h = jj / P.Tq;
+  int t, k;
+  P.decode(jj - h * P.Tq, t, k);
+  return kind * H * P.nqt + h * P.nqt + t + (2 * k > P.cost(t) ? 1 : 0);
+}
+
+__device__ __forceinline__ float4 f4scale(f4v v, float s) { return make_float4(v[0] * s, v[1] * s, v[2] * s, v[3] * s); }
+
+// one wave, R query tiles [t0, t0 + R) of head h against key tiles [kb0, kb1) of their span:
+// per-unit partial (m, l, o[8]) into LDS pr[R][16][10]
+template <int R>
+__device__ __forceinline__ void fwd3_group(const float* __restrict__ Qp, Rsrc rk, Rsrc rv, int64_t hb, int Nq,
+                                           const BPlan& P, int t0, int klo, int kb0, int kb1, float qscale,
+                                           int i, int g, float* __restrict__ pr) {
+  const int ok_ = off_pair(i, g), ov_ = off_quad(i, g);
+  const int cmax = (Nq - 16) * 32;
+  int ilo, ihi;
+  P.tile_isect(t0, ilo, ihi);
+  const int cb = klo + 16 * kb0, ce = klo + 16 * kb1;
+  float bq0[R], bq1[R], m[R], thr[R], l[R];
+  f4v o[R], cin[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int row = 16 * (t0 + j) + i;
+    const float2 bq = ld2(Qp + hb + (int64_t)min(row, Nq - 1) * 8 + 2 * g);
+    bq0[j] = bq.x * qscale;
+    bq1[j] = bq.y * qscale;
+    m[j] = -INFINITY;
+    thr[j] = -INFINITY;
+    l[j] = 0.f;
+    o[j] = f4z();
+    cin[j] = f4z();
+  }
+  auto tile = [&](float2 kk, float4 vv, int k0) {
+    const bool full = k0 >= ilo && k0 + 16 <= ihi && k0 + 16 <= ce;
+    f4v s[R];
+    auto scores = [&]() {
+#pragma unroll
+      for (int j = 0; j < R; ++j) s[j] = mfma(kk.x, bq0[j], cin[j]);
+#pragma unroll
+      for (int j = 0; j < R; ++j) s[j] = mfma(kk.y, bq1[j], s[j]);
+      if (!full) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          int rb, re;
+          P.row_span(16 * (t0 + j) + i, rb, re);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 4 * g + r;
+            if (!(key >= rb && key < re && key < ce)) s[j][r] = -INFINITY;
+          }
+        }
+      }
+    };
+    scores();
+    bool trig = false;
+#pragma unroll
+    for (int j = 0; j < R; ++j) trig |= max4(s[j]) > thr[j];
+    if (__any(trig)) {
+      // move the row references (rare: a score beyond the reference by > kTau), rescale
+      // o and l, and re-issue the score MFMAs against the new reference (keeps s in place)
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const float base = -cin[j][0];
+        const float mn = fmaxf(m[j], wmax16(max4(s[j])) + base);
+        if (mn > -INFINITY) {
+          const float f = fexp2(m[j] - mn);
+          o[j] = o[j] * f;
+          l[j] *= f;
+          m[j] = mn;
+          thr[j] = kTau;
+          cin[j] = f4v{-mn, -mn, -mn, -mn};
+        }
+      }
+      scores();
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const float p0 = fexp2(s[j][0]), p1 = fexp2(s[j][1]), p2 = fexp2(s[j][2]), p3 = fexp2(s[j][3]);
+      o[j] = mfma(vv.x, p0, o[j]);
+      o[j] = mfma(vv.y, p1, o[j]);
+      o[j] = mfma(vv.z, p2, o[j]);
+      o[j] = mfma(vv.w, p3, o[j]);
+      l[j] += (p0 + p1) + (p2 + p3);
+    }
+  };
+  if (cb < ce) {
+    float2 ka = bl2(rk, ok_, min(cb * 32, cmax));
+    float4 va = bl4(rv, ov_, min(cb * 32, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+    float2 kb = bl2(rk, ok_, min(cb * 32 + 512, cmax));
+    float4 vb = bl4(rv, ov_, min(cb * 32 + 512, cmax));
+    __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = cb; k0 < ce; k0 += 32) {
+      tile(ka, va, k0);
+      ka = bl2(rk, ok_, min(k0 * 32 + 1024, cmax));
+      va = bl4(rv, ov_, min(k0 * 32 + 1024, cmax));
+      __builtin_amdgcn_sched_barrier(0);
+      if (k0 + 16 < ce) tile(kb, vb, k0 + 16);
+      kb = bl2(rk, ok_, min(k0 * 32 + 1536, cmax));
+      vb = bl4(rv, ov_, min(k0 * 32 + 1536, cmax));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float lt = l[j] + __shfl_xor(l[j], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    float* q = pr + (j * 16 + i) * 10;
+    if (g < 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[2 + 4 * g + r] = o[j][r];
+    } else if (g == 2) {
+      q[0] = m[j];
+      q[1] = lt;
+    }
+  }
+}
+
+// forward: O [N, 8H], NL [H][Nq] (-LSE2; rows N..Nq: 0)
+template <int kRF>
+__global__ void __launch_bounds__(64 * kNW3) attn8_fwd3_kernel(const float* __restrict__ Qp,
+                                                               const float* __restrict__ Kp,
+                                                               const float* __restrict__ Vq, int N, int Nq, int H,
+                                                               const int* __restrict__ seg_ptr, int nseg,
+                                                               float qscale, float* __restrict__ O,
+                                                               float* __restrict__ NL) {
+  __shared__ float red[kNW3][kRF][16][10];
+  // the wave index is uniform: readfirstlane keeps the group loop scalar (no exec branches)
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  BPlan P;
+  P.init(N, nseg >= 2 ? seg_ptr[1] : N);
+  const int nqt = P.nqt, ntiles = H * P.Tq, G = gridDim.x, b = blockIdx.x;
+  const int uA = uni(b == 0 ? 0 : nearest_unit(P, ntiles, H, (int)((int64_t)b * ntiles / G), ntiles));
+  const int uB = uni(b + 1 >= G ? H * nqt : nearest_unit(P, ntiles, H, (int)((int64_t)(b + 1) * ntiles / G), ntiles));
+  for (int u = uA; u < uB;) {
+    const int h = uni(u / nqt), t0 = uni(u - h * nqt), ty = P.type(t0);
+    int R = 1;
+    while (R < kRF && u + R < uB && t0 + R < nqt && P.type(t0 + R) == ty) ++R;
+    R = uni(R);
+    const int cost = P.cost(t0), klo = P.lo(t0);
+    const int kb0 = uni(w * cost / kNW3), kb1 = uni((w + 1) * cost / kNW3);
+    const int64_t hb = (int64_t)h * Nq * 8;
+    const Rsrc rk = mk_rsrc(Kp + hb, Nq * 8), rv = mk_rsrc(Vq + hb, Nq * 8);
+    float* pr = &red[w][0][0][0];
+    switch (R) {
+      case 1: if constexpr (kRF >= 1) fwd3_group<1>(Qp, rk, rv, hb, Nq, P, t0, klo, kb0, kb1, qscale, i, g, pr); break;
+      case 2: if constexpr (kRF >= 2) fwd3_group<2>(Qp, rk, rv, hb, Nq, P, t0, klo, kb0, kb1, qscale, i, g, pr); break;
+      case 3: if constexpr (kRF >= 3) fwd3_group<3>(Qp, rk, rv, hb, Nq, P, t0, klo, kb0, kb1, qscale, i, g, pr); break;
+      case 4: if constexpr (kRF >= 4) fwd3_group<4>(Qp, rk, rv, hb, Nq, P, t0, klo, kb0, kb1, qscale, i, g, pr); break;
+      case 5: if constexpr (kRF >= 5) fwd3_group<5>(Qp, rk, rv, hb, Nq, P, t0, klo, kb0, kb1, qscale, i, g, pr); break;
+      default: break;
+    }
+    __syncthreads();
+    // merge the 16 wave partials of each unit in wave order: thread -> (unit, query, d)
+    for (int idx = threadIdx.x; idx < R * 128; idx += 64 * kNW3) {
+      const int j = idx >> 7, qi = (idx >> 3) & 15, d = idx & 7;
+      float M = -INFINITY;
+#pragma unroll 4
+      for (int v = 0; v < kNW3; ++v) M = fmaxf(M, red[v][j][qi][0]);
+      float lsum = 0.f, a = 0.f;
+      if (M > -INFINITY) {
+#pragma unroll 4
+        for (int v = 0; v < kNW3; ++v) {
+          const float f = fexp2(red[v][j][qi][0] - M);
+          lsum = fmaf(red[v][j][qi][1], f, lsum);
+          a = fmaf(red[v][j][qi][2 + d], f, a);
+        }
+      }
+      const int q = 16 * (t0 + j) + qi;
+      if (q < N) {
+        O[(int64_t)q * 8 * H + h * 8 + d] = lsum > 0.f ? a * (1.f / lsum) : 0.f;
+        if (d == 0) NL[(int64_t)h * Nq + q] = lsum > 0.f ? -(M + __log2f(lsum)) : INFINITY;
+      } else if (q < Nq && d == 0) {
+        NL[(int64_t)h * Nq + q] = 0.f;
+      }
+    }
+    __syncthreads();
+    u += R;
+  }
+}
+
+// one wave, R query tiles of head h (dQ) against key tiles [kb0, kb1) of their span
+template <int R>
+__device__ __forceinline__ void dq3_group(const A8Bwd2& a, int64_t hb, int h, const BPlan& P, int t0, int klo,
+                                          int kb0, int kb1, int i, int g, float* __restrict__ pr) {
+  const int Nq = a.Nq, N = a.N;
+  const int op = off_pair(i, g), oq = off_quad(i, g);
+  const int cmax = (Nq - 16) * 32;
+  int ilo, ihi;
+  P.tile_isect(t0, ilo, ihi);
+  const int cb = klo + 16 * kb0, ce = klo + 16 * kb1;
+  const Rsrc rk = mk_rsrc(a.Kp + hb, Nq * 8), rv = mk_rsrc(a.Vp + hb, Nq * 8), rkt = mk_rsrc(a.Kq + hb, Nq * 8);
+  float bq0[R], bq1[R], bo0[R], bo1[R];
+  f4v cs[R], cd[R], dq[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int row = 16 * (t0 + j) + i, rc = min(row, Nq - 1);
+    const float2 bq = ld2(a.Qp + hb + (int64_t)rc * 8 + 2 * g);
+    const float2 bo = ld2(a.dOp + hb + (int64_t)rc * 8 + 2 * g);
+    bq0[j] = bq.x * a.qscale;
+    bq1[j] = bq.y * a.qscale;
+    bo0[j] = bo.x;
+    bo1[j] = bo.y;
+    const float nl = row < N ? a.NL[(int64_t)h * Nq + row] : 0.f;
+    const float nd = row < N ? a.ndelta[(int64_t)h * Nq + row] : 0.f;
+    cs[j] = f4v{nl, nl, nl, nl};
+    cd[j] = f4v{nd, nd, nd, nd};
+    dq[j] = f4z();
+  }
+  auto tile = [&](float2 kk, float2 vv, float4 kt, int k0) {
+    const bool full = k0 >= ilo && k0 + 16 <= ihi && k0 + 16 <= ce;
+    f4v s[R], dp[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      s[j] = mfma(kk.x, bq0[j], cs[j]);
+      dp[j] = mfma(vv.x, bo0[j], cd[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      s[j] = mfma(kk.y, bq1[j], s[j]);
+      dp[j] = mfma(vv.y, bo1[j], dp[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[r] = fexp2(s[j][r]) * dp[j][r];
+      if (!full) {
+        int rb, re;
+        P.row_span(16 * (t0 + j) + i, rb, re);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 4 * g + r;
+          if (!(key >= rb && key < re && key < ce)) ds[r] = 0.f;
+        }
+      }
+      dq[j] = mfma(kt.x, ds[0], dq[j]);
+      dq[j] = mfma(kt.y, ds[1], dq[j]);
+      dq[j] = mfma(kt.z, ds[2], dq[j]);
+      dq[j] = mfma(kt.w, ds[3], dq[j]);
+    }
+  };
+  if (cb < ce) {
+    int o0 = min(cb * 32, cmax), o1 = min(cb * 32 + 512, cmax);
+    float2 ka = bl2(rk, op, o0), va = bl2(rv, op, o0);
+    float4 ta = bl4(rkt, oq, o0);
+    __builtin_amdgcn_sched_barrier(0);
+    float2 kb = bl2(rk, op, o1), vb = bl2(rv, op, o1);
+    float4 tb = bl4(rkt, oq, o1);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = cb; k0 < ce; k0 += 32) {
+      tile(ka, va, ta, k0);
+      o0 = min(k0 * 32 + 1024, cmax);
+      ka = bl2(rk, op, o0);
+      va = bl2(rv, op, o0);
+      ta = bl4(rkt, oq, o0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k0 + 16 < ce) tile(kb, vb, tb, k0 + 16);
+      o1 = min(k0 * 32 + 1536, cmax);
+      kb = bl2(rk, op, o1);
+      vb = bl2(rv, op, o1);
+      tb = bl4(rkt, oq, o1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (g < 2) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[(j * 16 + i) * 16 + 4 * g + r] = dq[j][r];
+  }
+}
+
+// one wave, R key tiles of head h (dK, dV) against query tiles [kb0, kb1) of their span
+template <int R>
+__device__ __forceinline__ void dkv3_group(const A8Bwd2& a, int64_t hb, int h, const BPlan& P, int t0, int klo,
+                                           int kb0, int kb1, int i, int g, float* __restrict__ pr) {
+  const int Nq = a.Nq;
+  const int op = off_pair(i, g), oq = off_quad(i, g), os = 16 * g;
+  const int cmax = (Nq - 16) * 32;
+  int ilo, ihi;
+  P.tile_isect(t0, ilo, ihi);
+  const int cb = klo + 16 * kb0, ce = klo + 16 * kb1;
+  const Rsrc rq = mk_rsrc(a.Qp + hb, Nq * 8), ro = mk_rsrc(a.dOp + hb, Nq * 8);
+  const Rsrc rqt = mk_rsrc(a.Qq + hb, Nq * 8), rot = mk_rsrc(a.dOq + hb, Nq * 8);
+  const Rsrc rl = mk_rsrc(a.NL + (int64_t)h * Nq, Nq), rd = mk_rsrc(a.ndelta + (int64_t)h * Nq, Nq);
+  float bk0[R], bk1[R], bv0[R], bv1[R];
+  f4v dk[R], dv[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int row = 16 * (t0 + j) + i, rc = min(row, Nq - 1);
+    const float2 bk = ld2(a.Kp + hb + (int64_t)rc * 8 + 2 * g);
+    const float2 bv = ld2(a.Vp + hb + (int64_t)rc * 8 + 2 * g);
+    bk0[j] = bk.x * a.qscale;
+    bk1[j] = bk.y * a.qscale;
+    bv0[j] = bv.x;
+    bv1[j] = bv.y;
+    dk[j] = f4z();
+    dv[j] = f4z();
+  }
+  struct T6 {
+    float2 q, o;
+    float4 qt, ot, nl, nd;
+  };
+  auto load = [&](int q0) {
+    const int ob = min(q0 * 32, cmax), os_ = min(q0 * 4, (Nq - 16) * 4);
+    T6 x;
+    x.q = bl2(rq, op, ob);
+    x.o = bl2(ro, op, ob);
+    x.qt = bl4(rqt, oq, ob);
+    x.ot = bl4(rot, oq, ob);
+    x.nl = bl4(rl, os, os_);
+    x.nd = bl4(rd, os, os_);
+    return x;
+  };
+  auto tile = [&](const T6& x, int q0) {
+    const bool full = q0 >= ilo && q0 + 16 <= ihi && q0 + 16 <= ce;
+    const f4v nl = f4v{x.nl.x, x.nl.y, x.nl.z, x.nl.w}, nd = f4v{x.nd.x, x.nd.y, x.nd.z, x.nd.w};
+    f4v s[R], dp[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      s[j] = mfma(x.q.x, bk0[j], nl);
+      dp[j] = mfma(x.o.x, bv0[j], nd);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      s[j] = mfma(x.q.y, bk1[j], s[j]);
+      dp[j] = mfma(x.o.y, bv1[j], dp[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = fexp2(s[j][r]);
+      if (!full) {
+        int rb, re;
+        P.row_span(16 * (t0 + j) + i, rb, re);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = q0 + 4 * g + r;
+          if (!(qq >= rb && qq < re && qq < ce)) p[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds[r] = p[r] * dp[j][r];
+      dv[j] = mfma(x.ot.x, p[0], dv[j]);
+      dk[j] = mfma(x.qt.x, ds[0], dk[j]);
+      dv[j] = mfma(x.ot.y, p[1], dv[j]);
+      dk[j] = mfma(x.qt.y, ds[1], dk[j]);
+      dv[j] = mfma(x.ot.z, p[2], dv[j]);
+      dk[j] = mfma(x.qt.z, ds[2], dk[j]);
+      dv[j] = mfma(x.ot.w, p[3], dv[j]);
+      dk[j] = mfma(x.qt.w, ds[3], dk[j]);
+    }
+  };
+  if (cb < ce) {
+    T6 xa = load(cb);
+    __builtin_amdgcn_sched_barrier(0);
+    T6 xb = load(cb + 16);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int q0 = cb; q0 < ce; q0 += 32) {
+      tile(xa, q0);
+      xa = load(q0 + 32);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q0 + 16 < ce) tile(xb, q0 + 16);
+      xb = load(q0 + 48);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (g < 2) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[(j * 16 + i) * 16 + 4 * g + r] = dk[j][r];
+        pr[(j * 16 + i) * 16 + 8 + 4 * g + r] = dv[j][r];
+      }
+  }
+}
+
+// backward: dqkv [N, 24H] = [dQ | dK | dV] (dQ, dK scaled by `scale`).  Units: dQ units
+// [0, H nqt), dK/dV units [H nqt, 2 H nqt); flattened tile weights 2 and 3.
+template <int kRQ, int kRK>
+__global__ void __launch_bounds__(64 * kNW3) attn8_bwd3_kernel(A8Bwd2 a, int nseg) {
+  __shared__ float red[kNW3][kRK > kRQ ? kRK : kRQ][16][16];
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int N = a.N, Nq = a.Nq, H = a.H, F = 8 * H;
+  BPlan P;
+  P.init(N, nseg >= 2 ? a.seg_ptr[1] : N);
+  const int nqt = P.nqt, D = H * P.Tq, G = gridDim.x, b = blockIdx.x, U = H * nqt;
+  const int64_t wtot = 5LL * D;
+  auto tile_at = [D](int64_t z) -> int {
+    return z <= 2LL * D ? (int)((z + 1) / 2) : D + (int)((z - 2LL * D + 2) / 3);
+  };
+  const int uA = uni(b == 0 ? 0 : nearest_unit(P, D, H, tile_at((int64_t)b * wtot / G), 2 * D));
+  const int uB = uni(b + 1 >= G ? 2 * U : nearest_unit(P, D, H, tile_at((int64_t)(b + 1) * wtot / G), 2 * D));
+  for (int u = uA; u < uB;) {
+    const int kind = u < U ? 0 : 1, uu = u - kind * U;
+    const int h = uni(uu / nqt), t0 = uni(uu - h * nqt), ty = P.type(t0);
+    const int rmax = kind == 0 ? kRQ : kRK;
+    int R = 1;
+    while (R < rmax && u + R < uB && t0 + R < nqt && (u + R < U) == (kind == 0) && P.type(t0 + R) == ty) ++R;
+    R = uni(R);
+    const int cost = P.cost(t0), klo = P.lo(t0);
+    const int kb0 = uni(w * cost / kNW3), kb1 = uni((w + 1) * cost / kNW3);
+    const int64_t hb = (int64_t)h * Nq * 8;
+    float* pr = &red[w][0][0][0];
+    if (kind == 0) {
+      switch (R) {
+        case 1: if constexpr (kRQ >= 1) dq3_group<1>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 2: if constexpr (kRQ >= 2) dq3_group<2>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 3: if constexpr (kRQ >= 3) dq3_group<3>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 4: if constexpr (kRQ >= 4) dq3_group<4>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 5: if constexpr (kRQ >= 5) dq3_group<5>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        default: break;
+      }
+    } else {
+      switch (R) {
+        case 1: if constexpr (kRK >= 1) dkv3_group<1>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 2: if constexpr (kRK >= 2) dkv3_group<2>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 3: if constexpr (kRK >= 3) dkv3_group<3>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 4: if constexpr (kRK >= 4) dkv3_group<4>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        case 5: if constexpr (kRK >= 5) dkv3_group<5>(a, hb, h, P, t0, klo, kb0, kb1, i, g, pr); break;
+        default: break;
+      }
+    }
+    __syncthreads();
+    // sum the 16 wave partials in wave order: thread -> (unit, row, column)
+    const int ncol = kind == 0 ? 8 : 16;
+    for (int idx = threadIdx.x; idx < R * 16 * ncol; idx += 64 * kNW3) {
+      const int j = idx / (16 * ncol), rr = idx - j * 16 * ncol, ri = rr / ncol, c = rr - ri * ncol;
+      float v = 0.f;
+#pragma unroll 4
+      for (int x = 0; x < kNW3; ++x) v += red[x][j][ri][c];
+      const int row = 16 * (t0 + j) + ri;
+      if (row < N) {
+        float* dst = a.dqkv + (int64_t)row * 3 * F + h * 8 + (c & 7);
+        if (kind == 0)
+          dst[0] = v * a.scale;
+        else if (c < 8)
+          dst[F] = v * a.scale;
+        else
+          dst[2 * F] = v;
+      }
+    }
+    __syncthreads();
+    u += R;
+  }
+}
+
+// Backward v2 on quad-block MFMAs (fp32): the three 8-wide products (dQ, dK, dV), which
+// waste half of every 16x16x4, run as v_mfma_f32_4x4x1_16b_f32 blocks with the lane's own
+// dS / P value as the A operand and quad-layout float4s as B (as attn8_fwd2q_kernel).
+template <int W>
+__device__ __forceinline__ void attn8_bwd2q_dq(const A8Bwd2& a, int bx, float* red) {
+  const int h = blockIdx.y;
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int N = a.N, Nq = a.Nq;
+  const int base = bx * 16;
+  const SpanR<1> sp = span_rt<1>(base, i, N, a.seg_id, a.seg_ptr, W, w);
+  const int64_t hb = (int64_t)h * Nq * 8;
+  const Rsrc rk = mk_rsrc(a.Kp + hb, Nq * 8), rv = mk_rsrc(a.Vp + hb, Nq * 8), rkt = mk_rsrc(a.Kq + hb, Nq * 8);
+  const int op = off_pair(i, g), oq0 = (32 * g + 4 * (i & 3)) * 4, oq1 = oq0 + 64;
+  const int q = sp.row[0], qc = min(q, Nq - 1);
+  const float2 bq = ld2(a.Qp + hb + (int64_t)qc * 8 + 2 * g);
+  const float2 bo = ld2(a.dOp + hb + (int64_t)qc * 8 + 2 * g);
+  const float bq0 = bq.x * a.qscale, bq1 = bq.y * a.qscale, bo0 = bo.x, bo1 = bo.y;
+  const float nl = q < N ? a.NL[(int64_t)h * Nq + q] : 0.f;
+  const float nd = q < N ? a.ndelta[(int64_t)h * Nq + q] : 0.f;
+  const f4v cs = f4v{nl, nl, nl, nl}, cd = f4v{nd, nd, nd, nd};
+  f4v dq0 = f4z(), dq1 = f4z();
+  struct T {
+    float2 k, v;
+    float4 t0, t1;
+  };
+  auto load = [&](int k0) {
+    const int o = min(k0 * 32, (Nq - 16) * 32);
+    T x;
+    x.k = bl2(rk, op, o);
+    x.v = bl2(rv, op, o);
+    x.t0 = bl4(rkt, oq0, o);
+    x.t1 = bl4(rkt, oq1, o);
+    return x;
+  };
+  auto tile = [&](const T& x, int k0) {
+    f4v s = mfma(x.k.x, bq0, cs), dp = mfma(x.v.x, bo0, cd);
+    s = mfma(x.k.y, bq1, s);
+    dp = mfma(x.v.y, bo1, dp);
+    float ds[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ds[r] = fexp2(s[r]) * dp[r];
+    const bool full = k0 >= sp.ilo && k0 + 16 <= sp.ihi && k0 + 16 <= sp.ce;
+    if (!full) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 4 * g + r;
+        if (!(key >= sp.b[0] && key < sp.e[0] && key < sp.ce)) ds[r] = 0.f;
+      }
+    }
+    dq0 = mfma4(ds[0], x.t0.x, dq0);
+    dq1 = mfma4(ds[0], x.t1.x, dq1);
+    dq0 = mfma4(ds[1], x.t0.y, dq0);
+    dq1 = mfma4(ds[1], x.t1.y, dq1);
+    dq0 = mfma4(ds[2], x.t0.z, dq0);
+    dq1 = mfma4(ds[2], x.t1.z, dq1);
+    dq0 = mfma4(ds[3], x.t0.w, dq0);
+    dq1 = mfma4(ds[3], x.t1.w, dq1);
+  };
+  T xa = load(sp.cb);
+  __builtin_amdgcn_sched_barrier(0);
+  T xb = load(sp.cb + 16);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int k0 = sp.cb; k0 < sp.ce; k0 += 32) {
+    tile(xa, k0);
+    xa = load(k0 + 32);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(xb, k0 + 16);
+    xb = load(k0 + 48);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    dq0[r] += __shfl_xor(dq0[r], 16, 64);
+    dq0[r] += __shfl_xor(dq0[r], 32, 64);
+    dq1[r] += __shfl_xor(dq1[r], 16, 64);
+    dq1[r] += __shfl_xor(dq1[r], 32, 64);
+  }
+  // red [W][16 rows][8]: lane i of group 0 holds rows 4(i/4) + r, dims i%4 and 4 + i%4
+  if (g == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(w * 16 + 4 * (i >> 2) + r) * 8 + (i & 3)] = dq0[r];
+      red[(w * 16 + 4 * (i >> 2) + r) * 8 + 4 + (i & 3)] = dq1[r];
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 128; idx += 64 * W) {
+    const int qi = idx >> 3, d = idx & 7;
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < W; ++u) v += red[(u * 16 + qi) * 8 + d];
+    const int qq = base + qi;
+    if (qq < N) a.dqkv[(int64_t)qq * 24 * a.H + h * 8 + d] = v * a.scale;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void attn8_bwd2q_dkv(const A8Bwd2& a, int bx, float* red) {
+  const int h = blockIdx.y;
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int N = a.N, Nq = a.Nq;
+  const int base = bx * 16;
+  const SpanR<1> sp = span_rt<1>(base, i, N, a.seg_id, a.seg_ptr, W, w);
+  const int64_t hb = (int64_t)h * Nq * 8;
+  const Rsrc rq = mk_rsrc(a.Qp + hb, Nq * 8), ro = mk_rsrc(a.dOp + hb, Nq * 8);
+  const Rsrc rqt = mk_rsrc(a.Qq + hb, Nq * 8), rot = mk_rsrc(a.dOq + hb, Nq * 8);
+  const Rsrc rl = mk_rsrc(a.NL + (int64_t)h * Nq, Nq), rd = mk_rsrc(a.ndelta + (int64_t)h * Nq, Nq);
+  const int op = off_pair(i, g), oq0 = (32 * g + 4 * (i & 3)) * 4, oq1 = oq0 + 64, os = 16 * g;
+  const int kc = min(sp.row[0], Nq - 1);
+  const float2 bk = ld2(a.Kp + hb + (int64_t)kc * 8 + 2 * g);
+  const float2 bv = ld2(a.Vp + hb + (int64_t)kc * 8 + 2 * g);
+  const float bk0 = bk.x * a.qscale, bk1 = bk.y * a.qscale, bv0 = bv.x, bv1 = bv.y;
+  f4v dk0 = f4z(), dk1 = f4z(), dv0 = f4z(), dv1 = f4z();
+  struct T {
+    float2 q, o;
+    float4 qt0, qt1, ot0, ot1, nl, nd;
+  };
+  auto load = [&](int q0) {
+    const int ob = min(q0 * 32, (Nq - 16) * 32), os_ = min(q0 * 4, (Nq - 16) * 4);
+    T x;
+    x.q = bl2(rq, op, ob);
+    x.o = bl2(ro, op, ob);
+    x.nl = bl4(rl, os, os_);
+    x.nd = bl4(rd, os, os_);
+    x.qt0 = bl4(rqt, oq0, ob);
+    x.qt1 = bl4(rqt, oq1, ob);
+    x.ot0 = bl4(rot, oq0, ob);
+    x.ot1 = bl4(rot, oq1, ob);
+    return x;
+  };
+  auto tile = [&](const T& x, int q0) {
+    const f4v nl = f4v{x.nl.x, x.nl.y, x.nl.z, x.nl.w}, nd = f4v{x.nd.x, x.nd.y, x.nd.z, x.nd.w};
+    f4v s = mfma(x.q.x, bk0, nl), dp = mfma(x.o.x, bv0, nd);
+    s = mfma(x.q.y, bk1, s);
+    dp = mfma(x.o.y, bv1, dp);
+    float p[4], ds[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = fexp2(s[r]);
+    const bool full = q0 >= sp.ilo && q0 + 16 <= sp.ihi && q0 + 16 <= sp.ce;
+    if (!full) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + 4 * g + r;
+        if (!(qq >= sp.b[0] && qq < sp.e[0] && qq < sp.ce)) p[r] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ds[r] = p[r] * dp[r];
+    dv0 = mfma4(p[0], x.ot0.x, dv0);
+    dv1 = mfma4(p[0], x.ot1.x, dv1);
+    dk0 = mfma4(ds[0], x.qt0.x, dk0);
+    dk1 = mfma4(ds[0], x.qt1.x, dk1);
+    dv0 = mfma4(p[1], x.ot0.y, dv0);
+    dv1 = mfma4(p[1], x.ot1.y, dv1);
+    dk0 = mfma4(ds[1], x.qt0.y, dk0);
+    dk1 = mfma4(ds[1], x.qt1.y, dk1);
+    dv0 = mfma4(p[2], x.ot0.z, dv0);
+    dv1 = mfma4(p[2], x.ot1.z, dv1);
+    dk0 = mfma4(ds[2], x.qt0.z, dk0);
+    dk1 = mfma4(ds[2], x.qt1.z, dk1);
+    dv0 = mfma4(p[3], x.ot0.w, dv0);
+    dv1 = mfma4(p[3], x.ot1.w, dv1);
+    dk0 = mfma4(ds[3], x.qt0.w, dk0);
+    dk1 = mfma4(ds[3], x.qt1.w, dk1);
+  };
+  T xa = load(sp.cb);
+  __builtin_amdgcn_sched_barrier(0);
+  T xb = load(sp.cb + 16);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int q0 = sp.cb; q0 < sp.ce; q0 += 32) {
+    tile(xa, q0);
+    xa = load(q0 + 32);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(xb, q0 + 16);
+    xb = load(q0 + 48);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    dk0[r] += __shfl_xor(dk0[r], 16, 64);
+    dk0[r] += __shfl_xor(dk0[r], 32, 64);
+    dk1[r] += __shfl_xor(dk1[r], 16, 64);
+    dk1[r] += __shfl_xor(dk1[r], 32, 64);
+    dv0[r] += __shfl_xor(dv0[r], 16, 64);
+    dv0[r] += __shfl_xor(dv0[r], 32, 64);
+    dv1[r] += __shfl_xor(dv1[r], 16, 64);
+    dv1[r] += __shfl_xor(dv1[r], 32, 64);
+  }
+  // red [W][16 rows][16]: (dK | dV) of key rows 4(i/4) + r, dims i%4 and 4 + i%4
+  if (g == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float* row = red + (w * 16 + 4 * (i >> 2) + r) * 16;
+      row[i & 3] = dk0[r];
+      row[4 + (i & 3)] = dk1[r];
+      row[8 + (i & 3)] = dv0[r];
+      row[12 + (i & 3)] = dv1[r];
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 256; idx += 64 * W) {
+    const int ki = idx >> 4, c = idx & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < W; ++u) v += red[(u * 16 + ki) * 16 + c];
+    const int k = base + ki;
+    if (k < N) {
+      const int F = 8 * a.H;
+      a.dqkv[(int64_t)k * 3 * F + (c < 8 ? F : 2 * F) + h * 8 + (c & 7)] = c < 8 ? v * a.scale : v;
+    }
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn8_bwd2q_kernel(A8Bwd2 a) {
+  __shared__ float red[W * 16 * 16];
+  if ((int)blockIdx.x < a.nbq)
+    attn8_bwd2q_dq<W>(a, blockIdx.x, red);
+  else
+    attn8_bwd2q_dkv<W>(a, blockIdx.x - a.nbq, red);
+}
+
 // ------------------------------------------------------------------------------------ host
 constexpr int kRT = 2;  // row tiles per wave (grid-split kernels)
 
@@ -1124,10 +2045,24 @@ static int pick_splits(int N, int H, int64_t splits) {
 // splits < 0 forces W = -splits (sweeps and tests).
 static int pick_w(int ntiles) { return ntiles >= 32 ? 8 : (ntiles >= 12 ? 4 : 2); }
 
+// HYDRA_ATTN8_QUAD=0 keeps the 16x16x4 P.V product (A/B)
+static bool quad_enabled() {
+  static int flag = -1;
+  if (flag < 0) {
+    const char* e = std::getenv("HYDRA_ATTN8_QUAD");
+    flag = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return flag == 1;
+}
+
 template <int W, bool BF>
 static void fwd2_go(const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H, const int* sid,
                     const int* sptr, float qs, float* O, float* L) {
   dim3 grid(ceil_div(Nq, 16), H);
+  if (!BF && quad_enabled()) {
+    attn8_fwd2q_kernel<W><<<grid, 64 * W, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
+    return;
+  }
   attn8_fwd2_kernel<1, W, BF><<<grid, 64 * W, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
 }
 
@@ -1145,8 +2080,62 @@ static void launch_fwd2_p(int var, const float* Qp, const float* Kp, const float
   }
 }
 
+// v3 (persistent, cost-balanced) eligibility: fp32, batch-scope segment layouts (<= 2
+// contiguous segments ending at N), Nq the 16-row padding of N.  HYDRA_ATTN8_V3=0 keeps v2.
+static bool v3_enabled() {
+  static int flag = -1;
+  if (flag < 0) {
+    const char* e = std::getenv("HYDRA_ATTN8_V3");
+    flag = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return flag == 1;
+}
+static bool v3_ok(int var, int N, int Nq, int nseg, bool bf16) {
+  return v3_enabled() && var == 0 && !bf16 && nseg >= 1 && nseg <= 2 && Nq == 16 * ceil_div(N, 16) && N > 0;
+}
+static int v3_grid(int64_t units) {
+  static int per_cu = -1;
+  if (per_cu < 0) {
+    const char* e = std::getenv("HYDRA_ATTN8_V3_PERCU");
+    per_cu = e ? std::max(1, std::min(4, std::atoi(e))) : 1;
+  }
+  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)num_cus() * per_cu, units));
+}
+// group-size caps (forward, dQ, dK/dV); HYDRA_ATTN8_V3_R="rf,rq,rk" for sweeps
+static void v3_caps(int& rf, int& rq, int& rk) {
+  static int c[3] = {2, 1, 1};
+  static bool init = false;
+  if (!init) {
+    init = true;
+    if (const char* e = std::getenv("HYDRA_ATTN8_V3_R")) {
+      int a = 0, b = 0, d = 0;
+      if (std::sscanf(e, "%d,%d,%d", &a, &b, &d) == 3 && a >= 1 && a <= 4 && b >= 1 && b <= 3 && d >= 1 && d <= 3) {
+        c[0] = a;
+        c[1] = b;
+        c[2] = d;
+      }
+    }
+  }
+  rf = c[0];
+  rq = c[1];
+  rk = c[2];
+}
+
 static void launch_fwd2(int var, const float* Qp, const float* Kp, const float* Vq, int N, int Nq, int H,
-                        const int* sid, const int* sptr, float qs, float* O, float* L, bool bf16 = false) {
+                        const int* sid, const int* sptr, float qs, float* O, float* L, bool bf16 = false,
+                        int nseg = 0) {
+  if (v3_ok(var, N, Nq, nseg, bf16)) {
+    int rf, rq, rk;
+    v3_caps(rf, rq, rk);
+    const int G = v3_grid((int64_t)H * (Nq / 16));
+    switch (rf) {
+      case 1: attn8_fwd3_kernel<1><<<G, 64 * kNW3, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sptr, nseg, qs, O, L); break;
+      case 2: attn8_fwd3_kernel<2><<<G, 64 * kNW3, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sptr, nseg, qs, O, L); break;
+      case 3: attn8_fwd3_kernel<3><<<G, 64 * kNW3, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sptr, nseg, qs, O, L); break;
+      default: attn8_fwd3_kernel<4><<<G, 64 * kNW3, 0, stream()>>>(Qp, Kp, Vq, N, Nq, H, sptr, nseg, qs, O, L); break;
+    }
+    return;
+  }
   if (bf16)
     launch_fwd2_p<true>(var, Qp, Kp, Vq, N, Nq, H, sid, sptr, qs, O, L);
   else
@@ -1157,6 +2146,10 @@ template <int W, bool BF>
 static void bwd2_go(A8Bwd2 b) {
   b.nbq = ceil_div(b.Nq, 16);
   dim3 grid(2 * b.nbq, b.H);
+  if (!BF && quad_enabled()) {
+    attn8_bwd2q_kernel<W><<<grid, 64 * W, 0, stream()>>>(b);
+    return;
+  }
   attn8_bwd2_kernel<1, W, BF><<<grid, 64 * W, 0, stream()>>>(b);
 }
 
@@ -1173,7 +2166,23 @@ static void launch_bwd2_p(int var, const A8Bwd2& b) {
   }
 }
 
-static void launch_bwd2(int var, const A8Bwd2& b, bool bf16 = false) {
+static void launch_bwd2(int var, const A8Bwd2& b, bool bf16 = false, int nseg = 0) {
+  if (v3_ok(var, b.N, b.Nq, nseg, bf16)) {
+    int rf, rq, rk;
+    v3_caps(rf, rq, rk);
+    const int G = v3_grid(2LL * b.H * (b.Nq / 16));
+    if (rq == 1 && rk == 1)
+      attn8_bwd3_kernel<1, 1><<<G, 64 * kNW3, 0, stream()>>>(b, nseg);
+    else if (rq == 2 && rk == 1)
+      attn8_bwd3_kernel<2, 1><<<G, 64 * kNW3, 0, stream()>>>(b, nseg);
+    else if (rq == 2 && rk == 2)
+      attn8_bwd3_kernel<2, 2><<<G, 64 * kNW3, 0, stream()>>>(b, nseg);
+    else if (rq == 3 && rk == 2)
+      attn8_bwd3_kernel<3, 2><<<G, 64 * kNW3, 0, stream()>>>(b, nseg);
+    else
+      attn8_bwd3_kernel<3, 3><<<G, 64 * kNW3, 0, stream()>>>(b, nseg);
+    return;
+  }
   if (bf16)
     launch_bwd2_p<true>(var, b);
   else
@@ -1229,7 +2238,7 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
   if (splits <= 0) {  // v2: one launch, in-workgroup key split (variant -splits, 0 = default)
     launch_fwd2((int)(-splits), Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(), (int)N, (int)Nq,
                 (int)H, seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), qs, O.data_ptr<float>(), L.data_ptr<float>(),
-                bf16);
+                bf16, (int)seg_ptr.numel() - 1);
     return {O, L};
   }
   const int S = pick_splits((int)N, (int)H, splits);
@@ -1382,7 +2391,7 @@ at::Tensor attn8_bwd_packed(const at::Tensor& ndelta, const at::Tensor& dOp, con
   b.scale = (float)scale;
   b.qscale = (float)scale * kLog2e;
   b.dqkv = dqkv.data_ptr<float>();
-  launch_bwd2(0, b, bf16);
+  launch_bwd2(0, b, bf16, (int)seg_ptr.numel() - 1);
   return dqkv;
 }
 
@@ -1415,7 +2424,7 @@ at::Tensor attn8_bwd(const at::Tensor& dO, const at::Tensor& O, const at::Tensor
     b.scale = (float)scale;
     b.qscale = (float)scale * kLog2e;
     b.dqkv = dqkv.data_ptr<float>();
-    launch_bwd2((int)(-splits), b);
+    launch_bwd2((int)(-splits), b, false, (int)seg_ptr.numel() - 1);
     return dqkv;
   }
   const int S = pick_splits((int)N, (int)H, splits);

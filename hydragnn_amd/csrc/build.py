@@ -44,6 +44,20 @@ def sources():
     return sorted(glob.glob(os.path.join(HERE, "*.hip")) + glob.glob(os.path.join(HERE, "*.cpp")))
 
 
+def source_digest():
+    """sha256 over every native source and header (names + bytes): written next to the
+    library at build time and checked at load time, so a stale ``_C.so`` (sources edited,
+    library not rebuilt) fails loudly instead of running old kernels."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(sources() + glob.glob(os.path.join(HERE, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def _headers_mtime():
     hs = glob.glob(os.path.join(HERE, "*.h"))
     return max([os.path.getmtime(h) for h in hs] + [0.0])
@@ -96,6 +110,8 @@ def build(jobs=None, force=False, verbose=True):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(OUT + ".srchash", "w") as fh:
+        fh.write(source_digest() + "\n")
     if verbose:
         print(f"[hydragnn_amd] built {OUT} from {len(srcs)} sources for {ARCH}")
     return OUT

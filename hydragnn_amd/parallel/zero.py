@@ -105,9 +105,12 @@ class ZeroRedundancyOptimizer(torch.optim.Optimizer):
         ``reduce_grads`` path needs the other ranks' flags (one small all-reduce + a host
         read; that path is never captured).  Without it every rank already holds averaged
         gradients (DDP wrapper / the captured step's bucketed all-reduce, which attaches a
-        gradient to every parameter), so the local flags are the global ones."""
-        if all(f == 1.0 for f in used):
-            return []
+        gradient to every parameter), so the local flags are the global ones.
+
+        The all-reduce runs on EVERY rank whenever it is needed, even when this rank's
+        flags are all 1: another rank may lack a gradient (a branch absent from its batch),
+        and skipping the collective on one rank only would desynchronise the collective
+        sequence.  The host-side early return is taken only when no reduction is needed."""
         if self.world > 1 and self.reduce_grads:
             t = torch.tensor(used, device=self.flat.device, dtype=self.flat.dtype)
             dist.all_reduce(t, group=self.group)

@@ -273,6 +273,13 @@ class TrainStep:
                 if hasattr(optimizer, "set_usage_flags"):
                     optimizer.set_usage_flags({p: self.sync.flags[k:k + 1] for k, ps in enumerate(groups)
                                                for p in ps})
+                else:
+                    import warnings
+
+                    warnings.warn(f"{type(optimizer).__name__} cannot take the captured step's per-branch usage "
+                                  "flags: heads of branches absent from a batch still get weight and moment "
+                                  "decay (use FusedAdamW, or eager mode, for skip-if-no-grad semantics)",
+                                  RuntimeWarning, stacklevel=2)
         elif not isinstance(self.model, DistributedDataParallel) and self.taskpar is None:
             self.flat_grads = FlatGrads(params)
         self.node_bucket, self.edge_bucket = node_bucket, edge_bucket

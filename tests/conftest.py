@@ -28,14 +28,3 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
-
-
-import os as _os
-
-if _os.environ.get("HYDRA_PNA_CHECK") == "1":  # debug aid (tools/pna_agg_check.py)
-    import sys as _sys
-
-    _sys.path.insert(0, _os.path.join(_os.path.dirname(__file__), "..", "tools"))
-    import pna_agg_check as _pc
-
-    _pc.install()

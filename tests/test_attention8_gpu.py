@@ -111,3 +111,33 @@ def test_attn8_bf16_mfma_close_to_reference(N, scope):
     nd32[:, :N] = -(dO * O32).view(N, H, 8).sum(-1).t()
     dq32 = ops.attn8_bwd_packed(nd32, dOp, dOq, L32, Qp, Qq, Kp, Kq, Vp, sid, sptr, N, sc)
     torch.testing.assert_close(dq32.double().cpu(), g, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,nv,H", [(1, 1, 1), (16, 16, 8), (33, 20, 2), (700, 700, 8), (700, 0, 1),
+                                    (2311, 2311, 8), (2528, 2311, 8), (2560, 2400, 4), (4100, 3000, 8)])
+def test_attn8_v3_persistent_batch_scope(N, nv, H):
+    """v3 (one 16-wave workgroup per CU, units dealt by cost, wave pieces merged in LDS):
+    batch-scope layouts with and without a padding segment, row counts on and off the
+    16-row grid, against the float64 reference; bitwise deterministic across launches."""
+    torch.manual_seed(N + nv + H)
+    dev = torch.device("cuda")
+    ops = _native.ops()
+    qkv = (torch.randn(N, 24 * H, device=dev) * 1.5).contiguous()
+    sid, sptr = make_segments(N, "batch", num_valid=nv if nv < N else None, device=dev)
+    sc = 1.0 / math.sqrt(8)
+    Qp, Qq, Kp, Kq, Vp, Vq = ops.attn8_pack(qkv, H)
+    O, L2 = ops.attn8_fwd(Qp, Kp, Vq, sid, sptr, N, sc, 0)
+    O2, L22 = ops.attn8_fwd(Qp, Kp, Vq, sid, sptr, N, sc, 0)
+    assert torch.equal(O, O2) and torch.equal(L2, L22)
+    Nq = Qp.shape[1]
+    if Nq > N:
+        assert torch.all(L2[:, N:] == 0)
+    x = qkv.double().cpu().requires_grad_()
+    ref = attention_reference(x, H, sid.cpu(), sc)
+    torch.testing.assert_close(O.double().cpu(), ref.detach(), rtol=2e-5, atol=2e-5)
+    dO = torch.randn(N, 8 * H, device=dev)
+    ref.backward(dO.double().cpu())
+    dqkv = ops.attn8_bwd(dO, O, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, sc, 0)
+    dqkv2 = ops.attn8_bwd(dO, O, L2, Qp, Qq, Kp, Kq, Vp, sid, sptr, sc, 0)
+    assert torch.equal(dqkv, dqkv2)
+    torch.testing.assert_close(dqkv.double().cpu(), x.grad, rtol=1e-4, atol=1e-4)

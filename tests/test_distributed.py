@@ -281,6 +281,35 @@ def _zero_unused_body(rank, world):
                 opt.load_state_dict(bad)
 
 
+def _zero_one_rank_unused_body(rank, world):
+    """Only rank 1 lacks a gradient for the last parameter (its batch has no sample of that
+    branch): every rank must still join the usage-flag all-reduce (a rank-local early return
+    would desynchronise the collectives), and the parameter is USED globally, so it is
+    updated with the average of the gradients that exist (zeros from rank 1)."""
+    from hydragnn_amd.parallel.zero import ZeroRedundancyOptimizer
+
+    for elementwise in (True, False):
+        torch.manual_seed(5)
+        ref, sh = _mlp(), _mlp()
+        sh.load_state_dict(ref.state_dict())
+        mk = lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.1)  # noqa: E731
+        opt_ref = mk(ref.parameters())
+        opt = ZeroRedundancyOptimizer(list(sh.parameters()), mk, reduce_grads=True, elementwise=elementwise)
+        nparam = len(list(ref.parameters()))
+        for it in range(3):
+            g = [[torch.randn_like(p) for p in ref.parameters()] for _ in range(world)]
+            for i, p in enumerate(ref.parameters()):
+                p.grad = sum(g[r][i] for r in range(world) if not (r == 1 and i == nparam - 1)) / world
+            for i, p in enumerate(sh.parameters()):
+                p.grad = None if (rank == 1 and i == nparam - 1) else g[rank][i].clone()
+            opt_ref.step()
+            opt.step()
+            opt_ref.zero_grad(set_to_none=True)
+            opt.zero_grad(set_to_none=True)
+        for a, b in zip(sh.parameters(), ref.parameters()):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
 def _syncbn_body(rank, world):
     from hydragnn_amd.parallel.ddp import SyncBatchNorm
 
@@ -527,6 +556,10 @@ def test_nan_guard_is_global():
 
 def test_zero1_unused_parameters():
     run_ranks("_zero_unused_body")
+
+
+def test_zero1_unused_on_one_rank_only():
+    run_ranks("_zero_one_rank_unused_body")
 
 
 def test_syncbatchnorm_matches_full_batch():

@@ -28,7 +28,7 @@ tb = graph_time(lambda: ops.attn_bwd(dO, qkv, O, L, sid, sptr, H, sc, N, 0))
 print(f"valu      : fwd {tf:7.1f} us  bwd {tb:7.1f} us", flush=True)
 pk = ops.attn8_pack(qkv, H)
 print("v2 auto shape (W fwd, W bwd):", list(ops.attn8_v2_shape(N, H)), flush=True)
-names = {0: "v2 auto"}
+names = {0: "v3 auto" if os.environ.get("HYDRA_ATTN8_V3", "1") != "0" else "v2 auto"}
 for S in [8, 0, -2, -3, -4, -5, -6, -8]:
     O8, L8 = ops.attn8_fwd(pk[0], pk[2], pk[5], sid, sptr, N, sc, S)
     d8 = ops.attn8_bwd(dO, O8, L8, pk[0], pk[1], pk[2], pk[3], pk[4], sid, sptr, sc, S)

@@ -30,6 +30,6 @@ C=""
 for c in TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
   have "${c%_sum}" && C="$C $c"
 done
-[ -n "$C" ] && { run_pass C $C TCC_HIT_sum || exit $?; }
+[ -n "$C" ] && { run_pass C $C TCC_HIT_sum TCC_MISS_sum || exit $?; }
 python3 tools/pmc_roofline.py $OUT > gpurun_out/pmc_top_summary.txt 2>&1
 cat gpurun_out/pmc_top_summary.txt | head -80

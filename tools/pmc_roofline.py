@@ -72,8 +72,10 @@ def main(d, top=14):
         wt = 100.0 * c.get("SQ_WAIT_ANY", 0.0) / wc if wc else 0.0
         by = 64.0 * (c.get("TCC_EA0_RDREQ_sum", 0.0) + c.get("TCC_EA0_WRREQ_sum", 0.0))
         gbs = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
-        h, m = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
-        l2 = 100.0 * h / (h + m) if h + m else float("nan")
+        # L2 hit rate needs BOTH counters of the same pass (TCC_MISS_sum was missing before
+        # round 5, which printed a constant 100 %): report n/a rather than a fake rate
+        h, m = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+        l2 = 100.0 * h / (h + m) if (h is not None and m is not None and h + m > 0) else float("nan")
         if us < 4:
             b = "launch"
         elif mf >= 60:

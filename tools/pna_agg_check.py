@@ -1,4 +1,4 @@
-"""Debug aid: HYDRA_PNA_CHECK=1 compares every fused PNA aggregation (ops.pna.pna_aggregate)
+"""Debug aid (python tools/pna_agg_check.py <pytest args>): compares every fused PNA aggregation (ops.pna.pna_aggregate)
 with the composite, forward and backward, and prints the largest differences (eager only)."""
 import torch
 
@@ -43,3 +43,13 @@ def install():
     pna.pna_aggregate = checked
     import hydragnn_amd.models.painn as painn
     painn.pna_aggregate = checked
+
+
+if __name__ == "__main__":
+    # python tools/pna_agg_check.py <pytest args>: run pytest in-process with the checker installed
+    import sys
+
+    import pytest
+
+    install()
+    sys.exit(pytest.main(sys.argv[1:]))
