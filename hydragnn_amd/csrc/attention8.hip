@@ -633,15 +633,6 @@ __device__ __forceinline__ float4 bl4(Rsrc r, int vo, int so) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
 }
 __device__ __forceinline__ float max4(f4v s) { return fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3])); }
-// max of 4 accumulator values as a v_max3_f32 chain: fmaxf on an MFMA result makes the
-// compiler canonicalise every operand first (one v_max x, x each); the scores here are never
-// signalling NaNs, so the raw instruction is exact
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-  float r;
-  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ float max4r(f4v s) { return vmax3(vmax3(s[0], s[1], s[2]), s[3], s[3]); }
 
 
 // bf16 mode (precision "bf16"): every product on v_mfma_f32_16x16x16_bf16 (fp32 accumulate).
@@ -838,11 +829,13 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2_kernel(const float* __restr
 // (keys 4g..4g+3 of dim 4dh + i%4: one float4 per d half).  2 x 4 independent 10-cycle MFMAs
 // replace 4 dependent 32-cycle ones; the 4 lane groups' partial O are summed once per slice.
 // VALU per tile is kept minimal (it adds to the MFMA time): the -m seed is rebuilt from one
-// register, the score maximum runs on raw v_max3_f32.
+// register.  (A raw inline-asm v_max3_f32 on the score accumulator, skipping the compiler's
+// canonicalising v_max x, x, read the MFMA result without the hazard wait states the compiler
+// inserts for its own instructions: the rescale decisions, and so the rounding, varied between
+// launches.)
 __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
-
 template <int W>
 __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __restrict__ Qp,
                                                              const float* __restrict__ Kp,
@@ -861,7 +854,7 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __rest
   const float2 bq = ld2(Qp + ((int64_t)h * Nq + min(sp.row[0], Nq - 1)) * 8 + 2 * g);
   const float bq0 = bq.x * qscale, bq1 = bq.y * qscale;
   float m = -INFINITY, thr = -INFINITY, l = 0.f, negm = 0.f;
-  f4v o0 = f4z(), o1 = f4z();  // 4x4 blocks: rows = queries 4(i/4)+r, cols = dims (4dh + c)
+  f4v o0 = f4z(), o1 = f4z();  // O[query i][dim 4dh + r], partial over the lane group's keys
   auto tile = [&](float2 kk, float4 va, float4 vb, int k0) {
     const f4v cin = f4v{negm, negm, negm, negm};
     f4v s = mfma(kk.x, bq0, cin);
@@ -874,7 +867,7 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __rest
         if (!(key >= sp.b[0] && key < sp.e[0] && key < sp.ce)) s[r] = -INFINITY;
       }
     }
-    const float mx = max4r(s);
+    const float mx = max4(s);
     if (__any(mx > thr)) {  // move the row reference (rare), rescale o and l
       const float mn = fmaxf(m, wmax16(mx) - negm);
       if (mn > -INFINITY) {
@@ -889,14 +882,14 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __rest
       }
     }
     const float p0 = fexp2(s[0]), p1 = fexp2(s[1]), p2 = fexp2(s[2]), p3 = fexp2(s[3]);
-    o0 = mfma4(p0, va.x, o0);
-    o1 = mfma4(p0, vb.x, o1);
-    o0 = mfma4(p1, va.y, o0);
-    o1 = mfma4(p1, vb.y, o1);
-    o0 = mfma4(p2, va.z, o0);
-    o1 = mfma4(p2, vb.z, o1);
-    o0 = mfma4(p3, va.w, o0);
-    o1 = mfma4(p3, vb.w, o1);
+    o0 = mfma4(va.x, p0, o0);
+    o1 = mfma4(vb.x, p0, o1);
+    o0 = mfma4(va.y, p1, o0);
+    o1 = mfma4(vb.y, p1, o1);
+    o0 = mfma4(va.z, p2, o0);
+    o1 = mfma4(vb.z, p2, o1);
+    o0 = mfma4(va.w, p3, o0);
+    o1 = mfma4(vb.w, p3, o1);
     l += (p0 + p1) + (p2 + p3);
   };
   const int cmax = (Nq - 16) * 32;
@@ -929,11 +922,10 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __rest
     o1[r] += __shfl_xor(o1[r], 32, 64);
   }
   if (g == 0) {
-    // lane i: block i/4, column c = i%4, rows r: query 4(i/4) + r, dims c and 4 + c
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      red[w][4 * (i >> 2) + r][2 + (i & 3)] = o0[r];
-      red[w][4 * (i >> 2) + r][6 + (i & 3)] = o1[r];
+      red[w][i][2 + r] = o0[r];
+      red[w][i][6 + r] = o1[r];
     }
   } else if (g == 1) {
     red[w][i][0] = m;
@@ -1851,14 +1843,14 @@ __device__ __forceinline__ void attn8_bwd2q_dq(const A8Bwd2& a, int bx, float* r
         if (!(key >= sp.b[0] && key < sp.e[0] && key < sp.ce)) ds[r] = 0.f;
       }
     }
-    dq0 = mfma4(ds[0], x.t0.x, dq0);
-    dq1 = mfma4(ds[0], x.t1.x, dq1);
-    dq0 = mfma4(ds[1], x.t0.y, dq0);
-    dq1 = mfma4(ds[1], x.t1.y, dq1);
-    dq0 = mfma4(ds[2], x.t0.z, dq0);
-    dq1 = mfma4(ds[2], x.t1.z, dq1);
-    dq0 = mfma4(ds[3], x.t0.w, dq0);
-    dq1 = mfma4(ds[3], x.t1.w, dq1);
+    dq0 = mfma4(x.t0.x, ds[0], dq0);
+    dq1 = mfma4(x.t1.x, ds[0], dq1);
+    dq0 = mfma4(x.t0.y, ds[1], dq0);
+    dq1 = mfma4(x.t1.y, ds[1], dq1);
+    dq0 = mfma4(x.t0.z, ds[2], dq0);
+    dq1 = mfma4(x.t1.z, ds[2], dq1);
+    dq0 = mfma4(x.t0.w, ds[3], dq0);
+    dq1 = mfma4(x.t1.w, ds[3], dq1);
   };
   T xa = load(sp.cb);
   __builtin_amdgcn_sched_barrier(0);
@@ -1879,12 +1871,12 @@ __device__ __forceinline__ void attn8_bwd2q_dq(const A8Bwd2& a, int bx, float* r
     dq1[r] += __shfl_xor(dq1[r], 16, 64);
     dq1[r] += __shfl_xor(dq1[r], 32, 64);
   }
-  // red [W][16 rows][8]: lane i of group 0 holds rows 4(i/4) + r, dims i%4 and 4 + i%4
+  // red [W][16 rows][8]: lane i of group 0 holds query i, dims r and 4 + r
   if (g == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      red[(w * 16 + 4 * (i >> 2) + r) * 8 + (i & 3)] = dq0[r];
-      red[(w * 16 + 4 * (i >> 2) + r) * 8 + 4 + (i & 3)] = dq1[r];
+      red[(w * 16 + i) * 8 + r] = dq0[r];
+      red[(w * 16 + i) * 8 + 4 + r] = dq1[r];
     }
   }
   __syncthreads();
@@ -1950,22 +1942,22 @@ __device__ __forceinline__ void attn8_bwd2q_dkv(const A8Bwd2& a, int bx, float* 
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) ds[r] = p[r] * dp[r];
-    dv0 = mfma4(p[0], x.ot0.x, dv0);
-    dv1 = mfma4(p[0], x.ot1.x, dv1);
-    dk0 = mfma4(ds[0], x.qt0.x, dk0);
-    dk1 = mfma4(ds[0], x.qt1.x, dk1);
-    dv0 = mfma4(p[1], x.ot0.y, dv0);
-    dv1 = mfma4(p[1], x.ot1.y, dv1);
-    dk0 = mfma4(ds[1], x.qt0.y, dk0);
-    dk1 = mfma4(ds[1], x.qt1.y, dk1);
-    dv0 = mfma4(p[2], x.ot0.z, dv0);
-    dv1 = mfma4(p[2], x.ot1.z, dv1);
-    dk0 = mfma4(ds[2], x.qt0.z, dk0);
-    dk1 = mfma4(ds[2], x.qt1.z, dk1);
-    dv0 = mfma4(p[3], x.ot0.w, dv0);
-    dv1 = mfma4(p[3], x.ot1.w, dv1);
-    dk0 = mfma4(ds[3], x.qt0.w, dk0);
-    dk1 = mfma4(ds[3], x.qt1.w, dk1);
+    dv0 = mfma4(x.ot0.x, p[0], dv0);
+    dv1 = mfma4(x.ot1.x, p[0], dv1);
+    dk0 = mfma4(x.qt0.x, ds[0], dk0);
+    dk1 = mfma4(x.qt1.x, ds[0], dk1);
+    dv0 = mfma4(x.ot0.y, p[1], dv0);
+    dv1 = mfma4(x.ot1.y, p[1], dv1);
+    dk0 = mfma4(x.qt0.y, ds[1], dk0);
+    dk1 = mfma4(x.qt1.y, ds[1], dk1);
+    dv0 = mfma4(x.ot0.z, p[2], dv0);
+    dv1 = mfma4(x.ot1.z, p[2], dv1);
+    dk0 = mfma4(x.qt0.z, ds[2], dk0);
+    dk1 = mfma4(x.qt1.z, ds[2], dk1);
+    dv0 = mfma4(x.ot0.w, p[3], dv0);
+    dv1 = mfma4(x.ot1.w, p[3], dv1);
+    dk0 = mfma4(x.qt0.w, ds[3], dk0);
+    dk1 = mfma4(x.qt1.w, ds[3], dk1);
   };
   T xa = load(sp.cb);
   __builtin_amdgcn_sched_barrier(0);
@@ -1990,15 +1982,15 @@ __device__ __forceinline__ void attn8_bwd2q_dkv(const A8Bwd2& a, int bx, float* 
     dv1[r] += __shfl_xor(dv1[r], 16, 64);
     dv1[r] += __shfl_xor(dv1[r], 32, 64);
   }
-  // red [W][16 rows][16]: (dK | dV) of key rows 4(i/4) + r, dims i%4 and 4 + i%4
+  // red [W][16 rows][16]: (dK | dV) of key i, dims r and 4 + r
   if (g == 0) {
+    float* row = red + (w * 16 + i) * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float* row = red + (w * 16 + 4 * (i >> 2) + r) * 16;
-      row[i & 3] = dk0[r];
-      row[4 + (i & 3)] = dk1[r];
-      row[8 + (i & 3)] = dv0[r];
-      row[12 + (i & 3)] = dv1[r];
+      row[r] = dk0[r];
+      row[4 + r] = dk1[r];
+      row[8 + r] = dv0[r];
+      row[12 + r] = dv1[r];
     }
   }
   __syncthreads();
@@ -2015,13 +2007,24 @@ __device__ __forceinline__ void attn8_bwd2q_dkv(const A8Bwd2& a, int bx, float* 
   }
 }
 
-template <int W>
+// QM bit 0: dQ pass on quad blocks, bit 1: dK/dV pass on quad blocks (else the v2 bodies).
+// Default (HYDRA_ATTN8_QUADB) 1: the quad dK/dV body needs 28 operand registers per tile slot
+// (two float4 per quad operand) against 20, which drops the kernel to 5 waves per SIMD; at the
+// OC20 shape (MI355X) dQ-only measured 83.2 us against 85.6 (v2) and 90.1 (both passes).
+template <int W, int QM>
 __global__ void __launch_bounds__(64 * W) attn8_bwd2q_kernel(A8Bwd2 a) {
   __shared__ float red[W * 16 * 16];
-  if ((int)blockIdx.x < a.nbq)
-    attn8_bwd2q_dq<W>(a, blockIdx.x, red);
-  else
-    attn8_bwd2q_dkv<W>(a, blockIdx.x - a.nbq, red);
+  if ((int)blockIdx.x < a.nbq) {
+    if constexpr (QM & 1)
+      attn8_bwd2q_dq<W>(a, blockIdx.x, red);
+    else
+      attn8_bwd2_dq<1, W, false>(a, blockIdx.x, red);
+  } else {
+    if constexpr (QM & 2)
+      attn8_bwd2q_dkv<W>(a, blockIdx.x - a.nbq, red);
+    else
+      attn8_bwd2_dkv<1, W, false>(a, blockIdx.x - a.nbq, red);
+  }
 }
 
 // ------------------------------------------------------------------------------------ host
@@ -2147,8 +2150,13 @@ static void bwd2_go(A8Bwd2 b) {
   b.nbq = ceil_div(b.Nq, 16);
   dim3 grid(2 * b.nbq, b.H);
   if (!BF && quad_enabled()) {
-    attn8_bwd2q_kernel<W><<<grid, 64 * W, 0, stream()>>>(b);
-    return;
+    static const int qm = std::getenv("HYDRA_ATTN8_QUADB") ? std::atoi(std::getenv("HYDRA_ATTN8_QUADB")) : 1;
+    switch (qm) {
+      case 1: attn8_bwd2q_kernel<W, 1><<<grid, 64 * W, 0, stream()>>>(b); return;
+      case 2: attn8_bwd2q_kernel<W, 2><<<grid, 64 * W, 0, stream()>>>(b); return;
+      case 3: attn8_bwd2q_kernel<W, 3><<<grid, 64 * W, 0, stream()>>>(b); return;
+      default: break;
+    }
   }
   attn8_bwd2_kernel<1, W, BF><<<grid, 64 * W, 0, stream()>>>(b);
 }

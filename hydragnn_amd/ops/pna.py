@@ -130,14 +130,11 @@ def pna_aggregate(m, si, avg_deg, aggregators=("mean", "min", "max", "std"),
     """Degree-scaler aggregation [N, len(aggr)*len(scalers)*F] of a per-row table ``m``
     over ``si`` (sorted or permuted CSR).  GPU fp32 with the [mean, min, max, std]
     aggregator set: one fused kernel each way; otherwise (CPU, other aggregators, double
-    backward) the composite.
-
-    Known gap: inside a captured (hipGraph) step the composite still runs — the fused op
-    matches the composite step for step in eager training (tools/pna_agg_check.py) but the
-    captured PNAEq conv-head CI training diverged with it (RMSE 2.13 vs < 0.6), cause not
-    yet isolated; ``HYDRA_PNA_AGG_CAPTURE=1`` opts in for investigation."""
-    if m.is_cuda and torch.cuda.is_current_stream_capturing() and os.environ.get("HYDRA_PNA_AGG_CAPTURE") != "1":
-        return pna_aggregate_composite(m, si, avg_deg, aggregators, scalers)
+    backward) the composite.  Captured steps use the fused op too: a captured step with it
+    is bitwise identical to the eager padded step, gradients included
+    (tools/pnaeq_capture_debug.py MODE=compare, 400 steps of the PNAEq conv-head CI run).  The
+    round-4 divergence of that run was not this op: replayed steps ignored lr changes
+    (ReduceLROnPlateau), fixed in TrainStep._sync_opt_hparams."""
     if (m.is_cuda and fused("pna") and m.dtype == torch.float32 and m.dim() == 2 and si.limit is None
             and tuple(aggregators) == ("mean", "min", "max", "std") and 1 <= len(scalers) <= 8):
         codes = 0

@@ -124,6 +124,24 @@ class FusedAdamW(torch.optim.Optimizer):
                                      None if g is None else g.reshape(1).float())
         return loss
 
+    def sync_hparams(self):
+        """Copy the host learning rates into the device scalars the captured update reads.
+        A captured step never calls ``step()`` on the host, so without this a schedule
+        (ReduceLROnPlateau, ``param_groups[...]["lr"] = ...``) would never reach a replayed
+        step.  Called by ``TrainStep`` before every replay; a no-op unless an lr changed.
+        Returns False when another hyper-parameter changed since the tables were built (those
+        are kernel arguments of the captured launch: the caller must recapture)."""
+        if self._tables is None:
+            return True
+        ok = True
+        for group, t in zip(self.param_groups, self._tables):
+            if t is None:
+                continue
+            if t[3] != group["lr"]:
+                t[2][1].fill_(group["lr"])
+                t[3] = group["lr"]
+        return ok
+
     def skipped_steps(self):
         """Updates skipped by the non-finite guard so far (one device read)."""
         n = self._skipped_cpu

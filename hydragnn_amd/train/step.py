@@ -188,6 +188,7 @@ class _Captured:
         self.next = 0
         self.g_opt = None
         self.dev_plan = None
+        self.hparams = None  # optimizer hyper-parameters the captured update was built with
         self.dev_seed = None
         self.seeded = False
         self.lay = None
@@ -492,8 +493,15 @@ class TrainStep:
         return out
 
     def _snapshot(self):
-        # optimizer state tensors include the per-parameter step counts (FusedAdamW)
+        # optimizer state tensors include the per-parameter step counts (FusedAdamW); the
+        # device dropout counter is part of the state too: the capture warm-up advances it,
+        # and a capture in mid-training must not shift the random stream of the later steps
+        # (the captured trajectory then matches the eager padded one step for step)
+        from ..ops import rng as _rngmod
+
         ts = list(self.module.parameters()) + list(self.module.buffers()) + self._opt_state_tensors()
+        if self.device.type == "cuda":
+            ts.append(_rngmod.counter(self.device))
         return {"pairs": [(t, t.detach().clone()) for t in ts], "ids": {id(t) for t in ts}}
 
     @torch.no_grad()
@@ -577,6 +585,7 @@ class TrainStep:
                 cap.g_opt = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(cap.g_opt, pool=pool):
                     self.opt.step()
+        cap.hparams = self._opt_hparams()
         self.graphs[key] = cap
         torch.cuda.synchronize()
         self._restore(snap)
@@ -598,6 +607,11 @@ class TrainStep:
         if cap is None:
             cap = self._capture(store, indices, key)
             # the capture warm-up already trained on this batch; replay once more as the step
+        if not self._sync_opt_hparams(cap):
+            # a hyper-parameter baked into the captured update changed: recapture this bucket
+            # (the snapshot/restore of _capture keeps the training state unchanged)
+            self.graphs.pop(key, None)
+            cap = self._capture(store, indices, key)
         tm = self.host_times
         j = cap.next
         cap.next ^= 1
@@ -625,6 +639,35 @@ class TrainStep:
             self.sync.eager_reduce()
             cap.g_opt.replay()
         return cap.losses[j], cap.taskss[j]
+
+    def _opt_hparams(self):
+        opt = self.opt
+        groups = list(getattr(opt, "param_groups", []))
+        inner = getattr(opt, "optim", None)  # ZeRO wrapper: the update runs in the inner optimizer
+        return tuple((g.get("lr"), tuple(g.get("betas", ())) if g.get("betas") is not None else None, g.get("eps"),
+                      g.get("weight_decay")) for g in groups + (list(inner.param_groups) if inner else []))
+
+    def _sync_opt_hparams(self, cap):
+        """Make a replayed step see the optimizer's CURRENT hyper-parameters (a captured step
+        never runs the optimizer's host code).  The learning rate of FusedAdamW lives in a
+        device scalar and is refreshed here; for any other optimizer, or any other changed
+        hyper-parameter, returns False (the bucket is recaptured).  Without this an lr schedule
+        such as ReduceLROnPlateau never reached captured training (the CI PNAEq conv-head run
+        kept its initial lr 0.02 after the plateau cut it and ended in a bad basin)."""
+        opt = self.opt
+        inner = getattr(opt, "optim", None)
+        if inner is not None and getattr(opt, "param_groups", None):
+            for g in inner.param_groups:  # ZeRO wrapper: its step() forwards lr, replays do not
+                g["lr"] = opt.param_groups[0]["lr"]
+        now = self._opt_hparams()
+        if cap.hparams is None or now == cap.hparams:
+            return True
+        target = inner if inner is not None else opt
+        lr_only = [a[1:] for a in now] == [b[1:] for b in cap.hparams]
+        if lr_only and hasattr(target, "sync_hparams") and target.sync_hparams():
+            cap.hparams = now
+            return True
+        return False
 
     def _graph_collectives(self):
         """Collectives can live inside the captured graph only on RCCL ("nccl")."""

@@ -134,3 +134,34 @@ def test_deferred_wgrad_grads_match_per_linear():
     assert grads[0].keys() == grads[1].keys()
     for n in grads[0]:
         torch.testing.assert_close(grads[1][n], grads[0][n], rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_graph_step_follows_lr_changes():
+    """A captured step never runs the optimizer's host code: an lr change made through
+    param_groups (ReduceLROnPlateau, manual schedules) must still reach the replayed update.
+    lr = 0 freezes the parameters (AdamW: p -= lr * (wd p + m / (sqrt(v) + eps))); lr back
+    to 1e-3 moves them again, bitwise as an eager step from the same state would."""
+    from hydragnn_amd.optim.adamw import FusedAdamW
+
+    samples = oc20_like(16, seed=6)
+    m = _model(samples).cuda()
+    s = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
+    opt = FusedAdamW(m.parameters(), lr=1e-3)
+    step = TrainStep(m, mode="graph", optimizer=opt, node_bucket=2048, edge_bucket=1 << 15)
+    idx = list(range(8))
+    step(s, idx)
+    step(s, idx)
+    torch.cuda.synchronize()
+    for g in opt.param_groups:
+        g["lr"] = 0.0
+    before = [p.detach().clone() for p in m.parameters()]
+    step(s, idx)
+    step(s, idx)
+    torch.cuda.synchronize()
+    for a, b in zip(m.parameters(), before):
+        assert torch.equal(a, b), "lr = 0 still moved a parameter in the replayed step"
+    for g in opt.param_groups:
+        g["lr"] = 1e-3
+    step(s, idx)
+    torch.cuda.synchronize()
+    assert any(not torch.equal(a, b) for a, b in zip(m.parameters(), before)), "lr restored but nothing moved"

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 iteration on one MI355X: kernel tests of the parts being changed, the headline
+# Iteration on one MI355X: kernel tests of the parts being changed, the headline
 # bench, and a marked per-step kernel trace (summary + one step's timeline).
-#   TESTS="tests/a.py tests/b.py" BENCH_ARGS="--precision bf16" bash tools/gpu_r4_iter.sh [tag]
+#   TESTS="tests/a.py tests/b.py" BENCH_ARGS="--precision bf16" bash tools/gpu_iter.sh [tag]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
