@@ -1719,8 +1719,24 @@ at::Tensor gf_embed_fwd(const at::Tensor& A_, const at::Tensor& B_, const at::Te
 // wp: 7 tensors per layer (dWab, dWr, dWd, dbc, W_pre, encW, encb); em: 5 per embedding
 // (Ta, Tb, Wa, Wb, Wl).  Returns per layer [dW_pre, db_pre, dencW, dencb], then per embedding
 // [dWa, dWb, dWl], then dfreq (when dfw is given).
+// Parameter-gradient outputs: the caller's tensors (e.g. the training step's flat gradient
+// slots, parallel/gradslots.py) when given, else fresh ones.  outs, when present, holds one
+// contiguous fp32 tensor per gradient output of the op, in output order.
+static at::Tensor gout_or(const c10::optional<at::TensorList>& outs, size_t i, size_t n_expected,
+                          at::IntArrayRef shape, const at::TensorOptions& opt) {
+  if (!outs.has_value()) return at::empty(shape, opt);
+  HY_CHECK(outs->size() == n_expected, "gradient outputs: one tensor per parameter gradient");
+  const at::Tensor& t = (*outs)[i];
+  int64_t n = 1;
+  for (auto d : shape) n *= d;
+  HY_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n,
+           "gradient outputs: contiguous fp32 tensors of the parameters' sizes");
+  return t.view(shape);
+}
+
 std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::vector<at::Tensor>& em,
-                                  const c10::optional<at::Tensor>& dfw) {
+                                  const c10::optional<at::Tensor>& dfw,
+                                  c10::optional<at::TensorList> gouts) {
   HY_CHECK(wp.size() % 7 == 0 && wp.size() / 7 <= (size_t)kFinMaxL && em.size() % 5 == 0 && em.size() <= 10,
            "gf_finish: 7 tensors per layer (<= 8 layers), 5 per embedding (<= 2)");
   Finish a{};
@@ -1739,7 +1755,9 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
                  t[4].size(0) == F && t[4].size(1) == 3 * F && t[5].size(0) == F && t[5].size(1) == F + a.d &&
                  t[6].numel() == F,
              "gf_finish: weight-prep shapes");
-    auto dW = at::empty_like(t[4]), db = at::empty({F}, opt), dencW = at::empty_like(t[5]), dencb = at::empty({F}, opt);
+    const size_t ng = 4 * (wp.size() / 7) + 3 * (em.size() / 5) + ((dfw.has_value() && dfw->defined()) ? 1 : 0);
+    auto dW = gout_or(gouts, 4 * l, ng, t[4].sizes(), opt), db = gout_or(gouts, 4 * l + 1, ng, {F}, opt);
+    auto dencW = gout_or(gouts, 4 * l + 2, ng, t[5].sizes(), opt), dencb = gout_or(gouts, 4 * l + 3, ng, {F}, opt);
     a.wp[l] = FinWprep{t[0].data_ptr<float>(), t[1].data_ptr<float>(), t[2].data_ptr<float>(), t[3].data_ptr<float>(),
                        t[4].data_ptr<float>(), t[5].data_ptr<float>(), t[6].data_ptr<float>(), dW.data_ptr<float>(),
                        db.data_ptr<float>(), dencW.data_ptr<float>(), dencb.data_ptr<float>()};
@@ -1755,7 +1773,10 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
     HY_CHECK(t[0].numel() == F * ka && t[1].numel() == F * kb && t[2].size(0) == F && t[3].size(0) == F &&
                  t[4].size(0) == F && t[4].size(1) == 2 * F,
              "gf_finish: embedding shapes");
-    auto dWa = at::empty_like(t[2]), dWb = at::empty_like(t[3]), dWl = at::empty_like(t[4]);
+    const size_t ng = 4 * (wp.size() / 7) + 3 * (em.size() / 5) + ((dfw.has_value() && dfw->defined()) ? 1 : 0);
+    const size_t g0 = 4 * a.L + 3 * m;
+    auto dWa = gout_or(gouts, g0, ng, t[2].sizes(), opt), dWb = gout_or(gouts, g0 + 1, ng, t[3].sizes(), opt);
+    auto dWl = gout_or(gouts, g0 + 2, ng, t[4].sizes(), opt);
     a.em[m] = FinEmb{t[0].data_ptr<float>(), t[1].data_ptr<float>(), t[2].data_ptr<float>(), t[3].data_ptr<float>(),
                      t[4].data_ptr<float>(), dWa.data_ptr<float>(), dWb.data_ptr<float>(), dWl.data_ptr<float>(),
                      (int)ka, (int)kb};
@@ -1767,7 +1788,8 @@ std::vector<at::Tensor> gf_finish(const std::vector<at::Tensor>& wp, const std::
   if (dfw.has_value() && dfw->defined()) {
     HY_CHECK(dfw->dim() == 2 && dfw->size(0) == dfw->size(1) && dfw->is_contiguous(), "gf_finish: dfw [K, K]");
     a.K = (int)dfw->size(0);
-    auto dfreq = at::empty({a.K}, opt);
+    const size_t ng = 4 * (size_t)a.L + 3 * (size_t)a.ne + 1;
+    auto dfreq = gout_or(gouts, ng - 1, ng, {a.K}, opt);
     a.dfw = dfw->data_ptr<float>();
     a.dfreq = dfreq.data_ptr<float>();
     HY_CHECK(a.K <= 256, "gf_finish: dfw [K, K] with K <= 256");
@@ -1812,13 +1834,15 @@ std::vector<at::Tensor> gf_mlp_bwd(const at::Tensor& g, const at::Tensor& z3, co
                                    const at::Tensor& saved, const at::Tensor& g3, const at::Tensor& g4, double eps3,
                                    double eps4, const at::Tensor& md, const at::Tensor& W2, const at::Tensor& W1,
                                    const at::Tensor& z1, const at::Tensor& z2, const c10::optional<at::Tensor>& rng,
-                                   int64_t salt2, int64_t salt3, double p, const c10::optional<at::Tensor>& nv) {
+                                   int64_t salt2, int64_t salt3, double p, const c10::optional<at::Tensor>& nv,
+                                   c10::optional<at::TensorList> gouts) {
   const int64_t N = z3.size(0), F = z3.size(1);
   chk(g, N, F, "g");
   chk(md, N, 2 * F, "md");
   auto o = z3.options();
   auto dg = at::empty({N, F}, o), dpre = at::empty({N, 2 * F}, o), dout = at::empty({N, F}, o);
-  auto dw3 = at::empty({F}, o), db3 = at::empty({F}, o), dw4 = at::empty({F}, o), db4 = at::empty({F}, o);
+  auto dw3 = gout_or(gouts, 0, 4, {F}, o), db3 = gout_or(gouts, 1, 4, {F}, o), dw4 = gout_or(gouts, 2, 4, {F}, o),
+       db4 = gout_or(gouts, 3, 4, {F}, o);
   MlpBwd a{};
   a.g = g.data_ptr<float>();
   a.z3 = z3.data_ptr<float>();
@@ -1850,13 +1874,13 @@ std::vector<at::Tensor> gf_mlp_bwd(const at::Tensor& g, const at::Tensor& z3, co
 std::vector<at::Tensor> gf_loc_bwd(const at::Tensor& dout, const at::Tensor& z1, const at::Tensor& acc,
                                    const at::Tensor& saved, const at::Tensor& gamma1, const at::Tensor& Wl,
                                    const at::Tensor& Wp, const c10::optional<at::Tensor>& rng, int64_t salt0, double p,
-                                   const c10::optional<at::Tensor>& nv) {
+                                   const c10::optional<at::Tensor>& nv, c10::optional<at::TensorList> gouts) {
   const int64_t N = z1.size(0), F = z1.size(1);
   chk(dout, N, F, "dout");
   chk(Wp, F, 17 * F, "Wpost");
   auto o = z1.options();
   auto dz1 = at::empty({N, F}, o), dq = at::empty({N, F}, o), dp = at::empty({N, F}, o),
-       dZ = at::empty({N, 17 * F}, o), dw1 = at::empty({F}, o), db1 = at::empty({F}, o);
+       dZ = at::empty({N, 17 * F}, o), dw1 = gout_or(gouts, 0, 2, {F}, o), db1 = gout_or(gouts, 1, 2, {F}, o);
   LocBwd a{dout.data_ptr<float>(), z1.data_ptr<float>(), site_ptr(acc, 4, (int)F), saved.data_ptr<float>(),
            gamma1.data_ptr<float>(), BNG{dw1.data_ptr<float>(), db1.data_ptr<float>()}, Wl.data_ptr<float>(),
            Wp.data_ptr<float>(), dz1.data_ptr<float>(), dq.data_ptr<float>(), dp.data_ptr<float>(),
@@ -1868,12 +1892,14 @@ std::vector<at::Tensor> gf_loc_bwd(const at::Tensor& dout, const at::Tensor& z1,
 std::vector<at::Tensor> gf_att_bwd(const at::Tensor& dout, const at::Tensor& z2, const at::Tensor& acc,
                                    const at::Tensor& saved, const at::Tensor& gamma2, const at::Tensor& Wo,
                                    const c10::optional<at::Tensor>& rng, int64_t salt1, double p,
-                                   const c10::optional<at::Tensor>& nv, const c10::optional<at::Tensor>& O) {
+                                   const c10::optional<at::Tensor>& nv, const c10::optional<at::Tensor>& O,
+                                   c10::optional<at::TensorList> gouts) {
   const int64_t N = z2.size(0), F = z2.size(1);
   chk(dout, N, F, "dout");
   auto o = z2.options();
   const bool packed = O.has_value() && O->defined();
-  auto dz2 = at::empty({N, F}, o), da = at::empty({N, F}, o), dw2 = at::empty({F}, o), db2 = at::empty({F}, o);
+  auto dz2 = at::empty({N, F}, o), da = at::empty({N, F}, o), dw2 = gout_or(gouts, 0, 2, {F}, o),
+       db2 = gout_or(gouts, 1, 2, {F}, o);
   auto dO = packed ? at::empty({0}, o) : at::empty({N, F}, o);
   AttBwd a{dout.data_ptr<float>(), z2.data_ptr<float>(), site_ptr(acc, 4, (int)F), saved.data_ptr<float>(),
            gamma2.data_ptr<float>(), BNG{dw2.data_ptr<float>(), db2.data_ptr<float>()}, Wo.data_ptr<float>(),
@@ -1955,7 +1981,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "Tensor(d!)? nbt3, Tensor(e!)? rm4, Tensor(f!)? rv4, Tensor(g!)? nbt4, float mom3, float eps3, float mom4, "
       "float eps4, Tensor? nv, Tensor? gptr) -> Tensor[]");
   m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor");
-  m.def("gf_finish(Tensor[] wp, Tensor[] em, Tensor? dfw) -> Tensor[]");
+  m.def("gf_finish(Tensor[] wp, Tensor[] em, Tensor? dfw, Tensor[]? gouts=None) -> Tensor[]");
   m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
   m.def("gf_edge_fwd_multi(Tensor[] r, Tensor e, Tensor[] Wr, Tensor[] Wd, Tensor[] bc) -> Tensor[]");
   m.def(
@@ -1966,14 +1992,14 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "Tensor? gidx, Tensor? gptr) -> Tensor");
   m.def(
       "gf_mlp_bwd(Tensor g, Tensor z3, Tensor(a!) acc, Tensor saved, Tensor g3, Tensor g4, float eps3, float eps4, "
-      "Tensor md, Tensor W2, Tensor W1, Tensor z1, Tensor z2, Tensor? rng, int salt2, int salt3, float p, Tensor? nv) "
-      "-> Tensor[]");
+      "Tensor md, Tensor W2, Tensor W1, Tensor z1, Tensor z2, Tensor? rng, int salt2, int salt3, float p, Tensor? nv, "
+      "Tensor[]? gouts=None) -> Tensor[]");
   m.def(
       "gf_loc_bwd(Tensor dout, Tensor z1, Tensor acc, Tensor saved, Tensor gamma1, Tensor Wl, Tensor Wp, Tensor? rng, "
-      "int salt0, float p, Tensor? nv) -> Tensor[]");
+      "int salt0, float p, Tensor? nv, Tensor[]? gouts=None) -> Tensor[]");
   m.def(
       "gf_att_bwd(Tensor dout, Tensor z2, Tensor acc, Tensor saved, Tensor gamma2, Tensor Wo, Tensor? rng, int salt1, "
-      "float p, Tensor? nv, Tensor? O=None) -> Tensor[]");
+      "float p, Tensor? nv, Tensor? O=None, Tensor[]? gouts=None) -> Tensor[]");
   m.def(
       "gf_node_bwd(Tensor dAB, Tensor dqkv, Tensor Wab, Tensor Win, Tensor dZ, Tensor dz1, Tensor dz2, Tensor x, "
       "Tensor? z3p, Tensor? savedp, Tensor(a!)? accp, Tensor? nv) -> Tensor");

@@ -767,6 +767,162 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_fused_kernel(const float
 // the global loss lv: the workgroups seed d / n and the reducer rescales dW, db and dx by 1/lv.
 constexpr int kHlRows = 16;
 
+// The row-split kernel is ONE compact instantiation for every layer count: its layer loops
+// are rolled and read their widths / LDS offsets from a table built in LDS at entry.  The
+// per-NL unrolled form was ~36 KB of straight-line code executed once per launch by 3
+// workgroups: every layer paid its instruction-cache misses (~1.8k cycles per layer even at
+// K = 8, tools/bench_head_loss.py --stamps), which was most of the kernel's 32 us.
+// LDS layout: every matrix is [rows][r32(cols) + 4] with rows of W / b padded to r32(O) and
+// zero padding, so the 8-deep operand groups of hl_dotp read unconditionally (no per-step
+// bounds branches) and the +4 row stride spreads a 16 x 4-lane tile read over distinct banks.
+__device__ __host__ __forceinline__ int hl_r32(int v) { return (v + 31) / 32 * 32; }
+__device__ __host__ __forceinline__ int hl_ldp(int cols) { return hl_r32(cols) + 4; }
+
+struct HlTab {
+  int n, Gp, ldy, x, dy, dy2, tg, mk, total;
+  int dims[kMlpMaxLayers + 1];
+  int relu[kMlpMaxLayers];
+  int goff[kMlpMaxLayers + 1];
+  int w[kMlpMaxLayers], b[kMlpMaxLayers], act[kMlpMaxLayers];
+  const float* W[kMlpMaxLayers];
+  const float* bias[kMlpMaxLayers];
+  // LDS copy jobs (hl_jobs): W_0..W_{n-1}, b_0..b_{n-1}, the x rows, the target rows.  Rows
+  // of a job past its source rows, and columns past its width, are zero padding.  Row jobs
+  // (x, target) start at the workgroup's first row and hold its Gl rows (pr < 0: pr = Gl).
+  int njobs;
+  const float* jsrc[2 * kMlpMaxLayers + 2];
+  int jnr[2 * kMlpMaxLayers + 2], jpr[2 * kMlpMaxLayers + 2], jw[2 * kMlpMaxLayers + 2];
+  int jsld[2 * kMlpMaxLayers + 2], jdst[2 * kMlpMaxLayers + 2], jdld[2 * kMlpMaxLayers + 2];
+  int jzw[2 * kMlpMaxLayers + 2], jrow[2 * kMlpMaxLayers + 2];
+  // destinations of the reduced gradients: dW_l at gout[2l], db_l at gout[2l + 1]
+  float* gout[2 * kMlpMaxLayers];
+};
+
+// host: the copy-job table of a launch over x [G, D0] / target [G, Do]
+inline void hl_jobs(HlTab& T, const float* x, const float* target) {
+  const int n = T.n;
+  int j = 0;
+  auto job = [&](const float* src, int nr, int pr, int w, int sld, int dst, int dld, int zw, int row) {
+    T.jsrc[j] = src;
+    T.jnr[j] = nr;
+    T.jpr[j] = pr;
+    T.jw[j] = w;
+    T.jsld[j] = sld;
+    T.jdst[j] = dst;
+    T.jdld[j] = dld;
+    T.jzw[j] = zw;
+    T.jrow[j] = row;
+    ++j;
+  };
+  for (int l = 0; l < n; ++l)
+    job(T.W[l], T.dims[l + 1], hl_r32(T.dims[l + 1]), T.dims[l], T.dims[l], T.w[l], hl_ldp(T.dims[l]),
+        hl_ldp(T.dims[l]), 0);
+  for (int l = 0; l < n; ++l) job(T.bias[l], 1, 1, T.dims[l + 1], 0, T.b[l], 0, hl_r32(T.dims[l + 1]), 0);
+  job(x, 0, T.Gp, T.dims[0], T.dims[0], T.x, hl_ldp(T.dims[0]), hl_ldp(T.dims[0]), 1);
+  job(target, 0, -1, T.dims[n], T.dims[n], T.tg, T.dims[n], T.dims[n], 1);
+  T.njobs = j;
+  while (j < 2 * kMlpMaxLayers + 2) job(nullptr, 0, 0, 0, 0, 0, 0, 0, 0);
+}
+
+__device__ __host__ inline void hl_tab_fill(HlTab& T, const MlpArgs& a, int G) {
+  const int n = a.n;
+  T.n = n;
+  T.Gp = hl_r16(G);
+  int o = 0, mw = a.dims[0];
+  for (int l = 0; l <= n; ++l) {
+    T.dims[l] = a.dims[l];
+    T.goff[l] = a.goff[l];
+  }
+  for (int l = 0; l < n; ++l) {
+    T.relu[l] = a.relu[l];
+    T.W[l] = a.W[l];
+    T.bias[l] = a.b[l];
+    T.w[l] = o;
+    o += hl_r32(a.dims[l + 1]) * hl_ldp(a.dims[l]);
+    mw = a.dims[l + 1] > mw ? a.dims[l + 1] : mw;
+  }
+  for (int l = 0; l < n; ++l) {
+    T.b[l] = o;
+    o += hl_r32(a.dims[l + 1]);
+  }
+  T.x = o;
+  o += T.Gp * hl_ldp(a.dims[0]);
+  for (int l = 0; l < n; ++l) {
+    T.act[l] = o;
+    o += T.Gp * hl_ldp(a.dims[l + 1]);
+  }
+  T.ldy = hl_ldp(mw);
+  T.dy = o;
+  o += T.Gp * T.ldy;
+  T.dy2 = o;
+  o += T.Gp * T.ldy;
+  T.tg = o;
+  o += G * a.dims[n];
+  T.mk = o;
+  o += T.Gp;
+  T.total = (o + 3) & ~3;  // whole float4s (the zero fill)
+}
+
+__device__ __forceinline__ int hl_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int hl_rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float* hl_rlp(const float* p, int l) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return (float*)(((uint64_t)hi << 32) | lo);
+}
+
+// 16 x 16 tile product over K4 k-steps (K4 a multiple of 8, <= 32, operands zero-padded):
+// the operands of 16 steps are read from LDS before their MFMAs (one LDS latency per 64-deep
+// slice, not one per 8 steps)
+__device__ __forceinline__ f4v_hl hl_tile(const float* ap, int sa, const float* bp, int sb, int K4) {
+  f4v_hl a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  for (int k = 0; k < K4; k += 16) {
+    const bool two = k + 8 < K4;
+    float x[16], y[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = ap[(k + j) * sa];
+      y[j] = bp[(k + j) * sb];
+    }
+    if (two) {
+#pragma unroll
+      for (int j = 8; j < 16; ++j) {
+        x[j] = ap[(k + j) * sa];
+        y[j] = bp[(k + j) * sb];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      a0 = hl_mfma(x[j], y[j], a0);
+      a1 = hl_mfma(x[j + 1], y[j + 1], a1);
+    }
+    if (two) {
+#pragma unroll
+      for (int j = 8; j < 16; j += 2) {
+        a0 = hl_mfma(x[j], y[j], a0);
+        a1 = hl_mfma(x[j + 1], y[j + 1], a1);
+      }
+    }
+  }
+  return a0 + a1;
+}
+
+// 16 x 16 tile over exactly 4 k-steps (the weight gradients: K = the 16 rows of a block)
+__device__ __forceinline__ f4v_hl hl_tile4(const float* ap, int sa, const float* bp, int sb) {
+  float x[4], y[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[j] = ap[j * sa];
+    y[j] = bp[j * sb];
+  }
+  f4v_hl a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  a0 = hl_mfma(x[0], y[0], a0);
+  a1 = hl_mfma(x[1], y[1], a1);
+  a0 = hl_mfma(x[2], y[2], a0);
+  a1 = hl_mfma(x[3], y[3], a1);
+  return a0 + a1;
+}
+
 __device__ __forceinline__ bool hl_arrive(int* counter, int expected) {
   __shared__ int flag;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -787,39 +943,205 @@ __device__ __forceinline__ bool hl_arrive(int* counter, int expected) {
   return true;
 }
 
-template <int NL>
 __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
-    const float* __restrict__ x, int G, MlpArgs a, const float* __restrict__ target, const bool* __restrict__ mask,
-    int kind, float* __restrict__ out, float* __restrict__ pred, float* __restrict__ grads, float* __restrict__ dx,
-    float* __restrict__ part, double* __restrict__ lpart, int* __restrict__ cnt, long long* dbg) {
+    const float* __restrict__ x, int G, const HlTab tab, const float* __restrict__ target,
+    const bool* __restrict__ mask, int kind, float* __restrict__ out, float* __restrict__ pred,
+    float* __restrict__ grads, float* __restrict__ dx, float* __restrict__ part, double* __restrict__ lpart,
+    int* __restrict__ cnt, long long* dbg, int full) {
+  // full = 0: the input-gradient chain only (dx; the training step's critical path, see
+  // ops/mlp.py): no predictions, loss, weight gradients or cross-workgroup reduction.
+  // full = 1 with dx == null: everything but dx (the side-stream twin of a full = 0 launch)
   hl_stamp(dbg, 0);
   extern __shared__ float sm[];
+  __shared__ double redk[kHlWaves], redl[kHlWaves];
   const int R = gridDim.x, b = blockIdx.x, row0 = b * kHlRows, Gl = min(kHlRows, G - row0);
-  const int Do = a.dims[NL], D0 = a.dims[0], nw = a.goff[NL];
-  const HlLayout L = hl_layout<NL>(a, Gl);
-  // kept elements of the whole batch (loads issued ahead of the staging wait)
-  double kc = 0.0;
-  for (int r = threadIdx.x; r < G; r += kHlThreads) kc += (mask == nullptr || mask[r]) ? (double)Do : 0.0;
-  hl_stamp(dbg, 1);
-  hl_stage<NL>(a, L, x + (int64_t)row0 * D0, nullptr, target + (int64_t)row0 * Do,
-               mask == nullptr ? nullptr : mask + row0, Gl, sm);
-  hl_stamp(dbg, 2);
-  hl_chain<NL>(a, L, Gl, sm, nullptr, dbg);
-  const float* P = sm + L.act[NL - 1];
-  const int ldo = hl_ld(Do);
-  double ls = 0.0;
-  for (int idx = threadIdx.x; idx < Gl * Do; idx += kHlThreads) {
-    const int r = idx / Do, o = idx % Do;
-    const float p = P[r * ldo + o];
-    pred[(int64_t)row0 * Do + idx] = p;
-    if (sm[L.mk + r] != 0.f) ls += (double)loss_term_hl(kind, p - sm[L.tg + idx]);
+  const int tid = threadIdx.x, wv = hl_u(tid >> 6), lane = tid & 63, li = lane & 15, lg = lane >> 4;
+  const int n = tab.n, Gp = tab.Gp, D0 = tab.dims[0], nw = tab.goff[n];
+  // per-layer parameters held lane-indexed (lane l: layer l), broadcast with v_readlane
+  const int ll = min(lane, kMlpMaxLayers - 1);
+  const int v_dims = tab.dims[min(lane, kMlpMaxLayers)], v_goff = tab.goff[min(lane, kMlpMaxLayers)];
+  const int v_relu = tab.relu[ll], v_w = tab.w[ll], v_b = tab.b[ll], v_act = tab.act[ll];
+  float* const v_gout = tab.gout[min(lane, 2 * kMlpMaxLayers - 1)];
+  const int Do = hl_rl(v_dims, n);
+  // lane j: copy job j's parameters; with the row mask these are the only loads ahead of the
+  // copies (all issued together: one memory round trip), consumed before any copy is issued
+  // (a wait on them after the copies would also wait for every copy)
+  const int jl = min(lane, 2 * kMlpMaxLayers + 1);
+  const float* j_src = tab.jsrc[jl];
+  const int j_nr = tab.jnr[jl], j_pr = tab.jpr[jl], j_w = tab.jw[jl], j_sld = tab.jsld[jl], j_dst = tab.jdst[jl];
+  const int j_dld = tab.jdld[jl], j_zw = tab.jzw[jl], j_row = tab.jrow[jl];
+  double kr = 0.0;
+  for (int r = tid; r < G; r += kHlThreads) kr += (mask == nullptr || mask[r]) ? 1.0 : 0.0;
+  if (tid < Gp) sm[tab.mk + tid] = (tid < Gl && (mask == nullptr || mask[row0 + tid])) ? 1.f : 0.f;
+  for (int off = 32; off > 0; off >>= 1) kr += __shfl_xor(kr, off);
+  if (lane == 0) redk[wv] = kr;
+  int base = 0;
+  const int nj = tab.njobs;
+  for (int j = 0; j < nj; ++j) {
+    const float* src = hl_rlp(j_src, j);
+    int nr = hl_rl(j_nr, j), pr = hl_rl(j_pr, j);
+    const int width = hl_rl(j_w, j), sld = hl_rl(j_sld, j);
+    const int dst = hl_rl(j_dst, j), dld = hl_rl(j_dld, j), zw = hl_rl(j_zw, j);
+    if (hl_rl(j_row, j)) {
+      src += (int64_t)row0 * sld;
+      nr = Gl;
+      if (pr < 0) pr = Gl;
+    }
+    for (int r = (wv - base % kHlWaves + kHlWaves) % kHlWaves; r < pr; r += kHlWaves) {
+      if (r < nr) {
+        for (int c0 = 0; c0 < width; c0 += 64)
+          if (c0 + lane < width)
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void*)(src + (int64_t)r * sld + c0 + lane),
+                (__attribute__((address_space(3))) void*)(sm + dst + r * dld + c0), 4, 0, 0);
+      }
+      for (int c = (r < nr ? width : 0) + lane; c < zw; c += 64) sm[dst + r * dld + c] = 0.f;
+    }
+    base += pr;
   }
-  const double2 tot = hl_block_sum2(ls, kc);
+  // activations, dY buffers: plain zero fill (disjoint from every copy)
+  for (int e = tab.act[0] + 4 * tid; e < tab.tg; e += 4 * kHlThreads)
+    *reinterpret_cast<float4*>(sm + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+  hl_stamp(dbg, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  hl_sync();
+  hl_stamp(dbg, 2);
+  double kept = 0.0;
+#pragma unroll
+  for (int k = 0; k < kHlWaves; ++k) kept += redk[k];
+  kept *= (double)Do;
+  // forward chain: A_l = act(A_{l-1} W_l^T + b_l), 16 x 16 output tiles per wave
+  for (int l = 0; l < n; ++l) {
+    const int I = hl_rl(v_dims, l), O = hl_rl(v_dims, l + 1);
+    const float* in = sm + (l == 0 ? tab.x : hl_rl(v_act, l > 0 ? l - 1 : 0));
+    const float* W = sm + hl_rl(v_w, l);
+    const float* bb = sm + hl_rl(v_b, l);
+    float* outp = sm + hl_rl(v_act, l);
+    const bool rl = hl_rl(v_relu, l) != 0;
+    const int ldi = hl_ldp(I), ldo = hl_ldp(O), ct = hl_r16(O) / 16, tiles = (Gp / 16) * ct, K4 = hl_r32(I) / 4;
+    for (int t = wv; t < tiles; t += kHlWaves) {
+      const int r0 = (t / ct) * 16, c0 = (t % ct) * 16;
+      const f4v_hl acc = hl_tile(in + (r0 + li) * ldi + lg, 4, W + (c0 + li) * ldi + lg, 4, K4);
+      const int col = c0 + li;
+      const float bias = bb[col];  // zero past O
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 4 * lg + r;
+        float v = acc[r] + bias;
+        if (rl) v = fmaxf(v, 0.f);
+        outp[row * ldo + col] = (row < Gl && col < O) ? v : 0.f;
+      }
+    }
+    hl_sync();
+    hl_stamp(dbg, 3 + l);
+  }
+  // predictions, the loss partial and the loss gradient in one pass (the normalisation is the
+  // batch's kept count, known to every workgroup; RMSE's 1 / lv is applied by the reducer)
+  const int ldy = tab.ldy;
+  float* DY = sm + tab.dy;
+  float* DY2 = sm + tab.dy2;
+  {
+    const float* P = sm + hl_rl(v_act, n - 1);
+    const float* TG = sm + tab.tg;
+    const float* MKp = sm + tab.mk;
+    const int ldP = hl_ldp(Do);
+    const bool rl = hl_rl(v_relu, n - 1) != 0;
+    const float den = kept > 0.0 ? (float)kept : 1.f;
+    double ls = 0.0;
+    for (int idx = tid; idx < Gl * Do; idx += kHlThreads) {
+      const int r = idx / Do, o = idx % Do;
+      const float p = P[r * ldP + o];
+      if (full) pred[(int64_t)row0 * Do + idx] = p;
+      float v = 0.f;
+      if (MKp[r] != 0.f) {
+        const float d = p - TG[idx];
+        ls += (double)loss_term_hl(kind, d);
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        switch (kind) {
+          case 1: v = sgn / den; break;
+          case 3: v = (fabsf(d) < 1.f ? d : sgn) / den; break;
+          case 2: v = d / den; break;
+          default: v = 2.f * d / den; break;
+        }
+      }
+      DY[r * ldy + o] = (rl && p <= 0.f) ? 0.f : v;
+    }
+    for (int off = 32; off > 0; off >>= 1) ls += __shfl_xor(ls, off);
+    if (lane == 0) redl[wv] = ls;
+  }
+  hl_sync();
   hl_stamp(dbg, 19);
-  // lv = 1: RMSE's 1 / lv is applied by the reducer
-  hl_backward<NL>(a, L, Gl, sm, target, mask, kind, 1.f, 1.f, (float)tot.y, part + (int64_t)b * nw,
-                  dx + (int64_t)row0 * D0, dbg);
-  if (threadIdx.x == 0) lpart[b] = tot.x;
+  // backward, per layer in reverse: DY' = (DY W) * relu'(A_in) on waves 0..nx-1 (the chain),
+  // while the other waves form dW = DY^T A_in (K = the block's rows) and db = sum_r DY
+  float* pb = part + (int64_t)b * nw;
+  float* dxb = dx + (int64_t)row0 * D0;
+  for (int l = n - 1; l >= 0; --l) {
+    const int I = hl_rl(v_dims, l), O = hl_rl(v_dims, l + 1);
+    const float* ain = sm + (l == 0 ? tab.x : hl_rl(v_act, l > 0 ? l - 1 : 0));
+    const float* W = sm + hl_rl(v_w, l);
+    float* gl = pb + hl_rl(v_goff, l);
+    const int lda = hl_ldp(I), ti = hl_r16(I) / 16, to = hl_r16(O) / 16, nx = (Gp / 16) * ti;
+    const int w0 = nx < kHlWaves - 2 ? nx : 0, nd = kHlWaves - w0;
+    if (full && wv >= w0) {
+      for (int t = wv - w0; t < to * ti; t += nd) {
+        const int o0 = (t / ti) * 16, i0 = (t % ti) * 16;
+        f4v_hl acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < Gp; k0 += 16) {
+          const f4v_hl p4 = hl_tile4(DY + (k0 + lg) * ldy + o0 + li, 4 * ldy, ain + (k0 + lg) * lda + i0 + li, 4 * lda);
+          acc += p4;
+        }
+        const int i = i0 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int o = o0 + 4 * lg + r;
+          if (o < O && i < I) gl[o * I + i] = acc[r];
+        }
+      }
+    }
+    {
+      const int c = tid - (kHlThreads - 128);  // the last two waves
+      for (int o = c; full && o >= 0 && o < O; o += 128) {
+        float v = 0.f;
+        for (int r = 0; r < Gl; ++r) v += DY[r * ldy + o];
+        gl[O * I + o] = v;
+      }
+    }
+    const bool msk = l > 0 && hl_rl(v_relu, l > 0 ? l - 1 : 0) != 0;
+    const int K4 = hl_r32(O) / 4, i32 = hl_r32(I);
+    for (int t = wv; t < nx; t += kHlWaves) {
+      const int r0 = (t / ti) * 16, i0 = (t % ti) * 16;
+      const f4v_hl acc = hl_tile(DY + (r0 + li) * ldy + lg, 4, W + lg * lda + i0 + li, 4 * lda, K4);
+      const int col = i0 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + 4 * lg + r;
+        float v = acc[r];
+        if (msk && !(ain[row * lda + col] > 0.f)) v = 0.f;
+        const bool live = row < Gl && col < I;
+        if (l == 0) {
+          if (live && dx != nullptr) dxb[row * I + col] = v;
+        } else {
+          DY2[row * ldy + col] = live ? v : 0.f;
+          // columns [r16(I), r32(I)) of DY' are read (as zeros) by the next layer's tiles
+          if (col + 16 >= ti * 16 && col + 16 < i32) DY2[row * ldy + col + 16] = 0.f;
+        }
+      }
+    }
+    hl_sync();
+    hl_stamp(dbg, 20 + l);
+    float* sw = DY;
+    DY = DY2;
+    DY2 = sw;
+  }
+  if (!full) return;
+  double2 tot;
+  {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < kHlWaves; ++k) t += redl[k];
+    tot = make_double2(t, kept);
+  }
+  if (tid == 0) lpart[b] = tot.x;
   if (!hl_arrive(cnt, R)) return;
   __shared__ float scale_s;
   if (threadIdx.x == 0) {
@@ -855,10 +1177,16 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = e0 + u * kHlThreads;
-      if (e < nw) grads[e] = v[u] * sc;
+      float* dst = nullptr;
+      for (int l = 0; l < n; ++l) {  // element e of the gradient image -> its tensor
+        const int g0 = hl_rl(v_goff, l), oi = hl_rl(v_dims, l) * hl_rl(v_dims, l + 1);
+        if (e >= g0 && e < hl_rl(v_goff, l + 1))
+          dst = e < g0 + oi ? hl_rlp(v_gout, 2 * l) + (e - g0) : hl_rlp(v_gout, 2 * l + 1) + (e - g0 - oi);
+      }
+      if (dst != nullptr) *dst = v[u] * sc;
     }
   }
-  if (kind == 2)
+  if (kind == 2 && dx != nullptr)
     for (int e = threadIdx.x; e < G * D0; e += kHlThreads) dx[e] *= sc;
   hl_stamp(dbg, 31);
 }
@@ -893,8 +1221,6 @@ static void hl_attrs() {
                       (int)kHlMaxLds);
   hipFuncSetAttribute((const void*)head_loss_fused_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)kHlMaxLds);
-  hipFuncSetAttribute((const void*)head_loss_rows_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)kHlMaxLds);
 }
 
 static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::optional<at::Tensor>& mask,
@@ -916,6 +1242,8 @@ static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::
     hl_attrs<6>();
     hl_attrs<7>();
     hl_attrs<8>();
+    hipFuncSetAttribute((const void*)head_loss_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)kHlMaxLds);
     return true;
   }();
   (void)once;
@@ -979,12 +1307,37 @@ std::vector<at::Tensor> head_loss_bwd(const at::Tensor& gout, const at::Tensor& 
   return out;
 }
 
+// the ticket counter of head_loss_rows_kernel: persistent per (device, stream) — launches on
+// one stream never overlap, and the reducer resets it to zero (an at::zeros per call was a
+// fill launch on the step's critical path)
+static at::Tensor hl_counter(const at::Tensor& like) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> counters;
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair((int)like.get_device(), stream());
+  auto it = counters.find(key);
+  if (it == counters.end()) it = counters.emplace(key, at::zeros({1}, like.options().dtype(at::kInt))).first;
+  return it->second;
+}
+
+static bool hl_rows_split() {
+  // row-split launch (head_loss_rows_kernel); HYDRA_HEADLOSS_ROWS=0: the one-workgroup kernel
+  static const bool on = [] {
+    const char* e = std::getenv("HYDRA_HEADLOSS_ROWS");
+    return e == nullptr || std::string(e) != "0";
+  }();
+  return on;
+}
+
 // returns [stats [2], pred [G, out], dx, dW_0, db_0, dW_1, db_1, ...] (gradients of the loss
-// itself, upstream gradient 1)
+// itself, upstream gradient 1).  grads_out: optional fp32 buffer of the gradient image
+// (goff[n] elements, e.g. a slice of the step's flat gradient buffer) written in place;
+// want_dx = false: dx is not written (returned empty) — the twin of a head_loss_dx launch.
 std::vector<at::Tensor> head_loss_fused(const at::Tensor& x_, at::TensorList Ws_, at::TensorList bs_,
                                         at::IntArrayRef relu, const at::Tensor& target,
                                         const c10::optional<at::Tensor>& mask, int64_t kind,
-                                        const c10::optional<at::Tensor>& dbg) {
+                                        const c10::optional<at::Tensor>& dbg,
+                                        c10::optional<at::TensorList> grads_out, bool want_dx) {
   HY_CHECK_CUDA(x_);
   auto x = x_.contiguous();
   HY_CHECK_F32(x);
@@ -1001,55 +1354,102 @@ std::vector<at::Tensor> head_loss_fused(const at::Tensor& x_, at::TensorList Ws_
   const int64_t G = x.size(0);
   auto stats = at::empty({2}, x.options());
   auto pred = at::empty({G, a.dims[a.n]}, x.options());
-  auto flat = at::empty({a.goff[a.n]}, x.options());
-  auto dx = at::empty_like(x);
+  // gradient tensors: dW_0, db_0, dW_1, ... (caller-provided, e.g. the step's gradient slots, or
+  // views of one fresh buffer)
+  std::vector<at::Tensor> gts;
+  if (grads_out.has_value()) {
+    HY_CHECK((int)grads_out->size() == 2 * a.n, "head_loss_fused: grads_out holds dW_l, db_l for every layer");
+    for (int l = 0; l < a.n; ++l)
+      for (int k = 0; k < 2; ++k) {
+        const at::Tensor& t = (*grads_out)[2 * l + k];
+        const int64_t want = k == 0 ? (int64_t)a.dims[l + 1] * a.dims[l] : a.dims[l + 1];
+        HY_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == want &&
+                     t.get_device() == x.get_device(),
+                 "head_loss_fused: grads_out tensors must be contiguous fp32 shaped like the weights and biases");
+        gts.push_back(t);
+      }
+  } else {
+    auto flat = at::empty({a.goff[a.n]}, x.options());
+    for (int l = 0; l < a.n; ++l) {
+      const int O = a.dims[l + 1], I = a.dims[l];
+      gts.push_back(flat.narrow(0, a.goff[l], O * I).view({O, I}));
+      gts.push_back(flat.narrow(0, a.goff[l] + O * I, O));
+    }
+  }
+  auto dx = want_dx ? at::empty_like(x) : at::empty({0}, x.options());
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
-  // row-split launch (head_loss_rows_kernel); HYDRA_HEADLOSS_ROWS=0: the one-workgroup kernel
-  static const bool rows_split = [] {
-    const char* e = std::getenv("HYDRA_HEADLOSS_ROWS");
-    return e == nullptr || std::string(e) != "0";
-  }();
-  if (rows_split) {
+  HlTab tab;
+  hl_tab_fill(tab, a, (int)std::min<int64_t>(G, kHlRows));
+  hl_jobs(tab, x.data_ptr<float>(), target.data_ptr<float>());
+  for (int k = 0; k < 2 * a.n; ++k) tab.gout[k] = gts[k].data_ptr<float>();
+  if (hl_rows_split() && sizeof(float) * (size_t)tab.total <= kHlMaxLds) {
     const int R = (int)ceil_div(G, (int64_t)kHlRows);
-    const size_t lds = hl_lds(a, (int)std::min<int64_t>(G, kHlRows));
+    const size_t lds = sizeof(float) * (size_t)tab.total;
     auto part = at::empty({(int64_t)R * a.goff[a.n]}, x.options());
     auto lpart = at::empty({R}, x.options().dtype(at::kDouble));
-    // the ticket counter: persistent per (device, stream) — launches on one stream never
-    // overlap, and the reducer resets it to zero (an at::zeros here was a fill launch on the
-    // step's critical path)
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, at::Tensor> counters;
-    at::Tensor cnt;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto key = std::make_pair((int)x.get_device(), stream());
-      auto it = counters.find(key);
-      if (it == counters.end()) it = counters.emplace(key, at::zeros({1}, x.options().dtype(at::kInt))).first;
-      cnt = it->second;
-    }
-#define HL_ROWS(N)                                                                                              \
-  head_loss_rows_kernel<N><<<R, kHlThreads, lds, stream()>>>(                                                   \
-      x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),         \
-      pred.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(),             \
-      lpart.data_ptr<double>(), cnt.data_ptr<int>(), dp)
-    HL_NL_SWITCH(a.n, HL_ROWS)
-#undef HL_ROWS
+    auto cnt = hl_counter(x);
+    head_loss_rows_kernel<<<R, kHlThreads, lds, stream()>>>(
+        x.data_ptr<float>(), (int)G, tab, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),
+        pred.data_ptr<float>(), nullptr, want_dx ? dx.data_ptr<float>() : nullptr,
+        part.data_ptr<float>(), lpart.data_ptr<double>(), cnt.data_ptr<int>(), dp, 1);
   } else {
+    HY_CHECK(want_dx, "head_loss_fused: want_dx = false needs the row-split kernel");
     const size_t lds = hl_lds(a, (int)G);
+    auto flat = at::empty({a.goff[a.n]}, x.options());
 #define HL_FUSED(N)                                                                                            \
   head_loss_fused_kernel<N><<<1, kHlThreads, lds, stream()>>>(                                                 \
       x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(), mp, (int)kind, stats.data_ptr<float>(),        \
       pred.data_ptr<float>(), flat.data_ptr<float>(), dx.data_ptr<float>(), dp)
     HL_NL_SWITCH(a.n, HL_FUSED)
 #undef HL_FUSED
+    for (int l = 0; l < a.n; ++l) {
+      const int O = a.dims[l + 1], I = a.dims[l];
+      gts[2 * l].view(-1).copy_(flat.narrow(0, a.goff[l], O * I));
+      gts[2 * l + 1].view(-1).copy_(flat.narrow(0, a.goff[l] + O * I, O));
+    }
   }
   std::vector<at::Tensor> out{stats, pred, dx};
   for (int l = 0; l < a.n; ++l) {
     const int O = a.dims[l + 1], I = a.dims[l];
-    out.push_back(flat.narrow(0, a.goff[l], O * I).view({O, I}));
-    out.push_back(flat.narrow(0, a.goff[l] + O * I, O));
+    out.push_back(gts[2 * l].view({O, I}));
+    out.push_back(gts[2 * l + 1].view({O}));
   }
   return out;
+}
+
+// dx of the masked loss (upstream gradient 1) alone: the forward chain and the input-gradient
+// chain, nothing else (no predictions, loss value, weight gradients or cross-workgroup step).
+// Not for RMSE (its dx needs the batch loss).  Pairs with head_loss_fused(want_dx=false) on a
+// side stream.
+at::Tensor head_loss_dx(const at::Tensor& x_, at::TensorList Ws_, at::TensorList bs_, at::IntArrayRef relu,
+                        const at::Tensor& target, const c10::optional<at::Tensor>& mask, int64_t kind,
+                        const c10::optional<at::Tensor>& dbg) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK(x.dim() == 2, "head_loss: x must be [G, D]");
+  HY_CHECK(kind != 2, "head_loss_dx: RMSE's input gradient needs the batch loss (use head_loss_fused)");
+  std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
+  auto a = make_args(x, Ws, bs, relu.vec());
+  hl_checks(x, target, mask, a, kind);
+  long long* dp = nullptr;
+  if (dbg.has_value() && dbg->defined()) {
+    HY_CHECK(dbg->is_cuda() && dbg->scalar_type() == at::kLong && dbg->is_contiguous() && dbg->numel() >= 32,
+             "head_loss_dx: dbg must be int64 [>= 32]");
+    dp = (long long*)dbg->data_ptr<int64_t>();
+  }
+  const int64_t G = x.size(0);
+  auto dx = at::empty_like(x);
+  const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
+  HlTab tab;
+  hl_tab_fill(tab, a, (int)std::min<int64_t>(G, kHlRows));
+  hl_jobs(tab, x.data_ptr<float>(), target.data_ptr<float>());
+  HY_CHECK(sizeof(float) * (size_t)tab.total <= kHlMaxLds, "head_loss_dx: chain exceeds the LDS budget");
+  const int R = (int)ceil_div(G, (int64_t)kHlRows);
+  head_loss_rows_kernel<<<R, kHlThreads, sizeof(float) * (size_t)tab.total, stream()>>>(
+      x.data_ptr<float>(), (int)G, tab, target.data_ptr<float>(), mp, (int)kind, nullptr, nullptr, nullptr,
+      dx.data_ptr<float>(), nullptr, nullptr, nullptr, dp, 0);
+  return dx;
 }
 
 }  // namespace hy
@@ -1067,8 +1467,11 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "Tensor? mask, Tensor stats, int kind) -> Tensor[]");
   m.def(
       "head_loss_fused(Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, int kind, "
-      "Tensor? dbg=None) -> "
+      "Tensor? dbg=None, Tensor[]? grads_out=None, bool want_dx=True) -> "
       "Tensor[]");
+  m.def(
+      "head_loss_dx(Tensor x, Tensor[] Ws, Tensor[] bs, int[] relu, Tensor target, Tensor? mask, int kind, "
+      "Tensor? dbg=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
@@ -1077,4 +1480,5 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("head_loss_fwd", hy::head_loss_fwd);
   m.impl("head_loss_bwd", hy::head_loss_bwd);
   m.impl("head_loss_fused", hy::head_loss_fused);
+  m.impl("head_loss_dx", hy::head_loss_dx);
 }

@@ -96,19 +96,34 @@ __global__ void __launch_bounds__(256) pna_fwd_kernel(
     for (int i = 0; i < VEC; ++i) {
       s.v[i] = 0.f; s2.v[i] = 0.f; mn.v[i] = INFINITY; mx.v[i] = -INFINITY; imn[i] = -1; imx[i] = -1;
     }
-    for (int e = beg; e < end; ++e) {
-      const int j = src[e];
-      const Vec<VEC> b = ld<VEC>(AB + (int64_t)j * ldab + F + f0);
-      Vec<VEC> cc, g;
-      if (C) cc = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc.v[i] = 0.f; }
-      if (G) g = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g.v[i] = 1.f; }
+    // edges in batches of EB: every source index, then every gathered row of the batch, is in
+    // flight together (one edge at a time paid two dependent memory latencies per edge:
+    // src[e], then AB[src[e]]); the statistics still fold edge by edge in CSR order
+    constexpr int EB = VEC == 1 ? 8 : 4;
+    for (int e0 = beg; e0 < end; e0 += EB) {
+      int js[EB];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        const float m = (a.v[i] + b.v[i] + cc.v[i]) * g.v[i];
-        s.v[i] += m;
-        s2.v[i] = add_sq_nofma(s2.v[i], m);  // no FMA: see the variance note below
-        if (m < mn.v[i]) { mn.v[i] = m; imn[i] = e; }
-        if (m > mx.v[i]) { mx.v[i] = m; imx[i] = e; }
+      for (int k = 0; k < EB; ++k) js[k] = src[min(e0 + k, end - 1)];
+      Vec<VEC> b[EB], cc[EB], g[EB];
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int e = min(e0 + k, end - 1);
+        b[k] = ld<VEC>(AB + (int64_t)js[k] * ldab + F + f0);
+        if (C) cc[k] = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc[k].v[i] = 0.f; }
+        if (G) g[k] = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g[k].v[i] = 1.f; }
+      }
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int e = e0 + k;
+        if (e >= end) break;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float m = (a.v[i] + b[k].v[i] + cc[k].v[i]) * g[k].v[i];
+          s.v[i] += m;
+          s2.v[i] = add_sq_nofma(s2.v[i], m);  // no FMA: see the variance note below
+          if (m < mn.v[i]) { mn.v[i] = m; imn[i] = e; }
+          if (m > mx.v[i]) { mx.v[i] = m; imx[i] = e; }
+        }
       }
     }
     // var = E[m^2] - E[m]^2 exactly as PyG's StdAggregation evaluates it (rounded products,
@@ -204,26 +219,39 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
     Vec<VEC> da;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) da.v[i] = 0.f;
-    for (int e = beg; e < end; ++e) {
-      const int j = src[e];
-      const Vec<VEC> b = ld<VEC>(AB + (int64_t)j * ldab + F + f0);
-      Vec<VEC> cc, g;
-      if (C) cc = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc.v[i] = 0.f; }
-      if (G) g = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g.v[i] = 1.f; }
-      Vec<VEC> dp, dg;
+    // edge batches as in the forward: gathers of a batch in flight together
+    constexpr int EB = VEC == 1 ? 8 : 4;
+    for (int e0 = beg; e0 < end; e0 += EB) {
+      int js[EB];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        const float pre = a.v[i] + b.v[i] + cc.v[i];
-        const float m = pre * g.v[i];
-        float dm = dmean.v[i] + (m - mean.v[i]) * kstd.v[i];
-        if (e == imn[i]) dm += dmin.v[i];
-        if (e == imx[i]) dm += dmax.v[i];
-        dp.v[i] = dm * g.v[i];
-        dg.v[i] = dm * pre;
-        da.v[i] += dp.v[i];
+      for (int k = 0; k < EB; ++k) js[k] = src[min(e0 + k, end - 1)];
+      Vec<VEC> b[EB], cc[EB], g[EB];
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int e = min(e0 + k, end - 1);
+        b[k] = ld<VEC>(AB + (int64_t)js[k] * ldab + F + f0);
+        if (C) cc[k] = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc[k].v[i] = 0.f; }
+        if (G) g[k] = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g[k].v[i] = 1.f; }
       }
-      st<VEC>(dpre + (int64_t)e * F + f0, dp);
-      if (dG) st<VEC>(dG + (int64_t)e * F + f0, dg);
+#pragma unroll
+      for (int k = 0; k < EB; ++k) {
+        const int e = e0 + k;
+        if (e >= end) break;
+        Vec<VEC> dp, dg;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float pre = a.v[i] + b[k].v[i] + cc[k].v[i];
+          const float m = pre * g[k].v[i];
+          float dm = dmean.v[i] + (m - mean.v[i]) * kstd.v[i];
+          if (e == imn[i]) dm += dmin.v[i];
+          if (e == imx[i]) dm += dmax.v[i];
+          dp.v[i] = dm * g[k].v[i];
+          dg.v[i] = dm * pre;
+          da.v[i] += dp.v[i];
+        }
+        st<VEC>(dpre + (int64_t)e * F + f0, dp);
+        if (dG) st<VEC>(dG + (int64_t)e * F + f0, dg);
+      }
     }
     st<VEC>(dA + (int64_t)n * ldda + f0, da);
   }

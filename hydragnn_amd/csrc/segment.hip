@@ -94,27 +94,38 @@ __global__ void __launch_bounds__(256) seg_sum_kernel(const float* __restrict__ 
   const float inv = MEAN ? 1.f / (float)max(end - beg, 1) : 1.f;
   for (int v = c; v < nv; v += tpr) {
     T a0 = V::zero(), a1 = V::zero();
-    int e = beg + k;
-    for (; e + KS < end; e += 2 * KS) {
-      const int r0 = perm ? perm[e] : e;
-      const int r1 = perm ? perm[e + KS] : e + KS;
-      if constexpr (GM) {
-        a0 = V::add(a0, vmul(reinterpret_cast<const T*>(w + (int64_t)r0 * F)[v],
-                             reinterpret_cast<const T*>(x + (int64_t)gidx[r0] * F)[v]));
-        a1 = V::add(a1, vmul(reinterpret_cast<const T*>(w + (int64_t)r1 * F)[v],
-                             reinterpret_cast<const T*>(x + (int64_t)gidx[r1] * F)[v]));
-      } else {
-        a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
-        a1 = V::add(a1, reinterpret_cast<const T*>(x + (int64_t)r1 * F)[v]);
+    // this stream's rows e = beg + k, + KS, ... alternate between a0 and a1; U row pairs per
+    // batch with every index load, then every row load, in flight together (one pair at a
+    // time paid the perm -> row dependent latency per pair).  Rows past the segment are
+    // clamped loads that are never added: the fold order is the pairwise one regardless.
+    constexpr int U = VEC == 4 ? 2 : 4;
+    for (int e = beg + k; e < end; e += 2 * KS * U) {
+      int i0[U], i1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ea = min(e + 2 * KS * u, end - 1), eb = min(e + 2 * KS * u + KS, end - 1);
+        i0[u] = perm ? perm[ea] : ea;
+        i1[u] = perm ? perm[eb] : eb;
       }
-    }
-    if (e < end) {
-      const int r0 = perm ? perm[e] : e;
-      if constexpr (GM)
-        a0 = V::add(a0, vmul(reinterpret_cast<const T*>(w + (int64_t)r0 * F)[v],
-                             reinterpret_cast<const T*>(x + (int64_t)gidx[r0] * F)[v]));
-      else
-        a0 = V::add(a0, reinterpret_cast<const T*>(x + (int64_t)r0 * F)[v]);
+      T x0[U], x1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (GM) {
+          x0[u] = vmul(reinterpret_cast<const T*>(w + (int64_t)i0[u] * F)[v],
+                       reinterpret_cast<const T*>(x + (int64_t)gidx[i0[u]] * F)[v]);
+          x1[u] = vmul(reinterpret_cast<const T*>(w + (int64_t)i1[u] * F)[v],
+                       reinterpret_cast<const T*>(x + (int64_t)gidx[i1[u]] * F)[v]);
+        } else {
+          x0[u] = reinterpret_cast<const T*>(x + (int64_t)i0[u] * F)[v];
+          x1[u] = reinterpret_cast<const T*>(x + (int64_t)i1[u] * F)[v];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ea = e + 2 * KS * u;
+        if (ea < end) a0 = V::add(a0, x0[u]);
+        if (ea + KS < end) a1 = V::add(a1, x1[u]);
+      }
     }
     T a = V::add(a0, a1);
 #pragma unroll

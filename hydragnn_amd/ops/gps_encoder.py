@@ -43,6 +43,7 @@ import torch
 from .. import _native
 from . import pna as _mode
 from . import streams as _streams
+from ..parallel import gradslots as _gradslots
 
 NREP = 8
 SITES = 11  # fwd BN1 (2) + BN2 (2) + BN3 (2) + bwd pair (2) + bwd BN1/BN2 (3)
@@ -350,6 +351,8 @@ class _GPSEncoder(torch.autograd.Function):
         ctx.radial = (rbf, drdf, Rl, Gl)
         ctx.emb = e
         ctx.freq_grad = bool(freq.requires_grad)
+        # the parameter objects themselves (gradient slots are keyed by parameter)
+        ctx.pobj = (freq, (Wne, Wpe, Wnl, Wee, Wrp, Wel), flat)
         ctx.save_for_backward(xin, pe, eattr, rpe, Wne, Wpe, Wnl, Wee, Wrp, Wel, xL, *flat)
         return xL, pooled
 
@@ -371,11 +374,25 @@ class _GPSEncoder(torch.autograd.Function):
         g = ops.gf_pair_stats_bwd(dxL, xL, st[L - 1]["z3"], saved[L - 1], acc[L - 1], nv, dpool, cfg.gidx, cfg.gptr)
         empty = torch.empty(0, device=dev, dtype=torch.float32)
         dys, xs, dws, dbs = [], [], [], []
+        # parameter gradients go straight into the training step's flat-buffer slots when it
+        # provides them (parallel/gradslots.py): autograd then hands back the slot views and
+        # the step packs nothing
+        pfreq, pemb, pflat = ctx.pobj
+        ctx.pobj = None
+        pobj = [pflat[NP * l: NP * (l + 1)] for l in range(L)]
 
-        def item(dy, x, W, with_bias):
+        def gsl(*ps):
+            return _gradslots.slots(list(ps))
+
+        def item(dy, x, W, with_bias, pW=None, pb=None):
             shape = W if isinstance(W, tuple) else W.shape
-            dW = torch.empty(shape, device=dev, dtype=torch.float32)
-            db = torch.empty(shape[0], device=dev, dtype=torch.float32) if with_bias else None
+            sl = gsl(pW, pb) if (pW is not None and pb is not None) else (gsl(pW) if pW is not None else None)
+            dW = sl[0] if sl is not None else torch.empty(shape, device=dev, dtype=torch.float32)
+            if with_bias:
+                db = sl[1] if (sl is not None and pb is not None) else torch.empty(shape[0], device=dev,
+                                                                                 dtype=torch.float32)
+            else:
+                db = None
             dys.append(dy)
             xs.append(x)
             dws.append(dW)
@@ -401,9 +418,10 @@ class _GPSEncoder(torch.autograd.Function):
              g1, b1n, g2, b2n, g3, b3n, g4, b4n, W1, b1, W2, b2, Wemb, bemb, Wrl) = prm[l]
             s0, s1, s2, s3 = cfg.salts[l]
             n1, n2, n3, n4 = cfg.bns[l]
+            P = pobj[l]
             dg, dpre, dout, dw3, db3, dw4, db4 = ops.gf_mlp_bwd(g, s["z3"], acc[l], saved[l], g3, g4, float(n3.eps),
                                                                float(n4.eps), s["md"], W2, W1, s["z1"], s["z2"], rng,
-                                                               s2, s3, p, nv)
+                                                               s2, s3, p, nv, gsl(P[16], P[17], P[18], P[19]))
             side = _Side(dev, cfg.side)
             with side:
                 side.used(dout)
@@ -412,21 +430,23 @@ class _GPSEncoder(torch.autograd.Function):
                     # come out of the output-projection backward's epilogue: no packing launch
                     pk = s["pk"]
                     dz2, da, _, dw2n, db2n, nd, dOp, dOq = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng,
-                                                                          s1, p, nv, s["O"])
+                                                                          s1, p, nv, s["O"], gsl(P[14], P[15]))
                     dqkv = ops.attn8_bwd_packed(nd, dOp, dOq, s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid,
                                                 cfg.sptr, s["x"].shape[0], cfg.scale, cfg.bf16)
                     dO = None
                 elif cfg.a8:
-                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
+                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv,
+                                                             None, gsl(P[14], P[15]))
                     pk = s["pk"]
                     dqkv = ops.attn8_bwd(dO, s["O"], s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid, cfg.sptr,
                                          cfg.scale, cfg.splits)
                 else:
-                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv)
+                    dz2, da, dO, dw2n, db2n = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng, s1, p, nv,
+                                                             None, gsl(P[14], P[15]))
                     dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale,
                                         cfg.span, cfg.splits)
             dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
-                                                         nv)
+                                                         nv, gsl(P[12], P[13]))
             if wside and lo < len(dys):
                 # the previous layer's weight gradients: enqueued here so they run beside this
                 # layer's attention backward (long, matrix-core bound) rather than beside the
@@ -474,17 +494,17 @@ class _GPSEncoder(torch.autograd.Function):
                 dx0 = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], None, None, None, nv)
             base = NP * l
             gw = {}
-            gw["Wemb"] = item(dr, rbf, Wemb, True)
-            gw["Wrl"] = item(dG, rbf, Wrl, False)
-            gw["Win"] = item(dqkv, s["x"], Win, True)
-            gw["Wo"] = item(da, s["O"], Wo, True)
+            gw["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
+            gw["Wrl"] = item(dG, rbf, Wrl, False, P[26])
+            gw["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
+            gw["Wo"] = item(da, s["O"], Wo, True, P[2], P[3])
             gw["Wab"] = item(dAB, s["x"], s["Wab"], False)
             gw["Wr"] = item(dE, Rl[l], s["Wr"], True)
             gw["Wd"] = item(dE, e, s["Wd"], False)
-            gw["Wpost"] = item(dp, s["Z"], Wpost, True)
-            gw["Wlin"] = item(dq, s["p"], Wlin, True)
-            gw["W1"] = item(dpre, s["out"], W1, True)
-            gw["W2"] = item(dg, s["md"], W2, True)
+            gw["Wpost"] = item(dp, s["Z"], Wpost, True, P[8], P[9])
+            gw["Wlin"] = item(dq, s["p"], Wlin, True, P[10], P[11])
+            gw["W1"] = item(dpre, s["out"], W1, True, P[20], P[21])
+            gw["W2"] = item(dg, s["md"], W2, True, P[22], P[23])
             wg.append((l, gw))
             grads[base + 12], grads[base + 13] = dw1n, db1n
             grads[base + 14], grads[base + 15] = dw2n, db2n
@@ -506,10 +526,13 @@ class _GPSEncoder(torch.autograd.Function):
         # grouped launch pair
         ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
         # weight-prep backward of every layer, embedding weights and dfreq: one launch
-        wp = []
+        wp, fp = [], []
         for l, gw in wg:
             wp += [gw["Wab"][0], gw["Wr"][0], gw["Wd"][0], gw["Wr"][1], prm[l][4], prm[l][6], prm[l][7]]
-        fin = ops.gf_finish(wp, [tn[0], tn[1], Wne, Wpe, Wnl, te[0], te[1], Wee, Wrp, Wel], dfreq_w)
+            fp += list(pobj[l][4:8])  # dWpre, dbpre, dWenc, dbenc
+        fp += list(pemb) + ([pfreq] if dfreq_w is not None else [])
+        fin = ops.gf_finish(wp, [tn[0], tn[1], Wne, Wpe, Wnl, te[0], te[1], Wee, Wrp, Wel], dfreq_w,
+                            _gradslots.slots(fp))
         dfreq = fin[4 * L + 6] if dfreq_w is not None else None
         emb_g = fin[4 * L: 4 * L + 6]  # node dWa, dWb, dWl, edge dWa, dWb, dWl
         for k, (l, gw) in enumerate(wg):

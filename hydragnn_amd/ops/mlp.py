@@ -12,7 +12,9 @@ import torch
 from torch import nn
 
 from .. import _native
+from ..parallel import gradslots as _gradslots
 from . import pna as _mode
+from . import streams as _streams
 
 MAX_ROWS = 1024
 ROWS = 4  # rows per workgroup (csrc/mlp.hip kMlpRows)
@@ -132,7 +134,11 @@ class _HeadLoss(torch.autograd.Function):
     def forward(ctx, x, target, mask, kind, relu, fused, *params):
         ctx.fused = fused
         ctx.set_materialize_grads(False)  # no zero-filled gradient for pred
+        ctx.slotted = False
         if fused:
+            sl = _side_slots(x, kind, params)
+            if sl is not None:
+                return _HeadLoss._forward_side(ctx, x, target, mask, kind, relu, params, sl)
             out = _native.ops().head_loss_fused(x, params[0::2], params[1::2], relu, target, mask, kind)
             stats, pred = out[0], out[1]
             ctx.grads = out[2:]
@@ -145,7 +151,46 @@ class _HeadLoss(torch.autograd.Function):
         return stats[0], pred
 
     @staticmethod
+    def _forward_side(ctx, x, target, mask, kind, relu, params, sl):
+        """Training step with gradient slots: the critical path gets only dx (the forward and
+        input-gradient chains, ``head_loss_dx``); the same kernel in full mode runs on a side
+        stream and writes predictions, the loss and every weight gradient — straight into the
+        step's flat gradient slots — overlapped with the encoder's backward."""
+        ops = _native.ops()
+        Ws, bs = params[0::2], params[1::2]
+        dx = ops.head_loss_dx(x, Ws, bs, relu, target, mask, kind)
+        main = torch.cuda.current_stream(x.device)
+        side = _streams.side_stream(x.device, 4)
+        side.wait_stream(main)
+        for t in (x, target, mask):
+            if t is not None:
+                t.record_stream(side)
+        with torch.cuda.stream(side):
+            out = ops.head_loss_fused(x, Ws, bs, relu, target, mask, kind, None, sl, False)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        stats, pred = out[0], out[1]
+        # loss / predictions are read after the step's gradient join (finish): the main stream
+        # waits for the side stream there; until then keep their memory out of reuse
+        stats.record_stream(main)
+        pred.record_stream(main)
+        _gradslots.provide(list(params), ev)
+        ctx.slotted = True
+        ctx.dx = dx
+        ctx.nparams = len(params)
+        ctx.mark_non_differentiable(pred)
+        return stats[0], pred
+
+    @staticmethod
     def backward(ctx, g, _gpred):
+        if ctx.slotted:
+            dx = ctx.dx
+            ctx.dx = None
+            if g is None:
+                return (None,) * (6 + ctx.nparams)
+            if not getattr(g, "_hydra_unit_seed", False):
+                raise RuntimeError("head_loss: slotted gradients need the step's unit backward seed")
+            return (dx, None, None, None, None, None) + (None,) * ctx.nparams
         if ctx.fused:
             grads = ctx.grads
             ctx.grads = None
@@ -158,6 +203,17 @@ class _HeadLoss(torch.autograd.Function):
         out = _native.ops().head_loss_bwd(g.reshape(1).contiguous(), x, acts, params[0::2], params[1::2], ctx.relu,
                                           target, mask, stats, ctx.kind)
         return (out[0], None, None, None, None, None, *out[1:])
+
+
+def _side_slots(x, kind, params):
+    """Gradient slots for the head's parameters when the side-stream split applies (training
+    step under ``parallel.gradslots.use``, CUDA, not RMSE — its dx needs the batch loss;
+    ``HYDRA_HEADLOSS_SIDE=0`` disables), else None."""
+    if not x.is_cuda or kind == _KIND["rmse"] or os.environ.get("HYDRA_HEADLOSS_SIDE", "1") != "1":
+        return None
+    if not _streams.enabled(x):
+        return None
+    return _gradslots.slots(params)
 
 
 def head_loss(x, layers, target, mask, kind, fused=None):

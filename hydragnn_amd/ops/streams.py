@@ -26,7 +26,8 @@ def side_stream(device, slot=0):
     """Cached side stream ``slot`` of ``device`` (slot 0: branch forks; slot 1: the
     attention backward's dK/dV pass, which forks again from inside a side branch;
     slot 2: the fused GPS encoder's edge chain (forward) and per-layer weight gradients /
-    edge backward (backward); slot 3: the first layer's edge backward)."""
+    edge backward (backward); slot 3: the first layer's edge backward; slot 4: the fused
+    graph head's weight-gradient twin, ops/mlp.py)."""
     key = (torch.device(device).index, slot)
     s = _side.get(key)
     if s is None:

@@ -6,7 +6,7 @@ checkpoints (``optimizer_state_dict``) and ``ReduceLROnPlateau`` work.  The
 learning rate and step counter are device scalars: changing ``lr`` through
 ``param_groups`` is picked up at the next ``step()`` without recapturing.
 
-GPU: one kernel launch for all parameters (+1 tiny counter kernel).  CPU: the
+GPU: one kernel launch for all parameters (its last block advances the step counts).  CPU: the
 plain-torch update (reference math), used by the CPU tests.
 """
 import struct

@@ -261,7 +261,35 @@ class BucketedGradSync:
         self.comm = torch.cuda.Stream(device=dev, priority=-1) if dev.type == "cuda" else None
         for p in self.params:
             p.register_post_accumulate_grad_hook(self._hook)
+        # gradient slots (parallel/gradslots.py): parameters whose gradient an op wrote straight
+        # into its flat slot this step (no pack copy), and the side-stream events behind them
+        self.provided = {}
+        self.side_events = []
+        self.guard_packed = True
+        self._slot_ptr = {p: self.flat.data_ptr() + self.offset[p] * self.flat.element_size() for p in self.params}
         self.attach()
+
+    def slot(self, p):
+        """``p``'s view of the flat buffer (None for a parameter this sync does not hold)."""
+        o = self.offset.get(p)
+        return None if o is None else self.flat[o:o + p.numel()].view_as(p)
+
+    def provide(self, params, event=None):
+        """Declare that this step's gradients of ``params`` are (or, after ``event`` on a side
+        stream, will be) in their slots: the pack copies skip them, the bucket countdown counts
+        them (an op that writes slots returns no autograd gradient for them), and the bucket's
+        all-reduce / ``finish`` wait for ``event``."""
+        if event is not None:
+            self.side_events.append(event)
+        for p in params:
+            self.provided[id(p)] = p
+            self._hook(p)
+
+    def _in_place(self, p):
+        if id(p) in self.provided:
+            return True
+        g = p.grad
+        return g is not None and g.is_contiguous() and g.data_ptr() == self._slot_ptr[p]
 
     # -- grad storage
     def attach(self):
@@ -293,6 +321,8 @@ class BucketedGradSync:
         self.works = []
         self.next = 0
         self.counted = set()
+        for p in list(self.provided.values()):  # slots written during the forward (before begin)
+            self._hook(p)
 
     def _hook(self, p):
         if not self.active:
@@ -324,22 +354,43 @@ class BucketedGradSync:
         return z[:n]
 
     def _pack(self, bi):
+        """Copy the bucket's gradients into the flat buffer: one batched copy per contiguous run
+        of parameters whose gradient is not already in its slot (one run, one launch, in the
+        common case)."""
         s, e, ps = self.buckets[bi]
-        gs = [p.grad.reshape(-1) if p.grad is not None else self._zeros(p.numel()) for p in ps]
-        if e == self.total + 1 + self.nflags:
+        runs, start, cur = [], None, []
+        for p in ps:
+            if self._in_place(p):
+                if cur:
+                    runs.append((start, cur))
+                    cur = []
+                continue
+            if not cur:
+                start = self.offset[p]
+            cur.append(p.grad.reshape(-1) if p.grad is not None else self._zeros(p.numel()))
+        self.guard_packed = self.active or self.world > 1 or self.nflags > 0
+        if e == self.total + 1 + self.nflags and self.guard_packed:
+            # the guard slot (+ usage flags) rides with the last bucket's reduce; a lone rank
+            # without flags reads the loss itself (TrainStep._set_guard) and packs nothing here
+            if not cur:
+                start = self.total
             loss = self._loss
-            gs.append(loss.detach().reshape(1).to(self.flat.dtype) if loss is not None else
-                      torch.zeros(1, device=self.flat.device, dtype=self.flat.dtype))
+            cur.append(loss.detach().reshape(1).to(self.flat.dtype) if loss is not None else
+                       torch.zeros(1, device=self.flat.device, dtype=self.flat.dtype))
             if self.nflags:
                 f = self._flag_src
-                gs.append(f.detach().reshape(-1).to(self.flat.dtype) if f is not None else
-                          torch.ones(self.nflags, device=self.flat.device, dtype=self.flat.dtype))
-        out = self.flat[s:e]
-        if len(gs) == 1:
-            out.copy_(gs[0])
-        else:
-            torch.cat(gs, out=out)
-        return out
+                cur.append(f.detach().reshape(-1).to(self.flat.dtype) if f is not None else
+                           torch.ones(self.nflags, device=self.flat.device, dtype=self.flat.dtype))
+        if cur:
+            runs.append((start, cur))
+        for start, gs in runs:
+            n = sum(g.numel() for g in gs)
+            out = self.flat[start:start + n]
+            if len(gs) == 1:
+                out.copy_(gs[0])
+            else:
+                torch.cat(gs, out=out)
+        return self.flat[s:e]
 
     def _launch(self, bi):
         if self.launched[bi]:
@@ -351,6 +402,8 @@ class BucketedGradSync:
             self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             return
         self.comm.wait_stream(torch.cuda.current_stream())
+        for ev in self.side_events:  # slot writers on side streams
+            self.comm.wait_event(ev)
         with torch.cuda.stream(self.comm):
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
 
@@ -375,6 +428,11 @@ class BucketedGradSync:
         else:
             for bi in range(len(self.buckets)):
                 self._pack(bi)
+        if self.flat.is_cuda:
+            for ev in self.side_events:
+                torch.cuda.current_stream().wait_event(ev)
+        self.side_events = []
+        self.provided = {}
         self.works = []
         self.active = False
         self.attach()
@@ -464,11 +522,28 @@ class MultiGradSync:
         self.nflags = self.syncs[0].nflags
         self.flags = self.syncs[0].flags
 
+    @property
+    def guard_packed(self):
+        return self.syncs[0].guard_packed
+
     def set_loss(self, loss):
         self.syncs[0].set_loss(loss)
 
     def set_flags(self, src):
         self.syncs[0].set_flags(src)
+
+    def slot(self, p):
+        for s in self.syncs:
+            v = s.slot(p)
+            if v is not None:
+                return v
+        return None
+
+    def provide(self, params, event=None):
+        for s in self.syncs:
+            mine = [p for p in params if p in s.offset]
+            if mine:
+                s.provide(mine, event)
 
     def begin(self):
         for s in self.syncs:

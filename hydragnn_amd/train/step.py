@@ -452,10 +452,14 @@ class TrainStep:
         return batch_loss(self.module, pred, batch)
 
     def _body_fwd_bwd(self, store, cap, sync=True):
+        from ..parallel import gradslots
+
         self._zero()
         batch = store.assemble(cap.dev_plan, cap.lay, branch_sorted=store.dataset_name is not None)
-        loss, tasks = self._loss(batch)
-        self._backward(loss, sync=sync)
+        # ops may write gradients straight into the flat buffer's slots (parallel/gradslots.py)
+        with gradslots.use(self.sync):
+            loss, tasks = self._loss(batch)
+            self._backward(loss, sync=sync)
         self._set_guard(loss)
         return loss.detach(), [t.detach() for t in tasks]
 
@@ -467,7 +471,7 @@ class TrainStep:
         guard slot of the gradient buffer (sum of the ranks' losses); the eager DDP path
         all-reduces a copy of the loss."""
         g = loss.detach()
-        if self.sync is not None:
+        if self.sync is not None and self.sync.guard_packed:
             g = self.sync.guard
         elif self.world > 1 and isinstance(self.model, DistributedDataParallel):
             import torch.distributed as dist

@@ -205,6 +205,33 @@ def test_fused_adamw_matches_cpu():
         torch.testing.assert_close(b.detach(), c.detach(), rtol=1e-5, atol=1e-6)
 
 
+def test_fused_adamw_guard_and_step_counts():
+    """A NaN guard skips the whole update (parameters, moments, step counts) and is counted;
+    the launch's last block advances every used parameter's step count exactly once (one
+    launch, no separate counter kernel)."""
+    from hydragnn_amd.optim.adamw import FusedAdamW
+
+    torch.manual_seed(1)
+    ps = [torch.randn(5000, device=DEV).requires_grad_(), torch.randn(3, 3, device=DEV).requires_grad_()]
+    opt = FusedAdamW(ps, lr=1e-2)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt.step()
+    before = [p.detach().clone() for p in ps]
+    assert [float(opt.state[p]["step"]) for p in ps] == [1.0, 1.0]
+    opt.guard = torch.tensor(float("nan"), device=DEV)
+    opt.step()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(ps, before))
+    assert [float(opt.state[p]["step"]) for p in ps] == [1.0, 1.0]
+    assert opt.skipped_steps() == 1
+    opt.guard = torch.tensor(0.5, device=DEV)
+    for _ in range(3):
+        opt.step()
+    assert [float(opt.state[p]["step"]) for p in ps] == [4.0, 4.0]
+    assert not any(torch.equal(a, b) for a, b in zip(ps, before))
+
+
 @pytest.mark.parametrize("F", [64, 7, 300])
 @pytest.mark.parametrize("masked", [False, True])
 def test_batchnorm_fused(F, masked):

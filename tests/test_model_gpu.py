@@ -165,3 +165,24 @@ def test_graph_step_follows_lr_changes():
     step(s, idx)
     torch.cuda.synchronize()
     assert any(not torch.equal(a, b) for a, b in zip(m.parameters(), before)), "lr restored but nothing moved"
+
+
+def test_graph_step_head_gradient_slots_match(monkeypatch):
+    """The fused graph head under gradient slots (ops/mlp.py _forward_side: dx-only kernel on
+    the critical path, the full kernel on a side stream writing weight gradients straight
+    into the flat buffer) trains bitwise like the single-launch head (HYDRA_HEADLOSS_SIDE=0)."""
+    samples = oc20_like(48, seed=9)
+    base = _model(samples).cuda()
+    s = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
+    batches = [list(range(i, i + 16)) for i in range(0, 32, 4)]
+    params, losses = [], []
+    for side in ("0", "1"):
+        monkeypatch.setenv("HYDRA_HEADLOSS_SIDE", side)
+        m = copy.deepcopy(base)
+        step = TrainStep(m, mode="graph", node_bucket=2048, edge_bucket=1 << 15)
+        losses.append([float(step(s, b)[0]) for b in batches])
+        torch.cuda.synchronize()
+        params.append([p.detach().clone() for p in m.parameters()])
+    assert losses[0] == losses[1], losses
+    for a, b in zip(*params):
+        assert torch.equal(a, b)

@@ -45,12 +45,14 @@ def main():
         ops.head_loss_fused(x, Ws, bs, relu, t, m, 1, dbg)
         torch.cuda.synchronize()
         st = dbg.cpu().tolist()
-        n = len(dims) - 1
-        marks = [("start", 0), ("layout", 1), ("stage", 2)] + [(f"fwd{l}", 3 + l) for l in range(n)] + \
-                [("loss", 19)] + [(f"bwd{l}", 20 + l) for l in reversed(range(n))] + [("end", 31)]
+        # row-split kernel marks: 0 start, 1 table + zero fill, 2 staged, 3 forward chain,
+        # 19 loss, 20 backward chain, 31 end (reduce by the last workgroup)
+        names = {0: "start", 1: "zero", 2: "stage", 3: "fwd", 19: "loss", 20: "bwd", 31: "end"}
         prev = st[0]
         txt = []
-        for name, i in marks:
+        for i, name in sorted(names.items()):
+            if st[i] == 0:
+                continue
             txt.append(f"{name} +{st[i] - prev}")
             prev = st[i]
         print("   stamps (shader clocks, s_memtime): " + ", ".join(txt), flush=True)
