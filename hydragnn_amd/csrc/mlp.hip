@@ -953,7 +953,8 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
   // full = 1 with dx == null: everything but dx (the side-stream twin of a full = 0 launch)
   hl_stamp(dbg, 0);
   extern __shared__ float sm[];
-  __shared__ double redk[kHlWaves], redl[kHlWaves];
+  __shared__ double redl[kHlWaves];
+  __shared__ int redk[kHlWaves];
   const int R = gridDim.x, b = blockIdx.x, row0 = b * kHlRows, Gl = min(kHlRows, G - row0);
   const int tid = threadIdx.x, wv = hl_u(tid >> 6), lane = tid & 63, li = lane & 15, lg = lane >> 4;
   const int n = tab.n, Gp = tab.Gp, D0 = tab.dims[0], nw = tab.goff[n];
@@ -970,13 +971,26 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
   const float* j_src = tab.jsrc[jl];
   const int j_nr = tab.jnr[jl], j_pr = tab.jpr[jl], j_w = tab.jw[jl], j_sld = tab.jsld[jl], j_dst = tab.jdst[jl];
   const int j_dld = tab.jdld[jl], j_zw = tab.jzw[jl], j_row = tab.jrow[jl];
-  double kr = 0.0;
-  for (int r = tid; r < G; r += kHlThreads) kr += (mask == nullptr || mask[r]) ? 1.0 : 0.0;
-  if (tid < Gp) sm[tab.mk + tid] = (tid < Gl && (mask == nullptr || mask[row0 + tid])) ? 1.f : 0.f;
-  for (int off = 32; off > 0; off >>= 1) kr += __shfl_xor(kr, off);
+  // the row-mask reads go out with the table loads (clamped, unconditional: a guarded load
+  // would be waited for on its own, one more memory round trip before the copies)
+  const bool mk_all = mask == nullptr || mask[min(tid, G - 1)];
+  const bool mk_own = mask == nullptr || mask[row0 + min(tid, Gl - 1)];
+  // kept rows per wave: ballot + popcount (no shuffle rounds)
+  int kr = __popcll(__ballot(tid < G && mk_all));
+  for (int r0 = kHlThreads; r0 < G; r0 += kHlThreads) {
+    const int r = r0 + tid;
+    kr += __popcll(__ballot(r < G && (mask == nullptr || mask[min(r, G - 1)])));
+  }
+  if (tid < Gp) sm[tab.mk + tid] = (tid < Gl && mk_own) ? 1.f : 0.f;
   if (lane == 0) redk[wv] = kr;
-  int base = 0;
+  hl_stamp(dbg, 28);
   const int nj = tab.njobs;
+  // LDS-DMA copy jobs: one wave instruction per (matrix row, 64-column chunk), rows dealt
+  // round-robin to the waves (continuing across jobs), every copy in flight together; each
+  // row's zero padding is written by the wave that copies it (disjoint addresses).
+  // (Measured alternatives, tools/bench_head_loss.py: zero stores in a separate pass before
+  // the copies, and register staging of 16 rows per wave with one wait, were both slower.)
+  int base = 0;
   for (int j = 0; j < nj; ++j) {
     const float* src = hl_rlp(j_src, j);
     int nr = hl_rl(j_nr, j), pr = hl_rl(j_pr, j);
@@ -1002,14 +1016,15 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
   // activations, dY buffers: plain zero fill (disjoint from every copy)
   for (int e = tab.act[0] + 4 * tid; e < tab.tg; e += 4 * kHlThreads)
     *reinterpret_cast<float4*>(sm + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+  hl_stamp(dbg, 29);
   hl_stamp(dbg, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   hl_sync();
   hl_stamp(dbg, 2);
-  double kept = 0.0;
+  int keptr = 0;
 #pragma unroll
-  for (int k = 0; k < kHlWaves; ++k) kept += redk[k];
-  kept *= (double)Do;
+  for (int k = 0; k < kHlWaves; ++k) keptr += redk[k];
+  const double kept = (double)keptr * (double)Do;
   // forward chain: A_l = act(A_{l-1} W_l^T + b_l), 16 x 16 output tiles per wave
   for (int l = 0; l < n; ++l) {
     const int I = hl_rl(v_dims, l), O = hl_rl(v_dims, l + 1);
@@ -1183,7 +1198,7 @@ __global__ void __launch_bounds__(kHlThreads) head_loss_rows_kernel(
         if (e >= g0 && e < hl_rl(v_goff, l + 1))
           dst = e < g0 + oi ? hl_rlp(v_gout, 2 * l) + (e - g0) : hl_rlp(v_gout, 2 * l + 1) + (e - g0 - oi);
       }
-      if (dst != nullptr) *dst = v[u] * sc;
+      if (dst != nullptr) *(__attribute__((address_space(1))) float*)dst = v[u] * sc;
     }
   }
   if (kind == 2 && dx != nullptr)

@@ -67,17 +67,17 @@ __global__ void __launch_bounds__(256) adamw_kernel(const TensorRef* __restrict_
       r.p[k] = p - step_size * m / denom;
     }
   }
-  // ticket: every block's step read happened above (its value fed the update)
+  // ticket: every block's step read happened above (its value fed the update, before the
+  // barrier), so the last ticket orders the increments after every read.  No fences: nothing
+  // written here is read by another block of this launch (a release fence per block was an
+  // L2 write-back each, +7 us on the OC20 step)
   __shared__ int last;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (threadIdx.x == 0)
     last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  }
   __syncthreads();
   if (!last) return;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     *ticket = 0;  // every ticket of this launch is drawn
     if (bad && has_skip) state[2] += 1.f;
   }

@@ -219,8 +219,9 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
     Vec<VEC> da;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) da.v[i] = 0.f;
-    // edge batches as in the forward: gathers of a batch in flight together
-    constexpr int EB = VEC == 1 ? 8 : 4;
+    // edge batches as in the forward: gathers of a batch in flight together (4 edges: the
+    // backward co-runs with the attention backward, and 8-edge batches doubled its registers)
+    constexpr int EB = VEC == 1 ? 4 : 2;
     for (int e0 = beg; e0 < end; e0 += EB) {
       int js[EB];
 #pragma unroll

@@ -44,6 +44,13 @@ class PNAConvFused(nn.Module):
         Fi = in_channels
         self.F_in, self.F_out = Fi, out_channels
         n_in = 3 if (plus or edge_dim is not None) else 2
+        # parameter creation and initialisation in the reference's order, draw for draw (the
+        # init seed then reproduces the reference's initial weights): PyG PNAConv creates its
+        # edge encoder first; the PNAPlus conv (PNAPlusStack.py:180-210) creates it last; both
+        # then re-draw edge encoder, pre-, post-NN and lin in reset_parameters
+        # (PNAPlusStack.py:212-220, PyG PNAConv.reset_parameters)
+        if not plus and edge_dim is not None:
+            self.edge_encoder = Linear(edge_dim, Fi)
         self.pre_nns = ModuleList([Sequential(Linear(n_in * Fi, Fi))])
         self.post_nns = ModuleList([Sequential(Linear(17 * Fi, out_channels))])
         self.lin = Linear(out_channels, out_channels)
@@ -52,10 +59,16 @@ class PNAConvFused(nn.Module):
             self.rbf_emb = Sequential(Linear(num_radial, Fi), nn.ReLU())
             if edge_dim is not None:
                 self.edge_encoder = Linear(Fi + edge_dim, Fi)
-        elif edge_dim is not None:
-            self.edge_encoder = Linear(edge_dim, Fi)
         self.register_buffer("deg", torch.as_tensor(deg, dtype=torch.float32))
         self.avg_deg = pna_avg_deg(self.deg)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        if getattr(self, "edge_encoder", None) is not None:
+            self.edge_encoder.reset_parameters()
+        self.pre_nns[0][0].reset_parameters()
+        self.post_nns[0][0].reset_parameters()
+        self.lin.reset_parameters()
 
     def forward(self, inv, equiv, ctx):
         x = inv

@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native
+from ..parallel import gradslots as _gradslots
 from . import pna as _mode
 
 _PREC = {"fp32": 0, "bf16": 1}
@@ -142,9 +143,18 @@ def flush_deferred_wgrads():
             full = k0 == 0 and k1 == W.shape[1]
             a = not (id(W) in fresh and (b is None or b.grad is None))
             if W.grad is None:
-                W.grad = torch.empty_like(W) if id(W) in fresh else torch.zeros_like(W)
+                # the step's flat-buffer slot when it provides one (parallel/gradslots.py)
+                sl = _gradslots.slots([W])
+                if sl is not None:
+                    W.grad = sl[0] if id(W) in fresh else sl[0].zero_()
+                else:
+                    W.grad = torch.empty_like(W) if id(W) in fresh else torch.zeros_like(W)
             if b is not None and b.grad is None:
-                b.grad = torch.empty_like(b) if not a else torch.zeros_like(b)
+                sl = _gradslots.slots([b])
+                if sl is not None:
+                    b.grad = sl[0] if not a else sl[0].zero_()
+                else:
+                    b.grad = torch.empty_like(b) if not a else torch.zeros_like(b)
             if a and id(W) in fresh:
                 # (a fresh weight block paired with an already-accumulating bias: the block's
                 # columns must start from zero too)

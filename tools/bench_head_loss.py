@@ -31,6 +31,16 @@ def main():
                     (33, [64, 1]), (33, [64, 50, 1]), (33, [8, 8, 1])]:
         Ws = [torch.randn(dims[i + 1], dims[i], device=dev) * 0.1 for i in range(len(dims) - 1)]
         bs = [torch.randn(dims[i + 1], device=dev) * 0.1 for i in range(len(dims) - 1)]
+        if os.environ.get("HL_CONTIG") == "1":  # every weight and bias as a view of one buffer
+            n = sum(w.numel() + b.numel() for w, b in zip(Ws, bs))
+            buf = torch.empty(n, device=dev)
+            off, W2, b2 = 0, [], []
+            for w, b in zip(Ws, bs):
+                W2.append(buf[off:off + w.numel()].view_as(w).copy_(w))
+                off += w.numel()
+                b2.append(buf[off:off + b.numel()].copy_(b))
+                off += b.numel()
+            Ws, bs = W2, b2
         relu = [1] * (len(dims) - 2) + [0]
         x = torch.randn(G, dims[0], device=dev)
         t = torch.randn(G, dims[-1], device=dev)
@@ -47,10 +57,10 @@ def main():
         st = dbg.cpu().tolist()
         # row-split kernel marks: 0 start, 1 table + zero fill, 2 staged, 3 forward chain,
         # 19 loss, 20 backward chain, 31 end (reduce by the last workgroup)
-        names = {0: "start", 1: "zero", 2: "stage", 3: "fwd", 19: "loss", 20: "bwd", 31: "end"}
+        names = {0: "start", 28: "table+mask", 29: "copies issued", 1: "zero", 2: "stage", 3: "fwd0", 19: "fwd+loss", 20: "bwd", 31: "end"}
         prev = st[0]
         txt = []
-        for i, name in sorted(names.items()):
+        for i, name in sorted(names.items(), key=lambda kv: [0, 28, 29, 1, 2, 3, 19, 20, 31].index(kv[0])):
             if st[i] == 0:
                 continue
             txt.append(f"{name} +{st[i] - prev}")
