@@ -57,8 +57,14 @@ def main():
         samples = bc._targets_for_store(samples, ht)
     store = DeviceGraphStore(samples, dev, head_types=None if forces else ht, head_dims=None if forces else hd)
     nbk = 512
+    cap = a.bucket_mb
+    if cap is None:
+        # the bucket size a multi-rank run picks (BucketedGradSync: half the gradient bytes,
+        # >= 256 KB, <= 32 MB); a lone rank would otherwise keep one bucket
+        nbytes = 4 * sum(p.numel() for p in model.parameters() if p.requires_grad)
+        cap = min(max(nbytes // 2 + 1, 256 * 1024), 32 * 1024 * 1024) / (1024 * 1024)
     ts = TrainStep(model, lr=1e-3, mode="graph", world=1, node_bucket=nbk, edge_bucket=8 * nbk,
-                   bucket_cap_mb=a.bucket_mb, compute_grad_energy=forces)
+                   bucket_cap_mb=cap, compute_grad_energy=forces)
     syncs = getattr(ts.sync, "syncs", [ts.sync])
     for k, s in enumerate(syncs):
         def launch(bi, o=s._launch, k=k):
@@ -85,7 +91,11 @@ def main():
     b0, b1 = win[0].time_range.start, win[0].time_range.end
     launches = sorted(e.time_range.start for e in ev
                       if "LaunchKernel" in e.name and b0 <= e.time_range.start <= b1)
-    ars = sorted((e.time_range.start, e.name) for e in ev if e.name.startswith("gradsync_bucket_"))
+    first = {}
+    for e in ev:  # one marker per bucket launch (the profiler may report a range twice)
+        if e.name.startswith("gradsync_bucket_"):
+            first[e.name] = min(first.get(e.name, e.time_range.start), e.time_range.start)
+    ars = sorted((t, n) for n, t in first.items())
     after = [sum(1 for t in launches if t > s0) for s0, _ in ars]
     res = {"config": a.config, "precision": a.precision, "buckets": sum(len(s.buckets) for s in syncs),
            "allreduces": len(ars), "backward_kernel_launches": len(launches), "launches_after_each_allreduce": after,
