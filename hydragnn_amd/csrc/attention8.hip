@@ -25,6 +25,7 @@
 //          rows 4g..4g+3 of column d = i as one float4 — the A fragment of a product
 //          summed over 16 rows.
 #include "common.h"
+#include "pna_body.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -837,16 +838,14 @@ __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 template <int W>
-__global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __restrict__ Qp,
-                                                             const float* __restrict__ Kp,
-                                                             const float* __restrict__ Vq, int N, int Nq, int H,
-                                                             const int* __restrict__ seg_id,
-                                                             const int* __restrict__ seg_ptr, float qscale,
-                                                             float* __restrict__ O, float* __restrict__ NL) {
+__device__ __forceinline__ void attn8_fwd2q_body(const float* __restrict__ Qp, const float* __restrict__ Kp,
+                                                 const float* __restrict__ Vq, int N, int Nq, int H,
+                                                 const int* __restrict__ seg_id, const int* __restrict__ seg_ptr,
+                                                 float qscale, float* __restrict__ O, float* __restrict__ NL,
+                                                 int qtile, int h) {
   __shared__ float red[W][16][10];
-  const int h = blockIdx.y;
   const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-  const int qbase = blockIdx.x * 16;
+  const int qbase = qtile * 16;
   const SpanR<1> sp = span_rt<1>(qbase, i, N, seg_id, seg_ptr, W, w);
   const Rsrc rk = mk_rsrc(Kp + (int64_t)h * Nq * 8, Nq * 8), rv = mk_rsrc(Vq + (int64_t)h * Nq * 8, Nq * 8);
   // K pair fragment of row k0 + i; V quad float4s of keys k0 + 4g..+3, dims i%4 and 4 + i%4
@@ -954,6 +953,51 @@ __global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __rest
       NL[(int64_t)h * Nq + qq] = 0.f;
     }
   }
+}
+
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn8_fwd2q_kernel(const float* __restrict__ Qp,
+                                                             const float* __restrict__ Kp,
+                                                             const float* __restrict__ Vq, int N, int Nq, int H,
+                                                             const int* __restrict__ seg_id,
+                                                             const int* __restrict__ seg_ptr, float qscale,
+                                                             float* __restrict__ O, float* __restrict__ NL) {
+  attn8_fwd2q_body<W>(Qp, Kp, Vq, N, Nq, H, seg_id, seg_ptr, qscale, O, NL, blockIdx.x, blockIdx.y);
+}
+
+// The GPS layer's two independent branches in ONE launch: workgroups [0, nA) run the
+// attention forward (query tile, head), the rest the PNA message + aggregation forward
+// (pna_body.h, one wave per node).  In the captured step the two were a stream fork / join
+// (attention on a side stream): every fork or join edge of a hipGraph costs ~7 us on MI355X
+// (tools/graph_fork_cost.py) and each layer paid two on its critical path.  Attention
+// workgroups come first in the grid (the long ones dispatch first); the PNA workgroups fill
+// the remaining slots exactly as the second stream's did.
+struct PnaFwdArgs {
+  const float *x, *AB, *C, *G;
+  const int *src, *rowptr;
+  float* Z;
+  int *amin, *amax;
+  int ldab, N, F, tpr;
+  float avg_log, avg_lin;
+};
+
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn8_pna_fwd_kernel(const float* __restrict__ Qp,
+                                                               const float* __restrict__ Kp,
+                                                               const float* __restrict__ Vq, int N, int Nq, int H,
+                                                               const int* __restrict__ seg_id,
+                                                               const int* __restrict__ seg_ptr, float qscale,
+                                                               float* __restrict__ O, float* __restrict__ NL, int nqt,
+                                                               PnaFwdArgs p) {
+  const int b = blockIdx.x, nA = nqt * H;
+  if (b < nA) {
+    attn8_fwd2q_body<W>(Qp, Kp, Vq, N, Nq, H, seg_id, seg_ptr, qscale, O, NL, b % nqt, b / nqt);
+    return;
+  }
+  const int rpb = 64 * W / p.tpr;
+  pna_fwd_node<1>(p.x, p.AB, p.ldab, p.C, p.G, p.src, p.rowptr, p.Z, p.amin, p.amax,
+                  (b - nA) * rpb + (int)threadIdx.x / p.tpr, (int)threadIdx.x % p.tpr, p.N, p.F, p.avg_log,
+                  p.avg_lin, p.tpr);
 }
 
 // Backward v2: blocks [0, nbq) produce dQ for RT query tiles (W waves split the keys),
@@ -2268,6 +2312,63 @@ std::vector<at::Tensor> attn8_fwd(const at::Tensor& Qp, const at::Tensor& Kp, co
   return {O, L};
 }
 
+// attention forward + PNA forward as one launch (see attn8_pna_fwd_kernel); fp32, v2 quad
+// path only.  Returns [O, LSE2, Z, amin, amax].
+std::vector<at::Tensor> attn8_pna_fwd(const at::Tensor& Qp, const at::Tensor& Kp, const at::Tensor& Vq,
+                                      const at::Tensor& seg_id, const at::Tensor& seg_ptr, int64_t N, double scale,
+                                      const at::Tensor& x, const at::Tensor& AB, const c10::optional<at::Tensor>& C_,
+                                      const c10::optional<at::Tensor>& G_, const at::Tensor& src,
+                                      const at::Tensor& rowptr, double avg_log, double avg_lin) {
+  const int64_t H = Qp.size(0), Nq = Qp.size(1);
+  HY_CHECK(Qp.is_contiguous() && Kp.is_contiguous() && Vq.is_contiguous() && Qp.size(2) == 8 && Nq % 16 == 0 &&
+               Nq >= N && Kp.sizes() == Qp.sizes() && Vq.numel() == Qp.numel(),
+           "attn8_pna_fwd: packed operands [H, Nq, 8] (Nq % 16 == 0)");
+  chk_seg(seg_id, seg_ptr, N);
+  HY_CHECK(quad_enabled(), "attn8_pna_fwd: the quad-block forward path only");
+  HY_CHECK_F32(x);
+  HY_CHECK_F32(AB);
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(x.is_contiguous() && x.dim() == 2 && x.size(0) == N, "attn8_pna_fwd: x [N, F]");
+  const int F = (int)x.size(1);
+  HY_CHECK(F == 64, "attn8_pna_fwd: the one-wave-per-node PNA layout (F = 64)");
+  HY_CHECK(AB.size(0) == N && AB.size(1) == 2 * F && AB.stride(1) == 1, "attn8_pna_fwd: AB [N, 2F]");
+  HY_CHECK(rowptr.numel() == N + 1, "attn8_pna_fwd: rowptr [N + 1]");
+  const int64_t E = src.numel();
+  auto edge = [&](const c10::optional<at::Tensor>& t) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    HY_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 && t->size(0) == E &&
+                 t->size(1) == F,
+             "attn8_pna_fwd: edge terms [E, F]");
+    return t->data_ptr<float>();
+  };
+  auto opt = Qp.options();
+  auto O = at::empty({N, 8 * H}, opt), L = at::empty({H, Nq}, opt);
+  auto Z = at::empty({N, 17 * F}, opt);
+  auto amin = at::empty({N, F}, opt.dtype(at::kInt)), amax = at::empty({N, F}, opt.dtype(at::kInt));
+  if (N == 0) return {O, L, Z, amin, amax};
+  PnaFwdArgs p{x.data_ptr<float>(), AB.data_ptr<float>(), edge(C_), edge(G_), src.data_ptr<int>(),
+               rowptr.data_ptr<int>(), Z.data_ptr<float>(), amin.data_ptr<int>(), amax.data_ptr<int>(),
+               (int)AB.stride(0), (int)N, F, 64, (float)avg_log, (float)avg_lin};
+  const float qs = (float)scale * kLog2e;
+  const int nqt = ceil_div(Nq, 16);
+  const int W = pick_w(ceil_div(N, 16));
+#define HY_APF(WW)                                                                                              \
+  attn8_pna_fwd_kernel<WW><<<nqt * (int)H + ceil_div(N, 64 * (WW) / 64), 64 * (WW), 0, stream()>>>(           \
+      Qp.data_ptr<float>(), Kp.data_ptr<float>(), Vq.data_ptr<float>(), (int)N, (int)Nq, (int)H,               \
+      seg_id.data_ptr<int>(), seg_ptr.data_ptr<int>(), qs, O.data_ptr<float>(), L.data_ptr<float>(), nqt, p)
+  switch (W) {
+    case 2: HY_APF(2); break;
+    case 3: HY_APF(3); break;
+    case 4: HY_APF(4); break;
+    case 5: HY_APF(5); break;
+    case 6: HY_APF(6); break;
+    default: HY_APF(8); break;
+  }
+#undef HY_APF
+  return {O, L, Z, amin, amax};
+}
+
 // dqkv [N, 24H] from dO [N, 8H] (and O, LSE2 of the forward)
 // Backward in parts (the dQ and dK/dV passes are independent given delta; running them
 // on two streams measured slower in the GPS step, see ops/gps_encoder.py):
@@ -2484,6 +2585,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("attn8_pack(Tensor qkv, int H) -> Tensor[]");
   m.def("attn8_v2_shape(int N, int H) -> int[]", hy::a8::attn8_v2_shape);
   m.def(
+      "attn8_pna_fwd(Tensor Qp, Tensor Kp, Tensor Vq, Tensor seg_id, Tensor seg_ptr, int N, float scale, Tensor x, "
+      "Tensor AB, Tensor? C, Tensor? G, Tensor src, Tensor rowptr, float avg_log, float avg_lin) -> Tensor[]");
+  m.def(
       "attn8_fwd(Tensor Qp, Tensor Kp, Tensor Vq, Tensor seg_id, Tensor seg_ptr, int N, float scale, int splits, "
       "bool bf16=False) -> Tensor[]");
   m.def(
@@ -2497,6 +2601,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("attn8_pack", hy::a8::attn8_pack);
   m.impl("attn8_fwd", hy::a8::attn8_fwd);
+  m.impl("attn8_pna_fwd", hy::a8::attn8_pna_fwd);
   m.impl("attn8_bwd", hy::a8::attn8_bwd);
   m.impl("attn8_bwd_packed", hy::a8::attn8_bwd_packed);
 }

@@ -21,54 +21,9 @@
 //                             by-source permutation)
 //   dG_e   = dm_e * pre_e
 #include "common.h"
+#include "pna_body.h"
 
 namespace hy {
-
-template <int VEC>
-struct Vec {
-  float v[VEC];
-};
-
-template <int VEC>
-__device__ __forceinline__ Vec<VEC> ld(const float* p) {
-  Vec<VEC> r;
-  if constexpr (VEC == 4) {
-    float4 t = *reinterpret_cast<const float4*>(p);
-    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
-  }
-  return r;
-}
-
-template <int VEC>
-__device__ __forceinline__ void st(float* p, const Vec<VEC>& r) {
-  if constexpr (VEC == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) p[i] = r.v[i];
-  }
-}
-
-constexpr float kStdEps = 1e-5f;
-
-// PyG's StdAggregation evaluates var = E[m^2] - E[m]^2 with rounded products (separate
-// torch kernels); these helpers keep the compiler from contracting them into FMAs
-// (the build uses -ffp-contract=fast), see the note in pna_fwd_kernel.
-__device__ __forceinline__ float add_sq_nofma(float acc, float m) {
-#pragma clang fp contract(off)
-  const float sq = m * m;
-  return acc + sq;
-}
-__device__ __forceinline__ float var_nofma(float s, float s2, float d, float& mean) {
-#pragma clang fp contract(off)
-  mean = s / d;
-  const float m2 = s2 / d;
-  const float mm = mean * mean;
-  return m2 - mm;
-}
 
 // AB: [N, ldab] with A at column offset 0 and B at column offset F.
 template <int VEC>
@@ -77,94 +32,8 @@ __global__ void __launch_bounds__(256) pna_fwd_kernel(
     const float* __restrict__ G, const int* __restrict__ src, const int* __restrict__ rowptr,
     float* __restrict__ Z, int* __restrict__ amin, int* __restrict__ amax, int N, int F, float avg_log,
     float avg_lin, int tpr, int rpb) {
-  const int n = blockIdx.x * rpb + threadIdx.x / tpr;
-  const int c = threadIdx.x % tpr;
-  if (n >= N) return;
-  const int beg = rowptr[n], end = rowptr[n + 1];
-  const int cnt = end - beg;
-  const float d = (float)max(cnt, 1);
-  const float lg = logf(d + 1.f);
-  const float sc[4] = {1.f, lg / avg_log, avg_log / lg, d / avg_lin};
-  const int ldz = 17 * F;
-  const int nv = F / VEC;
-  for (int v = c; v < nv; v += tpr) {
-    const int f0 = v * VEC;
-    const Vec<VEC> a = ld<VEC>(AB + (int64_t)n * ldab + f0);
-    Vec<VEC> s, s2, mn, mx;
-    int imn[VEC], imx[VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      s.v[i] = 0.f; s2.v[i] = 0.f; mn.v[i] = INFINITY; mx.v[i] = -INFINITY; imn[i] = -1; imx[i] = -1;
-    }
-    // edges in batches of EB: every source index, then every gathered row of the batch, is in
-    // flight together (one edge at a time paid two dependent memory latencies per edge:
-    // src[e], then AB[src[e]]); the statistics still fold edge by edge in CSR order
-    constexpr int EB = VEC == 1 ? 8 : 4;
-    for (int e0 = beg; e0 < end; e0 += EB) {
-      int js[EB];
-#pragma unroll
-      for (int k = 0; k < EB; ++k) js[k] = src[min(e0 + k, end - 1)];
-      Vec<VEC> b[EB], cc[EB], g[EB];
-#pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const int e = min(e0 + k, end - 1);
-        b[k] = ld<VEC>(AB + (int64_t)js[k] * ldab + F + f0);
-        if (C) cc[k] = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc[k].v[i] = 0.f; }
-        if (G) g[k] = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g[k].v[i] = 1.f; }
-      }
-#pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const int e = e0 + k;
-        if (e >= end) break;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          const float m = (a.v[i] + b[k].v[i] + cc[k].v[i]) * g[k].v[i];
-          s.v[i] += m;
-          s2.v[i] = add_sq_nofma(s2.v[i], m);  // no FMA: see the variance note below
-          if (m < mn.v[i]) { mn.v[i] = m; imn[i] = e; }
-          if (m > mx.v[i]) { mx.v[i] = m; imx[i] = e; }
-        }
-      }
-    }
-    // var = E[m^2] - E[m]^2 exactly as PyG's StdAggregation evaluates it (rounded products,
-    // true divisions, NO fused multiply-add).  The formula cancels catastrophically when the
-    // messages of a node are (nearly) equal; with FMA contraction the rounding error of m^2
-    // survives the cancellation (var = fl(m^2) - m^2 != 0 for a single neighbour), crosses
-    // the 1e-5 clamp for |m| >~ 20 and switches std from 0 to >= 3e-3 — a systematic
-    // forward difference that the trajectory bisection (tools/trajectory_bisect.py) traced
-    // as the only source of GPU-vs-CPU training drift.
-    Vec<VEC> mean, sd;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      const float var = var_nofma(s.v[i], s2.v[i], d, mean.v[i]);
-      float t = sqrtf(fmaxf(var, kStdEps));
-      sd.v[i] = (t <= sqrtf(kStdEps)) ? 0.f : t;
-      if (cnt == 0) { mn.v[i] = 0.f; mx.v[i] = 0.f; }
-    }
-    float* zr = Z + (int64_t)n * ldz;
-    st<VEC>(zr + f0, ld<VEC>(x + (int64_t)n * F + f0));
-#pragma unroll
-    for (int sidx = 0; sidx < 4; ++sidx) {
-      float* zb = zr + F + sidx * 4 * F + f0;
-      Vec<VEC> t0, t1, t2, t3;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        t0.v[i] = mean.v[i] * sc[sidx];
-        t1.v[i] = mn.v[i] * sc[sidx];
-        t2.v[i] = mx.v[i] * sc[sidx];
-        t3.v[i] = sd.v[i] * sc[sidx];
-      }
-      st<VEC>(zb, t0);
-      st<VEC>(zb + F, t1);
-      st<VEC>(zb + 2 * F, t2);
-      st<VEC>(zb + 3 * F, t3);
-    }
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      amin[(int64_t)n * F + f0 + i] = imn[i];
-      amax[(int64_t)n * F + f0 + i] = imx[i];
-    }
-  }
+  pna_fwd_node<VEC>(x, AB, ldab, C, G, src, rowptr, Z, amin, amax, blockIdx.x * rpb + threadIdx.x / tpr,
+                    threadIdx.x % tpr, N, F, avg_log, avg_lin, tpr);
 }
 
 template <int VEC>
@@ -188,13 +57,13 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
   for (int v = c; v < nv; v += tpr) {
     const int f0 = v * VEC;
     const float* dzr = dZ + (int64_t)n * ldz + F + f0;
-    Vec<VEC> dmean, dmin, dmax, dstd;
+    PVec<VEC> dmean, dmin, dmax, dstd;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) { dmean.v[i] = 0.f; dmin.v[i] = 0.f; dmax.v[i] = 0.f; dstd.v[i] = 0.f; }
 #pragma unroll
     for (int sidx = 0; sidx < 4; ++sidx) {
       const float* b = dzr + sidx * 4 * F;
-      const Vec<VEC> g0 = ld<VEC>(b), g1 = ld<VEC>(b + F), g2 = ld<VEC>(b + 2 * F), g3 = ld<VEC>(b + 3 * F);
+      const PVec<VEC> g0 = pld<VEC>(b), g1 = pld<VEC>(b + F), g2 = pld<VEC>(b + 2 * F), g3 = pld<VEC>(b + 3 * F);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         dmean.v[i] = fmaf(sc[sidx], g0.v[i], dmean.v[i]);
@@ -204,9 +73,9 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
       }
     }
     const float* zr = Z + (int64_t)n * ldz + F + f0;  // identity block
-    const Vec<VEC> mean = ld<VEC>(zr);
-    const Vec<VEC> sd = ld<VEC>(zr + 3 * F);
-    Vec<VEC> kstd;  // d std / d m_e = (m_e - mean) * kstd
+    const PVec<VEC> mean = pld<VEC>(zr);
+    const PVec<VEC> sd = pld<VEC>(zr + 3 * F);
+    PVec<VEC> kstd;  // d std / d m_e = (m_e - mean) * kstd
     int imn[VEC], imx[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -215,8 +84,8 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
       imn[i] = amin[(int64_t)n * F + f0 + i];
       imx[i] = amax[(int64_t)n * F + f0 + i];
     }
-    const Vec<VEC> a = ld<VEC>(AB + (int64_t)n * ldab + f0);
-    Vec<VEC> da;
+    const PVec<VEC> a = pld<VEC>(AB + (int64_t)n * ldab + f0);
+    PVec<VEC> da;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) da.v[i] = 0.f;
     // edge batches as in the forward: gathers of a batch in flight together (4 edges: the
@@ -226,19 +95,19 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
       int js[EB];
 #pragma unroll
       for (int k = 0; k < EB; ++k) js[k] = src[min(e0 + k, end - 1)];
-      Vec<VEC> b[EB], cc[EB], g[EB];
+      PVec<VEC> b[EB], cc[EB], g[EB];
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
         const int e = min(e0 + k, end - 1);
-        b[k] = ld<VEC>(AB + (int64_t)js[k] * ldab + F + f0);
-        if (C) cc[k] = ld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc[k].v[i] = 0.f; }
-        if (G) g[k] = ld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g[k].v[i] = 1.f; }
+        b[k] = pld<VEC>(AB + (int64_t)js[k] * ldab + F + f0);
+        if (C) cc[k] = pld<VEC>(C + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) cc[k].v[i] = 0.f; }
+        if (G) g[k] = pld<VEC>(G + (int64_t)e * F + f0); else { for (int i = 0; i < VEC; ++i) g[k].v[i] = 1.f; }
       }
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
         const int e = e0 + k;
         if (e >= end) break;
-        Vec<VEC> dp, dg;
+        PVec<VEC> dp, dg;
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           const float pre = a.v[i] + b[k].v[i] + cc[k].v[i];
@@ -250,11 +119,11 @@ __global__ void __launch_bounds__(256) pna_bwd_kernel(
           dg.v[i] = dm * pre;
           da.v[i] += dp.v[i];
         }
-        st<VEC>(dpre + (int64_t)e * F + f0, dp);
-        if (dG) st<VEC>(dG + (int64_t)e * F + f0, dg);
+        pst<VEC>(dpre + (int64_t)e * F + f0, dp);
+        if (dG) pst<VEC>(dG + (int64_t)e * F + f0, dg);
       }
     }
-    st<VEC>(dA + (int64_t)n * ldda + f0, da);
+    pst<VEC>(dA + (int64_t)n * ldda + f0, da);
   }
 }
 

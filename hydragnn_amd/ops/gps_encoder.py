@@ -288,6 +288,11 @@ class _GPSEncoder(torch.autograd.Function):
         x0 = ops.gf_embed_fwd(xin, pe, Wne, Wpe, Wnl, cfg.nv)
         # BN statistics sites: 3 fixed-point 64-bit words per statistic (deterministic integer
         # atomics, csrc/gps_fused.hip col_sum_add); zeroed by the first node launch
+        # the attention + PNA forward as one launch (fp32 quad-block attention, F = 64);
+        # HYDRA_GPS_ONE_LAUNCH=0: the two-stream form
+        one_launch = (cfg.a8 and not cfg.bf16 and cfg.splits <= 0 and F == 64
+                      and os.environ.get("HYDRA_ATTN8_QUAD", "1") != "0"
+                      and os.environ.get("HYDRA_GPS_ONE_LAUNCH", "1") == "1")
         acc = torch.empty(L, 3 * NREP * SITES * F, device=dev, dtype=torch.float64)
         saved = torch.empty(L, NSAVED, F, device=dev, dtype=torch.float32)
         st = []
@@ -312,6 +317,29 @@ class _GPSEncoder(torch.autograd.Function):
             x, AB = outs[0], outs[1]
             pk = outs[2:] if cfg.a8 else None
             qkv = None if cfg.a8 else outs[2]
+            if one_launch:
+                # attention + PNA aggregation as ONE launch on this stream (no fork / join:
+                # each hipGraph fork or join edge cost ~7 us on the layer's critical path)
+                if edge_pending:
+                    emain.wait_stream(estream)
+                    for t in [e, rbf, drdf, *Rl, *Gl, *Cs]:
+                        if t is not None:
+                            t.record_stream(emain)
+                    edge_pending = False
+                C = Cs[l] if hoist else ops.gf_edge_fwd(r, e, Wr, Wd, bc)
+                O, LSE, Z, amin, amax = ops.attn8_pna_fwd(pk[0], pk[2], pk[5], cfg.sid, cfg.sptr, x.shape[0],
+                                                          cfg.scale, x, AB, C, G, cfg.src.index, cfg.dst.rowptr,
+                                                          cfg.avg[l][0], cfg.avg[l][1])
+                z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
+                pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
+                n1, n2, _, _ = cfg.bns[l]
+                rm1, rv1, nb1, m1, e1 = _bn_state(n1)
+                rm2, rv2, nb2, m2, e2 = _bn_state(n2)
+                out, md, z3 = ops.gf_mlp_fwd(z1, z2, acc[l], saved[l], [g1, b1n, g2, b2n], rm1, rv1, nb1, rm2, rv2,
+                                             nb2, m1, e1, m2, e2, W1, b1, W2, b2, rng, s2, s3, p, nv)
+                st.append(dict(x=x, AB=AB, qkv=qkv, pk=pk, O=O, LSE=LSE, z2=z2, C=C, Z=Z, amin=amin, amax=amax,
+                               p=pl, z1=z1, out=out, md=md, z3=z3, Wab=Wab, Wr=Wr, Wd=Wd))
+                continue
             side = _Side(dev, cfg.side)
             with side:
                 side.used(x, *(pk if cfg.a8 else [qkv]))

@@ -10,6 +10,8 @@
                        (captured step: dense per-row branch select)
   5b multibranch_mace  the BASELINE.json variant of config 5 with MACE (hidden 64, l_max 2,
                        correlation 2, 3 layers), 5 branches, batch 32
+  qm9_schnet_gps       the reference QM9 example architecture: SchNet x 2 + GPS (8 heads)
+  oc20_gps_h128        config 4 at hidden 128 (16 heads)
 
 All synthetic data / random-init weights, fp32.  Prints one JSON line per config.
 Usage: python tools/bench_configs.py [names...] [--steps 20] [--warmup 5]
@@ -61,6 +63,34 @@ def qm9_schnet(dev):
     return m, s, 64, ["graph"], [1], False
 
 
+def qm9_schnet_gps(dev):
+    """The reference QM9 example's architecture (examples/qm9/qm9.json): SchNet hidden 64 x 2
+    layers + GPS multihead attention (8 heads, pe_dim 2), 10 gaussians, 8 filters, batch 64."""
+    from hydragnn_amd.data.transforms import laplacian_pe, relative_pe
+
+    s = _with_edges(molecules_like(1024, seed=1), 7.0, 5)
+    for k, g in enumerate(s):
+        g.pe = laplacian_pe(g.edge_index, g.num_nodes, 2, seed=k)
+        g.rel_pe = relative_pe(g.pe, g.edge_index)
+    heads = {"graph": _gheads(1, [50, 25], 5)}
+    m = create_model("SchNet", 1, 64, [1], 2, "GPS", "multihead", 8, ["graph"], heads, "relu", "mse", [1.0], 2,
+                     num_gaussians=10, num_filters=8, radius=7.0, max_neighbours=5, dropout=0.0)
+    return m, s, 64, ["graph"], [1], False
+
+
+def oc20_gps_h128(dev):
+    """BASELINE config 4 (OC20 PNAPlus + GPS, bench.py) at hidden 128 (16 heads of 8)."""
+    from hydragnn_amd.data.synthetic import oc20_like
+
+    s = oc20_like(512, seed=1000, radius=10.0, max_neighbours=10, pe_dim=16)
+    deg = degree_histogram(s, max_degree=10).to(torch.float64)
+    heads = {"graph": _gheads(1, [50, 25], 50)}
+    m = create_model("PNAPlus", 4, 128, [1], 16, "GPS", "multihead", 16, ["graph"], heads, "relu", "mae", [1.0], 3,
+                     pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=10.0, max_neighbours=10,
+                     dropout=0.0)
+    return m, s, 32, ["graph"], [1], False
+
+
 def md17_painn_forces(dev):
     s = _with_edges(md_trajectory(1024, seed=2, num_atoms=21), 5.0, 20)
     heads = {"node": _nheads(1, [64, 32])}
@@ -95,7 +125,7 @@ def multibranch_mace(dev):
 
 
 CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
-           "multibranch_mace": multibranch_mace}
+           "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128}
 
 
 def _targets_for_store(samples, head_types):
