@@ -324,13 +324,13 @@ struct OprojFwd {
   int N;
 };
 
-template <int F>
-__global__ void __launch_bounds__(256) oproj_fwd_kernel(OprojFwd a) {
+template <int F, int NT = 256>
+__device__ __forceinline__ void oproj_fwd_body(const OprojFwd& a, int bid) {
   constexpr int LD = F + 4;
   __shared__ __attribute__((aligned(16))) float os[BM * LD];
   const int nv = a.nvp ? min(*a.nvp, a.N) : a.N;
-  const int row0 = blockIdx.x * BM;
-  for (int idx = threadIdx.x; idx < BM * F / 4; idx += 256) {
+  const int row0 = bid * BM;
+  for (int idx = threadIdx.x; idx < BM * F / 4; idx += NT) {
     const int r = idx / (F / 4), c = (idx % (F / 4)) * 4, row = row0 + r;
     *reinterpret_cast<float4*>(os + r * LD + c) =
         row < a.N ? *reinterpret_cast<const float4*>(a.o + (int64_t)row * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -354,6 +354,11 @@ __global__ void __launch_bounds__(256) oproj_fwd_kernel(OprojFwd a) {
   }
 }
 
+template <int F>
+__global__ void __launch_bounds__(256) oproj_fwd_kernel(OprojFwd a) {
+  oproj_fwd_body<F>(a, blockIdx.x);
+}
+
 // ------------------------------------------------------------------------------------
 // Forward 3 (main): p = Z Wpost^T + bpost ; z1 = drop(p Wlin^T + blin) + x ; BN1 statistics.
 // 512 threads: waves w and w + 4 split the 17F-deep product in halves (folded through LDS).
@@ -373,13 +378,13 @@ struct PostFwd {
 };
 
 template <int F>
-__global__ void __launch_bounds__(512) post_fwd_kernel(PostFwd a) {
+__device__ __forceinline__ void post_fwd_body(const PostFwd& a, int bid) {
   constexpr int K = 17 * F, LDZ = K + 4, LD = F + 4;
   __shared__ __attribute__((aligned(16))) float zs[BM * LDZ];
   __shared__ __attribute__((aligned(16))) float ps[BM * LD];
   __shared__ f4v red[4][64];
   const int nv = a.nvp ? min(*a.nvp, a.N) : a.N;
-  const int row0 = blockIdx.x * BM;
+  const int row0 = bid * BM;
   for (int idx = threadIdx.x; idx < BM * K / 4; idx += 512) {
     const int r = idx / (K / 4), c = (idx % (K / 4)) * 4, row = row0 + r;
     *reinterpret_cast<float4*>(zs + r * LDZ + c) =
@@ -426,6 +431,22 @@ __global__ void __launch_bounds__(512) post_fwd_kernel(PostFwd a) {
     }
     stats2(q, row0, nv, a.site, F, col);
   }
+}
+
+template <int F>
+__global__ void __launch_bounds__(512) post_fwd_kernel(PostFwd a) {
+  post_fwd_body<F>(a, blockIdx.x);
+}
+
+// The output projection and the local post-NN of a layer in one launch (both read only the
+// outputs of the attention + PNA launch; one dispatch and one tail instead of two in a row):
+// workgroups [0, nP) run post_fwd, the rest oproj_fwd (its loops stride 512 threads).
+template <int F>
+__global__ void __launch_bounds__(512) oproj_post_fwd_kernel(PostFwd pa, OprojFwd oa, int nP) {
+  if ((int)blockIdx.x < nP)
+    post_fwd_body<F>(pa, blockIdx.x);
+  else
+    oproj_fwd_body<F, 512>(oa, blockIdx.x - nP);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1505,6 +1526,36 @@ at::Tensor gf_oproj_fwd(const at::Tensor& o, const at::Tensor& Wo, const at::Ten
   return z2;
 }
 
+// oproj + post in one launch (oproj_post_fwd_kernel): returns [z2, p, z1]
+std::vector<at::Tensor> gf_oproj_post_fwd(const at::Tensor& o, const at::Tensor& Wo, const at::Tensor& bo,
+                                          const at::Tensor& Z, const at::Tensor& Wp, const at::Tensor& bp,
+                                          const at::Tensor& Wl, const at::Tensor& bl, const at::Tensor& x,
+                                          const at::Tensor& acc, const c10::optional<at::Tensor>& rng, int64_t salt1,
+                                          int64_t salt0, double p, const c10::optional<at::Tensor>& nv) {
+  const int64_t N = x.size(0), F = x.size(1);
+  chk(o, N, F, "o");
+  chk(x, N, F, "x");
+  chk(Wo, F, F, "Wo");
+  chk(Z, N, 17 * F, "Z");
+  chk(Wp, F, 17 * F, "Wpost");
+  chk(Wl, F, F, "Wlin");
+  auto z2 = at::empty({N, F}, x.options()), pp = at::empty({N, F}, x.options()), z1 = at::empty({N, F}, x.options());
+  if (N == 0) return {z2, pp, z1};
+  OprojFwd oa{o.data_ptr<float>(), Wo.data_ptr<float>(), bo.data_ptr<float>(), x.data_ptr<float>(),
+              z2.data_ptr<float>(), site_ptr(acc, 1, (int)F), mk_drop(rng, salt1, p), nvptr(nv), (int)N};
+  PostFwd pa{Z.data_ptr<float>(), Wp.data_ptr<float>(), bp.data_ptr<float>(), Wl.data_ptr<float>(),
+             bl.data_ptr<float>(), x.data_ptr<float>(), pp.data_ptr<float>(), z1.data_ptr<float>(),
+             site_ptr(acc, 0, (int)F), mk_drop(rng, salt0, p), nvptr(nv), (int)N};
+  const int nb = ceil_div(N, BM);
+  if (F == 64)
+    oproj_post_fwd_kernel<64><<<2 * nb, 512, 0, stream()>>>(pa, oa, nb);
+  else if (F == 32)
+    oproj_post_fwd_kernel<32><<<2 * nb, 512, 0, stream()>>>(pa, oa, nb);
+  else
+    HY_CHECK(false, "gps_fused: hidden dim must be 32 or 64, got ", F);
+  return {z2, pp, z1};
+}
+
 std::vector<at::Tensor> gf_post_fwd(const at::Tensor& Z, const at::Tensor& Wp, const at::Tensor& bp,
                                     const at::Tensor& Wl, const at::Tensor& bl, const at::Tensor& x,
                                     const at::Tensor& acc, const c10::optional<at::Tensor>& rng, int64_t salt, double p,
@@ -1982,6 +2033,9 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
       "float eps4, Tensor? nv, Tensor? gptr) -> Tensor[]");
   m.def("gf_embed_fwd(Tensor A, Tensor B, Tensor Wa, Tensor Wb, Tensor Wl, Tensor? nv) -> Tensor");
   m.def("gf_finish(Tensor[] wp, Tensor[] em, Tensor? dfw, Tensor[]? gouts=None) -> Tensor[]");
+  m.def(
+      "gf_oproj_post_fwd(Tensor o, Tensor Wo, Tensor bo, Tensor Z, Tensor Wp, Tensor bp, Tensor Wl, Tensor bl, "
+      "Tensor x, Tensor(a!) acc, Tensor? rng, int salt1, int salt0, float p, Tensor? nv) -> Tensor[]");
   m.def("gf_edge_fwd(Tensor r, Tensor e, Tensor Wr, Tensor Wd, Tensor bc) -> Tensor");
   m.def("gf_edge_fwd_multi(Tensor[] r, Tensor e, Tensor[] Wr, Tensor[] Wd, Tensor[] bc) -> Tensor[]");
   m.def(
@@ -2013,6 +2067,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("gf_final_fwd", hy::gf::gf_final_fwd);
   m.impl("gf_embed_fwd", hy::gf::gf_embed_fwd);
   m.impl("gf_finish", hy::gf::gf_finish);
+  m.impl("gf_oproj_post_fwd", hy::gf::gf_oproj_post_fwd);
   m.impl("gf_edge_fwd", hy::gf::gf_edge_fwd);
   m.impl("gf_edge_fwd_multi", hy::gf::gf_edge_fwd_multi);
   m.impl("gf_edge_bwd", hy::gf::gf_edge_bwd);

@@ -330,8 +330,8 @@ class _GPSEncoder(torch.autograd.Function):
                 O, LSE, Z, amin, amax = ops.attn8_pna_fwd(pk[0], pk[2], pk[5], cfg.sid, cfg.sptr, x.shape[0],
                                                           cfg.scale, x, AB, C, G, cfg.src.index, cfg.dst.rowptr,
                                                           cfg.avg[l][0], cfg.avg[l][1])
-                z2 = ops.gf_oproj_fwd(O, Wo, bo, x, acc[l], rng, s1, p, nv)
-                pl, z1 = ops.gf_post_fwd(Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s0, p, nv)
+                z2, pl, z1 = ops.gf_oproj_post_fwd(O, Wo, bo, Z, Wpost, bpost, Wlin, blin, x, acc[l], rng, s1, s0,
+                                                   p, nv)
                 n1, n2, _, _ = cfg.bns[l]
                 rm1, rv1, nb1, m1, e1 = _bn_state(n1)
                 rm2, rv2, nb2, m2, e2 = _bn_state(n2)
