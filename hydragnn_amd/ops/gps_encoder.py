@@ -440,6 +440,11 @@ class _GPSEncoder(torch.autograd.Function):
             wstream = _streams.side_stream(dev, 2)
         lo = 0
         edge_ev = None
+        # HYDRA_GPS_ATTN_MAIN=1: the attention branch on the main stream and the local chain on
+        # the side stream (measured 0.990 vs 0.917 ms/step on MI355X: the runtime's queue
+        # mapping then put the attention beside the weight-gradient launches); default: the
+        # attention branch on the side stream
+        attn_main = cfg.side and os.environ.get("HYDRA_GPS_ATTN_MAIN", "0") == "1"
         for l in reversed(range(L)):
             s = st[l]
             (Win, bin_, Wo, bo, Wpre, bpre, Wenc, benc, Wpost, bpost, Wlin, blin,
@@ -450,9 +455,7 @@ class _GPSEncoder(torch.autograd.Function):
             dg, dpre, dout, dw3, db3, dw4, db4 = ops.gf_mlp_bwd(g, s["z3"], acc[l], saved[l], g3, g4, float(n3.eps),
                                                                float(n4.eps), s["md"], W2, W1, s["z1"], s["z2"], rng,
                                                                s2, s3, p, nv, gsl(P[16], P[17], P[18], P[19]))
-            side = _Side(dev, cfg.side)
-            with side:
-                side.used(dout)
+            def attn_branch():
                 if cfg.a8 and cfg.splits <= 0:
                     # the attention backward's operands (-delta, dO in the pair / quad layouts)
                     # come out of the output-projection backward's epilogue: no packing launch
@@ -473,47 +476,93 @@ class _GPSEncoder(torch.autograd.Function):
                                                              None, gsl(P[14], P[15]))
                     dqkv = ops.attn_bwd(dO, s["qkv"], s["O"], s["LSE"], cfg.sid, cfg.sptr, cfg.heads, cfg.scale,
                                         cfg.span, cfg.splits)
-            dz1, dq, dp, dZ, dw1n, db1n = ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p,
-                                                         nv, gsl(P[12], P[13]))
-            if wside and lo < len(dys):
-                # the previous layer's weight gradients: enqueued here so they run beside this
-                # layer's attention backward (long, matrix-core bound) rather than beside the
-                # short node / MLP / delta kernels that lead into it (the critical path)
-                wstream.wait_stream(wmain)
-                with torch.cuda.stream(wstream):
-                    ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
-                lo = len(dys)
-            dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], Gl[l], cfg.src.index, cfg.dst.rowptr,
-                                      s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
-            ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
-            # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch.
-            # Nothing of the layer chain reads them (only weight gradients and the embedding /
-            # radial backward at the end): with the weight-gradient stream it runs there, off
-            # the local branch's critical path
-            if wside and l > 0:
-                wstream.wait_stream(wmain)
-                with torch.cuda.stream(wstream):
+                return dz2, da, dO, dqkv, dw2n, db2n
+
+            def loc_bwd():
+                return ops.gf_loc_bwd(dout, s["z1"], acc[l], saved[l], g1, Wlin, Wpost, rng, s0, p, nv,
+                                      gsl(P[12], P[13]))
+
+            def pna_branch():
+                dE, dG, dAB = ops.pna_bwd(dZ, s["Z"], s["AB"], s["C"], Gl[l], cfg.src.index, cfg.dst.rowptr,
+                                          s["amin"], s["amax"], cfg.avg[l][0], cfg.avg[l][1])
+                ops.seg_sum_out(dE, cfg.src.rowptr, cfg.src.perm, dAB[:, F:])
+                return dE, dG, dAB
+
+            def wgrad_prev():
+                nonlocal lo
+                if wside and lo < len(dys):
+                    # the previous layer's weight gradients: enqueued here so they run beside this
+                    # layer's attention backward (long, matrix-core bound) rather than beside the
+                    # short node / MLP / delta kernels that lead into it (the critical path)
+                    wstream.wait_stream(wmain)
+                    with torch.cuda.stream(wstream):
+                        ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+                    lo = len(dys)
+
+            def edge_launch(after):
+                # dr (masked by the radial ReLU), de += dC Wd, drbf += dr Wemb + dG Wlin: one launch.
+                # Nothing of the layer chain reads them (only weight gradients and the embedding /
+                # radial backward at the end): with the weight-gradient stream it runs there, off
+                # the local branch's critical path.  ``after``: the event of the local chain
+                nonlocal de, drbf, edge_ev
+                if wside and l > 0:
+                    wstream.wait_event(after)
+                    with torch.cuda.stream(wstream):
+                        dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+                    edge_ev = torch.cuda.Event()
+                    edge_ev.record(wstream)
+                elif wside:
+                    # the first layer's: the weight-gradient stream is still busy with layer 1's
+                    # weight gradients, so a fourth stream runs it beside the attention backward,
+                    # behind the previous edge launch (accumulated de / drbf) through an event
+                    e3 = _streams.side_stream(dev, 3)
+                    e3.wait_event(after)
+                    if edge_ev is not None:
+                        e3.wait_event(edge_ev)
+                    with torch.cuda.stream(e3):
+                        dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
+                    edge_ev = torch.cuda.Event()
+                    edge_ev.record(e3)
+                else:
                     dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
-                edge_ev = torch.cuda.Event()
-                edge_ev.record(wstream)
-            elif wside:
-                # the first layer's: the weight-gradient stream is still busy with layer 1's
-                # weight gradients, so a fourth stream runs it beside the attention backward,
-                # behind the previous edge launch (accumulated de / drbf) through an event
-                e3 = _streams.side_stream(dev, 3)
-                e3.wait_stream(wmain)
-                if edge_ev is not None:
-                    e3.wait_event(edge_ev)
-                with torch.cuda.stream(e3):
-                    dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
-                edge_ev = torch.cuda.Event()
-                edge_ev.record(e3)
+                return dr
+
+            if attn_main:
+                # the attention branch (the long one) stays on the main stream: a hipGraph fork
+                # delays the branch it starts and a join the node that waits (~7 us each, see
+                # tools/graph_fork_cost.py), so the local chain (loc -> PNA -> dB segment sum,
+                # shorter) takes the side stream and its join is ready when attention ends
+                loc = _Side(dev, True)
+                with loc:
+                    loc.used(dout)
+                    dz1, dq, dp, dZ, dw1n, db1n = loc_bwd()
+                    dE, dG, dAB = pna_branch()
+                    lev = torch.cuda.Event()
+                    lev.record(loc.side)
+                wgrad_prev()
+                dz2, da, dO, dqkv, dw2n, db2n = attn_branch()
+                if wside:
+                    dr = edge_launch(lev)
+                loc.join(dz1, dq, dp, dZ, dw1n, db1n, dE, dG, dAB)
+                if not wside:
+                    dr = edge_launch(None)
             else:
-                dr, de, drbf = ops.gf_edge_bwd(dE, s["Wr"], s["Wd"], Rl[l], de, dG, Wemb, Wrl, drbf, K)
-            # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
-            # MI355X: the attention passes are throughput-bound once they overlap the local
-            # branch, 209 vs 200 us per layer)
-            side.join(dz2, da, dO, dqkv, dw2n, db2n)
+                side = _Side(dev, cfg.side)
+                with side:
+                    side.used(dout)
+                    dz2, da, dO, dqkv, dw2n, db2n = attn_branch()
+                dz1, dq, dp, dZ, dw1n, db1n = loc_bwd()
+                wgrad_prev()
+                dE, dG, dAB = pna_branch()
+                mev = None
+                if wside:
+                    mev = torch.cuda.Event()
+                    mev.record(wmain)
+                dr = edge_launch(mev)
+                # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
+                # MI355X: the attention passes are throughput-bound once they overlap the local
+                # branch, 209 vs 200 us per layer)
+                side.join(dz2, da, dO, dqkv, dw2n, db2n)
             if l > 0:
                 sp = st[l - 1]
                 g = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], sp["z3"], saved[l - 1], acc[l - 1],

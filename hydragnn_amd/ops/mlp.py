@@ -158,9 +158,11 @@ class _HeadLoss(torch.autograd.Function):
         step's flat gradient slots — overlapped with the encoder's backward."""
         ops = _native.ops()
         Ws, bs = params[0::2], params[1::2]
-        dx = ops.head_loss_dx(x, Ws, bs, relu, target, mask, kind)
         main = torch.cuda.current_stream(x.device)
         side = _streams.side_stream(x.device, 4)
+        # the twin is forked BEFORE the dx launch: a hipGraph node with two successors on
+        # different streams delays both (~7 us), and the dx launch's successor is the encoder
+        # backward (the critical path)
         side.wait_stream(main)
         for t in (x, target, mask):
             if t is not None:
@@ -169,6 +171,7 @@ class _HeadLoss(torch.autograd.Function):
             out = ops.head_loss_fused(x, Ws, bs, relu, target, mask, kind, None, sl, False)
         ev = torch.cuda.Event()
         ev.record(side)
+        dx = ops.head_loss_dx(x, Ws, bs, relu, target, mask, kind)
         stats, pred = out[0], out[1]
         # loss / predictions are read after the step's gradient join (finish): the main stream
         # waits for the side stream there; until then keep their memory out of reuse
