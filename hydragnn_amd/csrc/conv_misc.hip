@@ -354,6 +354,7 @@ at::Tensor scaled_silu_fwd(const at::Tensor& x_, double s) {
   auto x = x_.contiguous();
   HY_CHECK_F32(x);
   HY_CHECK(x.numel() % 4 == 0, "scaled_silu: numel must be a multiple of 4");
+  HY_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "scaled_silu: x must be 16-byte aligned (float4)");
   auto y = at::empty_like(x);
   const int64_t n4 = x.numel() / 4;
   if (n4 > 0)
@@ -369,6 +370,8 @@ at::Tensor scaled_silu_bwd(const at::Tensor& g_, const at::Tensor& x_, double s)
   HY_CHECK_F32(g);
   HY_CHECK_F32(x);
   HY_CHECK(g.numel() == x.numel() && x.numel() % 4 == 0, "scaled_silu_bwd: shapes");
+  HY_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+           "scaled_silu_bwd: g and x must be 16-byte aligned (float4)");
   auto dx = at::empty_like(x);
   const int64_t n4 = x.numel() / 4;
   if (n4 > 0)

@@ -440,6 +440,11 @@ class _GPSEncoder(torch.autograd.Function):
             wstream = _streams.side_stream(dev, 2)
         lo = 0
         edge_ev = None
+        # layer 0's ready weight gradients on the edge stream during its attention backward
+        # (HYDRA_EARLY_WGRAD=0: all of them at the end)
+        early0 = wside and os.environ.get("HYDRA_EARLY_WGRAD", "1") == "1"
+        early_done = False
+        gw0 = dfreq_w = te = None
         # HYDRA_GPS_ATTN_MAIN=1: the attention branch on the main stream and the local chain on
         # the side stream (measured 0.990 vs 0.917 ms/step on MI355X: the runtime's queue
         # mapping then put the attention beside the weight-gradient launches); default: the
@@ -455,6 +460,8 @@ class _GPSEncoder(torch.autograd.Function):
             dg, dpre, dout, dw3, db3, dw4, db4 = ops.gf_mlp_bwd(g, s["z3"], acc[l], saved[l], g3, g4, float(n3.eps),
                                                                float(n4.eps), s["md"], W2, W1, s["z1"], s["z2"], rng,
                                                                s2, s3, p, nv, gsl(P[16], P[17], P[18], P[19]))
+            att_ev = [None]
+
             def attn_branch():
                 if cfg.a8 and cfg.splits <= 0:
                     # the attention backward's operands (-delta, dO in the pair / quad layouts)
@@ -462,6 +469,8 @@ class _GPSEncoder(torch.autograd.Function):
                     pk = s["pk"]
                     dz2, da, _, dw2n, db2n, nd, dOp, dOq = ops.gf_att_bwd(dout, s["z2"], acc[l], saved[l], g2, Wo, rng,
                                                                           s1, p, nv, s["O"], gsl(P[14], P[15]))
+                    att_ev[0] = torch.cuda.Event()
+                    att_ev[0].record()  # da ready (the early weight gradients of layer 0 wait on it)
                     dqkv = ops.attn8_bwd_packed(nd, dOp, dOq, s["LSE"], pk[0], pk[1], pk[2], pk[3], pk[4], cfg.sid,
                                                 cfg.sptr, s["x"].shape[0], cfg.scale, cfg.bf16)
                     dO = None
@@ -559,6 +568,32 @@ class _GPSEncoder(torch.autograd.Function):
                     mev = torch.cuda.Event()
                     mev.record(wmain)
                 dr = edge_launch(mev)
+                if early0 and l == 0 and att_ev[0] is not None:
+                    # layer 0's weight gradients whose factors are ready (all but Win's dqkv and the
+                    # node embedding's dx0), the edge embeddings' and dfreq: one grouped launch on
+                    # the first layer's edge stream, beside the attention backward, instead of on
+                    # the main stream after the last node launch (the step's tail)
+                    gw0 = {}
+                    gw0["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
+                    gw0["Wrl"] = item(dG, rbf, Wrl, False, P[26])
+                    gw0["Wo"] = item(da, s["O"], Wo, True, P[2], P[3])
+                    gw0["Wab"] = item(dAB, s["x"], s["Wab"], False)
+                    gw0["Wr"] = item(dE, Rl[l], s["Wr"], True)
+                    gw0["Wd"] = item(dE, e, s["Wd"], False)
+                    gw0["Wpost"] = item(dp, s["Z"], Wpost, True, P[8], P[9])
+                    gw0["Wlin"] = item(dq, s["p"], Wlin, True, P[10], P[11])
+                    gw0["W1"] = item(dpre, s["out"], W1, True, P[20], P[21])
+                    gw0["W2"] = item(dg, s["md"], W2, True, P[22], P[23])
+                    dfreq_w = item(drbf, drdf, (K, K), False)[0] if ctx.freq_grad else None
+                    te = [item(de, eattr, (F, eattr.shape[1]), False)[0], item(de, rpe, (F, rpe.shape[1]), False)[0]]
+                    e3 = _streams.side_stream(dev, 3)  # holds the layer's edge launch (de / drbf final)
+                    e3.wait_event(att_ev[0])
+                    with torch.cuda.stream(e3):
+                        ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+                    lo = len(dys)
+                    edge_ev = torch.cuda.Event()
+                    edge_ev.record(e3)
+                    early_done = True
                 # (fanning the dQ and dK/dV passes out onto two more streams measured slower on
                 # MI355X: the attention passes are throughput-bound once they overlap the local
                 # branch, 209 vs 200 us per layer)
@@ -570,18 +605,22 @@ class _GPSEncoder(torch.autograd.Function):
             else:
                 dx0 = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], None, None, None, nv)
             base = NP * l
-            gw = {}
-            gw["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
-            gw["Wrl"] = item(dG, rbf, Wrl, False, P[26])
-            gw["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
-            gw["Wo"] = item(da, s["O"], Wo, True, P[2], P[3])
-            gw["Wab"] = item(dAB, s["x"], s["Wab"], False)
-            gw["Wr"] = item(dE, Rl[l], s["Wr"], True)
-            gw["Wd"] = item(dE, e, s["Wd"], False)
-            gw["Wpost"] = item(dp, s["Z"], Wpost, True, P[8], P[9])
-            gw["Wlin"] = item(dq, s["p"], Wlin, True, P[10], P[11])
-            gw["W1"] = item(dpre, s["out"], W1, True, P[20], P[21])
-            gw["W2"] = item(dg, s["md"], W2, True, P[22], P[23])
+            if early_done and l == 0:
+                gw = gw0
+                gw["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
+            else:
+                gw = {}
+                gw["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
+                gw["Wrl"] = item(dG, rbf, Wrl, False, P[26])
+                gw["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
+                gw["Wo"] = item(da, s["O"], Wo, True, P[2], P[3])
+                gw["Wab"] = item(dAB, s["x"], s["Wab"], False)
+                gw["Wr"] = item(dE, Rl[l], s["Wr"], True)
+                gw["Wd"] = item(dE, e, s["Wd"], False)
+                gw["Wpost"] = item(dp, s["Z"], Wpost, True, P[8], P[9])
+                gw["Wlin"] = item(dq, s["p"], Wlin, True, P[10], P[11])
+                gw["W1"] = item(dpre, s["out"], W1, True, P[20], P[21])
+                gw["W2"] = item(dg, s["md"], W2, True, P[22], P[23])
             wg.append((l, gw))
             grads[base + 12], grads[base + 13] = dw1n, db1n
             grads[base + 14], grads[base + 15] = dw2n, db2n
@@ -595,10 +634,12 @@ class _GPSEncoder(torch.autograd.Function):
             for t in (dr, de, drbf):
                 if t is not None:
                     t.record_stream(wmain)
-        dfreq_w = item(drbf, drdf, (K, K), False)[0] if ctx.freq_grad else None
+        if not early_done:
+            dfreq_w = item(drbf, drdf, (K, K), False)[0] if ctx.freq_grad else None
         # embeddings: only the narrow products dy^T [A | B] (see csrc/gps_fused.hip, EmbFwd)
         tn = [item(dx0, xin, (F, xin.shape[1]), False)[0], item(dx0, pe, (F, pe.shape[1]), False)[0]]
-        te = [item(de, eattr, (F, eattr.shape[1]), False)[0], item(de, rpe, (F, rpe.shape[1]), False)[0]]
+        if not early_done:
+            te = [item(de, eattr, (F, eattr.shape[1]), False)[0], item(de, rpe, (F, rpe.shape[1]), False)[0]]
         # every weight gradient of the stack (incl. the radial basis and its frequencies): one
         # grouped launch pair
         ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))

@@ -447,6 +447,9 @@ class _ScaledSilu(torch.autograd.Function):
         from .. import _native
 
         (x,) = ctx.saved_tensors
+        g = g.contiguous()
+        if g.data_ptr() % 16:  # the kernel reads float4s: a sliced view can be misaligned
+            g = g.clone()
         return _native.ops().scaled_silu_bwd(g, x, ctx.s), None
 
 
@@ -454,7 +457,9 @@ def scaled_silu(x, s):
     from . import pna as _mode
 
     if x.is_cuda and x.dtype == torch.float32 and x.numel() % 4 == 0 and _mode.fused("mlp"):
-        return _ScaledSilu.apply(x.contiguous(), float(s))
+        xc = x.contiguous()
+        if xc.data_ptr() % 16 == 0:  # float4 loads (a contiguous row slice can start mid-vector)
+            return _ScaledSilu.apply(xc, float(s))
     return torch.nn.functional.silu(x * s)
 
 
