@@ -31,6 +31,7 @@ struct SbfArgs {
   int T, n, K;
   float inv_cut, pa, pb, pc;
   int p;             // envelope exponent + 1
+  const int* limit;  // optional device scalar: triplets at or past it are padding (zero basis)
 };
 
 __device__ __forceinline__ void envelope(double x, int p, double a, double b, double c, double& u, double& du) {
@@ -69,6 +70,11 @@ __device__ __forceinline__ void geom(const SbfArgs& a, int t, float3& v1, float3
 __global__ void sbf_fwd_kernel(SbfArgs a, float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.T) return;
+  float* o = out + (int64_t)t * a.n * a.K;
+  if (a.limit && t >= *a.limit) {
+    for (int q = 0; q < a.n * a.K; ++q) o[q] = 0.f;
+    return;
+  }
   float3 v1, v2;
   double d, ct, n1, n2;
   geom(a, t, v1, v2, d, ct, n1, n2);
@@ -78,7 +84,6 @@ __global__ void sbf_fwd_kernel(SbfArgs a, float* __restrict__ out) {
   P[0] = 1.0;
   if (a.n > 1) P[1] = ct;
   for (int l = 1; l + 1 < a.n; ++l) P[l + 1] = ((2 * l + 1) * ct * P[l] - l * P[l - 1]) / (l + 1);
-  float* o = out + (int64_t)t * a.n * a.K;
   double j[MAXL + 1];
   for (int l = 0; l < a.n; ++l) {
     const double cb = sqrt((2 * l + 1) / (4.0 * M_PI)) * P[l];
@@ -96,7 +101,7 @@ __global__ void sbf_fwd_kernel(SbfArgs a, float* __restrict__ out) {
 
 __global__ void sbf_bwd_kernel(SbfArgs a, const float* __restrict__ gout, float* __restrict__ dvec) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.T) return;
+  if (t >= a.T || (a.limit && t >= *a.limit)) return;
   float3 v1, v2;
   double d, ct, n1, n2;
   geom(a, t, v1, v2, d, ct, n1, n2);
@@ -166,7 +171,8 @@ __global__ void sbf_bwd_kernel(SbfArgs a, const float* __restrict__ gout, float*
 using namespace dn;
 
 static SbfArgs sbf_args(const at::Tensor& vec, const at::Tensor& kj, const at::Tensor& ji, const at::Tensor& z,
-                        const at::Tensor& nrm, double cutoff, int64_t exponent) {
+                        const at::Tensor& nrm, double cutoff, int64_t exponent,
+                        const c10::optional<at::Tensor>& limit) {
   HY_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() && vec.dim() == 2 &&
                vec.size(1) == 3,
            "sbf: vec [E, 3] fp32");
@@ -190,20 +196,28 @@ static SbfArgs sbf_args(const at::Tensor& vec, const at::Tensor& kj, const at::T
   a.pa = (float)(-(a.p + 1) * (a.p + 2) / 2.0);
   a.pb = (float)(a.p * (a.p + 2));
   a.pc = (float)(-a.p * (a.p + 1) / 2.0);
+  a.limit = nullptr;
+  if (limit.has_value() && limit->defined()) {
+    HY_CHECK(limit->is_cuda() && limit->scalar_type() == at::kInt && limit->numel() == 1,
+             "sbf: limit must be a device int32 scalar");
+    a.limit = limit->data_ptr<int>();
+  }
   return a;
 }
 
 at::Tensor dimenet_sbf_fwd(const at::Tensor& vec, const at::Tensor& kj, const at::Tensor& ji, const at::Tensor& z,
-                           const at::Tensor& nrm, double cutoff, int64_t exponent) {
-  SbfArgs a = sbf_args(vec, kj, ji, z, nrm, cutoff, exponent);
+                           const at::Tensor& nrm, double cutoff, int64_t exponent,
+                           const c10::optional<at::Tensor>& limit) {
+  SbfArgs a = sbf_args(vec, kj, ji, z, nrm, cutoff, exponent, limit);
   auto out = at::empty({(int64_t)a.T, (int64_t)a.n * a.K}, vec.options());
   if (a.T) sbf_fwd_kernel<<<ceil_div(a.T, 128), 128, 0, stream()>>>(a, out.data_ptr<float>());
   return out;
 }
 
 at::Tensor dimenet_sbf_bwd(const at::Tensor& gout, const at::Tensor& vec, const at::Tensor& kj, const at::Tensor& ji,
-                           const at::Tensor& z, const at::Tensor& nrm, double cutoff, int64_t exponent) {
-  SbfArgs a = sbf_args(vec, kj, ji, z, nrm, cutoff, exponent);
+                           const at::Tensor& z, const at::Tensor& nrm, double cutoff, int64_t exponent,
+                           const c10::optional<at::Tensor>& limit) {
+  SbfArgs a = sbf_args(vec, kj, ji, z, nrm, cutoff, exponent, limit);
   HY_CHECK(gout.scalar_type() == at::kFloat && gout.is_contiguous() && gout.numel() == (int64_t)a.T * a.n * a.K,
            "sbf_bwd: gout [T, n*K]");
   auto dvec = at::zeros_like(vec);
@@ -214,10 +228,10 @@ at::Tensor dimenet_sbf_bwd(const at::Tensor& gout, const at::Tensor& vec, const 
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("dimenet_sbf_fwd(Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent) -> Tensor");
+  m.def("dimenet_sbf_fwd(Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent, Tensor? limit=None) -> Tensor");
   m.def(
-      "dimenet_sbf_bwd(Tensor gout, Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent) "
-      "-> Tensor");
+      "dimenet_sbf_bwd(Tensor gout, Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent, "
+      "Tensor? limit=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

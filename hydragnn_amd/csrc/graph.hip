@@ -557,9 +557,96 @@ std::tuple<at::Tensor, at::Tensor> radius_static_fill(const at::Tensor& pos_, co
   return {src, dst};
 }
 
+// ------------------------------------------------------------------ static-capacity triplets
+// Capturable DimeNet triplets for a statically padded batch (the eager builder above needs
+// the host to learn T before it can allocate).  Only edges whose receiver is a valid node
+// emit triplets (padding edges join padding nodes, which every layer zeroes), in the
+// eager order: grouped by e_ji ascending, k ascending.  The index arrays have a fixed
+// capacity Tcap (an upper bound the data store derives from its per-graph triplet counts);
+// slots [T, Tcap) are dummy triplets of the last edge (kj = ji = E-1): they sort last in
+// both CSR views, their basis rows are zeroed by the sbf kernels (device limit), and the
+// segment sums stop at T.
+__global__ void __launch_bounds__(256) tri_static_count_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                               const int* __restrict__ rowptr,
+                                                               const bool* __restrict__ mask, int E,
+                                                               int* __restrict__ counts) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int j = src[e], i = dst[e];
+  int c = 0;
+  if (mask == nullptr || mask[i]) {
+    const int en = rowptr[j + 1];
+    for (int k = rowptr[j]; k < en; ++k) c += src[k] != i;
+  }
+  counts[e] = c;
+}
+
+__global__ void __launch_bounds__(256) tri_static_fill_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                              const int* __restrict__ rowptr,
+                                                              const bool* __restrict__ mask, int E,
+                                                              const int* __restrict__ tptr, int Tcap,
+                                                              int* __restrict__ kj, int* __restrict__ ji) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = tptr[E];
+  if (x < E && (mask == nullptr || mask[dst[x]])) {
+    const int j = src[x], i = dst[x];
+    int o = tptr[x];
+    const int en = rowptr[j + 1];
+    for (int k = rowptr[j]; k < en && o < Tcap; ++k) {
+      if (src[k] == i) continue;  // k != i
+      kj[o] = k;
+      ji[o] = x;
+      ++o;
+    }
+  }
+  if (x >= total && x < Tcap) {
+    kj[x] = E - 1;
+    ji[x] = E - 1;
+  }
+}
+
+// (src, dst) int32 [E] destination-sorted, rowptr int32 [N+1], mask bool [N] or None -> counts [E]
+at::Tensor triplets_static_count(const at::Tensor& src, const at::Tensor& dst, const at::Tensor& rowptr,
+                                 const c10::optional<at::Tensor>& mask) {
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(dst);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK(src.numel() == dst.numel() && src.is_contiguous() && dst.is_contiguous(), "triplets_static: src/dst [E]");
+  const int E = (int)src.numel();
+  if (mask.has_value())
+    HY_CHECK(mask->scalar_type() == at::kBool && mask->numel() == rowptr.numel() - 1, "triplets_static: mask [N]");
+  auto counts = at::empty({E}, src.options());
+  if (E)
+    tri_static_count_kernel<<<ceil_div(E, 256), 256, 0, stream()>>>(
+        src.data_ptr<int>(), dst.data_ptr<int>(), rowptr.data_ptr<int>(),
+        mask.has_value() ? mask->data_ptr<bool>() : nullptr, E, counts.data_ptr<int>());
+  return counts;
+}
+
+// tptr int32 [E+1]: exclusive scan of the counts -> (kj, ji) int32 [Tcap]
+std::tuple<at::Tensor, at::Tensor> triplets_static_fill(const at::Tensor& src, const at::Tensor& dst,
+                                                        const at::Tensor& rowptr,
+                                                        const c10::optional<at::Tensor>& mask, const at::Tensor& tptr,
+                                                        int64_t Tcap) {
+  HY_CHECK_I32(tptr);
+  const int E = (int)src.numel();
+  HY_CHECK(E > 0 && tptr.numel() == E + 1 && Tcap > 0 && Tcap < (1LL << 31), "triplets_static_fill: sizes");
+  if (mask.has_value())
+    HY_CHECK(mask->scalar_type() == at::kBool && mask->numel() == rowptr.numel() - 1, "triplets_static: mask [N]");
+  auto kj = at::empty({Tcap}, src.options()), ji = at::empty({Tcap}, src.options());
+  const int n = (int)std::max<int64_t>(E, Tcap);
+  tri_static_fill_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(
+      src.data_ptr<int>(), dst.data_ptr<int>(), rowptr.data_ptr<int>(),
+      mask.has_value() ? mask->data_ptr<bool>() : nullptr, E, tptr.data_ptr<int>(), (int)Tcap, kj.data_ptr<int>(),
+      ji.data_ptr<int>());
+  return {kj, ji};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("triplets_static_count(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask) -> Tensor");
+  m.def("triplets_static_fill(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask, Tensor tptr, int Tcap) -> (Tensor, Tensor)");
   m.def(
       "radius_graph(Tensor pos, Tensor node_graph, Tensor gptr, float r, int max_nb, bool loop, bool nearest, "
       "Tensor? cell, Tensor? reps) -> (Tensor, Tensor)");
@@ -576,6 +663,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radius_graph", hy::radius_graph);
   m.impl("triplets", hy::triplets);
+  m.impl("triplets_static_count", hy::triplets_static_count);
+  m.impl("triplets_static_fill", hy::triplets_static_fill);
   m.impl("radius_static_count", hy::radius_static_count);
   m.impl("radius_static_fill", hy::radius_static_fill);
   m.impl("radius_graph_cells", hy::radius_graph_cells);

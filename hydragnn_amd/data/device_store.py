@@ -28,6 +28,7 @@ extra attention segment), padded edges are spread over the padded nodes
 and the device scalars ``num_valid`` / ``num_graphs_valid`` drive the masked
 reductions.
 """
+import functools
 import os
 import time
 
@@ -129,6 +130,33 @@ class DeviceGraphStore:
         else:
             Np, Ep, Gp = N, E, G
         return Layout(Np, Ep, Gp, padded, self.attn_scope)
+
+    def triplet_cap(self, G):
+        """Upper bound on the DimeNet triplet count (k -> j -> i, k != i) of any batch of at
+        most ``G`` graphs: the sum of the ``G`` largest per-graph counts, rounded up to 256.
+        A padded batch carries it (``triplet_cap``) so the model can build its triplets on the
+        device with a fixed capacity (models/dimenet.triplets_static)."""
+        cs = getattr(self, "_tri_cum", None)
+        if cs is None:
+            S = self.num_samples
+            e_sample = np.repeat(np.arange(S), self.n_edges)
+            gs = self.src_local + self.node_off[:-1][e_sample]
+            gd = self.dst_local + self.node_off[:-1][e_sample]
+            Ntot = int(self.node_off[-1])
+            indeg = np.bincount(gd, minlength=Ntot)
+            per_edge = indeg[gs].astype(np.int64)
+            # minus the in-edges k -> j of j whose source is i (the back edges of j -> i)
+            key = gs * Ntot + gd
+            rkey = gd * Ntot + gs
+            uk, uc = np.unique(key, return_counts=True)
+            pos = np.searchsorted(uk, rkey)
+            pos_c = np.minimum(pos, max(uk.size - 1, 0))
+            back = np.where((uk.size > 0) & (uk[pos_c] == rkey), uc[pos_c], 0) if uk.size else np.zeros_like(rkey)
+            per_edge -= back
+            t = np.bincount(e_sample, weights=per_edge, minlength=S).astype(np.int64)
+            cs = self._tri_cum = np.concatenate([[0], np.cumsum(np.sort(t)[::-1])])
+        G = max(0, min(int(G), cs.size - 1))
+        return int(max(256, -(-int(cs[G]) // 256) * 256))
 
     def _native_plan_args(self):
         t = getattr(self, "_plan_t", None)
@@ -373,6 +401,7 @@ class DeviceGraphStore:
                 s["num_valid"] = scal[0]
                 s["graph_mask"] = gmask
                 s["node_mask"] = nmask
+                s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1)  # host int, computed on demand
             return b
         return self._assemble_torch(dev_buf, lay, host_ids, branch_sorted)
 
@@ -448,6 +477,7 @@ class DeviceGraphStore:
             s["num_valid"] = nvalid
             s["graph_mask"] = gmask
             s["node_mask"] = nmask.view(-1)
+            s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1)  # host int, computed on demand
         if self.dataset_name is not None:
             dn = self.dataset_name_dev.index_select(0, sid)
             if lay.padded:

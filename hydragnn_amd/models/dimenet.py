@@ -75,12 +75,12 @@ class _TripletSBF(torch.autograd.Function):
     sbf[t] from vec[e_ji], vec[e_kj]; backward returns d vec (analytic)."""
 
     @staticmethod
-    def forward(ctx, vec, kj, ji, layer):
+    def forward(ctx, vec, kj, ji, layer, limit=None):
         from .. import _native
 
         ctx.save_for_backward(vec, kj, ji)
-        ctx.layer = layer
-        return _native.ops().dimenet_sbf_fwd(vec, kj, ji, layer.zeros, layer.norm, layer.cutoff, layer.exponent)
+        ctx.layer, ctx.limit = layer, limit
+        return _native.ops().dimenet_sbf_fwd(vec, kj, ji, layer.zeros, layer.norm, layer.cutoff, layer.exponent, limit)
 
     @staticmethod
     def backward(ctx, g):
@@ -88,8 +88,9 @@ class _TripletSBF(torch.autograd.Function):
 
         vec, kj, ji = ctx.saved_tensors
         L = ctx.layer
-        dvec = _native.ops().dimenet_sbf_bwd(g.contiguous(), vec, kj, ji, L.zeros, L.norm, L.cutoff, L.exponent)
-        return dvec, None, None, None
+        dvec = _native.ops().dimenet_sbf_bwd(g.contiguous(), vec, kj, ji, L.zeros, L.norm, L.cutoff, L.exponent,
+                                             ctx.limit)
+        return dvec, None, None, None, None
 
 
 class SphericalBasisLayer(nn.Module):
@@ -128,8 +129,10 @@ class SphericalBasisLayer(nn.Module):
             self.num_radial <= 8
 
     def from_vectors(self, vec, kj_si, ji_si):
-        """sbf directly from edge vectors (the GPU path: angle + basis in one kernel)."""
-        return _TripletSBF.apply(vec.contiguous(), kj_si.index, ji_si.index, self)
+        """sbf directly from edge vectors (the GPU path: angle + basis in one kernel).  A
+        static triplet list (``triplets_static``) carries its real count as the indices'
+        ``limit``: the basis rows of the padding triplets are zero."""
+        return _TripletSBF.apply(vec.contiguous(), kj_si.index, ji_si.index, self, ji_si.limit)
 
 
 # ----------------------------------------------------------------------------- triplets
@@ -152,6 +155,43 @@ def triplets_csr(dst_si, src_si, num_nodes):
     e_kj = start + off
     keep = src[e_kj] != dst[e_ji]  # k != i
     return e_kj[keep], e_ji[keep]
+
+
+def triplets_static(dst_si, src_si, node_mask, Tcap):
+    """Triplets of a statically padded batch with FIXED capacity ``Tcap`` and no host
+    synchronisation (capturable; csrc/graph.hip ``triplets_static_*``).  Only edges into
+    valid nodes emit triplets (padding edges join padding nodes), in the order of
+    ``triplets_csr``; slots [T, Tcap) are dummy triplets of the last edge, sorted last in
+    both views.  Returns (kj_si, ji_si) whose ``limit`` (device int32 scalar) is T: segment
+    sums stop there and the basis kernels zero the padding rows."""
+    src, dst, rowptr = src_si.index, dst_si.index, dst_si.rowptr
+    E = src.numel()
+    mask = None if node_mask is None else node_mask.view(-1).bool()
+    if src.is_cuda:
+        from .. import _native
+
+        counts = _native.ops().triplets_static_count(src, dst, rowptr, mask)
+        tptr = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0, dtype=torch.int32)])
+        kj, ji = _native.ops().triplets_static_fill(src, dst, rowptr, mask, tptr, int(Tcap))
+    else:  # CPU twin (padded_step tests): the eager order, then the dummy tail
+        kj_v, ji_v = triplets_csr(dst_si, src_si, rowptr.numel() - 1)
+        if mask is not None:
+            keep = mask[dst.long()[ji_v]]
+            kj_v, ji_v = kj_v[keep], ji_v[keep]
+        T = kj_v.numel()
+        if T > Tcap:
+            raise RuntimeError(f"triplets_static: {T} triplets exceed the capacity {Tcap}")
+        kj = torch.full((Tcap,), E - 1, dtype=torch.int32)
+        ji = torch.full((Tcap,), E - 1, dtype=torch.int32)
+        kj[:T], ji[:T] = kj_v.int(), ji_v.int()
+        tptr = torch.zeros(E + 1, dtype=torch.int32)
+        tptr[1:] = torch.cumsum(torch.bincount(ji_v.long(), minlength=E), 0).int()
+    limit = tptr[E:E + 1].clamp(max=int(Tcap))
+    jrp = tptr.clamp(max=int(Tcap))
+    jrp[E:].fill_(int(Tcap))  # the dummy tail belongs to the last edge
+    vals, perm = torch.sort(kj, stable=True)
+    krp = torch.searchsorted(vals, torch.arange(E + 1, dtype=torch.int32, device=kj.device), out_int32=True)
+    return (seg.SegIndex(kj, krp, perm.to(torch.int32), E, limit), seg.SegIndex(ji, jrp, None, E, limit))
 
 
 # ----------------------------------------------------------------------------- blocks
@@ -271,7 +311,9 @@ class DimeNetLayer(nn.Module):
 
 class DIMEStack(Base):
     is_edge_model = True
-    capturable = False  # triplet count is data dependent
+    # a statically padded batch carries the store's triplet capacity: the triplets are then
+    # built on the device with fixed shapes (triplets_static), so the step is capturable
+    capturable = True
 
     def __init__(self, input_args, conv_args, basis_emb_size, envelope_exponent, int_emb_size, out_emb_size,
                  num_after_skip, num_before_skip, num_radial, num_spherical, edge_dim, radius, *args,
@@ -313,10 +355,15 @@ class DIMEStack(Base):
         x, pos, ctx = super()._embedding(data)
         assert data.pos is not None, "DimeNet requires node positions (data.pos) to be set."
         N = data.num_nodes
-        idx_kj, idx_ji = triplets_csr(ctx.dst_si, ctx.src_si, N)
         E = ctx.dst_si.index.numel()
-        ctx.kj_si = seg.SegIndex.from_index(idx_kj, E, sorted_=False)
-        ctx.ji_si = seg.SegIndex.from_index(idx_ji, E, sorted_=True)
+        tcap = data.get("triplet_cap")  # padded batch: the store's capacity (host int, lazy)
+        tcap = tcap() if callable(tcap) else tcap
+        if tcap is not None and E > 0:
+            ctx.kj_si, ctx.ji_si = triplets_static(ctx.dst_si, ctx.src_si, data.get("node_mask"), tcap)
+        else:
+            idx_kj, idx_ji = triplets_csr(ctx.dst_si, ctx.src_si, N)
+            ctx.kj_si = seg.SegIndex.from_index(idx_kj, E, sorted_=False)
+            ctx.ji_si = seg.SegIndex.from_index(idx_ji, E, sorted_=True)
         vec, dist = edge_vectors_and_lengths(data.pos, ctx.dst_si, ctx.src_si, data.get("edge_shifts"))
         d = dist.view(-1)
         ctx.rbf = self.rbf(d)
@@ -329,6 +376,9 @@ class DIMEStack(Base):
         b = torch.linalg.cross(pos_ji, pos_ki).norm(dim=-1)
         angle = torch.atan2(b, a)
         ctx.sbf = self.sbf(d, angle, ctx.kj_si)
+        if ctx.kj_si.limit is not None:  # padding triplets: zero basis rows
+            live = torch.arange(ctx.sbf.shape[0], device=d.device) < ctx.kj_si.limit
+            ctx.sbf = ctx.sbf * live.view(-1, 1).to(ctx.sbf.dtype)
         return x, pos, ctx
 
     def __str__(self):

@@ -110,3 +110,95 @@ def test_schnet_static_inforward_graph_padded_equals_eager(equivariance):
         le = float(eager(store, idx)[0])
         lp = float(padded(store, idx)[0])
         assert abs(le - lp) <= 1e-4 * max(1.0, abs(le)), (le, lp)
+
+
+def _dimenet(samples):
+    heads = {"graph": [{"type": "branch-0", "architecture": {"num_sharedlayers": 1, "dim_sharedlayers": 8,
+                                                             "num_headlayers": 1, "dim_headlayers": [8]}}]}
+    for s in samples:
+        s.y = s.energy.view(-1, 1) if "energy" in s else s.y.view(-1, 1)
+        s.y_loc = torch.tensor([[0, 1]])
+    torch.manual_seed(0)
+    return create_model("DimeNet", 1, 16, [1], 0, "", "", 0, ["graph"], heads, "relu", "mae", [1.0], 2,
+                        radius=5.0, max_neighbours=8, num_radial=5, envelope_exponent=5, basis_emb_size=4,
+                        int_emb_size=8, out_emb_size=8, num_after_skip=1, num_before_skip=1, num_spherical=3,
+                        dropout=0.0, use_gpu=False)
+
+
+def test_store_triplet_cap_bounds_every_batch():
+    """DeviceGraphStore.triplet_cap(G) >= the real triplet count of any G-graph batch."""
+    from hydragnn_amd.models.dimenet import triplets_csr
+    from hydragnn_amd.ops.segment import SegIndex
+
+    samples = _samples()
+    store = DeviceGraphStore(samples, "cpu")
+    per = []
+    for s in samples:
+        n = s.num_nodes
+        dst_si = SegIndex.from_index(s.edge_index[1], n, sorted_=True)
+        src_si = SegIndex.from_index(s.edge_index[0], n)
+        per.append(triplets_csr(dst_si, src_si, n)[0].numel())
+    per = sorted(per, reverse=True)
+    for G in (1, 3, 4, 16):
+        cap = store.triplet_cap(G)
+        assert cap >= sum(per[:G]) and cap % 256 == 0 and cap < sum(per[:G]) + 256
+
+
+def test_dimenet_static_triplets_padded_equals_eager():
+    """DimeNet's triplets in the padded (capturable) step come from the fixed-capacity
+    builder (models/dimenet.triplets_static: valid receivers only, dummy tail with zero
+    basis rows); the step equals the eager step (data-dependent builder)."""
+    samples = _samples()
+    m1 = _dimenet(samples)
+    m2 = copy.deepcopy(m1)
+    assert m1.capturable
+    store = DeviceGraphStore(samples, "cpu", head_types=["graph"], head_dims=[1])
+    eager = TrainStep(m1, lr=1e-3, mode="eager")
+    padded = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=512)
+    rng = np.random.default_rng(1)
+    for _ in range(3):
+        idx = list(rng.choice(len(store), 4, replace=False))
+        le = float(eager(store, idx)[0])
+        lp = float(padded(store, idx)[0])
+        assert abs(le - lp) <= 1e-4 * max(1.0, abs(le)), (le, lp)
+
+
+@pytest.mark.gpu
+def test_dimenet_captured_step_matches_eager_gpu():
+    """The captured DimeNet step (device triplet builder with static capacity, sbf kernels
+    honouring the device limit) follows the eager trajectory."""
+    samples = _samples()
+    m1 = _dimenet(samples).cuda()
+    m2 = copy.deepcopy(m1)
+    store = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
+    eager = TrainStep(m1, lr=1e-3, mode="eager")
+    graph = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=512)
+    rng = np.random.default_rng(1)
+    for _ in range(4):
+        idx = list(rng.choice(len(store), 4, replace=False))
+        le = float(eager(store, idx)[0])
+        lg = float(graph(store, idx)[0])
+        assert abs(le - lg) <= 1e-3 * max(1.0, abs(le)), (le, lg)
+    assert graph.graphs, "the DimeNet step was not captured"
+
+
+@pytest.mark.gpu
+def test_dimenet_static_triplets_device_matches_cpu():
+    """csrc/graph.hip triplets_static_* == the CPU twin (indices, CSR views, limit)."""
+    from hydragnn_amd.models.dimenet import triplets_static
+
+    samples = _samples()
+    store = DeviceGraphStore(samples, "cpu")
+    idx = [0, 3, 5, 7]
+    N, E = store.sizes_of(idx)
+    lay = store.layout(idx, Np=N + 9, Ep=E + 40, Gp=len(idx) + 1)
+    b = store.assemble(store.upload(idx, lay), lay)
+    cap = b.get("triplet_cap")()
+    a_kj, a_ji = triplets_static(b.dst_si, b.src_si, b.get("node_mask"), cap)
+    d = lambda si: si.to("cuda")  # noqa: E731
+    b_kj, b_ji = triplets_static(d(b.dst_si), d(b.src_si), b.get("node_mask").cuda(), cap)
+    for x, y in ((a_kj, b_kj), (a_ji, b_ji)):
+        assert torch.equal(x.index, y.index.cpu()) and torch.equal(x.rowptr, y.rowptr.cpu())
+        assert torch.equal(x.limit, y.limit.cpu())
+    assert torch.equal(a_kj.perm, b_kj.perm.cpu())
+    assert 0 < int(a_kj.limit) <= cap

@@ -12,6 +12,7 @@
                        correlation 2, 3 layers), 5 branches, batch 32
   qm9_schnet_gps       the reference QM9 example architecture: SchNet x 2 + GPS (8 heads)
   oc20_gps_h128        config 4 at hidden 128 (16 heads)
+  qm9_dimenet          DimeNet++ (reference example hyper-parameters), hidden 64 x 3, batch 64
 
 All synthetic data / random-init weights, fp32.  Prints one JSON line per config.
 Usage: python tools/bench_configs.py [names...] [--steps 20] [--warmup 5]
@@ -91,6 +92,20 @@ def oc20_gps_h128(dev):
     return m, s, 32, ["graph"], [1], False
 
 
+def qm9_dimenet(dev):
+    """DimeNet++ with the reference's example hyper-parameters (examples/mptrj/*.json:
+    int_emb 64, basis_emb 8, out_emb 128, 1 + 2 residual layers, 6 radial x 7 spherical),
+    hidden 64 x 3 layers on QM9-shaped molecules, radius 5, batch 64 (captured step: the
+    triplets come from the static-capacity device builder)."""
+    s = _with_edges(molecules_like(1024, seed=1), 5.0, 20)
+    heads = {"graph": _gheads(1, [50, 25], 50)}
+    m = create_model("DimeNet", 1, 64, [1], 0, "", "", 0, ["graph"], heads, "relu", "mae", [1.0], 3,
+                     radius=5.0, max_neighbours=20, num_radial=6, num_spherical=7, envelope_exponent=5,
+                     basis_emb_size=8, int_emb_size=64, out_emb_size=128, num_after_skip=2, num_before_skip=1,
+                     dropout=0.0)
+    return m, s, 64, ["graph"], [1], False
+
+
 def md17_painn_forces(dev):
     s = _with_edges(md_trajectory(1024, seed=2, num_atoms=21), 5.0, 20)
     heads = {"node": _nheads(1, [64, 32])}
@@ -125,7 +140,8 @@ def multibranch_mace(dev):
 
 
 CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
-           "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128}
+           "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128,
+           "qm9_dimenet": qm9_dimenet}
 
 
 def _targets_for_store(samples, head_types):
