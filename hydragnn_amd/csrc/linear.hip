@@ -399,6 +399,7 @@ struct WgProb {
   int vec;    // bit0: dY float4 path, bit1: X float4 path
   int accumulate;
   int ldw;    // row stride of dW (a column block of a wider weight gradient: ldw > I)
+  int trans;  // the problem was swapped (dY <-> X): dW is written transposed
 };
 
 struct WgArgs {
@@ -541,7 +542,8 @@ __global__ void __launch_bounds__(256) wgrad_grouped_reduce_kernel(WgArgs) {
   for (int u = 0; u < 8; ++u)
     if (s0 + u < S) acc[u] += part[(int64_t)(s0 + u) * ld + j];
   const float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  float* dst = j < nw ? P.dw + (j / P.I) * P.ldw + (j % P.I) : P.db + (j - nw);
+  float* dst = j < nw ? (P.trans ? P.dw + (j % P.I) * P.ldw + (j / P.I) : P.dw + (j / P.I) * P.ldw + (j % P.I))
+                      : P.db + (j - nw);
   *dst = P.accumulate ? *dst + v : v;
 }
 
@@ -574,6 +576,11 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       const int64_t k = c0 + q;
       auto dY = dYs[k].stride(1) == 1 ? dYs[k] : dYs[k].contiguous();
       auto X = Xs[k].stride(1) == 1 ? Xs[k] : Xs[k].contiguous();
+      // a wide-input, narrow-output map without bias (e.g. DimeNet's sbf projection
+      // [T, 42] -> 8 over ~10^5 triplet rows): dW^T = X^T dY is a narrow problem, whose
+      // VALU body has no 64 x 64 tile to waste 7/8 of and needs no 16-byte operands
+      const bool swap = X.size(1) > kWgNarrow && dY.size(1) <= kWgNarrow && !(dbs[k].defined() && dbs[k].numel() > 0);
+      if (swap) std::swap(dY, X);
       keep.push_back(dY);
       keep.push_back(X);
       HY_CHECK(dY.is_cuda() && X.is_cuda() && dY.scalar_type() == at::kFloat && X.scalar_type() == at::kFloat,
@@ -583,7 +590,7 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       const int O = (int)dY.size(1), I = (int)X.size(1);
       const auto& dW = dWs[k];
       HY_CHECK(dW.scalar_type() == at::kFloat && dW.numel() == (int64_t)O * I &&
-                   (dW.is_contiguous() || (dW.dim() == 2 && dW.stride(1) == 1 && dW.size(0) == O)),
+                   (dW.is_contiguous() || (dW.dim() == 2 && dW.stride(1) == 1 && dW.size(0) == (swap ? I : O))),
                "linear_wgrad_grouped: dW must be fp32 [O, I] with unit column stride");
       const bool hb = dbs[k].defined() && dbs[k].numel() > 0;
       if (hb)
@@ -594,7 +601,8 @@ void linear_wgrad_grouped(at::TensorList dYs, at::TensorList Xs, at::TensorList 
       P.dy = dY.data_ptr<float>();
       P.x = X.data_ptr<float>();
       P.dw = dW.data_ptr<float>();
-      P.ldw = (dW.dim() == 2 && !dW.is_contiguous()) ? (int)dW.stride(0) : I;
+      P.ldw = (dW.dim() == 2 && !dW.is_contiguous()) ? (int)dW.stride(0) : (swap ? O : I);
+      P.trans = swap ? 1 : 0;
       P.db = hb ? dbs[k].data_ptr<float>() : nullptr;
       P.ldy = (int)dY.stride(0);
       P.ldx = (int)X.stride(0);

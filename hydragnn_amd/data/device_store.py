@@ -131,11 +131,12 @@ class DeviceGraphStore:
             Np, Ep, Gp = N, E, G
         return Layout(Np, Ep, Gp, padded, self.attn_scope)
 
-    def triplet_cap(self, G):
+    def triplet_cap(self, G, Ep=None):
         """Upper bound on the DimeNet triplet count (k -> j -> i, k != i) of any batch of at
-        most ``G`` graphs: the sum of the ``G`` largest per-graph counts, rounded up to 256.
-        A padded batch carries it (``triplet_cap``) so the model can build its triplets on the
-        device with a fixed capacity (models/dimenet.triplets_static)."""
+        most ``G`` graphs (and at most ``Ep`` edges): the smaller of the sum of the ``G``
+        largest per-graph counts and ``Ep`` x the largest per-graph triplets-per-edge ratio,
+        rounded up to 256.  A padded batch carries it (``triplet_cap``) so the model can build
+        its triplets on the device with a fixed capacity (models/dimenet.triplets_static)."""
         cs = getattr(self, "_tri_cum", None)
         if cs is None:
             S = self.num_samples
@@ -155,8 +156,13 @@ class DeviceGraphStore:
             per_edge -= back
             t = np.bincount(e_sample, weights=per_edge, minlength=S).astype(np.int64)
             cs = self._tri_cum = np.concatenate([[0], np.cumsum(np.sort(t)[::-1])])
+            ne = self.n_edges
+            self._tri_ratio = float(np.max(t[ne > 0] / ne[ne > 0])) if (ne > 0).any() else 0.0
         G = max(0, min(int(G), cs.size - 1))
-        return int(max(256, -(-int(cs[G]) // 256) * 256))
+        cap = int(cs[G])
+        if Ep is not None:  # T = sum_g r_g E_g <= max_g r_g * Ep
+            cap = min(cap, int(np.ceil(self._tri_ratio * int(Ep))) + 1)
+        return int(max(256, -(-cap // 256) * 256))
 
     def _native_plan_args(self):
         t = getattr(self, "_plan_t", None)
@@ -401,7 +407,7 @@ class DeviceGraphStore:
                 s["num_valid"] = scal[0]
                 s["graph_mask"] = gmask
                 s["node_mask"] = nmask
-                s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1)  # host int, computed on demand
+                s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand
             return b
         return self._assemble_torch(dev_buf, lay, host_ids, branch_sorted)
 
@@ -477,7 +483,7 @@ class DeviceGraphStore:
             s["num_valid"] = nvalid
             s["graph_mask"] = gmask
             s["node_mask"] = nmask.view(-1)
-            s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1)  # host int, computed on demand
+            s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand
         if self.dataset_name is not None:
             dn = self.dataset_name_dev.index_select(0, sid)
             if lay.padded:

@@ -138,10 +138,18 @@ def test_store_triplet_cap_bounds_every_batch():
         dst_si = SegIndex.from_index(s.edge_index[1], n, sorted_=True)
         src_si = SegIndex.from_index(s.edge_index[0], n)
         per.append(triplets_csr(dst_si, src_si, n)[0].numel())
-    per = sorted(per, reverse=True)
+    ne = [s.num_edges for s in samples]
+    ratio = max(t / e for t, e in zip(per, ne))
+    srt = sorted(per, reverse=True)
     for G in (1, 3, 4, 16):
         cap = store.triplet_cap(G)
-        assert cap >= sum(per[:G]) and cap % 256 == 0 and cap < sum(per[:G]) + 256
+        assert cap >= sum(srt[:G]) and cap % 256 == 0 and cap < sum(srt[:G]) + 256
+    rng = np.random.default_rng(0)
+    for _ in range(20):  # the edge-ratio bound holds for every batch within the edge budget
+        idx = rng.choice(len(samples), 4, replace=False)
+        E = sum(ne[i] for i in idx)
+        cap = store.triplet_cap(4, E)
+        assert sum(per[i] for i in idx) <= cap <= max(256, ratio * E + 257)
 
 
 def test_dimenet_static_triplets_padded_equals_eager():

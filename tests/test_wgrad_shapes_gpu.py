@@ -23,3 +23,25 @@ def test_linear_wgrad_shapes(M, O, I):
     _native.ops().linear_wgrad_grouped([dy], [x], dWs, dbs, [0])
     torch.testing.assert_close(dWs[0], dy.t() @ x, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dbs[0], dy.sum(0), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [37, 5000, 200000])
+@pytest.mark.parametrize("O,I", [(8, 42), (16, 64), (3, 17)])
+@pytest.mark.parametrize("block", [False, True])
+def test_grouped_wgrad_swapped_narrow(M, O, I, block):
+    """Bias-free wide-input / narrow-output maps (DimeNet's sbf projection, [T, 42] -> 8)
+    run as the transposed narrow problem; dW written transposed, also into a column block
+    of a wider gradient, plain and accumulating."""
+    g = torch.Generator(device="cpu").manual_seed(M + O * 7 + I)
+    dy = torch.randn(M, O, generator=g).cuda()
+    x = torch.randn(M, I, generator=g).cuda()
+    ref = (dy.double().t() @ x.double()).float()
+    full = torch.randn(O, I + 5, generator=g).cuda()
+    dW = full[:, 2:2 + I] if block else torch.zeros(O, I, device="cuda")
+    before = full.clone()
+    _native.ops().linear_wgrad_grouped([dy], [x], [dW], [torch.empty(0, device="cuda")], [0])
+    torch.testing.assert_close(dW, ref, rtol=1e-4, atol=1e-3 * max(1.0, M ** 0.5 / 10))
+    _native.ops().linear_wgrad_grouped([dy], [x], [dW], [torch.empty(0, device="cuda")], [1])
+    torch.testing.assert_close(dW, 2 * ref, rtol=1e-4, atol=2e-3 * max(1.0, M ** 0.5 / 10))
+    if block:  # the columns outside the block are untouched
+        assert torch.equal(full[:, :2], before[:, :2]) and torch.equal(full[:, 2 + I:], before[:, 2 + I:])

@@ -189,13 +189,15 @@ def run(name, steps, warmup, dev):
     if os.environ.get("BENCH_OP_PROFILE") == "1":  # op-level attribution of 3 steps
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        shapes = os.environ.get("BENCH_OP_SHAPES") == "1"  # group by input shapes too
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=shapes) as prof:
             for _ in range(3):
                 step(draw())
             torch.cuda.synchronize()
         # BENCH_OP_SORT=count: the most frequently launched ops first (launch-bound steps)
         key = "count" if os.environ.get("BENCH_OP_SORT") == "count" else "self_device_time_total"
-        print(prof.key_averages().table(sort_by=key, row_limit=70), flush=True)
+        print(prof.key_averages(group_by_input_shape=shapes).table(sort_by=key, row_limit=70, max_name_column_width=60,
+                                                                   max_shapes_column_width=70), flush=True)
     mark = os.environ.get("HYDRA_PROFILE_MARK") == "1"
     if mark:  # spin kernels bracket the timed steps: rocpd_summary.py --between spin_kernel
         torch.cuda._sleep(1000)
