@@ -557,6 +557,204 @@ std::tuple<at::Tensor, at::Tensor> radius_static_fill(const at::Tensor& pos_, co
   return {src, dst};
 }
 
+// ------------------------------------------------------------------ static radius graph, one launch
+// The same graph for small batches (QM9-sized: ~10^3 nodes, ~10^4 edge slots) in ONE
+// workgroup: count -> exclusive scan -> fill -> source CSR (count, scan, stable placement)
+// all in LDS.  The multi-launch form (count, scan, fill, index_add, scan, radix sort by
+// source, casts and copies: ~15 launches) is launch-bound at this size.  The source view
+// is stable (edges of one source in ascending edge order, as a stable sort gives): real
+// edges are placed by LDS atomics and each bucket's few entries insertion-sorted; the
+// padding slots (all of source `dummy`) are appended after its real edges in slot order.
+constexpr int kRsThreads = 1024;
+
+// exclusive scan of a[0, n) in place (LDS), returns the total; every thread must call
+__device__ int rs_block_scan(int* a, int n, int* part) {
+  const int t = threadIdx.x;
+  const int per = (n + kRsThreads - 1) / kRsThreads;
+  const int b = min(n, t * per), e = min(n, b + per);
+  int s = 0;
+  for (int i = b; i < e; ++i) s += a[i];
+  part[t] = s;
+  __syncthreads();
+  // Hillis-Steele over the 1024 partial sums (10 steps)
+  for (int o = 1; o < kRsThreads; o <<= 1) {
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;  // exclusive prefix of this thread's chunk
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  const int total = part[kRsThreads - 1];
+  __syncthreads();
+  return total;
+}
+
+__global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
+    const float* __restrict__ pos, const int64_t* __restrict__ node_graph, const int64_t* __restrict__ gptr,
+    const bool* __restrict__ mask, int N, int G, float r2, int cap, int Ecap, int dummy, int* __restrict__ src_o,
+    int* __restrict__ dst_o, int* __restrict__ drp_o, int* __restrict__ limit_o, int* __restrict__ srp_o,
+    int* __restrict__ sperm_o, long long* __restrict__ dbg) {
+#define RS_STAMP(n) \
+  if (dbg && threadIdx.x == 0) dbg[n] = (long long)__builtin_amdgcn_s_memtime()
+  extern __shared__ int lds[];
+  int* part = lds;                 // [kRsThreads]
+  int* rp = part + kRsThreads;     // [N + 1] receiver counts -> row starts
+  int* sc = rp + N + 1;            // [N + 1] source counts -> source row starts
+  int* fc = sc + N + 1;            // [N] placement cursors
+  int* lsrc = fc + N;              // [Ecap]
+  int* lperm = lsrc + Ecap;        // [Ecap]
+  float* lpos = reinterpret_cast<float*>(lperm + Ecap);  // [3N] positions (the scans below are
+  int* lng = reinterpret_cast<int*>(lpos + 3 * N);       // [N] node -> graph  serial per thread:
+  int* lgp = lng + N;                                    // [G + 1] graph starts  LDS, not L2, latency)
+  int* lmk = lgp + G + 1;                                // [N] valid-node flags
+  __shared__ int s_dummy_real;
+  const int t = threadIdx.x;
+  RS_STAMP(0);
+  for (int i = t; i < 3 * N; i += kRsThreads) lpos[i] = pos[i];
+  for (int i = t; i < N; i += kRsThreads) {
+    lng[i] = (int)node_graph[i];
+    lmk[i] = mask ? (int)mask[i] : 1;
+    sc[i] = 0;
+    fc[i] = 0;
+  }
+  for (int i = t; i <= G; i += kRsThreads) lgp[i] = (int)gptr[i];
+  __syncthreads();
+  RS_STAMP(1);
+  for (int i = t; i < N; i += kRsThreads) {
+    int c = 0;
+    if (lmk[i]) {
+      const int g = lng[i];
+      const float xi = lpos[3 * i], yi = lpos[3 * i + 1], zi = lpos[3 * i + 2];
+      const int j1 = lgp[g + 1];
+      for (int j = lgp[g]; j < j1 && c < cap; ++j) {
+        if (j == i || !lmk[j]) continue;
+        const float dx = lpos[3 * j] - xi, dy = lpos[3 * j + 1] - yi, dz = lpos[3 * j + 2] - zi;
+        if (dx * dx + dy * dy + dz * dz <= r2) ++c;
+      }
+    }
+    rp[i] = c;
+  }
+  __syncthreads();
+  RS_STAMP(2);
+  const int total = rs_block_scan(rp, N, part);  // <= N * cap <= Ecap (host-checked)
+  RS_STAMP(3);
+  for (int i = t; i < N; i += kRsThreads) {
+    drp_o[i] = rp[i];
+    if (lmk[i]) {
+      const int g = lng[i];
+      const float xi = lpos[3 * i], yi = lpos[3 * i + 1], zi = lpos[3 * i + 2];
+      int q = rp[i];
+      const int q1 = i + 1 < N ? rp[i + 1] : total;
+      const int j1 = lgp[g + 1];
+      for (int j = lgp[g]; j < j1 && q < q1; ++j) {
+        if (j == i || !lmk[j]) continue;
+        const float dx = lpos[3 * j] - xi, dy = lpos[3 * j + 1] - yi, dz = lpos[3 * j + 2] - zi;
+        if (dx * dx + dy * dy + dz * dz <= r2) {
+          lsrc[q] = j;
+          dst_o[q] = i;
+          ++q;
+        }
+      }
+    }
+  }
+  for (int e = total + t; e < Ecap; e += kRsThreads) {
+    lsrc[e] = dummy;
+    dst_o[e] = dummy;
+  }
+  if (t == 0) {
+    drp_o[N] = Ecap;  // the padding slots belong to the last (padding) receiver
+    limit_o[0] = total;
+  }
+  __syncthreads();
+  RS_STAMP(4);
+  for (int e = t; e < total; e += kRsThreads) atomicAdd(&sc[lsrc[e]], 1);
+  __syncthreads();
+  RS_STAMP(5);
+  if (t == 0) {
+    s_dummy_real = sc[dummy];
+    sc[dummy] += Ecap - total;
+  }
+  __syncthreads();
+  RS_STAMP(6);
+  rs_block_scan(sc, N, part);
+  RS_STAMP(7);
+  if (t == 0) sc[N] = Ecap;
+  __syncthreads();
+  RS_STAMP(8);
+  for (int e = t; e < total; e += kRsThreads) {
+    const int s = lsrc[e];
+    lperm[sc[s] + atomicAdd(&fc[s], 1)] = e;
+  }
+  const int dbase = sc[dummy] + s_dummy_real;
+  for (int e = total + t; e < Ecap; e += kRsThreads) lperm[dbase + (e - total)] = e;
+  __syncthreads();
+  RS_STAMP(9);
+  for (int s = t; s < N; s += kRsThreads) {  // stable order: sort each bucket's real edges
+    const int b = sc[s], n = s == dummy ? s_dummy_real : sc[s + 1] - b;
+    for (int a = 1; a < n; ++a) {
+      const int v = lperm[b + a];
+      int k = a - 1;
+      while (k >= 0 && lperm[b + k] > v) {
+        lperm[b + k + 1] = lperm[b + k];
+        --k;
+      }
+      lperm[b + k + 1] = v;
+    }
+  }
+  __syncthreads();
+  RS_STAMP(10);
+  for (int e = t; e < Ecap; e += kRsThreads) {
+    src_o[e] = lsrc[e];
+    sperm_o[e] = lperm[e];
+  }
+  for (int i = t; i <= N; i += kRsThreads) srp_o[i] = sc[i];
+  RS_STAMP(11);
+#undef RS_STAMP
+}
+
+// -> (src, dst, drp, limit, srp, sperm), or an empty list when the batch is too large for
+// one workgroup's LDS (the caller then uses the multi-launch builder)
+std::vector<at::Tensor> radius_static_small(const at::Tensor& pos_, const at::Tensor& node_graph,
+                                            const at::Tensor& gptr, const c10::optional<at::Tensor>& mask, double r,
+                                            int64_t cap, int64_t Ecap, int64_t dummy,
+                                            const c10::optional<at::Tensor>& dbg) {
+  HY_CHECK_CUDA(pos_);
+  auto pos = pos_.to(at::kFloat).contiguous();
+  HY_CHECK(node_graph.scalar_type() == at::kLong && gptr.scalar_type() == at::kLong && node_graph.is_contiguous() &&
+               gptr.is_contiguous(),
+           "radius_static_small: int64 batch/ptr");
+  const int64_t N = pos.size(0);
+  if (mask.has_value()) HY_CHECK(mask->scalar_type() == at::kBool && mask->numel() == N, "radius_static: mask [N] bool");
+  HY_CHECK(N > 0 && dummy >= 0 && dummy < N && Ecap >= N * cap, "radius_static_small: sizes");
+  const int64_t G = gptr.numel() - 1;
+  HY_CHECK(G >= 0 && node_graph.numel() == N, "radius_static_small: batch/ptr sizes");
+  const int64_t lds = 4 * (kRsThreads + 3 * N + 2 + 2 * Ecap + 3 * N + N + G + 1 + N);
+  if (lds > 150 * 1024) return {};
+  static bool attr = false;
+  if (!attr) {
+    // (the kernel's static LDS counts against the same 160 KB: ask for what it can use)
+    HY_CHECK(hipFuncSetAttribute((const void*)rs_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 150 * 1024) == hipSuccess,
+             "radius_static_small: LDS attribute");
+    attr = true;
+  }
+  auto io = pos.options().dtype(at::kInt);
+  auto src = at::empty({Ecap}, io), dst = at::empty({Ecap}, io), drp = at::empty({N + 1}, io),
+       limit = at::empty({1}, io), srp = at::empty({N + 1}, io), sperm = at::empty({Ecap}, io);
+  rs_small_kernel<<<1, kRsThreads, lds, stream()>>>(
+      pos.data_ptr<float>(), node_graph.data_ptr<int64_t>(), gptr.data_ptr<int64_t>(),
+      mask.has_value() ? mask->data_ptr<bool>() : nullptr, (int)N, (int)G, (float)(r * r), (int)cap, (int)Ecap,
+      (int)dummy,
+      src.data_ptr<int>(), dst.data_ptr<int>(), drp.data_ptr<int>(), limit.data_ptr<int>(), srp.data_ptr<int>(),
+      sperm.data_ptr<int>(), dbg.has_value() ? (long long*)dbg->data_ptr<int64_t>() : nullptr);
+  return {src, dst, drp, limit, srp, sperm};
+}
+
 // ------------------------------------------------------------------ static-capacity triplets
 // Capturable DimeNet triplets for a statically padded batch (the eager builder above needs
 // the host to learn T before it can allocate).  Only edges whose receiver is a valid node
@@ -645,6 +843,9 @@ std::tuple<at::Tensor, at::Tensor> triplets_static_fill(const at::Tensor& src, c
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def(
+      "radius_static_small(Tensor pos, Tensor node_graph, Tensor gptr, Tensor? mask, float r, int cap, int Ecap, "
+      "int dummy, Tensor? dbg=None) -> Tensor[]");
   m.def("triplets_static_count(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask) -> Tensor");
   m.def("triplets_static_fill(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask, Tensor tptr, int Tcap) -> (Tensor, Tensor)");
   m.def(
@@ -664,6 +865,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radius_graph", hy::radius_graph);
   m.impl("triplets", hy::triplets);
   m.impl("triplets_static_count", hy::triplets_static_count);
+  m.impl("radius_static_small", hy::radius_static_small);
   m.impl("triplets_static_fill", hy::triplets_static_fill);
   m.impl("radius_static_count", hy::radius_static_count);
   m.impl("radius_static_fill", hy::radius_static_fill);

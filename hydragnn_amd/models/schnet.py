@@ -34,6 +34,51 @@ class ShiftedSoftplus(nn.Module):
         return F.softplus(x) - self.shift
 
 
+class _CFFilter(torch.autograd.Function):
+    """W = (ssp(rbf W1^T + b1) W2^T + b2) * C in one HIP launch each way (csrc/schnet.hip).
+    The backward kernel emits the row factors of the four weight/bias gradients; they join
+    the step's deferred grouped weight-gradient launch (ops/linear.py) when it is open, else
+    one grouped launch here."""
+
+    @staticmethod
+    def forward(ctx, rbf, C, W1, b1, W2, b2):
+        from .. import _native
+
+        Wf, H1 = _native.ops().cf_filter_fwd(rbf, W1, b1, W2, b2, C)
+        ctx.save_for_backward(rbf, C, H1, W2)
+        ctx.params = (W1, b1, W2, b2)
+        return Wf
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+        from ..ops import linear as _lin
+
+        rbf, C, H1, W2 = ctx.saved_tensors
+        dH2, A1, dH1 = _native.ops().cf_filter_bwd(g, C, H1, W2)
+        W1p, b1p, W2p, b2p = ctx.params
+        if _lin._can_defer(W1p, b1p) and _lin._can_defer(W2p, b2p):
+            _lin._defer["items"].append((dH2, A1, W2p, b2p))
+            _lin._defer["items"].append((dH1, rbf, W1p, b1p))
+            return None, None, None, None, None, None
+        dW1, db1 = torch.empty_like(W1p), torch.empty_like(b1p)
+        dW2, db2 = torch.empty_like(W2p), torch.empty_like(b2p)
+        _native.ops().linear_wgrad_grouped([dH2, dH1], [A1, rbf], [dW2, dW1], [db2, db1], [0, 0])
+        return None, None, dW1, db1, dW2, db2
+
+
+def _filter_fusable(nn_, h, C):
+    from ..ops.pna import fused
+
+    if not (h.is_cuda and h.dtype == torch.float32 and h.dim() == 2 and h.shape[1] <= 64 and fused("cfconv")
+            and not h.requires_grad and not C.requires_grad and isinstance(nn_, nn.Sequential) and len(nn_) == 3):
+        return False
+    l1, act, l2 = nn_[0], nn_[1], nn_[2]
+    return (isinstance(l1, nn.Linear) and isinstance(act, ShiftedSoftplus) and isinstance(l2, nn.Linear)
+            and l1.bias is not None and l2.bias is not None and l1.in_features == h.shape[1]
+            and l1.out_features == l2.in_features == l2.out_features <= 64)
+
+
 class CFConv(nn.Module):
     def __init__(self, in_channels, out_channels, num_filters, nn_, cutoff, equivariant):
         super().__init__()
@@ -57,7 +102,11 @@ class CFConv(nn.Module):
         dst_si, src_si, dist, rbf, eattr = g
         C = cosine_cutoff(dist, self.cutoff, masked=False)  # one launch on the GPU
         h = rbf if eattr is None else torch.cat([rbf, eattr], -1)
-        W = self.nn(h) * C.view(-1, 1)
+        if _filter_fusable(self.nn, h, C):
+            l1, l2 = self.nn[0], self.nn[2]
+            W = _CFFilter.apply(h, C.reshape(-1).contiguous(), l1.weight, l1.bias, l2.weight, l2.bias)
+        else:
+            W = self.nn(h) * C.view(-1, 1)
         x = self.lin1(inv)
         if self.equivariant:
             coord_diff, _ = edge_vectors_and_lengths(pos, dst_si, src_si, None, normalize=True, eps=1.0)

@@ -6,6 +6,8 @@ out sorted by destination (CSR-ready) with a stable by-source permutation, so th
 result plugs straight into the segment ops.  Cap policy follows torch_cluster: the
 first ``max_num_neighbors`` sources in index order.
 """
+import os
+
 import torch
 
 from .segment import SegIndex
@@ -110,6 +112,12 @@ def interaction_graph_static(pos, data, r, max_num_neighbors=None):
     batch, ptr = data.batch.long(), data.ptr.long()
     dummy = N - 1
     p = pos.detach()
+    if p.is_cuda and os.environ.get("HYDRA_RS_SMALL", "1") == "1":
+        # small batches: the whole builder (both CSR views) in one workgroup, one launch
+        out = _native.ops().radius_static_small(p, batch, ptr, mask, float(r), cap, Ecap, dummy)
+        if out:
+            src, dst, drp, limit, srp, sperm = out
+            return SegIndex(dst, drp, None, N, limit), SegIndex(src, srp, sperm, N, limit)
     if p.is_cuda:
         counts = _native.ops().radius_static_count(p, batch, ptr, mask, float(r), cap)
         rowptr = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0, dtype=torch.int32)])

@@ -287,13 +287,17 @@ def test_cell_list_radius_graph_large_structure_linear_time():
 
 
 @pytest.mark.gpu
-def test_static_radius_graph_gpu_matches_cpu_twin():
-    """Capturable in-forward radius graph (csrc/graph.hip radius_static_*): same edges,
-    CSR views and padding layout as the CPU twin, no host sync (fixed capacity)."""
+@pytest.mark.parametrize("big", [False, True])
+@pytest.mark.parametrize("small_kernel", ["1", "0"])
+def test_static_radius_graph_gpu_matches_cpu_twin(big, small_kernel, monkeypatch):
+    """Capturable in-forward radius graph (csrc/graph.hip radius_static_*, the one-workgroup
+    builder and the multi-launch one): same edges, CSR views (stable source order), limit
+    and padding layout as the CPU twin, no host sync (fixed capacity)."""
     from hydragnn_amd.ops.radius import interaction_graph_static
 
+    monkeypatch.setenv("HYDRA_RS_SMALL", small_kernel)
     g = torch.Generator().manual_seed(3)
-    sizes = [7, 12, 1, 9]
+    sizes = [7, 12, 1, 9] if not big else [int(x) for x in torch.randint(1, 30, (120,), generator=g)]
     pos = torch.cat([torch.rand(n, 3, generator=g) * 3 for n in sizes] + [torch.zeros(3, 3)])
     batch = torch.cat([torch.full((n,), i) for i, n in enumerate(sizes)] + [torch.full((3,), len(sizes))])
     ptr = torch.tensor([0] + list(np.cumsum(sizes + [3])))
@@ -311,6 +315,6 @@ def test_static_radius_graph_gpu_matches_cpu_twin():
     a_dst, a_src = interaction_graph_static(pos, data("cpu"), 1.5, 4)
     b_dst, b_src = interaction_graph_static(pos.cuda(), data("cuda"), 1.5, 4)
     for x, y in [(a_dst.index, b_dst.index), (a_dst.rowptr, b_dst.rowptr), (a_src.index, b_src.index),
-                 (a_src.rowptr, b_src.rowptr), (a_src.perm, b_src.perm)]:
+                 (a_src.rowptr, b_src.rowptr), (a_src.perm, b_src.perm), (a_dst.limit, b_dst.limit)]:
         assert torch.equal(x, y.cpu())
     assert a_dst.index.numel() == pos.shape[0] * 4

@@ -1,0 +1,37 @@
+"""SchNet continuous-filter network in one HIP launch each way (csrc/schnet.hip,
+reference SCFStack.py:214-293): W = (ssp(rbf W1^T + b1) W2^T + b2) * C against the
+plain-torch module chain in fp64 — values and every weight/bias gradient, with and
+without the deferred grouped weight-gradient launch."""
+import pytest
+import torch
+from torch import nn
+
+from hydragnn_amd.models.layers import Linear
+from hydragnn_amd.models.schnet import ShiftedSoftplus, _CFFilter, _filter_fusable
+from hydragnn_amd.ops import linear as lin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("E,K,F", [(1, 50, 64), (333, 50, 64), (5000, 10, 8), (2049, 64, 64), (100, 7, 33)])
+@pytest.mark.parametrize("defer", [False, True])
+def test_cf_filter_matches_module(E, K, F, defer):
+    torch.manual_seed(E + K + F)
+    net = nn.Sequential(Linear(K, F), ShiftedSoftplus(), Linear(F, F)).cuda()
+    rbf = torch.rand(E, K, device="cuda")
+    C = torch.rand(E, device="cuda")
+    assert _filter_fusable(net, rbf, C)
+    G = torch.randn(E, F, device="cuda")
+    with lin.deferred_wgrad(defer):
+        out = _CFFilter.apply(rbf, C, net[0].weight, net[0].bias, net[2].weight, net[2].bias)
+        (out * G).sum().backward()
+    got = [p.grad.clone() for p in net.parameters()]
+    ref_net = nn.Sequential(nn.Linear(K, F), ShiftedSoftplus(), nn.Linear(F, F)).double()
+    with torch.no_grad():
+        for a, b in zip(ref_net.parameters(), net.parameters()):
+            a.copy_(b.double().cpu())
+    ref = ref_net(rbf.double().cpu()) * C.double().cpu().view(-1, 1)
+    (ref * G.double().cpu()).sum().backward()
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-5, atol=1e-5)
+    for a, b in zip(got, ref_net.parameters()):
+        torch.testing.assert_close(a.double().cpu(), b.grad, rtol=1e-4, atol=1e-4 * max(1.0, E ** 0.5 / 10))
