@@ -656,6 +656,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
         const float dx = lpos[3 * j] - xi, dy = lpos[3 * j + 1] - yi, dz = lpos[3 * j + 2] - zi;
         if (dx * dx + dy * dy + dz * dz <= r2) {
           lsrc[q] = j;
+          src_o[q] = j;
           dst_o[q] = i;
           ++q;
         }
@@ -664,6 +665,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
   }
   for (int e = total + t; e < Ecap; e += kRsThreads) {
     lsrc[e] = dummy;
+    src_o[e] = dummy;
     dst_o[e] = dummy;
   }
   if (t == 0) {
@@ -705,13 +707,11 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
       }
       lperm[b + k + 1] = v;
     }
+    for (int a = 0; a < n; ++a) sperm_o[b + a] = lperm[b + a];
   }
+  for (int e = total + t; e < Ecap; e += kRsThreads) sperm_o[dbase + (e - total)] = e;
   __syncthreads();
   RS_STAMP(10);
-  for (int e = t; e < Ecap; e += kRsThreads) {
-    src_o[e] = lsrc[e];
-    sperm_o[e] = lperm[e];
-  }
   for (int i = t; i <= N; i += kRsThreads) srp_o[i] = sc[i];
   RS_STAMP(11);
 #undef RS_STAMP

@@ -52,15 +52,28 @@ __global__ void __launch_bounds__(256) cf_filter_fwd_kernel(const float* __restr
   __shared__ float ws[2][kMaxW][kMaxW + 1];  // W1, W2 rows (odd stride: row-per-lane reads conflict-free)
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int e0 = blockIdx.x * kEB;
-  for (int i = threadIdx.x; i < kEB * kMaxW; i += 256) {
-    const int r = i >> 6, k = i & 63;
-    xs[r][k] = (e0 + r < E && k < K) ? rbf[(int64_t)(e0 + r) * ldr + k] : 0.f;
+  // every global load of the staging is issued before the first LDS store (a loop that
+  // stores each load to LDS waits one memory latency per iteration)
+  float tx[kEB / 4], t1[kMaxW / 4], t2[kMaxW / 4];
+#pragma unroll
+  for (int u = 0; u < kEB / 4; ++u) {
+    const int r = q + 4 * u;
+    tx[u] = (e0 + r < E && c < K) ? rbf[(int64_t)(e0 + r) * ldr + c] : 0.f;
   }
-  for (int r = q; r < F; r += 4) {  // row r of W1 / W2: lanes over its columns (coalesced)
-    if (c < K) ws[0][r][c] = W1[r * K + c];
-    if (c < F) ws[1][r][c] = W2[r * F + c];
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) {  // row r of W1 / W2: lanes over its columns (coalesced)
+    const int r = q + 4 * u;
+    t1[u] = (r < F && c < K) ? W1[r * K + c] : 0.f;
+    t2[u] = (r < F && c < F) ? W2[r * F + c] : 0.f;
   }
   const float bias1 = c < F ? b1[c] : 0.f, bias2 = c < F ? b2[c] : 0.f;
+#pragma unroll
+  for (int u = 0; u < kEB / 4; ++u) xs[q + 4 * u][c] = tx[u];
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) {
+    ws[0][q + 4 * u][c] = t1[u];
+    ws[1][q + 4 * u][c] = t2[u];
+  }
   __syncthreads();
   float w[kMaxW];
 #pragma unroll
@@ -91,14 +104,19 @@ __global__ void __launch_bounds__(256) cf_filter_bwd_kernel(const float* __restr
   __shared__ __attribute__((aligned(16))) float gs[kEB][kLd];
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int e0 = blockIdx.x * kEB;
-  for (int i = threadIdx.x; i < kEB * kMaxW; i += 256) {
-    const int r = i >> 6, k = i & 63, e = e0 + r;
-    float g = 0.f;
-    if (e < E && k < F) {
-      g = dW[(int64_t)e * F + k] * C[e];
-      dH2[(int64_t)e * F + k] = g;
-    }
-    gs[r][k] = g;
+  float tg[kEB / 4], tc[kEB / 4];
+#pragma unroll
+  for (int u = 0; u < kEB / 4; ++u) {  // all loads in flight before any use
+    const int e = e0 + q + 4 * u;
+    tg[u] = (e < E && c < F) ? dW[(int64_t)e * F + c] : 0.f;
+    tc[u] = e < E ? C[e] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kEB / 4; ++u) {
+    const int r = q + 4 * u, e = e0 + r;
+    const float g = tg[u] * tc[u];
+    if (e < E && c < F) dH2[(int64_t)e * F + c] = g;
+    gs[r][c] = g;
   }
   // dgrad operand: column c of W2 (da1[e, c] = sum_j dh2[e, j] W2[j, c])
   float w[kMaxW];

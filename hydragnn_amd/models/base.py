@@ -586,10 +586,11 @@ class Base(nn.Module):
             return None
         _rng.advance(next(self.parameters()).device)
         x, equiv, ctx = self.encode(data)
-        x_graph = ctx.pooled if ctx.get("pooled") is not None else seg.segment_mean(x, ctx.graph_si)
+        fused_enc = ctx.get("pooled") is not None  # the whole-encoder fused path pooled already
+        x_graph = ctx.pooled if fused_enc else seg.segment_mean(x, ctx.graph_si)
         if x_graph.shape[0] != G or x_graph.shape[1] != self.hidden_dim:
             raise RuntimeError("fused_train_loss: pooled features do not match the targets")
-        loss, _ = _mlp.head_loss(x_graph, layers, target, mask, self.loss_function_type)
+        loss, _ = _mlp.head_loss(x_graph, layers, target, mask, self.loss_function_type, side=fused_enc)
         return loss, [loss]
 
     # ------------------------------------------------------------------ losses

@@ -208,25 +208,38 @@ class _HeadLoss(torch.autograd.Function):
         return (out[0], None, None, None, None, None, *out[1:])
 
 
+_side_state = {"ok": True}
+
+
 def _side_slots(x, kind, params):
     """Gradient slots for the head's parameters when the side-stream split applies (training
-    step under ``parallel.gradslots.use``, CUDA, not RMSE — its dx needs the batch loss;
-    ``HYDRA_HEADLOSS_SIDE=0`` disables), else None."""
-    if not x.is_cuda or kind == _KIND["rmse"] or os.environ.get("HYDRA_HEADLOSS_SIDE", "1") != "1":
+    step under ``parallel.gradslots.use``, CUDA, not RMSE — its dx needs the batch loss), else
+    None.  ``HYDRA_HEADLOSS_SIDE``: ``auto`` (default) follows the caller's hint (``head_loss``
+    ``side``: on for the fused GPS encoder, where the twin overlaps the multi-stream backward;
+    measured off for launch-bound steps such as QM9 SchNet: 0.51 vs 0.57-0.67 ms/step), ``1``
+    always, ``0`` never."""
+    mode = os.environ.get("HYDRA_HEADLOSS_SIDE", "auto")
+    if not x.is_cuda or kind == _KIND["rmse"] or mode == "0" or (mode != "1" and not _side_state["ok"]):
         return None
     if not _streams.enabled(x):
         return None
     return _gradslots.slots(params)
 
 
-def head_loss(x, layers, target, mask, kind, fused=None):
+def head_loss(x, layers, target, mask, kind, fused=None, side=True):
     """(loss, pred) of a masked-loss graph head over the pooled features ``x``.  ``fused``
     (default: when grad mode is on; ``HYDRA_HEADLOSS_FUSED=0`` disables): gradients computed
-    inside the forward launch (see ``_HeadLoss``)."""
+    inside the forward launch (see ``_HeadLoss``).  ``side``: the side-stream split may apply
+    (see ``_side_slots``)."""
     params = []
     for m, _ in layers:
         params += [m.weight, m.bias]
     if fused is None:
         fused = torch.is_grad_enabled() and os.environ.get("HYDRA_HEADLOSS_FUSED", "1") == "1"
-    return _HeadLoss.apply(x.contiguous(), target.contiguous(), None if mask is None else mask.contiguous(),
-                           _KIND[kind], [int(r) for _, r in layers], bool(fused), *params)
+    prev = _side_state["ok"]
+    _side_state["ok"] = bool(side)
+    try:
+        return _HeadLoss.apply(x.contiguous(), target.contiguous(), None if mask is None else mask.contiguous(),
+                               _KIND[kind], [int(r) for _, r in layers], bool(fused), *params)
+    finally:
+        _side_state["ok"] = prev
