@@ -614,6 +614,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
   int* lmk = lgp + G + 1;                                // [N] valid-node flags
   __shared__ int s_dummy_real;
   const int t = threadIdx.x;
+  const int probe = dbg ? (int)dbg[15] : 0;  // profiling only: 1 = skip the sort-phase / srp stores
   RS_STAMP(0);
   for (int i = t; i < 3 * N; i += kRsThreads) lpos[i] = pos[i];
   for (int i = t; i < N; i += kRsThreads) {
@@ -707,12 +708,14 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
       }
       lperm[b + k + 1] = v;
     }
-    for (int a = 0; a < n; ++a) sperm_o[b + a] = lperm[b + a];
+    if (!(probe & 1))
+      for (int a = 0; a < n; ++a) sperm_o[b + a] = lperm[b + a];
   }
   for (int e = total + t; e < Ecap; e += kRsThreads) sperm_o[dbase + (e - total)] = e;
   __syncthreads();
   RS_STAMP(10);
-  for (int i = t; i <= N; i += kRsThreads) srp_o[i] = sc[i];
+  if (!(probe & 1))
+    for (int i = t; i <= N; i += kRsThreads) srp_o[i] = sc[i];
   RS_STAMP(11);
 #undef RS_STAMP
 }

@@ -44,13 +44,20 @@ for G in (4, 16, 64, 128, 256):
 # per-phase shader-clock stamps of one call (thread 0 of the workgroup, s_memtime)
 from hydragnn_amd import _native  # noqa: E402
 
-for G in (4, 64):
+for G, probe in ((4, 0), (64, 0), (64, 1)):
     pos, d = batch(G)
     dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+    dbg[15] = probe
     N = pos.shape[0]
     for _ in range(2):
         _native.ops().radius_static_small(pos, d.batch.long(), d.ptr.long(), d["node_mask"], 5.0, 5, N * 5, N - 1, dbg)
     torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        _native.ops().radius_static_small(pos, d.batch.long(), d.ptr.long(), d["node_mask"], 5.0, 5, N * 5, N - 1, dbg)
+    torch.cuda.synchronize()
+    print(f"  {1e6 * (time.perf_counter() - t0) / 50:.1f} us per raw call")
     st = dbg.cpu().tolist()[:12]
     names = ["start", "stage", "count", "scan", "fill", "srccnt", "dummy", "scan2", "place", "sort", "out"]
-    print(f"G {G}: " + ", ".join(f"{n} +{st[i + 1] - st[i]}" for i, n in enumerate(names[1:])), flush=True)
+    print(f"G {G} probe {probe}: " + ", ".join(f"{n} +{st[i + 1] - st[i]}" for i, n in enumerate(names[1:])), flush=True)
