@@ -562,9 +562,10 @@ std::tuple<at::Tensor, at::Tensor> radius_static_fill(const at::Tensor& pos_, co
 // workgroup: count -> exclusive scan -> fill -> source CSR (count, scan, stable placement)
 // all in LDS.  The multi-launch form (count, scan, fill, index_add, scan, radix sort by
 // source, casts and copies: ~15 launches) is launch-bound at this size.  The source view
-// is stable (edges of one source in ascending edge order, as a stable sort gives): real
-// edges are placed by LDS atomics and each bucket's few entries insertion-sorted; the
-// padding slots (all of source `dummy`) are appended after its real edges in slot order.
+// is stable (edges of one source in ascending edge order, as a stable sort gives): the
+// thread of a source walks its graph's receivers in order and finds the source in each
+// receiver's (source-ascending) row; the padding slots (all of source `dummy`) are
+// appended after its real edges in slot order.
 constexpr int kRsThreads = 1024;
 
 // exclusive scan of a[0, n) in place (LDS), returns the total; every thread must call
@@ -689,33 +690,49 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
   if (t == 0) sc[N] = Ecap;
   __syncthreads();
   RS_STAMP(8);
-  for (int e = t; e < total; e += kRsThreads) {
-    const int s = lsrc[e];
-    lperm[sc[s] + atomicAdd(&fc[s], 1)] = e;
+  // stable placement without sorting: the thread of source s walks the receivers of its graph
+  // in ascending order (= ascending edge id) and finds s in each receiver's row (rows list
+  // their sources in ascending order, at most `cap` of them).  (Atomic placement plus a
+  // per-bucket insertion sort was 30-40 us here: the first sources of every graph are taken
+  // by all its receivers, so their buckets are long.)
+  for (int s = t; s < N; s += kRsThreads) {
+    if (!lmk[s]) continue;  // sources of real edges are valid nodes
+    int k = sc[s];
+    const int g = lng[s];
+    const int j1 = lgp[g + 1];
+    if (cap <= 8) {  // rows of <= 8 sources: branch-free probe, all LDS reads in flight
+      for (int i = lgp[g]; i < j1; ++i) {
+        const int q0 = rp[i], q1 = i + 1 < N ? rp[i + 1] : total;
+        int hit = -1;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int q = q0 + c;
+          const int v = lsrc[min(q, Ecap - 1)];
+          hit = (q < q1 && v == s) ? q : hit;
+        }
+        if (hit >= 0) lperm[k++] = hit;
+      }
+    } else {
+      for (int i = lgp[g]; i < j1; ++i) {
+        const int q1 = i + 1 < N ? rp[i + 1] : total;
+        for (int q = rp[i]; q < q1; ++q) {
+          const int v = lsrc[q];
+          if (v >= s) {
+            if (v == s) lperm[k++] = q;
+            break;
+          }
+        }
+      }
+    }
   }
   const int dbase = sc[dummy] + s_dummy_real;
   for (int e = total + t; e < Ecap; e += kRsThreads) lperm[dbase + (e - total)] = e;
   __syncthreads();
   RS_STAMP(9);
-  for (int s = t; s < N; s += kRsThreads) {  // stable order: sort each bucket's real edges
-    const int b = sc[s], n = s == dummy ? s_dummy_real : sc[s + 1] - b;
-    for (int a = 1; a < n; ++a) {
-      const int v = lperm[b + a];
-      int k = a - 1;
-      while (k >= 0 && lperm[b + k] > v) {
-        lperm[b + k + 1] = lperm[b + k];
-        --k;
-      }
-      lperm[b + k + 1] = v;
-    }
-    if (!(probe & 1))
-      for (int a = 0; a < n; ++a) sperm_o[b + a] = lperm[b + a];
-  }
-  for (int e = total + t; e < Ecap; e += kRsThreads) sperm_o[dbase + (e - total)] = e;
-  __syncthreads();
-  RS_STAMP(10);
+  for (int e = t; e < Ecap; e += kRsThreads) sperm_o[e] = lperm[e];
   if (!(probe & 1))
     for (int i = t; i <= N; i += kRsThreads) srp_o[i] = sc[i];
+  RS_STAMP(13);
   RS_STAMP(11);
 #undef RS_STAMP
 }

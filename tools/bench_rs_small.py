@@ -58,6 +58,7 @@ for G, probe in ((4, 0), (64, 0), (64, 1)):
         _native.ops().radius_static_small(pos, d.batch.long(), d.ptr.long(), d["node_mask"], 5.0, 5, N * 5, N - 1, dbg)
     torch.cuda.synchronize()
     print(f"  {1e6 * (time.perf_counter() - t0) / 50:.1f} us per raw call")
-    st = dbg.cpu().tolist()[:12]
-    names = ["start", "stage", "count", "scan", "fill", "srccnt", "dummy", "scan2", "place", "sort", "out"]
-    print(f"G {G} probe {probe}: " + ", ".join(f"{n} +{st[i + 1] - st[i]}" for i, n in enumerate(names[1:])), flush=True)
+    st = dbg.cpu().tolist()[:14]
+    names = ["stage", "count", "scan", "fill", "srccnt", "dummy", "scan2", "cap", "place"]
+    ph = [f"{n} +{st[i + 1] - st[i]}" for i, n in enumerate(names)] + [f"out +{st[11] - st[9]}"]
+    print(f"G {G} probe {probe}: " + ", ".join(ph), flush=True)
