@@ -700,17 +700,18 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
     int k = sc[s];
     const int g = lng[s];
     const int j1 = lgp[g + 1];
-    if (cap <= 8) {  // rows of <= 8 sources: branch-free probe, all LDS reads in flight
+    if (cap <= 8) {  // rows of <= 8 sources: unconditional window loads (all in flight), no branches
+      int q0 = rp[lgp[g]];
       for (int i = lgp[g]; i < j1; ++i) {
-        const int q0 = rp[i], q1 = i + 1 < N ? rp[i + 1] : total;
+        const int q1 = i + 1 < N ? rp[i + 1] : total;
+        int vv[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) vv[c] = lsrc[min(q0 + c, Ecap - 1)];
         int hit = -1;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int q = q0 + c;
-          const int v = lsrc[min(q, Ecap - 1)];
-          hit = (q < q1 && v == s) ? q : hit;
-        }
+        for (int c = 0; c < 8; ++c) hit = (vv[c] == s) & (q0 + c < q1) ? q0 + c : hit;
         if (hit >= 0) lperm[k++] = hit;
+        q0 = q1;
       }
     } else {
       for (int i = lgp[g]; i < j1; ++i) {
