@@ -22,6 +22,7 @@ from torch import nn
 
 from ..ops import segment as seg
 from ..ops.geometry import BesselBasis, Envelope, edge_vectors_and_lengths
+from ..ops.linear import linear_cols
 from .layers import Linear
 from .base import Base
 
@@ -229,11 +230,12 @@ class HydraEmbeddingBlock(nn.Module):
     def forward(self, x, rbf, dst_si, src_si, edge_attr=None):
         H = x.shape[1]
         W = self.lin.weight
-        nb = torch.nn.functional.linear(x, torch.cat([W[:, :H], W[:, H:2 * H]], 0))  # [x_i | x_j] blocks
-        h = seg.gather(nb[:, :W.shape[0]], dst_si) + seg.gather(nb[:, W.shape[0]:], src_si) + self.lin.bias
-        h = h + torch.nn.functional.linear(self.act(self.lin_rbf(rbf)), W[:, 2 * H:3 * H])
+        # concat-linear split: the node blocks [x_i | x_j] at node level, then gathered; every
+        # column block's weight gradient joins the deferred grouped launch (ops.linear.linear_cols)
+        h = seg.gather(linear_cols(x, W, 0), dst_si) + seg.gather(linear_cols(x, W, H), src_si) + self.lin.bias
+        h = h + linear_cols(self.act(self.lin_rbf(rbf)), W, 2 * H)
         if edge_attr is not None and hasattr(self, "edge_lin"):
-            h = h + torch.nn.functional.linear(self.act(self.edge_lin(edge_attr)), W[:, 3 * H:])
+            h = h + linear_cols(self.act(self.edge_lin(edge_attr)), W, 3 * H)
         return self.act(h)
 
 

@@ -62,6 +62,9 @@ def weight_images(Ws, kps=None, nps=None, need=(True, True)):
     return out
 
 
+stats = {"nt": 0}  # bf16 MFMA GEMM launches issued (incl. recorded into captured graphs)
+
+
 def nt(A, B, K, N, *, A2=None, k1=None, bias=None, act=0, gate=None, addg=None, addg_idx=None, outf=None, beta=0.0,
        outb=None, ones_col=-1, rowvec=None, rowdot=None, bm=None):
     """epi(A @ B^T): A [M, >=K] padded bf16 (or [A | A2] concatenated at column k1), B
@@ -71,6 +74,7 @@ def nt(A, B, K, N, *, A2=None, k1=None, bias=None, act=0, gate=None, addg=None, 
         # the glds-staged 64-row tile measured fastest on every EGNN shape on MI355X
         # (profiles/r3_bench_bgemm.log: 752 TF/s at 35k x 896 x 896 vs 571 for hipBLASLt)
         bm = GEMM_TILE
+    stats["nt"] += 1
     _native.ops().bg_nt(A, A2, K if k1 is None else k1, B, K, N, bias, act, gate, addg, addg_idx, outf, beta, outb,
                         ones_col, rowvec, rowdot, bm)
 

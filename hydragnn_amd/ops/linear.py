@@ -204,6 +204,46 @@ class _TallLinear(torch.autograd.Function):
         return dx, dW, db
 
 
+class _ColBlockLinear(torch.autograd.Function):
+    """y = x @ W[:, k0:k0+K]^T for a column block of a (concat-)linear weight: the block's
+    weight gradient joins the deferred grouped launch as a column-block problem (``_span``)
+    instead of autograd's slice backward (a zero-filled full gradient plus a library GEMM
+    with a ~10^4-row reduction dimension on a handful of workgroups)."""
+
+    @staticmethod
+    def forward(ctx, x, W, k0):
+        K = x.shape[1]
+        w = W[:, k0:k0 + K]
+        ctx.save_for_backward(x, W)
+        ctx.k0 = k0
+        return F.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        k0, K = ctx.k0, x.shape[1]
+        w = W[:, k0:k0 + K]
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            if _can_defer(W, None):
+                _defer["items"].append((dy, x, W, None, k0))
+            else:
+                dW = torch.zeros_like(W)
+                g, _ = _native.ops().linear_wgrad(dy.contiguous(), x.contiguous(), False)
+                dW[:, k0:k0 + K] = g
+        return dx, dW, None
+
+
+def linear_cols(x, W, k0):
+    """``F.linear(x, W[:, k0:k0 + x.shape[1]])`` — one column block of a concat-linear weight
+    (GPU fp32 tall inputs: grouped deferred weight gradient; otherwise plain autograd)."""
+    if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[0] >= MIN_ROWS and \
+            torch.is_grad_enabled() and W.requires_grad and _mode.fused("linear"):
+        return _ColBlockLinear.apply(x.contiguous(), W, int(k0))
+    return F.linear(x, W[:, k0:k0 + x.shape[1]])
+
+
 _EDGE_LINEAR = os.environ.get("HYDRA_EDGE_LINEAR", "1") == "1"
 
 

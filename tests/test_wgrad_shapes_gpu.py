@@ -45,3 +45,26 @@ def test_grouped_wgrad_swapped_narrow(M, O, I, block):
     torch.testing.assert_close(dW, 2 * ref, rtol=1e-4, atol=2e-3 * max(1.0, M ** 0.5 / 10))
     if block:  # the columns outside the block are untouched
         assert torch.equal(full[:, :2], before[:, :2]) and torch.equal(full[:, 2 + I:], before[:, 2 + I:])
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_linear_cols_matches_slices(defer):
+    """ops.linear.linear_cols: column blocks of one concat-linear weight (DimeNet's embedding
+    block) with the blocks' weight gradients in the deferred grouped launch == autograd
+    through weight slices."""
+    from hydragnn_amd.ops import linear as lin
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    W0 = torch.randn(64, 200, generator=g)
+    xs = [torch.randn(3000, k, generator=g).cuda() for k in (64, 64, 64, 8)]
+    offs = [0, 64, 128, 192]
+    G = torch.randn(3000, 64, generator=g).cuda()
+    Wa = torch.nn.Parameter(W0.clone().cuda())
+    with lin.deferred_wgrad(defer):
+        y = sum(lin.linear_cols(x, Wa, k0) for x, k0 in zip(xs, offs))
+        (y * G).sum().backward()
+    Wb = W0.clone().cuda().requires_grad_()
+    yb = sum(torch.nn.functional.linear(x, Wb[:, k0:k0 + x.shape[1]]) for x, k0 in zip(xs, offs))
+    (yb * G).sum().backward()
+    torch.testing.assert_close(y, yb, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(Wa.grad, Wb.grad, rtol=1e-4, atol=1e-2)
