@@ -167,7 +167,8 @@ def run(name, steps, warmup, dev):
     rng = np.random.default_rng(0)
     if forces:
         ts = TrainStep(model, lr=1e-3, mode=os.environ.get("BENCH_FORCES_MODE", "graph"), compute_grad_energy=True,
-                       node_bucket=512, edge_bucket=4096)
+                       node_bucket=int(os.environ.get("BENCH_NODE_BUCKET", "512")),
+                       edge_bucket=int(os.environ.get("BENCH_EDGE_BUCKET", "4096")))
         ts.prepare(store, B)
         ts.precapture(store, B)
 
