@@ -326,6 +326,9 @@ class _EngineSumF32(_TallLinearSum):
 
 
 MIN_ROWS = 1024  # below this the library GEMM is already latency-bound and fine
+# HYDRA_ENGINE_FWD1=1: single-input tall fp32 forwards on the engine instead of the library GEMM
+# (A/B on MI355X, profiles/r5_ab_engine_fwd1.log: DimeNet 3.12 -> 3.44 ms, SchNet 0.404 -> 0.427 ms: off)
+_ENGINE_FWD1 = os.environ.get("HYDRA_ENGINE_FWD1", "0") == "1"
 BF16_MIN_MACS = int(os.environ.get("HYDRA_BF16_MIN_MACS", str(1 << 26)))
 ENGINE_SUM_MAX_ROWS = 8192  # fp32 multi-input sums above this use the library GEMM pair
 
@@ -369,7 +372,10 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     tall = engine and xs[0].shape[0] >= MIN_ROWS and torch.is_grad_enabled() and \
         any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
     if len(pairs) == 1:
-        y = _TallLinear.apply(xs[0], ws[0], b) if tall else F.linear(xs[0], ws[0], b)
+        if tall and _ENGINE_FWD1 and xs[0].shape[0] < ENGINE_SUM_MAX_ROWS * 4:
+            y = _EngineSumF32.apply(b, xs[0], ws[0])  # HYDRA_ENGINE_FWD1=1: engine forward (A/B knob)
+        else:
+            y = _TallLinear.apply(xs[0], ws[0], b) if tall else F.linear(xs[0], ws[0], b)
     elif tall:
         flat = []
         for x, w in zip(xs, ws):
