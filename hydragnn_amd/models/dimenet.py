@@ -202,6 +202,38 @@ def _glorot_orthogonal(w, scale=2.0):
     w.data *= s.sqrt()
 
 
+class _ResMLP(torch.autograd.Function):
+    """y = x + silu(lin2(silu(lin1(x)))) in one HIP launch each way (csrc/resmlp.hip); the
+    backward kernel emits the weight gradients' row factors, which join the deferred grouped
+    weight-gradient launch (ops/linear.py) when it is open."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        from .. import _native
+
+        y, H1, H2 = _native.ops().res_mlp_fwd(x, W1, b1, W2, b2)
+        ctx.save_for_backward(x, H1, H2, W1, W2)
+        ctx.params = (W1, b1, W2, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+        from ..ops import linear as _lin
+
+        x, H1, H2, W1, W2 = ctx.saved_tensors
+        dx, dH2, A1, dH1 = _native.ops().res_mlp_bwd(g, H1, H2, W1, W2)
+        W1p, b1p, W2p, b2p = ctx.params
+        if _lin._can_defer(W1p, b1p) and _lin._can_defer(W2p, b2p):
+            _lin._defer["items"].append((dH2, A1, W2p, b2p))
+            _lin._defer["items"].append((dH1, x, W1p, b1p))
+            return dx, None, None, None, None
+        dW1, db1 = torch.empty_like(W1p), torch.empty_like(b1p)
+        dW2, db2 = torch.empty_like(W2p), torch.empty_like(b2p)
+        _native.ops().linear_wgrad_grouped([dH2, dH1], [A1, x], [dW2, dW1], [db2, db1], [0, 0])
+        return dx, dW1, db1, dW2, db2
+
+
 class ResidualLayer(nn.Module):
     def __init__(self, hidden, act):
         super().__init__()
@@ -213,6 +245,11 @@ class ResidualLayer(nn.Module):
             l.bias.data.fill_(0)
 
     def forward(self, x):
+        from ..ops.pna import fused
+
+        if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] <= 64 and x.shape[0] >= 1024
+                and isinstance(self.act, nn.SiLU) and fused("resmlp") and torch.is_grad_enabled()):
+            return _ResMLP.apply(x.contiguous(), self.lin1.weight, self.lin1.bias, self.lin2.weight, self.lin2.bias)
         return x + self.act(self.lin2(self.act(self.lin1(x))))
 
 

@@ -35,3 +35,41 @@ def test_cf_filter_matches_module(E, K, F, defer):
     torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-5, atol=1e-5)
     for a, b in zip(got, ref_net.parameters()):
         torch.testing.assert_close(a.double().cpu(), b.grad, rtol=1e-4, atol=1e-4 * max(1.0, E ** 0.5 / 10))
+
+
+@pytest.mark.parametrize("M,F", [(1030, 64), (5000, 32), (2049, 17)])
+@pytest.mark.parametrize("defer", [False, True])
+def test_residual_silu_block_matches_module(M, F, defer):
+    """DimeNet++ ResidualLayer in one launch each way (csrc/resmlp.hip):
+    y = x + silu(lin2(silu(lin1(x)))) against the fp64 module chain — values, dx and every
+    weight/bias gradient."""
+    from hydragnn_amd.models.dimenet import ResidualLayer
+
+    torch.manual_seed(M + F)
+    layer = ResidualLayer(F, nn.SiLU()).cuda()
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    x = torch.randn(M, F, device="cuda", requires_grad=True)
+    G = torch.randn(M, F, device="cuda")
+    with lin.deferred_wgrad(defer):
+        y = layer(x)
+        (y * G).sum().backward()
+    assert y.grad_fn is not None and "ResMLP" in type(y.grad_fn).__name__
+    x64 = x.detach().double().cpu().requires_grad_()
+    l1 = nn.Linear(F, F).double()
+    l2 = nn.Linear(F, F).double()
+    with torch.no_grad():
+        l1.weight.copy_(layer.lin1.weight.double().cpu())
+        l1.bias.copy_(layer.lin1.bias.double().cpu())
+        l2.weight.copy_(layer.lin2.weight.double().cpu())
+        l2.bias.copy_(layer.lin2.bias.double().cpu())
+    act = nn.SiLU()
+    ref = x64 + act(l2(act(l1(x64))))
+    (ref * G.double().cpu()).sum().backward()
+    torch.testing.assert_close(y.double().cpu(), ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double().cpu(), x64.grad, rtol=1e-4, atol=1e-4)
+    tol = 1e-4 * max(1.0, M ** 0.5 / 10)
+    for got, want in ((layer.lin1.weight.grad, l1.weight.grad), (layer.lin1.bias.grad, l1.bias.grad),
+                      (layer.lin2.weight.grad, l2.weight.grad), (layer.lin2.bias.grad, l2.bias.grad)):
+        torch.testing.assert_close(got.double().cpu(), want, rtol=1e-4, atol=tol)
