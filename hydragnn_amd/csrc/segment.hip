@@ -602,9 +602,85 @@ at::Tensor seg_pna_agg_bwd(const at::Tensor& g_, const at::Tensor& x, const at::
   return dx;
 }
 
+
+// ------------------------------------------------------------------ element CSR (one wave)
+// Owner index over a FEW segments (MACE's per-element weight tables: ~10-100 elements over a
+// batch's nodes) -> (rowptr [S+1], stable permutation [N]) in ONE launch of one wave, instead
+// of the count/scan/radix-sort chain (~9 launches per step).  Counts by LDS atomics, a scan
+// of the S counts, then the nodes in order, 64 at a time: each lane's rank among the earlier
+// lanes of the same segment comes from ballots over the chunk's distinct values (a
+// stable counting sort), and each segment's leader lane advances its cursor.
+constexpr int kElemMaxS = 1024;
+
+__global__ void __launch_bounds__(64) elem_csr_kernel(const int64_t* __restrict__ idx, int N, int S,
+                                                      int* __restrict__ rowptr, int* __restrict__ perm,
+                                                      int* __restrict__ idx32) {
+  __shared__ int cnt[kElemMaxS + 1];
+  __shared__ int cur[kElemMaxS];
+  const int lane = threadIdx.x;
+  for (int s = lane; s < S; s += 64) {
+    cnt[s] = 0;
+    cur[s] = 0;
+  }
+  __syncthreads();
+  for (int n = lane; n < N; n += 64) {
+    const int v = (int)idx[n];
+    idx32[n] = v;
+    atomicAdd(&cnt[v], 1);
+  }
+  __syncthreads();
+  if (lane == 0) {  // S is small: one lane's serial scan
+    int run = 0;
+    for (int s = 0; s < S; ++s) {
+      const int c = cnt[s];
+      cnt[s] = run;
+      run += c;
+    }
+    cnt[S] = run;
+  }
+  __syncthreads();
+  for (int s = lane; s <= S; s += 64) rowptr[s] = cnt[s];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int n0 = 0; n0 < N; n0 += 64) {
+    const int n = n0 + lane;
+    const bool act = n < N;
+    const int v = act ? (int)idx[n] : -1;
+    unsigned long long todo = __ballot(act);
+    int rank = 0, count = 0;
+    while (todo) {  // one round per distinct value of the chunk
+      const int src = __ffsll((long long)todo) - 1;
+      const int u = __shfl(v, src, 64);
+      const unsigned long long same = __ballot(act && v == u);
+      if (v == u) {
+        rank = __popcll(same & lt);
+        count = __popcll(same);
+      }
+      todo &= ~same;
+    }
+    if (act) perm[cnt[v] + cur[v] + rank] = n;
+    __syncthreads();
+    if (act && rank == count - 1) cur[v] += count;  // the segment's last lane in the chunk
+    __syncthreads();
+  }
+}
+
+// idx int64 [N] in [0, S) -> (index int32 [N], rowptr int32 [S+1], perm int32 [N])
+std::vector<at::Tensor> elem_csr(const at::Tensor& idx_, int64_t S) {
+  HY_CHECK_CUDA(idx_);
+  auto idx = idx_.to(at::kLong).contiguous().view({-1});
+  const int64_t N = idx.numel();
+  HY_CHECK(S > 0 && S <= kElemMaxS && N < (1LL << 31), "elem_csr: 0 < segments <= ", kElemMaxS);
+  auto io = idx.options().dtype(at::kInt);
+  auto rowptr = at::empty({S + 1}, io), perm = at::empty({N}, io), idx32 = at::empty({N}, io);
+  elem_csr_kernel<<<1, 64, 0, stream()>>>(idx.data_ptr<int64_t>(), (int)N, (int)S, rowptr.data_ptr<int>(),
+                                          perm.data_ptr<int>(), idx32.data_ptr<int>());
+  return {idx32, rowptr, perm};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("elem_csr(Tensor idx, int S) -> Tensor[]");
   m.def("seg_pna_agg(Tensor x, Tensor rowptr, Tensor? perm, int S, int codes, float avg_log, float avg_lin, "
         "float eps, float sqrt_eps) -> (Tensor, Tensor, Tensor)");
   m.def("seg_pna_agg_bwd(Tensor g, Tensor x, Tensor rowptr, Tensor? perm, Tensor stat, Tensor arg, int S, "
@@ -620,6 +696,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("elem_csr", hy::elem_csr);
   m.impl("seg_sum", hy::seg_sum);
   m.impl("gather_rows", hy::gather_rows);
   m.impl("seg_minmax", hy::seg_minmax);

@@ -219,6 +219,12 @@ def element_index(elem, num_elements):
     from . import segment as seg
 
     elem = elem.view(-1)
+    if elem.is_cuda and 0 < num_elements <= 1024 and elem.numel() > 0:
+        # one launch (csrc/segment.hip elem_csr: stable counting sort in one wave)
+        from .. import _native
+
+        idx32, rowptr, perm = _native.ops().elem_csr(elem, int(num_elements))
+        return seg.SegIndex(idx32, rowptr, perm, num_elements)
     counts = torch.zeros(num_elements, dtype=torch.float32, device=elem.device).index_add_(
         0, elem.long(), torch.ones(elem.shape[0], dtype=torch.float32, device=elem.device))  # exact integer sums
     rowptr = torch.cat([counts.new_zeros(1), counts.cumsum(0)]).to(torch.int32)

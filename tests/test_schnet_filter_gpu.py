@@ -73,3 +73,19 @@ def test_residual_silu_block_matches_module(M, F, defer):
     for got, want in ((layer.lin1.weight.grad, l1.weight.grad), (layer.lin1.bias.grad, l1.bias.grad),
                       (layer.lin2.weight.grad, l2.weight.grad), (layer.lin2.bias.grad, l2.bias.grad)):
         torch.testing.assert_close(got.double().cpu(), want, rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("N,S", [(1, 1), (77, 5), (550, 10), (4000, 118), (130, 1024)])
+def test_element_index_one_wave_matches_cpu(N, S):
+    """ops.o3.element_index on the GPU (csrc/segment.hip elem_csr: stable counting sort in
+    one wave) == the CPU twin (bincount + stable sort): index, CSR and permutation."""
+    from hydragnn_amd.ops.o3 import element_index
+
+    g = torch.Generator().manual_seed(N + S)
+    elem = torch.randint(0, S, (N,), generator=g)
+    if N > 10:
+        elem[::7] = 0  # long runs of one element
+    a = element_index(elem, S)
+    b = element_index(elem.cuda(), S)
+    assert torch.equal(a.index, b.index.cpu()) and torch.equal(a.rowptr, b.rowptr.cpu())
+    assert torch.equal(a.perm, b.perm.cpu())
