@@ -861,12 +861,93 @@ std::tuple<at::Tensor, at::Tensor> triplets_static_fill(const at::Tensor& src, c
   return {kj, ji};
 }
 
+// kj view of the static triplets without a sort: the triplets with kj = k (edge a -> j) are
+// (k, e) for the out-edges e = (j -> i) of j (ascending e: the source CSR's stable order)
+// with i valid and i != a; their ids tptr[e] + pos(k in e's list) ascend with e.  pos is k's
+// rank among j's in-edges, minus one if the skipped in-edge (i -> j) precedes it.
+// MODE 0: counts[k]; MODE 1: perm at kptr[k] (+ the dummy tail of the last edge).
+template <int MODE>
+__global__ void __launch_bounds__(256) tri_kj_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                     const int* __restrict__ rowptr, const int* __restrict__ srowptr,
+                                                     const int* __restrict__ sperm, const bool* __restrict__ mask,
+                                                     int E, const int* __restrict__ tptr, int Tcap,
+                                                     const int* __restrict__ kptr, int* __restrict__ out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < E) {
+    const int k = x, a = src[k], j = dst[k];
+    const int r0 = rowptr[j], r1 = rowptr[j + 1];
+    int c = 0;
+    const int o = MODE ? kptr[k] : 0;
+    for (int q = srowptr[j]; q < srowptr[j + 1]; ++q) {
+      const int e = sperm[q], i = dst[e];
+      if (i == a || (mask && !mask[i])) continue;
+      if constexpr (MODE) {
+        int pos = k - r0;
+        for (int p = r0; p < k; ++p)  // the in-edge of j from i, if it precedes k, is skipped in e's list
+          if (src[p] == i) {
+            --pos;
+            break;
+          }
+        const int t = tptr[e] + pos;
+        if (o + c < Tcap && t < Tcap) out[o + c] = t;
+      }
+      ++c;
+    }
+    (void)r1;
+    if constexpr (!MODE) out[k] = c;
+  }
+  if constexpr (MODE) {  // dummy triplets [T, Tcap) belong to the last edge, after its real ones
+    const int T = min(tptr[E], Tcap);
+    const int base = kptr[E];  // the scanned real total (== T unless the capacity overflowed)
+    for (int t = T + x; t < Tcap; t += gridDim.x * blockDim.x) {
+      const int q = base + (t - T);
+      if (q < Tcap) out[q] = t;
+    }
+  }
+}
+
+// (src, dst, rowptr, srowptr, sperm) of the edge graph, mask, tptr -> (kptr [E+1] with
+// kptr[E] = Tcap, perm [Tcap]): the kj CSR view of triplets_static_fill's list
+std::tuple<at::Tensor, at::Tensor> triplets_static_kj(const at::Tensor& src, const at::Tensor& dst,
+                                                      const at::Tensor& rowptr, const at::Tensor& srowptr,
+                                                      const at::Tensor& sperm, const c10::optional<at::Tensor>& mask,
+                                                      const at::Tensor& tptr, int64_t Tcap) {
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(dst);
+  HY_CHECK_I32(rowptr);
+  HY_CHECK_I32(srowptr);
+  HY_CHECK_I32(sperm);
+  HY_CHECK_I32(tptr);
+  const int E = (int)src.numel();
+  HY_CHECK(E > 0 && sperm.numel() == E && tptr.numel() == E + 1 && srowptr.numel() == rowptr.numel() && Tcap > 0,
+           "triplets_static_kj: sizes");
+  const bool* mk = mask.has_value() ? mask->data_ptr<bool>() : nullptr;
+  auto counts = at::empty({E}, src.options());
+  tri_kj_kernel<0><<<ceil_div(E, 256), 256, 0, stream()>>>(
+      src.data_ptr<int>(), dst.data_ptr<int>(), rowptr.data_ptr<int>(), srowptr.data_ptr<int>(),
+      sperm.data_ptr<int>(), mk, E, tptr.data_ptr<int>(), (int)Tcap, nullptr, counts.data_ptr<int>());
+  auto kptr = at::cat({at::zeros({1}, src.options()), at::cumsum(counts, 0, at::kInt)});
+  // the scanned real total stays at kptr[E] for the dummy base; the view's last row start
+  // is Tcap (the dummy tail belongs to the last edge)
+  auto perm = at::empty({Tcap}, src.options());
+  const int n = std::max<int>(E, (int)std::min<int64_t>(Tcap, 1 << 20));
+  tri_kj_kernel<1><<<ceil_div(n, 256), 256, 0, stream()>>>(
+      src.data_ptr<int>(), dst.data_ptr<int>(), rowptr.data_ptr<int>(), srowptr.data_ptr<int>(),
+      sperm.data_ptr<int>(), mk, E, tptr.data_ptr<int>(), (int)Tcap, kptr.data_ptr<int>(), perm.data_ptr<int>());
+  auto rp = kptr.clone();
+  rp.narrow(0, E, 1).fill_((int)Tcap);
+  return {rp, perm};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "radius_static_small(Tensor pos, Tensor node_graph, Tensor gptr, Tensor? mask, float r, int cap, int Ecap, "
       "int dummy, Tensor? dbg=None) -> Tensor[]");
+  m.def(
+      "triplets_static_kj(Tensor src, Tensor dst, Tensor rowptr, Tensor srowptr, Tensor sperm, Tensor? mask, "
+      "Tensor tptr, int Tcap) -> (Tensor, Tensor)");
   m.def("triplets_static_count(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask) -> Tensor");
   m.def("triplets_static_fill(Tensor src, Tensor dst, Tensor rowptr, Tensor? mask, Tensor tptr, int Tcap) -> (Tensor, Tensor)");
   m.def(
@@ -886,6 +967,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("radius_graph", hy::radius_graph);
   m.impl("triplets", hy::triplets);
   m.impl("triplets_static_count", hy::triplets_static_count);
+  m.impl("triplets_static_kj", hy::triplets_static_kj);
   m.impl("radius_static_small", hy::radius_static_small);
   m.impl("triplets_static_fill", hy::triplets_static_fill);
   m.impl("radius_static_count", hy::radius_static_count);

@@ -15,6 +15,7 @@ segment sum.  The spherical basis uses spherical Bessel functions j_l(z_ln r)
 harmonics Y_l^0(angle) = sqrt((2l+1)/4pi) P_l(cos angle), enveloped as in PyG.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -174,7 +175,13 @@ def triplets_static(dst_si, src_si, node_mask, Tcap):
         counts = _native.ops().triplets_static_count(src, dst, rowptr, mask)
         tptr = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0, dtype=torch.int32)])
         kj, ji = _native.ops().triplets_static_fill(src, dst, rowptr, mask, tptr, int(Tcap))
+        kview = None
+        if src_si.perm is not None and os.environ.get("HYDRA_TRIPLET_KJ_SORT", "0") != "1":
+            # kj CSR view without a sort (csrc/graph.hip triplets_static_kj)
+            kview = _native.ops().triplets_static_kj(src, dst, rowptr, src_si.rowptr, src_si.perm, mask, tptr,
+                                                     int(Tcap))
     else:  # CPU twin (padded_step tests): the eager order, then the dummy tail
+        kview = None
         kj_v, ji_v = triplets_csr(dst_si, src_si, rowptr.numel() - 1)
         if mask is not None:
             keep = mask[dst.long()[ji_v]]
@@ -190,8 +197,11 @@ def triplets_static(dst_si, src_si, node_mask, Tcap):
     limit = tptr[E:E + 1].clamp(max=int(Tcap))
     jrp = tptr.clamp(max=int(Tcap))
     jrp[E:].fill_(int(Tcap))  # the dummy tail belongs to the last edge
-    vals, perm = torch.sort(kj, stable=True)
-    krp = torch.searchsorted(vals, torch.arange(E + 1, dtype=torch.int32, device=kj.device), out_int32=True)
+    if kview is not None:
+        krp, perm = kview
+    else:
+        vals, perm = torch.sort(kj, stable=True)
+        krp = torch.searchsorted(vals, torch.arange(E + 1, dtype=torch.int32, device=kj.device), out_int32=True)
     return (seg.SegIndex(kj, krp, perm.to(torch.int32), E, limit), seg.SegIndex(ji, jrp, None, E, limit))
 
 
