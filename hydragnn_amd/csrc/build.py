@@ -4,7 +4,9 @@ Every ``*.hip`` / ``*.cpp`` file in this directory is compiled directly with
 ``hipcc --offload-arch=gfx950`` (no hipify, no CUDA shims) against the PyTorch
 headers and linked into one shared object whose ops register themselves under
 ``torch.ops.hydra.*`` (TORCH_LIBRARY).  Objects are cached in ``csrc/build/``
-and rebuilt only when a source or header is newer.
+and rebuilt unless the digest stored with the object matches its source, the local
+headers and the flags; the library's digest is derived from the digests of the objects
+it was linked from.
 
 Usage:  python -m hydragnn_amd.csrc.build [-j N] [--force]
 """
@@ -44,30 +46,57 @@ def sources():
     return sorted(glob.glob(os.path.join(HERE, "*.hip")) + glob.glob(os.path.join(HERE, "*.cpp")))
 
 
-def source_digest():
-    """sha256 over every native source and header (names + bytes): written next to the
-    library at build time and checked at load time, so a stale ``_C.so`` (sources edited,
-    library not rebuilt) fails loudly instead of running old kernels."""
+def _headers_bytes():
+    out = b""
+    for h in sorted(glob.glob(os.path.join(HERE, "*.h"))):
+        with open(h, "rb") as fh:
+            out += os.path.basename(h).encode() + fh.read()
+    return out
+
+
+def object_digest(src, flags=(ARCH, "-O3"), headers=None):
+    """sha256 of ONE translation unit's inputs: its bytes, every local header and the
+    compile flags.  Stored beside the object (``<obj>.srchash``); an object is reused only
+    when this digest matches (not by mtime: a copy that preserves times cannot pass off
+    stale objects)."""
     import hashlib
 
     h = hashlib.sha256()
-    for f in sorted(sources() + glob.glob(os.path.join(HERE, "*.h"))):
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
+    h.update(os.path.basename(src).encode())
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    h.update(_headers_bytes() if headers is None else headers)
+    h.update("\0".join(flags).encode())
     return h.hexdigest()
 
 
-def _headers_mtime():
-    hs = glob.glob(os.path.join(HERE, "*.h"))
-    return max([os.path.getmtime(h) for h in hs] + [0.0])
+def source_digest():
+    """sha256 over the per-object digests of every native source (names + bytes + headers):
+    written next to the library at link time FROM THE DIGESTS OF THE OBJECTS LINKED, and
+    checked at load time, so a stale ``_C.so`` (sources edited, library not rebuilt) fails
+    loudly instead of running old kernels."""
+    import hashlib
+
+    hb = _headers_bytes()
+    h = hashlib.sha256()
+    for f in sources():
+        h.update(object_digest(f, headers=hb).encode())
+    return h.hexdigest()
+
+
+def _read(path):
+    try:
+        with open(path) as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
 
 
 def _compile(src, inc, abi, force):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if (not force) and os.path.exists(obj):
-        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
-            return obj, None
+    want = object_digest(src)
+    if (not force) and os.path.exists(obj) and _read(obj + ".srchash") == want:
+        return obj, None, False
     py_inc = sysconfig.get_paths()["include"]
     cmd = [
         _hipcc(),
@@ -83,10 +112,14 @@ def _compile(src, inc, abi, force):
         f"-I{HERE}",
         f"-I{py_inc}",
     ] + [f"-I{p}" for p in inc] + ["-c", src, "-o", obj]
+    if os.path.exists(obj + ".srchash"):
+        os.remove(obj + ".srchash")
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        return obj, f"FAILED: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
-    return obj, None
+        return obj, f"FAILED: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}", True
+    with open(obj + ".srchash", "w") as fh:
+        fh.write(want + "\n")
+    return obj, None, True
 
 
 def build(jobs=None, force=False, verbose=True):
@@ -94,24 +127,36 @@ def build(jobs=None, force=False, verbose=True):
     inc, lib, abi = _torch_paths()
     srcs = sources()
     jobs = jobs or min(8, os.cpu_count() or 4, len(srcs) or 1)
-    objs, errs = [], []
+    objs, errs, rebuilt = [], [], False
     with cf.ThreadPoolExecutor(jobs) as ex:
-        for obj, err in ex.map(lambda s: _compile(s, inc, abi, force), srcs):
+        for obj, err, fresh in ex.map(lambda s: _compile(s, inc, abi, force), srcs):
             objs.append(obj)
+            rebuilt |= fresh
             if err:
                 errs.append(err)
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
-    newest = max(os.path.getmtime(o) for o in objs)
-    if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
+    # the library digest is derived from the digests stored with the objects being linked
+    import hashlib
+
+    h = hashlib.sha256()
+    for o in objs:
+        d = _read(o + ".srchash")
+        if d is None:
+            raise RuntimeError(f"{o} has no source digest")
+        h.update(d.encode())
+    linked = h.hexdigest()
+    if force or rebuilt or not os.path.exists(OUT) or _read(OUT + ".srchash") != linked:
+        if os.path.exists(OUT + ".srchash"):
+            os.remove(OUT + ".srchash")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
             f"-L{lib}", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{lib}",
         ]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    with open(OUT + ".srchash", "w") as fh:
-        fh.write(source_digest() + "\n")
+        with open(OUT + ".srchash", "w") as fh:
+            fh.write(linked + "\n")
     if verbose:
         print(f"[hydragnn_amd] built {OUT} from {len(srcs)} sources for {ARCH}")
     return OUT

@@ -614,7 +614,7 @@ constexpr int kElemMaxS = 1024;
 
 __global__ void __launch_bounds__(64) elem_csr_kernel(const int64_t* __restrict__ idx, int N, int S,
                                                       int* __restrict__ rowptr, int* __restrict__ perm,
-                                                      int* __restrict__ idx32) {
+                                                      int* __restrict__ idx32, int* __restrict__ err) {
   __shared__ int cnt[kElemMaxS + 1];
   __shared__ int cur[kElemMaxS];
   const int lane = threadIdx.x;
@@ -623,11 +623,16 @@ __global__ void __launch_bounds__(64) elem_csr_kernel(const int64_t* __restrict_
     cur[s] = 0;
   }
   __syncthreads();
+  int bad = 0;
   for (int n = lane; n < N; n += 64) {
-    const int v = (int)idx[n];
+    const int64_t r = idx[n];
+    const bool ok = r >= 0 && r < S;
+    bad += ok ? 0 : 1;
+    const int v = ok ? (int)r : S - 1;  // out of range: clamped for memory safety, flagged
     idx32[n] = v;
     atomicAdd(&cnt[v], 1);
   }
+  if (__ballot(bad != 0) && err != nullptr && lane == 0) atomicMax(err, 1);
   __syncthreads();
   if (lane == 0) {  // S is small: one lane's serial scan
     int run = 0;
@@ -644,7 +649,8 @@ __global__ void __launch_bounds__(64) elem_csr_kernel(const int64_t* __restrict_
   for (int n0 = 0; n0 < N; n0 += 64) {
     const int n = n0 + lane;
     const bool act = n < N;
-    const int v = act ? (int)idx[n] : -1;
+    int v = act ? (int)idx[n] : -1;
+    if (act && (v < 0 || v >= S)) v = S - 1;
     unsigned long long todo = __ballot(act);
     int rank = 0, count = 0;
     while (todo) {  // one round per distinct value of the chunk
@@ -665,22 +671,25 @@ __global__ void __launch_bounds__(64) elem_csr_kernel(const int64_t* __restrict_
 }
 
 // idx int64 [N] in [0, S) -> (index int32 [N], rowptr int32 [S+1], perm int32 [N])
-std::vector<at::Tensor> elem_csr(const at::Tensor& idx_, int64_t S) {
+std::vector<at::Tensor> elem_csr(const at::Tensor& idx_, int64_t S, const c10::optional<at::Tensor>& err) {
   HY_CHECK_CUDA(idx_);
   auto idx = idx_.to(at::kLong).contiguous().view({-1});
   const int64_t N = idx.numel();
   HY_CHECK(S > 0 && S <= kElemMaxS && N < (1LL << 31), "elem_csr: 0 < segments <= ", kElemMaxS);
+  HY_CHECK(!err.has_value() || (err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1),
+           "elem_csr: err must be a device int32 flag");
   auto io = idx.options().dtype(at::kInt);
   auto rowptr = at::empty({S + 1}, io), perm = at::empty({N}, io), idx32 = at::empty({N}, io);
   elem_csr_kernel<<<1, 64, 0, stream()>>>(idx.data_ptr<int64_t>(), (int)N, (int)S, rowptr.data_ptr<int>(),
-                                          perm.data_ptr<int>(), idx32.data_ptr<int>());
+                                          perm.data_ptr<int>(), idx32.data_ptr<int>(),
+                                          err.has_value() ? err->data_ptr<int>() : nullptr);
   return {idx32, rowptr, perm};
 }
 
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("elem_csr(Tensor idx, int S) -> Tensor[]");
+  m.def("elem_csr(Tensor idx, int S, Tensor(a!)? err=None) -> Tensor[]");
   m.def("seg_pna_agg(Tensor x, Tensor rowptr, Tensor? perm, int S, int codes, float avg_log, float avg_lin, "
         "float eps, float sqrt_eps) -> (Tensor, Tensor, Tensor)");
   m.def("seg_pna_agg_bwd(Tensor g, Tensor x, Tensor rowptr, Tensor? perm, Tensor stat, Tensor arg, int S, "

@@ -159,6 +159,23 @@ def triplets_csr(dst_si, src_si, num_nodes):
     return e_kj[keep], e_ji[keep]
 
 
+def _note_overflow(total, Tcap):
+    """Record a device triplet count above the static capacity (the fill kernels clamp to
+    ``Tcap``, so such a batch would train on a truncated triplet set): folded into a
+    persistent device flag (``ops/devcheck.py``) that the epoch loop turns into an error."""
+    from ..ops import devcheck
+
+    f = devcheck.flag(total.device, "triplet_cap")
+    torch.maximum(f, total.sub(Tcap), out=f)
+    devcheck.debug_check("triplet_cap", total.device)
+
+
+def check_triplet_overflow():
+    from ..ops import devcheck
+
+    devcheck.check_all()
+
+
 def triplets_static(dst_si, src_si, node_mask, Tcap):
     """Triplets of a statically padded batch with FIXED capacity ``Tcap`` and no host
     synchronisation (capturable; csrc/graph.hip ``triplets_static_*``).  Only edges into
@@ -194,6 +211,8 @@ def triplets_static(dst_si, src_si, node_mask, Tcap):
         kj[:T], ji[:T] = kj_v.int(), ji_v.int()
         tptr = torch.zeros(E + 1, dtype=torch.int32)
         tptr[1:] = torch.cumsum(torch.bincount(ji_v.long(), minlength=E), 0).int()
+    if src.is_cuda:
+        _note_overflow(tptr[E:E + 1], int(Tcap))
     limit = tptr[E:E + 1].clamp(max=int(Tcap))
     jrp = tptr.clamp(max=int(Tcap))
     jrp[E:].fill_(int(Tcap))  # the dummy tail belongs to the last edge

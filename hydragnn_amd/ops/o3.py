@@ -223,7 +223,11 @@ def element_index(elem, num_elements):
         # one launch (csrc/segment.hip elem_csr: stable counting sort in one wave)
         from .. import _native
 
-        idx32, rowptr, perm = _native.ops().elem_csr(elem, int(num_elements))
+        from . import devcheck
+
+        idx32, rowptr, perm = _native.ops().elem_csr(elem, int(num_elements),
+                                                     devcheck.flag(elem.device, "elem_range"))
+        devcheck.debug_check("elem_range", elem.device)
         return seg.SegIndex(idx32, rowptr, perm, num_elements)
     counts = torch.zeros(num_elements, dtype=torch.float32, device=elem.device).index_add_(
         0, elem.long(), torch.ones(elem.shape[0], dtype=torch.float32, device=elem.device))  # exact integer sums

@@ -76,7 +76,8 @@ class FusedAdamW(torch.optim.Optimizer):
             rb = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
             bt = torch.tensor(blocks, dtype=torch.int32).view(-1).to(dev)
             state = torch.tensor([0.0, group["lr"], 0.0], dtype=torch.float32, device=dev)
-            tables.append([rb, bt, state, group["lr"], tuple(p.grad.data_ptr() for p in ps), ps])
+            tables.append([rb, bt, state, group["lr"], tuple(p.grad.data_ptr() for p in ps), ps,
+                           self._hp_key(group)])
         self._tables = tables
 
     def _tables_valid(self):
@@ -124,6 +125,11 @@ class FusedAdamW(torch.optim.Optimizer):
                                      None if g is None else g.reshape(1).float())
         return loss
 
+    @staticmethod
+    def _hp_key(group):
+        """The hyper-parameters a captured launch bakes in as kernel arguments (not lr)."""
+        return (tuple(float(b) for b in group["betas"]), float(group["eps"]), float(group["weight_decay"]))
+
     def sync_hparams(self):
         """Copy the host learning rates into the device scalars the captured update reads.
         A captured step never calls ``step()`` on the host, so without this a schedule
@@ -137,6 +143,8 @@ class FusedAdamW(torch.optim.Optimizer):
         for group, t in zip(self.param_groups, self._tables):
             if t is None:
                 continue
+            if t[6] != self._hp_key(group):
+                ok = False  # betas / eps / weight decay are captured launch arguments
             if t[3] != group["lr"]:
                 t[2][1].fill_(group["lr"])
                 t[3] = group["lr"]

@@ -187,9 +187,9 @@ class BucketedGradSync:
     (≈ the order backward produces them) and cut into contiguous buckets.  Backward
     runs with ``p.grad = None`` so autograd hands over each fresh gradient without an
     accumulate kernel; a post-accumulate hook counts the bucket down and, when the
-    bucket is complete, packs it (one batched copy + the 1/world pre-scale) on the
-    compute stream and launches its all-reduce on a dedicated high-priority comm
-    stream that waits only on that pack.  The rest of backward keeps running on the
+    bucket is complete, a dedicated high-priority comm stream joins the compute stream
+    (and the side streams that write gradient slots), packs the bucket (one batched
+    copy + the 1/world pre-scale) and launches its all-reduce.  The rest of backward keeps running on the
     compute stream while RCCL moves the bucket over xGMI; ``finish`` joins the comm
     stream back before the optimizer reads the buffer.
 
@@ -396,15 +396,22 @@ class BucketedGradSync:
         if self.launched[bi]:
             return
         self.launched[bi] = True
-        buf = self._pack(bi)
-        buf.mul_(1.0 / self.world)
         if self.comm is None:
+            buf = self._pack(bi)
+            buf.mul_(1.0 / self.world)
             self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             return
+        # pack, pre-scale and reduce all run on the comm stream AFTER it joined the compute
+        # stream and every side-stream slot writer: the guard's loss and the head twin's weight
+        # gradients come from side streams, so a pack / scale on the compute stream could read
+        # or scale a slot before its writer finished.  The packed sources (p.grad, the loss, the
+        # usage flags) stay referenced until finish() joins this stream back.
         self.comm.wait_stream(torch.cuda.current_stream())
         for ev in self.side_events:  # slot writers on side streams
             self.comm.wait_event(ev)
         with torch.cuda.stream(self.comm):
+            buf = self._pack(bi)
+            buf.mul_(1.0 / self.world)
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
 
     def eager_reduce(self):
@@ -426,6 +433,9 @@ class BucketedGradSync:
             for w in self.works:
                 w.wait()
         else:
+            if self.flat.is_cuda:  # the loss / slots written on side streams, before the pack reads them
+                for ev in self.side_events:
+                    torch.cuda.current_stream().wait_event(ev)
             for bi in range(len(self.buckets)):
                 self._pack(bi)
         if self.flat.is_cuda:
@@ -540,10 +550,13 @@ class MultiGradSync:
         return None
 
     def provide(self, params, event=None):
-        for s in self.syncs:
+        for i, s in enumerate(self.syncs):
             mine = [p for p in params if p in s.offset]
             if mine:
                 s.provide(mine, event)
+            elif i == 0 and event is not None:
+                # the side stream also produced the loss the guard holder packs
+                s.side_events.append(event)
 
     def begin(self):
         for s in self.syncs:

@@ -456,6 +456,9 @@ def train_validate_test(model, optimizer, train_loader, val_loader, test_loader,
             if epoch == 0:
                 tr.reset()
         _sync_running_stats(model)
+        from ..ops import devcheck
+
+        devcheck.check_all()  # device input checks of captured steps (triplet capacity, element ids)
         t_train = time.time() - t0
         sk = getattr(getattr(optimizer, "optim", optimizer), "skipped_steps", None)
         if sk is not None:

@@ -80,3 +80,40 @@ def test_provided_params_count_down_their_bucket():
     assert launched == [0]
     sync._hook(ps[1])
     assert launched == [0, 1]
+
+
+import pytest
+
+
+@pytest.mark.gpu
+def test_guard_waits_for_side_stream_loss():
+    """The step guard (loss) and slot gradients written on a side stream are packed only
+    after that stream's event (the pack used to read the loss unsynchronised)."""
+    dev = torch.device("cuda")
+    ps = [torch.nn.Parameter(torch.randn(64, 64, device=dev)) for _ in range(3)]
+    sync = BucketedGradSync(ps, bucket_cap_mb=1e9, nflags=1)  # usage flags -> guard packed
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    for trial in range(3):
+        sync.release()
+        sync.begin()
+        loss = torch.zeros((), device=dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(20_000_000)  # the side stream lags far behind the main stream
+            loss.fill_(1.5 + trial)
+            sl = sync.slot(ps[2])
+            sl.fill_(float(trial + 1))
+        ev = torch.cuda.Event()
+        ev.record(side)
+        sync.set_loss(loss)
+        sync.set_flags(torch.ones(1, device=dev))
+        sync.provide([ps[2]], ev)
+        for p in ps[:2]:
+            p.grad = torch.full_like(p, 0.5)
+        sync.finish()
+        assert sync.guard_packed
+        torch.cuda.synchronize()
+        assert float(sync.guard) == 1.5 + trial
+        assert torch.all(ps[2].grad == float(trial + 1))
+        assert torch.all(ps[0].grad == 0.5)
