@@ -1239,7 +1239,7 @@ static void hl_attrs() {
 }
 
 static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::optional<at::Tensor>& mask,
-                      const MlpArgs& a, int64_t kind) {
+                      const MlpArgs& a, int64_t kind, bool one_wg = true) {
   const int64_t G = x.size(0);
   HY_CHECK(kind >= 0 && kind <= 3, "head_loss: unknown loss kind");
   HY_CHECK(target.is_contiguous() && target.scalar_type() == at::kFloat && target.numel() == G * a.dims[a.n],
@@ -1247,7 +1247,8 @@ static void hl_checks(const at::Tensor& x, const at::Tensor& target, const c10::
   if (mask.has_value() && mask->defined())
     HY_CHECK(mask->scalar_type() == at::kBool && mask->is_contiguous() && mask->numel() == G,
              "head_loss: bool mask [G]");
-  HY_CHECK(G >= 1 && hl_lds(a, (int)G) <= kHlMaxLds, "head_loss: rows x widths exceed one workgroup's LDS");
+  HY_CHECK(G >= 1 && (!one_wg || hl_lds(a, (int)G) <= kHlMaxLds),
+           "head_loss: rows x widths exceed one workgroup's LDS");
   static bool once = [] {
     hl_attrs<1>();
     hl_attrs<2>();
@@ -1432,6 +1433,185 @@ std::vector<at::Tensor> head_loss_fused(const at::Tensor& x_, at::TensorList Ws_
   return out;
 }
 
+// ------------------------------------------------------------ dx chain: one workgroup per row
+// The dx-only launch sits on the training step's critical path.  The row-split kernel above
+// runs it on ceil(G / 16) workgroups (3 at the OC20 batch) walking 16-row MFMA tiles.  Rows
+// are independent through the forward, the loss gradient (MAE / MSE / smooth-L1: the batch's
+// kept count is the only coupling, and every workgroup counts it itself) and the dgrad chain,
+// so here ONE workgroup (4 waves) owns ONE row:
+//   * every weight matrix and bias is DMA'd into LDS at entry (global_load_lds, all copies
+//     in flight together: one memory round trip);
+//   * forward, per layer: lane i of wave w forms x[i] W[16 w + jj][i] for its 16 outputs jj
+//     (conflict-free LDS rows); the wave's [16][64] product tile goes through LDS once and
+//     lane t sums a quarter row (out[16 w + t / 4] after two xor shuffles) — a register
+//     butterfly with per-lane half selects was compiled into 16-way select chains;
+//   * backward, per layer: dh[i] = sum_j W[j][i] dy[j] from the same LDS rows against
+//     broadcast dy reads; the 4 waves' partials meet in LDS.
+// The layer loops are ROLLED: the chain executes once per launch, and a first version with
+// the layers unrolled (weights held in registers) was 8.5k instructions of straight-line code
+// whose instruction-cache misses alone took ~30 us.  Widths: input <= 64 CI, every later
+// width <= 64, layers <= 8.  Not RMSE (its dx needs the batch loss).
+template <int CI>
+__global__ void __launch_bounds__(256) head_dx_row_kernel(const float* __restrict__ x, int G, const MlpArgs a,
+                                                          const float* __restrict__ target,
+                                                          const bool* __restrict__ mask, int kind,
+                                                          float* __restrict__ dx) {
+  constexpr int IW = 64 * CI;
+  extern __shared__ float sm[];  // W_0, b_0, W_1, b_1, ... (dense, a.woff / biases after each W)
+  __shared__ float act[kMlpMaxLayers + 1][IW];
+  __shared__ float part[4][IW];
+  __shared__ float dyb[IW];
+  __shared__ float red[4 * 16 * 65];
+  __shared__ int kc[4];
+  const int g = blockIdx.x, tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  // per-layer parameters held lane-indexed (lane l: layer l) and broadcast with v_readlane:
+  // dynamic indexing of the by-value argument struct inside the layer loops expands into
+  // select chains (code size: this kernel runs once per launch, instruction fetch bound)
+  const int ll = lane < kMlpMaxLayers ? lane : kMlpMaxLayers - 1;
+  const int v_dims = a.dims[lane <= kMlpMaxLayers ? lane : kMlpMaxLayers], v_relu = a.relu[ll];
+  const float* v_W = a.W[ll];
+  const float* v_b = a.b[ll];
+  const int n = a.n, D0 = a.dims[0], Do = hl_rl(v_dims, n);
+  // 1) LDS-DMA of every layer's W [O, I] then b [O], 64 floats per wave instruction
+  {
+    int off = 0, chunk = 0;
+    for (int l = 0; l < n; ++l) {
+      const int O = hl_rl(v_dims, l + 1), I = hl_rl(v_dims, l);
+      for (int part2 = 0; part2 < 2; ++part2) {
+        const float* src = part2 == 0 ? hl_rlp(v_W, l) : hl_rlp(v_b, l);
+        const int cnt = part2 == 0 ? O * I : O;
+        for (int c0 = 0; c0 < cnt; c0 += 64, ++chunk)
+          if ((chunk & 3) == w && c0 + lane < cnt)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + c0 + lane),
+                                             (__attribute__((address_space(3))) void*)(sm + off + c0), 4, 0, 0);
+        off += cnt;
+      }
+    }
+  }
+  // 2) the row, the kept count, zeroed buffers
+  const bool keep = mask == nullptr || mask[g];
+  int k = 0;
+  for (int t = tid; t < G; t += 256) k += (mask == nullptr || mask[t]) ? 1 : 0;
+  for (int off = 32; off > 0; off >>= 1) k += __shfl_xor(k, off, 64);
+  if (lane == 0) kc[w] = k;
+  for (int e = tid; e < (kMlpMaxLayers + 1) * IW; e += 256) (&act[0][0])[e] = 0.f;
+  for (int e = tid; e < IW; e += 256) dyb[e] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < D0; i += 256) act[0][i] = x[(int64_t)g * D0 + i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // 3) forward chain (rolled over layers)
+  int off = 0;
+  for (int l = 0; l < n; ++l) {
+    const int O = hl_rl(v_dims, l + 1), I = hl_rl(v_dims, l);
+    const float* Wl = sm + off;
+    float v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      const int i = lane + 64 * c;
+      const float xi = act[l][i];
+      const bool iok = i < I;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = 16 * w + jj;
+        const bool ok = iok && j < O;
+        const float wv = Wl[ok ? j * I + i : 0];
+        v[jj] = fmaf(ok ? wv : 0.f, xi, v[jj]);
+      }
+    }
+    // cross-lane sum over i through LDS: the wave's [16][64] product tile, then lane t sums
+    // a quarter (16 columns) of row t / 4 and the 4 quarters meet by two xor shuffles
+    float* rw = red + w * 16 * 65;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) rw[jj * 65 + lane] = v[jj];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave reads its own tile back
+    __builtin_amdgcn_wave_barrier();
+    float o = 0.f;
+    {
+      const float* rr = rw + (lane >> 2) * 65 + 16 * (lane & 3);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o += rr[r];
+    }
+    o += __shfl_xor(o, 1, 64);
+    o += __shfl_xor(o, 2, 64);
+    const int j = 16 * w + (lane >> 2);
+    const float bj = sm[off + O * I + (j < O ? j : 0)];
+    o += bj;
+    if (hl_rl(v_relu, l)) o = fmaxf(o, 0.f);
+    if ((lane & 3) == 0) act[l + 1][j] = j < O ? o : 0.f;
+    off += O * I + O;
+    __syncthreads();
+  }
+  // 4) loss gradient of the row (upstream gradient 1): MSE 2d / n, MAE sgn(d) / n, smooth-L1
+  // clamp(d) / n over the batch's n = kept rows x outputs
+  if (w == 0 && lane < Do) {
+    const float den0 = (float)(kc[0] + kc[1] + kc[2] + kc[3]) * (float)Do;
+    const float den = den0 > 0.f ? den0 : 1.f;
+    const float p = act[n][lane];
+    float v = 0.f;
+    if (keep) {
+      const float d = p - target[(int64_t)g * Do + lane];
+      const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      v = kind == 1 ? sgn / den : (kind == 3 ? (fabsf(d) < 1.f ? d : sgn) / den : 2.f * d / den);
+    }
+    dyb[lane] = (hl_rl(v_relu, n - 1) && p <= 0.f) ? 0.f : v;
+  }
+  __syncthreads();
+  // 5) dgrad chain (rolled, layers in reverse)
+  for (int l = n - 1; l >= 0; --l) {
+    const int O = hl_rl(v_dims, l + 1), I = hl_rl(v_dims, l);
+    off -= O * I + O;
+    const float* Wl = sm + off;
+    float dj[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) dj[jj] = dyb[16 * w + jj];
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      const int i = lane + 64 * c;
+      const bool iok = i < I;
+      float s2 = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = 16 * w + jj;
+        const bool ok = iok && j < O;
+        const float wv = Wl[ok ? j * I + i : 0];
+        s2 = fmaf(ok ? wv : 0.f, dj[jj], s2);
+      }
+      part[w][i] = s2;
+    }
+    __syncthreads();
+    for (int t = tid; t < IW; t += 256) {
+      float s2 = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+      if (l == 0) {
+        if (t < I) dx[(int64_t)g * I + t] = s2;
+      } else {
+        if (hl_rl(v_relu, l > 0 ? l - 1 : 0) && !(act[l][t] > 0.f)) s2 = 0.f;
+        dyb[t] = t < I ? s2 : 0.f;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static size_t hdx_lds(const MlpArgs& a) {
+  size_t f = 0;
+  for (int l = 0; l < a.n; ++l) f += (size_t)a.dims[l + 1] * a.dims[l] + a.dims[l + 1];
+  return f * sizeof(float);
+}
+
+static bool hdx_row_eligible(const MlpArgs& a, int64_t kind) {
+  static const bool on = [] {
+    const char* e = std::getenv("HYDRA_HEADDX_ROW");
+    return e == nullptr || std::string(e) != "0";
+  }();
+  if (!on || kind == 2 || a.n < 1 || a.n > kMlpMaxLayers || a.dims[0] > 128) return false;
+  for (int l = 1; l <= a.n; ++l)
+    if (a.dims[l] > 64) return false;
+  return hdx_lds(a) <= 96 * 1024;
+}
+
 // dx of the masked loss (upstream gradient 1) alone: the forward chain and the input-gradient
 // chain, nothing else (no predictions, loss value, weight gradients or cross-workgroup step).
 // Not for RMSE (its dx needs the batch loss).  Pairs with head_loss_fused(want_dx=false) on a
@@ -1446,7 +1626,7 @@ at::Tensor head_loss_dx(const at::Tensor& x_, at::TensorList Ws_, at::TensorList
   HY_CHECK(kind != 2, "head_loss_dx: RMSE's input gradient needs the batch loss (use head_loss_fused)");
   std::vector<at::Tensor> Ws(Ws_.begin(), Ws_.end()), bs(bs_.begin(), bs_.end());
   auto a = make_args(x, Ws, bs, relu.vec());
-  hl_checks(x, target, mask, a, kind);
+  hl_checks(x, target, mask, a, kind, !hdx_row_eligible(a, kind));
   long long* dp = nullptr;
   if (dbg.has_value() && dbg->defined()) {
     HY_CHECK(dbg->is_cuda() && dbg->scalar_type() == at::kLong && dbg->is_contiguous() && dbg->numel() >= 32,
@@ -1456,6 +1636,22 @@ at::Tensor head_loss_dx(const at::Tensor& x_, at::TensorList Ws_, at::TensorList
   const int64_t G = x.size(0);
   auto dx = at::empty_like(x);
   const bool* mp = mask.has_value() && mask->defined() ? mask->data_ptr<bool>() : nullptr;
+  if (dp == nullptr && hdx_row_eligible(a, kind)) {
+    const size_t lds = hdx_lds(a);
+    static bool attrs = [] {
+      hipFuncSetAttribute((const void*)head_dx_row_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+      hipFuncSetAttribute((const void*)head_dx_row_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+      return true;
+    }();
+    (void)attrs;
+    if (a.dims[0] <= 64)
+      head_dx_row_kernel<1><<<(int)G, 256, lds, stream()>>>(x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(),
+                                                            mp, (int)kind, dx.data_ptr<float>());
+    else
+      head_dx_row_kernel<2><<<(int)G, 256, lds, stream()>>>(x.data_ptr<float>(), (int)G, a, target.data_ptr<float>(),
+                                                            mp, (int)kind, dx.data_ptr<float>());
+    return dx;
+  }
   HlTab tab;
   hl_tab_fill(tab, a, (int)std::min<int64_t>(G, kHlRows));
   hl_jobs(tab, x.data_ptr<float>(), target.data_ptr<float>());

@@ -254,8 +254,8 @@ class _ResMLP(torch.autograd.Function):
         dx, dH2, A1, dH1 = _native.ops().res_mlp_bwd(g, H1, H2, W1, W2)
         W1p, b1p, W2p, b2p = ctx.params
         if _lin._can_defer(W1p, b1p) and _lin._can_defer(W2p, b2p):
-            _lin._defer["items"].append((dH2, A1, W2p, b2p))
-            _lin._defer["items"].append((dH1, x, W1p, b1p))
+            _lin._record((dH2, A1, W2p, b2p))
+            _lin._record((dH1, x, W1p, b1p))
             return dx, None, None, None, None
         dW1, db1 = torch.empty_like(W1p), torch.empty_like(b1p)
         dW2, db2 = torch.empty_like(W2p), torch.empty_like(b2p)

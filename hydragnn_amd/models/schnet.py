@@ -58,8 +58,8 @@ class _CFFilter(torch.autograd.Function):
         dH2, A1, dH1 = _native.ops().cf_filter_bwd(g, C, H1, W2)
         W1p, b1p, W2p, b2p = ctx.params
         if _lin._can_defer(W1p, b1p) and _lin._can_defer(W2p, b2p):
-            _lin._defer["items"].append((dH2, A1, W2p, b2p))
-            _lin._defer["items"].append((dH1, rbf, W1p, b1p))
+            _lin._record((dH2, A1, W2p, b2p))
+            _lin._record((dH1, rbf, W1p, b1p))
             return None, None, None, None, None, None
         dW1, db1 = torch.empty_like(W1p), torch.empty_like(b1p)
         dW2, db2 = torch.empty_like(W2p), torch.empty_like(b2p)

@@ -22,6 +22,7 @@ GPU, ``precision("bf16")``, ReLU convs without attention / recurrence / checkpoi
 import torch
 
 from .. import _native
+from ..parallel import gradslots as _gradslots
 from . import bgemm as bg
 
 
@@ -194,14 +195,32 @@ class _EGNNWide(torch.autograd.Function):
             F, H, Hp, Kx, Ho = L["F"], L["H"], L["Hp"], L["Kx"], L["Ho"]
             Hop = bg.pad128(Ho)
             p = params[offs[li]:offs[li] + L["np"]]
-            g = [torch.empty_like(t) for t in p]
+            # gradient slots of the step's flat buffer (parallel/gradslots.py): the layer's
+            # weight gradients are written there and handed to the bucketed all-reduce as soon
+            # as the layer is done, so the buckets of the last layers reduce while the earlier
+            # layers' backward still runs (returned through autograd they all arrived at the end)
+            sl = _gradslots.slots(p) if all(isinstance(t, torch.nn.Parameter) for t in p) else None
+            g = list(sl) if sl is not None else [torch.empty_like(t) for t in p]
+            given = set()
+
+            def give(*ks, p=p, sl=sl, given=given):
+                # hand finished slot gradients to the bucketed all-reduce, sub-block by
+                # sub-block as the layer's backward produces them
+                if sl is None:
+                    return
+                ks = [k for k in ks if k < len(p) and k not in given]
+                given.update(ks)
+                if ks:
+                    _gradslots.provide([p[k] for k in ks])
             # node MLP
             dn2 = bg.cast_pad(dx, Hop, gate=S["xn"], ones=False)
             bg.wgrad(dn2, S["n1"], Hop, Hp, [(g[6], 0, g[7], H)])
+            give(6, 7)
             dn1 = torch.empty((N, Hp), device=dev, dtype=torch.bfloat16)
             bg.nt(dn2, im["n2T"], Hop, H, gate=S["n1"], outb=dn1)
             bg.wgrad(dn1, S["xb"], Hp, Kx + Hp, [(g[4][:, :F], 0, g[5], F), (g[4][:, F:], 0, None, -1, Kx)],
                      X2=S["agg"], kc1=Kx)
+            give(4, 5)
             dxa = torch.empty((N, Kx + Hp), device=dev, dtype=torch.float32)
             bg.nt(dn1, im["n1T"], Hp, Kx + Hp, outf=dxa)
             dagg = dxa[:, Kx:Kx + H]
@@ -217,6 +236,7 @@ class _EGNNWide(torch.autograd.Function):
                                           p[10].reshape(-1), L["cw"], dc1, dcd, part)
                 ops.bg_slab_reduce(part, nblk, 1, Hp, 0, 0, 1, H, g[10], 0.0, -1, None)
                 bg.wgrad(dc1, S["m"], Hp, Hp, [(g[8], 0, g[9], H)])
+                give(8, 9, 10)
                 bg.nt(dc1, im["c1T"], Hp, H, addg=dagg, addg_idx=src.index, gate=S["m"], outb=dZ2)
                 if DEBUG is not None:
                     DEBUG[("dc1", li)] = dc1
@@ -224,6 +244,7 @@ class _EGNNWide(torch.autograd.Function):
             else:
                 ops.egnn_gather_gate(dagg, src.index, S["m"], H, dZ2)
             bg.wgrad(dZ2, S["h1"], Hp, Hp, [(g[2], 0, g[3], H)])
+            give(2, 3)
             dh1 = torch.empty((E, Hp), device=dev, dtype=torch.bfloat16)
             dr = None  # d loss / d|d_e| (the radial input of edge_mlp[0]), from the fp32 epilogue
             if li > 0:
@@ -239,6 +260,7 @@ class _EGNNWide(torch.autograd.Function):
             bg.wgrad(dh1, S["sc"], Hp, 128, [(g[0][:, 2 * F:2 * F + ns], 0, g[1], ns)])
             del dh1
             bg.wgrad(dAB, S["xb"], 2 * Hp, Kx, [(g[0][:, :F], 0, None, -1), (g[0][:, F:2 * F], Hp, None, -1)])
+            give(0, 1)
             if li > 0:  # the input features and positions are data
                 dx = dxa[:, :F]
                 bg.nt(dAB, im["abT"], 2 * Hp, F, outf=dx, beta=1.0)
@@ -247,8 +269,11 @@ class _EGNNWide(torch.autograd.Function):
                 dpos = dpos_in
                 if DEBUG is not None:
                     DEBUG[li] = dpos_in.clone()
-            for j in range(L["np"]):
-                grads[offs[li] + j] = g[j]
+            if sl is not None:
+                give(*range(len(p)))  # anything not handed over above
+            else:
+                for j in range(L["np"]):
+                    grads[offs[li] + j] = g[j]
         ctx.saved = ctx.imgs = None
         return (None, None, None, None, *grads)
 

@@ -63,7 +63,7 @@ def _row_contig(t):
 # recorded weight gradient and writes / accumulates it into ``W.grad`` / ``b.grad``
 # (csrc/linear.hip, ``linear_wgrad_grouped``), then runs the parameters'
 # post-accumulate-grad hooks (the bucketed all-reduce of the captured step).
-_defer = {"on": False, "items": []}
+_defer = {"on": False, "items": [], "early": 0}  # early: flushes triggered by a waiting bucket
 
 
 def _can_defer(W, b):
@@ -89,6 +89,24 @@ class deferred_wgrad:
         return False
 
 
+def _record(item):
+    """Record one deferred weight-gradient problem.  Under a step's gradient sync whose next
+    bucket now waits only on deferred problems, flush everything recorded so far at once
+    (``BucketedGradSync.deferred_flush_ready``): that bucket's all-reduce then overlaps the
+    rest of backward instead of starting after the end-of-backward flush."""
+    _defer["items"].append(item)
+    s = _gradslots.active()
+    if s is None or not hasattr(s, "note_deferred"):
+        return
+    s.note_deferred(item[2:4])
+    if os.environ.get("HYDRA_EARLY_WGRAD_FLUSH", "1") == "1" and s.deferred_flush_ready():
+        _defer["early"] += 1
+        held = s.deferred_held
+        flushed = [p for it in _defer["items"] if not held(it) for p in it[2:4] if p is not None]
+        flush_deferred_wgrads(keep=held)
+        s.expect_echo(flushed)
+
+
 def _span(it):
     k0 = it[4] if len(it) > 4 else 0  # column block [k0, k0 + K) of W (row programs)
     return k0, k0 + it[1].shape[1]
@@ -103,8 +121,16 @@ def _conflict(a, b):
     return a[3] is not None and a[3] is b[3]
 
 
-def flush_deferred_wgrads():
-    items, _defer["items"] = _defer["items"], []
+def flush_deferred_wgrads(keep=None):
+    """Compute every recorded weight gradient (grouped launches) and run the parameters'
+    post-accumulate hooks.  ``keep(item)`` True: leave that problem recorded for a later flush
+    (an early flush skips parameters whose bucket must wait for the end of backward)."""
+    items = _defer["items"]
+    if keep is not None:
+        _defer["items"] = [it for it in items if keep(it)]
+        items = [it for it in items if not keep(it)]
+    else:
+        _defer["items"] = []
     if not items:
         return
     # one launch covers problems with disjoint outputs (column blocks of one weight included);
@@ -165,12 +191,34 @@ def flush_deferred_wgrads():
             dbs.append(b.grad if b is not None else torch.empty(0, device=dy.device))
             acc.append(1 if a else 0)
             touched += [W] + ([b] if b is not None else [])
-        _native.ops().linear_wgrad_grouped(dys, xs, dws, dbs, acc)
-    seen = set()
-    for p in touched:
-        if id(p) not in seen:
-            seen.add(id(p))
-            _run_post_hooks(p)
+        if dys[0].is_cuda:
+            _native.ops().linear_wgrad_grouped(dys, xs, dws, dbs, acc)
+        else:  # CPU twin (multi-rank gloo tests of the flush / bucket protocol)
+            _cpu_grouped(dys, xs, dws, dbs, acc)
+
+    s = _gradslots.active()
+    mark = s is not None and hasattr(s, "deferred_flush")
+    if mark:
+        s.deferred_flush(True)
+    try:
+        seen = set()
+        for p in touched:
+            if id(p) not in seen:
+                seen.add(id(p))
+                _run_post_hooks(p)
+    finally:
+        if mark:
+            s.deferred_flush(False)
+
+
+@torch.no_grad()
+def _cpu_grouped(dys, xs, dws, dbs, acc):
+    for dy, x, dw, db, a in zip(dys, xs, dws, dbs, acc):
+        gw = dy.t() @ x
+        dw.add_(gw) if a else dw.copy_(gw)
+        if db.numel():
+            gb = dy.sum(0)
+            db.add_(gb) if a else db.copy_(gb)
 
 
 def _run_post_hooks(p):
@@ -195,7 +243,7 @@ class _TallLinear(torch.autograd.Function):
         dW = db = None
         Wp, bp = ctx.params
         if ctx.needs_input_grad[1] and (not ctx.has_b or ctx.needs_input_grad[2]) and _can_defer(Wp, bp):
-            _defer["items"].append((dy, x, Wp, bp))
+            _record((dy, x, Wp, bp))
             return dx, None, None
         if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
             dW, db = _native.ops().linear_wgrad(dy, x, ctx.has_b)
@@ -227,7 +275,7 @@ class _ColBlockLinear(torch.autograd.Function):
         dW = None
         if ctx.needs_input_grad[1]:
             if _can_defer(W, None):
-                _defer["items"].append((dy, x, W, None, k0))
+                _record((dy, x, W, None, k0))
             else:
                 dW = torch.zeros_like(W)
                 g, _ = _native.ops().linear_wgrad(dy.contiguous(), x.contiguous(), False)
@@ -289,7 +337,7 @@ class _TallLinearSum(torch.autograd.Function):
                 (not ctx.has_b or ctx.needs_input_grad[0]) and all(_can_defer(w, None) for w in wps) and \
                 _can_defer(wps[0], bp) and len({id(w) for w in wps}) == len(wps):
             for j, (x, w) in enumerate(zip(xs, ws)):
-                _defer["items"].append((dy, x, wps[j], bp if j == 0 else None))
+                _record((dy, x, wps[j], bp if j == 0 else None))
                 grads += [_dgrad(dy, w) if ctx.needs_input_grad[1 + 2 * j] else None, None]
             return (None, *grads)
         # non-leaf weights (e.g. the PNA weight-prep outputs): all k weight gradients of this

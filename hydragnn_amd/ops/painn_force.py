@@ -510,7 +510,7 @@ def _dev_wgrads_defer(dm, get, N, ws):
     weight-gradient launch (ops/linear.py deferred_wgrad): every row program of the
     backward, first- and second-order, shares one launch pair per round, accumulating in
     place into ``.grad`` (no per-program launches, no autograd accumulation adds)."""
-    from .linear import _defer
+    from .linear import _record
 
     for rnd in dm.rounds:
         for (pid, k0, G, X, bias, acc) in rnd:
@@ -518,7 +518,7 @@ def _dev_wgrads_defer(dm, get, N, ws):
             if G.nc == 3:
                 g = g.reshape(N * 3, G.w)
                 x = x.reshape(N * 3, X.w)
-            _defer["items"].append((g, x, ws[pid], ws[bias] if bias is not None else None, k0))
+            _record((g, x, ws[pid], ws[bias] if bias is not None else None, k0))
 
 
 def _dev_wgrads(dm, get, N, ws):

@@ -179,6 +179,16 @@ class DistributedDataParallel(nn.Module):
         return super().state_dict(*a, **k)
 
 
+def default_bucket_cap(nbytes, min_buckets=2):
+    """Bucket size in bytes for ``nbytes`` of gradients.  Small GNN models: a few buckets so
+    the first all-reduce starts mid-backward.  Large models (> 64 MB): at least 8 buckets of
+    at most 32 MB — the last bucket (the first layers' gradients) is inherently exposed after
+    backward, so it is kept small; 4-32 MB rings still run at link bandwidth over xGMI."""
+    if nbytes > 64 * 1024 * 1024:
+        min_buckets = max(min_buckets, 8)
+    return min(max(nbytes // min_buckets + 1, 256 * 1024), 32 * 1024 * 1024)
+
+
 class BucketedGradSync:
     """Gradient all-reduce for the hipGraph-captured training step, overlapped with
     backward (reference DDP ``distributed.py:332-351``).
@@ -227,9 +237,7 @@ class BucketedGradSync:
         self._loss = None
         nbytes = total * self.flat.element_size()
         if bucket_cap_mb is None:
-            # small GNN models: a few buckets so the first all-reduce starts mid-backward; large
-            # models: 32 MB buckets (bandwidth-efficient ring size over the xGMI links)
-            cap = min(max(nbytes // min_buckets + 1, 256 * 1024), 32 * 1024 * 1024)
+            cap = default_bucket_cap(nbytes, min_buckets)
         else:
             cap = int(bucket_cap_mb * 1024 * 1024)
         self.offset = {}
@@ -266,6 +274,18 @@ class BucketedGradSync:
         self.provided = {}
         self.side_events = []
         self.guard_packed = True
+        # early flush of deferred grouped weight gradients (ops/linear.py deferred_wgrad): the
+        # parameters recorded as deferred this step, and — learned from the previous step —
+        # those that must wait for the end-of-backward flush (recorded more than once, or with
+        # an ordinary autograd contribution as well: an early flush would reduce their bucket
+        # before the last contribution arrived)
+        self._deferred = {}
+        self._ordinary = set()
+        self._in_flush = False
+        self._defer_known = False
+        self._defer_hold = set()
+        self._echoed = set()  # deferred parameters whose None-gradient hook already ran
+        self._echo = set()    # flushed early, their op's None-gradient hook still to come
         self._slot_ptr = {p: self.flat.data_ptr() + self.offset[p] * self.flat.element_size() for p in self.params}
         self.attach()
 
@@ -283,7 +303,8 @@ class BucketedGradSync:
             self.side_events.append(event)
         for p in params:
             self.provided[id(p)] = p
-            self._hook(p)
+            if self.active:
+                self._count(p)
 
     def _in_place(self, p):
         if id(p) in self.provided:
@@ -322,11 +343,68 @@ class BucketedGradSync:
         self.next = 0
         self.counted = set()
         for p in list(self.provided.values()):  # slots written during the forward (before begin)
-            self._hook(p)
+            if self.active:
+                self._count(p)
+
+    def note_deferred(self, params):
+        """``params`` got a deferred weight-gradient record (not yet computed)."""
+        for p in params:
+            if p is not None and p in self.offset:
+                self._deferred[id(p)] = self._deferred.get(id(p), 0) + 1
+
+    def deferred_flush_ready(self):
+        """True when the next bucket in launch order waits only on deferred gradients (none
+        of them held back): flushing the recorded problems now lets its all-reduce start
+        before the end of backward."""
+        if not (self.active and self._defer_known) or self.next >= len(self.buckets):
+            return False
+        _, _, ps = self.buckets[self.next]
+        waiting = False
+        for p in ps:
+            if id(p) in self.counted:
+                continue
+            if id(p) in self._defer_hold or id(p) not in self._deferred:
+                return False
+            waiting = True
+        return waiting
+
+    def deferred_held(self, item):
+        """A recorded problem that an early flush must leave for the end of backward."""
+        return any(p is not None and (id(p) in self._defer_hold or p not in self.offset) for p in item[2:4])
+
+    def expect_echo(self, params):
+        """Parameters flushed early: the None-gradient hook of the op that recorded them may
+        still arrive (autograd runs it after that op's backward returns) — ignore it once."""
+        for p in params:
+            if id(p) not in self._echoed:
+                self._echo.add(id(p))
+
+    def deferred_flush(self, flushing):
+        """Bracket of a deferred flush's post-accumulate hooks (their contributions are the
+        deferred ones, not ordinary autograd ones)."""
+        self._in_flush = flushing
 
     def _hook(self, p):
         if not self.active:
             return
+        if not self._in_flush and id(p) in self._echo:
+            self._echo.discard(id(p))
+            self._echoed.add(id(p))
+            return
+        if p.grad is None:
+            self._echoed.add(id(p))
+            # autograd runs post-accumulate hooks even for a None contribution: an op that
+            # deferred this weight gradient (ops/linear.py deferred_wgrad) or wrote it into its
+            # slot (provide) returned None.  A deferred gradient arrives with the flush, a
+            # provided one was counted by provide(); counting it now would launch the bucket's
+            # all-reduce before the gradient exists.  (A parameter with no gradient at all this
+            # step is reduced as zeros by finish().)
+            return
+        if not self._in_flush:
+            self._ordinary.add(id(p))
+        self._count(p)
+
+    def _count(self, p):
         bi = self.bucket_of[p]
         if id(p) in self.counted:
             # a second gradient contribution (a parameter used by both a deferred grouped
@@ -444,6 +522,13 @@ class BucketedGradSync:
         self.side_events = []
         self.provided = {}
         self.works = []
+        if self.active:
+            self._defer_hold = {k for k, c in self._deferred.items() if c > 1 or k in self._ordinary}
+            self._defer_known = True
+        self._deferred = {}
+        self._ordinary = set()
+        self._echoed = set()
+        self._echo = set()
         self.active = False
         self.attach()
 
@@ -557,6 +642,41 @@ class MultiGradSync:
             elif i == 0 and event is not None:
                 # the side stream also produced the loss the guard holder packs
                 s.side_events.append(event)
+
+    def note_deferred(self, params):
+        for s in self.syncs:
+            s.note_deferred(params)
+
+    def deferred_flush_ready(self):
+        return any(s.deferred_flush_ready() for s in self.syncs)
+
+    def deferred_held(self, item):
+        """A recorded problem that an early flush must leave for the end of backward."""
+        return any(p is not None and (id(p) in self._defer_hold or p not in self.offset) for p in item[2:4])
+
+    def expect_echo(self, params):
+        """Parameters flushed early: the None-gradient hook of the op that recorded them may
+        still arrive (autograd runs it after that op's backward returns) — ignore it once."""
+        for p in params:
+            if id(p) not in self._echoed:
+                self._echo.add(id(p))
+
+    def deferred_flush(self, flushing):
+        for s in self.syncs:
+            s.deferred_flush(flushing)
+
+    def deferred_held(self, item):
+        # a problem is flushed early only when no sync holds it (each sync sees its own params)
+        ps = [p for p in item[2:4] if p is not None]
+        for s in self.syncs:
+            mine = [p for p in ps if p in s.offset]
+            if any(id(p) in s._defer_hold for p in mine):
+                return True
+        return not all(any(p in s.offset for s in self.syncs) for p in ps)
+
+    def expect_echo(self, params):
+        for s in self.syncs:
+            s.expect_echo([p for p in params if p in s.offset])
 
     def begin(self):
         for s in self.syncs:

@@ -601,3 +601,92 @@ def test_bn_running_stats_synced_per_epoch():
 
 def test_aggr_backend_flag():
     run_ranks("_aggr_backend_body")
+
+
+# ------------------------------------------------- early flush of deferred weight gradients
+
+class _DeferLin(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is DEFERRED (recorded for the grouped flush, as
+    the GPU tall linears do), so the CPU gloo ranks exercise the flush / bucket protocol."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x)
+        ctx.params = (W, b)
+        return x @ W.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        from hydragnn_amd.ops import linear as _lin
+
+        (x,) = ctx.saved_tensors
+        W, b = ctx.params
+        assert _lin._can_defer(W, b)
+        _lin._record((dy, x, W, b))
+        return dy @ W, None, None
+
+
+def _early_flush_body(rank, world):
+    from hydragnn_amd.ops import linear as _lin
+    from hydragnn_amd.parallel import gradslots
+    from hydragnn_amd.parallel.ddp import BucketedGradSync
+
+    def run(early):
+        os.environ["HYDRA_EARLY_WGRAD_FLUSH"] = "1" if early else "0"
+        torch.manual_seed(0)
+        lins = [torch.nn.Linear(48, 48) for _ in range(6)]
+        params = [p for l in lins for p in (l.weight, l.bias)]
+        sync = BucketedGradSync(params, bucket_cap_mb=0.02)  # ~2 layers per bucket
+        assert len(sync.buckets) >= 3
+        launches = []
+        orig = sync._launch
+
+        def launch(bi):
+            launches.append((bi, len(_lin._defer["items"])))
+            return orig(bi)
+        sync._launch = launch
+        outs = []
+        for step in range(2):
+            g = torch.Generator().manual_seed(100 * rank + step)
+            x = torch.randn(64, 48, generator=g)
+            sync.release()
+            sync.set_loss(None)
+            launches.clear()
+            _lin._defer["early"] = 0
+            with gradslots.use(sync):
+                sync.begin()
+                with _lin.deferred_wgrad(True):
+                    h = x
+                    for l in lins:
+                        h = torch.relu(_DeferLin.apply(h, l.weight, l.bias))
+                    h.pow(2).mean().backward()
+                sync.finish()
+            outs.append(sync.flat[:sync.total].clone())
+        return outs, list(launches), _lin._defer["early"]
+
+    base, _, n0 = run(False)
+    got, launches, n1 = run(True)
+    assert n0 == 0
+    # step 2 (the first with the learned hold set) flushed early: buckets were reduced while
+    # deferred problems of earlier layers were still unrecorded
+    assert n1 >= 2, n1
+    assert any(k > 0 or bi < len(launches) - 1 for bi, k in launches[:-1])
+    for a, b in zip(base, got):
+        assert torch.equal(a, b)  # bit-identical to the end-of-backward flush
+    # and equal to the rank average of plain autograd gradients
+    torch.manual_seed(0)
+    lins = [torch.nn.Linear(48, 48) for _ in range(6)]
+    g = torch.Generator().manual_seed(100 * rank + 1)
+    x = torch.randn(64, 48, generator=g)
+    h = x
+    for l in lins:
+        h = torch.relu(l(h))
+    h.pow(2).mean().backward()
+    local = torch.cat([p.grad.reshape(-1) for p in reversed([p for l in lins for p in (l.weight, l.bias)])])
+    allg = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(allg, local)
+    torch.testing.assert_close(got[1], sum(allg) / world, rtol=1e-5, atol=1e-6)
+
+
+def test_early_deferred_wgrad_flush_two_ranks():
+    run_ranks("_early_flush_body")

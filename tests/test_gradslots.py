@@ -1,5 +1,6 @@
 """Gradient slots (parallel/gradslots.py): ops writing gradients straight into the flat
 buffer of BucketedGradSync; the pack copies only the rest, in contiguous runs."""
+import pytest
 import torch
 
 from hydragnn_amd.parallel import gradslots
@@ -78,11 +79,11 @@ def test_provided_params_count_down_their_bucket():
     sync.begin()
     # ps[2] is the first parameter of the reversed flat order: bucket 0 is complete
     assert launched == [0]
-    sync._hook(ps[1])
+    sync._hook(ps[1])  # autograd's hook for a None contribution (a deferred weight gradient)
+    assert launched == [0]
+    ps[1].grad = torch.zeros(4)
+    sync._hook(ps[1])  # the gradient itself
     assert launched == [0, 1]
-
-
-import pytest
 
 
 @pytest.mark.gpu

@@ -78,3 +78,33 @@ def test_head_loss_fused_unit_seed():
             ref = got
         for a, b in zip(got, ref):
             torch.testing.assert_close(a, b * float(seed), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["mae", "mse", "smooth_l1"])
+@pytest.mark.parametrize("G,dims,masked", [(33, [64, 50, 50, 50, 25, 1], True), (1, [32, 16, 1], False),
+                                           (100, [128, 64, 3], True), (7, [128, 50, 50, 50, 50, 25, 2], True),
+                                           (5, [64, 96, 1], False)])
+def test_head_loss_dx_matches_torch(kind, G, dims, masked):
+    """head_loss_dx (the dx-only launch of the training step's critical path; the
+    one-workgroup-per-row kernel for widths <= 64, the row-split kernel otherwise) == the
+    autograd input gradient of the fp32 Linear/ReLU chain and masked mean loss."""
+    dev = torch.device("cuda")
+    torch.manual_seed(7 * G + len(dims))
+    lins = [torch.nn.Linear(dims[i], dims[i + 1]).to(dev) for i in range(len(dims) - 1)]
+    seq = []
+    for i, l in enumerate(lins):
+        seq.append(l)
+        if i < len(lins) - 1:
+            seq.append(torch.nn.ReLU())
+    seq = torch.nn.Sequential(*seq)
+    x = torch.randn(G, dims[0], device=dev)
+    target = torch.randn(G, dims[-1], device=dev)
+    mask = (torch.arange(G, device=dev) < max(1, G - 2)) if masked else None
+    relu = [1] * (len(lins) - 1) + [0]
+    from hydragnn_amd import _native
+
+    dx = _native.ops().head_loss_dx(x, [l.weight.detach() for l in lins], [l.bias.detach() for l in lins], relu,
+                                    target, mask, {"mse": 0, "mae": 1, "smooth_l1": 3}[kind])
+    xr = x.clone().requires_grad_(True)
+    (gxr,) = torch.autograd.grad(_ref_loss(kind, seq(xr), target, mask), [xr])
+    torch.testing.assert_close(dx, gxr, rtol=1e-4, atol=1e-6)

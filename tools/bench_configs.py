@@ -79,6 +79,18 @@ def qm9_schnet_gps(dev):
     return m, s, 64, ["graph"], [1], False
 
 
+def oc20_gps(dev):
+    """BASELINE config 4 exactly as bench.py runs it (hidden 64, 8 heads, 3 layers)."""
+    from hydragnn_amd.data.synthetic import oc20_like
+
+    s = oc20_like(512, seed=1000, radius=10.0, max_neighbours=10, pe_dim=16)
+    deg = degree_histogram(s, max_degree=10).to(torch.float64)
+    heads = {"graph": _gheads(1, [50, 25], 50)}
+    m = create_model("PNAPlus", 4, 64, [1], 16, "GPS", "multihead", 8, ["graph"], heads, "relu", "mae", [1.0], 3,
+                     pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=10.0, max_neighbours=10)
+    return m, s, 32, ["graph"], [1], False
+
+
 def oc20_gps_h128(dev):
     """BASELINE config 4 (OC20 PNAPlus + GPS, bench.py) at hidden 128 (16 heads of 8)."""
     from hydragnn_amd.data.synthetic import oc20_like
@@ -141,6 +153,7 @@ def multibranch_mace(dev):
 
 CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
            "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128,
+           "oc20_gps": oc20_gps,
            "qm9_dimenet": qm9_dimenet}
 
 

@@ -10,8 +10,9 @@ all-reduce.  A 1-rank all-reduce moves no data, so only the position is measured
 
     python tools/overlap_check.py [--config multibranch_egnn] [--precision bf16]
 
-Prints one JSON line: buckets, backward kernel launches, launches after the first / each
-all-reduce, and the fraction after the first one.  Run as its own process."""
+Prints one JSON line: per bucket its bytes and the backward launches after its all-reduce,
+and the headline ``bytes_overlapped_fraction``: the share of gradient bytes whose all-reduce
+is enqueued before the last 20 % of the backward launches.  Run as its own process."""
 import argparse
 import json
 import os
@@ -59,10 +60,12 @@ def main():
     nbk = 512
     cap = a.bucket_mb
     if cap is None:
-        # the bucket size a multi-rank run picks (BucketedGradSync: half the gradient bytes,
-        # >= 256 KB, <= 32 MB); a lone rank would otherwise keep one bucket
+        # the bucket size a multi-rank run picks (ddp.default_bucket_cap); a lone rank would
+        # otherwise keep one bucket
+        from hydragnn_amd.parallel.ddp import default_bucket_cap
+
         nbytes = 4 * sum(p.numel() for p in model.parameters() if p.requires_grad)
-        cap = min(max(nbytes // 2 + 1, 256 * 1024), 32 * 1024 * 1024) / (1024 * 1024)
+        cap = default_bucket_cap(nbytes) / (1024 * 1024)
     ts = TrainStep(model, lr=1e-3, mode="graph", world=1, node_bucket=nbk, edge_bucket=8 * nbk,
                    bucket_cap_mb=cap, compute_grad_energy=forces)
     syncs = getattr(ts.sync, "syncs", [ts.sync])
@@ -97,9 +100,24 @@ def main():
             first[e.name] = min(first.get(e.name, e.time_range.start), e.time_range.start)
     ars = sorted((t, n) for n, t in first.items())
     after = [sum(1 for t in launches if t > s0) for s0, _ in ars]
+    nb = max(len(launches), 1)
+
+    def nbytes(name):
+        k, bi = (int(v) for v in name[len("gradsync_bucket_"):].split("_"))
+        s0, e0, _ = syncs[k].buckets[bi]
+        return 4 * (e0 - s0)
+
+    per = [{"bucket": n[len("gradsync_bucket_"):], "bytes": nbytes(n), "launches_after": c,
+            "fraction_after": round(c / nb, 4)} for (_, n), c in zip(ars, after)]
+    total = sum(b["bytes"] for b in per) or 1
+    # headline: the share of gradient BYTES whose all-reduce is enqueued before the last 20 %
+    # of the backward kernel launches (those reduces have >= 20 % of backward left to hide in)
+    over = sum(b["bytes"] for b in per if b["fraction_after"] >= 0.2)
     res = {"config": a.config, "precision": a.precision, "buckets": sum(len(s.buckets) for s in syncs),
-           "allreduces": len(ars), "backward_kernel_launches": len(launches), "launches_after_each_allreduce": after,
-           "fraction_after_first": round(after[0] / max(len(launches), 1), 4) if after else 0.0}
+           "allreduces": len(ars), "backward_kernel_launches": len(launches),
+           "bytes_overlapped_fraction": round(over / total, 4), "gradient_bytes": total,
+           "per_bucket": per, "launches_after_each_allreduce": after,
+           "fraction_after_first": round(after[0] / nb, 4) if after else 0.0}
     print(json.dumps(res), flush=True)
     dist.destroy_process_group()
 
