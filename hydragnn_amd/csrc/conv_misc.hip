@@ -313,6 +313,117 @@ std::tuple<at::Tensor, at::Tensor> edge_gather_act_bwd(const at::Tensor& g_, con
 }
 
 
+// MACE radial FCN first layer with its concat input split at node level (reference
+// mace_utils/modules/blocks.py:354-387, conv_tp_weights over cat[edge_feats, down[src],
+// down[dst]]): z = A[src] + B[dst] + et with ab = down @ [W_src | W_dst] ([N, 2H], one node
+// GEMM) and et = edge_feats @ W_edge ([E, H]); y = silu(s z) in one pass (float4 columns).
+// Backward: dz = g s silu'(s z) (z recomputed); dA / dB are CSR segment sums of dz.
+__global__ void __launch_bounds__(256) edge_gather_silu_fwd_kernel(
+    const float* __restrict__ ab, int ld, int64_t boff, const int* __restrict__ src, const int* __restrict__ dst,
+    const float* __restrict__ et, int64_t E, int H4, float s, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * H4) return;
+  const int64_t e = t / H4;
+  const int c = (int)(t - e * H4);
+  const float4 a = reinterpret_cast<const float4*>(ab + (int64_t)src[e] * ld)[c];
+  const float4 b = reinterpret_cast<const float4*>(ab + boff + (int64_t)dst[e] * ld)[c];
+  const float4 x = et != nullptr ? reinterpret_cast<const float4*>(et)[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float z[4] = {a.x + b.x + x.x, a.y + b.y + x.y, a.z + b.z + x.z, a.w + b.w + x.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float u = s * z[k];
+    z[k] = u / (1.f + __expf(-u));
+  }
+  reinterpret_cast<float4*>(out)[t] = make_float4(z[0], z[1], z[2], z[3]);
+}
+
+__global__ void __launch_bounds__(256) edge_gather_silu_bwd_kernel(
+    const float* __restrict__ g, const float* __restrict__ ab, int ld, int64_t boff, const int* __restrict__ src,
+    const int* __restrict__ dst, const float* __restrict__ et, int64_t E, int H4, float s, float* __restrict__ dz) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * H4) return;
+  const int64_t e = t / H4;
+  const int c = (int)(t - e * H4);
+  const float4 a = reinterpret_cast<const float4*>(ab + (int64_t)src[e] * ld)[c];
+  const float4 b = reinterpret_cast<const float4*>(ab + boff + (int64_t)dst[e] * ld)[c];
+  const float4 x = et != nullptr ? reinterpret_cast<const float4*>(et)[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 gv = reinterpret_cast<const float4*>(g)[t];
+  const float z[4] = {a.x + b.x + x.x, a.y + b.y + x.y, a.z + b.z + x.z, a.w + b.w + x.w};
+  const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+  float d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float u = s * z[k];
+    const float sg = 1.f / (1.f + __expf(-u));
+    d[k] = gg[k] * s * sg * (1.f + u * (1.f - sg));
+  }
+  reinterpret_cast<float4*>(dz)[t] = make_float4(d[0], d[1], d[2], d[3]);
+}
+
+// ab: [N, 2H] (A | B column blocks) or [2, N, H] (A block, then B block)
+struct EgsLayout {
+  int ld, H;
+  int64_t boff;
+};
+static EgsLayout egs_checks(const at::Tensor& ab, const at::Tensor& src, const at::Tensor& dst,
+                            const c10::optional<at::Tensor>& et) {
+  HY_CHECK_CUDA(ab);
+  HY_CHECK_F32(ab);
+  HY_CHECK_I32(src);
+  HY_CHECK_I32(dst);
+  HY_CHECK(dst.numel() == src.numel(), "edge_gather_silu: src / dst [E]");
+  HY_CHECK(ab.is_contiguous() && reinterpret_cast<uintptr_t>(ab.data_ptr()) % 16 == 0 &&
+               (ab.dim() == 2 || (ab.dim() == 3 && ab.size(0) == 2)),
+           "edge_gather_silu: ab [N, 2H] or [2, N, H] contiguous, 16-byte aligned");
+  EgsLayout L;
+  if (ab.dim() == 2) {
+    L.H = (int)(ab.size(1) / 2);
+    L.ld = (int)ab.size(1);
+    L.boff = L.H;
+  } else {
+    L.H = (int)ab.size(2);
+    L.ld = L.H;
+    L.boff = ab.size(1) * ab.size(2);
+  }
+  HY_CHECK(L.H % 4 == 0, "edge_gather_silu: H % 4 == 0");
+  if (et.has_value() && et->defined())
+    HY_CHECK(et->is_contiguous() && et->scalar_type() == at::kFloat && et->numel() == src.numel() * L.H &&
+                 reinterpret_cast<uintptr_t>(et->data_ptr()) % 16 == 0,
+             "edge_gather_silu: et [E, H] contiguous fp32");
+  return L;
+}
+
+at::Tensor edge_gather_silu_fwd(const at::Tensor& ab, const at::Tensor& src, const at::Tensor& dst,
+                                const c10::optional<at::Tensor>& et, double s) {
+  const EgsLayout L = egs_checks(ab, src, dst, et);
+  const int64_t E = src.numel();
+  const int H = L.H;
+  auto out = at::empty({E, H}, ab.options());
+  const int64_t n = E * (H / 4);
+  if (n > 0)
+    edge_gather_silu_fwd_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(
+        ab.data_ptr<float>(), L.ld, L.boff, src.data_ptr<int>(), dst.data_ptr<int>(),
+        et.has_value() && et->defined() ? et->data_ptr<float>() : nullptr, E, H / 4, (float)s, out.data_ptr<float>());
+  return out;
+}
+
+at::Tensor edge_gather_silu_bwd(const at::Tensor& g_, const at::Tensor& ab, const at::Tensor& src,
+                                const at::Tensor& dst, const c10::optional<at::Tensor>& et, double s) {
+  const EgsLayout L = egs_checks(ab, src, dst, et);
+  auto g = g_.contiguous();
+  const int64_t E = src.numel();
+  const int H = L.H;
+  HY_CHECK(g.numel() == E * H && g.scalar_type() == at::kFloat, "edge_gather_silu_bwd: grad [E, H]");
+  auto dz = at::empty({E, H}, ab.options());
+  const int64_t n = E * (H / 4);
+  if (n > 0)
+    edge_gather_silu_bwd_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(
+        g.data_ptr<float>(), ab.data_ptr<float>(), L.ld, L.boff, src.data_ptr<int>(), dst.data_ptr<int>(),
+        et.has_value() && et->defined() ? et->data_ptr<float>() : nullptr, E, H / 4, (float)s, dz.data_ptr<float>());
+  return dz;
+}
+
+
 // MACE FullyConnectedNet hidden activation y = silu(s x) (the e3nn second-moment
 // normalisation and the next layer's 1/sqrt(fan_in) folded into one scale s, reference
 // e3nn nn.FullyConnectedNet used by mace_utils/modules/blocks.py:354-387): one launch each
@@ -386,6 +497,8 @@ at::Tensor scaled_silu_bwd(const at::Tensor& g_, const at::Tensor& x_, double s)
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("scaled_silu_fwd(Tensor x, float s) -> Tensor");
   m.def("scaled_silu_bwd(Tensor g, Tensor x, float s) -> Tensor");
+  m.def("edge_gather_silu_fwd(Tensor ab, Tensor src, Tensor dst, Tensor? et, float s) -> Tensor");
+  m.def("edge_gather_silu_bwd(Tensor g, Tensor ab, Tensor src, Tensor dst, Tensor? et, float s) -> Tensor");
   m.def(
       "edge_gather_act_fwd(Tensor ab, Tensor src, Tensor dst, Tensor r, Tensor w, Tensor b, Tensor? et, int act) -> "
       "Tensor");
@@ -402,6 +515,8 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("scaled_silu_fwd", hy::scaled_silu_fwd);
   m.impl("scaled_silu_bwd", hy::scaled_silu_bwd);
   m.impl("edge_gather_act_fwd", hy::edge_gather_act_fwd);
+  m.impl("edge_gather_silu_fwd", hy::edge_gather_silu_fwd);
+  m.impl("edge_gather_silu_bwd", hy::edge_gather_silu_bwd);
   m.impl("edge_gather_act_bwd", hy::edge_gather_act_bwd);
   m.impl("cg_gate_fwd", hy::cg_gate_fwd);
   m.impl("cg_gate_bwd", hy::cg_gate_bwd);

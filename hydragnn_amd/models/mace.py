@@ -196,7 +196,8 @@ class InteractionBlock(nn.Module):
         sc = self.skip_linear(h)
         up = self.linear_up(h)
         down = self.linear_down(h)
-        w = self.conv_tp_weights(torch.cat([edge_feats, seg.gather(down, src_si), seg.gather(down, dst_si)], -1))
+        # radial FCN over cat[edge_feats, down[src], down[dst]]: first layer split at node level
+        w = self.conv_tp_weights.forward_split(edge_feats, down, src_si, dst_si)
         # gather -> uvu tensor product -> segment sum, fused on the GPU (one launch each way)
         msg = self.linear(self.conv_tp.conv(up, edge_attrs, w, src_si, dst_si))  # scales folded (init)
         return _to_channels(msg, self.target_irreps), sc

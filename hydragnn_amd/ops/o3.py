@@ -483,6 +483,58 @@ def _mm_tall(x, W):
     return x @ W
 
 
+def _seg():
+    from . import segment
+
+    return segment
+
+
+class _FCNFirstSplit(torch.autograd.Function):
+    """First layer of the MACE radial FCN over cat[edge_feats, down[src], down[dst]] with the
+    concatenation split at node level: y = silu(s (ef W_e + (down W_s)[src] + (down W_d)[dst]))
+    where W1 = [W_e; W_s; W_d] ([nef + 2 nd, nd], e3nn x @ W layout).  Forward: one node-level
+    batched GEMM, one tall GEMM, one gather + silu pass (csrc/conv_misc.hip edge_gather_silu);
+    backward: one pass for dz, two CSR segment sums for dA / dB, ONE grouped weight-gradient
+    launch pair for the three row blocks of dW1 (written in place), one batched GEMM for
+    d down.  First order (composite mode keeps the torch chain)."""
+
+    @staticmethod
+    def forward(ctx, ef, down, W1, s, src_si, dst_si):
+        from .. import _native
+
+        nef, nd = ef.shape[1], down.shape[1]
+        ab = torch.matmul(down.unsqueeze(0), W1[nef:].view(2, nd, nd))  # [2, N, nd]: A block, B block
+        et = ef @ W1[:nef]
+        ctx.save_for_backward(ef, down, W1, ab, et)
+        ctx.cfg = (s, src_si, dst_si)
+        return _native.ops().edge_gather_silu_fwd(ab, src_si.index, dst_si.index, et, s)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        ops = _native.ops()
+        ef, down, W1, ab, et = ctx.saved_tensors
+        s, src_si, dst_si = ctx.cfg
+        nef, nd = ef.shape[1], down.shape[1]
+        dz = ops.edge_gather_silu_bwd(g, ab, src_si.index, dst_si.index, et, s)
+        seg = _seg()
+        # CSR sums (they stop at the batch's real edge count when the index carries a limit)
+        dA, dB = seg.segment_sum(dz, src_si), seg.segment_sum(dz, dst_si)
+        dW1 = None
+        if ctx.needs_input_grad[2]:
+            dW1 = torch.empty_like(W1)
+            e = torch.empty(0, device=g.device, dtype=g.dtype)
+            # row blocks of dW1 = x_block^T dy_block (the grouped kernel's dy^T x with roles swapped)
+            ops.linear_wgrad_grouped([ef, down, down], [dz, dA, dB], [dW1[:nef], dW1[nef:nef + nd], dW1[nef + nd:]],
+                                     [e, e, e], [0, 0, 0])
+        ddown = None
+        if ctx.needs_input_grad[1]:
+            ddown = torch.addmm(dA @ W1[nef:nef + nd].t(), dB, W1[nef + nd:].t())
+        def_ = dz @ W1[:nef].t() if ctx.needs_input_grad[0] else None
+        return def_, ddown, dW1, None, None, None
+
+
 class FullyConnectedNet(nn.Module):
     """e3nn ``nn.FullyConnectedNet`` with silu: no biases, N(0,1) weights, 1/sqrt(fan_in),
     second-moment-normalised activation between layers."""
@@ -500,12 +552,27 @@ class FullyConnectedNet(nn.Module):
         1/sqrt(fan_in) times the previous activation's normalisation."""
         return (_SILU_C if len(self.weights) > 1 else 1.0) / math.sqrt(self.weights[-1].shape[0])
 
-    def forward(self, x):
+    def forward_split(self, edge_feats, down, src_si, dst_si):
+        """``forward(cat[edge_feats, down[src], down[dst]])`` with the first layer's
+        concatenation split at node level (``_FCNFirstSplit``) on the GPU."""
+        from . import pna as _mode
+
+        W1 = self.weights[0]
+        nd = down.shape[1]
+        if (down.is_cuda and down.dtype == torch.float32 and len(self.weights) > 1 and nd % 4 == 0 and
+                W1.shape[0] == edge_feats.shape[1] + 2 * nd and _mode.fused("linear")):
+            x = _FCNFirstSplit.apply(edge_feats.contiguous(), down.contiguous(), W1, 1.0 / math.sqrt(W1.shape[0]),
+                                     src_si, dst_si)
+            return self.forward(x, start=1, carry=_SILU_C)
+        return self.forward(torch.cat([edge_feats, _seg().gather(down, src_si), _seg().gather(down, dst_si)], -1))
+
+    def forward(self, x, start=0, carry=1.0):
         # the activation normalisation C and the next layer's 1/sqrt(fan_in) are ONE multiply
         # of the pre-activation (same values as scaling after each step)
         n = len(self.weights)
-        carry = 1.0
         for i, W in enumerate(self.weights):
+            if i < start:
+                continue
             x = _mm_tall(x, W)
             s = carry / math.sqrt(W.shape[0])
             if i < n - 1:

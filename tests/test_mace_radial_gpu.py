@@ -50,3 +50,46 @@ def test_scaled_silu_matches_torch(shape, s):
     y.backward(go.float().cuda())
     torch.testing.assert_close(y.double().cpu(), torch.nn.functional.silu(x * s), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(xd.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,E,nef,nd", [(60, 700, 8, 64), (9, 40, 5, 16)])
+def test_fcn_first_layer_split_matches_concat(N, E, nef, nd):
+    """MACE radial FCN with the first layer's cat[edge_feats, down[src], down[dst]] split at
+    node level (ops/o3.py _FCNFirstSplit, csrc/conv_misc.hip edge_gather_silu) == the
+    concatenated fp64 FullyConnectedNet: values and the gradients of edge_feats, down and
+    every weight."""
+    from hydragnn_amd.ops import segment as seg
+    from hydragnn_amd.ops.o3 import FullyConnectedNet, _FCNFirstSplit
+
+    g = torch.Generator().manual_seed(N + E)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values
+    src = torch.randint(0, N, (E,), generator=g)
+    ef = torch.randn(E, nef, generator=g, dtype=torch.float64)
+    down = torch.randn(N, nd, generator=g, dtype=torch.float64)
+    fcn = FullyConnectedNet([nef + 2 * nd, nd, nd, 3 * nd]).double()
+    go = torch.randn(E, 3 * nd, generator=g, dtype=torch.float64)
+    efr, downr = ef.clone().requires_grad_(True), down.clone().requires_grad_(True)
+    ref = fcn(torch.cat([efr, downr[src], downr[dst]], -1))
+    ref.backward(go)
+    gref = [efr.grad, downr.grad] + [w.grad.clone() for w in fcn.weights]
+
+    dev = torch.device("cuda")
+    fcn = fcn.float().to(dev)
+    for w in fcn.weights:
+        w.grad = None
+    dst_si = seg.SegIndex.from_index(dst.int().to(dev), N, sorted_=True)
+    src_si = seg.SegIndex.from_index(src.int().to(dev), N, sorted_=False)
+    efd = ef.float().to(dev).requires_grad_(True)
+    downd = down.float().to(dev).requires_grad_(True)
+    out = fcn.forward_split(efd, downd, src_si, dst_si)
+    names = []
+    fn = out.grad_fn
+    while fn is not None and len(names) < 20:
+        names.append(type(fn).__name__)
+        fn = fn.next_functions[0][0] if fn.next_functions else None
+    assert any("FCNFirstSplit" in n for n in names), names
+    out.backward(go.float().to(dev))
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
+    got = [efd.grad, downd.grad] + [w.grad for w in fcn.weights]
+    for a, b in zip(got, gref):
+        torch.testing.assert_close(a.double().cpu(), b, rtol=1e-4, atol=1e-4)
