@@ -310,8 +310,19 @@ void store_plan_expand(const at::Tensor& seed, at::TensorList tabs, at::Tensor o
     HY_CHECK(rng->is_cuda() && rng->scalar_type() == at::kLong && rng->numel() >= 1, "store_plan_expand: rng int64");
     rp = rng->data_ptr<int64_t>();
   }
-  HY_CHECK_CUDA(seed);
-  HY_CHECK_I32(seed);
+  // seed: a device tensor, or the pinned host buffer itself (zero-copy: the kernel reads the
+  // ids over the host link, which saves the step graph its H2D copy node)
+  HY_CHECK(seed.scalar_type() == at::kInt && seed.is_contiguous(), "store_plan_expand: int32 seed");
+  const int* seed_ptr = nullptr;
+  if (seed.is_cuda()) {
+    seed_ptr = seed.data_ptr<int>();
+  } else {
+    HY_CHECK(seed.is_pinned(), "store_plan_expand: a host seed must be pinned");
+    void* dp = nullptr;
+    HY_CHECK(hipHostGetDevicePointer(&dp, seed.data_ptr(), 0) == hipSuccess && dp != nullptr,
+             "store_plan_expand: pinned seed is not device-mapped");
+    seed_ptr = static_cast<const int*>(dp);
+  }
   HY_CHECK_I32(out);
   HY_CHECK(tabs.size() == 9, "store_plan_expand: 9 per-sample tables");
   for (const auto& x : tabs) HY_CHECK(x.is_cuda() && x.scalar_type() == at::kInt && x.is_contiguous(),
@@ -334,7 +345,7 @@ void store_plan_expand(const at::Tensor& seed, at::TensorList tabs, at::Tensor o
   PlanOut o{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12]};
   const int64_t work = Np + Ep + Gp + 1;
   const int blocks = (int)std::min<int64_t>(ceil_div(work, (int64_t)256), 1024);
-  plan_expand_kernel<<<blocks, 256, 0, stream()>>>(seed.data_ptr<int>(), t, o, (int)Np, (int)Ep, (int)Gp,
+  plan_expand_kernel<<<blocks, 256, 0, stream()>>>(seed_ptr, t, o, (int)Np, (int)Ep, (int)Gp,
                                                    padded ? 1 : 0, batch_scope ? 1 : 0, rp);
 }
 

@@ -440,9 +440,12 @@ class _GPSEncoder(torch.autograd.Function):
             wstream = _streams.side_stream(dev, 2)
         lo = 0
         edge_ev = None
-        # layer 0's ready weight gradients on the edge stream during its attention backward
-        # (HYDRA_EARLY_WGRAD=0: all of them at the end)
-        early0 = wside and os.environ.get("HYDRA_EARLY_WGRAD", "1") == "1"
+        # HYDRA_EARLY_WGRAD=1: layer 0's ready weight gradients on the edge stream during its
+        # attention backward
+        # (default off: at layer 0 the local chain is the longer branch, so the early launch
+        # could not start before it ended and only split the tail into two launch pairs;
+        # measured 0.905-0.914 vs 0.921-0.923 ms/step with it on MI355X)
+        early0 = wside and os.environ.get("HYDRA_EARLY_WGRAD", "0") == "1"
         early_done = False
         gw0 = dfreq_w = te = None
         # HYDRA_GPS_ATTN_MAIN=1: the attention branch on the main stream and the local chain on

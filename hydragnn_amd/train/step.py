@@ -570,11 +570,15 @@ class TrainStep:
             pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
-                if cap.seeded:  # first nodes: H2D of the sample ids, device-side plan
-                    cap.dev_seed.copy_(cap.pinned[j], non_blocking=True)
+                if cap.seeded:  # first node: the device-side plan from the sample ids
+                    # the plan kernel reads the ids straight from the pinned host buffer
+                    # (HYDRA_SEED_ZEROCOPY=0: an H2D copy node first)
+                    zc = os.environ.get("HYDRA_SEED_ZEROCOPY", "1") == "1"
+                    if not zc:
+                        cap.dev_seed.copy_(cap.pinned[j], non_blocking=True)
                     # the plan launch also advances the dropout counter (the model's per-step
                     # advance is folded into it: one launch less in the step)
-                    store.plan_device(cap.dev_seed, cap.lay, cap.dev_plan, rng=rng_ctr)
+                    store.plan_device(cap.pinned[j] if zc else cap.dev_seed, cap.lay, cap.dev_plan, rng=rng_ctr)
                     _rngmod.fold_next_advance(self.device)
                 else:  # first node: H2D of the plan
                     cap.dev_plan.copy_(cap.pinned[j], non_blocking=True)
