@@ -446,6 +446,12 @@ class _GPSEncoder(torch.autograd.Function):
         # could not start before it ended and only split the tail into two launch pairs;
         # measured 0.905-0.914 vs 0.921-0.923 ms/step with it on MI355X)
         early0 = wside and os.environ.get("HYDRA_EARLY_WGRAD", "0") == "1"
+        # HYDRA_L0_WGRAD_SIDE=1: layer 0's joined-branch weight gradients on a side stream beside
+        # its node backward (see below; off by default: measured 0.912-0.923 vs 0.900-0.913
+        # ms/step on MI355X, the fork / join and the shared CUs cost more than the overlap)
+        late0 = wside and os.environ.get("HYDRA_GPS_ATTN_MAIN", "0") != "1" and \
+            os.environ.get("HYDRA_L0_WGRAD_SIDE", "0") == "1"
+        l0_ev = None
         early_done = False
         gw0 = dfreq_w = te = None
         # HYDRA_GPS_ATTN_MAIN=1: the attention branch on the main stream and the local chain on
@@ -601,6 +607,29 @@ class _GPSEncoder(torch.autograd.Function):
                 # MI355X: the attention passes are throughput-bound once they overlap the local
                 # branch, 209 vs 200 us per layer)
                 side.join(dz2, da, dO, dqkv, dw2n, db2n)
+            if l == 0 and late0 and not early_done:
+                # layer 0's weight gradients whose factors are final once both branches joined
+                # (all but the edge embedding's, whose dr comes from the edge launch): one grouped
+                # launch on a fifth stream beside the node backward and the layer's edge
+                # backward, so the step's tail keeps only the small embedding problems
+                gl0 = {}
+                gl0["Wrl"] = item(dG, rbf, Wrl, False, P[26])
+                gl0["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
+                gl0["Wo"] = item(da, s["O"], Wo, True, P[2], P[3])
+                gl0["Wab"] = item(dAB, s["x"], s["Wab"], False)
+                gl0["Wr"] = item(dE, Rl[l], s["Wr"], True)
+                gl0["Wd"] = item(dE, e, s["Wd"], False)
+                gl0["Wpost"] = item(dp, s["Z"], Wpost, True, P[8], P[9])
+                gl0["Wlin"] = item(dq, s["p"], Wlin, True, P[10], P[11])
+                gl0["W1"] = item(dpre, s["out"], W1, True, P[20], P[21])
+                gl0["W2"] = item(dg, s["md"], W2, True, P[22], P[23])
+                s5 = _streams.side_stream(dev, 5)
+                s5.wait_stream(wmain)
+                with torch.cuda.stream(s5):
+                    ops.linear_wgrad_grouped(dys[lo:], xs[lo:], dws[lo:], dbs[lo:], [0] * (len(dys) - lo))
+                lo = len(dys)
+                l0_ev = torch.cuda.Event()
+                l0_ev.record(s5)
             if l > 0:
                 sp = st[l - 1]
                 g = ops.gf_node_bwd(dAB, dqkv, s["Wab"], Win, dZ, dz1, dz2, s["x"], sp["z3"], saved[l - 1], acc[l - 1],
@@ -611,6 +640,9 @@ class _GPSEncoder(torch.autograd.Function):
             if early_done and l == 0:
                 gw = gw0
                 gw["Win"] = item(dqkv, s["x"], Win, True, P[0], P[1])
+            elif l0_ev is not None and l == 0:
+                gw = gl0
+                gw["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
             else:
                 gw = {}
                 gw["Wemb"] = item(dr, rbf, Wemb, True, P[24], P[25])
@@ -632,6 +664,8 @@ class _GPSEncoder(torch.autograd.Function):
         if wside:
             # the edge backward's outputs (and the overlapped weight gradients) join the main stream
             wmain.wait_stream(wstream)
+            if l0_ev is not None:
+                wmain.wait_event(l0_ev)
             if edge_ev is not None:
                 wmain.wait_event(edge_ev)
             for t in (dr, de, drbf):
