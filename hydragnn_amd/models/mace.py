@@ -15,6 +15,7 @@ and a read-out after the embedding and after every layer whose predictions are
 reduced with the CSR segment sum over destinations (deterministic, HIP on GPU).
 """
 import math
+import os
 import warnings
 
 import torch
@@ -23,6 +24,7 @@ from torch.nn import ModuleDict, ModuleList, Sequential
 
 from .. import _native
 from ..ops import o3
+from ..ops import branch_mlp as _bmlp
 from ..ops import segment as seg
 from ..ops.pna import fused
 from ..ops.geometry import edge_vectors_and_lengths
@@ -279,6 +281,12 @@ class _PerNodeMLP(nn.Module):
         return h.transpose(0, 1).reshape(G * nn_, -1)
 
 
+def _bmlp_ok():
+    from ..ops.pna import fused
+
+    return fused("linear") and os.environ.get("HYDRA_BRANCH_MLP", "1") == "1"
+
+
 class MultiheadDecoderBlock(nn.Module):
     """Linear (intermediate) or non-linear (last) MACE read-out over all heads
     (reference ``blocks.py:417-767``)."""
@@ -343,7 +351,7 @@ class MultiheadDecoderBlock(nn.Module):
         steps = []
         for m in mods:
             if isinstance(m, nn.Linear):
-                steps.append([m.weight, m.bias, None, 1.0])
+                steps.append([m.weight, m.bias, None, 1.0, (m.weight, 0)])
             elif isinstance(m, _ScalarLinear):
                 lin = m.lin
                 if len(lin.paths) != 1 or lin.paths[0][0] != 0 or lin.irreps_in.blocks[0][1] != 0:
@@ -351,7 +359,7 @@ class MultiheadDecoderBlock(nn.Module):
                 # raw weight view; the (branch-independent) path normalisation is applied once
                 # to the stacked product instead of once per branch weight
                 _, _, _, mi, mo, a = lin.paths[0]
-                steps.append([lin.weight.view(mi, mo).t(), None, None, a])
+                steps.append([lin.weight.view(mi, mo).t(), None, None, a, (lin.weight, 1)])
                 continue
             elif steps and steps[-1][2] is None and not isinstance(m, (nn.Sequential, _PerNodeMLP)):
                 steps[-1][2] = m
@@ -370,6 +378,18 @@ class MultiheadDecoderBlock(nn.Module):
         key = (tag, rid.shape[0])
         if key not in cache:
             cache[key] = (rid.clamp(min=0).view(-1, 1, 1), (rid >= 0).to(torch.float32).view(-1, 1))
+        return cache[key]
+
+    @staticmethod
+    def _rid32(ctx, rid, tag):
+        """int32 row -> branch ids (padding rows -1), built once per forward per row kind."""
+        cache = ctx.get("_mace_rid32")
+        if cache is None:
+            cache = {}
+            ctx._mace_rid32 = cache
+        key = (tag, rid.shape[0])
+        if key not in cache:
+            cache[key] = rid.to(torch.int32).contiguous()
         return cache[key]
 
     def _stacked_dense(self, names, gfeat, sc, dn, dn_node, ctx=None):
@@ -400,6 +420,12 @@ class MultiheadDecoderBlock(nn.Module):
                 return None
             x, rid = (gfeat, dn) if t == "graph" else (sc, dn_node)
             R = x.shape[0]
+            if ctx is not None and _bmlp_ok():
+                # every row through its own branch's chain: one launch each way (ops/branch_mlp.py)
+                bch = [[(st[4][0], st[4][1], st[1], st[2], st[3]) for st in c] for c in chains]
+                if _bmlp.eligible(x, bch):
+                    outs.append(_bmlp.branch_mlp(x, self._rid32(ctx, rid, t), bch, hd))
+                    continue
             h = None  # [nb, features, R]: weights multiply from the LEFT, so the weight
             # gradients come out in the parameters' own layout (no per-parameter copies)
             for li in range(len(chains[0])):
