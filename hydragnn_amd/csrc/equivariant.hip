@@ -115,17 +115,25 @@ __global__ void __launch_bounds__(256) tp_uvu_bwd_kernel(const float* __restrict
 __device__ __forceinline__ int tp_lcode(int l1, int l2, int l3) { return (l1 * 4 + l2) * 4 + l3; }
 
 // out[n, u, :] = sum_{e in dst segment} w[e, u] * C(x1[src_e, u, :], Y_e)
+// The node's edge list (edge id, gathered node) is held lane-indexed in two VGPRs (lane q:
+// edge q of the chunk, loaded once per node) and broadcast with v_readlane: the index loads
+// were a dependent memory latency in front of every edge's row loads, paid again for every
+// instruction of the product (and, in the source-CSR backward, two of them: perm then dst).
+__device__ __forceinline__ int tp_rl(int v, int q) { return __builtin_amdgcn_readlane(v, q); }
+
 template <int L1, int L2, int L3>
 __device__ __forceinline__ void conv_fwd_body(const float* __restrict__ x1, int ld1, const float* __restrict__ y,
-                                              int ld2, const float* __restrict__ w, int ldw,
-                                              const int* __restrict__ src, int e0, int e1, const int* r,
-                                              const float* __restrict__ C, int u, float* __restrict__ o) {
+                                              int ld2, const float* __restrict__ w, int ldw, int v_e, int v_n,
+                                              int cnt, const int* r, const float* __restrict__ C, int u,
+                                              float* __restrict__ o, bool first) {
   constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
   float acc[D3];
 #pragma unroll
-  for (int k = 0; k < D3; ++k) acc[k] = 0.f;
-  for (int e = e0; e < e1; ++e) {
-    const float* a = x1 + (int64_t)src[e] * ld1 + r[4] + u * D1;
+  for (int k = 0; k < D3; ++k) acc[k] = first ? 0.f : o[k];
+#pragma unroll 2
+  for (int q = 0; q < cnt; ++q) {
+    const int e = tp_rl(v_e, q);
+    const float* a = x1 + (int64_t)tp_rl(v_n, q) * ld1 + r[4] + u * D1;
     const float* yb = y + (int64_t)e * ld2 + r[5];
     const float wu = w[(int64_t)e * ldw + r[6] + u];
     float av[D1], yv[D2];
@@ -149,17 +157,17 @@ __device__ __forceinline__ void conv_fwd_body(const float* __restrict__ x1, int 
 // gx1[n, u, :] += sum_{e in src segment} w[e, u] * C^T(go[dst_e, u, :], Y_e)
 template <int L1, int L2, int L3>
 __device__ __forceinline__ void conv_bwdx_body(const float* __restrict__ go, int ldo, const float* __restrict__ y,
-                                               int ld2, const float* __restrict__ w, int ldw,
-                                               const int* __restrict__ dst, const int* __restrict__ sperm, int b,
-                                               int eN, const int* r, const float* __restrict__ C, int u,
+                                               int ld2, const float* __restrict__ w, int ldw, int v_e, int v_n,
+                                               int cnt, const int* r, const float* __restrict__ C, int u,
                                                float* __restrict__ o) {
   constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
   float ga[D1];
 #pragma unroll
   for (int i = 0; i < D1; ++i) ga[i] = 0.f;
-  for (int q = b; q < eN; ++q) {
-    const int e = sperm ? sperm[q] : q;
-    const float* g = go + (int64_t)dst[e] * ldo + r[7] + u * D3;
+#pragma unroll 2
+  for (int q = 0; q < cnt; ++q) {
+    const int e = tp_rl(v_e, q);
+    const float* g = go + (int64_t)tp_rl(v_n, q) * ldo + r[7] + u * D3;
     const float* yb = y + (int64_t)e * ld2 + r[5];
     const float wu = w[(int64_t)e * ldw + r[6] + u];
     float gv[D3], yv[D2];
@@ -219,23 +227,29 @@ __global__ void __launch_bounds__(256) tp_conv_fwd_kernel(const float* __restric
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
   const int e0 = drp[n], e1 = drp[n + 1];
-  for (int t = 0; t < nins; ++t) {
-    const int* r = ins + t * kInsCols;
-    const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
-    const float* C = cg + r[8];
-    for (int u = lane; u < m; u += 64) {
-      float* o = out + (int64_t)n * ldo + r[7] + u * (2 * r[2] + 1);
-      switch (code) {
-#define HY_X(a, b, c)                                                             \
-  case (a * 4 + b) * 4 + c:                                                       \
-    conv_fwd_body<a, b, c>(x1, ld1, y, ld2, w, ldw, src, e0, e1, r, C, u, o); \
+  for (int c0 = e0; c0 < e1 || c0 == e0; c0 += 64) {  // chunks of 64 edges (one, typically)
+    const int cnt = min(64, e1 - c0);
+    const int q = c0 + (lane < cnt ? lane : 0);
+    const int v_e = q, v_n = cnt > 0 ? src[q < e1 ? q : e0] : 0;
+    for (int t = 0; t < nins; ++t) {
+      const int* r = ins + t * kInsCols;
+      const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
+      const float* C = cg + r[8];
+      for (int u = lane; u < m; u += 64) {
+        float* o = out + (int64_t)n * ldo + r[7] + u * (2 * r[2] + 1);
+        switch (code) {
+#define HY_X(a, b, c)                                                                           \
+  case (a * 4 + b) * 4 + c:                                                                     \
+    conv_fwd_body<a, b, c>(x1, ld1, y, ld2, w, ldw, v_e, v_n, cnt, r, C, u, o, c0 == e0); \
     break;
-        HY_TP_LCASES(HY_X)
+          HY_TP_LCASES(HY_X)
 #undef HY_X
-        default:
-          break;
+          default:
+            break;
+        }
       }
     }
+    if (cnt <= 0) break;
   }
 }
 
@@ -252,21 +266,27 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_x_kernel(const float* __restr
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
   const int b = srp[n], eN = srp[n + 1];
-  for (int t = 0; t < nins; ++t) {
-    const int* r = ins + t * kInsCols;
-    const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
-    const float* C = cg + r[8];
-    for (int u = lane; u < m; u += 64) {
-      float* o = gx1 + (int64_t)n * ld1 + r[4] + u * (2 * r[0] + 1);
-      switch (code) {
-#define HY_X(a, b_, c)                                                                      \
-  case (a * 4 + b_) * 4 + c:                                                                \
-    conv_bwdx_body<a, b_, c>(go, ldo, y, ld2, w, ldw, dst, sperm, b, eN, r, C, u, o); \
+  for (int c0 = b; c0 < eN; c0 += 64) {  // chunks of 64 source edges (one, typically)
+    const int cnt = min(64, eN - c0);
+    const int q = c0 + (lane < cnt ? lane : 0);
+    const int v_e = sperm ? sperm[q] : q;
+    const int v_n = dst[v_e];
+    for (int t = 0; t < nins; ++t) {
+      const int* r = ins + t * kInsCols;
+      const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
+      const float* C = cg + r[8];
+      for (int u = lane; u < m; u += 64) {
+        float* o = gx1 + (int64_t)n * ld1 + r[4] + u * (2 * r[0] + 1);
+        switch (code) {
+#define HY_X(a, b_, c)                                                                    \
+  case (a * 4 + b_) * 4 + c:                                                              \
+    conv_bwdx_body<a, b_, c>(go, ldo, y, ld2, w, ldw, v_e, v_n, cnt, r, C, u, o); \
     break;
-        HY_TP_LCASES(HY_X)
+          HY_TP_LCASES(HY_X)
 #undef HY_X
-        default:
-          break;
+          default:
+            break;
+        }
       }
     }
   }
