@@ -78,7 +78,7 @@ __device__ __forceinline__ const float* rlp(const float* p, int l) {
 }
 
 __global__ void __launch_bounds__(256) fwd_kernel(const float* __restrict__ x, const int* __restrict__ rid, Args a,
-                                                  float* __restrict__ out) {
+                                                  const float* __restrict__ acc, float* __restrict__ out) {
   __shared__ float hbuf[kMaxW];
   __shared__ float zbuf[kMaxW];
   __shared__ float red[4 * 16 * 65];
@@ -96,7 +96,8 @@ __global__ void __launch_bounds__(256) fwd_kernel(const float* __restrict__ x, c
   float* v_hs = a.hs[ll];
   float* v_zs = a.zs[ll];
   if (b < 0) {  // padding row: zero output (its saved values are never read through a slab)
-    for (int j = tid; j < a.hd; j += 256) out[(int64_t)r * a.hd + j] = 0.f;
+    for (int j = tid; j < a.hd; j += 256)
+      out[(int64_t)r * a.hd + j] = acc != nullptr ? acc[(int64_t)r * a.hd + j] : 0.f;
     for (int l = 0; l < L; ++l) {
       const int I = rl(v_dims, l), O = rl(v_dims, l + 1);
       float* hs = (float*)rlp(v_hs, l);
@@ -165,7 +166,8 @@ __global__ void __launch_bounds__(256) fwd_kernel(const float* __restrict__ x, c
     }
     __syncthreads();
   }
-  for (int j = tid; j < a.hd; j += 256) out[(int64_t)r * a.hd + j] = hbuf[j];
+  for (int j = tid; j < a.hd; j += 256)
+    out[(int64_t)r * a.hd + j] = hbuf[j] + (acc != nullptr ? acc[(int64_t)r * a.hd + j] : 0.f);
 }
 
 __global__ void __launch_bounds__(256) bwd_kernel(const float* __restrict__ gout, const int* __restrict__ rid, Args a,
@@ -268,11 +270,18 @@ static bm::Args bm_args(const at::Tensor& x, const at::Tensor& rid, const at::Te
   return a;
 }
 
+// acc (optional, [R, hd]): added to the output (read-outs summed over the stack's layers)
 std::vector<at::Tensor> branch_mlp_fwd(const at::Tensor& x, const at::Tensor& rid, const at::Tensor& ptab, int64_t nb,
                                        at::IntArrayRef dims, at::IntArrayRef acts, at::IntArrayRef trans,
-                                       at::ArrayRef<double> scales, int64_t hd) {
+                                       at::ArrayRef<double> scales, int64_t hd, const c10::optional<at::Tensor>& acc) {
   bm::Args a = bm_args(x, rid, ptab, nb, dims, acts, trans, scales, hd);
   const int64_t R = x.size(0);
+  const float* ap = nullptr;
+  if (acc.has_value() && acc->defined()) {
+    HY_CHECK(acc->is_cuda() && acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() == R * hd,
+             "branch_mlp: acc [R, hd] contiguous fp32");
+    ap = acc->data_ptr<float>();
+  }
   auto out = at::empty({R, hd}, x.options());
   std::vector<at::Tensor> res{out};
   for (int l = 0; l < a.L; ++l) res.push_back(at::empty({R, (int64_t)a.dims[l]}, x.options()));
@@ -281,7 +290,8 @@ std::vector<at::Tensor> branch_mlp_fwd(const at::Tensor& x, const at::Tensor& ri
     a.hs[l] = res[1 + l].data_ptr<float>();
     a.zs[l] = res[1 + a.L + l].data_ptr<float>();
   }
-  if (R > 0) bm::fwd_kernel<<<(int)R, 256, 0, stream()>>>(x.data_ptr<float>(), rid.data_ptr<int>(), a, out.data_ptr<float>());
+  if (R > 0)
+    bm::fwd_kernel<<<(int)R, 256, 0, stream()>>>(x.data_ptr<float>(), rid.data_ptr<int>(), a, ap, out.data_ptr<float>());
   return res;
 }
 
@@ -313,7 +323,7 @@ std::vector<at::Tensor> branch_mlp_bwd(const at::Tensor& gout_, const at::Tensor
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def(
       "branch_mlp_fwd(Tensor x, Tensor rid, Tensor ptab, int nb, int[] dims, int[] acts, int[] trans, "
-      "float[] scales, int hd) -> Tensor[]");
+      "float[] scales, int hd, Tensor? acc=None) -> Tensor[]");
   m.def(
       "branch_mlp_bwd(Tensor gout, Tensor x, Tensor rid, Tensor ptab, int nb, int[] dims, int[] acts, "
       "int[] trans, float[] scales, int hd, Tensor[] zs) -> Tensor[]");

@@ -392,7 +392,7 @@ class MultiheadDecoderBlock(nn.Module):
             cache[key] = rid.to(torch.int32).contiguous()
         return cache[key]
 
-    def _stacked_dense(self, names, gfeat, sc, dn, dn_node, ctx=None):
+    def _stacked_dense(self, names, gfeat, sc, dn, dn_node, ctx=None, acc=None):
         """Dense multi-branch decode with the branches STACKED: per layer one GEMM over all
         branches (the first layer's weights concatenated along the output, later layers one
         batched product), then one per-row gather of the row's own branch.  Same values as
@@ -403,7 +403,7 @@ class MultiheadDecoderBlock(nn.Module):
         if [int(b.split("-")[1]) for b in names] != list(range(nb)):
             return None
         outs = []
-        for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
+        for ih, (hd, hn, t) in enumerate(zip(self.head_dims, self.heads_NN, self.head_type)):
             chains = []
             for bt in names:
                 mods = list(hn[bt]) if isinstance(hn[bt], nn.Sequential) else None
@@ -424,7 +424,11 @@ class MultiheadDecoderBlock(nn.Module):
                 # every row through its own branch's chain: one launch each way (ops/branch_mlp.py)
                 bch = [[(st[4][0], st[4][1], st[1], st[2], st[3]) for st in c] for c in chains]
                 if _bmlp.eligible(x, bch):
-                    outs.append(_bmlp.branch_mlp(x, self._rid32(ctx, rid, t), bch, hd))
+                    a = acc[ih] if acc is not None else None
+                    if a is not None and not (a.shape == (R, hd) and a.dtype == x.dtype):
+                        a = None
+                    o = _bmlp.branch_mlp(x, self._rid32(ctx, rid, t), bch, hd, acc=a)
+                    outs.append(o if (a is not None or acc is None) else o + acc[ih])
                     continue
             h = None  # [nb, features, R]: weights multiply from the LEFT, so the weight
             # gradients come out in the parameters' own layout (no per-parameter copies)
@@ -447,14 +451,24 @@ class MultiheadDecoderBlock(nn.Module):
             if ctx is not None:
                 idx, valid = self._row_select(ctx, rid, t)
                 sel = h.gather(1, idx.expand(R, 1, hd)).squeeze(1)
-                outs.append(sel * valid.to(sel.dtype))
+                outs.append(sel * valid.to(sel.dtype) if acc is None else acc[ih] + sel * valid.to(sel.dtype))
             else:
                 sel = h.gather(1, rid.clamp(min=0).view(R, 1, 1).expand(R, 1, hd)).squeeze(1)
-                outs.append(torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype,
-                                                                                  device=sel.device)))
+                sel = torch.where((rid >= 0).unsqueeze(1), sel, torch.zeros((), dtype=sel.dtype, device=sel.device))
+                outs.append(sel if acc is None else acc[ih] + sel)
         return outs
 
-    def forward(self, node_features, ctx, ids):
+    def forward(self, node_features, ctx, ids, acc=None):
+        """Read-out of every head; ``acc`` (the previous layers' summed read-outs): the result
+        is ``acc + read-out`` (fused into the branch kernel on the captured path)."""
+        if acc is not None:
+            out = self._forward(node_features, ctx, ids, acc)
+            if isinstance(out, tuple):  # (outputs, fused) from the stacked path
+                return out[0]
+            return [a + b for a, b in zip(acc, out)]
+        return self._forward(node_features, ctx, ids, None)
+
+    def _forward(self, node_features, ctx, ids, acc):
         gsi = ctx.graph_si
         # the read-outs only use the scalar channels; the stack hands over just those
         sc = node_features if node_features.shape[1] == self.input_scalar_dim else \
@@ -472,9 +486,9 @@ class MultiheadDecoderBlock(nn.Module):
             if dn_node is None:  # once per forward (shared by every read-out)
                 dn_node = ctx._mace_dn_node = dn.index_select(0, data.batch)
             names = sorted(self.heads_NN[0].keys(), key=lambda k: int(k.split("-")[1]))
-            stacked = self._stacked_dense(names, gfeat, sc, dn, dn_node, ctx)
+            stacked = self._stacked_dense(names, gfeat, sc, dn, dn_node, ctx, acc=acc)
             if stacked is not None:
-                return stacked
+                return (stacked, True) if acc is not None else stacked
             for hd, hn, t in zip(self.head_dims, self.heads_NN, self.head_type):
                 feats, rid = (gfeat, dn) if t == "graph" else (node_features, dn_node)
                 out = feats.new_zeros(feats.shape[0], hd)
@@ -674,8 +688,7 @@ class MACEStack(Base):
         outputs = self.multihead_decoders[0](ctx.node_attributes, ctx, ids)
         for conv, readout in zip(self.graph_convs, self.multihead_decoders[1:]):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)
-            out = readout(inv, ctx, ids)  # read-outs map the scalar block only
-            outputs = [a + b for a, b in zip(outputs, out)]
+            outputs = readout(inv, ctx, ids, acc=outputs)  # scalar block only; + the running sum
         return outputs
 
     def __str__(self):

@@ -70,9 +70,10 @@ def _ptab(chains, dev):
 
 class _BranchMLP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, rid, meta, *params):
+    def forward(ctx, x, rid, acc, meta, *params):
         L, nb, dims, acts, trans, scales, hd, ptab, layout = meta
-        res = _native.ops().branch_mlp_fwd(x, rid, ptab, nb, dims, acts, trans, scales, hd)
+        res = _native.ops().branch_mlp_fwd(x, rid, ptab, nb, dims, acts, trans, scales, hd,
+                                           None if acc is None else acc.contiguous())
         out, hs, zs = res[0], res[1:1 + L], res[1 + L:1 + 2 * L]
         ctx.save_for_backward(x, rid, *hs, *zs)
         ctx.meta = meta
@@ -112,11 +113,12 @@ class _BranchMLP(torch.autograd.Function):
             pg = [None] * len(params)
         else:
             pg = grads
-        return (dx if ctx.needs_input_grad[0] else None, None, None, *pg)
+        return (dx if ctx.needs_input_grad[0] else None, None, g if ctx.needs_input_grad[2] else None, None, *pg)
 
 
-def branch_mlp(x, rid, chains, hd):
-    """``out[r] = chain_{rid[r]}(x[r])[:hd]`` (rows with rid < 0: zero).  ``rid`` int32 [R]."""
+def branch_mlp(x, rid, chains, hd, acc=None):
+    """``out[r] = chain_{rid[r]}(x[r])[:hd]`` (rows with rid < 0: zero), plus ``acc`` [R, hd]
+    when given (summed read-outs: no separate add).  ``rid`` int32 [R]."""
     L, nb = len(chains[0]), len(chains)
     x = x.contiguous()
     dims = _dims(chains, x.shape[1])
@@ -137,4 +139,4 @@ def branch_mlp(x, rid, chains, hd):
             row.append((wi, bi))
         layout.append(row)
     meta = (L, nb, dims, acts, trans, scales, int(hd), _ptab(chains, x.device), layout)
-    return _BranchMLP.apply(x, rid, meta, *params)
+    return _BranchMLP.apply(x, rid, acc, meta, *params)

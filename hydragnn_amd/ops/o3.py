@@ -503,7 +503,8 @@ class _FCNFirstSplit(torch.autograd.Function):
         from .. import _native
 
         nef, nd = ef.shape[1], down.shape[1]
-        ab = torch.matmul(down.unsqueeze(0), W1[nef:].view(2, nd, nd))  # [2, N, nd]: A block, B block
+        # [N, 2 nd] = down @ [W_s | W_d] (one GEMM; the column blocks of W1[nef:] side by side)
+        ab = down @ W1[nef:].view(2, nd, nd).permute(1, 0, 2).reshape(nd, 2 * nd)
         et = ef @ W1[:nef]
         ctx.save_for_backward(ef, down, W1, ab, et)
         ctx.cfg = (s, src_si, dst_si)

@@ -72,3 +72,20 @@ def test_branch_mlp_matches_per_row_loop(R, dims, acts, trans, nb):
                 gb = b.grad if b.grad is not None else torch.zeros_like(b)
                 rgb = rb.grad if rb.grad is not None else torch.zeros_like(rb)
                 torch.testing.assert_close(gb.double().cpu(), rgb, rtol=1e-4, atol=1e-5)
+
+
+def test_branch_mlp_accumulates_into_previous_readouts():
+    """``acc``: out = acc + chain(x) (padding rows keep acc), d acc = the upstream gradient."""
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    chains = [[(nn.Parameter(torch.randn(3, 16, generator=g).to(dev)), 0,
+                nn.Parameter(torch.randn(3, generator=g).to(dev)), None, 1.0)] for _ in range(2)]
+    x = torch.randn(9, 16, generator=g).to(dev).requires_grad_(True)
+    rid = torch.tensor([0, 1, -1, 1, 0, 0, -1, 1, 1], dtype=torch.int32, device=dev)
+    acc = torch.randn(9, 3, generator=g).to(dev).requires_grad_(True)
+    out = bm.branch_mlp(x, rid, chains, 3, acc=acc)
+    base = bm.branch_mlp(x.detach(), rid, chains, 3)
+    torch.testing.assert_close(out, acc.detach() + base, rtol=1e-6, atol=1e-6)
+    go = torch.randn(9, 3, generator=g).to(dev)
+    out.backward(go)
+    torch.testing.assert_close(acc.grad, go)

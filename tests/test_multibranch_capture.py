@@ -128,8 +128,8 @@ def test_mace_stacked_dense_decode_matches_branch_loop(monkeypatch):
     calls = []
     orig = MultiheadDecoderBlock._stacked_dense
 
-    def spy(self, *a):
-        out = orig(self, *a)
+    def spy(self, *a, **kw):
+        out = orig(self, *a, **kw)
         calls.append(out is not None)
         return out
 
@@ -142,7 +142,7 @@ def test_mace_stacked_dense_decode_matches_branch_loop(monkeypatch):
     monkeypatch.setattr(MultiheadDecoderBlock, "_stacked_dense", spy)
     l1, g1 = run()
     assert calls and all(calls)
-    monkeypatch.setattr(MultiheadDecoderBlock, "_stacked_dense", lambda self, *a: None)
+    monkeypatch.setattr(MultiheadDecoderBlock, "_stacked_dense", lambda self, *a, **kw: None)
     l2, g2 = run()
     assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l2))
     assert g1.keys() == g2.keys()
