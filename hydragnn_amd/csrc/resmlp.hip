@@ -158,6 +158,102 @@ __global__ void __launch_bounds__(256) res_mlp_bwd_kernel(const float* __restric
   }
 }
 
+// One SiLU linear in one launch each way (the DimeNet++ interaction / embedding blocks'
+// act(lin(x)) * m + a chains, reference DIMEStack.py -> PyG InteractionPPBlock):
+//   forward   z = x W^T + b,  y = silu(z) * mul + add      (mul / add optional, [M, O])
+//   backward  g = dy * mul,  dz = g * silu'(z),  dx = dz W,  dmul = dy * silu(z)
+// (z saved by the forward; the weight gradient's row factors (dz, x) join the step's grouped
+// weight-gradient launch).  I, O <= 64; layout as the residual block above.
+__global__ void __launch_bounds__(256) lin_act_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                          const float* __restrict__ b, const float* __restrict__ mul,
+                                                          const float* __restrict__ add, int M, int I, int O,
+                                                          float* __restrict__ y, float* __restrict__ Z) {
+  __shared__ __attribute__((aligned(16))) float xs[kRB][kLd];
+  __shared__ float ws[kMaxW][kMaxW + 1];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * kRB;
+  float tx[kRB / 4], tw[kMaxW / 4];
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) {
+    const int m = m0 + q + 4 * u;
+    tx[u] = (m < M && c < I) ? x[(int64_t)m * I + c] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) {
+    const int r = q + 4 * u;
+    tw[u] = (r < O && c < I) ? W[r * I + c] : 0.f;
+  }
+  const float bias = (b != nullptr && c < O) ? b[c] : 0.f;
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) xs[q + 4 * u][c] = tx[u];
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) ws[q + 4 * u][c] = tw[u];
+  __syncthreads();
+  float w[kMaxW];
+#pragma unroll
+  for (int k = 0; k < kMaxW; ++k) w[k] = (c < O && k < I) ? ws[c][k] : 0.f;
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) {
+    const int r = q + 4 * u, m = m0 + r;
+    if (m < M && c < O) {
+      const float z = bias + rowdot(xs[r], w);
+      const int64_t o = (int64_t)m * O + c;
+      Z[o] = z;
+      float v = silu(z);
+      if (mul != nullptr) v *= mul[o];
+      if (add != nullptr) v += add[o];
+      y[o] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) lin_act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ Z,
+                                                          const float* __restrict__ W, const float* __restrict__ mul,
+                                                          int M, int I, int O, float* __restrict__ dx,
+                                                          float* __restrict__ dZ, float* __restrict__ dmul) {
+  __shared__ __attribute__((aligned(16))) float gs[kRB][kLd];
+  __shared__ float ws[kMaxW][kMaxW + 1];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * kRB;
+  float tg[kRB / 4], tz[kRB / 4], tm[kRB / 4], tw[kMaxW / 4];
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) {
+    const int m = m0 + q + 4 * u;
+    const bool ok = m < M && c < O;
+    tg[u] = ok ? dy[(int64_t)m * O + c] : 0.f;
+    tz[u] = ok ? Z[(int64_t)m * O + c] : 0.f;
+    tm[u] = (ok && mul != nullptr) ? mul[(int64_t)m * O + c] : 1.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) {
+    const int r = q + 4 * u;
+    tw[u] = (r < O && c < I) ? W[r * I + c] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxW / 4; ++u) ws[q + 4 * u][c] = tw[u];
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) {
+    const int r = q + 4 * u, m = m0 + r;
+    const float g = tg[u] * tm[u] * dsilu(tz[u]);
+    if (m < M && c < O) {
+      const int64_t o = (int64_t)m * O + c;
+      dZ[o] = g;
+      if (dmul != nullptr) dmul[o] = tg[u] * silu(tz[u]);
+    }
+    gs[r][c] = c < O ? g : 0.f;
+  }
+  __syncthreads();
+  // dx[m, i] = sum_o dz[m, o] W[o, i]: column i of W
+  float w[kMaxW];
+#pragma unroll
+  for (int k = 0; k < kMaxW; ++k) w[k] = (k < O && c < I) ? ws[k][c] : 0.f;
+#pragma unroll
+  for (int u = 0; u < kRB / 4; ++u) {
+    const int r = q + 4 * u, m = m0 + r;
+    if (m < M && c < I) dx[(int64_t)m * I + c] = rowdot(gs[r], w);
+  }
+}
+
 }  // namespace rm
 
 static void rm_check(const at::Tensor& t, const char* name) {
@@ -208,14 +304,76 @@ std::vector<at::Tensor> res_mlp_bwd(const at::Tensor& dy_, const at::Tensor& H1,
   return {dx, dH2, A1, dH1};
 }
 
+// x [M, I], W [O, I], b [O] | None, mul / add [M, O] | None -> (y, z)
+std::vector<at::Tensor> lin_act_fwd(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
+                                    const c10::optional<at::Tensor>& mul, const c10::optional<at::Tensor>& add) {
+  rm_check(x, "x");
+  rm_check(W, "W");
+  HY_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == x.size(1) && x.size(1) <= rm::kMaxW && W.size(0) <= rm::kMaxW,
+           "lin_act_fwd: x [M, I], W [O, I], I, O <= 64");
+  const int64_t M = x.size(0);
+  const int I = (int)x.size(1), O = (int)W.size(0);
+  const float *bp = nullptr, *mp = nullptr, *ap = nullptr;
+  if (b.has_value() && b->defined()) {
+    rm_check(*b, "b");
+    HY_CHECK(b->numel() == O, "lin_act_fwd: b [O]");
+    bp = b->data_ptr<float>();
+  }
+  if (mul.has_value() && mul->defined()) {
+    rm_check(*mul, "mul");
+    HY_CHECK(mul->numel() == M * O, "lin_act_fwd: mul [M, O]");
+    mp = mul->data_ptr<float>();
+  }
+  if (add.has_value() && add->defined()) {
+    rm_check(*add, "add");
+    HY_CHECK(add->numel() == M * O, "lin_act_fwd: add [M, O]");
+    ap = add->data_ptr<float>();
+  }
+  auto y = at::empty({M, O}, x.options()), Z = at::empty({M, O}, x.options());
+  if (M)
+    rm::lin_act_fwd_kernel<<<ceil_div(M, rm::kRB), 256, 0, stream()>>>(x.data_ptr<float>(), W.data_ptr<float>(), bp, mp,
+                                                                         ap, (int)M, I, O, y.data_ptr<float>(),
+                                                                         Z.data_ptr<float>());
+  return {y, Z};
+}
+
+// -> (dx, dz, dmul | empty)
+std::vector<at::Tensor> lin_act_bwd(const at::Tensor& dy_, const at::Tensor& Z, const at::Tensor& W,
+                                    const c10::optional<at::Tensor>& mul, bool want_dmul) {
+  auto dy = dy_.contiguous();
+  rm_check(dy, "dy");
+  rm_check(Z, "Z");
+  rm_check(W, "W");
+  const int64_t M = Z.size(0);
+  const int O = (int)Z.size(1), I = (int)W.size(1);
+  HY_CHECK(dy.sizes() == Z.sizes() && W.size(0) == O && I <= rm::kMaxW && O <= rm::kMaxW, "lin_act_bwd: shapes");
+  const float* mp = nullptr;
+  if (mul.has_value() && mul->defined()) {
+    rm_check(*mul, "mul");
+    HY_CHECK(mul->sizes() == Z.sizes(), "lin_act_bwd: mul [M, O]");
+    mp = mul->data_ptr<float>();
+  }
+  auto dx = at::empty({M, (int64_t)I}, Z.options()), dZ = at::empty_like(Z);
+  auto dmul = want_dmul ? at::empty_like(Z) : at::empty({0}, Z.options());
+  if (M)
+    rm::lin_act_bwd_kernel<<<ceil_div(M, rm::kRB), 256, 0, stream()>>>(
+        dy.data_ptr<float>(), Z.data_ptr<float>(), W.data_ptr<float>(), mp, (int)M, I, O, dx.data_ptr<float>(),
+        dZ.data_ptr<float>(), want_dmul ? dmul.data_ptr<float>() : nullptr);
+  return {dx, dZ, dmul};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("res_mlp_fwd(Tensor x, Tensor W1, Tensor b1, Tensor W2, Tensor b2) -> Tensor[]");
   m.def("res_mlp_bwd(Tensor dy, Tensor H1, Tensor H2, Tensor W1, Tensor W2) -> Tensor[]");
+  m.def("lin_act_fwd(Tensor x, Tensor W, Tensor? b, Tensor? mul, Tensor? add) -> Tensor[]");
+  m.def("lin_act_bwd(Tensor dy, Tensor Z, Tensor W, Tensor? mul, bool want_dmul) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("res_mlp_fwd", hy::res_mlp_fwd);
   m.impl("res_mlp_bwd", hy::res_mlp_bwd);
+  m.impl("lin_act_fwd", hy::lin_act_fwd);
+  m.impl("lin_act_bwd", hy::lin_act_bwd);
 }

@@ -263,6 +263,60 @@ class _ResMLP(torch.autograd.Function):
         return dx, dW1, db1, dW2, db2
 
 
+class _SiluLinear(torch.autograd.Function):
+    """y = silu(x W^T + b) * mul + add in one HIP launch each way (csrc/resmlp.hip lin_act);
+    the weight gradient's row factors join the deferred grouped weight-gradient launch."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, mul, add):
+        from .. import _native
+
+        y, Z = _native.ops().lin_act_fwd(x, W, b, mul, add)
+        ctx.save_for_backward(x, Z, W, mul)
+        ctx.params = (W, b)
+        ctx.has_add = add is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+        from ..ops import linear as _lin
+
+        x, Z, W, mul = ctx.saved_tensors
+        want_dmul = mul is not None and ctx.needs_input_grad[3]
+        dx, dZ, dmul = _native.ops().lin_act_bwd(g, Z, W, mul, want_dmul)
+        Wp, bp = ctx.params
+        dadd = g if (ctx.has_add and ctx.needs_input_grad[4]) else None
+        dmul = dmul if want_dmul else None
+        if _lin._can_defer(Wp, bp):
+            _lin._record((dZ, x, Wp, bp))
+            return dx, None, None, dmul, dadd
+        dW = torch.empty_like(Wp)
+        db = torch.empty_like(bp) if bp is not None else torch.empty(0, device=g.device, dtype=g.dtype)
+        _native.ops().linear_wgrad_grouped([dZ], [x], [dW], [db], [0])
+        return dx, dW, (db if bp is not None else None), dmul, dadd
+
+
+def silu_lin(lin, act, x, mul=None, add=None):
+    """``act(lin(x)) * mul + add`` (mul / add optional): one fused HIP launch each way for
+    SiLU on GPU fp32 edge-sized rows (widths <= 64), the module chain otherwise."""
+    from ..ops.pna import fused
+
+    W = lin.weight
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[0] >= 1024 and x.shape[1] <= 64 and
+            W.shape[0] <= 64 and isinstance(act, nn.SiLU) and fused("resmlp") and torch.is_grad_enabled() and
+            (mul is None or mul.shape == (x.shape[0], W.shape[0])) and
+            (add is None or add.shape == (x.shape[0], W.shape[0]))):
+        return _SiluLinear.apply(x.contiguous(), W, lin.bias, None if mul is None else mul.contiguous(),
+                                 None if add is None else add.contiguous())
+    y = act(lin(x))
+    if mul is not None:
+        y = y * mul
+    if add is not None:
+        y = y + add
+    return y
+
+
 class ResidualLayer(nn.Module):
     def __init__(self, hidden, act):
         super().__init__()
@@ -328,15 +382,16 @@ class InteractionPPBlock(nn.Module):
                 l.bias.data.fill_(0)
 
     def forward(self, x, rbf, sbf, kj_si, ji_si):
-        x_ji = self.act(self.lin_ji(x))
-        x_kj = self.act(self.lin_kj(x)) * self.lin_rbf2(self.lin_rbf1(rbf))
-        x_kj = self.act(self.lin_down(x_kj))
+        # every act(lin(.)) (* / +) step is one fused launch each way (silu_lin)
+        x_ji = silu_lin(self.lin_ji, self.act, x)
+        x_kj = silu_lin(self.lin_kj, self.act, x, mul=self.lin_rbf2(self.lin_rbf1(rbf)))
+        x_kj = silu_lin(self.lin_down, self.act, x_kj)
         sbf = self.lin_sbf2(self.lin_sbf1(sbf))
         x_kj = seg.gather_mul_sum(x_kj, sbf, kj_si, ji_si)  # triplet gather * sbf -> sum, one pass
-        h = x_ji + self.act(self.lin_up(x_kj))
+        h = silu_lin(self.lin_up, self.act, x_kj, add=x_ji)
         for layer in self.layers_before_skip:
             h = layer(h)
-        h = self.act(self.lin(h)) + x
+        h = silu_lin(self.lin, self.act, h, add=x)
         for layer in self.layers_after_skip:
             h = layer(h)
         return h

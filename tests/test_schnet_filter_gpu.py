@@ -89,3 +89,52 @@ def test_element_index_one_wave_matches_cpu(N, S):
     b = element_index(elem.cuda(), S)
     assert torch.equal(a.index, b.index.cpu()) and torch.equal(a.rowptr, b.rowptr.cpu())
     assert torch.equal(a.perm, b.perm.cpu())
+
+
+@pytest.mark.parametrize("I,O,bias,mul,add", [(64, 64, True, False, False), (64, 64, True, True, False),
+                                              (64, 48, False, False, True), (40, 64, True, True, True)])
+def test_dimenet_silu_linear_matches_fp64(I, O, bias, mul, add):
+    """DimeNet++ act(lin(x)) * m + a step in one launch each way (models/dimenet.py silu_lin,
+    csrc/resmlp.hip lin_act) == the fp64 module chain: values, dx, dW, db, dmul, dadd."""
+    from torch import nn
+
+    from hydragnn_amd.models.dimenet import _SiluLinear, silu_lin
+
+    g = torch.Generator().manual_seed(I + O + 2 * mul + add)
+    M = 3000
+    lin = nn.Linear(I, O, bias=bias).double()
+    x = torch.randn(M, I, generator=g, dtype=torch.float64)
+    m = torch.randn(M, O, generator=g, dtype=torch.float64) if mul else None
+    a = torch.randn(M, O, generator=g, dtype=torch.float64) if add else None
+    go = torch.randn(M, O, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    mr = m.clone().requires_grad_(True) if mul else None
+    ar = a.clone().requires_grad_(True) if add else None
+    ref = torch.nn.functional.silu(lin(xr))
+    if mul:
+        ref = ref * mr
+    if add:
+        ref = ref + ar
+    ref.backward(go)
+    dev = torch.device("cuda")
+    lind = nn.Linear(I, O, bias=bias).to(dev)
+    with torch.no_grad():
+        lind.weight.copy_(lin.weight.float())
+        if bias:
+            lind.bias.copy_(lin.bias.float())
+    xd = x.float().to(dev).requires_grad_(True)
+    md = m.float().to(dev).requires_grad_(True) if mul else None
+    ad = a.float().to(dev).requires_grad_(True) if add else None
+    out = silu_lin(lind, nn.SiLU(), xd, mul=md, add=ad)
+    assert isinstance(out.grad_fn.__class__, type) and "SiluLinear" in type(out.grad_fn).__name__
+    out.backward(go.float().to(dev))
+    tol = dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), **tol)
+    torch.testing.assert_close(xd.grad.double().cpu(), xr.grad, **tol)
+    torch.testing.assert_close(lind.weight.grad.double().cpu(), lin.weight.grad, rtol=1e-4, atol=1e-3)
+    if bias:
+        torch.testing.assert_close(lind.bias.grad.double().cpu(), lin.bias.grad, rtol=1e-4, atol=1e-3)
+    if mul:
+        torch.testing.assert_close(md.grad.double().cpu(), mr.grad, **tol)
+    if add:
+        torch.testing.assert_close(ad.grad.double().cpu(), ar.grad, **tol)
