@@ -46,7 +46,15 @@ def make_segments(num_nodes, scope="batch", ptr=None, num_valid=None, device=Non
     raise ValueError(f"unknown attention scope {scope}")
 
 
-def attention_reference(qkv, heads, seg_id, scale=None):
+def attention_reference(qkv, heads, seg_id, scale=None, seg_ptr=None):
+    """Plain-torch segment attention (the numerics oracle, and the twice-differentiable path
+    of force training).  With ``seg_ptr`` and many short segments (graph scope) it runs on a
+    dense per-segment batch [S, H, L, L] (the reference's to_dense_batch form) instead of
+    masking an [H, N, N] score matrix: memory O(sum of L^2), not O(N^2)."""
+    if seg_ptr is not None and seg_ptr.numel() > 2:
+        out = _attention_dense_batch(qkv, heads, seg_id, seg_ptr, scale)
+        if out is not None:
+            return out
     N, F3 = qkv.shape
     F = F3 // 3
     D = F // heads
@@ -61,6 +69,31 @@ def attention_reference(qkv, heads, seg_id, scale=None):
     p = torch.softmax(s, dim=-1)
     o = torch.matmul(p, v)
     return o.transpose(0, 1).reshape(N, F)
+
+
+def _attention_dense_batch(qkv, heads, seg_id, seg_ptr, scale):
+    N, F3 = qkv.shape
+    F = F3 // 3
+    D = F // heads
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    S = seg_ptr.numel() - 1
+    ptr = seg_ptr.long()
+    lens = ptr[1:] - ptr[:-1]
+    L = int(lens.max())  # host sync: the composite (eager) path only
+    if S * L * L * 2 > N * N:  # one long segment dominates: the masked form is no larger
+        return None
+    sid = seg_id.long()
+    pos = torch.arange(N, device=qkv.device) - ptr[sid]
+    idx = sid * L + pos  # row of each token in the dense [S * L] layout
+    dense = qkv.new_zeros(S * L, F3).index_copy(0, idx, qkv)  # differentiable in qkv (any order)
+    dense = dense.view(S, L, 3, heads, D).permute(2, 0, 3, 1, 4)  # [3, S, H, L, D]
+    q, k, v = dense[0], dense[1], dense[2]
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale  # [S, H, L, L]
+    valid = torch.arange(L, device=qkv.device).view(1, L) < lens.view(S, 1)  # [S, L] real keys
+    s = s.masked_fill(~valid.view(S, 1, 1, L), float("-inf"))
+    o = torch.matmul(torch.softmax(s, dim=-1), v)  # [S, H, L, D]
+    o = o.permute(0, 2, 1, 3).reshape(S * L, F)
+    return o.index_select(0, idx)
 
 
 _SPLITS = int(os.environ.get("HYDRA_ATTN_SPLITS", "0"))  # 0 = kernel heuristic
@@ -116,4 +149,4 @@ def segment_attention(qkv, heads, seg_id, seg_ptr, scale=None):
     if (qkv.is_cuda and qkv.dtype == torch.float32 and D in (4, 8, 16, 32, 64)
             and _pna_mode.fused("attn")):
         return _FlashAttn.apply(qkv, seg_id, seg_ptr, heads, scale)
-    return attention_reference(qkv, heads, seg_id, scale)
+    return attention_reference(qkv, heads, seg_id, scale, seg_ptr=seg_ptr)

@@ -182,3 +182,30 @@ def test_fcn_folded_scales_match_definition():
     torch.testing.assert_close(f(x), h)
     f.defer_last_scale = True
     torch.testing.assert_close(f(x) * f.last_scale(), h)
+
+
+def test_composite_attention_dense_batch_matches_masked_to_second_order():
+    """Force training's composite attention on many short segments runs as a dense
+    per-segment batch [S, H, L, L] (memory O(sum L^2), not O(N^2)); values, first and second
+    derivatives equal the masked [H, N, N] form."""
+    from hydragnn_amd.ops import attention as A
+
+    g = torch.Generator().manual_seed(0)
+    lens = [int(x) for x in torch.randint(2, 10, (20,), generator=g)]
+    N, H, D = sum(lens), 4, 4
+    F = H * D
+    ptr = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
+    sid = torch.repeat_interleave(torch.arange(len(lens)), torch.tensor(lens)).int()
+    qkv = torch.randn(N, 3 * F, generator=g, dtype=torch.float64, requires_grad=True)
+    assert A._attention_dense_batch(qkv, H, sid, ptr, None) is not None
+    a = A.attention_reference(qkv, H, sid)
+    b = A.attention_reference(qkv, H, sid, seg_ptr=ptr)
+    torch.testing.assert_close(a, b)
+    w = torch.randn(a.shape, generator=g, dtype=torch.float64)
+    ga, = torch.autograd.grad((a * w).sum(), qkv, create_graph=True)
+    gb, = torch.autograd.grad((b * w).sum(), qkv, create_graph=True)
+    torch.testing.assert_close(ga, gb)
+    h = torch.randn(ga.shape, generator=g, dtype=torch.float64)
+    gga, = torch.autograd.grad((ga * h).sum(), qkv)
+    ggb, = torch.autograd.grad((gb * h).sum(), qkv)
+    torch.testing.assert_close(gga, ggb)
