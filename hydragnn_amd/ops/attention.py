@@ -48,10 +48,12 @@ def make_segments(num_nodes, scope="batch", ptr=None, num_valid=None, device=Non
 
 def attention_reference(qkv, heads, seg_id, scale=None, seg_ptr=None):
     """Plain-torch segment attention (the numerics oracle, and the twice-differentiable path
-    of force training).  With ``seg_ptr`` and many short segments (graph scope) it runs on a
+    of force training).  In composite mode (force training, eager), with ``seg_ptr`` and many
+    short segments (graph scope) it runs on a
     dense per-segment batch [S, H, L, L] (the reference's to_dense_batch form) instead of
     masking an [H, N, N] score matrix: memory O(sum of L^2), not O(N^2)."""
-    if seg_ptr is not None and seg_ptr.numel() > 2:
+    if seg_ptr is not None and seg_ptr.numel() > 2 and _pna_mode._state["composite"] and \
+            not (qkv.is_cuda and torch.cuda.is_current_stream_capturing()):
         out = _attention_dense_batch(qkv, heads, seg_id, seg_ptr, scale)
         if out is not None:
             return out

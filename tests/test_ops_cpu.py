@@ -198,8 +198,11 @@ def test_composite_attention_dense_batch_matches_masked_to_second_order():
     sid = torch.repeat_interleave(torch.arange(len(lens)), torch.tensor(lens)).int()
     qkv = torch.randn(N, 3 * F, generator=g, dtype=torch.float64, requires_grad=True)
     assert A._attention_dense_batch(qkv, H, sid, ptr, None) is not None
+    from hydragnn_amd.ops.pna import composite_mode
+
     a = A.attention_reference(qkv, H, sid)
-    b = A.attention_reference(qkv, H, sid, seg_ptr=ptr)
+    with composite_mode(True):
+        b = A.attention_reference(qkv, H, sid, seg_ptr=ptr)
     torch.testing.assert_close(a, b)
     w = torch.randn(a.shape, generator=g, dtype=torch.float64)
     ga, = torch.autograd.grad((a * w).sum(), qkv, create_graph=True)
