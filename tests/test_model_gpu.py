@@ -170,19 +170,27 @@ def test_graph_step_follows_lr_changes():
 def test_graph_step_head_gradient_slots_match(monkeypatch):
     """The fused graph head under gradient slots (ops/mlp.py _forward_side: dx-only kernel on
     the critical path, the full kernel on a side stream writing weight gradients straight
-    into the flat buffer) trains bitwise like the single-launch head (HYDRA_HEADLOSS_SIDE=0)."""
+    into the flat buffer) trains like the single-launch head (HYDRA_HEADLOSS_SIDE=0).  The
+    dx-only kernel is the one-workgroup-per-row chain (csrc/mlp.hip head_dx_row_kernel), whose
+    summation order differs from the row-split kernel's, so the match is to fp32 rounding
+    (it was bitwise while both launches ran the same kernel)."""
     samples = oc20_like(48, seed=9)
     base = _model(samples).cuda()
     s = DeviceGraphStore(samples, "cuda", head_types=["graph"], head_dims=[1])
     batches = [list(range(i, i + 16)) for i in range(0, 32, 4)]
-    params, losses = [], []
+    grads, losses = [], []
     for side in ("0", "1"):
         monkeypatch.setenv("HYDRA_HEADLOSS_SIDE", side)
         m = copy.deepcopy(base)
         step = TrainStep(m, mode="graph", node_bucket=2048, edge_bucket=1 << 15)
-        losses.append([float(step(s, b)[0]) for b in batches])
+        ls = [float(step(s, batches[0])[0])]
         torch.cuda.synchronize()
-        params.append([p.detach().clone() for p in m.parameters()])
-    assert losses[0] == losses[1], losses
-    for a, b in zip(*params):
-        assert torch.equal(a, b)
+        # the first step's gradients (AdamW amplifies rounding of near-zero gradient entries
+        # into parameter differences of order lr, so parameters are not compared)
+        grads.append([p.grad.detach().clone() for p in m.parameters() if p.grad is not None])
+        ls += [float(step(s, b)[0]) for b in batches[1:]]
+        losses.append(ls)
+    torch.testing.assert_close(torch.tensor(losses[0]), torch.tensor(losses[1]), rtol=1e-4, atol=1e-6)
+    assert len(grads[0]) == len(grads[1]) > 0
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
