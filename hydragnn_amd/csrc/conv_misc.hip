@@ -313,6 +313,65 @@ std::tuple<at::Tensor, at::Tensor> edge_gather_act_bwd(const at::Tensor& g_, con
 }
 
 
+// Between-layer ReLU of a padded batch with its padding rows zeroed (models/base.py encode:
+// act -> _zero_rows), one launch each way instead of relu + where (+ their backward pair).
+// keep: bool [N] (row kept) or null.  Backward needs only y: dx = (y > 0) g (masked rows
+// have y = 0, so they get no gradient).
+__global__ void __launch_bounds__(256) relu_rowmask_fwd_kernel(const float4* __restrict__ x,
+                                                               const bool* __restrict__ keep, int64_t n4, int F4,
+                                                               float4* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const bool k = keep == nullptr || keep[i / F4];
+  const float4 v = x[i];
+  y[i] = k ? make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f))
+           : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void __launch_bounds__(256) relu_rowmask_bwd_kernel(const float4* __restrict__ g,
+                                                               const float4* __restrict__ y, int64_t n4,
+                                                               float4* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4 gv = g[i], yv = y[i];
+  dx[i] = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f, yv.z > 0.f ? gv.z : 0.f,
+                      yv.w > 0.f ? gv.w : 0.f);
+}
+
+at::Tensor relu_rowmask_fwd(const at::Tensor& x_, const c10::optional<at::Tensor>& keep) {
+  HY_CHECK_CUDA(x_);
+  auto x = x_.contiguous();
+  HY_CHECK_F32(x);
+  HY_CHECK(x.dim() == 2 && x.size(1) % 4 == 0, "relu_rowmask: x [N, F], F % 4 == 0");
+  const bool* kp = nullptr;
+  if (keep.has_value() && keep->defined()) {
+    HY_CHECK(keep->is_cuda() && keep->scalar_type() == at::kBool && keep->is_contiguous() &&
+                 keep->numel() == x.size(0),
+             "relu_rowmask: keep bool [N]");
+    kp = keep->data_ptr<bool>();
+  }
+  auto y = at::empty_like(x);
+  const int64_t n4 = x.numel() / 4;
+  if (n4 > 0)
+    relu_rowmask_fwd_kernel<<<ceil_div(n4, 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(x.data_ptr<float>()), kp, n4, (int)(x.size(1) / 4),
+        reinterpret_cast<float4*>(y.data_ptr<float>()));
+  return y;
+}
+
+at::Tensor relu_rowmask_bwd(const at::Tensor& g_, const at::Tensor& y) {
+  auto g = g_.contiguous();
+  HY_CHECK(g.sizes() == y.sizes() && y.is_contiguous() && g.scalar_type() == at::kFloat, "relu_rowmask_bwd: shapes");
+  auto dx = at::empty_like(y);
+  const int64_t n4 = y.numel() / 4;
+  if (n4 > 0)
+    relu_rowmask_bwd_kernel<<<ceil_div(n4, 256), 256, 0, stream()>>>(
+        reinterpret_cast<const float4*>(g.data_ptr<float>()), reinterpret_cast<const float4*>(y.data_ptr<float>()),
+        n4, reinterpret_cast<float4*>(dx.data_ptr<float>()));
+  return dx;
+}
+
+
 // MACE radial FCN first layer with its concat input split at node level (reference
 // mace_utils/modules/blocks.py:354-387, conv_tp_weights over cat[edge_feats, down[src],
 // down[dst]]): z = A[src] + B[dst] + et with ab = down @ [W_src | W_dst] ([N, 2H], one node
@@ -498,6 +557,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("scaled_silu_fwd(Tensor x, float s) -> Tensor");
   m.def("scaled_silu_bwd(Tensor g, Tensor x, float s) -> Tensor");
   m.def("edge_gather_silu_fwd(Tensor ab, Tensor src, Tensor dst, Tensor? et, float s) -> Tensor");
+  m.def("relu_rowmask_fwd(Tensor x, Tensor? keep) -> Tensor");
+  m.def("relu_rowmask_bwd(Tensor g, Tensor y) -> Tensor");
   m.def("edge_gather_silu_bwd(Tensor g, Tensor ab, Tensor src, Tensor dst, Tensor? et, float s) -> Tensor");
   m.def(
       "edge_gather_act_fwd(Tensor ab, Tensor src, Tensor dst, Tensor r, Tensor w, Tensor b, Tensor? et, int act) -> "
@@ -516,6 +577,8 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("scaled_silu_bwd", hy::scaled_silu_bwd);
   m.impl("edge_gather_act_fwd", hy::edge_gather_act_fwd);
   m.impl("edge_gather_silu_fwd", hy::edge_gather_silu_fwd);
+  m.impl("relu_rowmask_fwd", hy::relu_rowmask_fwd);
+  m.impl("relu_rowmask_bwd", hy::relu_rowmask_bwd);
   m.impl("edge_gather_silu_bwd", hy::edge_gather_silu_bwd);
   m.impl("edge_gather_act_bwd", hy::edge_gather_act_bwd);
   m.impl("cg_gate_fwd", hy::cg_gate_fwd);

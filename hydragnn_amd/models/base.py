@@ -311,9 +311,7 @@ class Base(nn.Module):
                 inv = norm_add(inv, bn, ctx.get("num_valid"), relu=True, zero_pad=keep is not None)
                 continue
             h = bn(inv, ctx.get("num_valid")) if isinstance(bn, BatchNorm) else bn(inv)
-            inv = self.activation_function(h)
-            if keep is not None:
-                inv = _zero_rows(inv, keep)
+            inv = _act_zero_rows(self.activation_function, h, keep)
         return inv, equiv, ctx
 
     def _fused_encode(self, inv, equiv, ctx):
@@ -682,6 +680,36 @@ class Base(nn.Module):
 
     def __str__(self):
         return "Base"
+
+
+class _ReluRowMask(torch.autograd.Function):
+    """relu(x) with the padding rows zeroed, one HIP launch each way (csrc/conv_misc.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, keep):
+        from .. import _native
+
+        y = _native.ops().relu_rowmask_fwd(x, keep)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        (y,) = ctx.saved_tensors
+        return _native.ops().relu_rowmask_bwd(g, y), None
+
+
+def _act_zero_rows(act, h, keep):
+    """``_zero_rows(act(h), keep)``: one fused launch each way for ReLU on GPU fp32 rows."""
+    from ..ops.pna import fused
+
+    if (isinstance(act, torch.nn.ReLU) and h.is_cuda and h.dtype == torch.float32 and h.dim() == 2 and
+            h.shape[1] % 4 == 0 and (keep is None or keep.dtype == torch.bool) and fused("norm")):
+        return _ReluRowMask.apply(h, None if keep is None else keep.contiguous())
+    out = act(h)
+    return _zero_rows(out, keep) if keep is not None else out
 
 
 def _zero_rows(t, keep):

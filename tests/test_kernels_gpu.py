@@ -628,3 +628,22 @@ def test_gather_mul_sum_slack_limit():
         torch.cuda.synchronize()
         times[slack] = (time.perf_counter() - t) / 50
     assert times[400_000] < 2.0 * times[0] + 20e-6, times
+
+
+def test_relu_rowmask_matches_torch():
+    """Between-layer ReLU + padding-row zeroing in one launch each way (models/base.py
+    _act_zero_rows, csrc/conv_misc.hip relu_rowmask) == relu then torch.where."""
+    from hydragnn_amd.models.base import _act_zero_rows, _zero_rows
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(301, 64, generator=g).cuda().requires_grad_(True)
+    keep = (torch.rand(301, generator=g) > 0.2).cuda()
+    y = _act_zero_rows(torch.nn.ReLU(), x, keep)
+    assert "ReluRowMask" in type(y.grad_fn).__name__
+    xr = x.detach().clone().requires_grad_(True)
+    yr = _zero_rows(torch.relu(xr), keep)
+    torch.testing.assert_close(y, yr, rtol=0, atol=0)
+    go = torch.randn(301, 64, generator=g).cuda()
+    y.backward(go)
+    yr.backward(go)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=0, atol=0)
