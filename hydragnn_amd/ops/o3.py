@@ -435,8 +435,15 @@ class _TallMM(torch.autograd.Function):
     def backward(ctx, g):
         from .. import _native
 
+        from . import linear as _lin
+
         x, W = ctx.saved_tensors
         dx = g @ W.t() if ctx.needs_input_grad[0] else None
+        if ctx.needs_input_grad[1] and _lin._can_defer(W, None):
+            # the step's grouped weight-gradient flush: dy^T x with the roles swapped is
+            # x^T g = dW in the e3nn [in, out] layout (a full-width "column block" of W)
+            _lin._record((x, g.contiguous(), W, None))
+            return dx, None
         dW = _native.ops().linear_wgrad(x, g.contiguous(), False)[0] if ctx.needs_input_grad[1] else None
         return dx, dW
 
