@@ -23,7 +23,7 @@ from .. import _native
 class SegIndex:
     """Row -> segment mapping with a CSR view (all index tensors int32)."""
 
-    __slots__ = ("index", "rowptr", "perm", "num_segments", "limit", "_deg", "_index64", "_onehot_t")
+    __slots__ = ("index", "rowptr", "perm", "num_segments", "limit", "_deg", "_index64", "_onehot_t", "_invdeg")
 
     def __init__(self, index, rowptr, perm, num_segments, limit=None):
         self.index = index
@@ -35,6 +35,7 @@ class SegIndex:
         # tail owned by one segment is not summed serially (static in-forward radius graph)
         self.limit = limit
         self._deg = None
+        self._invdeg = None
         self._index64 = None
         self._onehot_t = None
 
@@ -62,6 +63,14 @@ class SegIndex:
         if self._deg is None:
             self._deg = (self.rowptr[1:] - self.rowptr[:-1]).to(dtype)
         return self._deg
+
+    def inv_degree(self, dtype=torch.float32):
+        """1 / max(degree, 1) per segment (cached with the index)."""
+        d = getattr(self, "_invdeg", None)
+        if d is None or d.dtype != dtype:
+            d = 1.0 / self.degree(dtype).clamp(min=1.0)
+            self._invdeg = d
+        return d
 
     def to(self, device):
         p = None if self.perm is None else self.perm.to(device, non_blocking=True)
@@ -277,7 +286,31 @@ def segment_sum(x, si, limit=None):
     return _SegSum.apply(x, si, limit)
 
 
+class _SegMean(torch.autograd.Function):
+    """Native segment mean: the division rides in the segment-sum kernel (one launch instead
+    of sum + clamp + divide); backward = gather of g / degree."""
+
+    @staticmethod
+    def forward(ctx, x, si, limit):
+        ctx.si = si
+        tail = x.shape[1:]
+        lim = limit if limit is not None else si.limit
+        if lim is not None and not (lim.dtype == torch.int32 and (si.perm is None or si.limit is lim)):
+            lim = None
+        out = _native.ops().seg_sum(x.reshape(x.shape[0], _width(tail)), si.rowptr, si.perm, si.num_segments, True,
+                                    lim)
+        return out.view((si.num_segments,) + tuple(tail))
+
+    @staticmethod
+    def backward(ctx, g):
+        si = ctx.si
+        inv = si.inv_degree(g.dtype)
+        return _Gather.apply(g * inv.view(-1, *([1] * (g.dim() - 1))), si), None, None
+
+
 def segment_mean(x, si, limit=None):
+    if _use_native(x) and x.dtype == torch.float32 and x.dim() >= 1 and x.shape[0] > 0:
+        return _SegMean.apply(x, si, limit)
     s = _SegSum.apply(x, si, limit)
     deg = si.degree(s.dtype).clamp(min=1.0).to(s.device)
     return s / deg.view(-1, *([1] * (s.dim() - 1)))

@@ -647,3 +647,37 @@ def test_relu_rowmask_matches_torch():
     y.backward(go)
     yr.backward(go)
     torch.testing.assert_close(x.grad, xr.grad, rtol=0, atol=0)
+
+
+def test_segment_mean_native_matches_cpu_with_limit_and_grad():
+    """segment_mean on the GPU (division fused into the segment-sum kernel, ops/segment.py
+    _SegMean) == the CPU composite, with a padded tail skipped by the limit, values and the
+    input gradient (also to second order, as force training differentiates it twice)."""
+    from hydragnn_amd.ops import segment as seg
+
+    g = torch.Generator().manual_seed(11)
+    N, S = 500, 37
+    idx = torch.sort(torch.randint(0, S - 1, (N,), generator=g)).values
+    idx[-40:] = S - 1  # the padding segment
+    x = torch.randn(N, 24, generator=g, dtype=torch.float64)
+    x[-40:] = 0.0
+    lim = torch.tensor([N - 40], dtype=torch.int32)
+    si_c = seg.SegIndex.from_index(idx.int(), S, sorted_=True)
+    xc = x.clone().requires_grad_(True)
+    ref = seg.segment_mean(xc, si_c)
+    go = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (gr,) = torch.autograd.grad((ref * go).sum(), xc, create_graph=True)
+    dev = torch.device("cuda")
+    si_d = seg.SegIndex.from_index(idx.int().to(dev), S, sorted_=True)
+    xd = x.float().to(dev).requires_grad_(True)
+    out = seg.segment_mean(xd, si_d, limit=lim.to(dev))
+    assert "SegMean" in type(out.grad_fn).__name__
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    (gd,) = torch.autograd.grad((out * go.float().to(dev)).sum(), xd, create_graph=True)
+    torch.testing.assert_close(gd.double().cpu()[:-40], gr.detach()[:-40], rtol=1e-5, atol=1e-6)
+    # the mean is linear: its gradient does not depend on x (no second-order term), and the
+    # create_graph backward must not fail (force training differentiates through it twice)
+    if gd.requires_grad:
+        h = torch.randn(gd.shape, generator=g)
+        (ggd,) = torch.autograd.grad((gd * h.to(dev)).sum(), xd, allow_unused=True)
+        assert ggd is None or torch.all(ggd == 0)
