@@ -218,6 +218,20 @@ class EquivariantProductBasisBlock(nn.Module):
         return out + sc if (self.use_sc and sc is not None) else out
 
 
+def _joined(inv, equiv):
+    """``cat([inv, equiv], 1)`` — or, when the two are the adjacent column blocks of one
+    [N, F] tensor (the previous layer's output, split for the read-out), that tensor itself:
+    no copy forward, no split / concat pair backward (autograd sums the read-out's gradient
+    of the ``inv`` view and this layer's gradient of the whole)."""
+    b = inv._base
+    if (b is not None and equiv._base is b and b.dim() == 2 and inv.dim() == 2 and equiv.dim() == 2 and
+            b.is_contiguous() and inv.storage_offset() == b.storage_offset() and
+            inv.shape[1] + equiv.shape[1] == b.shape[1] and equiv.storage_offset() == b.storage_offset() + inv.shape[1]
+            and inv.shape[0] == b.shape[0] == equiv.shape[0]):
+        return b
+    return torch.cat([inv, equiv], 1)
+
+
 class MACELayer(nn.Module):
     def __init__(self, inter, prod, sizing, n_scalars_out):
         super().__init__()
@@ -225,7 +239,7 @@ class MACELayer(nn.Module):
         self.n_scalars_out = n_scalars_out
 
     def forward(self, inv, equiv, ctx):
-        h = torch.cat([inv, equiv], 1)
+        h = _joined(inv, equiv)
         m, sc = self.inter(h, ctx.edge_attributes, ctx.edge_features, ctx.dst_si, ctx.src_si)
         h = self.sizing(self.prod(m, sc, ctx.elem))
         # one split (backward: one concat) instead of two slices (a zero-fill + copy each)

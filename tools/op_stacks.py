@@ -19,24 +19,27 @@ from hydragnn_amd.train.step import TrainStep  # noqa: E402
 
 def main():
     name = sys.argv[1]
-    ops = sys.argv[2:] or ["aten::copy_", "aten::fill_", "aten::mul", "aten::add_", "aten::cat", "aten::mm",
-                           "aten::sum", "aten::div", "aten::clone", "aten::zeros"]
+    ops = sys.argv[2:] or ["aten::copy_", "aten::fill_", "aten::mul", "aten::add_", "aten::add", "aten::cat",
+                           "aten::mm", "aten::sum", "aten::div", "aten::clone", "aten::zeros", "aten::zero_",
+                           "aten::index_add_", "aten::gather", "aten::where"]
     dev = torch.device("cuda:0")
     model, samples, B, ht, hd, forces = bc.CONFIGS[name](dev)
     model = model.to(dev)
     if not forces:
         samples = bc._targets_for_store(samples, ht)
     store = DeviceGraphStore(samples, dev, head_types=None if forces else ht, head_dims=None if forces else hd)
-    ts = TrainStep(model, lr=1e-3, mode="eager", compute_grad_energy=forces)
+    padded = os.environ.get("OP_STACKS_PADDED", "1") == "1"  # the captured step's computation
+    ts = TrainStep(model, lr=1e-3, mode="graph" if padded else "eager", compute_grad_energy=forces)
+    run = ts.padded_step if padded else ts
     rng = np.random.default_rng(0)
     draw = lambda: list(rng.choice(len(store), size=B, replace=False))  # noqa: E731
     for _ in range(3):
-        ts(store, draw())
+        run(store, draw())
     torch.cuda.synchronize()
     steps = 2
     with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         for _ in range(steps):
-            ts(store, draw())
+            run(store, draw())
         torch.cuda.synchronize()
     c = collections.Counter()
     for e in prof.events():
