@@ -738,6 +738,232 @@ __global__ void __launch_bounds__(kRsThreads) rs_small_kernel(
 #undef RS_STAMP
 }
 
+// The same graph with ONE WORKGROUP PER GRAPH (two launches): the single-workgroup builder
+// walks every receiver of the batch on one CU (~30 us at QM9 batch 64); edges never leave
+// their graph, so graph g's edges are one contiguous id range [E0_g, E0_g + tot_g) in both
+// CSR views (its receivers' rows, and its sources' rows: every edge's source is in the same
+// graph), with E0_g = sum of the earlier graphs' totals.
+//   pass 1 (per graph): receiver counts (first `cap` sources within r, index order) and the
+//     source counts of the graph's edges -> cnt[N], scnt[N], tot[G];
+//   pass 2 (per graph): E0_g from tot, local scans -> drp / srp rows, the receiver rows
+//     (src, dst) and the stable source permutation (source s walks the graph's receivers in
+//     ascending order and finds itself in each row, as the one-workgroup builder); the last
+//     graph's workgroup also lays out the padding slots [total, Ecap) (source / receiver
+//     `dummy`, after dummy's real edges in the source view).
+// Output identical to rs_small_kernel / the CPU twin.
+constexpr int kRgThreads = 256;
+constexpr int kRgMaxEdges = 8192;  // a graph's edge list held in LDS (n_g * cap)
+
+__device__ __forceinline__ int rg_scan(int* a, int n, int* part) {
+  // exclusive scan of a[0, n) in LDS (n <= a few thousand), returns the total
+  const int t = threadIdx.x;
+  const int per = (n + kRgThreads - 1) / kRgThreads;
+  const int b = min(n, t * per), e = min(n, b + per);
+  int s = 0;
+  for (int i = b; i < e; ++i) s += a[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < kRgThreads; o <<= 1) {
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int i = b; i < e; ++i) {
+    const int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  const int total = part[kRgThreads - 1];
+  __syncthreads();
+  return total;
+}
+
+__device__ __forceinline__ bool rg_near(const float* __restrict__ pos, int i, int j, float r2) {
+  const float dx = pos[3 * j] - pos[3 * i], dy = pos[3 * j + 1] - pos[3 * i + 1], dz = pos[3 * j + 2] - pos[3 * i + 2];
+  return dx * dx + dy * dy + dz * dz <= r2;
+}
+
+__global__ void __launch_bounds__(kRgThreads) rg_count_kernel(const float* __restrict__ pos,
+                                                              const int64_t* __restrict__ gptr,
+                                                              const bool* __restrict__ mask, float r2, int cap,
+                                                              int max_nodes, int* __restrict__ cnt,
+                                                              int* __restrict__ scnt, int* __restrict__ tot,
+                                                              int* __restrict__ err) {
+  __shared__ int part[kRgThreads];
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int p0 = (int)gptr[g], p1 = (int)gptr[g + 1];
+  // a graph above the dataset's node bound (its edge list would not fit the fill kernel's
+  // LDS) gets no edges and raises the device flag (ops/devcheck.py); the padding graph has
+  // no valid node, so no edges either, whatever its size
+  const bool over = p1 - p0 > max_nodes;
+  for (int i = p0 + t; i < p1; i += kRgThreads) scnt[i] = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int i = p0 + t; i < p1; i += kRgThreads) {
+    int c = 0;
+    if (over) {
+      if (mask == nullptr || mask[i]) atomicMax(err, p1 - p0);
+    } else if (mask == nullptr || mask[i]) {
+      for (int j = p0; j < p1 && c < cap; ++j) {
+        if (j == i || (mask != nullptr && !mask[j])) continue;
+        if (rg_near(pos, i, j, r2)) {
+          ++c;
+          atomicAdd(&scnt[j], 1);  // order-free count (device atomics on the graph's own rows)
+        }
+      }
+    }
+    cnt[i] = c;
+    mine += c;
+  }
+  part[t] = mine;
+  __syncthreads();
+  for (int o = kRgThreads / 2; o > 0; o >>= 1) {
+    if (t < o) part[t] += part[t + o];
+    __syncthreads();
+  }
+  if (t == 0) tot[g] = part[0];
+}
+
+__global__ void __launch_bounds__(kRgThreads) rg_fill_kernel(
+    const float* __restrict__ pos, const int64_t* __restrict__ gptr, const bool* __restrict__ mask, int N, int G,
+    float r2, int cap, int Ecap, int dummy, const int* __restrict__ cnt, const int* __restrict__ scnt,
+    const int* __restrict__ tot, int* __restrict__ src_o, int* __restrict__ dst_o, int* __restrict__ drp_o,
+    int* __restrict__ limit_o, int* __restrict__ srp_o, int* __restrict__ sperm_o) {
+  extern __shared__ int lds[];
+  __shared__ int part[kRgThreads];
+  __shared__ int s_e0, s_total;
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int p0 = (int)gptr[g], p1 = (int)gptr[g + 1], n = p1 - p0;
+  int* rp = lds;             // [n + 1] local receiver row starts
+  int* sp = rp + n + 1;      // [n + 1] local source row starts
+  int* lsrc = sp + n + 1;    // [n * cap] the graph's edges (local ids, receiver order)
+  // E0_g and the batch total from the per-graph totals
+  {
+    int a = 0, b = 0;
+    for (int k = t; k < G; k += kRgThreads) {
+      const int v = tot[k];
+      b += v;
+      if (k < g) a += v;
+    }
+    part[t] = a;
+    __syncthreads();
+    for (int o = kRgThreads / 2; o > 0; o >>= 1) {
+      if (t < o) part[t] += part[t + o];
+      __syncthreads();
+    }
+    if (t == 0) s_e0 = part[0];
+    __syncthreads();
+    part[t] = b;
+    __syncthreads();
+    for (int o = kRgThreads / 2; o > 0; o >>= 1) {
+      if (t < o) part[t] += part[t + o];
+      __syncthreads();
+    }
+    if (t == 0) s_total = part[0];
+    __syncthreads();
+  }
+  const int E0 = s_e0, total = s_total;
+  if (tot[g] == 0) {  // no edges (the padding graph): empty rows, no LDS use
+    for (int i = t; i < n; i += kRgThreads) {
+      drp_o[p0 + i] = E0;
+      srp_o[p0 + i] = E0;
+    }
+  } else {
+  for (int i = t; i < n; i += kRgThreads) {
+    rp[i] = cnt[p0 + i];
+    sp[i] = scnt[p0 + i];
+  }
+  __syncthreads();
+  const int tg = rg_scan(rp, n, part);
+  rg_scan(sp, n, part);
+  if (t == 0) {
+    rp[n] = tg;
+    sp[n] = tg;
+  }
+  __syncthreads();
+  // receiver rows
+  for (int i = t; i < n; i += kRgThreads) {
+    const int gi = p0 + i;
+    drp_o[gi] = E0 + rp[i];
+    int q = rp[i];
+    const int q1 = rp[i + 1];
+    if (mask == nullptr || mask[gi]) {
+      for (int j = p0; j < p1 && q < q1; ++j) {
+        if (j == gi || (mask != nullptr && !mask[j])) continue;
+        if (rg_near(pos, gi, j, r2)) {
+          lsrc[q] = j - p0;
+          src_o[E0 + q] = j;
+          dst_o[E0 + q] = gi;
+          ++q;
+        }
+      }
+    }
+    srp_o[gi] = E0 + sp[i];
+  }
+  __syncthreads();
+  // stable source permutation: source s walks the receivers in ascending order
+  for (int s = t; s < n; s += kRgThreads) {
+    int k = sp[s];
+    for (int i = 0; i < n; ++i) {
+      for (int q = rp[i]; q < rp[i + 1]; ++q) {
+        const int v = lsrc[q];
+        if (v >= s) {
+          if (v == s) sperm_o[E0 + k++] = E0 + q;
+          break;
+        }
+      }
+    }
+  }
+  }
+  if (g == G - 1) {  // the padding slots, owned by `dummy` (the last node, in the last graph)
+    for (int e = total + t; e < Ecap; e += kRgThreads) {
+      src_o[e] = dummy;
+      dst_o[e] = dummy;
+      sperm_o[e] = e;
+    }
+    if (t == 0) {
+      drp_o[N] = Ecap;
+      srp_o[N] = Ecap;
+      limit_o[0] = total;
+    }
+  }
+}
+
+// per-graph builder: -> (src, dst, drp, limit, srp, sperm), or an empty list when a graph's
+// edge list cannot be held in LDS (the caller then uses the one-workgroup builder)
+std::vector<at::Tensor> radius_static_graphs(const at::Tensor& pos_, const at::Tensor& gptr,
+                                             const c10::optional<at::Tensor>& mask, double r, int64_t cap,
+                                             int64_t Ecap, int64_t dummy, int64_t max_nodes,
+                                             const at::Tensor& err) {
+  HY_CHECK_CUDA(pos_);
+  auto pos = pos_.to(at::kFloat).contiguous();
+  HY_CHECK(gptr.scalar_type() == at::kLong && gptr.is_contiguous() && gptr.is_cuda(), "radius_static_graphs: int64 ptr");
+  const int64_t N = pos.size(0), G = gptr.numel() - 1;
+  if (mask.has_value()) HY_CHECK(mask->scalar_type() == at::kBool && mask->numel() == N, "radius_static: mask [N] bool");
+  HY_CHECK(N > 0 && G >= 1 && dummy == N - 1 && Ecap >= N * cap, "radius_static_graphs: sizes (dummy = last node)");
+  HY_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1 && err.is_cuda(), "radius_static_graphs: int32 flag");
+  // edges of one graph: at most n * min(cap, n - 1); n <= max_nodes for every real graph
+  const int64_t per = std::min<int64_t>(cap, std::max<int64_t>(max_nodes - 1, 0));
+  if (max_nodes <= 0 || max_nodes * per > kRgMaxEdges) return {};
+  const size_t lds = sizeof(int) * (size_t)(2 * (max_nodes + 1) + max_nodes * per);
+  auto io = pos.options().dtype(at::kInt);
+  auto src = at::empty({Ecap}, io), dst = at::empty({Ecap}, io), drp = at::empty({N + 1}, io),
+       limit = at::empty({1}, io), srp = at::empty({N + 1}, io), sperm = at::empty({Ecap}, io);
+  auto cnt = at::empty({N}, io), scnt = at::empty({N}, io), tot = at::empty({G}, io);
+  const bool* mp = mask.has_value() ? mask->data_ptr<bool>() : nullptr;
+  rg_count_kernel<<<(int)G, kRgThreads, 0, stream()>>>(pos.data_ptr<float>(), gptr.data_ptr<int64_t>(), mp,
+                                                       (float)(r * r), (int)cap, (int)max_nodes,
+                                                       cnt.data_ptr<int>(), scnt.data_ptr<int>(), tot.data_ptr<int>(),
+                                                       err.data_ptr<int>());
+  rg_fill_kernel<<<(int)G, kRgThreads, lds, stream()>>>(
+      pos.data_ptr<float>(), gptr.data_ptr<int64_t>(), mp, (int)N, (int)G, (float)(r * r), (int)cap, (int)Ecap,
+      (int)dummy, cnt.data_ptr<int>(), scnt.data_ptr<int>(), tot.data_ptr<int>(), src.data_ptr<int>(),
+      dst.data_ptr<int>(), drp.data_ptr<int>(), limit.data_ptr<int>(), srp.data_ptr<int>(), sperm.data_ptr<int>());
+  return {src, dst, drp, limit, srp, sperm};
+}
+
 // -> (src, dst, drp, limit, srp, sperm), or an empty list when the batch is too large for
 // one workgroup's LDS (the caller then uses the multi-launch builder)
 std::vector<at::Tensor> radius_static_small(const at::Tensor& pos_, const at::Tensor& node_graph,
@@ -942,6 +1168,8 @@ std::tuple<at::Tensor, at::Tensor> triplets_static_kj(const at::Tensor& src, con
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("radius_static_graphs(Tensor pos, Tensor gptr, Tensor? mask, float r, int cap, int Ecap, int dummy, "
+        "int max_nodes, Tensor err) -> Tensor[]");
   m.def(
       "radius_static_small(Tensor pos, Tensor node_graph, Tensor gptr, Tensor? mask, float r, int cap, int Ecap, "
       "int dummy, Tensor? dbg=None) -> Tensor[]");
@@ -969,6 +1197,7 @@ TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
   m.impl("triplets_static_count", hy::triplets_static_count);
   m.impl("triplets_static_kj", hy::triplets_static_kj);
   m.impl("radius_static_small", hy::radius_static_small);
+  m.impl("radius_static_graphs", hy::radius_static_graphs);
   m.impl("triplets_static_fill", hy::triplets_static_fill);
   m.impl("radius_static_count", hy::radius_static_count);
   m.impl("radius_static_fill", hy::radius_static_fill);

@@ -70,6 +70,7 @@ class DeviceGraphStore:
         nn_ = np.array([s.num_nodes for s in samples], dtype=np.int64)
         ne = np.array([s.num_edges for s in samples], dtype=np.int64)
         self.n_nodes, self.n_edges = nn_, ne
+        self.max_graph_nodes = int(nn_.max()) if S else 0  # static bound for per-graph kernels
         self.node_off = np.zeros(S + 1, dtype=np.int64)
         self.node_off[1:] = np.cumsum(nn_)
         self.edge_off = np.zeros(S + 1, dtype=np.int64)
@@ -405,6 +406,7 @@ class DeviceGraphStore:
             s["targets"] = targets
             if lay.padded:
                 s["num_valid"] = scal[0]
+                s["max_graph_nodes"] = self.max_graph_nodes
                 s["graph_mask"] = gmask
                 s["node_mask"] = nmask
                 s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand
@@ -481,6 +483,7 @@ class DeviceGraphStore:
         s["targets"] = targets
         if lay.padded:
             s["num_valid"] = nvalid
+            s["max_graph_nodes"] = self.max_graph_nodes
             s["graph_mask"] = gmask
             s["node_mask"] = nmask.view(-1)
             s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand

@@ -334,8 +334,9 @@ class Base(nn.Module):
         return [int(i) for i in torch.unique(dn).tolist()]
 
     def branch_names(self):
-        return sorted((k for k in self.graph_shared.keys()), key=lambda k: int(k.split("-")[1])) \
-            if len(self.graph_shared) else [f"branch-{i}" for i in range(self.num_branches)]
+        gs = self._modules.get("graph_shared")
+        return sorted((k for k in gs.keys()), key=lambda k: int(k.split("-")[1])) \
+            if gs is not None and len(gs) else [f"branch-{i}" for i in range(self.num_branches)]
 
     def branch_param_groups(self):
         """Per-branch decoder parameters (graph shared MLP + every head's branch module), in
@@ -379,7 +380,6 @@ class Base(nn.Module):
         padding rows (dataset id -1) get zeros."""
         data = ctx.data
         dn = data.dataset_name.view(-1)
-        self._note_branch_presence(dn)
         dn_node = dn.index_select(0, data.batch)
         outputs, outputs_var = [], []
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
@@ -446,16 +446,25 @@ class Base(nn.Module):
             x_graph = seg.segment_mean(x, gsi, limit=data.get("num_valid"))
         outputs, outputs_var = [], []
         nb = self.num_branches
+        if nb > 1 and data.get("dataset_name") is not None:
+            # per-branch usage flags of the captured step (also written by eager steps of a
+            # graph-mode TrainStep: mixed batches of a branch-keyed one step eagerly)
+            self._note_branch_presence(data.dataset_name.view(-1))
         if nb > 1 and data.get("branch_graph_ranges") is not None:
             return self._decode_ranges(x, x_graph, equiv, ctx)
         ids = self._branch_ids(data) if nb > 1 else [0]
         if ids is None:
             return self._decode_dense(x, x_graph, equiv, ctx)
         G = x_graph.shape[0]
+        # one branch in the batch (every batch of an SC25 rank, which loads one dataset; the
+        # branch-keyed captured step): its heads on all rows, no masks (padding rows are
+        # masked out of the loss)
+        single = nb == 1 or len(ids) == 1
+        b0 = "branch-0" if nb == 1 else f"branch-{ids[0]}"
         for head_dim, headloc, t in zip(self.head_dims, self.heads_NN, self.head_type):
             if t == "graph":
-                if nb == 1:
-                    out = sequential_chain(x_graph, self.graph_shared["branch-0"], headloc["branch-0"])
+                if single:
+                    out = sequential_chain(x_graph, self.graph_shared[b0], headloc[b0])
                     head, headvar = out[:, :head_dim], out[:, head_dim:] ** 2
                 else:
                     dn = data.dataset_name.view(-1)
@@ -469,8 +478,8 @@ class Base(nn.Module):
                         headvar = headvar.index_put((mask,), out[:, head_dim:] ** 2)
             else:
                 nt = self.config_heads["node"][0]["architecture"]["type"]
-                if nb == 1:
-                    x_node = self._node_head(headloc["branch-0"], nt, x, equiv, ctx, data.get("batch"))
+                if single:
+                    x_node = self._node_head(headloc[b0], nt, x, equiv, ctx, data.get("batch"))
                     head, headvar = x_node[:, :head_dim], x_node[:, head_dim:] ** 2
                 else:
                     dn = data.dataset_name.view(-1)

@@ -580,9 +580,24 @@ class MACEStack(Base):
 
 
     def branch_param_groups(self):
-        """No per-branch usage groups: the multi-branch read-outs are STACKED (one weight
-        tensor holds every branch, ``_decode_stacked``), so a parameter is always used."""
-        return []
+        """Per-branch read-out parameters of every layer's decoder (graph shared MLP + each
+        head's branch module), in branch id order: the usage groups of the captured step, so a
+        branch absent from a batch keeps torch's skip-if-no-grad semantics (its heads get a
+        zero gradient from the dense / branch-keyed decode, and FusedAdamW skips them)."""
+        if self.num_branches <= 1:
+            return []
+        names = sorted(self.multihead_decoders[0].heads_NN[0].keys(), key=lambda k: int(k.split("-")[1]))
+        groups = []
+        for bt in names:
+            ps = []
+            for dec in self.multihead_decoders:
+                if bt in dec.graph_shared:
+                    ps += list(dec.graph_shared[bt].parameters())
+                for hn in dec.heads_NN:
+                    if bt in hn:
+                        ps += list(hn[bt].parameters())
+            groups.append([p for p in ps if p.requires_grad])
+        return groups
 
     def __init__(self, input_args, conv_args, r_max, radial_type, distance_transform, num_bessel, edge_dim, max_ell,
                  node_max_ell, avg_num_neighbors, num_polynomial_cutoff, correlation, *args, **kwargs):
@@ -699,6 +714,8 @@ class MACEStack(Base):
     def forward(self, data):
         inv, equiv, ctx = self._embedding(data)
         ids = self._branch_ids(data) if self.num_branches > 1 else [0]
+        if self.num_branches > 1 and data.get("dataset_name") is not None:
+            self._note_branch_presence(data.dataset_name.view(-1))  # captured step's usage flags
         outputs = self.multihead_decoders[0](ctx.node_attributes, ctx, ids)
         for conv, readout in zip(self.graph_convs, self.multihead_decoders[1:]):
             inv, equiv = self._run_conv(conv, inv, equiv, ctx)

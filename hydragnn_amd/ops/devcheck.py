@@ -14,6 +14,7 @@ _FLAGS = {}
 _WHAT = {
     "elem_range": "element ids outside [0, num_elements)",
     "triplet_cap": "triplets above the static capacity (largest excess)",
+    "radius_graph_size": "a graph above the store's largest graph in the radius builder (its size)",
 }
 
 

@@ -112,6 +112,19 @@ def interaction_graph_static(pos, data, r, max_num_neighbors=None):
     batch, ptr = data.batch.long(), data.ptr.long()
     dummy = N - 1
     p = pos.detach()
+    nmax = data.get("max_graph_nodes")
+    if p.is_cuda and nmax and os.environ.get("HYDRA_RS_GRAPHS", "1") == "1":
+        # one workgroup per graph, two launches (csrc/graph.hip rg_*): the dataset's largest
+        # graph (a host int the store keeps) sizes the LDS edge list, fixed for a captured
+        # bucket; a graph above it gets no edges and sets the "radius_graph_size" flag
+        from . import devcheck
+
+        out = _native.ops().radius_static_graphs(p, ptr, mask, float(r), cap, Ecap, dummy, int(nmax),
+                                                 devcheck.flag(p.device, "radius_graph_size"))
+        devcheck.debug_check("radius_graph_size", p.device)
+        if out:
+            src, dst, drp, limit, srp, sperm = out
+            return SegIndex(dst, drp, None, N, limit), SegIndex(src, srp, sperm, N, limit)
     if p.is_cuda and os.environ.get("HYDRA_RS_SMALL", "1") == "1":
         # small batches: the whole builder (both CSR views) in one workgroup, one launch
         out = _native.ops().radius_static_small(p, batch, ptr, mask, float(r), cap, Ecap, dummy)

@@ -192,6 +192,7 @@ class _Captured:
         self.dev_seed = None
         self.seeded = False
         self.lay = None
+        self.branch = None  # branch-keyed capture: the batch's single branch id
 
     # the most recently replayed graph's outputs (and graph 0 for callers that want one)
     @property
@@ -225,7 +226,15 @@ class TrainStep:
         self.mode = mode
         dev = next(self.module.parameters()).device
         self.device = dev
-        if mode == "graph" and getattr(self.module, "num_branches", 1) > 1 and not self._capture_multibranch():
+        # multi-branch models: a batch of ONE branch (every batch of an SC25 rank, which loads
+        # one dataset) is captured under a branch-keyed bucket and decodes that branch's heads
+        # only; a mixed batch replays a dense-decode capture when that pays
+        # (_capture_multibranch), else steps eagerly.  HYDRA_BRANCH_KEYED=0: no keying.
+        multi = getattr(self.module, "num_branches", 1) > 1
+        self.dense_ok = mode == "graph" and multi and self._capture_multibranch()
+        self.branch_keyed = (mode == "graph" and multi and self.taskpar is None
+                             and os.environ.get("HYDRA_BRANCH_KEYED", "1") == "1")
+        if mode == "graph" and multi and not self.dense_ok and not self.branch_keyed:
             self.mode = mode = "eager"
         if world > 1 and mode == "eager" and not isinstance(model, DistributedDataParallel) and self.taskpar is None:
             self.model = DistributedDataParallel(model)
@@ -395,19 +404,23 @@ class TrainStep:
         nb, eb = self.node_bucket, self.edge_bucket
         return (int(math.ceil((N + 2) / nb) * nb), int(math.ceil(max(E, 1) / eb) * eb))
 
-    def prepare(self, store, batch_size, samples=1024, seed=1234):
-        """Pre-compute the bucket set a random sampler will hit (capture happens lazily)."""
+    def prepare(self, store, batch_size, samples=1024, seed=1234, draw=None):
+        """Pre-compute the bucket set a random sampler will hit (capture happens lazily).
+        ``draw(rng) -> indices``: the sampler (default: uniform without replacement)."""
         self.B = batch_size
         if self.mode != "graph":
             return
         rng = np.random.default_rng(seed)
         seen = set()
         for _ in range(samples):
-            idx = rng.choice(len(store), size=min(batch_size, len(store)), replace=False)
-            seen.add(self.bucket_of(*store.sizes_of(idx)))
-        self.expected = sorted(seen)
+            idx = draw(rng) if draw is not None else rng.choice(len(store), size=min(batch_size, len(store)),
+                                                                 replace=False)
+            key = self._key(store, idx)
+            if key is not None:
+                seen.add(key)
+        self.expected = sorted(seen, key=lambda k: tuple(-1 if v is None else v for v in k))
 
-    def precapture(self, store, batch_size, max_draws=2000, seed=4321):
+    def precapture(self, store, batch_size, max_draws=2000, seed=4321, draw=None):
         """Capture every bucket ``prepare`` predicted, on real batches drawn at random,
         so no capture (hundreds of ms) lands inside a timed/training region."""
         if self.mode != "graph" or self.device.type != "cuda":
@@ -417,18 +430,38 @@ class TrainStep:
         for _ in range(max_draws):
             if not todo:
                 break
-            idx = rng.choice(len(store), size=min(batch_size, len(store)), replace=False)
-            key = self.bucket_of(*store.sizes_of(idx))
+            idx = draw(rng) if draw is not None else rng.choice(len(store), size=min(batch_size, len(store)),
+                                                                 replace=False)
+            key = self._key(store, idx)
             if key in todo and key not in self.graphs:
                 self._capture(store, idx, key)
                 todo.discard(key)
         self._frozen = bool(self.graphs)
 
-    def _pick(self, N, E):
-        want = self.bucket_of(N, E)
+    def _branch_tag(self, store, indices):
+        """Branch-keyed capture: the branch id of a single-branch batch, None for a mixed one."""
+        if not self.branch_keyed or getattr(store, "dataset_name", None) is None:
+            return None
+        dn = store.dataset_name[np.asarray(indices, dtype=np.int64)].reshape(-1)
+        b = int(dn[0])
+        return b if bool((dn == b).all()) else None
+
+    def _key(self, store, indices):
+        """Capture key of a batch: its (node, edge) bucket, plus the branch tag for a
+        branch-keyed step; None when the batch steps eagerly (mixed, no dense capture)."""
+        key = self.bucket_of(*store.sizes_of(indices))
+        if not self.branch_keyed:
+            return key
+        tag = self._branch_tag(store, indices)
+        if tag is None and not self.dense_ok:
+            return None
+        return key + (tag,)
+
+    def _pick(self, N, E, tag=()):
+        want = self.bucket_of(N, E) + tag
         if want in self.graphs:
             return want
-        cands = [k for k in self.graphs if k[0] >= N + 2 and k[1] >= E]
+        cands = [k for k in self.graphs if k[0] >= N + 2 and k[1] >= E and k[2:] == tag]
         # after precapture (or at the cap) a rare unseen bucket replays the captured bucket
         # with the least padded work that fits: extra padding costs microseconds, a capture
         # ~50 ms.  Edge rows cost ~1/avg_degree of a node row (attention, dense maps).
@@ -455,7 +488,10 @@ class TrainStep:
         from ..parallel import gradslots
 
         self._zero()
-        batch = store.assemble(cap.dev_plan, cap.lay, branch_sorted=store.dataset_name is not None)
+        # branch-keyed capture: the batch's single branch is a host constant of the graph
+        host_ids = None if getattr(cap, "branch", None) is None else [cap.branch]
+        batch = store.assemble(cap.dev_plan, cap.lay, host_ids=host_ids,
+                               branch_sorted=store.dataset_name is not None)
         # ops may write gradients straight into the flat buffer's slots (parallel/gradslots.py)
         with gradslots.use(self.sync):
             loss, tasks = self._loss(batch)
@@ -525,7 +561,8 @@ class TrainStep:
             indices = store.branch_order(indices)[0]
         snap = self._snapshot()
         cap = _Captured()
-        Np, Ep = key
+        Np, Ep = key[:2]
+        cap.branch = key[2] if len(key) > 2 else None
         cap.lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap.dev_plan = torch.empty(cap.lay.total, dtype=torch.int32, device=self.device)
         # device-side plan: the step uploads only [G, sample ids] and expands the plan in the
@@ -610,7 +647,13 @@ class TrainStep:
 
     def graph_step(self, store, indices):
         N, E = store.sizes_of(indices)
-        key = self._pick(N, E)
+        tag = ()
+        if self.branch_keyed:
+            b = self._branch_tag(store, indices)
+            if b is None and not self.dense_ok:
+                return self.eager(store, indices)  # mixed batch, dense decode does not pay
+            tag = (b,)
+        key = self._pick(N, E, tag)
         cap = self.graphs.get(key)
         if cap is None:
             cap = self._capture(store, indices, key)
@@ -688,8 +731,12 @@ class TrainStep:
         eagerly — the CPU twin of ``graph_step`` used to test the padding logic."""
         N, E = store.sizes_of(indices)
         Np, Ep = self.bucket_of(N, E)
-        lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap = _Captured()
+        if self.branch_keyed:
+            cap.branch = self._branch_tag(store, indices)
+            if cap.branch is None and not self.dense_ok:
+                return self.eager(store, indices)
+        lay = store.layout(indices, Np=Np, Ep=Ep, Gp=len(indices) + 1)
         cap.lay = lay
         cap.dev_plan = store.upload(indices, lay)
         loss, tasks = self._body_fwd_bwd(store, cap)  # same bucketed sync as graph_step

@@ -289,13 +289,15 @@ def test_cell_list_radius_graph_large_structure_linear_time():
 @pytest.mark.gpu
 @pytest.mark.parametrize("big", [False, True])
 @pytest.mark.parametrize("small_kernel", ["1", "0"])
-def test_static_radius_graph_gpu_matches_cpu_twin(big, small_kernel, monkeypatch):
+@pytest.mark.parametrize("per_graph", ["1", "0"])
+def test_static_radius_graph_gpu_matches_cpu_twin(big, small_kernel, per_graph, monkeypatch):
     """Capturable in-forward radius graph (csrc/graph.hip radius_static_*, the one-workgroup
     builder and the multi-launch one): same edges, CSR views (stable source order), limit
     and padding layout as the CPU twin, no host sync (fixed capacity)."""
     from hydragnn_amd.ops.radius import interaction_graph_static
 
     monkeypatch.setenv("HYDRA_RS_SMALL", small_kernel)
+    monkeypatch.setenv("HYDRA_RS_GRAPHS", per_graph)
     g = torch.Generator().manual_seed(3)
     sizes = [7, 12, 1, 9] if not big else [int(x) for x in torch.randint(1, 30, (120,), generator=g)]
     pos = torch.cat([torch.rand(n, 3, generator=g) * 3 for n in sizes] + [torch.zeros(3, 3)])
@@ -308,7 +310,7 @@ def test_static_radius_graph_gpu_matches_cpu_twin(big, small_kernel, monkeypatch
             return dict.get(self, k, d)
 
     def data(dev):
-        d = D(node_mask=mask.to(dev))
+        d = D(node_mask=mask.to(dev), max_graph_nodes=max(sizes))
         d.batch, d.ptr = batch.to(dev), ptr.to(dev)
         return d
 
@@ -318,3 +320,30 @@ def test_static_radius_graph_gpu_matches_cpu_twin(big, small_kernel, monkeypatch
                  (a_src.rowptr, b_src.rowptr), (a_src.perm, b_src.perm), (a_dst.limit, b_dst.limit)]:
         assert torch.equal(x, y.cpu())
     assert a_dst.index.numel() == pos.shape[0] * 4
+
+
+@pytest.mark.gpu
+def test_static_radius_graph_per_graph_size_bound_flags():
+    """A graph above the store's ``max_graph_nodes`` bound gets no edges in the per-graph
+    builder and sets the device flag that the epoch check turns into an error."""
+    from hydragnn_amd.ops import devcheck
+    from hydragnn_amd.ops.radius import interaction_graph_static
+
+    sizes = [5, 9]
+    pos = torch.rand(sum(sizes) + 2, 3) * 0.5
+    ptr = torch.tensor([0, 5, 14, 16])
+    batch = torch.cat([torch.zeros(5), torch.ones(9), torch.full((2,), 2)]).long()
+    mask = torch.cat([torch.ones(14, dtype=torch.bool), torch.zeros(2, dtype=torch.bool)])
+
+    class D(dict):
+        def get(self, k, d=None):
+            return dict.get(self, k, d)
+
+    d = D(node_mask=mask.cuda(), max_graph_nodes=6)
+    d.batch, d.ptr = batch.cuda(), ptr.cuda()
+    dst, src = interaction_graph_static(pos.cuda(), d, 2.0, 4)
+    torch.cuda.synchronize()
+    assert int(dst.limit) == 5 * 4  # graph 0 only (all its pairs within r, cap 4)
+    assert int(devcheck.flag(pos.cuda().device, "radius_graph_size")) == 9
+    with pytest.raises(RuntimeError, match="largest graph"):
+        devcheck.check_all()

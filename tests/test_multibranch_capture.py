@@ -4,8 +4,10 @@ The reference decodes a multi-dataset batch by masking graphs per branch
 (``Base.py:482-560``); the host-side branch ranges used by the eager store path change
 from batch to batch, so the captured step decodes densely instead: every branch head on
 every row, selected per row by the dataset id on the device (``Base._decode_dense``).
+A batch of ONE branch (every batch of an SC25 rank, which loads one dataset) is captured
+under a branch-keyed bucket and decodes only that branch's heads.
 Checks: padded step (the CPU twin of the captured step) == eager step, on CPU for
-EGNN / SchNet / MACE, and captured == eager on the GPU."""
+EGNN / SchNet / MACE, and captured == eager on the GPU, mixed and single-branch batches."""
 import copy
 
 import numpy as np
@@ -49,7 +51,9 @@ def _model(mt):
                         node_max_ell=1, avg_num_neighbors=5.0, correlation=2)
 
 
-def _compare(mt, dev, tol):
+def _compare(mt, dev, tol, plan=(None,) * 4):
+    """``plan``: per step, the branch id every graph of the batch comes from (an SC25 rank's
+    batches; the branch-keyed captured step), or None for a mixed batch."""
     samples = _data()
     m1 = _model(mt).to(dev)
     m2 = copy.deepcopy(m1)
@@ -58,10 +62,15 @@ def _compare(mt, dev, tol):
     cap = TrainStep(m2, lr=1e-3, mode="graph", node_bucket=64, edge_bucket=256)
     assert cap.mode == "graph"
     rng = np.random.default_rng(0)
-    for _ in range(4):
-        idx = list(rng.choice(len(samples), 6, replace=False))
+    for b in plan:
+        pool = np.arange(len(samples)) if b is None else np.arange(b, len(samples), NB)
+        idx = list(rng.choice(pool, min(6, len(pool)), replace=False))
         le, lc = float(eager(store, idx)[0]), float(cap(store, idx)[0])
         assert abs(le - lc) <= tol * max(1.0, abs(le)), (le, lc)
+    # heads of branches absent from a step kept torch's skip-if-no-grad semantics
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p1, p2, rtol=100 * tol, atol=100 * tol)
+    return cap
 
 
 @pytest.mark.parametrize("mt", ["EGNN", "SchNet", "MACE"])
@@ -69,10 +78,27 @@ def test_multibranch_padded_step_equals_eager(mt):
     _compare(mt, "cpu", 1e-4)
 
 
+SC25_PLAN = (0, 1, 0, 2, None, 1)  # single-branch batches, one mixed
+
+
+@pytest.mark.parametrize("mt", ["EGNN", "MACE"])
+@pytest.mark.parametrize("dense", ["1", "0"])
+def test_multibranch_branch_keyed_padded_step_equals_eager(mt, dense, monkeypatch):
+    """Single-branch batches decode only their branch's heads under a branch-keyed bucket;
+    a mixed batch takes the dense decode (dense=1) or an eager step (dense=0)."""
+    monkeypatch.setenv("HYDRA_MULTIBRANCH_CAPTURE", dense)
+    cap = _compare(mt, "cpu", 1e-4, SC25_PLAN)
+    assert cap.branch_keyed and cap.dense_ok == (dense == "1")
+
+
 def test_multibranch_capture_policy(monkeypatch):
     m = _model("EGNN")
-    assert TrainStep(m, mode="graph").mode == "graph"  # small model: dense capture
+    ts = TrainStep(m, mode="graph")
+    assert ts.mode == "graph" and ts.dense_ok and ts.branch_keyed  # small model: dense capture
     monkeypatch.setenv("HYDRA_MULTIBRANCH_CAPTURE", "0")
+    ts = TrainStep(m, mode="graph")
+    assert ts.mode == "graph" and not ts.dense_ok  # single-branch batches still capture
+    monkeypatch.setenv("HYDRA_BRANCH_KEYED", "0")
     assert TrainStep(m, mode="graph").mode == "eager"
 
 
@@ -80,6 +106,17 @@ def test_multibranch_capture_policy(monkeypatch):
 @pytest.mark.parametrize("mt", ["EGNN", "MACE"])
 def test_multibranch_captured_step_equals_eager_gpu(mt):
     _compare(mt, "cuda", 2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mt", ["EGNN", "MACE"])
+@pytest.mark.parametrize("dense", ["1", "0"])
+def test_multibranch_branch_keyed_captured_equals_eager_gpu(mt, dense, monkeypatch):
+    monkeypatch.setenv("HYDRA_MULTIBRANCH_CAPTURE", dense)
+    cap = _compare(mt, "cuda", 2e-3, SC25_PLAN)
+    keys = set(cap.graphs)
+    assert {k[2] for k in keys} >= {0, 1, 2}  # one capture per branch (same bucket)
+    assert (None in {k[2] for k in keys}) == (dense == "1")
 
 
 @pytest.mark.gpu

@@ -178,12 +178,25 @@ def run(name, steps, warmup, dev):
         samples = _targets_for_store(samples, ht)
     store = DeviceGraphStore(samples, dev, head_types=None if forces else ht, head_dims=None if forces else hd)
     rng = np.random.default_rng(0)
+    sampler = None
+    single = os.environ.get("BENCH_SINGLE_BRANCH") == "1" and store.dataset_name is not None
+    if single:
+        # the reference SC25 layout: each rank loads ONE dataset, so every batch holds one
+        # branch; on one GPU the steps rotate over the branches (the per-rank mean)
+        dn = store.dataset_name.reshape(-1)
+        pools = [np.flatnonzero(dn == b) for b in np.unique(dn)]
+        turn = [0]
+
+        def sampler(r):
+            p = pools[turn[0] % len(pools)]
+            turn[0] += 1
+            return list(r.choice(p, size=min(B, len(p)), replace=False))
     if forces:
         ts = TrainStep(model, lr=1e-3, mode=os.environ.get("BENCH_FORCES_MODE", "graph"), compute_grad_energy=True,
                        node_bucket=int(os.environ.get("BENCH_NODE_BUCKET", "512")),
                        edge_bucket=int(os.environ.get("BENCH_EDGE_BUCKET", "4096")))
-        ts.prepare(store, B)
-        ts.precapture(store, B)
+        ts.prepare(store, B, draw=sampler)
+        ts.precapture(store, B, draw=sampler)
 
         def step(idx):
             return ts(store, idx)[0]
@@ -193,13 +206,13 @@ def run(name, steps, warmup, dev):
         mode = os.environ.get("BENCH_MODE", "eager" if not getattr(model, "capturable", True) else "graph")
         nbk = 512 if name.startswith("multibranch") else 256
         ts = TrainStep(model, lr=1e-3, mode=mode, node_bucket=nbk, edge_bucket=8 * nbk)
-        ts.prepare(store, B)
+        ts.prepare(store, B, draw=sampler)
         if ts.mode == "graph":
-            ts.precapture(store, B)
+            ts.precapture(store, B, draw=sampler)
 
         def step(idx):
             return ts(store, idx)[0]
-    draw = lambda: list(rng.choice(len(store), size=B, replace=False))  # noqa: E731
+    draw = (lambda: sampler(rng)) if single else (lambda: list(rng.choice(len(store), size=B, replace=False)))
     for _ in range(warmup):
         step(draw())
     torch.cuda.synchronize()
@@ -236,6 +249,8 @@ def run(name, steps, warmup, dev):
         from hydragnn_amd.ops import bgemm as _bg
 
         dtype = "bf16" if _bg.stats["nt"] else "fp32 (bf16 requested; every map below the bf16 size threshold)"
+    if single:
+        name += "/single-branch-batches"
     return {"metric": "training graphs/sec (1 GPU)", "config": name, "value": round(B * steps / el, 2),
             "unit": "graphs/s", "ms_per_step": round(1000 * el / steps, 3), "batch": B, "avg_nodes": round(nodes, 1),
             "params": sum(p.numel() for p in model.parameters()), "dtype": dtype, "final_loss": float(loss),
