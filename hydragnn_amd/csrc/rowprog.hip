@@ -44,6 +44,7 @@ struct Args {
   const float* mask;  // [N] 0/1 or null
   long long* dbg;     // optional per-instruction cycle stamps of workgroup 0 (profiling)
   int nwp;            // pointers [0, nwp) are the program's weights (L2 prefetch)
+  int rb;             // rows a workgroup owns (<= kBM; the 16-row MFMA tiles run half / quarter full)
   int wlen[kMaxPtr];  // their element counts
   float* p[kMaxPtr];
 };
@@ -170,9 +171,10 @@ __device__ void ew_fast(const Args& A, const Opd& y, const Opd& a, const Opd& b,
   const bool hb = b.nc != 0, hc = c.nc != 0;
   const int ync = (OP == E_DOT3 || OP == E_NORM3) ? 1 : y.nc;
   const int ybase = kBM * y.loff + y.c0;
+  const int nlim = min(A.N, r0 + A.rb);
   for (int i = threadIdx.x >> 6; i < kBM; i += NT / 64) {
     const int row = r0 + i;
-    if (row >= A.N) break;
+    if (row >= nlim) break;
     const float m = (OP == E_MASK) ? (A.mask ? G(A.mask)[row] : 1.f) : 1.f;
     for (int cc = 0; cc < ync; ++cc)
       for (int f = lane; f < y.w; f += 64) {
@@ -218,9 +220,10 @@ __device__ void ew_slow(const Args& A, const Ins& I, int r0, lfloat* smem) {
             c = opd(A, I, 8 + 3 * kOpdInts);
   const int ync = (op == E_DOT3 || op == E_NORM3) ? 1 : y.nc;
   const int lane = threadIdx.x & 63;
+  const int nlim = min(A.N, r0 + A.rb);
   for (int i = threadIdx.x >> 6; i < kBM; i += NT / 64) {
     const int row = r0 + i;
-    if (row >= A.N) break;
+    if (row >= nlim) break;
     for (int cc = 0; cc < ync; ++cc)
       for (int f = lane; f < y.w; f += 64) {
         float r;
@@ -332,7 +335,8 @@ __device__ void run_lin(const Args& A, const Ins& I, int r0, lfloat* smem) {
   const int i = lane & 15, g = lane >> 4;
   const int ntn = (y.w + 15) >> 4, tiles = y.nc * ntn;
   const int arow = r0 + i;
-  const bool rok = arow < A.N;
+  const int nlim = min(A.N, r0 + A.rb);
+  const bool rok = arow < nlim;
   for (int tile = wv; tile < tiles; tile += nw) {
     const int c = tile / ntn, n0 = (tile % ntn) * 16, n = n0 + i;
     const bool nok = n < y.w;
@@ -394,7 +398,7 @@ __device__ void run_lin(const Args& A, const Ins& I, int r0, lfloat* smem) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int il = 4 * g + r, row = r0 + il;
-        if (row < A.N) wr(smem, y, il, row, c, n, s[r] + bb, acc);
+        if (row < nlim) wr(smem, y, il, row, c, n, s[r] + bb, acc);
       }
     }
   }
@@ -409,7 +413,7 @@ template <int NT>
 __global__ void __launch_bounds__(NT) rowprog_kernel(Args A) {
   extern __shared__ float smem_[];
   lfloat* smem = (lfloat*)smem_;
-  const int r0 = blockIdx.x * kBM;
+  const int r0 = blockIdx.x * A.rb;
   __attribute__((address_space(3))) int* prog = (__attribute__((address_space(3))) int*)(smem + kBM * A.lds_w);
   const __attribute__((address_space(1))) int* gins = (const __attribute__((address_space(1))) int*)A.ins;
   for (int t = threadIdx.x; t < A.nins * kInsInts; t += NT) prog[t] = gins[t];
@@ -507,7 +511,22 @@ void rowprog_run(const at::Tensor& prog, const at::Tensor& ws, const c10::option
     hipFuncSetAttribute((const void*)rpg::rowprog_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const int grid = ceil_div(N, rpg::kBM);
+  // rows per workgroup: a small batch would fill a quarter of the 256 CUs with 16-row
+  // blocks (md17 PAINN: 64 workgroups); every instruction is latency-bound, so smaller
+  // blocks (the 16-row MFMA tiles then partly empty) spread the same program over more CUs.
+  // HYDRA_ROWPROG_ROWS = 16 / 8 / 4 / 2 / 1 forces the block height.
+  static int rows_env = [] {
+    const char* e = std::getenv("HYDRA_ROWPROG_ROWS");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 16 || v == 8 || v == 4 || v == 2 || v == 1) ? v : 0;
+  }();
+  int rb = rows_env;
+  if (rb == 0) {
+    rb = rpg::kBM;
+    while (rb > 4 && ceil_div(N, rb) < 2 * num_cus()) rb >>= 1;
+  }
+  a.rb = rb;
+  const int grid = ceil_div(N, rb);
   if (nt == 1024)
     rpg::rowprog_kernel<1024><<<grid, 1024, lds, stream()>>>(a);
   else if (nt == 512)
