@@ -28,7 +28,8 @@ namespace hy {
 namespace il {
 
 constexpr int TR = 4;          // rows (nodes) per forward tile (N / 4 workgroups: fills the chip)
-constexpr int MAXCOLS = 1024;  // input columns held in LDS (TR * 1024 * 4 B = 16 KB)
+constexpr int MAXCOLS = 4096;  // input columns held in LDS (TR * 4096 * 4 B = 64 KB; a MACE
+                               // message row after the uvu product is ~1.6 k columns)
 
 // orientation-specific path entry: source column offset, reduction length, weight
 // offset / strides (index = w_off + r * w_rs + o * w_os), degree width d, scale a
@@ -165,7 +166,7 @@ at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Te
   HY_CHECK(cols.scalar_type() == at::kInt && cols.dim() == 2 && cols.size(1) == 4 && cols.is_contiguous(),
            "irreps_linear: column table int32 [Dout, 4]");
   const int64_t N = x.size(0), Din = x.size(1), Dout = cols.size(0);
-  HY_CHECK(Din <= MAXCOLS, "irreps_linear: at most 1024 input columns");
+  HY_CHECK(Din <= MAXCOLS, "irreps_linear: at most 4096 input columns");
   auto out = at::empty({N, Dout}, x.options());
   if (N == 0 || Dout == 0) return out;
   const size_t lds = (size_t)TR * Din * sizeof(float);

@@ -383,7 +383,7 @@ class DeviceGraphStore:
         """Build a GraphBatch from a packed device plan (device ops only; graph-capturable).
         ``branch_sorted``: the sample indices were ordered by ``branch_order`` (graphs, and so
         nodes, grouped by branch id, padding last): enables branch-grouped decoding."""
-        if dev_buf.is_cuda and self.dataset_name is None:
+        if dev_buf.is_cuda:
             views = []
             o = 0
             for sz in lay.sizes:
@@ -410,8 +410,21 @@ class DeviceGraphStore:
                 s["graph_mask"] = gmask
                 s["node_mask"] = nmask
                 s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand
+            self._branch_fields(s, views[11], gmask if lay.padded else None, host_ids, branch_sorted)
             return b
         return self._assemble_torch(dev_buf, lay, host_ids, branch_sorted)
+
+    def _branch_fields(self, s, sidx, gmask, host_ids, branch_sorted):
+        """Multi-branch batches: per-graph dataset ids (-1 on padding graphs), two launches."""
+        if self.dataset_name is None:
+            return
+        dn = self.dataset_name_dev.index_select(0, sidx)
+        if gmask is not None:
+            dn = torch.where(gmask, dn, -1)
+        s["dataset_name"] = dn.view(-1, 1)
+        s["branch_sorted"] = bool(branch_sorted)
+        if host_ids is not None:
+            s["dataset_ids_host"] = host_ids
 
     def _assemble_torch(self, dev_buf, lay, host_ids=None, branch_sorted=False):
         """Plain-torch assembly: the CPU path, multi-branch batches, and the oracle of the
@@ -487,14 +500,7 @@ class DeviceGraphStore:
             s["graph_mask"] = gmask
             s["node_mask"] = nmask.view(-1)
             s["triplet_cap"] = functools.partial(self.triplet_cap, lay.Gp - 1, lay.Ep)  # host int, computed on demand
-        if self.dataset_name is not None:
-            dn = self.dataset_name_dev.index_select(0, sid)
-            if lay.padded:
-                dn = torch.where(gmask, dn, torch.full_like(dn, -1))
-            s["dataset_name"] = dn.view(-1, 1)
-            s["branch_sorted"] = bool(branch_sorted)
-            if host_ids is not None:
-                s["dataset_ids_host"] = host_ids
+        self._branch_fields(s, sid, gmask, host_ids, branch_sorted)
         return b
 
     def branch_order(self, indices):

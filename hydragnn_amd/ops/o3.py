@@ -344,7 +344,8 @@ class O3Linear(nn.Module):
         from . import pna as _mode
 
         return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == self.irreps_in.dim
-                and 0 < x.shape[1] <= 1024 and len(self.paths) > 0 and self.irreps_in.lmax <= 4
+                and 0 < x.shape[1] <= 4096 and self.irreps_out.dim <= 4096 and len(self.paths) > 0
+                and self.irreps_in.lmax <= 4
                 and _mode.fused("o3linear"))
 
     def path_weights(self):

@@ -17,6 +17,9 @@ CASES = [
     (I([(16, 0, 1), (24, 1, -1), (8, 0, 1), (5, 2, 1)]), I([(70, 0, 1), (3, 1, -1), (130, 2, 1)]), 37),
     (I([(64, 0, 1), (64, 1, -1), (64, 2, 1)]), I([(64, 0, 1)]), 1000),
     (I([(118, 0, 1)]), I([(64, 0, 1)]), 17),
+    # a MACE message row after the uvu product (> 1024 columns: several blocks per l)
+    (I([(64, 0, 1), (64, 1, -1), (64, 2, 1), (64, 1, -1), (64, 0, 1), (64, 2, 1), (64, 1, -1), (64, 3, -1),
+        (64, 2, 1)]), I([(64, 0, 1), (64, 1, -1), (64, 2, 1)]), 300),
 ]
 
 

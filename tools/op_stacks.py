@@ -37,6 +37,33 @@ def main():
         run(store, draw())
     torch.cuda.synchronize()
     steps = 2
+    if os.environ.get("OP_STACKS_MODE") == "dispatch":
+        # TorchDispatchMode: the Python call site of every aten op (forward) and the autograd
+        # node of backward ops, without relying on the profiler's stack capture
+        import traceback
+
+        from torch.utils._python_dispatch import TorchDispatchMode
+
+        c = collections.Counter()
+        want = {o.split("::")[1] for o in ops}
+
+        class Spy(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                base = func.overloadpacket.__name__
+                if base in want:
+                    st = [f"{f.filename.split('repo/')[-1]}:{f.lineno} {f.name}" for f in traceback.extract_stack()
+                          if "hydragnn_amd" in f.filename]
+                    key = " <- ".join(st[-2:][::-1]) if st else "(autograd / outside the package)"
+                    c[(base, key)] += 1
+                return func(*args, **(kwargs or {}))
+
+        with Spy():
+            for _ in range(steps):
+                run(store, draw())
+            torch.cuda.synchronize()
+        for (n, k), v in c.most_common(80):
+            print(f"{v / steps:7.1f}  {n:14s} {k[:220]}")
+        return
     with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         for _ in range(steps):
             run(store, draw())

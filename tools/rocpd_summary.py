@@ -21,8 +21,14 @@ def main():
     ap.add_argument("--sequence", type=int, default=0, help="print the last N dispatches in launch order")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = list(c.execute("select name, start, end, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, lds_size "
-                          "from kernels order by start"))
+    # workgroups of a dispatch over all three grid dimensions (grid sizes are in work-items)
+    try:
+        rows = list(c.execute("select name, start, end, grid_x * grid_y * grid_z, "
+                              "workgroup_x * workgroup_y * workgroup_z, vgpr_count, accum_vgpr_count, lds_size "
+                              "from kernels order by start"))
+    except sqlite3.OperationalError:
+        rows = list(c.execute("select name, start, end, grid_x, workgroup_x, vgpr_count, accum_vgpr_count, lds_size "
+                              "from kernels order by start"))
     if not rows:
         print("no kernels")
         return
