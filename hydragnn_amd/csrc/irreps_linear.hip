@@ -179,7 +179,7 @@ at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Te
 
 // dW (flat, like W) of the linear: jobs int32 [J, 8]; scale fp32 [numel] (a_p per element)
 at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const at::Tensor& jobs,
-                               const at::Tensor& scale, int64_t max_d) {
+                               const at::Tensor& scale, int64_t max_d, const c10::optional<at::Tensor>& out) {
   at::Tensor x = x_.contiguous(), g = g_.contiguous();
   HY_CHECK(x.is_cuda() && g.is_cuda() && x.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat &&
                x.dim() == 2 && g.dim() == 2 && x.size(0) == g.size(0),
@@ -190,7 +190,15 @@ at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const
            "irreps_linear_wgrad: scale fp32 [numel]");
   HY_CHECK(max_d >= 1 && max_d <= 9, "irreps_linear_wgrad: l <= 4");
   const int64_t N = x.size(0), numel = scale.numel(), J = jobs.size(0);
-  auto dW = at::empty({numel}, x.options());
+  // out: the weight's gradient slot in the step's flat buffer (parallel/gradslots.py)
+  at::Tensor dW;
+  if (out.has_value() && out->defined()) {
+    HY_CHECK(out->is_cuda() && out->scalar_type() == at::kFloat && out->is_contiguous() && out->numel() == numel,
+             "irreps_linear_wgrad: out fp32 contiguous [numel]");
+    dW = *out;
+  } else {
+    dW = at::empty({numel}, x.options());
+  }
   if (numel == 0) return dW;
   if (N == 0 || J == 0) return dW.zero_();
   // splits: ~256 workgroups over the chip, at least NCH nodes each, at most 64 (the reduce
@@ -212,7 +220,7 @@ at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("irreps_linear(Tensor x, Tensor W, Tensor paths, Tensor cols) -> Tensor");
-  m.def("irreps_linear_wgrad(Tensor x, Tensor g, Tensor jobs, Tensor scale, int max_d) -> Tensor");
+  m.def("irreps_linear_wgrad(Tensor x, Tensor g, Tensor jobs, Tensor scale, int max_d, Tensor? out=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

@@ -167,7 +167,8 @@ __global__ void __launch_bounds__(256) res_mlp_bwd_kernel(const float* __restric
 __global__ void __launch_bounds__(256) lin_act_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                           const float* __restrict__ b, const float* __restrict__ mul,
                                                           const float* __restrict__ add, int M, int I, int O,
-                                                          float* __restrict__ y, float* __restrict__ Z) {
+                                                          float scale, int trans, float* __restrict__ y,
+                                                          float* __restrict__ Z) {
   __shared__ __attribute__((aligned(16))) float xs[kRB][kLd];
   __shared__ float ws[kMaxW][kMaxW + 1];
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(256) lin_act_fwd_kernel(const float* __restric
 #pragma unroll
   for (int u = 0; u < kMaxW / 4; ++u) {
     const int r = q + 4 * u;
-    tw[u] = (r < O && c < I) ? W[r * I + c] : 0.f;
+    tw[u] = (r < O && c < I) ? W[trans ? c * O + r : r * I + c] : 0.f;
   }
   const float bias = (b != nullptr && c < O) ? b[c] : 0.f;
 #pragma unroll
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(256) lin_act_fwd_kernel(const float* __restric
   for (int u = 0; u < kRB / 4; ++u) {
     const int r = q + 4 * u, m = m0 + r;
     if (m < M && c < O) {
-      const float z = bias + rowdot(xs[r], w);
+      const float z = scale * (bias + rowdot(xs[r], w));
       const int64_t o = (int64_t)m * O + c;
       Z[o] = z;
       float v = silu(z);
@@ -209,8 +210,9 @@ __global__ void __launch_bounds__(256) lin_act_fwd_kernel(const float* __restric
 
 __global__ void __launch_bounds__(256) lin_act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ Z,
                                                           const float* __restrict__ W, const float* __restrict__ mul,
-                                                          int M, int I, int O, float* __restrict__ dx,
-                                                          float* __restrict__ dZ, float* __restrict__ dmul) {
+                                                          int M, int I, int O, float scale, int trans,
+                                                          float* __restrict__ dx, float* __restrict__ dZ,
+                                                          float* __restrict__ dmul) {
   __shared__ __attribute__((aligned(16))) float gs[kRB][kLd];
   __shared__ float ws[kMaxW][kMaxW + 1];
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
@@ -227,14 +229,14 @@ __global__ void __launch_bounds__(256) lin_act_bwd_kernel(const float* __restric
 #pragma unroll
   for (int u = 0; u < kMaxW / 4; ++u) {
     const int r = q + 4 * u;
-    tw[u] = (r < O && c < I) ? W[r * I + c] : 0.f;
+    tw[u] = (r < O && c < I) ? W[trans ? c * O + r : r * I + c] : 0.f;
   }
 #pragma unroll
   for (int u = 0; u < kMaxW / 4; ++u) ws[q + 4 * u][c] = tw[u];
 #pragma unroll
   for (int u = 0; u < kRB / 4; ++u) {
     const int r = q + 4 * u, m = m0 + r;
-    const float g = tg[u] * tm[u] * dsilu(tz[u]);
+    const float g = tg[u] * tm[u] * dsilu(tz[u]) * scale;
     if (m < M && c < O) {
       const int64_t o = (int64_t)m * O + c;
       dZ[o] = g;
@@ -305,14 +307,18 @@ std::vector<at::Tensor> res_mlp_bwd(const at::Tensor& dy_, const at::Tensor& H1,
 }
 
 // x [M, I], W [O, I], b [O] | None, mul / add [M, O] | None -> (y, z)
+// scale s: z = s (x W^T + b) (the activation's pre-scale; dZ carries it back); trans: W is
+// [I, O] (the e3nn ``x @ W`` layout) instead of [O, I]
 std::vector<at::Tensor> lin_act_fwd(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
-                                    const c10::optional<at::Tensor>& mul, const c10::optional<at::Tensor>& add) {
+                                    const c10::optional<at::Tensor>& mul, const c10::optional<at::Tensor>& add,
+                                    double scale, bool trans) {
   rm_check(x, "x");
   rm_check(W, "W");
-  HY_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == x.size(1) && x.size(1) <= rm::kMaxW && W.size(0) <= rm::kMaxW,
-           "lin_act_fwd: x [M, I], W [O, I], I, O <= 64");
+  const int64_t Wi = trans ? W.size(0) : W.size(1), Wo = trans ? W.size(1) : W.size(0);
+  HY_CHECK(x.dim() == 2 && W.dim() == 2 && Wi == x.size(1) && x.size(1) <= rm::kMaxW && Wo <= rm::kMaxW,
+           "lin_act_fwd: x [M, I], W [O, I] ([I, O] with trans), I, O <= 64");
   const int64_t M = x.size(0);
-  const int I = (int)x.size(1), O = (int)W.size(0);
+  const int I = (int)x.size(1), O = (int)Wo;
   const float *bp = nullptr, *mp = nullptr, *ap = nullptr;
   if (b.has_value() && b->defined()) {
     rm_check(*b, "b");
@@ -332,21 +338,22 @@ std::vector<at::Tensor> lin_act_fwd(const at::Tensor& x, const at::Tensor& W, co
   auto y = at::empty({M, O}, x.options()), Z = at::empty({M, O}, x.options());
   if (M)
     rm::lin_act_fwd_kernel<<<ceil_div(M, rm::kRB), 256, 0, stream()>>>(x.data_ptr<float>(), W.data_ptr<float>(), bp, mp,
-                                                                         ap, (int)M, I, O, y.data_ptr<float>(),
-                                                                         Z.data_ptr<float>());
+                                                                         ap, (int)M, I, O, (float)scale, trans ? 1 : 0,
+                                                                         y.data_ptr<float>(), Z.data_ptr<float>());
   return {y, Z};
 }
 
 // -> (dx, dz, dmul | empty)
 std::vector<at::Tensor> lin_act_bwd(const at::Tensor& dy_, const at::Tensor& Z, const at::Tensor& W,
-                                    const c10::optional<at::Tensor>& mul, bool want_dmul) {
+                                    const c10::optional<at::Tensor>& mul, bool want_dmul, double scale, bool trans) {
   auto dy = dy_.contiguous();
   rm_check(dy, "dy");
   rm_check(Z, "Z");
   rm_check(W, "W");
   const int64_t M = Z.size(0);
-  const int O = (int)Z.size(1), I = (int)W.size(1);
-  HY_CHECK(dy.sizes() == Z.sizes() && W.size(0) == O && I <= rm::kMaxW && O <= rm::kMaxW, "lin_act_bwd: shapes");
+  const int O = (int)Z.size(1), I = (int)(trans ? W.size(0) : W.size(1));
+  HY_CHECK(dy.sizes() == Z.sizes() && (trans ? W.size(1) : W.size(0)) == O && I <= rm::kMaxW && O <= rm::kMaxW,
+           "lin_act_bwd: shapes");
   const float* mp = nullptr;
   if (mul.has_value() && mul->defined()) {
     rm_check(*mul, "mul");
@@ -357,8 +364,8 @@ std::vector<at::Tensor> lin_act_bwd(const at::Tensor& dy_, const at::Tensor& Z, 
   auto dmul = want_dmul ? at::empty_like(Z) : at::empty({0}, Z.options());
   if (M)
     rm::lin_act_bwd_kernel<<<ceil_div(M, rm::kRB), 256, 0, stream()>>>(
-        dy.data_ptr<float>(), Z.data_ptr<float>(), W.data_ptr<float>(), mp, (int)M, I, O, dx.data_ptr<float>(),
-        dZ.data_ptr<float>(), want_dmul ? dmul.data_ptr<float>() : nullptr);
+        dy.data_ptr<float>(), Z.data_ptr<float>(), W.data_ptr<float>(), mp, (int)M, I, O, (float)scale, trans ? 1 : 0,
+        dx.data_ptr<float>(), dZ.data_ptr<float>(), want_dmul ? dmul.data_ptr<float>() : nullptr);
   return {dx, dZ, dmul};
 }
 
@@ -367,8 +374,10 @@ std::vector<at::Tensor> lin_act_bwd(const at::Tensor& dy_, const at::Tensor& Z, 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("res_mlp_fwd(Tensor x, Tensor W1, Tensor b1, Tensor W2, Tensor b2) -> Tensor[]");
   m.def("res_mlp_bwd(Tensor dy, Tensor H1, Tensor H2, Tensor W1, Tensor W2) -> Tensor[]");
-  m.def("lin_act_fwd(Tensor x, Tensor W, Tensor? b, Tensor? mul, Tensor? add) -> Tensor[]");
-  m.def("lin_act_bwd(Tensor dy, Tensor Z, Tensor W, Tensor? mul, bool want_dmul) -> Tensor[]");
+  m.def("lin_act_fwd(Tensor x, Tensor W, Tensor? b, Tensor? mul, Tensor? add, float scale=1.0, bool trans=False) "
+        "-> Tensor[]");
+  m.def("lin_act_bwd(Tensor dy, Tensor Z, Tensor W, Tensor? mul, bool want_dmul, float scale=1.0, bool trans=False) "
+        "-> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {

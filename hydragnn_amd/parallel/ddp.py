@@ -436,9 +436,12 @@ class BucketedGradSync:
         of parameters whose gradient is not already in its slot (one run, one launch, in the
         common case)."""
         s, e, ps = self.buckets[bi]
-        runs, start, cur = [], None, []
+        runs, start, cur, extra = [], None, [], []
         for p in ps:
             if self._in_place(p):
+                g = p.grad
+                if id(p) in self.provided and g is not None and g.data_ptr() != self._slot_ptr[p]:
+                    extra.append(p)  # a second, autograd-returned contribution of a slot-written gradient
                 if cur:
                     runs.append((start, cur))
                     cur = []
@@ -468,6 +471,8 @@ class BucketedGradSync:
                 out.copy_(gs[0])
             else:
                 torch.cat(gs, out=out)
+        for p in extra:
+            self.slot(p).add_(p.grad.view_as(p))
         return self.flat[s:e]
 
     def _launch(self, bi):

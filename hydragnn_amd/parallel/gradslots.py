@@ -34,9 +34,14 @@ def active():
 
 
 def slots(params):
-    """Flat-buffer views for every parameter of ``params`` (None unless all have one)."""
+    """Flat-buffer views for every parameter of ``params`` (None unless all have one, or when
+    one of them was already provided this step: a second use of a shared weight returns its
+    gradient through autograd, and the bucket pack adds it to the slot)."""
     s = _active
     if s is None:
+        return None
+    done = getattr(s, "provided", None)
+    if done is not None and any(id(p) in done for p in params):
         return None
     out = []
     for p in params:

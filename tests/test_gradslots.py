@@ -53,6 +53,26 @@ def test_pack_skips_provided_and_in_place_slots():
     assert not sync.provided and not sync.side_events
 
 
+def test_shared_weight_second_use_adds_to_its_slot():
+    """A weight used twice in one step: the first use writes its slot, the second gets no
+    slot (its gradient comes back through autograd) and the pack adds it to the slot."""
+    ps = _params([(3, 4), (5,)])
+    sync = BucketedGradSync(ps, bucket_cap_mb=1e9)
+    g1, g2, g0 = torch.randn(5), torch.randn(5), torch.randn(3, 4)
+    sync.release()
+    sync.set_loss(torch.tensor(1.0))
+    sync.begin()
+    with gradslots.use(sync):
+        sl = gradslots.slots([ps[1]])
+        sl[0].copy_(g1)
+        gradslots.provide([ps[1]])
+        assert gradslots.slots([ps[1]]) is None  # second use: autograd returns its gradient
+    ps[1].grad = g2.clone()
+    ps[0].grad = g0.clone()
+    sync.finish()
+    torch.testing.assert_close(sync.flat, _expected(sync, {ps[0]: g0, ps[1]: g1 + g2}, None), rtol=0, atol=1e-6)
+
+
 def test_slots_none_outside_a_step_or_for_foreign_params():
     ps = _params([(2,), (3,)])
     other = _params([(4,)], seed=3)

@@ -52,15 +52,18 @@ def test_scaled_silu_matches_torch(shape, s):
     torch.testing.assert_close(xd.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("linact", [False, True])
 @pytest.mark.parametrize("N,E,nef,nd", [(60, 700, 8, 64), (9, 40, 5, 16)])
-def test_fcn_first_layer_split_matches_concat(N, E, nef, nd):
+def test_fcn_first_layer_split_matches_concat(N, E, nef, nd, linact, monkeypatch):
     """MACE radial FCN with the first layer's cat[edge_feats, down[src], down[dst]] split at
     node level (ops/o3.py _FCNFirstSplit, csrc/conv_misc.hip edge_gather_silu) == the
     concatenated fp64 FullyConnectedNet: values and the gradients of edge_feats, down and
-    every weight."""
+    every weight (``linact``: the hidden layer runs csrc/resmlp.hip lin_act, _LinSilu)."""
+    from hydragnn_amd.ops import o3
     from hydragnn_amd.ops import segment as seg
     from hydragnn_amd.ops.o3 import FullyConnectedNet, _FCNFirstSplit
 
+    monkeypatch.setattr(o3, "_FCN_LINACT", linact)
     g = torch.Generator().manual_seed(N + E)
     dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values
     src = torch.randint(0, N, (E,), generator=g)
@@ -88,6 +91,7 @@ def test_fcn_first_layer_split_matches_concat(N, E, nef, nd):
         names.append(type(fn).__name__)
         fn = fn.next_functions[0][0] if fn.next_functions else None
     assert any("FCNFirstSplit" in n for n in names), names
+    assert any("LinSilu" in n for n in names) == linact, names  # hidden layer: GEMM + silu in one launch
     out.backward(go.float().to(dev))
     torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
     got = [efd.grad, downd.grad] + [w.grad for w in fcn.weights]
