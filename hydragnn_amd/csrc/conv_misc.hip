@@ -215,7 +215,7 @@ std::tuple<at::Tensor, at::Tensor> mf_dgrad(const at::Tensor& g_, const at::Tens
 // ---------------------------------------------------------------------------------------
 // EGNN edge first stage (reference EGCLStack.py:240-262, edge_mlp[0..1] over
 // cat[x_row, x_col, |d|, e]): the concat-linear's node blocks are one node GEMM
-// ab = [A | B]; here   h[e] = act(A[src[e]] + B[dst[e]] + r[e] * w + b)   in one pass over
+// ab = [A | B]; here   h[e] = act(A[src[e]] + B[dst[e]] + r[e] . w + b)   in one pass over
 // the [E, H] output (the composite is 2 gathers + 3 elementwise passes + the activation,
 // six [E, H] streams; for the SC25 EGNN H = 866, E ~ 35k: 121 MB each).
 // act: 0 none, 1 relu, 2 silu.  Backward: dz = g * act'(z) (z recomputed) and
@@ -232,6 +232,19 @@ __device__ __forceinline__ float act_d(int act, float z) {
   return 1.f;
 }
 
+// r [E, K] scalar edge features with their weight rows w [K, H] (K <= 4: the radial length,
+// plus narrow edge attributes: the SC25 configs' one-column edge_attr), folded into the pass
+// instead of an [E, H] outer-product GEMM and its re-read
+template <int K>
+__device__ __forceinline__ float rw_term(const float* __restrict__ r, const float* __restrict__ w, int64_t e, int c,
+                                         int H) {
+  float v = 0.f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) v = fmaf(r[e * K + j], w[j * H + c], v);
+  return v;
+}
+
+template <int K>
 __global__ void __launch_bounds__(256) edge_gather_act_fwd_kernel(
     const float* __restrict__ ab, int ld, const int* __restrict__ src, const int* __restrict__ dst,
     const float* __restrict__ r, const float* __restrict__ w, const float* __restrict__ b,
@@ -240,11 +253,12 @@ __global__ void __launch_bounds__(256) edge_gather_act_fwd_kernel(
   if (t >= E * H) return;
   const int64_t e = t / H;
   const int c = (int)(t - e * H);
-  const float z = ab[(int64_t)src[e] * ld + c] + ab[(int64_t)dst[e] * ld + H + c] + r[e] * w[c] + b[c] +
+  const float z = ab[(int64_t)src[e] * ld + c] + ab[(int64_t)dst[e] * ld + H + c] + rw_term<K>(r, w, e, c, H) + b[c] +
                   (et != nullptr ? et[t] : 0.f);
   out[t] = act_f(act, z);
 }
 
+template <int K>
 __global__ void __launch_bounds__(256) edge_gather_act_bwd_kernel(
     const float* __restrict__ g, const float* __restrict__ ab, int ld, const int* __restrict__ src,
     const int* __restrict__ dst, const float* __restrict__ r, const float* __restrict__ w, const float* __restrict__ b,
@@ -254,16 +268,26 @@ __global__ void __launch_bounds__(256) edge_gather_act_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const float* a_row = ab + (int64_t)src[e] * ld;
   const float* b_row = ab + (int64_t)dst[e] * ld + H;
-  const float re = r[e];
-  float acc = 0.f;
+  float re[K], acc[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    re[j] = r[e * K + j];
+    acc[j] = 0.f;
+  }
   for (int c = lane; c < H; c += 64) {
-    const float z = a_row[c] + b_row[c] + re * w[c] + b[c] + (et != nullptr ? et[e * H + c] : 0.f);
+    float z = a_row[c] + b_row[c] + b[c] + (et != nullptr ? et[e * H + c] : 0.f);
+#pragma unroll
+    for (int j = 0; j < K; ++j) z = fmaf(re[j], w[j * H + c], z);
     const float d = g[e * H + c] * act_d(act, z);
     dz[e * H + c] = d;
-    acc = fmaf(d, w[c], acc);
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[j] = fmaf(d, w[j * H + c], acc[j]);
   }
-  acc = wave_sum(acc);
-  if (lane == 0) dr[e] = acc;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) dr[e * K + j] = v;
+  }
 }
 
 static const float* opt_et(const c10::optional<at::Tensor>& et, int64_t E, int H) {
@@ -283,14 +307,24 @@ at::Tensor edge_gather_act_fwd(const at::Tensor& ab, const at::Tensor& src, cons
   HY_CHECK_I32(dst);
   const int64_t E = src.numel();
   const int H = (int)(ab.size(1) / 2);
-  HY_CHECK(dst.numel() == E && r.numel() == E && r.is_contiguous() && w.numel() == H && b.numel() == H &&
-               w.is_contiguous() && b.is_contiguous(),
-           "edge_gather_act: r [E], w / b [H]");
+  const int64_t K = E > 0 ? r.numel() / E : 1;
+  HY_CHECK(dst.numel() == E && r.numel() == E * K && K >= 1 && K <= 4 && r.is_contiguous() && w.numel() == K * H &&
+               b.numel() == H && w.is_contiguous() && b.is_contiguous(),
+           "edge_gather_act: r [E, K <= 4], w [K, H], b [H]");
   auto out = at::empty({E, H}, ab.options());
-  if (E * H > 0)
-    edge_gather_act_fwd_kernel<<<ceil_div(E * H, 256), 256, 0, stream()>>>(
-        ab.data_ptr<float>(), (int)ab.stride(0), src.data_ptr<int>(), dst.data_ptr<int>(), r.data_ptr<float>(),
-        w.data_ptr<float>(), b.data_ptr<float>(), opt_et(et, E, H), E, H, (int)act, out.data_ptr<float>());
+  if (E * H > 0) {
+#define HY_EGA_F(KK)                                                                                                  \
+  edge_gather_act_fwd_kernel<KK><<<ceil_div(E * H, 256), 256, 0, stream()>>>(                                       \
+      ab.data_ptr<float>(), (int)ab.stride(0), src.data_ptr<int>(), dst.data_ptr<int>(), r.data_ptr<float>(),       \
+      w.data_ptr<float>(), b.data_ptr<float>(), opt_et(et, E, H), E, H, (int)act, out.data_ptr<float>())
+    switch (K) {
+      case 1: HY_EGA_F(1); break;
+      case 2: HY_EGA_F(2); break;
+      case 3: HY_EGA_F(3); break;
+      default: HY_EGA_F(4); break;
+    }
+#undef HY_EGA_F
+  }
   return out;
 }
 
@@ -302,13 +336,24 @@ std::tuple<at::Tensor, at::Tensor> edge_gather_act_bwd(const at::Tensor& g_, con
   const int64_t E = src.numel();
   const int H = (int)(ab.size(1) / 2);
   HY_CHECK(g.numel() == E * H, "edge_gather_act_bwd: grad [E, H]");
+  const int64_t K = E > 0 ? r.numel() / E : 1;
+  HY_CHECK(K >= 1 && K <= 4 && r.numel() == E * K && w.numel() == K * H, "edge_gather_act_bwd: r [E, K], w [K, H]");
   auto dz = at::empty({E, H}, ab.options());
-  auto dr = at::empty({E}, ab.options());
-  if (E > 0)
-    edge_gather_act_bwd_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(
-        g.data_ptr<float>(), ab.data_ptr<float>(), (int)ab.stride(0), src.data_ptr<int>(), dst.data_ptr<int>(),
-        r.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), opt_et(et, E, H), E, H, (int)act,
-        dz.data_ptr<float>(), dr.data_ptr<float>());
+  auto dr = at::empty({E, K}, ab.options());
+  if (E > 0) {
+#define HY_EGA_B(KK)                                                                                                  \
+  edge_gather_act_bwd_kernel<KK><<<ceil_div(E, 4), 256, 0, stream()>>>(                                             \
+      g.data_ptr<float>(), ab.data_ptr<float>(), (int)ab.stride(0), src.data_ptr<int>(), dst.data_ptr<int>(),       \
+      r.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), opt_et(et, E, H), E, H, (int)act,              \
+      dz.data_ptr<float>(), dr.data_ptr<float>())
+    switch (K) {
+      case 1: HY_EGA_B(1); break;
+      case 2: HY_EGA_B(2); break;
+      case 3: HY_EGA_B(3); break;
+      default: HY_EGA_B(4); break;
+    }
+#undef HY_EGA_B
+  }
   return {dz, dr};
 }
 

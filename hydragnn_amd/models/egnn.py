@@ -29,8 +29,10 @@ from .base import Base
 
 
 class _EdgeGatherAct(torch.autograd.Function):
-    """act(A[src] + B[dst] + r w + b (+ e-term)) in one pass (csrc/conv_misc.hip); backward:
-    one pass for dz / dr, CSR segment sums for dA / dB, a GEMV for dw."""
+    """act(A[src] + B[dst] + r w + b (+ e-term)) in one pass (csrc/conv_misc.hip): r [E, K]
+    scalar edge features (the radial length, plus narrow edge attributes) with their weight
+    rows w [K, H]; backward: one pass for dz / dr, CSR segment sums for dA / dB, one K-row
+    GEMM for dw."""
 
     @staticmethod
     def forward(ctx, ab, r, w, b, et, src_si, dst_si, act):
@@ -45,7 +47,8 @@ class _EdgeGatherAct(torch.autograd.Function):
         src_si, dst_si, act = ctx.cfg
         dz, dr = _native.ops().edge_gather_act_bwd(g, ab, src_si.index, dst_si.index, r, w, b, et, act)
         dab = torch.cat([seg.segment_sum(dz, src_si), seg.segment_sum(dz, dst_si)], 1)
-        dw = (r.view(1, -1) @ dz).view(-1)  # row-vector GEMV (the dz^T r form ran at 4 workgroups)
+        K = w.numel() // dz.shape[1]
+        dw = (r.view(-1, K).t() @ dz).view_as(w)  # [K, E] x [E, H] (the dz^T r form ran at 4 workgroups)
         return dab, dr.view_as(r), dw, dz.sum(0), (dz if et is not None else None), None, None, None
 
 
@@ -102,9 +105,14 @@ class E_GCL(nn.Module):
         ab = linear(x, torch.cat([Wb[0], Wb[1]], 0))
         act_code = _ACT_CODE.get(type(self.edge_mlp[1]))
         if x.is_cuda and x.dtype == torch.float32 and fused("egnn") and act_code is not None:
-            et = linear(edge_attr, Wb[3]).contiguous() if len(ws) == 4 else None
-            h = _EdgeGatherAct.apply(ab.contiguous(), radial.reshape(-1).contiguous(), Wb[2].reshape(-1).contiguous(),
-                                     l0.bias, et, src_si, dst_si, act_code)
+            r, w, et = radial.reshape(-1, 1), Wb[2].t(), None
+            if len(ws) == 4 and ws[3] <= 3:
+                # narrow edge attributes join the radial column inside the pass (no [E, H] term)
+                r, w = torch.cat([r, edge_attr.reshape(-1, ws[3])], 1), torch.cat([w, Wb[3].t()], 0)
+            elif len(ws) == 4:
+                et = linear(edge_attr, Wb[3]).contiguous()
+            h = _EdgeGatherAct.apply(ab.contiguous(), r.contiguous(), w.contiguous(), l0.bias, et, src_si, dst_si,
+                                     act_code)
         else:
             h = seg.gather(ab[:, :l0.out_features], src_si) + seg.gather(ab[:, l0.out_features:], dst_si)
             h = h + radial * Wb[2].view(1, -1) + l0.bias

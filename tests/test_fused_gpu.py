@@ -247,10 +247,12 @@ def test_fused_mfconv_banks_match_composite():
         torch.testing.assert_close(a, c, rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("edge,act", [(False, "relu"), (True, "silu")])
+@pytest.mark.parametrize("edge,act", [(0, "relu"), (2, "silu"), (1, "relu"), (5, "silu")])
 def test_fused_egnn_edge_stage_matches_composite(edge, act):
     """EGNN edge_mlp first stage act(A[src] + B[dst] + r w + b (+ e-term)) fused (one pass
-    each way, csrc/conv_misc.hip) vs the composite; full E_GCL layer outputs and grads."""
+    each way, csrc/conv_misc.hip) vs the composite; full E_GCL layer outputs and grads, the
+    edge attributes' included.  Edge attributes of <= 3 columns join the radial column in
+    the pass (r [E, K], w [K, H]); wider ones are a separate [E, H] term."""
     from torch import nn
 
     from hydragnn_amd.data.device_store import DeviceGraphStore
@@ -263,13 +265,13 @@ def test_fused_egnn_edge_stage_matches_composite(edge, act):
     samples = oc20_like(6, seed=4, radius=5.0, max_neighbours=10, pe_dim=2, min_atoms=20, max_atoms=40)
     b = DeviceGraphStore(samples, "cuda").batch(list(range(6)))
     H = 40
-    layer = E_GCL(H, H, H, edge_attr_dim=2 if edge else 0, act_fn=nn.ReLU() if act == "relu" else nn.SiLU(),
+    layer = E_GCL(H, H, H, edge_attr_dim=edge, act_fn=nn.ReLU() if act == "relu" else nn.SiLU(),
                   equivariant=True).cuda()
     x = torch.randn(b.num_nodes, H, device="cuda", requires_grad=True)
     pos = b.pos.clone().requires_grad_(True)
-    ctx = Ctx(dst_si=b.dst_si, src_si=b.src_si,
-              edge_attr=torch.rand(b.edge_index.shape[1], 2, device="cuda") if edge else None)
-    params = [x, pos] + list(layer.parameters())
+    ea = torch.rand(b.edge_index.shape[1], edge, device="cuda", requires_grad=True) if edge else None
+    ctx = Ctx(dst_si=b.dst_si, src_si=b.src_si, edge_attr=ea)
+    params = [x, pos] + ([ea] if edge else []) + list(layer.parameters())
     o1 = layer(x, pos, ctx)
     gx, gp = torch.randn_like(o1[0]), torch.randn_like(o1[1])
     g1 = torch.autograd.grad(o1, params, (gx, gp), allow_unused=True)
