@@ -91,17 +91,22 @@ def oc20_gps(dev):
     return m, s, 32, ["graph"], [1], False
 
 
-def oc20_gps_h128(dev):
+def oc20_gps_h128(dev, nheads=16):
     """BASELINE config 4 (OC20 PNAPlus + GPS, bench.py) at hidden 128 (16 heads of 8)."""
     from hydragnn_amd.data.synthetic import oc20_like
 
     s = oc20_like(512, seed=1000, radius=10.0, max_neighbours=10, pe_dim=16)
     deg = degree_histogram(s, max_degree=10).to(torch.float64)
     heads = {"graph": _gheads(1, [50, 25], 50)}
-    m = create_model("PNAPlus", 4, 128, [1], 16, "GPS", "multihead", 16, ["graph"], heads, "relu", "mae", [1.0], 3,
-                     pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=10.0, max_neighbours=10,
+    m = create_model("PNAPlus", 4, 128, [1], 16, "GPS", "multihead", nheads, ["graph"], heads, "relu", "mae", [1.0],
+                     3, pna_deg=deg, edge_dim=1, envelope_exponent=5, num_radial=6, radius=10.0, max_neighbours=10,
                      dropout=0.0)
     return m, s, 32, ["graph"], [1], False
+
+
+def oc20_gps_h128_8h(dev):
+    """Config 4 at hidden 128 with the BASELINE's 8 heads (head width 16)."""
+    return oc20_gps_h128(dev, nheads=8)
 
 
 def qm9_dimenet(dev):
@@ -153,6 +158,7 @@ def multibranch_mace(dev):
 
 CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
            "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128,
+           "oc20_gps_h128_8h": oc20_gps_h128_8h,
            "oc20_gps": oc20_gps,
            "qm9_dimenet": qm9_dimenet}
 
