@@ -839,6 +839,7 @@ __global__ void __launch_bounds__(kRgThreads) rg_fill_kernel(
   int* rp = lds;             // [n + 1] local receiver row starts
   int* sp = rp + n + 1;      // [n + 1] local source row starts
   int* lsrc = sp + n + 1;    // [n * cap] the graph's edges (local ids, receiver order)
+  int* ldst = lsrc + n * min(cap, max(n - 1, 0));  // [same] their local receivers
   // E0_g and the batch total from the per-graph totals
   {
     int a = 0, b = 0;
@@ -903,18 +904,28 @@ __global__ void __launch_bounds__(kRgThreads) rg_fill_kernel(
     srp_o[gi] = E0 + sp[i];
   }
   __syncthreads();
-  // stable source permutation: source s walks the receivers in ascending order
-  for (int s = t; s < n; s += kRgThreads) {
-    int k = sp[s];
-    for (int i = 0; i < n; ++i) {
-      for (int q = rp[i]; q < rp[i + 1]; ++q) {
-        const int v = lsrc[q];
-        if (v >= s) {
-          if (v == s) sperm_o[E0 + k++] = E0 + q;
-          break;
-        }
+  for (int i = t; i < n; i += kRgThreads)
+    for (int q = rp[i]; q < rp[i + 1]; ++q) ldst[q] = i;
+  __syncthreads();
+  // stable source permutation, one thread per edge: edge q (receiver i, source s) is the
+  // rank-th edge of source s in receiver order, rank = the number of receivers i' < i whose
+  // row holds s (a binary search each: rows ascend by source)
+  for (int q = t; q < tg; q += kRgThreads) {
+    const int s = lsrc[q], i = ldst[q];
+    int rank = 0;
+    for (int i2 = 0; i2 < i; ++i2) {
+      const int end = rp[i2 + 1];
+      int lo = rp[i2], hi = end;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (lsrc[mid] < s)
+          lo = mid + 1;
+        else
+          hi = mid;
       }
+      rank += (lo < end && lsrc[lo] == s) ? 1 : 0;
     }
+    sperm_o[E0 + sp[s] + rank] = E0 + q;
   }
   }
   if (g == G - 1) {  // the padding slots, owned by `dummy` (the last node, in the last graph)
@@ -947,7 +958,14 @@ std::vector<at::Tensor> radius_static_graphs(const at::Tensor& pos_, const at::T
   // edges of one graph: at most n * min(cap, n - 1); n <= max_nodes for every real graph
   const int64_t per = std::min<int64_t>(cap, std::max<int64_t>(max_nodes - 1, 0));
   if (max_nodes <= 0 || max_nodes * per > kRgMaxEdges) return {};
-  const size_t lds = sizeof(int) * (size_t)(2 * (max_nodes + 1) + max_nodes * per);
+  const size_t lds = sizeof(int) * (size_t)(2 * (max_nodes + 1) + 2 * max_nodes * per);
+  static bool attr = false;
+  if (!attr) {  // edges + their receivers: up to 2 x 32 KB of dynamic LDS
+    HY_CHECK(hipFuncSetAttribute((const void*)rg_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 80 * 1024) == hipSuccess,
+             "radius_static_graphs: LDS attribute");
+    attr = true;
+  }
   auto io = pos.options().dtype(at::kInt);
   auto src = at::empty({Ecap}, io), dst = at::empty({Ecap}, io), drp = at::empty({N + 1}, io),
        limit = at::empty({1}, io), srp = at::empty({N + 1}, io), sperm = at::empty({Ecap}, io);
