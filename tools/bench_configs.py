@@ -131,6 +131,32 @@ def md17_painn_forces(dev):
     return m, s, 32, ["node"], [1], True
 
 
+def _md17_forces(mpnn, **kw):
+    """MD17-shaped energy + force training (config 3's data and head) for another stack: the
+    force path of these stacks runs the composite (twice-differentiable torch) ops."""
+    s = _with_edges(md_trajectory(1024, seed=2, num_atoms=21), 5.0, 20)
+    heads = {"node": _nheads(1, [64, 32])}
+    m = create_model(mpnn, 1, 64, [1], 0, "", "", 0, ["node"], heads, "relu", "mse", [1.0], 3,
+                     num_radial=6, radius=5.0, max_neighbours=20, equivariance=True, dropout=0.0, **kw)
+    return m, s, 32, ["node"], [1], True
+
+
+def md17_egnn_forces(dev):
+    """EGNN energy + forces (the atomistic examples' --compute_grad_energy, e.g. mptrj)."""
+    return _md17_forces("EGNN", edge_dim=None)
+
+
+def md17_pnaeq_forces(dev):
+    """PNAEq energy + forces (the physics-informed multibranch GFM example's stack)."""
+    s = _with_edges(md_trajectory(1024, seed=2, num_atoms=21), 5.0, 20)
+    deg = degree_histogram(s, max_degree=20).to(torch.float64)
+    heads = {"node": _nheads(1, [64, 32])}
+    m = create_model("PNAEq", 1, 64, [1], 0, "", "", 0, ["node"], heads, "relu", "mse", [1.0], 3,
+                     num_radial=6, radius=5.0, max_neighbours=20, equivariance=True, dropout=0.0, edge_dim=None,
+                     pna_deg=deg, envelope_exponent=5)
+    return m, s, 32, ["node"], [1], True
+
+
 def _multibranch(mpnn, dev, hidden, layers, hd, batch, in_dim=4, **kw):
     out = []
     for k in range(5):
@@ -158,7 +184,8 @@ def multibranch_mace(dev):
 
 CONFIGS = {"qm9_schnet": qm9_schnet, "md17_painn_forces": md17_painn_forces, "multibranch_egnn": multibranch_egnn,
            "multibranch_mace": multibranch_mace, "qm9_schnet_gps": qm9_schnet_gps, "oc20_gps_h128": oc20_gps_h128,
-           "oc20_gps_h128_8h": oc20_gps_h128_8h,
+           "oc20_gps_h128_8h": oc20_gps_h128_8h, "md17_egnn_forces": md17_egnn_forces,
+           "md17_pnaeq_forces": md17_pnaeq_forces,
            "oc20_gps": oc20_gps,
            "qm9_dimenet": qm9_dimenet}
 
