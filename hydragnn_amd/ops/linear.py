@@ -252,6 +252,85 @@ class _TallLinear(torch.autograd.Function):
         return dx, dW, db
 
 
+class _WGrad2(torch.autograd.Function):
+    """dW = dy^T x (+ db = sum_n dy) on the split-K weight-gradient kernel, differentiable once
+    more: the weight gradient formed inside a create_graph backward (force training's first
+    pass) stays part of the second pass's graph."""
+
+    @staticmethod
+    def forward(ctx, dy, x, has_b):
+        ctx.save_for_backward(dy, x)
+        dW, db = _native.ops().linear_wgrad(dy.contiguous(), x.contiguous(), has_b)
+        return dW, db
+
+    @staticmethod
+    def backward(ctx, gW, gb):
+        dy, x = ctx.saved_tensors
+        d_dy = x @ gW.t() if gW is not None else None
+        if gb is not None and gb.numel():
+            d_dy = gb.expand(dy.shape[0], -1) if d_dy is None else d_dy + gb
+        d_x = dy @ gW if gW is not None else None
+        return d_dy, d_x, None
+
+
+class _MM2(torch.autograd.Function):
+    """dx = dy @ W recorded by a create_graph backward: its own weight gradient dy^T h (an
+    edge- or node-length reduction, the second-order term of force training) runs on the
+    split-K kernel instead of a library GEMM that picks 2 workgroups for K ~ 10^4."""
+
+    @staticmethod
+    def forward(ctx, dy, W):
+        ctx.save_for_backward(dy, W)
+        return dy @ W
+
+    @staticmethod
+    def backward(ctx, h):
+        dy, W = ctx.saved_tensors
+        d_dy = h @ W.t() if ctx.needs_input_grad[0] else None
+        d_W = None
+        if ctx.needs_input_grad[1]:
+            # dW[o, i] = sum_n dy[n, o] h[n, i]: the kernel's dY^T X with (dY, X) = (dy, h)
+            d_W, _ = _native.ops().linear_wgrad(dy.contiguous(), h.contiguous(), False)
+        return d_dy, d_W
+
+
+class _LinearC(torch.autograd.Function):
+    """Composite-mode (force training) linear: twice differentiable like F.linear, with every
+    weight gradient of both backward passes on the split-K kernel (``_WGrad2`` / ``_MM2``)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return F.linear(x, W, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _MM2.apply(dy, W) if torch.is_grad_enabled() else dy @ W
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            if torch.is_grad_enabled():
+                dW, db = _WGrad2.apply(dy, x, ctx.has_b)
+            else:
+                dW, db = _native.ops().linear_wgrad(dy.contiguous(), x.contiguous(), ctx.has_b)
+            if not ctx.has_b:
+                db = None
+        return dx, dW, db
+
+
+def _composite_tall(x, W, b):
+    """The composite-mode linear takes the split-K weight gradients (GPU fp32, tall input)."""
+    return (_mode._state["composite"] and "linear" not in _mode._state["off"] and _COMPOSITE_SK and x.is_cuda
+            and x.dtype == torch.float32 and W.dtype == torch.float32 and x.dim() == 2 and x.shape[0] >= MIN_ROWS
+            and torch.is_grad_enabled() and (x.requires_grad or W.requires_grad))
+
+
+# HYDRA_COMPOSITE_SPLITK=0: composite-mode linears on plain F.linear (autograd's library GEMMs)
+_COMPOSITE_SK = os.environ.get("HYDRA_COMPOSITE_SPLITK", "1") == "1"
+
+
 class _ColBlockLinear(torch.autograd.Function):
     """y = x @ W[:, k0:k0+K]^T for a column block of a (concat-)linear weight: the block's
     weight gradient joins the deferred grouped launch as a column-block problem (``_span``)
@@ -419,6 +498,8 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     # narrow maps (e.g. an 866 -> 1 projection) and multi-input sums stay on the fp32 path
     tall = engine and xs[0].shape[0] >= MIN_ROWS and torch.is_grad_enabled() and \
         any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
+    if len(pairs) == 1 and act == ACT_NONE and residual is None and _composite_tall(xs[0], ws[0], b):
+        return _LinearC.apply(xs[0], ws[0], b)
     if len(pairs) == 1:
         if tall and _ENGINE_FWD1 and xs[0].shape[0] < ENGINE_SUM_MAX_ROWS * 4:
             y = _EngineSumF32.apply(b, xs[0], ws[0])  # HYDRA_ENGINE_FWD1=1: engine forward (A/B knob)

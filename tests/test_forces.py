@@ -65,6 +65,41 @@ def test_captured_force_step_matches_eager_gpu():
         assert abs(le - lg) <= 1e-3 * max(1.0, abs(le)), (le, lg)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mpnn", ["EGNN", "PNAEq"])
+def test_composite_linear_splitk_matches_library_gemms_gpu(mpnn, monkeypatch):
+    """Force training's composite linears (ops/linear.py _LinearC: both backward passes' weight
+    gradients on the split-K kernel, twice differentiable) == plain F.linear: one force
+    step's energy / force loss and every parameter gradient."""
+    from hydragnn_amd.ops import linear as lin
+    from hydragnn_amd.ops.pna import composite_mode
+
+    samples = _samples(160)  # >= MIN_ROWS node and edge rows: the split-K path runs
+    store = DeviceGraphStore(samples, "cuda")
+    batch = store.batch(list(range(150)))
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(lin, "_COMPOSITE_SK", on)
+        torch.manual_seed(0)
+        m = _model(mpnn).cuda()
+        b = store.batch(list(range(150)))
+        b.pos.requires_grad_(True)
+        with composite_mode(True):
+            pred = m(b)
+            loss, _ = m.energy_force_loss(pred, b)
+            ps = [p for p in m.parameters() if p.requires_grad]
+            gs = torch.autograd.grad(loss, ps, allow_unused=True)
+        grads.append((float(loss), gs))
+    assert batch.num_nodes >= lin.MIN_ROWS
+    (l1, g1), (l2, g2) = grads
+    assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l2)), (l1, l2)
+    for a, c in zip(g1, g2):
+        if a is None or c is None:
+            assert a is None and c is None
+            continue
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-5)
+
+
 def test_force_test_returns_samples_and_dump(tmp_path, monkeypatch):
     """``test()`` on a force run returns per-graph energy samples (head 0) and, with
     HYDRAGNN_DUMP_TESTDATA=1, per-sample energy/force records (ref ``train_validate_test.py:642-705``)."""
