@@ -279,8 +279,9 @@ class _MM2(torch.autograd.Function):
     split-K kernel instead of a library GEMM that picks 2 workgroups for K ~ 10^4."""
 
     @staticmethod
-    def forward(ctx, dy, W):
+    def forward(ctx, dy, W, Wp=None):
         ctx.save_for_backward(dy, W)
+        ctx.param = Wp  # the Parameter (deferral needs it: W may be a view or detached alias)
         return dy @ W
 
     @staticmethod
@@ -289,9 +290,14 @@ class _MM2(torch.autograd.Function):
         d_dy = h @ W.t() if ctx.needs_input_grad[0] else None
         d_W = None
         if ctx.needs_input_grad[1]:
-            # dW[o, i] = sum_n dy[n, o] h[n, i]: the kernel's dY^T X with (dY, X) = (dy, h)
-            d_W, _ = _native.ops().linear_wgrad(dy.contiguous(), h.contiguous(), False)
-        return d_dy, d_W
+            # dW[o, i] = sum_n dy[n, o] h[n, i]: the kernel's dY^T X with (dY, X) = (dy, h);
+            # inside the step's backward it joins the deferred grouped launch
+            Wp = ctx.param
+            if Wp is not None and _can_defer(Wp, None):
+                _record((dy, h.contiguous(), Wp, None))
+            else:
+                d_W, _ = _native.ops().linear_wgrad(dy.contiguous(), h.contiguous(), False)
+        return d_dy, d_W, None
 
 
 class _LinearC(torch.autograd.Function):
@@ -302,17 +308,23 @@ class _LinearC(torch.autograd.Function):
     def forward(ctx, x, W, b):
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.params = (W, b)
         return F.linear(x, W, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
+        Wp, bp = ctx.params
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
-            dx = _MM2.apply(dy, W) if torch.is_grad_enabled() else dy @ W
+            dx = _MM2.apply(dy, W, Wp if isinstance(Wp, torch.nn.Parameter) else None) if torch.is_grad_enabled() \
+                else dy @ W
         if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
             if torch.is_grad_enabled():
                 dW, db = _WGrad2.apply(dy, x, ctx.has_b)
+            elif ctx.needs_input_grad[1] and (not ctx.has_b or ctx.needs_input_grad[2]) and _can_defer(Wp, bp):
+                _record((dy, x, Wp, bp))  # the step's deferred grouped weight-gradient launch
+                return dx, None, None
             else:
                 dW, db = _native.ops().linear_wgrad(dy.contiguous(), x.contiguous(), ctx.has_b)
             if not ctx.has_b:
