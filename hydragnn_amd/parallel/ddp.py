@@ -180,10 +180,17 @@ class DistributedDataParallel(nn.Module):
 
 
 def default_bucket_cap(nbytes, min_buckets=2):
-    """Bucket size in bytes for ``nbytes`` of gradients.  Small GNN models: a few buckets so
-    the first all-reduce starts mid-backward.  Large models (> 64 MB): at least 8 buckets of
-    at most 32 MB — the last bucket (the first layers' gradients) is inherently exposed after
-    backward, so it is kept small; 4-32 MB rings still run at link bandwidth over xGMI."""
+    """Bucket size in bytes for ``nbytes`` of gradients.  Up to 4 MB (the OC20 PNAPlus+GPS
+    headline: 1.7 MB): ONE bucket.  An all-reduce that small is latency-bound over xGMI
+    (tens of microseconds whatever its size), and the fused GPS encoder hands back its
+    gradients at the end of its backward anyway (tools/overlap_check.py measured its three
+    buckets all enqueued after the last backward kernels).  So one collective beats a
+    sequence of three.  Medium models: a few buckets, so the first all-reduce starts
+    mid-backward.  Large models (> 64 MB): at least 8 buckets of at most 32 MB.  The last
+    bucket (the first layers' gradients) is inherently exposed after backward, so it is kept
+    small; 4-32 MB rings still run at link bandwidth over xGMI."""
+    if nbytes <= 4 * 1024 * 1024:
+        return nbytes + 1
     if nbytes > 64 * 1024 * 1024:
         min_buckets = max(min_buckets, 8)
     return min(max(nbytes // min_buckets + 1, 256 * 1024), 32 * 1024 * 1024)
