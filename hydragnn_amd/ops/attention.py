@@ -143,11 +143,37 @@ class _FlashAttn(torch.autograd.Function):
         return ops.attn_bwd_combine(pq, pkv), None, None, None, None
 
 
+class _Attn8(torch.autograd.Function):
+    """8-wide heads on the MFMA attention of csrc/attention8.hip (the fused GPS encoder's
+    kernels) for the module path: pack (pair / quad layouts), one forward launch, one backward
+    launch.  The QM9 SchNet + GPS layers (hidden 64, 8 heads) ran the packed-fp32 VALU
+    kernels here (~100 us per layer each way at 1.1 k tokens)."""
+
+    @staticmethod
+    def forward(ctx, qkv, seg_id, seg_ptr, heads, scale):
+        ops = _native.ops()
+        N = qkv.shape[0]
+        Qp, Qq, Kp, Kq, Vp, Vq = ops.attn8_pack(qkv, heads)
+        O, L2 = ops.attn8_fwd(Qp, Kp, Vq, seg_id, seg_ptr, N, scale, 0)
+        ctx.save_for_backward(O, L2, Qp, Qq, Kp, Kq, Vp, seg_id, seg_ptr)
+        ctx.scale = scale
+        return O
+
+    @staticmethod
+    def backward(ctx, dO):
+        O, L2, Qp, Qq, Kp, Kq, Vp, seg_id, seg_ptr = ctx.saved_tensors
+        dqkv = _native.ops().attn8_bwd(dO.contiguous(), O, L2, Qp, Qq, Kp, Kq, Vp, seg_id, seg_ptr, ctx.scale, 0)
+        return dqkv, None, None, None, None
+
+
 def segment_attention(qkv, heads, seg_id, seg_ptr, scale=None):
     """Multi-head self-attention on packed ``qkv`` [N, 3F] -> [N, F]."""
     F = qkv.shape[1] // 3
     D = F // heads
     scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    if (qkv.is_cuda and qkv.dtype == torch.float32 and D == 8 and _pna_mode.fused("attn")
+            and _pna_mode.fused("attn8") and qkv.shape[0] > 0):
+        return _Attn8.apply(qkv.contiguous(), seg_id, seg_ptr, heads, scale)
     if (qkv.is_cuda and qkv.dtype == torch.float32 and D in (4, 8, 16, 32, 64)
             and _pna_mode.fused("attn")):
         return _FlashAttn.apply(qkv, seg_id, seg_ptr, heads, scale)

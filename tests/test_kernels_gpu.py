@@ -136,6 +136,8 @@ def test_attention(D, scope):
     ref = attention_reference(qc, H, seg_id)
     qg = qkv.to(DEV).requires_grad_()
     out = segment_attention(qg, H, seg_id.to(DEV), seg_ptr.to(DEV))
+    # 8-wide heads: the MFMA kernels of csrc/attention8.hip; the rest: packed-fp32 VALU
+    assert ("Attn8" in type(out.grad_fn).__name__) == (D == 8), type(out.grad_fn).__name__
     torch.testing.assert_close(out.cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
     g = torch.randn_like(ref)
     ref.backward(g)
