@@ -225,9 +225,236 @@ at::Tensor dimenet_sbf_bwd(const at::Tensor& gout, const at::Tensor& vec, const 
   return dvec;
 }
 
+
+// ------------------------------------------------------------------ low-rank triplet filter
+// DimeNet++ interaction (reference DIMEStack.py -> PyG InteractionPPBlock):
+//     sbf = lin_sbf2(lin_sbf1(sbf_raw))     [T, I] = s8 [T, B] x W2^T  (B = basis_emb, 8)
+//     out[e] = sum_{t in ji-row e} x_kj[kj(t)] * sbf[t]
+// The [T, I] filter (T ~ 3e5 triplets: 87 MB written then read back, twice each way) is never
+// formed: each output column c recomputes w[t, c] = s8[t] . W2[c] (B FMAs) from the 32-byte
+// s8 row.  Backward: dx = the same kernel over the kj CSR with g gathered by ji; and
+// u[t, c] = x[kj(t), c] g[ji(t), c] feeds ds8[t] = u[t] W2 (wave reductions) and
+// dW2 = sum_t u[t]^T s8[t] (per-workgroup partials, one reduce launch).
+constexpr int kLrB = 8;  // basis width
+
+// out[r, :] = sum over CSR row r (positions through perm) of x[gidx[t], :] * (s8[t] W2^T)
+__global__ void __launch_bounds__(256) lr_gms_kernel(const float* __restrict__ x, const float* __restrict__ s8,
+                                                     const float* __restrict__ W2, const int* __restrict__ gidx,
+                                                     const int* __restrict__ rowptr, const int* __restrict__ perm,
+                                                     const int* __restrict__ row_limit, int N, int F, int tpr,
+                                                     int rpb, float* __restrict__ out) {
+  const int r = blockIdx.x * rpb + threadIdx.x / tpr;
+  const int v = threadIdx.x % tpr;  // float4 column group
+  if (r >= N || 4 * v >= F) return;
+  const int end = row_limit ? min(rowptr[r + 1], *row_limit) : rowptr[r + 1];
+  const int beg = min(rowptr[r], end);
+  float wc[4][kLrB];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < kLrB; ++j) wc[q][j] = W2[(4 * v + q) * kLrB + j];
+  // U rows per batch: every index load, then every row load, in flight together (one row
+  // at a time paid the perm -> gidx -> row chain of dependent latencies per triplet)
+  constexpr int U = 8;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int e = beg; e < end; e += U) {
+    int tt[U], gi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ee = min(e + u, end - 1);
+      tt[u] = perm ? perm[ee] : ee;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) gi[u] = gidx[tt[u]];
+    float4 xv[U], s0[U], s1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xv[u] = reinterpret_cast<const float4*>(x + (int64_t)gi[u] * F)[v];
+      s0[u] = reinterpret_cast<const float4*>(s8 + (int64_t)tt[u] * kLrB)[0];
+      s1[u] = reinterpret_cast<const float4*>(s8 + (int64_t)tt[u] * kLrB)[1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e + u >= end) break;
+      const float sv[kLrB] = {s0[u].x, s0[u].y, s0[u].z, s0[u].w, s1[u].x, s1[u].y, s1[u].z, s1[u].w};
+      float wq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float p = 0.f;
+#pragma unroll
+        for (int j = 0; j < kLrB; ++j) p = fmaf(sv[j], wc[q][j], p);
+        wq[q] = p;
+      }
+      a.x = fmaf(xv[u].x, wq[0], a.x);
+      a.y = fmaf(xv[u].y, wq[1], a.y);
+      a.z = fmaf(xv[u].z, wq[2], a.z);
+      a.w = fmaf(xv[u].w, wq[3], a.w);
+    }
+  }
+  reinterpret_cast<float4*>(out + (int64_t)r * F)[v] = a;
+}
+
+// u[t, c] = x[ia[t], c] * g[ib[t], c] (t < Tlim): ds8[t, j] = sum_c u W2[c, j] and per-block
+// partials dW2p[blk][c][j] = sum_{t of blk} u[t, c] s8[t, j].  One wave per triplet stripe,
+// lane = column (F <= 64) for the loads and the dW2 sums; ds8 goes through LDS: a batch of 8
+// triplets' u rows is staged, then lane (triplet u, basis j) forms its dot product over the
+// columns (per-triplet wave reductions were 8 chains of 6 dependent lane permutes).
+constexpr int kLrWaves = 4, kLrPerWave = 256;
+__global__ void __launch_bounds__(64 * kLrWaves) lr_wgrad_kernel(const float* __restrict__ x,
+                                                                 const int* __restrict__ ia,
+                                                                 const float* __restrict__ g,
+                                                                 const int* __restrict__ ib,
+                                                                 const float* __restrict__ s8,
+                                                                 const float* __restrict__ W2, int T, int F,
+                                                                 const int* __restrict__ t_limit,
+                                                                 float* __restrict__ ds8,
+                                                                 float* __restrict__ dW2p) {
+  __shared__ float red[kLrWaves][64][kLrB];
+  __shared__ float w2s[64][kLrB + 1];
+  __shared__ float su[kLrWaves][8][65];
+  const int w = threadIdx.x >> 6, c = threadIdx.x & 63;
+  const int Te = t_limit ? min(T, *t_limit) : T;
+  const bool live = c < F;
+  for (int k = threadIdx.x; k < 64 * kLrB; k += 64 * kLrWaves) {
+    const int cc = k / kLrB, j = k % kLrB;
+    w2s[cc][j] = cc < F ? W2[cc * kLrB + j] : 0.f;
+  }
+  __syncthreads();
+  float acc[kLrB];
+#pragma unroll
+  for (int j = 0; j < kLrB; ++j) acc[j] = 0.f;
+  const int t0 = (blockIdx.x * kLrWaves + w) * kLrPerWave;
+  const int t1 = min(t0 + kLrPerWave, T);
+  constexpr int U = 8;  // triplets per batch: all their loads in flight together
+  const int myu = c >> 3, myj = c & 7;  // ds8 lane role: (triplet of the batch, basis index)
+  for (int tb = t0; tb < t1; tb += U) {
+    int ja[U], jb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tb + u, t1 - 1);
+      ja[u] = ia[t];
+      jb[u] = ib[t];
+    }
+    float xu[U], gu[U];
+    float4 s0[U], s1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tb + u, t1 - 1);
+      xu[u] = live ? x[(int64_t)ja[u] * F + c] : 0.f;
+      gu[u] = live ? g[(int64_t)jb[u] * F + c] : 0.f;
+      s0[u] = reinterpret_cast<const float4*>(s8 + (int64_t)t * kLrB)[0];
+      s1[u] = reinterpret_cast<const float4*>(s8 + (int64_t)t * kLrB)[1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tb + u;
+      // padding triplets (t >= Te) and the stripe's tail: no share of either gradient
+      const float uu = (t < t1 && t < Te) ? xu[u] * gu[u] : 0.f;
+      su[w][u][c] = uu;
+      const float sv[kLrB] = {s0[u].x, s0[u].y, s0[u].z, s0[u].w, s1[u].x, s1[u].y, s1[u].z, s1[u].w};
+#pragma unroll
+      for (int j = 0; j < kLrB; ++j) acc[j] = fmaf(uu, sv[j], acc[j]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float d = 0.f;
+#pragma unroll 8
+    for (int cc = 0; cc < 64; ++cc) d = fmaf(su[w][myu][cc], w2s[cc][myj], d);
+    const int t = tb + myu;
+    if (t < t1) ds8[(int64_t)t * kLrB + myj] = d;
+    __builtin_amdgcn_wave_barrier();  // su is rewritten by the next batch
+  }
+#pragma unroll
+  for (int j = 0; j < kLrB; ++j) red[w][c][j] = acc[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * kLrB; k += 64 * kLrWaves) {
+    const int cc = k / kLrB;
+    if (cc >= F) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < kLrWaves; ++q) v += red[q][cc][k % kLrB];
+    dW2p[(int64_t)blockIdx.x * F * kLrB + k] = v;
+  }
+}
+
+// out[k] = sum_b p[b][k]: 32 threads per element over the partials, then an LDS fold
+__global__ void __launch_bounds__(256) lr_wreduce_kernel(const float* __restrict__ p, int nb, int n,
+                                                         float* __restrict__ out) {
+  __shared__ float part[8][33];
+  const int e = threadIdx.x >> 5, l = threadIdx.x & 31;
+  const int k = blockIdx.x * 8 + e;
+  float a = 0.f;
+  if (k < n)
+    for (int b = l; b < nb; b += 32) a += p[(int64_t)b * n + k];
+  part[e][l] = a;
+  __syncthreads();
+  if (l == 0 && k < n) {
+    float v = 0.f;
+    for (int q = 0; q < 32; ++q) v += part[e][q];
+    out[k] = v;
+  }
+}
+
+at::Tensor lr_gather_mul_sum(const at::Tensor& x_, const at::Tensor& s8_, const at::Tensor& W2_,
+                             const at::Tensor& gidx, const at::Tensor& rowptr, const c10::optional<at::Tensor>& perm,
+                             int64_t N, const c10::optional<at::Tensor>& limit) {
+  auto x = x_.contiguous(), s8 = s8_.contiguous(), W2 = W2_.contiguous();
+  HY_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && s8.scalar_type() == at::kFloat &&
+               W2.scalar_type() == at::kFloat && gidx.scalar_type() == at::kInt && rowptr.scalar_type() == at::kInt,
+           "lr_gather_mul_sum: fp32 operands, int32 indices");
+  const int F = (int)x.size(1);
+  HY_CHECK(x.dim() == 2 && F % 4 == 0 && s8.dim() == 2 && s8.size(1) == kLrB && W2.size(0) == F &&
+               W2.size(1) == kLrB && gidx.numel() == s8.size(0) && rowptr.numel() == N + 1,
+           "lr_gather_mul_sum: x [*, F % 4 == 0], s8 [T, 8], W2 [F, 8], gidx [T], rowptr [N + 1]");
+  auto out = at::empty({N, F}, x.options());
+  if (N == 0) return out;
+  const int* pp = (perm.has_value() && perm->defined()) ? perm->data_ptr<int>() : nullptr;
+  const int* lim = (limit.has_value() && limit->defined()) ? limit->data_ptr<int>() : nullptr;
+  int tpr = 1;
+  while (tpr < F / 4 && tpr < 64) tpr <<= 1;
+  HY_CHECK(tpr * 4 >= F, "lr_gather_mul_sum: F <= 256");
+  const int rpb = 256 / tpr;
+  lr_gms_kernel<<<ceil_div(N, rpb), 256, 0, stream()>>>(x.data_ptr<float>(), s8.data_ptr<float>(),
+                                                       W2.data_ptr<float>(), gidx.data_ptr<int>(),
+                                                       rowptr.data_ptr<int>(), pp, lim, (int)N, F, tpr, rpb,
+                                                       out.data_ptr<float>());
+  return out;
+}
+
+// -> (ds8 [T, 8], dW2 [F, 8])
+std::vector<at::Tensor> lr_filter_grad(const at::Tensor& x_, const at::Tensor& ia, const at::Tensor& g_,
+                                       const at::Tensor& ib, const at::Tensor& s8_, const at::Tensor& W2_,
+                                       const c10::optional<at::Tensor>& t_limit) {
+  auto x = x_.contiguous(), g = g_.contiguous(), s8 = s8_.contiguous(), W2 = W2_.contiguous();
+  const int64_t T = s8.size(0);
+  const int F = (int)x.size(1);
+  HY_CHECK(F <= 64 && g.size(1) == F && ia.numel() == T && ib.numel() == T && W2.size(0) == F &&
+               W2.size(1) == kLrB && s8.size(1) == kLrB,
+           "lr_filter_grad: F <= 64, ia / ib [T], s8 [T, 8], W2 [F, 8]");
+  auto ds8 = at::empty({T, kLrB}, x.options()), dW2 = at::empty({F, kLrB}, x.options());
+  const int per = kLrWaves * kLrPerWave;
+  const int nb = (int)std::max<int64_t>(1, ceil_div(T, per));
+  auto part = at::empty({nb, F * kLrB}, x.options());
+  if (T > 0)
+    lr_wgrad_kernel<<<nb, 64 * kLrWaves, 0, stream()>>>(
+        x.data_ptr<float>(), ia.data_ptr<int>(), g.data_ptr<float>(), ib.data_ptr<int>(), s8.data_ptr<float>(),
+        W2.data_ptr<float>(), (int)T, F, (t_limit.has_value() && t_limit->defined()) ? t_limit->data_ptr<int>() : nullptr,
+        ds8.data_ptr<float>(), part.data_ptr<float>());
+  else
+    part.zero_();
+  lr_wreduce_kernel<<<ceil_div(F * kLrB, 8), 256, 0, stream()>>>(part.data_ptr<float>(), nb, F * kLrB,
+                                                                dW2.data_ptr<float>());
+  return {ds8, dW2};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("lr_gather_mul_sum(Tensor x, Tensor s8, Tensor W2, Tensor gidx, Tensor rowptr, Tensor? perm, int N, "
+        "Tensor? limit=None) -> Tensor");
+  m.def("lr_filter_grad(Tensor x, Tensor ia, Tensor g, Tensor ib, Tensor s8, Tensor W2, Tensor? t_limit=None) "
+        "-> Tensor[]");
   m.def("dimenet_sbf_fwd(Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent, Tensor? limit=None) -> Tensor");
   m.def(
       "dimenet_sbf_bwd(Tensor gout, Tensor vec, Tensor kj, Tensor ji, Tensor z, Tensor nrm, float cutoff, int exponent, "
@@ -235,6 +462,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("lr_gather_mul_sum", hy::lr_gather_mul_sum);
+  m.impl("lr_filter_grad", hy::lr_filter_grad);
   m.impl("dimenet_sbf_fwd", hy::dimenet_sbf_fwd);
   m.impl("dimenet_sbf_bwd", hy::dimenet_sbf_bwd);
 }

@@ -359,6 +359,50 @@ class HydraEmbeddingBlock(nn.Module):
         return self.act(h)
 
 
+class _LowRankGMS(torch.autograd.Function):
+    """``gather_mul_sum(x_kj, s8 @ W2^T, kj_si, ji_si)`` without the [T, I] triplet filter
+    (csrc/dimenet.hip lr_gather_mul_sum / lr_filter_grad): the filter is recomputed per
+    column from the 8-wide basis row.  First order (composite mode keeps the torch chain)."""
+
+    @staticmethod
+    def forward(ctx, x, s8, W2, gsi, ssi):
+        from .. import _native
+
+        ctx.save_for_backward(x, s8, W2)
+        ctx.gsi, ctx.ssi = gsi, ssi
+        return _native.ops().lr_gather_mul_sum(x.contiguous(), s8.contiguous(), W2, gsi.index, ssi.rowptr,
+                                               ssi.perm, ssi.num_segments, ssi.limit)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+
+        x, s8, W2 = ctx.saved_tensors
+        gsi, ssi = ctx.gsi, ctx.ssi
+        ops = _native.ops()
+        g = g.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # dx[k] = sum_{t: kj(t) = k} g[ji(t)] * w[t]: the same kernel over the kj CSR
+            dx = ops.lr_gather_mul_sum(g, s8, W2, ssi.index, gsi.rowptr, gsi.perm, x.shape[0], gsi.limit)
+        ds8 = dW2 = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            ds8, dW2 = ops.lr_filter_grad(x, gsi.index, g, ssi.index, s8, W2, ssi.limit)
+        return dx, ds8, dW2, None, None
+
+
+def _lowrank_ok(x, s8, W2):
+    from ..ops.pna import fused
+
+    return (x.is_cuda and x.dtype == torch.float32 and s8.dtype == torch.float32 and x.dim() == 2
+            and x.shape[1] % 4 == 0 and x.shape[1] <= 64 and s8.shape[1] == 8 and fused("dimenet_lr")
+            and _LOWRANK)
+
+
+# HYDRA_DIMENET_LOWRANK=0: materialise the [T, I] filter (lin_sbf2) and use gather_mul_sum
+_LOWRANK = os.environ.get("HYDRA_DIMENET_LOWRANK", "1") == "1"
+
+
 class InteractionPPBlock(nn.Module):
     def __init__(self, hidden_channels, int_emb_size, basis_emb_size, num_spherical, num_radial, num_before_skip,
                  num_after_skip, act):
@@ -386,8 +430,12 @@ class InteractionPPBlock(nn.Module):
         x_ji = silu_lin(self.lin_ji, self.act, x)
         x_kj = silu_lin(self.lin_kj, self.act, x, mul=self.lin_rbf2(self.lin_rbf1(rbf)))
         x_kj = silu_lin(self.lin_down, self.act, x_kj)
-        sbf = self.lin_sbf2(self.lin_sbf1(sbf))
-        x_kj = seg.gather_mul_sum(x_kj, sbf, kj_si, ji_si)  # triplet gather * sbf -> sum, one pass
+        s8 = self.lin_sbf1(sbf)
+        if _lowrank_ok(x_kj, s8, self.lin_sbf2.weight):
+            # the [T, I] filter s8 W2^T is recomputed per column inside the pass (never stored)
+            x_kj = _LowRankGMS.apply(x_kj, s8, self.lin_sbf2.weight, kj_si, ji_si)
+        else:
+            x_kj = seg.gather_mul_sum(x_kj, self.lin_sbf2(s8), kj_si, ji_si)  # gather * sbf -> sum
         h = silu_lin(self.lin_up, self.act, x_kj, add=x_ji)
         for layer in self.layers_before_skip:
             h = layer(h)

@@ -58,3 +58,35 @@ def test_sbf_matches_composite(n_sph, n_rad):
     (ref * G.double().cpu()).sum().backward()
     torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(p1.grad.double().cpu(), p2.grad, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("F", [64, 16])
+def test_lowrank_triplet_filter_matches_materialised(F):
+    """DimeNet++ interaction: gather_mul_sum with the low-rank triplet filter s8 W2^T
+    recomputed per column (models/dimenet.py _LowRankGMS, csrc/dimenet.hip lr_*) == the
+    materialised filter in fp64: output and the gradients of x_kj, s8 and W2."""
+    from hydragnn_amd.models.dimenet import _LowRankGMS
+
+    pos, src, dst = _graph(seed=3)
+    N, E = pos.shape[0], src.numel()
+    dst_si = seg.SegIndex.from_index(dst.to(dev), N, sorted_=True)
+    src_si = seg.SegIndex.from_index(src.to(dev), N, sorted_=False)
+    kj, ji = triplets_csr(dst_si, src_si, N)
+    kj_si = seg.SegIndex.from_index(kj, E, sorted_=False)
+    ji_si = seg.SegIndex.from_index(ji, E, sorted_=True)
+    T = kj.numel()
+    g = torch.Generator().manual_seed(F)
+    x = torch.randn(E, F, generator=g)
+    s8 = torch.randn(T, 8, generator=g)
+    W2 = torch.randn(F, 8, generator=g)
+    go = torch.randn(E, F, generator=g)
+    xs = [t.to(dev).requires_grad_() for t in (x, s8, W2)]
+    out = _LowRankGMS.apply(xs[0], xs[1], xs[2], kj_si, ji_si)
+    out.backward(go.to(dev))
+    xr = [t.double().requires_grad_() for t in (x, s8, W2)]
+    filt = xr[1] @ xr[2].t()
+    ref = torch.zeros(E, F, dtype=torch.float64).index_add_(0, ji.long().cpu(), xr[0][kj.long().cpu()] * filt)
+    ref.backward(go.double())
+    torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
+    for a, b in zip(xs, xr):
+        torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-4, atol=1e-3)
