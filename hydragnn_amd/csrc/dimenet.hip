@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(256) lr_gms_kernel(const float* __restrict__ x
 // lane = column (F <= 64) for the loads and the dW2 sums; ds8 goes through LDS: a batch of 8
 // triplets' u rows is staged, then lane (triplet u, basis j) forms its dot product over the
 // columns (per-triplet wave reductions were 8 chains of 6 dependent lane permutes).
-constexpr int kLrWaves = 4, kLrPerWave = 256;
+constexpr int kLrWaves = 4, kLrPerWave = 64;
 __global__ void __launch_bounds__(64 * kLrWaves) lr_wgrad_kernel(const float* __restrict__ x,
                                                                  const int* __restrict__ ia,
                                                                  const float* __restrict__ g,
