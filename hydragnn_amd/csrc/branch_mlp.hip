@@ -29,6 +29,7 @@ constexpr int kMaxL = 8, kMaxB = 8, kMaxW = 128;  // layers, branches, widths
 
 struct Args {
   int L, nb, R, hd;
+  int ldx;  // row stride of x (a column slice of a wider row, e.g. the scalar block)
   int dims[kMaxL + 1];
   int act[kMaxL];      // after layer l: 0 none, 1 relu, 2 silu, 3 tanh, 4 sigmoid
   int trans[kMaxL];
@@ -111,7 +112,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(const float* __restrict__ x, c
   {
     const int I0 = a.dims[0];
     const float s0 = a.scale[0];
-    for (int i = tid; i < kMaxW; i += 256) hbuf[i] = i < I0 ? s0 * x[(int64_t)r * I0 + i] : 0.f;
+    for (int i = tid; i < kMaxW; i += 256) hbuf[i] = i < I0 ? s0 * x[(int64_t)r * a.ldx + i] : 0.f;
   }
   __syncthreads();
   for (int l = 0; l < L; ++l) {
@@ -249,9 +250,10 @@ static bm::Args bm_args(const at::Tensor& x, const at::Tensor& rid, const at::Te
   HY_CHECK(nb >= 1 && nb <= bm::kMaxB, "branch_mlp: 1..8 branches");
   HY_CHECK(ptab.is_cuda() && ptab.scalar_type() == at::kLong && ptab.is_contiguous() && ptab.numel() == 2 * L * nb,
            "branch_mlp: pointer table int64 [2, L, nb]");
-  HY_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) == dims[0] && rid.numel() == x.size(0) && rid.is_cuda(),
-           "branch_mlp: x [R, I0] contiguous, rid [R]");
+  HY_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) == dims[0] && rid.numel() == x.size(0) && rid.is_cuda(),
+           "branch_mlp: x [R, I0] with unit column stride, rid [R]");
   bm::Args a{};
+  a.ldx = (int)x.stride(0);
   a.L = L;
   a.nb = nb;
   a.R = (int)x.size(0);
@@ -305,7 +307,7 @@ std::vector<at::Tensor> branch_mlp_bwd(const at::Tensor& gout_, const at::Tensor
   const int64_t R = x.size(0);
   HY_CHECK(gout.scalar_type() == at::kFloat && gout.numel() == R * hd, "branch_mlp_bwd: grad [R, hd]");
   HY_CHECK((int)zs.size() == a.L, "branch_mlp_bwd: saved pre-activations per layer");
-  auto dx = at::empty_like(x);
+  auto dx = at::empty({x.size(0), x.size(1)}, x.options());  // dense, whatever x's row stride
   std::vector<at::Tensor> res{dx};
   for (int l = 0; l < a.L; ++l) {
     HY_CHECK(zs[l].is_contiguous() && zs[l].numel() == R * a.dims[l + 1], "branch_mlp_bwd: zs[l] [R, O_l]");

@@ -120,7 +120,8 @@ def branch_mlp(x, rid, chains, hd, acc=None):
     """``out[r] = chain_{rid[r]}(x[r])[:hd]`` (rows with rid < 0: zero), plus ``acc`` [R, hd]
     when given (summed read-outs: no separate add).  ``rid`` int32 [R]."""
     L, nb = len(chains[0]), len(chains)
-    x = x.contiguous()
+    if x.stride(1) != 1:  # a column slice of wider rows is read in place (row stride)
+        x = x.contiguous()
     dims = _dims(chains, x.shape[1])
     acts = [act_code(s[3]) for s in chains[0]]
     trans = [int(s[1]) for s in chains[0]]

@@ -521,8 +521,10 @@ class _FCNFirstSplit(torch.autograd.Function):
         from .. import _native
 
         nef, nd = ef.shape[1], down.shape[1]
-        # [N, 2 nd] = down @ [W_s | W_d] (one GEMM; the column blocks of W1[nef:] side by side)
-        ab = down @ W1[nef:].view(2, nd, nd).permute(1, 0, 2).reshape(nd, 2 * nd)
+        # [2, N, nd] = down @ W_s, down @ W_d: one batched GEMM over the row blocks of W1[nef:]
+        # with a stride-0 batch operand (the [N, 2 nd] side-by-side form needed a transposing
+        # copy of the weight every step); edge_gather_silu takes either layout
+        ab = torch.bmm(down.unsqueeze(0).expand(2, -1, -1), W1[nef:].view(2, nd, nd))
         et = ef @ W1[:nef]
         ctx.save_for_backward(ef, down, W1, ab, et)
         ctx.cfg = (s, src_si, dst_si)

@@ -57,12 +57,15 @@ def test_branch_mlp_matches_per_row_loop(R, dims, acts, trans, nb):
     dev = torch.device("cuda")
     dchains = [[(nn.Parameter(W.detach().to(dev)), tr, None if b is None else nn.Parameter(b.detach().to(dev)), a, s)
                 for (W, tr, b, a, s) in c] for c in chains]
-    xd = x.float().to(dev).requires_grad_(True)
-    assert bm.eligible(xd, dchains)
+    # the input as a column slice of wider rows (the MACE scalar block): read with its stride
+    wide = torch.cat([x.float(), torch.randn(R, 5, generator=g)], 1).to(dev).requires_grad_(True)
+    xd = wide[:, :dims[0]]
+    assert bm.eligible(xd, dchains) and not xd.is_contiguous()
     out = bm.branch_mlp(xd, rid.int().to(dev), dchains, dims[-1])
     out.backward(go.float().to(dev))
     torch.testing.assert_close(out.double().cpu(), ref.detach(), rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(xd.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(wide.grad[:, :dims[0]].double().cpu(), xr.grad, rtol=1e-4, atol=1e-5)
+    assert not wide.grad[:, dims[0]:].abs().sum()
     for c, rc in zip(dchains, ref_chains):
         for (W, _, b, _, _), (rW, _, rb, _, _) in zip(c, rc):
             gw = W.grad if W.grad is not None else torch.zeros_like(W)
