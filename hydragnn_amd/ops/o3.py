@@ -874,6 +874,7 @@ class _SymConNative(torch.autograd.Function):
         Wcat = torch.cat([w for w in weights], 1).contiguous()  # [ne, Ktot, H]
         ctx.save_for_backward(x, Wcat, ents, grps)
         ctx.elem_si, ctx.shapes, ctx.ne = elem_si, shapes, ne
+        ctx.params = weights
         return _native.ops().symcon_fwd(x.contiguous(), elem_si.index, Wcat, ents, grps, out_cols)
 
     @staticmethod
@@ -887,7 +888,20 @@ class _SymConNative(torch.autograd.Function):
         # per-element reduction over nodes: few, long segments (every node of an element,
         # padding nodes included) -> one GEMM with the element one-hot (a CSR walk of the
         # longest segment was 80+ us per layer on MI355X)
-        dW = (ctx.elem_si.onehot_t(dWn.dtype) @ dWn.view(N, Ktot * H)).view(ctx.ne, Ktot, H)
+        oh = ctx.elem_si.onehot_t(dWn.dtype)
+        from ..parallel import gradslots as _gs
+
+        sl = _gs.slots(list(ctx.params))
+        if sl is not None:
+            # every weight's gradient GEMM writes its own slot of the step's flat buffer (the
+            # column blocks of one GEMM were strided views: a contiguous copy each, then the pack)
+            o = 0
+            for K, w in zip(ctx.shapes, sl):
+                torch.mm(oh, dWn[:, o:o + K].reshape(N, K * H), out=w.view(ctx.ne, K * H))
+                o += K
+            _gs.provide(list(ctx.params))
+            return (dx, None, None, None, None, None, *([None] * len(ctx.shapes)))
+        dW = (oh @ dWn.view(N, Ktot * H)).view(ctx.ne, Ktot, H)
         grads, o = [], 0
         for K in ctx.shapes:
             grads.append(dW[:, o:o + K])

@@ -54,6 +54,8 @@ def main():
                     st = [f"{f.filename.split('repo/')[-1]}:{f.lineno} {f.name}" for f in traceback.extract_stack()
                           if "hydragnn_amd" in f.filename]
                     key = " <- ".join(st[-2:][::-1]) if st else "(autograd / outside the package)"
+                    if not st and os.environ.get("OP_STACKS_SHAPES") == "1":
+                        key += " " + str([tuple(a.shape) for a in args if torch.is_tensor(a)][:3])
                     c[(base, key)] += 1
                 return func(*args, **(kwargs or {}))
 
