@@ -596,9 +596,125 @@ at::Tensor scaled_silu_bwd(const at::Tensor& g_, const at::Tensor& x_, double s)
   return dx;
 }
 
+
+// Energy + force loss of a statically padded batch (models/base.py energy_force_loss,
+// reference Base.py:582-636) in one single-workgroup launch each way instead of ~20 small
+// torch kernels (masked means, the |true| ratio that weights the force term, their sums):
+//   e_loss = sum_g m_g L(eP - eT) / sum m_g;  f_loss = sum_n m_n sum_c L(fP - fT) / (3 sum m_n)
+//   fw = w * mean_g |eT| / (mean_{n,c} |fT| + 1e-8)   (masked means, counts clamped at 1)
+//   tot = w e_loss + fw f_loss.     kind: 0 mse, 1 mae.
+// Backward: dE_g = (g_tot w + g_e) m_g L'(d_g) / sum m_g,  dF = g_tot fw m_n L'(d) / (3 sum m_n).
+constexpr int kEfThreads = 256;
+__device__ __forceinline__ float ef_l(int kind, float d) { return kind == 0 ? d * d : fabsf(d); }
+__device__ __forceinline__ float ef_dl(int kind, float d) {
+  return kind == 0 ? 2.f * d : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+}
+__device__ __forceinline__ float block_sum_ef(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int k = 0; k < kEfThreads / 64; ++k) t += sh[k];
+  return t;
+}
+
+__global__ void __launch_bounds__(kEfThreads) ef_loss_fwd_kernel(const float* __restrict__ ep,
+                                                                 const float* __restrict__ et,
+                                                                 const bool* __restrict__ gm, int G,
+                                                                 const float* __restrict__ fp,
+                                                                 const float* __restrict__ ft,
+                                                                 const bool* __restrict__ nm, int N, int kind,
+                                                                 float w, float* __restrict__ out) {
+  __shared__ float sh[kEfThreads / 64];
+  float se = 0.f, cg = 0.f, ga = 0.f;
+  for (int g = threadIdx.x; g < G; g += kEfThreads)
+    if (gm[g]) {
+      se += ef_l(kind, ep[g] - et[g]);
+      cg += 1.f;
+      ga += fabsf(et[g]);
+    }
+  float sf = 0.f, cn = 0.f, fa = 0.f;
+  for (int i = threadIdx.x; i < 3 * N; i += kEfThreads)
+    if (nm[i / 3]) {
+      sf += ef_l(kind, fp[i] - ft[i]);
+      cn += 1.f;
+      fa += fabsf(ft[i]);
+    }
+  se = block_sum_ef(se, sh);
+  cg = block_sum_ef(cg, sh);
+  ga = block_sum_ef(ga, sh);
+  sf = block_sum_ef(sf, sh);
+  cn = block_sum_ef(cn, sh);
+  fa = block_sum_ef(fa, sh);
+  if (threadIdx.x == 0) {
+    const float e_loss = se / cg, f_loss = sf / cn;  // (cn counts components: 3 per valid atom)
+    const float ge = ga / fmaxf(cg, 1.f), fam = fa / fmaxf(cn, 3.f);
+    const float fw = w * ge / (fam + 1e-8f);
+    out[0] = e_loss * w + f_loss * fw;
+    out[1] = e_loss;
+    out[2] = fw;
+    out[3] = cg;
+    out[4] = cn;
+  }
+}
+
+__global__ void __launch_bounds__(256) ef_loss_bwd_kernel(const float* __restrict__ ep, const float* __restrict__ et,
+                                                          const bool* __restrict__ gm, int G,
+                                                          const float* __restrict__ fp, const float* __restrict__ ft,
+                                                          const bool* __restrict__ nm, int N, int kind, float w,
+                                                          const float* __restrict__ st,
+                                                          const float* __restrict__ gtot,
+                                                          const float* __restrict__ ge_,
+                                                          float* __restrict__ dE, float* __restrict__ dF) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const float gt = gtot ? gtot[0] : 0.f, gel = ge_ ? ge_[0] : 0.f;
+  if (i < G) dE[i] = gm[i] ? (gt * w + gel) * ef_dl(kind, ep[i] - et[i]) / st[3] : 0.f;
+  if (i < 3 * N) dF[i] = nm[i / 3] ? gt * st[2] * ef_dl(kind, fp[i] - ft[i]) / st[4] : 0.f;
+}
+
+// -> stats [5]: (tot, e_loss, fw, valid graphs, valid force components)
+at::Tensor ef_loss_fwd(const at::Tensor& ep, const at::Tensor& et, const at::Tensor& gm, const at::Tensor& fp,
+                       const at::Tensor& ft, const at::Tensor& nm, int64_t kind, double w) {
+  for (const auto* t : {&ep, &et, &fp, &ft})
+    HY_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "ef_loss: fp32 contiguous");
+  const int64_t G = ep.numel(), N = fp.numel() / 3;
+  HY_CHECK(et.numel() == G && gm.numel() == G && ft.numel() == 3 * N && nm.numel() == N &&
+               gm.scalar_type() == at::kBool && nm.scalar_type() == at::kBool && gm.is_contiguous() &&
+               nm.is_contiguous() && (kind == 0 || kind == 1),
+           "ef_loss: energy [G] / mask [G], forces [N, 3] / mask [N], kind mse | mae");
+  auto st = at::empty({5}, ep.options());
+  ef_loss_fwd_kernel<<<1, kEfThreads, 0, stream()>>>(ep.data_ptr<float>(), et.data_ptr<float>(), gm.data_ptr<bool>(),
+                                                     (int)G, fp.data_ptr<float>(), ft.data_ptr<float>(),
+                                                     nm.data_ptr<bool>(), (int)N, (int)kind, (float)w,
+                                                     st.data_ptr<float>());
+  return st;
+}
+
+std::vector<at::Tensor> ef_loss_bwd(const at::Tensor& ep, const at::Tensor& et, const at::Tensor& gm,
+                                    const at::Tensor& fp, const at::Tensor& ft, const at::Tensor& nm, int64_t kind,
+                                    double w, const at::Tensor& st, const c10::optional<at::Tensor>& gtot,
+                                    const c10::optional<at::Tensor>& ge) {
+  const int64_t G = ep.numel(), N = fp.numel() / 3;
+  auto dE = at::empty_like(ep), dF = at::empty_like(fp);
+  const int64_t n = std::max<int64_t>(G, 3 * N);
+  const float* gp = (gtot.has_value() && gtot->defined()) ? gtot->data_ptr<float>() : nullptr;
+  const float* ep_ = (ge.has_value() && ge->defined()) ? ge->data_ptr<float>() : nullptr;
+  if (n > 0)
+    ef_loss_bwd_kernel<<<ceil_div(n, 256), 256, 0, stream()>>>(
+        ep.data_ptr<float>(), et.data_ptr<float>(), gm.data_ptr<bool>(), (int)G, fp.data_ptr<float>(),
+        ft.data_ptr<float>(), nm.data_ptr<bool>(), (int)N, (int)kind, (float)w, st.data_ptr<float>(), gp, ep_,
+        dE.data_ptr<float>(), dF.data_ptr<float>());
+  return {dE, dF};
+}
+
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
+  m.def("ef_loss_fwd(Tensor ep, Tensor et, Tensor gm, Tensor fp, Tensor ft, Tensor nm, int kind, float w) -> Tensor");
+  m.def("ef_loss_bwd(Tensor ep, Tensor et, Tensor gm, Tensor fp, Tensor ft, Tensor nm, int kind, float w, Tensor st, "
+        "Tensor? gtot, Tensor? ge) -> Tensor[]");
   m.def("scaled_silu_fwd(Tensor x, float s) -> Tensor");
   m.def("scaled_silu_bwd(Tensor g, Tensor x, float s) -> Tensor");
   m.def("edge_gather_silu_fwd(Tensor ab, Tensor src, Tensor dst, Tensor? et, float s) -> Tensor");
@@ -618,6 +734,8 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
 }
 
 TORCH_LIBRARY_IMPL(hydra, CUDA, m) {
+  m.impl("ef_loss_fwd", hy::ef_loss_fwd);
+  m.impl("ef_loss_bwd", hy::ef_loss_bwd);
   m.impl("scaled_silu_fwd", hy::scaled_silu_fwd);
   m.impl("scaled_silu_bwd", hy::scaled_silu_bwd);
   m.impl("edge_gather_act_fwd", hy::edge_gather_act_fwd);

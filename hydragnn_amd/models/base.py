@@ -672,6 +672,13 @@ class Base(nn.Module):
             e_loss = self.loss_function(graph_energy_pred, graph_energy_true)
             f_loss = self.loss_function(forces_pred, forces_true)
             fw = w * torch.mean(torch.abs(graph_energy_true)) / (torch.mean(torch.abs(forces_true)) + 1e-8)
+        elif _ef_fused_ok(self.loss_function_type, graph_energy_pred, forces_pred, gmask, nmask):
+            # one launch each way (csrc/conv_misc.hip ef_loss): the loss is differentiated once
+            # (the training backward), so composite mode does not apply to it
+            tot, e_loss = _EFLoss.apply(graph_energy_pred.contiguous(), graph_energy_true.contiguous(),
+                                        gmask.contiguous(), forces_pred.contiguous(), forces_true.contiguous(),
+                                        nmask.contiguous(), _EF_KIND[self.loss_function_type], float(w))
+            return tot, [e_loss]
         else:
             # statically padded batch (captured step): the dummy graph / padding atoms are masked out
             from ..train.step import masked_loss
@@ -689,6 +696,42 @@ class Base(nn.Module):
 
     def __str__(self):
         return "Base"
+
+
+_EF_KIND = {"mse": 0, "mae": 1}
+
+
+def _ef_fused_ok(kind, ep, fp, gmask, nmask):
+    from ..ops import pna as _mode
+
+    return (kind in _EF_KIND and ep.is_cuda and ep.dtype == torch.float32 and fp.dtype == torch.float32
+            and fp.dim() == 2 and fp.shape[1] == 3 and gmask is not None and nmask is not None
+            and gmask.dtype == torch.bool and nmask.dtype == torch.bool and gmask.numel() == ep.numel()
+            and nmask.numel() == fp.shape[0] and "efloss" not in _mode._state["off"])
+
+
+class _EFLoss(torch.autograd.Function):
+    """Masked energy + force loss of a padded batch (``Base.energy_force_loss``) in one HIP
+    launch each way; outputs (total, energy loss)."""
+
+    @staticmethod
+    def forward(ctx, ep, et, gm, fp, ft, nm, kind, w):
+        from .. import _native
+
+        st = _native.ops().ef_loss_fwd(ep, et, gm, fp, ft, nm, kind, w)
+        ctx.save_for_backward(ep, et, gm, fp, ft, nm, st)
+        ctx.kind, ctx.w = kind, w
+        return st[0], st[1]
+
+    @staticmethod
+    def backward(ctx, g_tot, g_e):
+        from .. import _native
+
+        ep, et, gm, fp, ft, nm, st = ctx.saved_tensors
+        dE, dF = _native.ops().ef_loss_bwd(ep, et, gm, fp, ft, nm, ctx.kind, ctx.w, st,
+                                           None if g_tot is None else g_tot.reshape(1).contiguous(),
+                                           None if g_e is None else g_e.reshape(1).contiguous())
+        return dE, None, None, dF, None, None, None, None
 
 
 class _ReluRowMask(torch.autograd.Function):

@@ -258,3 +258,35 @@ def test_dimenet_static_triplets_device_matches_cpu():
         assert torch.equal(x.limit, y.limit.cpu())
     assert torch.equal(a_kj.perm, b_kj.perm.cpu())
     assert 0 < int(a_kj.limit) <= cap
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mse", "mae"])
+def test_fused_energy_force_loss_matches_masked_torch(kind):
+    """models/base.py _EFLoss (csrc/conv_misc.hip ef_loss, one launch each way) == the torch
+    masked energy + force loss of a padded batch: total, energy loss and both gradients."""
+    from hydragnn_amd.models.base import _EF_KIND, _EFLoss
+    from hydragnn_amd.train.step import masked_loss
+
+    g = torch.Generator().manual_seed(len(kind))
+    G, N, w = 9, 70, 0.7
+    ep, et = torch.randn(G, generator=g), torch.randn(G, generator=g)
+    fp, ft = torch.randn(N, 3, generator=g), torch.randn(N, 3, generator=g)
+    gm = torch.rand(G, generator=g) > 0.2
+    nm = torch.rand(N, generator=g) > 0.2
+    ep[~gm] = float("nan")  # padding rows never reach the loss
+    dev = torch.device("cuda")
+    a = [t.to(dev).requires_grad_() for t in (ep, fp)]
+    tot, el = _EFLoss.apply(a[0], et.to(dev), gm.to(dev), a[1], ft.to(dev), nm.to(dev), _EF_KIND[kind], w)
+    (tot * 1.3 + el * 0.4).backward()
+    b = [t.clone().double().requires_grad_() for t in (ep, fp)]
+    e_loss = masked_loss(kind, b[0].view(-1, 1), et.double().view(-1, 1), gm)
+    f_loss = masked_loss(kind, b[1], ft.double(), nm)
+    ge = et.double().abs()[gm].sum() / gm.sum().clamp(min=1)
+    fa = ft.double().abs()[nm].sum() / (nm.sum().clamp(min=1) * 3)
+    ref = e_loss * w + f_loss * (w * ge / (fa + 1e-8))
+    (ref * 1.3 + e_loss * 0.4).backward()
+    torch.testing.assert_close(tot.double().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(el.double().cpu(), e_loss.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a[0].grad.double().cpu(), torch.nan_to_num(b[0].grad), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a[1].grad.double().cpu(), b[1].grad, rtol=1e-5, atol=1e-6)
