@@ -161,6 +161,7 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restric
 template <bool IS_MAX>
 __global__ void __launch_bounds__(256) seg_minmax_kernel(const float* __restrict__ x,
                                                          const int* __restrict__ rowptr,
+                                                         const int* __restrict__ perm,
                                                          float* __restrict__ out,
                                                          int* __restrict__ arg, int N, int F) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -170,8 +171,14 @@ __global__ void __launch_bounds__(256) seg_minmax_kernel(const float* __restrict
   float best = IS_MAX ? -INFINITY : INFINITY;
   int besti = -1;
   for (int e = beg; e < end; ++e) {
-    const float v = x[(int64_t)e * F + f];
-    if (IS_MAX ? (v > best) : (v < best)) { best = v; besti = e; }
+    // permuted CSR (e.g. the source view): rows arrive out of order, so ties go to the
+    // smallest row id explicitly (the composite's first-row rule)
+    const int row = perm ? perm[e] : e;
+    const float v = x[(int64_t)row * F + f];
+    if ((IS_MAX ? (v > best) : (v < best)) || (v == best && besti >= 0 && row < besti)) {
+      best = v;
+      besti = row;
+    }
   }
   out[t] = besti < 0 ? 0.f : best;
   arg[t] = besti;
@@ -492,7 +499,7 @@ at::Tensor gather_rows(const at::Tensor& x_, const at::Tensor& idx) {
 }
 
 std::tuple<at::Tensor, at::Tensor> seg_minmax(const at::Tensor& x_, const at::Tensor& rowptr, int64_t N,
-                                              bool is_max) {
+                                              bool is_max, const c10::optional<at::Tensor>& perm) {
   HY_CHECK_CUDA(x_);
   auto x = as2d(x_).contiguous();
   HY_CHECK_F32(x);
@@ -501,13 +508,18 @@ std::tuple<at::Tensor, at::Tensor> seg_minmax(const at::Tensor& x_, const at::Te
   auto out = at::empty({N, F}, x.options());
   auto arg = at::empty({N, F}, x.options().dtype(at::kInt));
   const int64_t tot = N * F;
+  const int* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    HY_CHECK_I32(*perm);
+    pp = perm->data_ptr<int>();
+  }
   if (tot > 0) {
     if (is_max)
       seg_minmax_kernel<true><<<ceil_div(tot, 256), 256, 0, stream()>>>(
-          x.data_ptr<float>(), rowptr.data_ptr<int>(), out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
+          x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
     else
       seg_minmax_kernel<false><<<ceil_div(tot, 256), 256, 0, stream()>>>(
-          x.data_ptr<float>(), rowptr.data_ptr<int>(), out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
+          x.data_ptr<float>(), rowptr.data_ptr<int>(), pp, out.data_ptr<float>(), arg.data_ptr<int>(), N, F);
   }
   return {out, arg};
 }
@@ -696,7 +708,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
         "int codes, float avg_log, float avg_lin) -> Tensor");
   m.def("seg_sum(Tensor x, Tensor rowptr, Tensor? perm, int N, bool mean, Tensor? limit=None) -> Tensor");
   m.def("gather_rows(Tensor x, Tensor idx) -> Tensor");
-  m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max) -> (Tensor, Tensor)");
+  m.def("seg_minmax(Tensor x, Tensor rowptr, int N, bool is_max, Tensor? perm=None) -> (Tensor, Tensor)");
   m.def("scatter_arg(Tensor g, Tensor arg, int E) -> Tensor");
   m.def("gather_arg(Tensor x, Tensor arg) -> Tensor");
   m.def("gather_mul_sum(Tensor x, Tensor w, Tensor gidx, Tensor rowptr, Tensor? perm, int N, Tensor? limit=None) -> Tensor");

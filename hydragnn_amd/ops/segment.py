@@ -209,8 +209,8 @@ class _GatherArg(torch.autograd.Function):
 class _SegMinMax(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, si, is_max):
-        if _use_native(x) and x.dtype == torch.float32 and si.perm is None and x.dim() == 2:
-            out, arg = _native.ops().seg_minmax(x, si.rowptr, si.num_segments, is_max)
+        if _use_native(x) and x.dtype == torch.float32 and x.dim() == 2:
+            out, arg = _native.ops().seg_minmax(x, si.rowptr, si.num_segments, is_max, si.perm)
         else:
             out, arg = _cpu_segment_minmax(x, si, is_max)
         ctx.save_for_backward(arg)

@@ -59,15 +59,19 @@ def test_segment_sum_gather(F):
         torch.testing.assert_close(xng.grad.cpu(), ref_g, rtol=1e-5, atol=1e-5)
 
 
-def test_segment_minmax():
-    dst_si, _, E = _graph()
-    x = torch.randn(E, 16)
+@pytest.mark.parametrize("view", ["dst", "src"])
+def test_segment_minmax(view):
+    """Native segment min / max == the CPU composite, sorted (dst) and permuted (src) CSR;
+    ties (rounded values) go to the smallest row id in both."""
+    dst_si, src_si, E = _graph()
+    si = dst_si if view == "dst" else src_si
+    x = torch.randn(E, 16).mul(4).round()  # many ties
     for is_max in (True, False):
         f = seg.segment_max if is_max else seg.segment_min
         xc = x.clone().requires_grad_()
-        ref = f(xc, dst_si)
+        ref = f(xc, si)
         xg = x.to(DEV).requires_grad_()
-        out = f(xg, dst_si.to(DEV))
+        out = f(xg, si.to(DEV))
         torch.testing.assert_close(out.cpu(), ref.detach())
         g = torch.randn_like(ref)
         ref.backward(g)
