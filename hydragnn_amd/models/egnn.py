@@ -22,7 +22,7 @@ from torch import nn
 from .. import _native
 from ..ops import segment as seg
 from ..ops.geometry import edge_vectors_and_lengths
-from ..ops.linear import linear
+from ..ops.linear import ACT_RELU, linear
 from ..ops.pna import fused
 from .layers import Linear
 from .base import Base
@@ -119,7 +119,11 @@ class E_GCL(nn.Module):
             if len(ws) == 4:
                 h = h + linear(edge_attr, Wb[3])
             h = self.edge_mlp[1](h)
-        out = self.edge_mlp[3](self.edge_mlp[2](h))
+        l2, a2 = self.edge_mlp[2], self.edge_mlp[3]
+        if isinstance(a2, nn.ReLU) and l2.bias is not None:
+            out = linear(h, l2.weight, l2.bias, act=ACT_RELU)  # ReLU in the GEMM epilogue (tall maps)
+        else:
+            out = a2(l2(h))
         if self.attention:
             out = out * self.att_mlp(out)
         return out
@@ -132,7 +136,12 @@ class E_GCL(nn.Module):
         return out
 
     def coord_model(self, pos, coord_diff, m, src_si):
-        trans = (coord_diff * self.coord_mlp(m)).clamp(-100.0, 100.0)
+        c0, a0 = self.coord_mlp[0], self.coord_mlp[1]
+        if isinstance(a0, nn.ReLU) and c0.bias is not None:
+            phi = self.coord_mlp[2:](linear(m, c0.weight, c0.bias, act=ACT_RELU))  # ReLU in the epilogue
+        else:
+            phi = self.coord_mlp(m)
+        trans = (coord_diff * phi).clamp(-100.0, 100.0)
         return pos + seg.segment_mean(trans, src_si) * self.coords_weight
 
     def forward(self, inv, equiv, ctx):

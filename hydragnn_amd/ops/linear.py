@@ -343,6 +343,36 @@ def _composite_tall(x, W, b):
 _COMPOSITE_SK = os.environ.get("HYDRA_COMPOSITE_SPLITK", "1") == "1"
 
 
+class _TallLinearRelu(torch.autograd.Function):
+    """relu(x W^T + b) with the ReLU in the library GEMM's epilogue (torch._addmm_activation:
+    no separate [M, O] activation pass); backward masks dy by y > 0, then as _TallLinear."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        y = torch._addmm_activation(b, x, W.t())
+        ctx.save_for_backward(x, W, y)
+        ctx.params = (W, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, y = ctx.saved_tensors
+        dz = torch.ops.aten.threshold_backward(dy, y, 0.0)
+        dx = dz @ W if ctx.needs_input_grad[0] else None
+        Wp, bp = ctx.params
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2] and _can_defer(Wp, bp):
+            _record((dz, x, Wp, bp))
+            return dx, None, None
+        dW = db = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dW, db = _native.ops().linear_wgrad(dz, x, True)
+        return dx, dW, db
+
+
+# HYDRA_LINEAR_RELU_EPI=0: tall linear + ReLU as two launches (GEMM, then the activation)
+_RELU_EPI = os.environ.get("HYDRA_LINEAR_RELU_EPI", "1") == "1"
+
+
 class _ColBlockLinear(torch.autograd.Function):
     """y = x @ W[:, k0:k0+K]^T for a column block of a (concat-)linear weight: the block's
     weight gradient joins the deferred grouped launch as a column-block problem (``_span``)
@@ -512,6 +542,9 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
         any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
     if len(pairs) == 1 and act == ACT_NONE and residual is None and _composite_tall(xs[0], ws[0], b):
         return _LinearC.apply(xs[0], ws[0], b)
+    if (len(pairs) == 1 and tall and act == ACT_RELU and b is not None and residual is None and _RELU_EPI
+            and not _ENGINE_FWD1):
+        return _TallLinearRelu.apply(xs[0], ws[0], b)
     if len(pairs) == 1:
         if tall and _ENGINE_FWD1 and xs[0].shape[0] < ENGINE_SUM_MAX_ROWS * 4:
             y = _EngineSumF32.apply(b, xs[0], ws[0])  # HYDRA_ENGINE_FWD1=1: engine forward (A/B knob)
