@@ -33,7 +33,7 @@ def _flops(name, shapes):
         if name in ("aten::mm",):
             (m, k), (_, n) = shapes[0], shapes[1]
             return 2.0 * m * n * k
-        if name == "aten::addmm":
+        if name in ("aten::addmm", "aten::_addmm_activation"):
             (m, k), (_, n) = shapes[1], shapes[2]
             return 2.0 * m * n * k
         if name in ("aten::bmm",):
