@@ -7,7 +7,12 @@
 // to output block io of the same (l, p) with the weight W_p[mi, mo] (flat weight vector
 // at w_off, row-major) times the path normalisation a_p:
 //
-//     out[n, io(o, c)] = sum_{p -> io} a_p sum_i x[n, ii(i, c)] W_p[i, o]
+//     out[n, io(o, c)] = sum_{p -> io} a_p sum_i x[n, ii(i, c)] W_p[i, o]  (+ res[n, io(o, c)])
+//
+// The optional residual ``res`` is added in the epilogue: the MACE product block's skip
+// connection (``linear(.) + sc``) forward, and, in the transposed orientation, the sum of
+// the input gradients of several linears reading the same rows (skip / up / down of one
+// interaction) without a separate add pass each.
 //
 // The torch composite is a transposing copy + GEMM + transposing copy per path plus a
 // concat (and a zero-fill + copy per slice in backward); for MACE widths (64 channels,
@@ -44,7 +49,8 @@ struct Col {
 
 __global__ __launch_bounds__(256) void il_fwd_kernel(const float* __restrict__ x, int N, int Din,
                                                      const float* __restrict__ W, const Path* __restrict__ paths,
-                                                     const Col* __restrict__ cols, int Dout, float* __restrict__ out) {
+                                                     const Col* __restrict__ cols, int Dout,
+                                                     const float* __restrict__ res, float* __restrict__ out) {
   extern __shared__ float xs[];  // [TR][Din]
   const int n0 = blockIdx.x * TR;
   const int rows = min(TR, N - n0);
@@ -68,6 +74,8 @@ __global__ __launch_bounds__(256) void il_fwd_kernel(const float* __restrict__ x
         for (int r = 0; r < TR; ++r) acc[r] = fmaf(xr[r * Din], w, acc[r]);
       }
     }
+    if (res != nullptr)
+      for (int r = 0; r < rows; ++r) acc[r] += res[(int64_t)(n0 + r) * Dout + j];
     for (int r = 0; r < rows; ++r) out[(int64_t)(n0 + r) * Dout + j] = acc[r];
   }
 }
@@ -156,8 +164,9 @@ __global__ void il_wreduce_kernel(const float* __restrict__ slab, int S, int64_t
 using namespace il;
 
 // x [N, Din] fp32; W flat fp32; paths int32 [P, 7] (last column: float bits of a);
-// cols int32 [Dout, 4]
-at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Tensor& paths, const at::Tensor& cols) {
+// cols int32 [Dout, 4]; res (optional) fp32 [N, Dout] added to the output
+at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Tensor& paths, const at::Tensor& cols,
+                         const c10::optional<at::Tensor>& res_) {
   at::Tensor x = x_.contiguous();
   HY_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 2, "irreps_linear: x [N, Din] fp32");
   HY_CHECK(W.is_cuda() && W.scalar_type() == at::kFloat && W.is_contiguous(), "irreps_linear: W fp32 contiguous");
@@ -167,12 +176,20 @@ at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Te
            "irreps_linear: column table int32 [Dout, 4]");
   const int64_t N = x.size(0), Din = x.size(1), Dout = cols.size(0);
   HY_CHECK(Din <= MAXCOLS, "irreps_linear: at most 4096 input columns");
+  at::Tensor res;
+  if (res_.has_value() && res_->defined()) {
+    res = res_->contiguous();
+    HY_CHECK(res.is_cuda() && res.scalar_type() == at::kFloat && res.dim() == 2 && res.size(0) == N &&
+                 res.size(1) == Dout,
+             "irreps_linear: res fp32 [N, Dout]");
+  }
   auto out = at::empty({N, Dout}, x.options());
   if (N == 0 || Dout == 0) return out;
   const size_t lds = (size_t)TR * Din * sizeof(float);
   il_fwd_kernel<<<dim3((unsigned)ceil_div(N, TR), (unsigned)ceil_div(Dout, 256)), 256, lds, stream()>>>(x.data_ptr<float>(), (int)N, (int)Din, W.data_ptr<float>(),
                                                          reinterpret_cast<const Path*>(paths.data_ptr()),
                                                          reinterpret_cast<const Col*>(cols.data_ptr()), (int)Dout,
+                                                         res.defined() ? res.data_ptr<float>() : nullptr,
                                                          out.data_ptr<float>());
   return out;
 }
@@ -219,7 +236,7 @@ at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const
 }  // namespace hy
 
 TORCH_LIBRARY_FRAGMENT(hydra, m) {
-  m.def("irreps_linear(Tensor x, Tensor W, Tensor paths, Tensor cols) -> Tensor");
+  m.def("irreps_linear(Tensor x, Tensor W, Tensor paths, Tensor cols, Tensor? res=None) -> Tensor");
   m.def("irreps_linear_wgrad(Tensor x, Tensor g, Tensor jobs, Tensor scale, int max_d, Tensor? out=None) -> Tensor");
 }
 

@@ -195,9 +195,9 @@ class InteractionBlock(nn.Module):
         self.skip_linear = o3.O3Linear(node_feats_irreps, hidden_irreps)
 
     def forward(self, h, edge_attrs, edge_feats, dst_si, src_si):
-        sc = self.skip_linear(h)
-        up = self.linear_up(h)
-        down = self.linear_down(h)
+        # three linears over the same rows: natively their input gradients are one chain of
+        # launches with the partial sum in each epilogue (no autograd add per extra consumer)
+        sc, up, down = o3.linear_multi([self.skip_linear, self.linear_up, self.linear_down], h)
         # radial FCN over cat[edge_feats, down[src], down[dst]]: first layer split at node level
         w = self.conv_tp_weights.forward_split(edge_feats, down, src_si, dst_si)
         # gather -> uvu tensor product -> segment sum, fused on the GPU (one launch each way)
@@ -214,8 +214,8 @@ class EquivariantProductBasisBlock(nn.Module):
         self.linear = o3.O3Linear(target_irreps, target_irreps)
 
     def forward(self, x, sc, elem):
-        out = self.linear(self.symmetric_contractions(x, elem))
-        return out + sc if (self.use_sc and sc is not None) else out
+        # the skip connection is added in the linear's epilogue (natively: no add pass)
+        return self.linear(self.symmetric_contractions(x, elem), residual=sc if self.use_sc else None)
 
 
 def _joined(inv, equiv):

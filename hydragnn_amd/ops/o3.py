@@ -237,19 +237,34 @@ def element_index(elem, num_elements):
     return seg.SegIndex(elem.to(torch.int32), rowptr, perm, num_elements)
 
 
+def _il_wgrad(x, g, W, jobs, maxd, wscale):
+    """Weight gradient of one native o3.Linear; written straight into the weight's slot of
+    the step's flat gradient buffer when there is one (then None is returned)."""
+    from .. import _native
+    from ..parallel import gradslots as _gs
+
+    sl = _gs.slots([W])
+    dW = _native.ops().irreps_linear_wgrad(x, g, jobs, wscale, maxd, None if sl is None else sl[0].view(-1))
+    if sl is not None:
+        _gs.provide([W])
+        return None
+    return dW
+
+
 class _IrrepsLinear(torch.autograd.Function):
     """Native o3.Linear (csrc/irreps_linear.hip): forward and input gradient are the same
     column-table kernel in two orientations; the weight gradient is a split node reduction
-    (first-order; composite mode runs the torch path)."""
+    (first-order; composite mode runs the torch path).  An optional residual ``res`` is
+    added in the forward kernel's epilogue (its gradient is the output gradient itself)."""
 
     @staticmethod
-    def forward(ctx, x, W, fwd, bwd, jobs, maxd, wscale):
+    def forward(ctx, x, W, fwd, bwd, jobs, maxd, wscale, res=None):
         from .. import _native
 
         x = x.contiguous()
         ctx.save_for_backward(x, W)
         ctx.tabs = (bwd, jobs, maxd, wscale)
-        return _native.ops().irreps_linear(x, W, fwd[0], fwd[1])
+        return _native.ops().irreps_linear(x, W, fwd[0], fwd[1], res)
 
     @staticmethod
     def backward(ctx, g):
@@ -259,17 +274,58 @@ class _IrrepsLinear(torch.autograd.Function):
         bwd, jobs, maxd, wscale = ctx.tabs
         g = g.contiguous()
         dx = _native.ops().irreps_linear(g, W, bwd[0], bwd[1]) if ctx.needs_input_grad[0] else None
-        dW = None
-        if ctx.needs_input_grad[1]:
-            from ..parallel import gradslots as _gs
+        dW = _il_wgrad(x, g, W, jobs, maxd, wscale) if ctx.needs_input_grad[1] else None
+        return dx, dW, None, None, None, None, None, (g if ctx.needs_input_grad[7] else None)
 
-            # the step's flat gradient buffer: the reduce kernel writes the slot directly
-            sl = _gs.slots([W])
-            dW = _native.ops().irreps_linear_wgrad(x, g, jobs, wscale, maxd, None if sl is None else sl[0].view(-1))
-            if sl is not None:
-                _gs.provide([W])
-                dW = None
-        return dx, dW, None, None, None, None, None
+
+class _IrrepsLinearMulti(torch.autograd.Function):
+    """Several native o3.Linears reading the same rows x (the skip / up / down linears of a
+    MACE interaction).  Forward: one launch each, as separately.  Backward: the input
+    gradient is ONE chain of transposed-orientation launches, each adding the previous
+    partial sum in its epilogue, instead of a launch each plus an autograd add per extra
+    consumer (csrc/irreps_linear.hip ``res``)."""
+
+    @staticmethod
+    def forward(ctx, x, tabs, *Ws):
+        from .. import _native
+
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        ctx.save_for_backward(x, *Ws)
+        ctx.tabs = tabs
+        return tuple(_native.ops().irreps_linear(x, W, t[0][0], t[0][1]) for W, t in zip(Ws, tabs))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        from .. import _native
+
+        x, *Ws = ctx.saved_tensors
+        ops = _native.ops()
+        dx, dWs = None, []
+        for W, t, g, need in zip(Ws, ctx.tabs, gs, ctx.needs_input_grad[2:]):
+            if g is None:
+                dWs.append(None)
+                continue
+            g = g.contiguous()
+            (_fwd, bwd, jobs, maxd, wscale) = t
+            if ctx.needs_input_grad[0]:
+                dx = ops.irreps_linear(g, W, bwd[0], bwd[1], dx)
+            dWs.append(_il_wgrad(x, g, W, jobs, maxd, wscale) if need else None)
+        if dx is None and ctx.needs_input_grad[0]:
+            dx = torch.zeros_like(x)
+        return (dx, None, *dWs)
+
+
+def linear_multi(lins, x):
+    """``[lin(x) for lin in lins]`` for o3.Linears sharing the input rows; native: one fused
+    input-gradient chain (``_IrrepsLinearMulti``)."""
+    if all(lin.native_ok(x) for lin in lins):
+        tabs = []
+        for lin in lins:
+            fwd, bwd, jobs, maxd = lin._native_tables(x.device)
+            tabs.append((fwd, bwd, jobs, maxd, lin.wscale))
+        return list(_IrrepsLinearMulti.apply(x, tuple(tabs), *[lin.weight for lin in lins]))
+    return [lin(x) for lin in lins]
 
 
 class O3Linear(nn.Module):
@@ -389,12 +445,15 @@ class O3Linear(nn.Module):
             return elem_si.onehot_t(table.dtype).t() @ table
         return seg.gather(table, elem_si)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
+        """``linear(x) (+ residual)``; natively the residual is added in the kernel epilogue."""
         from .linear import linear
 
-        if self.native_ok(x):
+        if self.native_ok(x) and (residual is None or residual.shape == (x.shape[0], self.irreps_out.dim)):
             fwd, bwd, jobs, maxd = self._native_tables(x.device)
-            return _IrrepsLinear.apply(x, self.weight, fwd, bwd, jobs, maxd, self.wscale)
+            return _IrrepsLinear.apply(x, self.weight, fwd, bwd, jobs, maxd, self.wscale, residual)
+        if residual is not None:
+            return self.forward(x) + residual
         N = x.shape[0]
         outs = [None] * len(self.irreps_out.blocks)
         # input blocks by ONE split (backward: one concat; per-block slices would zero-fill

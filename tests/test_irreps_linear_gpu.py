@@ -44,3 +44,38 @@ def test_irreps_linear_native_vs_torch(case):
     torch.testing.assert_close(y.double(), y_ref, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dx.double(), dx_ref, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dw.double(), dw_ref, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("drop", [None, 2])
+def test_irreps_linear_residual_and_multi(drop):
+    """Residual epilogue (``O3Linear(x, residual=r)``) and the shared-input chain
+    (``o3.linear_multi``: skip / up / down of a MACE interaction), with one output unused
+    (its gradient is None), against the fp64 torch composite."""
+    torch.manual_seed(7)
+    ir_in = I([(64, 0, 1), (64, 1, -1)])
+    outs = [I([(64, 0, 1), (64, 1, -1), (64, 2, 1)]), ir_in, I([(64, 0, 1)])]
+    lins = [o3.O3Linear(ir_in, o).cuda() for o in outs]
+    N = 301
+    x = torch.randn(N, ir_in.dim, device="cuda", requires_grad=True)
+    r = torch.randn(N, outs[1].dim, device="cuda", requires_grad=True)
+    gs = [torch.randn(N, o.dim, device="cuda") for o in outs]
+
+    def run(ls, xx, rr, gg):
+        ys = o3.linear_multi(ls, xx)
+        z = ls[1](ys[1], residual=rr)  # the product block's linear(.) + sc
+        loss = sum((y * g).sum() for k, (y, g) in enumerate(zip(ys, gg)) if k != drop) + (z * gg[1]).sum()
+        return torch.autograd.grad(loss, [xx, rr] + [lin.weight for lin in ls], allow_unused=True)
+
+    got = run(lins, x, r, gs)
+    with composite_mode(True):
+        lins64 = [o3.O3Linear(ir_in, o).double().cuda() for o in outs]
+        for a, b in zip(lins64, lins):
+            a.weight.data.copy_(b.weight.data.double())
+        ref = run(lins64, x.detach().double().requires_grad_(True), r.detach().double().requires_grad_(True),
+                  [g.double() for g in gs])
+    for a, b in zip(got, ref):
+        if b is None:  # the unused output's weight
+            assert a is None or not a.any()
+            continue
+        torch.testing.assert_close(a.double(), b, rtol=1e-4, atol=2e-3)
