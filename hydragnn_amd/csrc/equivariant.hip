@@ -227,11 +227,14 @@ __global__ void __launch_bounds__(256) tp_conv_fwd_kernel(const float* __restric
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
   const int e0 = drp[n], e1 = drp[n + 1];
+  // one wave per (node, instruction): every instruction writes its own output block, and a
+  // wave per node walking all of them left the chip at ~4 waves per CU for MACE batches
+  const int t = blockIdx.y;
   for (int c0 = e0; c0 < e1 || c0 == e0; c0 += 64) {  // chunks of 64 edges (one, typically)
     const int cnt = min(64, e1 - c0);
     const int q = c0 + (lane < cnt ? lane : 0);
     const int v_e = q, v_n = cnt > 0 ? src[q < e1 ? q : e0] : 0;
-    for (int t = 0; t < nins; ++t) {
+    {
       const int* r = ins + t * kInsCols;
       const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
       const float* C = cg + r[8];
@@ -265,14 +268,21 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_x_kernel(const float* __restr
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= N) return;
+  // one wave per (node, x1 block): the wave of the block's first instruction accumulates
+  // every instruction reading that block (disjoint gx1 slices across waves: no atomics, a
+  // fixed summation order); the other instructions' waves exit
+  const int tb = blockIdx.y, blk = ins[tb * kInsCols + 4];
+  for (int t = 0; t < tb; ++t)
+    if (ins[t * kInsCols + 4] == blk) return;
   const int b = srp[n], eN = srp[n + 1];
   for (int c0 = b; c0 < eN; c0 += 64) {  // chunks of 64 source edges (one, typically)
     const int cnt = min(64, eN - c0);
     const int q = c0 + (lane < cnt ? lane : 0);
     const int v_e = sperm ? sperm[q] : q;
     const int v_n = dst[v_e];
-    for (int t = 0; t < nins; ++t) {
+    for (int t = tb; t < nins; ++t) {
       const int* r = ins + t * kInsCols;
+      if (r[4] != blk) continue;
       const int m = r[3], code = tp_lcode(r[0], r[1], r[2]);
       const float* C = cg + r[8];
       for (int u = lane; u < m; u += 64) {
@@ -292,7 +302,10 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_x_kernel(const float* __restr
   }
 }
 
-// per edge: gw[e] and gy[e] (gy zero-initialised) from x1[src_e] and go[dst_e]
+// per edge: gw[e] and gy[e] (gy zero-initialised) from x1[src_e] and go[dst_e]; GY = false
+// (edge attributes without a gradient: energy training) drops the gY partial sums and their
+// per-instruction wave reductions
+template <bool GY>
 __global__ void __launch_bounds__(256) tp_conv_bwd_e_kernel(const float* __restrict__ go, int ldo,
                                                             const float* __restrict__ x1, int ld1,
                                                             const float* __restrict__ y, int ld2,
@@ -331,11 +344,13 @@ __global__ void __launch_bounds__(256) tp_conv_bwd_e_kernel(const float* __restr
     }
     // gyl is indexed with compile-time constants inside each case body; the reduction
     // below walks the (uniform) runtime width
+    if constexpr (GY) {
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      if (j < d2) {
-        const float v = wave_sum(gyl[j]);
-        if (lane == 0) gy[e * ld2 + r[5] + j] += v;
+      for (int j = 0; j < 7; ++j) {
+        if (j < d2) {
+          const float v = wave_sum(gyl[j]);
+          if (lane == 0) gy[e * ld2 + r[5] + j] += v;
+        }
       }
     }
   }
@@ -394,7 +409,7 @@ at::Tensor tp_conv_fwd(const at::Tensor& x1, const at::Tensor& y, const at::Tens
   HY_CHECK(x1.size(0) == N && w.size(0) == E && src.numel() == E, "tp_conv: shapes");
   auto out = at::empty({N, out_dim}, x1.options());
   if (N == 0) return out;
-  tp_conv_fwd_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(
+  tp_conv_fwd_kernel<<<dim3((unsigned)ceil_div(N, 4), (unsigned)ins.size(0)), 256, 0, stream()>>>(
       x1.data_ptr<float>(), (int)x1.size(1), y.data_ptr<float>(), (int)y.size(1), w.data_ptr<float>(),
       (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0), cg.data_ptr<float>(), src.data_ptr<int>(),
       drp.data_ptr<int>(), out.data_ptr<float>(), (int)out_dim, (int)N);
@@ -406,24 +421,27 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> tp_conv_bwd(const at::Tensor& go_
                                                            const at::Tensor& ins, const at::Tensor& cg,
                                                            const at::Tensor& src, const at::Tensor& dst,
                                                            const at::Tensor& srp,
-                                                           const c10::optional<at::Tensor>& sperm) {
+                                                           const c10::optional<at::Tensor>& sperm, bool need_gy) {
   auto go = go_.contiguous();
   check_ins(ins, cg);
   const int64_t N = x1.size(0), E = y.size(0);
   HY_CHECK(srp.numel() == N + 1 && dst.numel() == E && go.size(0) == N, "tp_conv_bwd: shapes");
-  auto gx1 = at::zeros_like(x1), gy = at::zeros_like(y), gw = at::empty_like(w);
+  auto gx1 = at::zeros_like(x1), gw = at::empty_like(w);
+  auto gy = need_gy ? at::zeros_like(y) : at::empty({0}, y.options());
   if (N)
-    tp_conv_bwd_x_kernel<<<ceil_div(N, 4), 256, 0, stream()>>>(
+    tp_conv_bwd_x_kernel<<<dim3((unsigned)ceil_div(N, 4), (unsigned)ins.size(0)), 256, 0, stream()>>>(
         go.data_ptr<float>(), (int)go.size(1), y.data_ptr<float>(), (int)y.size(1), w.data_ptr<float>(),
         (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0), cg.data_ptr<float>(), dst.data_ptr<int>(),
         srp.data_ptr<int>(), sperm.has_value() ? sperm->data_ptr<int>() : nullptr, gx1.data_ptr<float>(),
         (int)x1.size(1), (int)N);
-  if (E)
-    tp_conv_bwd_e_kernel<<<ceil_div(E, 4), 256, 0, stream()>>>(
+  if (E) {
+    auto* kern = need_gy ? tp_conv_bwd_e_kernel<true> : tp_conv_bwd_e_kernel<false>;
+    kern<<<ceil_div(E, 4), 256, 0, stream()>>>(
         go.data_ptr<float>(), (int)go.size(1), x1.data_ptr<float>(), (int)x1.size(1), y.data_ptr<float>(),
         (int)y.size(1), w.data_ptr<float>(), (int)w.size(1), ins.data_ptr<int>(), (int)ins.size(0),
-        cg.data_ptr<float>(), src.data_ptr<int>(), dst.data_ptr<int>(), gy.data_ptr<float>(), gw.data_ptr<float>(),
-        E);
+        cg.data_ptr<float>(), src.data_ptr<int>(), dst.data_ptr<int>(), need_gy ? gy.data_ptr<float>() : nullptr,
+        gw.data_ptr<float>(), E);
+  }
   return {gx1, gy, gw};
 }
 
@@ -433,7 +451,7 @@ TORCH_LIBRARY_FRAGMENT(hydra, m) {
   m.def("tp_conv_fwd(Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, Tensor src, Tensor drp, int out_dim) -> Tensor");
   m.def(
       "tp_conv_bwd(Tensor go, Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, Tensor src, Tensor dst, Tensor srp, "
-      "Tensor? sperm) -> (Tensor, Tensor, Tensor)");
+      "Tensor? sperm, bool need_gy=True) -> (Tensor, Tensor, Tensor)");
   m.def("tp_uvu_fwd(Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg, int out_dim) -> Tensor");
   m.def("tp_uvu_bwd(Tensor go, Tensor x1, Tensor y, Tensor w, Tensor ins, Tensor cg) -> (Tensor, Tensor, Tensor)");
 }

@@ -764,9 +764,10 @@ class _TPConv(torch.autograd.Function):
 
         x1, y, w, ins, cg = ctx.saved_tensors
         src_si, dst_si = ctx.si
+        need_gy = ctx.needs_input_grad[1]  # edge attributes: no gradient in energy training
         g1, gy, gw = _native.ops().tp_conv_bwd(go, x1, y, w, ins, cg, src_si.index, dst_si.index, src_si.rowptr,
-                                               src_si.perm)
-        return g1, gy, gw, None, None, None, None, None
+                                               src_si.perm, need_gy)
+        return g1, (gy if need_gy else None), gw, None, None, None, None, None
 
 
 class TensorProductUVU(nn.Module):

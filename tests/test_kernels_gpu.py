@@ -356,10 +356,12 @@ def test_tp_uvu_native_matches_reference(lmax_node, lmax_sh):
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("y_grad", [True, False])
 @pytest.mark.parametrize("lmax_node,lmax_sh", [(1, 2), (2, 3)])
-def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh):
+def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh, y_grad):
     """Fused MACE convolution (gather x1[src] -> uvu TP -> segment sum by dst, one launch
-    each way) == segment_sum(TP(gather)) reference, values and all three gradients."""
+    each way) == segment_sum(TP(gather)) reference, values and all three gradients (and,
+    for edge attributes without a gradient, the backward variant that skips gY)."""
     from hydragnn_amd.ops import o3
     from hydragnn_amd.ops import segment as seg
 
@@ -374,7 +376,7 @@ def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh):
     src_si = seg.SegIndex.from_index(src.to(DEV), N, sorted_=False)
     dst_si = seg.SegIndex.from_index(dst.to(DEV), N, sorted_=True)
     x1 = torch.randn(N, ir1.dim, device=DEV, requires_grad=True)
-    y = torch.randn(E, ir2.dim, device=DEV, requires_grad=True)
+    y = torch.randn(E, ir2.dim, device=DEV, requires_grad=y_grad)
     w = torch.randn(E, tp.weight_numel, device=DEV, requires_grad=True)
     out = tp.conv(x1, y, w, src_si, dst_si)
     xr, yr, wr = [t.detach().double().cpu().requires_grad_() for t in (x1, y, w)]
@@ -386,6 +388,9 @@ def test_tp_conv_fused_matches_composite(lmax_node, lmax_sh):
     out.backward(g.float().to(DEV))
     ref.backward(g)
     for a, b in zip((x1, y, w), (xr, yr, wr)):
+        if a is y and not y_grad:
+            assert y.grad is None
+            continue
         torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=1e-4, atol=1e-3)
 
 
