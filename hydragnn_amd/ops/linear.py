@@ -540,8 +540,13 @@ def linear_act(pairs, b=None, act=ACT_NONE, residual=None):
     # narrow maps (e.g. an 866 -> 1 projection) and multi-input sums stay on the fp32 path
     tall = engine and xs[0].shape[0] >= MIN_ROWS and torch.is_grad_enabled() and \
         any(t.requires_grad for t in xs + ws + ([b] if b is not None else []))
-    if len(pairs) == 1 and act == ACT_NONE and residual is None and _composite_tall(xs[0], ws[0], b):
-        return _LinearC.apply(xs[0], ws[0], b)
+    if len(pairs) == 1 and _composite_tall(xs[0], ws[0], b):
+        # force training: split-K weight gradients in both passes; the activation and the
+        # residual stay twice-differentiable torch ops
+        y = _LinearC.apply(xs[0], ws[0], b)
+        if act == ACT_RELU:
+            y = torch.relu(y)
+        return y if residual is None else y + residual
     if (len(pairs) == 1 and tall and act == ACT_RELU and b is not None and residual is None and _RELU_EPI
             and not _ENGINE_FWD1):
         return _TallLinearRelu.apply(xs[0], ws[0], b)
