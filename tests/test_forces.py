@@ -290,3 +290,21 @@ def test_fused_energy_force_loss_matches_masked_torch(kind):
     torch.testing.assert_close(el.double().cpu(), e_loss.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(a[0].grad.double().cpu(), torch.nan_to_num(b[0].grad), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(a[1].grad.double().cpu(), b[1].grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_composite_linear_relu_keeps_splitk():
+    """A tall Linear+ReLU in force training stays on the twice-differentiable split-K linear
+    (a regression once sent it to F.linear, whose weight gradients are 2-workgroup GEMMs)."""
+    from hydragnn_amd.ops.linear import ACT_RELU, MIN_ROWS, linear
+    from hydragnn_amd.ops.pna import composite_mode as _cm
+
+    x = torch.randn(max(MIN_ROWS, 4096), 64, device="cuda", requires_grad=True)
+    W = torch.nn.Parameter(torch.randn(32, 64, device="cuda"))
+    b = torch.nn.Parameter(torch.zeros(32, device="cuda"))
+    with _cm(True):
+        y = linear(x, W, b, act=ACT_RELU)
+    assert "LinearC" in y.grad_fn.next_functions[0][0].name()
+    with _cm(True):
+        ref = torch.relu(torch.nn.functional.linear(x, W, b))
+    torch.testing.assert_close(y, ref)
