@@ -29,6 +29,7 @@
 //     order (deterministic) and applies a_p.
 #include "common.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace hy {
@@ -225,9 +226,22 @@ at::Tensor irreps_linear_wgrad(const at::Tensor& x_, const at::Tensor& g_, const
   }
   if (numel == 0) return dW;
   if (N == 0 || J == 0) return dW.zero_();
-  // splits: ~256 workgroups over the chip, at least NCH nodes each, at most 64 (the reduce
+  // splits: ~512 workgroups over the chip, at least NCH nodes each, at most 128 (the reduce
   // reads every split's slab)
-  int64_t S = std::max<int64_t>(1, std::min<int64_t>({ceil_div(256, J), ceil_div(N, NCH), (int64_t)64}));
+  // HYDRA_IL_WG="target,cap": workgroups aimed for and the split cap (A/B knob)
+  static int wg_target = 512, wg_cap = 128;  // MACE on MI355X: 256,64 14.69 k; 512,128 14.84 k; 1024,256 14.86 k
+  static bool wg_init = false;
+  if (!wg_init) {
+    wg_init = true;
+    if (const char* e = std::getenv("HYDRA_IL_WG")) {
+      int a = 0, c = 0;
+      if (std::sscanf(e, "%d,%d", &a, &c) == 2 && a >= 1 && c >= 1 && c <= 256) {
+        wg_target = a;
+        wg_cap = c;
+      }
+    }
+  }
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>({ceil_div(wg_target, J), ceil_div(N, NCH), (int64_t)wg_cap}));
   const int64_t per = ceil_div(N, S);
   S = ceil_div(N, per);
   // every split writes every weight element of every path (partial tiles mask their pad)
