@@ -52,22 +52,23 @@ struct Col {
 
 // U: reduction steps unrolled (weight loads in flight per thread; the kernel is bound by
 // their latency at MACE sizes)
-template <int U>
+// RT: rows (nodes) per workgroup (the LDS tile the host sizes: RT x Din floats)
+template <int U, int RT>
 __global__ __launch_bounds__(256) void il_fwd_kernel(const float* __restrict__ x, int N, int Din,
                                                      const float* __restrict__ W, const Path* __restrict__ paths,
                                                      const Col* __restrict__ cols, int Dout,
                                                      const float* __restrict__ res, float* __restrict__ out) {
-  extern __shared__ float xs[];  // [TR][Din]
-  const int n0 = blockIdx.x * TR;
-  const int rows = min(TR, N - n0);
+  extern __shared__ float xs[];  // [RT][Din]
+  const int n0 = blockIdx.x * RT;
+  const int rows = min(RT, N - n0);
   for (int t = threadIdx.x; t < rows * Din; t += 256) xs[t] = x[(int64_t)n0 * Din + t];
   __syncthreads();
   const int j = blockIdx.y * 256 + threadIdx.x;  // one output column per thread
   if (j < Dout) {
     const Col cl = cols[j];
-    float acc[TR];
+    float acc[RT];
 #pragma unroll
-    for (int r = 0; r < TR; ++r) acc[r] = 0.f;
+    for (int r = 0; r < RT; ++r) acc[r] = 0.f;
     for (int q = cl.p0; q < cl.p1; ++q) {
       const Path P = paths[q];
       const float* Wp = W + P.w_off + (int64_t)cl.o * P.w_os;
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void il_fwd_kernel(const float* __restrict__ x
         const float w = Wp[(int64_t)i * P.w_rs] * P.a;
         const float* xr = xc + i * P.d;
 #pragma unroll
-        for (int r = 0; r < TR; ++r) acc[r] = fmaf(xr[r * Din], w, acc[r]);
+        for (int r = 0; r < RT; ++r) acc[r] = fmaf(xr[r * Din], w, acc[r]);
       }
     }
     if (res != nullptr)
@@ -191,10 +192,18 @@ at::Tensor irreps_linear(const at::Tensor& x_, const at::Tensor& W, const at::Te
   }
   auto out = at::empty({N, Dout}, x.options());
   if (N == 0 || Dout == 0) return out;
-  const size_t lds = (size_t)TR * Din * sizeof(float);
   static const int unroll = std::getenv("HYDRA_IL_UNROLL") ? std::atoi(std::getenv("HYDRA_IL_UNROLL")) : 8;  // MI355X MACE: 8 > 4 (+0.8%) >> 16 (-14%)
-  auto* kern = unroll >= 16 ? il_fwd_kernel<16> : (unroll >= 8 ? il_fwd_kernel<8> : il_fwd_kernel<4>);
-  kern<<<dim3((unsigned)ceil_div(N, TR), (unsigned)ceil_div(Dout, 256)), 256, lds, stream()>>>(x.data_ptr<float>(), (int)N, (int)Din, W.data_ptr<float>(),
+  // HYDRA_IL_ROWS = 8 / 4 / 2 / 1: nodes per workgroup (fewer: more workgroups, weights re-read)
+  static const int rows_env = std::getenv("HYDRA_IL_ROWS") ? std::atoi(std::getenv("HYDRA_IL_ROWS")) : 4;
+  // 8 rows while the tile fits the 64 KB default LDS allocation
+  const int rt = (rows_env >= 8 && 8 * Din * (int64_t)sizeof(float) <= 65536) ? 8
+               : (rows_env >= 4 ? 4 : (rows_env >= 2 ? 2 : 1));
+  const size_t lds = (size_t)rt * Din * sizeof(float);
+  auto* kern = rt == 8 ? (unroll >= 8 ? il_fwd_kernel<8, 8> : il_fwd_kernel<4, 8>)
+             : rt == 4 ? (unroll >= 16 ? il_fwd_kernel<16, 4> : (unroll >= 8 ? il_fwd_kernel<8, 4> : il_fwd_kernel<4, 4>))
+             : rt == 2 ? (unroll >= 8 ? il_fwd_kernel<8, 2> : il_fwd_kernel<4, 2>)
+                       : (unroll >= 8 ? il_fwd_kernel<8, 1> : il_fwd_kernel<4, 1>);
+  kern<<<dim3((unsigned)ceil_div(N, rt), (unsigned)ceil_div(Dout, 256)), 256, lds, stream()>>>(x.data_ptr<float>(), (int)N, (int)Din, W.data_ptr<float>(),
                                                          reinterpret_cast<const Path*>(paths.data_ptr()),
                                                          reinterpret_cast<const Col*>(cols.data_ptr()), (int)Dout,
                                                          res.defined() ? res.data_ptr<float>() : nullptr,
